@@ -1,0 +1,114 @@
+"""ctypes binding of libcyclone.so (include/cyclone.h).
+
+The library is built in-tree (cycloneml_amd/libcyclone.so, see
+cycloneml_amd/csrc/Makefile).  There is no fallback: if the shared object is
+missing or cannot be loaded this module raises, and every entry point refuses
+to run without a gfx950 device (CYC_ERR_NO_DEVICE).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcyclone.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cyclone.h")
+
+CYC_OK = 0
+CYC_ERR_INVALID_ARG = 1
+CYC_ERR_HIP = 2
+CYC_ERR_ALLOC = 3
+CYC_ERR_UNSUPPORTED = 4
+CYC_ERR_NO_DEVICE = 5
+
+_lib = None
+_lock = threading.Lock()
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f64 = ctypes.c_double
+_pi64 = ctypes.POINTER(ctypes.c_int64)
+_pi32 = ctypes.POINTER(ctypes.c_int32)
+
+# name -> (restype, argtypes).  Device pointers travel as c_void_p.
+SIGNATURES = {
+    "cyc_last_error": (ctypes.c_char_p, []),
+    "cyc_version": (ctypes.c_int, []),
+    "cyc_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "cyc_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "cyc_synchronize": (ctypes.c_int, [_vp]),
+    "cyc_row_norms_dev": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
+    "cyc_kmeans_plan_create": (ctypes.c_int, [_i32, _i32, _i64, ctypes.POINTER(_vp)]),
+    "cyc_kmeans_plan_destroy": (ctypes.c_int, [_vp]),
+    "cyc_kmeans_plan_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "cyc_kmeans_plan_get_timing": (ctypes.c_int, [_vp, ctypes.POINTER(_f64), _pi64]),
+    "cyc_kmeans_stats_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
+    "cyc_kmeans_assign_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _pi64,
+                                             _vp]),
+    "cyc_kmeans_accumulate_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
+                                                 _vp, _vp, _vp, _vp]),
+    "cyc_kmeans_update_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _f64, _vp, _vp]),
+}
+
+
+class CycloneError(RuntimeError):
+    """A libcyclone call failed (HIP error, allocation, unsupported shape)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[cyclone {code}] {msg}")
+        self.code = code
+
+
+class IllegalArgumentException(ValueError):
+    """A reference `require` failed (Scala IllegalArgumentException)."""
+
+
+def load():
+    """Load libcyclone.so; raises if it is missing (no silent fallback)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"libcyclone.so not found at {LIB_PATH}; build it with "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` "
+                    "(or make -C cycloneml_amd/csrc)")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int):
+    if rc == CYC_OK:
+        return
+    msg = load().cyc_last_error().decode(errors="replace")
+    if rc == CYC_ERR_INVALID_ARG:
+        raise IllegalArgumentException(msg)
+    raise CycloneError(rc, msg)
+
+
+def header_symbols(path: str = HEADER_PATH):
+    """Function names declared in include/cyclone.h."""
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(cyc_[a-z0-9_]+)\s*\(", txt)))
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None for None)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(stream=None) -> int | None:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

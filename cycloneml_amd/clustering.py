@@ -1,0 +1,191 @@
+"""KMeans on MI355X: host-side mirror of org.apache.spark.mllib.clustering.
+
+Mirrors mllib/clustering/KMeans.scala (the Lloyd loop :240-349 and its
+parameters) and KMeansModel; the per-partition body runs in libcyclone
+(cycloneml_amd/csrc/kmeans.hip).  Data stays resident in HBM: `run` takes a
+torch CUDA fp64 tensor of shape (n, d) -- one process per GPU holding its
+shard of the rows (the Spark partitions assigned to that GPU).  When
+torch.distributed is initialised, the reduceByKey/collectAsMap merge
+(KMeans.scala:308-311) and the DoubleAccumulator cost are one all-reduce of
+[sums | weights | cost] over RCCL (backend "nccl"), and every rank applies the
+same centroid update (:322-330).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class KMeansPlan:
+    """RAII wrapper of cyc_kmeans_plan (device scratch for one (d, k) shape)."""
+
+    def __init__(self, d: int, k: int, max_rows: int = 1):
+        self._lib = N.load()
+        h = ctypes.c_void_p()
+        N.check(self._lib.cyc_kmeans_plan_create(int(d), int(k), int(max_rows), ctypes.byref(h)))
+        self.handle = h
+        self.d, self.k = int(d), int(k)
+
+    def close(self):
+        if self.handle:
+            self._lib.cyc_kmeans_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_timing(self, enable: bool):
+        N.check(self._lib.cyc_kmeans_plan_set_timing(self.handle, int(enable)))
+
+    def get_timing(self):
+        ms = ctypes.c_double()
+        cnt = ctypes.c_int64()
+        N.check(self._lib.cyc_kmeans_plan_get_timing(self.handle, ctypes.byref(ms),
+                                                     ctypes.byref(cnt)))
+        return ms.value, cnt.value
+
+    def stats(self, C, out=None, stream=None):
+        N.check(self._lib.cyc_kmeans_stats_dev(self.handle, N.ptr(C), N.ptr(out),
+                                               N.stream_handle(stream)))
+        return out
+
+    def assign(self, X, xnorm, C, cnorm, assign, cost, stream=None, count_exact=False):
+        n_exact = ctypes.c_int64(0)
+        N.check(self._lib.cyc_kmeans_assign_dev(
+            self.handle, N.ptr(X), N.ptr(xnorm), int(X.shape[0]), N.ptr(C), N.ptr(cnorm),
+            N.ptr(assign), N.ptr(cost), ctypes.byref(n_exact) if count_exact else None,
+            N.stream_handle(stream)))
+        return n_exact.value
+
+    def accumulate(self, X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, assign=None,
+                   cost=None, stream=None):
+        N.check(self._lib.cyc_kmeans_accumulate_dev(
+            self.handle, N.ptr(X), N.ptr(xnorm), N.ptr(weights), int(X.shape[0]), N.ptr(C),
+            N.ptr(cnorm), N.ptr(sums), N.ptr(wsum), N.ptr(cost_sum), N.ptr(assign), N.ptr(cost),
+            N.stream_handle(stream)))
+
+    def update(self, C, cnorm, sums, wsum, epsilon, converged, stream=None):
+        N.check(self._lib.cyc_kmeans_update_dev(self.handle, N.ptr(C), N.ptr(cnorm), N.ptr(sums),
+                                                N.ptr(wsum), float(epsilon), N.ptr(converged),
+                                                N.stream_handle(stream)))
+
+
+def row_norms(X, out=None, stream=None):
+    """Vectors.norm(v, 2.0) per row, bit-exact (mllib/linalg/Vectors.scala:489-514)."""
+    torch = _torch()
+    if out is None:
+        out = torch.empty(X.shape[0], dtype=torch.float64, device=X.device)
+    N.check(N.load().cyc_row_norms_dev(N.ptr(X), int(X.shape[0]), int(X.shape[1]), N.ptr(out),
+                                       N.stream_handle(stream)))
+    return out
+
+
+class KMeansModel:
+    """mllib/clustering/KMeansModel.scala: centers (k x d), cost, numIter."""
+
+    def __init__(self, clusterCenters, trainingCost=0.0, numIter=0):
+        self.clusterCenters = np.ascontiguousarray(clusterCenters, dtype=np.float64)
+        self.trainingCost = float(trainingCost)
+        self.numIter = int(numIter)
+
+    @property
+    def k(self):
+        return self.clusterCenters.shape[0]
+
+
+class KMeans:
+    """mllib.clustering.KMeans with the reference's parameters and defaults
+    (KMeans.scala:48-60: k=2, maxIterations=20, epsilon=1e-4)."""
+
+    def __init__(self, k: int = 2, maxIterations: int = 20, epsilon: float = 1e-4,
+                 seed: int = 0):
+        self.k = k
+        self.maxIterations = maxIterations
+        self.epsilon = epsilon
+        self.seed = seed
+        self.initialModel = None
+        self.distanceMeasure = "euclidean"
+
+    # Builder setters (KMeans.scala:87-200)
+    def setK(self, k):
+        if not k > 0:
+            raise N.IllegalArgumentException(f"Number of clusters must be positive but got {k}")
+        self.k = k
+        return self
+
+    def setMaxIterations(self, m):
+        if not m >= 0:
+            raise N.IllegalArgumentException(
+                f"Maximum of iterations must be nonnegative but got {m}")
+        self.maxIterations = m
+        return self
+
+    def setEpsilon(self, eps):
+        if not eps >= 0:
+            raise N.IllegalArgumentException(
+                f"Distance threshold must be nonnegative but got {eps}")
+        self.epsilon = eps
+        return self
+
+    def setInitialModel(self, model: KMeansModel):
+        if model.k != self.k:
+            raise N.IllegalArgumentException("mismatched cluster count")
+        self.initialModel = model
+        return self
+
+    def setDistanceMeasure(self, dm: str):
+        if dm != "euclidean":
+            raise N.IllegalArgumentException(
+                "only the euclidean distance measure runs on the MI355X path")
+        self.distanceMeasure = dm
+        return self
+
+    def run(self, X, weights=None, xnorm=None, stream=None, iteration_callback=None):
+        """Lloyd's algorithm, KMeans.scala:240-349, on a device-resident shard.
+
+        X: torch.float64 CUDA tensor (n, d).  weights: optional (n,) tensor.
+        Returns KMeansModel (centers on the host)."""
+        torch = _torch()
+        if self.initialModel is None:
+            raise N.IllegalArgumentException(
+                "initialModel is required on the device path (setInitialModel); "
+                "k-means|| / random initialisation are host-side (SURVEY.md 8f)")
+        dev = X.device
+        n, d = X.shape
+        k = self.k
+        if xnorm is None:
+            xnorm = row_norms(X, stream=stream)
+        plan = KMeansPlan(d, k, n)
+        C = torch.from_numpy(self.initialModel.clusterCenters.copy()).to(dev)
+        cnorm = row_norms(C, stream=stream)
+        dist = torch.distributed if (torch.distributed.is_available()
+                                     and torch.distributed.is_initialized()) else None
+        world = dist.get_world_size() if dist else 1
+        buf = torch.empty(k * d + k + 1, dtype=torch.float64, device=dev)
+        sums, wsum, cost_sum = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
+        converged_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        iteration, converged, cost = 0, False, 0.0
+        while iteration < self.maxIterations and not converged:
+            buf.zero_()
+            plan.accumulate(X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, stream=stream)
+            if world > 1:
+                dist.all_reduce(buf)
+            plan.update(C, cnorm, sums, wsum, self.epsilon, converged_t, stream=stream)
+            converged = bool(converged_t.item())
+            cost = float(cost_sum.item())
+            if iteration_callback:
+                iteration_callback(iteration, cost)
+            iteration += 1
+        plan.close()
+        return KMeansModel(C.cpu().numpy(), cost, iteration)

@@ -1,0 +1,98 @@
+// common.hpp -- shared plumbing for libcyclone (gfx950 / MI355X only).
+//
+// Error model (include/cyclone.h): every extern "C" entry point returns an int
+// status and records a thread-local message readable through cyc_last_error().
+// Argument checks reproduce the reference's `require` messages so a JVM shim can
+// rethrow them as IllegalArgumentException (SURVEY.md 8(b) "Conventions").
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/cyclone.h"
+
+namespace cyc {
+
+void set_error(const std::string& msg);
+const std::string& get_error();
+
+// A hipError_t turned into a CYC_ERR_HIP status with a message.
+int hip_fail(hipError_t e, const char* what, const char* file, int line);
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Scratch memory grown on demand, one per (device, purpose).  Not thread-safe:
+// entry points that use it hold the owning plan's mutex.
+struct DeviceBuffer {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  int device = -1;
+  int reserve(size_t n);  // returns CYC_OK or an error status
+  void release();
+  ~DeviceBuffer() { release(); }
+};
+
+// Fixed-margin round-up.
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace cyc
+
+#define CYC_HIP(expr)                                                     \
+  do {                                                                    \
+    hipError_t _e = (expr);                                               \
+    if (_e != hipSuccess) return cyc::hip_fail(_e, #expr, __FILE__, __LINE__); \
+  } while (0)
+
+#define CYC_REQUIRE(cond, msg)                                            \
+  do {                                                                    \
+    if (!(cond)) {                                                        \
+      cyc::set_error(std::string("requirement failed: ") + (msg));        \
+      return CYC_ERR_INVALID_ARG;                                         \
+    }                                                                     \
+  } while (0)
+
+#define CYC_LAUNCH_CHECK(what)                                            \
+  do {                                                                    \
+    hipError_t _e = hipGetLastError();                                    \
+    if (_e != hipSuccess) return cyc::hip_fail(_e, what, __FILE__, __LINE__); \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// Device helpers shared by the kernels.
+// ---------------------------------------------------------------------------
+typedef double cyc_double4 __attribute__((ext_vector_type(4)));
+
+// Non-contracted arithmetic: the reference is JVM code, which never fuses
+// a*b+c.  Every translation unit is compiled with -ffp-contract=off and opens
+// with `#pragma clang fp contract(off)`; these helpers only name the intent in
+// the bit-exact paths (hipcc's __dadd_rn & co. are plain operators here).
+#pragma clang fp contract(off)
+__device__ __forceinline__ double dsub(double a, double b) { return a - b; }
+__device__ __forceinline__ double dmul(double a, double b) { return a * b; }
+__device__ __forceinline__ double dadd(double a, double b) { return a + b; }
+
+// mllib/linalg/Vectors.scala:580-587: score = v1(k) - v2(k); sum += score*score
+__device__ __forceinline__ double seq_sqdist(const double* __restrict__ a,
+                                             const double* __restrict__ b, int d) {
+  double s = 0.0;
+  for (int j = 0; j < d; ++j) {
+    double sc = dsub(a[j], b[j]);
+    s = dadd(s, dmul(sc, sc));
+  }
+  return s;
+}
+
+// mllib/linalg/Vectors.scala:500-507 norm(v, 2): sum += v*v; sqrt(sum)
+__device__ __forceinline__ double seq_norm2(const double* __restrict__ a, int d) {
+  double s = 0.0;
+  for (int j = 0; j < d; ++j) s = dadd(s, dmul(a[j], a[j]));
+  return __builtin_sqrt(s);  // correctly rounded f64 sqrt on gfx950
+}
+
+// ml/impl/Utils.scala:70-80
+__device__ __forceinline__ int64_t iut(int64_t i, int64_t j) {
+  return (i <= j) ? j * (j + 1) / 2 + i : i * (i + 1) / 2 + j;
+}

@@ -1,0 +1,862 @@
+// kmeans.hip -- KMeans Lloyd-iteration body on gfx950 (MI355X).
+//
+// Replaces mllib/clustering/KMeans.scala:275-334 (the mapPartitions body and
+// its reduceByKey merge) and DistanceMeasure.scala:48-118, 189-203, 282-350.
+//
+// Pipeline per iteration (all device-resident, one stream):
+//   1. k_center_transpose  C (k x d) -> Ct (d4 x kpad), zero padded: the MFMA
+//                          B operand, read straight from L2 (2 MB at k=1024).
+//   2. k_stats_pairs/diag  computeStatistics: 0.25*dist^2 packed upper + row
+//                          minima, dist = sqrt(sequential sqdist): bit-exact.
+//   3. k_kmeans_assign     fp64 MFMA (v_mfma_f64_16x16x4f64) screen of
+//                          |x|^2 + |c|^2 - 2 x.c for a 64-row LDS tile against
+//                          every center, with a rigorous error margin; a row
+//                          whose best center is separated from every other by
+//                          more than the margin gets that center and the exact
+//                          sequential sqdist (bit-identical to the reference);
+//                          other rows are queued for step 4.
+//   4. k_assign_exact      the reference's findClosest-with-statistics loop,
+//                          restated instruction for instruction, for queued
+//                          rows (ties, near ties, NaN/Inf).
+//   5. k_hist/k_scan*/k_scatter  stable counting sort of rows by cluster.
+//   6. k_chunk_sums/k_reduce_clusters  per-cluster sum of w*x, w, w*cost in a
+//                          fixed order (deterministic run to run).
+//   7. k_update_centers    centroid = (1/w)*sum, new norm, convergence flag.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int kWaves = 8;                 // waves per assign workgroup
+constexpr int kAssignThreads = kWaves * 64;
+constexpr int kSortTile = 4096;           // rows per counting-sort tile
+constexpr int kChunkRows = 256;           // rows per deterministic partial sum
+constexpr int kMaxK = 8192;               // LDS histogram bound for the sort
+
+// ---------------------------------------------------------------- helpers
+__global__ void k_row_norms(const double* __restrict__ X, int64_t n, int d,
+                            double* __restrict__ norms) {
+  // One lane per row; rows are staged through LDS so the global reads are
+  // coalesced (64 rows x 8 columns per step).
+  __shared__ double tile[64][9];
+  const int lane = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * 64;
+  double s = 0.0;
+  for (int c0 = 0; c0 < d; c0 += 8) {
+    for (int e = lane; e < 64 * 8; e += 64) {
+      int r = e >> 3, c = e & 7;
+      int64_t gr = row0 + r;
+      tile[r][c] = (gr < n && c0 + c < d) ? X[gr * d + c0 + c] : 0.0;
+    }
+    __syncthreads();
+    int lim = min(8, d - c0);
+    for (int c = 0; c < lim; ++c) s = dadd(s, dmul(tile[lane][c], tile[lane][c]));
+    __syncthreads();
+  }
+  int64_t gr = row0 + lane;
+  if (gr < n) norms[gr] = __builtin_sqrt(s);
+}
+
+__global__ void k_center_transpose(const double* __restrict__ C, int k, int d, int d4, int kpad,
+                                   double* __restrict__ Ct) {
+  int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = (int64_t)d4 * kpad;
+  if (idx >= total) return;
+  int j = (int)(idx / kpad), i = (int)(idx % kpad);
+  Ct[idx] = (i < k && j < d) ? C[(int64_t)i * d + j] : 0.0;
+}
+
+// computeStatistics pairs (DistanceMeasure.scala:55-66, Euclidean :275-277):
+// s = 0.25 * distance * distance, distance = Math.sqrt(sqdist(c_i, c_j)).
+__global__ void k_stats_pairs(const double* __restrict__ C, int k, int d,
+                              double* __restrict__ packed) {
+  int i = blockIdx.y * 16 + threadIdx.y;
+  int j = blockIdx.x * 16 + threadIdx.x;
+  if (i >= k || j >= k || j <= i) return;
+  double dist = __builtin_sqrt(seq_sqdist(C + (int64_t)i * d, C + (int64_t)j * d, d));
+  packed[iut(i, j)] = dmul(dmul(0.25, dist), dist);
+}
+
+// diag(i) = min over j != i (DistanceMeasure.scala:62-72); min is order free.
+__global__ void k_stats_diag(int k, double* __restrict__ packed) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  if (k == 1) { packed[0] = __builtin_nan(""); return; }
+  double m = __builtin_inf();
+  for (int j = 0; j < k; ++j) {
+    if (j == i) continue;
+    double s = packed[iut(i, j)];
+    if (s < m) m = s;
+  }
+  packed[iut(i, i)] = m;
+}
+
+// --------------------------------------------------------------- assign
+// Screening state of one (row, lane) slot: smallest lower bound L1 with its
+// center index I1 and upper bound U1, and the second smallest lower bound L2.
+// A row is decided when L2 > U1: every other center is provably farther than
+// I1 by more than the combined fp64 error, so the reference's pruned loop
+// (whose prunes only skip centers that cannot win) returns I1 as well.
+struct Slot {
+  double L1, U1, L2;
+  int I1;
+};
+
+__device__ __forceinline__ void slot_merge(Slot& a, double oL1, double oU1, double oL2, int oI1) {
+  double hi = fmax(a.L1, oL1);
+  double l2 = fmin(hi, fmin(a.L2, oL2));
+  if (oL1 < a.L1 || (oL1 == a.L1 && oI1 >= 0 && (a.I1 < 0 || oI1 < a.I1))) {
+    a.L1 = oL1;
+    a.U1 = oU1;
+    a.I1 = oI1;
+  }
+  a.L2 = l2;
+}
+
+// BM rows per workgroup (BM/16 MFMA row tiles per wave); 8 waves split the
+// centers in 16-wide slabs.  X tile lives in LDS with a row stride of
+// ldsStride doubles (== 2 mod 32: conflict-free ds_read_b64 A fragments).
+template <int BM>
+__global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
+    const double* __restrict__ X, const double* __restrict__ xnorm, int64_t n, int d, int d4,
+    int ldsStride, const double* __restrict__ Ct, const double* __restrict__ C,
+    const double* __restrict__ cnorm, int k, int kpad, double marginFac,
+    int32_t* __restrict__ assign, double* __restrict__ cost, int32_t* __restrict__ slowList,
+    unsigned int* __restrict__ slowCount) {
+  constexpr int T = BM / 16;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* Xs = smem;                                   // BM x ldsStride
+  double* xnS = Xs + BM * ldsStride;                   // BM
+  double* mrg = xnS + BM;                              // kWaves x BM x 4
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t row0 = (int64_t)blockIdx.x * BM;
+  const int rows = (int)min<int64_t>(BM, n - row0);
+
+  // Stage the contiguous BM x d block of X (zero padded to d4 and BM).
+  {
+    const double* src = X + row0 * d;
+    const int total = rows * d;  // < 2^31: BM * d <= 64 * 1240
+    for (int e = tid; e < total; e += kAssignThreads) {
+      int r = e / d, c = e - r * d;
+      Xs[r * ldsStride + c] = src[e];
+    }
+    for (int e = tid; e < BM * d4; e += kAssignThreads) {
+      int r = e / d4, c = e - r * d4;
+      if (r >= rows || c >= d) Xs[r * ldsStride + c] = 0.0;
+    }
+    if (tid < BM) xnS[tid] = (tid < rows) ? xnorm[row0 + tid] : 0.0;
+  }
+  __syncthreads();
+
+  Slot st[T][4];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st[t][r] = Slot{__builtin_inf(), __builtin_inf(), __builtin_inf(), -1};
+  unsigned poison = 0;  // bit (4t + r): a NaN reached this slot
+
+  const double* arow = Xs + (lane & 15) * ldsStride + (lane >> 4);
+  for (int nb = wave * 16; nb < kpad; nb += kWaves * 16) {
+    cyc_double4 acc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+    const double* bcol = Ct + (int64_t)(lane >> 4) * kpad + nb + (lane & 15);
+    // Main loop: 8 k-steps (32 dims) per group, B fragments loaded one group ahead.
+    double bcur[8], bnxt[8];
+    const int groups = d4 / 32;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) bcur[s] = (s * 4 < d4) ? bcol[(int64_t)(s * 4) * kpad] : 0.0;
+    for (int g = 0; g < groups; ++g) {
+      const int kb = g * 32;
+      if (g + 1 < groups) {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) bnxt[s] = bcol[(int64_t)(kb + 32 + s * 4) * kpad];
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+          double a = arow[t * 16 * ldsStride + kb + s * 4];
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bcur[s], acc[t], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s) bcur[s] = bnxt[s];
+    }
+    // Tail k-steps (d4 not a multiple of 32).
+    for (int kb = groups * 32; kb < d4; kb += 4) {
+      double b = bcol[(int64_t)kb * kpad];
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        double a = arow[t * 16 * ldsStride + kb];
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
+      }
+    }
+    // Epilogue: D[row = (lane>>4) + 4 r][col = lane & 15] for f64 16x16x4.
+    const int c = nb + (lane & 15);
+    if (c < k) {
+      const double cn = cnorm[c];
+      const double cn2 = cn * cn;
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = t * 16 + (lane >> 4) + 4 * r;
+          const double xn = xnS[row];
+          const double approx = (xn * xn + cn2) - 2.0 * acc[t][r];
+          const double sm = xn + cn;
+          const double M = (sm * sm) * marginFac;
+          const double L = approx - M, U = approx + M;
+          if (!(L == L) || !(U == U)) poison |= 1u << (4 * t + r);
+          Slot& S = st[t][r];
+          if (L < S.L1) {
+            S.L2 = S.L1;
+            S.L1 = L;
+            S.U1 = U;
+            S.I1 = c;
+          } else if (L < S.L2) {
+            S.L2 = L;
+          }
+        }
+      }
+    }
+  }
+
+  // Reduce each slot over the 16 lanes that hold the same row.
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      Slot& S = st[t][r];
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        double oL1 = __shfl_xor(S.L1, m), oU1 = __shfl_xor(S.U1, m), oL2 = __shfl_xor(S.L2, m);
+        int oI1 = __shfl_xor(S.I1, m);
+        slot_merge(S, oL1, oU1, oL2, oI1);
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) poison |= __shfl_xor(poison, m);
+
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = t * 16 + (lane >> 4) + 4 * r;
+        double* m = mrg + ((size_t)wave * BM + row) * 4;
+        const Slot& S = st[t][r];
+        m[0] = S.L1;
+        m[1] = S.U1;
+        m[2] = ((poison >> (4 * t + r)) & 1u) ? -__builtin_inf() : S.L2;
+        m[3] = (double)S.I1;
+      }
+    }
+  }
+  __syncthreads();
+
+  // One lane per row: merge the 8 waves, then decide or queue.
+  if (tid < rows) {
+    const int row = tid;
+    Slot S{__builtin_inf(), __builtin_inf(), __builtin_inf(), -1};
+    for (int w = 0; w < kWaves; ++w) {
+      const double* m = mrg + ((size_t)w * BM + row) * 4;
+      slot_merge(S, m[0], m[1], m[2], (int)m[3]);
+    }
+    const int64_t grow = row0 + row;
+    if (S.I1 >= 0 && S.L2 > S.U1) {
+      // Exact fastSquaredDistance(centers(I1), point) = Vectors.sqdist(c, x).
+      const double* crow = C + (int64_t)S.I1 * d;
+      const double* xrow = Xs + row * ldsStride;
+      double s = 0.0;
+      for (int j = 0; j < d; ++j) {
+        double sc = dsub(crow[j], xrow[j]);
+        s = dadd(s, dmul(sc, sc));
+      }
+      assign[grow] = S.I1;
+      cost[grow] = s;
+    } else {
+      unsigned slot = atomicAdd(slowCount, 1u);
+      slowList[slot] = (int32_t)grow;
+    }
+  }
+}
+
+// EuclideanDistanceMeasure.findClosest with statistics, DistanceMeasure.scala:
+// 282-313, for the rows the screen could not decide.
+__global__ void k_assign_exact(const double* __restrict__ X, const double* __restrict__ xnorm,
+                               int d, const double* __restrict__ C,
+                               const double* __restrict__ cnorm, int k,
+                               const double* __restrict__ stats,
+                               const int32_t* __restrict__ slowList,
+                               const unsigned int* __restrict__ slowCount,
+                               int32_t* __restrict__ assign, double* __restrict__ cost) {
+  const unsigned cnt = *slowCount;
+  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < cnt;
+       idx += gridDim.x * blockDim.x) {
+  const int64_t r = slowList[idx];
+  const double* x = X + r * d;
+  const double xn = xnorm[r];
+  double best = seq_sqdist(C, x, d);
+  int bestIndex = 0;
+  if (!(best < stats[0])) {
+    for (int i = 1; i < k; ++i) {
+      double normDiff = dsub(cnorm[i], xn);
+      double lowerBound = dmul(normDiff, normDiff);
+      if (lowerBound < best) {
+        if (stats[iut(i, bestIndex)] < best) {
+          double dd = seq_sqdist(C + (int64_t)i * d, x, d);
+          if (dd < stats[iut(i, i)]) {
+            best = dd;
+            bestIndex = i;
+            break;
+          }
+          if (dd < best) {
+            best = dd;
+            bestIndex = i;
+          }
+        }
+      }
+    }
+  }
+  assign[r] = bestIndex;
+  cost[r] = best;
+  }
+}
+
+// ------------------------------------------------------- counting sort
+__global__ void k_hist(const int32_t* __restrict__ assign, int64_t n, int k,
+                       int32_t* __restrict__ hist) {
+  extern __shared__ int32_t cnt[];
+  for (int c = threadIdx.x; c < k; c += blockDim.x) cnt[c] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * kSortTile;
+  const int64_t r1 = min<int64_t>(n, r0 + kSortTile);
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) atomicAdd(&cnt[assign[r]], 1);
+  __syncthreads();
+  for (int c = threadIdx.x; c < k; c += blockDim.x) hist[(int64_t)blockIdx.x * k + c] = cnt[c];
+}
+
+// Per cluster: exclusive running offset over tiles (in place) and the total.
+__global__ void k_scan_tiles(int32_t* __restrict__ hist, int tiles, int k,
+                             int64_t* __restrict__ total) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= k) return;
+  int64_t run = 0;
+  for (int t = 0; t < tiles; ++t) {
+    int32_t h = hist[(int64_t)t * k + c];
+    hist[(int64_t)t * k + c] = (int32_t)run;
+    run += h;
+  }
+  total[c] = run;
+}
+
+// Single block: cluster start offsets and chunk start offsets (exclusive scans).
+__global__ void k_scan_clusters(const int64_t* __restrict__ total, int k,
+                                int64_t* __restrict__ cstart, int64_t* __restrict__ chunkStart) {
+  __shared__ int64_t s_rows[1024], s_chunks[1024];
+  const int tid = threadIdx.x;
+  const int per = (k + 1023) / 1024;
+  int64_t rows = 0, chunks = 0;
+  for (int q = 0; q < per; ++q) {
+    int c = tid * per + q;
+    if (c < k) {
+      rows += total[c];
+      chunks += (total[c] + kChunkRows - 1) / kChunkRows;
+    }
+  }
+  s_rows[tid] = rows;
+  s_chunks[tid] = chunks;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    int64_t a = tid >= off ? s_rows[tid - off] : 0, b = tid >= off ? s_chunks[tid - off] : 0;
+    __syncthreads();
+    s_rows[tid] += a;
+    s_chunks[tid] += b;
+    __syncthreads();
+  }
+  int64_t rbase = tid ? s_rows[tid - 1] : 0, cbase = tid ? s_chunks[tid - 1] : 0;
+  for (int q = 0; q < per; ++q) {
+    int c = tid * per + q;
+    if (c < k) {
+      cstart[c] = rbase;
+      chunkStart[c] = cbase;
+      rbase += total[c];
+      cbase += (total[c] + kChunkRows - 1) / kChunkRows;
+    }
+  }
+  if (tid == 1023) {
+    cstart[k] = s_rows[1023];
+    chunkStart[k] = s_chunks[1023];
+  }
+}
+
+// One wave per tile, rows in order: perm[cstart[c] + tileOffset[c] + rank] = row.
+__global__ void k_scatter(const int32_t* __restrict__ assign, int64_t n, int k,
+                          const int32_t* __restrict__ tileOff, const int64_t* __restrict__ cstart,
+                          int32_t* __restrict__ perm) {
+  extern __shared__ int64_t pos[];
+  const int lane = threadIdx.x;
+  for (int c = lane; c < k; c += 64) pos[c] = cstart[c] + tileOff[(int64_t)blockIdx.x * k + c];
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * kSortTile;
+  const int64_t r1 = min<int64_t>(n, r0 + kSortTile);
+  for (int64_t base = r0; base < r1; base += 64) {
+    const int64_t r = base + lane;
+    const int c = (r < r1) ? assign[r] : -1;
+    int prior = 0, last = lane;
+    for (int j = 0; j < 64; ++j) {
+      int cj = __shfl(c, j);
+      if (cj == c) {
+        if (j < lane) ++prior;
+        last = j;
+      }
+    }
+    int64_t p = (c >= 0) ? pos[c] + prior : 0;
+    __builtin_amdgcn_wave_barrier();
+    if (c >= 0) {
+      perm[p] = (int32_t)r;
+      if (last == lane) pos[c] = p + 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Partial sums of up to kChunkRows rows of one cluster, rows in index order.
+__global__ void k_chunk_sums(const double* __restrict__ X, int d, const double* __restrict__ w,
+                             const double* __restrict__ cost, const int32_t* __restrict__ perm,
+                             const int64_t* __restrict__ cstart,
+                             const int64_t* __restrict__ chunkStart, int k,
+                             double* __restrict__ part, double* __restrict__ pw,
+                             double* __restrict__ pc) {
+  const int64_t ch = blockIdx.x;
+  if (ch >= chunkStart[k]) return;
+  // cluster = last c with chunkStart[c] <= ch (binary search, k+1 entries)
+  int lo = 0, hi = k;
+  while (hi - lo > 1) {
+    int mid = (lo + hi) >> 1;
+    if (chunkStart[mid] <= ch) lo = mid; else hi = mid;
+  }
+  const int c = lo;
+  const int64_t first = cstart[c] + (ch - chunkStart[c]) * kChunkRows;
+  const int64_t last = min<int64_t>(cstart[c + 1], first + kChunkRows);
+  for (int j = threadIdx.x; j < d; j += blockDim.x) {
+    double s = 0.0;
+    if (w) {
+      for (int64_t p = first; p < last; ++p) {
+        const int64_t r = perm[p];
+        s = dadd(s, dmul(w[r], X[r * d + j]));
+      }
+    } else {
+      for (int64_t p = first; p < last; ++p) s = dadd(s, X[(int64_t)perm[p] * d + j]);
+    }
+    part[ch * d + j] = s;
+  }
+  if (threadIdx.x == 0) {
+    double sw = 0.0, sc = 0.0;
+    for (int64_t p = first; p < last; ++p) {
+      const int64_t r = perm[p];
+      const double wt = w ? w[r] : 1.0;
+      sw = dadd(sw, wt);
+      sc = dadd(sc, dmul(cost[r], wt));
+    }
+    pw[ch] = sw;
+    pc[ch] = sc;
+  }
+}
+
+// Fold a cluster's chunks in chunk order and add into the caller's sums.
+__global__ void k_reduce_clusters(const double* __restrict__ part, const double* __restrict__ pw,
+                                  const double* __restrict__ pc,
+                                  const int64_t* __restrict__ chunkStart, int d,
+                                  double* __restrict__ sums, double* __restrict__ wsum,
+                                  double* __restrict__ ccost) {
+  const int c = blockIdx.x;
+  const int64_t a = chunkStart[c], b = chunkStart[c + 1];
+  if (a == b) {
+    if (threadIdx.x == 0) ccost[c] = 0.0;
+    return;
+  }
+  for (int j = threadIdx.x; j < d; j += blockDim.x) {
+    double s = 0.0;
+    for (int64_t ch = a; ch < b; ++ch) s = dadd(s, part[ch * d + j]);
+    sums[(int64_t)c * d + j] = dadd(sums[(int64_t)c * d + j], s);
+  }
+  if (threadIdx.x == 0) {
+    double sw = 0.0, sc = 0.0;
+    for (int64_t ch = a; ch < b; ++ch) {
+      sw = dadd(sw, pw[ch]);
+      sc = dadd(sc, pc[ch]);
+    }
+    wsum[c] = dadd(wsum[c], sw);
+    ccost[c] = sc;
+  }
+}
+
+// Single block, fixed-shape tree: cost_sum += sum_c ccost[c].
+__global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __restrict__ out) {
+  __shared__ double s[256];
+  double a = 0.0;
+  for (int c = threadIdx.x; c < k; c += 256) a = dadd(a, ccost[c]);
+  s[threadIdx.x] = a;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) s[threadIdx.x] = dadd(s[threadIdx.x], s[threadIdx.x + off]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = dadd(out[0], s[0]);
+}
+
+// centroid (DistanceMeasure.scala:200-203: scal(1/w, sum); new VectorWithNorm)
+// and isCenterConverged (:345-350).  Single block of 1024 threads.
+__global__ void k_update_centers(double* __restrict__ C, double* __restrict__ cnorm,
+                                 const double* __restrict__ sums, const double* __restrict__ wsum,
+                                 int k, int d, double eps2, int32_t* __restrict__ converged) {
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) s_ok = 1;
+  __syncthreads();
+  int ok = 1;
+  for (int c = threadIdx.x; c < k; c += blockDim.x) {
+    const double w = wsum[c];
+    if (!(w > 0)) continue;
+    const double a = 1.0 / w;
+    double* crow = C + (int64_t)c * d;
+    const double* srow = sums + (int64_t)c * d;
+    double moved = 0.0, nn = 0.0;
+    for (int j = 0; j < d; ++j) {
+      const double v = dmul(a, srow[j]);
+      const double sc = dsub(v, crow[j]);
+      moved = dadd(moved, dmul(sc, sc));
+      nn = dadd(nn, dmul(v, v));
+      crow[j] = v;
+    }
+    cnorm[c] = __builtin_sqrt(nn);
+    if (!(moved <= eps2)) ok = 0;
+  }
+  if (!ok) atomicAnd(&s_ok, 0);
+  __syncthreads();
+  if (threadIdx.x == 0 && converged) *converged = s_ok;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ plan
+struct cyc_kmeans_plan_s {
+  int d = 0, k = 0, d4 = 0, kpad = 0, bm = 0, ldsStride = 0;
+  int64_t max_rows = 0;
+  size_t assignLds = 0;
+  std::mutex mu;
+  cyc::DeviceBuffer ct, stats, slowList, slowCount, assignTmp, costTmp;
+  cyc::DeviceBuffer hist, total, cstart, chunkStart, perm, part, pw, pc, ccost;
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+  ~cyc_kmeans_plan_s() {
+    for (auto& e : events) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+  }
+};
+
+namespace {
+
+int pick_bm(int d4, int& stride, size_t& lds) {
+  const int cands[3] = {64, 32, 16};
+  for (int bm : cands) {
+    int s = d4 + ((2 - d4 % 32) + 32) % 32;  // stride == 2 (mod 32)
+    size_t bytes = ((size_t)bm * s + bm + (size_t)kWaves * bm * 4) * sizeof(double);
+    if (bytes <= 160 * 1024) {
+      stride = s;
+      lds = bytes;
+      return bm;
+    }
+  }
+  return 0;
+}
+
+template <int BM>
+int launch_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n,
+                  const double* C, const double* cnorm, int32_t* assign, double* cost,
+                  hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    CYC_HIP(hipFuncSetAttribute((const void*)k_kmeans_assign<BM>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const double marginFac = (double)(p->d + 16) * 0x1p-46;
+  const int64_t blocks = (n + BM - 1) / BM;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (p->timing) {
+    CYC_HIP(hipEventCreate(&e0));
+    CYC_HIP(hipEventCreate(&e1));
+    CYC_HIP(hipEventRecord(e0, st));
+  }
+  hipLaunchKernelGGL(k_kmeans_assign<BM>, dim3((unsigned)blocks), dim3(kAssignThreads),
+                     p->assignLds, st, X, xnorm, n, p->d, p->d4, p->ldsStride,
+                     (const double*)p->ct.ptr, C, cnorm, p->k, p->kpad, marginFac, assign, cost,
+                     (int32_t*)p->slowList.ptr, (unsigned int*)p->slowCount.ptr);
+  CYC_LAUNCH_CHECK("k_kmeans_assign");
+  if (p->timing) {
+    CYC_HIP(hipEventRecord(e1, st));
+    p->events.emplace_back(e0, e1);
+  }
+  return CYC_OK;
+}
+
+int do_stats(cyc_kmeans_plan p, const double* C, hipStream_t st) {
+  const int k = p->k, d = p->d;
+  {
+    int64_t total = (int64_t)p->d4 * p->kpad;
+    hipLaunchKernelGGL(k_center_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       st, C, k, d, p->d4, p->kpad, (double*)p->ct.ptr);
+    CYC_LAUNCH_CHECK("k_center_transpose");
+  }
+  dim3 g((k + 15) / 16, (k + 15) / 16);
+  hipLaunchKernelGGL(k_stats_pairs, g, dim3(16, 16), 0, st, C, k, d, (double*)p->stats.ptr);
+  CYC_LAUNCH_CHECK("k_stats_pairs");
+  hipLaunchKernelGGL(k_stats_diag, dim3((k + 255) / 256), dim3(256), 0, st, k,
+                     (double*)p->stats.ptr);
+  CYC_LAUNCH_CHECK("k_stats_diag");
+  return CYC_OK;
+}
+
+int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n,
+              const double* C, const double* cnorm, int32_t* assign, double* cost,
+              int64_t* n_exact_out, hipStream_t st) {
+  CYC_HIP(hipMemsetAsync(p->slowCount.ptr, 0, sizeof(unsigned int), st));
+  int rc = CYC_OK;
+  switch (p->bm) {
+    case 64: rc = launch_assign<64>(p, X, xnorm, n, C, cnorm, assign, cost, st); break;
+    case 32: rc = launch_assign<32>(p, X, xnorm, n, C, cnorm, assign, cost, st); break;
+    default: rc = launch_assign<16>(p, X, xnorm, n, C, cnorm, assign, cost, st); break;
+  }
+  if (rc) return rc;
+  // Exact emulation of the reference loop for undecided rows.  The queue
+  // length is read back only when the caller asks for it; otherwise a
+  // grid-stride launch drains whatever the queue holds without a host sync.
+  unsigned int h_slow = 0;
+  if (n_exact_out) {
+    CYC_HIP(hipMemcpyAsync(&h_slow, p->slowCount.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    CYC_HIP(hipStreamSynchronize(st));
+    *n_exact_out = h_slow;
+    if (h_slow) {
+      hipLaunchKernelGGL(k_assign_exact, dim3((h_slow + 63) / 64), dim3(64), 0, st, X, xnorm,
+                         p->d, C, cnorm, p->k, (const double*)p->stats.ptr,
+                         (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr,
+                         assign, cost);
+      CYC_LAUNCH_CHECK("k_assign_exact");
+    }
+  } else {
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_assign_exact, dim3(grid), dim3(256), 0, st, X, xnorm,
+                       p->d, C, cnorm, p->k, (const double*)p->stats.ptr,
+                       (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr, assign,
+                       cost);
+    CYC_LAUNCH_CHECK("k_assign_exact");
+  }
+  return CYC_OK;
+}
+
+int ensure_rows(cyc_kmeans_plan p, int64_t n) {
+  if (n <= p->max_rows && p->slowList.ptr) return CYC_OK;
+  int rc;
+  if ((rc = p->slowList.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1)))) return rc;
+  p->max_rows = std::max(p->max_rows, n);
+  return CYC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cyc_row_norms_dev(const double* X, int64_t n, int32_t d, double* norms, void* stream) {
+  CYC_REQUIRE(n >= 0 && d > 0, "n >= 0 and d > 0");
+  if (n == 0) return CYC_OK;
+  hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
+                     cyc::as_stream(stream), X, n, d, norms);
+  CYC_LAUNCH_CHECK("k_row_norms");
+  return CYC_OK;
+}
+
+int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_plan* plan) {
+  CYC_REQUIRE(plan != nullptr, "plan must not be null");
+  CYC_REQUIRE(d > 0, "Number of features must be positive");
+  CYC_REQUIRE(k >= 1, "Number of clusters must be positive but got " + std::to_string(k));
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    cyc::set_error("no HIP device visible");
+    return CYC_ERR_NO_DEVICE;
+  }
+  if (k > kMaxK) {
+    cyc::set_error("k > 8192 is not supported by the device counting sort");
+    return CYC_ERR_UNSUPPORTED;
+  }
+  auto* p = new cyc_kmeans_plan_s();
+  p->d = d;
+  p->k = k;
+  p->d4 = (int)cyc::round_up(d, 4);
+  p->kpad = (int)cyc::round_up(k, 16);
+  p->bm = pick_bm(p->d4, p->ldsStride, p->assignLds);
+  if (p->bm == 0) {
+    delete p;
+    cyc::set_error("d > 1240 is not supported by the LDS-resident assign kernel");
+    return CYC_ERR_UNSUPPORTED;
+  }
+  int rc;
+  if ((rc = p->ct.reserve(sizeof(double) * (size_t)p->d4 * p->kpad)) ||
+      (rc = p->stats.reserve(sizeof(double) * ((size_t)k * (k + 1) / 2))) ||
+      (rc = p->slowCount.reserve(64)) || (rc = ensure_rows(p, std::max<int64_t>(max_rows, 1)))) {
+    delete p;
+    return rc;
+  }
+  *plan = p;
+  return CYC_OK;
+}
+
+int cyc_kmeans_plan_destroy(cyc_kmeans_plan plan) {
+  delete plan;
+  return CYC_OK;
+}
+
+int cyc_kmeans_plan_set_timing(cyc_kmeans_plan p, int enable) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  std::lock_guard<std::mutex> g(p->mu);
+  p->timing = enable != 0;
+  return CYC_OK;
+}
+
+int cyc_kmeans_plan_get_timing(cyc_kmeans_plan p, double* total_ms, int64_t* launches) {
+  CYC_REQUIRE(p != nullptr && total_ms != nullptr && launches != nullptr,
+              "plan and outputs must not be null");
+  std::lock_guard<std::mutex> g(p->mu);
+  double tot = 0.0;
+  for (auto& e : p->events) {
+    CYC_HIP(hipEventSynchronize(e.second));
+    float ms = 0.f;
+    CYC_HIP(hipEventElapsedTime(&ms, e.first, e.second));
+    tot += ms;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  *total_ms = tot;
+  *launches = (int64_t)p->events.size();
+  p->events.clear();
+  return CYC_OK;
+}
+
+int cyc_kmeans_stats_dev(cyc_kmeans_plan p, const double* C, double* stats_out, void* stream) {
+  CYC_REQUIRE(p != nullptr && C != nullptr, "plan and centers must not be null");
+  std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  int rc = do_stats(p, C, st);
+  if (rc) return rc;
+  if (stats_out)
+    CYC_HIP(hipMemcpyAsync(stats_out, p->stats.ptr, sizeof(double) * ((size_t)p->k * (p->k + 1) / 2),
+                           hipMemcpyDeviceToDevice, st));
+  return CYC_OK;
+}
+
+int cyc_kmeans_assign_dev(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n,
+                          const double* C, const double* cnorm, int32_t* assign, double* cost,
+                          int64_t* n_exact_out, void* stream) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  CYC_REQUIRE(assign != nullptr && cost != nullptr, "assign and cost must not be null");
+  if (n_exact_out) *n_exact_out = 0;
+  if (n == 0) return CYC_OK;
+  std::lock_guard<std::mutex> g(p->mu);
+  int rc = ensure_rows(p, n);
+  if (rc) return rc;
+  return do_assign(p, X, xnorm, n, C, cnorm, assign, cost, n_exact_out, cyc::as_stream(stream));
+}
+
+int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* xnorm,
+                              const double* weights, int64_t n, const double* C,
+                              const double* cnorm, double* sums, double* wsum, double* cost_sum,
+                              int32_t* assign, double* cost, void* stream) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  CYC_REQUIRE(sums && wsum && cost_sum, "sums, wsum and cost_sum must not be null");
+  if (n == 0) return CYC_OK;
+  std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  const int k = p->k, d = p->d;
+  int rc = ensure_rows(p, n);
+  if (rc) return rc;
+  if (!assign) {
+    if ((rc = p->assignTmp.reserve(sizeof(int32_t) * (size_t)n))) return rc;
+    assign = (int32_t*)p->assignTmp.ptr;
+  }
+  if (!cost) {
+    if ((rc = p->costTmp.reserve(sizeof(double) * (size_t)n))) return rc;
+    cost = (double*)p->costTmp.ptr;
+  }
+  if ((rc = do_stats(p, C, st))) return rc;
+  if ((rc = do_assign(p, X, xnorm, n, C, cnorm, assign, cost, nullptr, st))) return rc;
+
+  const int tiles = (int)((n + kSortTile - 1) / kSortTile);
+  const int64_t maxChunks = (n + kChunkRows - 1) / kChunkRows + k;
+  if ((rc = p->hist.reserve(sizeof(int32_t) * (size_t)tiles * k)) ||
+      (rc = p->total.reserve(sizeof(int64_t) * (size_t)k)) ||
+      (rc = p->cstart.reserve(sizeof(int64_t) * (size_t)(k + 1))) ||
+      (rc = p->chunkStart.reserve(sizeof(int64_t) * (size_t)(k + 1))) ||
+      (rc = p->perm.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = p->part.reserve(sizeof(double) * (size_t)maxChunks * d)) ||
+      (rc = p->pw.reserve(sizeof(double) * (size_t)maxChunks)) ||
+      (rc = p->pc.reserve(sizeof(double) * (size_t)maxChunks)) ||
+      (rc = p->ccost.reserve(sizeof(double) * (size_t)k)))
+    return rc;
+  int32_t* hist = (int32_t*)p->hist.ptr;
+  hipLaunchKernelGGL(k_hist, dim3(tiles), dim3(256), sizeof(int32_t) * k, st, assign, n, k, hist);
+  CYC_LAUNCH_CHECK("k_hist");
+  hipLaunchKernelGGL(k_scan_tiles, dim3((k + 255) / 256), dim3(256), 0, st, hist, tiles, k,
+                     (int64_t*)p->total.ptr);
+  CYC_LAUNCH_CHECK("k_scan_tiles");
+  hipLaunchKernelGGL(k_scan_clusters, dim3(1), dim3(1024), 0, st, (const int64_t*)p->total.ptr, k,
+                     (int64_t*)p->cstart.ptr, (int64_t*)p->chunkStart.ptr);
+  CYC_LAUNCH_CHECK("k_scan_clusters");
+  hipLaunchKernelGGL(k_scatter, dim3(tiles), dim3(64), sizeof(int64_t) * k, st, assign, n, k,
+                     hist, (const int64_t*)p->cstart.ptr, (int32_t*)p->perm.ptr);
+  CYC_LAUNCH_CHECK("k_scatter");
+  // Number of chunks is data dependent; launch the upper bound and let the
+  // surplus blocks (ch >= chunkStart[k]) exit.
+  hipLaunchKernelGGL(k_chunk_sums, dim3((unsigned)maxChunks), dim3(256), 0, st, X, d, weights,
+                     cost, (const int32_t*)p->perm.ptr, (const int64_t*)p->cstart.ptr,
+                     (const int64_t*)p->chunkStart.ptr, k, (double*)p->part.ptr,
+                     (double*)p->pw.ptr, (double*)p->pc.ptr);
+  CYC_LAUNCH_CHECK("k_chunk_sums");
+  hipLaunchKernelGGL(k_reduce_clusters, dim3(k), dim3(256), 0, st, (const double*)p->part.ptr,
+                     (const double*)p->pw.ptr, (const double*)p->pc.ptr,
+                     (const int64_t*)p->chunkStart.ptr, d, sums, wsum, (double*)p->ccost.ptr);
+  CYC_LAUNCH_CHECK("k_reduce_clusters");
+  hipLaunchKernelGGL(k_cost_total, dim3(1), dim3(256), 0, st, (const double*)p->ccost.ptr, k,
+                     cost_sum);
+  CYC_LAUNCH_CHECK("k_cost_total");
+  return CYC_OK;
+}
+
+int cyc_kmeans_update_dev(cyc_kmeans_plan p, double* C, double* cnorm, const double* sums,
+                          const double* wsum, double epsilon, int32_t* converged_out,
+                          void* stream) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  CYC_REQUIRE(epsilon >= 0, "epsilon must be nonnegative");
+  std::lock_guard<std::mutex> g(p->mu);
+  hipLaunchKernelGGL(k_update_centers, dim3(1), dim3(1024), 0, cyc::as_stream(stream), C, cnorm,
+                     sums, wsum, p->k, p->d, epsilon * epsilon, converged_out);
+  CYC_LAUNCH_CHECK("k_update_centers");
+  return CYC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,110 @@
+/*
+ * cyclone.h -- C ABI of libcyclone, the MI355X (gfx950) backend for the MLlib
+ * linear-algebra hot path of wmeddie/CycloneML (Spark 3.3 MLlib).
+ *
+ * Two layers:
+ *   - device-pointer entry points (suffix _dev): operands already resident in
+ *     HBM, a HIP stream passed as void*.  These are what a multi-GPU driver
+ *     (one process per GPU, RCCL all-reduce of the outputs) calls.
+ *   - host-pointer entry points over library-owned resident datasets
+ *     (cyc_dataset_*): what a JVM shim (JNI / Panama)
+ *     binds in place of the per-partition Scala loops.
+ *
+ * Conventions
+ *   - Every function returns CYC_OK (0) or a CYC_ERR_* code; the message is
+ *     thread-local and read with cyc_last_error().  CYC_ERR_INVALID_ARG
+ *     carries the reference's `require` text (IllegalArgumentException).
+ *   - All floating point is IEEE fp64; indices are int32 (Spark's Int) and row
+ *     counts int64.  Dense matrices are row-major (InstanceBlock / an RDD of
+ *     DenseVector rows); CSR is (rowptr int64[n+1], colidx int32, values).
+ *   - Accumulating outputs (sums, gradients, Gramians, loss/weight sums) are
+ *     ADDED to, like the reference aggregators' `add`; zero them first.
+ *   - There is no CPU fallback: without a gfx950 device every entry point
+ *     returns CYC_ERR_NO_DEVICE.
+ *   - Calls on one plan/dataset are serialized by the caller (a plan owns
+ *     scratch memory); distinct plans may be used from distinct threads.
+ */
+#ifndef CYCLONE_H
+#define CYCLONE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CYC_OK 0
+#define CYC_ERR_INVALID_ARG 1 /* a reference `require` failed              */
+#define CYC_ERR_HIP 2         /* HIP runtime error                          */
+#define CYC_ERR_ALLOC 3       /* device allocation failed                   */
+#define CYC_ERR_UNSUPPORTED 4 /* shape outside what the kernels support     */
+#define CYC_ERR_NO_DEVICE 5   /* no usable gfx950 device                    */
+
+/* ------------------------------------------------------------------ misc */
+const char* cyc_last_error(void);
+int cyc_version(void); /* major*10000 + minor*100 + patch */
+int cyc_device_count(int* count);
+int cyc_set_device(int device);
+int cyc_synchronize(void* stream);
+
+/* ------------------------------------------------------------- vectors */
+/* norms[i] = Vectors.norm(row i, 2.0) bit-exactly (mllib/linalg/Vectors.scala:
+ * 489-514, sequential sum of squares, correctly rounded sqrt).              */
+int cyc_row_norms_dev(const double* X, int64_t n, int32_t d, double* norms, void* stream);
+
+/* ---------------------------------------------------------------- KMeans */
+/* Replaces the Lloyd-iteration body of mllib/clustering/KMeans.scala:275-334:
+ * DistanceMeasure.computeStatistics[Distributedly] (DistanceMeasure.scala:
+ * 48-118), EuclideanDistanceMeasure.findClosest with statistics (:282-313),
+ * updateClusterSum / clusterWeightSum / costAccum (KMeans.scala:299-304) and
+ * centroid + isCenterConverged (:322-330).  Dense points and centers.
+ *
+ * Assignments and per-point costs are bit-identical to the reference's
+ * findClosest.  Sums/weights/cost are summed in a fixed (deterministic) order
+ * that differs from a Spark partitioning, so they agree to ~1e-15 relative.  */
+typedef struct cyc_kmeans_plan_s* cyc_kmeans_plan;
+
+int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_plan* plan);
+int cyc_kmeans_plan_destroy(cyc_kmeans_plan plan);
+
+/* Measurement hook (bench.py's roofline): when enabled, every launch of the
+ * dominant kernel (the MFMA assign kernel) is bracketed by HIP events on the
+ * caller's stream.  get_timing waits for the recorded events, returns the
+ * summed kernel time in ms and the launch count, and resets the record. */
+int cyc_kmeans_plan_set_timing(cyc_kmeans_plan plan, int enable);
+int cyc_kmeans_plan_get_timing(cyc_kmeans_plan plan, double* total_ms, int64_t* launches);
+
+/* computeStatistics for the given centers: fills the plan's packed k(k+1)/2
+ * statistics (and copies them to stats_out if non-NULL, device memory). */
+int cyc_kmeans_stats_dev(cyc_kmeans_plan plan, const double* C, double* stats_out, void* stream);
+
+/* findClosest(centers, stats, point) for n points (stats from the last
+ * cyc_kmeans_stats_dev on this plan).  assign[n], cost[n] device outputs.
+ * *n_exact_out (host, may be NULL) receives how many points needed the
+ * exact-emulation path (ties / near ties of the fp64 screening). */
+int cyc_kmeans_assign_dev(cyc_kmeans_plan plan, const double* X, const double* xnorm, int64_t n,
+                          const double* C, const double* cnorm, int32_t* assign, double* cost,
+                          int64_t* n_exact_out, void* stream);
+
+/* One partition's contribution to a Lloyd iteration: statistics + assign +
+ * per-cluster sums.  sums[k*d] += sum of w*x, wsum[k] += sum of w,
+ * cost_sum[0] += sum of w*cost.  weights may be NULL (unit weights).
+ * assign/cost may be NULL.  All pointers are device memory. */
+int cyc_kmeans_accumulate_dev(cyc_kmeans_plan plan, const double* X, const double* xnorm,
+                              const double* weights, int64_t n, const double* C,
+                              const double* cnorm, double* sums, double* wsum, double* cost_sum,
+                              int32_t* assign, double* cost, void* stream);
+
+/* centroid = scal(1/wsum, sum) and a fresh norm for every cluster with
+ * wsum > 0; converged_out (device int32) = 1 iff every such center moved by
+ * fastSquaredDistance <= epsilon^2. C and cnorm are updated in place. */
+int cyc_kmeans_update_dev(cyc_kmeans_plan plan, double* C, double* cnorm, const double* sums,
+                          const double* wsum, double epsilon, int32_t* converged_out,
+                          void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CYCLONE_H */

@@ -1,0 +1,608 @@
+/*
+ * cyclone_oracle.c -- CPU restatement of the reference's MLlib hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * kernels in cycloneml_amd/csrc.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.  The product path never links it.
+ *
+ * Every function restates one Scala loop of the reference (wmeddie/CycloneML,
+ * a Spark 3.3.0-SNAPSHOT MLlib tree mounted at /root/reference) in the same
+ * evaluation order.  Compile with -ffp-contract=off: the JVM never fuses
+ * a*b+c, so neither may we.  Where the reference calls netlib BLAS
+ * (dev.ludovic.netlib 2.2.0, not present in the container) the restatement
+ * follows the published netlib reference loops (Fortran BLAS dgemv/dgemm/
+ * dspr/ddot/daxpy/dscal), the algorithm JavaBLAS / f2j implement.
+ *
+ * Parity pinning: see DESIGN.md "Oracle" -- the reference's known-answer
+ * tests (RowMatrixSuite gram, KMeansSuite weighted centers, BLASSuite,
+ * aggregator suites' naive loops) are committed under tests/golden and
+ * checked by tests/test_oracle_golden.py.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------ */
+/* Vectors / MLUtils                                                        */
+/* ------------------------------------------------------------------------ */
+
+/* mllib/linalg/Vectors.scala:489-514 (p == 2): sum += v*v; sqrt(sum) */
+double orc_norm2(const double* x, int64_t n) {
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) s += x[i] * x[i];
+  return sqrt(s);
+}
+
+/* mllib/linalg/Vectors.scala:580-587 dense/dense sqdist:
+ *   score = v1(k) - v2(k); squaredDistance += score * score            */
+double orc_sqdist(const double* a, const double* b, int64_t n) {
+  double s = 0.0;
+  for (int64_t k = 0; k < n; ++k) {
+    double score = a[k] - b[k];
+    s += score * score;
+  }
+  return s;
+}
+
+/* mllib/linalg/Vectors.scala:598-622 sqdist(sparse v1, dense v2) */
+double orc_sqdist_sparse_dense(const int32_t* idx, const double* val, int64_t nnz,
+                               const double* dense, int64_t n) {
+  int64_t kv1 = 0;
+  int64_t iv1 = nnz > 0 ? idx[0] : -1;
+  double s = 0.0;
+  for (int64_t kv2 = 0; kv2 < n; ++kv2) {
+    double score;
+    if (kv2 != iv1) {
+      score = dense[kv2];
+    } else {
+      score = val[kv1] - dense[kv2];
+      if (kv1 < nnz - 1) { kv1 += 1; iv1 = idx[kv1]; }
+    }
+    s += score * score;
+  }
+  return s;
+}
+
+/* mllib/linalg/BLAS.scala:153-169 dot(sparse x, dense y): sum += xv(k) * y(xi(k)) */
+double orc_dot_sparse_dense(const int32_t* idx, const double* val, int64_t nnz,
+                            const double* dense) {
+  double s = 0.0;
+  for (int64_t k = 0; k < nnz; ++k) s += val[k] * dense[idx[k]];
+  return s;
+}
+
+/* mllib/util/MLUtils.scala:44-50 EPSILON = 2^-52 (the halving loop) */
+static double orc_epsilon(void) {
+  double eps = 1.0;
+  while ((1.0 + (eps / 2.0)) != 1.0) eps /= 2.0;
+  return eps;
+}
+
+/* mllib/util/MLUtils.scala:533-576 fastSquaredDistance, v1 dense (a center)
+ * and v2 sparse (a libsvm point): the norm-trick branch :560-573 with
+ * precision = 1e-6.  v1.isInstanceOf[DenseVector] && v2 dense takes sqdist
+ * directly (:557-558); that case is orc_sqdist. */
+double orc_fast_sqdist_dense_sparse(const double* v1, double norm1,
+                                    const int32_t* idx, const double* val, int64_t nnz,
+                                    double norm2, int64_t n) {
+  const double EPS = orc_epsilon();
+  const double precision = 1e-6;
+  double sumSquaredNorm = norm1 * norm1 + norm2 * norm2;
+  double normDiff = norm1 - norm2;
+  double precisionBound1 = 2.0 * EPS * sumSquaredNorm / (normDiff * normDiff + EPS);
+  double sqDist;
+  if (precisionBound1 < precision) {
+    /* dot(v1 dense, v2 sparse) dispatches to dot(sparse, dense) */
+    sqDist = sumSquaredNorm - 2.0 * orc_dot_sparse_dense(idx, val, nnz, v1);
+  } else {
+    double dotValue = orc_dot_sparse_dense(idx, val, nnz, v1);
+    sqDist = fmax(sumSquaredNorm - 2.0 * dotValue, 0.0);
+    double precisionBound2 = EPS * (sumSquaredNorm + 2.0 * fabs(dotValue)) / (sqDist + EPS);
+    if (precisionBound2 > precision) {
+      sqDist = orc_sqdist_sparse_dense(idx, val, nnz, v1, n);
+    }
+  }
+  return sqDist;
+}
+
+/* ml/impl/Utils.scala:70-80 indexUpperTriangular */
+static inline int64_t orc_iut(int64_t i, int64_t j) {
+  return (i <= j) ? j * (j + 1) / 2 + i : i * (i + 1) / 2 + j;
+}
+
+/* ------------------------------------------------------------------------ */
+/* KMeans (dense points, Euclidean)                                          */
+/* ------------------------------------------------------------------------ */
+
+/* DistanceMeasure.scala:48-76 computeStatistics + Euclidean :275-277
+ * s = 0.25 * distance * distance, distance = sqrt(fastSquaredDistance).
+ * packed has k(k+1)/2 entries; k == 1 gives {NaN}.                        */
+void orc_kmeans_stats(const double* C, int64_t k, int64_t d, double* packed) {
+  if (k == 1) { packed[0] = NAN; return; }
+  double* diag = (double*)malloc(sizeof(double) * k);
+  for (int64_t i = 0; i < k; ++i) diag[i] = INFINITY;
+  for (int64_t i = 0; i < k; ++i) {
+    for (int64_t j = i + 1; j < k; ++j) {
+      double dist = sqrt(orc_sqdist(C + i * d, C + j * d, d));
+      double s = 0.25 * dist * dist;
+      packed[orc_iut(i, j)] = s;
+      if (s < diag[i]) diag[i] = s;
+      if (s < diag[j]) diag[j] = s;
+    }
+  }
+  for (int64_t i = 0; i < k; ++i) packed[orc_iut(i, i)] = diag[i];
+  free(diag);
+}
+
+/* DistanceMeasure.scala:282-313 EuclideanDistanceMeasure.findClosest with
+ * statistics, dense centers and dense point (fastSquaredDistance == sqdist). */
+void orc_find_closest_stats(const double* C, const double* cnorm, int64_t k, int64_t d,
+                            const double* stats, const double* x, double xnorm,
+                            int32_t* out_idx, double* out_dist) {
+  double best = orc_sqdist(C, x, d);
+  if (best < stats[0]) { *out_idx = 0; *out_dist = best; return; }
+  int64_t bestIndex = 0;
+  for (int64_t i = 1; i < k; ++i) {
+    double normDiff = cnorm[i] - xnorm;
+    double lowerBound = normDiff * normDiff;
+    if (lowerBound < best) {
+      if (stats[orc_iut(i, bestIndex)] < best) {
+        double dd = orc_sqdist(C + i * d, x, d);
+        if (dd < stats[orc_iut(i, i)]) { *out_idx = (int32_t)i; *out_dist = dd; return; }
+        if (dd < best) { best = dd; bestIndex = i; }
+      }
+    }
+  }
+  *out_idx = (int32_t)bestIndex;
+  *out_dist = best;
+}
+
+/* DistanceMeasure.scala:318-340 findClosest without statistics */
+void orc_find_closest(const double* C, const double* cnorm, int64_t k, int64_t d,
+                      const double* x, double xnorm, int32_t* out_idx, double* out_dist) {
+  double best = INFINITY;
+  int64_t bestIndex = 0;
+  for (int64_t i = 0; i < k; ++i) {
+    double lb = cnorm[i] - xnorm;
+    lb = lb * lb;
+    if (lb < best) {
+      double dd = orc_sqdist(C + i * d, x, d);
+      if (dd < best) { best = dd; bestIndex = i; }
+    }
+  }
+  *out_idx = (int32_t)bestIndex;
+  *out_dist = best;
+}
+
+/* Same as orc_find_closest_stats but the point is sparse (libsvm input,
+ * config #1); distances go through the norm trick of MLUtils:560-573. */
+void orc_find_closest_stats_sparse(const double* C, const double* cnorm, int64_t k, int64_t d,
+                                   const double* stats, const int32_t* idx, const double* val,
+                                   int64_t nnz, double xnorm, int32_t* out_idx, double* out_dist) {
+  double best = orc_fast_sqdist_dense_sparse(C, cnorm[0], idx, val, nnz, xnorm, d);
+  if (best < stats[0]) { *out_idx = 0; *out_dist = best; return; }
+  int64_t bestIndex = 0;
+  for (int64_t i = 1; i < k; ++i) {
+    double normDiff = cnorm[i] - xnorm;
+    double lowerBound = normDiff * normDiff;
+    if (lowerBound < best) {
+      if (stats[orc_iut(i, bestIndex)] < best) {
+        double dd = orc_fast_sqdist_dense_sparse(C + i * d, cnorm[i], idx, val, nnz, xnorm, d);
+        if (dd < stats[orc_iut(i, i)]) { *out_idx = (int32_t)i; *out_dist = dd; return; }
+        if (dd < best) { best = dd; bestIndex = i; }
+      }
+    }
+  }
+  *out_idx = (int32_t)bestIndex;
+  *out_dist = best;
+}
+
+/* One Spark partition of the Lloyd iteration body, KMeans.scala:287-306:
+ *   (bestCenter, cost) = findClosest(centers, stats, point)
+ *   costAccum.add(cost * point.weight)
+ *   updateClusterSum = axpy(point.weight, point.vector, sums(bestCenter))
+ *   clusterWeightSum(bestCenter) += point.weight
+ * sums (k*d), wsum (k) and *cost accumulate (caller zeroes them).
+ * assign/dist (optional, may be NULL) receive the per-point findClosest.
+ * weights == NULL means unit weights.  netlib daxpy: y(i) = y(i) + da*x(i),
+ * and a da == 0 call is a no-op.                                          */
+void orc_kmeans_partition(const double* X, const double* xnorm, const double* w,
+                          int64_t n, int64_t d, const double* C, const double* cnorm,
+                          const double* stats, int64_t k, int32_t* assign, double* dist,
+                          double* sums, double* wsum, double* cost) {
+  double c = *cost;
+  for (int64_t r = 0; r < n; ++r) {
+    int32_t bi; double bd;
+    orc_find_closest_stats(C, cnorm, k, d, stats, X + r * d, xnorm[r], &bi, &bd);
+    double wt = w ? w[r] : 1.0;
+    if (assign) assign[r] = bi;
+    if (dist) dist[r] = bd;
+    c += bd * wt;
+    if (wt != 0.0) {
+      double* s = sums + (int64_t)bi * d;
+      const double* x = X + r * d;
+      for (int64_t j = 0; j < d; ++j) s[j] = s[j] + wt * x[j];
+    }
+    wsum[bi] += wt;
+  }
+  *cost = c;
+}
+
+/* mllib/linalg/BLAS.scala:63-118 axpy(1.0, sumweight2, sumweight1) merge of
+ * reduceByKey (KMeans.scala:308-311), in place: a += b                     */
+void orc_axpy(int64_t n, double alpha, const double* x, double* y) {
+  if (alpha == 0.0) return;
+  for (int64_t i = 0; i < n; ++i) y[i] = y[i] + alpha * x[i];
+}
+
+/* KMeans.scala:322-330 + DistanceMeasure.scala:200-203 centroid and
+ * :345-350 isCenterConverged (Euclidean: fastSquaredDistance <= eps^2).
+ * Updates C/cnorm in place for clusters with wsum > 0; returns 1 if every
+ * updated center converged.                                              */
+int orc_kmeans_update_centers(double* C, double* cnorm, const double* sums, const double* wsum,
+                              int64_t k, int64_t d, double epsilon) {
+  int converged = 1;
+  double* nc = (double*)malloc(sizeof(double) * d);
+  for (int64_t j = 0; j < k; ++j) {
+    if (!(wsum[j] > 0)) continue;
+    double a = 1.0 / wsum[j];
+    for (int64_t t = 0; t < d; ++t) nc[t] = a * sums[j * d + t];
+    double nn = orc_norm2(nc, d);
+    if (converged && !(orc_sqdist(nc, C + j * d, d) <= epsilon * epsilon)) converged = 0;
+    memcpy(C + j * d, nc, sizeof(double) * d);
+    cnorm[j] = nn;
+  }
+  free(nc);
+  return converged;
+}
+
+/* ------------------------------------------------------------------------ */
+/* ml.impl.Utils                                                            */
+/* ------------------------------------------------------------------------ */
+
+/* ml/impl/Utils.scala:91-97 log1pExp */
+double orc_log1pexp(double x) {
+  if (x > 0) return x + log1p(exp(-x));
+  return log1p(exp(x));
+}
+
+/* ml/impl/Utils.scala:108-135 strided softmax, in place on arr[offset + step*i] */
+void orc_softmax(double* arr, int64_t n, int64_t offset, int64_t step) {
+  double maxValue = -1.7976931348623157e308; /* Double.MinValue */
+  int64_t end = offset + step * n;
+  for (int64_t i = offset; i < end; i += step) {
+    double v = arr[i];
+    if (isinf(v) && v > 0) {
+      for (int64_t t = offset; t < end; t += step) arr[t] = 0.0 * arr[t];
+      arr[i] = 1.0;
+      return;
+    } else if (v > maxValue) {
+      maxValue = v;
+    }
+  }
+  double sum = 0.0;
+  for (int64_t i = offset; i < end; i += step) {
+    double e = exp(arr[i] - maxValue);
+    arr[i] = e;
+    sum += e;
+  }
+  double a = 1.0 / sum;
+  for (int64_t i = offset; i < end; i += step) arr[i] = a * arr[i];
+}
+
+/* ------------------------------------------------------------------------ */
+/* Logistic block aggregators                                                */
+/* ------------------------------------------------------------------------ */
+
+/* A block as InstanceBlock (ml/feature/Instance.scala:39-106): either dense
+ * row-major S x F (values != NULL, rowptr == NULL) or CSR (rowptr/colidx/
+ * values, isTransposed = true).  weights == NULL means all-unit weights
+ * (Instance.scala:134-138 stores an empty array).                          */
+typedef struct {
+  int64_t S, F;
+  const double* labels;
+  const double* weights;
+  const double* values;
+  const int64_t* rowptr;
+  const int32_t* colidx;
+} orc_block;
+
+/* margin of row i: netlib dgemv "T" on the row-major block (BLAS.scala:621-631):
+ * temp += a(l,i)*x(l) sequentially, y = alpha*temp + y (beta == 1 skips the
+ * beta scaling).  CSR: BLAS.scala:777-789 sum += Avals(i) * x(Acols(i)),
+ * y = beta*y + sum*alpha.  Both reduce to y + temp for alpha = beta = 1. */
+static double orc_row_dot(const orc_block* b, int64_t i, const double* coef) {
+  double t = 0.0;
+  if (b->rowptr) {
+    for (int64_t p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p)
+      t += b->values[p] * coef[b->colidx[p]];
+  } else {
+    const double* row = b->values + i * b->F;
+    for (int64_t f = 0; f < b->F; ++f) t += row[f] * coef[f];
+  }
+  return t;
+}
+
+/* BinaryLogisticBlockAggregator.add, BinaryLogisticBlockAggregator.scala:81-145.
+ * coef has F (+1 if fitIntercept) entries; grad (same size), *lossSum,
+ * *weightSum accumulate.  scaledMean is used iff fitWithMean.             */
+void orc_binary_logistic_add(const orc_block* b, const double* coef, int fitIntercept,
+                             int fitWithMean, const double* scaledMean, double* grad,
+                             double* lossSum, double* weightSum) {
+  const int64_t S = b->S, F = b->F;
+  int anyPositive = 0;
+  for (int64_t i = 0; i < S; ++i) if (!b->weights || b->weights[i] != 0) anyPositive = 1;
+  if (!anyPositive) return;                                     /* :88 */
+  double marginOffset = NAN;                                    /* :67-72 */
+  if (fitWithMean) {
+    double dd = 0.0;                                            /* javaBLAS.ddot */
+    for (int64_t f = 0; f < F; ++f) dd += coef[f] * scaledMean[f];
+    marginOffset = coef[F] - dd;
+  }
+  double* arr = (double*)calloc((size_t)S, sizeof(double));
+  if (fitIntercept) {
+    double off = fitWithMean ? marginOffset : coef[F];
+    for (int64_t i = 0; i < S; ++i) arr[i] = off;
+  }
+  for (int64_t i = 0; i < S; ++i) arr[i] = arr[i] + orc_row_dot(b, i, coef);  /* :97 */
+  double localLoss = 0.0, localW = 0.0, multSum = 0.0;
+  for (int64_t i = 0; i < S; ++i) {                             /* :104-122 */
+    double w = b->weights ? b->weights[i] : 1.0;
+    localW += w;
+    if (w > 0) {
+      double label = b->labels[i];
+      double margin = arr[i];
+      if (label > 0) localLoss += w * orc_log1pexp(-margin);
+      else localLoss += w * (orc_log1pexp(-margin) + margin);
+      double mult = w * (1.0 / (1.0 + exp(-margin)) - label);
+      arr[i] = mult;
+      multSum += mult;
+    } else {
+      arr[i] = 0.0;
+    }
+  }
+  *lossSum += localLoss;
+  *weightSum += localW;
+  int allZero = 1;
+  for (int64_t i = 0; i < S; ++i) if (arr[i] != 0) { allZero = 0; break; }
+  if (!allZero) {
+    /* :130 gemv(1.0, A^T, arr, 1.0, grad): netlib dgemv "N" column loop
+     * (dense) / BLAS.scala:790-804 CSC scatter (sparse): y(row) += a*(x*alpha) */
+    for (int64_t i = 0; i < S; ++i) {
+      double t = arr[i];
+      if (b->rowptr) {
+        double xv = t * 1.0;
+        for (int64_t p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p)
+          grad[b->colidx[p]] += b->values[p] * xv;
+      } else {
+        if (t != 0.0) {
+          const double* row = b->values + i * F;
+          for (int64_t f = 0; f < F; ++f) grad[f] = grad[f] + t * row[f];
+        }
+      }
+    }
+    if (fitWithMean) {                                          /* :132-137 javaBLAS.daxpy */
+      double a = -multSum;
+      if (a != 0.0) for (int64_t f = 0; f < F; ++f) grad[f] = grad[f] + a * scaledMean[f];
+    }
+    if (fitIntercept) grad[F] += multSum;                       /* :139-142 */
+  }
+  free(arr);
+}
+
+/* MultinomialLogisticBlockAggregator.add, .scala:101-189 (dense blocks and
+ * CSR blocks).  coef: C*F linear part, column-major C x F (coef[f*C + c]),
+ * then C intercepts if fitIntercept.  grad has the same layout.            */
+void orc_multinomial_logistic_add(const orc_block* b, const double* coef, int64_t C,
+                                  int fitIntercept, int fitWithMean, const double* scaledMean,
+                                  double* grad, double* lossSum, double* weightSum) {
+  const int64_t S = b->S, F = b->F;
+  int anyPositive = 0;
+  for (int64_t i = 0; i < S; ++i) if (!b->weights || b->weights[i] != 0) anyPositive = 1;
+  if (!anyPositive) return;
+  const double* linear = coef;               /* linear(c,f) = coef[f*C + c] */
+  const double* intercept = fitIntercept ? coef + C * F : NULL;
+  double* offset = NULL;
+  if (fitWithMean) {
+    /* marginOffset :86-92: gemv(-1.0, linear, scaledMean, 1.0, intercept copy):
+     * netlib dgemv "N" (C x F col-major): column loop, temp = alpha*x(j),
+     * y(i) += temp*a(i,j) */
+    offset = (double*)malloc(sizeof(double) * C);
+    for (int64_t c = 0; c < C; ++c) offset[c] = intercept[c];
+    for (int64_t f = 0; f < F; ++f) {
+      if (scaledMean[f] != 0.0) {
+        double t = -1.0 * scaledMean[f];
+        for (int64_t c = 0; c < C; ++c) offset[c] = offset[c] + t * linear[f * C + c];
+      }
+    }
+  }
+  /* mat S x C column-major: arr[c*S + i] */
+  double* arr = (double*)calloc((size_t)(S * C), sizeof(double));
+  if (fitIntercept) {
+    const double* off = fitWithMean ? offset : intercept;
+    for (int64_t c = 0; c < C; ++c)
+      if (off[c] != 0) for (int64_t i = 0; i < S; ++i) arr[c * S + i] = off[c];
+  }
+  /* :122 gemm(1.0, A, linear^T, 1.0, mat) -> netlib dgemm("T","T") for dense:
+   * c(i,j) = alpha*temp + beta*c(i,j), temp = sum_l a(l,i)*b(j,l) in l order.
+   * CSR A: BLAS.scala gemm(SparseMatrix transposed): per (row, col of B)
+   * sum += Avals(k) * B(Arows(k), colCounterForB) then C = beta*C + sum*alpha. */
+  for (int64_t c = 0; c < C; ++c) {
+    for (int64_t i = 0; i < S; ++i) {
+      double t = 0.0;
+      if (b->rowptr) {
+        for (int64_t p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p)
+          t += b->values[p] * linear[(int64_t)b->colidx[p] * C + c];
+        arr[c * S + i] = 1.0 * arr[c * S + i] + t * 1.0;
+      } else {
+        const double* row = b->values + i * F;
+        for (int64_t f = 0; f < F; ++f) t += row[f] * linear[f * C + c];
+        arr[c * S + i] = 1.0 * t + 1.0 * arr[c * S + i];
+      }
+    }
+  }
+  double localLoss = 0.0, localW = 0.0;
+  for (int64_t i = 0; i < S; ++i) {                              /* :129-142 */
+    double w = b->weights ? b->weights[i] : 1.0;
+    localW += w;
+    if (w > 0) {
+      int64_t labelIndex = i + (int64_t)b->labels[i] * S;
+      orc_softmax(arr, C, i, S);
+      localLoss -= w * log(arr[labelIndex]);
+      if (w != 1) for (int64_t c = 0; c < C; ++c) arr[c * S + i] = w * arr[c * S + i];
+      arr[labelIndex] -= w;
+    } else {
+      for (int64_t c = 0; c < C; ++c) arr[c * S + i] = 0.0 * arr[c * S + i];
+    }
+  }
+  *lossSum += localLoss;
+  *weightSum += localW;
+  /* :153 dgemm("T","T", C, F, S, 1.0, mat, S, A, F, 1.0, grad, C):
+   * grad(c, f) = 1.0*temp + 1.0*grad(c,f), temp = sum_s mat(s,c)*A(s,f)   */
+  if (b->rowptr) {
+    /* :157-161 sparse: linearGradSumMat (F x C) = sm^T x mat via BLAS.gemm
+     * with a non-transposed CSC (the transpose of the CSR block): for each
+     * column of B (class c) and each CSC column s: Bval = mat(s,c)*alpha,
+     * C(row=f) += Avals * Bval; then gradientSumArray(f*C + c) += v.        */
+    double* lg = (double*)calloc((size_t)(F * C), sizeof(double));
+    for (int64_t c = 0; c < C; ++c) {
+      for (int64_t s = 0; s < S; ++s) {
+        double bv = arr[c * S + s] * 1.0;
+        for (int64_t p = b->rowptr[s]; p < b->rowptr[s + 1]; ++p)
+          lg[c * F + b->colidx[p]] += b->values[p] * bv;
+      }
+    }
+    for (int64_t c = 0; c < C; ++c)
+      for (int64_t f = 0; f < F; ++f) grad[f * C + c] += lg[c * F + f];
+    free(lg);
+  } else {
+    for (int64_t f = 0; f < F; ++f) {
+      for (int64_t c = 0; c < C; ++c) {
+        double t = 0.0;
+        for (int64_t s = 0; s < S; ++s) t += arr[c * S + s] * b->values[s * F + f];
+        grad[f * C + c] = 1.0 * t + 1.0 * grad[f * C + c];
+      }
+    }
+  }
+  if (fitIntercept) {                                             /* :165-186 */
+    double* ms = (double*)calloc((size_t)C, sizeof(double));
+    for (int64_t c = 0; c < C; ++c)
+      for (int64_t i = 0; i < S; ++i) ms[c] += arr[c * S + i];
+    if (fitWithMean) {
+      /* netlib dger(C, F, -1.0, ms, 1, scaledMean, 1, grad, C):
+       * for j: if y(j) != 0: temp = alpha*y(j); a(i,j) += x(i)*temp */
+      for (int64_t f = 0; f < F; ++f) {
+        if (scaledMean[f] != 0.0) {
+          double t = -1.0 * scaledMean[f];
+          for (int64_t c = 0; c < C; ++c) grad[f * C + c] = grad[f * C + c] + ms[c] * t;
+        }
+      }
+    }
+    for (int64_t c = 0; c < C; ++c) grad[C * F + c] = grad[C * F + c] + 1.0 * ms[c];
+    free(ms);
+  }
+  free(arr);
+  free(offset);
+}
+
+/* Python-friendly entry points (plain pointers, no struct) */
+void orc_binary_logistic_add_dense(int64_t S, int64_t F, const double* X, const double* labels,
+                                   const double* weights, const double* coef, int fitIntercept,
+                                   int fitWithMean, const double* scaledMean, double* grad,
+                                   double* lossSum, double* weightSum) {
+  orc_block b = {S, F, labels, weights, X, NULL, NULL};
+  orc_binary_logistic_add(&b, coef, fitIntercept, fitWithMean, scaledMean, grad, lossSum, weightSum);
+}
+
+void orc_binary_logistic_add_csr(int64_t S, int64_t F, const int64_t* rowptr,
+                                 const int32_t* colidx, const double* vals, const double* labels,
+                                 const double* weights, const double* coef, int fitIntercept,
+                                 int fitWithMean, const double* scaledMean, double* grad,
+                                 double* lossSum, double* weightSum) {
+  orc_block b = {S, F, labels, weights, vals, rowptr, colidx};
+  orc_binary_logistic_add(&b, coef, fitIntercept, fitWithMean, scaledMean, grad, lossSum, weightSum);
+}
+
+void orc_multinomial_logistic_add_dense(int64_t S, int64_t F, int64_t C, const double* X,
+                                        const double* labels, const double* weights,
+                                        const double* coef, int fitIntercept, int fitWithMean,
+                                        const double* scaledMean, double* grad, double* lossSum,
+                                        double* weightSum) {
+  orc_block b = {S, F, labels, weights, X, NULL, NULL};
+  orc_multinomial_logistic_add(&b, coef, C, fitIntercept, fitWithMean, scaledMean, grad, lossSum,
+                               weightSum);
+}
+
+void orc_multinomial_logistic_add_csr(int64_t S, int64_t F, int64_t C, const int64_t* rowptr,
+                                      const int32_t* colidx, const double* vals,
+                                      const double* labels, const double* weights,
+                                      const double* coef, int fitIntercept, int fitWithMean,
+                                      const double* scaledMean, double* grad, double* lossSum,
+                                      double* weightSum) {
+  orc_block b = {S, F, labels, weights, vals, rowptr, colidx};
+  orc_multinomial_logistic_add(&b, coef, C, fitIntercept, fitWithMean, scaledMean, grad, lossSum,
+                               weightSum);
+}
+
+/* ------------------------------------------------------------------------ */
+/* RowMatrix Gramian / covariance                                            */
+/* ------------------------------------------------------------------------ */
+
+/* netlib dspr("U", n, alpha, x, 1, ap) reference loop, called per dense row
+ * by mllib/linalg/BLAS.scala:268 (RowMatrix.scala:139-158):
+ *   kk = 0; for j: if x(j) != 0: temp = alpha*x(j); k = kk;
+ *     for i <= j: ap(k) += x(i)*temp; kk += j + 1                         */
+void orc_dspr_upper(int64_t n, double alpha, const double* x, double* ap) {
+  int64_t kk = 0;
+  for (int64_t j = 0; j < n; ++j) {
+    if (x[j] != 0.0) {
+      double temp = alpha * x[j];
+      int64_t k = kk;
+      for (int64_t i = 0; i <= j; ++i, ++k) ap[k] = ap[k] + x[i] * temp;
+    }
+    kk += j + 1;
+  }
+}
+
+/* mllib/linalg/BLAS.scala:269-298 spr for a sparse vector */
+void orc_spr_sparse(double alpha, const int32_t* idx, const double* val, int64_t nnz, double* U) {
+  int64_t colStartIdx = 0, prevCol = 0;
+  for (int64_t j = 0; j < nnz; ++j) {
+    int64_t col = idx[j];
+    colStartIdx += (col - prevCol) * (col + prevCol + 1) / 2;
+    double av = alpha * val[j];
+    for (int64_t i = 0; i <= j; ++i) U[colStartIdx + idx[i]] += av * val[i];
+    prevCol = col;
+  }
+}
+
+/* RowMatrix.computeGramianMatrix seqOp over one partition (RowMatrix.scala:139-158).
+ * mean != NULL gives computeDenseVectorCovariance's seqOp (:171-190):
+ * na(index) = ta(index) - means(index); spr(1.0, na, U).                  */
+void orc_gramian_partition(const double* X, int64_t rows, int64_t n, const double* mean,
+                           double* U) {
+  double* na = mean ? (double*)malloc(sizeof(double) * n) : NULL;
+  for (int64_t r = 0; r < rows; ++r) {
+    const double* x = X + r * n;
+    if (mean) {
+      for (int64_t t = 0; t < n; ++t) na[t] = x[t] - mean[t];
+      x = na;
+    }
+    orc_dspr_upper(n, 1.0, x, U);
+  }
+  free(na);
+}
+
+/* RowMatrix.scala:845-867 triuToFull (column-major n x n) */
+void orc_triu_to_full(int64_t n, const double* U, double* G) {
+  int64_t idx = 0;
+  for (int64_t col = 0; col < n; ++col) {
+    for (int64_t row = 0; row < col; ++row) {
+      double v = U[idx++];
+      G[col * n + row] = v;
+      G[row * n + col] = v;
+    }
+    G[col * n + col] = U[idx++];
+  }
+}

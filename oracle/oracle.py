@@ -1,0 +1,370 @@
+"""ctypes wrapper around the CPU restatement in cyclone_oracle.c.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py as the parity checker.  The product package
+(cycloneml_amd) never imports this module.
+
+Each wrapper cites the reference Scala it restates (paths relative to
+/root/reference).  Arrays are numpy float64 / int32 / int64, C-contiguous.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+_lock = threading.Lock()
+
+_D = ctypes.POINTER(ctypes.c_double)
+_I32 = ctypes.POINTER(ctypes.c_int32)
+_I64 = ctypes.POINTER(ctypes.c_int64)
+_i64 = ctypes.c_int64
+
+
+def build() -> str:
+    """Compile liboracle.so with the committed Makefile (gcc, -ffp-contract=off)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    with _lock:
+        if _lib is None:
+            src = os.path.join(_HERE, "cyclone_oracle.c")
+            if (not os.path.exists(_LIB_PATH)
+                    or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)):
+                build()
+            L = ctypes.CDLL(_LIB_PATH)
+            sig = {
+                "orc_norm2": (ctypes.c_double, [_D, _i64]),
+                "orc_sqdist": (ctypes.c_double, [_D, _D, _i64]),
+                "orc_kmeans_stats": (None, [_D, _i64, _i64, _D]),
+                "orc_find_closest_stats": (None, [_D, _D, _i64, _i64, _D, _D, ctypes.c_double,
+                                                  _I32, _D]),
+                "orc_find_closest": (None, [_D, _D, _i64, _i64, _D, ctypes.c_double, _I32, _D]),
+                "orc_find_closest_stats_sparse": (None, [_D, _D, _i64, _i64, _D, _I32, _D, _i64,
+                                                         ctypes.c_double, _I32, _D]),
+                "orc_kmeans_partition": (None, [_D, _D, _D, _i64, _i64, _D, _D, _D, _i64, _I32,
+                                                _D, _D, _D, _D]),
+                "orc_axpy": (None, [_i64, ctypes.c_double, _D, _D]),
+                "orc_kmeans_update_centers": (ctypes.c_int, [_D, _D, _D, _D, _i64, _i64,
+                                                             ctypes.c_double]),
+                "orc_log1pexp": (ctypes.c_double, [ctypes.c_double]),
+                "orc_softmax": (None, [_D, _i64, _i64, _i64]),
+                "orc_binary_logistic_add_dense": (None, [_i64, _i64, _D, _D, _D, _D, ctypes.c_int,
+                                                         ctypes.c_int, _D, _D, _D, _D]),
+                "orc_binary_logistic_add_csr": (None, [_i64, _i64, _I64, _I32, _D, _D, _D, _D,
+                                                       ctypes.c_int, ctypes.c_int, _D, _D, _D,
+                                                       _D]),
+                "orc_multinomial_logistic_add_dense": (None, [_i64, _i64, _i64, _D, _D, _D, _D,
+                                                              ctypes.c_int, ctypes.c_int, _D, _D,
+                                                              _D, _D]),
+                "orc_multinomial_logistic_add_csr": (None, [_i64, _i64, _i64, _I64, _I32, _D, _D,
+                                                            _D, _D, ctypes.c_int, ctypes.c_int,
+                                                            _D, _D, _D, _D]),
+                "orc_dspr_upper": (None, [_i64, ctypes.c_double, _D, _D]),
+                "orc_spr_sparse": (None, [ctypes.c_double, _I32, _D, _i64, _D]),
+                "orc_gramian_partition": (None, [_D, _i64, _i64, _D, _D]),
+                "orc_triu_to_full": (None, [_i64, _D, _D]),
+            }
+            for name, (res, args) in sig.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def _p(a, ty=_D):
+    if a is None:
+        return None
+    return a.ctypes.data_as(ty)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+# --------------------------------------------------------------------------
+# Vectors / KMeans
+# --------------------------------------------------------------------------
+
+def norm2(x) -> float:
+    """mllib/linalg/Vectors.scala:489-514"""
+    x = _f64(x)
+    return lib().orc_norm2(_p(x), x.size)
+
+
+def row_norms(X) -> np.ndarray:
+    X = _f64(X)
+    return np.array([norm2(X[i]) for i in range(X.shape[0])], dtype=np.float64)
+
+
+def sqdist(a, b) -> float:
+    """mllib/linalg/Vectors.scala:580-587"""
+    a, b = _f64(a), _f64(b)
+    return lib().orc_sqdist(_p(a), _p(b), a.size)
+
+
+def kmeans_stats(C) -> np.ndarray:
+    """DistanceMeasure.scala:48-76 computeStatistics (Euclidean :275-277)."""
+    C = _f64(C)
+    k, d = C.shape
+    out = np.empty(k * (k + 1) // 2, dtype=np.float64)
+    lib().orc_kmeans_stats(_p(C), k, d, _p(out))
+    return out
+
+
+def find_closest_stats(C, cnorm, stats, x, xnorm):
+    """DistanceMeasure.scala:282-313"""
+    C, cnorm, stats, x = _f64(C), _f64(cnorm), _f64(stats), _f64(x)
+    idx = ctypes.c_int32()
+    dist = ctypes.c_double()
+    lib().orc_find_closest_stats(_p(C), _p(cnorm), C.shape[0], C.shape[1], _p(stats), _p(x),
+                                 float(xnorm), ctypes.byref(idx), ctypes.byref(dist))
+    return idx.value, dist.value
+
+
+def find_closest(C, cnorm, x, xnorm):
+    """DistanceMeasure.scala:318-340"""
+    C, cnorm, x = _f64(C), _f64(cnorm), _f64(x)
+    idx = ctypes.c_int32()
+    dist = ctypes.c_double()
+    lib().orc_find_closest(_p(C), _p(cnorm), C.shape[0], C.shape[1], _p(x), float(xnorm),
+                           ctypes.byref(idx), ctypes.byref(dist))
+    return idx.value, dist.value
+
+
+def find_closest_stats_sparse(C, cnorm, stats, idx, val, xnorm):
+    """DistanceMeasure.scala:282-313 with a SparseVector point (MLUtils.scala:560-573)."""
+    C, cnorm, stats, val = _f64(C), _f64(cnorm), _f64(stats), _f64(val)
+    idx = np.ascontiguousarray(idx, dtype=np.int32)
+    oi = ctypes.c_int32()
+    od = ctypes.c_double()
+    lib().orc_find_closest_stats_sparse(_p(C), _p(cnorm), C.shape[0], C.shape[1], _p(stats),
+                                        _p(idx, _I32), _p(val), idx.size, float(xnorm),
+                                        ctypes.byref(oi), ctypes.byref(od))
+    return oi.value, od.value
+
+
+def kmeans_partition(X, xnorm, w, C, cnorm, stats, want_assign=True):
+    """KMeans.scala:287-306 mapPartitions body over one partition.
+
+    Returns (assign, dist, sums[k,d], wsum[k], cost)."""
+    X, xnorm, C, cnorm, stats = _f64(X), _f64(xnorm), _f64(C), _f64(cnorm), _f64(stats)
+    w = None if w is None else _f64(w)
+    n, d = X.shape
+    k = C.shape[0]
+    assign = np.empty(n, dtype=np.int32) if want_assign else None
+    dist = np.empty(n, dtype=np.float64) if want_assign else None
+    sums = np.zeros((k, d), dtype=np.float64)
+    wsum = np.zeros(k, dtype=np.float64)
+    cost = ctypes.c_double(0.0)
+    lib().orc_kmeans_partition(_p(X), _p(xnorm), _p(w), n, d, _p(C), _p(cnorm), _p(stats), k,
+                               _p(assign, _I32), _p(dist), _p(sums), _p(wsum),
+                               ctypes.byref(cost))
+    return assign, dist, sums, wsum, cost.value
+
+
+def kmeans_iteration(X, xnorm, w, C, cnorm, num_partitions=1, threads=None):
+    """One Lloyd iteration, KMeans.scala:275-334, with the rows split into
+    `num_partitions` contiguous Spark partitions run on `threads` host threads
+    (Spark local[N]).  Partition results merge in partition order with
+    axpy(1.0, ...) (the reduceByKey combiner :308-310).
+
+    Returns dict(assign, dist, sums, wsum, cost, centers, cnorm, converged)
+    where centers/cnorm are the updated model (:322-330)."""
+    X, xnorm, C, cnorm = _f64(X), _f64(xnorm), _f64(C), _f64(cnorm)
+    n = X.shape[0]
+    stats = kmeans_stats(C)
+    bounds = np.linspace(0, n, num_partitions + 1).astype(np.int64)
+
+    def run(p):
+        a, b = bounds[p], bounds[p + 1]
+        return kmeans_partition(X[a:b], xnorm[a:b], None if w is None else w[a:b], C, cnorm,
+                                stats)
+
+    if threads and threads > 1 and num_partitions > 1:
+        with ThreadPoolExecutor(threads) as ex:
+            parts = list(ex.map(run, range(num_partitions)))
+    else:
+        parts = [run(p) for p in range(num_partitions)]
+    assign = np.concatenate([p[0] for p in parts])
+    dist = np.concatenate([p[1] for p in parts])
+    sums = parts[0][2].copy()
+    wsum = parts[0][3].copy()
+    cost = 0.0
+    for p in parts:
+        cost += p[4]
+    for p in parts[1:]:
+        for j in range(sums.shape[0]):
+            if p[3][j] > 0:
+                if wsum[j] > 0:
+                    lib().orc_axpy(sums.shape[1], 1.0, _p(np.ascontiguousarray(p[2][j])),
+                                   sums[j].ctypes.data_as(_D))
+                else:
+                    sums[j] = p[2][j]
+                wsum[j] = wsum[j] + p[3][j]
+    C2, cn2 = C.copy(), cnorm.copy()
+    conv = update_centers(C2, cn2, sums, wsum)
+    return dict(assign=assign, dist=dist, sums=sums, wsum=wsum, cost=cost, centers=C2,
+                cnorm=cn2, converged=conv, stats=stats)
+
+
+def update_centers(C, cnorm, sums, wsum, epsilon=1e-4) -> bool:
+    """KMeans.scala:322-330 centroid + isCenterConverged, in place."""
+    assert C.flags.c_contiguous and cnorm.flags.c_contiguous
+    sums, wsum = _f64(sums), _f64(wsum)
+    k, d = C.shape
+    return bool(lib().orc_kmeans_update_centers(_p(C), _p(cnorm), _p(sums), _p(wsum), k, d,
+                                                float(epsilon)))
+
+
+# --------------------------------------------------------------------------
+# Logistic aggregators
+# --------------------------------------------------------------------------
+
+def log1pexp(x: float) -> float:
+    return lib().orc_log1pexp(float(x))
+
+
+def binary_logistic_add(block, coef, fit_intercept, fit_with_mean, scaled_mean, state):
+    """BinaryLogisticBlockAggregator.add (.scala:81-145).
+
+    block: dict(labels, weights|None, X (dense S x F) | rowptr/colidx/values, F)
+    state: dict(grad, loss, weight) updated in place."""
+    L = lib()
+    coef = _f64(coef)
+    sm = None if scaled_mean is None else _f64(scaled_mean)
+    labels = _f64(block["labels"])
+    weights = None if block.get("weights") is None else _f64(block["weights"])
+    loss = ctypes.c_double(state["loss"])
+    wsum = ctypes.c_double(state["weight"])
+    g = state["grad"]
+    if "X" in block:
+        X = _f64(block["X"])
+        L.orc_binary_logistic_add_dense(X.shape[0], X.shape[1], _p(X), _p(labels), _p(weights),
+                                        _p(coef), int(fit_intercept), int(fit_with_mean), _p(sm),
+                                        _p(g), ctypes.byref(loss), ctypes.byref(wsum))
+    else:
+        rp = np.ascontiguousarray(block["rowptr"], dtype=np.int64)
+        ci = np.ascontiguousarray(block["colidx"], dtype=np.int32)
+        v = _f64(block["values"])
+        L.orc_binary_logistic_add_csr(rp.size - 1, block["F"], _p(rp, _I64), _p(ci, _I32), _p(v),
+                                      _p(labels), _p(weights), _p(coef), int(fit_intercept),
+                                      int(fit_with_mean), _p(sm), _p(g), ctypes.byref(loss),
+                                      ctypes.byref(wsum))
+    state["loss"], state["weight"] = loss.value, wsum.value
+
+
+def multinomial_logistic_add(block, coef, num_classes, fit_intercept, fit_with_mean,
+                             scaled_mean, state):
+    """MultinomialLogisticBlockAggregator.add (.scala:101-189)."""
+    L = lib()
+    coef = _f64(coef)
+    sm = None if scaled_mean is None else _f64(scaled_mean)
+    labels = _f64(block["labels"])
+    weights = None if block.get("weights") is None else _f64(block["weights"])
+    loss = ctypes.c_double(state["loss"])
+    wsum = ctypes.c_double(state["weight"])
+    g = state["grad"]
+    if "X" in block:
+        X = _f64(block["X"])
+        L.orc_multinomial_logistic_add_dense(X.shape[0], X.shape[1], num_classes, _p(X),
+                                             _p(labels), _p(weights), _p(coef),
+                                             int(fit_intercept), int(fit_with_mean), _p(sm),
+                                             _p(g), ctypes.byref(loss), ctypes.byref(wsum))
+    else:
+        rp = np.ascontiguousarray(block["rowptr"], dtype=np.int64)
+        ci = np.ascontiguousarray(block["colidx"], dtype=np.int32)
+        v = _f64(block["values"])
+        L.orc_multinomial_logistic_add_csr(rp.size - 1, block["F"], num_classes, _p(rp, _I64),
+                                           _p(ci, _I32), _p(v), _p(labels), _p(weights),
+                                           _p(coef), int(fit_intercept), int(fit_with_mean),
+                                           _p(sm), _p(g), ctypes.byref(loss),
+                                           ctypes.byref(wsum))
+    state["loss"], state["weight"] = loss.value, wsum.value
+
+
+# --------------------------------------------------------------------------
+# Gramian
+# --------------------------------------------------------------------------
+
+def dspr_upper(x, U, alpha=1.0):
+    x = _f64(x)
+    lib().orc_dspr_upper(x.size, float(alpha), _p(x), _p(U))
+
+
+def spr_sparse(idx, val, U, alpha=1.0):
+    idx = np.ascontiguousarray(idx, dtype=np.int32)
+    val = _f64(val)
+    lib().orc_spr_sparse(float(alpha), _p(idx, _I32), _p(val), idx.size, _p(U))
+
+
+def gramian_partition(X, mean=None, U=None):
+    """RowMatrix.scala:139-158 seqOp (or :171-190 with mean)."""
+    X = _f64(X)
+    rows, n = X.shape
+    if U is None:
+        U = np.zeros(n * (n + 1) // 2, dtype=np.float64)
+    lib().orc_gramian_partition(_p(X), rows, n, _p(None if mean is None else _f64(mean)), _p(U))
+    return U
+
+
+def triu_to_full(n, U) -> np.ndarray:
+    """RowMatrix.scala:845-867; returns the column-major n*n array."""
+    U = _f64(U)
+    G = np.empty(n * n, dtype=np.float64)
+    lib().orc_triu_to_full(n, _p(U), _p(G))
+    return G
+
+
+# --------------------------------------------------------------------------
+# java.util.Random (for regenerating the reference suites' datasets)
+# --------------------------------------------------------------------------
+
+class JavaRandom:
+    """java.util.Random: 48-bit LCG, nextDouble, nextGaussian (polar method).
+
+    Used to regenerate DistanceMeasureSuite.scala:37-53 inputs.  StrictMath
+    log/sqrt are replaced by Python's math (correctly rounded sqrt; log may
+    differ by an ulp in rare cases, which only perturbs test data)."""
+
+    def __init__(self, seed: int):
+        self.seed = (seed ^ 0x5DEECE66D) & ((1 << 48) - 1)
+        self._next_gaussian = None
+
+    def _next(self, bits: int) -> int:
+        self.seed = (self.seed * 0x5DEECE66D + 0xB) & ((1 << 48) - 1)
+        r = self.seed >> (48 - bits)
+        if r >= 1 << (bits - 1):
+            r -= 1 << bits
+        return r
+
+    def next_double(self) -> float:
+        hi = self._next(26) & ((1 << 26) - 1)
+        lo = self._next(27) & ((1 << 27) - 1)
+        return ((hi << 27) + lo) * (1.0 / (1 << 53))
+
+    def next_gaussian(self) -> float:
+        import math
+        if self._next_gaussian is not None:
+            g, self._next_gaussian = self._next_gaussian, None
+            return g
+        while True:
+            v1 = 2 * self.next_double() - 1
+            v2 = 2 * self.next_double() - 1
+            s = v1 * v1 + v2 * v2
+            if 0 < s < 1:
+                break
+        mul = math.sqrt(-2 * math.log(s) / s)
+        self._next_gaussian = v2 * mul
+        return v1 * mul

@@ -1,0 +1,231 @@
+"""GPU parity tests: libcyclone KMeans kernels vs the CPU restatement (oracle/).
+
+Bar (BASELINE.json north_star): assignments and per-point costs bit-exact;
+sums / centers within 1e-10 relative (we assert tighter where the order is
+known).  Every call goes through the C ABI (cycloneml_amd/_native.py).
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, cuda):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+
+
+def _plan(d, k, n=1):
+    from cycloneml_amd.clustering import KMeansPlan
+    return KMeansPlan(d, k, n)
+
+
+def _gpu_assign(X, C, cuda, count_exact=True):
+    import torch
+    from cycloneml_amd.clustering import row_norms
+    Xd, Cd = _dev(X, cuda), _dev(C, cuda)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = _plan(X.shape[1], C.shape[0], X.shape[0])
+    p.stats(Cd)
+    a = torch.empty(X.shape[0], dtype=torch.int32, device=cuda)
+    c = torch.empty(X.shape[0], dtype=torch.float64, device=cuda)
+    n_exact = p.assign(Xd, xn, Cd, cn, a, c, count_exact=count_exact)
+    torch.cuda.synchronize()
+    return a.cpu().numpy(), c.cpu().numpy(), n_exact, xn.cpu().numpy(), cn.cpu().numpy()
+
+
+def _oracle_assign(X, C):
+    xn, cn = oracle.row_norms(X), oracle.row_norms(C)
+    stats = oracle.kmeans_stats(C)
+    a, dist, *_ = oracle.kmeans_partition(X, xn, None, C, cn, stats)
+    return a, dist
+
+
+@pytest.mark.parametrize("n,d", [(1, 1), (63, 3), (1000, 8), (777, 13), (4096, 256), (300, 257)])
+def test_row_norms_bitexact(cuda, n, d):
+    from cycloneml_amd.clustering import row_norms
+    rng = np.random.default_rng(n * 31 + d)
+    X = rng.normal(size=(n, d)) * rng.uniform(0.1, 100, size=(n, 1))
+    got = row_norms(_dev(X, cuda)).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.row_norms(X))
+
+
+@pytest.mark.parametrize("k,d", [(1, 4), (2, 3), (17, 5), (130, 64), (1024, 256)])
+def test_stats_bitexact(cuda, k, d):
+    import torch
+    rng = np.random.default_rng(k + d)
+    C = rng.normal(size=(k, d)) * 3.0
+    p = _plan(d, k)
+    out = torch.empty(k * (k + 1) // 2, dtype=torch.float64, device=cuda)
+    p.stats(_dev(C, cuda), out)
+    got = out.cpu().numpy()
+    ref = oracle.kmeans_stats(C) if k <= 200 else None
+    if ref is None:
+        # k=1024: check a deterministic sample of pairs against the restatement
+        idx = rng.integers(0, k, size=(200, 2))
+        for i, j in idx:
+            i, j = int(min(i, j)), int(max(i, j))
+            if i == j:
+                continue
+            dist = np.sqrt(oracle.sqdist(C[i], C[j]))
+            assert got[j * (j + 1) // 2 + i] == 0.25 * dist * dist
+        return
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+    np.testing.assert_array_equal(got[~np.isnan(got)], ref[~np.isnan(ref)])
+
+
+@pytest.mark.parametrize("n,d,k", [(2000, 2, 2), (3000, 3, 5), (1000, 8, 10), (2500, 16, 37),
+                                   (2000, 64, 130), (1500, 256, 300), (700, 300, 33),
+                                   (500, 513, 20), (64, 1, 1)])
+def test_assign_bitexact(cuda, n, d, k):
+    rng = np.random.default_rng(n + d + k)
+    true_c = rng.normal(scale=4.0, size=(max(k // 2, 1), d))
+    X = true_c[rng.integers(0, true_c.shape[0], n)] + rng.normal(size=(n, d))
+    C = X[rng.choice(n, size=k, replace=False)] if k <= n else rng.normal(size=(k, d))
+    a, c, n_exact, xn, cn = _gpu_assign(X, C, cuda)
+    np.testing.assert_array_equal(xn, oracle.row_norms(X))
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a, ra)
+    np.testing.assert_array_equal(c, rc)
+
+
+def test_distance_measure_suite(cuda):
+    """DistanceMeasureSuite.scala:28-63 data (java.util.Random(42), k=10, dim=8,
+    1000 points): findClosest with and without statistics agree (reference
+    assertion), and the GPU equals both bit for bit."""
+    rng = oracle.JavaRandom(42)
+    C = np.array([[rng.next_gaussian() for _ in range(8)] for _ in range(10)])
+    X = np.array([[rng.next_gaussian() for _ in range(8)] for _ in range(1000)])
+    cn = oracle.row_norms(C)
+    stats = oracle.kmeans_stats(C)
+    for x in X[:200]:
+        xn = oracle.norm2(x)
+        assert oracle.find_closest(C, cn, x, xn) == oracle.find_closest_stats(C, cn, stats, x, xn)
+    a, c, *_ = _gpu_assign(X, C, cuda)
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a, ra)
+    np.testing.assert_array_equal(c, rc)
+
+
+def test_assign_ties_and_duplicates(cuda):
+    """Duplicate centers and points equidistant to two centers force the
+    exact-emulation path; results must still be the reference's."""
+    rng = np.random.default_rng(7)
+    d = 24
+    base = rng.normal(size=(6, d))
+    C = np.vstack([base, base[:3], base[2:4] * 1.0])          # duplicated centers
+    mid = 0.5 * (C[0] + C[1])
+    X = np.vstack([rng.normal(size=(500, d)), np.repeat(mid[None], 50, 0), C,
+                   C[:4] + 1e-13])
+    a, c, n_exact, *_ = _gpu_assign(X, C, cuda)
+    ra, rc = _oracle_assign(X, C)
+    assert n_exact > 0
+    np.testing.assert_array_equal(a, ra)
+    np.testing.assert_array_equal(c, rc)
+
+
+def test_assign_nonfinite(cuda):
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(200, 16))
+    X[5, 3] = np.nan
+    X[7, 0] = np.inf
+    X[9, :] = 1e200
+    C = rng.normal(size=(9, 16))
+    a, c, n_exact, *_ = _gpu_assign(X, C, cuda)
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a, ra)
+    np.testing.assert_array_equal(c, rc)   # NaN == NaN under assert_array_equal
+
+
+@pytest.mark.parametrize("n,d,k,weighted", [(5000, 16, 12, False), (20000, 256, 64, True),
+                                            (3000, 7, 1, False)])
+def test_lloyd_iteration(cuda, n, d, k, weighted):
+    import torch
+    from cycloneml_amd.clustering import row_norms
+    rng = np.random.default_rng(n + k)
+    X = rng.normal(size=(n, d)) + rng.integers(0, 5, size=(n, 1)) * 3.0
+    C = X[rng.choice(n, size=k, replace=False)].copy()
+    w = rng.uniform(0.5, 2.0, size=n) if weighted else None
+    ref = oracle.kmeans_iteration(X, oracle.row_norms(X), w, C, oracle.row_norms(C))
+    Xd, Cd = _dev(X, cuda), _dev(C, cuda)
+    wd = None if w is None else _dev(w, cuda)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = _plan(d, k, n)
+    sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+    wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+    cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    pc = torch.empty(n, dtype=torch.float64, device=cuda)
+    p.accumulate(Xd, xn, wd, Cd, cn, sums, wsum, cost, a, pc)
+    conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+    p.update(Cd, cn, sums, wsum, 1e-4, conv)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(a.cpu().numpy(), ref["assign"])
+    np.testing.assert_array_equal(pc.cpu().numpy(), ref["dist"])
+    np.testing.assert_allclose(wsum.cpu().numpy(), ref["wsum"], rtol=1e-12)
+    np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
+                               atol=1e-10 * np.abs(ref["sums"]).max())
+    assert abs(cost.item() - ref["cost"]) <= 1e-12 * abs(ref["cost"])
+    np.testing.assert_allclose(Cd.cpu().numpy(), ref["centers"], rtol=1e-10,
+                               atol=1e-12 * np.abs(ref["centers"]).max())
+    np.testing.assert_allclose(cn.cpu().numpy(), ref["cnorm"], rtol=1e-12)
+    assert bool(conv.item()) == ref["converged"]
+
+
+def test_weighted_centers_exact(cuda):
+    """ml/clustering/KMeansSuite.scala:323-411 'Two centers with weightCol':
+    exact (===) centers after convergence, up to the order of the clusters."""
+    from cycloneml_amd.clustering import KMeans, KMeansModel
+    import torch
+    pts = np.array([[0.0, 0.0], [0.0, 0.1], [0.1, 0.0], [9.0, 0.0], [9.0, 0.2], [9.2, 0.0]])
+    for w, expect in [
+        ([2.0] * 6, {(9.066666666666666, 0.06666666666666667),
+                     (0.03333333333333333, 0.03333333333333333)}),
+        ([1.0, 2.0, 3.0, 2.5, 1.0, 2.0], {(9.072727272727272, 0.03636363636363637),
+                                          (0.05, 0.03333333333333333)}),
+    ]:
+        km = KMeans(k=2, maxIterations=10).setInitialModel(KMeansModel(pts[[0, 3]]))
+        model = km.run(_dev(pts, cuda), weights=_dev(np.array(w), cuda))
+        got = {tuple(map(float, c)) for c in model.clusterCenters}
+        assert got == expect
+
+
+def test_full_config_properties(cuda):
+    """BASELINE config 2 shape (10M x 256, k=1024): size-independent checks --
+    a sampled subset of rows equals the restatement bit for bit, weights sum
+    to n, and sum of cluster sums equals the column sums of X."""
+    import torch
+    from cycloneml_amd.clustering import row_norms
+    n, d, k = 10_000_000, 256, 1024
+    g = torch.Generator(device=cuda).manual_seed(0)
+    true_c = torch.randn(k, d, generator=g, device=cuda, dtype=torch.float64) * 4.0
+    lab = torch.randint(0, k, (n,), generator=g, device=cuda)
+    X = true_c[lab]
+    X += torch.randn(n, d, generator=g, device=cuda, dtype=torch.float64)
+    del lab
+    C = X[:k].clone()
+    xn, cn = row_norms(X), row_norms(C)
+    p = _plan(d, k, n)
+    sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+    wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+    cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    pc = torch.empty(n, dtype=torch.float64, device=cuda)
+    p.accumulate(X, xn, None, C, cn, sums, wsum, cost, a, pc)
+    torch.cuda.synchronize()
+    assert wsum.sum().item() == n
+    colsum = X.sum(0)
+    np.testing.assert_allclose(sums.view(k, d).sum(0).cpu().numpy(), colsum.cpu().numpy(),
+                               rtol=1e-9, atol=1e-6)
+    assert abs(cost.item() - pc.sum().item()) <= 1e-10 * cost.item()
+    rows = np.random.default_rng(0).choice(n, 300, replace=False)
+    Ch = C.cpu().numpy()
+    chn = oracle.row_norms(Ch)
+    stats = oracle.kmeans_stats(Ch)
+    Xs = X[torch.from_numpy(rows).to(cuda)].cpu().numpy()
+    ah, ch = a.cpu().numpy()[rows], pc.cpu().numpy()[rows]
+    for i in range(len(rows)):
+        idx, dist = oracle.find_closest_stats(Ch, chn, stats, Xs[i], oracle.norm2(Xs[i]))
+        assert (idx, dist) == (int(ah[i]), float(ch[i]))
