@@ -51,6 +51,21 @@ SIGNATURES = {
     "cyc_kmeans_accumulate_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
                                                  _vp, _vp, _vp, _vp]),
     "cyc_kmeans_update_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _f64, _vp, _vp]),
+    "cyc_gramian_plan_create": (ctypes.c_int, [_i32, ctypes.POINTER(_vp)]),
+    "cyc_gramian_plan_destroy": (ctypes.c_int, [_vp]),
+    "cyc_gramian_accumulate_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    "cyc_col_sums_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
+    "cyc_triu_to_full_dev": (ctypes.c_int, [_i32, _vp, _vp, _vp]),
+    "cyc_covariance_finalize_dev": (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp]),
+    "cyc_logistic_plan_create": (ctypes.c_int, [_i32, _i32, ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(_vp)]),
+    "cyc_logistic_plan_destroy": (ctypes.c_int, [_vp]),
+    "cyc_binary_logistic_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp,
+                                                         _vp, _vp, _vp, _vp]),
+    "cyc_binary_logistic_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                                                       _vp, _vp, _vp, _vp, _vp]),
+    "cyc_multinomial_logistic_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp,
+                                                              _vp, _vp, _vp, _vp, _vp]),
 }
 
 

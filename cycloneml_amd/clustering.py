@@ -17,6 +17,7 @@ import ctypes
 import numpy as np
 
 from . import _native as N
+from . import parallel
 
 
 def _torch():
@@ -168,10 +169,8 @@ class KMeans:
             xnorm = row_norms(X, stream=stream)
         plan = KMeansPlan(d, k, n)
         C = torch.from_numpy(self.initialModel.clusterCenters.copy()).to(dev)
+        parallel.broadcast_(C)             # bcCenters (KMeans.scala:276)
         cnorm = row_norms(C, stream=stream)
-        dist = torch.distributed if (torch.distributed.is_available()
-                                     and torch.distributed.is_initialized()) else None
-        world = dist.get_world_size() if dist else 1
         buf = torch.empty(k * d + k + 1, dtype=torch.float64, device=dev)
         sums, wsum, cost_sum = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
         converged_t = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -179,8 +178,7 @@ class KMeans:
         while iteration < self.maxIterations and not converged:
             buf.zero_()
             plan.accumulate(X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, stream=stream)
-            if world > 1:
-                dist.all_reduce(buf)
+            parallel.allreduce_(buf)       # reduceByKey + collectAsMap + costAccum
             plan.update(C, cnorm, sums, wsum, self.epsilon, converged_t, stream=stream)
             converged = bool(converged_t.item())
             cost = float(cost_sum.item())

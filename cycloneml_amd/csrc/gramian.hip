@@ -1,0 +1,307 @@
+// gramian.hip -- RowMatrix Gramian / dense covariance on gfx950 (MI355X).
+//
+// Replaces the per-row BLAS.spr seqOp of RowMatrix.computeGramianMatrix
+// (mllib/linalg/distributed/RowMatrix.scala:130-161) and of
+// computeDenseVectorCovariance (:163-220), plus triuToFull (:845-867).
+//
+// U (packed upper, column-major: U[j(j+1)/2 + i], i <= j) += sum_r x_r x_r^T
+// is a syrk with a huge contraction dimension (rows).  Layout / schedule:
+//   - output split in 128 x 128 tiles, only the upper block triangle;
+//   - rows split in S contiguous ranges (split-K) so that tiles x S >> 256
+//     CUs; each workgroup accumulates its tile over its range with
+//     v_mfma_f64_16x16x4f64 (4 waves, 64 x 64 per wave = 16 accumulators);
+//   - 16-row chunks of the two 128-column panels are staged through LDS
+//     (row stride 144 doubles: the two 16-lane halves of a ds_read_b64 hit
+//     disjoint banks), the next chunk prefetched into registers;
+//   - the covariance variant subtracts the mean while staging, which is the
+//     reference's na(index) = ta(index) - means(index) bit for bit;
+//   - partial tiles go to slabs, a second kernel folds the S slabs in fixed
+//     order into U (deterministic, no atomics).
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <mutex>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int TILE = 128;
+constexpr int KC = 16;             // rows per LDS chunk
+constexpr int LDSW = TILE + 16;    // LDS row stride (doubles)
+constexpr int GT = 256;            // threads per workgroup
+
+__global__ __launch_bounds__(GT, 2) void k_gram_tiles(
+    const double* __restrict__ X, int64_t nrows, int p, const double* __restrict__ mean,
+    int tilesPerSide, int64_t rowsPerSplit, double* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) double Ai[KC * LDSW];
+  __shared__ __attribute__((aligned(16))) double Aj[KC * LDSW];
+  // blockIdx.x -> (tile pair ti <= tj), blockIdx.y -> row split
+  int t = blockIdx.x, ti = 0;
+  while (t >= tilesPerSide - ti) { t -= tilesPerSide - ti; ++ti; }
+  const int tj = ti + t;
+  const int I0 = ti * TILE, J0 = tj * TILE;
+  const int64_t r0 = (int64_t)blockIdx.y * rowsPerSplit;
+  const int64_t r1 = min<int64_t>(nrows, r0 + rowsPerSplit);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wy = wave >> 1, wx = wave & 1;
+
+  cyc_double4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+
+  // Staging map: KC rows x 128 cols per panel = 2048 doubles; 256 threads x 8.
+  // thread -> row sr = tid >> 4, cols sc..sc+7 (sc = (tid & 15) * 8)
+  const int sr = tid >> 4, sc = (tid & 15) * 8;
+  double ri[8], rj[8];
+  auto load_panel = [&](const double* rowp, int c0, double* dst) {
+    if ((p & 1) == 0 && c0 + 8 <= p) {
+      // 64 contiguous bytes per thread: 4 x 16-byte loads
+      const double2* v = reinterpret_cast<const double2*>(rowp + c0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        double2 t2 = v[e];
+        dst[2 * e] = t2.x;
+        dst[2 * e + 1] = t2.y;
+      }
+      if (mean) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dst[e] = dsub(dst[e], mean[c0 + e]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c0 + e;
+        double v = 0.0;
+        if (c < p) {
+          v = rowp[c];
+          if (mean) v = dsub(v, mean[c]);
+        }
+        dst[e] = v;
+      }
+    }
+  };
+  auto load = [&](int64_t rb) {
+    const int64_t r = rb + sr;
+    if (r < r1) {
+      const double* rowp = X + r * p;
+      load_panel(rowp, I0 + sc, ri);
+      load_panel(rowp, J0 + sc, rj);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ri[e] = rj[e] = 0.0;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      Ai[sr * LDSW + sc + e] = ri[e];
+      Aj[sr * LDSW + sc + e] = rj[e];
+    }
+  };
+
+  if (r0 < r1) load(r0);
+  for (int64_t rb = r0; rb < r1; rb += KC) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (rb + KC < r1) load(rb + KC);
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 4) {
+      double a[4], b[4];
+      const int krow = kk + (lane >> 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[q] = Ai[krow * LDSW + wy * 64 + q * 16 + (lane & 15)];
+        b[q] = Aj[krow * LDSW + wx * 64 + q * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int qa = 0; qa < 4; ++qa)
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb)
+          acc[qa][qb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[qa], b[qb], acc[qa][qb], 0, 0, 0);
+    }
+  }
+
+  // slab layout: [split][tilepair][i (128)][j (128)]
+  const int pairs = tilesPerSide * (tilesPerSide + 1) / 2;
+  double* out = slab + ((size_t)blockIdx.y * pairs + blockIdx.x) * TILE * TILE;
+#pragma unroll
+  for (int qa = 0; qa < 4; ++qa)
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = wy * 64 + qa * 16 + (lane >> 4) + 4 * r;
+        const int j = wx * 64 + qb * 16 + (lane & 15);
+        out[i * TILE + j] = acc[qa][qb][r];
+      }
+}
+
+// U[iut(I0+i, J0+j)] += sum over splits (fixed order), upper triangle only.
+__global__ void k_gram_fold(const double* __restrict__ slab, int splits, int tilesPerSide, int p,
+                            double* __restrict__ U) {
+  const int pair = blockIdx.y;
+  int t = pair, ti = 0;
+  while (t >= tilesPerSide - ti) { t -= tilesPerSide - ti; ++ti; }
+  const int tj = ti + t;
+  const int pairs = tilesPerSide * (tilesPerSide + 1) / 2;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;   // i * 128 + j
+  if (e >= TILE * TILE) return;
+  const int i = e / TILE, j = e % TILE;
+  const int gi = ti * TILE + i, gj = tj * TILE + j;
+  if (gi >= p || gj >= p || gi > gj) return;
+  double s = 0.0;
+  for (int sp = 0; sp < splits; ++sp) s = dadd(s, slab[((size_t)sp * pairs + pair) * TILE * TILE + e]);
+  const int64_t idx = (int64_t)gj * (gj + 1) / 2 + gi;
+  U[idx] = dadd(U[idx], s);
+}
+
+// RowMatrix.triuToFull (:845-867): column-major full matrix from packed upper.
+__global__ void k_triu_to_full(int n, const double* __restrict__ U, double* __restrict__ G) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)n * n) return;
+  const int col = (int)(e / n), row = (int)(e % n);
+  G[e] = U[iut(row, col)];
+}
+
+// computeDenseVectorCovariance (:203-217): M(i,j) / (m - 1.0), symmetric.
+__global__ void k_cov_finalize(int n, const double* __restrict__ U, double m1,
+                               double* __restrict__ G) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)n * n) return;
+  const int col = (int)(e / n), row = (int)(e % n);
+  G[e] = U[iut(row, col)] / m1;
+}
+
+// Column sums over a row range per thread (coalesced across the columns of a
+// row), one partial per (split, column); folded in split order.  Feeds the
+// mean of Statistics.colStats (mllib/stat/Statistics.scala:57) used by
+// RowMatrix.computeCovariance (:452-467).
+__global__ void k_col_partial(const double* __restrict__ X, int64_t nrows, int p,
+                              int64_t rowsPerSplit, double* __restrict__ part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rowsPerSplit;
+  const int64_t r1 = min<int64_t>(nrows, r0 + rowsPerSplit);
+  double s = 0.0;
+  for (int64_t r = r0; r < r1; ++r) s = dadd(s, X[r * p + c]);
+  part[(int64_t)blockIdx.y * p + c] = s;
+}
+
+__global__ void k_col_fold(const double* __restrict__ part, int splits, int p,
+                           double* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p) return;
+  double s = 0.0;
+  for (int sp = 0; sp < splits; ++sp) s = dadd(s, part[(int64_t)sp * p + c]);
+  out[c] = dadd(out[c], s);
+}
+
+}  // namespace
+
+struct cyc_gramian_plan_s {
+  int p = 0;
+  std::mutex mu;
+  cyc::DeviceBuffer slab;
+};
+
+extern "C" {
+
+int cyc_gramian_plan_create(int32_t ncols, cyc_gramian_plan* plan) {
+  CYC_REQUIRE(plan != nullptr, "plan must not be null");
+  if (ncols > 65535)
+    CYC_REQUIRE(false, "Argument with more than 65535 cols: " + std::to_string(ncols));
+  CYC_REQUIRE(ncols > 0, "ncols must be positive");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    cyc::set_error("no HIP device visible");
+    return CYC_ERR_NO_DEVICE;
+  }
+  auto* p = new cyc_gramian_plan_s();
+  p->p = ncols;
+  *plan = p;
+  return CYC_OK;
+}
+
+int cyc_gramian_plan_destroy(cyc_gramian_plan plan) {
+  delete plan;
+  return CYC_OK;
+}
+
+int cyc_gramian_accumulate_dev(cyc_gramian_plan plan, const double* X, int64_t nrows,
+                               const double* mean, double* U, void* stream) {
+  CYC_REQUIRE(plan != nullptr && U != nullptr, "plan and U must not be null");
+  CYC_REQUIRE(nrows >= 0, "nrows >= 0");
+  if (nrows == 0) return CYC_OK;
+  std::lock_guard<std::mutex> g(plan->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  const int p = plan->p;
+  const int tps = (p + TILE - 1) / TILE;
+  const int pairs = tps * (tps + 1) / 2;
+  // split-K: aim for >= 2048 workgroups, at least 64 rows per split
+  int64_t splits = std::max<int64_t>(1, (2048 + pairs - 1) / pairs);
+  splits = std::min<int64_t>(splits, std::max<int64_t>(1, nrows / 64));
+  int64_t rps = cyc::round_up((nrows + splits - 1) / splits, KC);
+  splits = (nrows + rps - 1) / rps;
+  int rc = plan->slab.reserve(sizeof(double) * (size_t)splits * pairs * TILE * TILE);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_gram_tiles, dim3(pairs, (unsigned)splits), dim3(GT), 0, st, X, nrows, p,
+                     mean, tps, rps, (double*)plan->slab.ptr);
+  CYC_LAUNCH_CHECK("k_gram_tiles");
+  hipLaunchKernelGGL(k_gram_fold, dim3(TILE * TILE / 256, pairs), dim3(256), 0, st,
+                     (const double*)plan->slab.ptr, (int)splits, tps, p, U);
+  CYC_LAUNCH_CHECK("k_gram_fold");
+  return CYC_OK;
+}
+
+int cyc_col_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
+                     void* stream) {
+  CYC_REQUIRE(plan != nullptr && sums != nullptr, "plan and sums must not be null");
+  CYC_REQUIRE(nrows >= 0, "nrows >= 0");
+  if (nrows == 0) return CYC_OK;
+  std::lock_guard<std::mutex> g(plan->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  const int p = plan->p;
+  const int ctiles = (p + 255) / 256;
+  int64_t splits = std::max<int64_t>(1, std::min<int64_t>(4096 / ctiles, nrows / 256));
+  const int64_t rps = (nrows + splits - 1) / splits;
+  splits = (nrows + rps - 1) / rps;
+  int rc = plan->slab.reserve(sizeof(double) * (size_t)splits * p);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_col_partial, dim3(ctiles, (unsigned)splits), dim3(256), 0, st, X, nrows, p,
+                     rps, (double*)plan->slab.ptr);
+  CYC_LAUNCH_CHECK("k_col_partial");
+  hipLaunchKernelGGL(k_col_fold, dim3(ctiles), dim3(256), 0, st, (const double*)plan->slab.ptr,
+                     (int)splits, p, sums);
+  CYC_LAUNCH_CHECK("k_col_fold");
+  return CYC_OK;
+}
+
+int cyc_triu_to_full_dev(int32_t n, const double* U, double* G, void* stream) {
+  CYC_REQUIRE(n > 0 && U && G, "n > 0 and non-null buffers");
+  const int64_t tot = (int64_t)n * n;
+  hipLaunchKernelGGL(k_triu_to_full, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     cyc::as_stream(stream), n, U, G);
+  CYC_LAUNCH_CHECK("k_triu_to_full");
+  return CYC_OK;
+}
+
+int cyc_covariance_finalize_dev(int32_t n, const double* U, int64_t m, double* G, void* stream) {
+  CYC_REQUIRE(m > 1, "RowMatrix.computeCovariance called on matrix with only " +
+                         std::to_string(m) + " rows.  Cannot compute the covariance of a "
+                         "RowMatrix with <= 1 row.");
+  CYC_REQUIRE(n > 0 && U && G, "n > 0 and non-null buffers");
+  const int64_t tot = (int64_t)n * n;
+  hipLaunchKernelGGL(k_cov_finalize, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     cyc::as_stream(stream), n, U, (double)m - 1.0, G);
+  CYC_LAUNCH_CHECK("k_cov_finalize");
+  return CYC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,734 @@
+// logistic.hip -- LogisticRegression block aggregators on gfx950 (MI355X).
+//
+// Binary:      ml/optim/aggregator/BinaryLogisticBlockAggregator.scala:81-145
+// Multinomial: ml/optim/aggregator/MultinomialLogisticBlockAggregator.scala:101-189
+// Merge:       DifferentiableLossAggregator.scala:49-59 (gradientSum, lossSum,
+//              weightSum add up; done here in a fixed order, deterministic
+//              except the sparse binary gradient, see below).
+//
+// The device holds all blocks of a shard as one matrix (InstanceBlock rows
+// concatenated: dense row-major n x F, or CSR); one call is the whole
+// treeAggregate seqOp over the shard.
+//
+// Kernels
+//   k_binlog_dense<FPL>  HBM-bound: one wave per row stream, each lane holds
+//                        FPL coefficients and FPL gradient accumulators in
+//                        registers; margin by a fixed-shape wave reduction,
+//                        loss/multiplier epilogue, grad += mult * x.  One pass
+//                        over X.  Per-wave partials folded in wave order.
+//   k_binlog_csr         one wave per row: coef gathered by column index,
+//                        gradient scattered with hardware fp64 atomics
+//                        (global_atomic_add_f64).  One pass over the CSR.
+//   k_mlr_margins<CT>    margins = X W^T on fp64 MFMA (16x16x4), X staged in
+//                        LDS 64 x 64 at a time, W (C x F, 410 KB) read from
+//                        L2; softmax / loss / multiplier epilogue in
+//                        registers (cross-lane max and sum); writes the
+//                        multiplier matrix (n x CP) and per-wave partials.
+//   k_mlr_grad<CT>       grad^T (CP x F) = mult^T X on fp64 MFMA, split-K
+//                        over rows, 16-row chunks of both operands in LDS,
+//                        partial tiles to slabs folded in fixed order.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <mutex>
+
+#include "common.hpp"
+
+namespace {
+
+__device__ __forceinline__ double wave_sum_bcast(double s) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
+  return __shfl(s, 0);  // every lane takes lane 0's association order
+}
+
+// ml/impl/Utils.scala:91-97
+__device__ __forceinline__ double log1p_exp(double x) {
+  return x > 0 ? x + log1p(exp(-x)) : log1p(exp(x));
+}
+
+// Per-row binary epilogue, BinaryLogisticBlockAggregator.scala:104-122.
+// Returns the multiplier; accumulates loss and weight.
+__device__ __forceinline__ double bin_row(double margin, double w, double label, double& loss,
+                                          double& wsum) {
+  wsum += w;
+  if (w > 0) {
+    if (label > 0) loss += w * log1p_exp(-margin);
+    else loss += w * (log1p_exp(-margin) + margin);
+    return w * (1.0 / (1.0 + exp(-margin)) - label);
+  }
+  return 0.0;
+}
+
+template <int FPL>
+__global__ __launch_bounds__(256) void k_binlog_dense(
+    const double* __restrict__ X, const double* __restrict__ labels,
+    const double* __restrict__ weights, int64_t n, int F, const double* __restrict__ coef,
+    int fitIntercept, double offset, int64_t rowsPerWave, double* __restrict__ slabG,
+    double* __restrict__ slabS) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t r0 = gw * rowsPerWave;
+  const int64_t r1 = min<int64_t>(n, r0 + rowsPerWave);
+  double cf[FPL], g[FPL];
+#pragma unroll
+  for (int j = 0; j < FPL; ++j) {
+    const int f = lane + 64 * j;
+    cf[j] = f < F ? coef[f] : 0.0;
+    g[j] = 0.0;
+  }
+  double loss = 0.0, wsum = 0.0, msum = 0.0;
+  for (int64_t r = r0; r < r1; ++r) {
+    const double* xr = X + r * F;
+    double x[FPL];
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < FPL; ++j) {
+      const int f = lane + 64 * j;
+      x[j] = f < F ? xr[f] : 0.0;
+      s += x[j] * cf[j];
+    }
+    const double dot = wave_sum_bcast(s);
+    const double margin = fitIntercept ? offset + dot : dot;
+    const double w = weights ? weights[r] : 1.0;
+    const double mult = bin_row(margin, w, labels[r], loss, wsum);
+    msum += mult;
+    if (mult != 0.0) {
+#pragma unroll
+      for (int j = 0; j < FPL; ++j) g[j] += mult * x[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < FPL; ++j) {
+    const int f = lane + 64 * j;
+    if (f < F) slabG[gw * F + f] = g[j];
+  }
+  if (lane == 0) {
+    slabS[gw * 3 + 0] = loss;
+    slabS[gw * 3 + 1] = wsum;
+    slabS[gw * 3 + 2] = msum;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_binlog_csr(
+    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
+    const double* __restrict__ vals, const double* __restrict__ labels,
+    const double* __restrict__ weights, int64_t n, const double* __restrict__ coef,
+    int fitIntercept, double offset, int64_t rowsPerWave, double* __restrict__ gradAcc,
+    double* __restrict__ slabS) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t r0 = gw * rowsPerWave;
+  const int64_t r1 = min<int64_t>(n, r0 + rowsPerWave);
+  double loss = 0.0, wsum = 0.0, msum = 0.0;
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t p0 = rowptr[r], p1 = rowptr[r + 1];
+    // first 64 nonzeros stay in registers for the scatter
+    const int64_t q = p0 + lane;
+    double v0 = 0.0;
+    int c0 = 0;
+    if (q < p1) {
+      v0 = vals[q];
+      c0 = colidx[q];
+    }
+    double s = (q < p1) ? v0 * coef[c0] : 0.0;
+    for (int64_t p = q + 64; p < p1; p += 64) s += vals[p] * coef[colidx[p]];
+    const double dot = wave_sum_bcast(s);
+    const double margin = fitIntercept ? offset + dot : dot;
+    const double w = weights ? weights[r] : 1.0;
+    const double mult = bin_row(margin, w, labels[r], loss, wsum);
+    msum += mult;
+    if (mult != 0.0) {
+      if (q < p1) unsafeAtomicAdd(&gradAcc[c0], v0 * mult);
+      for (int64_t p = q + 64; p < p1; p += 64) unsafeAtomicAdd(&gradAcc[colidx[p]], vals[p] * mult);
+    }
+  }
+  if (lane == 0) {
+    slabS[gw * 3 + 0] = loss;
+    slabS[gw * 3 + 1] = wsum;
+    slabS[gw * 3 + 2] = msum;
+  }
+}
+
+// Fold per-wave scalars in wave order: out3 = {loss, wsum, msum}.
+__global__ void k_fold_scalars(const double* __restrict__ slabS, int64_t waves, int width,
+                               double* __restrict__ out) {
+  __shared__ double sh[256];
+  for (int c = 0; c < width; ++c) {
+    double a = 0.0;
+    const int64_t per = (waves + 255) / 256;
+    const int64_t w0 = threadIdx.x * per, w1 = min<int64_t>(waves, w0 + per);
+    for (int64_t w = w0; w < w1; ++w) a += slabS[w * width + c];
+    sh[threadIdx.x] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+      for (int i = 0; i < 256; ++i) t += sh[i];
+      out[c] = t;
+    }
+    __syncthreads();
+  }
+}
+
+// grad[f] += sum_w slabG[w][f] (or += gradAcc[f]); then the fitWithMean
+// correction (daxpy(-multiplierSum, scaledMean), :132-137) and the intercept
+// (:139-142).  scal = {loss, wsum, msum}.
+__global__ void k_binlog_fold(const double* __restrict__ slabG, int64_t waves,
+                              const double* __restrict__ gradAcc, int F,
+                              const double* __restrict__ scal, int fitIntercept, int fitWithMean,
+                              const double* __restrict__ scaledMean, double* __restrict__ grad,
+                              double* __restrict__ lossSum, double* __restrict__ weightSum) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  const double msum = scal[2];
+  if (f < F) {
+    double s = 0.0;
+    if (slabG) {
+      for (int64_t w = 0; w < waves; ++w) s += slabG[w * F + f];
+    } else {
+      s = gradAcc[f];
+    }
+    double gf = grad[f] + s;
+    if (fitWithMean) gf = gf + (-msum) * scaledMean[f];
+    grad[f] = gf;
+  }
+  if (f == 0) {
+    if (fitIntercept) grad[F] += msum;
+    *lossSum += scal[0];
+    *weightSum += scal[1];
+  }
+}
+
+// marginOffset (Binary :67-72): coef[F] - sum_f coef[f]*scaledMean[f]
+__global__ void k_binlog_offset(const double* __restrict__ coef, const double* __restrict__ sm,
+                                int F, double* __restrict__ out) {
+  double dd = 0.0;
+  for (int f = 0; f < F; ++f) dd += coef[f] * sm[f];
+  out[0] = coef[F] - dd;
+}
+
+// --------------------------------------------------------- multinomial
+// marginOffset (Multinomial :86-92): intercept + gemv(-1.0, linear, scaledMean)
+// with netlib dgemv "N" column order.
+__global__ void k_mlr_offset(const double* __restrict__ coef, const double* __restrict__ sm,
+                             int F, int C, double* __restrict__ off) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double o = coef[(int64_t)C * F + c];
+  for (int f = 0; f < F; ++f) {
+    if (sm[f] != 0.0) {
+      const double t = -1.0 * sm[f];
+      o = o + t * coef[(int64_t)f * C + c];
+    }
+  }
+  off[c] = o;
+}
+
+constexpr int MR = 64;     // rows per margin tile
+constexpr int MK = 64;     // features per LDS chunk
+constexpr int MKS = MK + 2;
+
+template <int CT>
+__global__ __launch_bounds__(256, 2) void k_mlr_margins(
+    const double* __restrict__ X, const double* __restrict__ labels,
+    const double* __restrict__ weights, int64_t n, int F, int C, const double* __restrict__ coef,
+    const double* __restrict__ offset, double* __restrict__ mult, double* __restrict__ slabS,
+    double* __restrict__ slabMS) {
+  constexpr int CP = CT * 16;
+  __shared__ __attribute__((aligned(16))) double Xs[MR * MKS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t tiles = (n + MR - 1) / MR;
+  double loss = 0.0, wsum = 0.0;
+  double ms[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) ms[ct] = 0.0;
+  double offc[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int c = ct * 16 + (lane & 15);
+    offc[ct] = (offset && c < C) ? offset[c] : 0.0;
+  }
+
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int64_t r0 = tile * MR;
+    cyc_double4 acc[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[ct] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+    for (int f0 = 0; f0 < F; f0 += MK) {
+      __syncthreads();
+      for (int e = tid; e < MR * MK; e += 256) {
+        const int rr = e / MK, ff = e % MK;
+        const int64_t r = r0 + rr;
+        const int f = f0 + ff;
+        Xs[rr * MKS + ff] = (r < n && f < F) ? X[r * F + f] : 0.0;
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int kk = 0; kk < MK; kk += 4) {
+        const double a = Xs[(wave * 16 + (lane & 15)) * MKS + kk + (lane >> 4)];
+        const int f = f0 + kk + (lane >> 4);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int c = ct * 16 + (lane & 15);
+          const double b = (f < F && c < C) ? coef[(int64_t)f * C + c] : 0.0;
+          acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[ct], 0, 0, 0);
+        }
+      }
+    }
+    // Epilogue: lane holds rows (lane>>4) + 4r of this wave's 16, classes
+    // 16 ct + (lane & 15).
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = r0 + wave * 16 + (lane >> 4) + 4 * r;
+      const bool rowok = row < n;
+      double m[CT];
+      double mx = -1.7976931348623157e308;  // Double.MinValue (Utils.scala:113)
+      int infc = 1 << 30;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int c = ct * 16 + (lane & 15);
+        m[ct] = acc[ct][r] + offc[ct];  // 1.0*temp + 1.0*offset (netlib dgemm)
+        if (c < C) {
+          if (m[ct] == __builtin_inf()) infc = min(infc, c);
+          else if (m[ct] > mx) mx = m[ct];
+        }
+      }
+#pragma unroll
+      for (int k = 1; k < 16; k <<= 1) {
+        mx = fmax(mx, __shfl_xor(mx, k));
+        infc = min(infc, __shfl_xor(infc, k));
+      }
+      double p[CT];
+      if (infc < (1 << 30)) {
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int c = ct * 16 + (lane & 15);
+          p[ct] = (c == infc) ? 1.0 : 0.0 * m[ct];
+        }
+      } else {
+        double sum = 0.0;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int c = ct * 16 + (lane & 15);
+          p[ct] = (c < C) ? exp(m[ct] - mx) : 0.0;
+          sum += p[ct];
+        }
+#pragma unroll
+        for (int k = 1; k < 16; k <<= 1) sum += __shfl_xor(sum, k);
+        sum = __shfl(sum, lane & 48);  // one association order per row
+        const double inv = 1.0 / sum;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) p[ct] = inv * p[ct];
+      }
+      const double w = rowok ? (weights ? weights[row] : 1.0) : 0.0;
+      const int label = rowok ? (int)labels[row] : 0;
+      // probability of the label class, from the lane that holds it
+      double pl = 0.0;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        if (ct == (label >> 4)) pl = p[ct];
+      pl = __shfl(pl, (lane & 48) | (label & 15));
+      if (rowok && (lane & 15) == 0) {
+        wsum += w;
+        if (w > 0) loss -= w * log(pl);
+      }
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const int c = ct * 16 + (lane & 15);
+        double mu;
+        if (w > 0) {
+          mu = (w != 1.0) ? w * p[ct] : p[ct];
+          if (c == label) mu -= w;
+        } else {
+          mu = 0.0 * p[ct];
+        }
+        if (c >= C || !rowok) mu = 0.0;
+        if (rowok) mult[row * CP + c] = mu;
+        ms[ct] += mu;
+      }
+    }
+  }
+  // per-wave partials: loss/wsum from lanes with (lane & 15) == 0, multSum
+  // per class summed over the 4 row groups of the wave.
+#pragma unroll
+  for (int k = 16; k < 64; k <<= 1) {
+    loss += __shfl_xor(loss, k);
+    wsum += __shfl_xor(wsum, k);
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) ms[ct] += __shfl_xor(ms[ct], k);
+  }
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+  if (lane == 0) {
+    slabS[gw * 2 + 0] = loss;
+    slabS[gw * 2 + 1] = wsum;
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) slabMS[gw * CP + ct * 16 + lane] = ms[ct];
+  }
+}
+
+constexpr int GR = 16;    // rows per LDS chunk in the gradient GEMM
+constexpr int GF = 256;   // features per workgroup
+constexpr int GFS = GF + 16;
+
+template <int CT>
+__global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mult,
+                                                  const double* __restrict__ X, int64_t n, int F,
+                                                  int64_t rowsPerSplit,
+                                                  double* __restrict__ slab) {
+  constexpr int CP = CT * 16;
+  constexpr int CPS = CP + ((16 - CP % 32) + 32) % 32;
+  __shared__ __attribute__((aligned(16))) double Ms[GR * CPS];
+  __shared__ __attribute__((aligned(16))) double Xs[GR * GFS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int F0 = blockIdx.x * GF;
+  const int64_t r0 = (int64_t)blockIdx.y * rowsPerSplit;
+  const int64_t r1 = min<int64_t>(n, r0 + rowsPerSplit);
+  cyc_double4 acc[CT][2];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) acc[ct][0] = acc[ct][1] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+  for (int64_t rb = r0; rb < r1; rb += GR) {
+    __syncthreads();
+    for (int e = tid; e < GR * CP; e += 512) {
+      const int rr = e / CP, c = e % CP;
+      const int64_t r = rb + rr;
+      Ms[rr * CPS + c] = (r < r1) ? mult[r * CP + c] : 0.0;
+    }
+    for (int e = tid; e < GR * GF; e += 512) {
+      const int rr = e / GF, ff = e % GF;
+      const int64_t r = rb + rr;
+      const int f = F0 + ff;
+      Xs[rr * GFS + ff] = (r < r1 && f < F) ? X[r * F + f] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < GR; kk += 4) {
+      const int krow = kk + (lane >> 4);
+      double b0 = Xs[krow * GFS + wave * 32 + (lane & 15)];
+      double b1 = Xs[krow * GFS + wave * 32 + 16 + (lane & 15)];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) {
+        const double a = Ms[krow * CPS + ct * 16 + (lane & 15)];
+        acc[ct][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b0, acc[ct][0], 0, 0, 0);
+        acc[ct][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b1, acc[ct][1], 0, 0, 0);
+      }
+    }
+  }
+  // slab[split][ftile][c][f_local]
+  double* out = slab + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * CP * GF;
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = ct * 16 + (lane >> 4) + 4 * r;
+        const int fl = wave * 32 + q * 16 + (lane & 15);
+        out[(size_t)c * GF + fl] = acc[ct][q][r];
+      }
+}
+
+// grad[f*C + c] += sum_s slab (fixed order); the dger fitWithMean correction
+// (:180-181) and the intercept daxpy (:184-185).  ms[CP] = total multSum.
+__global__ void k_mlr_fold(const double* __restrict__ slab, int splits, int ftiles, int CP, int F,
+                           int C, const double* __restrict__ ms, int fitIntercept,
+                           int fitWithMean, const double* __restrict__ sm,
+                           double* __restrict__ grad) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // c * F + f
+  if (e < (int64_t)C * F) {
+    const int c = (int)(e / F), f = (int)(e % F);
+    const int ft = f / GF, fl = f % GF;
+    double s = 0.0;
+    for (int sp = 0; sp < splits; ++sp)
+      s += slab[(((size_t)sp * ftiles + ft) * CP + c) * GF + fl];
+    double g = 1.0 * s + 1.0 * grad[(int64_t)f * C + c];
+    if (fitIntercept && fitWithMean && sm[f] != 0.0) g = g + ms[c] * (-1.0 * sm[f]);
+    grad[(int64_t)f * C + c] = g;
+  }
+  if (fitIntercept && e < C) grad[(int64_t)C * F + e] = grad[(int64_t)C * F + e] + 1.0 * ms[e];
+}
+
+// Fold per-wave class sums: out[c] = sum_w slabMS[w][c]; scalars likewise.
+__global__ void k_fold_columns(const double* __restrict__ slab, int64_t rows, int width,
+                               double* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= width) return;
+  double s = 0.0;
+  for (int64_t w = 0; w < rows; ++w) s += slab[w * width + c];
+  out[c] = s;
+}
+
+__global__ void k_add_scalars(const double* __restrict__ s2, double* __restrict__ lossSum,
+                              double* __restrict__ weightSum) {
+  *lossSum += s2[0];
+  *weightSum += s2[1];
+}
+
+}  // namespace
+
+struct cyc_logistic_plan_s {
+  int F = 0, C = 1, fitIntercept = 0, fitWithMean = 0;
+  std::mutex mu;
+  cyc::DeviceBuffer slabG, slabS, slabMS, gradAcc, scal, offset, multBuf, gslab, msTot;
+};
+
+namespace {
+
+int check_common(cyc_logistic_plan p, const double* coef, const double* sm) {
+  CYC_REQUIRE(p != nullptr && coef != nullptr, "plan and coefficients must not be null");
+  if (p->fitWithMean) {
+    CYC_REQUIRE(p->fitIntercept, "for training without intercept, should not center the vectors");
+    CYC_REQUIRE(sm != nullptr, "scaled means is required when center the vectors");
+  }
+  return CYC_OK;
+}
+
+template <int FPL>
+void launch_bin_dense(dim3 g, hipStream_t st, const double* X, const double* labels,
+                      const double* weights, int64_t n, int F, const double* coef, int fi,
+                      double offset, int64_t rpw, double* sg, double* ss) {
+  hipLaunchKernelGGL(k_binlog_dense<FPL>, g, dim3(256), 0, st, X, labels, weights, n, F, coef, fi,
+                     offset, rpw, sg, ss);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cyc_logistic_plan_create(int32_t numFeatures, int32_t numClasses, int fitIntercept,
+                             int fitWithMean, cyc_logistic_plan* plan) {
+  CYC_REQUIRE(plan != nullptr, "plan must not be null");
+  CYC_REQUIRE(numFeatures > 0, "numFeatures must be positive");
+  CYC_REQUIRE(numClasses >= 1, "numClasses must be positive");
+  if (fitWithMean)
+    CYC_REQUIRE(fitIntercept, "for training without intercept, should not center the vectors");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    cyc::set_error("no HIP device visible");
+    return CYC_ERR_NO_DEVICE;
+  }
+  auto* p = new cyc_logistic_plan_s();
+  p->F = numFeatures;
+  p->C = numClasses;
+  p->fitIntercept = fitIntercept != 0;
+  p->fitWithMean = fitWithMean != 0;
+  *plan = p;
+  return CYC_OK;
+}
+
+int cyc_logistic_plan_destroy(cyc_logistic_plan plan) {
+  delete plan;
+  return CYC_OK;
+}
+
+int cyc_binary_logistic_add_dense_dev(cyc_logistic_plan p, const double* X, const double* labels,
+                                      const double* weights, int64_t n, const double* coef,
+                                      const double* scaledMean, double* grad, double* lossSum,
+                                      double* weightSum, void* stream) {
+  int rc = check_common(p, coef, scaledMean);
+  if (rc) return rc;
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  if (n == 0) return CYC_OK;
+  const int F = p->F;
+  if (F > 64 * 32) {
+    cyc::set_error("dense binary aggregator supports numFeatures <= 2048 (use CSR blocks)");
+    return CYC_ERR_UNSUPPORTED;
+  }
+  std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  const int64_t waves = std::min<int64_t>(4096, n);
+  const int64_t rpw = (n + waves - 1) / waves;
+  const int64_t nw = (n + rpw - 1) / rpw;
+  const int64_t blocks = (nw + 3) / 4;
+  const int64_t wtot = blocks * 4;
+  if ((rc = p->slabG.reserve(sizeof(double) * (size_t)wtot * F)) ||
+      (rc = p->slabS.reserve(sizeof(double) * (size_t)wtot * 3)) ||
+      (rc = p->scal.reserve(sizeof(double) * 4)) || (rc = p->offset.reserve(sizeof(double) * 2)))
+    return rc;
+  double offset = 0.0;
+  if (p->fitIntercept) {
+    if (p->fitWithMean) {
+      hipLaunchKernelGGL(k_binlog_offset, dim3(1), dim3(1), 0, st, coef, scaledMean, F,
+                         (double*)p->offset.ptr);
+      CYC_HIP(hipMemcpyAsync(&offset, p->offset.ptr, sizeof(double), hipMemcpyDeviceToHost, st));
+    } else {
+      CYC_HIP(hipMemcpyAsync(&offset, coef + F, sizeof(double), hipMemcpyDeviceToHost, st));
+    }
+    CYC_HIP(hipStreamSynchronize(st));
+  }
+  // zero the partial slabs of waves beyond nw (they still get written: rows empty)
+  dim3 grid((unsigned)blocks);
+  const int fpl = (F + 63) / 64;
+  double* sg = (double*)p->slabG.ptr;
+  double* ss = (double*)p->slabS.ptr;
+  if (fpl <= 1) launch_bin_dense<1>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
+  else if (fpl <= 2) launch_bin_dense<2>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
+  else if (fpl <= 4) launch_bin_dense<4>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
+  else if (fpl <= 8) launch_bin_dense<8>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
+  else if (fpl <= 16) launch_bin_dense<16>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
+  else launch_bin_dense<32>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
+  CYC_LAUNCH_CHECK("k_binlog_dense");
+  hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, ss, wtot, 3, (double*)p->scal.ptr);
+  CYC_LAUNCH_CHECK("k_fold_scalars");
+  hipLaunchKernelGGL(k_binlog_fold, dim3((F + 255) / 256), dim3(256), 0, st, sg, wtot, nullptr,
+                     F, (const double*)p->scal.ptr, p->fitIntercept, p->fitWithMean, scaledMean,
+                     grad, lossSum, weightSum);
+  CYC_LAUNCH_CHECK("k_binlog_fold");
+  return CYC_OK;
+}
+
+int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
+                                    const int32_t* colidx, const double* vals,
+                                    const double* labels, const double* weights, int64_t n,
+                                    const double* coef, const double* scaledMean, double* grad,
+                                    double* lossSum, double* weightSum, void* stream) {
+  int rc = check_common(p, coef, scaledMean);
+  if (rc) return rc;
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  if (n == 0) return CYC_OK;
+  const int F = p->F;
+  std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  const int64_t waves = std::min<int64_t>(16384, n);
+  const int64_t rpw = (n + waves - 1) / waves;
+  const int64_t nw = (n + rpw - 1) / rpw;
+  const int64_t blocks = (nw + 3) / 4;
+  const int64_t wtot = blocks * 4;
+  if ((rc = p->gradAcc.reserve(sizeof(double) * (size_t)F)) ||
+      (rc = p->slabS.reserve(sizeof(double) * (size_t)wtot * 3)) ||
+      (rc = p->scal.reserve(sizeof(double) * 4)) || (rc = p->offset.reserve(sizeof(double) * 2)))
+    return rc;
+  double offset = 0.0;
+  if (p->fitIntercept) {
+    if (p->fitWithMean) {
+      hipLaunchKernelGGL(k_binlog_offset, dim3(1), dim3(1), 0, st, coef, scaledMean, F,
+                         (double*)p->offset.ptr);
+      CYC_HIP(hipMemcpyAsync(&offset, p->offset.ptr, sizeof(double), hipMemcpyDeviceToHost, st));
+    } else {
+      CYC_HIP(hipMemcpyAsync(&offset, coef + F, sizeof(double), hipMemcpyDeviceToHost, st));
+    }
+    CYC_HIP(hipStreamSynchronize(st));
+  }
+  CYC_HIP(hipMemsetAsync(p->gradAcc.ptr, 0, sizeof(double) * (size_t)F, st));
+  hipLaunchKernelGGL(k_binlog_csr, dim3((unsigned)blocks), dim3(256), 0, st, rowptr, colidx, vals,
+                     labels, weights, n, coef, p->fitIntercept, offset, rpw,
+                     (double*)p->gradAcc.ptr, (double*)p->slabS.ptr);
+  CYC_LAUNCH_CHECK("k_binlog_csr");
+  hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, (const double*)p->slabS.ptr, wtot,
+                     3, (double*)p->scal.ptr);
+  CYC_LAUNCH_CHECK("k_fold_scalars");
+  hipLaunchKernelGGL(k_binlog_fold, dim3((F + 255) / 256), dim3(256), 0, st, nullptr, 0,
+                     (const double*)p->gradAcc.ptr, F, (const double*)p->scal.ptr,
+                     p->fitIntercept, p->fitWithMean, scaledMean, grad, lossSum, weightSum);
+  CYC_LAUNCH_CHECK("k_binlog_fold");
+  return CYC_OK;
+}
+
+int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
+                                           const double* labels, const double* weights,
+                                           int64_t n, const double* coef,
+                                           const double* scaledMean, double* grad,
+                                           double* lossSum, double* weightSum, void* stream) {
+  int rc = check_common(p, coef, scaledMean);
+  if (rc) return rc;
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  if (n == 0) return CYC_OK;
+  const int F = p->F, C = p->C;
+  if (C > 128) {
+    cyc::set_error("multinomial aggregator supports numClasses <= 128");
+    return CYC_ERR_UNSUPPORTED;
+  }
+  const int CT = (C + 15) / 16, CP = CT * 16;
+  std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  // Rows are processed in chunks so the multiplier matrix stays small.
+  const int64_t chunk = std::min<int64_t>(n, 4 << 20);
+  const int mblocks = 2048;
+  const int64_t mwaves = (int64_t)mblocks * 4;
+  const int ftiles = (F + GF - 1) / GF;
+  if ((rc = p->multBuf.reserve(sizeof(double) * (size_t)chunk * CP)) ||
+      (rc = p->slabS.reserve(sizeof(double) * (size_t)mwaves * 2)) ||
+      (rc = p->slabMS.reserve(sizeof(double) * (size_t)mwaves * CP)) ||
+      (rc = p->scal.reserve(sizeof(double) * 4)) ||
+      (rc = p->msTot.reserve(sizeof(double) * CP)) ||
+      (rc = p->offset.reserve(sizeof(double) * (size_t)C)))
+    return rc;
+  const double* off = nullptr;
+  if (p->fitIntercept) {
+    if (p->fitWithMean) {
+      hipLaunchKernelGGL(k_mlr_offset, dim3((C + 63) / 64), dim3(64), 0, st, coef, scaledMean, F,
+                         C, (double*)p->offset.ptr);
+      CYC_LAUNCH_CHECK("k_mlr_offset");
+      off = (const double*)p->offset.ptr;
+    } else {
+      off = coef + (int64_t)C * F;
+    }
+  }
+  for (int64_t c0 = 0; c0 < n; c0 += chunk) {
+    const int64_t m = std::min(chunk, n - c0);
+    const double* Xc = X + c0 * F;
+    const double* lc = labels + c0;
+    const double* wc = weights ? weights + c0 : nullptr;
+    const int64_t tiles = (m + MR - 1) / MR;
+    const unsigned mb = (unsigned)std::min<int64_t>(mblocks, tiles);
+    CYC_HIP(hipMemsetAsync(p->slabS.ptr, 0, sizeof(double) * (size_t)mwaves * 2, st));
+    CYC_HIP(hipMemsetAsync(p->slabMS.ptr, 0, sizeof(double) * (size_t)mwaves * CP, st));
+#define CYC_MLR_M(CTV)                                                                        \
+  hipLaunchKernelGGL(k_mlr_margins<CTV>, dim3(mb), dim3(256), 0, st, Xc, lc, wc, m, F, C, coef, \
+                     off, (double*)p->multBuf.ptr, (double*)p->slabS.ptr, (double*)p->slabMS.ptr)
+    switch (CT) {
+      case 1: CYC_MLR_M(1); break;
+      case 2: CYC_MLR_M(2); break;
+      case 3: CYC_MLR_M(3); break;
+      case 4: CYC_MLR_M(4); break;
+      case 5: CYC_MLR_M(5); break;
+      case 6: CYC_MLR_M(6); break;
+      case 7: CYC_MLR_M(7); break;
+      default: CYC_MLR_M(8); break;
+    }
+#undef CYC_MLR_M
+    CYC_LAUNCH_CHECK("k_mlr_margins");
+    // split-K over rows for the gradient GEMM: ~2048 workgroups
+    int64_t splits = std::max<int64_t>(1, 2048 / ftiles);
+    splits = std::min<int64_t>(splits, std::max<int64_t>(1, m / 64));
+    const int64_t rps = cyc::round_up((m + splits - 1) / splits, GR);
+    splits = (m + rps - 1) / rps;
+    if ((rc = p->gslab.reserve(sizeof(double) * (size_t)splits * ftiles * CP * GF))) return rc;
+#define CYC_MLR_G(CTV)                                                                         \
+  hipLaunchKernelGGL(k_mlr_grad<CTV>, dim3(ftiles, (unsigned)splits), dim3(512), 0, st,         \
+                     (const double*)p->multBuf.ptr, Xc, m, F, rps, (double*)p->gslab.ptr)
+    switch (CT) {
+      case 1: CYC_MLR_G(1); break;
+      case 2: CYC_MLR_G(2); break;
+      case 3: CYC_MLR_G(3); break;
+      case 4: CYC_MLR_G(4); break;
+      case 5: CYC_MLR_G(5); break;
+      case 6: CYC_MLR_G(6); break;
+      case 7: CYC_MLR_G(7); break;
+      default: CYC_MLR_G(8); break;
+    }
+#undef CYC_MLR_G
+    CYC_LAUNCH_CHECK("k_mlr_grad");
+    hipLaunchKernelGGL(k_fold_columns, dim3((CP + 127) / 128), dim3(128), 0, st,
+                       (const double*)p->slabMS.ptr, mwaves, CP, (double*)p->msTot.ptr);
+    CYC_LAUNCH_CHECK("k_fold_columns");
+    hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, (const double*)p->slabS.ptr,
+                       mwaves, 2, (double*)p->scal.ptr);
+    CYC_LAUNCH_CHECK("k_fold_scalars");
+    const int64_t tot = std::max<int64_t>((int64_t)C * F, C);
+    hipLaunchKernelGGL(k_mlr_fold, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st,
+                       (const double*)p->gslab.ptr, (int)splits, ftiles, CP, F, C,
+                       (const double*)p->msTot.ptr, p->fitIntercept, p->fitWithMean, scaledMean,
+                       grad);
+    CYC_LAUNCH_CHECK("k_mlr_fold");
+    hipLaunchKernelGGL(k_add_scalars, dim3(1), dim3(1), 0, st, (const double*)p->scal.ptr,
+                       lossSum, weightSum);
+    CYC_LAUNCH_CHECK("k_add_scalars");
+  }
+  return CYC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,159 @@
+"""RowMatrix on MI355X: host-side mirror of
+mllib/linalg/distributed/RowMatrix.scala (Gramian, covariance, PCA).
+
+`rows` is this rank's device-resident shard (torch fp64 CUDA tensor, n x p,
+row-major: an RDD of DenseVector rows).  computeGramianMatrix /
+computeCovariance run the fp64-MFMA syrk of libcyclone and, when
+torch.distributed is initialised, merge the packed triangle with one
+all-reduce (the treeAggregate combOp U1 += U2, :149-157).  The eigensolve of
+PCA stays on the host (breeze svd on the driver in the reference, :501).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from . import parallel
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _dist():
+    torch = _torch()
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        return torch.distributed
+    return None
+
+
+class GramianPlan:
+    def __init__(self, ncols):
+        self._lib = N.load()
+        h = ctypes.c_void_p()
+        N.check(self._lib.cyc_gramian_plan_create(int(ncols), ctypes.byref(h)))
+        self.handle = h
+        self.p = int(ncols)
+
+    def close(self):
+        if self.handle:
+            self._lib.cyc_gramian_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def accumulate(self, X, U, mean=None, stream=None):
+        N.check(self._lib.cyc_gramian_accumulate_dev(self.handle, N.ptr(X), int(X.shape[0]),
+                                                     N.ptr(mean), N.ptr(U),
+                                                     N.stream_handle(stream)))
+
+    def col_sums(self, X, out, stream=None):
+        N.check(self._lib.cyc_col_sums_dev(self.handle, N.ptr(X), int(X.shape[0]), N.ptr(out),
+                                           N.stream_handle(stream)))
+
+
+def triu_to_full(n, U, stream=None):
+    """RowMatrix.triuToFull (:845-867) on device; returns the (n, n) matrix."""
+    torch = _torch()
+    G = torch.empty(n * n, dtype=torch.float64, device=U.device)
+    N.check(N.load().cyc_triu_to_full_dev(int(n), N.ptr(U), N.ptr(G), N.stream_handle(stream)))
+    return G.view(n, n).t()   # column-major storage -> G[i, j]
+
+
+class RowMatrix:
+    """RowMatrix(rows) over a device-resident shard."""
+
+    def __init__(self, rows, nRows: int = 0, nCols: int = 0):
+        self.rows = rows
+        self._nRows = nRows
+        self._nCols = nCols
+
+    def numCols(self) -> int:
+        if self._nCols <= 0:
+            if self.rows.shape[0] == 0 and _dist() is None:
+                raise RuntimeError("Cannot determine the number of cols because it is not "
+                                   "specified in the constructor and the rows RDD is empty.")
+            self._nCols = int(self.rows.shape[1])
+        return self._nCols
+
+    def numRows(self) -> int:
+        if self._nRows <= 0:
+            n = int(self.rows.shape[0])
+            d = _dist()
+            if d is not None:
+                t = _torch().tensor([n], dtype=_torch().int64, device=self.rows.device)
+                d.all_reduce(t)
+                n = int(t.item())
+            if n == 0:
+                raise RuntimeError("Cannot determine the number of rows because it is not "
+                                   "specified in the constructor and the rows RDD is empty.")
+            self._nRows = n
+        return self._nRows
+
+    @staticmethod
+    def _checkNumColumns(cols):
+        if cols > 65535:
+            raise N.IllegalArgumentException(f"Argument with more than 65535 cols: {cols}")
+
+    def _packed(self, mean=None):
+        torch = _torch()
+        n = self.numCols()
+        self._checkNumColumns(n)
+        U = torch.zeros(n * (n + 1) // 2, dtype=torch.float64, device=self.rows.device)
+        plan = GramianPlan(n)
+        plan.accumulate(self.rows, U, mean)
+        parallel.allreduce_(U)             # treeAggregate combOp U1 += U2
+        return U
+
+    def computeGramianMatrixPacked(self):
+        return self._packed()
+
+    def computeGramianMatrix(self) -> np.ndarray:
+        """RowMatrix.scala:130-161; returns the full n x n matrix (host)."""
+        n = self.numCols()
+        return triu_to_full(n, self._packed()).cpu().numpy()
+
+    def _column_mean(self):
+        torch = _torch()
+        n = self.numCols()
+        s = torch.zeros(n, dtype=torch.float64, device=self.rows.device)
+        GramianPlan(n).col_sums(self.rows, s)
+        parallel.allreduce_(s)
+        m = self.numRows()
+        return s / m, m
+
+    def computeCovariance(self) -> np.ndarray:
+        """RowMatrix.scala:452-467 -> computeDenseVectorCovariance (:163-220)."""
+        torch = _torch()
+        n = self.numCols()
+        self._checkNumColumns(n)
+        mean, m = self._column_mean()
+        if not m > 1:
+            raise N.IllegalArgumentException(
+                f"RowMatrix.computeCovariance called on matrix with only {m} rows.  Cannot "
+                "compute the covariance of a RowMatrix with <= 1 row.")
+        U = self._packed(mean)
+        G = torch.empty(n * n, dtype=torch.float64, device=U.device)
+        N.check(N.load().cyc_covariance_finalize_dev(int(n), N.ptr(U), int(m), N.ptr(G),
+                                                     N.stream_handle()))
+        return G.view(n, n).t().cpu().numpy()
+
+    def computePrincipalComponentsAndExplainedVariance(self, k: int):
+        """RowMatrix.scala:486-513 (n <= 65535 branch); eigensolve on host."""
+        n = self.numCols()
+        if not (0 < k <= n):
+            raise N.IllegalArgumentException(f"k = {k} out of range (0, n = {n}]")
+        cov = self.computeCovariance()
+        u, s, _ = np.linalg.svd(cov)
+        explained = s / s.sum()
+        return u[:, :k].copy(), explained[:k].copy()
+
+    def computePrincipalComponents(self, k: int):
+        return self.computePrincipalComponentsAndExplainedVariance(k)[0]

@@ -1,0 +1,294 @@
+"""Logistic-regression loss aggregation on MI355X.
+
+Host-side mirror of
+  ml/optim/aggregator/DifferentiableLossAggregator.scala:30-80
+  ml/optim/aggregator/BinaryLogisticBlockAggregator.scala:41-146
+  ml/optim/aggregator/MultinomialLogisticBlockAggregator.scala:45-190
+  ml/optim/loss/RDDLossFunction.scala:47-70 (+ L2Regularization)
+with the same names, argument meaning and `require` messages.  A "block" is
+a device-resident InstanceBlock (ml/feature/Instance.scala:39-106): all
+blocks of a shard concatenated into one dense row-major (n x F) tensor or one
+CSR triple, with labels and optional weights (None = the empty weights array
+of an all-unit-weight block).  `add` runs the whole shard through
+libcyclone's aggregator kernels; `merge` and `RDDLossFunction.calculate`
+reproduce treeAggregate, with an RCCL all-reduce across ranks.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+from . import parallel
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class DeviceInstanceBlock:
+    """InstanceBlock rows resident in HBM (dense or CSR, isTransposed=true)."""
+
+    def __init__(self, labels, weights=None, X=None, rowptr=None, colidx=None, values=None,
+                 numFeatures=None):
+        self.labels = labels
+        self.weights = weights
+        self.X = X
+        self.rowptr, self.colidx, self.values = rowptr, colidx, values
+        if X is not None:
+            self.numFeatures = int(X.shape[1])
+            self.size = int(X.shape[0])
+        else:
+            if numFeatures is None:
+                raise N.IllegalArgumentException("numFeatures is required for CSR blocks")
+            self.numFeatures = int(numFeatures)
+            self.size = int(rowptr.shape[0]) - 1
+        if int(labels.shape[0]) != self.size:
+            raise N.IllegalArgumentException("requirement failed")  # Instance.scala:43
+        if weights is not None and int(weights.shape[0]) != self.size:
+            raise N.IllegalArgumentException("requirement failed")  # Instance.scala:46
+
+    @property
+    def is_sparse(self):
+        return self.X is None
+
+    @staticmethod
+    def from_numpy(labels, weights=None, X=None, csr=None, numFeatures=None, device="cuda"):
+        torch = _torch()
+        t = lambda a, dt: None if a is None else torch.as_tensor(np.ascontiguousarray(a, dtype=dt), device=device)
+        if csr is not None:
+            rp, ci, v = csr
+            return DeviceInstanceBlock(t(labels, np.float64), t(weights, np.float64),
+                                       rowptr=t(rp, np.int64), colidx=t(ci, np.int32),
+                                       values=t(v, np.float64), numFeatures=numFeatures)
+        return DeviceInstanceBlock(t(labels, np.float64), t(weights, np.float64),
+                                   X=t(X, np.float64))
+
+
+class _LogisticPlan:
+    def __init__(self, F, C, fit_intercept, fit_with_mean):
+        self._lib = N.load()
+        h = ctypes.c_void_p()
+        N.check(self._lib.cyc_logistic_plan_create(int(F), int(C), int(bool(fit_intercept)),
+                                                   int(bool(fit_with_mean)), ctypes.byref(h)))
+        self.handle = h
+
+    def __del__(self):
+        try:
+            if self.handle:
+                self._lib.cyc_logistic_plan_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+class DifferentiableLossAggregator:
+    """State {weightSum, lossSum, gradientSumArray} kept on the device."""
+
+    dim: int
+
+    def _init_state(self, device):
+        torch = _torch()
+        self._state = torch.zeros(self.dim + 2, dtype=torch.float64, device=device)
+
+    @property
+    def gradientSumArray(self):
+        return self._state[:self.dim]
+
+    @property
+    def _loss_sum(self):
+        return self._state[self.dim:self.dim + 1]
+
+    @property
+    def _weight_sum(self):
+        return self._state[self.dim + 1:self.dim + 2]
+
+    @property
+    def weight(self) -> float:
+        return float(self._state[self.dim + 1].item())
+
+    def merge(self, other):
+        """DifferentiableLossAggregator.scala:49-59"""
+        if self.dim != other.dim:
+            raise N.IllegalArgumentException(
+                f"Dimensions mismatch when merging with another {type(self).__name__}. "
+                f"Expecting {self.dim} but got {other.dim}.")
+        if other.weight != 0:
+            self._state += other._state
+        return self
+
+    def allreduce(self, group=None):
+        """treeAggregate across ranks: one RCCL (or gloo) all-reduce of the
+        [gradientSum | lossSum | weightSum] buffer."""
+        parallel.allreduce_(self._state, group=group)
+        return self
+
+    @property
+    def gradient(self) -> np.ndarray:
+        """DifferentiableLossAggregator.scala:62-68"""
+        ws = self.weight
+        if not ws > 0.0:
+            raise N.IllegalArgumentException(
+                f"The effective number of instances should be greater than 0.0, but was {ws}.")
+        g = self.gradientSumArray.cpu().numpy().copy()
+        return (1.0 / ws) * g
+
+    @property
+    def loss(self) -> float:
+        """DifferentiableLossAggregator.scala:74-78"""
+        ws = self.weight
+        if not ws > 0.0:
+            raise N.IllegalArgumentException(
+                f"The effective number of instances should be greater than 0.0, but was {ws}.")
+        return float(self._state[self.dim].item()) / ws
+
+
+def _check_block(agg, block):
+    if agg.numFeatures != block.numFeatures:
+        raise N.IllegalArgumentException(
+            "Dimensions mismatch when adding new instance. Expecting "
+            f"{agg.numFeatures} but got {block.numFeatures}.")
+    if block.weights is not None and bool((block.weights < 0).any().item()):
+        w = block.weights.cpu().numpy()
+        raise N.IllegalArgumentException(
+            f"instance weights {'[' + ','.join(map(str, w)) + ']'} has to be >= 0.0")
+
+
+class BinaryLogisticBlockAggregator(DifferentiableLossAggregator):
+    """BinaryLogisticBlockAggregator(bcInverseStd, bcScaledMean, fitIntercept,
+    fitWithMean)(bcCoefficients)."""
+
+    def __init__(self, inverseStd, scaledMean, fitIntercept, fitWithMean, coefficients,
+                 device="cuda"):
+        torch = _torch()
+        inverseStd = np.asarray(inverseStd, dtype=np.float64)
+        if fitWithMean:
+            if not fitIntercept:
+                raise N.IllegalArgumentException(
+                    "requirement failed: for training without intercept, should not center "
+                    "the vectors")
+            if scaledMean is None or len(scaledMean) != len(inverseStd):
+                raise N.IllegalArgumentException(
+                    "requirement failed: scaled means is required when center the vectors")
+        if not isinstance(coefficients, (np.ndarray, list, tuple)) and not torch.is_tensor(
+                coefficients):
+            raise N.IllegalArgumentException(
+                f"coefficients only supports dense vector but got type {type(coefficients)}.)")
+        self.numFeatures = len(inverseStd)
+        self.fitIntercept, self.fitWithMean = bool(fitIntercept), bool(fitWithMean)
+        self.coef = torch.as_tensor(np.asarray(coefficients, dtype=np.float64), device=device) \
+            if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
+        self.dim = int(self.coef.shape[0])
+        self.scaledMean = None if scaledMean is None else torch.as_tensor(
+            np.asarray(scaledMean, dtype=np.float64), device=device)
+        self._plan = _LogisticPlan(self.numFeatures, 1, self.fitIntercept, self.fitWithMean)
+        self._init_state(device)
+
+    def add(self, block: DeviceInstanceBlock, stream=None):
+        """BinaryLogisticBlockAggregator.scala:81-145 over every block of the shard."""
+        _check_block(self, block)
+        lib = N.load()
+        s = N.stream_handle(stream)
+        if block.is_sparse:
+            N.check(lib.cyc_binary_logistic_add_csr_dev(
+                self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx), N.ptr(block.values),
+                N.ptr(block.labels), N.ptr(block.weights), block.size, N.ptr(self.coef),
+                N.ptr(self.scaledMean), N.ptr(self.gradientSumArray), N.ptr(self._loss_sum),
+                N.ptr(self._weight_sum), s))
+        else:
+            N.check(lib.cyc_binary_logistic_add_dense_dev(
+                self._plan.handle, N.ptr(block.X), N.ptr(block.labels), N.ptr(block.weights),
+                block.size, N.ptr(self.coef), N.ptr(self.scaledMean),
+                N.ptr(self.gradientSumArray), N.ptr(self._loss_sum), N.ptr(self._weight_sum), s))
+        return self
+
+
+class MultinomialLogisticBlockAggregator(DifferentiableLossAggregator):
+    """MultinomialLogisticBlockAggregator: coefficients column-major
+    (numClasses x numFeatures) followed by numClasses intercepts."""
+
+    def __init__(self, inverseStd, scaledMean, fitIntercept, fitWithMean, coefficients,
+                 device="cuda"):
+        torch = _torch()
+        inverseStd = np.asarray(inverseStd, dtype=np.float64)
+        if fitWithMean:
+            if not fitIntercept:
+                raise N.IllegalArgumentException(
+                    "requirement failed: for training without intercept, should not center "
+                    "the vectors")
+            if scaledMean is None or len(scaledMean) != len(inverseStd):
+                raise N.IllegalArgumentException(
+                    "requirement failed: scaled means is required when center the vectors")
+        self.numFeatures = len(inverseStd)
+        self.fitIntercept, self.fitWithMean = bool(fitIntercept), bool(fitWithMean)
+        self.coef = torch.as_tensor(np.asarray(coefficients, dtype=np.float64), device=device) \
+            if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
+        self.dim = int(self.coef.shape[0])
+        fpi = self.numFeatures + 1 if self.fitIntercept else self.numFeatures
+        self.numClasses = self.dim // fpi
+        if self.dim != self.numClasses * fpi:
+            raise N.IllegalArgumentException("requirement failed")
+        self.scaledMean = None if scaledMean is None else torch.as_tensor(
+            np.asarray(scaledMean, dtype=np.float64), device=device)
+        self._plan = _LogisticPlan(self.numFeatures, self.numClasses, self.fitIntercept,
+                                   self.fitWithMean)
+        self._init_state(device)
+
+    def add(self, block: DeviceInstanceBlock, stream=None):
+        """MultinomialLogisticBlockAggregator.scala:101-189 over the shard."""
+        _check_block(self, block)
+        if block.is_sparse:
+            raise N.CycloneError(N.CYC_ERR_UNSUPPORTED,
+                                 "sparse blocks for the multinomial aggregator are not on the "
+                                 "device path yet")
+        N.check(N.load().cyc_multinomial_logistic_add_dense_dev(
+            self._plan.handle, N.ptr(block.X), N.ptr(block.labels), N.ptr(block.weights),
+            block.size, N.ptr(self.coef), N.ptr(self.scaledMean), N.ptr(self.gradientSumArray),
+            N.ptr(self._loss_sum), N.ptr(self._weight_sum), N.stream_handle(stream)))
+        return self
+
+
+class L2Regularization:
+    """ml/optim/loss/DifferentiableRegularization.scala L2Regularization:
+    loss = 0.5 * regParam * sum(coef_j^2) over regularized indices, gradient
+    regParam * coef_j (applyFeaturesStd = None branch)."""
+
+    def __init__(self, regParam, shouldApply=lambda j: True):
+        self.regParam = regParam
+        self.shouldApply = shouldApply
+
+    def calculate(self, coefficients):
+        c = np.asarray(coefficients, dtype=np.float64)
+        grad = np.zeros_like(c)
+        s = 0.0
+        for j, v in enumerate(c):
+            if self.shouldApply(j):
+                s += v * v
+                grad[j] = v * self.regParam
+        return 0.5 * s * self.regParam, grad
+
+
+class RDDLossFunction:
+    """ml/optim/loss/RDDLossFunction.scala:47-70: one full data pass per
+    evaluation.  `blocks` are this rank's device-resident shard(s); the
+    treeAggregate merge is an all-reduce when torch.distributed is initialised."""
+
+    def __init__(self, blocks, getAggregator, regularization=None):
+        self.blocks = blocks if isinstance(blocks, (list, tuple)) else [blocks]
+        self.getAggregator = getAggregator
+        self.regularization = regularization
+
+    def calculate(self, coefficients):
+        agg = self.getAggregator(coefficients)
+        for b in self.blocks:
+            agg.add(b)
+        agg.allreduce()
+        gradient = agg.gradient
+        loss = agg.loss
+        if self.regularization is not None:
+            regLoss, regGrad = self.regularization.calculate(coefficients)
+            gradient = gradient + regGrad          # BLAS.axpy(1.0, regGradient, gradient)
+            loss = loss + regLoss
+        return loss, gradient

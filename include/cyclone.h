@@ -103,6 +103,58 @@ int cyc_kmeans_update_dev(cyc_kmeans_plan plan, double* C, double* cnorm, const 
                           const double* wsum, double epsilon, int32_t* converged_out,
                           void* stream);
 
+/* ------------------------------------------------------ RowMatrix Gramian */
+/* Replaces the BLAS.spr seqOp of RowMatrix.computeGramianMatrix
+ * (mllib/linalg/distributed/RowMatrix.scala:130-161) and of
+ * computeDenseVectorCovariance (:163-220).  U is the packed upper triangle
+ * (column-major, U[j(j+1)/2 + i], i <= j) of n(n+1)/2 doubles; the call adds
+ * sum_r x_r x_r^T over the dense row-major rows (x_r - mean if mean != NULL).
+ * fp64 MFMA syrk, deterministic fixed-order split-K reduction. */
+typedef struct cyc_gramian_plan_s* cyc_gramian_plan;
+
+int cyc_gramian_plan_create(int32_t ncols, cyc_gramian_plan* plan);
+int cyc_gramian_plan_destroy(cyc_gramian_plan plan);
+int cyc_gramian_accumulate_dev(cyc_gramian_plan plan, const double* X, int64_t nrows,
+                               const double* mean, double* U, void* stream);
+/* sums[c] += sum over rows of X[r][c] (fixed order): the mean pre-pass of
+ * RowMatrix.computeCovariance (Statistics.colStats, :456). */
+int cyc_col_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
+                     void* stream);
+/* RowMatrix.triuToFull (:845-867): G (n x n column-major) from U. */
+int cyc_triu_to_full_dev(int32_t n, const double* U, double* G, void* stream);
+/* computeDenseVectorCovariance's finish (:203-217): G = full(U) / (m - 1). */
+int cyc_covariance_finalize_dev(int32_t n, const double* U, int64_t m, double* G, void* stream);
+
+/* ---------------------------------------------- logistic block aggregators */
+/* BinaryLogisticBlockAggregator.add (ml/optim/aggregator/
+ * BinaryLogisticBlockAggregator.scala:81-145) and
+ * MultinomialLogisticBlockAggregator.add (...Multinomial...scala:101-189)
+ * over every block of a device-resident shard (blocks concatenated: dense
+ * row-major n x F, or CSR).  Features are already scaled by inverseStd, as
+ * in the reference.  Accumulates into grad (same layout as the coefficients:
+ * binary F [+1]; multinomial C x F column-major [+ C intercepts]), *lossSum
+ * and *weightSum (device doubles), like the aggregator's add + merge.
+ * weights may be NULL (all-unit weights, InstanceBlock's empty array). */
+typedef struct cyc_logistic_plan_s* cyc_logistic_plan;
+
+int cyc_logistic_plan_create(int32_t numFeatures, int32_t numClasses, int fitIntercept,
+                             int fitWithMean, cyc_logistic_plan* plan);
+int cyc_logistic_plan_destroy(cyc_logistic_plan plan);
+int cyc_binary_logistic_add_dense_dev(cyc_logistic_plan plan, const double* X,
+                                      const double* labels, const double* weights, int64_t n,
+                                      const double* coef, const double* scaledMean, double* grad,
+                                      double* lossSum, double* weightSum, void* stream);
+int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan plan, const int64_t* rowptr,
+                                    const int32_t* colidx, const double* vals,
+                                    const double* labels, const double* weights, int64_t n,
+                                    const double* coef, const double* scaledMean, double* grad,
+                                    double* lossSum, double* weightSum, void* stream);
+int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan plan, const double* X,
+                                           const double* labels, const double* weights,
+                                           int64_t n, const double* coef,
+                                           const double* scaledMean, double* grad,
+                                           double* lossSum, double* weightSum, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

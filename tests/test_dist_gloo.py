@@ -1,0 +1,136 @@
+"""Multi-process (world_size 2, gloo on CPU) tests of the N>1 path: row
+sharding + the single all-reduce merge (cycloneml_amd/parallel.py) that
+replaces treeAggregate / reduceByKey.  The per-shard partial that the GPU
+kernels compute is produced here by the CPU restatement (oracle) so the
+merge and update logic runs without a device; results must match the
+single-process reference on all rows."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, fn(rank, world)))
+    except Exception as e:  # surface failures to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    return out
+
+
+def _kmeans_rank(rank, world):
+    import oracle
+    from cycloneml_amd import parallel
+    rng = np.random.default_rng(0)
+    n, d, k = 3001, 12, 7
+    X = rng.normal(size=(n, d)) + rng.integers(0, 4, size=(n, 1)) * 3.0
+    C = X[:k].copy()
+    Ct = torch.from_numpy(C.copy()) if rank == 0 else torch.zeros(k, d, dtype=torch.float64)
+    parallel.broadcast_(Ct)
+    C = Ct.numpy().copy()
+    cn = oracle.row_norms(C)
+    a, b = parallel.shard_bounds(n, rank, world)
+    Xs = X[a:b]
+    stats = oracle.kmeans_stats(C)
+    assign, dist_, sums, wsum, cost = oracle.kmeans_partition(Xs, oracle.row_norms(Xs), None, C,
+                                                              cn, stats)
+    buf = torch.from_numpy(np.concatenate([sums.ravel(), wsum, [cost]]))
+    parallel.allreduce_(buf)
+    sums2 = buf[:k * d].numpy().reshape(k, d)
+    wsum2 = buf[k * d:k * d + k].numpy()
+    C2, cn2 = C.copy(), cn.copy()
+    oracle.update_centers(C2, cn2, sums2, wsum2)
+    ref = oracle.kmeans_iteration(X, oracle.row_norms(X), None, C, cn)
+    ok_assign = np.array_equal(assign, ref["assign"][a:b])
+    ok_c = np.allclose(C2, ref["centers"], rtol=1e-12, atol=1e-12)
+    ok_w = np.array_equal(wsum2, ref["wsum"])
+    ok_cost = abs(buf[-1].item() - ref["cost"]) <= 1e-12 * ref["cost"]
+    return ok_assign and ok_c and ok_w and ok_cost
+
+
+def _aggregator_rank(rank, world):
+    import oracle
+    from cycloneml_amd.optim import DifferentiableLossAggregator
+    rng = np.random.default_rng(1)
+    n, F = 999, 9
+    X = rng.normal(size=(n, F))
+    y = (rng.uniform(size=n) < 0.4).astype(float)
+    w = rng.uniform(0.5, 1.5, size=n)
+    coef = rng.normal(size=F + 1)
+    from cycloneml_amd import parallel
+    a, b = parallel.shard_bounds(n, rank, world)
+    st = dict(grad=np.zeros(F + 1), loss=0.0, weight=0.0)
+    oracle.binary_logistic_add(dict(labels=y[a:b], weights=w[a:b], X=X[a:b]), coef, True, False,
+                               None, st)
+    agg = DifferentiableLossAggregator()
+    agg.dim = F + 1
+    agg._init_state("cpu")
+    agg._state[:F + 1] = torch.from_numpy(st["grad"])
+    agg._state[F + 1] = st["loss"]
+    agg._state[F + 2] = st["weight"]
+    agg.allreduce()
+    ref = dict(grad=np.zeros(F + 1), loss=0.0, weight=0.0)
+    oracle.binary_logistic_add(dict(labels=y, weights=w, X=X), coef, True, False, None, ref)
+    return (np.allclose(agg.gradient, ref["grad"] / ref["weight"], rtol=1e-12)
+            and abs(agg.loss - ref["loss"] / ref["weight"]) <= 1e-12 * abs(agg.loss))
+
+
+def _gramian_rank(rank, world):
+    import oracle
+    from cycloneml_amd import parallel
+    rng = np.random.default_rng(2)
+    X = rng.uniform(size=(501, 6))
+    a, b = parallel.shard_bounds(501, rank, world)
+    U = torch.from_numpy(oracle.gramian_partition(X[a:b]))
+    parallel.allreduce_(U)
+    return bool(np.allclose(U.numpy(), oracle.gramian_partition(X), rtol=1e-13))
+
+
+@pytest.mark.parametrize("fn", [_kmeans_rank, _aggregator_rank, _gramian_rank])
+def test_two_rank_merge(fn):
+    out = _run(fn)
+    assert out == {0: True, 1: True}, out
+
+
+def test_shard_bounds_cover_rows():
+    from cycloneml_amd.parallel import shard_bounds
+    for n in (0, 1, 7, 10_000_001):
+        for w in (1, 2, 3, 8):
+            b = [shard_bounds(n, r, w) for r in range(w)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+            assert max(e - s for s, e in b) - min(e - s for s, e in b) <= 1

@@ -1,0 +1,248 @@
+"""Pin the CPU restatement (oracle/) against the reference's own known-answer
+tests and fixtures (tests/golden/reference_known_answers.json, each entry
+citing its Scala source).  CPU only."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                   "reference_known_answers.json")))
+
+
+def test_gram_known_answer_dense_and_sparse():
+    g = GOLD["rowmatrix_gram"]
+    X = np.array(g["rows"])
+    U = oracle.gramian_partition(X)
+    assert list(oracle.triu_to_full(3, U)) == g["expected_colmajor"]
+    U2 = np.zeros(6)
+    for idx, val in g["sparse_rows"]:
+        oracle.spr_sparse(idx, val, U2)
+    assert list(oracle.triu_to_full(3, U2)) == g["expected_colmajor"]
+
+
+def test_spr_known_answer():
+    s = GOLD["blas_spr"]
+    U = np.array(s["U"])
+    oracle.dspr_upper(s["x"], U, s["alpha"])
+    np.testing.assert_allclose(U, s["expected"], rtol=0, atol=s["abs_tol"])
+    U2 = np.array(s["U"])
+    oracle.spr_sparse(s["sparse_idx"], s["sparse_val"], U2, 0.1)
+    np.testing.assert_allclose(U2, s["expected_sparse"], rtol=0, atol=s["abs_tol_sparse"])
+
+
+def _cov_oracle(X):
+    m = X.shape[0]
+    mean = X.sum(0) / m
+    n = X.shape[1]
+    U = oracle.gramian_partition(X, mean)
+    G = oracle.triu_to_full(n, U).reshape(n, n).T
+    return G / (m - 1.0)
+
+
+def test_covariance_and_pca_known_answers():
+    g = GOLD["rowmatrix_gram"]
+    X = np.array(g["rows"])
+    cov = _cov_oracle(X)
+    np.testing.assert_allclose(cov, np.cov(X.T), atol=1e-12)
+    u, s, _ = np.linalg.svd(cov)
+    pca = GOLD["rowmatrix_pca"]
+    pc = np.array(pca["principal_components_rows"])
+    for j in range(3):
+        assert min(np.abs(u[:, j] - pc[:, j]).max(), np.abs(u[:, j] + pc[:, j]).max()) < 1e-6
+    np.testing.assert_allclose(s / s.sum(), pca["explained_variance"], atol=1e-6)
+    acc = np.array(GOLD["rowmatrix_cov_accuracy"]["rows"])
+    np.testing.assert_allclose(np.abs(_cov_oracle(acc)), np.abs(np.cov(acc.T)), atol=1e-6)
+
+
+def _lloyd(points, w, C, max_iter=20, eps=1e-4):
+    C = np.array(C, dtype=np.float64)
+    cn = oracle.row_norms(C)
+    xn = oracle.row_norms(points)
+    for _ in range(max_iter):
+        r = oracle.kmeans_iteration(points, xn, w, C, cn)
+        C, cn = r["centers"], r["cnorm"]
+        if r["converged"]:
+            break
+    return C, r
+
+
+def test_weighted_kmeans_exact_centers():
+    g = GOLD["kmeans_weighted_two_centers"]
+    pts = np.array(g["points"])
+    for case in g["cases"]:
+        C, _ = _lloyd(pts, np.array(case["weights"]), pts[[0, 3]])
+        assert {tuple(c) for c in C} == {tuple(c) for c in case["centers"]}
+
+
+def test_kmeans_example_sparse_path():
+    """KMeansExample input through the sparse (norm-trick) findClosest."""
+    g = GOLD["kmeans_example_data"]
+    idx, val = [], []
+    for line in g["libsvm"]:
+        toks = line.split()[1:]
+        idx.append([int(t.split(":")[0]) - 1 for t in toks])
+        val.append([float(t.split(":")[1]) for t in toks])
+    dense = np.zeros((6, 3))
+    for r in range(6):
+        dense[r, idx[r]] = val[r]
+    C = dense[[0, 3]].copy()
+    for _ in range(20):
+        cn = oracle.row_norms(C)
+        stats = oracle.kmeans_stats(C)
+        assign = [oracle.find_closest_stats_sparse(C, cn, stats, idx[r], val[r],
+                                                   oracle.norm2(val[r]))[0] for r in range(6)]
+        newC = np.array([dense[[r for r in range(6) if assign[r] == j]].mean(0) for j in range(2)])
+        if np.allclose(newC, C):
+            break
+        C = newC
+    clusters = sorted(sorted(r for r in range(6) if assign[r] == j) for j in range(2))
+    assert clusters == g["expected_clusters"]
+    np.testing.assert_allclose(sorted(C.tolist()), g["expected_centers_approx"], atol=1e-12)
+
+
+def test_distance_measure_suite_with_vs_without_stats():
+    """DistanceMeasureSuite.scala:55-67 (java.util.Random(42), k=10, dim=8)."""
+    rng = oracle.JavaRandom(42)
+    C = np.array([[rng.next_gaussian() for _ in range(8)] for _ in range(10)])
+    X = np.array([[rng.next_gaussian() for _ in range(8)] for _ in range(1000)])
+    cn = oracle.row_norms(C)
+    stats = oracle.kmeans_stats(C)
+    for x in X:
+        xn = oracle.norm2(x)
+        i1, c1 = oracle.find_closest(C, cn, x, xn)
+        i2, c2 = oracle.find_closest_stats(C, cn, stats, x, xn)
+        assert i1 == i2
+        assert abs(c1 - c2) <= 1e-10 * min(abs(c1), abs(c2)) or c1 == c2
+
+
+def test_java_random_matches_known_sequence():
+    # java.util.Random(42).nextDouble() / nextGaussian() published values
+    r = oracle.JavaRandom(42)
+    assert r.next_double() == 0.7275636800328681
+    r = oracle.JavaRandom(42)
+    assert abs(r.next_gaussian() - 1.1419053154730547) < 1e-15
+
+
+def test_utils_softmax_and_log1pexp():
+    a = np.array([1.0, 2.0, 3.0])
+    oracle.lib().orc_softmax(a.ctypes.data_as(oracle._D), 3, 0, 1)
+    e = np.exp(np.array([1.0, 2.0, 3.0]) - 3.0)
+    np.testing.assert_allclose(a, e / e.sum(), rtol=1e-15)
+    b = np.array([1.0, np.inf, 3.0, np.inf])
+    oracle.lib().orc_softmax(b.ctypes.data_as(oracle._D), 4, 0, 1)
+    assert list(b) == [0.0, 1.0, 0.0, np.inf * 0.0] or (b[1] == 1.0 and b[0] == 0.0)
+    assert oracle.log1pexp(800.0) == 800.0
+    assert oracle.log1pexp(-800.0) == 0.0
+    assert abs(oracle.log1pexp(0.5) - np.log1p(np.exp(0.5))) < 1e-15
+
+
+# ------------------------------------------------------------- aggregators
+
+def _summ(instances):
+    """Summarizer mean/std (weighted, unbiased; Summarizer.scala:673-690)."""
+    X = np.array([f for _, _, f in instances])
+    w = np.array([w for _, w, _ in instances])
+    W = w.sum()
+    mean = (w[:, None] * X).sum(0) / W
+    denom = W - (w * w).sum() / W
+    var = (w[:, None] * (X - mean) ** 2).sum(0) / denom
+    return mean, np.sqrt(var)
+
+
+def _blocks(scaled, bs, sparse):
+    out = []
+    for s in range(0, len(scaled), bs):
+        grp = scaled[s:s + bs]
+        labels = np.array([l for l, _, _ in grp])
+        weights = np.array([w for _, w, _ in grp])
+        X = np.array([f for _, _, f in grp])
+        if sparse:
+            rp, ci, vv = [0], [], []
+            for row in X:
+                nz = np.nonzero(row)[0]
+                ci += list(nz)
+                vv += list(row[nz])
+                rp.append(len(ci))
+            out.append(dict(labels=labels, weights=weights, rowptr=np.array(rp),
+                            colidx=np.array(ci, dtype=np.int32), values=np.array(vv),
+                            F=X.shape[1]))
+        else:
+            out.append(dict(labels=labels, weights=weights, X=X))
+    return out
+
+
+@pytest.mark.parametrize("fit_intercept,fit_with_mean", [(False, False), (True, False),
+                                                         (True, True)])
+def test_binary_aggregator_vs_naive_loop(fit_intercept, fit_with_mean):
+    """BinaryLogisticBlockAggregatorSuite.scala:131-264 naive expectations."""
+    g = GOLD["logistic_aggregator_instances"]
+    inst = [(l, w, np.array(f)) for l, w, f in g["binary"]]
+    mean, std = _summ(inst)
+    inv = np.where(std != 0, 1.0 / std, 0.0)
+    coef = np.array(g["binary_coef"])
+    icpt = g["binary_intercept"] if fit_intercept else 0.0
+    W = sum(w for _, w, _ in inst)
+    loss, grad, gi = 0.0, np.zeros(2), 0.0
+    for l, w, f in inst:
+        x = f - mean if fit_with_mean else f
+        margin = (coef / std) @ x + icpt
+        prob = 1.0 / (1.0 + np.exp(-margin))
+        loss += -w * l * np.log(prob) - w * (1.0 - l) * np.log1p(-prob)
+        grad += w * (prob - l) * x / std
+        gi += w * (prob - l)
+    exp_loss = loss / W
+    exp_grad = np.append(grad, gi) / W if fit_intercept else grad / W
+    scaled = [(l, w, f * inv) for l, w, f in inst]
+    full_coef = np.append(coef, icpt) if fit_intercept else coef
+    for bs in g["block_sizes"]:
+        for sparse in (False, True):
+            st = dict(grad=np.zeros(full_coef.size), loss=0.0, weight=0.0)
+            for b in _blocks(scaled, bs, sparse):
+                oracle.binary_logistic_add(b, full_coef, fit_intercept, fit_with_mean,
+                                           inv * mean if fit_with_mean else None, st)
+            assert abs(st["loss"] / st["weight"] - exp_loss) <= 1e-9 * abs(exp_loss)
+            np.testing.assert_allclose(st["grad"] / st["weight"], exp_grad, rtol=1e-9)
+
+
+@pytest.mark.parametrize("fit_intercept,fit_with_mean", [(False, False), (True, False),
+                                                         (True, True)])
+def test_multinomial_aggregator_vs_naive_loop(fit_intercept, fit_with_mean):
+    """MultinomialLogisticBlockAggregatorSuite.scala:134-346 naive expectations."""
+    g = GOLD["logistic_aggregator_instances"]
+    inst = [(l, w, np.array(f)) for l, w, f in g["multinomial"]]
+    C, F = 3, 2
+    mean, std = _summ(inst)
+    inv = np.where(std != 0, 1.0 / std, 0.0)
+    coef = np.array(g["multinomial_coef"])          # column-major C x F
+    icpt = np.array(g["multinomial_intercept"]) if fit_intercept else np.zeros(C)
+    Wm = np.array([[coef[f * C + c] / std[f] for f in range(F)] for c in range(C)])
+    W = sum(w for _, w, _ in inst)
+    loss = 0.0
+    grad = np.zeros(C * F)
+    gi = np.zeros(C)
+    for l, w, f in inst:
+        x = f - mean if fit_with_mean else f
+        m = Wm @ x + icpt
+        p = np.exp(m) / np.exp(m).sum()
+        loss += w * (np.log(np.exp(m).sum()) - m[int(l)])
+        for c in range(C):
+            d = w * (p[c] - (1.0 if c == int(l) else 0.0))
+            for ff in range(F):
+                grad[ff * C + c] += d * x[ff] / std[ff]
+            gi[c] += d
+    exp_loss = loss / W
+    exp_grad = (np.concatenate([grad, gi]) if fit_intercept else grad) / W
+    scaled = [(l, w, f * inv) for l, w, f in inst]
+    full = np.concatenate([coef, icpt]) if fit_intercept else coef
+    for bs in g["block_sizes"]:
+        for sparse in (False, True):
+            st = dict(grad=np.zeros(full.size), loss=0.0, weight=0.0)
+            for b in _blocks(scaled, bs, sparse):
+                oracle.multinomial_logistic_add(b, full, C, fit_intercept, fit_with_mean,
+                                                inv * mean if fit_with_mean else None, st)
+            assert abs(st["loss"] / st["weight"] - exp_loss) <= 1e-9 * abs(exp_loss)
+            np.testing.assert_allclose(st["grad"] / st["weight"], exp_grad, rtol=1e-9)
