@@ -1,17 +1,27 @@
 #!/usr/bin/env python3
 """bench.py -- rows/s per training iteration on MI355X (BASELINE.json metric).
 
-Default workload (BASELINE.json configs[1]): KMeans k=1024 on synthetic dense
-fp64 10M x 256, one Lloyd iteration per step (KMeans.scala:275-334: statistics,
-findClosest for every row, per-cluster sums/weights/cost, merge, centroid
-update).  With --gpus N (launched one process per GPU by torch.distributed.run)
-every rank holds its own 10M-row shard in HBM (weak scaling) and the merge is
-one RCCL all-reduce of [sums | weights | cost] per iteration.
+Default workload (BASELINE.json configs[1], the config the metric is quoted
+on): KMeans k=1024 on synthetic dense fp64 10M x 256, one Lloyd iteration per
+step (KMeans.scala:275-334: statistics, findClosest for every row,
+per-cluster sums/weights/cost, merge, centroid update).
 
-Prints ONE JSON line on rank 0.  `roofline` is for the dominant kernel (the
-fp64-MFMA assign kernel), timed with HIP events on its own stream inside the
-timed region; `cpu_baseline` is the CPU restatement (oracle/, a C port of the
-reference loops) run on a bounded sample on this host's cores.
+Other workloads (--workload), each one training iteration per step:
+  gramian      RowMatrix.computeGramianMatrix pass (configs[2]; the 100M x 1024
+               matrix does not fit one GPU, so each GPU holds a 12.5M-row shard:
+               the 8-GPU split of the config)
+  lr_multi     multinomial LR, 100 classes, 512 dense features (configs[3]);
+               one RDDLossFunction.calculate per step, 6.25M-row shard per GPU
+  lr_sparse    binomial LR on CSR, 1M features, 64 nnz/row (configs[4]);
+               one RDDLossFunction.calculate per step, 25M-row shard per GPU
+With --gpus N (one process per GPU via torch.distributed.run) every rank
+holds its own shard in HBM (weak scaling) and the merge is one RCCL
+all-reduce per iteration.
+
+Prints ONE JSON line on rank 0.  `roofline` is for the workload's dominant
+kernel, timed with HIP events on the stream it runs on inside the timed
+region (cyc_profile_*); `cpu_baseline` is the CPU restatement (oracle/, a C
+port of the reference loops) on a bounded sample of the same data.
 """
 from __future__ import annotations
 
@@ -27,16 +37,17 @@ sys.path.insert(0, ROOT)
 FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 (vector = matrix) spec, BASELINE.md section 2
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 
+DEFAULT_ROWS = {"kmeans": 10_000_000, "gramian": 12_500_000, "lr_multi": 6_250_000,
+                "lr_sparse": 25_000_000}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="kmeans", choices=["kmeans"])
-    ap.add_argument("--rows", type=int, default=10_000_000, help="rows per GPU")
-    ap.add_argument("--dim", type=int, default=256)
-    ap.add_argument("--k", type=int, default=1024)
+    ap.add_argument("--workload", default="kmeans", choices=sorted(DEFAULT_ROWS))
+    ap.add_argument("--rows", type=int, default=0, help="rows per GPU (0 = workload default)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU time of the cpu_baseline sample (0 disables)")
     return ap.parse_args()
@@ -44,47 +55,310 @@ def parse():
 
 def pmc_traffic(name):
     """HBM bytes per launch of `name` from the committed rocprofv3 --pmc summary
-    (profiles/*_pmc.json written by tools/pmc_summary.py), else None."""
+    (profiles/*_pmc.json written by tools/pmc_summary.py), scaled to this
+    run's rows when the profile was taken at another size; else None."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            if name in d:
-                return d[name].get("hbm_bytes_per_launch")
+            if name in d and d[name].get("hbm_bytes_per_launch"):
+                return d[name]["hbm_bytes_per_launch"], d.get("_rows_per_launch")
         except Exception:
             continue
-    return None
+    return None, None
 
 
-def cpu_baseline_kmeans(Xs, C, seconds):
-    """Time the CPU restatement (oracle.kmeans_iteration) on a bounded sample,
-    rows split into one Spark-like partition per thread (local[N])."""
-    import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
-    xn = oracle.row_norms(Xs)
-    cn = oracle.row_norms(C)
-    # calibrate on a small slice, then size the sample for ~`seconds`
-    m = min(2000, Xs.shape[0])
+def cpu_threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+
+
+def timed_parallel(fn, parts, threads):
+    from concurrent.futures import ThreadPoolExecutor
     t0 = time.perf_counter()
-    oracle.kmeans_iteration(Xs[:m], xn[:m], None, C, cn, num_partitions=1)
-    t1 = time.perf_counter() - t0
-    stats_t0 = time.perf_counter()
-    oracle.kmeans_stats(C)
-    t_stats = time.perf_counter() - stats_t0
-    per_row = max((t1 - t_stats) / m, 1e-9)
-    rows = int(min(Xs.shape[0], max(threads * 1000, seconds * threads / per_row)))
-    rows = max(rows - rows % threads, threads)
-    t0 = time.perf_counter()
-    oracle.kmeans_iteration(Xs[:rows], xn[:rows], None, C, cn, num_partitions=threads,
-                            threads=threads)
-    el = time.perf_counter() - t0
-    return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"{rows} rows of the same synthetic 256-dim data, same k=1024 centers, "
-                      f"one Lloyd iteration (stats+findClosest+sums+merge+update), "
-                      f"{threads} partitions on {threads} threads, {el:.1f} s"}
+    with ThreadPoolExecutor(threads) as ex:
+        out = list(ex.map(fn, parts))
+    return time.perf_counter() - t0, out
+
+
+# ---------------------------------------------------------------- workloads
+
+class KMeansWorkload:
+    kernel = "k_kmeans_assign"
+    bound = "mfma"
+
+    def __init__(self, n, dev, rank):
+        import torch
+        from cycloneml_amd import parallel
+        from cycloneml_amd.clustering import KMeansPlan, row_norms
+        self.n, self.d, self.k = n, 256, 1024
+        d, k = self.d, self.k
+        # BASELINE config 2 / SURVEY 8d: 1024 true centers ~ N(0, 4^2) per dim
+        # + point noise N(0, 1); torch Philox on device, seeded per rank.
+        g = torch.Generator(device=dev).manual_seed(1234)
+        true_c = torch.randn(k, d, generator=g, device=dev, dtype=torch.float64) * 4.0
+        gr = torch.Generator(device=dev).manual_seed(1000 + rank)
+        X = torch.empty(n, d, dtype=torch.float64, device=dev)
+        for s in range(0, n, 1 << 20):
+            e = min(n, s + (1 << 20))
+            lab = torch.randint(0, k, (e - s,), generator=gr, device=dev)
+            X[s:e] = true_c[lab] + torch.randn(e - s, d, generator=gr, device=dev,
+                                               dtype=torch.float64)
+        self.X = X
+        self.xnorm = row_norms(X)
+        self.C0 = X[:k].clone()           # setInitialModel semantics: rows 0..k-1
+        parallel.broadcast_(self.C0)
+        self.C = self.C0.clone()
+        self.cnorm = row_norms(self.C)
+        self.plan = KMeansPlan(d, k, n)
+        self.buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=dev)
+        self.conv = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.parallel = parallel
+
+    def step(self):
+        k, d = self.k, self.d
+        buf = self.buf
+        sums, wsum, cost = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
+        buf.zero_()
+        self.plan.accumulate(self.X, self.xnorm, None, self.C, self.cnorm, sums, wsum, cost)
+        self.parallel.allreduce_(buf)
+        self.plan.update(self.C, self.cnorm, sums, wsum, 1e-4, self.conv)
+
+    def work_per_launch(self, launches_per_step):
+        return 2.0 * self.k * self.d * self.n / launches_per_step   # flops
+
+    def describe(self):
+        return (f"KMeans k={self.k} Lloyd iteration, dense fp64 {self.n} x {self.d} rows per GPU "
+                "(BASELINE configs[1])")
+
+    def cpu_baseline(self, seconds):
+        import numpy as np
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        threads = cpu_threads()
+        m = min(self.n, 400_000)
+        Xs = np.ascontiguousarray(self.X[:m].cpu().numpy())
+        C = self.C0.cpu().numpy()
+        xn, cn = oracle.row_norms(Xs), oracle.row_norms(C)
+        t0 = time.perf_counter()
+        oracle.kmeans_iteration(Xs[:2000], xn[:2000], None, C, cn)
+        t1 = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        oracle.kmeans_stats(C)
+        per_row = max((t1 - (time.perf_counter() - t0)) / 2000, 1e-9)
+        rows = int(min(m, max(threads * 1000, seconds * threads / per_row)))
+        rows -= rows % threads
+        t0 = time.perf_counter()
+        oracle.kmeans_iteration(Xs[:rows], xn[:rows], None, C, cn, num_partitions=threads,
+                                threads=threads)
+        el = time.perf_counter() - t0
+        return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
+                "sample": f"{rows} rows of the same data, same k={self.k} centers, one Lloyd "
+                          f"iteration (stats+findClosest+sums+merge+update) as {threads} "
+                          f"partitions on {threads} threads, {el:.1f} s"}
+
+
+class GramianWorkload:
+    kernel = "k_gram_tiles"
+    bound = "mfma"
+
+    def __init__(self, n, dev, rank):
+        import torch
+        from cycloneml_amd import parallel
+        from cycloneml_amd.linalg import GramianPlan
+        self.n, self.p = n, 1024
+        g = torch.Generator(device=dev).manual_seed(77 + rank)
+        self.X = torch.empty(n, self.p, dtype=torch.float64, device=dev)
+        for s in range(0, n, 1 << 20):
+            e = min(n, s + (1 << 20))
+            self.X[s:e] = torch.rand(e - s, self.p, generator=g, device=dev, dtype=torch.float64)
+        self.U = torch.zeros(self.p * (self.p + 1) // 2, dtype=torch.float64, device=dev)
+        self.plan = GramianPlan(self.p)
+        self.parallel = parallel
+
+    def step(self):
+        self.U.zero_()
+        self.plan.accumulate(self.X, self.U)
+        self.parallel.allreduce_(self.U)
+
+    def work_per_launch(self, launches_per_step):
+        return float(self.n) * self.p * (self.p + 1) / launches_per_step   # flops (upper)
+
+    def describe(self):
+        return (f"RowMatrix.computeGramianMatrix pass, dense fp64 {self.n} x {self.p} rows per "
+                "GPU, U[0,1) (BASELINE configs[2], 8-GPU shard of 100M rows)")
+
+    def cpu_baseline(self, seconds):
+        import numpy as np
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        threads = cpu_threads()
+        Xs = np.ascontiguousarray(self.X[:200_000].cpu().numpy())
+        t0 = time.perf_counter()
+        oracle.gramian_partition(Xs[:200])
+        per_row = (time.perf_counter() - t0) / 200
+        rows = int(min(Xs.shape[0], max(threads * 50, seconds * threads / per_row)))
+        rows -= rows % threads
+        parts = np.array_split(Xs[:rows], threads)
+        el, Us = timed_parallel(oracle.gramian_partition, parts, threads)
+        return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
+                "sample": f"{rows} rows x 1024 of the same data, per-row netlib dspr as "
+                          f"{threads} partitions on {threads} threads, {el:.1f} s"}
+
+
+class LRMultiWorkload:
+    kernel = "k_mlr_grad"
+    kernels = ("k_mlr_margins", "k_mlr_grad")
+    bound = "mfma"
+
+    def __init__(self, n, dev, rank):
+        import torch
+        from cycloneml_amd.optim import (DeviceInstanceBlock, MultinomialLogisticBlockAggregator,
+                                         RDDLossFunction)
+        self.n, self.F, self.C = n, 512, 100
+        F, C = self.F, self.C
+        g = torch.Generator(device=dev).manual_seed(11)
+        Wt = torch.randn(F, C, generator=g, device=dev, dtype=torch.float64) / F ** 0.5
+        gr = torch.Generator(device=dev).manual_seed(500 + rank)
+        X = torch.empty(n, F, dtype=torch.float64, device=dev)
+        y = torch.empty(n, dtype=torch.float64, device=dev)
+        for s in range(0, n, 1 << 19):
+            e = min(n, s + (1 << 19))
+            X[s:e] = torch.randn(e - s, F, generator=gr, device=dev, dtype=torch.float64)
+            pr = torch.softmax(X[s:e] @ Wt, dim=1)
+            y[s:e] = torch.multinomial(pr, 1, generator=gr).squeeze(1).to(torch.float64)
+        self.block = DeviceInstanceBlock(y, None, X=X)
+        import numpy as np
+        self.coef = np.random.default_rng(3).normal(size=C * F + C) * 0.01
+        self.scaledMean = np.zeros(F)
+        self.fn = RDDLossFunction([self.block], lambda c: MultinomialLogisticBlockAggregator(
+            np.ones(F), self.scaledMean, True, True, c, device=dev))
+
+    def step(self):
+        self.fn.calculate(self.coef)
+
+    def work_per_launch(self, launches_per_step):
+        return 2.0 * self.n * self.F * self.C / launches_per_step
+
+    def describe(self):
+        return (f"multinomial LR ({self.C} classes) RDDLossFunction.calculate, dense fp64 "
+                f"{self.n} x {self.F} rows per GPU, fitIntercept+standardization "
+                "(BASELINE configs[3], 8-GPU shard of 50M rows)")
+
+    def cpu_baseline(self, seconds):
+        import numpy as np
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        threads = cpu_threads()
+        X = self.block.X[:100_000].cpu().numpy()
+        y = self.block.labels[:100_000].cpu().numpy()
+
+        def part(rng_):
+            a, b = rng_
+            st = dict(grad=np.zeros(self.coef.size), loss=0.0, weight=0.0)
+            for s in range(a, b, 256):      # InstanceBlock of 256 rows (1 MiB)
+                e = min(b, s + 256)
+                oracle.multinomial_logistic_add(dict(labels=y[s:e], weights=None, X=X[s:e]),
+                                                self.coef, self.C, True, True, self.scaledMean,
+                                                st)
+            return st
+        t0 = time.perf_counter()
+        part((0, 256))
+        per_row = (time.perf_counter() - t0) / 256
+        rows = int(min(X.shape[0], max(threads * 256, seconds * threads / per_row)))
+        rows -= rows % (threads * 256)
+        step = rows // threads
+        el, _ = timed_parallel(part, [(i * step, (i + 1) * step) for i in range(threads)],
+                               threads)
+        return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
+                "sample": f"{rows} rows of the same data in 256-row blocks (1 MiB), "
+                          f"{threads} partitions on {threads} threads, {el:.1f} s"}
+
+
+class LRSparseWorkload:
+    kernel = "k_binlog_csr"
+    bound = "hbm"
+
+    def __init__(self, n, dev, rank):
+        import torch
+        from cycloneml_amd.optim import (BinaryLogisticBlockAggregator, DeviceInstanceBlock,
+                                         RDDLossFunction)
+        self.n, self.F, self.k = n, 1_000_000, 64
+        F, k = self.F, self.k
+        g = torch.Generator(device=dev).manual_seed(2)
+        w_true = torch.randn(F, generator=g, device=dev, dtype=torch.float64) * 0.5
+        gr = torch.Generator(device=dev).manual_seed(900 + rank)
+        cols = torch.empty(n * k, dtype=torch.int32, device=dev)
+        vals = torch.empty(n * k, dtype=torch.float64, device=dev)
+        y = torch.empty(n, dtype=torch.float64, device=dev)
+        step = 1 << 20
+        for s in range(0, n, step):
+            e = min(n, s + step)
+            # 64 distinct sorted columns per row: one per 1/64 band + offset
+            band = F // k
+            c = (torch.arange(k, device=dev) * band).unsqueeze(0) + \
+                torch.randint(0, band, (e - s, k), generator=gr, device=dev)
+            cols[s * k:e * k] = c.to(torch.int32).reshape(-1)
+            v = torch.rand(e - s, k, generator=gr, device=dev, dtype=torch.float64)
+            vals[s * k:e * k] = v.reshape(-1)
+            m = (v * w_true[c]).sum(1)
+            y[s:e] = (torch.rand(e - s, generator=gr, device=dev, dtype=torch.float64)
+                      < torch.sigmoid(m)).to(torch.float64)
+        rowptr = torch.arange(0, n * k + 1, k, dtype=torch.int64, device=dev)
+        self.block = DeviceInstanceBlock(y, None, rowptr=rowptr, colidx=cols, values=vals,
+                                         numFeatures=F)
+        import numpy as np
+        self.coef = np.random.default_rng(4).normal(size=F + 1) * 0.01
+        self.fn = RDDLossFunction([self.block], lambda c: BinaryLogisticBlockAggregator(
+            np.ones(F), None, True, False, c, device=dev))
+
+    def step(self):
+        self.fn.calculate(self.coef)
+
+    def work_per_launch(self, launches_per_step):
+        return self.n * (self.k * 12 + 8 + 8) / launches_per_step   # bytes (SURVEY 8d)
+
+    def describe(self):
+        return (f"binomial LR RDDLossFunction.calculate on CSR {self.n} rows x {self.F} "
+                f"features, {self.k} nnz/row per GPU (BASELINE configs[4], 8-GPU shard "
+                "of 200M rows)")
+
+    def cpu_baseline(self, seconds):
+        import numpy as np
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        threads = cpu_threads()
+        m = 400_000
+        rp = self.block.rowptr[:m + 1].cpu().numpy()
+        ci = self.block.colidx[:m * self.k].cpu().numpy()
+        vv = self.block.values[:m * self.k].cpu().numpy()
+        y = self.block.labels[:m].cpu().numpy()
+
+        def part(rng_):
+            a, b = rng_
+            st = dict(grad=np.zeros(self.F + 1), loss=0.0, weight=0.0)
+            for s in range(a, b, 1345):     # CSR InstanceBlock of 1345 rows (1 MiB)
+                e = min(b, s + 1345)
+                oracle.binary_logistic_add(dict(labels=y[s:e], weights=None,
+                                                rowptr=rp[s:e + 1] - rp[s],
+                                                colidx=ci[rp[s]:rp[e]], values=vv[rp[s]:rp[e]],
+                                                F=self.F), self.coef, True, False, None, st)
+            return st
+        t0 = time.perf_counter()
+        part((0, 1345 * 4))
+        per_row = (time.perf_counter() - t0) / (1345 * 4)
+        rows = int(min(m, max(threads * 1345, seconds * threads / per_row)))
+        step = rows // threads
+        rows = step * threads
+        el, _ = timed_parallel(part, [(i * step, (i + 1) * step) for i in range(threads)],
+                               threads)
+        return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
+                "sample": f"{rows} rows of the same CSR data in 1345-row blocks (1 MiB), "
+                          f"{threads} partitions on {threads} threads, {el:.1f} s"}
+
+
+WORKLOADS = {"kmeans": KMeansWorkload, "gramian": GramianWorkload, "lr_multi": LRMultiWorkload,
+             "lr_sparse": LRSparseWorkload}
 
 
 def main():
@@ -102,81 +376,54 @@ def main():
     torch.cuda.set_device(dev)
 
     from cycloneml_amd import _native as N
-    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    from cycloneml_amd import parallel
     N.load()
-
-    n, d, k = args.rows, args.dim, args.k
-    # Synthetic data (BASELINE config 2 / SURVEY 8d): 1024 true centers
-    # ~ N(0, 4^2) per dim + point noise N(0, 1); generated on device with
-    # torch's Philox generator (seeded), resident in HBM before timing.
-    g = torch.Generator(device=dev).manual_seed(1234)
-    true_c = torch.randn(k, d, generator=g, device=dev, dtype=torch.float64) * 4.0
-    gr = torch.Generator(device=dev).manual_seed(1000 + rank)
-    X = torch.empty(n, d, dtype=torch.float64, device=dev)
-    chunk = 1 << 20
-    for s in range(0, n, chunk):
-        e = min(n, s + chunk)
-        lab = torch.randint(0, k, (e - s,), generator=gr, device=dev)
-        X[s:e] = true_c[lab] + torch.randn(e - s, d, generator=gr, device=dev,
-                                           dtype=torch.float64)
-    del true_c
-    xnorm = row_norms(X)
-    C0 = X[:k].clone()                     # setInitialModel semantics: rows 0..k-1
-    if world > 1:
-        dist.broadcast(C0, 0)
-    C = C0.clone()
-    cnorm = row_norms(C)
-    plan = KMeansPlan(d, k, n)
-    buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=dev)
-    sums, wsum, cost_sum = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
-    conv = torch.zeros(1, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream()
-
-    def step():
-        buf.zero_()
-        plan.accumulate(X, xnorm, None, C, cnorm, sums, wsum, cost_sum, stream=stream)
-        if world > 1:
-            dist.all_reduce(buf)
-        plan.update(C, cnorm, sums, wsum, 1e-4, conv, stream=stream)
+    n = args.rows or DEFAULT_ROWS[args.workload]
+    wl = WORKLOADS[args.workload](n, dev, rank)
 
     for _ in range(args.warmup):
-        step()
+        wl.step()
     torch.cuda.synchronize()
-    plan.set_timing(True)
-    plan.get_timing()  # reset
+    kernels = getattr(wl, "kernels", (wl.kernel,))
+    N.profile_enable(True)
+    for kname in kernels:
+        N.profile_query(kname)            # reset
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        wl.step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    assign_ms, launches = plan.get_timing()
-    plan.set_timing(False)
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    total_rows = n * world * args.steps
-    value = total_rows / el
-    avg_launch_s = (assign_ms / max(launches, 1)) / 1e3
-    flops_per_launch = 2.0 * k * d * n
-    achieved = flops_per_launch / avg_launch_s / 1e12 if launches else None
-    traffic = pmc_traffic("k_kmeans_assign")
+    prof = {kname: N.profile_query(kname) for kname in kernels}
+    N.profile_enable(False)
+    el = parallel.max_over_ranks(el, dev)
+    value = n * world * args.steps / el
+
+    kms, launches = prof[wl.kernel]
+    avg_s = kms / max(launches, 1) / 1e3
+    per_launch = wl.work_per_launch(launches / args.steps) if launches else 0.0
+    achieved = per_launch / avg_s if launches else None
+    if wl.bound == "mfma":
+        unit, peak = "TFLOP/s", FP64_PEAK_TFLOPS
+        achieved = achieved / 1e12 if achieved else None
+    else:
+        unit, peak = "GB/s", HBM_PEAK_GBS
+        achieved = achieved / 1e9 if achieved else None
+    traffic, prof_rows = pmc_traffic(wl.kernel)
+    if traffic and prof_rows:
+        traffic = traffic * (n / (prof_rows))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        import numpy as np
-        m = min(n, 400_000)
-        Xs = X[:m].cpu().numpy()
-        cpu = cpu_baseline_kmeans(np.ascontiguousarray(Xs), C0.cpu().numpy(), args.cpu_seconds)
+        cpu = wl.cpu_baseline(args.cpu_seconds)
 
     if rank == 0:
         line = {
-            "metric": "rows/s per training iteration (KMeans Lloyd iteration)",
+            "metric": "rows/s per training iteration",
             "value": value,
             "unit": "rows/s",
             "n_gpus": world,
@@ -187,17 +434,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (torch Philox, seeded): 1024 Gaussian centers sd 4 + N(0,1) noise",
-            "config": {"workload": "KMeans k=1024 Lloyd iteration, dense fp64 "
-                                   f"{n} x {d} rows per GPU (BASELINE configs[1])",
-                       "rows_per_gpu": n, "dim": d, "k": k,
+            "data": "synthetic, generated on device (torch Philox, seeded per rank)",
+            "config": {"workload": wl.describe(), "rows_per_gpu": n,
                        "parallelism": f"dp{world} (row shards, RCCL all-reduce merge)"},
-            "roofline": {"kernel": "k_kmeans_assign", "bound": "mfma",
-                         "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
+            "roofline": {"kernel": wl.kernel, "bound": wl.bound, "achieved": achieved,
+                         "peak": peak, "unit": unit,
+                         "frac": (achieved / peak) if achieved else None,
                          "traffic": traffic,
-                         "avg_launch_ms": avg_launch_s * 1e3, "launches": launches,
-                         "flops_per_launch": flops_per_launch},
+                         "avg_launch_ms": avg_s * 1e3, "launches": launches,
+                         "work_per_launch": per_launch,
+                         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()}},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -40,11 +40,11 @@ SIGNATURES = {
     "cyc_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "cyc_set_device": (ctypes.c_int, [ctypes.c_int]),
     "cyc_synchronize": (ctypes.c_int, [_vp]),
+    "cyc_profile_enable": (ctypes.c_int, [ctypes.c_int]),
+    "cyc_profile_query": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_f64), _pi64]),
     "cyc_row_norms_dev": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "cyc_kmeans_plan_create": (ctypes.c_int, [_i32, _i32, _i64, ctypes.POINTER(_vp)]),
     "cyc_kmeans_plan_destroy": (ctypes.c_int, [_vp]),
-    "cyc_kmeans_plan_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
-    "cyc_kmeans_plan_get_timing": (ctypes.c_int, [_vp, ctypes.POINTER(_f64), _pi64]),
     "cyc_kmeans_stats_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     "cyc_kmeans_assign_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _pi64,
                                              _vp]),
@@ -114,6 +114,18 @@ def header_symbols(path: str = HEADER_PATH):
     txt = open(path).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(cyc_[a-z0-9_]+)\s*\(", txt)))
+
+
+def profile_enable(on: bool):
+    check(load().cyc_profile_enable(int(on)))
+
+
+def profile_query(kernel: str):
+    """(total_ms, launches) of `kernel` since the last query (HIP events)."""
+    ms = _f64()
+    cnt = _i64()
+    check(load().cyc_profile_query(kernel.encode(), ctypes.byref(ms), ctypes.byref(cnt)))
+    return ms.value, cnt.value
 
 
 def ptr(t) -> int | None:

@@ -46,16 +46,6 @@ class KMeansPlan:
         except Exception:
             pass
 
-    def set_timing(self, enable: bool):
-        N.check(self._lib.cyc_kmeans_plan_set_timing(self.handle, int(enable)))
-
-    def get_timing(self):
-        ms = ctypes.c_double()
-        cnt = ctypes.c_int64()
-        N.check(self._lib.cyc_kmeans_plan_get_timing(self.handle, ctypes.byref(ms),
-                                                     ctypes.byref(cnt)))
-        return ms.value, cnt.value
-
     def stats(self, C, out=None, stream=None):
         N.check(self._lib.cyc_kmeans_stats_dev(self.handle, N.ptr(C), N.ptr(out),
                                                N.stream_handle(stream)))

@@ -1,8 +1,13 @@
 // capi.cpp -- misc C-ABI entry points, error plumbing and scratch buffers.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "common.hpp"
 
@@ -48,9 +53,55 @@ void DeviceBuffer::release() {
   device = -1;
 }
 
+static std::atomic<bool> g_prof{false};
+static std::mutex g_prof_mu;
+static std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> g_prof_events;
+
+KernelTimer::KernelTimer(const char* n, hipStream_t s) : name(n), st(s) {
+  if (!g_prof.load()) return;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventRecord(e0, st) != hipSuccess) e0 = nullptr;
+}
+
+KernelTimer::~KernelTimer() {
+  if (!e0) return;
+  hipEvent_t e1 = nullptr;
+  if (hipEventCreate(&e1) != hipSuccess || hipEventRecord(e1, st) != hipSuccess) return;
+  std::lock_guard<std::mutex> g(g_prof_mu);
+  g_prof_events[name].emplace_back(e0, e1);
+}
+
 }  // namespace cyc
 
 extern "C" {
+
+int cyc_profile_enable(int enable) {
+  cyc::g_prof.store(enable != 0);
+  return CYC_OK;
+}
+
+int cyc_profile_query(const char* kernel, double* total_ms, int64_t* launches) {
+  CYC_REQUIRE(kernel && total_ms && launches, "kernel name and outputs must not be null");
+  std::lock_guard<std::mutex> g(cyc::g_prof_mu);
+  double tot = 0.0;
+  int64_t cnt = 0;
+  auto it = cyc::g_prof_events.find(kernel);
+  if (it != cyc::g_prof_events.end()) {
+    for (auto& e : it->second) {
+      CYC_HIP(hipEventSynchronize(e.second));
+      float ms = 0.f;
+      CYC_HIP(hipEventElapsedTime(&ms, e.first, e.second));
+      tot += ms;
+      ++cnt;
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+    cyc::g_prof_events.erase(it);
+  }
+  *total_ms = tot;
+  *launches = cnt;
+  return CYC_OK;
+}
+
 
 const char* cyc_last_error(void) { return cyc::get_error().c_str(); }
 

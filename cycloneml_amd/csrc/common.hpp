@@ -35,6 +35,16 @@ struct DeviceBuffer {
   ~DeviceBuffer() { release(); }
 };
 
+// Measurement hook (cyc_profile_enable / cyc_profile_query): brackets one
+// launch of a named kernel with HIP events on its stream when enabled.
+struct KernelTimer {
+  KernelTimer(const char* name, hipStream_t st);
+  ~KernelTimer();
+  const char* name;
+  hipStream_t st;
+  hipEvent_t e0 = nullptr;
+};
+
 // Fixed-margin round-up.
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 

@@ -251,9 +251,12 @@ int cyc_gramian_accumulate_dev(cyc_gramian_plan plan, const double* X, int64_t n
   splits = (nrows + rps - 1) / rps;
   int rc = plan->slab.reserve(sizeof(double) * (size_t)splits * pairs * TILE * TILE);
   if (rc) return rc;
+  {
+  cyc::KernelTimer timer("k_gram_tiles", st);
   hipLaunchKernelGGL(k_gram_tiles, dim3(pairs, (unsigned)splits), dim3(GT), 0, st, X, nrows, p,
                      mean, tps, rps, (double*)plan->slab.ptr);
   CYC_LAUNCH_CHECK("k_gram_tiles");
+  }
   hipLaunchKernelGGL(k_gram_fold, dim3(TILE * TILE / 256, pairs), dim3(256), 0, st,
                      (const double*)plan->slab.ptr, (int)splits, tps, p, U);
   CYC_LAUNCH_CHECK("k_gram_fold");

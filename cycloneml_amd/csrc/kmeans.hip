@@ -559,14 +559,6 @@ struct cyc_kmeans_plan_s {
   std::mutex mu;
   cyc::DeviceBuffer ct, stats, slowList, slowCount, assignTmp, costTmp;
   cyc::DeviceBuffer hist, total, cstart, chunkStart, perm, part, pw, pc, ccost;
-  bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
-  ~cyc_kmeans_plan_s() {
-    for (auto& e : events) {
-      (void)hipEventDestroy(e.first);
-      (void)hipEventDestroy(e.second);
-    }
-  }
 };
 
 namespace {
@@ -597,21 +589,12 @@ int launch_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64
   }
   const double marginFac = (double)(p->d + 16) * 0x1p-46;
   const int64_t blocks = (n + BM - 1) / BM;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (p->timing) {
-    CYC_HIP(hipEventCreate(&e0));
-    CYC_HIP(hipEventCreate(&e1));
-    CYC_HIP(hipEventRecord(e0, st));
-  }
+  cyc::KernelTimer timer("k_kmeans_assign", st);
   hipLaunchKernelGGL(k_kmeans_assign<BM>, dim3((unsigned)blocks), dim3(kAssignThreads),
                      p->assignLds, st, X, xnorm, n, p->d, p->d4, p->ldsStride,
                      (const double*)p->ct.ptr, C, cnorm, p->k, p->kpad, marginFac, assign, cost,
                      (int32_t*)p->slowList.ptr, (unsigned int*)p->slowCount.ptr);
   CYC_LAUNCH_CHECK("k_kmeans_assign");
-  if (p->timing) {
-    CYC_HIP(hipEventRecord(e1, st));
-    p->events.emplace_back(e0, e1);
-  }
   return CYC_OK;
 }
 
@@ -727,32 +710,6 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
 
 int cyc_kmeans_plan_destroy(cyc_kmeans_plan plan) {
   delete plan;
-  return CYC_OK;
-}
-
-int cyc_kmeans_plan_set_timing(cyc_kmeans_plan p, int enable) {
-  CYC_REQUIRE(p != nullptr, "plan must not be null");
-  std::lock_guard<std::mutex> g(p->mu);
-  p->timing = enable != 0;
-  return CYC_OK;
-}
-
-int cyc_kmeans_plan_get_timing(cyc_kmeans_plan p, double* total_ms, int64_t* launches) {
-  CYC_REQUIRE(p != nullptr && total_ms != nullptr && launches != nullptr,
-              "plan and outputs must not be null");
-  std::lock_guard<std::mutex> g(p->mu);
-  double tot = 0.0;
-  for (auto& e : p->events) {
-    CYC_HIP(hipEventSynchronize(e.second));
-    float ms = 0.f;
-    CYC_HIP(hipEventElapsedTime(&ms, e.first, e.second));
-    tot += ms;
-    (void)hipEventDestroy(e.first);
-    (void)hipEventDestroy(e.second);
-  }
-  *total_ms = tot;
-  *launches = (int64_t)p->events.size();
-  p->events.clear();
   return CYC_OK;
 }
 

@@ -562,6 +562,7 @@ int cyc_binary_logistic_add_dense_dev(cyc_logistic_plan p, const double* X, cons
   // zero the partial slabs of waves beyond nw (they still get written: rows empty)
   dim3 grid((unsigned)blocks);
   const int fpl = (F + 63) / 64;
+  cyc::KernelTimer* timer = new cyc::KernelTimer("k_binlog_dense", st);
   double* sg = (double*)p->slabG.ptr;
   double* ss = (double*)p->slabS.ptr;
   if (fpl <= 1) launch_bin_dense<1>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
@@ -570,6 +571,7 @@ int cyc_binary_logistic_add_dense_dev(cyc_logistic_plan p, const double* X, cons
   else if (fpl <= 8) launch_bin_dense<8>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
   else if (fpl <= 16) launch_bin_dense<16>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
   else launch_bin_dense<32>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
+  delete timer;
   CYC_LAUNCH_CHECK("k_binlog_dense");
   hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, ss, wtot, 3, (double*)p->scal.ptr);
   CYC_LAUNCH_CHECK("k_fold_scalars");
@@ -613,9 +615,11 @@ int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
     CYC_HIP(hipStreamSynchronize(st));
   }
   CYC_HIP(hipMemsetAsync(p->gradAcc.ptr, 0, sizeof(double) * (size_t)F, st));
+  cyc::KernelTimer* timer = new cyc::KernelTimer("k_binlog_csr", st);
   hipLaunchKernelGGL(k_binlog_csr, dim3((unsigned)blocks), dim3(256), 0, st, rowptr, colidx, vals,
                      labels, weights, n, coef, p->fitIntercept, offset, rpw,
                      (double*)p->gradAcc.ptr, (double*)p->slabS.ptr);
+  delete timer;
   CYC_LAUNCH_CHECK("k_binlog_csr");
   hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, (const double*)p->slabS.ptr, wtot,
                      3, (double*)p->scal.ptr);
@@ -679,6 +683,7 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
 #define CYC_MLR_M(CTV)                                                                        \
   hipLaunchKernelGGL(k_mlr_margins<CTV>, dim3(mb), dim3(256), 0, st, Xc, lc, wc, m, F, C, coef, \
                      off, (double*)p->multBuf.ptr, (double*)p->slabS.ptr, (double*)p->slabMS.ptr)
+    cyc::KernelTimer* tm = new cyc::KernelTimer("k_mlr_margins", st);
     switch (CT) {
       case 1: CYC_MLR_M(1); break;
       case 2: CYC_MLR_M(2); break;
@@ -690,6 +695,7 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
       default: CYC_MLR_M(8); break;
     }
 #undef CYC_MLR_M
+    delete tm;
     CYC_LAUNCH_CHECK("k_mlr_margins");
     // split-K over rows for the gradient GEMM: ~2048 workgroups
     int64_t splits = std::max<int64_t>(1, 2048 / ftiles);
@@ -700,6 +706,7 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
 #define CYC_MLR_G(CTV)                                                                         \
   hipLaunchKernelGGL(k_mlr_grad<CTV>, dim3(ftiles, (unsigned)splits), dim3(512), 0, st,         \
                      (const double*)p->multBuf.ptr, Xc, m, F, rps, (double*)p->gslab.ptr)
+    cyc::KernelTimer* tg = new cyc::KernelTimer("k_mlr_grad", st);
     switch (CT) {
       case 1: CYC_MLR_G(1); break;
       case 2: CYC_MLR_G(2); break;
@@ -711,6 +718,7 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
       default: CYC_MLR_G(8); break;
     }
 #undef CYC_MLR_G
+    delete tg;
     CYC_LAUNCH_CHECK("k_mlr_grad");
     hipLaunchKernelGGL(k_fold_columns, dim3((CP + 127) / 128), dim3(128), 0, st,
                        (const double*)p->slabMS.ptr, mwaves, CP, (double*)p->msTot.ptr);

@@ -48,6 +48,14 @@ int cyc_device_count(int* count);
 int cyc_set_device(int device);
 int cyc_synchronize(void* stream);
 
+/* Measurement hook (bench.py's roofline): while enabled, every launch of a
+ * workload's dominant kernel (k_kmeans_assign, k_gram_tiles, k_mlr_margins,
+ * k_mlr_grad, k_binlog_dense, k_binlog_csr) is bracketed by HIP events on the
+ * stream it runs on.  query waits for the recorded events of `kernel`,
+ * returns their summed time (ms) and count, and forgets them. */
+int cyc_profile_enable(int enable);
+int cyc_profile_query(const char* kernel, double* total_ms, int64_t* launches);
+
 /* ------------------------------------------------------------- vectors */
 /* norms[i] = Vectors.norm(row i, 2.0) bit-exactly (mllib/linalg/Vectors.scala:
  * 489-514, sequential sum of squares, correctly rounded sqrt).              */
@@ -67,13 +75,6 @@ typedef struct cyc_kmeans_plan_s* cyc_kmeans_plan;
 
 int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_plan* plan);
 int cyc_kmeans_plan_destroy(cyc_kmeans_plan plan);
-
-/* Measurement hook (bench.py's roofline): when enabled, every launch of the
- * dominant kernel (the MFMA assign kernel) is bracketed by HIP events on the
- * caller's stream.  get_timing waits for the recorded events, returns the
- * summed kernel time in ms and the launch count, and resets the record. */
-int cyc_kmeans_plan_set_timing(cyc_kmeans_plan plan, int enable);
-int cyc_kmeans_plan_get_timing(cyc_kmeans_plan plan, double* total_ms, int64_t* launches);
 
 /* computeStatistics for the given centers: fills the plan's packed k(k+1)/2
  * statistics (and copies them to stats_out if non-NULL, device memory). */

@@ -11,7 +11,7 @@ count of the assign kernel's X stream (20.48 GB per launch at 10M x 256
 reads as 19.1e6 KB, i.e. unhalved), so no factor is applied.  WRITE_SIZE is
 exact for streaming stores.  Both are per launch, like roofline.achieved.
 
-usage: tools/pmc_summary.py gpurun_out/<tag> profiles/<tag>
+usage: tools/pmc_summary.py gpurun_out/<tag> profiles/<tag> [rows_per_launch]
 """
 import collections
 import csv
@@ -27,7 +27,7 @@ def mean_counter(path):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
-def main(src, dst_prefix):
+def main(src, dst_prefix, rows=None):
     stats = {}
     ks = os.path.join(src, "trace", "run_kernel_stats.csv")
     for r in csv.DictReader(open(ks)):
@@ -42,6 +42,8 @@ def main(src, dst_prefix):
         out[name] = dict(s, fetch_kb=f, write_kb=w,
                          hbm_bytes_per_launch=None if f is None or w is None
                          else (f + w) * 1024.0)
+    if rows:
+        out["_rows_per_launch"] = int(rows)
     os.makedirs(os.path.dirname(dst_prefix) or ".", exist_ok=True)
     json.dump(out, open(dst_prefix + "_pmc.json", "w"), indent=1, sort_keys=True)
     with open(ks) as fi, open(dst_prefix + "_kernel_stats.csv", "w") as fo:
@@ -50,4 +52,4 @@ def main(src, dst_prefix):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
