@@ -277,6 +277,7 @@ class LRMultiWorkload:
 
 class LRSparseWorkload:
     kernel = "k_binlog_csr"
+    kernels = ("k_binlog_csr", "k_binlog_csc_grad")
     bound = "hbm"
 
     def __init__(self, n, dev, rank):
@@ -307,6 +308,7 @@ class LRSparseWorkload:
         rowptr = torch.arange(0, n * k + 1, k, dtype=torch.int64, device=dev)
         self.block = DeviceInstanceBlock(y, None, rowptr=rowptr, colidx=cols, values=vals,
                                          numFeatures=F)
+        self.block.prepare()      # one-time CSC copy (untimed, like blokify)
         import numpy as np
         self.coef = np.random.default_rng(4).normal(size=F + 1) * 0.01
         self.fn = RDDLossFunction([self.block], lambda c: BinaryLogisticBlockAggregator(

@@ -63,7 +63,12 @@ SIGNATURES = {
     "cyc_binary_logistic_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp,
                                                          _vp, _vp, _vp, _vp]),
     "cyc_binary_logistic_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
-                                                       _vp, _vp, _vp, _vp, _vp]),
+                                                       _vp, _vp, _vp, _vp, _vp, _vp]),
+    "cyc_csc_build_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(_vp)]),
+    "cyc_csc_destroy": (ctypes.c_int, [_vp]),
+    "cyc_csc_rows": (_i64, [_vp]),
+    "cyc_csc_arrays": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                      ctypes.POINTER(_vp)]),
     "cyc_multinomial_logistic_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp,
                                                               _vp, _vp, _vp, _vp, _vp]),
 }

@@ -45,6 +45,11 @@ struct KernelTimer {
   hipEvent_t e0 = nullptr;
 };
 
+// One-time CSR -> CSC transpose (csc.hip): colptr int64[F+1], rowidx int32,
+// cvals fp64; each column's rows in increasing order.
+int build_csc(const int64_t* rowptr, const int32_t* colidx, const double* vals, int64_t n, int F,
+              DeviceBuffer& colptr, DeviceBuffer& rowidx, DeviceBuffer& cvals, hipStream_t st);
+
 // Fixed-margin round-up.
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 

@@ -153,6 +153,58 @@ __global__ __launch_bounds__(256) void k_binlog_csr(
   }
 }
 
+// Pass 1 of the deterministic sparse path: margins / loss / multiplier per
+// row (no scatter), mult[r] kept for pass 2.
+__global__ __launch_bounds__(256) void k_binlog_csr_mult(
+    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
+    const double* __restrict__ vals, const double* __restrict__ labels,
+    const double* __restrict__ weights, int64_t n, const double* __restrict__ coef,
+    int fitIntercept, double offset, int64_t rowsPerWave, double* __restrict__ mult,
+    double* __restrict__ slabS) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t r0 = gw * rowsPerWave;
+  const int64_t r1 = min<int64_t>(n, r0 + rowsPerWave);
+  double loss = 0.0, wsum = 0.0, msum = 0.0;
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t p0 = rowptr[r], p1 = rowptr[r + 1];
+    double s = 0.0;
+    for (int64_t p = p0 + lane; p < p1; p += 64) s += vals[p] * coef[colidx[p]];
+    const double dot = wave_sum_bcast(s);
+    const double margin = fitIntercept ? offset + dot : dot;
+    const double w = weights ? weights[r] : 1.0;
+    const double m = bin_row(margin, w, labels[r], loss, wsum);
+    msum += m;
+    if (lane == 0) mult[r] = m;
+  }
+  if (lane == 0) {
+    slabS[gw * 3 + 0] = loss;
+    slabS[gw * 3 + 1] = wsum;
+    slabS[gw * 3 + 2] = msum;
+  }
+}
+
+// Pass 2: gradient by columns from the CSC copy, grad[f] = sum over the
+// column's rows (row order) of vals * mult[row]; one wave per column run,
+// fixed-shape reduction, no atomics (deterministic).  The reference scatters
+// the same products into grad[f] row by row (BLAS.scala:790-804).
+__global__ __launch_bounds__(256) void k_binlog_csc_grad(
+    const int64_t* __restrict__ colptr, const int32_t* __restrict__ rowidx,
+    const double* __restrict__ cvals, const double* __restrict__ mult, int F,
+    int colsPerWave, double* __restrict__ gradAcc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t c0 = gw * colsPerWave;
+  const int64_t c1 = min<int64_t>(F, c0 + colsPerWave);
+  for (int64_t c = c0; c < c1; ++c) {
+    const int64_t q0 = colptr[c], q1 = colptr[c + 1];
+    double s = 0.0;
+    for (int64_t q = q0 + lane; q < q1; q += 64) s += cvals[q] * mult[rowidx[q]];
+    s = wave_sum_bcast(s);
+    if (lane == 0) gradAcc[c] = s;
+  }
+}
+
 // Fold per-wave scalars in wave order: out3 = {loss, wsum, msum}.
 __global__ void k_fold_scalars(const double* __restrict__ slabS, int64_t waves, int width,
                                double* __restrict__ out) {
@@ -473,6 +525,7 @@ struct cyc_logistic_plan_s {
   int F = 0, C = 1, fitIntercept = 0, fitWithMean = 0;
   std::mutex mu;
   cyc::DeviceBuffer slabG, slabS, slabMS, gradAcc, scal, offset, multBuf, gslab, msTot;
+  cyc::DeviceBuffer rowMult;
 };
 
 namespace {
@@ -559,20 +612,21 @@ int cyc_binary_logistic_add_dense_dev(cyc_logistic_plan p, const double* X, cons
     }
     CYC_HIP(hipStreamSynchronize(st));
   }
-  // zero the partial slabs of waves beyond nw (they still get written: rows empty)
+  // waves past the last row still write (zero) partials, so the fold reads all
   dim3 grid((unsigned)blocks);
   const int fpl = (F + 63) / 64;
-  cyc::KernelTimer* timer = new cyc::KernelTimer("k_binlog_dense", st);
   double* sg = (double*)p->slabG.ptr;
   double* ss = (double*)p->slabS.ptr;
+  {
+  cyc::KernelTimer timer("k_binlog_dense", st);
   if (fpl <= 1) launch_bin_dense<1>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
   else if (fpl <= 2) launch_bin_dense<2>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
   else if (fpl <= 4) launch_bin_dense<4>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
   else if (fpl <= 8) launch_bin_dense<8>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
   else if (fpl <= 16) launch_bin_dense<16>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
   else launch_bin_dense<32>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
-  delete timer;
   CYC_LAUNCH_CHECK("k_binlog_dense");
+  }
   hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, ss, wtot, 3, (double*)p->scal.ptr);
   CYC_LAUNCH_CHECK("k_fold_scalars");
   hipLaunchKernelGGL(k_binlog_fold, dim3((F + 255) / 256), dim3(256), 0, st, sg, wtot, nullptr,
@@ -586,7 +640,8 @@ int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
                                     const int32_t* colidx, const double* vals,
                                     const double* labels, const double* weights, int64_t n,
                                     const double* coef, const double* scaledMean, double* grad,
-                                    double* lossSum, double* weightSum, void* stream) {
+                                    double* lossSum, double* weightSum, cyc_csc csc,
+                                    void* stream) {
   int rc = check_common(p, coef, scaledMean);
   if (rc) return rc;
   CYC_REQUIRE(n >= 0, "n >= 0");
@@ -614,13 +669,39 @@ int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
     }
     CYC_HIP(hipStreamSynchronize(st));
   }
-  CYC_HIP(hipMemsetAsync(p->gradAcc.ptr, 0, sizeof(double) * (size_t)F, st));
-  cyc::KernelTimer* timer = new cyc::KernelTimer("k_binlog_csr", st);
-  hipLaunchKernelGGL(k_binlog_csr, dim3((unsigned)blocks), dim3(256), 0, st, rowptr, colidx, vals,
-                     labels, weights, n, coef, p->fitIntercept, offset, rpw,
-                     (double*)p->gradAcc.ptr, (double*)p->slabS.ptr);
-  delete timer;
-  CYC_LAUNCH_CHECK("k_binlog_csr");
+  const int64_t* colptr = nullptr;
+  const int32_t* rowidx = nullptr;
+  const double* cvals = nullptr;
+  if (csc) {
+    CYC_REQUIRE(cyc_csc_rows(csc) == n, "the CSC copy does not match the CSR rows");
+    cyc_csc_arrays(csc, &colptr, &rowidx, &cvals);
+  }
+  if (csc) {
+    // Deterministic two-pass path: CSR margins -> mult, CSC column sums.
+    if ((rc = p->rowMult.reserve(sizeof(double) * (size_t)n))) return rc;
+    {
+      cyc::KernelTimer timer("k_binlog_csr", st);
+      hipLaunchKernelGGL(k_binlog_csr_mult, dim3((unsigned)blocks), dim3(256), 0, st, rowptr,
+                         colidx, vals, labels, weights, n, coef, p->fitIntercept, offset, rpw,
+                         (double*)p->rowMult.ptr, (double*)p->slabS.ptr);
+      CYC_LAUNCH_CHECK("k_binlog_csr_mult");
+    }
+    const int64_t cwaves = std::min<int64_t>(65536, F);
+    const int cpw = (int)((F + cwaves - 1) / cwaves);
+    const int64_t cblocks = ((F + cpw - 1) / cpw + 3) / 4;
+    cyc::KernelTimer timer("k_binlog_csc_grad", st);
+    hipLaunchKernelGGL(k_binlog_csc_grad, dim3((unsigned)cblocks), dim3(256), 0, st,
+                       colptr, rowidx, cvals, (const double*)p->rowMult.ptr, F, cpw,
+                       (double*)p->gradAcc.ptr);
+    CYC_LAUNCH_CHECK("k_binlog_csc_grad");
+  } else {
+    CYC_HIP(hipMemsetAsync(p->gradAcc.ptr, 0, sizeof(double) * (size_t)F, st));
+    cyc::KernelTimer timer("k_binlog_csr", st);
+    hipLaunchKernelGGL(k_binlog_csr, dim3((unsigned)blocks), dim3(256), 0, st, rowptr, colidx,
+                       vals, labels, weights, n, coef, p->fitIntercept, offset, rpw,
+                       (double*)p->gradAcc.ptr, (double*)p->slabS.ptr);
+    CYC_LAUNCH_CHECK("k_binlog_csr");
+  }
   hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, (const double*)p->slabS.ptr, wtot,
                      3, (double*)p->scal.ptr);
   CYC_LAUNCH_CHECK("k_fold_scalars");
@@ -683,7 +764,8 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
 #define CYC_MLR_M(CTV)                                                                        \
   hipLaunchKernelGGL(k_mlr_margins<CTV>, dim3(mb), dim3(256), 0, st, Xc, lc, wc, m, F, C, coef, \
                      off, (double*)p->multBuf.ptr, (double*)p->slabS.ptr, (double*)p->slabMS.ptr)
-    cyc::KernelTimer* tm = new cyc::KernelTimer("k_mlr_margins", st);
+    {
+    cyc::KernelTimer tm("k_mlr_margins", st);
     switch (CT) {
       case 1: CYC_MLR_M(1); break;
       case 2: CYC_MLR_M(2); break;
@@ -695,8 +777,8 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
       default: CYC_MLR_M(8); break;
     }
 #undef CYC_MLR_M
-    delete tm;
     CYC_LAUNCH_CHECK("k_mlr_margins");
+    }
     // split-K over rows for the gradient GEMM: ~2048 workgroups
     int64_t splits = std::max<int64_t>(1, 2048 / ftiles);
     splits = std::min<int64_t>(splits, std::max<int64_t>(1, m / 64));
@@ -706,7 +788,8 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
 #define CYC_MLR_G(CTV)                                                                         \
   hipLaunchKernelGGL(k_mlr_grad<CTV>, dim3(ftiles, (unsigned)splits), dim3(512), 0, st,         \
                      (const double*)p->multBuf.ptr, Xc, m, F, rps, (double*)p->gslab.ptr)
-    cyc::KernelTimer* tg = new cyc::KernelTimer("k_mlr_grad", st);
+    {
+    cyc::KernelTimer tg("k_mlr_grad", st);
     switch (CT) {
       case 1: CYC_MLR_G(1); break;
       case 2: CYC_MLR_G(2); break;
@@ -718,8 +801,8 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
       default: CYC_MLR_G(8); break;
     }
 #undef CYC_MLR_G
-    delete tg;
     CYC_LAUNCH_CHECK("k_mlr_grad");
+    }
     hipLaunchKernelGGL(k_fold_columns, dim3((CP + 127) / 128), dim3(128), 0, st,
                        (const double*)p->slabMS.ptr, mwaves, CP, (double*)p->msTot.ptr);
     CYC_LAUNCH_CHECK("k_fold_columns");

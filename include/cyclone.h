@@ -138,6 +138,20 @@ int cyc_covariance_finalize_dev(int32_t n, const double* U, int64_t m, double* G
  * weights may be NULL (all-unit weights, InstanceBlock's empty array). */
 typedef struct cyc_logistic_plan_s* cyc_logistic_plan;
 
+/* Column-major copy of a resident CSR shard, built once (outside the
+ * training loop, like InstanceBlock.blokifyWithMaxMemUsage,
+ * ml/feature/Instance.scala:146-187) by a stable sort of the nonzeros by
+ * column.  Passing it to cyc_binary_logistic_add_csr_dev replaces the
+ * gradient's fp64-atomic scatter by per-column sums (deterministic, each
+ * column's rows in the reference's order).  Costs 12 bytes per nonzero. */
+typedef struct cyc_csc_s* cyc_csc;
+int cyc_csc_build_dev(const int64_t* rowptr, const int32_t* colidx, const double* vals,
+                      int64_t n, int32_t numFeatures, void* stream, cyc_csc* out);
+int cyc_csc_destroy(cyc_csc csc);
+int64_t cyc_csc_rows(cyc_csc csc);
+int cyc_csc_arrays(cyc_csc csc, const int64_t** colptr, const int32_t** rowidx,
+                   const double** values);
+
 int cyc_logistic_plan_create(int32_t numFeatures, int32_t numClasses, int fitIntercept,
                              int fitWithMean, cyc_logistic_plan* plan);
 int cyc_logistic_plan_destroy(cyc_logistic_plan plan);
@@ -149,7 +163,8 @@ int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan plan, const int64_t* rowpt
                                     const int32_t* colidx, const double* vals,
                                     const double* labels, const double* weights, int64_t n,
                                     const double* coef, const double* scaledMean, double* grad,
-                                    double* lossSum, double* weightSum, void* stream);
+                                    double* lossSum, double* weightSum, cyc_csc csc,
+                                    void* stream);
 int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan plan, const double* X,
                                            const double* labels, const double* weights,
                                            int64_t n, const double* coef,

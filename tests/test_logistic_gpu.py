@@ -44,18 +44,20 @@ def _oracle_block(X, csr, labels, w, F):
     return dict(labels=labels, weights=w, X=X)
 
 
-@pytest.mark.parametrize("sparse", [False, True])
+@pytest.mark.parametrize("sparse", [False, True, "csc"])
 @pytest.mark.parametrize("fi,fwm", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("n,F", [(1, 3), (257, 17), (3000, 64), (2000, 300)])
 def test_binary_vs_oracle(cuda, sparse, fi, fwm, n, F):
     from cycloneml_amd.optim import BinaryLogisticBlockAggregator, DeviceInstanceBlock
-    rng = np.random.default_rng(n * 7 + F + sparse)
-    X, csr, labels, w = _make(n, F, sparse, rng, zero_w=True)
+    rng = np.random.default_rng(n * 7 + F + bool(sparse))
+    X, csr, labels, w = _make(n, F, bool(sparse), rng, zero_w=True)
     coef = rng.normal(size=F + (1 if fi else 0)) * 0.5
     sm = rng.normal(size=F) * 0.1 if fwm else None
     st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
     oracle.binary_logistic_add(_oracle_block(X, csr, labels, w, F), coef, fi, fwm, sm, st)
     blk = DeviceInstanceBlock.from_numpy(labels, w, X=X, csr=csr, numFeatures=F, device=cuda)
+    if sparse == "csc":
+        blk.prepare()
     agg = BinaryLogisticBlockAggregator(np.ones(F), sm, fi, fwm, coef, device=cuda).add(blk)
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
@@ -150,3 +152,13 @@ def test_sparse_config5_shape_properties(cuda):
     a2 = BinaryLogisticBlockAggregator(np.ones(F), None, True, False, coef, device=cuda).add(sub)
     _rel_close(a2.gradientSumArray.cpu().numpy(), st["grad"])
     assert a2.weight == m and agg.weight == n
+    # deterministic CSC path: same result within tolerance, bitwise run to run
+    blk.prepare()
+    a3 = BinaryLogisticBlockAggregator(np.ones(F), None, True, False, coef, device=cuda).add(blk)
+    a4 = BinaryLogisticBlockAggregator(np.ones(F), None, True, False, coef, device=cuda).add(blk)
+    g3 = a3.gradientSumArray.cpu().numpy()
+    _rel_close(g3, agg.gradientSumArray.cpu().numpy(), rtol=1e-10)
+    assert np.array_equal(g3, a4.gradientSumArray.cpu().numpy())
+    sub.prepare()
+    a5 = BinaryLogisticBlockAggregator(np.ones(F), None, True, False, coef, device=cuda).add(sub)
+    _rel_close(a5.gradientSumArray.cpu().numpy(), st["grad"])
