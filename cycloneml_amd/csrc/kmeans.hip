@@ -106,14 +106,35 @@ __global__ void k_stats_diag(int k, double* __restrict__ packed) {
 // A row is decided when L2 > U1: every other center is provably farther than
 // I1 by more than the combined fp64 error, so the reference's pruned loop
 // (whose prunes only skip centers that cannot win) returns I1 as well.
+//
+// The bounds are kept in fp32 rounded outward (L down, U up): the interval
+// only widens, so a decided row is still provably decided; rows whose gap is
+// below fp32 resolution (~1e-7 relative) simply go to the exact path.  This
+// halves the per-lane state (16 slots per lane) and keeps the kernel in
+// registers.
 struct Slot {
-  double L1, U1, L2;
+  float L1, U1, L2;
   int I1;
 };
 
-__device__ __forceinline__ void slot_merge(Slot& a, double oL1, double oU1, double oL2, int oI1) {
-  double hi = fmax(a.L1, oL1);
-  double l2 = fmin(hi, fmin(a.L2, oL2));
+// one fp32 ulp toward -inf / +inf (f finite, not NaN)
+__device__ __forceinline__ float ulp_down(float f) {
+  int b = __float_as_int(f);
+  if (f == 0.0f) return -__int_as_float(1);
+  return __int_as_float(f > 0.0f ? b - 1 : b + 1);
+}
+__device__ __forceinline__ float f_down(double x) {
+  float f = (float)x;
+  return ((double)f > x) ? ulp_down(f) : f;
+}
+__device__ __forceinline__ float f_up(double x) {
+  float f = (float)x;
+  return ((double)f < x) ? -ulp_down(-f) : f;
+}
+
+__device__ __forceinline__ void slot_merge(Slot& a, float oL1, float oU1, float oL2, int oI1) {
+  float hi = fmaxf(a.L1, oL1);
+  float l2 = fminf(hi, fminf(a.L2, oL2));
   if (oL1 < a.L1 || (oL1 == a.L1 && oI1 >= 0 && (a.I1 < 0 || oI1 < a.I1))) {
     a.L1 = oL1;
     a.U1 = oU1;
@@ -158,92 +179,126 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
   }
   __syncthreads();
 
-  Slot st[T][4];
+  // Per-(row slot, lane) screening state in plain scalar arrays (static
+  // indices only, so they stay in registers).
+  float sL1[T * 4], sU1[T * 4], sL2[T * 4];
+  int sI1[T * 4];
 #pragma unroll
-  for (int t = 0; t < T; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) st[t][r] = Slot{__builtin_inf(), __builtin_inf(), __builtin_inf(), -1};
+  for (int q = 0; q < T * 4; ++q) {
+    sL1[q] = sU1[q] = sL2[q] = __builtin_inff();
+    sI1[q] = -1;
+  }
   unsigned poison = 0;  // bit (4t + r): a NaN reached this slot
-
   const double* arow = Xs + (lane & 15) * ldsStride + (lane >> 4);
-  for (int nb = wave * 16; nb < kpad; nb += kWaves * 16) {
-    cyc_double4 acc[T];
+  cyc_double4 acc[T];
+
+  // Screening update for one finished 16-center slab (centers nb .. nb+15).
+#define CYC_EPILOGUE(NB, CN)                                                   \
+  do {                                                                         \
+    const int c_ = (NB) + (lane & 15);                                         \
+    if (c_ < k) {                                                              \
+      const double cn_ = (CN);                                                 \
+      const double cn2_ = cn_ * cn_;                                           \
+      _Pragma("unroll") for (int t = 0; t < T; ++t) {                          \
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) {                        \
+          const int q = 4 * t + r;                                             \
+          const double xn = xnS[t * 16 + (lane >> 4) + 4 * r];                 \
+          const double approx = (xn * xn + cn2_) - 2.0 * acc[t][r];            \
+          const double sm = xn + cn_;                                          \
+          const double M = (sm * sm) * marginFac;                              \
+          const double L = approx - M, U = approx + M;                         \
+          if (!(L == L) || !(U == U)) poison |= 1u << q;                       \
+          if (L < sL1[q]) {                                                    \
+            sL2[q] = sL1[q];                                                   \
+            sL1[q] = f_down(L);                                                \
+            sU1[q] = f_up(U);                                                  \
+            sI1[q] = c_;                                                       \
+          } else if (L < sL2[q]) {                                             \
+            sL2[q] = f_down(L);                                                \
+          }                                                                    \
+        }                                                                      \
+      }                                                                        \
+    }                                                                          \
+  } while (0)
+
+  const int nslabs = (kpad - wave * 16 + kWaves * 16 - 1) / (kWaves * 16);
+  if ((d4 & 15) == 0) {
+    // Flat software pipeline over (slab, 16-dim group) steps: the B fragments
+    // of step i+1 are in flight while step i's 4 x T MFMAs run.  Two named
+    // register buffers keep every index static.
+    const int G = d4 / 16;
+    const int total = nslabs * G;
+    double cn = 0.0;
+    double b0[4], b1[4];
+#define CYC_LOADB(B, I)                                                             \
+  do {                                                                              \
+    const int nb_ = wave * 16 + ((I) / G) * (kWaves * 16);                          \
+    const double* bc_ = Ct + (int64_t)(((I) % G) * 16 + (lane >> 4)) * kpad + nb_ + \
+                        (lane & 15);                                                \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s) B[s] = bc_[(int64_t)(s * 4) * kpad]; \
+  } while (0)
+#define CYC_COMPUTE(B, I)                                                           \
+  do {                                                                              \
+    const int g_ = (I) % G;                                                         \
+    const int nb_ = wave * 16 + ((I) / G) * (kWaves * 16);                          \
+    if (g_ == 0) {                                                                  \
+      _Pragma("unroll") for (int t = 0; t < T; ++t) acc[t] = cyc_double4{0.0, 0.0, 0.0, 0.0}; \
+      const int c0_ = nb_ + (lane & 15);                                            \
+      cn = c0_ < k ? cnorm[c0_] : 0.0;                                              \
+    }                                                                               \
+    _Pragma("unroll") for (int s = 0; s < 4; ++s) {                                 \
+      _Pragma("unroll") for (int t = 0; t < T; ++t) {                               \
+        const double a_ = arow[t * 16 * ldsStride + g_ * 16 + s * 4];               \
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_, B[s], acc[t], 0, 0, 0);   \
+      }                                                                             \
+    }                                                                               \
+    if (g_ == G - 1) CYC_EPILOGUE(nb_, cn);                                         \
+  } while (0)
+    if (total > 0) CYC_LOADB(b0, 0);
+    for (int i = 0; i < total; i += 2) {
+      if (i + 1 < total) CYC_LOADB(b1, i + 1);
+      CYC_COMPUTE(b0, i);
+      if (i + 2 < total) CYC_LOADB(b0, i + 2);
+      if (i + 1 < total) CYC_COMPUTE(b1, i + 1);
+    }
+#undef CYC_LOADB
+#undef CYC_COMPUTE
+  } else {
+    for (int nb = wave * 16; nb < kpad; nb += kWaves * 16) {
 #pragma unroll
-    for (int t = 0; t < T; ++t) acc[t] = cyc_double4{0.0, 0.0, 0.0, 0.0};
-    const double* bcol = Ct + (int64_t)(lane >> 4) * kpad + nb + (lane & 15);
-    // Main loop: 8 k-steps (32 dims) per group, B fragments loaded one group ahead.
-    double bcur[8], bnxt[8];
-    const int groups = d4 / 32;
-#pragma unroll
-    for (int s = 0; s < 8; ++s) bcur[s] = (s * 4 < d4) ? bcol[(int64_t)(s * 4) * kpad] : 0.0;
-    for (int g = 0; g < groups; ++g) {
-      const int kb = g * 32;
-      if (g + 1 < groups) {
-#pragma unroll
-        for (int s = 0; s < 8; ++s) bnxt[s] = bcol[(int64_t)(kb + 32 + s * 4) * kpad];
-      }
-#pragma unroll
-      for (int s = 0; s < 8; ++s) {
+      for (int t = 0; t < T; ++t) acc[t] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+      const double* bcol = Ct + (int64_t)(lane >> 4) * kpad + nb + (lane & 15);
+      for (int kb = 0; kb < d4; kb += 4) {
+        const double b = bcol[(int64_t)kb * kpad];
 #pragma unroll
         for (int t = 0; t < T; ++t) {
-          double a = arow[t * 16 * ldsStride + kb + s * 4];
-          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bcur[s], acc[t], 0, 0, 0);
+          const double a = arow[t * 16 * ldsStride + kb];
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
         }
       }
-#pragma unroll
-      for (int s = 0; s < 8; ++s) bcur[s] = bnxt[s];
-    }
-    // Tail k-steps (d4 not a multiple of 32).
-    for (int kb = groups * 32; kb < d4; kb += 4) {
-      double b = bcol[(int64_t)kb * kpad];
-#pragma unroll
-      for (int t = 0; t < T; ++t) {
-        double a = arow[t * 16 * ldsStride + kb];
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
-      }
-    }
-    // Epilogue: D[row = (lane>>4) + 4 r][col = lane & 15] for f64 16x16x4.
-    const int c = nb + (lane & 15);
-    if (c < k) {
-      const double cn = cnorm[c];
-      const double cn2 = cn * cn;
-#pragma unroll
-      for (int t = 0; t < T; ++t) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = t * 16 + (lane >> 4) + 4 * r;
-          const double xn = xnS[row];
-          const double approx = (xn * xn + cn2) - 2.0 * acc[t][r];
-          const double sm = xn + cn;
-          const double M = (sm * sm) * marginFac;
-          const double L = approx - M, U = approx + M;
-          if (!(L == L) || !(U == U)) poison |= 1u << (4 * t + r);
-          Slot& S = st[t][r];
-          if (L < S.L1) {
-            S.L2 = S.L1;
-            S.L1 = L;
-            S.U1 = U;
-            S.I1 = c;
-          } else if (L < S.L2) {
-            S.L2 = L;
-          }
-        }
-      }
+      const int c = nb + (lane & 15);
+      CYC_EPILOGUE(nb, c < k ? cnorm[c] : 0.0);
     }
   }
+#undef CYC_EPILOGUE
 
   // Reduce each slot over the 16 lanes that hold the same row.
 #pragma unroll
   for (int t = 0; t < T; ++t) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      Slot& S = st[t][r];
+      const int q = 4 * t + r;
+      Slot S{sL1[q], sU1[q], sL2[q], sI1[q]};
 #pragma unroll
       for (int m = 1; m < 16; m <<= 1) {
-        double oL1 = __shfl_xor(S.L1, m), oU1 = __shfl_xor(S.U1, m), oL2 = __shfl_xor(S.L2, m);
+        float oL1 = __shfl_xor(S.L1, m), oU1 = __shfl_xor(S.U1, m), oL2 = __shfl_xor(S.L2, m);
         int oI1 = __shfl_xor(S.I1, m);
         slot_merge(S, oL1, oU1, oL2, oI1);
       }
+      sL1[q] = S.L1;
+      sU1[q] = S.U1;
+      sL2[q] = S.L2;
+      sI1[q] = S.I1;
     }
   }
 #pragma unroll
@@ -256,11 +311,11 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
       for (int r = 0; r < 4; ++r) {
         const int row = t * 16 + (lane >> 4) + 4 * r;
         double* m = mrg + ((size_t)wave * BM + row) * 4;
-        const Slot& S = st[t][r];
-        m[0] = S.L1;
-        m[1] = S.U1;
-        m[2] = ((poison >> (4 * t + r)) & 1u) ? -__builtin_inf() : S.L2;
-        m[3] = (double)S.I1;
+        const int q = 4 * t + r;
+        m[0] = sL1[q];
+        m[1] = sU1[q];
+        m[2] = ((poison >> q) & 1u) ? -__builtin_inf() : (double)sL2[q];
+        m[3] = (double)sI1[q];
       }
     }
   }
@@ -269,10 +324,10 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
   // One lane per row: merge the 8 waves, then decide or queue.
   if (tid < rows) {
     const int row = tid;
-    Slot S{__builtin_inf(), __builtin_inf(), __builtin_inf(), -1};
+    Slot S{__builtin_inff(), __builtin_inff(), __builtin_inff(), -1};
     for (int w = 0; w < kWaves; ++w) {
       const double* m = mrg + ((size_t)w * BM + row) * 4;
-      slot_merge(S, m[0], m[1], m[2], (int)m[3]);
+      slot_merge(S, (float)m[0], (float)m[1], (float)m[2], (int)m[3]);
     }
     const int64_t grow = row0 + row;
     if (S.I1 >= 0 && S.L2 > S.U1) {

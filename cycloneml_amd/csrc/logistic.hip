@@ -278,10 +278,15 @@ __global__ void k_mlr_offset(const double* __restrict__ coef, const double* __re
   off[c] = o;
 }
 
-constexpr int MR = 64;     // rows per margin tile
-constexpr int MK = 64;     // features per LDS chunk
-constexpr int MKS = MK + 2;
+constexpr int MR = 128;    // rows per margin tile (4 waves x 32 rows)
+constexpr int MK = 32;     // features per LDS chunk
+constexpr int MKS = MK + 2;  // X chunk row stride: == 2 (mod 32) doubles
 
+// margins = X W^T (+ offset) for 128-row tiles; X and W chunks of 32
+// features staged through LDS (coalesced loads), 2 row tiles x CT class tiles
+// of 16x16 per wave on v_mfma_f64_16x16x4f64; softmax/loss/multiplier
+// epilogue in registers.  Persistent over tiles; 2 workgroups per CU so one
+// stages while the other computes.
 template <int CT>
 __global__ __launch_bounds__(256, 2) void k_mlr_margins(
     const double* __restrict__ X, const double* __restrict__ labels,
@@ -289,7 +294,9 @@ __global__ __launch_bounds__(256, 2) void k_mlr_margins(
     const double* __restrict__ offset, double* __restrict__ mult, double* __restrict__ slabS,
     double* __restrict__ slabMS) {
   constexpr int CP = CT * 16;
+  constexpr int CPS = CP + ((16 - CP % 32) + 32) % 32;  // == 16 (mod 32) doubles
   __shared__ __attribute__((aligned(16))) double Xs[MR * MKS];
+  __shared__ __attribute__((aligned(16))) double Ws[MK * CPS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t tiles = (n + MR - 1) / MR;
   double loss = 0.0, wsum = 0.0;
@@ -305,100 +312,111 @@ __global__ __launch_bounds__(256, 2) void k_mlr_margins(
 
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t r0 = tile * MR;
-    cyc_double4 acc[CT];
+    cyc_double4 acc[2][CT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) acc[ct] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[t][ct] = cyc_double4{0.0, 0.0, 0.0, 0.0};
     for (int f0 = 0; f0 < F; f0 += MK) {
       __syncthreads();
+      // X chunk: 128 rows x 32 features
       for (int e = tid; e < MR * MK; e += 256) {
-        const int rr = e / MK, ff = e % MK;
+        const int rr = e >> 5, ff = e & 31;
         const int64_t r = r0 + rr;
         const int f = f0 + ff;
         Xs[rr * MKS + ff] = (r < n && f < F) ? X[r * F + f] : 0.0;
       }
+      // W chunk: features f0..f0+31 are one contiguous run of coef (f*C + c)
+      const int fl = min(MK, F - f0);
+      for (int e = tid; e < MK * CP; e += 256) {
+        const int ff = e / CP, c = e - ff * CP;
+        Ws[ff * CPS + c] = (ff < fl && c < C) ? coef[(int64_t)(f0 + ff) * C + c] : 0.0;
+      }
       __syncthreads();
-#pragma unroll 4
+#pragma unroll
       for (int kk = 0; kk < MK; kk += 4) {
-        const double a = Xs[(wave * 16 + (lane & 15)) * MKS + kk + (lane >> 4)];
-        const int f = f0 + kk + (lane >> 4);
+        const double a0 = Xs[(wave * 32 + (lane & 15)) * MKS + kk + (lane >> 4)];
+        const double a1 = Xs[(wave * 32 + 16 + (lane & 15)) * MKS + kk + (lane >> 4)];
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-          const int c = ct * 16 + (lane & 15);
-          const double b = (f < F && c < C) ? coef[(int64_t)f * C + c] : 0.0;
-          acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[ct], 0, 0, 0);
+          const double b = Ws[(kk + (lane >> 4)) * CPS + ct * 16 + (lane & 15)];
+          acc[0][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, acc[0][ct], 0, 0, 0);
+          acc[1][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc[1][ct], 0, 0, 0);
         }
       }
     }
-    // Epilogue: lane holds rows (lane>>4) + 4r of this wave's 16, classes
+    // Epilogue: lane holds rows 32 wave + 16 t + (lane>>4) + 4r, classes
     // 16 ct + (lane & 15).
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int64_t row = r0 + wave * 16 + (lane >> 4) + 4 * r;
-      const bool rowok = row < n;
-      double m[CT];
-      double mx = -1.7976931348623157e308;  // Double.MinValue (Utils.scala:113)
-      int infc = 1 << 30;
+    for (int t = 0; t < 2; ++t) {
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        const int c = ct * 16 + (lane & 15);
-        m[ct] = acc[ct][r] + offc[ct];  // 1.0*temp + 1.0*offset (netlib dgemm)
-        if (c < C) {
-          if (m[ct] == __builtin_inf()) infc = min(infc, c);
-          else if (m[ct] > mx) mx = m[ct];
-        }
-      }
-#pragma unroll
-      for (int k = 1; k < 16; k <<= 1) {
-        mx = fmax(mx, __shfl_xor(mx, k));
-        infc = min(infc, __shfl_xor(infc, k));
-      }
-      double p[CT];
-      if (infc < (1 << 30)) {
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = r0 + wave * 32 + t * 16 + (lane >> 4) + 4 * r;
+        const bool rowok = row < n;
+        double m[CT];
+        double mx = -1.7976931348623157e308;  // Double.MinValue (Utils.scala:113)
+        int infc = 1 << 30;
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
           const int c = ct * 16 + (lane & 15);
-          p[ct] = (c == infc) ? 1.0 : 0.0 * m[ct];
-        }
-      } else {
-        double sum = 0.0;
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          const int c = ct * 16 + (lane & 15);
-          p[ct] = (c < C) ? exp(m[ct] - mx) : 0.0;
-          sum += p[ct];
+          m[ct] = acc[t][ct][r] + offc[ct];  // 1.0*temp + 1.0*offset (netlib dgemm)
+          if (c < C) {
+            if (m[ct] == __builtin_inf()) infc = min(infc, c);
+            else if (m[ct] > mx) mx = m[ct];
+          }
         }
 #pragma unroll
-        for (int k = 1; k < 16; k <<= 1) sum += __shfl_xor(sum, k);
-        sum = __shfl(sum, lane & 48);  // one association order per row
-        const double inv = 1.0 / sum;
+        for (int k = 1; k < 16; k <<= 1) {
+          mx = fmax(mx, __shfl_xor(mx, k));
+          infc = min(infc, __shfl_xor(infc, k));
+        }
+        double p[CT];
+        if (infc < (1 << 30)) {
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) p[ct] = inv * p[ct];
-      }
-      const double w = rowok ? (weights ? weights[row] : 1.0) : 0.0;
-      const int label = rowok ? (int)labels[row] : 0;
-      // probability of the label class, from the lane that holds it
-      double pl = 0.0;
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct)
-        if (ct == (label >> 4)) pl = p[ct];
-      pl = __shfl(pl, (lane & 48) | (label & 15));
-      if (rowok && (lane & 15) == 0) {
-        wsum += w;
-        if (w > 0) loss -= w * log(pl);
-      }
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        const int c = ct * 16 + (lane & 15);
-        double mu;
-        if (w > 0) {
-          mu = (w != 1.0) ? w * p[ct] : p[ct];
-          if (c == label) mu -= w;
+          for (int ct = 0; ct < CT; ++ct) {
+            const int c = ct * 16 + (lane & 15);
+            p[ct] = (c == infc) ? 1.0 : 0.0 * m[ct];
+          }
         } else {
-          mu = 0.0 * p[ct];
+          double sum = 0.0;
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) {
+            const int c = ct * 16 + (lane & 15);
+            p[ct] = (c < C) ? exp(m[ct] - mx) : 0.0;
+            sum += p[ct];
+          }
+#pragma unroll
+          for (int k = 1; k < 16; k <<= 1) sum += __shfl_xor(sum, k);
+          sum = __shfl(sum, lane & 48);  // one association order per row
+          const double inv = 1.0 / sum;
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) p[ct] = inv * p[ct];
         }
-        if (c >= C || !rowok) mu = 0.0;
-        if (rowok) mult[row * CP + c] = mu;
-        ms[ct] += mu;
+        const double w = rowok ? (weights ? weights[row] : 1.0) : 0.0;
+        const int label = rowok ? (int)labels[row] : 0;
+        double pl = 0.0;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          if (ct == (label >> 4)) pl = p[ct];
+        pl = __shfl(pl, (lane & 48) | (label & 15));
+        if (rowok && (lane & 15) == 0) {
+          wsum += w;
+          if (w > 0) loss -= w * log(pl);
+        }
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int c = ct * 16 + (lane & 15);
+          double mu;
+          if (w > 0) {
+            mu = (w != 1.0) ? w * p[ct] : p[ct];
+            if (c == label) mu -= w;
+          } else {
+            mu = 0.0 * p[ct];
+          }
+          if (c >= C || !rowok) mu = 0.0;
+          if (rowok) mult[row * CP + c] = mu;
+          ms[ct] += mu;
+        }
       }
     }
   }
@@ -442,20 +460,41 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
   cyc_double4 acc[CT][2];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) acc[ct][0] = acc[ct][1] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+  // Register prefetch of the next 16-row chunk while this one is multiplied.
+  constexpr int MPT = (GR * CP + 511) / 512;   // mult doubles per thread
+  constexpr int XPT = GR * GF / 512;           // X doubles per thread (8)
+  double mreg[MPT], xreg[XPT];
+  auto load_regs = [&](int64_t rb) {
+#pragma unroll
+    for (int i = 0; i < MPT; ++i) {
+      const int e = tid + 512 * i;
+      const int rr = e / CP, c = e - rr * CP;
+      mreg[i] = (e < GR * CP && rb + rr < r1) ? mult[(rb + rr) * CP + c] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int e = tid + 512 * i;
+      const int rr = e >> 8, ff = e & (GF - 1);
+      const int f = F0 + ff;
+      xreg[i] = (rb + rr < r1 && f < F) ? X[(rb + rr) * F + f] : 0.0;
+    }
+  };
+  if (r0 < r1) load_regs(r0);
   for (int64_t rb = r0; rb < r1; rb += GR) {
     __syncthreads();
-    for (int e = tid; e < GR * CP; e += 512) {
-      const int rr = e / CP, c = e % CP;
-      const int64_t r = rb + rr;
-      Ms[rr * CPS + c] = (r < r1) ? mult[r * CP + c] : 0.0;
+#pragma unroll
+    for (int i = 0; i < MPT; ++i) {
+      const int e = tid + 512 * i;
+      const int rr = e / CP, c = e - rr * CP;
+      if (e < GR * CP) Ms[rr * CPS + c] = mreg[i];
     }
-    for (int e = tid; e < GR * GF; e += 512) {
-      const int rr = e / GF, ff = e % GF;
-      const int64_t r = rb + rr;
-      const int f = F0 + ff;
-      Xs[rr * GFS + ff] = (r < r1 && f < F) ? X[r * F + f] : 0.0;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int e = tid + 512 * i;
+      Xs[(e >> 8) * GFS + (e & (GF - 1))] = xreg[i];
     }
     __syncthreads();
+    if (rb + GR < r1) load_regs(rb + GR);
 #pragma unroll
     for (int kk = 0; kk < GR; kk += 4) {
       const int krow = kk + (lane >> 4);
@@ -731,7 +770,7 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
   hipStream_t st = cyc::as_stream(stream);
   // Rows are processed in chunks so the multiplier matrix stays small.
   const int64_t chunk = std::min<int64_t>(n, 4 << 20);
-  const int mblocks = 2048;
+  const int mblocks = 512;   // persistent: 2 per CU
   const int64_t mwaves = (int64_t)mblocks * 4;
   const int ftiles = (F + GF - 1) / GF;
   if ((rc = p->multBuf.reserve(sizeof(double) * (size_t)chunk * CP)) ||
