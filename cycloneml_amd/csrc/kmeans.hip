@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -348,6 +349,214 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
   }
 }
 
+// Second-generation assign kernel (the default when d4 % 32 == 0 and the
+// center norms fit in LDS):
+//   - per (row slot, lane) only the lower bounds L1 (best), L2 (second) in
+//     fp32 rounded down and the best index; the upper bound of the best
+//     center is rebuilt at the end as next_up(L1) + 2 M(best) from its norm,
+//     which is >= its true upper bound, so certification stays conservative;
+//   - branch-free epilogue (selects), center norms read from LDS (no global
+//     load that would force a vmcnt(0) drain of the B prefetch);
+//   - B fragments for 32 dims (8 MFMA k-steps) ping-pong between two named
+//     register sets, one step ahead.
+// ABL (timing ablations for tools/kmeans_ab.py, wrong results by design):
+// 0 = real kernel; 1 = no epilogue; 2 = no B loads (B from registers);
+// 3 = neither.
+template <int BM, int ABL>
+__global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign2(
+    const double* __restrict__ X, const double* __restrict__ xnorm, int64_t n, int d, int d4,
+    int ldsStride, const double* __restrict__ Ct, const double* __restrict__ C,
+    const double* __restrict__ cnorm, int k, int kpad, double marginFac,
+    int32_t* __restrict__ assign, double* __restrict__ cost, int32_t* __restrict__ slowList,
+    unsigned int* __restrict__ slowCount) {
+  constexpr int T = BM / 16;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double* Xs = smem;                      // BM x ldsStride
+  double* xnS = Xs + BM * ldsStride;      // BM
+  double* mrg = xnS + BM;                 // kWaves x BM x 4
+  double* cnS = mrg + kWaves * BM * 4;    // kpad center norms
+  double* xqS = cnS + kpad;               // BM: xn^2 (1 - 2 fac)
+  // Margin M' = 2 fac (|x|^2 + |c|^2) >= fac (|x| + |c|)^2, so the lower bound
+  // is L = (xq + cq) - 2 x.c with xq = |x|^2 (1 - 2 fac), cq likewise.
+  const double fac2 = 2.0 * marginFac;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
+  const int64_t row0 = (int64_t)blockIdx.x * BM;
+  const int rows = (int)min<int64_t>(BM, n - row0);
+  {
+    const double* src = X + row0 * d;
+    const int total = rows * d;
+    for (int e = tid; e < total; e += kAssignThreads) {
+      int r = e / d, c = e - r * d;
+      Xs[r * ldsStride + c] = src[e];
+    }
+    for (int e = tid; e < BM * d4; e += kAssignThreads) {
+      int r = e / d4, c = e - r * d4;
+      if (r >= rows || c >= d) Xs[r * ldsStride + c] = 0.0;
+    }
+    if (tid < BM) {
+      const double xn = (tid < rows) ? xnorm[row0 + tid] : 0.0;
+      xnS[tid] = xn;
+      xqS[tid] = (xn * xn) * (1.0 - fac2);
+    }
+    for (int c = tid; c < kpad; c += kAssignThreads) cnS[c] = c < k ? cnorm[c] : 0.0;
+  }
+  __syncthreads();
+  // B fragments through a buffer descriptor: per-lane byte offset constant,
+  // the (group, k-step, slab) part in an SGPR soffset -> no VALU address math.
+  const auto ctR = __builtin_amdgcn_make_buffer_rsrc((void*)Ct, (short)0, d4 * kpad * 8,
+                                                     0x00020000);
+  const int laneOff = ((lane >> 4) * kpad + (lane & 15)) * 8;
+
+  float sL1[T * 4], sL2[T * 4];
+  int sI1[T * 4];
+#pragma unroll
+  for (int q = 0; q < T * 4; ++q) {
+    sL1[q] = sL2[q] = __builtin_inff();
+    sI1[q] = -1;
+  }
+  unsigned poison = 0;
+  const double* arow = Xs + (lane & 15) * ldsStride + (lane >> 4);
+  cyc_double4 acc[T];
+  const int G = d4 / 32;
+  const int nslabs = (kpad - wave * 16 + kWaves * 16 - 1) / (kWaves * 16);
+  const int total = nslabs * G;
+  double b0[8], b1[8];
+
+#define CYC_LOADB(B, I)                                                              \
+  do {                                                                               \
+    const int nb_ = wave * 16 + ((I) / G) * (kWaves * 16);                           \
+    const int so_ = ((((I) % G) * 32) * kpad + nb_) * 8;                             \
+    if (ABL & 2) {                                                                   \
+      _Pragma("unroll") for (int s = 0; s < 8; ++s) B[s] = (double)(so_ + s);        \
+    } else {                                                                         \
+    _Pragma("unroll") for (int s = 0; s < 8; ++s)                                    \
+      B[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(          \
+          ctR, laneOff, so_ + s * 32 * kpad, 0));                                    \
+    }                                                                                \
+  } while (0)
+#define CYC_COMPUTE(B, I)                                                            \
+  do {                                                                               \
+    const int g_ = (I) % G;                                                          \
+    if (g_ == 0) {                                                                   \
+      _Pragma("unroll") for (int t = 0; t < T; ++t) acc[t] = cyc_double4{0.0, 0.0, 0.0, 0.0}; \
+    }                                                                                \
+    _Pragma("unroll") for (int s = 0; s < 8; ++s) {                                  \
+      _Pragma("unroll") for (int t = 0; t < T; ++t) {                                \
+        const double a_ = arow[t * 16 * ldsStride + g_ * 32 + s * 4];                \
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_, B[s], acc[t], 0, 0, 0);    \
+      }                                                                              \
+    }                                                                                \
+    if ((ABL & 1) && g_ == G - 1) {                                                  \
+      _Pragma("unroll") for (int t = 0; t < T; ++t) __builtin_nontemporal_store(acc[t][0], (double*)xnS + 0 * t + BM); \
+    }                                                                                \
+    if (!(ABL & 1) && g_ == G - 1) {                                                 \
+      const int c_ = wave * 16 + ((I) / G) * (kWaves * 16) + (lane & 15);            \
+      const double cn_ = cnS[c_];                                                    \
+      const double cq_ = (cn_ * cn_) * (1.0 - fac2);                                 \
+      const bool cok_ = c_ < k;                                                      \
+      _Pragma("unroll") for (int t = 0; t < T; ++t) {                                \
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) {                              \
+          const int q = 4 * t + r;                                                   \
+          const double xq = xqS[t * 16 + (lane >> 4) + 4 * r];                       \
+          const double L = (xq + cq_) - (acc[t][r] + acc[t][r]);                      \
+          poison |= (cok_ && !(L == L)) ? (1u << q) : 0u;                            \
+          const float fL = (float)L;   /* f32 rounding mode is toward -inf here */   \
+          const bool lt = cok_ && fL < sL1[q];                                       \
+          const float l2 = cok_ ? fminf(sL2[q], fL) : sL2[q];                        \
+          sL2[q] = lt ? sL1[q] : l2;                                                 \
+          sI1[q] = lt ? c_ : sI1[q];                                                 \
+          sL1[q] = lt ? fL : sL1[q];                                                 \
+        }                                                                            \
+      }                                                                              \
+    }                                                                                \
+  } while (0)
+  // MODE.FP_ROUND single-precision bits [1:0] = 2 (toward -inf): every
+  // (float) conversion of a lower bound in the loop rounds down.
+  __builtin_amdgcn_s_setreg(0x801, 2);
+  if (total > 0) CYC_LOADB(b0, 0);
+  for (int i = 0; i < total; i += 2) {
+    if (i + 1 < total) CYC_LOADB(b1, i + 1);
+    CYC_COMPUTE(b0, i);
+    if (i + 2 < total) CYC_LOADB(b0, i + 2);
+    if (i + 1 < total) CYC_COMPUTE(b1, i + 1);
+  }
+  __builtin_amdgcn_s_setreg(0x801, 0);   // back to round-to-nearest-even
+#undef CYC_LOADB
+#undef CYC_COMPUTE
+
+  // Reduce each slot over the 16 lanes that hold the same row.
+#pragma unroll
+  for (int q = 0; q < T * 4; ++q) {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) {
+      const float oL1 = __shfl_xor(sL1[q], m), oL2 = __shfl_xor(sL2[q], m);
+      const int oI1 = __shfl_xor(sI1[q], m);
+      const float hi = fmaxf(sL1[q], oL1);
+      sL2[q] = fminf(hi, fminf(sL2[q], oL2));
+      const bool take = oL1 < sL1[q] || (oL1 == sL1[q] && oI1 >= 0 && (sI1[q] < 0 || oI1 < sI1[q]));
+      sI1[q] = take ? oI1 : sI1[q];
+      sL1[q] = take ? oL1 : sL1[q];
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < 16; m <<= 1) poison |= __shfl_xor(poison, m);
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = 4 * t + r;
+        double* m = mrg + ((size_t)wave * BM + t * 16 + (lane >> 4) + 4 * r) * 4;
+        m[0] = sL1[q];
+        m[1] = ((poison >> q) & 1u) ? -__builtin_inf() : (double)sL2[q];
+        m[2] = (double)sI1[q];
+      }
+    }
+  }
+  __syncthreads();
+
+  if (tid < rows) {
+    const int row = tid;
+    float L1 = __builtin_inff(), L2 = __builtin_inff();
+    int I1 = -1;
+    for (int w = 0; w < kWaves; ++w) {
+      const double* m = mrg + ((size_t)w * BM + row) * 4;
+      const float oL1 = (float)m[0], oL2 = (float)m[1];
+      const int oI1 = (int)m[2];
+      const float hi = fmaxf(L1, oL1);
+      L2 = fminf(hi, fminf(L2, oL2));
+      if (oL1 < L1 || (oL1 == L1 && oI1 >= 0 && (I1 < 0 || oI1 < I1))) {
+        L1 = oL1;
+        I1 = oI1;
+      }
+    }
+    const int64_t grow = row0 + row;
+    bool decided = false;
+    if (I1 >= 0 && L1 == L1 && L1 < __builtin_inff()) {
+      const double xn = xnS[row], cn = cnS[I1];
+      const double M = (xn * xn + cn * cn) * fac2;
+      const double U = (double)(-ulp_down(-L1)) + 2.0 * M * (1.0 + 0x1p-40);
+      decided = (double)L2 > U;
+    }
+    if (decided) {
+      const double* crow = C + (int64_t)I1 * d;
+      const double* xrow = Xs + row * ldsStride;
+      double s = 0.0;
+      for (int j = 0; j < d; ++j) {
+        double sc = dsub(crow[j], xrow[j]);
+        s = dadd(s, dmul(sc, sc));
+      }
+      assign[grow] = I1;
+      cost[grow] = s;
+    } else {
+      unsigned slot = atomicAdd(slowCount, 1u);
+      slowList[slot] = (int32_t)grow;
+    }
+  }
+}
+
 // EuclideanDistanceMeasure.findClosest with statistics, DistanceMeasure.scala:
 // 282-313, for the rows the screen could not decide.
 __global__ void k_assign_exact(const double* __restrict__ X, const double* __restrict__ xnorm,
@@ -609,6 +818,9 @@ __global__ void k_update_centers(double* __restrict__ C, double* __restrict__ cn
 // ------------------------------------------------------------------ plan
 struct cyc_kmeans_plan_s {
   int d = 0, k = 0, d4 = 0, kpad = 0, bm = 0, ldsStride = 0;
+  int variant = 1;          // 2: k_kmeans_assign2 (default when it applies)
+  int ldsStride2 = 0;
+  size_t assignLds2 = 0;
   int64_t max_rows = 0;
   size_t assignLds = 0;
   std::mutex mu;
@@ -640,11 +852,29 @@ int launch_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64
   if (!attr_set) {
     CYC_HIP(hipFuncSetAttribute((const void*)k_kmeans_assign<BM>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_kmeans_assign2<BM, 0>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_kmeans_assign2<BM, 1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_kmeans_assign2<BM, 2>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_kmeans_assign2<BM, 3>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
   const double marginFac = (double)(p->d + 16) * 0x1p-46;
   const int64_t blocks = (n + BM - 1) / BM;
   cyc::KernelTimer timer("k_kmeans_assign", st);
+#define CYC_A2(ABLV)                                                                          \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_kmeans_assign2<BM, ABLV>), dim3((unsigned)blocks), dim3(kAssignThreads), \
+                     p->assignLds2, st, X, xnorm, n, p->d, p->d4, p->ldsStride2,               \
+                     (const double*)p->ct.ptr, C, cnorm, p->k, p->kpad, marginFac, assign, cost, \
+                     (int32_t*)p->slowList.ptr, (unsigned int*)p->slowCount.ptr)
+  if (p->variant == 2) CYC_A2(0);
+  else if (p->variant == 21) CYC_A2(1);
+  else if (p->variant == 22) CYC_A2(2);
+  else if (p->variant == 23) CYC_A2(3);
+  else
   hipLaunchKernelGGL(k_kmeans_assign<BM>, dim3((unsigned)blocks), dim3(kAssignThreads),
                      p->assignLds, st, X, xnorm, n, p->d, p->d4, p->ldsStride,
                      (const double*)p->ct.ptr, C, cnorm, p->k, p->kpad, marginFac, assign, cost,
@@ -747,6 +977,16 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
   p->d4 = (int)cyc::round_up(d, 4);
   p->kpad = (int)cyc::round_up(k, 16);
   p->bm = pick_bm(p->d4, p->ldsStride, p->assignLds);
+  // variant 2: row stride d4 + 1 (== 1 mod 16 doubles: the two 16-lane
+  // halves of a ds_read2_b64 fragment read hit distinct banks)
+  p->ldsStride2 = p->d4 + 1;
+  p->assignLds2 = p->assignLds + sizeof(double) * ((size_t)p->kpad + p->bm) -
+                  sizeof(double) * (size_t)p->bm * (p->ldsStride - p->ldsStride2);
+  p->variant = ((p->d4 % 32) == 0 && p->assignLds2 <= 160 * 1024) ? 2 : 1;
+  if (const char* v = std::getenv("CYC_KMEANS_ASSIGN")) {
+    const int want = std::atoi(v);
+    if (want == 1 || (p->variant == 2 && want >= 21 && want <= 23)) p->variant = want;
+  }
   if (p->bm == 0) {
     delete p;
     cyc::set_error("d > 1240 is not supported by the LDS-resident assign kernel");

@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""A/B the KMeans assign kernel variants in ONE process (interleaved rounds),
+on the BASELINE config 2 shape; checks the variants agree bit for bit.
+usage: python tools/kmeans_ab.py [rows]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
+    d, k = 256, 1024
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(1234)
+    true_c = torch.randn(k, d, generator=g, device=dev, dtype=torch.float64) * 4.0
+    X = torch.empty(n, d, dtype=torch.float64, device=dev)
+    for s in range(0, n, 1 << 20):
+        e = min(n, s + (1 << 20))
+        lab = torch.randint(0, k, (e - s,), generator=g, device=dev)
+        X[s:e] = true_c[lab] + torch.randn(e - s, d, generator=g, device=dev, dtype=torch.float64)
+    xn = row_norms(X)
+    C = X[:k].clone()
+    cn = row_norms(C)
+    plans = {}
+    only = os.environ.get("AB_ONLY")
+    variants = os.environ.get("AB_VARIANTS", "1,2").split(",")
+    for v in ((only,) if only else variants):
+        os.environ["CYC_KMEANS_ASSIGN"] = v
+        plans[v] = KMeansPlan(d, k, n)
+        plans[v].stats(C)
+    outs = {v: (torch.empty(n, dtype=torch.int32, device=dev),
+                torch.empty(n, dtype=torch.float64, device=dev)) for v in plans}
+    N.profile_enable(True)
+    res = {v: [] for v in plans}
+    for rnd in range(4):
+        for v, p in plans.items():
+            N.profile_query("k_kmeans_assign")
+            nex = p.assign(X, xn, C, cn, *outs[v], count_exact=True)
+            torch.cuda.synchronize()
+            ms, cnt = N.profile_query("k_kmeans_assign")
+            if rnd > 0:
+                res[v].append(ms)
+            print(f"round {rnd} variant {v}: {ms:.2f} ms, exact-path rows {nex}", flush=True)
+    for v in res:
+        best = min(res[v])
+        print(f"variant {v}: best {best:.2f} ms = {2.0 * k * d * n / best / 1e9:.1f} TFLOP/s")
+    if only or "1" not in plans or "2" not in plans:
+        return
+    same = all(torch.equal(outs["1"][i], outs["2"][i]) for i in range(2))
+    print("variants bit-identical:", same)
+    sys.exit(0 if same else 1)
+
+
+if __name__ == "__main__":
+    main()
