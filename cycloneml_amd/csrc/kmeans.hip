@@ -832,7 +832,10 @@ namespace {
 
 int pick_bm(int d4, int& stride, size_t& lds) {
   const int cands[3] = {64, 32, 16};
+  int maxbm = 64;
+  if (const char* v = std::getenv("CYC_KMEANS_BM")) maxbm = std::atoi(v);
   for (int bm : cands) {
+    if (bm > maxbm) continue;
     int s = d4 + ((2 - d4 % 32) + 32) % 32;  // stride == 2 (mod 32)
     size_t bytes = ((size_t)bm * s + bm + (size_t)kWaves * bm * 4) * sizeof(double);
     if (bytes <= 160 * 1024) {
