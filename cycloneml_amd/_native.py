@@ -50,6 +50,7 @@ SIGNATURES = {
                                              _vp]),
     "cyc_kmeans_accumulate_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
                                                  _vp, _vp, _vp, _vp]),
+    "cyc_kmeans_last_tiers": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_update_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _f64, _vp, _vp]),
     "cyc_gramian_plan_create": (ctypes.c_int, [_i32, ctypes.POINTER(_vp)]),
     "cyc_gramian_plan_destroy": (ctypes.c_int, [_vp]),
@@ -71,6 +72,22 @@ SIGNATURES = {
                                       ctypes.POINTER(_vp)]),
     "cyc_multinomial_logistic_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp,
                                                               _vp, _vp, _vp, _vp, _vp]),
+    # resident datasets: host pointers
+    "cyc_dataset_dense_create": (ctypes.c_int, [_i32, _i64, ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(_vp)]),
+    "cyc_dataset_csr_create": (ctypes.c_int, [_i32, _i64, _i64, ctypes.c_int, ctypes.c_int,
+                                              ctypes.POINTER(_vp)]),
+    "cyc_dataset_destroy": (ctypes.c_int, [_vp]),
+    "cyc_dataset_rows": (_i64, [_vp]),
+    "cyc_dataset_append_dense": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64]),
+    "cyc_dataset_append_csr": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64]),
+    "cyc_kmeans_iter": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "cyc_logreg_binary_eval": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, _vp,
+                                              _vp, _vp]),
+    "cyc_logreg_multinomial_eval": (ctypes.c_int, [_vp, _i32, _vp, ctypes.c_int, ctypes.c_int,
+                                                   _vp, _vp, _vp, _vp]),
+    "cyc_gramian": (ctypes.c_int, [_vp, _vp, _vp]),
+    "cyc_col_sums": (ctypes.c_int, [_vp, _vp]),
 }
 
 

@@ -59,6 +59,13 @@ class KMeansPlan:
             N.stream_handle(stream)))
         return n_exact.value
 
+    def last_tiers(self):
+        """(rows left to the fp64 screen, rows left to the exact loop) of the
+        last assign(count_exact=True)."""
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(self._lib.cyc_kmeans_last_tiers(self.handle, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
     def accumulate(self, X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, assign=None,
                    cost=None, stream=None):
         N.check(self._lib.cyc_kmeans_accumulate_dev(

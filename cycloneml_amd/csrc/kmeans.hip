@@ -368,7 +368,8 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign2(
     int ldsStride, const double* __restrict__ Ct, const double* __restrict__ C,
     const double* __restrict__ cnorm, int k, int kpad, double marginFac,
     int32_t* __restrict__ assign, double* __restrict__ cost, int32_t* __restrict__ slowList,
-    unsigned int* __restrict__ slowCount) {
+    unsigned int* __restrict__ slowCount, const int32_t* __restrict__ rowList,
+    const unsigned int* __restrict__ rowCount) {
   constexpr int T = BM / 16;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double* Xs = smem;                      // BM x ldsStride
@@ -376,27 +377,31 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign2(
   double* mrg = xnS + BM;                 // kWaves x BM x 4
   double* cnS = mrg + kWaves * BM * 4;    // kpad center norms
   double* xqS = cnS + kpad;               // BM: xn^2 (1 - 2 fac)
+  // Row source: rows row0.. of X (full pass, one block per tile), or the
+  // rows queued in rowList by the bf16 screen (grid-stride over its tiles).
+  const int64_t nsrc = rowList ? (int64_t)*rowCount : n;
+  for (int64_t blk = blockIdx.x; blk * BM < nsrc; blk += gridDim.x) {
+#define CYC_GROW(i) (rowList ? (int64_t)rowList[row0 + (i)] : row0 + (i))
   // Margin M' = 2 fac (|x|^2 + |c|^2) >= fac (|x| + |c|)^2, so the lower bound
   // is L = (xq + cq) - 2 x.c with xq = |x|^2 (1 - 2 fac), cq likewise.
   const double fac2 = 2.0 * marginFac;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR)
-  const int64_t row0 = (int64_t)blockIdx.x * BM;
-  const int rows = (int)min<int64_t>(BM, n - row0);
+  const int64_t row0 = blk * BM;
+  const int rows = (int)min<int64_t>(BM, nsrc - row0);
   {
-    const double* src = X + row0 * d;
     const int total = rows * d;
     for (int e = tid; e < total; e += kAssignThreads) {
       int r = e / d, c = e - r * d;
-      Xs[r * ldsStride + c] = src[e];
+      Xs[r * ldsStride + c] = X[CYC_GROW(r) * d + c];
     }
     for (int e = tid; e < BM * d4; e += kAssignThreads) {
       int r = e / d4, c = e - r * d4;
       if (r >= rows || c >= d) Xs[r * ldsStride + c] = 0.0;
     }
     if (tid < BM) {
-      const double xn = (tid < rows) ? xnorm[row0 + tid] : 0.0;
+      const double xn = (tid < rows) ? xnorm[CYC_GROW(tid)] : 0.0;
       xnS[tid] = xn;
       xqS[tid] = (xn * xn) * (1.0 - fac2);
     }
@@ -532,7 +537,7 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign2(
         I1 = oI1;
       }
     }
-    const int64_t grow = row0 + row;
+    const int64_t grow = CYC_GROW(row);
     bool decided = false;
     if (I1 >= 0 && L1 == L1 && L1 < __builtin_inff()) {
       const double xn = xnS[row], cn = cnS[I1];
@@ -554,6 +559,313 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign2(
       unsigned slot = atomicAdd(slowCount, 1u);
       slowList[slot] = (int32_t)grow;
     }
+  }
+  __syncthreads();   // LDS is restaged by the next tile
+  }
+#undef CYC_GROW
+}
+
+// ---------------------------------------------------- bf16x3 screen (tier 1)
+// Third-generation assign (the default where it fits): the screen's dot
+// products x.c run on the bf16 matrix cores instead of fp64 ones, 32x the
+// MFMA rate, with a rigorous error bound; fp64 only decides.
+//
+// Split every value v (fp64) into v = vh + vl + ev with vh = bf16(v),
+// vl = bf16(v - vh) (the subtraction is exact), |ev| <= 2^-16 |v| (1.0001).
+// Then s = xh.ch + xl.ch + xh.cl (three bf16 products per element, f32
+// accumulation: v_mfma_f32_16x16x32_bf16 over K = 3 d32) satisfies
+//   |x.c - s| <= E = eps (|x|^2 + |c|^2) / 2 + tau,
+//   eps = 3.1 * 2^-16 (split) + 2 * 1.03 * (3 d32 + 64) * 2^-23 (f32 sums of
+//         up to 3 d32 terms, any faithful/directed rounding, 2x headroom)
+//         + 2^-20,
+// using sum|x_i||c_i| <= |x||c| <= (|x|^2 + |c|^2)/2, and tau = 2^-58 for
+// bf16 / f32 underflow (values are capped at |v| <= 2^56: a row with
+// |x| > 2^56 or a NaN goes to the fp64 tier, and a center beyond the cap
+// turns the screen off for the launch).  Lower bound of every distance:
+//   L_j = xq + cq_j - 2 s_j,  xq = |x|^2 (1 - eps) - 2 tau,  cq = |c|^2 (1 - eps),
+// computed with f32 rounding toward -inf (MODE register) so it stays a lower
+// bound; the best center's upper bound is L1 + (2 eps + 2^-20)(|x|^2 + |c|^2)
+// + 4 tau.  A row whose second-smallest lower bound exceeds that is decided
+// exactly as in the fp64 screen (k_kmeans_assign2) and gets the sequential
+// fp64 sqdist; every other row is queued for the fp64 screen.
+//
+// Tiling: 64 rows per workgroup (4 waves, two workgroups per CU), the rows'
+// bf16 hi / lo images in LDS; each wave owns every 4th 16-center tile and
+// streams its centers' pre-split B fragments (1 KiB per wave-load) from L2,
+// TB tiles at a time, each fragment feeding 4 row tiles.
+typedef __bf16 cyc_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float cyc_float4 __attribute__((ext_vector_type(4)));
+
+constexpr int kS3Waves = 4;
+constexpr int kS3Threads = kS3Waves * 64;
+constexpr int kS3BM = 64;
+
+__device__ __forceinline__ void split_bf16(double v, unsigned short& h, unsigned short& l) {
+  const __bf16 hb = (__bf16)(float)v;
+  const double r = v - (double)(float)hb;   // exact: hb is within 2^-8 |v| of v
+  const __bf16 lb = (__bf16)(float)r;
+  h = __builtin_bit_cast(unsigned short, hb);
+  l = __builtin_bit_cast(unsigned short, lb);
+}
+
+// Centers -> B fragments of v_mfma_f32_16x16x32_bf16 (lane l of 16-center tile
+// ct, k-step ks holds centers ct*16 + (l & 15), dims ks*32 + 8 (l >> 4) + 0..7),
+// hi image then lo image per (ct, ks): Cb[((ct KS + ks) 2 + part) 64 + l].
+// cq[c] = |c|^2 (1 - eps) rounded down (+inf for padding); screenOk cleared if
+// a center is beyond the 2^56 cap or not finite.
+__global__ void k_center_split(const double* __restrict__ C, const double* __restrict__ cnorm,
+                               int k, int d, int KS, int ktp, double omE, uint4* __restrict__ Cb,
+                               float* __restrict__ cq, int* __restrict__ screenOk) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)ktp * KS * 64;
+  if (idx < total) {
+    const int lane = (int)(idx & 63);
+    const int64_t t = idx >> 6;
+    const int ks = (int)(t % KS), ct = (int)(t / KS);
+    const int c = ct * 16 + (lane & 15), j0 = ks * 32 + 8 * (lane >> 4);
+    unsigned short h[8], l[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int j = j0 + e;
+      split_bf16((c < k && j < d) ? C[(int64_t)c * d + j] : 0.0, h[e], l[e]);
+    }
+    uint4 ph, pl;
+    ph.x = h[0] | ((unsigned)h[1] << 16); ph.y = h[2] | ((unsigned)h[3] << 16);
+    ph.z = h[4] | ((unsigned)h[5] << 16); ph.w = h[6] | ((unsigned)h[7] << 16);
+    pl.x = l[0] | ((unsigned)l[1] << 16); pl.y = l[2] | ((unsigned)l[3] << 16);
+    pl.z = l[4] | ((unsigned)l[5] << 16); pl.w = l[6] | ((unsigned)l[7] << 16);
+    Cb[((t * 2) + 0) * 64 + lane] = ph;
+    Cb[((t * 2) + 1) * 64 + lane] = pl;
+  }
+  if (idx < (int64_t)ktp * 16) {
+    const int c = (int)idx;
+    if (c < k) {
+      const double cn = cnorm[c];
+      if (!(cn <= 0x1p56)) atomicAnd(screenOk, 0);
+      cq[c] = f_down((cn * cn) * omE);
+    } else {
+      cq[c] = __builtin_inff();
+    }
+  }
+}
+
+template <int TB>
+__global__ __launch_bounds__(kS3Threads, 2) void k_kmeans_assign3(
+    const double* __restrict__ X, const double* __restrict__ xnorm, int64_t n, int d, int KS,
+    const uint4* __restrict__ Cb, const float* __restrict__ cq, int ktp,
+    const int* __restrict__ screenOk, const double* __restrict__ C,
+    const double* __restrict__ cnorm, double omE, double tauL,
+    double facU, double tauU, int32_t* __restrict__ assign, double* __restrict__ cost,
+    int32_t* __restrict__ list, unsigned int* __restrict__ listCount) {
+  constexpr int BM = kS3BM, TA = BM / 16, W = kS3Waves;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem3[];
+  const int SA = KS * 4 + 1;                       // 16-byte chunks per row (+1 pad)
+  uint4* Ah = smem3;                               // BM x SA: bf16 hi image
+  uint4* Al = Ah + BM * SA;                        // BM x SA: bf16 lo image
+  float* mL1 = (float*)(Al + BM * SA);             // W x BM
+  float* mL2 = mL1 + W * BM;                       // W x BM
+  int* mI1 = (int*)(mL2 + W * BM);                 // W x BM
+  float* xqS = (float*)(mI1 + W * BM);             // BM
+  int* exI = (int*)(xqS + BM);                     // BM: decided center or -1
+  double* Xd = (double*)smem3;                     // exact phase: 32 x (d + 1), over Ah/Al
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t row0 = (int64_t)blockIdx.x * BM;
+  const int rows = (int)min<int64_t>(BM, n - row0);
+  if (*screenOk == 0) {
+    if (tid < rows) {
+      const unsigned slot = atomicAdd(listCount, 1u);
+      list[slot] = (int32_t)(row0 + tid);
+    }
+    return;
+  }
+  // Stage: one 8-element chunk per thread-step, split into the two images.
+  const int chunks = KS * 4;
+  for (int e = tid; e < BM * chunks; e += kS3Threads) {
+    const int r = e / chunks, ch = e - r * chunks;
+    const double* src = X + (row0 + r) * d;
+    unsigned short h[8], l[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int j = ch * 8 + q;
+      split_bf16((r < rows && j < d) ? src[j] : 0.0, h[q], l[q]);
+    }
+    uint4 ph, pl;
+    ph.x = h[0] | ((unsigned)h[1] << 16); ph.y = h[2] | ((unsigned)h[3] << 16);
+    ph.z = h[4] | ((unsigned)h[5] << 16); ph.w = h[6] | ((unsigned)h[7] << 16);
+    pl.x = l[0] | ((unsigned)l[1] << 16); pl.y = l[2] | ((unsigned)l[3] << 16);
+    pl.z = l[4] | ((unsigned)l[5] << 16); pl.w = l[6] | ((unsigned)l[7] << 16);
+    Ah[r * SA + ch] = ph;
+    Al[r * SA + ch] = pl;
+  }
+  if (tid < BM) {
+    const double xn = tid < rows ? xnorm[row0 + tid] : 0.0;
+    xqS[tid] = (xn <= 0x1p56) ? f_down((xn * xn) * omE - tauL) : -__builtin_inff();
+  }
+  __syncthreads();
+
+  float sL1[TA * 4], sL2[TA * 4];
+  int sI1[TA * 4];
+#pragma unroll
+  for (int q = 0; q < TA * 4; ++q) {
+    sL1[q] = sL2[q] = __builtin_inff();
+    sI1[q] = -1;
+  }
+  const uint4* ah = Ah + (lane & 15) * SA + (lane >> 4);
+  const uint4* al = Al + (lane & 15) * SA + (lane >> 4);
+  const int groups = ktp / (W * TB);
+  const int total = groups * KS;
+  cyc_float4 acc[TA][TB];
+  uint4 bh0[TB], bl0[TB], bh1[TB], bl1[TB];
+  float cqv[TB];
+
+  // tile tb of group g of this wave: ct = (g TB + tb) W + wave
+#define CYC_LOADB3(BH, BL, I)                                                        \
+  do {                                                                               \
+    const int g_ = (I) / KS, ks_ = (I) - g_ * KS;                                    \
+    _Pragma("unroll") for (int tb = 0; tb < TB; ++tb) {                              \
+      const int ct_ = (g_ * TB + tb) * W + wave;                                     \
+      const uint4* p_ = Cb + ((size_t)(ct_ * KS + ks_) * 2) * 64 + lane;             \
+      BH[tb] = p_[0];                                                                \
+      BL[tb] = p_[64];                                                               \
+    }                                                                                \
+  } while (0)
+#define CYC_COMPUTE3(BH, BL, I)                                                      \
+  do {                                                                               \
+    const int g_ = (I) / KS, ks_ = (I) - g_ * KS;                                    \
+    if (ks_ == 0) {                                                                  \
+      _Pragma("unroll") for (int tb = 0; tb < TB; ++tb) {                            \
+        cqv[tb] = cq[((g_ * TB + tb) * W + wave) * 16 + (lane & 15)];                \
+        _Pragma("unroll") for (int ta = 0; ta < TA; ++ta)                            \
+          acc[ta][tb] = cyc_float4{0.f, 0.f, 0.f, 0.f};                              \
+      }                                                                              \
+    }                                                                                \
+    _Pragma("unroll") for (int ta = 0; ta < TA; ++ta) {                              \
+      const cyc_bf16x8 xh_ = __builtin_bit_cast(cyc_bf16x8, ah[ta * 16 * SA + ks_ * 4]); \
+      const cyc_bf16x8 xl_ = __builtin_bit_cast(cyc_bf16x8, al[ta * 16 * SA + ks_ * 4]); \
+      _Pragma("unroll") for (int tb = 0; tb < TB; ++tb) {                            \
+        const cyc_bf16x8 ch_ = __builtin_bit_cast(cyc_bf16x8, BH[tb]);               \
+        const cyc_bf16x8 cl_ = __builtin_bit_cast(cyc_bf16x8, BL[tb]);               \
+        acc[ta][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh_, ch_, acc[ta][tb], 0, 0, 0); \
+        acc[ta][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xl_, ch_, acc[ta][tb], 0, 0, 0); \
+        acc[ta][tb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xh_, cl_, acc[ta][tb], 0, 0, 0); \
+      }                                                                              \
+    }                                                                                \
+    if (ks_ == KS - 1) {                                                             \
+      _Pragma("unroll") for (int tb = 0; tb < TB; ++tb) {                            \
+        const int c_ = ((g_ * TB + tb) * W + wave) * 16 + (lane & 15);               \
+        _Pragma("unroll") for (int ta = 0; ta < TA; ++ta) {                          \
+          _Pragma("unroll") for (int r = 0; r < 4; ++r) {                            \
+            const int q = 4 * ta + r;                                                \
+            const float L = (xqS[ta * 16 + 4 * (lane >> 4) + r] + cqv[tb]) -         \
+                            2.0f * acc[ta][tb][r];                                   \
+            const bool lt = L < sL1[q];                                              \
+            const float l2 = fminf(sL2[q], L);                                       \
+            sL2[q] = lt ? sL1[q] : l2;                                               \
+            sI1[q] = lt ? c_ : sI1[q];                                               \
+            sL1[q] = lt ? L : sL1[q];                                                \
+          }                                                                          \
+        }                                                                            \
+      }                                                                              \
+    }                                                                                \
+  } while (0)
+  // MODE.FP_ROUND single-precision bits [1:0] = 2 (toward -inf) for the
+  // bounds (and the f32 accumulation, which the error bound allows).
+  __builtin_amdgcn_s_setreg(0x801, 2);
+  if (total > 0) CYC_LOADB3(bh0, bl0, 0);
+  for (int i = 0; i < total; i += 2) {
+    if (i + 1 < total) CYC_LOADB3(bh1, bl1, i + 1);
+    CYC_COMPUTE3(bh0, bl0, i);
+    if (i + 2 < total) CYC_LOADB3(bh0, bl0, i + 2);
+    if (i + 1 < total) CYC_COMPUTE3(bh1, bl1, i + 1);
+  }
+  __builtin_amdgcn_s_setreg(0x801, 0);
+#undef CYC_LOADB3
+#undef CYC_COMPUTE3
+
+  // Reduce each slot over the 16 lanes (columns) that hold the same row.
+#pragma unroll
+  for (int q = 0; q < TA * 4; ++q) {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) {
+      const float oL1 = __shfl_xor(sL1[q], m), oL2 = __shfl_xor(sL2[q], m);
+      const int oI1 = __shfl_xor(sI1[q], m);
+      const float hi = fmaxf(sL1[q], oL1);
+      sL2[q] = fminf(hi, fminf(sL2[q], oL2));
+      const bool take = oL1 < sL1[q] || (oL1 == sL1[q] && oI1 >= 0 && (sI1[q] < 0 || oI1 < sI1[q]));
+      sI1[q] = take ? oI1 : sI1[q];
+      sL1[q] = take ? oL1 : sL1[q];
+    }
+  }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int ta = 0; ta < TA; ++ta) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = 4 * ta + r, row = ta * 16 + 4 * (lane >> 4) + r;
+        mL1[wave * BM + row] = sL1[q];
+        mL2[wave * BM + row] = sL2[q];
+        mI1[wave * BM + row] = sI1[q];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < BM) {
+    const int row = tid;
+    float L1 = __builtin_inff(), L2 = __builtin_inff();
+    int I1 = -1;
+    for (int w = 0; w < W; ++w) {
+      const float oL1 = mL1[w * BM + row], oL2 = mL2[w * BM + row];
+      const int oI1 = mI1[w * BM + row];
+      const float hi = fmaxf(L1, oL1);
+      L2 = fminf(hi, fminf(L2, oL2));
+      if (oL1 < L1 || (oL1 == L1 && oI1 >= 0 && (I1 < 0 || oI1 < I1))) {
+        L1 = oL1;
+        I1 = oI1;
+      }
+    }
+    bool decided = false;
+    if (row < rows && I1 >= 0 && L1 > -__builtin_inff() && L1 < __builtin_inff()) {
+      const double xn = xnorm[row0 + row], cn = cnorm[I1];
+      const double U = (double)L1 + facU * (xn * xn + cn * cn) + tauU;
+      decided = (double)L2 > U;
+    }
+    exI[row] = -1;
+    if (row < rows) {
+      if (decided) {
+        exI[row] = I1;
+      } else {
+        const unsigned slot = atomicAdd(listCount, 1u);
+        list[slot] = (int32_t)(row0 + row);
+      }
+    }
+  }
+  __syncthreads();
+  // Exact phase: the decided rows' sequential fp64 sqdist, 32 rows at a time
+  // staged (coalesced, second read of the tile, from L2 / MALL) over the
+  // images' LDS.
+  for (int half = 0; half < BM / 32; ++half) {
+    const int r0 = half * 32, nr = min(32, rows - r0);
+    if (nr <= 0) break;
+    for (int e = tid; e < nr * d; e += kS3Threads) {
+      const int r = e / d, c = e - r * d;
+      Xd[r * (d + 1) + c] = X[(row0 + r0 + r) * d + c];
+    }
+    __syncthreads();
+    if (tid < nr && exI[r0 + tid] >= 0) {
+      const int I1 = exI[r0 + tid];
+      const double* crow = C + (int64_t)I1 * d;
+      const double* xrow = Xd + tid * (d + 1);
+      double s = 0.0;
+      for (int j = 0; j < d; ++j) {
+        const double sc = dsub(crow[j], xrow[j]);
+        s = dadd(s, dmul(sc, sc));
+      }
+      assign[row0 + r0 + tid] = I1;
+      cost[row0 + r0 + tid] = s;
+    }
+    __syncthreads();
   }
 }
 
@@ -818,9 +1130,17 @@ __global__ void k_update_centers(double* __restrict__ C, double* __restrict__ cn
 // ------------------------------------------------------------------ plan
 struct cyc_kmeans_plan_s {
   int d = 0, k = 0, d4 = 0, kpad = 0, bm = 0, ldsStride = 0;
-  int variant = 1;          // 2: k_kmeans_assign2 (default when it applies)
+  int variant = 1;          // 2: k_kmeans_assign2 (fp64 screen), 3: bf16x3 screen
   int ldsStride2 = 0;
   size_t assignLds2 = 0;
+  // bf16x3 screen (variant 3): k-steps of 32 dims, padded 16-center tiles,
+  // center tiles per wave group, LDS bytes, error-bound constants
+  int ks3 = 0, ktp3 = 0, tb3 = 2;
+  size_t lds3 = 0;
+  double omE3 = 1.0, tauL3 = 0.0, facU3 = 0.0, tauU3 = 0.0;
+  int64_t lastTier2 = 0;    // rows the bf16 screen queued (last counted call)
+  int64_t lastExact = 0;    // rows the fp64 screen queued (last counted call)
+  cyc::DeviceBuffer cb3, cq3, ok3, list3, list3Count;
   int64_t max_rows = 0;
   size_t assignLds = 0;
   std::mutex mu;
@@ -850,7 +1170,8 @@ int pick_bm(int d4, int& stride, size_t& lds) {
 template <int BM>
 int launch_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n,
                   const double* C, const double* cnorm, int32_t* assign, double* cost,
-                  hipStream_t st) {
+                  hipStream_t st, const int32_t* rowList = nullptr,
+                  const unsigned int* rowCount = nullptr) {
   static bool attr_set = false;
   if (!attr_set) {
     CYC_HIP(hipFuncSetAttribute((const void*)k_kmeans_assign<BM>,
@@ -866,14 +1187,15 @@ int launch_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64
     attr_set = true;
   }
   const double marginFac = (double)(p->d + 16) * 0x1p-46;
-  const int64_t blocks = (n + BM - 1) / BM;
-  cyc::KernelTimer timer("k_kmeans_assign", st);
+  // list mode (rows queued by the bf16 screen): persistent grid over the queue
+  const int64_t blocks = rowList ? std::min<int64_t>((n + BM - 1) / BM, 1024) : (n + BM - 1) / BM;
+  cyc::KernelTimer timer(rowList ? "k_kmeans_assign_fp64" : "k_kmeans_assign", st);
 #define CYC_A2(ABLV)                                                                          \
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_kmeans_assign2<BM, ABLV>), dim3((unsigned)blocks), dim3(kAssignThreads), \
                      p->assignLds2, st, X, xnorm, n, p->d, p->d4, p->ldsStride2,               \
                      (const double*)p->ct.ptr, C, cnorm, p->k, p->kpad, marginFac, assign, cost, \
-                     (int32_t*)p->slowList.ptr, (unsigned int*)p->slowCount.ptr)
-  if (p->variant == 2) CYC_A2(0);
+                     (int32_t*)p->slowList.ptr, (unsigned int*)p->slowCount.ptr, rowList, rowCount)
+  if (p->variant == 2 || p->variant == 3) CYC_A2(0);
   else if (p->variant == 21) CYC_A2(1);
   else if (p->variant == 22) CYC_A2(2);
   else if (p->variant == 23) CYC_A2(3);
@@ -903,25 +1225,67 @@ int do_stats(cyc_kmeans_plan p, const double* C, hipStream_t st) {
   return CYC_OK;
 }
 
+template <int TB>
+int launch_assign3(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n,
+                   const double* C, const double* cnorm, int32_t* assign, double* cost,
+                   hipStream_t st) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_kmeans_assign3<TB>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  cyc::KernelTimer timer("k_kmeans_assign", st);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_kmeans_assign3<TB>), dim3((unsigned)((n + kS3BM - 1) / kS3BM)),
+                     dim3(kS3Threads), p->lds3, st, X, xnorm, n, p->d, p->ks3,
+                     (const uint4*)p->cb3.ptr, (const float*)p->cq3.ptr, p->ktp3,
+                     (const int*)p->ok3.ptr, C, cnorm, p->omE3, p->tauL3, p->facU3, p->tauU3,
+                     assign, cost, (int32_t*)p->list3.ptr, (unsigned int*)p->list3Count.ptr);
+  CYC_LAUNCH_CHECK("k_kmeans_assign3");
+  return CYC_OK;
+}
+
 int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n,
               const double* C, const double* cnorm, int32_t* assign, double* cost,
               int64_t* n_exact_out, hipStream_t st) {
   CYC_HIP(hipMemsetAsync(p->slowCount.ptr, 0, sizeof(unsigned int), st));
   int rc = CYC_OK;
+  const int32_t* rowList = nullptr;
+  const unsigned int* rowCount = nullptr;
+  if (p->variant == 3) {
+    // tier 1: bf16x3 screen over every row; undecided rows -> list3
+    CYC_HIP(hipMemsetAsync(p->list3Count.ptr, 0, sizeof(unsigned int), st));
+    CYC_HIP(hipMemsetAsync(p->ok3.ptr, 1, sizeof(int), st));
+    const int64_t tot = (int64_t)p->ktp3 * p->ks3 * 64;
+    hipLaunchKernelGGL(k_center_split, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, C,
+                       cnorm, p->k, p->d, p->ks3, p->ktp3, p->omE3, (uint4*)p->cb3.ptr,
+                       (float*)p->cq3.ptr, (int*)p->ok3.ptr);
+    CYC_LAUNCH_CHECK("k_center_split");
+    rc = p->tb3 == 4 ? launch_assign3<4>(p, X, xnorm, n, C, cnorm, assign, cost, st)
+                     : launch_assign3<2>(p, X, xnorm, n, C, cnorm, assign, cost, st);
+    if (rc) return rc;
+    rowList = (const int32_t*)p->list3.ptr;
+    rowCount = (const unsigned int*)p->list3Count.ptr;
+  }
+  // tier 2: fp64 MFMA screen (every row, or the queued ones)
   switch (p->bm) {
-    case 64: rc = launch_assign<64>(p, X, xnorm, n, C, cnorm, assign, cost, st); break;
-    case 32: rc = launch_assign<32>(p, X, xnorm, n, C, cnorm, assign, cost, st); break;
-    default: rc = launch_assign<16>(p, X, xnorm, n, C, cnorm, assign, cost, st); break;
+    case 64: rc = launch_assign<64>(p, X, xnorm, n, C, cnorm, assign, cost, st, rowList, rowCount); break;
+    case 32: rc = launch_assign<32>(p, X, xnorm, n, C, cnorm, assign, cost, st, rowList, rowCount); break;
+    default: rc = launch_assign<16>(p, X, xnorm, n, C, cnorm, assign, cost, st, rowList, rowCount); break;
   }
   if (rc) return rc;
   // Exact emulation of the reference loop for undecided rows.  The queue
   // length is read back only when the caller asks for it; otherwise a
   // grid-stride launch drains whatever the queue holds without a host sync.
-  unsigned int h_slow = 0;
+  unsigned int h_slow = 0, h_tier2 = 0;
   if (n_exact_out) {
     CYC_HIP(hipMemcpyAsync(&h_slow, p->slowCount.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    if (rowCount)
+      CYC_HIP(hipMemcpyAsync(&h_tier2, rowCount, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     CYC_HIP(hipStreamSynchronize(st));
     *n_exact_out = h_slow;
+    p->lastTier2 = rowCount ? (int64_t)h_tier2 : n;
+    p->lastExact = h_slow;
     if (h_slow) {
       hipLaunchKernelGGL(k_assign_exact, dim3((h_slow + 63) / 64), dim3(64), 0, st, X, xnorm,
                          p->d, C, cnorm, p->k, (const double*)p->stats.ptr,
@@ -944,6 +1308,9 @@ int ensure_rows(cyc_kmeans_plan p, int64_t n) {
   if (n <= p->max_rows && p->slowList.ptr) return CYC_OK;
   int rc;
   if ((rc = p->slowList.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1)))) return rc;
+  if (p->variant == 3 &&
+      (rc = p->list3.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1))))
+    return rc;
   p->max_rows = std::max(p->max_rows, n);
   return CYC_OK;
 }
@@ -986,9 +1353,28 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
   p->assignLds2 = p->assignLds + sizeof(double) * ((size_t)p->kpad + p->bm) -
                   sizeof(double) * (size_t)p->bm * (p->ldsStride - p->ldsStride2);
   p->variant = ((p->d4 % 32) == 0 && p->assignLds2 <= 160 * 1024) ? 2 : 1;
+  // bf16x3 screen in front of the fp64 one where its LDS tile fits
+  p->ks3 = (int)((d + 31) / 32);
+  p->lds3 = (size_t)2 * kS3BM * (p->ks3 * 4 + 1) * 16 + (size_t)kS3Waves * kS3BM * 12 +
+            (size_t)kS3BM * 8;
+  const bool fits3 = p->variant == 2 && p->lds3 <= 160 * 1024;
+  if (fits3) p->variant = 3;
   if (const char* v = std::getenv("CYC_KMEANS_ASSIGN")) {
     const int want = std::atoi(v);
-    if (want == 1 || (p->variant == 2 && want >= 21 && want <= 23)) p->variant = want;
+    if (want == 1 || (p->d4 % 32 == 0 && p->assignLds2 <= 160 * 1024 && want >= 2 && want <= 23 &&
+                      (want != 3 || fits3)))
+      p->variant = want;
+  }
+  if (const char* v = std::getenv("CYC_S3_TB")) p->tb3 = std::atoi(v) == 4 ? 4 : 2;
+  {
+    p->ktp3 = (int)cyc::round_up((k + 15) / 16, kS3Waves * p->tb3);
+    const double d32 = 32.0 * p->ks3;
+    const double eps = 3.1 * 0x1p-16 + 2.0 * 1.03 * (3.0 * d32 + 64.0) * 0x1p-23 + 0x1p-20;
+    const double tau = 0x1p-58;
+    p->omE3 = 1.0 - eps;
+    p->tauL3 = 2.0 * tau;
+    p->facU3 = (2.0 * eps + 0x1p-20) * (1.0 + 0x1p-20);
+    p->tauU3 = 4.0 * tau;
   }
   if (p->bm == 0) {
     delete p;
@@ -996,6 +1382,13 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
     return CYC_ERR_UNSUPPORTED;
   }
   int rc;
+  if (p->variant == 3 &&
+      ((rc = p->cb3.reserve((size_t)p->ktp3 * p->ks3 * 2 * 64 * 16)) ||
+       (rc = p->cq3.reserve(sizeof(float) * (size_t)p->ktp3 * 16)) ||
+       (rc = p->ok3.reserve(64)) || (rc = p->list3Count.reserve(64)))) {
+    delete p;
+    return rc;
+  }
   if ((rc = p->ct.reserve(sizeof(double) * (size_t)p->d4 * p->kpad)) ||
       (rc = p->stats.reserve(sizeof(double) * ((size_t)k * (k + 1) / 2))) ||
       (rc = p->slowCount.reserve(64)) || (rc = ensure_rows(p, std::max<int64_t>(max_rows, 1)))) {
@@ -1003,6 +1396,14 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
     return rc;
   }
   *plan = p;
+  return CYC_OK;
+}
+
+int cyc_kmeans_last_tiers(cyc_kmeans_plan p, int64_t* fp64_screen_rows, int64_t* exact_rows) {
+  CYC_REQUIRE(p != nullptr && fp64_screen_rows && exact_rows, "arguments must not be null");
+  std::lock_guard<std::mutex> g(p->mu);
+  *fp64_screen_rows = p->lastTier2;
+  *exact_rows = p->lastExact;
   return CYC_OK;
 }
 

@@ -88,6 +88,11 @@ int cyc_kmeans_assign_dev(cyc_kmeans_plan plan, const double* X, const double* x
                           const double* C, const double* cnorm, int32_t* assign, double* cost,
                           int64_t* n_exact_out, void* stream);
 
+/* Screening tiers of the last cyc_kmeans_assign_dev call that asked for
+ * n_exact_out: rows the bf16x3 screen left to the fp64 MFMA screen (all rows
+ * when the bf16 screen is off), and rows left to the exact emulation. */
+int cyc_kmeans_last_tiers(cyc_kmeans_plan plan, int64_t* fp64_screen_rows, int64_t* exact_rows);
+
 /* One partition's contribution to a Lloyd iteration: statistics + assign +
  * per-cluster sums.  sums[k*d] += sum of w*x, wsum[k] += sum of w,
  * cost_sum[0] += sum of w*cost.  weights may be NULL (unit weights).
@@ -170,6 +175,55 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan plan, const double*
                                            int64_t n, const double* coef,
                                            const double* scaledMean, double* grad,
                                            double* lossSum, double* weightSum, void* stream);
+
+/* ------------------------------------------- resident datasets (host API) */
+/* Layer 2 for a JVM shim: a library-owned HBM copy of one
+ * partition's rows, appended once from host blocks (an InstanceBlock's
+ * row-major values / CSR arrays, labels and weights, Instance.scala:39-106),
+ * then evaluated per iteration with host-pointer model inputs and
+ * host-pointer aggregator outputs (ADDED to, like `add`).  The calls wrap
+ * the _dev entry points above on the dataset's own stream and return after
+ * the outputs are on the host.  Row norms (KMeans) and the CSC copy (sparse
+ * binary LR) are built on first use and rebuilt after an append.
+ *   cyc_kmeans_iter             KMeans.scala:287-311 (one partition of a Lloyd
+ *                               iteration: statistics, findClosest, sums)
+ *   cyc_logreg_*_eval           RDDLossFunction.scala:56-70's seqOp over the
+ *                               partition's blocks
+ *   cyc_gramian, cyc_col_sums   RowMatrix.scala:130-161, :163-220, :456
+ * Dense datasets serve every entry point; CSR datasets serve the binary
+ * logistic aggregator (others return CYC_ERR_UNSUPPORTED). */
+typedef struct cyc_dataset_s* cyc_dataset;
+
+int cyc_dataset_dense_create(int32_t numFeatures, int64_t capacity_rows, int has_labels,
+                             int has_weights, cyc_dataset* out);
+int cyc_dataset_csr_create(int32_t numFeatures, int64_t capacity_rows, int64_t capacity_nnz,
+                           int has_labels, int has_weights, cyc_dataset* out);
+int cyc_dataset_destroy(cyc_dataset ds);
+int64_t cyc_dataset_rows(cyc_dataset ds);
+/* X: rows x numFeatures row-major.  labels / weights: `rows` doubles, required
+ * iff the dataset was created with them. */
+int cyc_dataset_append_dense(cyc_dataset ds, const double* X, const double* labels,
+                             const double* weights, int64_t rows);
+/* rowptr: rows+1 entries (any base: rowptr[0] is subtracted), colidx in
+ * [0, numFeatures), sorted within a row as in SparseVector. */
+int cyc_dataset_append_csr(cyc_dataset ds, const int64_t* rowptr, const int32_t* colidx,
+                           const double* vals, const double* labels, const double* weights,
+                           int64_t rows);
+
+/* centers: k x d row-major.  sums[k*d] += sum w*x, wsum[k] += sum w,
+ * cost[0] += sum w*cost; assign_opt (may be NULL) receives the rows'
+ * cluster indices. */
+int cyc_kmeans_iter(cyc_dataset ds, const double* centers, int32_t k, double* sums, double* wsum,
+                    double* cost, int32_t* assign_opt);
+int cyc_logreg_binary_eval(cyc_dataset ds, const double* coef, int fitIntercept, int fitWithMean,
+                           const double* scaledMean, double* grad, double* lossSum,
+                           double* weightSum);
+int cyc_logreg_multinomial_eval(cyc_dataset ds, int32_t numClasses, const double* coef,
+                                int fitIntercept, int fitWithMean, const double* scaledMean,
+                                double* grad, double* lossSum, double* weightSum);
+/* U: packed upper n(n+1)/2 (column-major); mean_opt centers the rows. */
+int cyc_gramian(cyc_dataset ds, const double* mean_opt, double* U);
+int cyc_col_sums(cyc_dataset ds, double* sums);
 
 #ifdef __cplusplus
 }

@@ -187,8 +187,7 @@ def test_cblas_dgemm_layouts(cuda, layout):
     m, n, k = 37, 21, 50
     A, B, C = rng.normal(size=(m, k)), rng.normal(size=(k, n)), rng.normal(size=(m, n))
     order = "C" if layout == 101 else "F"
-    a, b, c = (np.ascontiguousarray(M) if order == "C" else np.asfortranarray(M)
-               for M in (A, B, C))
+    a, b, c = (M.copy(order=order) for M in (A, B, C))
     lda, ldb, ldc = (k, n, n) if order == "C" else (m, k, m)
     blas.load().cblas_dgemm(layout, 111, 111, m, n, k, 2.0, a.ctypes.data, lda, b.ctypes.data,
                             ldb, 0.5, c.ctypes.data, ldc)

@@ -1,0 +1,157 @@
+"""Resident-dataset host layer (cyc_dataset_*, cyc_kmeans_iter,
+cyc_logreg_*_eval, cyc_gramian, cyc_col_sums) against the CPU restatement.
+Same bars as the _dev paths: KMeans assignments bit-exact, everything fp64
+within 1e-10 relative."""
+import numpy as np
+import pytest
+
+import oracle
+from cycloneml_amd import _native as N
+from cycloneml_amd.dataset import ResidentDataset
+
+
+def test_dataset_requires_device_or_valid_args():
+    import torch
+    with pytest.raises(N.IllegalArgumentException, match="Number of features"):
+        ResidentDataset.dense(0, 10)
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    with pytest.raises(N.CycloneError) as e:
+        ResidentDataset.dense(4, 10)
+    assert e.value.code == N.CYC_ERR_NO_DEVICE
+
+
+def _rel_close(got, ref, rtol=1e-10):
+    got, ref = np.asarray(got), np.asarray(ref)
+    scale = max(np.abs(ref).max(), 1e-300)
+    np.testing.assert_allclose(got, ref, rtol=rtol, atol=rtol * scale)
+
+
+def _csr(n, F, rng, nnz=8):
+    rp, ci, vv = [0], [], []
+    for _ in range(n):
+        k = int(rng.integers(0, 2 * nnz + 1))
+        cols = np.sort(rng.choice(F, size=min(k, F), replace=False))
+        ci += list(cols)
+        vv += list(rng.uniform(-1, 1, size=cols.size))
+        rp.append(len(ci))
+    return np.array(rp, np.int64), np.array(ci, np.int32), np.array(vv)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("weighted", [False, True])
+def test_kmeans_iter_in_chunks(cuda, weighted):
+    rng = np.random.default_rng(11)
+    n, d, k = 5000, 40, 24
+    X = rng.normal(size=(n, d)) + rng.integers(0, 6, size=(n, 1)) * 3.0
+    w = rng.uniform(0.5, 2.0, size=n) if weighted else None
+    C = X[:k].copy()
+    ds = ResidentDataset.dense(d, n, weights=weighted)
+    for s, e in ((0, 1000), (1000, 1001), (1001, n)):   # three appended blocks
+        ds.append_dense(X[s:e], weights=None if w is None else w[s:e])
+    assert ds.numRows == n
+    sums, wsum, cost, assign = ds.kmeans_iter(C, want_assign=True)
+    ref = oracle.kmeans_iteration(X, oracle.row_norms(X), w, C, oracle.row_norms(C))
+    assert np.array_equal(assign, ref["assign"])
+    _rel_close(sums, ref["sums"])
+    _rel_close(wsum, ref["wsum"])
+    assert abs(cost[0] - ref["cost"]) <= 1e-10 * ref["cost"]
+    # outputs accumulate (aggregator add semantics)
+    ds.kmeans_iter(C, sums, wsum, cost)
+    _rel_close(sums, 2 * ref["sums"])
+    # appending rows invalidates the cached norms
+    X2 = rng.normal(size=(10, d))
+    with pytest.raises(N.IllegalArgumentException, match="capacity exceeded"):
+        ds.append_dense(X2, weights=np.ones(10) if weighted else None)
+
+
+@pytest.mark.gpu
+def test_kmeans_iter_norms_refresh_after_append(cuda):
+    rng = np.random.default_rng(12)
+    n, d, k = 600, 16, 5
+    X = rng.normal(size=(n, d)) * 2
+    C = X[:k].copy()
+    ds = ResidentDataset.dense(d, n)
+    ds.append_dense(X[:300])
+    ds.kmeans_iter(C)
+    ds.append_dense(X[300:])
+    _, _, _, a = ds.kmeans_iter(C, want_assign=True)
+    ref = oracle.kmeans_iteration(X, oracle.row_norms(X), None, C, oracle.row_norms(C))
+    assert np.array_equal(a, ref["assign"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sparse", [False, True])
+@pytest.mark.parametrize("fi,fwm", [(False, False), (True, False), (True, True)])
+def test_binary_eval(cuda, sparse, fi, fwm):
+    rng = np.random.default_rng(21 + fi + 2 * fwm)
+    n, F = 3000, 50
+    y = rng.integers(0, 2, size=n).astype(np.float64)
+    w = rng.uniform(0.1, 2.0, size=n)
+    coef = rng.normal(size=F + (1 if fi else 0)) * 0.3
+    sm = rng.normal(size=F) * 0.1 if fwm else None
+    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+    if sparse:
+        rp, ci, vv = _csr(n, F, rng)
+        ds = ResidentDataset.csr(F, n, ci.size, labels=True, weights=True)
+        h = n // 2
+        ds.append_csr(rp[:h + 1], ci[:rp[h]], vv[:rp[h]], y[:h], w[:h])
+        ds.append_csr(rp[h:], ci[rp[h]:], vv[rp[h]:], y[h:], w[h:])  # rowptr base rp[h]
+        blk = dict(labels=y, weights=w, rowptr=rp, colidx=ci, values=vv, F=F)
+    else:
+        X = rng.normal(size=(n, F))
+        ds = ResidentDataset.dense(F, n, labels=True, weights=True).append_dense(X, y, w)
+        blk = dict(labels=y, weights=w, X=X)
+    oracle.binary_logistic_add(blk, coef, fi, fwm, sm, st)
+    grad, lw = ds.binary_logistic_eval(coef, fi, fwm, sm)
+    _rel_close(grad, st["grad"])
+    assert abs(lw[0] - st["loss"]) <= 1e-10 * abs(st["loss"])
+    assert abs(lw[1] - st["weight"]) <= 1e-12 * st["weight"]
+    g2, _ = ds.binary_logistic_eval(coef, fi, fwm, sm)
+    assert np.array_equal(g2, grad)  # deterministic run to run
+
+
+@pytest.mark.gpu
+def test_multinomial_eval(cuda):
+    rng = np.random.default_rng(31)
+    n, F, C = 2000, 48, 7
+    X = rng.normal(size=(n, F))
+    y = rng.integers(0, C, size=n).astype(np.float64)
+    coef = rng.normal(size=C * F + C) / np.sqrt(F)
+    sm = rng.normal(size=F) * 0.1
+    ds = ResidentDataset.dense(F, n, labels=True).append_dense(X, y)
+    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+    oracle.multinomial_logistic_add(dict(labels=y, weights=None, X=X), coef, C, True, True, sm,
+                                    st)
+    grad, lw = ds.multinomial_logistic_eval(C, coef, True, True, sm)
+    _rel_close(grad, st["grad"])
+    assert abs(lw[0] - st["loss"]) <= 1e-10 * abs(st["loss"])
+    assert lw[1] == st["weight"]
+
+
+@pytest.mark.gpu
+def test_gramian_and_col_sums(cuda):
+    rng = np.random.default_rng(41)
+    n, F = 1500, 70
+    X = rng.uniform(size=(n, F))
+    ds = ResidentDataset.dense(F, n).append_dense(X)
+    _rel_close(ds.gramian(), oracle.gramian_partition(X))
+    mean = X.mean(axis=0)
+    _rel_close(ds.gramian(mean=mean), oracle.gramian_partition(X, mean))
+    _rel_close(ds.col_sums(), X.sum(axis=0), rtol=1e-12)
+
+
+@pytest.mark.gpu
+def test_dataset_errors(cuda):
+    ds = ResidentDataset.csr(5, 4, 8, labels=True)
+    with pytest.raises(N.IllegalArgumentException, match="out of range"):
+        ds.append_csr(np.array([0, 1]), np.array([5]), np.array([1.0]), np.zeros(1))
+    with pytest.raises(N.IllegalArgumentException, match="labels must not be null"):
+        ds.append_csr(np.array([0, 1]), np.array([1]), np.array([1.0]))
+    ds.append_csr(np.array([0, 1]), np.array([1]), np.array([1.0]), np.zeros(1))
+    with pytest.raises(N.CycloneError) as e:
+        ds.kmeans_iter(np.ones((2, 5)))
+    assert e.value.code == N.CYC_ERR_UNSUPPORTED
+    dd = ResidentDataset.dense(3, 2)
+    with pytest.raises(N.IllegalArgumentException, match="holds no labels"):
+        dd.binary_logistic_eval(np.zeros(3), False)

@@ -229,3 +229,80 @@ def test_full_config_properties(cuda):
     for i in range(len(rows)):
         idx, dist = oracle.find_closest_stats(Ch, chn, stats, Xs[i], oracle.norm2(Xs[i]))
         assert (idx, dist) == (int(ah[i]), float(ch[i]))
+
+
+def _assign_variant(X, C, cuda, variant, monkeypatch):
+    """Assign through a plan built with CYC_KMEANS_ASSIGN=variant; returns
+    (assign, cost, fp64-screen rows, exact rows)."""
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    monkeypatch.setenv("CYC_KMEANS_ASSIGN", str(variant))
+    Xd, Cd = _dev(X, cuda), _dev(C, cuda)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = KMeansPlan(X.shape[1], C.shape[0], X.shape[0])
+    p.stats(Cd)
+    a = torch.empty(X.shape[0], dtype=torch.int32, device=cuda)
+    c = torch.empty(X.shape[0], dtype=torch.float64, device=cuda)
+    n_exact = p.assign(Xd, xn, Cd, cn, a, c, count_exact=True)
+    torch.cuda.synchronize()
+    t2, ex = p.last_tiers()
+    assert ex == n_exact
+    return a.cpu().numpy(), c.cpu().numpy(), t2, ex
+
+
+@pytest.mark.parametrize("n,d,k", [(4000, 32, 7), (3000, 64, 130), (2000, 256, 300),
+                                   (1000, 96, 1), (700, 512, 40), (5000, 128, 1024)])
+def test_bf16_screen_matches_fp64_screen(cuda, monkeypatch, n, d, k):
+    """Tier 1 (bf16x3 screen) + tier 2 (fp64 screen on its leftovers) equals
+    the fp64 screen alone and the restatement, bit for bit; on separated
+    clusters the bf16 screen decides most rows."""
+    rng = np.random.default_rng(n + 3 * d + k)
+    true_c = rng.normal(scale=4.0, size=(max(k, 1), d))
+    X = true_c[rng.integers(0, true_c.shape[0], n)] + rng.normal(size=(n, d))
+    C = true_c + rng.normal(scale=0.1, size=true_c.shape)
+    a3, c3, t2, _ = _assign_variant(X, C, cuda, 3, monkeypatch)
+    a2, c2, t2b, _ = _assign_variant(X, C, cuda, 2, monkeypatch)
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a3, ra)
+    np.testing.assert_array_equal(c3, rc)
+    np.testing.assert_array_equal(a2, a3)
+    np.testing.assert_array_equal(c2, c3)
+    assert t2b == n                      # variant 2: every row through the fp64 screen
+    assert t2 <= max(n // 20, 5), t2     # separated clusters: bf16 decides >= 95%
+
+
+def test_bf16_screen_hard_cases(cuda, monkeypatch):
+    """Near ties, duplicate centers, huge rows (> 2^56), tiny-scale rows and
+    NaN / Inf rows fall through the bf16 screen to the fp64 screen / exact
+    loop and still match the reference."""
+    rng = np.random.default_rng(17)
+    d, k = 64, 20
+    C = rng.normal(scale=3.0, size=(k, d))
+    C[7] = C[3]                                           # duplicate center
+    X = np.vstack([
+        C[rng.integers(0, k, 800)] + rng.normal(size=(800, d)),
+        0.5 * (C[0] + C[1]) + rng.normal(scale=1e-9, size=(40, d)),   # near ties
+        C[rng.integers(0, k, 30)] * 1e18,                 # |x| > 2^56
+        C[rng.integers(0, k, 30)] * 1e-30,                # bf16 underflow scale
+        C[:5] + 1e-14,
+    ])
+    X[805, 2] = np.nan
+    X[806, 0] = -np.inf
+    a3, c3, t2, ex = _assign_variant(X, C, cuda, 3, monkeypatch)
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a3, ra)
+    np.testing.assert_array_equal(c3, rc)
+    assert t2 >= 100 and ex > 0
+
+
+def test_bf16_screen_off_for_huge_center(cuda, monkeypatch):
+    rng = np.random.default_rng(19)
+    d, k, n = 32, 9, 1500
+    C = rng.normal(size=(k, d))
+    C[4] *= 1e20                                          # |c| > 2^56: screen off
+    X = rng.normal(size=(n, d)) * 2
+    a3, c3, t2, _ = _assign_variant(X, C, cuda, 3, monkeypatch)
+    assert t2 == n
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a3, ra)
+    np.testing.assert_array_equal(c3, rc)
