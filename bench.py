@@ -111,6 +111,13 @@ class KMeansWorkload:
         self.C = self.C0.clone()
         self.cnorm = row_norms(self.C)
         self.plan = KMeansPlan(d, k, n)
+        # per-fit row image (int8 limbs, 3 B/element): built once before the
+        # Lloyd loop like the cached norms (KMeans.scala:263-270), untimed
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        self.rows = self.plan.rows(X)
+        torch.cuda.synchronize()
+        self.prep_ms = (time.perf_counter() - t0) * 1e3
         self.buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=dev)
         self.conv = torch.zeros(1, dtype=torch.int32, device=dev)
         self.parallel = parallel
@@ -120,7 +127,8 @@ class KMeansWorkload:
         buf = self.buf
         sums, wsum, cost = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
         buf.zero_()
-        self.plan.accumulate(self.X, self.xnorm, None, self.C, self.cnorm, sums, wsum, cost)
+        self.plan.accumulate(self.X, self.xnorm, None, self.C, self.cnorm, sums, wsum, cost,
+                             rows=self.rows)
         self.parallel.allreduce_(buf)
         self.plan.update(self.C, self.cnorm, sums, wsum, 1e-4, self.conv)
 

@@ -46,10 +46,13 @@ SIGNATURES = {
     "cyc_kmeans_plan_create": (ctypes.c_int, [_i32, _i32, _i64, ctypes.POINTER(_vp)]),
     "cyc_kmeans_plan_destroy": (ctypes.c_int, [_vp]),
     "cyc_kmeans_stats_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
-    "cyc_kmeans_assign_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _pi64,
-                                             _vp]),
-    "cyc_kmeans_accumulate_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
-                                                 _vp, _vp, _vp, _vp]),
+    "cyc_kmeans_assign_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
+                                             _pi64, _vp]),
+    "cyc_kmeans_accumulate_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                                 _vp, _vp, _vp, _vp, _vp]),
+    "cyc_kmeans_rows_create": (ctypes.c_int, [_vp, _vp, _i64, _vp, ctypes.POINTER(_vp)]),
+    "cyc_kmeans_rows_destroy": (ctypes.c_int, [_vp]),
+    "cyc_kmeans_rows_bytes": (_i64, [_vp]),
     "cyc_kmeans_last_tiers": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_update_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _f64, _vp, _vp]),
     "cyc_gramian_plan_create": (ctypes.c_int, [_i32, ctypes.POINTER(_vp)]),

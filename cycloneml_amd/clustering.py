@@ -51,12 +51,18 @@ class KMeansPlan:
                                                N.stream_handle(stream)))
         return out
 
-    def assign(self, X, xnorm, C, cnorm, assign, cost, stream=None, count_exact=False):
+    def rows(self, X, stream=None):
+        """Per-fit row image of X for the exact-integer i8 screen (built once,
+        like the norms KMeans.scala:263-270 caches); X must stay unchanged."""
+        return KMeansRows(self, X, stream)
+
+    def assign(self, X, xnorm, C, cnorm, assign, cost, stream=None, count_exact=False,
+               rows=None):
         n_exact = ctypes.c_int64(0)
         N.check(self._lib.cyc_kmeans_assign_dev(
-            self.handle, N.ptr(X), N.ptr(xnorm), int(X.shape[0]), N.ptr(C), N.ptr(cnorm),
-            N.ptr(assign), N.ptr(cost), ctypes.byref(n_exact) if count_exact else None,
-            N.stream_handle(stream)))
+            self.handle, N.ptr(X), N.ptr(xnorm), _rows_handle(rows), int(X.shape[0]), N.ptr(C),
+            N.ptr(cnorm), N.ptr(assign), N.ptr(cost),
+            ctypes.byref(n_exact) if count_exact else None, N.stream_handle(stream)))
         return n_exact.value
 
     def last_tiers(self):
@@ -67,16 +73,48 @@ class KMeansPlan:
         return a.value, b.value
 
     def accumulate(self, X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, assign=None,
-                   cost=None, stream=None):
+                   cost=None, stream=None, rows=None):
         N.check(self._lib.cyc_kmeans_accumulate_dev(
-            self.handle, N.ptr(X), N.ptr(xnorm), N.ptr(weights), int(X.shape[0]), N.ptr(C),
-            N.ptr(cnorm), N.ptr(sums), N.ptr(wsum), N.ptr(cost_sum), N.ptr(assign), N.ptr(cost),
-            N.stream_handle(stream)))
+            self.handle, N.ptr(X), N.ptr(xnorm), _rows_handle(rows), N.ptr(weights),
+            int(X.shape[0]), N.ptr(C), N.ptr(cnorm), N.ptr(sums), N.ptr(wsum), N.ptr(cost_sum),
+            N.ptr(assign), N.ptr(cost), N.stream_handle(stream)))
 
     def update(self, C, cnorm, sums, wsum, epsilon, converged, stream=None):
         N.check(self._lib.cyc_kmeans_update_dev(self.handle, N.ptr(C), N.ptr(cnorm), N.ptr(sums),
                                                 N.ptr(wsum), float(epsilon), N.ptr(converged),
                                                 N.stream_handle(stream)))
+
+
+class KMeansRows:
+    """RAII wrapper of cyc_kmeans_rows: the int8 three-limb image of a fixed
+    row block (3 bytes per element), built once per fit."""
+
+    def __init__(self, plan: KMeansPlan, X, stream=None):
+        self._lib = N.load()
+        h = ctypes.c_void_p()
+        N.check(self._lib.cyc_kmeans_rows_create(plan.handle, N.ptr(X), int(X.shape[0]),
+                                                 N.stream_handle(stream), ctypes.byref(h)))
+        self.handle = h
+        self.X = X            # keeps the rows alive while the image is in use
+
+    @property
+    def nbytes(self):
+        return int(self._lib.cyc_kmeans_rows_bytes(self.handle)) if self.handle else 0
+
+    def close(self):
+        if self.handle:
+            self._lib.cyc_kmeans_rows_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _rows_handle(rows):
+    return None if rows is None else rows.handle
 
 
 def row_norms(X, out=None, stream=None):
@@ -165,6 +203,7 @@ class KMeans:
         if xnorm is None:
             xnorm = row_norms(X, stream=stream)
         plan = KMeansPlan(d, k, n)
+        rows = plan.rows(X, stream=stream)     # once per fit, like the cached norms
         C = torch.from_numpy(self.initialModel.clusterCenters.copy()).to(dev)
         parallel.broadcast_(C)             # bcCenters (KMeans.scala:276)
         cnorm = row_norms(C, stream=stream)
@@ -174,7 +213,8 @@ class KMeans:
         iteration, converged, cost = 0, False, 0.0
         while iteration < self.maxIterations and not converged:
             buf.zero_()
-            plan.accumulate(X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, stream=stream)
+            plan.accumulate(X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, stream=stream,
+                            rows=rows)
             parallel.allreduce_(buf)       # reduceByKey + collectAsMap + costAccum
             plan.update(C, cnorm, sums, wsum, self.epsilon, converged_t, stream=stream)
             converged = bool(converged_t.item())
@@ -182,5 +222,6 @@ class KMeans:
             if iteration_callback:
                 iteration_callback(iteration, cost)
             iteration += 1
+        rows.close()
         plan.close()
         return KMeansModel(C.cpu().numpy(), cost, iteration)

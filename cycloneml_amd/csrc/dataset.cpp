@@ -44,6 +44,7 @@ struct cyc_dataset_s {
   // derived
   cyc::DeviceBuffer xnorm;
   bool xnorm_ok = false;
+  std::map<int, cyc_kmeans_rows> krows;   // per-plan row image (built on first use)
   cyc_csc csc = nullptr;
   // plans
   std::map<int, cyc_kmeans_plan> kplans;
@@ -54,6 +55,7 @@ struct cyc_dataset_s {
   std::vector<int64_t> rp_tmp;
 
   ~cyc_dataset_s() {
+    for (auto& kv : krows) cyc_kmeans_rows_destroy(kv.second);
     for (auto& kv : kplans) cyc_kmeans_plan_destroy(kv.second);
     for (auto& kv : lplans) cyc_logistic_plan_destroy(kv.second);
     if (gplan) cyc_gramian_plan_destroy(gplan);
@@ -62,6 +64,8 @@ struct cyc_dataset_s {
   }
   void invalidate() {
     xnorm_ok = false;
+    for (auto& kv : krows) cyc_kmeans_rows_destroy(kv.second);
+    krows.clear();
     if (csc) {
       cyc_csc_destroy(csc);
       csc = nullptr;
@@ -265,6 +269,15 @@ int cyc_kmeans_iter(cyc_dataset ds, const double* centers, int32_t k, double* su
     ds->kplans[k] = plan;
   }
   if (int rc = ensure_norms(ds)) return rc;
+  cyc_kmeans_rows img;
+  auto ri = ds->krows.find(k);
+  if (ri != ds->krows.end()) {
+    img = ri->second;
+  } else {
+    if (int rc = cyc_kmeans_rows_create(plan, (const double*)ds->X.ptr, ds->rows, ds->st, &img))
+      return rc;
+    ds->krows[k] = img;
+  }
   const size_t kd = (size_t)k * ds->F;
   double *dC, *dCn, *dS, *dW;
   int rc;
@@ -281,7 +294,7 @@ int cyc_kmeans_iter(cyc_dataset ds, const double* centers, int32_t k, double* su
     dA = (int32_t*)ds->in2.ptr;
   }
   if ((rc = cyc_kmeans_accumulate_dev(plan, (const double*)ds->X.ptr, (const double*)ds->xnorm.ptr,
-                                      ds->has_weights ? (const double*)ds->weights.ptr : nullptr,
+                                      img, ds->has_weights ? (const double*)ds->weights.ptr : nullptr,
                                       ds->rows, dC, dCn, dS, dW, dS + kd, dA, nullptr, ds->st)))
     return rc;
   if ((rc = download(sums, dS, kd, ds->st)) || (rc = download(wsum, dW, k, ds->st)) ||

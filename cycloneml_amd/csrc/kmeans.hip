@@ -34,6 +34,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "kmeans_i8.hpp"
 
 namespace {
 
@@ -332,16 +333,20 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
     }
     const int64_t grow = row0 + row;
     if (S.I1 >= 0 && S.L2 > S.U1) {
-      // Exact fastSquaredDistance(centers(I1), point) = Vectors.sqdist(c, x).
-      const double* crow = C + (int64_t)S.I1 * d;
-      const double* xrow = Xs + row * ldsStride;
-      double s = 0.0;
-      for (int j = 0; j < d; ++j) {
-        double sc = dsub(crow[j], xrow[j]);
-        s = dadd(s, dmul(sc, sc));
+      // Exact fastSquaredDistance(centers(I1), point) = Vectors.sqdist(c, x)
+      // (when the caller wants per-row costs; the Lloyd path computes them
+      // in k_chunk_sums).
+      if (cost) {
+        const double* crow = C + (int64_t)S.I1 * d;
+        const double* xrow = Xs + row * ldsStride;
+        double s = 0.0;
+        for (int j = 0; j < d; ++j) {
+          double sc = dsub(crow[j], xrow[j]);
+          s = dadd(s, dmul(sc, sc));
+        }
+        cost[grow] = s;
       }
       assign[grow] = S.I1;
-      cost[grow] = s;
     } else {
       unsigned slot = atomicAdd(slowCount, 1u);
       slowList[slot] = (int32_t)grow;
@@ -546,15 +551,17 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign2(
       decided = (double)L2 > U;
     }
     if (decided) {
-      const double* crow = C + (int64_t)I1 * d;
-      const double* xrow = Xs + row * ldsStride;
-      double s = 0.0;
-      for (int j = 0; j < d; ++j) {
-        double sc = dsub(crow[j], xrow[j]);
-        s = dadd(s, dmul(sc, sc));
+      if (cost) {
+        const double* crow = C + (int64_t)I1 * d;
+        const double* xrow = Xs + row * ldsStride;
+        double s = 0.0;
+        for (int j = 0; j < d; ++j) {
+          double sc = dsub(crow[j], xrow[j]);
+          s = dadd(s, dmul(sc, sc));
+        }
+        cost[grow] = s;
       }
       assign[grow] = I1;
-      cost[grow] = s;
     } else {
       unsigned slot = atomicAdd(slowCount, 1u);
       slowList[slot] = (int32_t)grow;
@@ -842,6 +849,10 @@ __global__ __launch_bounds__(kS3Threads, 2) void k_kmeans_assign3(
     }
   }
   __syncthreads();
+  if (!cost) {
+    if (tid < rows && exI[tid] >= 0) assign[row0 + tid] = exI[tid];
+    return;
+  }
   // Exact phase: the decided rows' sequential fp64 sqdist, 32 rows at a time
   // staged (coalesced, second read of the tile, from L2 / MALL) over the
   // images' LDS.
@@ -870,44 +881,71 @@ __global__ __launch_bounds__(kS3Threads, 2) void k_kmeans_assign3(
 }
 
 // EuclideanDistanceMeasure.findClosest with statistics, DistanceMeasure.scala:
-// 282-313, for the rows the screen could not decide.
-__global__ void k_assign_exact(const double* __restrict__ X, const double* __restrict__ xnorm,
-                               int d, const double* __restrict__ C,
-                               const double* __restrict__ cnorm, int k,
-                               const double* __restrict__ stats,
-                               const int32_t* __restrict__ slowList,
-                               const unsigned int* __restrict__ slowCount,
-                               int32_t* __restrict__ assign, double* __restrict__ cost) {
+// 282-313, for the rows the screens could not decide.  One wave per queued row.
+// The reference loop visits centers in order; its state (bestDistance,
+// bestIndex) changes only at an update, so the wave evaluates 64 consecutive
+// centers at once against the current state: every lane whose center the
+// loop would visit computes the exact sequential sqdist (Vectors.scala:580-587,
+// the same operation order as the reference), a ballot finds the first lane
+// whose visit changes the state (a `return` at :303 or an update at :304-306),
+// the state advances to it, and the lanes after it are re-evaluated against
+// the new state (reusing the distances already computed).  Lanes before the
+// first event have no side effect in the reference either, so the returned
+// (index, distance) is the reference's, bit for bit; distances of centers the
+// reference would not visit may be computed speculatively and are discarded.
+__global__ __launch_bounds__(256) void k_assign_exact(
+    const double* __restrict__ X, const double* __restrict__ xnorm, int d,
+    const double* __restrict__ C, const double* __restrict__ cnorm, int k,
+    const double* __restrict__ stats, const int32_t* __restrict__ slowList,
+    const unsigned int* __restrict__ slowCount, int32_t* __restrict__ assign,
+    double* __restrict__ cost) {
   const unsigned cnt = *slowCount;
-  for (unsigned idx = blockIdx.x * blockDim.x + threadIdx.x; idx < cnt;
-       idx += gridDim.x * blockDim.x) {
-  const int64_t r = slowList[idx];
-  const double* x = X + r * d;
-  const double xn = xnorm[r];
-  double best = seq_sqdist(C, x, d);
-  int bestIndex = 0;
-  if (!(best < stats[0])) {
-    for (int i = 1; i < k; ++i) {
-      double normDiff = dsub(cnorm[i], xn);
-      double lowerBound = dmul(normDiff, normDiff);
-      if (lowerBound < best) {
-        if (stats[iut(i, bestIndex)] < best) {
-          double dd = seq_sqdist(C + (int64_t)i * d, x, d);
-          if (dd < stats[iut(i, i)]) {
-            best = dd;
-            bestIndex = i;
-            break;
-          }
-          if (dd < best) {
-            best = dd;
-            bestIndex = i;
-          }
+  const int lane = threadIdx.x & 63;
+  const unsigned wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const unsigned nw = (gridDim.x * blockDim.x) >> 6;
+  for (unsigned idx = wid; idx < cnt; idx += nw) {
+    const int64_t r = slowList[idx];
+    const double* x = X + r * d;
+    const double xn = xnorm[r];
+    double best = seq_sqdist(C, x, d);          // :286, uniform across the wave
+    int bi = 0;
+    bool done = best < stats[0];                // :287
+    for (int i0 = 1; !done && i0 < k; i0 += 64) {
+      const int i = i0 + lane;
+      const bool valid = i < k;
+      double lb = __builtin_inf(), sii = 0.0;
+      if (valid) {
+        const double nd = dsub(cnorm[i], xn);     // :294-295
+        lb = dmul(nd, nd);
+        sii = stats[iut(i, i)];
+      }
+      double dd = 0.0;
+      bool have = false;
+      int pos = 0;
+      for (;;) {
+        const bool visit = valid && lane >= pos && lb < best && stats[iut(i, bi)] < best;
+        if (visit && !have) {
+          dd = seq_sqdist(C + (int64_t)i * d, x, d);
+          have = true;
         }
+        const bool brk = visit && dd < sii;
+        const bool ev = visit && (brk || dd < best);
+        const unsigned long long m = __ballot(ev);
+        if (!m) break;
+        const int f = __ffsll((long long)m) - 1;
+        best = __shfl(dd, f);
+        bi = i0 + f;
+        if (__shfl((int)brk, f)) {
+          done = true;
+          break;
+        }
+        pos = f + 1;
       }
     }
-  }
-  assign[r] = bestIndex;
-  cost[r] = best;
+    if (lane == 0) {
+      assign[r] = bi;
+      if (cost) cost[r] = best;
+    }
   }
 }
 
@@ -1009,16 +1047,99 @@ __global__ void k_scatter(const int32_t* __restrict__ assign, int64_t n, int k,
   }
 }
 
-// Partial sums of up to kChunkRows rows of one cluster, rows in index order.
-__global__ void k_chunk_sums(const double* __restrict__ X, int d, const double* __restrict__ w,
-                             const double* __restrict__ cost, const int32_t* __restrict__ perm,
-                             const int64_t* __restrict__ cstart,
-                             const int64_t* __restrict__ chunkStart, int k,
-                             double* __restrict__ part, double* __restrict__ pw,
-                             double* __restrict__ pc) {
+// Partial sums of up to kChunkRows rows of one cluster, rows in index order
+// (updateClusterSum, DistanceMeasure.scala:189-191: axpy(w, x, sum)), their
+// weights, and each row's cost = fastSquaredDistance(center, row) = the
+// sequential Vectors.sqdist (Vectors.scala:580-587) that findClosest returns
+// for the chosen center, summed as w * cost (KMeans.scala:302) in row order.
+// The cost is fused here because the rows are read anyway: thread j holds
+// dims j, j+256, ... (NJ of them) and writes (c_j - x_j)^2 of G rows to LDS;
+// G threads then run the G sequential sums.  costOut (may be NULL) receives
+// the per-row costs.
+template <int NJ>
+__global__ __launch_bounds__(256) void k_chunk_sums(
+    const double* __restrict__ X, int d, const double* __restrict__ w,
+    const double* __restrict__ C, const int32_t* __restrict__ perm,
+    const int64_t* __restrict__ cstart, const int64_t* __restrict__ chunkStart, int k,
+    double* __restrict__ part, double* __restrict__ pw, double* __restrict__ pc,
+    double* __restrict__ costOut) {
+  constexpr int G = 16;
+  __shared__ double sq[G * (NJ * 256 + 1)];
+  __shared__ double rcost[G];
   const int64_t ch = blockIdx.x;
   if (ch >= chunkStart[k]) return;
-  // cluster = last c with chunkStart[c] <= ch (binary search, k+1 entries)
+  int lo = 0, hi = k;   // cluster = last c with chunkStart[c] <= ch
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (chunkStart[mid] <= ch) lo = mid; else hi = mid;
+  }
+  const int c = lo;
+  const int64_t first = cstart[c] + (ch - chunkStart[c]) * kChunkRows;
+  const int64_t last = min<int64_t>(cstart[c + 1], first + kChunkRows);
+  const int tid = threadIdx.x;
+  constexpr int SQS = NJ * 256 + 1;
+  double s[NJ], cj[NJ];
+#pragma unroll
+  for (int q = 0; q < NJ; ++q) {
+    const int j = tid + 256 * q;
+    s[q] = 0.0;
+    cj[q] = j < d ? C[(int64_t)c * d + j] : 0.0;
+  }
+  double sw = 0.0, sc = 0.0;
+  for (int64_t g0 = first; g0 < last; g0 += G) {
+    const int gn = (int)min<int64_t>(G, last - g0);
+    for (int pp = 0; pp < gn; ++pp) {
+      const int64_t r = perm[g0 + pp];
+      const double wr = w ? w[r] : 1.0;
+#pragma unroll
+      for (int q = 0; q < NJ; ++q) {
+        const int j = tid + 256 * q;
+        if (j < d) {
+          const double x = X[r * d + j];
+          s[q] = w ? dadd(s[q], dmul(wr, x)) : dadd(s[q], x);
+          const double df = dsub(cj[q], x);
+          sq[pp * SQS + j] = dmul(df, df);
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < gn) {
+      double t = 0.0;
+      for (int j = 0; j < d; ++j) t = dadd(t, sq[tid * SQS + j]);
+      rcost[tid] = t;
+      if (costOut) costOut[perm[g0 + tid]] = t;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int pp = 0; pp < gn; ++pp) {
+        const double wt = w ? w[perm[g0 + pp]] : 1.0;
+        sw = dadd(sw, wt);
+        sc = dadd(sc, dmul(rcost[pp], wt));
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NJ; ++q) {
+    const int j = tid + 256 * q;
+    if (j < d) part[ch * d + j] = s[q];
+  }
+  if (tid == 0) {
+    pw[ch] = sw;
+    pc[ch] = sc;
+  }
+}
+
+// Same without the fused cost (d > 1024): costs come from k_row_cost.
+__global__ void k_chunk_sums_nocost(const double* __restrict__ X, int d,
+                                    const double* __restrict__ w,
+                                    const double* __restrict__ cost,
+                                    const int32_t* __restrict__ perm,
+                                    const int64_t* __restrict__ cstart,
+                                    const int64_t* __restrict__ chunkStart, int k,
+                                    double* __restrict__ part, double* __restrict__ pw,
+                                    double* __restrict__ pc) {
+  const int64_t ch = blockIdx.x;
+  if (ch >= chunkStart[k]) return;
   int lo = 0, hi = k;
   while (hi - lo > 1) {
     int mid = (lo + hi) >> 1;
@@ -1050,6 +1171,35 @@ __global__ void k_chunk_sums(const double* __restrict__ X, int d, const double* 
     pw[ch] = sw;
     pc[ch] = sc;
   }
+}
+
+// cost[r] = Vectors.sqdist(C[assign[r]], X[r]) (Vectors.scala:580-587): the
+// distance findClosest returns for the chosen center.  64-row tiles staged
+// through LDS 8 columns at a time (coalesced), one lane per row.
+__global__ void k_row_cost(const double* __restrict__ X, int64_t n, int d,
+                           const double* __restrict__ C, const int32_t* __restrict__ assign,
+                           double* __restrict__ cost) {
+  __shared__ double tile[64][9];
+  const int lane = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * 64;
+  const int64_t myr = row0 + lane;
+  const double* crow = myr < n ? C + (int64_t)assign[myr] * d : C;
+  double s = 0.0;
+  for (int c0 = 0; c0 < d; c0 += 8) {
+    for (int e = lane; e < 64 * 8; e += 64) {
+      const int r = e >> 3, c = e & 7;
+      const int64_t gr = row0 + r;
+      tile[r][c] = (gr < n && c0 + c < d) ? X[gr * d + c0 + c] : 0.0;
+    }
+    __syncthreads();
+    const int lim = min(8, d - c0);
+    for (int c = 0; c < lim; ++c) {
+      const double df = dsub(crow[c0 + c], tile[lane][c]);
+      s = dadd(s, dmul(df, df));
+    }
+    __syncthreads();
+  }
+  if (myr < n) cost[myr] = s;
 }
 
 // Fold a cluster's chunks in chunk order and add into the caller's sums.
@@ -1141,11 +1291,23 @@ struct cyc_kmeans_plan_s {
   int64_t lastTier2 = 0;    // rows the bf16 screen queued (last counted call)
   int64_t lastExact = 0;    // rows the fp64 screen queued (last counted call)
   cyc::DeviceBuffer cb3, cq3, ok3, list3, list3Count;
+  // i8 exact-integer screen (kmeans_i8.hip), used with a row image
+  int ktp8 = 0;
+  cyc::DeviceBuffer cb8, cq8, g8, prm8, scr8;
   int64_t max_rows = 0;
   size_t assignLds = 0;
   std::mutex mu;
   cyc::DeviceBuffer ct, stats, slowList, slowCount, assignTmp, costTmp;
   cyc::DeviceBuffer hist, total, cstart, chunkStart, perm, part, pw, pc, ccost;
+};
+
+// Per-fit row image for the i8 screen (cyc_kmeans_rows_create).
+struct cyc_kmeans_rows_s {
+  const double* X = nullptr;
+  int64_t n = 0;
+  int d = 0;
+  bool usable = false;     // d <= 512
+  cyc::DeviceBuffer img, meta;
 };
 
 namespace {
@@ -1245,14 +1407,30 @@ int launch_assign3(cyc_kmeans_plan p, const double* X, const double* xnorm, int6
   return CYC_OK;
 }
 
-int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n,
-              const double* C, const double* cnorm, int32_t* assign, double* cost,
+int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmeans_rows rows,
+              int64_t n, const double* C, const double* cnorm, int32_t* assign, double* cost,
               int64_t* n_exact_out, hipStream_t st) {
   CYC_HIP(hipMemsetAsync(p->slowCount.ptr, 0, sizeof(unsigned int), st));
   int rc = CYC_OK;
   const int32_t* rowList = nullptr;
   const unsigned int* rowCount = nullptr;
-  if (p->variant == 3) {
+  if (rows && rows->usable) {
+    // tier 1: exact-integer i8 screen over every row; undecided rows -> list3
+    CYC_HIP(hipMemsetAsync(p->list3Count.ptr, 0, sizeof(unsigned int), st));
+    if ((rc = cyc::km8::centers_prepare(C, cnorm, p->k, p->d, p->ktp8, p->cb8.ptr,
+                                        (float*)p->cq8.ptr, (double*)p->g8.ptr,
+                                        (cyc::km8::CenterParams*)p->prm8.ptr,
+                                        (double*)p->scr8.ptr, st)))
+      return rc;
+    if ((rc = cyc::km8::screen(rows->img.ptr, (const int2*)rows->meta.ptr, xnorm, n, p->d,
+                               p->cb8.ptr, (const float*)p->cq8.ptr, (const double*)p->g8.ptr,
+                               cnorm, (const cyc::km8::CenterParams*)p->prm8.ptr, p->ktp8,
+                               assign, (int32_t*)p->list3.ptr, (unsigned int*)p->list3Count.ptr,
+                               st)))
+      return rc;
+    rowList = (const int32_t*)p->list3.ptr;
+    rowCount = (const unsigned int*)p->list3Count.ptr;
+  } else if (p->variant == 3) {
     // tier 1: bf16x3 screen over every row; undecided rows -> list3
     CYC_HIP(hipMemsetAsync(p->list3Count.ptr, 0, sizeof(unsigned int), st));
     CYC_HIP(hipMemsetAsync(p->ok3.ptr, 1, sizeof(int), st));
@@ -1287,14 +1465,14 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n
     p->lastTier2 = rowCount ? (int64_t)h_tier2 : n;
     p->lastExact = h_slow;
     if (h_slow) {
-      hipLaunchKernelGGL(k_assign_exact, dim3((h_slow + 63) / 64), dim3(64), 0, st, X, xnorm,
+      hipLaunchKernelGGL(k_assign_exact, dim3((unsigned)std::min<unsigned>((h_slow + 3) / 4, 4096)), dim3(256), 0, st, X, xnorm,
                          p->d, C, cnorm, p->k, (const double*)p->stats.ptr,
                          (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr,
                          assign, cost);
       CYC_LAUNCH_CHECK("k_assign_exact");
     }
   } else {
-    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 1024);
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 2048);
     hipLaunchKernelGGL(k_assign_exact, dim3(grid), dim3(256), 0, st, X, xnorm,
                        p->d, C, cnorm, p->k, (const double*)p->stats.ptr,
                        (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr, assign,
@@ -1308,9 +1486,7 @@ int ensure_rows(cyc_kmeans_plan p, int64_t n) {
   if (n <= p->max_rows && p->slowList.ptr) return CYC_OK;
   int rc;
   if ((rc = p->slowList.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1)))) return rc;
-  if (p->variant == 3 &&
-      (rc = p->list3.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1))))
-    return rc;
+  if ((rc = p->list3.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(n, 1)))) return rc;
   p->max_rows = std::max(p->max_rows, n);
   return CYC_OK;
 }
@@ -1385,9 +1561,25 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
   if (p->variant == 3 &&
       ((rc = p->cb3.reserve((size_t)p->ktp3 * p->ks3 * 2 * 64 * 16)) ||
        (rc = p->cq3.reserve(sizeof(float) * (size_t)p->ktp3 * 16)) ||
-       (rc = p->ok3.reserve(64)) || (rc = p->list3Count.reserve(64)))) {
+       (rc = p->ok3.reserve(64)))) {
     delete p;
     return rc;
+  }
+  if ((rc = p->list3Count.reserve(64))) {
+    delete p;
+    return rc;
+  }
+  if (d <= cyc::km8::kMaxD) {
+    const int ks8 = (d + 63) / 64;
+    p->ktp8 = (int)cyc::round_up((k + 15) / 16, cyc::km8::kWaves);
+    if ((rc = p->cb8.reserve((size_t)p->ktp8 * ks8 * 3 * 64 * 16)) ||
+        (rc = p->cq8.reserve(sizeof(float) * (size_t)p->ktp8 * 16)) ||
+        (rc = p->g8.reserve(sizeof(double) * (size_t)p->ktp8 * 16)) ||
+        (rc = p->prm8.reserve(sizeof(cyc::km8::CenterParams))) ||
+        (rc = p->scr8.reserve(sizeof(double) * 2 * (size_t)k))) {
+      delete p;
+      return rc;
+    }
   }
   if ((rc = p->ct.reserve(sizeof(double) * (size_t)p->d4 * p->kpad)) ||
       (rc = p->stats.reserve(sizeof(double) * ((size_t)k * (k + 1) / 2))) ||
@@ -1424,28 +1616,76 @@ int cyc_kmeans_stats_dev(cyc_kmeans_plan p, const double* C, double* stats_out, 
   return CYC_OK;
 }
 
-int cyc_kmeans_assign_dev(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n,
-                          const double* C, const double* cnorm, int32_t* assign, double* cost,
-                          int64_t* n_exact_out, void* stream) {
+int cyc_kmeans_rows_create(cyc_kmeans_plan p, const double* X, int64_t n, void* stream,
+                           cyc_kmeans_rows* out) {
+  CYC_REQUIRE(p != nullptr && out != nullptr, "plan and out must not be null");
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  CYC_REQUIRE(X != nullptr || n == 0, "X must not be null");
+  auto* r = new cyc_kmeans_rows_s();
+  r->X = X;
+  r->n = n;
+  r->d = p->d;
+  r->usable = p->d <= cyc::km8::kMaxD && p->ktp8 > 0;
+  if (r->usable && n > 0) {
+    int rc;
+    if ((rc = r->img.reserve((size_t)n * cyc::km8::image_row_bytes(p->d))) ||
+        (rc = r->meta.reserve(sizeof(int2) * (size_t)n)) ||
+        (rc = cyc::km8::rows_quantize(X, n, p->d, r->img.ptr, (int2*)r->meta.ptr,
+                                      cyc::as_stream(stream)))) {
+      delete r;
+      return rc;
+    }
+  }
+  *out = r;
+  return CYC_OK;
+}
+
+int cyc_kmeans_rows_destroy(cyc_kmeans_rows rows) {
+  delete rows;
+  return CYC_OK;
+}
+
+int64_t cyc_kmeans_rows_bytes(cyc_kmeans_rows rows) {
+  return rows ? (int64_t)(rows->img.bytes + rows->meta.bytes) : 0;
+}
+
+namespace {
+int check_rows(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* X, int64_t n) {
+  CYC_REQUIRE(rows == nullptr || (rows->X == X && rows->n == n && rows->d == p->d),
+              "the row image was built for other rows (cyc_kmeans_rows_create)");
+  return CYC_OK;
+}
+}  // namespace
+
+int cyc_kmeans_assign_dev(cyc_kmeans_plan p, const double* X, const double* xnorm,
+                          cyc_kmeans_rows rows, int64_t n, const double* C, const double* cnorm,
+                          int32_t* assign, double* cost, int64_t* n_exact_out, void* stream) {
   CYC_REQUIRE(p != nullptr, "plan must not be null");
   CYC_REQUIRE(n >= 0, "n >= 0");
   CYC_REQUIRE(assign != nullptr && cost != nullptr, "assign and cost must not be null");
   if (n_exact_out) *n_exact_out = 0;
   if (n == 0) return CYC_OK;
+  if (int rc = check_rows(p, rows, X, n)) return rc;
   std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
   int rc = ensure_rows(p, n);
   if (rc) return rc;
-  return do_assign(p, X, xnorm, n, C, cnorm, assign, cost, n_exact_out, cyc::as_stream(stream));
+  if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, n_exact_out, st))) return rc;
+  hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n, p->d, C,
+                     (const int32_t*)assign, cost);
+  CYC_LAUNCH_CHECK("k_row_cost");
+  return CYC_OK;
 }
 
 int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* xnorm,
-                              const double* weights, int64_t n, const double* C,
-                              const double* cnorm, double* sums, double* wsum, double* cost_sum,
-                              int32_t* assign, double* cost, void* stream) {
+                              cyc_kmeans_rows rows, const double* weights, int64_t n,
+                              const double* C, const double* cnorm, double* sums, double* wsum,
+                              double* cost_sum, int32_t* assign, double* cost, void* stream) {
   CYC_REQUIRE(p != nullptr, "plan must not be null");
   CYC_REQUIRE(n >= 0, "n >= 0");
   CYC_REQUIRE(sums && wsum && cost_sum, "sums, wsum and cost_sum must not be null");
   if (n == 0) return CYC_OK;
+  if (int rc = check_rows(p, rows, X, n)) return rc;
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
   const int k = p->k, d = p->d;
@@ -1455,12 +1695,19 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
     if ((rc = p->assignTmp.reserve(sizeof(int32_t) * (size_t)n))) return rc;
     assign = (int32_t*)p->assignTmp.ptr;
   }
-  if (!cost) {
-    if ((rc = p->costTmp.reserve(sizeof(double) * (size_t)n))) return rc;
-    cost = (double*)p->costTmp.ptr;
-  }
   if ((rc = do_stats(p, C, st))) return rc;
-  if ((rc = do_assign(p, X, xnorm, n, C, cnorm, assign, cost, nullptr, st))) return rc;
+  if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st))) return rc;
+  // d > 1024: per-row costs first (k_chunk_sums fuses them for d <= 1024)
+  const int nj = (d + 255) / 256;
+  if (nj > 4) {
+    if (!cost) {
+      if ((rc = p->costTmp.reserve(sizeof(double) * (size_t)n))) return rc;
+      cost = (double*)p->costTmp.ptr;
+    }
+    hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n, d, C,
+                       (const int32_t*)assign, cost);
+    CYC_LAUNCH_CHECK("k_row_cost");
+  }
 
   const int tiles = (int)((n + kSortTile - 1) / kSortTile);
   const int64_t maxChunks = (n + kChunkRows - 1) / kChunkRows + k;
@@ -1488,11 +1735,25 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   CYC_LAUNCH_CHECK("k_scatter");
   // Number of chunks is data dependent; launch the upper bound and let the
   // surplus blocks (ch >= chunkStart[k]) exit.
-  hipLaunchKernelGGL(k_chunk_sums, dim3((unsigned)maxChunks), dim3(256), 0, st, X, d, weights,
-                     cost, (const int32_t*)p->perm.ptr, (const int64_t*)p->cstart.ptr,
-                     (const int64_t*)p->chunkStart.ptr, k, (double*)p->part.ptr,
-                     (double*)p->pw.ptr, (double*)p->pc.ptr);
-  CYC_LAUNCH_CHECK("k_chunk_sums");
+  {
+    cyc::KernelTimer timer("k_chunk_sums", st);
+    const dim3 grid((unsigned)maxChunks);
+#define CYC_CS(NJ)                                                                              \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_chunk_sums<NJ>), grid, dim3(256), 0, st, X, d, weights, C, \
+                     (const int32_t*)p->perm.ptr, (const int64_t*)p->cstart.ptr,               \
+                     (const int64_t*)p->chunkStart.ptr, k, (double*)p->part.ptr,               \
+                     (double*)p->pw.ptr, (double*)p->pc.ptr, cost)
+    if (nj == 1) CYC_CS(1);
+    else if (nj == 2) CYC_CS(2);
+    else if (nj <= 4) CYC_CS(4);
+    else
+      hipLaunchKernelGGL(k_chunk_sums_nocost, grid, dim3(256), 0, st, X, d, weights,
+                         (const double*)cost, (const int32_t*)p->perm.ptr,
+                         (const int64_t*)p->cstart.ptr, (const int64_t*)p->chunkStart.ptr, k,
+                         (double*)p->part.ptr, (double*)p->pw.ptr, (double*)p->pc.ptr);
+#undef CYC_CS
+    CYC_LAUNCH_CHECK("k_chunk_sums");
+  }
   hipLaunchKernelGGL(k_reduce_clusters, dim3(k), dim3(256), 0, st, (const double*)p->part.ptr,
                      (const double*)p->pw.ptr, (const double*)p->pc.ptr,
                      (const int64_t*)p->chunkStart.ptr, d, sums, wsum, (double*)p->ccost.ptr);

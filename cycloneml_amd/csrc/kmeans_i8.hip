@@ -1,0 +1,534 @@
+// kmeans_i8.hip -- tier 1 of the KMeans assignment (EuclideanDistanceMeasure.
+// findClosest, mllib/clustering/DistanceMeasure.scala:282-313) on gfx950: an
+// exact-integer screen of the dot products x.c on the i8 matrix cores
+// (v_mfma_i32_16x16x64_i8), with a rigorous error bound; fp64 only decides.
+//
+// Fixed-point split.  A row x (fp64) gets the exponent ex with every
+// |x_j| 2^(7-ex) <= 127 and is written as three int8 limbs per element,
+//   x_j 2^(7-ex) = a_j + b_j / 2^7 + c_j / 2^14 + r_j / 2^14,  |r_j| <= 1/2,
+// a = rint(u), b = rint(128 (u - a)), c = rint(128 (128 (u - a) - b)): every
+// step is exact in fp64, |a| <= 127, |b|, |c| <= 64, so |x_j - xh_j| <= 2^(ex-22).
+// Centers use ONE exponent ec for the launch.  Then
+//   xh.ch = 2^(ex+ec-14) (S1 + S2 / 2^7 + S3 / 2^14 + dropped),
+//   S1 = a.a', S2 = a.b' + b.a', S3 = a.c' + b.b' + c.a'   (6 i8 MFMAs / 64 dims)
+// accumulated EXACTLY in int32 (d <= 512: |128 S1 + S2| < 2^31), and
+//   |x.c - 2^(ex+ec-14)(S1 + S2/2^7 + S3/2^14)|
+//      <= Ax |c|_1 + Ac |xh|_1 + 1.004 d 2^22 Ax Ac,   Ax = 2^(ex-22), Ac = 2^(ec-22)
+// (quantization of both operands, plus the dropped b.c', c.b', c.c' terms,
+// |b|,|c| <= 64).  AM-GM with one balance mu > 0 per launch makes the bound
+// separable: <= fx + gc with
+//   fx = mu Ax^2 / 2 + |xh|_1^2 / (2 mu) + 0.502 d 2^22 Ax^2,   gc likewise.
+// So every distance obeys
+//   |x|^2 + |c|^2 - 2 s - 2 (fx + gc) <= |x - c|^2 <= |x|^2 + |c|^2 - 2 s + 2 (fx + gc),
+//   2 s = 2^(ex+ec-20) (128 S1 + S2 + S3 / 2^7).
+// The kernel keeps, per row, the two smallest of L'_c = cq_c - 2 s (f32,
+// MODE rounding toward -inf; cq_c = |c|^2 (1 - epsF) - 2 gc rounded down) and
+// the index of the smallest; f32 conversion / fma errors are below
+// 2^-21 (|x|^2 + |c|^2) and absorbed by epsF = 2^-20.  A row is certified
+// when  L'_2 - L'_1 > 4 (fx + g_1) + 2 epsF (|x|^2 + |c_1|^2) + slack: then
+// its best center's upper bound lies below every other center's lower
+// bound, the reference's pruned loop (whose prunes only skip centers that
+// cannot win) returns the same index, and the row is assigned here.  Every
+// other row (ties, near ties, NaN/Inf, |x_j| >= 2^50) is queued for the fp64
+// MFMA screen and, behind it, the reference loop itself.
+//
+// The margin is ~1e-6 relative (vs ~2.5e-4 for a bf16 x3 split with f32
+// accumulation), so practically only true near-ties reach the fp64 tiers.
+//
+// Data flow: the row image (3 D bytes per row, D = 64 ceil(d/64)) is built
+// once per fit (rows_quantize; the reference likewise caches the rows with
+// their norms once per fit, KMeans.scala:263-270); the center image (3 D
+// bytes per center, ~0.75 MB at k=1024, d=256) is rebuilt per iteration and
+// stays in each XCD's L2 while every workgroup streams it.
+#include "kmeans_i8.hpp"
+
+#include <climits>
+
+#include "common.hpp"
+
+namespace cyc {
+namespace km8 {
+namespace {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// one f32 ulp toward -inf; f32 rounded down / up from fp64
+__device__ __forceinline__ float ulp_dn(float f) {
+  const int b = __float_as_int(f);
+  if (f == 0.0f) return -__int_as_float(1);
+  return __int_as_float(f > 0.0f ? b - 1 : b + 1);
+}
+__device__ __forceinline__ float fdown(double x) {
+  const float f = (float)x;
+  return ((double)f > x) ? ulp_dn(f) : f;
+}
+__device__ __forceinline__ float fup(double x) {
+  const float f = (float)x;
+  return ((double)f < x) ? -ulp_dn(-f) : f;
+}
+
+constexpr int kMinExp = -50, kMaxExp = 50;
+constexpr double kEpsF = 0x1p-20;
+
+__device__ __forceinline__ int choose_exp(double m) {
+  if (!(m > 0.0)) return kMinExp;
+  int E;
+  const double f = __builtin_frexp(m, &E);   // m = f 2^E, f in [0.5, 1)
+  const int e = (f * 128.0 >= 127.5) ? E + 1 : E;
+  return e < kMinExp ? kMinExp : e;          // a coarser grid is always valid
+}
+
+// three limbs of v on the 2^(e-7) grid (exact fp64 steps)
+__device__ __forceinline__ void quant3(double v, int e, int& a, int& b, int& c) {
+  const double u = __builtin_ldexp(v, 7 - e);
+  const double ar = __builtin_rint(u);
+  const double t = (u - ar) * 128.0;
+  const double br = __builtin_rint(t);
+  const double cr = __builtin_rint((t - br) * 128.0);
+  a = (int)ar;
+  b = (int)br;
+  c = (int)cr;
+}
+
+__device__ __forceinline__ unsigned pack4(const int* v) {
+  return (unsigned)(v[0] & 0xff) | ((unsigned)(v[1] & 0xff) << 8) |
+         ((unsigned)(v[2] & 0xff) << 16) | ((unsigned)(v[3] & 0xff) << 24);
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = __builtin_fmax(v, __shfl_xor(v, m));
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+// fx (or gc): separable half of the error bound (see the header comment)
+__device__ __forceinline__ double err_term(int e, double n1, double mu, int d) {
+  const double A = __builtin_ldexp(1.0, e - 22);
+  const double kd = 0.502 * (double)d * 0x1p22;
+  return (0.5 * mu * A * A + 0.5 * n1 * n1 / mu + kd * A * A) * (1.0 + 0x1p-40);
+}
+
+// One wave per row: limbs into the image, exponent and |xh|_1 bound into meta.
+__global__ __launch_bounds__(256) void k_rows_quantize(const double* __restrict__ X, int64_t n,
+                                                       int d, int D, unsigned* __restrict__ img,
+                                                       int2* __restrict__ meta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < n; row += nw) {
+    const double* x = X + row * d;
+    double v[8];
+    double m = 0.0, s1 = 0.0;
+    bool fin = true;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = p * 256 + 4 * lane + q;
+        const double t = j < d ? x[j] : 0.0;
+        v[4 * p + q] = t;
+        fin = fin && __builtin_isfinite(t);
+        m = __builtin_fmax(m, __builtin_fabs(t));
+        s1 += __builtin_fabs(t);
+      }
+    }
+    m = wave_max(m);
+    s1 = wave_sum(s1);
+    const bool allFin = __all(fin);
+    const int e = choose_exp(m);
+    const bool bad = !allFin || e > kMaxExp;
+    unsigned* dst = img + row * (int64_t)(3 * D / 4);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int j0 = p * 256 + 4 * lane;
+      if (j0 < D) {
+        int a[4], b[4], c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (bad) {
+            a[q] = b[q] = c[q] = 0;
+          } else {
+            quant3(v[4 * p + q], e, a[q], b[q], c[q]);
+          }
+        }
+        dst[j0 / 4] = pack4(a);
+        dst[(D + j0) / 4] = pack4(b);
+        dst[(2 * D + j0) / 4] = pack4(c);
+      }
+    }
+    if (lane == 0) {
+      // |xh|_1 <= |x|_1 + d 2^(e-22); the fp64 sum is rounded up generously
+      const double n1 = bad ? 0.0 : s1 * (1.0 + 0x1p-40) + (double)d * __builtin_ldexp(1.0, e - 22);
+      meta[row] = make_int2(bad ? INT_MIN : e, __float_as_int(fup(n1)));
+    }
+  }
+}
+
+// One wave per center: max |c_j|, |c|_1, finiteness.
+__global__ __launch_bounds__(256) void k_centers_scan(const double* __restrict__ C, int k, int d,
+                                                      double* __restrict__ cmax,
+                                                      double* __restrict__ cn1) {
+  const int lane = threadIdx.x & 63;
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (c >= k) return;
+  double m = 0.0, s1 = 0.0;
+  bool fin = true;
+  for (int j = lane; j < d; j += 64) {
+    const double t = C[(int64_t)c * d + j];
+    fin = fin && __builtin_isfinite(t);
+    m = __builtin_fmax(m, __builtin_fabs(t));
+    s1 += __builtin_fabs(t);
+  }
+  m = wave_max(m);
+  s1 = wave_sum(s1);
+  const bool allFin = __all(fin);
+  if (lane == 0) {
+    cmax[c] = allFin ? m : __builtin_inf();
+    cn1[c] = s1 * (1.0 + 0x1p-40);
+  }
+}
+
+// Single block: the launch's exponent, balance and on/off flag.
+__global__ __launch_bounds__(256) void k_centers_params(int k, const double* __restrict__ cmax,
+                                                        const double* __restrict__ cn1,
+                                                        CenterParams* __restrict__ prm) {
+  __shared__ double sm[256], sn[256];
+  double m = 0.0, nmax = 0.0;
+  for (int c = threadIdx.x; c < k; c += 256) {
+    m = __builtin_fmax(m, cmax[c]);
+    nmax = __builtin_fmax(nmax, cn1[c]);
+    if (!(cmax[c] <= 0x1p60)) m = __builtin_inf();   // non-finite center
+  }
+  sm[threadIdx.x] = m;
+  sn[threadIdx.x] = nmax;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      sm[threadIdx.x] = __builtin_fmax(sm[threadIdx.x], sm[threadIdx.x + off]);
+      sn[threadIdx.x] = __builtin_fmax(sn[threadIdx.x], sn[threadIdx.x + off]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double gm = sm[0];
+    const int ec = choose_exp(__builtin_isfinite(gm) ? gm : 0.0);
+    CenterParams p;
+    p.ok = (__builtin_isfinite(gm) && ec <= kMaxExp) ? 1 : 0;
+    p.ec = ec;
+    const double Ac = __builtin_ldexp(1.0, ec - 22);
+    const double mu = sn[0] / Ac;
+    p.mu = (mu > 0.0 && __builtin_isfinite(mu)) ? mu : 1.0;
+    *prm = p;
+  }
+}
+
+// Packed B fragments of v_mfma_i32_16x16x64_i8: lane l of 16-center tile ct,
+// 64-dim step ks holds center ct*16 + (l & 15), dims ks*64 + 16 (l >> 4) + 0..15
+// (the same element order as the rows' A fragments), limb planes a', b', c':
+// Cb[((ct KS + ks) 3 + limb) 64 + l].  Plus cq (f32, rounded down) and g.
+__global__ __launch_bounds__(256) void k_centers_pack(
+    const double* __restrict__ C, const double* __restrict__ cnorm, int k, int d, int KS, int ktp,
+    const double* __restrict__ cn1, const CenterParams* __restrict__ prm, uint4* __restrict__ Cb,
+    float* __restrict__ cq, double* __restrict__ g) {
+  const CenterParams p = *prm;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)ktp * KS * 64;
+  if (idx < total) {
+    const int lane = (int)(idx & 63);
+    const int64_t t = idx >> 6;
+    const int ks = (int)(t % KS), ct = (int)(t / KS);
+    const int c = ct * 16 + (lane & 15), j0 = ks * 64 + 16 * (lane >> 4);
+    int a[16], b[16], cc[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int j = j0 + e;
+      const double v = (p.ok && c < k && j < d) ? C[(int64_t)c * d + j] : 0.0;
+      quant3(v, p.ec, a[e], b[e], cc[e]);
+    }
+    uint4 pa, pb, pc;
+    pa.x = pack4(a); pa.y = pack4(a + 4); pa.z = pack4(a + 8); pa.w = pack4(a + 12);
+    pb.x = pack4(b); pb.y = pack4(b + 4); pb.z = pack4(b + 8); pb.w = pack4(b + 12);
+    pc.x = pack4(cc); pc.y = pack4(cc + 4); pc.z = pack4(cc + 8); pc.w = pack4(cc + 12);
+    uint4* dst = Cb + (t * 3) * 64 + lane;
+    dst[0] = pa;
+    dst[64] = pb;
+    dst[128] = pc;
+  }
+  if (idx < (int64_t)ktp * 16) {
+    const int c = (int)idx;
+    if (c < k && p.ok) {
+      const double gc = err_term(p.ec, cn1[c], p.mu, d);
+      const double cn = cnorm[c];
+      g[c] = gc;
+      cq[c] = fdown((cn * cn) * (1.0 - kEpsF) - 2.0 * gc);
+    } else {
+      g[c] = 0.0;
+      cq[c] = __builtin_inff();
+    }
+  }
+}
+
+__device__ __forceinline__ v4i as_v4i(uint4 u) { return __builtin_bit_cast(v4i, u); }
+
+// BM = 64 rows per workgroup (4 row tiles), 4 waves; wave w owns the 16-center
+// tiles w, w+4, w+8, ...  The row image lives in LDS with a row stride of
+// 12 KS + 2 16-byte chunks (== 2 mod 4: conflict-free ds_read_b128 fragment
+// reads); B fragments come from L2 one 64-dim step ahead.
+template <int KS>
+__global__ __launch_bounds__(256, 2) void k_screen(
+    const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
+    int64_t n, int d, const uint4* __restrict__ Cb, const float* __restrict__ cq,
+    const double* __restrict__ g, const double* __restrict__ cnorm,
+    const CenterParams* __restrict__ prm, int ktp, int32_t* __restrict__ assign,
+    int32_t* __restrict__ list, unsigned int* __restrict__ listCount) {
+  constexpr int BM = kBM, W = kWaves, CH = 12 * KS, STR = CH + 2;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem8[];
+  uint4* As = smem8;                          // BM x STR chunks
+  float* mL1 = (float*)(As + BM * STR);       // W x BM
+  float* mL2 = mL1 + W * BM;                  // W x BM
+  int* mI1 = (int*)(mL2 + W * BM);            // W x BM
+  int* exS = mI1 + W * BM;                    // BM
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t row0 = (int64_t)blockIdx.x * BM;
+  const int rows = (int)min<int64_t>(BM, n - row0);
+  const CenterParams P = *prm;
+  if (!P.ok) {
+    if (tid < rows) list[atomicAdd(listCount, 1u)] = (int32_t)(row0 + tid);
+    return;
+  }
+  {
+    const uint4* src = Xq + row0 * CH;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll 4
+    for (int e = tid; e < BM * CH; e += 256) {
+      const int r = e / CH, ch = e - r * CH;
+      if (r < rows) {
+        const v4u v = __builtin_nontemporal_load((const v4u*)(src + e));
+        As[r * STR + ch] = make_uint4(v.x, v.y, v.z, v.w);
+      } else {
+        As[r * STR + ch] = z;
+      }
+    }
+    if (tid < BM) exS[tid] = tid < rows ? meta[row0 + tid].x : INT_MIN;
+  }
+  __syncthreads();
+
+  // Per row slot q = 4 ta + r (row ta*16 + 4 (lane >> 4) + r): 2^(ex+ec-20).
+  float F1[16];
+#pragma unroll
+  for (int ta = 0; ta < 4; ++ta) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ex = exS[ta * 16 + 4 * (lane >> 4) + r];
+      F1[4 * ta + r] = ex == INT_MIN ? 0.0f : __builtin_ldexpf(1.0f, ex + P.ec - 20);
+    }
+  }
+  float sL1[16], sL2[16];
+  int sI1[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    sL1[q] = sL2[q] = __builtin_inff();
+    sI1[q] = -1;
+  }
+  const uint4* ap = As + (lane & 15) * STR + (lane >> 4);
+  const int nT = ktp / W;
+  const uint4* cb = Cb + (size_t)wave * KS * 192 + lane;
+  const size_t tstride = (size_t)W * KS * 192;
+  uint4 n0 = cb[0], n1 = cb[64], n2 = cb[128];
+
+  // MODE.FP_ROUND single precision = toward -inf (the L' are lower bounds)
+  __builtin_amdgcn_s_setreg(0x801, 2);
+  for (int t = 0; t < nT; ++t) {
+    const float cqv = cq[(t * W + wave) * 16 + (lane & 15)];
+    v4i acc[4][3];
+#pragma unroll
+    for (int ta = 0; ta < 4; ++ta)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) acc[ta][s] = v4i{0, 0, 0, 0};
+#pragma unroll 1
+    for (int ks = 0; ks < KS; ++ks) {
+      const v4i b0 = as_v4i(n0), b1 = as_v4i(n1), b2 = as_v4i(n2);
+      if (ks + 1 < KS) {
+        const uint4* nx = cb + (ks + 1) * 192;
+        n0 = nx[0];
+        n1 = nx[64];
+        n2 = nx[128];
+      } else if (t + 1 < nT) {
+        const uint4* nx = cb + tstride;
+        n0 = nx[0];
+        n1 = nx[64];
+        n2 = nx[128];
+      }
+#pragma unroll
+      for (int ta = 0; ta < 4; ++ta) {
+        const uint4* a = ap + ta * 16 * STR + ks * 4;
+        const v4i a0 = as_v4i(a[0]), a1 = as_v4i(a[4 * KS]), a2 = as_v4i(a[8 * KS]);
+        acc[ta][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b0, acc[ta][0], 0, 0, 0);
+        acc[ta][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b1, acc[ta][1], 0, 0, 0);
+        acc[ta][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, b0, acc[ta][1], 0, 0, 0);
+        acc[ta][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b2, acc[ta][2], 0, 0, 0);
+        acc[ta][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, b1, acc[ta][2], 0, 0, 0);
+        acc[ta][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, b0, acc[ta][2], 0, 0, 0);
+      }
+    }
+    cb += tstride;
+    const int c = (t * W + wave) * 16 + (lane & 15);
+#pragma unroll
+    for (int ta = 0; ta < 4; ++ta) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = 4 * ta + r;
+        const int T = acc[ta][0][r] * 128 + acc[ta][1][r];
+        const float V = __builtin_fmaf((float)acc[ta][2][r], 0x1p-7f, (float)T);
+        const float L = __builtin_fmaf(-F1[q], V, cqv);
+        const bool lt = L < sL1[q];
+        sL2[q] = lt ? sL1[q] : __builtin_fminf(sL2[q], L);
+        sI1[q] = lt ? c : sI1[q];
+        sL1[q] = lt ? L : sL1[q];
+      }
+    }
+  }
+  __builtin_amdgcn_s_setreg(0x801, 0);
+
+  // Reduce each slot over the 16 lanes (centers) that hold the same row.
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) {
+      const float oL1 = __shfl_xor(sL1[q], m), oL2 = __shfl_xor(sL2[q], m);
+      const int oI1 = __shfl_xor(sI1[q], m);
+      sL2[q] = __builtin_fminf(__builtin_fmaxf(sL1[q], oL1), __builtin_fminf(sL2[q], oL2));
+      const bool take = oL1 < sL1[q] || (oL1 == sL1[q] && oI1 >= 0 && (sI1[q] < 0 || oI1 < sI1[q]));
+      sI1[q] = take ? oI1 : sI1[q];
+      sL1[q] = take ? oL1 : sL1[q];
+    }
+  }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int ta = 0; ta < 4; ++ta) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = 4 * ta + r, row = ta * 16 + 4 * (lane >> 4) + r;
+        mL1[wave * BM + row] = sL1[q];
+        mL2[wave * BM + row] = sL2[q];
+        mI1[wave * BM + row] = sI1[q];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < rows) {
+    const int row = tid;
+    const int ex = exS[row];
+    float L1 = __builtin_inff(), L2 = __builtin_inff();
+    int I1 = -1;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const float oL1 = mL1[w * BM + row], oL2 = mL2[w * BM + row];
+      const int oI1 = mI1[w * BM + row];
+      L2 = __builtin_fminf(__builtin_fmaxf(L1, oL1), __builtin_fminf(L2, oL2));
+      if (oL1 < L1 || (oL1 == L1 && oI1 >= 0 && (I1 < 0 || oI1 < I1))) {
+        L1 = oL1;
+        I1 = oI1;
+      }
+    }
+    bool decided = false;
+    if (ex != INT_MIN && I1 >= 0 && __builtin_isfinite(L1)) {
+      const double xn = xnorm[row0 + row], cn = cnorm[I1];
+      const double xx = xn * xn, cc = cn * cn;
+      const double n1 = (double)__int_as_float(meta[row0 + row].y);
+      const double fx = err_term(ex, n1, P.mu, d);
+      const double l1 = (double)L1;
+      const double M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) +
+                        0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g[I1]) +
+                        0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
+                                   __builtin_fmin(__builtin_fabs((double)L2), 0x1p120)) +
+                        0x1p-90) *
+                       (1.0 + 0x1p-30);
+      // exact difference of two floats; L2 = +inf: no other real center
+      decided = !__builtin_isfinite(L2) || ((double)L2 - l1) > M;
+    }
+    if (decided) {
+      assign[row0 + row] = I1;
+    } else {
+      list[atomicAdd(listCount, 1u)] = (int32_t)(row0 + row);
+    }
+  }
+}
+
+template <int KS>
+int launch_screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
+                  const void* Cb, const float* cq, const double* g, const double* cnorm,
+                  const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
+                  unsigned int* listCount, hipStream_t st) {
+  constexpr int STR = 12 * KS + 2;
+  const size_t lds = (size_t)kBM * STR * 16 + (size_t)kWaves * kBM * 12 + (size_t)kBM * 4;
+  static bool attr = false;
+  if (!attr) {
+    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_screen<KS>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr = true;
+  }
+  KernelTimer timer("k_kmeans_assign", st);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen<KS>), dim3((unsigned)((n + kBM - 1) / kBM)),
+                     dim3(256), lds, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
+                     cq, g, cnorm, prm, ktp, assign, list, listCount);
+  CYC_LAUNCH_CHECK("k_kmeans_screen_i8");
+  return CYC_OK;
+}
+
+}  // namespace
+
+int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipStream_t st) {
+  if (n <= 0) return CYC_OK;
+  const int D = 64 * ((d + 63) / 64);
+  const int64_t blocks = std::min<int64_t>((n + 3) / 4, 65536);
+  hipLaunchKernelGGL(k_rows_quantize, dim3((unsigned)blocks), dim3(256), 0, st, X, n, d, D,
+                     (unsigned*)img, meta);
+  CYC_LAUNCH_CHECK("k_rows_quantize");
+  return CYC_OK;
+}
+
+int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp, void* Cb,
+                    float* cq, double* g, CenterParams* prm, double* scratch, hipStream_t st) {
+  const int KS = (d + 63) / 64;
+  double* cmax = scratch;
+  double* cn1 = scratch + k;
+  hipLaunchKernelGGL(k_centers_scan, dim3((unsigned)((k + 3) / 4)), dim3(256), 0, st, C, k, d,
+                     cmax, cn1);
+  CYC_LAUNCH_CHECK("k_centers_scan");
+  hipLaunchKernelGGL(k_centers_params, dim3(1), dim3(256), 0, st, k, (const double*)cmax,
+                     (const double*)cn1, prm);
+  CYC_LAUNCH_CHECK("k_centers_params");
+  const int64_t total = std::max<int64_t>((int64_t)ktp * KS * 64, (int64_t)ktp * 16);
+  hipLaunchKernelGGL(k_centers_pack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, C,
+                     cnorm, k, d, KS, ktp, (const double*)cn1, (const CenterParams*)prm,
+                     (uint4*)Cb, cq, g);
+  CYC_LAUNCH_CHECK("k_centers_pack");
+  return CYC_OK;
+}
+
+int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
+           const void* Cb, const float* cq, const double* g, const double* cnorm,
+           const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
+           unsigned int* listCount, hipStream_t st) {
+  if (n <= 0) return CYC_OK;
+  switch ((d + 63) / 64) {
+#define CYC_S8(K) \
+  case K: return launch_screen<K>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp, assign, list, listCount, st);
+    CYC_S8(1) CYC_S8(2) CYC_S8(3) CYC_S8(4) CYC_S8(5) CYC_S8(6) CYC_S8(7) CYC_S8(8)
+#undef CYC_S8
+    default:
+      set_error("the i8 screen supports d <= 512");
+      return CYC_ERR_UNSUPPORTED;
+  }
+}
+
+}  // namespace km8
+}  // namespace cyc

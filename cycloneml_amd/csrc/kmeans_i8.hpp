@@ -1,0 +1,46 @@
+// kmeans_i8.hpp -- tier 1 of the KMeans assignment (kmeans_i8.hip): an
+// exact-integer screen of |x - c|^2 on the gfx950 i8 matrix cores, used when
+// a per-fit row image exists (cyc_kmeans_rows) and d <= 512.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace cyc {
+namespace km8 {
+
+constexpr int kMaxD = 512;    // |T| = |128 S_aa + S_ab| < 2^31 needs d <= 512
+constexpr int kBM = 64;       // rows per workgroup
+constexpr int kWaves = 4;     // waves per workgroup (centers split across them)
+
+// Per-launch center constants, written on device by centers_prepare().
+struct CenterParams {
+  int ec;      // global center exponent: every |c_j| <= 2^ec * 127.5/128
+  int ok;      // 0: some center is non-finite or beyond 2^50 (screen off)
+  double mu;   // AM-GM balance of the separable error bound
+};
+
+// Bytes per row of the image: three int8 limb planes of D = 64 ceil(d/64).
+inline int64_t image_row_bytes(int d) { return 3 * 64 * (int64_t)((d + 63) / 64); }
+
+// X (n x d, row-major fp64) -> img (n rows of image_row_bytes) and meta
+// (per row: int exponent or INT32_MIN when the row cannot be screened, and
+// the float bits of an upper bound of the 1-norm of the quantized row).
+int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipStream_t st);
+
+// Centers -> packed B fragments (Cb), per-center lower-bound constants cq
+// (float, +inf for padding), error terms g (fp64) and the launch's params.
+// scratch: >= 2k doubles + 1 int.  ktp: 16-center tiles, a multiple of kWaves.
+int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp, void* Cb,
+                    float* cq, double* g, CenterParams* prm, double* scratch, hipStream_t st);
+
+// Screen every row: certified rows get assign[row]; the others are appended
+// to list (listCount is NOT cleared here).
+int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
+           const void* Cb, const float* cq, const double* g, const double* cnorm,
+           const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
+           unsigned int* listCount, hipStream_t st);
+
+}  // namespace km8
+}  // namespace cyc

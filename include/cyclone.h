@@ -80,27 +80,43 @@ int cyc_kmeans_plan_destroy(cyc_kmeans_plan plan);
  * statistics (and copies them to stats_out if non-NULL, device memory). */
 int cyc_kmeans_stats_dev(cyc_kmeans_plan plan, const double* C, double* stats_out, void* stream);
 
+/* Per-fit row image (KMeans.scala:263-270 caches the rows with their norms
+ * once per fit; this caches a second view of the same rows): the int8
+ * three-limb fixed-point image that the exact-integer screen streams, 3 bytes
+ * per (64-padded) element + 8 bytes per row.  Built once from X (n x d device
+ * rows); X must not change while the image is used.  For d > 512 the image is
+ * empty and the calls below use the bf16 / fp64 screens instead.  Passing the
+ * image is optional everywhere (NULL = no i8 tier). */
+typedef struct cyc_kmeans_rows_s* cyc_kmeans_rows;
+int cyc_kmeans_rows_create(cyc_kmeans_plan plan, const double* X, int64_t n, void* stream,
+                           cyc_kmeans_rows* rows);
+int cyc_kmeans_rows_destroy(cyc_kmeans_rows rows);
+int64_t cyc_kmeans_rows_bytes(cyc_kmeans_rows rows);
+
 /* findClosest(centers, stats, point) for n points (stats from the last
  * cyc_kmeans_stats_dev on this plan).  assign[n], cost[n] device outputs.
+ * rows: NULL or the image of exactly these X, n.
  * *n_exact_out (host, may be NULL) receives how many points needed the
- * exact-emulation path (ties / near ties of the fp64 screening). */
-int cyc_kmeans_assign_dev(cyc_kmeans_plan plan, const double* X, const double* xnorm, int64_t n,
-                          const double* C, const double* cnorm, int32_t* assign, double* cost,
-                          int64_t* n_exact_out, void* stream);
+ * exact-emulation path (ties / near ties the screens cannot separate). */
+int cyc_kmeans_assign_dev(cyc_kmeans_plan plan, const double* X, const double* xnorm,
+                          cyc_kmeans_rows rows, int64_t n, const double* C, const double* cnorm,
+                          int32_t* assign, double* cost, int64_t* n_exact_out, void* stream);
 
 /* Screening tiers of the last cyc_kmeans_assign_dev call that asked for
- * n_exact_out: rows the bf16x3 screen left to the fp64 MFMA screen (all rows
- * when the bf16 screen is off), and rows left to the exact emulation. */
+ * n_exact_out: rows the first screen (i8 with a row image, else bf16x3) left
+ * to the fp64 MFMA screen (all rows when neither runs), and rows left to the
+ * exact emulation. */
 int cyc_kmeans_last_tiers(cyc_kmeans_plan plan, int64_t* fp64_screen_rows, int64_t* exact_rows);
 
 /* One partition's contribution to a Lloyd iteration: statistics + assign +
  * per-cluster sums.  sums[k*d] += sum of w*x, wsum[k] += sum of w,
  * cost_sum[0] += sum of w*cost.  weights may be NULL (unit weights).
- * assign/cost may be NULL.  All pointers are device memory. */
+ * rows: NULL or the image of exactly these X, n.  assign/cost (per-row
+ * outputs) may be NULL.  All pointers are device memory. */
 int cyc_kmeans_accumulate_dev(cyc_kmeans_plan plan, const double* X, const double* xnorm,
-                              const double* weights, int64_t n, const double* C,
-                              const double* cnorm, double* sums, double* wsum, double* cost_sum,
-                              int32_t* assign, double* cost, void* stream);
+                              cyc_kmeans_rows rows, const double* weights, int64_t n,
+                              const double* C, const double* cnorm, double* sums, double* wsum,
+                              double* cost_sum, int32_t* assign, double* cost, void* stream);
 
 /* centroid = scal(1/wsum, sum) and a fresh norm for every cluster with
  * wsum > 0; converged_out (device int32) = 1 iff every such center moved by

@@ -139,9 +139,11 @@ def test_assign_nonfinite(cuda):
     np.testing.assert_array_equal(c, rc)   # NaN == NaN under assert_array_equal
 
 
+@pytest.mark.parametrize("use_rows", [False, True])
 @pytest.mark.parametrize("n,d,k,weighted", [(5000, 16, 12, False), (20000, 256, 64, True),
-                                            (3000, 7, 1, False)])
-def test_lloyd_iteration(cuda, n, d, k, weighted):
+                                            (3000, 7, 1, False), (4000, 600, 9, True),
+                                            (1500, 1100, 5, False)])
+def test_lloyd_iteration(cuda, n, d, k, weighted, use_rows):
     import torch
     from cycloneml_amd.clustering import row_norms
     rng = np.random.default_rng(n + k)
@@ -158,7 +160,8 @@ def test_lloyd_iteration(cuda, n, d, k, weighted):
     cost = torch.zeros(1, dtype=torch.float64, device=cuda)
     a = torch.empty(n, dtype=torch.int32, device=cuda)
     pc = torch.empty(n, dtype=torch.float64, device=cuda)
-    p.accumulate(Xd, xn, wd, Cd, cn, sums, wsum, cost, a, pc)
+    rows = p.rows(Xd) if use_rows else None
+    p.accumulate(Xd, xn, wd, Cd, cn, sums, wsum, cost, a, pc, rows=rows)
     conv = torch.zeros(1, dtype=torch.int32, device=cuda)
     p.update(Cd, cn, sums, wsum, 1e-4, conv)
     torch.cuda.synchronize()
@@ -213,8 +216,10 @@ def test_full_config_properties(cuda):
     cost = torch.zeros(1, dtype=torch.float64, device=cuda)
     a = torch.empty(n, dtype=torch.int32, device=cuda)
     pc = torch.empty(n, dtype=torch.float64, device=cuda)
-    p.accumulate(X, xn, None, C, cn, sums, wsum, cost, a, pc)
+    rows = p.rows(X)
+    p.accumulate(X, xn, None, C, cn, sums, wsum, cost, a, pc, rows=rows)
     torch.cuda.synchronize()
+    del rows
     assert wsum.sum().item() == n
     colsum = X.sum(0)
     np.testing.assert_allclose(sums.view(k, d).sum(0).cpu().numpy(), colsum.cpu().numpy(),
@@ -231,9 +236,10 @@ def test_full_config_properties(cuda):
         assert (idx, dist) == (int(ah[i]), float(ch[i]))
 
 
-def _assign_variant(X, C, cuda, variant, monkeypatch):
-    """Assign through a plan built with CYC_KMEANS_ASSIGN=variant; returns
-    (assign, cost, fp64-screen rows, exact rows)."""
+def _assign_variant(X, C, cuda, variant, monkeypatch, use_rows=False):
+    """Assign through a plan built with CYC_KMEANS_ASSIGN=variant (and the
+    i8 row image when use_rows); returns (assign, cost, fp64-screen rows,
+    exact rows)."""
     import torch
     from cycloneml_amd.clustering import KMeansPlan, row_norms
     monkeypatch.setenv("CYC_KMEANS_ASSIGN", str(variant))
@@ -243,7 +249,8 @@ def _assign_variant(X, C, cuda, variant, monkeypatch):
     p.stats(Cd)
     a = torch.empty(X.shape[0], dtype=torch.int32, device=cuda)
     c = torch.empty(X.shape[0], dtype=torch.float64, device=cuda)
-    n_exact = p.assign(Xd, xn, Cd, cn, a, c, count_exact=True)
+    rows = p.rows(Xd) if use_rows else None
+    n_exact = p.assign(Xd, xn, Cd, cn, a, c, count_exact=True, rows=rows)
     torch.cuda.synchronize()
     t2, ex = p.last_tiers()
     assert ex == n_exact
@@ -306,3 +313,100 @@ def test_bf16_screen_off_for_huge_center(cuda, monkeypatch):
     ra, rc = _oracle_assign(X, C)
     np.testing.assert_array_equal(a3, ra)
     np.testing.assert_array_equal(c3, rc)
+
+
+@pytest.mark.parametrize("n,d,k", [(4000, 32, 7), (3000, 64, 130), (2000, 256, 300),
+                                   (1000, 96, 1), (700, 512, 40), (5000, 128, 1024),
+                                   (900, 1, 3), (1200, 100, 33), (800, 300, 64)])
+def test_i8_screen_matches_reference(cuda, monkeypatch, n, d, k):
+    """Tier 1 = exact-integer i8 screen (row image), then the fp64 screen and
+    the exact loop on its leftovers: bit-identical to the restatement and to
+    the fp64 screen alone; on separated clusters the i8 screen decides
+    (nearly) every row."""
+    rng = np.random.default_rng(n + 5 * d + k)
+    true_c = rng.normal(scale=4.0, size=(max(k, 1), d))
+    X = true_c[rng.integers(0, true_c.shape[0], n)] + rng.normal(size=(n, d))
+    C = true_c + rng.normal(scale=0.1, size=true_c.shape)
+    a8, c8, t2, _ = _assign_variant(X, C, cuda, 2, monkeypatch, use_rows=True)
+    a2, c2, _, _ = _assign_variant(X, C, cuda, 2, monkeypatch)
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a8, ra)
+    np.testing.assert_array_equal(c8, rc)
+    np.testing.assert_array_equal(a2, a8)
+    np.testing.assert_array_equal(c2, c8)
+    assert t2 <= max(n // 100, 3), t2
+
+
+def test_i8_screen_near_ties_and_dense_clusters(cuda, monkeypatch):
+    """Centers drawn from the data itself (setInitialModel on rows, as in the
+    bench config) and close center pairs: many near ties, all resolved to the
+    reference's index."""
+    rng = np.random.default_rng(23)
+    n, d, k = 6000, 256, 256
+    true_c = rng.normal(scale=4.0, size=(k // 2, d))
+    X = true_c[rng.integers(0, k // 2, n)] + rng.normal(size=(n, d))
+    C = X[:k].copy()
+    a8, c8, t2, ex = _assign_variant(X, C, cuda, 2, monkeypatch, use_rows=True)
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a8, ra)
+    np.testing.assert_array_equal(c8, rc)
+
+
+def test_i8_screen_hard_cases(cuda, monkeypatch):
+    """Near ties, duplicate centers, huge rows (> 2^50), tiny-scale rows,
+    all-zero rows and NaN / Inf rows fall through the i8 screen to the fp64
+    screen / exact loop and still match the reference."""
+    rng = np.random.default_rng(29)
+    d, k = 64, 20
+    C = rng.normal(scale=3.0, size=(k, d))
+    C[7] = C[3]                                           # duplicate center
+    X = np.vstack([
+        C[rng.integers(0, k, 800)] + rng.normal(size=(800, d)),
+        0.5 * (C[0] + C[1]) + rng.normal(scale=1e-9, size=(40, d)),   # near ties
+        C[rng.integers(0, k, 30)] * 1e18,                 # beyond 2^50
+        C[rng.integers(0, k, 30)] * 1e-30,                # tiny scale
+        np.zeros((5, d)),
+        C[:5] + 1e-14,
+    ])
+    X[805, 2] = np.nan
+    X[806, 0] = -np.inf
+    a8, c8, t2, ex = _assign_variant(X, C, cuda, 2, monkeypatch, use_rows=True)
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a8, ra)
+    np.testing.assert_array_equal(c8, rc)
+    assert t2 >= 100 and ex > 0
+
+
+@pytest.mark.parametrize("scale", [1e20, 1e-40])
+def test_i8_screen_extreme_centers(cuda, monkeypatch, scale):
+    """A center beyond 2^50 turns the i8 screen off for the launch; tiny
+    centers still screen correctly (coarser grid)."""
+    rng = np.random.default_rng(31)
+    d, k, n = 32, 9, 1500
+    C = rng.normal(size=(k, d))
+    C[4] *= scale
+    X = rng.normal(size=(n, d)) * 2
+    a8, c8, t2, _ = _assign_variant(X, C, cuda, 2, monkeypatch, use_rows=True)
+    if scale > 1:
+        assert t2 == n
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a8, ra)
+    np.testing.assert_array_equal(c8, rc)
+
+
+def test_rows_image_guard(cuda):
+    """The row image is bound to its rows: other X or n is refused with the
+    reference-style message."""
+    import torch
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    X = _dev(np.random.default_rng(1).normal(size=(100, 16)), cuda)
+    C = X[:4].clone()
+    p = KMeansPlan(16, 4, 100)
+    p.stats(C)
+    rows = p.rows(X)
+    assert rows.nbytes == 100 * 3 * 64 + 100 * 8
+    a = torch.empty(100, dtype=torch.int32, device=cuda)
+    c = torch.empty(100, dtype=torch.float64, device=cuda)
+    with pytest.raises(N.IllegalArgumentException, match="row image"):
+        p.assign(X[:50], row_norms(X[:50]), C, row_norms(C), a, c, rows=rows)

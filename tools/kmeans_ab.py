@@ -28,11 +28,14 @@ def main():
     cn = row_norms(C)
     plans = {}
     only = os.environ.get("AB_ONLY")
-    variants = os.environ.get("AB_VARIANTS", "2,3").split(",")
+    variants = os.environ.get("AB_VARIANTS", "3,8").split(",")
+    rows = {}
     for v in ((only,) if only else variants):
-        os.environ["CYC_KMEANS_ASSIGN"] = v
+        # "8": fp64 screen plan + the i8 row image in front of it
+        os.environ["CYC_KMEANS_ASSIGN"] = "2" if v == "8" else v
         plans[v] = KMeansPlan(d, k, n)
         plans[v].stats(C)
+        rows[v] = plans[v].rows(X) if v == "8" else None
     outs = {v: (torch.empty(n, dtype=torch.int32, device=dev),
                 torch.empty(n, dtype=torch.float64, device=dev)) for v in plans}
     N.profile_enable(True)
@@ -41,7 +44,7 @@ def main():
         for v, p in plans.items():
             N.profile_query("k_kmeans_assign")
             N.profile_query("k_kmeans_assign_fp64")
-            nex = p.assign(X, xn, C, cn, *outs[v], count_exact=True)
+            nex = p.assign(X, xn, C, cn, *outs[v], count_exact=True, rows=rows[v])
             torch.cuda.synchronize()
             ms, cnt = N.profile_query("k_kmeans_assign")
             ms2, _ = N.profile_query("k_kmeans_assign_fp64")
@@ -54,7 +57,7 @@ def main():
         best = min(res[v])
         print(f"variant {v}: best {best:.2f} ms = {2.0 * k * d * n / best / 1e9:.1f} "
               "fp64-equivalent TFLOP/s")
-    real = [v for v in plans if v in ("1", "2", "3")]
+    real = [v for v in plans if v in ("1", "2", "3", "8")]
     if only or len(real) < 2:
         return
     same = all(torch.equal(outs[real[0]][i], outs[v][i]) for v in real[1:] for i in range(2))

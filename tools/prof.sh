@@ -1,6 +1,8 @@
 #!/bin/bash
 # Profiling recipe run on the GPU box (see DESIGN.md "Measurement").
-# usage: bash tools_prof.sh <tag> [bench args...]
+# usage: bash tools/prof.sh <tag> [bench args...]
+# Three separate rocprofv3 runs: kernel trace + stats, then FETCH_SIZE and
+# WRITE_SIZE each in its own --pmc pass (MI355X_MICROARCH.md, HBM section).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=$1; shift
@@ -8,6 +10,6 @@ export TMPDIR=/tmp
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 "$@" > $OUT/trace.log 2>&1 || exit $?
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T -d $OUT/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 "$@" > $OUT/pmc_fetch.log 2>&1 || exit $?
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T -d $OUT/pmc_write -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 "$@" > $OUT/pmc_write.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 "$@" > $OUT/trace.log 2>&1 || exit $?
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T -d $OUT/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 "$@" > $OUT/pmc_fetch.log 2>&1 || exit $?
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T -d $OUT/pmc_write -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 "$@" > $OUT/pmc_write.log 2>&1 || exit $?
