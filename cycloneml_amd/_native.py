@@ -71,6 +71,8 @@ SIGNATURES = {
     "cyc_csc_build_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(_vp)]),
     "cyc_csc_destroy": (ctypes.c_int, [_vp]),
     "cyc_csc_rows": (_i64, [_vp]),
+    "cyc_csc_blocks": (ctypes.c_int, [_vp, _pi64, _pi64]),
+    "cyc_csc_slices": (ctypes.c_int, [_vp, _pi32, _pi32, _vp, _vp, _vp]),
     "cyc_csc_arrays": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                                       ctypes.POINTER(_vp)]),
     "cyc_multinomial_logistic_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp,

@@ -45,8 +45,12 @@ struct KernelTimer {
   hipEvent_t e0 = nullptr;
 };
 
-// One-time CSR -> CSC transpose (csc.hip): colptr int64[F+1], rowidx int32,
-// cvals fp64; each column's rows in increasing order.
+// One-time CSR -> row-blocked CSC transpose (csc.hip): rows in blocks of
+// kCscRowBlock; colptr int64[nblocks F + 1] (block-major, then column),
+// rowidx int32, cvals fp64; each (block, column)'s rows in increasing order.
+constexpr int64_t kCscRowBlock = 1 << 18;
+// column-slice width of the sliced CSR copy (fp64 coefficients per slice)
+constexpr int kSliceCols = 1 << 18;
 int build_csc(const int64_t* rowptr, const int32_t* colidx, const double* vals, int64_t n, int F,
               DeviceBuffer& colptr, DeviceBuffer& rowidx, DeviceBuffer& cvals, hipStream_t st);
 

@@ -304,17 +304,19 @@ __global__ __launch_bounds__(256, 2) void k_screen(
     return;
   }
   {
+    // every load in flight before the first LDS write (3 KS chunks per thread)
+    constexpr int PER = BM * CH / 256;
     const uint4* src = Xq + row0 * CH;
-    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll 4
-    for (int e = tid; e < BM * CH; e += 256) {
-      const int r = e / CH, ch = e - r * CH;
-      if (r < rows) {
-        const v4u v = __builtin_nontemporal_load((const v4u*)(src + e));
-        As[r * STR + ch] = make_uint4(v.x, v.y, v.z, v.w);
-      } else {
-        As[r * STR + ch] = z;
-      }
+    const int lim = rows * CH;
+    v4u st[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      st[i] = __builtin_nontemporal_load((const v4u*)(src + min(tid + 256 * i, lim - 1)));
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + 256 * i, r = e / CH, ch = e - r * CH;
+      As[r * STR + ch] = e < lim ? make_uint4(st[i].x, st[i].y, st[i].z, st[i].w)
+                                 : make_uint4(0u, 0u, 0u, 0u);
     }
     if (tid < BM) exS[tid] = tid < rows ? meta[row0 + tid].x : INT_MIN;
   }
@@ -341,44 +343,75 @@ __global__ __launch_bounds__(256, 2) void k_screen(
   const int nT = ktp / W;
   const uint4* cb = Cb + (size_t)wave * KS * 192 + lane;
   const size_t tstride = (size_t)W * KS * 192;
-  uint4 n0 = cb[0], n1 = cb[64], n2 = cb[128];
+  // Register rings, all indices static after unrolling: B fragments one
+  // 64-dim step ahead (KS is even, so a tile always starts on B0), A
+  // fragments one (step, row tile) ahead (4 per step, so always on A0).
+  v4i B0[3], B1[3], A0[3], A1[3];
+#define CYC_LDB(DST, P)                                  \
+  do {                                                   \
+    DST[0] = as_v4i((P)[0]);                             \
+    DST[1] = as_v4i((P)[64]);                            \
+    DST[2] = as_v4i((P)[128]);                           \
+  } while (0)
+#define CYC_LDA(DST, KS_, TA_)                           \
+  do {                                                   \
+    const uint4* a_ = ap + (TA_) * 16 * STR + (KS_) * 4; \
+    DST[0] = as_v4i(a_[0]);                              \
+    DST[1] = as_v4i(a_[4 * KS]);                         \
+    DST[2] = as_v4i(a_[8 * KS]);                         \
+  } while (0)
+#define CYC_MM(ACC, A, B)                                                    \
+  do {                                                                       \
+    ACC[0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[0], ACC[0], 0, 0, 0); \
+    ACC[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[1], ACC[1], 0, 0, 0); \
+    ACC[1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[0], ACC[1], 0, 0, 0); \
+    ACC[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[0], B[2], ACC[2], 0, 0, 0); \
+    ACC[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[1], B[1], ACC[2], 0, 0, 0); \
+    ACC[2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(A[2], B[0], ACC[2], 0, 0, 0); \
+  } while (0)
+  // one (step, row tile): prefetch the next A, then 6 MFMAs
+#define CYC_TA(KS_, TA_, AC, AN, BC)                                          \
+  do {                                                                        \
+    if ((TA_) < 3) CYC_LDA(AN, KS_, (TA_) + 1);                               \
+    else CYC_LDA(AN, ((KS_) + 1 < KS ? (KS_) + 1 : 0), 0);                    \
+    CYC_MM(acc[TA_], AC, BC);                                                 \
+    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);                        \
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);                        \
+  } while (0)
+#define CYC_KSTEP(KS_, BC, BN)                                                \
+  do {                                                                        \
+    CYC_LDB(BN, ((KS_) + 1 < KS ? cb + ((KS_) + 1) * 192 : cbn));             \
+    __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);                        \
+    CYC_TA(KS_, 0, A0, A1, BC);                                               \
+    CYC_TA(KS_, 1, A1, A0, BC);                                               \
+    CYC_TA(KS_, 2, A0, A1, BC);                                               \
+    CYC_TA(KS_, 3, A1, A0, BC);                                               \
+  } while (0)
+  CYC_LDB(B0, cb);
+  CYC_LDA(A0, 0, 0);
 
   // MODE.FP_ROUND single precision = toward -inf (the L' are lower bounds)
   __builtin_amdgcn_s_setreg(0x801, 2);
   for (int t = 0; t < nT; ++t) {
     const float cqv = cq[(t * W + wave) * 16 + (lane & 15)];
+    // next tile's B (the last tile re-reads its own: harmless, branch free)
+    const uint4* cbn = cb + (t + 1 < nT ? tstride : 0);
     v4i acc[4][3];
 #pragma unroll
     for (int ta = 0; ta < 4; ++ta)
 #pragma unroll
       for (int s = 0; s < 3; ++s) acc[ta][s] = v4i{0, 0, 0, 0};
-#pragma unroll 1
-    for (int ks = 0; ks < KS; ++ks) {
-      const v4i b0 = as_v4i(n0), b1 = as_v4i(n1), b2 = as_v4i(n2);
-      if (ks + 1 < KS) {
-        const uint4* nx = cb + (ks + 1) * 192;
-        n0 = nx[0];
-        n1 = nx[64];
-        n2 = nx[128];
-      } else if (t + 1 < nT) {
-        const uint4* nx = cb + tstride;
-        n0 = nx[0];
-        n1 = nx[64];
-        n2 = nx[128];
-      }
 #pragma unroll
-      for (int ta = 0; ta < 4; ++ta) {
-        const uint4* a = ap + ta * 16 * STR + ks * 4;
-        const v4i a0 = as_v4i(a[0]), a1 = as_v4i(a[4 * KS]), a2 = as_v4i(a[8 * KS]);
-        acc[ta][0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b0, acc[ta][0], 0, 0, 0);
-        acc[ta][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b1, acc[ta][1], 0, 0, 0);
-        acc[ta][1] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, b0, acc[ta][1], 0, 0, 0);
-        acc[ta][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, b2, acc[ta][2], 0, 0, 0);
-        acc[ta][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, b1, acc[ta][2], 0, 0, 0);
-        acc[ta][2] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a2, b0, acc[ta][2], 0, 0, 0);
-      }
+    for (int kp = 0; kp < KS; kp += 2) {
+      CYC_KSTEP(kp, B0, B1);
+      CYC_KSTEP(kp + 1, B1, B0);
     }
-    cb += tstride;
+#undef CYC_KSTEP
+#undef CYC_TA
+#undef CYC_MM
+#undef CYC_LDA
+#undef CYC_LDB
+    cb = cbn;
     const int c = (t * W + wave) * 16 + (lane & 15);
 #pragma unroll
     for (int ta = 0; ta < 4; ++ta) {
@@ -487,7 +520,7 @@ int launch_screen(const void* img, const int2* meta, const double* xnorm, int64_
 
 int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipStream_t st) {
   if (n <= 0) return CYC_OK;
-  const int D = 64 * ((d + 63) / 64);
+  const int D = 64 * ksteps(d);
   const int64_t blocks = std::min<int64_t>((n + 3) / 4, 65536);
   hipLaunchKernelGGL(k_rows_quantize, dim3((unsigned)blocks), dim3(256), 0, st, X, n, d, D,
                      (unsigned*)img, meta);
@@ -497,7 +530,7 @@ int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipS
 
 int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp, void* Cb,
                     float* cq, double* g, CenterParams* prm, double* scratch, hipStream_t st) {
-  const int KS = (d + 63) / 64;
+  const int KS = ksteps(d);
   double* cmax = scratch;
   double* cn1 = scratch + k;
   hipLaunchKernelGGL(k_centers_scan, dim3((unsigned)((k + 3) / 4)), dim3(256), 0, st, C, k, d,
@@ -519,10 +552,10 @@ int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, in
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
            unsigned int* listCount, hipStream_t st) {
   if (n <= 0) return CYC_OK;
-  switch ((d + 63) / 64) {
+  switch (ksteps(d)) {
 #define CYC_S8(K) \
   case K: return launch_screen<K>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp, assign, list, listCount, st);
-    CYC_S8(1) CYC_S8(2) CYC_S8(3) CYC_S8(4) CYC_S8(5) CYC_S8(6) CYC_S8(7) CYC_S8(8)
+    CYC_S8(2) CYC_S8(4) CYC_S8(6) CYC_S8(8)
 #undef CYC_S8
     default:
       set_error("the i8 screen supports d <= 512");

@@ -21,8 +21,12 @@ struct CenterParams {
   double mu;   // AM-GM balance of the separable error bound
 };
 
-// Bytes per row of the image: three int8 limb planes of D = 64 ceil(d/64).
-inline int64_t image_row_bytes(int d) { return 3 * 64 * (int64_t)((d + 63) / 64); }
+// 64-dim k-steps of the i8 MFMA, rounded up to even (the kernel's register
+// rings alternate per step); the padding limbs are zero.
+inline int ksteps(int d) { return ((d + 127) / 128) * 2; }
+
+// Bytes per row of the image: three int8 limb planes of D = 64 ksteps(d).
+inline int64_t image_row_bytes(int d) { return 3 * 64 * (int64_t)ksteps(d); }
 
 // X (n x d, row-major fp64) -> img (n rows of image_row_bytes) and meta
 // (per row: int exponent or INT32_MIN when the row cannot be screened, and

@@ -205,6 +205,143 @@ __global__ __launch_bounds__(256) void k_binlog_csc_grad(
   }
 }
 
+// Pass 1, grouped: a wave takes 64 consecutive rows at a time, 8 lanes per
+// row (8 rows per round, each row's nonzeros strided over its 8 lanes and
+// summed by a 3-step butterfly), then hands row i's partial dot to lane i so
+// the per-row epilogue (log1p/exp, BinaryLogisticBlockAggregator.scala:
+// 104-122) runs once per row instead of once per lane.  Over a column-sliced
+// CSR (csc.hip) the pass runs once per slice: dots[r] accumulates the slices'
+// partial dots in slice order (first: =, else +=) and the last slice turns
+// dots[r] into the multiplier in place, written coalesced.
+__global__ __launch_bounds__(256) void k_binlog_csr_mult8(
+    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
+    const double* __restrict__ vals, const double* __restrict__ labels,
+    const double* __restrict__ weights, int64_t n, const double* __restrict__ coef,
+    int fitIntercept, double offset, int first, int last, double* __restrict__ dots,
+    double* __restrict__ slabS) {
+  const int lane = threadIdx.x & 63, sub = lane & 7, grp = lane >> 3;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  double loss = 0.0, wsum = 0.0, msum = 0.0;
+  for (int64_t g0 = gw * 64; g0 < n; g0 += nw * 64) {
+    // row bounds of the 64 rows by one coalesced load, then shuffles
+    const int64_t myr = g0 + lane < n ? g0 + lane : n;
+    const int64_t rp0 = rowptr[myr];
+    const int64_t rp1 = rowptr[myr + 1 < n ? myr + 1 : n];
+    // every round's first 16 nonzeros in flight at once (8 lanes x 2), then
+    // the gathers, then the products; longer rows finish in a tail loop
+    int64_t beg[8], end[8];
+    int ci[8][2];
+    double vv[8][2], cf[8][2];
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      beg[rr] = __shfl(rp0, rr * 8 + grp);
+      end[rr] = __shfl(rp1, rr * 8 + grp);
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int64_t p = beg[rr] + sub + 8 * it;
+        const bool ok = p < end[rr];
+        ci[rr][it] = ok ? __builtin_nontemporal_load(colidx + p) : 0;
+        vv[rr][it] = ok ? __builtin_nontemporal_load(vals + p) : 0.0;
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+      for (int it = 0; it < 2; ++it) cf[rr][it] = coef[ci[rr][it]];
+    double mydot = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      double s = vv[rr][0] * cf[rr][0];
+      s += vv[rr][1] * cf[rr][1];
+      for (int64_t p = beg[rr] + sub + 16; p < end[rr]; p += 8)
+        s += __builtin_nontemporal_load(vals + p) * coef[__builtin_nontemporal_load(colidx + p)];
+      s += __shfl_xor(s, 1);
+      s += __shfl_xor(s, 2);
+      s += __shfl_xor(s, 4);
+      const double v = __shfl(s, 8 * (lane & 7));
+      if ((lane >> 3) == rr) mydot = v;
+    }
+    const int64_t row = g0 + lane;
+    if (row < n) {
+      const double dot = first ? mydot : dots[row] + mydot;
+      if (!last) {
+        dots[row] = dot;
+      } else {
+        const double margin = fitIntercept ? offset + dot : dot;
+        const double w = weights ? weights[row] : 1.0;
+        const double m = bin_row(margin, w, labels[row], loss, wsum);
+        msum += m;
+        dots[row] = m;
+      }
+    }
+  }
+  if (!last) return;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    loss += __shfl_xor(loss, m);
+    wsum += __shfl_xor(wsum, m);
+    msum += __shfl_xor(msum, m);
+  }
+  if (lane == 0) {
+    slabS[gw * 3 + 0] = loss;
+    slabS[gw * 3 + 1] = wsum;
+    slabS[gw * 3 + 2] = msum;
+  }
+}
+
+// Pass 2 over one row block of the row-blocked CSC (csc.hip): 16 lanes per
+// column, products vals * mult[row] (the block's 2 MB multiplier slice stays
+// in L2), fixed 4-step butterfly, gradAcc[c] = (first ? 0 : gradAcc[c]) + s.
+// Deterministic: blocks in order, a block's rows in order within each lane.
+__global__ __launch_bounds__(256) void k_binlog_csc_grad_blk(
+    const int64_t* __restrict__ colptrB, const int32_t* __restrict__ rowidx,
+    const double* __restrict__ cvals, const double* __restrict__ mult, int F, int first,
+    double* __restrict__ gradAcc) {
+  // 16 lanes per group of 4 consecutive columns; the first 32 nonzeros of
+  // each column are loaded before any gather (all in flight at once)
+  const int sub = threadIdx.x & 15, lane = threadIdx.x & 63, gbase = lane & 48;
+  const int64_t c0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4) * 4;
+  const int64_t ci = c0 + (sub < 5 ? sub : 4);
+  const int64_t cp = colptrB[ci < F ? ci : (int64_t)F];
+  int64_t b[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) b[i] = __shfl(cp, gbase + i);
+  int ri[4][2];
+  double vv[4][2], mm[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int64_t q = b[i] + sub + 16 * it;
+      const bool ok = c0 + i < F && q < b[i + 1];
+      ri[i][it] = ok ? __builtin_nontemporal_load(rowidx + q) : -1;
+      vv[i][it] = ok ? __builtin_nontemporal_load(cvals + q) : 0.0;
+    }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int it = 0; it < 2; ++it) mm[i][it] = ri[i][it] >= 0 ? mult[ri[i][it]] : 0.0;
+  double sv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    double s = vv[i][0] * mm[i][0];
+    s += vv[i][1] * mm[i][1];
+    if (c0 + i < F)
+      for (int64_t q = b[i] + sub + 32; q < b[i + 1]; q += 16)
+        s += __builtin_nontemporal_load(cvals + q) * mult[__builtin_nontemporal_load(rowidx + q)];
+    s += __shfl_xor(s, 8);
+    s += __shfl_xor(s, 4);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 1);
+    sv[i] = s;
+  }
+  if (sub < 4 && c0 + sub < F) {
+    const double s = sub == 0 ? sv[0] : sub == 1 ? sv[1] : sub == 2 ? sv[2] : sv[3];
+    gradAcc[c0 + sub] = first ? s : gradAcc[c0 + sub] + s;
+  }
+}
+
 // Fold per-wave scalars in wave order: out3 = {loss, wsum, msum}.
 __global__ void k_fold_scalars(const double* __restrict__ slabS, int64_t waves, int width,
                                double* __restrict__ out) {
@@ -688,9 +825,9 @@ int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
   const int F = p->F;
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
-  const int64_t waves = std::min<int64_t>(16384, n);
+  const int64_t waves = csc ? std::min<int64_t>(8192, (n + 63) / 64) : std::min<int64_t>(16384, n);
   const int64_t rpw = (n + waves - 1) / waves;
-  const int64_t nw = (n + rpw - 1) / rpw;
+  const int64_t nw = csc ? waves : (n + rpw - 1) / rpw;
   const int64_t blocks = (nw + 3) / 4;
   const int64_t wtot = blocks * 4;
   if ((rc = p->gradAcc.reserve(sizeof(double) * (size_t)F)) ||
@@ -716,23 +853,35 @@ int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
     cyc_csc_arrays(csc, &colptr, &rowidx, &cvals);
   }
   if (csc) {
-    // Deterministic two-pass path: CSR margins -> mult, CSC column sums.
+    // Deterministic two-pass path: CSR margins -> mult, then the row-blocked
+    // CSC's column sums, one row block at a time.
     if ((rc = p->rowMult.reserve(sizeof(double) * (size_t)n))) return rc;
     {
+      int32_t S = 1, width = 0;
+      const int64_t* rowptrS = nullptr;
+      const int32_t* colS = nullptr;
+      const double* valS = nullptr;
+      cyc_csc_slices(csc, &S, &width, &rowptrS, &colS, &valS);
       cyc::KernelTimer timer("k_binlog_csr", st);
-      hipLaunchKernelGGL(k_binlog_csr_mult, dim3((unsigned)blocks), dim3(256), 0, st, rowptr,
-                         colidx, vals, labels, weights, n, coef, p->fitIntercept, offset, rpw,
-                         (double*)p->rowMult.ptr, (double*)p->slabS.ptr);
-      CYC_LAUNCH_CHECK("k_binlog_csr_mult");
+      for (int sl = 0; sl < S; ++sl) {
+        const int64_t* rp = S > 1 ? rowptrS + (int64_t)sl * n : rowptr;
+        hipLaunchKernelGGL(k_binlog_csr_mult8, dim3((unsigned)blocks), dim3(256), 0, st, rp,
+                           S > 1 ? colS : colidx, S > 1 ? valS : vals, labels, weights, n, coef,
+                           p->fitIntercept, offset, sl == 0 ? 1 : 0, sl == S - 1 ? 1 : 0,
+                           (double*)p->rowMult.ptr, (double*)p->slabS.ptr);
+      }
+      CYC_LAUNCH_CHECK("k_binlog_csr_mult8");
     }
-    const int64_t cwaves = std::min<int64_t>(65536, F);
-    const int cpw = (int)((F + cwaves - 1) / cwaves);
-    const int64_t cblocks = ((F + cpw - 1) / cpw + 3) / 4;
+    int64_t rpb = 0, nb = 0;
+    cyc_csc_blocks(csc, &rpb, &nb);
+    const unsigned cgrid = (unsigned)((((int64_t)F + 3) / 4 * 16 + 255) / 256);
     cyc::KernelTimer timer("k_binlog_csc_grad", st);
-    hipLaunchKernelGGL(k_binlog_csc_grad, dim3((unsigned)cblocks), dim3(256), 0, st,
-                       colptr, rowidx, cvals, (const double*)p->rowMult.ptr, F, cpw,
-                       (double*)p->gradAcc.ptr);
-    CYC_LAUNCH_CHECK("k_binlog_csc_grad");
+    for (int64_t b = 0; b < nb; ++b) {
+      hipLaunchKernelGGL(k_binlog_csc_grad_blk, dim3(cgrid), dim3(256), 0, st,
+                         colptr + b * F, rowidx, cvals, (const double*)p->rowMult.ptr, F,
+                         b == 0 ? 1 : 0, (double*)p->gradAcc.ptr);
+    }
+    CYC_LAUNCH_CHECK("k_binlog_csc_grad_blk");
   } else {
     CYC_HIP(hipMemsetAsync(p->gradAcc.ptr, 0, sizeof(double) * (size_t)F, st));
     cyc::KernelTimer timer("k_binlog_csr", st);

@@ -162,14 +162,25 @@ typedef struct cyc_logistic_plan_s* cyc_logistic_plan;
 /* Column-major copy of a resident CSR shard, built once (outside the
  * training loop, like InstanceBlock.blokifyWithMaxMemUsage,
  * ml/feature/Instance.scala:146-187) by a stable sort of the nonzeros by
- * column.  Passing it to cyc_binary_logistic_add_csr_dev replaces the
- * gradient's fp64-atomic scatter by per-column sums (deterministic, each
- * column's rows in the reference's order).  Costs 12 bytes per nonzero. */
+ * (row block, column).  Passing it to cyc_binary_logistic_add_csr_dev
+ * replaces the gradient's fp64-atomic scatter by per-column sums
+ * (deterministic: blocks in order, each block's rows in order).  Costs 12
+ * bytes per nonzero + 8 bytes per (row block, column). */
 typedef struct cyc_csc_s* cyc_csc;
 int cyc_csc_build_dev(const int64_t* rowptr, const int32_t* colidx, const double* vals,
                       int64_t n, int32_t numFeatures, void* stream, cyc_csc* out);
 int cyc_csc_destroy(cyc_csc csc);
 int64_t cyc_csc_rows(cyc_csc csc);
+/* The copy is row-blocked (rows_per_block rows per block): colptr has
+ * nblocks * numFeatures + 1 entries, block b / column c spanning
+ * [colptr[b F + c], colptr[b F + c + 1]) of rowidx / values. */
+int cyc_csc_blocks(cyc_csc csc, int64_t* rows_per_block, int64_t* nblocks);
+/* For numFeatures > 2^18 the handle also holds a column-sliced CSR copy
+ * (nslices slices of `width` columns, each a CSR over all rows: rowptrS has
+ * nslices * n + 1 entries) that the margin pass walks slice by slice so the
+ * gathered coefficients stay in L2.  nslices == 1: no sliced copy. */
+int cyc_csc_slices(cyc_csc csc, int32_t* nslices, int32_t* width, const int64_t** rowptrS,
+                   const int32_t** colS, const double** valS);
 int cyc_csc_arrays(cyc_csc csc, const int64_t** colptr, const int32_t** rowidx,
                    const double** values);
 

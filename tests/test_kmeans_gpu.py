@@ -405,8 +405,36 @@ def test_rows_image_guard(cuda):
     p = KMeansPlan(16, 4, 100)
     p.stats(C)
     rows = p.rows(X)
-    assert rows.nbytes == 100 * 3 * 64 + 100 * 8
+    assert rows.nbytes == 100 * 3 * 128 + 100 * 8
     a = torch.empty(100, dtype=torch.int32, device=cuda)
     c = torch.empty(100, dtype=torch.float64, device=cuda)
     with pytest.raises(N.IllegalArgumentException, match="row image"):
         p.assign(X[:50], row_norms(X[:50]), C, row_norms(C), a, c, rows=rows)
+
+
+@pytest.mark.parametrize("n,d,k,weighted", [(5000, 16, 12, False), (20000, 256, 64, True),
+                                            (3000, 300, 7, True), (2000, 700, 5, False)])
+def test_lloyd_iteration_no_row_costs(cuda, n, d, k, weighted):
+    """accumulate without per-row outputs (the training loop's call): the
+    streaming cluster-sum pass folds w (c - x)^2 per dimension; sums, weights
+    and centers as with row costs, the cost total within 1e-12 relative."""
+    import torch
+    from cycloneml_amd.clustering import row_norms
+    rng = np.random.default_rng(n + k + 1)
+    X = rng.normal(size=(n, d)) + rng.integers(0, 5, size=(n, 1)) * 3.0
+    C = X[rng.choice(n, size=k, replace=False)].copy()
+    w = rng.uniform(0.5, 2.0, size=n) if weighted else None
+    ref = oracle.kmeans_iteration(X, oracle.row_norms(X), w, C, oracle.row_norms(C))
+    Xd, Cd = _dev(X, cuda), _dev(C, cuda)
+    wd = None if w is None else _dev(w, cuda)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = _plan(d, k, n)
+    sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+    wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+    cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+    p.accumulate(Xd, xn, wd, Cd, cn, sums, wsum, cost, rows=p.rows(Xd))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(wsum.cpu().numpy(), ref["wsum"], rtol=1e-12)
+    np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
+                               atol=1e-10 * np.abs(ref["sums"]).max())
+    assert abs(cost.item() - ref["cost"]) <= 1e-12 * abs(ref["cost"])
