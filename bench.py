@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 
 FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 (vector = matrix) spec, BASELINE.md section 2
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
+I8_PEAK_TOPS = 5000.0     # dense i8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md)
 
 DEFAULT_ROWS = {"kmeans": 10_000_000, "gramian": 12_500_000, "lr_multi": 6_250_000,
                 "lr_sparse": 25_000_000}
@@ -53,17 +54,19 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(name):
-    """HBM bytes per launch of `name` from the committed rocprofv3 --pmc summary
-    (profiles/*_pmc.json written by tools/pmc_summary.py), scaled to this
-    run's rows when the profile was taken at another size; else None."""
+def pmc_traffic(workload, kernels, launches_per_step, rows):
+    """HBM bytes per timed launch of the dominant kernel, from the latest
+    committed rocprofv3 --pmc summary of this workload
+    (profiles/r<NN>_<workload>_pmc.json, tools/pmc_summary.py: separate
+    FETCH_SIZE / WRITE_SIZE passes, gfx950 corrections applied there), scaled
+    to this run's rows; (None, None) when there is none."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            if name in d and d[name].get("hbm_bytes_per_launch"):
-                return d[name]["hbm_bytes_per_launch"], d.get("_rows_per_launch")
+            per_step = sum(d[k]["hbm_bytes_per_step"] for k in kernels)
+            return per_step / launches_per_step * rows / d["_rows"], os.path.basename(f)
         except Exception:
             continue
     return None, None
@@ -84,8 +87,15 @@ def timed_parallel(fn, parts, threads):
 # ---------------------------------------------------------------- workloads
 
 class KMeansWorkload:
+    """The dominant kernel is the exact-integer i8 screen (k_screen, timed as
+    k_kmeans_assign): its work is 6 i8 limb products of 2 x 64 ops per
+    (row, padded center, 64-dim step), priced against the dense i8 MFMA peak;
+    the fp64-equivalent rate (2 k d flop per row) is reported beside it."""
     kernel = "k_kmeans_assign"
+    pmc_kernels = ("k_screen",)
     bound = "mfma"
+    unit = "TOPS"
+    peak = I8_PEAK_TOPS
 
     def __init__(self, n, dev, rank):
         import torch
@@ -133,7 +143,16 @@ class KMeansWorkload:
         self.plan.update(self.C, self.cnorm, sums, wsum, 1e-4, self.conv)
 
     def work_per_launch(self, launches_per_step):
-        return 2.0 * self.k * self.d * self.n / launches_per_step   # flops
+        D = 128 * ((self.d + 127) // 128)                 # 64-dim steps, even count
+        kpad = 16 * (((self.k + 15) // 16 + 3) // 4 * 4)  # 16-center tiles, 4 waves
+        return 12.0 * D * kpad * self.n / launches_per_step   # i8 ops
+
+    def extra_roofline(self, launches_per_step, avg_s):
+        flops = 2.0 * self.k * self.d * self.n / launches_per_step
+        return {"algorithmic_fp64_flop_per_launch": flops,
+                "fp64_equivalent_tflops": flops / avg_s / 1e12,
+                "note": "i8 ops = exact 3-limb integer screen (6 MFMA limb products); "
+                        "fp64-equivalent = 2kd flop/row over the same time"}
 
     def describe(self):
         return (f"KMeans k={self.k} Lloyd iteration, dense fp64 {self.n} x {self.d} rows per GPU "
@@ -168,6 +187,7 @@ class KMeansWorkload:
 
 class GramianWorkload:
     kernel = "k_gram_tiles"
+    pmc_kernels = ("k_gram_tiles",)
     bound = "mfma"
 
     def __init__(self, n, dev, rank):
@@ -215,8 +235,9 @@ class GramianWorkload:
 
 
 class LRMultiWorkload:
-    kernel = "k_mlr_grad"
+    kernel = "k_mlr_margins"
     kernels = ("k_mlr_margins", "k_mlr_grad")
+    pmc_kernels = ("k_mlr_margins",)
     bound = "mfma"
 
     def __init__(self, n, dev, rank):
@@ -284,8 +305,12 @@ class LRMultiWorkload:
 
 
 class LRSparseWorkload:
+    """Roofline on the margin pass (timed as k_binlog_csr; the slices'
+    k_binlog_csr_mult8 launches), whose read set is exactly SURVEY 8(d)'s
+    784 B/row; the gradient pass (k_binlog_csc_grad) is listed beside it."""
     kernel = "k_binlog_csr"
     kernels = ("k_binlog_csr", "k_binlog_csc_grad")
+    pmc_kernels = ("k_binlog_csr_mult8",)
     bound = "hbm"
 
     def __init__(self, n, dev, rank):
@@ -418,14 +443,16 @@ def main():
     per_launch = wl.work_per_launch(launches / args.steps) if launches else 0.0
     achieved = per_launch / avg_s if launches else None
     if wl.bound == "mfma":
-        unit, peak = "TFLOP/s", FP64_PEAK_TFLOPS
+        unit = getattr(wl, "unit", "TFLOP/s")
+        peak = getattr(wl, "peak", FP64_PEAK_TFLOPS)
         achieved = achieved / 1e12 if achieved else None
     else:
         unit, peak = "GB/s", HBM_PEAK_GBS
         achieved = achieved / 1e9 if achieved else None
-    traffic, prof_rows = pmc_traffic(wl.kernel)
-    if traffic and prof_rows:
-        traffic = traffic * (n / (prof_rows))
+    traffic, traffic_src = (pmc_traffic(args.workload, wl.pmc_kernels, launches / args.steps, n)
+                            if launches else (None, None))
+    extra = wl.extra_roofline(launches / args.steps, avg_s) if (
+        launches and hasattr(wl, "extra_roofline")) else {}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -450,10 +477,11 @@ def main():
             "roofline": {"kernel": wl.kernel, "bound": wl.bound, "achieved": achieved,
                          "peak": peak, "unit": unit,
                          "frac": (achieved / peak) if achieved else None,
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "avg_launch_ms": avg_s * 1e3, "launches": launches,
                          "work_per_launch": per_launch,
-                         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()}},
+                         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
+                         **extra},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -57,6 +57,35 @@ int build_csc(const int64_t* rowptr, const int32_t* colidx, const double* vals, 
 // Fixed-margin round-up.
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// Compute units of the current device (256 on MI355X), for grid sizing.
+inline int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  return cus;
+}
+
+// Split count s in [lo, hi] for a grid of per x s workgroups that runs
+// `slots` at a time: the s whose last round is fullest (ties: the smallest),
+// so a split-K launch has no near-empty tail round.
+inline int64_t balanced_splits(int64_t per, int64_t lo, int64_t hi, int64_t slots) {
+  if (hi < lo) hi = lo;
+  int64_t best = lo;
+  double bestEff = -1.0;
+  for (int64_t s = lo; s <= hi; ++s) {
+    const int64_t wgs = per * s;
+    const int64_t rounds = (wgs + slots - 1) / slots;
+    const double eff = (double)wgs / (double)(rounds * slots);
+    if (eff > bestEff + 1e-9) {
+      bestEff = eff;
+      best = s;
+    }
+  }
+  return best;
+}
+
 }  // namespace cyc
 
 #define CYC_HIP(expr)                                                     \

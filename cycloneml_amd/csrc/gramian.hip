@@ -244,8 +244,13 @@ int cyc_gramian_accumulate_dev(cyc_gramian_plan plan, const double* X, int64_t n
   const int p = plan->p;
   const int tps = (p + TILE - 1) / TILE;
   const int pairs = tps * (tps + 1) / 2;
-  // split-K: aim for >= 2048 workgroups, at least 64 rows per split
-  int64_t splits = std::max<int64_t>(1, (2048 + pairs - 1) / pairs);
+  // split-K: at least 4 rounds of workgroups (2 per CU) and at least 64 rows
+  // per split, with the split count whose last round is fullest (36 tile
+  // pairs x 57 splits = 2052 workgroups ran 5 rounds, the 5th holding 4;
+  // 36 x 71 = 2556 fill 4.99 rounds).
+  const int64_t slots = 2 * (int64_t)cyc::device_cus();
+  const int64_t lo = std::max<int64_t>(1, (4 * slots + pairs - 1) / pairs);
+  int64_t splits = cyc::balanced_splits(pairs, lo, 2 * lo, slots);
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, nrows / 64));
   int64_t rps = cyc::round_up((nrows + splits - 1) / splits, KC);
   splits = (nrows + rps - 1) / rps;

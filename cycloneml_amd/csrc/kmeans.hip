@@ -77,29 +77,96 @@ __global__ void k_center_transpose(const double* __restrict__ C, int k, int d, i
   Ct[idx] = (i < k && j < d) ? C[(int64_t)i * d + j] : 0.0;
 }
 
-// computeStatistics pairs (DistanceMeasure.scala:55-66, Euclidean :275-277):
-// s = 0.25 * distance * distance, distance = Math.sqrt(sqdist(c_i, c_j)).
-__global__ void k_stats_pairs(const double* __restrict__ C, int k, int d,
-                              double* __restrict__ packed) {
-  int i = blockIdx.y * 16 + threadIdx.y;
-  int j = blockIdx.x * 16 + threadIdx.x;
-  if (i >= k || j >= k || j <= i) return;
-  double dist = __builtin_sqrt(seq_sqdist(C + (int64_t)i * d, C + (int64_t)j * d, d));
-  packed[iut(i, j)] = dmul(dmul(0.25, dist), dist);
+constexpr unsigned long long kInfBits = 0x7FF0000000000000ull;   // +Infinity
+constexpr int kStT = 32;    // centers per statistics tile side
+constexpr int kStC = 32;    // dimensions per LDS chunk of the statistics
+
+__global__ void k_fill_u64(unsigned long long* __restrict__ p, int n, unsigned long long v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
 }
 
-// diag(i) = min over j != i (DistanceMeasure.scala:62-72); min is order free.
-__global__ void k_stats_diag(int k, double* __restrict__ packed) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= k) return;
-  if (k == 1) { packed[0] = __builtin_nan(""); return; }
-  double m = __builtin_inf();
-  for (int j = 0; j < k; ++j) {
-    if (j == i) continue;
-    double s = packed[iut(i, j)];
-    if (s < m) m = s;
+// computeStatistics pairs (DistanceMeasure.scala:55-66, Euclidean :275-277):
+// s = 0.25 * distance * distance, distance = Math.sqrt(sqdist(c_i, c_j)).
+// One workgroup per 32 x 32 tile of the upper block triangle: 32-dimension
+// chunks of both center tiles in LDS, 2 x 2 pairs per thread, every pair's
+// sum sequential over the dimensions in order (bit-exact).  The row minima
+// of the diagonal (:62-63) go to dmin as fp64 bit patterns: a statistic is
+// >= +0 or NaN, and for those the unsigned bit order is the value order with
+// every NaN above +Infinity, so atomicMin never keeps a NaN -- just as the
+// reference's `if (s < diagValues(i))` skips it.
+__global__ __launch_bounds__(256) void k_stats_pairs(const double* __restrict__ C, int k, int d,
+                                                     int tps, double* __restrict__ packed,
+                                                     unsigned long long* __restrict__ dmin) {
+  __shared__ double Ci[kStT][kStC + 1], Cj[kStT][kStC + 1];
+  __shared__ unsigned long long rmin[kStT], cmin[kStT];
+  int t = blockIdx.x, bi = 0;
+  while (t >= tps - bi) {
+    t -= tps - bi;
+    ++bi;
   }
-  packed[iut(i, i)] = m;
+  const int bj = bi + t;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  if (threadIdx.x < kStT) rmin[threadIdx.x] = cmin[threadIdx.x] = kInfBits;
+  double s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
+  for (int c0 = 0; c0 < d; c0 += kStC) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < kStT * kStC; e += 256) {
+      const int r = e >> 5, cc = e & 31, col = c0 + cc;
+      const int gi = bi * kStT + r, gj = bj * kStT + r;
+      Ci[r][cc] = (gi < k && col < d) ? C[(int64_t)gi * d + col] : 0.0;
+      Cj[r][cc] = (gj < k && col < d) ? C[(int64_t)gj * d + col] : 0.0;
+    }
+    __syncthreads();
+    const int lim = min(kStC, d - c0);
+    for (int cc = 0; cc < lim; ++cc) {
+      const double a0 = Ci[ty][cc], a1 = Ci[ty + 16][cc];
+      const double b0 = Cj[tx][cc], b1 = Cj[tx + 16][cc];
+      double q = dsub(a0, b0);
+      s00 = dadd(s00, dmul(q, q));
+      q = dsub(a0, b1);
+      s01 = dadd(s01, dmul(q, q));
+      q = dsub(a1, b0);
+      s10 = dadd(s10, dmul(q, q));
+      q = dsub(a1, b1);
+      s11 = dadd(s11, dmul(q, q));
+    }
+  }
+  const double sv[2][2] = {{s00, s01}, {s10, s11}};
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int i = bi * kStT + ty + 16 * a, j = bj * kStT + tx + 16 * b;
+      if (i < k && j < k && j > i) {
+        const double dist = __builtin_sqrt(sv[a][b]);
+        const double v = dmul(dmul(0.25, dist), dist);
+        packed[iut(i, j)] = v;
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+        atomicMin(&rmin[ty + 16 * a], bits);
+        atomicMin(&cmin[tx + 16 * b], bits);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kStT) {
+    const int i = bi * kStT + threadIdx.x, j = bj * kStT + threadIdx.x;
+    if (i < k && rmin[threadIdx.x] != kInfBits) atomicMin(&dmin[i], rmin[threadIdx.x]);
+    if (j < k && cmin[threadIdx.x] != kInfBits) atomicMin(&dmin[j], cmin[threadIdx.x]);
+  }
+}
+
+// diagonal (:69-74): packed(i, i) = min over j != i (+Infinity when every
+// statistic of the row is NaN); k == 1 gives the single NaN of :50.
+__global__ void k_stats_diag(int k, double* __restrict__ packed,
+                             const unsigned long long* __restrict__ dmin) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  if (k == 1) {
+    packed[0] = __builtin_nan("");
+    return;
+  }
+  packed[iut(i, i)] = __longlong_as_double((long long)dmin[i]);
 }
 
 // --------------------------------------------------------------- assign
@@ -962,18 +1029,47 @@ __global__ void k_hist(const int32_t* __restrict__ assign, int64_t n, int k,
   for (int c = threadIdx.x; c < k; c += blockDim.x) hist[(int64_t)blockIdx.x * k + c] = cnt[c];
 }
 
-// Per cluster: exclusive running offset over tiles (in place) and the total.
-__global__ void k_scan_tiles(int32_t* __restrict__ hist, int tiles, int k,
-                             int64_t* __restrict__ total) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
+// Per cluster: exclusive running offset over the tiles (in place) and the
+// total, as a segmented scan (integer sums: any grouping gives the same
+// offsets).  1. per (tile segment, cluster) sums; 2. per cluster, the
+// segments' exclusive offsets and the total; 3. the offsets inside segments.
+constexpr int kScanSegs = 64;
+
+__global__ void k_scan_seg(const int32_t* __restrict__ hist, int tiles, int k, int segT,
+                           int32_t* __restrict__ segsum) {
+  const int c = blockIdx.x * 64 + threadIdx.x, s = blockIdx.y;
+  if (c >= k) return;
+  const int t0 = s * segT, t1 = min(tiles, t0 + segT);
+  int sum = 0;
+#pragma unroll 8
+  for (int t = t0; t < t1; ++t) sum += hist[(int64_t)t * k + c];
+  segsum[(int64_t)s * k + c] = sum;
+}
+
+__global__ void k_scan_segoff(int32_t* __restrict__ segsum, int segs, int k,
+                              int64_t* __restrict__ total) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= k) return;
   int64_t run = 0;
-  for (int t = 0; t < tiles; ++t) {
-    int32_t h = hist[(int64_t)t * k + c];
-    hist[(int64_t)t * k + c] = (int32_t)run;
+  for (int s = 0; s < segs; ++s) {
+    const int32_t h = segsum[(int64_t)s * k + c];
+    segsum[(int64_t)s * k + c] = (int32_t)run;
     run += h;
   }
   total[c] = run;
+}
+
+__global__ void k_scan_apply(int32_t* __restrict__ hist, int tiles, int k, int segT,
+                             const int32_t* __restrict__ segoff) {
+  const int c = blockIdx.x * 64 + threadIdx.x, s = blockIdx.y;
+  if (c >= k) return;
+  const int t0 = s * segT, t1 = min(tiles, t0 + segT);
+  int32_t run = segoff[(int64_t)s * k + c];
+  for (int t = t0; t < t1; ++t) {
+    const int32_t h = hist[(int64_t)t * k + c];
+    hist[(int64_t)t * k + c] = run;
+    run += h;
+  }
 }
 
 // Single block: cluster start offsets and chunk start offsets (exclusive scans).
@@ -1303,19 +1399,36 @@ __global__ void k_reduce_clusters(const double* __restrict__ part, const double*
     if (threadIdx.x == 0) ccost[c] = 0.0;
     return;
   }
+  // chunk order kept; 8 chunks' loads in flight per step
   for (int j = threadIdx.x; j < d; j += blockDim.x) {
     double s = 0.0;
-    for (int64_t ch = a; ch < b; ++ch) s = dadd(s, part[ch * d + j]);
+    int64_t ch = a;
+    for (; ch + 8 <= b; ch += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(ch + u) * d + j];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s = dadd(s, v[u]);
+    }
+    for (; ch < b; ++ch) s = dadd(s, part[ch * d + j]);
     sums[(int64_t)c * d + j] = dadd(sums[(int64_t)c * d + j], s);
   }
-  if (threadIdx.x == 0) {
-    double sw = 0.0, sc = 0.0;
-    for (int64_t ch = a; ch < b; ++ch) {
-      sw = dadd(sw, pw[ch]);
-      sc = dadd(sc, pc[ch]);
+  // the weight and cost folds on two other waves
+  const int tw = 64 % blockDim.x, tc = 128 % blockDim.x;
+  if (threadIdx.x == tw || threadIdx.x == tc) {
+    const double* src = threadIdx.x == tw ? pw : pc;
+    double s = 0.0;
+    int64_t ch = a;
+    for (; ch + 8 <= b; ch += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[ch + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s = dadd(s, v[u]);
     }
-    wsum[c] = dadd(wsum[c], sw);
-    ccost[c] = sc;
+    for (; ch < b; ++ch) s = dadd(s, src[ch]);
+    if (threadIdx.x == tw) wsum[c] = dadd(wsum[c], s);
+    else ccost[c] = s;
   }
 }
 
@@ -1334,34 +1447,37 @@ __global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __
 }
 
 // centroid (DistanceMeasure.scala:200-203: scal(1/w, sum); new VectorWithNorm)
-// and isCenterConverged (:345-350).  Single block of 1024 threads.
-__global__ void k_update_centers(double* __restrict__ C, double* __restrict__ cnorm,
-                                 const double* __restrict__ sums, const double* __restrict__ wsum,
-                                 int k, int d, double eps2, int32_t* __restrict__ converged) {
-  __shared__ int s_ok;
-  if (threadIdx.x == 0) s_ok = 1;
+// and isCenterConverged (:345-350).  One 64-lane workgroup per center: the
+// elementwise part in parallel, then lane 0 runs the two sequential sums (the
+// moved distance and the new norm, in index order) from LDS.  The caller sets
+// *converged = 1 first; a center that moved clears it.
+__global__ __launch_bounds__(64) void k_update_centers(
+    double* __restrict__ C, double* __restrict__ cnorm, const double* __restrict__ sums,
+    const double* __restrict__ wsum, int k, int d, double eps2, int32_t* __restrict__ converged) {
+  extern __shared__ double upd[];   // 2 d
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const double w = wsum[c];
+  if (!(w > 0)) return;
+  const double a = 1.0 / w;
+  double* crow = C + (int64_t)c * d;
+  const double* srow = sums + (int64_t)c * d;
+  for (int j = lane; j < d; j += 64) {
+    const double v = dmul(a, srow[j]);
+    const double sc = dsub(v, crow[j]);
+    upd[j] = dmul(sc, sc);
+    upd[d + j] = dmul(v, v);
+    crow[j] = v;
+  }
   __syncthreads();
-  int ok = 1;
-  for (int c = threadIdx.x; c < k; c += blockDim.x) {
-    const double w = wsum[c];
-    if (!(w > 0)) continue;
-    const double a = 1.0 / w;
-    double* crow = C + (int64_t)c * d;
-    const double* srow = sums + (int64_t)c * d;
+  if (lane == 0) {
     double moved = 0.0, nn = 0.0;
     for (int j = 0; j < d; ++j) {
-      const double v = dmul(a, srow[j]);
-      const double sc = dsub(v, crow[j]);
-      moved = dadd(moved, dmul(sc, sc));
-      nn = dadd(nn, dmul(v, v));
-      crow[j] = v;
+      moved = dadd(moved, upd[j]);
+      nn = dadd(nn, upd[d + j]);
     }
     cnorm[c] = __builtin_sqrt(nn);
-    if (!(moved <= eps2)) ok = 0;
+    if (!(moved <= eps2) && converged) atomicAnd(converged, 0);
   }
-  if (!ok) atomicAnd(&s_ok, 0);
-  __syncthreads();
-  if (threadIdx.x == 0 && converged) *converged = s_ok;
 }
 
 }  // namespace
@@ -1386,7 +1502,7 @@ struct cyc_kmeans_plan_s {
   int64_t max_rows = 0;
   size_t assignLds = 0;
   std::mutex mu;
-  cyc::DeviceBuffer ct, stats, slowList, slowCount, assignTmp, costTmp;
+  cyc::DeviceBuffer ct, stats, dmin, segsum, slowList, slowCount, assignTmp, costTmp;
   cyc::DeviceBuffer hist, total, cstart, chunkStart, perm, part, pw, pc, ccost;
 };
 
@@ -1467,11 +1583,15 @@ int do_stats(cyc_kmeans_plan p, const double* C, hipStream_t st) {
                        st, C, k, d, p->d4, p->kpad, (double*)p->ct.ptr);
     CYC_LAUNCH_CHECK("k_center_transpose");
   }
-  dim3 g((k + 15) / 16, (k + 15) / 16);
-  hipLaunchKernelGGL(k_stats_pairs, g, dim3(16, 16), 0, st, C, k, d, (double*)p->stats.ptr);
+  const int tps = (k + kStT - 1) / kStT;
+  unsigned long long* dmin = (unsigned long long*)p->dmin.ptr;
+  hipLaunchKernelGGL(k_fill_u64, dim3((k + 255) / 256), dim3(256), 0, st, dmin, k, kInfBits);
+  CYC_LAUNCH_CHECK("k_fill_u64");
+  hipLaunchKernelGGL(k_stats_pairs, dim3((unsigned)(tps * (tps + 1) / 2)), dim3(256), 0, st, C, k,
+                     d, tps, (double*)p->stats.ptr, dmin);
   CYC_LAUNCH_CHECK("k_stats_pairs");
   hipLaunchKernelGGL(k_stats_diag, dim3((k + 255) / 256), dim3(256), 0, st, k,
-                     (double*)p->stats.ptr);
+                     (double*)p->stats.ptr, (const unsigned long long*)dmin);
   CYC_LAUNCH_CHECK("k_stats_diag");
   return CYC_OK;
 }
@@ -1672,6 +1792,7 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
   }
   if ((rc = p->ct.reserve(sizeof(double) * (size_t)p->d4 * p->kpad)) ||
       (rc = p->stats.reserve(sizeof(double) * ((size_t)k * (k + 1) / 2))) ||
+      (rc = p->dmin.reserve(sizeof(unsigned long long) * (size_t)k)) ||
       (rc = p->slowCount.reserve(64)) || (rc = ensure_rows(p, std::max<int64_t>(max_rows, 1)))) {
     delete p;
     return rc;
@@ -1813,9 +1934,21 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   int32_t* hist = (int32_t*)p->hist.ptr;
   hipLaunchKernelGGL(k_hist, dim3(tiles), dim3(256), sizeof(int32_t) * k, st, assign, n, k, hist);
   CYC_LAUNCH_CHECK("k_hist");
-  hipLaunchKernelGGL(k_scan_tiles, dim3((k + 255) / 256), dim3(256), 0, st, hist, tiles, k,
-                     (int64_t*)p->total.ptr);
-  CYC_LAUNCH_CHECK("k_scan_tiles");
+  {
+    const int segT = (tiles + std::min(kScanSegs, tiles) - 1) / std::min(kScanSegs, tiles);
+    const int segs = (tiles + segT - 1) / segT;
+    if ((rc = p->segsum.reserve(sizeof(int32_t) * (size_t)segs * k))) return rc;
+    int32_t* segsum = (int32_t*)p->segsum.ptr;
+    hipLaunchKernelGGL(k_scan_seg, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0, st,
+                       (const int32_t*)hist, tiles, k, segT, segsum);
+    CYC_LAUNCH_CHECK("k_scan_seg");
+    hipLaunchKernelGGL(k_scan_segoff, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, st, segsum,
+                       segs, k, (int64_t*)p->total.ptr);
+    CYC_LAUNCH_CHECK("k_scan_segoff");
+    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0,
+                       st, hist, tiles, k, segT, (const int32_t*)segsum);
+    CYC_LAUNCH_CHECK("k_scan_apply");
+  }
   hipLaunchKernelGGL(k_scan_clusters, dim3(1), dim3(1024), 0, st, (const int64_t*)p->total.ptr, k,
                      (int64_t*)p->cstart.ptr, (int64_t*)p->chunkStart.ptr);
   CYC_LAUNCH_CHECK("k_scan_clusters");
@@ -1868,8 +2001,11 @@ int cyc_kmeans_update_dev(cyc_kmeans_plan p, double* C, double* cnorm, const dou
   CYC_REQUIRE(p != nullptr, "plan must not be null");
   CYC_REQUIRE(epsilon >= 0, "epsilon must be nonnegative");
   std::lock_guard<std::mutex> g(p->mu);
-  hipLaunchKernelGGL(k_update_centers, dim3(1), dim3(1024), 0, cyc::as_stream(stream), C, cnorm,
-                     sums, wsum, p->k, p->d, epsilon * epsilon, converged_out);
+  hipStream_t st = cyc::as_stream(stream);
+  if (converged_out) CYC_HIP(hipMemsetD32Async((hipDeviceptr_t)converged_out, 1, 1, st));
+  hipLaunchKernelGGL(k_update_centers, dim3((unsigned)p->k), dim3(64),
+                     sizeof(double) * 2 * (size_t)p->d, st, C, cnorm, sums, wsum, p->k, p->d,
+                     epsilon * epsilon, converged_out);
   CYC_LAUNCH_CHECK("k_update_centers");
   return CYC_OK;
 }

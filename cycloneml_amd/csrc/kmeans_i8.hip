@@ -280,7 +280,7 @@ __device__ __forceinline__ v4i as_v4i(uint4 u) { return __builtin_bit_cast(v4i, 
 // 12 KS + 2 16-byte chunks (== 2 mod 4: conflict-free ds_read_b128 fragment
 // reads); B fragments come from L2 one 64-dim step ahead.
 template <int KS>
-__global__ __launch_bounds__(256, 2) void k_screen(
+__global__ __launch_bounds__(256, KS <= 4 ? 3 : 2) void k_screen(
     const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
     int64_t n, int d, const uint4* __restrict__ Cb, const float* __restrict__ cq,
     const double* __restrict__ g, const double* __restrict__ cnorm,
@@ -289,10 +289,12 @@ __global__ __launch_bounds__(256, 2) void k_screen(
   constexpr int BM = kBM, W = kWaves, CH = 12 * KS, STR = CH + 2;
   extern __shared__ __attribute__((aligned(16))) uint4 smem8[];
   uint4* As = smem8;                          // BM x STR chunks
-  float* mL1 = (float*)(As + BM * STR);       // W x BM
+  int* exS = (int*)(As + BM * STR);           // BM
+  // after the main loop the row image is dead: the per-wave slot minima
+  // reuse it (3 KB), so d <= 256 fits three workgroups per CU
+  float* mL1 = (float*)As;                    // W x BM
   float* mL2 = mL1 + W * BM;                  // W x BM
   int* mI1 = (int*)(mL2 + W * BM);            // W x BM
-  int* exS = mI1 + W * BM;                    // BM
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -421,10 +423,12 @@ __global__ __launch_bounds__(256, 2) void k_screen(
         const int T = acc[ta][0][r] * 128 + acc[ta][1][r];
         const float V = __builtin_fmaf((float)acc[ta][2][r], 0x1p-7f, (float)T);
         const float L = __builtin_fmaf(-F1[q], V, cqv);
+        // two smallest with sL1 <= sL2: the median of (sL1, sL2, L) is the
+        // new second smallest
         const bool lt = L < sL1[q];
-        sL2[q] = lt ? sL1[q] : __builtin_fminf(sL2[q], L);
+        sL2[q] = __builtin_amdgcn_fmed3f(sL1[q], sL2[q], L);
         sI1[q] = lt ? c : sI1[q];
-        sL1[q] = lt ? L : sL1[q];
+        sL1[q] = __builtin_fminf(sL1[q], L);
       }
     }
   }
@@ -443,6 +447,7 @@ __global__ __launch_bounds__(256, 2) void k_screen(
       sL1[q] = take ? oL1 : sL1[q];
     }
   }
+  __syncthreads();   // every wave is done reading the row image (mL1.. alias it)
   if ((lane & 15) == 0) {
 #pragma unroll
     for (int ta = 0; ta < 4; ++ta) {
@@ -501,7 +506,7 @@ int launch_screen(const void* img, const int2* meta, const double* xnorm, int64_
                   const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
                   unsigned int* listCount, hipStream_t st) {
   constexpr int STR = 12 * KS + 2;
-  const size_t lds = (size_t)kBM * STR * 16 + (size_t)kWaves * kBM * 12 + (size_t)kBM * 4;
+  const size_t lds = (size_t)kBM * STR * 16 + (size_t)kBM * 4;   // slot minima alias the image
   static bool attr = false;
   if (!attr) {
     CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_screen<KS>),

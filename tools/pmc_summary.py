@@ -1,23 +1,31 @@
 #!/usr/bin/env python3
-"""Summarise a tools/prof.sh run into profiles/<tag>_pmc.json.
+"""Summarise a tools/prof.sh run into profiles/<prefix>_pmc.json and
+profiles/<prefix>_kernel_stats.csv.
 
-Per kernel: mean duration (kernel trace), mean FETCH_SIZE / WRITE_SIZE (KB,
-from the two separate --pmc passes) and hbm_bytes_per_launch.
+Per kernel (rocprofv3 -T names): calls and mean duration (kernel trace +
+--stats), the mean FETCH_SIZE / WRITE_SIZE per dispatch from the two
+separate --pmc passes (KB), and HBM bytes per dispatch and per step.
 
-gfx950 correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE reads exactly half
-the bytes of a wide (16 B/lane) coalesced stream.  Our streaming kernels load
-8 B per lane; for those the counter was calibrated against the known byte
-count of the assign kernel's X stream (20.48 GB per launch at 10M x 256
-reads as 19.1e6 KB, i.e. unhalved), so no factor is applied.  WRITE_SIZE is
-exact for streaming stores.  Both are per launch, like roofline.achieved.
+gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE reads exactly half
+the bytes of a 16-B-per-lane streaming read, so it is doubled for kernels
+whose stream is 16 B per lane (FETCH_X2).  8-B-per-lane streams were
+calibrated on a known byte count (the fp64 X stream of 10M x 256 rows,
+20.48 GB per launch, read as 19.1e6 KB: unhalved) and are taken as they are
+(FETCH_X1); other access patterns are marked uncalibrated.  WRITE_SIZE is
+exact for streaming stores.
 
-usage: tools/pmc_summary.py gpurun_out/<tag> profiles/<tag> [rows_per_launch]
+usage: tools/pmc_summary.py gpurun_out/<tag> profiles/<prefix> <rows> <iterations>
+  rows: rows per GPU of the profiled run; iterations: warmup + steps.
 """
 import collections
 import csv
 import json
 import os
 import sys
+
+FETCH_X2 = {"k_screen", "k_gram_tiles", "k_rows_quantize"}
+FETCH_X1 = {"k_chunk_sums_fast", "k_chunk_sums", "k_mlr_margins", "k_mlr_grad", "k_row_norms",
+            "k_binlog_dense", "k_assign_exact", "k_kmeans_assign2"}
 
 
 def mean_counter(path):
@@ -27,7 +35,7 @@ def mean_counter(path):
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
-def main(src, dst_prefix, rows=None):
+def main(src, dst_prefix, rows, iters):
     stats = {}
     ks = os.path.join(src, "trace", "run_kernel_stats.csv")
     for r in csv.DictReader(open(ks)):
@@ -35,15 +43,24 @@ def main(src, dst_prefix, rows=None):
                             "pct": float(r["Percentage"])}
     fetch = mean_counter(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
     write = mean_counter(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
-    out = {}
+    out = {"_rows": int(rows), "_iterations": int(iters),
+           "_note": "fetch_kb_raw is rocprofv3 FETCH_SIZE per dispatch; hbm bytes use the "
+                    "corrected fetch plus WRITE_SIZE"}
     for name, s in stats.items():
         f = fetch.get((name, "FETCH_SIZE"))
         w = write.get((name, "WRITE_SIZE"))
-        out[name] = dict(s, fetch_kb=f, write_kb=w,
-                         hbm_bytes_per_launch=None if f is None or w is None
-                         else (f + w) * 1024.0)
-    if rows:
-        out["_rows_per_launch"] = int(rows)
+        if name in FETCH_X2:
+            fac, cal = 2.0, "x2 (16 B/lane stream, gfx950 half count)"
+        elif name in FETCH_X1:
+            fac, cal = 1.0, "x1 (8 B/lane stream, calibrated)"
+        else:
+            fac, cal = 1.0, "uncalibrated"
+        rec = dict(s, fetch_kb_raw=f, fetch_correction=cal, write_kb=w)
+        if f is not None and w is not None:
+            b = (f * fac + w) * 1024.0
+            rec["hbm_bytes_per_dispatch"] = b
+            rec["hbm_bytes_per_step"] = b * s["calls"] / float(iters)
+        out[name] = rec
     os.makedirs(os.path.dirname(dst_prefix) or ".", exist_ok=True)
     json.dump(out, open(dst_prefix + "_pmc.json", "w"), indent=1, sort_keys=True)
     with open(ks) as fi, open(dst_prefix + "_kernel_stats.csv", "w") as fo:
@@ -52,4 +69,4 @@ def main(src, dst_prefix, rows=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+    main(sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4])
