@@ -55,6 +55,11 @@ SIGNATURES = {
     "cyc_kmeans_rows_bytes": (_i64, [_vp]),
     "cyc_kmeans_last_tiers": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_update_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _f64, _vp, _vp]),
+    "cyc_row_norms_csr_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
+    "cyc_kmeans_assign_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                                 _vp, _vp]),
+    "cyc_kmeans_accumulate_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cyc_gramian_plan_create": (ctypes.c_int, [_i32, ctypes.POINTER(_vp)]),
     "cyc_gramian_plan_destroy": (ctypes.c_int, [_vp]),
     "cyc_gramian_accumulate_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),

@@ -79,6 +79,21 @@ class KMeansPlan:
             int(X.shape[0]), N.ptr(C), N.ptr(cnorm), N.ptr(sums), N.ptr(wsum), N.ptr(cost_sum),
             N.ptr(assign), N.ptr(cost), N.stream_handle(stream)))
 
+    def assign_csr(self, rowptr, colidx, values, xnorm, C, cnorm, assign, cost, stream=None):
+        """findClosest for CSR rows (sparse points, dense centers); statistics
+        from the last stats() call."""
+        N.check(self._lib.cyc_kmeans_assign_csr_dev(
+            self.handle, N.ptr(rowptr), N.ptr(colidx), N.ptr(values), N.ptr(xnorm),
+            int(rowptr.shape[0]) - 1, N.ptr(C), N.ptr(cnorm), N.ptr(assign), N.ptr(cost),
+            N.stream_handle(stream)))
+
+    def accumulate_csr(self, rowptr, colidx, values, xnorm, weights, C, cnorm, sums, wsum,
+                       cost_sum, assign=None, cost=None, stream=None):
+        N.check(self._lib.cyc_kmeans_accumulate_csr_dev(
+            self.handle, N.ptr(rowptr), N.ptr(colidx), N.ptr(values), N.ptr(xnorm),
+            N.ptr(weights), int(rowptr.shape[0]) - 1, N.ptr(C), N.ptr(cnorm), N.ptr(sums),
+            N.ptr(wsum), N.ptr(cost_sum), N.ptr(assign), N.ptr(cost), N.stream_handle(stream)))
+
     def update(self, C, cnorm, sums, wsum, epsilon, converged, stream=None):
         N.check(self._lib.cyc_kmeans_update_dev(self.handle, N.ptr(C), N.ptr(cnorm), N.ptr(sums),
                                                 N.ptr(wsum), float(epsilon), N.ptr(converged),
@@ -124,6 +139,17 @@ def row_norms(X, out=None, stream=None):
         out = torch.empty(X.shape[0], dtype=torch.float64, device=X.device)
     N.check(N.load().cyc_row_norms_dev(N.ptr(X), int(X.shape[0]), int(X.shape[1]), N.ptr(out),
                                        N.stream_handle(stream)))
+    return out
+
+
+def row_norms_csr(rowptr, values, out=None, stream=None):
+    """Vectors.norm(sparse, 2.0) per CSR row (stored values, in order)."""
+    torch = _torch()
+    n = int(rowptr.shape[0]) - 1
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=values.device)
+    N.check(N.load().cyc_row_norms_csr_dev(N.ptr(rowptr), N.ptr(values), n, N.ptr(out),
+                                           N.stream_handle(stream)))
     return out
 
 
@@ -223,5 +249,41 @@ class KMeans:
                 iteration_callback(iteration, cost)
             iteration += 1
         rows.close()
+        plan.close()
+        return KMeansModel(C.cpu().numpy(), cost, iteration)
+
+    def run_csr(self, rowptr, colidx, values, numFeatures, weights=None, stream=None,
+                iteration_callback=None):
+        """Lloyd's algorithm over sparse points (libsvm input, KMeansExample):
+        CSR rowptr (int64), colidx (int32), values (fp64) CUDA tensors; the
+        centers are dense, as in the reference after the first iteration."""
+        torch = _torch()
+        if self.initialModel is None:
+            raise N.IllegalArgumentException(
+                "initialModel is required on the device path (setInitialModel); "
+                "k-means|| / random initialisation are host-side (SURVEY.md 8f)")
+        dev = values.device
+        d, k = int(numFeatures), self.k
+        n = int(rowptr.shape[0]) - 1
+        xnorm = row_norms_csr(rowptr, values, stream=stream)
+        plan = KMeansPlan(d, k, n)
+        C = torch.from_numpy(self.initialModel.clusterCenters.copy()).to(dev)
+        parallel.broadcast_(C)
+        cnorm = row_norms(C, stream=stream)
+        buf = torch.empty(k * d + k + 1, dtype=torch.float64, device=dev)
+        sums, wsum, cost_sum = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
+        converged_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        iteration, converged, cost = 0, False, 0.0
+        while iteration < self.maxIterations and not converged:
+            buf.zero_()
+            plan.accumulate_csr(rowptr, colidx, values, xnorm, weights, C, cnorm, sums, wsum,
+                                cost_sum, stream=stream)
+            parallel.allreduce_(buf)
+            plan.update(C, cnorm, sums, wsum, self.epsilon, converged_t, stream=stream)
+            converged = bool(converged_t.item())
+            cost = float(cost_sum.item())
+            if iteration_callback:
+                iteration_callback(iteration, cost)
+            iteration += 1
         plan.close()
         return KMeansModel(C.cpu().numpy(), cost, iteration)

@@ -4,7 +4,8 @@
 // Scala loops:
 //
 //   cyc_kmeans_iter              KMeans.scala:287-311 (mapPartitions body of
-//                                one Lloyd iteration, incl. computeStatistics)
+//                                one Lloyd iteration, incl. computeStatistics;
+//                                dense or sparse rows)
 //   cyc_logreg_binary_eval       RDDLossFunction.scala:56-70 seqOp over the
 //                                partition's blocks with
 //                                BinaryLogisticBlockAggregator.add (:81-145)
@@ -158,9 +159,12 @@ int ensure_norms(cyc_dataset ds) {
   if (ds->xnorm_ok) return CYC_OK;
   if (int rc = ds->xnorm.reserve(sizeof(double) * std::max<int64_t>(ds->rows, 1))) return rc;
   if (ds->rows) {
-    if (int rc = cyc_row_norms_dev((const double*)ds->X.ptr, ds->rows, ds->F,
-                                   (double*)ds->xnorm.ptr, ds->st))
-      return rc;
+    int rc = ds->sparse ? cyc_row_norms_csr_dev((const int64_t*)ds->rowptr.ptr,
+                                                (const double*)ds->vals.ptr, ds->rows,
+                                                (double*)ds->xnorm.ptr, ds->st)
+                        : cyc_row_norms_dev((const double*)ds->X.ptr, ds->rows, ds->F,
+                                            (double*)ds->xnorm.ptr, ds->st);
+    if (rc) return rc;
   }
   ds->xnorm_ok = true;
   return CYC_OK;
@@ -255,10 +259,6 @@ int cyc_dataset_append_csr(cyc_dataset ds, const int64_t* rowptr, const int32_t*
 int cyc_kmeans_iter(cyc_dataset ds, const double* centers, int32_t k, double* sums, double* wsum,
                     double* cost, int32_t* assign_opt) {
   CYC_REQUIRE(ds != nullptr && centers && sums && wsum && cost, "arguments must not be null");
-  if (ds->sparse) {
-    cyc::set_error("KMeans over a CSR dataset is not supported by the device path");
-    return CYC_ERR_UNSUPPORTED;
-  }
   DeviceGuard g(ds->device);
   cyc_kmeans_plan plan;
   auto it = ds->kplans.find(k);
@@ -269,9 +269,11 @@ int cyc_kmeans_iter(cyc_dataset ds, const double* centers, int32_t k, double* su
     ds->kplans[k] = plan;
   }
   if (int rc = ensure_norms(ds)) return rc;
-  cyc_kmeans_rows img;
+  cyc_kmeans_rows img = nullptr;
   auto ri = ds->krows.find(k);
-  if (ri != ds->krows.end()) {
+  if (ds->sparse) {
+    // sparse rows: no row image (the screens are dense-only)
+  } else if (ri != ds->krows.end()) {
     img = ri->second;
   } else {
     if (int rc = cyc_kmeans_rows_create(plan, (const double*)ds->X.ptr, ds->rows, ds->st, &img))
@@ -293,10 +295,16 @@ int cyc_kmeans_iter(cyc_dataset ds, const double* centers, int32_t k, double* su
     if ((rc = ds->in2.reserve(sizeof(int32_t) * std::max<int64_t>(ds->rows, 1)))) return rc;
     dA = (int32_t*)ds->in2.ptr;
   }
-  if ((rc = cyc_kmeans_accumulate_dev(plan, (const double*)ds->X.ptr, (const double*)ds->xnorm.ptr,
-                                      img, ds->has_weights ? (const double*)ds->weights.ptr : nullptr,
-                                      ds->rows, dC, dCn, dS, dW, dS + kd, dA, nullptr, ds->st)))
-    return rc;
+  const double* w = ds->has_weights ? (const double*)ds->weights.ptr : nullptr;
+  if (ds->sparse)
+    rc = cyc_kmeans_accumulate_csr_dev(plan, (const int64_t*)ds->rowptr.ptr,
+                                       (const int32_t*)ds->colidx.ptr, (const double*)ds->vals.ptr,
+                                       (const double*)ds->xnorm.ptr, w, ds->rows, dC, dCn, dS, dW,
+                                       dS + kd, dA, nullptr, ds->st);
+  else
+    rc = cyc_kmeans_accumulate_dev(plan, (const double*)ds->X.ptr, (const double*)ds->xnorm.ptr,
+                                   img, w, ds->rows, dC, dCn, dS, dW, dS + kd, dA, nullptr, ds->st);
+  if (rc) return rc;
   if ((rc = download(sums, dS, kd, ds->st)) || (rc = download(wsum, dW, k, ds->st)) ||
       (rc = download(cost, dS + kd, 1, ds->st)))
     return rc;

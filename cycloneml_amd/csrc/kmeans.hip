@@ -1446,6 +1446,8 @@ __global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __
   if (threadIdx.x == 0) out[0] = dadd(out[0], s[0]);
 }
 
+constexpr int kUpdLds = 3072;   // widest center staged in LDS by k_update_centers
+
 // centroid (DistanceMeasure.scala:200-203: scal(1/w, sum); new VectorWithNorm)
 // and isCenterConverged (:345-350).  One 64-lane workgroup per center: the
 // elementwise part in parallel, then lane 0 runs the two sequential sums (the
@@ -1454,13 +1456,30 @@ __global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __
 __global__ __launch_bounds__(64) void k_update_centers(
     double* __restrict__ C, double* __restrict__ cnorm, const double* __restrict__ sums,
     const double* __restrict__ wsum, int k, int d, double eps2, int32_t* __restrict__ converged) {
-  extern __shared__ double upd[];   // 2 d
+  extern __shared__ double upd[];   // 2 d (d <= kUpdLds)
   const int c = blockIdx.x, lane = threadIdx.x;
   const double w = wsum[c];
   if (!(w > 0)) return;
   const double a = 1.0 / w;
   double* crow = C + (int64_t)c * d;
   const double* srow = sums + (int64_t)c * d;
+  if (d > kUpdLds) {
+    // wide (sparse-input) centers: lane 0 reads both rows in order first
+    if (lane == 0) {
+      double moved = 0.0, nn = 0.0;
+      for (int j = 0; j < d; ++j) {
+        const double v = dmul(a, srow[j]);
+        const double sc = dsub(v, crow[j]);
+        moved = dadd(moved, dmul(sc, sc));
+        nn = dadd(nn, dmul(v, v));
+      }
+      cnorm[c] = __builtin_sqrt(nn);
+      if (!(moved <= eps2) && converged) atomicAnd(converged, 0);
+    }
+    __syncthreads();
+    for (int j = lane; j < d; j += 64) crow[j] = dmul(a, srow[j]);
+    return;
+  }
   for (int j = lane; j < d; j += 64) {
     const double v = dmul(a, srow[j]);
     const double sc = dsub(v, crow[j]);
@@ -1480,11 +1499,158 @@ __global__ __launch_bounds__(64) void k_update_centers(
   }
 }
 
+// ------------------------------------------------------------ sparse points
+// KMeansExample's input (BASELINE configs[0]) is libsvm, i.e. SparseVector
+// points against dense centers: fastSquaredDistance then takes the norm-trick
+// branch (MLUtils.scala:560-573) with BLAS.dot(sparse, dense)
+// (mllib/linalg/BLAS.scala:153-169) and the sqdist(sparse, dense) fallback
+// (Vectors.scala:598-622).  These kernels restate that path for CSR rows.
+
+// Vectors.norm(sparse, 2) (Vectors.scala:489-514 over the stored values)
+__global__ void k_row_norms_csr(const int64_t* __restrict__ rowptr,
+                                const double* __restrict__ vals, int64_t n,
+                                double* __restrict__ norms) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  double s = 0.0;
+  for (int64_t q = rowptr[r]; q < rowptr[r + 1]; ++q) s = dadd(s, dmul(vals[q], vals[q]));
+  norms[r] = __builtin_sqrt(s);
+}
+
+// java.lang.Math.max(a, 0.0): NaN stays NaN, -0.0 becomes +0.0
+__device__ __forceinline__ double jmax0(double a) {
+  if (a != a) return a;
+  return a > 0.0 ? a : 0.0;
+}
+
+// MLUtils.fastSquaredDistance(v1 = dense center, norm1, v2 = sparse point,
+// norm2) with precision 1e-6 (:533-576), the reference's operation order.
+__device__ double fast_sqdist_ds(const double* __restrict__ c, double norm1,
+                                 const int32_t* __restrict__ idx,
+                                 const double* __restrict__ val, int64_t nnz, double norm2,
+                                 int d) {
+  const double EPS = 0x1p-52;                         // MLUtils.EPSILON (:44-50)
+  const double sumSq = dadd(dmul(norm1, norm1), dmul(norm2, norm2));
+  const double nd = dsub(norm1, norm2);
+  const double pb1 = dmul(dmul(2.0, EPS), sumSq) / dadd(dmul(nd, nd), EPS);
+  double dot = 0.0;                                   // dot(sparse, dense), nnz order
+  for (int64_t q = 0; q < nnz; ++q) dot = dadd(dot, dmul(val[q], c[idx[q]]));
+  if (pb1 < 1e-6) return dsub(sumSq, dmul(2.0, dot));
+  double sq = jmax0(dsub(sumSq, dmul(2.0, dot)));
+  const double pb2 = dmul(EPS, dadd(sumSq, dmul(2.0, __builtin_fabs(dot)))) / dadd(sq, EPS);
+  if (pb2 > 1e-6) {                                   // Vectors.sqdist(sparse, dense)
+    int64_t kv1 = 0;
+    int iv1 = nnz > 0 ? idx[0] : -1;
+    double t = 0.0;
+    for (int kv2 = 0; kv2 < d; ++kv2) {
+      double score;
+      if (kv2 != iv1) {
+        score = c[kv2];
+      } else {
+        score = dsub(val[kv1], c[kv2]);
+        if (kv1 < nnz - 1) {
+          ++kv1;
+          iv1 = idx[kv1];
+        }
+      }
+      t = dadd(t, dmul(score, score));
+    }
+    sq = t;
+  }
+  return sq;
+}
+
+// EuclideanDistanceMeasure.findClosest with statistics (DistanceMeasure.scala:
+// 282-313) for sparse rows: the wave-parallel replay of k_assign_exact with
+// fastSquaredDistance as the distance.  Every row takes this path (the
+// screens are dense-only); one wave per row, grid-stride.
+__global__ __launch_bounds__(256) void k_assign_sparse(
+    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
+    const double* __restrict__ vals, const double* __restrict__ xnorm, int64_t n, int d,
+    const double* __restrict__ C, const double* __restrict__ cnorm, int k,
+    const double* __restrict__ stats, int32_t* __restrict__ assign, double* __restrict__ cost) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wid; r < n; r += nw) {
+    const int64_t q0 = rowptr[r], nnz = rowptr[r + 1] - q0;
+    const int32_t* idx = colidx + q0;
+    const double* val = vals + q0;
+    const double xn = xnorm[r];
+    double best = fast_sqdist_ds(C, cnorm[0], idx, val, nnz, xn, d);   // :286
+    int bi = 0;
+    bool done = best < stats[0];                                       // :287
+    for (int i0 = 1; !done && i0 < k; i0 += 64) {
+      const int i = i0 + lane;
+      const bool valid = i < k;
+      double lb = __builtin_inf(), sii = 0.0;
+      if (valid) {
+        const double ndf = dsub(cnorm[i], xn);                         // :294-295
+        lb = dmul(ndf, ndf);
+        sii = stats[iut(i, i)];
+      }
+      double dd = 0.0;
+      bool have = false;
+      int pos = 0;
+      for (;;) {
+        const bool visit = valid && lane >= pos && lb < best && stats[iut(i, bi)] < best;
+        if (visit && !have) {
+          dd = fast_sqdist_ds(C + (int64_t)i * d, cnorm[i], idx, val, nnz, xn, d);
+          have = true;
+        }
+        const bool brk = visit && dd < sii;
+        const bool ev = visit && (brk || dd < best);
+        const unsigned long long m = __ballot(ev);
+        if (!m) break;
+        const int f = __ffsll((long long)m) - 1;
+        best = __shfl(dd, f);
+        bi = i0 + f;
+        if (__shfl((int)brk, f)) {
+          done = true;
+          break;
+        }
+        pos = f + 1;
+      }
+    }
+    if (lane == 0) {
+      assign[r] = bi;
+      if (cost) cost[r] = best;
+    }
+  }
+}
+
+// updateClusterSum for sparse points (DistanceMeasure.scala:189-191, i.e.
+// mllib BLAS.axpy(w, sparse x, sum), BLAS.scala:93-112), clusterWeightSum and
+// costAccum (KMeans.scala:301-304).  One wave per row with fp64 atomics: the
+// sums agree with any partition order of the reference to rounding (they are
+// not bitwise reproducible run to run, unlike the dense path).
+__global__ __launch_bounds__(256) void k_sparse_sums(
+    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
+    const double* __restrict__ vals, const double* __restrict__ w, int64_t n, int d,
+    const int32_t* __restrict__ assign, const double* __restrict__ cost,
+    double* __restrict__ sums, double* __restrict__ wsum, double* __restrict__ costSum) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wid; r < n; r += nw) {
+    const int c = assign[r];
+    const double wr = w ? w[r] : 1.0;
+    double* y = sums + (int64_t)c * d;
+    for (int64_t q = rowptr[r] + lane; q < rowptr[r + 1]; q += 64)
+      unsafeAtomicAdd(&y[colidx[q]], wr == 1.0 ? vals[q] : dmul(wr, vals[q]));
+    if (lane == 0) {
+      unsafeAtomicAdd(&wsum[c], wr);
+      unsafeAtomicAdd(costSum, dmul(cost[r], wr));
+    }
+  }
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ plan
 struct cyc_kmeans_plan_s {
   int d = 0, k = 0, d4 = 0, kpad = 0, bm = 0, ldsStride = 0;
+  bool dense_ok = true;     // d fits the LDS-resident dense assign kernels (d <= 1240)
   int variant = 1;          // 2: k_kmeans_assign2 (fp64 screen), 3: bf16x3 screen
   int ldsStride2 = 0;
   size_t assignLds2 = 0;
@@ -1577,7 +1743,7 @@ int launch_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64
 
 int do_stats(cyc_kmeans_plan p, const double* C, hipStream_t st) {
   const int k = p->k, d = p->d;
-  {
+  if (p->dense_ok) {
     int64_t total = (int64_t)p->d4 * p->kpad;
     hipLaunchKernelGGL(k_center_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        st, C, k, d, p->d4, p->kpad, (double*)p->ct.ptr);
@@ -1761,11 +1927,8 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
     p->facU3 = (2.0 * eps + 0x1p-20) * (1.0 + 0x1p-20);
     p->tauU3 = 4.0 * tau;
   }
-  if (p->bm == 0) {
-    delete p;
-    cyc::set_error("d > 1240 is not supported by the LDS-resident assign kernel");
-    return CYC_ERR_UNSUPPORTED;
-  }
+  // d > 1240: no LDS-resident dense assign; the plan still serves sparse rows
+  p->dense_ok = p->bm != 0;
   int rc;
   if (p->variant == 3 &&
       ((rc = p->cb3.reserve((size_t)p->ktp3 * p->ks3 * 2 * 64 * 16)) ||
@@ -1790,7 +1953,7 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
       return rc;
     }
   }
-  if ((rc = p->ct.reserve(sizeof(double) * (size_t)p->d4 * p->kpad)) ||
+  if ((p->dense_ok && (rc = p->ct.reserve(sizeof(double) * (size_t)p->d4 * p->kpad))) ||
       (rc = p->stats.reserve(sizeof(double) * ((size_t)k * (k + 1) / 2))) ||
       (rc = p->dmin.reserve(sizeof(unsigned long long) * (size_t)k)) ||
       (rc = p->slowCount.reserve(64)) || (rc = ensure_rows(p, std::max<int64_t>(max_rows, 1)))) {
@@ -1876,6 +2039,10 @@ int cyc_kmeans_assign_dev(cyc_kmeans_plan p, const double* X, const double* xnor
   if (n_exact_out) *n_exact_out = 0;
   if (n == 0) return CYC_OK;
   if (int rc = check_rows(p, rows, X, n)) return rc;
+  if (!p->dense_ok) {
+    cyc::set_error("d > 1240 is not supported by the LDS-resident assign kernel (dense rows)");
+    return CYC_ERR_UNSUPPORTED;
+  }
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
   int rc = ensure_rows(p, n);
@@ -1896,6 +2063,10 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   CYC_REQUIRE(sums && wsum && cost_sum, "sums, wsum and cost_sum must not be null");
   if (n == 0) return CYC_OK;
   if (int rc = check_rows(p, rows, X, n)) return rc;
+  if (!p->dense_ok) {
+    cyc::set_error("d > 1240 is not supported by the LDS-resident assign kernel (dense rows)");
+    return CYC_ERR_UNSUPPORTED;
+  }
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
   const int k = p->k, d = p->d;
@@ -2004,9 +2175,75 @@ int cyc_kmeans_update_dev(cyc_kmeans_plan p, double* C, double* cnorm, const dou
   hipStream_t st = cyc::as_stream(stream);
   if (converged_out) CYC_HIP(hipMemsetD32Async((hipDeviceptr_t)converged_out, 1, 1, st));
   hipLaunchKernelGGL(k_update_centers, dim3((unsigned)p->k), dim3(64),
-                     sizeof(double) * 2 * (size_t)p->d, st, C, cnorm, sums, wsum, p->k, p->d,
+                     p->d <= kUpdLds ? sizeof(double) * 2 * (size_t)p->d : 0, st, C, cnorm, sums, wsum, p->k, p->d,
                      epsilon * epsilon, converged_out);
   CYC_LAUNCH_CHECK("k_update_centers");
+  return CYC_OK;
+}
+
+
+int cyc_row_norms_csr_dev(const int64_t* rowptr, const double* vals, int64_t n, double* norms,
+                          void* stream) {
+  CYC_REQUIRE(n >= 0 && (n == 0 || (rowptr && norms)), "n >= 0 and non-null buffers");
+  if (n == 0) return CYC_OK;
+  hipLaunchKernelGGL(k_row_norms_csr, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     cyc::as_stream(stream), rowptr, vals, n, norms);
+  CYC_LAUNCH_CHECK("k_row_norms_csr");
+  return CYC_OK;
+}
+
+namespace {
+int sparse_assign(cyc_kmeans_plan p, const int64_t* rowptr, const int32_t* colidx,
+                  const double* vals, const double* xnorm, int64_t n, const double* C,
+                  const double* cnorm, int32_t* assign, double* cost, hipStream_t st) {
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 8192);
+  cyc::KernelTimer timer("k_kmeans_assign_sparse", st);
+  hipLaunchKernelGGL(k_assign_sparse, dim3(grid), dim3(256), 0, st, rowptr, colidx, vals, xnorm,
+                     n, p->d, C, cnorm, p->k, (const double*)p->stats.ptr, assign, cost);
+  CYC_LAUNCH_CHECK("k_assign_sparse");
+  return CYC_OK;
+}
+}  // namespace
+
+int cyc_kmeans_assign_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr, const int32_t* colidx,
+                              const double* vals, const double* xnorm, int64_t n, const double* C,
+                              const double* cnorm, int32_t* assign, double* cost, void* stream) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  CYC_REQUIRE(assign != nullptr && cost != nullptr, "assign and cost must not be null");
+  if (n == 0) return CYC_OK;
+  std::lock_guard<std::mutex> g(p->mu);
+  return sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost,
+                       cyc::as_stream(stream));
+}
+
+int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
+                                  const int32_t* colidx, const double* vals, const double* xnorm,
+                                  const double* weights, int64_t n, const double* C,
+                                  const double* cnorm, double* sums, double* wsum,
+                                  double* cost_sum, int32_t* assign, double* cost, void* stream) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  CYC_REQUIRE(sums && wsum && cost_sum, "sums, wsum and cost_sum must not be null");
+  if (n == 0) return CYC_OK;
+  std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  int rc;
+  if (!assign) {
+    if ((rc = p->assignTmp.reserve(sizeof(int32_t) * (size_t)n))) return rc;
+    assign = (int32_t*)p->assignTmp.ptr;
+  }
+  if (!cost) {
+    if ((rc = p->costTmp.reserve(sizeof(double) * (size_t)n))) return rc;
+    cost = (double*)p->costTmp.ptr;
+  }
+  if ((rc = do_stats(p, C, st))) return rc;
+  if ((rc = sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost, st)))
+    return rc;
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_sparse_sums, dim3(grid), dim3(256), 0, st, rowptr, colidx, vals, weights, n,
+                     p->d, (const int32_t*)assign, (const double*)cost, sums, wsum, cost_sum);
+  CYC_LAUNCH_CHECK("k_sparse_sums");
   return CYC_OK;
 }
 

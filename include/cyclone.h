@@ -125,6 +125,27 @@ int cyc_kmeans_update_dev(cyc_kmeans_plan plan, double* C, double* cnorm, const 
                           const double* wsum, double epsilon, int32_t* converged_out,
                           void* stream);
 
+/* Sparse (CSR) points against dense centers: KMeansExample's libsvm input
+ * (BASELINE configs[0]).  Distances are MLUtils.fastSquaredDistance's
+ * norm-trick branch (MLUtils.scala:533-576: BLAS.dot(sparse, dense), the
+ * precision bounds and the Vectors.sqdist(sparse, dense) fallback,
+ * Vectors.scala:598-622) and findClosest replays the reference loop, so
+ * assignments and costs are bit-identical; the cluster sums use the sparse
+ * axpy (mllib BLAS.scala:93-112) with fp64 atomics (order-free to rounding).
+ * xnorm = Vectors.norm of the stored values (cyc_row_norms_csr_dev).  The
+ * plan's d is numFeatures; plans with d > 1240 serve only these calls. */
+int cyc_row_norms_csr_dev(const int64_t* rowptr, const double* vals, int64_t n, double* norms,
+                          void* stream);
+/* statistics from the last cyc_kmeans_stats_dev on this plan */
+int cyc_kmeans_assign_csr_dev(cyc_kmeans_plan plan, const int64_t* rowptr, const int32_t* colidx,
+                              const double* vals, const double* xnorm, int64_t n, const double* C,
+                              const double* cnorm, int32_t* assign, double* cost, void* stream);
+int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan plan, const int64_t* rowptr,
+                                  const int32_t* colidx, const double* vals, const double* xnorm,
+                                  const double* weights, int64_t n, const double* C,
+                                  const double* cnorm, double* sums, double* wsum,
+                                  double* cost_sum, int32_t* assign, double* cost, void* stream);
+
 /* ------------------------------------------------------ RowMatrix Gramian */
 /* Replaces the BLAS.spr seqOp of RowMatrix.computeGramianMatrix
  * (mllib/linalg/distributed/RowMatrix.scala:130-161) and of
@@ -217,8 +238,8 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan plan, const double*
  *   cyc_logreg_*_eval           RDDLossFunction.scala:56-70's seqOp over the
  *                               partition's blocks
  *   cyc_gramian, cyc_col_sums   RowMatrix.scala:130-161, :163-220, :456
- * Dense datasets serve every entry point; CSR datasets serve the binary
- * logistic aggregator (others return CYC_ERR_UNSUPPORTED). */
+ * Dense datasets serve every entry point; CSR datasets serve KMeans and the
+ * binary logistic aggregator (others return CYC_ERR_UNSUPPORTED). */
 typedef struct cyc_dataset_s* cyc_dataset;
 
 int cyc_dataset_dense_create(int32_t numFeatures, int64_t capacity_rows, int has_labels,

@@ -97,7 +97,9 @@ double orc_fast_sqdist_dense_sparse(const double* v1, double norm1,
     sqDist = sumSquaredNorm - 2.0 * orc_dot_sparse_dense(idx, val, nnz, v1);
   } else {
     double dotValue = orc_dot_sparse_dense(idx, val, nnz, v1);
-    sqDist = fmax(sumSquaredNorm - 2.0 * dotValue, 0.0);
+    /* math.max(x, 0.0): NaN stays NaN, -0.0 becomes 0.0 (java.lang.Math.max) */
+    double t = sumSquaredNorm - 2.0 * dotValue;
+    sqDist = (t != t) ? t : (t > 0.0 ? t : 0.0);
     double precisionBound2 = EPS * (sumSquaredNorm + 2.0 * fabs(dotValue)) / (sqDist + EPS);
     if (precisionBound2 > precision) {
       sqDist = orc_sqdist_sparse_dense(idx, val, nnz, v1, n);
@@ -604,5 +606,44 @@ void orc_triu_to_full(int64_t n, const double* U, double* G) {
       G[row * n + col] = v;
     }
     G[col * n + col] = U[idx++];
+  }
+}
+
+/* One partition of the Lloyd body for sparse points (KMeans.scala:299-304):
+ * findClosest through the norm trick (orc_find_closest_stats_sparse),
+ * costAccum.add(cost * weight), updateClusterSum = mllib BLAS.axpy(weight,
+ * sparse x, sum) (mllib/linalg/BLAS.scala:93-112: y(idx) += x or a * x in
+ * nnz order) and clusterWeightSum += weight.  CSR rows; w NULL = unit.     */
+void orc_kmeans_partition_sparse(const int64_t* rowptr, const int32_t* colidx,
+                                 const double* vals, const double* xnorm, const double* w,
+                                 int64_t n, int64_t d, const double* C, const double* cnorm,
+                                 const double* stats, int64_t k, int32_t* assign, double* dist,
+                                 double* sums, double* wsum, double* cost) {
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t q0 = rowptr[r], nnz = rowptr[r + 1] - q0;
+    int32_t bi;
+    double bd;
+    orc_find_closest_stats_sparse(C, cnorm, k, d, stats, colidx + q0, vals + q0, nnz, xnorm[r],
+                                  &bi, &bd);
+    const double wt = w ? w[r] : 1.0;
+    *cost += bd * wt;
+    double* y = sums + (int64_t)bi * d;
+    if (wt == 1.0) {
+      for (int64_t q = 0; q < nnz; ++q) y[colidx[q0 + q]] += vals[q0 + q];
+    } else {
+      for (int64_t q = 0; q < nnz; ++q) y[colidx[q0 + q]] += wt * vals[q0 + q];
+    }
+    wsum[bi] += wt;
+    if (assign) assign[r] = bi;
+    if (dist) dist[r] = bd;
+  }
+}
+
+/* Vectors.norm(sparse, 2) of each CSR row (stored values in order) */
+void orc_row_norms_csr(const int64_t* rowptr, const double* vals, int64_t n, double* out) {
+  for (int64_t r = 0; r < n; ++r) {
+    double s = 0.0;
+    for (int64_t q = rowptr[r]; q < rowptr[r + 1]; ++q) s += vals[q] * vals[q];
+    out[r] = sqrt(s);
   }
 }

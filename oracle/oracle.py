@@ -70,6 +70,9 @@ def lib():
                 "orc_multinomial_logistic_add_csr": (None, [_i64, _i64, _i64, _I64, _I32, _D, _D,
                                                             _D, _D, ctypes.c_int, ctypes.c_int,
                                                             _D, _D, _D, _D]),
+                "orc_kmeans_partition_sparse": (None, [_I64, _I32, _D, _D, _D, _i64, _i64, _D,
+                                                       _D, _D, _i64, _I32, _D, _D, _D, _D]),
+                "orc_row_norms_csr": (None, [_I64, _D, _i64, _D]),
                 "orc_dspr_upper": (None, [_i64, ctypes.c_double, _D, _D]),
                 "orc_spr_sparse": (None, [ctypes.c_double, _I32, _D, _i64, _D]),
                 "orc_gramian_partition": (None, [_D, _i64, _i64, _D, _D]),
@@ -172,6 +175,36 @@ def kmeans_partition(X, xnorm, w, C, cnorm, stats, want_assign=True):
                                _p(assign, _I32), _p(dist), _p(sums), _p(wsum),
                                ctypes.byref(cost))
     return assign, dist, sums, wsum, cost.value
+
+
+def row_norms_csr(rowptr, vals) -> np.ndarray:
+    """Vectors.norm(sparse, 2) per CSR row (mllib/linalg/Vectors.scala:489-514)."""
+    rp = np.ascontiguousarray(rowptr, dtype=np.int64)
+    v = _f64(vals)
+    out = np.empty(len(rp) - 1)
+    lib().orc_row_norms_csr(_p(rp, _I64), _p(v), len(rp) - 1, _p(out))
+    return out
+
+
+def kmeans_partition_sparse(csr, xnorm, w, C, cnorm, stats):
+    """KMeans.scala:299-304 over sparse points (norm-trick findClosest, sparse
+    axpy sums).  Returns (assign, dist, sums (k x d), wsum, cost)."""
+    rp = np.ascontiguousarray(csr[0], dtype=np.int64)
+    ci = np.ascontiguousarray(csr[1], dtype=np.int32)
+    v = _f64(csr[2])
+    C = _f64(C)
+    k, d = C.shape
+    n = len(rp) - 1
+    a = np.empty(n, np.int32)
+    dist = np.empty(n)
+    sums = np.zeros(k * d)
+    wsum = np.zeros(k)
+    cost = np.zeros(1)
+    lib().orc_kmeans_partition_sparse(_p(rp, _I64), _p(ci, _I32), _p(v), _p(_f64(xnorm)),
+                                      _p(None if w is None else _f64(w)), n, d, _p(C),
+                                      _p(_f64(cnorm)), _p(_f64(stats)), k, _p(a, _I32), _p(dist),
+                                      _p(sums), _p(wsum), _p(cost))
+    return a, dist, sums.reshape(k, d), wsum, cost[0]
 
 
 def kmeans_iteration(X, xnorm, w, C, cnorm, num_partitions=1, threads=None):

@@ -150,8 +150,36 @@ def test_dataset_errors(cuda):
         ds.append_csr(np.array([0, 1]), np.array([1]), np.array([1.0]))
     ds.append_csr(np.array([0, 1]), np.array([1]), np.array([1.0]), np.zeros(1))
     with pytest.raises(N.CycloneError) as e:
-        ds.kmeans_iter(np.ones((2, 5)))
+        ds.gramian()
     assert e.value.code == N.CYC_ERR_UNSUPPORTED
     dd = ResidentDataset.dense(3, 2)
     with pytest.raises(N.IllegalArgumentException, match="holds no labels"):
         dd.binary_logistic_eval(np.zeros(3), False)
+
+
+@pytest.mark.gpu
+def test_dataset_csr_kmeans_iter(cuda):
+    """cyc_kmeans_iter over a CSR dataset (sparse points, KMeansExample's input
+    type): assignments bit-exact, sums / weights / cost to 1e-12 relative."""
+    rng = np.random.default_rng(21)
+    n, F, k = 700, 30, 6
+    rows, cols, vals = [0], [], []
+    for _ in range(n):
+        c = np.sort(rng.choice(F, size=int(rng.integers(1, 8)), replace=False))
+        cols.extend(c.tolist())
+        vals.extend(rng.normal(size=len(c)).tolist())
+        rows.append(len(cols))
+    rp, ci, v = np.array(rows, np.int64), np.array(cols, np.int32), np.array(vals)
+    w = rng.uniform(0.5, 1.5, n)
+    C = rng.normal(size=(k, F)) * 0.3
+    ds = ResidentDataset.csr(F, n, len(v), weights=True)
+    ds.append_csr(rp[:301], ci[:rp[300]], v[:rp[300]], weights=w[:300])
+    ds.append_csr(rp[300:] - rp[300], ci[rp[300]:], v[rp[300]:], weights=w[300:])
+    sums, wsum, cost, assign = ds.kmeans_iter(C, want_assign=True)
+    ra, _, rs, rw, rc = oracle.kmeans_partition_sparse((rp, ci, v), oracle.row_norms_csr(rp, v),
+                                                       w, C, oracle.row_norms(C),
+                                                       oracle.kmeans_stats(C))
+    np.testing.assert_array_equal(assign, ra)
+    _rel_close(sums, rs, rtol=1e-12)
+    _rel_close(wsum, rw, rtol=1e-12)
+    _rel_close(cost[0], rc, rtol=1e-12)

@@ -1,0 +1,148 @@
+"""GPU parity tests: KMeans over sparse (CSR) points -- KMeansExample's libsvm
+input, BASELINE configs[0] -- against the CPU restatement (oracle/:
+orc_find_closest_stats_sparse, orc_kmeans_partition_sparse).
+
+Bar: assignments and per-point costs bit-exact (the norm-trick
+fastSquaredDistance of MLUtils.scala:533-576 is replayed in the reference's
+order); cluster sums / weights / cost within 1e-12 relative (fp64 atomics:
+order-free to rounding); centers as the oracle's update to 1e-12.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                   "reference_known_answers.json")))
+
+
+def _dev(a, cuda):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+
+
+def _random_csr(rng, n, d, density):
+    rows, cols, vals = [0], [], []
+    for _ in range(n):
+        m = max(1, rng.binomial(d, density))
+        c = np.sort(rng.choice(d, size=m, replace=False))
+        cols.extend(c.tolist())
+        vals.extend((rng.normal(size=m) * 3.0 + rng.integers(-2, 3)).tolist())
+        rows.append(len(cols))
+    return (np.array(rows, np.int64), np.array(cols, np.int32), np.array(vals))
+
+
+def _dense(csr, d):
+    rp, ci, v = csr
+    X = np.zeros((len(rp) - 1, d))
+    for r in range(len(rp) - 1):
+        X[r, ci[rp[r]:rp[r + 1]]] = v[rp[r]:rp[r + 1]]
+    return X
+
+
+def _rel_close(a, b, rtol):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=rtol * max(1.0, float(np.abs(b).max())))
+
+
+def test_row_norms_csr_bitexact(cuda):
+    from cycloneml_amd.clustering import row_norms_csr
+    rng = np.random.default_rng(5)
+    csr = _random_csr(rng, 500, 70, 0.1)
+    got = row_norms_csr(_dev(csr[0], cuda), _dev(csr[2], cuda)).cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.row_norms_csr(csr[0], csr[2]))
+
+
+@pytest.mark.parametrize("n,d,k,density,weighted", [(3000, 40, 17, 0.2, False),
+                                                    (2000, 7, 3, 0.6, True),
+                                                    (1500, 300, 64, 0.05, True),
+                                                    (400, 5000, 5, 0.01, False)])
+def test_sparse_accumulate_vs_oracle(cuda, n, d, k, density, weighted):
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms, row_norms_csr
+    rng = np.random.default_rng(n + d + k)
+    csr = _random_csr(rng, n, d, density)
+    C = _dense(csr, d)[rng.choice(n, size=k, replace=False)] + rng.normal(size=(k, d)) * 0.01
+    w = rng.uniform(0.1, 2.0, n) if weighted else None
+    rp, ci, v = (_dev(a, cuda) for a in csr)
+    Cd = _dev(C, cuda)
+    xn = row_norms_csr(rp, v)
+    cn = row_norms(Cd)
+    p = KMeansPlan(d, k, n)
+    buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=cuda)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    c = torch.empty(n, dtype=torch.float64, device=cuda)
+    p.accumulate_csr(rp, ci, v, xn, None if w is None else _dev(w, cuda), Cd, cn,
+                     buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:], assign=a, cost=c)
+    torch.cuda.synchronize()
+    cnh = oracle.row_norms(C)
+    ra, rd, rs, rw, rc = oracle.kmeans_partition_sparse(csr, oracle.row_norms_csr(csr[0], csr[2]),
+                                                         w, C, cnh, oracle.kmeans_stats(C))
+    np.testing.assert_array_equal(a.cpu().numpy(), ra)
+    np.testing.assert_array_equal(c.cpu().numpy(), rd)
+    b = buf.cpu().numpy()
+    _rel_close(b[:k * d].reshape(k, d), rs, 1e-12)
+    _rel_close(b[k * d:k * d + k], rw, 1e-12)
+    _rel_close(b[k * d + k], rc, 1e-12)
+    # centroid update (wide centers for d > 3072 use the global-memory path)
+    conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+    p.update(Cd, cn, buf[:k * d], buf[k * d:k * d + k], 1e-4, conv)
+    Ch, cnh2 = C.copy(), cnh.copy()
+    rconv = oracle.update_centers(Ch, cnh2, b[:k * d], b[k * d:k * d + k], 1e-4)
+    np.testing.assert_array_equal(Cd.cpu().numpy(), Ch)
+    np.testing.assert_array_equal(cn.cpu().numpy(), cnh2)
+    assert bool(conv.item()) == rconv
+
+
+def test_sparse_assign_matches_find_closest(cuda):
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms, row_norms_csr
+    rng = np.random.default_rng(11)
+    n, d, k = 1200, 25, 40
+    csr = _random_csr(rng, n, d, 0.3)
+    # duplicated and near-duplicated centers exercise ties and the prunes
+    C = _dense(csr, d)[rng.choice(n, size=k, replace=False)]
+    C[5] = C[4]
+    C[7] = C[6] * (1 + 1e-15)
+    rp, ci, v = (_dev(a, cuda) for a in csr)
+    Cd = _dev(C, cuda)
+    xn, cn = row_norms_csr(rp, v), row_norms(Cd)
+    p = KMeansPlan(d, k, n)
+    p.stats(Cd)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    c = torch.empty(n, dtype=torch.float64, device=cuda)
+    p.assign_csr(rp, ci, v, xn, Cd, cn, a, c)
+    torch.cuda.synchronize()
+    cnh, st = oracle.row_norms(C), oracle.kmeans_stats(C)
+    xnh = oracle.row_norms_csr(csr[0], csr[2])
+    for r in range(n):
+        s0, s1 = csr[0][r], csr[0][r + 1]
+        i, dist = oracle.find_closest_stats_sparse(C, cnh, st, csr[1][s0:s1], csr[2][s0:s1],
+                                                   xnh[r])
+        assert int(a[r]) == i and float(c[r]) == dist, r
+
+
+def test_kmeans_example_on_device(cuda):
+    """KMeansExample's sample_kmeans_data.txt (6 libsvm rows) through the device
+    Lloyd loop from the initial centers rows 0 and 3: clusters {0,1,2} /
+    {3,4,5}, centers (0.1,0.1,0.1) / (9.1,9.1,9.1)."""
+    from cycloneml_amd.clustering import KMeans, KMeansModel
+    g = GOLD["kmeans_example_data"]
+    rows, cols, vals = [0], [], []
+    for line in g["libsvm"]:
+        for t in line.split()[1:]:
+            i, x = t.split(":")
+            cols.append(int(i) - 1)
+            vals.append(float(x))
+        rows.append(len(cols))
+    csr = (np.array(rows, np.int64), np.array(cols, np.int32), np.array(vals))
+    dense = _dense(csr, 3)
+    km = KMeans(k=2, maxIterations=20, epsilon=1e-4).setInitialModel(KMeansModel(dense[[0, 3]]))
+    model = km.run_csr(*(_dev(a, cuda) for a in csr), 3)
+    np.testing.assert_allclose(sorted(model.clusterCenters.tolist()),
+                               g["expected_centers_approx"], atol=1e-12)

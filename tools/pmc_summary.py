@@ -7,12 +7,13 @@ Per kernel (rocprofv3 -T names): calls and mean duration (kernel trace +
 separate --pmc passes (KB), and HBM bytes per dispatch and per step.
 
 gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE reads exactly half
-the bytes of a 16-B-per-lane streaming read, so it is doubled for kernels
-whose stream is 16 B per lane (FETCH_X2).  8-B-per-lane streams were
-calibrated on a known byte count (the fp64 X stream of 10M x 256 rows,
-20.48 GB per launch, read as 19.1e6 KB: unhalved) and are taken as they are
-(FETCH_X1); other access patterns are marked uncalibrated.  WRITE_SIZE is
-exact for streaming stores.
+the bytes of a coalesced streaming read.  Checked here on known byte counts
+for both widths: k_row_norms and k_chunk_sums_fast (8 B per lane) stream the
+20.48 GB of fp64 rows and read 10.0e6 KB; k_screen (16 B per lane) streams
+the 7.76 GB row image and reads 3.84e6 KB.  So FETCH_SIZE is doubled for the
+streaming kernels (FETCH_X2); gathers and other patterns are marked
+uncalibrated and taken as they are.  WRITE_SIZE is exact for streaming
+stores.  Fabric-side counts include Infinity-Cache hits.
 
 usage: tools/pmc_summary.py gpurun_out/<tag> profiles/<prefix> <rows> <iterations>
   rows: rows per GPU of the profiled run; iterations: warmup + steps.
@@ -23,9 +24,9 @@ import json
 import os
 import sys
 
-FETCH_X2 = {"k_screen", "k_gram_tiles", "k_rows_quantize"}
-FETCH_X1 = {"k_chunk_sums_fast", "k_chunk_sums", "k_mlr_margins", "k_mlr_grad", "k_row_norms",
-            "k_binlog_dense", "k_assign_exact", "k_kmeans_assign2"}
+FETCH_X2 = {"k_screen", "k_gram_tiles", "k_rows_quantize", "k_chunk_sums_fast", "k_chunk_sums",
+            "k_row_norms", "k_mlr_margins", "k_mlr_grad", "k_binlog_dense", "k_binlog_csr_mult8",
+            "k_binlog_csc_grad_blk", "k_summ_dense"}
 
 
 def mean_counter(path):
@@ -50,9 +51,7 @@ def main(src, dst_prefix, rows, iters):
         f = fetch.get((name, "FETCH_SIZE"))
         w = write.get((name, "WRITE_SIZE"))
         if name in FETCH_X2:
-            fac, cal = 2.0, "x2 (16 B/lane stream, gfx950 half count)"
-        elif name in FETCH_X1:
-            fac, cal = 1.0, "x1 (8 B/lane stream, calibrated)"
+            fac, cal = 2.0, "x2 (streaming read, gfx950 half count)"
         else:
             fac, cal = 1.0, "uncalibrated"
         rec = dict(s, fetch_kb_raw=f, fetch_correction=cal, write_kb=w)
