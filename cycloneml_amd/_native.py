@@ -82,6 +82,15 @@ SIGNATURES = {
                                       ctypes.POINTER(_vp)]),
     "cyc_multinomial_logistic_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp,
                                                               _vp, _vp, _vp, _vp, _vp]),
+    "cyc_csc_features": (_i32, [_vp]),
+    "cyc_summarizer_buffer_len": (_i64, [_i32]),
+    "cyc_summarizer_dense_dev": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _vp, _vp]),
+    "cyc_summarizer_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
+    "cyc_summarizer_merge_dev": (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp]),
+    "cyc_summarizer_metrics_dev": (ctypes.c_int, [_i32, _vp, _vp, _vp]),
+    "cyc_label_summarizer_dev": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "cyc_scale_columns_dense_dev": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
+    "cyc_scale_columns_csr_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
     # resident datasets: host pointers
     "cyc_dataset_dense_create": (ctypes.c_int, [_i32, _i64, ctypes.c_int, ctypes.c_int,
                                                 ctypes.POINTER(_vp)]),

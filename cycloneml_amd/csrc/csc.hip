@@ -264,6 +264,8 @@ int cyc_csc_destroy(cyc_csc csc) {
 
 int64_t cyc_csc_rows(cyc_csc csc) { return csc ? csc->n : -1; }
 
+int32_t cyc_csc_features(cyc_csc csc) { return csc ? csc->F : -1; }
+
 int cyc_csc_slices(cyc_csc csc, int32_t* nslices, int32_t* width, const int64_t** rowptrS,
                    const int32_t** colS, const double** valS) {
   CYC_REQUIRE(csc != nullptr, "csc must not be null");

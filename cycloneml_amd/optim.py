@@ -68,6 +68,12 @@ class DeviceInstanceBlock:
             self.csc = h
         return self
 
+    def drop_derived(self):
+        """Forget the CSC copy (after the values change, e.g. standardization)."""
+        if getattr(self, "csc", None):
+            N.load().cyc_csc_destroy(self.csc)
+            self.csc = None
+
     def __del__(self):
         try:
             if getattr(self, "csc", None):

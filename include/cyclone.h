@@ -192,6 +192,7 @@ int cyc_csc_build_dev(const int64_t* rowptr, const int32_t* colidx, const double
                       int64_t n, int32_t numFeatures, void* stream, cyc_csc* out);
 int cyc_csc_destroy(cyc_csc csc);
 int64_t cyc_csc_rows(cyc_csc csc);
+int32_t cyc_csc_features(cyc_csc csc);
 /* The copy is row-blocked (rows_per_block rows per block): colptr has
  * nblocks * numFeatures + 1 entries, block b / column c spanning
  * [colptr[b F + c], colptr[b F + c + 1]) of rowidx / values. */
@@ -223,6 +224,45 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan plan, const double*
                                            int64_t n, const double* coef,
                                            const double* scaledMean, double* grad,
                                            double* lossSum, double* weightSum, void* stream);
+
+/* ------------------------------------------------ summarizer pre-pass */
+/* The first pass of LogisticRegression.train (LogisticRegression.scala:
+ * 511-516, Summarizer.getClassificationSummarizers, ml/stat/Summarizer.scala:
+ * 228-241) and of RowMatrix/colStats, and the StandardScaler transform of
+ * trainImpl (:957-965), over a device-resident shard.
+ *
+ * SummarizerBuffer (Summarizer.scala:428-770): a buffer is
+ * cyc_summarizer_buffer_len(F) = 8 F + 5 doubles (device): per column mean,
+ * m2n, m2, l1, weightSum, nnz, max, min (structure of arrays), then count,
+ * totalWeightSum, weightSquareSum, a flag set when a row's weight failed
+ * `require(weight >= 0.0)` (:472) and that weight.  The rows are cut into
+ * partitions (dense: rows_per_partition rows; CSR: the row blocks of the CSC
+ * copy), each partition's buffer is add()-ed row by row in the reference's
+ * order and the partitions are merged (:562-617) in order.  Buffers of
+ * several shards merge with cyc_summarizer_merge_dev, in the given order.
+ * metrics (9 x F doubles): mean, variance, std, sum, numNonzeros, max, min,
+ * normL2, normL1 (:622-769); count and weightSum are buf[8F], buf[8F+1]. */
+int64_t cyc_summarizer_buffer_len(int32_t numFeatures);
+int cyc_summarizer_dense_dev(const double* X, const double* weights, int64_t n, int32_t F,
+                             int64_t rows_per_partition, double* buf, void* stream);
+int cyc_summarizer_csr_dev(cyc_csc csc, const double* weights, double* buf, void* stream);
+int cyc_summarizer_merge_dev(int32_t F, const double* bufs, int64_t count, double* out,
+                             void* stream);
+int cyc_summarizer_metrics_dev(int32_t F, const double* buf, double* metrics, void* stream);
+/* MultiClassSummarizer (ml/stat/MultiClassSummarizer.scala:30-98) of the
+ * labels: hist[max_classes] = per-class weight sums (classes >= max_classes
+ * are counted in max_label only), *invalid = countInvalid, *max_label = the
+ * largest valid label (-1: none; numClasses = max_label + 1; call again with
+ * a larger max_classes, at most 8192, when it does not fit).  All device. */
+int cyc_label_summarizer_dev(const double* labels, const double* weights, int64_t n,
+                             int64_t rows_per_partition, int32_t max_classes, double* hist,
+                             int64_t* invalid, int32_t* max_label, void* stream);
+/* StandardScaler transform with scale only (StandardScaler.scala:261-283),
+ * in place: dense values(i) *= scale(i); CSR values(k) *= scale(indices(k)). */
+int cyc_scale_columns_dense_dev(double* X, int64_t n, int32_t F, const double* scale,
+                                void* stream);
+int cyc_scale_columns_csr_dev(const int32_t* colidx, double* vals, int64_t nnz,
+                              const double* scale, void* stream);
 
 /* ------------------------------------------- resident datasets (host API) */
 /* Layer 2 for a JVM shim: a library-owned HBM copy of one

@@ -18,6 +18,8 @@
  * aggregator suites' naive loops) are committed under tests/golden and
  * checked by tests/test_oracle_golden.py.
  */
+#include <float.h>
+#include <limits.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -646,4 +648,187 @@ void orc_row_norms_csr(const int64_t* rowptr, const double* vals, int64_t n, dou
     for (int64_t q = rowptr[r]; q < rowptr[r + 1]; ++q) s += vals[q] * vals[q];
     out[r] = sqrt(s);
   }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Summarizer pre-pass (ml/stat/Summarizer.scala:428-770,                   */
+/* ml/stat/MultiClassSummarizer.scala:30-98)                                */
+/* ------------------------------------------------------------------------ */
+
+/* SummarizerBuffer state: 8 x F fields (mean, m2n, m2, l1, weightSum, nnz,
+ * max, min), then count, totalWeightSum, weightSquareSum, a flag for a weight
+ * that failed require(weight >= 0.0) (:472) and that weight.              */
+enum { OS_MEAN, OS_M2N, OS_M2, OS_L1, OS_WS, OS_NNZ, OS_MAX, OS_MIN, OS_FIELDS };
+#define OS_SCAL 5
+
+/* a fresh buffer, arrays as the first add allocates them (:475-493) */
+void orc_summ_init(int64_t F, double* st) {
+  memset(st, 0, sizeof(double) * (size_t)(OS_FIELDS * F + OS_SCAL));
+  for (int64_t c = 0; c < F; ++c) {
+    st[OS_MAX * F + c] = -DBL_MAX; /* Double.MinValue */
+    st[OS_MIN * F + c] = DBL_MAX;  /* Double.MaxValue */
+  }
+}
+
+/* add(nonZeroIterator, size, weight) (:471-546) for one row of nnz (index,
+ * value) pairs (idx == NULL: a dense row, index = position).             */
+void orc_summ_add_row(int64_t F, double* st, const int32_t* idx, const double* val, int64_t nnz,
+                      double w) {
+  double* s = st + OS_FIELDS * F;
+  if (!(w >= 0.0)) { /* require(weight >= 0.0): the reference throws */
+    if (s[3] == 0.0) {
+      s[3] = 1.0;
+      s[4] = w;
+    }
+    return;
+  }
+  if (w == 0.0) return;
+  for (int64_t q = 0; q < nnz; ++q) {
+    const int64_t c = idx ? idx[q] : q;
+    const double v = val[q];
+    if (v == 0.0) continue; /* nonZeroIterator */
+    if (st[OS_MAX * F + c] < v) st[OS_MAX * F + c] = v;
+    if (st[OS_MIN * F + c] > v) st[OS_MIN * F + c] = v;
+    const double prevMean = st[OS_MEAN * F + c];
+    const double diff = v - prevMean;
+    st[OS_MEAN * F + c] = prevMean + w * diff / (st[OS_WS * F + c] + w);
+    st[OS_M2N * F + c] += w * (v - st[OS_MEAN * F + c]) * diff;
+    st[OS_WS * F + c] += w;
+    st[OS_M2 * F + c] += w * v * v;
+    st[OS_L1 * F + c] += w * fabs(v);
+    st[OS_NNZ * F + c] += 1.0;
+  }
+  s[1] += w;
+  s[2] += w * w;
+  s[0] += 1.0;
+}
+
+static double orc_jmax(double a, double b) { /* java.lang.Math.max */
+  if (a != a) return a;
+  if (a == 0.0 && b == 0.0 && signbit(a)) return b;
+  return a >= b ? a : b;
+}
+static double orc_jmin(double a, double b) { /* java.lang.Math.min */
+  if (a != a) return a;
+  if (a == 0.0 && b == 0.0 && signbit(b)) return b;
+  return a <= b ? a : b;
+}
+
+/* a = a.merge(b) (:562-617) */
+void orc_summ_merge(int64_t F, double* a, const double* b) {
+  double* sa = a + OS_FIELDS * F;
+  const double* sb = b + OS_FIELDS * F;
+  const double bad = sa[3], badv = sa[4];
+  if (sa[1] != 0.0 && sb[1] != 0.0) {
+    sa[0] += sb[0];
+    sa[1] += sb[1];
+    sa[2] += sb[2];
+    for (int64_t c = 0; c < F; ++c) {
+      const double thisW = a[OS_WS * F + c], otherW = b[OS_WS * F + c];
+      const double tot = thisW + otherW;
+      if (tot != 0.0) {
+        const double dm = b[OS_MEAN * F + c] - a[OS_MEAN * F + c];
+        a[OS_MEAN * F + c] += dm * otherW / tot;
+        a[OS_M2N * F + c] += b[OS_M2N * F + c] + dm * dm * thisW * otherW / tot;
+      }
+      a[OS_WS * F + c] = tot;
+      a[OS_M2 * F + c] += b[OS_M2 * F + c];
+      a[OS_L1 * F + c] += b[OS_L1 * F + c];
+      a[OS_MAX * F + c] = orc_jmax(a[OS_MAX * F + c], b[OS_MAX * F + c]);
+      a[OS_MIN * F + c] = orc_jmin(a[OS_MIN * F + c], b[OS_MIN * F + c]);
+      a[OS_NNZ * F + c] = a[OS_NNZ * F + c] + b[OS_NNZ * F + c];
+    }
+  } else if (sa[1] == 0.0 && sb[1] != 0.0) {
+    memcpy(a, b, sizeof(double) * (size_t)(OS_FIELDS * F + 3));
+  }
+  if (bad != 0.0) {
+    sa[3] = bad;
+    sa[4] = badv;
+  } else if (sb[3] != 0.0) {
+    sa[3] = 1.0;
+    sa[4] = sb[4];
+  }
+}
+
+/* The rows cut into partitions of R rows, each a fresh buffer add()-ed row
+ * by row, merged in partition order into out (fresh).  Dense X or CSR.    */
+void orc_summarize(int64_t n, int64_t F, const double* X, const int64_t* rowptr,
+                   const int32_t* colidx, const double* vals, const double* w, int64_t R,
+                   double* out) {
+  double* part = (double*)malloc(sizeof(double) * (size_t)(OS_FIELDS * F + OS_SCAL));
+  orc_summ_init(F, out);
+  for (int64_t p0 = 0; p0 < n; p0 += R) {
+    const int64_t p1 = p0 + R < n ? p0 + R : n;
+    orc_summ_init(F, part);
+    for (int64_t r = p0; r < p1; ++r) {
+      const double wr = w ? w[r] : 1.0;
+      if (X) orc_summ_add_row(F, part, NULL, X + r * F, F, wr);
+      else orc_summ_add_row(F, part, colidx + rowptr[r], vals + rowptr[r],
+                            rowptr[r + 1] - rowptr[r], wr);
+    }
+    orc_summ_merge(F, out, part);
+  }
+  free(part);
+}
+
+/* metrics (:622-769) into out[9 x F]: mean, variance, std, sum, numNonzeros,
+ * max, min, normL2, normL1                                                 */
+void orc_summ_metrics(int64_t F, const double* st, double* out) {
+  const double* s = st + OS_FIELDS * F;
+  const double cnt = s[0], TW = s[1], TW2 = s[2];
+  const double den = TW - (TW2 / TW);
+  for (int64_t c = 0; c < F; ++c) {
+    const double mean = st[OS_MEAN * F + c], ws = st[OS_WS * F + c];
+    const double nnz = st[OS_NNZ * F + c];
+    out[0 * F + c] = mean * (ws / TW);
+    double var = 0.0;
+    if (den > 0.0) var = orc_jmax((st[OS_M2N * F + c] + mean * mean * ws * (TW - ws) / TW) / den, 0.0);
+    out[1 * F + c] = var;
+    out[2 * F + c] = sqrt(var);
+    out[3 * F + c] = mean * ws;
+    out[4 * F + c] = nnz;
+    double mx = st[OS_MAX * F + c], mn = st[OS_MIN * F + c];
+    if (nnz < cnt && mx < 0.0) mx = 0.0;
+    if (nnz < cnt && mn > 0.0) mn = 0.0;
+    out[5 * F + c] = mx;
+    out[6 * F + c] = mn;
+    out[7 * F + c] = sqrt(st[OS_M2 * F + c]);
+    out[8 * F + c] = st[OS_L1 * F + c];
+  }
+}
+
+static int orc_jtoint(double x) { /* Scala Double.toInt */
+  if (x != x) return 0;
+  if (x >= 2147483647.0) return INT_MAX;
+  if (x <= -2147483648.0) return INT_MIN;
+  return (int)x;
+}
+
+/* MultiClassSummarizer.add over partitions of R rows (:43-56), the
+ * partition maps merged in order (:66-79): hist[maxC] class weight sums
+ * (classes >= maxC only raise *maxLabel), *invalid, *maxLabel (-1: none). */
+void orc_label_summarize(int64_t n, const double* y, const double* w, int64_t R, int64_t maxC,
+                         double* hist, int64_t* invalid, int64_t* maxLabel) {
+  double* part = (double*)malloc(sizeof(double) * (size_t)maxC);
+  for (int64_t c = 0; c < maxC; ++c) hist[c] = 0.0;
+  *invalid = 0;
+  *maxLabel = -1;
+  for (int64_t p0 = 0; p0 < n; p0 += R) {
+    const int64_t p1 = p0 + R < n ? p0 + R : n;
+    for (int64_t c = 0; c < maxC; ++c) part[c] = 0.0;
+    for (int64_t r = p0; r < p1; ++r) {
+      const double wr = w ? w[r] : 1.0;
+      if (!(wr > 0.0)) continue;
+      const double lab = y[r];
+      const int li = orc_jtoint(lab);
+      if (lab - (double)li != 0.0 || lab < 0) {
+        *invalid += 1;
+      } else {
+        if (li > *maxLabel) *maxLabel = li;
+        if (li < maxC) part[li] = part[li] + wr;
+      }
+    }
+    for (int64_t c = 0; c < maxC; ++c) hist[c] = hist[c] + part[c];
+  }
+  free(part);
 }

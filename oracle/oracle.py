@@ -73,6 +73,12 @@ def lib():
                 "orc_kmeans_partition_sparse": (None, [_I64, _I32, _D, _D, _D, _i64, _i64, _D,
                                                        _D, _D, _i64, _I32, _D, _D, _D, _D]),
                 "orc_row_norms_csr": (None, [_I64, _D, _i64, _D]),
+                "orc_summ_init": (None, [_i64, _D]),
+                "orc_summ_add_row": (None, [_i64, _D, _I32, _D, _i64, ctypes.c_double]),
+                "orc_summ_merge": (None, [_i64, _D, _D]),
+                "orc_summarize": (None, [_i64, _i64, _D, _I64, _I32, _D, _D, _i64, _D]),
+                "orc_summ_metrics": (None, [_i64, _D, _D]),
+                "orc_label_summarize": (None, [_i64, _D, _D, _i64, _i64, _D, _I64, _I64]),
                 "orc_dspr_upper": (None, [_i64, ctypes.c_double, _D, _D]),
                 "orc_spr_sparse": (None, [ctypes.c_double, _I32, _D, _i64, _D]),
                 "orc_gramian_partition": (None, [_D, _i64, _i64, _D, _D]),
@@ -401,3 +407,78 @@ class JavaRandom:
         mul = math.sqrt(-2 * math.log(s) / s)
         self._next_gaussian = v2 * mul
         return v1 * mul
+
+
+# --------------------------------------------------------------------------
+# Summarizer pre-pass (ml/stat/Summarizer.scala:428-770,
+# ml/stat/MultiClassSummarizer.scala:30-98)
+# --------------------------------------------------------------------------
+
+SUMM_FIELDS = 8
+SUMM_SCALARS = 5
+SUMM_METRICS = ("mean", "variance", "std", "sum", "numNonzeros", "max", "min", "normL2",
+                "normL1")
+
+
+def summarizer_new(F):
+    st = np.empty(SUMM_FIELDS * F + SUMM_SCALARS)
+    lib().orc_summ_init(F, _p(st))
+    return st
+
+
+def summarizer_add(st, F, x=None, idx=None, val=None, weight=1.0):
+    """SummarizerBuffer.add(vector, weight): dense x, or sparse (idx, val)."""
+    if x is not None:
+        x = _f64(x)
+        lib().orc_summ_add_row(F, _p(st), None, _p(x), len(x), float(weight))
+    else:
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        val = _f64(val)
+        lib().orc_summ_add_row(F, _p(st), _p(idx, _I32), _p(val), len(val), float(weight))
+    return st
+
+
+def summarizer_merge(F, a, b):
+    """a.merge(b), in place on a."""
+    lib().orc_summ_merge(F, _p(a), _p(_f64(b)))
+    return a
+
+
+def summarize(F, X=None, csr=None, w=None, rows_per_partition=1 << 62):
+    """Partitions of rows_per_partition rows, each add()-ed in order, merged in
+    partition order (the device's schedule)."""
+    out = np.empty(SUMM_FIELDS * F + SUMM_SCALARS)
+    wp = None if w is None else _f64(w)
+    if X is not None:
+        X = _f64(X)
+        lib().orc_summarize(X.shape[0], F, _p(X), None, None, None, _p(wp),
+                            int(rows_per_partition), _p(out))
+    else:
+        rp = np.ascontiguousarray(csr[0], dtype=np.int64)
+        ci = np.ascontiguousarray(csr[1], dtype=np.int32)
+        v = _f64(csr[2])
+        lib().orc_summarize(len(rp) - 1, F, None, _p(rp, _I64), _p(ci, _I32), _p(v), _p(wp),
+                            int(rows_per_partition), _p(out))
+    return out
+
+
+def summarizer_metrics(F, st):
+    out = np.empty(9 * F)
+    lib().orc_summ_metrics(F, _p(_f64(st)), _p(out))
+    m = {name: out[i * F:(i + 1) * F].copy() for i, name in enumerate(SUMM_METRICS)}
+    m["count"] = st[SUMM_FIELDS * F]
+    m["weightSum"] = st[SUMM_FIELDS * F + 1]
+    return m
+
+
+def label_summarize(y, w=None, rows_per_partition=1 << 62, max_classes=1024):
+    """(histogram[:numClasses], countInvalid, numClasses)."""
+    y = _f64(y)
+    hist = np.empty(max_classes)
+    inv = np.zeros(1, np.int64)
+    mx = np.zeros(1, np.int64)
+    lib().orc_label_summarize(len(y), _p(y), _p(None if w is None else _f64(w)),
+                              int(rows_per_partition), int(max_classes), _p(hist),
+                              _p(inv, _I64), _p(mx, _I64))
+    nc = int(mx[0]) + 1
+    return hist[:nc].copy(), int(inv[0]), nc
