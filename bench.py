@@ -163,7 +163,7 @@ class KMeansWorkload:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         threads = cpu_threads()
-        m = min(self.n, 400_000)
+        m = min(self.n, 2_000_000)
         Xs = np.ascontiguousarray(self.X[:m].cpu().numpy())
         C = self.C0.cpu().numpy()
         xn, cn = oracle.row_norms(Xs), oracle.row_norms(C)
@@ -221,7 +221,7 @@ class GramianWorkload:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         threads = cpu_threads()
-        Xs = np.ascontiguousarray(self.X[:200_000].cpu().numpy())
+        Xs = np.ascontiguousarray(self.X[:1_500_000].cpu().numpy())
         t0 = time.perf_counter()
         oracle.gramian_partition(Xs[:200])
         per_row = (time.perf_counter() - t0) / 200
@@ -279,8 +279,8 @@ class LRMultiWorkload:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         threads = cpu_threads()
-        X = self.block.X[:100_000].cpu().numpy()
-        y = self.block.labels[:100_000].cpu().numpy()
+        X = self.block.X[:2_000_000].cpu().numpy()
+        y = self.block.labels[:2_000_000].cpu().numpy()
 
         def part(rng_):
             a, b = rng_
@@ -363,7 +363,7 @@ class LRSparseWorkload:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         threads = cpu_threads()
-        m = 400_000
+        m = min(self.n, 25_000_000)
         rp = self.block.rowptr[:m + 1].cpu().numpy()
         ci = self.block.colidx[:m * self.k].cpu().numpy()
         vv = self.block.values[:m * self.k].cpu().numpy()
