@@ -82,6 +82,8 @@ SIGNATURES = {
                                       ctypes.POINTER(_vp)]),
     "cyc_multinomial_logistic_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp,
                                                               _vp, _vp, _vp, _vp, _vp]),
+    "cyc_multinomial_logistic_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64,
+                                                            _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cyc_csc_features": (_i32, [_vp]),
     "cyc_summarizer_buffer_len": (_i64, [_i32]),
     "cyc_summarizer_dense_dev": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _vp, _vp]),

@@ -351,11 +351,18 @@ static int logreg_eval(cyc_dataset ds, int32_t C, const double* coef, int fi, in
     }
   } else {
     if (ds->sparse) {
-      cyc::set_error("multinomial logistic over a CSR dataset is not supported by the device path");
-      return CYC_ERR_UNSUPPORTED;
-    }
+      if (!ds->csc && ds->rows &&
+          (rc = cyc_csc_build_dev((const int64_t*)ds->rowptr.ptr, (const int32_t*)ds->colidx.ptr,
+                                  (const double*)ds->vals.ptr, ds->rows, ds->F, ds->st, &ds->csc)))
+        return rc;
+      rc = cyc_multinomial_logistic_add_csr_dev(
+          *plan, (const int64_t*)ds->rowptr.ptr, (const int32_t*)ds->colidx.ptr,
+          (const double*)ds->vals.ptr, y, w, ds->rows, dCoef, dMean, dG, dG + dim, dG + dim + 1,
+          ds->csc, ds->st);
+    } else {
     rc = cyc_multinomial_logistic_add_dense_dev(*plan, (const double*)ds->X.ptr, y, w, ds->rows,
                                                 dCoef, dMean, dG, dG + dim, dG + dim + 1, ds->st);
+    }
   }
   if (rc) return rc;
   if ((rc = download(grad, dG, dim, ds->st)) || (rc = download(lossSum, dG + dim, 1, ds->st)) ||

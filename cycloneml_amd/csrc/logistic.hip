@@ -695,6 +695,168 @@ __global__ void k_add_scalars(const double* __restrict__ s2, double* __restrict_
   *weightSum += s2[1];
 }
 
+// ----------------------------------------------------- multinomial, CSR rows
+// margins (:112-122 with the sparse-A gemm of ml/linalg/BLAS.scala:430-536:
+// per row, t = sum over its nonzeros in order of value * linear(c, col), then
+// C(i, c) = 1.0 * C(i, c) + t * 1.0 over the offset), Utils.softmax, loss and
+// multipliers (:129-142) as in k_mlr_margins.  One wave per row, class
+// c = lane + 64 q on its lane (CQ = classes per lane); mult is n x C.
+// Per-wave partials: slabS[w][2] = (loss, weight), slabMS[w][C] = multSum.
+template <int CQ>
+__global__ __launch_bounds__(256) void k_mlr_csr_margins(
+    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
+    const double* __restrict__ vals, const double* __restrict__ labels,
+    const double* __restrict__ weights, int64_t n, int C, const double* __restrict__ coef,
+    const double* __restrict__ offset, double* __restrict__ mult, double* __restrict__ slabS,
+    double* __restrict__ slabMS) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  double offc[CQ], ms[CQ];
+#pragma unroll
+  for (int q = 0; q < CQ; ++q) {
+    const int c = lane + 64 * q;
+    offc[q] = (offset && c < C) ? offset[c] : 0.0;
+    ms[q] = 0.0;
+  }
+  double loss = 0.0, wsum = 0.0;
+  for (int64_t r = gw; r < n; r += nw) {
+    double t[CQ];
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) t[q] = 0.0;
+    const int64_t p1 = rowptr[r + 1];
+    for (int64_t p = rowptr[r]; p < p1; ++p) {
+      const double v = vals[p];
+      const double* lin = coef + (int64_t)colidx[p] * C;
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) {
+        const int c = lane + 64 * q;
+        if (c < C) t[q] = t[q] + v * lin[c];
+      }
+    }
+    double m[CQ];
+    double mx = -1.7976931348623157e308;   // Double.MinValue (Utils.scala:113)
+    int infc = 1 << 30;
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) {
+      const int c = lane + 64 * q;
+      m[q] = 1.0 * offc[q] + t[q] * 1.0;
+      if (c < C) {
+        if (m[q] == __builtin_inf()) infc = min(infc, c);
+        else if (m[q] > mx) mx = m[q];
+      }
+    }
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+      mx = fmax(mx, __shfl_xor(mx, k));
+      infc = min(infc, __shfl_xor(infc, k));
+    }
+    double pr[CQ];
+    if (infc < (1 << 30)) {
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) {
+        const int c = lane + 64 * q;
+        pr[q] = (c == infc) ? 1.0 : 0.0 * m[q];
+      }
+    } else {
+      double sum = 0.0;
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) {
+        const int c = lane + 64 * q;
+        pr[q] = (c < C) ? exp(m[q] - mx) : 0.0;
+        sum += pr[q];
+      }
+      sum = wave_sum_bcast(sum);
+      const double inv = 1.0 / sum;
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) pr[q] = inv * pr[q];
+    }
+    const double w = weights ? weights[r] : 1.0;
+    const int label = (int)labels[r];
+    double pl = 0.0;
+#pragma unroll
+    for (int q = 0; q < CQ; ++q)
+      if (q == (label >> 6)) pl = pr[q];
+    pl = __shfl(pl, label & 63);
+    wsum += w;
+    if (w > 0) loss -= w * log(pl);
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) {
+      const int c = lane + 64 * q;
+      double mu;
+      if (w > 0) {
+        mu = (w != 1.0) ? w * pr[q] : pr[q];
+        if (c == label) mu -= w;
+      } else {
+        mu = 0.0 * pr[q];
+      }
+      if (c < C) {
+        mult[r * C + c] = mu;
+        ms[q] += mu;
+      }
+    }
+  }
+  if (lane == 0) {
+    slabS[gw * 2 + 0] = loss;
+    slabS[gw * 2 + 1] = wsum;
+  }
+#pragma unroll
+  for (int q = 0; q < CQ; ++q) {
+    const int c = lane + 64 * q;
+    if (c < C) slabMS[gw * C + c] = ms[q];
+  }
+}
+
+// gradient over the row-blocked CSC copy (:156-162, linearGradSumMat =
+// sm^T x mat): one wave per feature f, classes on lanes, blocks in order and
+// each block's rows in order; then gradientSumArray(f C + c) += v and the
+// fitWithMean dger correction (:175-182) with the total multiplier sums ms.
+template <int CQ>
+__global__ __launch_bounds__(256) void k_mlr_csc_grad(
+    const int64_t* __restrict__ colptr, const int32_t* __restrict__ rowidx,
+    const double* __restrict__ cv, int64_t nb, int F, int C, const double* __restrict__ mult,
+    const double* __restrict__ ms, int fitIntercept, int fitWithMean,
+    const double* __restrict__ sm, double* __restrict__ grad) {
+  const int lane = threadIdx.x & 63;
+  const int64_t f = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (f >= F) return;
+  double tot[CQ];
+#pragma unroll
+  for (int q = 0; q < CQ; ++q) tot[q] = 0.0;
+  for (int64_t b = 0; b < nb; ++b) {
+    const int64_t e = b * F + f;
+    double sb[CQ];
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) sb[q] = 0.0;
+    const int64_t k1 = colptr[e + 1];
+    for (int64_t k = colptr[e]; k < k1; ++k) {
+      const double v = cv[k];
+      const double* mrow = mult + (int64_t)rowidx[k] * C;
+#pragma unroll
+      for (int q = 0; q < CQ; ++q) {
+        const int c = lane + 64 * q;
+        if (c < C) sb[q] = sb[q] + v * mrow[c];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) tot[q] = tot[q] + sb[q];
+  }
+#pragma unroll
+  for (int q = 0; q < CQ; ++q) {
+    const int c = lane + 64 * q;
+    if (c >= C) continue;
+    double g = grad[f * C + c] + tot[q];
+    if (fitIntercept && fitWithMean && sm[f] != 0.0) g = g + ms[c] * (-1.0 * sm[f]);
+    grad[f * C + c] = g;
+  }
+}
+
+// intercept gradient (:184-185): grad[C F + c] += 1.0 * multSum[c]
+__global__ void k_mlr_icpt(int F, int C, const double* __restrict__ ms, double* __restrict__ grad) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) grad[(int64_t)C * F + c] = grad[(int64_t)C * F + c] + 1.0 * ms[c];
+}
+
 }  // namespace
 
 struct cyc_logistic_plan_s {
@@ -1007,6 +1169,103 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
                        lossSum, weightSum);
     CYC_LAUNCH_CHECK("k_add_scalars");
   }
+  return CYC_OK;
+}
+
+
+int cyc_multinomial_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
+                                         const int32_t* colidx, const double* vals,
+                                         const double* labels, const double* weights, int64_t n,
+                                         const double* coef, const double* scaledMean,
+                                         double* grad, double* lossSum, double* weightSum,
+                                         cyc_csc csc, void* stream) {
+  int rc = check_common(p, coef, scaledMean);
+  if (rc) return rc;
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  if (n == 0) return CYC_OK;
+  CYC_REQUIRE(csc != nullptr && cyc_csc_rows(csc) == n,
+              "a CSC copy of these rows is required (cyc_csc_build_dev)");
+  const int F = p->F, C = p->C;
+  if (C > 1024) {
+    cyc::set_error("multinomial CSR aggregator supports numClasses <= 1024");
+    return CYC_ERR_UNSUPPORTED;
+  }
+  const int cq = (C + 63) / 64;
+  std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  const int64_t waves = std::min<int64_t>(n, 8192);
+  const unsigned blocks = (unsigned)((waves + 3) / 4);
+  const int64_t wtot = (int64_t)blocks * 4;
+  if ((rc = p->multBuf.reserve(sizeof(double) * (size_t)n * C)) ||
+      (rc = p->slabS.reserve(sizeof(double) * (size_t)wtot * 2)) ||
+      (rc = p->slabMS.reserve(sizeof(double) * (size_t)wtot * C)) ||
+      (rc = p->scal.reserve(sizeof(double) * 4)) ||
+      (rc = p->msTot.reserve(sizeof(double) * (size_t)C)) ||
+      (rc = p->offset.reserve(sizeof(double) * (size_t)C)))
+    return rc;
+  const double* off = nullptr;
+  if (p->fitIntercept) {
+    if (p->fitWithMean) {
+      hipLaunchKernelGGL(k_mlr_offset, dim3((C + 63) / 64), dim3(64), 0, st, coef, scaledMean, F,
+                         C, (double*)p->offset.ptr);
+      CYC_LAUNCH_CHECK("k_mlr_offset");
+      off = (const double*)p->offset.ptr;
+    } else {
+      off = coef + (int64_t)C * F;
+    }
+  }
+  CYC_HIP(hipMemsetAsync(p->slabS.ptr, 0, sizeof(double) * (size_t)wtot * 2, st));
+  CYC_HIP(hipMemsetAsync(p->slabMS.ptr, 0, sizeof(double) * (size_t)wtot * C, st));
+  double* mult = (double*)p->multBuf.ptr;
+#define CYC_MLRC_M(Q)                                                                          \
+  hipLaunchKernelGGL(k_mlr_csr_margins<Q>, dim3(blocks), dim3(256), 0, st, rowptr, colidx, vals, \
+                     labels, weights, n, C, coef, off, mult, (double*)p->slabS.ptr,             \
+                     (double*)p->slabMS.ptr)
+  {
+    cyc::KernelTimer tm("k_mlr_csr_margins", st);
+    if (cq <= 1) CYC_MLRC_M(1);
+    else if (cq <= 2) CYC_MLRC_M(2);
+    else if (cq <= 4) CYC_MLRC_M(4);
+    else if (cq <= 8) CYC_MLRC_M(8);
+    else CYC_MLRC_M(16);
+    CYC_LAUNCH_CHECK("k_mlr_csr_margins");
+  }
+#undef CYC_MLRC_M
+  hipLaunchKernelGGL(k_fold_columns, dim3((C + 127) / 128), dim3(128), 0, st,
+                     (const double*)p->slabMS.ptr, wtot, C, (double*)p->msTot.ptr);
+  CYC_LAUNCH_CHECK("k_fold_columns");
+  hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, (const double*)p->slabS.ptr, wtot,
+                     2, (double*)p->scal.ptr);
+  CYC_LAUNCH_CHECK("k_fold_scalars");
+  int64_t R = 0, nb = 0;
+  if ((rc = cyc_csc_blocks(csc, &R, &nb))) return rc;
+  const int64_t* colptr;
+  const int32_t* rowidx;
+  const double* cv;
+  if ((rc = cyc_csc_arrays(csc, &colptr, &rowidx, &cv))) return rc;
+  const unsigned gblocks = (unsigned)(((int64_t)F + 3) / 4);
+#define CYC_MLRC_G(Q)                                                                          \
+  hipLaunchKernelGGL(k_mlr_csc_grad<Q>, dim3(gblocks), dim3(256), 0, st, colptr, rowidx, cv, nb, \
+                     F, C, (const double*)mult, (const double*)p->msTot.ptr, p->fitIntercept,   \
+                     p->fitWithMean, scaledMean, grad)
+  {
+    cyc::KernelTimer tg("k_mlr_csc_grad", st);
+    if (cq <= 1) CYC_MLRC_G(1);
+    else if (cq <= 2) CYC_MLRC_G(2);
+    else if (cq <= 4) CYC_MLRC_G(4);
+    else if (cq <= 8) CYC_MLRC_G(8);
+    else CYC_MLRC_G(16);
+    CYC_LAUNCH_CHECK("k_mlr_csc_grad");
+  }
+#undef CYC_MLRC_G
+  if (p->fitIntercept) {
+    hipLaunchKernelGGL(k_mlr_icpt, dim3((C + 255) / 256), dim3(256), 0, st, F, C,
+                       (const double*)p->msTot.ptr, grad);
+    CYC_LAUNCH_CHECK("k_mlr_icpt");
+  }
+  hipLaunchKernelGGL(k_add_scalars, dim3(1), dim3(1), 0, st, (const double*)p->scal.ptr, lossSum,
+                     weightSum);
+  CYC_LAUNCH_CHECK("k_add_scalars");
   return CYC_OK;
 }
 

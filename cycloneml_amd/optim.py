@@ -282,9 +282,14 @@ class MultinomialLogisticBlockAggregator(DifferentiableLossAggregator):
         """MultinomialLogisticBlockAggregator.scala:101-189 over the shard."""
         _check_block(self, block)
         if block.is_sparse:
-            raise N.CycloneError(N.CYC_ERR_UNSUPPORTED,
-                                 "sparse blocks for the multinomial aggregator are not on the "
-                                 "device path yet")
+            block.prepare(stream)          # CSC copy for the gradient (built once)
+            N.check(N.load().cyc_multinomial_logistic_add_csr_dev(
+                self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx),
+                N.ptr(block.values), N.ptr(block.labels), N.ptr(block.weights), block.size,
+                N.ptr(self.coef), N.ptr(self.scaledMean), N.ptr(self.gradientSumArray),
+                N.ptr(self._loss_sum), N.ptr(self._weight_sum), block.csc,
+                N.stream_handle(stream)))
+            return self
         N.check(N.load().cyc_multinomial_logistic_add_dense_dev(
             self._plan.handle, N.ptr(block.X), N.ptr(block.labels), N.ptr(block.weights),
             block.size, N.ptr(self.coef), N.ptr(self.scaledMean), N.ptr(self.gradientSumArray),

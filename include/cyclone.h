@@ -224,6 +224,15 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan plan, const double*
                                            int64_t n, const double* coef,
                                            const double* scaledMean, double* grad,
                                            double* lossSum, double* weightSum, void* stream);
+/* CSR rows (the sparse InstanceBlock branch of :122 and :156-162): margins
+ * by a wave per row, gradient over the CSC copy (required: built from these
+ * rows by cyc_csc_build_dev), numClasses <= 1024. */
+int cyc_multinomial_logistic_add_csr_dev(cyc_logistic_plan plan, const int64_t* rowptr,
+                                         const int32_t* colidx, const double* vals,
+                                         const double* labels, const double* weights, int64_t n,
+                                         const double* coef, const double* scaledMean,
+                                         double* grad, double* lossSum, double* weightSum,
+                                         cyc_csc csc, void* stream);
 
 /* ------------------------------------------------ summarizer pre-pass */
 /* The first pass of LogisticRegression.train (LogisticRegression.scala:
@@ -278,8 +287,8 @@ int cyc_scale_columns_csr_dev(const int32_t* colidx, double* vals, int64_t nnz,
  *   cyc_logreg_*_eval           RDDLossFunction.scala:56-70's seqOp over the
  *                               partition's blocks
  *   cyc_gramian, cyc_col_sums   RowMatrix.scala:130-161, :163-220, :456
- * Dense datasets serve every entry point; CSR datasets serve KMeans and the
- * binary logistic aggregator (others return CYC_ERR_UNSUPPORTED). */
+ * Dense datasets serve every entry point; CSR datasets serve KMeans and both
+ * logistic aggregators (the Gramian calls return CYC_ERR_UNSUPPORTED). */
 typedef struct cyc_dataset_s* cyc_dataset;
 
 int cyc_dataset_dense_create(int32_t numFeatures, int64_t capacity_rows, int has_labels,

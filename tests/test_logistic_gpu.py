@@ -82,6 +82,27 @@ def test_multinomial_vs_oracle(cuda, fi, fwm, n, F, C):
     assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * abs(st["loss"])
 
 
+@pytest.mark.parametrize("fi,fwm", [(False, False), (True, False), (True, True)])
+@pytest.mark.parametrize("n,F,C", [(1, 3, 2), (300, 20, 3), (2000, 64, 10), (1500, 300, 100),
+                                   (600, 50, 130)])
+def test_multinomial_csr_vs_oracle(cuda, fi, fwm, n, F, C):
+    """Sparse InstanceBlocks through the multinomial aggregator (:122 sparse
+    gemm, :156-162 sparse gradient): margins by row, gradient over the CSC copy."""
+    from cycloneml_amd.optim import DeviceInstanceBlock, MultinomialLogisticBlockAggregator
+    rng = np.random.default_rng(n + F * 5 + C)
+    _, csr, labels, w = _make(n, F, True, rng, classes=C, zero_w=True)
+    coef = rng.normal(size=C * F + (C if fi else 0)) * (1.0 / np.sqrt(F))
+    sm = rng.normal(size=F) * 0.1 if fwm else None
+    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+    oracle.multinomial_logistic_add(_oracle_block(None, csr, labels, w, F), coef, C, fi, fwm, sm,
+                                    st)
+    blk = DeviceInstanceBlock.from_numpy(labels, w, csr=csr, numFeatures=F, device=cuda)
+    agg = MultinomialLogisticBlockAggregator(np.ones(F), sm, fi, fwm, coef, device=cuda).add(blk)
+    _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
+    assert abs(agg.weight - st["weight"]) <= 1e-12 * max(st["weight"], 1e-300)
+    assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * max(abs(st["loss"]), 1e-300)
+
+
 def test_aggregator_requires(cuda):
     from cycloneml_amd import _native as N
     from cycloneml_amd.optim import BinaryLogisticBlockAggregator, DeviceInstanceBlock
