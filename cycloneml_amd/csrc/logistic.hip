@@ -415,37 +415,65 @@ __global__ void k_mlr_offset(const double* __restrict__ coef, const double* __re
   off[c] = o;
 }
 
-constexpr int MR = 128;    // rows per margin tile (4 waves x 32 rows)
-constexpr int MK = 32;     // features per LDS chunk
-constexpr int MKS = MK + 2;  // X chunk row stride: == 2 (mod 32) doubles
+constexpr int MR = 256;    // rows per margin tile (8 waves x 32 rows)
+constexpr int MK = 16;     // features per LDS chunk
+constexpr int MKS = MK + 2;  // X chunk row stride: 36 dwords, conflict-free ds_read_b64
+constexpr int MT = 512;    // threads per margin workgroup
 
-// margins = X W^T (+ offset) for 128-row tiles; X and W chunks of 32
+// margins = X W^T (+ offset) for 256-row tiles; X and W chunks of 16
 // features staged through LDS (coalesced loads), 2 row tiles x CT class tiles
 // of 16x16 per wave on v_mfma_f64_16x16x4f64; softmax/loss/multiplier
-// epilogue in registers.  Persistent over tiles; 2 workgroups per CU so one
-// stages while the other computes.
+// epilogue in registers.  Persistent over tiles, one 8-wave workgroup per CU;
+// the next chunk of X and W is loaded into registers while the current one is
+// multiplied (one LDS buffer, no load latency on the MFMA path), and the
+// 256-row tile halves the W re-reads per row of a 4-wave tile.
 template <int CT>
-__global__ __launch_bounds__(256, 2) void k_mlr_margins(
+__global__ __launch_bounds__(MT) void k_mlr_margins(
     const double* __restrict__ X, const double* __restrict__ labels,
     const double* __restrict__ weights, int64_t n, int F, int C, const double* __restrict__ coef,
     const double* __restrict__ offset, double* __restrict__ mult, double* __restrict__ slabS,
     double* __restrict__ slabMS) {
   constexpr int CP = CT * 16;
   constexpr int CPS = CP + ((16 - CP % 32) + 32) % 32;  // == 16 (mod 32) doubles
+  constexpr int XPT = MR * MK / MT;                     // X doubles per thread (16)
+  constexpr int WPT = (MK * CP + MT - 1) / MT;          // W doubles per thread
   __shared__ __attribute__((aligned(16))) double Xs[MR * MKS];
   __shared__ __attribute__((aligned(16))) double Ws[MK * CPS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t tiles = (n + MR - 1) / MR;
+  const int nch = (F + MK - 1) / MK;
   double loss = 0.0, wsum = 0.0;
   double ms[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) ms[ct] = 0.0;
-  double offc[CT];
+  double xr[XPT], wr[WPT];
+  // Loads go through buffer descriptors: one 32-bit VGPR offset per element
+  // (no 64-bit address math held across the loop); rows past n and padding
+  // classes read as zero (out-of-range offsets).  Host guarantees
+  // MR * F * 8 < 2^31 and C * F * 8 < 2^31.
+  constexpr int OOB = 0x7ff00000;
+  const auto wR = __builtin_amdgcn_make_buffer_rsrc((void*)coef, (short)0, C * F * 8, 0x00020000);
+  const int xlane = ((tid / MK) * F + (tid % MK)) * 8;
+  auto load_regs = [&](int64_t r0, int f0) {
+    const int64_t nr = min<int64_t>(MR, n - r0);
+    const auto xR = __builtin_amdgcn_make_buffer_rsrc((void*)(X + r0 * F), (short)0,
+                                                      (int)(nr * F * 8), 0x00020000);
+    const bool fok = f0 + (tid % MK) < F;
 #pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-    const int c = ct * 16 + (lane & 15);
-    offc[ct] = (offset && c < C) ? offset[c] : 0.0;
-  }
+    for (int i = 0; i < XPT; ++i) {
+      const int off = fok ? xlane + i * (MT / MK) * F * 8 + f0 * 8 : OOB;
+      xr[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xR, off, 0, 0));
+    }
+    // features f0..f0+MK-1 are one contiguous run of coef (f*C + c)
+    const int fl = min(MK, F - f0);
+#pragma unroll
+    for (int i = 0; i < WPT; ++i) {
+      const int e = tid + MT * i;
+      const int ff = e / CP, c = e - ff * CP;
+      const int off = (e < MK * CP && ff < fl && c < C) ? ((f0 + ff) * C + c) * 8 : OOB;
+      wr[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(wR, off, 0, 0));
+    }
+  };
 
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t r0 = tile * MR;
@@ -454,22 +482,22 @@ __global__ __launch_bounds__(256, 2) void k_mlr_margins(
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[t][ct] = cyc_double4{0.0, 0.0, 0.0, 0.0};
-    for (int f0 = 0; f0 < F; f0 += MK) {
+    load_regs(r0, 0);
+    for (int ch = 0; ch < nch; ++ch) {
       __syncthreads();
-      // X chunk: 128 rows x 32 features
-      for (int e = tid; e < MR * MK; e += 256) {
-        const int rr = e >> 5, ff = e & 31;
-        const int64_t r = r0 + rr;
-        const int f = f0 + ff;
-        Xs[rr * MKS + ff] = (r < n && f < F) ? X[r * F + f] : 0.0;
+#pragma unroll
+      for (int i = 0; i < XPT; ++i) {
+        const int e = tid + MT * i;
+        Xs[(e / MK) * MKS + (e % MK)] = xr[i];
       }
-      // W chunk: features f0..f0+31 are one contiguous run of coef (f*C + c)
-      const int fl = min(MK, F - f0);
-      for (int e = tid; e < MK * CP; e += 256) {
+#pragma unroll
+      for (int i = 0; i < WPT; ++i) {
+        const int e = tid + MT * i;
         const int ff = e / CP, c = e - ff * CP;
-        Ws[ff * CPS + c] = (ff < fl && c < C) ? coef[(int64_t)(f0 + ff) * C + c] : 0.0;
+        if (e < MK * CP) Ws[ff * CPS + c] = wr[i];
       }
       __syncthreads();
+      if (ch + 1 < nch) load_regs(r0, (ch + 1) * MK);
 #pragma unroll
       for (int kk = 0; kk < MK; kk += 4) {
         const double a0 = Xs[(wave * 32 + (lane & 15)) * MKS + kk + (lane >> 4)];
@@ -496,7 +524,8 @@ __global__ __launch_bounds__(256, 2) void k_mlr_margins(
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
           const int c = ct * 16 + (lane & 15);
-          m[ct] = acc[t][ct][r] + offc[ct];  // 1.0*temp + 1.0*offset (netlib dgemm)
+          const double oc = (offset && c < C) ? offset[c] : 0.0;
+          m[ct] = acc[t][ct][r] + oc;  // 1.0*temp + 1.0*offset (netlib dgemm)
           if (c < C) {
             if (m[ct] == __builtin_inf()) infc = min(infc, c);
             else if (m[ct] > mx) mx = m[ct];
@@ -566,7 +595,7 @@ __global__ __launch_bounds__(256, 2) void k_mlr_margins(
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) ms[ct] += __shfl_xor(ms[ct], k);
   }
-  const int64_t gw = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t gw = (int64_t)blockIdx.x * (MT / 64) + wave;
   if (lane == 0) {
     slabS[gw * 2 + 0] = loss;
     slabS[gw * 2 + 1] = wsum;
@@ -1076,13 +1105,18 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
     cyc::set_error("multinomial aggregator supports numClasses <= 128");
     return CYC_ERR_UNSUPPORTED;
   }
+  if ((int64_t)C * F * 8 >= INT32_MAX || (int64_t)MR * F * 8 >= INT32_MAX) {
+    cyc::set_error("dense multinomial aggregator supports numClasses * numFeatures < 2^28 "
+                   "and numFeatures < 2^20");
+    return CYC_ERR_UNSUPPORTED;
+  }
   const int CT = (C + 15) / 16, CP = CT * 16;
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
   // Rows are processed in chunks so the multiplier matrix stays small.
   const int64_t chunk = std::min<int64_t>(n, 4 << 20);
-  const int mblocks = 512;   // persistent: 2 per CU
-  const int64_t mwaves = (int64_t)mblocks * 4;
+  const int mblocks = 256;   // persistent: one 8-wave workgroup per CU
+  const int64_t mwaves = (int64_t)mblocks * (MT / 64);
   const int ftiles = (F + GF - 1) / GF;
   if ((rc = p->multBuf.reserve(sizeof(double) * (size_t)chunk * CP)) ||
       (rc = p->slabS.reserve(sizeof(double) * (size_t)mwaves * 2)) ||
@@ -1112,7 +1146,7 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
     CYC_HIP(hipMemsetAsync(p->slabS.ptr, 0, sizeof(double) * (size_t)mwaves * 2, st));
     CYC_HIP(hipMemsetAsync(p->slabMS.ptr, 0, sizeof(double) * (size_t)mwaves * CP, st));
 #define CYC_MLR_M(CTV)                                                                        \
-  hipLaunchKernelGGL(k_mlr_margins<CTV>, dim3(mb), dim3(256), 0, st, Xc, lc, wc, m, F, C, coef, \
+  hipLaunchKernelGGL(k_mlr_margins<CTV>, dim3(mb), dim3(MT), 0, st, Xc, lc, wc, m, F, C, coef, \
                      off, (double*)p->multBuf.ptr, (double*)p->slabS.ptr, (double*)p->slabMS.ptr)
     {
     cyc::KernelTimer tm("k_mlr_margins", st);
