@@ -48,6 +48,10 @@ SIGNATURES = {
     "cyc_kmeans_stats_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     "cyc_kmeans_assign_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
                                              _pi64, _vp]),
+    "cyc_kmeans_point_cost_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                                 _vp, _vp]),
+    "cyc_kmeans_point_cost_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp,
+                                                     _vp, _vp, _vp]),
     "cyc_kmeans_accumulate_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                                  _vp, _vp, _vp, _vp, _vp]),
     "cyc_kmeans_rows_create": (ctypes.c_int, [_vp, _vp, _i64, _vp, ctypes.POINTER(_vp)]),

@@ -65,6 +65,19 @@ class KMeansPlan:
             ctypes.byref(n_exact) if count_exact else None, N.stream_handle(stream)))
         return n_exact.value
 
+    def point_cost(self, X, xnorm, C, cnorm, assign, cost, stream=None, rows=None):
+        """findClosest(centers, point) without statistics for every row
+        (DistanceMeasure.pointCost, DistanceMeasure.scala:152-156, 318-340)."""
+        N.check(self._lib.cyc_kmeans_point_cost_dev(
+            self.handle, N.ptr(X), N.ptr(xnorm), _rows_handle(rows), int(X.shape[0]), N.ptr(C),
+            N.ptr(cnorm), N.ptr(assign), N.ptr(cost), N.stream_handle(stream)))
+
+    def point_cost_csr(self, rowptr, colidx, values, xnorm, C, cnorm, assign, cost, stream=None):
+        N.check(self._lib.cyc_kmeans_point_cost_csr_dev(
+            self.handle, N.ptr(rowptr), N.ptr(colidx), N.ptr(values), N.ptr(xnorm),
+            int(rowptr.shape[0]) - 1, N.ptr(C), N.ptr(cnorm), N.ptr(assign), N.ptr(cost),
+            N.stream_handle(stream)))
+
     def last_tiers(self):
         """(rows left to the fp64 screen, rows left to the exact loop) of the
         last assign(count_exact=True)."""
@@ -164,6 +177,93 @@ class KMeansModel:
     @property
     def k(self):
         return self.clusterCenters.shape[0]
+
+    # ---- device-side scoring (KMeansModel.scala:82-117) -----------------
+    def _device_state(self, device, n, csr_d=None):
+        torch = _torch()
+        key = (str(device), csr_d)
+        st = getattr(self, "_dev", None)
+        if st is None or st["key"] != key:
+            C = torch.from_numpy(self.clusterCenters).to(device)
+            d = self.clusterCenters.shape[1]
+            plan = KMeansPlan(d if csr_d is None else csr_d, self.k, max(1, n))
+            cnorm = row_norms(C)
+            # the model's lazy statistics (KMeansModel.scala:51-56)
+            plan.stats(C)
+            st = self._dev = {"key": key, "C": C, "cnorm": cnorm, "plan": plan}
+        return st
+
+    def predict(self, X, xnorm=None, stream=None):
+        """predict(points): findClosest(centersWithNorm, statistics, point)._1
+        for every row of the device matrix X (KMeansModel.scala:82-97).
+        Returns an int32 device tensor."""
+        torch = _torch()
+        n = int(X.shape[0])
+        st = self._device_state(X.device, n)
+        xn = row_norms(X, stream=stream) if xnorm is None else xnorm
+        a = torch.empty(n, dtype=torch.int32, device=X.device)
+        c = torch.empty(n, dtype=torch.float64, device=X.device)
+        if n:
+            st["plan"].assign(X, xn, st["C"], st["cnorm"], a, c, stream=stream)
+        return a
+
+    def predict_csr(self, rowptr, colidx, values, xnorm=None, stream=None):
+        """predict for CSR rows (SparseVector points; libsvm input)."""
+        torch = _torch()
+        n = int(rowptr.shape[0]) - 1
+        st = self._device_state(values.device, n, csr_d=self.clusterCenters.shape[1])
+        xn = row_norms_csr(rowptr, values, stream=stream) if xnorm is None else xnorm
+        a = torch.empty(n, dtype=torch.int32, device=values.device)
+        c = torch.empty(n, dtype=torch.float64, device=values.device)
+        if n:
+            st["plan"].assign_csr(rowptr, colidx, values, xn, st["C"], st["cnorm"], a, c,
+                                  stream=stream)
+        return a
+
+    def pointCosts(self, X, xnorm=None, stream=None):
+        """DistanceMeasure.pointCost (DistanceMeasure.scala:152-156) for every
+        row: (assign int32, cost fp64) device tensors."""
+        torch = _torch()
+        n = int(X.shape[0])
+        st = self._device_state(X.device, n)
+        xn = row_norms(X, stream=stream) if xnorm is None else xnorm
+        a = torch.empty(n, dtype=torch.int32, device=X.device)
+        c = torch.empty(n, dtype=torch.float64, device=X.device)
+        if n:
+            st["plan"].point_cost(X, xn, st["C"], st["cnorm"], a, c, stream=stream)
+        return a, c
+
+    def pointCosts_csr(self, rowptr, colidx, values, xnorm=None, stream=None):
+        torch = _torch()
+        n = int(rowptr.shape[0]) - 1
+        st = self._device_state(values.device, n, csr_d=self.clusterCenters.shape[1])
+        xn = row_norms_csr(rowptr, values, stream=stream) if xnorm is None else xnorm
+        a = torch.empty(n, dtype=torch.int32, device=values.device)
+        c = torch.empty(n, dtype=torch.float64, device=values.device)
+        if n:
+            st["plan"].point_cost_csr(rowptr, colidx, values, xn, st["C"], st["cnorm"], a, c,
+                                      stream=stream)
+        return a, c
+
+    def computeCost(self, X, xnorm=None, stream=None):
+        """computeCost(data) = data.map(pointCost).sum() (KMeansModel.scala:
+        110-117): per-row costs bit-identical to the reference; the sum runs
+        in a fixed device order, then across ranks (one all-reduce, like the
+        driver's fold over partitions)."""
+        _, c = self.pointCosts(X, xnorm, stream)
+        return self._sum_costs(c)
+
+    def computeCost_csr(self, rowptr, colidx, values, xnorm=None, stream=None):
+        _, c = self.pointCosts_csr(rowptr, colidx, values, xnorm, stream)
+        return self._sum_costs(c)
+
+    @staticmethod
+    def _sum_costs(c):
+        torch = _torch()
+        tot = c.sum().reshape(1) if c.numel() else torch.zeros(1, dtype=torch.float64,
+                                                               device=c.device)
+        parallel.allreduce_(tot)
+        return float(tot.item())
 
 
 class KMeans:

@@ -974,28 +974,30 @@ __global__ __launch_bounds__(256) void k_assign_exact(
     const int64_t r = slowList[idx];
     const double* x = X + r * d;
     const double xn = xnorm[r];
-    double best = seq_sqdist(C, x, d);          // :286, uniform across the wave
+    // stats == nullptr: findClosest(centers, point) (:318-340), best from +inf
+    const bool ns = stats == nullptr;
+    double best = ns ? __builtin_inf() : seq_sqdist(C, x, d);   // :286
     int bi = 0;
-    bool done = best < stats[0];                // :287
-    for (int i0 = 1; !done && i0 < k; i0 += 64) {
+    bool done = !ns && best < stats[0];                // :287
+    for (int i0 = ns ? 0 : 1; !done && i0 < k; i0 += 64) {
       const int i = i0 + lane;
       const bool valid = i < k;
       double lb = __builtin_inf(), sii = 0.0;
       if (valid) {
         const double nd = dsub(cnorm[i], xn);     // :294-295
         lb = dmul(nd, nd);
-        sii = stats[iut(i, i)];
+        sii = ns ? 0.0 : stats[iut(i, i)];
       }
       double dd = 0.0;
       bool have = false;
       int pos = 0;
       for (;;) {
-        const bool visit = valid && lane >= pos && lb < best && stats[iut(i, bi)] < best;
+        const bool visit = valid && lane >= pos && lb < best && (ns || stats[iut(i, bi)] < best);
         if (visit && !have) {
           dd = seq_sqdist(C + (int64_t)i * d, x, d);
           have = true;
         }
-        const bool brk = visit && dd < sii;
+        const bool brk = !ns && visit && dd < sii;
         const bool ev = visit && (brk || dd < best);
         const unsigned long long m = __ballot(ev);
         if (!m) break;
@@ -1014,6 +1016,14 @@ __global__ __launch_bounds__(256) void k_assign_exact(
       if (cost) cost[r] = best;
     }
   }
+}
+
+// pointCost of a row no center reaches (NaN/Inf coordinates): findClosest
+// without statistics keeps bestDistance = +Infinity (:321-337), while the
+// recomputed sqdist to center 0 is NaN or +Infinity.
+__global__ void k_nostats_cost_fix(int64_t n, double* __restrict__ cost) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < n && __builtin_isnan(cost[r])) cost[r] = __builtin_inf();
 }
 
 // ------------------------------------------------------- counting sort
@@ -1577,28 +1587,30 @@ __global__ __launch_bounds__(256) void k_assign_sparse(
     const int32_t* idx = colidx + q0;
     const double* val = vals + q0;
     const double xn = xnorm[r];
-    double best = fast_sqdist_ds(C, cnorm[0], idx, val, nnz, xn, d);   // :286
+    // stats == nullptr: findClosest(centers, point) (:318-340), best from +inf
+    const bool ns = stats == nullptr;
+    double best = ns ? __builtin_inf() : fast_sqdist_ds(C, cnorm[0], idx, val, nnz, xn, d);   // :286
     int bi = 0;
-    bool done = best < stats[0];                                       // :287
-    for (int i0 = 1; !done && i0 < k; i0 += 64) {
+    bool done = !ns && best < stats[0];                                       // :287
+    for (int i0 = ns ? 0 : 1; !done && i0 < k; i0 += 64) {
       const int i = i0 + lane;
       const bool valid = i < k;
       double lb = __builtin_inf(), sii = 0.0;
       if (valid) {
         const double ndf = dsub(cnorm[i], xn);                         // :294-295
         lb = dmul(ndf, ndf);
-        sii = stats[iut(i, i)];
+        sii = ns ? 0.0 : stats[iut(i, i)];
       }
       double dd = 0.0;
       bool have = false;
       int pos = 0;
       for (;;) {
-        const bool visit = valid && lane >= pos && lb < best && stats[iut(i, bi)] < best;
+        const bool visit = valid && lane >= pos && lb < best && (ns || stats[iut(i, bi)] < best);
         if (visit && !have) {
           dd = fast_sqdist_ds(C + (int64_t)i * d, cnorm[i], idx, val, nnz, xn, d);
           have = true;
         }
-        const bool brk = visit && dd < sii;
+        const bool brk = !ns && visit && dd < sii;
         const bool ev = visit && (brk || dd < best);
         const unsigned long long m = __ballot(ev);
         if (!m) break;
@@ -1784,7 +1796,11 @@ int launch_assign3(cyc_kmeans_plan p, const double* X, const double* xnorm, int6
 
 int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmeans_rows rows,
               int64_t n, const double* C, const double* cnorm, int32_t* assign, double* cost,
-              int64_t* n_exact_out, hipStream_t st) {
+              int64_t* n_exact_out, hipStream_t st, bool nostats = false) {
+  // nostats: findClosest(centers, point) (DistanceMeasure.scala:318-340); the
+  // screens certify only rows whose winner both loops return, so only the
+  // exact tier differs (no statistics prunes, best starts at +inf)
+  const double* statsArg = nostats ? nullptr : (const double*)p->stats.ptr;
   CYC_HIP(hipMemsetAsync(p->slowCount.ptr, 0, sizeof(unsigned int), st));
   int rc = CYC_OK;
   const int32_t* rowList = nullptr;
@@ -1841,7 +1857,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
     p->lastExact = h_slow;
     if (h_slow) {
       hipLaunchKernelGGL(k_assign_exact, dim3((unsigned)std::min<unsigned>((h_slow + 3) / 4, 4096)), dim3(256), 0, st, X, xnorm,
-                         p->d, C, cnorm, p->k, (const double*)p->stats.ptr,
+                         p->d, C, cnorm, p->k, statsArg,
                          (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr,
                          assign, cost);
       CYC_LAUNCH_CHECK("k_assign_exact");
@@ -1849,7 +1865,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
   } else {
     const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 2048);
     hipLaunchKernelGGL(k_assign_exact, dim3(grid), dim3(256), 0, st, X, xnorm,
-                       p->d, C, cnorm, p->k, (const double*)p->stats.ptr,
+                       p->d, C, cnorm, p->k, statsArg,
                        (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr, assign,
                        cost);
     CYC_LAUNCH_CHECK("k_assign_exact");
@@ -2054,6 +2070,33 @@ int cyc_kmeans_assign_dev(cyc_kmeans_plan p, const double* X, const double* xnor
   return CYC_OK;
 }
 
+int cyc_kmeans_point_cost_dev(cyc_kmeans_plan p, const double* X, const double* xnorm,
+                              cyc_kmeans_rows rows, int64_t n, const double* C,
+                              const double* cnorm, int32_t* assign, double* cost, void* stream) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  CYC_REQUIRE(assign != nullptr && cost != nullptr, "assign and cost must not be null");
+  if (n == 0) return CYC_OK;
+  if (int rc = check_rows(p, rows, X, n)) return rc;
+  if (!p->dense_ok) {
+    cyc::set_error("d > 1240 is not supported by the LDS-resident assign kernel (dense rows)");
+    return CYC_ERR_UNSUPPORTED;
+  }
+  std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  int rc = ensure_rows(p, n);
+  if (rc) return rc;
+  if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st, true)))
+    return rc;
+  hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n, p->d, C,
+                     (const int32_t*)assign, cost);
+  CYC_LAUNCH_CHECK("k_row_cost");
+  hipLaunchKernelGGL(k_nostats_cost_fix, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n,
+                     cost);
+  CYC_LAUNCH_CHECK("k_nostats_cost_fix");
+  return CYC_OK;
+}
+
 int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* xnorm,
                               cyc_kmeans_rows rows, const double* weights, int64_t n,
                               const double* C, const double* cnorm, double* sums, double* wsum,
@@ -2195,11 +2238,13 @@ int cyc_row_norms_csr_dev(const int64_t* rowptr, const double* vals, int64_t n, 
 namespace {
 int sparse_assign(cyc_kmeans_plan p, const int64_t* rowptr, const int32_t* colidx,
                   const double* vals, const double* xnorm, int64_t n, const double* C,
-                  const double* cnorm, int32_t* assign, double* cost, hipStream_t st) {
+                  const double* cnorm, int32_t* assign, double* cost, hipStream_t st,
+                  bool nostats = false) {
   const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 8192);
   cyc::KernelTimer timer("k_kmeans_assign_sparse", st);
   hipLaunchKernelGGL(k_assign_sparse, dim3(grid), dim3(256), 0, st, rowptr, colidx, vals, xnorm,
-                     n, p->d, C, cnorm, p->k, (const double*)p->stats.ptr, assign, cost);
+                     n, p->d, C, cnorm, p->k, nostats ? nullptr : (const double*)p->stats.ptr,
+                     assign, cost);
   CYC_LAUNCH_CHECK("k_assign_sparse");
   return CYC_OK;
 }
@@ -2215,6 +2260,19 @@ int cyc_kmeans_assign_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr, const in
   std::lock_guard<std::mutex> g(p->mu);
   return sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost,
                        cyc::as_stream(stream));
+}
+
+int cyc_kmeans_point_cost_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
+                                  const int32_t* colidx, const double* vals, const double* xnorm,
+                                  int64_t n, const double* C, const double* cnorm,
+                                  int32_t* assign, double* cost, void* stream) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  CYC_REQUIRE(assign != nullptr && cost != nullptr, "assign and cost must not be null");
+  if (n == 0) return CYC_OK;
+  std::lock_guard<std::mutex> g(p->mu);
+  return sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost,
+                       cyc::as_stream(stream), true);
 }
 
 int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,

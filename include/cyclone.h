@@ -102,6 +102,16 @@ int cyc_kmeans_assign_dev(cyc_kmeans_plan plan, const double* X, const double* x
                           cyc_kmeans_rows rows, int64_t n, const double* C, const double* cnorm,
                           int32_t* assign, double* cost, int64_t* n_exact_out, void* stream);
 
+/* findClosest(centers, point) WITHOUT statistics (DistanceMeasure.scala:
+ * 318-340): the loop behind DistanceMeasure.pointCost (:152-156), i.e.
+ * KMeansModel.computeCost (mllib/clustering/KMeansModel.scala:110-117) and the
+ * k-means|| cost updates (KMeans.scala:379-402).  Needs no statistics on the
+ * plan.  assign[n] / cost[n] bit-identical to the reference loop (a point no
+ * center reaches keeps cost +Infinity, index 0). */
+int cyc_kmeans_point_cost_dev(cyc_kmeans_plan plan, const double* X, const double* xnorm,
+                              cyc_kmeans_rows rows, int64_t n, const double* C,
+                              const double* cnorm, int32_t* assign, double* cost, void* stream);
+
 /* Screening tiers of the last cyc_kmeans_assign_dev call that asked for
  * n_exact_out: rows the first screen (i8 with a row image, else bf16x3) left
  * to the fp64 MFMA screen (all rows when neither runs), and rows left to the
@@ -140,6 +150,11 @@ int cyc_row_norms_csr_dev(const int64_t* rowptr, const double* vals, int64_t n, 
 int cyc_kmeans_assign_csr_dev(cyc_kmeans_plan plan, const int64_t* rowptr, const int32_t* colidx,
                               const double* vals, const double* xnorm, int64_t n, const double* C,
                               const double* cnorm, int32_t* assign, double* cost, void* stream);
+/* findClosest(centers, point) without statistics for CSR rows (pointCost). */
+int cyc_kmeans_point_cost_csr_dev(cyc_kmeans_plan plan, const int64_t* rowptr,
+                                  const int32_t* colidx, const double* vals, const double* xnorm,
+                                  int64_t n, const double* C, const double* cnorm,
+                                  int32_t* assign, double* cost, void* stream);
 int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan plan, const int64_t* rowptr,
                                   const int32_t* colidx, const double* vals, const double* xnorm,
                                   const double* weights, int64_t n, const double* C,

@@ -202,6 +202,53 @@ void orc_find_closest_stats_sparse(const double* C, const double* cnorm, int64_t
   *out_dist = best;
 }
 
+/* DistanceMeasure.scala:318-340 with a SparseVector point: findClosest
+ * without statistics, distances through MLUtils.fastSquaredDistance. */
+void orc_find_closest_sparse(const double* C, const double* cnorm, int64_t k, int64_t d,
+                             const int32_t* idx, const double* val, int64_t nnz, double xnorm,
+                             int32_t* out_idx, double* out_dist) {
+  double best = INFINITY;
+  int64_t bestIndex = 0;
+  for (int64_t i = 0; i < k; ++i) {
+    double lb = cnorm[i] - xnorm;
+    lb = lb * lb;
+    if (lb < best) {
+      double dd = orc_fast_sqdist_dense_sparse(C + i * d, cnorm[i], idx, val, nnz, xnorm, d);
+      if (dd < best) { best = dd; bestIndex = i; }
+    }
+  }
+  *out_idx = (int32_t)bestIndex;
+  *out_dist = best;
+}
+
+/* DistanceMeasure.pointCost (:152-156) for every row of a dense partition
+ * (KMeansModel.computeCost's map, KMeansModel.scala:110-117) plus the
+ * partition's RDD.sum fold (sequential, from 0.0).  Returns the sum. */
+double orc_point_costs(const double* X, const double* xnorm, int64_t n, int64_t d,
+                       const double* C, const double* cnorm, int64_t k, int32_t* assign,
+                       double* cost) {
+  double sum = 0.0;
+  for (int64_t r = 0; r < n; ++r) {
+    orc_find_closest(C, cnorm, k, d, X + r * d, xnorm[r], assign + r, cost + r);
+    sum += cost[r];
+  }
+  return sum;
+}
+
+/* Same for CSR rows. */
+double orc_point_costs_sparse(const int64_t* rowptr, const int32_t* colidx, const double* vals,
+                              const double* xnorm, int64_t n, int64_t d, const double* C,
+                              const double* cnorm, int64_t k, int32_t* assign, double* cost) {
+  double sum = 0.0;
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t q0 = rowptr[r];
+    orc_find_closest_sparse(C, cnorm, k, d, colidx + q0, vals + q0, rowptr[r + 1] - q0, xnorm[r],
+                            assign + r, cost + r);
+    sum += cost[r];
+  }
+  return sum;
+}
+
 /* One Spark partition of the Lloyd iteration body, KMeans.scala:287-306:
  *   (bestCenter, cost) = findClosest(centers, stats, point)
  *   costAccum.add(cost * point.weight)

@@ -50,6 +50,10 @@ def lib():
                 "orc_find_closest_stats": (None, [_D, _D, _i64, _i64, _D, _D, ctypes.c_double,
                                                   _I32, _D]),
                 "orc_find_closest": (None, [_D, _D, _i64, _i64, _D, ctypes.c_double, _I32, _D]),
+                "orc_point_costs": (ctypes.c_double, [_D, _D, _i64, _i64, _D, _D, _i64, _I32,
+                                                      _D]),
+                "orc_point_costs_sparse": (ctypes.c_double, [_I64, _I32, _D, _D, _i64, _i64, _D,
+                                                             _D, _i64, _I32, _D]),
                 "orc_find_closest_stats_sparse": (None, [_D, _D, _i64, _i64, _D, _I32, _D, _i64,
                                                          ctypes.c_double, _I32, _D]),
                 "orc_kmeans_partition": (None, [_D, _D, _D, _i64, _i64, _D, _D, _D, _i64, _I32,
@@ -150,6 +154,34 @@ def find_closest(C, cnorm, x, xnorm):
     lib().orc_find_closest(_p(C), _p(cnorm), C.shape[0], C.shape[1], _p(x), float(xnorm),
                            ctypes.byref(idx), ctypes.byref(dist))
     return idx.value, dist.value
+
+
+def point_costs(X, xnorm, C, cnorm):
+    """DistanceMeasure.pointCost (:152-156) per row (findClosest without
+    statistics, :318-340) and the sequential RDD.sum of one partition
+    (KMeansModel.computeCost, KMeansModel.scala:110-117).
+    Returns (assign, cost, sum)."""
+    X, xnorm, C, cnorm = _f64(X), _f64(xnorm), _f64(C), _f64(cnorm)
+    n, d = X.shape
+    a = np.zeros(n, dtype=np.int32)
+    c = np.zeros(n)
+    s = lib().orc_point_costs(_p(X), _p(xnorm), n, d, _p(C), _p(cnorm), C.shape[0], _p(a, _I32),
+                              _p(c))
+    return a, c, s
+
+
+def point_costs_sparse(csr, xnorm, C, cnorm):
+    """point_costs for CSR rows (csr = (rowptr int64, colidx int32, values))."""
+    rowptr, colidx, vals = csr
+    rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+    colidx = np.ascontiguousarray(colidx, dtype=np.int32)
+    vals, xnorm, C, cnorm = _f64(vals), _f64(xnorm), _f64(C), _f64(cnorm)
+    n = rowptr.size - 1
+    a = np.zeros(n, dtype=np.int32)
+    c = np.zeros(n)
+    s = lib().orc_point_costs_sparse(_p(rowptr, _I64), _p(colidx, _I32), _p(vals), _p(xnorm), n,
+                                     C.shape[1], _p(C), _p(cnorm), C.shape[0], _p(a, _I32), _p(c))
+    return a, c, s
 
 
 def find_closest_stats_sparse(C, cnorm, stats, idx, val, xnorm):

@@ -246,3 +246,42 @@ def test_multinomial_aggregator_vs_naive_loop(fit_intercept, fit_with_mean):
                                                 inv * mean if fit_with_mean else None, st)
             assert abs(st["loss"] / st["weight"] - exp_loss) <= 1e-9 * abs(exp_loss)
             np.testing.assert_allclose(st["grad"] / st["weight"], exp_grad, rtol=1e-9)
+
+
+def test_point_costs_restate_find_closest_without_statistics():
+    """orc_point_costs / orc_point_costs_sparse (pointCost, DistanceMeasure.scala:
+    152-156, 318-340) against a pure-Python restatement of the loop, and the
+    KMeansSuite "two clusters" points (mllib KMeansSuite.scala:255-278)."""
+    import math
+    rng = np.random.default_rng(3)
+    X = rng.normal(size=(60, 5))
+    C = X[:7].copy()
+    C[4] = C[2]
+    xn, cn = oracle.row_norms(X), oracle.row_norms(C)
+    a, c, s = oracle.point_costs(X, xn, C, cn)
+    for r in range(X.shape[0]):
+        best, bi = math.inf, 0
+        for i in range(C.shape[0]):
+            lb = (cn[i] - xn[r]) ** 2
+            if lb < best:
+                dd = 0.0
+                for j in range(X.shape[1]):
+                    t = C[i, j] - X[r, j]
+                    dd += t * t
+                if dd < best:
+                    best, bi = dd, i
+        assert a[r] == bi and c[r] == best
+    tot = 0.0
+    for v in c:
+        tot += v
+    assert s == tot
+    # sparse rows: the same points as CSR agree with the dense loop on indices
+    rowptr = np.arange(0, X.size + 1, X.shape[1], dtype=np.int64)
+    colidx = np.tile(np.arange(X.shape[1], dtype=np.int32), X.shape[0])
+    a2, c2, _ = oracle.point_costs_sparse((rowptr, colidx, X.ravel()), xn, C, cn)
+    assert np.array_equal(a2, a)
+    np.testing.assert_allclose(c2, c, rtol=1e-12, atol=1e-12)
+    P = np.array([[0.0, 0.0], [0.0, 0.1], [0.1, 0.0], [9.0, 0.0], [9.0, 0.2], [9.2, 0.0]])
+    Cp = np.array([[0.1 / 3, 0.1 / 3], [9.2 / 3 + 6.0, 0.2 / 3]])
+    ap, _, _ = oracle.point_costs(P, oracle.row_norms(P), Cp, oracle.row_norms(Cp))
+    assert list(ap) == [0, 0, 0, 1, 1, 1]
