@@ -77,6 +77,17 @@ SIGNATURES = {
                                                          _vp, _vp, _vp, _vp]),
     "cyc_binary_logistic_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
                                                        _vp, _vp, _vp, _vp, _vp, _vp]),
+    "cyc_hinge_plan_create": (ctypes.c_int, [_i32, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "cyc_hinge_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
+                                               _vp, _vp]),
+    "cyc_hinge_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                             _vp, _vp, _vp, _vp]),
+    "cyc_least_squares_plan_create": (ctypes.c_int, [_i32, ctypes.c_int, _f64, _f64,
+                                                     ctypes.POINTER(_vp)]),
+    "cyc_least_squares_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                                       _vp, _vp, _vp, _vp]),
+    "cyc_least_squares_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
+                                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cyc_csc_build_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(_vp)]),
     "cyc_csc_destroy": (ctypes.c_int, [_vp]),
     "cyc_csc_rows": (_i64, [_vp]),

@@ -50,11 +50,38 @@ __device__ __forceinline__ double log1p_exp(double x) {
   return x > 0 ? x + log1p(exp(-x)) : log1p(exp(x));
 }
 
-// Per-row binary epilogue, BinaryLogisticBlockAggregator.scala:104-122.
-// Returns the multiplier; accumulates loss and weight.
-__device__ __forceinline__ double bin_row(double margin, double w, double label, double& loss,
-                                          double& wsum) {
+// Row margin before the epilogue.  kind 0/1: offset + dot (dgemv "T" with
+// beta = 1 on the filled offset); kind 2 (LeastSquaresBlockAggregator.scala:
+// 84-86): arr = offset or 0.0, daxpy(-1/labelStd, labels, arr), then + dot.
+__device__ __forceinline__ double row_margin(int kind, int fitIntercept, double offset,
+                                             double lscale, double label, double dot) {
+  if (kind == 2) return ((fitIntercept ? offset : 0.0) + lscale * label) + dot;
+  return fitIntercept ? offset + dot : dot;
+}
+
+// Per-row epilogue by aggregator kind; returns the multiplier and
+// accumulates loss and weight.
+//   0 BinaryLogisticBlockAggregator.scala:104-122
+//   1 HingeBlockAggregator.scala:103-117 (labels {0,1} scaled to {-1,1};
+//     loss (1 - y' m) w and multiplier -y' w only where the loss is > 0)
+//   2 LeastSquaresBlockAggregator.scala:90-100 (every row: loss w d d / 2,
+//     multiplier w d)
+__device__ __forceinline__ double bin_row(int kind, double margin, double w, double label,
+                                          double& loss, double& wsum) {
   wsum += w;
+  if (kind == 2) {
+    loss += w * margin * margin / 2;
+    return w * margin;
+  }
+  if (w > 0 && kind == 1) {
+    const double ls = label + label - 1.0;
+    const double l = (1.0 - ls * margin) * w;
+    if (l > 0) {
+      loss += l;
+      return -ls * w;
+    }
+    return 0.0;
+  }
   if (w > 0) {
     if (label > 0) loss += w * log1p_exp(-margin);
     else loss += w * (log1p_exp(-margin) + margin);
@@ -67,7 +94,7 @@ template <int FPL>
 __global__ __launch_bounds__(256) void k_binlog_dense(
     const double* __restrict__ X, const double* __restrict__ labels,
     const double* __restrict__ weights, int64_t n, int F, const double* __restrict__ coef,
-    int fitIntercept, double offset, int64_t rowsPerWave, double* __restrict__ slabG,
+    int fitIntercept, int kind, double offset, double lscale, int64_t rowsPerWave, double* __restrict__ slabG,
     double* __restrict__ slabS) {
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -92,9 +119,9 @@ __global__ __launch_bounds__(256) void k_binlog_dense(
       s += x[j] * cf[j];
     }
     const double dot = wave_sum_bcast(s);
-    const double margin = fitIntercept ? offset + dot : dot;
+    const double margin = row_margin(kind, fitIntercept, offset, lscale, labels[r], dot);
     const double w = weights ? weights[r] : 1.0;
-    const double mult = bin_row(margin, w, labels[r], loss, wsum);
+    const double mult = bin_row(kind, margin, w, labels[r], loss, wsum);
     msum += mult;
     if (mult != 0.0) {
 #pragma unroll
@@ -117,7 +144,7 @@ __global__ __launch_bounds__(256) void k_binlog_csr(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const double* __restrict__ vals, const double* __restrict__ labels,
     const double* __restrict__ weights, int64_t n, const double* __restrict__ coef,
-    int fitIntercept, double offset, int64_t rowsPerWave, double* __restrict__ gradAcc,
+    int fitIntercept, int kind, double offset, double lscale, int64_t rowsPerWave, double* __restrict__ gradAcc,
     double* __restrict__ slabS) {
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -137,45 +164,14 @@ __global__ __launch_bounds__(256) void k_binlog_csr(
     double s = (q < p1) ? v0 * coef[c0] : 0.0;
     for (int64_t p = q + 64; p < p1; p += 64) s += vals[p] * coef[colidx[p]];
     const double dot = wave_sum_bcast(s);
-    const double margin = fitIntercept ? offset + dot : dot;
+    const double margin = row_margin(kind, fitIntercept, offset, lscale, labels[r], dot);
     const double w = weights ? weights[r] : 1.0;
-    const double mult = bin_row(margin, w, labels[r], loss, wsum);
+    const double mult = bin_row(kind, margin, w, labels[r], loss, wsum);
     msum += mult;
     if (mult != 0.0) {
       if (q < p1) unsafeAtomicAdd(&gradAcc[c0], v0 * mult);
       for (int64_t p = q + 64; p < p1; p += 64) unsafeAtomicAdd(&gradAcc[colidx[p]], vals[p] * mult);
     }
-  }
-  if (lane == 0) {
-    slabS[gw * 3 + 0] = loss;
-    slabS[gw * 3 + 1] = wsum;
-    slabS[gw * 3 + 2] = msum;
-  }
-}
-
-// Pass 1 of the deterministic sparse path: margins / loss / multiplier per
-// row (no scatter), mult[r] kept for pass 2.
-__global__ __launch_bounds__(256) void k_binlog_csr_mult(
-    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
-    const double* __restrict__ vals, const double* __restrict__ labels,
-    const double* __restrict__ weights, int64_t n, const double* __restrict__ coef,
-    int fitIntercept, double offset, int64_t rowsPerWave, double* __restrict__ mult,
-    double* __restrict__ slabS) {
-  const int lane = threadIdx.x & 63;
-  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int64_t r0 = gw * rowsPerWave;
-  const int64_t r1 = min<int64_t>(n, r0 + rowsPerWave);
-  double loss = 0.0, wsum = 0.0, msum = 0.0;
-  for (int64_t r = r0; r < r1; ++r) {
-    const int64_t p0 = rowptr[r], p1 = rowptr[r + 1];
-    double s = 0.0;
-    for (int64_t p = p0 + lane; p < p1; p += 64) s += vals[p] * coef[colidx[p]];
-    const double dot = wave_sum_bcast(s);
-    const double margin = fitIntercept ? offset + dot : dot;
-    const double w = weights ? weights[r] : 1.0;
-    const double m = bin_row(margin, w, labels[r], loss, wsum);
-    msum += m;
-    if (lane == 0) mult[r] = m;
   }
   if (lane == 0) {
     slabS[gw * 3 + 0] = loss;
@@ -217,7 +213,7 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const double* __restrict__ vals, const double* __restrict__ labels,
     const double* __restrict__ weights, int64_t n, const double* __restrict__ coef,
-    int fitIntercept, double offset, int first, int last, double* __restrict__ dots,
+    int fitIntercept, int kind, double offset, double lscale, int first, int last, double* __restrict__ dots,
     double* __restrict__ slabS) {
   const int lane = threadIdx.x & 63, sub = lane & 7, grp = lane >> 3;
   const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -268,9 +264,9 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
       if (!last) {
         dots[row] = dot;
       } else {
-        const double margin = fitIntercept ? offset + dot : dot;
+        const double margin = row_margin(kind, fitIntercept, offset, lscale, labels[row], dot);
         const double w = weights ? weights[row] : 1.0;
-        const double m = bin_row(margin, w, labels[row], loss, wsum);
+        const double m = bin_row(kind, margin, w, labels[row], loss, wsum);
         msum += m;
         dots[row] = m;
       }
@@ -391,11 +387,23 @@ __global__ void k_binlog_fold(const double* __restrict__ slabG, int64_t waves,
 }
 
 // marginOffset (Binary :67-72): coef[F] - sum_f coef[f]*scaledMean[f]
+// marginOffset: coef[F] - ddot(coef, scaledMean) (Binary :67-72, Hinge
+// :62-71), or for least squares (:57-62) labelMean / labelStd - ddot(...)
+// (base passed in, useBase = 1).
 __global__ void k_binlog_offset(const double* __restrict__ coef, const double* __restrict__ sm,
-                                int F, double* __restrict__ out) {
+                                int F, int useBase, double base, double* __restrict__ out) {
   double dd = 0.0;
   for (int f = 0; f < F; ++f) dd += coef[f] * sm[f];
-  out[0] = coef[F] - dd;
+  out[0] = (useBase ? base : coef[F]) - dd;
+}
+
+// LeastSquaresBlockAggregator.effectiveCoef (:48-55): coefficient or 0.0
+// where the feature's inverseStd is 0.
+__global__ void k_effective_coef(const double* __restrict__ coef,
+                                 const double* __restrict__ inverseStd, int F,
+                                 double* __restrict__ out) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f < F) out[f] = inverseStd[f] != 0 ? coef[f] : 0.0;
 }
 
 // --------------------------------------------------------- multinomial
@@ -890,6 +898,9 @@ __global__ void k_mlr_icpt(int F, int C, const double* __restrict__ ms, double* 
 
 struct cyc_logistic_plan_s {
   int F = 0, C = 1, fitIntercept = 0, fitWithMean = 0;
+  int loss = 0;   // binary plans: 0 logistic, 1 hinge (LinearSVC), 2 least squares
+  double labelStd = 1.0, labelMean = 0.0;   // least squares
+  cyc::DeviceBuffer effCoef;
   std::mutex mu;
   cyc::DeviceBuffer slabG, slabS, slabMS, gradAcc, scal, offset, multBuf, gslab, msTot;
   cyc::DeviceBuffer rowMult;
@@ -909,9 +920,10 @@ int check_common(cyc_logistic_plan p, const double* coef, const double* sm) {
 template <int FPL>
 void launch_bin_dense(dim3 g, hipStream_t st, const double* X, const double* labels,
                       const double* weights, int64_t n, int F, const double* coef, int fi,
-                      double offset, int64_t rpw, double* sg, double* ss) {
+                      int kind, double offset, double lscale, int64_t rpw, double* sg,
+                      double* ss) {
   hipLaunchKernelGGL(k_binlog_dense<FPL>, g, dim3(256), 0, st, X, labels, weights, n, F, coef, fi,
-                     offset, rpw, sg, ss);
+                     kind, offset, lscale, rpw, sg, ss);
 }
 
 }  // namespace
@@ -944,10 +956,31 @@ int cyc_logistic_plan_destroy(cyc_logistic_plan plan) {
   return CYC_OK;
 }
 
-int cyc_binary_logistic_add_dense_dev(cyc_logistic_plan p, const double* X, const double* labels,
-                                      const double* weights, int64_t n, const double* coef,
-                                      const double* scaledMean, double* grad, double* lossSum,
-                                      double* weightSum, void* stream) {
+namespace {
+// The margin offset every row starts from (see k_binlog_offset).  The
+// original coefficients go in (least squares: not the effective ones).
+int binary_offset(cyc_logistic_plan p, const double* coef, const double* scaledMean,
+                  hipStream_t st, double* offset) {
+  *offset = 0.0;
+  if (!p->fitIntercept) return CYC_OK;
+  if (p->fitWithMean || p->loss == 2) {
+    hipLaunchKernelGGL(k_binlog_offset, dim3(1), dim3(1), 0, st, coef, scaledMean, p->F,
+                       p->loss == 2 ? 1 : 0, p->labelMean / p->labelStd, (double*)p->offset.ptr);
+    CYC_LAUNCH_CHECK("k_binlog_offset");
+    CYC_HIP(hipMemcpyAsync(offset, p->offset.ptr, sizeof(double), hipMemcpyDeviceToHost, st));
+  } else {
+    CYC_HIP(hipMemcpyAsync(offset, coef + p->F, sizeof(double), hipMemcpyDeviceToHost, st));
+  }
+  CYC_HIP(hipStreamSynchronize(st));
+  return CYC_OK;
+}
+
+// kcoef: the coefficients the margins use when they differ from coef (least
+// squares' effectiveCoef); coef feeds the offset.
+int binary_add_dense(cyc_logistic_plan p, const double* X, const double* labels,
+                     const double* weights, int64_t n, const double* coef,
+                     const double* scaledMean, double* grad, double* lossSum, double* weightSum,
+                     void* stream, const double* kcoef = nullptr) {
   int rc = check_common(p, coef, scaledMean);
   if (rc) return rc;
   CYC_REQUIRE(n >= 0, "n >= 0");
@@ -969,16 +1002,10 @@ int cyc_binary_logistic_add_dense_dev(cyc_logistic_plan p, const double* X, cons
       (rc = p->scal.reserve(sizeof(double) * 4)) || (rc = p->offset.reserve(sizeof(double) * 2)))
     return rc;
   double offset = 0.0;
-  if (p->fitIntercept) {
-    if (p->fitWithMean) {
-      hipLaunchKernelGGL(k_binlog_offset, dim3(1), dim3(1), 0, st, coef, scaledMean, F,
-                         (double*)p->offset.ptr);
-      CYC_HIP(hipMemcpyAsync(&offset, p->offset.ptr, sizeof(double), hipMemcpyDeviceToHost, st));
-    } else {
-      CYC_HIP(hipMemcpyAsync(&offset, coef + F, sizeof(double), hipMemcpyDeviceToHost, st));
-    }
-    CYC_HIP(hipStreamSynchronize(st));
-  }
+  if ((rc = binary_offset(p, coef, scaledMean, st, &offset))) return rc;
+  const double* kc = kcoef ? kcoef : coef;
+  const double lscale = -1.0 / p->labelStd;
+  const int foldIcpt = p->loss == 2 ? 0 : p->fitIntercept;
   // waves past the last row still write (zero) partials, so the fold reads all
   dim3 grid((unsigned)blocks);
   const int fpl = (F + 63) / 64;
@@ -986,29 +1013,28 @@ int cyc_binary_logistic_add_dense_dev(cyc_logistic_plan p, const double* X, cons
   double* ss = (double*)p->slabS.ptr;
   {
   cyc::KernelTimer timer("k_binlog_dense", st);
-  if (fpl <= 1) launch_bin_dense<1>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
-  else if (fpl <= 2) launch_bin_dense<2>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
-  else if (fpl <= 4) launch_bin_dense<4>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
-  else if (fpl <= 8) launch_bin_dense<8>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
-  else if (fpl <= 16) launch_bin_dense<16>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
-  else launch_bin_dense<32>(grid, st, X, labels, weights, n, F, coef, p->fitIntercept, offset, rpw, sg, ss);
+  if (fpl <= 1) launch_bin_dense<1>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
+  else if (fpl <= 2) launch_bin_dense<2>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
+  else if (fpl <= 4) launch_bin_dense<4>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
+  else if (fpl <= 8) launch_bin_dense<8>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
+  else if (fpl <= 16) launch_bin_dense<16>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
+  else launch_bin_dense<32>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
   CYC_LAUNCH_CHECK("k_binlog_dense");
   }
   hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, ss, wtot, 3, (double*)p->scal.ptr);
   CYC_LAUNCH_CHECK("k_fold_scalars");
   hipLaunchKernelGGL(k_binlog_fold, dim3((F + 255) / 256), dim3(256), 0, st, sg, wtot, nullptr,
-                     F, (const double*)p->scal.ptr, p->fitIntercept, p->fitWithMean, scaledMean,
+                     F, (const double*)p->scal.ptr, foldIcpt, p->fitWithMean, scaledMean,
                      grad, lossSum, weightSum);
   CYC_LAUNCH_CHECK("k_binlog_fold");
   return CYC_OK;
 }
 
-int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
-                                    const int32_t* colidx, const double* vals,
-                                    const double* labels, const double* weights, int64_t n,
-                                    const double* coef, const double* scaledMean, double* grad,
-                                    double* lossSum, double* weightSum, cyc_csc csc,
-                                    void* stream) {
+int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* colidx,
+                   const double* vals, const double* labels, const double* weights, int64_t n,
+                   const double* coef, const double* scaledMean, double* grad, double* lossSum,
+                   double* weightSum, cyc_csc csc, void* stream,
+                   const double* kcoef = nullptr) {
   int rc = check_common(p, coef, scaledMean);
   if (rc) return rc;
   CYC_REQUIRE(n >= 0, "n >= 0");
@@ -1026,16 +1052,10 @@ int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
       (rc = p->scal.reserve(sizeof(double) * 4)) || (rc = p->offset.reserve(sizeof(double) * 2)))
     return rc;
   double offset = 0.0;
-  if (p->fitIntercept) {
-    if (p->fitWithMean) {
-      hipLaunchKernelGGL(k_binlog_offset, dim3(1), dim3(1), 0, st, coef, scaledMean, F,
-                         (double*)p->offset.ptr);
-      CYC_HIP(hipMemcpyAsync(&offset, p->offset.ptr, sizeof(double), hipMemcpyDeviceToHost, st));
-    } else {
-      CYC_HIP(hipMemcpyAsync(&offset, coef + F, sizeof(double), hipMemcpyDeviceToHost, st));
-    }
-    CYC_HIP(hipStreamSynchronize(st));
-  }
+  if ((rc = binary_offset(p, coef, scaledMean, st, &offset))) return rc;
+  const double* kc = kcoef ? kcoef : coef;
+  const double lscale = -1.0 / p->labelStd;
+  const int foldIcpt = p->loss == 2 ? 0 : p->fitIntercept;
   const int64_t* colptr = nullptr;
   const int32_t* rowidx = nullptr;
   const double* cvals = nullptr;
@@ -1057,8 +1077,9 @@ int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
       for (int sl = 0; sl < S; ++sl) {
         const int64_t* rp = S > 1 ? rowptrS + (int64_t)sl * n : rowptr;
         hipLaunchKernelGGL(k_binlog_csr_mult8, dim3((unsigned)blocks), dim3(256), 0, st, rp,
-                           S > 1 ? colS : colidx, S > 1 ? valS : vals, labels, weights, n, coef,
-                           p->fitIntercept, offset, sl == 0 ? 1 : 0, sl == S - 1 ? 1 : 0,
+                           S > 1 ? colS : colidx, S > 1 ? valS : vals, labels, weights, n, kc,
+                           p->fitIntercept, p->loss, offset, lscale, sl == 0 ? 1 : 0,
+                           sl == S - 1 ? 1 : 0,
                            (double*)p->rowMult.ptr, (double*)p->slabS.ptr);
       }
       CYC_LAUNCH_CHECK("k_binlog_csr_mult8");
@@ -1077,7 +1098,8 @@ int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
     CYC_HIP(hipMemsetAsync(p->gradAcc.ptr, 0, sizeof(double) * (size_t)F, st));
     cyc::KernelTimer timer("k_binlog_csr", st);
     hipLaunchKernelGGL(k_binlog_csr, dim3((unsigned)blocks), dim3(256), 0, st, rowptr, colidx,
-                       vals, labels, weights, n, coef, p->fitIntercept, offset, rpw,
+                       vals, labels, weights, n, kc, p->fitIntercept, p->loss, offset, lscale,
+                       rpw,
                        (double*)p->gradAcc.ptr, (double*)p->slabS.ptr);
     CYC_LAUNCH_CHECK("k_binlog_csr");
   }
@@ -1086,9 +1108,115 @@ int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
   CYC_LAUNCH_CHECK("k_fold_scalars");
   hipLaunchKernelGGL(k_binlog_fold, dim3((F + 255) / 256), dim3(256), 0, st, nullptr, 0,
                      (const double*)p->gradAcc.ptr, F, (const double*)p->scal.ptr,
-                     p->fitIntercept, p->fitWithMean, scaledMean, grad, lossSum, weightSum);
+                     foldIcpt, p->fitWithMean, scaledMean, grad, lossSum, weightSum);
   CYC_LAUNCH_CHECK("k_binlog_fold");
   return CYC_OK;
+}
+
+}  // namespace
+
+int cyc_binary_logistic_add_dense_dev(cyc_logistic_plan p, const double* X, const double* labels,
+                                      const double* weights, int64_t n, const double* coef,
+                                      const double* scaledMean, double* grad, double* lossSum,
+                                      double* weightSum, void* stream) {
+  CYC_REQUIRE(p == nullptr || p->loss == 0, "the plan is not a binary logistic plan");
+  return binary_add_dense(p, X, labels, weights, n, coef, scaledMean, grad, lossSum, weightSum,
+                          stream);
+}
+
+int cyc_binary_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
+                                    const int32_t* colidx, const double* vals,
+                                    const double* labels, const double* weights, int64_t n,
+                                    const double* coef, const double* scaledMean, double* grad,
+                                    double* lossSum, double* weightSum, cyc_csc csc,
+                                    void* stream) {
+  CYC_REQUIRE(p == nullptr || p->loss == 0, "the plan is not a binary logistic plan");
+  return binary_add_csr(p, rowptr, colidx, vals, labels, weights, n, coef, scaledMean, grad,
+                        lossSum, weightSum, csc, stream);
+}
+
+int cyc_hinge_plan_create(int32_t numFeatures, int fitIntercept, cyc_logistic_plan* plan) {
+  // HingeBlockAggregator centers whenever it fits an intercept (:62-72, :133-141)
+  int rc = cyc_logistic_plan_create(numFeatures, 1, fitIntercept, fitIntercept, plan);
+  if (rc == CYC_OK) (*plan)->loss = 1;
+  return rc;
+}
+
+int cyc_hinge_add_dense_dev(cyc_logistic_plan p, const double* X, const double* labels,
+                            const double* weights, int64_t n, const double* coef,
+                            const double* scaledMean, double* grad, double* lossSum,
+                            double* weightSum, void* stream) {
+  CYC_REQUIRE(p == nullptr || p->loss == 1, "the plan is not a hinge plan (cyc_hinge_plan_create)");
+  return binary_add_dense(p, X, labels, weights, n, coef, scaledMean, grad, lossSum, weightSum,
+                          stream);
+}
+
+int cyc_hinge_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* colidx,
+                          const double* vals, const double* labels, const double* weights,
+                          int64_t n, const double* coef, const double* scaledMean, double* grad,
+                          double* lossSum, double* weightSum, cyc_csc csc, void* stream) {
+  CYC_REQUIRE(p == nullptr || p->loss == 1, "the plan is not a hinge plan (cyc_hinge_plan_create)");
+  return binary_add_csr(p, rowptr, colidx, vals, labels, weights, n, coef, scaledMean, grad,
+                        lossSum, weightSum, csc, stream);
+}
+
+int cyc_least_squares_plan_create(int32_t numFeatures, int fitIntercept, double labelStd,
+                                  double labelMean, cyc_logistic_plan* plan) {
+  CYC_REQUIRE(labelStd > 0.0, "LeastSquaresBlockAggregator requires the label standard "
+                              "deviation to be positive.");
+  int rc = cyc_logistic_plan_create(numFeatures, 1, fitIntercept, 0, plan);
+  if (rc == CYC_OK) {
+    (*plan)->loss = 2;
+    (*plan)->labelStd = labelStd;
+    (*plan)->labelMean = labelMean;
+  }
+  return rc;
+}
+
+namespace {
+int ls_prepare(cyc_logistic_plan p, const double* coef, const double* inverseStd,
+               const double* scaledMean, hipStream_t st, const double** eff) {
+  CYC_REQUIRE(p != nullptr && p->loss == 2,
+              "the plan is not a least squares plan (cyc_least_squares_plan_create)");
+  CYC_REQUIRE(coef != nullptr && inverseStd != nullptr, "coef and inverseStd must not be null");
+  CYC_REQUIRE(!p->fitIntercept || scaledMean != nullptr,
+              "scaled means is required when fitting an intercept");
+  int rc;
+  if ((rc = p->effCoef.reserve(sizeof(double) * (size_t)p->F))) return rc;
+  hipLaunchKernelGGL(k_effective_coef, dim3((p->F + 255) / 256), dim3(256), 0, st, coef,
+                     inverseStd, p->F, (double*)p->effCoef.ptr);
+  CYC_LAUNCH_CHECK("k_effective_coef");
+  *eff = (const double*)p->effCoef.ptr;
+  return CYC_OK;
+}
+}  // namespace
+
+int cyc_least_squares_add_dense_dev(cyc_logistic_plan p, const double* X, const double* labels,
+                                    const double* weights, int64_t n, const double* coef,
+                                    const double* inverseStd, const double* scaledMean,
+                                    double* grad, double* lossSum, double* weightSum,
+                                    void* stream) {
+  const double* eff = nullptr;
+  hipStream_t st = cyc::as_stream(stream);
+  if (int rc = ls_prepare(p, coef, inverseStd, scaledMean, st, &eff)) return rc;
+  if (n <= 0) return n < 0 ? (cyc::set_error("n >= 0"), CYC_ERR_INVALID_ARG) : CYC_OK;
+  // the offset needs the original coefficients: computed first, from coef
+  return binary_add_dense(p, X, labels, weights, n, coef, scaledMean, grad, lossSum, weightSum,
+                          stream, eff);
+}
+
+int cyc_least_squares_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr,
+                                  const int32_t* colidx, const double* vals, const double* labels,
+                                  const double* weights, int64_t n, const double* coef,
+                                  const double* inverseStd, const double* scaledMean,
+                                  double* grad, double* lossSum, double* weightSum, cyc_csc csc,
+                                  void* stream) {
+  const double* eff = nullptr;
+  hipStream_t st = cyc::as_stream(stream);
+  if (int rc = ls_prepare(p, coef, inverseStd, scaledMean, st, &eff)) return rc;
+  if (n <= 0) return n < 0 ? (cyc::set_error("n >= 0"), CYC_ERR_INVALID_ARG) : CYC_OK;
+  return binary_add_csr(p, rowptr, colidx, vals, labels, weights, n, coef, scaledMean, grad,
+                        lossSum, weightSum, csc, stream, eff);
 }
 
 int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,

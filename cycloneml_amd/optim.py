@@ -98,22 +98,27 @@ class DeviceInstanceBlock:
 _PLANS = {}
 
 
-def _logistic_plan(F, C, fit_intercept, fit_with_mean, device):
+def _logistic_plan(F, C, fit_intercept, fit_with_mean, device, hinge=False):
     """Plans own device scratch; one per shape and device, reused across the
     aggregators RDDLossFunction creates every evaluation."""
-    key = (int(F), int(C), bool(fit_intercept), bool(fit_with_mean), str(device))
+    key = (int(F), int(C), bool(fit_intercept), bool(fit_with_mean), str(device), bool(hinge))
     p = _PLANS.get(key)
     if p is None:
-        p = _PLANS[key] = _LogisticPlan(F, C, fit_intercept, fit_with_mean)
+        p = _PLANS[key] = _LogisticPlan(F, C, fit_intercept, fit_with_mean, hinge)
     return p
 
 
 class _LogisticPlan:
-    def __init__(self, F, C, fit_intercept, fit_with_mean):
+    def __init__(self, F, C, fit_intercept, fit_with_mean, hinge=False):
         self._lib = N.load()
         h = ctypes.c_void_p()
-        N.check(self._lib.cyc_logistic_plan_create(int(F), int(C), int(bool(fit_intercept)),
-                                                   int(bool(fit_with_mean)), ctypes.byref(h)))
+        if hinge:
+            N.check(self._lib.cyc_hinge_plan_create(int(F), int(bool(fit_intercept)),
+                                                    ctypes.byref(h)))
+        else:
+            N.check(self._lib.cyc_logistic_plan_create(int(F), int(C), int(bool(fit_intercept)),
+                                                       int(bool(fit_with_mean)),
+                                                       ctypes.byref(h)))
         self.handle = h
 
     def __del__(self):
@@ -245,6 +250,115 @@ class BinaryLogisticBlockAggregator(DifferentiableLossAggregator):
                 block.size, N.ptr(self.coef), N.ptr(self.scaledMean),
                 N.ptr(self.gradientSumArray), N.ptr(self._loss_sum), N.ptr(self._weight_sum), s))
         return self
+
+
+class HingeBlockAggregator(DifferentiableLossAggregator):
+    """HingeBlockAggregator(bcInverseStd, bcScaledMean, fitIntercept)(bcCoefficients)
+    (ml/optim/aggregator/HingeBlockAggregator.scala:41-141, LinearSVC's loss):
+    the binary block kernels with the hinge epilogue; centers whenever it fits
+    an intercept."""
+
+    def __init__(self, inverseStd, scaledMean, fitIntercept, coefficients, device="cuda"):
+        torch = _torch()
+        inverseStd = np.asarray(inverseStd, dtype=np.float64)
+        if fitIntercept and (scaledMean is None or len(scaledMean) != len(inverseStd)):
+            raise N.IllegalArgumentException(
+                "requirement failed: scaled means is required when center the vectors")
+        if not isinstance(coefficients, (np.ndarray, list, tuple)) and not torch.is_tensor(
+                coefficients):
+            raise N.IllegalArgumentException(
+                f"coefficients only supports dense vector but got type {type(coefficients)}.)")
+        self.numFeatures = len(inverseStd)
+        self.fitIntercept = bool(fitIntercept)
+        self.coef = torch.as_tensor(np.asarray(coefficients, dtype=np.float64), device=device) \
+            if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
+        self.dim = int(self.coef.shape[0])
+        self.scaledMean = None if scaledMean is None else torch.as_tensor(
+            np.asarray(scaledMean, dtype=np.float64), device=device)
+        self._plan = _logistic_plan(self.numFeatures, 1, self.fitIntercept, self.fitIntercept,
+                                    device, hinge=True)
+        self._init_state(device)
+
+    def add(self, block: DeviceInstanceBlock, stream=None):
+        """HingeBlockAggregator.scala:81-141 over every block of the shard."""
+        _check_block(self, block)
+        lib = N.load()
+        s = N.stream_handle(stream)
+        if block.is_sparse:
+            N.check(lib.cyc_hinge_add_csr_dev(
+                self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx), N.ptr(block.values),
+                N.ptr(block.labels), N.ptr(block.weights), block.size, N.ptr(self.coef),
+                N.ptr(self.scaledMean), N.ptr(self.gradientSumArray), N.ptr(self._loss_sum),
+                N.ptr(self._weight_sum), block.csc, s))
+        else:
+            N.check(lib.cyc_hinge_add_dense_dev(
+                self._plan.handle, N.ptr(block.X), N.ptr(block.labels), N.ptr(block.weights),
+                block.size, N.ptr(self.coef), N.ptr(self.scaledMean),
+                N.ptr(self.gradientSumArray), N.ptr(self._loss_sum), N.ptr(self._weight_sum), s))
+        return self
+
+
+class LeastSquaresBlockAggregator(DifferentiableLossAggregator):
+    """LeastSquaresBlockAggregator(bcInverseStd, bcScaledMean, fitIntercept,
+    labelStd, labelMean)(bcCoefficients)
+    (ml/optim/aggregator/LeastSquaresBlockAggregator.scala:31-101): the binary
+    block kernels with the squared-error epilogue; dim = numFeatures."""
+
+    def __init__(self, inverseStd, scaledMean, fitIntercept, labelStd, labelMean, coefficients,
+                 device="cuda"):
+        torch = _torch()
+        if not labelStd > 0.0:
+            raise N.IllegalArgumentException(
+                "requirement failed: LeastSquaresBlockAggregator requires the label standard "
+                "deviation to be positive.")
+        if not isinstance(coefficients, (np.ndarray, list, tuple)) and not torch.is_tensor(
+                coefficients):
+            raise N.IllegalArgumentException(
+                f"coefficients only supports dense vector but got type {type(coefficients)}.)")
+        inv = np.asarray(inverseStd, dtype=np.float64)
+        self.numFeatures = len(inv)
+        self.fitIntercept = bool(fitIntercept)
+        self.inverseStd = torch.as_tensor(inv, device=device)
+        self.coef = torch.as_tensor(np.asarray(coefficients, dtype=np.float64), device=device) \
+            if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
+        self.dim = self.numFeatures
+        self.scaledMean = None if scaledMean is None else torch.as_tensor(
+            np.asarray(scaledMean, dtype=np.float64), device=device)
+        key = ("ls", self.numFeatures, self.fitIntercept, float(labelStd), float(labelMean),
+               str(device))
+        self._plan = _PLANS.get(key)
+        if self._plan is None:
+            self._plan = _PLANS[key] = _LeastSquaresPlan(self.numFeatures, self.fitIntercept,
+                                                         labelStd, labelMean)
+        self._init_state(device)
+
+    def add(self, block: DeviceInstanceBlock, stream=None):
+        """LeastSquaresBlockAggregator.scala:70-101 over every block of the shard."""
+        _check_block(self, block)
+        lib = N.load()
+        s = N.stream_handle(stream)
+        if block.is_sparse:
+            N.check(lib.cyc_least_squares_add_csr_dev(
+                self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx), N.ptr(block.values),
+                N.ptr(block.labels), N.ptr(block.weights), block.size, N.ptr(self.coef),
+                N.ptr(self.inverseStd), N.ptr(self.scaledMean), N.ptr(self.gradientSumArray),
+                N.ptr(self._loss_sum), N.ptr(self._weight_sum), block.csc, s))
+        else:
+            N.check(lib.cyc_least_squares_add_dense_dev(
+                self._plan.handle, N.ptr(block.X), N.ptr(block.labels), N.ptr(block.weights),
+                block.size, N.ptr(self.coef), N.ptr(self.inverseStd), N.ptr(self.scaledMean),
+                N.ptr(self.gradientSumArray), N.ptr(self._loss_sum), N.ptr(self._weight_sum), s))
+        return self
+
+
+class _LeastSquaresPlan(_LogisticPlan):
+    def __init__(self, F, fit_intercept, label_std, label_mean):
+        self._lib = N.load()
+        h = ctypes.c_void_p()
+        N.check(self._lib.cyc_least_squares_plan_create(int(F), int(bool(fit_intercept)),
+                                                        float(label_std), float(label_mean),
+                                                        ctypes.byref(h)))
+        self.handle = h
 
 
 class MultinomialLogisticBlockAggregator(DifferentiableLossAggregator):

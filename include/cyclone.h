@@ -221,6 +221,44 @@ int cyc_csc_slices(cyc_csc csc, int32_t* nslices, int32_t* width, const int64_t*
 int cyc_csc_arrays(cyc_csc csc, const int64_t** colptr, const int32_t** rowidx,
                    const double** values);
 
+/* HingeBlockAggregator (ml/optim/aggregator/HingeBlockAggregator.scala:
+ * 81-141, LinearSVC's loss): the binary kernels with the hinge epilogue
+ * (labels {0,1} -> {-1,1}; loss (1 - y' m) w and multiplier -y' w where the
+ * loss is positive).  The aggregator centers whenever it fits an intercept
+ * (marginOffset, :62-71), so the plan takes fitIntercept only.  Same
+ * arguments, layouts and tolerance as the binary logistic entry points. */
+int cyc_hinge_plan_create(int32_t numFeatures, int fitIntercept, cyc_logistic_plan* plan);
+int cyc_hinge_add_dense_dev(cyc_logistic_plan plan, const double* X, const double* labels,
+                            const double* weights, int64_t n, const double* coef,
+                            const double* scaledMean, double* grad, double* lossSum,
+                            double* weightSum, void* stream);
+int cyc_hinge_add_csr_dev(cyc_logistic_plan plan, const int64_t* rowptr, const int32_t* colidx,
+                          const double* vals, const double* labels, const double* weights,
+                          int64_t n, const double* coef, const double* scaledMean, double* grad,
+                          double* lossSum, double* weightSum, cyc_csc csc, void* stream);
+
+/* LeastSquaresBlockAggregator (ml/optim/aggregator/LeastSquaresBlockAggregator.
+ * scala:31-101, LinearRegression's "l-bfgs" loss): the binary kernels with
+ * margin (offset or 0) - label/labelStd + x.effectiveCoef, loss w d^2/2 and
+ * multiplier w d for every row.  dim = numFeatures (no intercept entry in
+ * coef or grad).  coef: the F original coefficients; inverseStd (device, F)
+ * zeroes the effective coefficients of constant features (:48-55); the
+ * offset labelMean/labelStd - coef.scaledMean (:57-62) uses coef itself.
+ * labelStd must be > 0 (the reference's require message). */
+int cyc_least_squares_plan_create(int32_t numFeatures, int fitIntercept, double labelStd,
+                                  double labelMean, cyc_logistic_plan* plan);
+int cyc_least_squares_add_dense_dev(cyc_logistic_plan plan, const double* X,
+                                    const double* labels, const double* weights, int64_t n,
+                                    const double* coef, const double* inverseStd,
+                                    const double* scaledMean, double* grad, double* lossSum,
+                                    double* weightSum, void* stream);
+int cyc_least_squares_add_csr_dev(cyc_logistic_plan plan, const int64_t* rowptr,
+                                  const int32_t* colidx, const double* vals, const double* labels,
+                                  const double* weights, int64_t n, const double* coef,
+                                  const double* inverseStd, const double* scaledMean,
+                                  double* grad, double* lossSum, double* weightSum, cyc_csc csc,
+                                  void* stream);
+
 int cyc_logistic_plan_create(int32_t numFeatures, int32_t numClasses, int fitIntercept,
                              int fitWithMean, cyc_logistic_plan* plan);
 int cyc_logistic_plan_destroy(cyc_logistic_plan plan);

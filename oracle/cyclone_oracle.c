@@ -442,6 +442,148 @@ void orc_binary_logistic_add(const orc_block* b, const double* coef, int fitInte
   free(arr);
 }
 
+/* HingeBlockAggregator.add, ml/optim/aggregator/HingeBlockAggregator.scala:
+ * 81-141 (LinearSVC).  Centers whenever it fits an intercept: marginOffset
+ * = coef[F] - ddot(coef, scaledMean) (:62-71); per row with weight > 0:
+ * y' = label + label - 1, loss = (1 - y' margin) w, counted with the
+ * multiplier -y' w only when loss > 0 (:103-117).                        */
+void orc_hinge_add(const orc_block* b, const double* coef, int fitIntercept,
+                   const double* scaledMean, double* grad, double* lossSum, double* weightSum) {
+  const int64_t S = b->S, F = b->F;
+  int anyPositive = 0;
+  for (int64_t i = 0; i < S; ++i) if (!b->weights || b->weights[i] != 0) anyPositive = 1;
+  if (!anyPositive) return;                                     /* :88 */
+  double marginOffset = NAN;
+  if (fitIntercept) {
+    double dd = 0.0;                                            /* javaBLAS.ddot */
+    for (int64_t f = 0; f < F; ++f) dd += coef[f] * scaledMean[f];
+    marginOffset = coef[F] - dd;
+  }
+  double* arr = (double*)calloc((size_t)S, sizeof(double));
+  if (fitIntercept) for (int64_t i = 0; i < S; ++i) arr[i] = marginOffset;   /* :93 */
+  for (int64_t i = 0; i < S; ++i) arr[i] = arr[i] + orc_row_dot(b, i, coef);  /* :94 */
+  double localLoss = 0.0, localW = 0.0, multSum = 0.0;
+  for (int64_t i = 0; i < S; ++i) {
+    double w = b->weights ? b->weights[i] : 1.0;
+    localW += w;
+    if (w > 0) {
+      double label = b->labels[i];
+      double labelScaled = label + label - 1.0;
+      double loss = (1.0 - labelScaled * arr[i]) * w;
+      if (loss > 0) {
+        localLoss += loss;
+        double mult = -labelScaled * w;
+        arr[i] = mult;
+        multSum += mult;
+      } else {
+        arr[i] = 0.0;
+      }
+    } else {
+      arr[i] = 0.0;
+    }
+  }
+  *lossSum += localLoss;
+  *weightSum += localW;
+  int allZero = 1;
+  for (int64_t i = 0; i < S; ++i) if (arr[i] != 0) { allZero = 0; break; }
+  if (!allZero) {                                               /* :127 gemv(A^T) */
+    for (int64_t i = 0; i < S; ++i) {
+      double t = arr[i];
+      if (b->rowptr) {
+        double xv = t * 1.0;
+        for (int64_t p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p)
+          grad[b->colidx[p]] += b->values[p] * xv;
+      } else if (t != 0.0) {
+        const double* row = b->values + i * F;
+        for (int64_t f = 0; f < F; ++f) grad[f] = grad[f] + t * row[f];
+      }
+    }
+    if (fitIntercept) {                                         /* :129-137 */
+      double a = -multSum;
+      if (a != 0.0) for (int64_t f = 0; f < F; ++f) grad[f] = grad[f] + a * scaledMean[f];
+      grad[F] += multSum;
+    }
+  }
+  free(arr);
+}
+
+void orc_hinge_add_dense(int64_t S, int64_t F, const double* X, const double* labels,
+                         const double* weights, const double* coef, int fitIntercept,
+                         const double* scaledMean, double* grad, double* lossSum,
+                         double* weightSum) {
+  orc_block b = {S, F, labels, weights, X, NULL, NULL};
+  orc_hinge_add(&b, coef, fitIntercept, scaledMean, grad, lossSum, weightSum);
+}
+
+void orc_hinge_add_csr(int64_t S, int64_t F, const int64_t* rowptr, const int32_t* colidx,
+                       const double* vals, const double* labels, const double* weights,
+                       const double* coef, int fitIntercept, const double* scaledMean,
+                       double* grad, double* lossSum, double* weightSum) {
+  orc_block b = {S, F, labels, weights, vals, rowptr, colidx};
+  orc_hinge_add(&b, coef, fitIntercept, scaledMean, grad, lossSum, weightSum);
+}
+
+/* LeastSquaresBlockAggregator.add, ml/optim/aggregator/
+ * LeastSquaresBlockAggregator.scala:70-101 (dim = F).  effectiveCoef zeroes
+ * the coefficients of features with inverseStd == 0 (:48-55); offset =
+ * labelMean / labelStd - javaBLAS.ddot(coef, scaledMean) (:57-62). */
+void orc_least_squares_add(const orc_block* b, const double* coef, const double* inverseStd,
+                           int fitIntercept, double labelStd, double labelMean,
+                           const double* scaledMean, double* grad, double* lossSum,
+                           double* weightSum) {
+  const int64_t S = b->S, F = b->F;
+  int anyPositive = 0;
+  for (int64_t i = 0; i < S; ++i) if (!b->weights || b->weights[i] != 0) anyPositive = 1;
+  if (!anyPositive) return;                                     /* :77 */
+  double* eff = (double*)malloc((size_t)(F > 0 ? F : 1) * sizeof(double));
+  for (int64_t f = 0; f < F; ++f) eff[f] = inverseStd[f] != 0 ? coef[f] : 0.0;
+  double offset = NAN;
+  if (fitIntercept) {
+    double dd = 0.0;
+    for (int64_t f = 0; f < F; ++f) dd += coef[f] * scaledMean[f];
+    offset = labelMean / labelStd - dd;
+  }
+  double* arr = (double*)calloc((size_t)S, sizeof(double));
+  if (fitIntercept) for (int64_t i = 0; i < S; ++i) arr[i] = offset;     /* :84 */
+  double a = -1.0 / labelStd;                                   /* :85 javaBLAS.daxpy */
+  for (int64_t i = 0; i < S; ++i) arr[i] += a * b->labels[i];
+  for (int64_t i = 0; i < S; ++i) arr[i] = arr[i] + orc_row_dot(b, i, eff);  /* :86 */
+  double localLoss = 0.0, localW = 0.0;
+  for (int64_t i = 0; i < S; ++i) {                             /* :91-99 */
+    double w = b->weights ? b->weights[i] : 1.0;
+    localW += w;
+    double diff = arr[i];
+    localLoss += w * diff * diff / 2;
+    arr[i] = w * diff;
+  }
+  *lossSum += localLoss;
+  *weightSum += localW;
+  for (int64_t i = 0; i < S; ++i) {                             /* :103 gemv(A^T) */
+    double t = arr[i];
+    if (b->rowptr) {
+      double xv = t * 1.0;
+      for (int64_t p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p)
+        grad[b->colidx[p]] += b->values[p] * xv;
+    } else if (t != 0.0) {
+      const double* row = b->values + i * F;
+      for (int64_t f = 0; f < F; ++f) grad[f] = grad[f] + t * row[f];
+    }
+  }
+  free(arr);
+  free(eff);
+}
+
+void orc_least_squares_add_block(int64_t S, int64_t F, const double* X, const int64_t* rowptr,
+                                 const int32_t* colidx, const double* labels,
+                                 const double* weights, const double* coef,
+                                 const double* inverseStd, int fitIntercept, double labelStd,
+                                 double labelMean, const double* scaledMean, double* grad,
+                                 double* lossSum, double* weightSum) {
+  orc_block b = {S, F, labels, weights, X, rowptr, colidx};
+  orc_least_squares_add(&b, coef, inverseStd, fitIntercept, labelStd, labelMean, scaledMean, grad,
+                        lossSum, weightSum);
+}
+
 /* MultinomialLogisticBlockAggregator.add, .scala:101-189 (dense blocks and
  * CSR blocks).  coef: C*F linear part, column-major C x F (coef[f*C + c]),
  * then C intercepts if fitIntercept.  grad has the same layout.            */

@@ -63,6 +63,13 @@ def lib():
                                                              ctypes.c_double]),
                 "orc_log1pexp": (ctypes.c_double, [ctypes.c_double]),
                 "orc_softmax": (None, [_D, _i64, _i64, _i64]),
+                "orc_hinge_add_dense": (None, [_i64, _i64, _D, _D, _D, _D, ctypes.c_int, _D, _D,
+                                               _D, _D]),
+                "orc_hinge_add_csr": (None, [_i64, _i64, _I64, _I32, _D, _D, _D, _D,
+                                             ctypes.c_int, _D, _D, _D, _D]),
+                "orc_least_squares_add_block": (None, [_i64, _i64, _D, _I64, _I32, _D, _D, _D,
+                                                       _D, ctypes.c_int, ctypes.c_double,
+                                                       ctypes.c_double, _D, _D, _D, _D]),
                 "orc_binary_logistic_add_dense": (None, [_i64, _i64, _D, _D, _D, _D, ctypes.c_int,
                                                          ctypes.c_int, _D, _D, _D, _D]),
                 "orc_binary_logistic_add_csr": (None, [_i64, _i64, _I64, _I32, _D, _D, _D, _D,
@@ -333,6 +340,60 @@ def binary_logistic_add(block, coef, fit_intercept, fit_with_mean, scaled_mean, 
                                       _p(labels), _p(weights), _p(coef), int(fit_intercept),
                                       int(fit_with_mean), _p(sm), _p(g), ctypes.byref(loss),
                                       ctypes.byref(wsum))
+    state["loss"], state["weight"] = loss.value, wsum.value
+
+
+def hinge_add(block, coef, fit_intercept, scaled_mean, state):
+    """HingeBlockAggregator.add (ml/optim/aggregator/HingeBlockAggregator.scala:81-141).
+
+    block / state as binary_logistic_add."""
+    L = lib()
+    coef = _f64(coef)
+    sm = None if scaled_mean is None else _f64(scaled_mean)
+    labels = _f64(block["labels"])
+    weights = None if block.get("weights") is None else _f64(block["weights"])
+    loss = ctypes.c_double(state["loss"])
+    wsum = ctypes.c_double(state["weight"])
+    g = state["grad"]
+    if "X" in block:
+        X = _f64(block["X"])
+        L.orc_hinge_add_dense(X.shape[0], X.shape[1], _p(X), _p(labels), _p(weights), _p(coef),
+                              int(fit_intercept), _p(sm), _p(g), ctypes.byref(loss),
+                              ctypes.byref(wsum))
+    else:
+        rp = np.ascontiguousarray(block["rowptr"], dtype=np.int64)
+        ci = np.ascontiguousarray(block["colidx"], dtype=np.int32)
+        v = _f64(block["values"])
+        L.orc_hinge_add_csr(rp.size - 1, block["F"], _p(rp, _I64), _p(ci, _I32), _p(v),
+                            _p(labels), _p(weights), _p(coef), int(fit_intercept), _p(sm), _p(g),
+                            ctypes.byref(loss), ctypes.byref(wsum))
+    state["loss"], state["weight"] = loss.value, wsum.value
+
+
+def least_squares_add(block, coef, inverse_std, fit_intercept, label_std, label_mean,
+                      scaled_mean, state):
+    """LeastSquaresBlockAggregator.add (.scala:70-101); dim = numFeatures.
+    block / state as binary_logistic_add."""
+    L = lib()
+    coef, inv = _f64(coef), _f64(inverse_std)
+    sm = None if scaled_mean is None else _f64(scaled_mean)
+    labels = _f64(block["labels"])
+    weights = None if block.get("weights") is None else _f64(block["weights"])
+    loss = ctypes.c_double(state["loss"])
+    wsum = ctypes.c_double(state["weight"])
+    if "X" in block:
+        X = _f64(block["X"])
+        S, F, rp, ci, v = X.shape[0], X.shape[1], None, None, X
+    else:
+        rp = np.ascontiguousarray(block["rowptr"], dtype=np.int64)
+        ci = np.ascontiguousarray(block["colidx"], dtype=np.int32)
+        v = _f64(block["values"])
+        S, F = rp.size - 1, block["F"]
+    L.orc_least_squares_add_block(S, F, _p(v), None if rp is None else _p(rp, _I64),
+                                  None if ci is None else _p(ci, _I32), _p(labels), _p(weights),
+                                  _p(coef), _p(inv), int(fit_intercept), float(label_std),
+                                  float(label_mean), _p(sm), _p(state["grad"]),
+                                  ctypes.byref(loss), ctypes.byref(wsum))
     state["loss"], state["weight"] = loss.value, wsum.value
 
 

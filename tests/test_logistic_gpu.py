@@ -209,3 +209,87 @@ def test_binary_sliced_csr_vs_oracle(cuda, fi, fwm, n, F, nnz):
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
     assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * abs(st["loss"])
+
+
+@pytest.mark.parametrize("sparse", [False, True, "csc"])
+@pytest.mark.parametrize("fi", [False, True])
+@pytest.mark.parametrize("n,F", [(1, 3), (257, 17), (3000, 64), (2000, 300)])
+def test_hinge_vs_oracle(cuda, sparse, fi, n, F):
+    """HingeBlockAggregator (LinearSVC) on the binary kernels
+    with the hinge epilogue vs the restatement (orc_hinge_add), 1e-10."""
+    from cycloneml_amd.optim import DeviceInstanceBlock, HingeBlockAggregator
+    rng = np.random.default_rng(n * 11 + F + bool(sparse))
+    X, csr, labels, w = _make(n, F, bool(sparse), rng, zero_w=True)
+    coef = rng.normal(size=F + (1 if fi else 0)) * 0.5
+    sm = rng.normal(size=F) * 0.1 if fi else None
+    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+    oracle.hinge_add(_oracle_block(X, csr, labels, w, F), coef, fi, sm, st)
+    blk = DeviceInstanceBlock.from_numpy(labels, w, X=X, csr=csr, numFeatures=F, device=cuda)
+    if sparse == "csc":
+        blk.prepare()
+    agg = HingeBlockAggregator(np.ones(F), sm, fi, coef, device=cuda).add(blk)
+    _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
+    assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
+    assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * max(abs(st["loss"]), 1e-300)
+
+
+def test_hinge_sliced_csr_and_plan_kinds(cuda):
+    """numFeatures > 2^18 (column-sliced margin pass) with the hinge
+    epilogue; a hinge plan refuses the logistic entry point and vice versa."""
+    import ctypes
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.optim import DeviceInstanceBlock, HingeBlockAggregator
+    rng = np.random.default_rng(5)
+    n, F = 500, 600_000
+    X, csr, labels, w = _make(n, F, True, rng, nnz=30, zero_w=True)
+    coef = rng.normal(size=F + 1) * 0.5
+    sm = rng.normal(size=F) * 0.1
+    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+    oracle.hinge_add(_oracle_block(X, csr, labels, w, F), coef, True, sm, st)
+    blk = DeviceInstanceBlock.from_numpy(labels, w, X=None, csr=csr, numFeatures=F, device=cuda)
+    blk.prepare()
+    agg = HingeBlockAggregator(np.ones(F), sm, True, coef, device=cuda).add(blk)
+    _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
+    assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * abs(st["loss"])
+    lib = N.load()
+    h = ctypes.c_void_p()
+    N.check(lib.cyc_hinge_plan_create(4, 0, ctypes.byref(h)))
+    rc = lib.cyc_binary_logistic_add_dense_dev(h, None, None, None, 1, None, None, None, None,
+                                               None, None)
+    assert rc != 0 and b"not a binary logistic plan" in lib.cyc_last_error()
+    lib.cyc_logistic_plan_destroy(h)
+
+
+@pytest.mark.parametrize("sparse", [False, True, "csc"])
+@pytest.mark.parametrize("fi", [False, True])
+@pytest.mark.parametrize("n,F", [(1, 3), (257, 17), (3000, 64), (2000, 300)])
+def test_least_squares_vs_oracle(cuda, sparse, fi, n, F):
+    """LeastSquaresBlockAggregator (LinearRegression) on the binary
+    kernels with the squared-error epilogue vs the restatement, 1e-10; one
+    constant feature (inverseStd 0) exercises effectiveCoef."""
+    from cycloneml_amd.optim import DeviceInstanceBlock, LeastSquaresBlockAggregator
+    rng = np.random.default_rng(n * 13 + F + bool(sparse))
+    X, csr, _, w = _make(n, F, bool(sparse), rng, zero_w=True)
+    labels = rng.normal(size=n) * 2.0 + 0.5
+    coef = rng.normal(size=F) * 0.5
+    inv = rng.uniform(0.5, 2.0, size=F)
+    inv[F // 2] = 0.0
+    sm = rng.normal(size=F) * 0.1 if fi else None
+    ystd, ymean = 1.7, 0.3
+    st = dict(grad=np.zeros(F), loss=0.0, weight=0.0)
+    oracle.least_squares_add(_oracle_block(X, csr, labels, w, F), coef, inv, fi, ystd, ymean, sm,
+                             st)
+    blk = DeviceInstanceBlock.from_numpy(labels, w, X=X, csr=csr, numFeatures=F, device=cuda)
+    if sparse == "csc":
+        blk.prepare()
+    agg = LeastSquaresBlockAggregator(inv, sm, fi, ystd, ymean, coef, device=cuda).add(blk)
+    _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
+    assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
+    assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * abs(st["loss"])
+
+
+def test_least_squares_requires(cuda):
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.optim import LeastSquaresBlockAggregator
+    with pytest.raises(N.IllegalArgumentException, match="label standard"):
+        LeastSquaresBlockAggregator(np.ones(3), None, False, 0.0, 0.0, np.zeros(3), device=cuda)

@@ -285,3 +285,80 @@ def test_point_costs_restate_find_closest_without_statistics():
     Cp = np.array([[0.1 / 3, 0.1 / 3], [9.2 / 3 + 6.0, 0.2 / 3]])
     ap, _, _ = oracle.point_costs(P, oracle.row_norms(P), Cp, oracle.row_norms(Cp))
     assert list(ap) == [0, 0, 0, 1, 1, 1]
+
+
+@pytest.mark.parametrize("fit_intercept", [False, True])
+def test_hinge_aggregator_vs_naive_loop(fit_intercept):
+    """HingeBlockAggregatorSuite.scala:128-219 naive expectations (its three
+    weighted instances, coefficients (1, 2), intercept 1.0; block sizes 1, 2,
+    4; dense and sparse blocks; relTol 1e-9)."""
+    inst = [(0.0, 0.1, np.array([1.0, 2.0])), (1.0, 0.5, np.array([1.5, 1.0])),
+            (0.0, 0.3, np.array([4.0, 0.5]))]
+    mean, std = _summ(inst)
+    inv = np.where(std != 0, 1.0 / std, 0.0)
+    coef = np.array([1.0, 2.0])
+    icpt = 1.0 if fit_intercept else 0.0
+    W = sum(w for _, w, _ in inst)
+    loss, grad, gi = 0.0, np.zeros(2), 0.0
+    for l, w, f in inst:
+        x = f - mean if fit_intercept else f
+        margin = (coef / std) @ x + icpt
+        ls = 2 * l - 1.0
+        if 1.0 > ls * margin:
+            loss += (1.0 - ls * margin) * w
+            grad += x * -ls * w / std
+            gi += -ls * w
+    exp_loss = loss / W
+    exp_grad = np.append(grad, gi) / W if fit_intercept else grad / W
+    scaled = [(l, w, f * inv) for l, w, f in inst]
+    full_coef = np.append(coef, icpt) if fit_intercept else coef
+    for bs in (1, 2, 4):
+        for sparse in (False, True):
+            st = dict(grad=np.zeros(full_coef.size), loss=0.0, weight=0.0)
+            for b in _blocks(scaled, bs, sparse):
+                oracle.hinge_add(b, full_coef, fit_intercept, inv * mean if fit_intercept else None,
+                                 st)
+            assert abs(st["loss"] / st["weight"] - exp_loss) <= 1e-9 * abs(exp_loss)
+            np.testing.assert_allclose(st["grad"] / st["weight"], exp_grad, rtol=1e-9)
+
+
+def test_least_squares_aggregator_vs_naive_loop():
+    """LeastSquaresBlockAggregatorSuite.scala:122-178 "check correctness" (its
+    three weighted instances, coefficients (1, 2), fitIntercept = true; block
+    sizes 1, 2, 4; dense and sparse blocks; relTol 1e-9), plus the constant
+    feature case (:45-49): effectiveCoef zeroes it."""
+    inst = [(0.0, 0.1, np.array([1.0, 2.0])), (1.0, 0.5, np.array([1.5, 1.0])),
+            (0.0, 0.3, np.array([4.0, 0.5]))]
+    mean, std = _summ(inst)
+    ymean, ystd = _summ([(0.0, w, np.array([l])) for l, w, _ in inst])
+    ymean, ystd = float(ymean[0]), float(ystd[0])
+    inv = np.where(std != 0, 1.0 / std, 0.0)
+    coef = np.array([1.0, 2.0])
+    W = sum(w for _, w, _ in inst)
+    errs = [coef @ ((f - mean) / std) - (l - ymean) / ystd for l, _, f in inst]
+    exp_loss = sum(w * e * e / 2.0 for e, (_, w, _) in zip(errs, inst)) / W
+    exp_grad = sum(e * w * f / std for e, (_, w, f) in zip(errs, inst)) / W
+    scaled = [(l, w, f * inv) for l, w, f in inst]
+    for bs in (1, 2, 4):
+        for sparse in (False, True):
+            st = dict(grad=np.zeros(2), loss=0.0, weight=0.0)
+            for b in _blocks(scaled, bs, sparse):
+                oracle.least_squares_add(b, coef, inv, True, ystd, ymean, inv * mean, st)
+            assert abs(st["loss"] / st["weight"] - exp_loss) <= 1e-9 * abs(exp_loss)
+            np.testing.assert_allclose(st["grad"] / st["weight"], exp_grad, rtol=1e-9)
+    # constant feature: the aggregator equals the one over the filtered feature
+    const = [(0.0, 0.1, np.array([1.0, 2.0])), (1.0, 0.5, np.array([1.0, 1.0])),
+             (1.0, 0.3, np.array([1.0, 0.5]))]
+    m2, s2 = _summ(const)
+    inv2 = np.where(s2 != 0, 1.0 / s2, 0.0)
+    ym, ys = _summ([(0.0, w, np.array([l])) for l, w, _ in const])
+    st = dict(grad=np.zeros(2), loss=0.0, weight=0.0)
+    oracle.least_squares_add(_blocks([(l, w, f * inv2) for l, w, f in const], 3, False)[0],
+                             coef, inv2, True, float(ys[0]), float(ym[0]), inv2 * m2, st)
+    stf = dict(grad=np.zeros(1), loss=0.0, weight=0.0)
+    oracle.least_squares_add(_blocks([(l, w, f[1:] * inv2[1:]) for l, w, f in const], 3,
+                                     False)[0], coef[1:], inv2[1:], True, float(ys[0]),
+                             float(ym[0]), (inv2 * m2)[1:], stf)
+    assert st["grad"][0] == 0.0
+    np.testing.assert_allclose(st["grad"][1:], stf["grad"], rtol=1e-12)
+    assert st["loss"] == pytest.approx(stf["loss"], rel=1e-12)
