@@ -66,9 +66,24 @@ __device__ __forceinline__ double row_margin(int kind, int fitIntercept, double 
 //     loss (1 - y' m) w and multiplier -y' w only where the loss is > 0)
 //   2 LeastSquaresBlockAggregator.scala:90-100 (every row: loss w d d / 2,
 //     multiplier w d)
+//   3 HuberBlockAggregator.scala:101-127 (quadratic inside sigma * epsilon,
+//     linear outside; sgs accumulates sigmaGradSum)
 __device__ __forceinline__ double bin_row(int kind, double margin, double w, double label,
-                                          double& loss, double& wsum) {
+                                          double& loss, double& wsum, double& sgs, double sigma,
+                                          double eps) {
   wsum += w;
+  if (w > 0 && kind == 3) {
+    const double ll = label - margin;
+    if (fabs(ll) <= sigma * eps) {
+      loss += 0.5 * w * (sigma + ll * ll / sigma);
+      const double lds = ll / sigma;
+      sgs += 0.5 * w * (1.0 - lds * lds);
+      return -1.0 * w * lds;
+    }
+    loss += 0.5 * w * (sigma + 2.0 * eps * fabs(ll) - sigma * eps * eps);
+    sgs += 0.5 * w * (1.0 - eps * eps);
+    return w * (ll >= 0 ? -1.0 : 1.0) * eps;
+  }
   if (kind == 2) {
     loss += w * margin * margin / 2;
     return w * margin;
@@ -94,7 +109,7 @@ template <int FPL>
 __global__ __launch_bounds__(256) void k_binlog_dense(
     const double* __restrict__ X, const double* __restrict__ labels,
     const double* __restrict__ weights, int64_t n, int F, const double* __restrict__ coef,
-    int fitIntercept, int kind, double offset, double lscale, int64_t rowsPerWave, double* __restrict__ slabG,
+    int fitIntercept, int kind, double offset, double lscale, double sigma, double eps, int64_t rowsPerWave, double* __restrict__ slabG,
     double* __restrict__ slabS) {
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -107,7 +122,7 @@ __global__ __launch_bounds__(256) void k_binlog_dense(
     cf[j] = f < F ? coef[f] : 0.0;
     g[j] = 0.0;
   }
-  double loss = 0.0, wsum = 0.0, msum = 0.0;
+  double loss = 0.0, wsum = 0.0, msum = 0.0, sgs = 0.0;
   for (int64_t r = r0; r < r1; ++r) {
     const double* xr = X + r * F;
     double x[FPL];
@@ -121,7 +136,7 @@ __global__ __launch_bounds__(256) void k_binlog_dense(
     const double dot = wave_sum_bcast(s);
     const double margin = row_margin(kind, fitIntercept, offset, lscale, labels[r], dot);
     const double w = weights ? weights[r] : 1.0;
-    const double mult = bin_row(kind, margin, w, labels[r], loss, wsum);
+    const double mult = bin_row(kind, margin, w, labels[r], loss, wsum, sgs, sigma, eps);
     msum += mult;
     if (mult != 0.0) {
 #pragma unroll
@@ -134,9 +149,10 @@ __global__ __launch_bounds__(256) void k_binlog_dense(
     if (f < F) slabG[gw * F + f] = g[j];
   }
   if (lane == 0) {
-    slabS[gw * 3 + 0] = loss;
-    slabS[gw * 3 + 1] = wsum;
-    slabS[gw * 3 + 2] = msum;
+    slabS[gw * 4 + 0] = loss;
+    slabS[gw * 4 + 1] = wsum;
+    slabS[gw * 4 + 2] = msum;
+    slabS[gw * 4 + 3] = sgs;
   }
 }
 
@@ -144,13 +160,13 @@ __global__ __launch_bounds__(256) void k_binlog_csr(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const double* __restrict__ vals, const double* __restrict__ labels,
     const double* __restrict__ weights, int64_t n, const double* __restrict__ coef,
-    int fitIntercept, int kind, double offset, double lscale, int64_t rowsPerWave, double* __restrict__ gradAcc,
+    int fitIntercept, int kind, double offset, double lscale, double sigma, double eps, int64_t rowsPerWave, double* __restrict__ gradAcc,
     double* __restrict__ slabS) {
   const int lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t r0 = gw * rowsPerWave;
   const int64_t r1 = min<int64_t>(n, r0 + rowsPerWave);
-  double loss = 0.0, wsum = 0.0, msum = 0.0;
+  double loss = 0.0, wsum = 0.0, msum = 0.0, sgs = 0.0;
   for (int64_t r = r0; r < r1; ++r) {
     const int64_t p0 = rowptr[r], p1 = rowptr[r + 1];
     // first 64 nonzeros stay in registers for the scatter
@@ -166,7 +182,7 @@ __global__ __launch_bounds__(256) void k_binlog_csr(
     const double dot = wave_sum_bcast(s);
     const double margin = row_margin(kind, fitIntercept, offset, lscale, labels[r], dot);
     const double w = weights ? weights[r] : 1.0;
-    const double mult = bin_row(kind, margin, w, labels[r], loss, wsum);
+    const double mult = bin_row(kind, margin, w, labels[r], loss, wsum, sgs, sigma, eps);
     msum += mult;
     if (mult != 0.0) {
       if (q < p1) unsafeAtomicAdd(&gradAcc[c0], v0 * mult);
@@ -174,9 +190,10 @@ __global__ __launch_bounds__(256) void k_binlog_csr(
     }
   }
   if (lane == 0) {
-    slabS[gw * 3 + 0] = loss;
-    slabS[gw * 3 + 1] = wsum;
-    slabS[gw * 3 + 2] = msum;
+    slabS[gw * 4 + 0] = loss;
+    slabS[gw * 4 + 1] = wsum;
+    slabS[gw * 4 + 2] = msum;
+    slabS[gw * 4 + 3] = sgs;
   }
 }
 
@@ -213,12 +230,12 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const double* __restrict__ vals, const double* __restrict__ labels,
     const double* __restrict__ weights, int64_t n, const double* __restrict__ coef,
-    int fitIntercept, int kind, double offset, double lscale, int first, int last, double* __restrict__ dots,
+    int fitIntercept, int kind, double offset, double lscale, double sigma, double eps, int first, int last, double* __restrict__ dots,
     double* __restrict__ slabS) {
   const int lane = threadIdx.x & 63, sub = lane & 7, grp = lane >> 3;
   const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
-  double loss = 0.0, wsum = 0.0, msum = 0.0;
+  double loss = 0.0, wsum = 0.0, msum = 0.0, sgs = 0.0;
   for (int64_t g0 = gw * 64; g0 < n; g0 += nw * 64) {
     // row bounds of the 64 rows by one coalesced load, then shuffles
     const int64_t myr = g0 + lane < n ? g0 + lane : n;
@@ -266,7 +283,7 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
       } else {
         const double margin = row_margin(kind, fitIntercept, offset, lscale, labels[row], dot);
         const double w = weights ? weights[row] : 1.0;
-        const double m = bin_row(kind, margin, w, labels[row], loss, wsum);
+        const double m = bin_row(kind, margin, w, labels[row], loss, wsum, sgs, sigma, eps);
         msum += m;
         dots[row] = m;
       }
@@ -278,11 +295,13 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
     loss += __shfl_xor(loss, m);
     wsum += __shfl_xor(wsum, m);
     msum += __shfl_xor(msum, m);
+    sgs += __shfl_xor(sgs, m);
   }
   if (lane == 0) {
-    slabS[gw * 3 + 0] = loss;
-    slabS[gw * 3 + 1] = wsum;
-    slabS[gw * 3 + 2] = msum;
+    slabS[gw * 4 + 0] = loss;
+    slabS[gw * 4 + 1] = wsum;
+    slabS[gw * 4 + 2] = msum;
+    slabS[gw * 4 + 3] = sgs;
   }
 }
 
@@ -364,8 +383,9 @@ __global__ void k_fold_scalars(const double* __restrict__ slabS, int64_t waves, 
 __global__ void k_binlog_fold(const double* __restrict__ slabG, int64_t waves,
                               const double* __restrict__ gradAcc, int F,
                               const double* __restrict__ scal, int fitIntercept, int fitWithMean,
-                              const double* __restrict__ scaledMean, double* __restrict__ grad,
-                              double* __restrict__ lossSum, double* __restrict__ weightSum) {
+                              int sigmaIdx, const double* __restrict__ scaledMean,
+                              double* __restrict__ grad, double* __restrict__ lossSum,
+                              double* __restrict__ weightSum) {
   const int f = blockIdx.x * blockDim.x + threadIdx.x;
   const double msum = scal[2];
   if (f < F) {
@@ -381,6 +401,7 @@ __global__ void k_binlog_fold(const double* __restrict__ slabG, int64_t waves,
   }
   if (f == 0) {
     if (fitIntercept) grad[F] += msum;
+    if (sigmaIdx >= 0) grad[sigmaIdx] += scal[3];   // Huber :138
     *lossSum += scal[0];
     *weightSum += scal[1];
   }
@@ -898,8 +919,9 @@ __global__ void k_mlr_icpt(int F, int C, const double* __restrict__ ms, double* 
 
 struct cyc_logistic_plan_s {
   int F = 0, C = 1, fitIntercept = 0, fitWithMean = 0;
-  int loss = 0;   // binary plans: 0 logistic, 1 hinge (LinearSVC), 2 least squares
+  int loss = 0;   // binary plans: 0 logistic, 1 hinge (LinearSVC), 2 least squares, 3 Huber
   double labelStd = 1.0, labelMean = 0.0;   // least squares
+  double epsilon = 1.35;                     // Huber
   cyc::DeviceBuffer effCoef;
   std::mutex mu;
   cyc::DeviceBuffer slabG, slabS, slabMS, gradAcc, scal, offset, multBuf, gslab, msTot;
@@ -920,10 +942,10 @@ int check_common(cyc_logistic_plan p, const double* coef, const double* sm) {
 template <int FPL>
 void launch_bin_dense(dim3 g, hipStream_t st, const double* X, const double* labels,
                       const double* weights, int64_t n, int F, const double* coef, int fi,
-                      int kind, double offset, double lscale, int64_t rpw, double* sg,
-                      double* ss) {
+                      int kind, double offset, double lscale, double sigma, double eps,
+                      int64_t rpw, double* sg, double* ss) {
   hipLaunchKernelGGL(k_binlog_dense<FPL>, g, dim3(256), 0, st, X, labels, weights, n, F, coef, fi,
-                     kind, offset, lscale, rpw, sg, ss);
+                     kind, offset, lscale, sigma, eps, rpw, sg, ss);
 }
 
 }  // namespace
@@ -998,7 +1020,7 @@ int binary_add_dense(cyc_logistic_plan p, const double* X, const double* labels,
   const int64_t blocks = (nw + 3) / 4;
   const int64_t wtot = blocks * 4;
   if ((rc = p->slabG.reserve(sizeof(double) * (size_t)wtot * F)) ||
-      (rc = p->slabS.reserve(sizeof(double) * (size_t)wtot * 3)) ||
+      (rc = p->slabS.reserve(sizeof(double) * (size_t)wtot * 4)) ||
       (rc = p->scal.reserve(sizeof(double) * 4)) || (rc = p->offset.reserve(sizeof(double) * 2)))
     return rc;
   double offset = 0.0;
@@ -1006,6 +1028,14 @@ int binary_add_dense(cyc_logistic_plan p, const double* X, const double* labels,
   const double* kc = kcoef ? kcoef : coef;
   const double lscale = -1.0 / p->labelStd;
   const int foldIcpt = p->loss == 2 ? 0 : p->fitIntercept;
+  // Huber: sigma = coefficientsArray.last (:97), its gradient entry last
+  double sigma = 0.0;
+  const int sigIdx = p->loss == 3 ? F + (p->fitIntercept ? 1 : 0) : -1;
+  if (p->loss == 3) {
+    CYC_HIP(hipMemcpyAsync(&sigma, coef + sigIdx, sizeof(double), hipMemcpyDeviceToHost, st));
+    CYC_HIP(hipStreamSynchronize(st));
+  }
+  const double eps = p->epsilon;
   // waves past the last row still write (zero) partials, so the fold reads all
   dim3 grid((unsigned)blocks);
   const int fpl = (F + 63) / 64;
@@ -1013,19 +1043,19 @@ int binary_add_dense(cyc_logistic_plan p, const double* X, const double* labels,
   double* ss = (double*)p->slabS.ptr;
   {
   cyc::KernelTimer timer("k_binlog_dense", st);
-  if (fpl <= 1) launch_bin_dense<1>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
-  else if (fpl <= 2) launch_bin_dense<2>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
-  else if (fpl <= 4) launch_bin_dense<4>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
-  else if (fpl <= 8) launch_bin_dense<8>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
-  else if (fpl <= 16) launch_bin_dense<16>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
-  else launch_bin_dense<32>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, rpw, sg, ss);
+  if (fpl <= 1) launch_bin_dense<1>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, sigma, eps, rpw, sg, ss);
+  else if (fpl <= 2) launch_bin_dense<2>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, sigma, eps, rpw, sg, ss);
+  else if (fpl <= 4) launch_bin_dense<4>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, sigma, eps, rpw, sg, ss);
+  else if (fpl <= 8) launch_bin_dense<8>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, sigma, eps, rpw, sg, ss);
+  else if (fpl <= 16) launch_bin_dense<16>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, sigma, eps, rpw, sg, ss);
+  else launch_bin_dense<32>(grid, st, X, labels, weights, n, F, kc, p->fitIntercept, p->loss, offset, lscale, sigma, eps, rpw, sg, ss);
   CYC_LAUNCH_CHECK("k_binlog_dense");
   }
-  hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, ss, wtot, 3, (double*)p->scal.ptr);
+  hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, ss, wtot, 4, (double*)p->scal.ptr);
   CYC_LAUNCH_CHECK("k_fold_scalars");
   hipLaunchKernelGGL(k_binlog_fold, dim3((F + 255) / 256), dim3(256), 0, st, sg, wtot, nullptr,
-                     F, (const double*)p->scal.ptr, foldIcpt, p->fitWithMean, scaledMean,
-                     grad, lossSum, weightSum);
+                     F, (const double*)p->scal.ptr, foldIcpt, p->fitWithMean, sigIdx,
+                     scaledMean, grad, lossSum, weightSum);
   CYC_LAUNCH_CHECK("k_binlog_fold");
   return CYC_OK;
 }
@@ -1048,7 +1078,7 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
   const int64_t blocks = (nw + 3) / 4;
   const int64_t wtot = blocks * 4;
   if ((rc = p->gradAcc.reserve(sizeof(double) * (size_t)F)) ||
-      (rc = p->slabS.reserve(sizeof(double) * (size_t)wtot * 3)) ||
+      (rc = p->slabS.reserve(sizeof(double) * (size_t)wtot * 4)) ||
       (rc = p->scal.reserve(sizeof(double) * 4)) || (rc = p->offset.reserve(sizeof(double) * 2)))
     return rc;
   double offset = 0.0;
@@ -1056,6 +1086,14 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
   const double* kc = kcoef ? kcoef : coef;
   const double lscale = -1.0 / p->labelStd;
   const int foldIcpt = p->loss == 2 ? 0 : p->fitIntercept;
+  // Huber: sigma = coefficientsArray.last (:97), its gradient entry last
+  double sigma = 0.0;
+  const int sigIdx = p->loss == 3 ? F + (p->fitIntercept ? 1 : 0) : -1;
+  if (p->loss == 3) {
+    CYC_HIP(hipMemcpyAsync(&sigma, coef + sigIdx, sizeof(double), hipMemcpyDeviceToHost, st));
+    CYC_HIP(hipStreamSynchronize(st));
+  }
+  const double eps = p->epsilon;
   const int64_t* colptr = nullptr;
   const int32_t* rowidx = nullptr;
   const double* cvals = nullptr;
@@ -1078,7 +1116,7 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
         const int64_t* rp = S > 1 ? rowptrS + (int64_t)sl * n : rowptr;
         hipLaunchKernelGGL(k_binlog_csr_mult8, dim3((unsigned)blocks), dim3(256), 0, st, rp,
                            S > 1 ? colS : colidx, S > 1 ? valS : vals, labels, weights, n, kc,
-                           p->fitIntercept, p->loss, offset, lscale, sl == 0 ? 1 : 0,
+                           p->fitIntercept, p->loss, offset, lscale, sigma, eps, sl == 0 ? 1 : 0,
                            sl == S - 1 ? 1 : 0,
                            (double*)p->rowMult.ptr, (double*)p->slabS.ptr);
       }
@@ -1098,17 +1136,17 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
     CYC_HIP(hipMemsetAsync(p->gradAcc.ptr, 0, sizeof(double) * (size_t)F, st));
     cyc::KernelTimer timer("k_binlog_csr", st);
     hipLaunchKernelGGL(k_binlog_csr, dim3((unsigned)blocks), dim3(256), 0, st, rowptr, colidx,
-                       vals, labels, weights, n, kc, p->fitIntercept, p->loss, offset, lscale,
+                       vals, labels, weights, n, kc, p->fitIntercept, p->loss, offset, lscale, sigma, eps,
                        rpw,
                        (double*)p->gradAcc.ptr, (double*)p->slabS.ptr);
     CYC_LAUNCH_CHECK("k_binlog_csr");
   }
   hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, (const double*)p->slabS.ptr, wtot,
-                     3, (double*)p->scal.ptr);
+                     4, (double*)p->scal.ptr);
   CYC_LAUNCH_CHECK("k_fold_scalars");
   hipLaunchKernelGGL(k_binlog_fold, dim3((F + 255) / 256), dim3(256), 0, st, nullptr, 0,
                      (const double*)p->gradAcc.ptr, F, (const double*)p->scal.ptr,
-                     foldIcpt, p->fitWithMean, scaledMean, grad, lossSum, weightSum);
+                     foldIcpt, p->fitWithMean, sigIdx, scaledMean, grad, lossSum, weightSum);
   CYC_LAUNCH_CHECK("k_binlog_fold");
   return CYC_OK;
 }
@@ -1156,6 +1194,36 @@ int cyc_hinge_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr, const int3
                           int64_t n, const double* coef, const double* scaledMean, double* grad,
                           double* lossSum, double* weightSum, cyc_csc csc, void* stream) {
   CYC_REQUIRE(p == nullptr || p->loss == 1, "the plan is not a hinge plan (cyc_hinge_plan_create)");
+  return binary_add_csr(p, rowptr, colidx, vals, labels, weights, n, coef, scaledMean, grad,
+                        lossSum, weightSum, csc, stream);
+}
+
+int cyc_huber_plan_create(int32_t numFeatures, int fitIntercept, double epsilon,
+                          cyc_logistic_plan* plan) {
+  CYC_REQUIRE(epsilon > 1.0, "epsilon must be > 1.0");
+  // centers whenever it fits an intercept (marginOffset :66-71, daxpy :131-134)
+  int rc = cyc_logistic_plan_create(numFeatures, 1, fitIntercept, fitIntercept, plan);
+  if (rc == CYC_OK) {
+    (*plan)->loss = 3;
+    (*plan)->epsilon = epsilon;
+  }
+  return rc;
+}
+
+int cyc_huber_add_dense_dev(cyc_logistic_plan p, const double* X, const double* labels,
+                            const double* weights, int64_t n, const double* coef,
+                            const double* scaledMean, double* grad, double* lossSum,
+                            double* weightSum, void* stream) {
+  CYC_REQUIRE(p == nullptr || p->loss == 3, "the plan is not a Huber plan (cyc_huber_plan_create)");
+  return binary_add_dense(p, X, labels, weights, n, coef, scaledMean, grad, lossSum, weightSum,
+                          stream);
+}
+
+int cyc_huber_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* colidx,
+                          const double* vals, const double* labels, const double* weights,
+                          int64_t n, const double* coef, const double* scaledMean, double* grad,
+                          double* lossSum, double* weightSum, cyc_csc csc, void* stream) {
+  CYC_REQUIRE(p == nullptr || p->loss == 3, "the plan is not a Huber plan (cyc_huber_plan_create)");
   return binary_add_csr(p, rowptr, colidx, vals, labels, weights, n, coef, scaledMean, grad,
                         lossSum, weightSum, csc, stream);
 }

@@ -351,6 +351,64 @@ class LeastSquaresBlockAggregator(DifferentiableLossAggregator):
         return self
 
 
+class HuberBlockAggregator(DifferentiableLossAggregator):
+    """HuberBlockAggregator(bcInverseStd, bcScaledMean, fitIntercept, epsilon)
+    (bcParameters) (ml/optim/aggregator/HuberBlockAggregator.scala:41-141):
+    the binary block kernels with the Huber epilogue; parameters = linear
+    terms, intercept (if fitIntercept), sigma."""
+
+    def __init__(self, inverseStd, scaledMean, fitIntercept, epsilon, parameters,
+                 device="cuda"):
+        torch = _torch()
+        inv = np.asarray(inverseStd, dtype=np.float64)
+        if fitIntercept and (scaledMean is None or len(scaledMean) != len(inv)):
+            raise N.IllegalArgumentException(
+                "requirement failed: scaled means is required when center the vectors")
+        self.numFeatures = len(inv)
+        self.fitIntercept = bool(fitIntercept)
+        self.coef = torch.as_tensor(np.asarray(parameters, dtype=np.float64), device=device) \
+            if not torch.is_tensor(parameters) else parameters.to(device, torch.float64)
+        self.dim = int(self.coef.shape[0])
+        if self.dim != self.numFeatures + (2 if self.fitIntercept else 1):
+            raise N.IllegalArgumentException(
+                f"requirement failed: parameters size {self.dim} does not match numFeatures "
+                f"{self.numFeatures} (+ intercept) + sigma")
+        self.scaledMean = None if scaledMean is None else torch.as_tensor(
+            np.asarray(scaledMean, dtype=np.float64), device=device)
+        key = ("huber", self.numFeatures, self.fitIntercept, float(epsilon), str(device))
+        self._plan = _PLANS.get(key)
+        if self._plan is None:
+            self._plan = _PLANS[key] = _HuberPlan(self.numFeatures, self.fitIntercept, epsilon)
+        self._init_state(device)
+
+    def add(self, block: DeviceInstanceBlock, stream=None):
+        """HuberBlockAggregator.scala:80-141 over every block of the shard."""
+        _check_block(self, block)
+        lib = N.load()
+        s = N.stream_handle(stream)
+        if block.is_sparse:
+            N.check(lib.cyc_huber_add_csr_dev(
+                self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx), N.ptr(block.values),
+                N.ptr(block.labels), N.ptr(block.weights), block.size, N.ptr(self.coef),
+                N.ptr(self.scaledMean), N.ptr(self.gradientSumArray), N.ptr(self._loss_sum),
+                N.ptr(self._weight_sum), block.csc, s))
+        else:
+            N.check(lib.cyc_huber_add_dense_dev(
+                self._plan.handle, N.ptr(block.X), N.ptr(block.labels), N.ptr(block.weights),
+                block.size, N.ptr(self.coef), N.ptr(self.scaledMean),
+                N.ptr(self.gradientSumArray), N.ptr(self._loss_sum), N.ptr(self._weight_sum), s))
+        return self
+
+
+class _HuberPlan(_LogisticPlan):
+    def __init__(self, F, fit_intercept, epsilon):
+        self._lib = N.load()
+        h = ctypes.c_void_p()
+        N.check(self._lib.cyc_huber_plan_create(int(F), int(bool(fit_intercept)), float(epsilon),
+                                                ctypes.byref(h)))
+        self.handle = h
+
+
 class _LeastSquaresPlan(_LogisticPlan):
     def __init__(self, F, fit_intercept, label_std, label_mean):
         self._lib = N.load()

@@ -237,6 +237,22 @@ int cyc_hinge_add_csr_dev(cyc_logistic_plan plan, const int64_t* rowptr, const i
                           int64_t n, const double* coef, const double* scaledMean, double* grad,
                           double* lossSum, double* weightSum, cyc_csc csc, void* stream);
 
+/* HuberBlockAggregator (ml/optim/aggregator/HuberBlockAggregator.scala:
+ * 41-141, LinearRegression with loss "huber"): the binary kernels with the
+ * Huber epilogue.  coef/grad hold F linear terms, the intercept if
+ * fitIntercept, then sigma (dim - 1); the aggregator centers whenever it fits
+ * an intercept.  epsilon > 1 (LinearRegression's param check). */
+int cyc_huber_plan_create(int32_t numFeatures, int fitIntercept, double epsilon,
+                          cyc_logistic_plan* plan);
+int cyc_huber_add_dense_dev(cyc_logistic_plan plan, const double* X, const double* labels,
+                            const double* weights, int64_t n, const double* coef,
+                            const double* scaledMean, double* grad, double* lossSum,
+                            double* weightSum, void* stream);
+int cyc_huber_add_csr_dev(cyc_logistic_plan plan, const int64_t* rowptr, const int32_t* colidx,
+                          const double* vals, const double* labels, const double* weights,
+                          int64_t n, const double* coef, const double* scaledMean, double* grad,
+                          double* lossSum, double* weightSum, cyc_csc csc, void* stream);
+
 /* LeastSquaresBlockAggregator (ml/optim/aggregator/LeastSquaresBlockAggregator.
  * scala:31-101, LinearRegression's "l-bfgs" loss): the binary kernels with
  * margin (offset or 0) - label/labelStd + x.effectiveCoef, loss w d^2/2 and

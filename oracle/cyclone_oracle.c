@@ -523,6 +523,82 @@ void orc_hinge_add_csr(int64_t S, int64_t F, const int64_t* rowptr, const int32_
   orc_hinge_add(&b, coef, fitIntercept, scaledMean, grad, lossSum, weightSum);
 }
 
+/* HuberBlockAggregator.add, ml/optim/aggregator/HuberBlockAggregator.scala:
+ * 80-141.  coef = F linear terms, intercept (fitIntercept), sigma (last);
+ * dim = F + 1 (+1).  Centers whenever it fits an intercept (:66-71). */
+void orc_huber_add(const orc_block* b, const double* coef, int fitIntercept, double epsilon,
+                   const double* scaledMean, double* grad, double* lossSum, double* weightSum) {
+  const int64_t S = b->S, F = b->F;
+  const int64_t dim = F + (fitIntercept ? 2 : 1);
+  int anyPositive = 0;
+  for (int64_t i = 0; i < S; ++i) if (!b->weights || b->weights[i] != 0) anyPositive = 1;
+  if (!anyPositive) return;                                     /* :87 */
+  double marginOffset = NAN;
+  if (fitIntercept) {
+    double dd = 0.0;
+    for (int64_t f = 0; f < F; ++f) dd += coef[f] * scaledMean[f];
+    marginOffset = coef[dim - 2] - dd;
+  }
+  double* arr = (double*)calloc((size_t)S, sizeof(double));
+  if (fitIntercept) for (int64_t i = 0; i < S; ++i) arr[i] = marginOffset;   /* :92 */
+  for (int64_t i = 0; i < S; ++i) arr[i] = arr[i] + orc_row_dot(b, i, coef);  /* :93 */
+  const double sigma = coef[dim - 1];
+  double sigmaGradSum = 0.0, localLoss = 0.0, localW = 0.0, multSum = 0.0;
+  for (int64_t i = 0; i < S; ++i) {                             /* :103-127 */
+    double w = b->weights ? b->weights[i] : 1.0;
+    localW += w;
+    if (w > 0) {
+      double linearLoss = b->labels[i] - arr[i];
+      if (fabs(linearLoss) <= sigma * epsilon) {
+        localLoss += 0.5 * w * (sigma + pow(linearLoss, 2.0) / sigma);
+        double lds = linearLoss / sigma;
+        double mult = -1.0 * w * lds;
+        arr[i] = mult;
+        multSum += mult;
+        sigmaGradSum += 0.5 * w * (1.0 - pow(lds, 2.0));
+      } else {
+        localLoss += 0.5 * w * (sigma + 2.0 * epsilon * fabs(linearLoss) - sigma * epsilon * epsilon);
+        double sign = linearLoss >= 0 ? -1.0 : 1.0;
+        double mult = w * sign * epsilon;
+        arr[i] = mult;
+        multSum += mult;
+        sigmaGradSum += 0.5 * w * (1.0 - epsilon * epsilon);
+      }
+    } else {
+      arr[i] = 0.0;
+    }
+  }
+  *lossSum += localLoss;
+  *weightSum += localW;
+  for (int64_t i = 0; i < S; ++i) {                             /* :131 gemv(A^T) */
+    double t = arr[i];
+    if (b->rowptr) {
+      double xv = t * 1.0;
+      for (int64_t p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p)
+        grad[b->colidx[p]] += b->values[p] * xv;
+    } else if (t != 0.0) {
+      const double* row = b->values + i * F;
+      for (int64_t f = 0; f < F; ++f) grad[f] = grad[f] + t * row[f];
+    }
+  }
+  if (fitIntercept) {                                           /* :133-140 */
+    double a = -multSum;
+    if (a != 0.0) for (int64_t f = 0; f < F; ++f) grad[f] = grad[f] + a * scaledMean[f];
+    grad[dim - 2] += multSum;
+  }
+  grad[dim - 1] += sigmaGradSum;                                /* :142 */
+  free(arr);
+}
+
+void orc_huber_add_block(int64_t S, int64_t F, const double* X, const int64_t* rowptr,
+                         const int32_t* colidx, const double* labels, const double* weights,
+                         const double* coef, int fitIntercept, double epsilon,
+                         const double* scaledMean, double* grad, double* lossSum,
+                         double* weightSum) {
+  orc_block b = {S, F, labels, weights, X, rowptr, colidx};
+  orc_huber_add(&b, coef, fitIntercept, epsilon, scaledMean, grad, lossSum, weightSum);
+}
+
 /* LeastSquaresBlockAggregator.add, ml/optim/aggregator/
  * LeastSquaresBlockAggregator.scala:70-101 (dim = F).  effectiveCoef zeroes
  * the coefficients of features with inverseStd == 0 (:48-55); offset =

@@ -293,3 +293,27 @@ def test_least_squares_requires(cuda):
     from cycloneml_amd.optim import LeastSquaresBlockAggregator
     with pytest.raises(N.IllegalArgumentException, match="label standard"):
         LeastSquaresBlockAggregator(np.ones(3), None, False, 0.0, 0.0, np.zeros(3), device=cuda)
+
+
+@pytest.mark.parametrize("sparse", [False, True, "csc"])
+@pytest.mark.parametrize("fi", [False, True])
+@pytest.mark.parametrize("n,F", [(1, 3), (257, 17), (3000, 64), (2000, 300)])
+def test_huber_vs_oracle(cuda, sparse, fi, n, F):
+    """HuberBlockAggregator (LinearRegression loss "huber") on the
+    binary kernels with the Huber epilogue vs the restatement, 1e-10; sigma
+    chosen so both the quadratic and the linear branch occur."""
+    from cycloneml_amd.optim import DeviceInstanceBlock, HuberBlockAggregator
+    rng = np.random.default_rng(n * 17 + F + bool(sparse))
+    X, csr, _, w = _make(n, F, bool(sparse), rng, zero_w=True)
+    labels = rng.normal(size=n) * 2.0
+    params = np.concatenate([rng.normal(size=F) * 0.3, [0.4] if fi else [], [0.9]])
+    sm = rng.normal(size=F) * 0.1 if fi else None
+    st = dict(grad=np.zeros(params.size), loss=0.0, weight=0.0)
+    oracle.huber_add(_oracle_block(X, csr, labels, w, F), params, fi, 1.35, sm, st)
+    blk = DeviceInstanceBlock.from_numpy(labels, w, X=X, csr=csr, numFeatures=F, device=cuda)
+    if sparse == "csc":
+        blk.prepare()
+    agg = HuberBlockAggregator(np.ones(F), sm, fi, 1.35, params, device=cuda).add(blk)
+    _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
+    assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
+    assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * abs(st["loss"])

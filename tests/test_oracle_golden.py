@@ -362,3 +362,49 @@ def test_least_squares_aggregator_vs_naive_loop():
     assert st["grad"][0] == 0.0
     np.testing.assert_allclose(st["grad"][1:], stf["grad"], rtol=1e-12)
     assert st["loss"] == pytest.approx(stf["loss"], rel=1e-12)
+
+
+@pytest.mark.parametrize("fit_intercept,sigma", [(False, 4.0), (True, 4.0), (True, 0.3),
+                                                 (False, 0.3)])
+def test_huber_aggregator_vs_naive_loop(fit_intercept, sigma):
+    """HuberBlockAggregatorSuite.scala:132-250 naive expectations (its three
+    instances, coefficients (1, 2), intercept 3.0, sigma 4.0, epsilon 1.35;
+    block sizes 1, 2, 4; dense and sparse blocks; relTol 1e-9); sigma 0.3
+    takes the suite's formulas into the linear branch too."""
+    inst = [(0.0, 0.1, np.array([1.0, 2.0])), (1.0, 0.5, np.array([1.5, 1.0])),
+            (0.0, 0.3, np.array([4.0, 0.5]))]
+    eps = 1.35
+    mean, std = _summ(inst)
+    inv = np.where(std != 0, 1.0 / std, 0.0)
+    coef = np.array([1.0, 2.0])
+    icpt = 3.0 if fit_intercept else 0.0
+    W = sum(w for _, w, _ in inst)
+    loss, gc, gi, gs = 0.0, np.zeros(2), 0.0, 0.0
+    for l, w, f in inst:
+        x = f - mean if fit_intercept else f
+        margin = (coef / std) @ x + icpt
+        ll = l - margin
+        if abs(ll) <= sigma * eps:
+            loss += 0.5 * w * (sigma + ll ** 2 / sigma)
+            gc += -1.0 * w * (ll / sigma) * (x / std)
+            gi += -1.0 * w * (ll / sigma)
+            gs += 0.5 * w * (1.0 - (ll / sigma) ** 2)
+        else:
+            loss += 0.5 * w * (sigma + 2.0 * eps * abs(ll) - sigma * eps * eps)
+            sign = -1.0 if ll >= 0 else 1.0
+            gc += w * sign * eps * (x / std)
+            gi += w * sign * eps
+            gs += 0.5 * w * (1.0 - eps * eps)
+    exp_grad = (np.concatenate([gc, [gi, gs]]) if fit_intercept else np.append(gc, gs)) / W
+    params = np.concatenate([coef, [icpt, sigma]]) if fit_intercept else np.append(coef, sigma)
+    scaled = [(l, w, f * inv) for l, w, f in inst]
+    for bs in (1, 2, 4):
+        for sparse in (False, True):
+            st = dict(grad=np.zeros(params.size), loss=0.0, weight=0.0)
+            for b in _blocks(scaled, bs, sparse):
+                oracle.huber_add(b, params, fit_intercept, eps,
+                                 inv * mean if fit_intercept else None, st)
+            assert abs(st["loss"] / st["weight"] - loss / W) <= 1e-9 * abs(loss / W)
+            # entries that cancel to ~0 in the all-linear case: absolute 1e-12
+            np.testing.assert_allclose(st["grad"] / st["weight"], exp_grad, rtol=1e-9,
+                                       atol=1e-12)
