@@ -737,14 +737,23 @@ __global__ void k_mlr_fold(const double* __restrict__ slab, int splits, int ftil
   if (fitIntercept && e < C) grad[(int64_t)C * F + e] = grad[(int64_t)C * F + e] + 1.0 * ms[e];
 }
 
-// Fold per-wave class sums: out[c] = sum_w slabMS[w][c]; scalars likewise.
-__global__ void k_fold_columns(const double* __restrict__ slab, int64_t rows, int width,
-                               double* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= width) return;
+// Fold per-wave class sums: out[c] = sum_w slabMS[w][c].  One 256-thread
+// workgroup per column: thread t sums rows t, t+256, ... in order, then a
+// fixed LDS tree -- deterministic, and no 2048-long dependent chain.
+__global__ __launch_bounds__(256) void k_fold_columns(const double* __restrict__ slab,
+                                                      int64_t rows, int width,
+                                                      double* __restrict__ out) {
+  __shared__ double sh[256];
+  const int c = blockIdx.x, t = threadIdx.x;
   double s = 0.0;
-  for (int64_t w = 0; w < rows; ++w) s += slab[w * width + c];
-  out[c] = s;
+  for (int64_t w = t; w < rows; w += 256) s += slab[w * width + c];
+  sh[t] = s;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (t < h) sh[t] += sh[t + h];
+    __syncthreads();
+  }
+  if (t == 0) out[c] = sh[0];
 }
 
 __global__ void k_add_scalars(const double* __restrict__ s2, double* __restrict__ lossSum,
@@ -1359,8 +1368,9 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
 #undef CYC_MLR_M
     CYC_LAUNCH_CHECK("k_mlr_margins");
     }
-    // split-K over rows for the gradient GEMM: ~2048 workgroups
-    int64_t splits = std::max<int64_t>(1, 2048 / ftiles);
+    // split-K over rows for the gradient GEMM: ~1024 workgroups (4 rounds of
+    // one per CU; fewer splits keep the k_mlr_fold read of the partials small)
+    int64_t splits = std::max<int64_t>(1, 1024 / ftiles);
     splits = std::min<int64_t>(splits, std::max<int64_t>(1, m / 64));
     const int64_t rps = cyc::round_up((m + splits - 1) / splits, GR);
     splits = (m + rps - 1) / rps;
@@ -1383,7 +1393,7 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
 #undef CYC_MLR_G
     CYC_LAUNCH_CHECK("k_mlr_grad");
     }
-    hipLaunchKernelGGL(k_fold_columns, dim3((CP + 127) / 128), dim3(128), 0, st,
+    hipLaunchKernelGGL(k_fold_columns, dim3(CP), dim3(256), 0, st,
                        (const double*)p->slabMS.ptr, mwaves, CP, (double*)p->msTot.ptr);
     CYC_LAUNCH_CHECK("k_fold_columns");
     hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, (const double*)p->slabS.ptr,
@@ -1461,7 +1471,7 @@ int cyc_multinomial_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* row
     CYC_LAUNCH_CHECK("k_mlr_csr_margins");
   }
 #undef CYC_MLRC_M
-  hipLaunchKernelGGL(k_fold_columns, dim3((C + 127) / 128), dim3(128), 0, st,
+  hipLaunchKernelGGL(k_fold_columns, dim3(C), dim3(256), 0, st,
                      (const double*)p->slabMS.ptr, wtot, C, (double*)p->msTot.ptr);
   CYC_LAUNCH_CHECK("k_fold_columns");
   hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, (const double*)p->slabS.ptr, wtot,
