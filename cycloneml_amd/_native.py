@@ -93,6 +93,14 @@ SIGNATURES = {
                                                        _vp, _vp, _vp, _vp]),
     "cyc_least_squares_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp,
                                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "cyc_libsvm_parse": (ctypes.c_int, [ctypes.c_char_p, _i64, _i32, ctypes.c_int,
+                                        ctypes.POINTER(_vp)]),
+    "cyc_libsvm_load_file": (ctypes.c_int, [ctypes.c_char_p, _i32, ctypes.c_int,
+                                            ctypes.POINTER(_vp)]),
+    "cyc_libsvm_sizes": (ctypes.c_int, [_vp, _pi64, _pi64, ctypes.POINTER(_i32)]),
+    "cyc_libsvm_copy": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "cyc_libsvm_upload": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "cyc_libsvm_destroy": (ctypes.c_int, [_vp]),
     "cyc_csc_build_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, ctypes.POINTER(_vp)]),
     "cyc_csc_destroy": (ctypes.c_int, [_vp]),
     "cyc_csc_rows": (_i64, [_vp]),

@@ -391,6 +391,27 @@ int cyc_logreg_multinomial_eval(cyc_dataset ds, int32_t numClasses, const double
 int cyc_gramian(cyc_dataset ds, const double* mean_opt, double* U);
 int cyc_col_sums(cyc_dataset ds, double* sums);
 
+/* ------------------------------------------------------- LIBSVM input */
+/* MLUtils.loadLibSVMFile's parse (mllib/util/MLUtils.scala:91-151:
+ * parseLibSVMFile, parseLibSVMRecord, computeNumFeatures) on the host, in
+ * parallel over line ranges, straight into CSR arrays for the device
+ * (KMeansExample's and the sparse LR configs' input format).  Rows keep file
+ * order; labels/values are bit-identical to Double.parseDouble; a bad record
+ * returns CYC_ERR_INVALID_ARG with the reference's require text.
+ * numFeatures <= 0: max(last index of each row, 0) + 1.  Host-only. */
+typedef struct cyc_libsvm_s* cyc_libsvm;
+int cyc_libsvm_parse(const char* text, int64_t len, int32_t numFeatures, int nthreads,
+                     cyc_libsvm* out);
+int cyc_libsvm_load_file(const char* path, int32_t numFeatures, int nthreads, cyc_libsvm* out);
+int cyc_libsvm_sizes(cyc_libsvm h, int64_t* n, int64_t* nnz, int32_t* numFeatures);
+/* host copies: labels[n], rowptr[n+1], colidx[nnz], values[nnz] (any may be NULL) */
+int cyc_libsvm_copy(cyc_libsvm h, double* labels, int64_t* rowptr, int32_t* colidx,
+                    double* values);
+/* device copies (same shapes), synchronous on the stream */
+int cyc_libsvm_upload(cyc_libsvm h, double* labels, int64_t* rowptr, int32_t* colidx,
+                      double* values, void* stream);
+int cyc_libsvm_destroy(cyc_libsvm h);
+
 #ifdef __cplusplus
 }
 #endif

@@ -601,3 +601,38 @@ def label_summarize(y, w=None, rows_per_partition=1 << 62, max_classes=1024):
                               _p(inv, _I64), _p(mx, _I64))
     nc = int(mx[0]) + 1
     return hist[:nc].copy(), int(inv[0]), nc
+
+
+def parse_libsvm(text, num_features=-1):
+    """Pure-Python restatement of MLUtils.parseLibSVMFile / parseLibSVMRecord /
+    computeNumFeatures (mllib/util/MLUtils.scala:91-151), small inputs only.
+    Returns (labels, (rowptr, colidx, values), numFeatures); raises
+    ValueError with the reference's require text on a bad record."""
+    labels, rowptr, colidx, values = [], [0], [], []
+    max_index = -1
+    for raw in text.split("\n"):
+        line = raw.strip("".join(chr(c) for c in range(33)))   # String.trim
+        if not line or line.startswith("#"):
+            continue
+        items = line.split(" ")
+        labels.append(float(items[0]))
+        previous = -1
+        for item in items[1:]:
+            if not item:
+                continue
+            iv = item.split(":")
+            current = int(iv[0]) - 1
+            value = float(iv[1])
+            if not current > previous:
+                raise ValueError("requirement failed: indices should be one-based and in "
+                                 f"ascending order; found current={current}, "
+                                 f'previous={previous}; line="{line}"')
+            previous = current
+            colidx.append(current)
+            values.append(value)
+        max_index = max(max_index, previous if previous >= 0 else 0)
+        rowptr.append(len(colidx))
+    nf = num_features if num_features > 0 else (max_index + 1 if labels else 1)
+    return (np.array(labels, dtype=np.float64),
+            (np.array(rowptr, dtype=np.int64), np.array(colidx, dtype=np.int32),
+             np.array(values, dtype=np.float64)), nf)
