@@ -96,6 +96,42 @@ class DeviceInstanceBlock:
 
 
 _PLANS = {}
+_PINNED = {}
+
+
+def _pinned(n):
+    """Page-locked host staging of n doubles, reused per size: the per-
+    evaluation model broadcast (host -> HBM) and gradient collect (HBM ->
+    host) go by DMA instead of through pageable bounce copies."""
+    torch = _torch()
+    t = _PINNED.get(n)
+    if t is None:
+        t = _PINNED[n] = torch.empty(n, dtype=torch.float64, pin_memory=True)
+    return t
+
+
+def _upload(a, device):
+    """Host coefficients -> a fresh device tensor (synchronous copy from the
+    pinned staging buffer, so the buffer is free again on return)."""
+    torch = _torch()
+    a = np.ascontiguousarray(a, dtype=np.float64).ravel()
+    dev = torch.device(device)
+    if dev.type != "cuda" or a.size == 0:
+        return torch.as_tensor(a, device=dev)
+    st = _pinned(a.size)
+    st.numpy()[:] = a
+    out = torch.empty(a.size, dtype=torch.float64, device=dev)
+    out.copy_(st)
+    return out
+
+
+def _download(t):
+    """Device vector -> new host numpy array via the pinned staging buffer."""
+    if t.device.type != "cuda" or t.numel() == 0:
+        return t.cpu().numpy().copy()
+    st = _pinned(t.numel())
+    st.copy_(t)
+    return st.numpy().copy()
 
 
 def _logistic_plan(F, C, fit_intercept, fit_with_mean, device, hinge=False):
@@ -178,7 +214,7 @@ class DifferentiableLossAggregator:
         if not ws > 0.0:
             raise N.IllegalArgumentException(
                 f"The effective number of instances should be greater than 0.0, but was {ws}.")
-        g = self.gradientSumArray.cpu().numpy().copy()
+        g = _download(self.gradientSumArray)
         return (1.0 / ws) * g
 
     @property
@@ -224,7 +260,7 @@ class BinaryLogisticBlockAggregator(DifferentiableLossAggregator):
                 f"coefficients only supports dense vector but got type {type(coefficients)}.)")
         self.numFeatures = len(inverseStd)
         self.fitIntercept, self.fitWithMean = bool(fitIntercept), bool(fitWithMean)
-        self.coef = torch.as_tensor(np.asarray(coefficients, dtype=np.float64), device=device) \
+        self.coef = _upload(coefficients, device) \
             if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
         self.dim = int(self.coef.shape[0])
         self.scaledMean = None if scaledMean is None else torch.as_tensor(
@@ -270,7 +306,7 @@ class HingeBlockAggregator(DifferentiableLossAggregator):
                 f"coefficients only supports dense vector but got type {type(coefficients)}.)")
         self.numFeatures = len(inverseStd)
         self.fitIntercept = bool(fitIntercept)
-        self.coef = torch.as_tensor(np.asarray(coefficients, dtype=np.float64), device=device) \
+        self.coef = _upload(coefficients, device) \
             if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
         self.dim = int(self.coef.shape[0])
         self.scaledMean = None if scaledMean is None else torch.as_tensor(
@@ -319,7 +355,7 @@ class LeastSquaresBlockAggregator(DifferentiableLossAggregator):
         self.numFeatures = len(inv)
         self.fitIntercept = bool(fitIntercept)
         self.inverseStd = torch.as_tensor(inv, device=device)
-        self.coef = torch.as_tensor(np.asarray(coefficients, dtype=np.float64), device=device) \
+        self.coef = _upload(coefficients, device) \
             if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
         self.dim = self.numFeatures
         self.scaledMean = None if scaledMean is None else torch.as_tensor(
@@ -366,7 +402,7 @@ class HuberBlockAggregator(DifferentiableLossAggregator):
                 "requirement failed: scaled means is required when center the vectors")
         self.numFeatures = len(inv)
         self.fitIntercept = bool(fitIntercept)
-        self.coef = torch.as_tensor(np.asarray(parameters, dtype=np.float64), device=device) \
+        self.coef = _upload(parameters, device) \
             if not torch.is_tensor(parameters) else parameters.to(device, torch.float64)
         self.dim = int(self.coef.shape[0])
         if self.dim != self.numFeatures + (2 if self.fitIntercept else 1):
@@ -437,7 +473,7 @@ class MultinomialLogisticBlockAggregator(DifferentiableLossAggregator):
                     "requirement failed: scaled means is required when center the vectors")
         self.numFeatures = len(inverseStd)
         self.fitIntercept, self.fitWithMean = bool(fitIntercept), bool(fitWithMean)
-        self.coef = torch.as_tensor(np.asarray(coefficients, dtype=np.float64), device=device) \
+        self.coef = _upload(coefficients, device) \
             if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
         self.dim = int(self.coef.shape[0])
         fpi = self.numFeatures + 1 if self.fitIntercept else self.numFeatures
