@@ -87,6 +87,11 @@ SIGNATURES = {
                                                _vp, _vp]),
     "cyc_huber_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                              _vp, _vp, _vp, _vp]),
+    "cyc_aft_plan_create": (ctypes.c_int, [_i32, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "cyc_aft_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
+                                             _vp, _vp]),
+    "cyc_aft_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                           _vp, _vp, _vp, _vp]),
     "cyc_least_squares_plan_create": (ctypes.c_int, [_i32, ctypes.c_int, _f64, _f64,
                                                      ctypes.POINTER(_vp)]),
     "cyc_least_squares_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,

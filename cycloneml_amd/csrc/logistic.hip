@@ -68,9 +68,21 @@ __device__ __forceinline__ double row_margin(int kind, int fitIntercept, double 
 //     multiplier w d)
 //   3 HuberBlockAggregator.scala:101-127 (quadratic inside sigma * epsilon,
 //     linear outside; sgs accumulates sigmaGradSum)
+//   4 AFTBlockAggregator.scala:95-108 (log-linear survival; w = censor)
 __device__ __forceinline__ double bin_row(int kind, double margin, double w, double label,
                                           double& loss, double& wsum, double& sgs, double sigma,
                                           double eps) {
+  if (kind == 4) {
+    // AFTBlockAggregator.scala:95-108: w is the censor delta, sigma =
+    // exp(log-sigma), every row counts 1 toward weightSum (:110)
+    const double e = (log(label) - margin) / sigma;
+    const double ee = exp(e);
+    loss += w * log(sigma) - w * e + ee;
+    const double m = (w - ee) / sigma;
+    sgs += w + m * sigma * e;
+    wsum += 1.0;
+    return m;
+  }
   wsum += w;
   if (w > 0 && kind == 3) {
     const double ll = label - margin;
@@ -928,7 +940,8 @@ __global__ void k_mlr_icpt(int F, int C, const double* __restrict__ ms, double* 
 
 struct cyc_logistic_plan_s {
   int F = 0, C = 1, fitIntercept = 0, fitWithMean = 0;
-  int loss = 0;   // binary plans: 0 logistic, 1 hinge (LinearSVC), 2 least squares, 3 Huber
+  int loss = 0;   // binary plans: 0 logistic, 1 hinge (LinearSVC), 2 least squares, 3 Huber,
+                  // 4 AFT survival
   double labelStd = 1.0, labelMean = 0.0;   // least squares
   double epsilon = 1.35;                     // Huber
   cyc::DeviceBuffer effCoef;
@@ -1038,11 +1051,13 @@ int binary_add_dense(cyc_logistic_plan p, const double* X, const double* labels,
   const double lscale = -1.0 / p->labelStd;
   const int foldIcpt = p->loss == 2 ? 0 : p->fitIntercept;
   // Huber: sigma = coefficientsArray.last (:97), its gradient entry last
+  // AFT: sigma = math.exp(coefficientsArray(dim - 1)) (:91), dim = F + 2
   double sigma = 0.0;
-  const int sigIdx = p->loss == 3 ? F + (p->fitIntercept ? 1 : 0) : -1;
-  if (p->loss == 3) {
+  const int sigIdx = p->loss == 3 ? F + (p->fitIntercept ? 1 : 0) : p->loss == 4 ? F + 1 : -1;
+  if (sigIdx >= 0) {
     CYC_HIP(hipMemcpyAsync(&sigma, coef + sigIdx, sizeof(double), hipMemcpyDeviceToHost, st));
     CYC_HIP(hipStreamSynchronize(st));
+    if (p->loss == 4) sigma = std::exp(sigma);
   }
   const double eps = p->epsilon;
   // waves past the last row still write (zero) partials, so the fold reads all
@@ -1096,11 +1111,13 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
   const double lscale = -1.0 / p->labelStd;
   const int foldIcpt = p->loss == 2 ? 0 : p->fitIntercept;
   // Huber: sigma = coefficientsArray.last (:97), its gradient entry last
+  // AFT: sigma = math.exp(coefficientsArray(dim - 1)) (:91), dim = F + 2
   double sigma = 0.0;
-  const int sigIdx = p->loss == 3 ? F + (p->fitIntercept ? 1 : 0) : -1;
-  if (p->loss == 3) {
+  const int sigIdx = p->loss == 3 ? F + (p->fitIntercept ? 1 : 0) : p->loss == 4 ? F + 1 : -1;
+  if (sigIdx >= 0) {
     CYC_HIP(hipMemcpyAsync(&sigma, coef + sigIdx, sizeof(double), hipMemcpyDeviceToHost, st));
     CYC_HIP(hipStreamSynchronize(st));
+    if (p->loss == 4) sigma = std::exp(sigma);
   }
   const double eps = p->epsilon;
   const int64_t* colptr = nullptr;
@@ -1234,6 +1251,31 @@ int cyc_huber_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr, const int3
                           double* lossSum, double* weightSum, cyc_csc csc, void* stream) {
   CYC_REQUIRE(p == nullptr || p->loss == 3, "the plan is not a Huber plan (cyc_huber_plan_create)");
   return binary_add_csr(p, rowptr, colidx, vals, labels, weights, n, coef, scaledMean, grad,
+                        lossSum, weightSum, csc, stream);
+}
+
+int cyc_aft_plan_create(int32_t numFeatures, int fitIntercept, cyc_logistic_plan* plan) {
+  // centers whenever it fits an intercept (marginOffset :52-58, daxpy :118-121)
+  int rc = cyc_logistic_plan_create(numFeatures, 1, fitIntercept, fitIntercept, plan);
+  if (rc == CYC_OK) (*plan)->loss = 4;
+  return rc;
+}
+
+int cyc_aft_add_dense_dev(cyc_logistic_plan p, const double* X, const double* labels,
+                          const double* censors, int64_t n, const double* coef,
+                          const double* scaledMean, double* grad, double* lossSum,
+                          double* weightSum, void* stream) {
+  CYC_REQUIRE(p == nullptr || p->loss == 4, "the plan is not an AFT plan (cyc_aft_plan_create)");
+  return binary_add_dense(p, X, labels, censors, n, coef, scaledMean, grad, lossSum, weightSum,
+                          stream);
+}
+
+int cyc_aft_add_csr_dev(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* colidx,
+                        const double* vals, const double* labels, const double* censors,
+                        int64_t n, const double* coef, const double* scaledMean, double* grad,
+                        double* lossSum, double* weightSum, cyc_csc csc, void* stream) {
+  CYC_REQUIRE(p == nullptr || p->loss == 4, "the plan is not an AFT plan (cyc_aft_plan_create)");
+  return binary_add_csr(p, rowptr, colidx, vals, labels, censors, n, coef, scaledMean, grad,
                         lossSum, weightSum, csc, stream);
 }
 

@@ -445,6 +445,68 @@ class _HuberPlan(_LogisticPlan):
         self.handle = h
 
 
+class AFTBlockAggregator(DifferentiableLossAggregator):
+    """AFTBlockAggregator(bcScaledMean, fitIntercept)(bcCoefficients)
+    (ml/optim/aggregator/AFTBlockAggregator.scala:30-130): the binary block
+    kernels with the AFT survival epilogue.  coefficients = F linear terms,
+    intercept, log(sigma); a block's `weights` carry the censors, as the
+    reference's InstanceBlock does (:97)."""
+
+    def __init__(self, scaledMean, fitIntercept, coefficients, device="cuda"):
+        torch = _torch()
+        if not isinstance(coefficients, (np.ndarray, list, tuple)) and not torch.is_tensor(
+                coefficients):
+            raise N.IllegalArgumentException(
+                f"coefficients only supports dense vector but got type {type(coefficients)}.")
+        self.coef = _upload(coefficients, device) \
+            if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
+        self.dim = int(self.coef.shape[0])
+        self.numFeatures = self.dim - 2
+        self.fitIntercept = bool(fitIntercept)
+        if self.fitIntercept and (scaledMean is None or len(scaledMean) != self.numFeatures):
+            raise N.IllegalArgumentException(
+                "requirement failed: scaled means is required when center the vectors")
+        self.scaledMean = None if scaledMean is None else torch.as_tensor(
+            np.asarray(scaledMean, dtype=np.float64), device=device)
+        key = ("aft", self.numFeatures, self.fitIntercept, str(device))
+        self._plan = _PLANS.get(key)
+        if self._plan is None:
+            self._plan = _PLANS[key] = _AFTPlan(self.numFeatures, self.fitIntercept)
+        self._init_state(device)
+
+    def add(self, block: DeviceInstanceBlock, stream=None):
+        """AFTBlockAggregator.scala:76-130 over every block of the shard."""
+        if self.numFeatures != block.numFeatures:
+            raise N.IllegalArgumentException(
+                "requirement failed: Dimensions mismatch when adding new instance. Expecting "
+                f"{self.numFeatures} but got {block.numFeatures}.")
+        if block.size and bool((block.labels <= 0).any().item()):      # :81
+            raise N.IllegalArgumentException(
+                "requirement failed: The lifetime or label should be greater than 0.")
+        lib = N.load()
+        s = N.stream_handle(stream)
+        if block.is_sparse:
+            N.check(lib.cyc_aft_add_csr_dev(
+                self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx), N.ptr(block.values),
+                N.ptr(block.labels), N.ptr(block.weights), block.size, N.ptr(self.coef),
+                N.ptr(self.scaledMean), N.ptr(self.gradientSumArray), N.ptr(self._loss_sum),
+                N.ptr(self._weight_sum), block.csc, s))
+        else:
+            N.check(lib.cyc_aft_add_dense_dev(
+                self._plan.handle, N.ptr(block.X), N.ptr(block.labels), N.ptr(block.weights),
+                block.size, N.ptr(self.coef), N.ptr(self.scaledMean),
+                N.ptr(self.gradientSumArray), N.ptr(self._loss_sum), N.ptr(self._weight_sum), s))
+        return self
+
+
+class _AFTPlan(_LogisticPlan):
+    def __init__(self, F, fit_intercept):
+        self._lib = N.load()
+        h = ctypes.c_void_p()
+        N.check(self._lib.cyc_aft_plan_create(int(F), int(bool(fit_intercept)), ctypes.byref(h)))
+        self.handle = h
+
+
 class _LeastSquaresPlan(_LogisticPlan):
     def __init__(self, F, fit_intercept, label_std, label_mean):
         self._lib = N.load()

@@ -253,6 +253,23 @@ int cyc_huber_add_csr_dev(cyc_logistic_plan plan, const int64_t* rowptr, const i
                           int64_t n, const double* coef, const double* scaledMean, double* grad,
                           double* lossSum, double* weightSum, cyc_csc csc, void* stream);
 
+/* AFTBlockAggregator (ml/optim/aggregator/AFTBlockAggregator.scala:30-130,
+ * AFTSurvivalRegression): the binary kernels with the log-linear survival
+ * epilogue.  coef/grad: F linear terms, intercept slot, log(sigma) (dim =
+ * F + 2; the intercept gradient stays 0 without fitIntercept).  censors[n]
+ * (the reference keeps them in Instance.weight) may be NULL (all 1);
+ * labels must be > 0 (checked by the caller, as the reference's require);
+ * weightSum counts rows. */
+int cyc_aft_plan_create(int32_t numFeatures, int fitIntercept, cyc_logistic_plan* plan);
+int cyc_aft_add_dense_dev(cyc_logistic_plan plan, const double* X, const double* labels,
+                          const double* censors, int64_t n, const double* coef,
+                          const double* scaledMean, double* grad, double* lossSum,
+                          double* weightSum, void* stream);
+int cyc_aft_add_csr_dev(cyc_logistic_plan plan, const int64_t* rowptr, const int32_t* colidx,
+                        const double* vals, const double* labels, const double* censors,
+                        int64_t n, const double* coef, const double* scaledMean, double* grad,
+                        double* lossSum, double* weightSum, cyc_csc csc, void* stream);
+
 /* LeastSquaresBlockAggregator (ml/optim/aggregator/LeastSquaresBlockAggregator.
  * scala:31-101, LinearRegression's "l-bfgs" loss): the binary kernels with
  * margin (offset or 0) - label/labelStd + x.effectiveCoef, loss w d^2/2 and

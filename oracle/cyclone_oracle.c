@@ -599,6 +599,65 @@ void orc_huber_add_block(int64_t S, int64_t F, const double* X, const int64_t* r
   orc_huber_add(&b, coef, fitIntercept, epsilon, scaledMean, grad, lossSum, weightSum);
 }
 
+/* AFTBlockAggregator.add, ml/optim/aggregator/AFTBlockAggregator.scala:76-130.
+ * coef = F linear, intercept slot, log(sigma) (dim = F + 2); the block's
+ * weights are the censors (NULL: 1.0); weightSum += size. */
+void orc_aft_add(const orc_block* b, const double* coef, int fitIntercept,
+                 const double* scaledMean, double* grad, double* lossSum, double* weightSum) {
+  const int64_t S = b->S, F = b->F, dim = F + 2;
+  double marginOffset = NAN;
+  if (fitIntercept) {                                           /* :52-58 */
+    double dd = 0.0;
+    for (int64_t f = 0; f < F; ++f) dd += coef[f] * scaledMean[f];
+    marginOffset = coef[dim - 2] - dd;
+  }
+  const double sigma = exp(coef[dim - 1]);                      /* :86 */
+  double* arr = (double*)calloc((size_t)(S > 0 ? S : 1), sizeof(double));
+  if (fitIntercept) for (int64_t i = 0; i < S; ++i) arr[i] = marginOffset;
+  for (int64_t i = 0; i < S; ++i) arr[i] = arr[i] + orc_row_dot(b, i, coef);  /* :91 */
+  double localLoss = 0.0, sigmaGradSum = 0.0, multSum = 0.0;
+  for (int64_t i = 0; i < S; ++i) {                             /* :99-110 */
+    double ti = b->labels[i];
+    double delta = b->weights ? b->weights[i] : 1.0;
+    double margin = arr[i];
+    double eps = (log(ti) - margin) / sigma;
+    double expEps = exp(eps);
+    localLoss += delta * log(sigma) - delta * eps + expEps;
+    double mult = (delta - expEps) / sigma;
+    arr[i] = mult;
+    multSum += mult;
+    sigmaGradSum += delta + mult * sigma * eps;
+  }
+  *lossSum += localLoss;
+  *weightSum += (double)S;
+  for (int64_t i = 0; i < S; ++i) {                             /* :116 gemv(A^T) */
+    double t = arr[i];
+    if (b->rowptr) {
+      double xv = t * 1.0;
+      for (int64_t p = b->rowptr[i]; p < b->rowptr[i + 1]; ++p)
+        grad[b->colidx[p]] += b->values[p] * xv;
+    } else if (t != 0.0) {
+      const double* row = b->values + i * F;
+      for (int64_t f = 0; f < F; ++f) grad[f] = grad[f] + t * row[f];
+    }
+  }
+  if (fitIntercept) {                                           /* :118-124 */
+    double a = -multSum;
+    if (a != 0.0) for (int64_t f = 0; f < F; ++f) grad[f] = grad[f] + a * scaledMean[f];
+    grad[dim - 2] += multSum;
+  }
+  grad[dim - 1] += sigmaGradSum;                                /* :126 */
+  free(arr);
+}
+
+void orc_aft_add_block(int64_t S, int64_t F, const double* X, const int64_t* rowptr,
+                       const int32_t* colidx, const double* labels, const double* censors,
+                       const double* coef, int fitIntercept, const double* scaledMean,
+                       double* grad, double* lossSum, double* weightSum) {
+  orc_block b = {S, F, labels, censors, X, rowptr, colidx};
+  orc_aft_add(&b, coef, fitIntercept, scaledMean, grad, lossSum, weightSum);
+}
+
 /* LeastSquaresBlockAggregator.add, ml/optim/aggregator/
  * LeastSquaresBlockAggregator.scala:70-101 (dim = F).  effectiveCoef zeroes
  * the coefficients of features with inverseStd == 0 (:48-55); offset =

@@ -69,6 +69,8 @@ def lib():
                                              ctypes.c_int, _D, _D, _D, _D]),
                 "orc_huber_add_block": (None, [_i64, _i64, _D, _I64, _I32, _D, _D, _D,
                                                ctypes.c_int, ctypes.c_double, _D, _D, _D, _D]),
+                "orc_aft_add_block": (None, [_i64, _i64, _D, _I64, _I32, _D, _D, _D, ctypes.c_int,
+                                             _D, _D, _D, _D]),
                 "orc_least_squares_add_block": (None, [_i64, _i64, _D, _I64, _I32, _D, _D, _D,
                                                        _D, ctypes.c_int, ctypes.c_double,
                                                        ctypes.c_double, _D, _D, _D, _D]),
@@ -393,6 +395,30 @@ def huber_add(block, params, fit_intercept, epsilon, scaled_mean, state):
                           None if ci is None else _p(ci, _I32), _p(labels), _p(weights),
                           _p(params), int(fit_intercept), float(epsilon), _p(sm),
                           _p(state["grad"]), ctypes.byref(loss), ctypes.byref(wsum))
+    state["loss"], state["weight"] = loss.value, wsum.value
+
+
+def aft_add(block, coef, fit_intercept, scaled_mean, state):
+    """AFTBlockAggregator.add (.scala:76-130); block["weights"] = censors."""
+    L = lib()
+    coef = _f64(coef)
+    sm = None if scaled_mean is None else _f64(scaled_mean)
+    labels = _f64(block["labels"])
+    cens = None if block.get("weights") is None else _f64(block["weights"])
+    loss = ctypes.c_double(state["loss"])
+    wsum = ctypes.c_double(state["weight"])
+    if "X" in block:
+        X = _f64(block["X"])
+        S, F, rp, ci, v = X.shape[0], X.shape[1], None, None, X
+    else:
+        rp = np.ascontiguousarray(block["rowptr"], dtype=np.int64)
+        ci = np.ascontiguousarray(block["colidx"], dtype=np.int32)
+        v = _f64(block["values"])
+        S, F = rp.size - 1, block["F"]
+    L.orc_aft_add_block(S, F, _p(v), None if rp is None else _p(rp, _I64),
+                        None if ci is None else _p(ci, _I32), _p(labels), _p(cens), _p(coef),
+                        int(fit_intercept), _p(sm), _p(state["grad"]), ctypes.byref(loss),
+                        ctypes.byref(wsum))
     state["loss"], state["weight"] = loss.value, wsum.value
 
 

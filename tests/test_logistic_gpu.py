@@ -317,3 +317,37 @@ def test_huber_vs_oracle(cuda, sparse, fi, n, F):
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
     assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * abs(st["loss"])
+
+
+@pytest.mark.parametrize("sparse", [False, True, "csc"])
+@pytest.mark.parametrize("fi", [False, True])
+@pytest.mark.parametrize("n,F", [(1, 3), (257, 17), (3000, 64), (2000, 300)])
+def test_aft_vs_oracle(cuda, sparse, fi, n, F):
+    """AFTBlockAggregator (AFTSurvivalRegression) on the binary
+    kernels with the survival epilogue vs the restatement, 1e-10; censors in
+    the weights slot, as the reference keeps them."""
+    from cycloneml_amd.optim import AFTBlockAggregator, DeviceInstanceBlock
+    rng = np.random.default_rng(n * 19 + F + bool(sparse))
+    X, csr, _, _ = _make(n, F, bool(sparse), rng)
+    labels = rng.exponential(2.0, size=n) + 1e-3
+    cens = (rng.uniform(size=n) < 0.6).astype(np.float64)
+    coef = np.concatenate([rng.normal(size=F) * 0.1, [0.3 if fi else 0.0], [0.2]])
+    sm = rng.normal(size=F) * 0.1 if fi else None
+    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+    oracle.aft_add(_oracle_block(X, csr, labels, cens, F), coef, fi, sm, st)
+    blk = DeviceInstanceBlock.from_numpy(labels, cens, X=X, csr=csr, numFeatures=F, device=cuda)
+    if sparse == "csc":
+        blk.prepare()
+    agg = AFTBlockAggregator(sm, fi, coef, device=cuda).add(blk)
+    _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
+    assert agg.weight == st["weight"] == n
+    assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * abs(st["loss"])
+
+
+def test_aft_requires_positive_labels(cuda):
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.optim import AFTBlockAggregator, DeviceInstanceBlock
+    blk = DeviceInstanceBlock.from_numpy(np.array([1.0, 0.0]), None, X=np.ones((2, 2)),
+                                         device=cuda)
+    with pytest.raises(N.IllegalArgumentException, match="greater than 0"):
+        AFTBlockAggregator(None, False, np.zeros(4), device=cuda).add(blk)
