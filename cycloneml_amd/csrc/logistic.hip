@@ -647,7 +647,7 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
   }
 }
 
-constexpr int GR = 16;    // rows per LDS chunk in the gradient GEMM
+constexpr int GR = 32;    // rows per LDS chunk in the gradient GEMM
 constexpr int GF = 256;   // features per workgroup
 constexpr int GFS = GF + 16;
 
@@ -667,23 +667,34 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
   cyc_double4 acc[CT][2];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) acc[ct][0] = acc[ct][1] = cyc_double4{0.0, 0.0, 0.0, 0.0};
-  // Register prefetch of the next 16-row chunk while this one is multiplied.
+  // Register prefetch of the next GR-row chunk while this one is multiplied.
+  // Loads go through buffer descriptors over this split's rows: 32-bit
+  // offsets, rows past the split and features past F read as zero
+  // (out-of-range offsets).  Host: rowsPerSplit * max(F, CP) * 8 < 2^31.
   constexpr int MPT = (GR * CP + 511) / 512;   // mult doubles per thread
-  constexpr int XPT = GR * GF / 512;           // X doubles per thread (8)
+  constexpr int XPT = GR * GF / 512;           // X doubles per thread
+  constexpr int OOB = 0x7ff00000;
   double mreg[MPT], xreg[XPT];
+  const int64_t nr = r1 > r0 ? r1 - r0 : 0;
+  const auto mR = __builtin_amdgcn_make_buffer_rsrc((void*)(mult + r0 * CP), (short)0,
+                                                    (int)(nr * CP * 8), 0x00020000);
+  const auto xR = __builtin_amdgcn_make_buffer_rsrc((void*)(X + r0 * F), (short)0,
+                                                    (int)(nr * F * 8), 0x00020000);
+  const bool fok = F0 + (tid & (GF - 1)) < F;
   auto load_regs = [&](int64_t rb) {
+    const int rowOff = (int)(rb - r0);
 #pragma unroll
     for (int i = 0; i < MPT; ++i) {
       const int e = tid + 512 * i;
-      const int rr = e / CP, c = e - rr * CP;
-      mreg[i] = (e < GR * CP && rb + rr < r1) ? mult[(rb + rr) * CP + c] : 0.0;
+      const int off = e < GR * CP ? (rowOff * CP + e) * 8 : OOB;
+      mreg[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(mR, off, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int e = tid + 512 * i;
-      const int rr = e >> 8, ff = e & (GF - 1);
-      const int f = F0 + ff;
-      xreg[i] = (rb + rr < r1 && f < F) ? X[(rb + rr) * F + f] : 0.0;
+      const int rr = e / GF, ff = e & (GF - 1);
+      const int off = fok ? ((rowOff + rr) * F + F0 + ff) * 8 : OOB;
+      xreg[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xR, off, 0, 0));
     }
   };
   if (r0 < r1) load_regs(r0);
@@ -698,7 +709,7 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
 #pragma unroll
     for (int i = 0; i < XPT; ++i) {
       const int e = tid + 512 * i;
-      Xs[(e >> 8) * GFS + (e & (GF - 1))] = xreg[i];
+      Xs[(e / GF) * GFS + (e & (GF - 1))] = xreg[i];
     }
     __syncthreads();
     if (rb + GR < r1) load_regs(rb + GR);
@@ -1414,7 +1425,10 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
     // one per CU; fewer splits keep the k_mlr_fold read of the partials small)
     int64_t splits = std::max<int64_t>(1, 1024 / ftiles);
     splits = std::min<int64_t>(splits, std::max<int64_t>(1, m / 64));
-    const int64_t rps = cyc::round_up((m + splits - 1) / splits, GR);
+    int64_t rps = cyc::round_up((m + splits - 1) / splits, GR);
+    // k_mlr_grad's buffer descriptors span one split: keep it under 2^31 bytes
+    const int64_t maxRps = ((int64_t)INT32_MAX / 8 / std::max(F, CP)) / GR * GR - GR;
+    if (rps > maxRps) rps = std::max<int64_t>(GR, maxRps);
     splits = (m + rps - 1) / rps;
     if ((rc = p->gslab.reserve(sizeof(double) * (size_t)splits * ftiles * CP * GF))) return rc;
 #define CYC_MLR_G(CTV)                                                                         \
