@@ -313,6 +313,25 @@ class KMeans:
         self.distanceMeasure = dm
         return self
 
+    @staticmethod
+    def updateParallelCosts(X, newCenters, costs=None, xnorm=None, stream=None):
+        """One k-means|| cost update on the device (KMeans.scala:392-396):
+        costs = min(pointCost(newCenters, x), cost) per row, pointCost being
+        findClosest without statistics (bit-exact per row).  costs=None starts
+        from +Infinity (:375).  Returns (costs, sum of costs); the sum is the
+        `costs.sum()` that scales the sampling probabilities (:398), one
+        all-reduce across ranks.  The sampling (XORShiftRandom per partition)
+        and LocalKMeans stay on the host, as in the reference driver."""
+        torch = _torch()
+        m = KMeansModel(np.asarray(newCenters, dtype=np.float64))
+        _, c = m.pointCosts(X, xnorm, stream)
+        if costs is not None:
+            c = torch.minimum(c, costs)   # math.min: NaN propagates either way
+        tot = c.sum().reshape(1) if c.numel() else torch.zeros(1, dtype=torch.float64,
+                                                               device=c.device)
+        parallel.allreduce_(tot)
+        return c, float(tot.item())
+
     def run(self, X, weights=None, xnorm=None, stream=None, iteration_callback=None):
         """Lloyd's algorithm, KMeans.scala:240-349, on a device-resident shard.
 

@@ -52,6 +52,7 @@ constexpr int64_t kCscRowBlock = 1 << 18;
 // column-slice width of the sliced CSR copy (fp64 coefficients per slice)
 constexpr int kSliceCols = 1 << 18;
 int build_csc(const int64_t* rowptr, const int32_t* colidx, const double* vals, int64_t n, int F,
+              int64_t rowBlock,
               DeviceBuffer& colptr, DeviceBuffer& rowidx, DeviceBuffer& cvals, hipStream_t st);
 
 // Fixed-margin round-up.

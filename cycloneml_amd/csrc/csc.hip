@@ -26,6 +26,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -46,10 +48,11 @@ __global__ void k_row_of(const int64_t* __restrict__ rowptr, int64_t n,
 
 // sort key of nonzero p: (row block, column)
 __global__ void k_csc_keys(const int32_t* __restrict__ rowOf, const int32_t* __restrict__ colidx,
-                           int64_t nnz, int F, int64_t* __restrict__ keys) {
+                           int64_t nnz, int F, int64_t rowBlock,
+                           int64_t* __restrict__ keys) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < nnz;
        p += (int64_t)gridDim.x * blockDim.x)
-    keys[p] = (int64_t)(rowOf[p] / cyc::kCscRowBlock) * F + colidx[p];
+    keys[p] = (int64_t)(rowOf[p] / rowBlock) * F + colidx[p];
 }
 
 __global__ void k_gather_csc(const int64_t* __restrict__ perm, int64_t nnz,
@@ -133,11 +136,11 @@ __global__ void k_slice_scatter(const int64_t* __restrict__ rowptr,
 namespace cyc {
 
 int build_csc(const int64_t* rowptr, const int32_t* colidx, const double* vals, int64_t n, int F,
-              DeviceBuffer& colptr, DeviceBuffer& rowidx, DeviceBuffer& cvals, hipStream_t st) {
+              int64_t rowBlock, DeviceBuffer& colptr, DeviceBuffer& rowidx, DeviceBuffer& cvals, hipStream_t st) {
   int64_t nnz = 0;
   CYC_HIP(hipMemcpyAsync(&nnz, rowptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
   CYC_HIP(hipStreamSynchronize(st));
-  const int64_t nb = std::max<int64_t>((n + kCscRowBlock - 1) / kCscRowBlock, 1);
+  const int64_t nb = std::max<int64_t>((n + rowBlock - 1) / rowBlock, 1);
   const int64_t nkeys = nb * F;
   int rc;
   if ((rc = colptr.reserve(sizeof(int64_t) * ((size_t)nkeys + 1))) ||
@@ -155,7 +158,7 @@ int build_csc(const int64_t* rowptr, const int32_t* colidx, const double* vals, 
   hipLaunchKernelGGL(k_row_of, dim3(4096), dim3(256), 0, st, rowptr, n, (int32_t*)rowOf.ptr);
   CYC_LAUNCH_CHECK("k_row_of");
   hipLaunchKernelGGL(k_csc_keys, dim3(8192), dim3(256), 0, st, (const int32_t*)rowOf.ptr, colidx,
-                     nnz, F, (int64_t*)keys.ptr);
+                     nnz, F, rowBlock, (int64_t*)keys.ptr);
   CYC_LAUNCH_CHECK("k_csc_keys");
   unsigned endBit = 1;
   while (endBit < 63 && ((int64_t)1 << endBit) < nkeys) ++endBit;
@@ -225,6 +228,7 @@ int build_slices(const int64_t* rowptr, const int32_t* colidx, const double* val
 struct cyc_csc_s {
   int64_t n = 0;
   int F = 0;
+  int64_t rpb = cyc::kCscRowBlock;   // rows per CSC row block
   cyc::DeviceBuffer colptr, rowidx, cvals;
   // column-sliced CSR (S > 1 only)
   int S = 1, width = 0;
@@ -240,7 +244,16 @@ int cyc_csc_build_dev(const int64_t* rowptr, const int32_t* colidx, const double
   auto* c = new cyc_csc_s();
   c->n = n;
   c->F = numFeatures;
-  int rc = cyc::build_csc(rowptr, colidx, vals, n, numFeatures, c->colptr, c->rowidx, c->cvals,
+  // rows per row block: the gradient pass keeps one block's multipliers
+  // (8 B per row) in L2; CYC_CSC_ROWBLOCK_LOG2 overrides (measurement)
+  static const int64_t rowBlock = [] {
+    const char* e = std::getenv("CYC_CSC_ROWBLOCK_LOG2");
+    const int l = e ? std::atoi(e) : 0;
+    return (l >= 10 && l <= 24) ? ((int64_t)1 << l) : cyc::kCscRowBlock;
+  }();
+  c->rpb = rowBlock;
+  int rc = cyc::build_csc(rowptr, colidx, vals, n, numFeatures, c->rpb, c->colptr, c->rowidx,
+                          c->cvals,
                           cyc::as_stream(stream));
   // slices of at most kSliceCols columns (2 MB of fp64 coefficients)
   c->S = (int)std::min<int64_t>(16, ((int64_t)numFeatures + cyc::kSliceCols - 1) / cyc::kSliceCols);
@@ -279,9 +292,8 @@ int cyc_csc_slices(cyc_csc csc, int32_t* nslices, int32_t* width, const int64_t*
 
 int cyc_csc_blocks(cyc_csc csc, int64_t* rows_per_block, int64_t* nblocks) {
   CYC_REQUIRE(csc != nullptr, "csc must not be null");
-  if (rows_per_block) *rows_per_block = cyc::kCscRowBlock;
-  if (nblocks)
-    *nblocks = std::max<int64_t>((csc->n + cyc::kCscRowBlock - 1) / cyc::kCscRowBlock, 1);
+  if (rows_per_block) *rows_per_block = csc->rpb;
+  if (nblocks) *nblocks = std::max<int64_t>((csc->n + csc->rpb - 1) / csc->rpb, 1);
   return CYC_OK;
 }
 

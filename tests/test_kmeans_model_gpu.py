@@ -111,3 +111,23 @@ def test_empty_input(cuda):
     X = torch.empty(0, 3, dtype=torch.float64, device=cuda)
     assert m.predict(X).numel() == 0
     assert m.computeCost(X) == 0.0
+
+
+def test_kmeans_parallel_cost_updates(cuda):
+    """k-means|| cost updates (KMeans.scala:375-398) on the device: costs start
+    at +inf and take min(pointCost(newCenters), cost) per step; every step
+    bit-exact vs the restatement's per-row findClosest without statistics."""
+    from cycloneml_amd.clustering import KMeans
+    rng = np.random.default_rng(11)
+    X = rng.normal(size=(4000, 24)) + rng.integers(0, 5, size=(4000, 1)) * 3.0
+    xn = oracle.row_norms(X)
+    want = np.full(X.shape[0], np.inf)
+    got, tot = None, 0.0
+    Xd = _dev(X, cuda)
+    for step in range(3):
+        C = X[rng.choice(X.shape[0], size=5 + 3 * step, replace=False)]
+        _, c, _ = oracle.point_costs(X, xn, C, oracle.row_norms(C))
+        want = np.minimum(want, c)
+        got, tot = KMeans.updateParallelCosts(Xd, C, got)
+        assert np.array_equal(got.cpu().numpy(), want)
+        assert tot == pytest.approx(float(want.sum()), rel=1e-12)
