@@ -962,7 +962,8 @@ __global__ __launch_bounds__(kS3Threads, 2) void k_kmeans_assign3(
 // reference would not visit may be computed speculatively and are discarded.
 __global__ __launch_bounds__(256) void k_assign_exact(
     const double* __restrict__ X, const double* __restrict__ xnorm, int d,
-    const double* __restrict__ C, const double* __restrict__ cnorm, int k,
+    const double* __restrict__ C, const double* __restrict__ Ct, int kpad,
+    const double* __restrict__ cnorm, int k,
     const double* __restrict__ stats, const int32_t* __restrict__ slowList,
     const unsigned int* __restrict__ slowCount, int32_t* __restrict__ assign,
     double* __restrict__ cost) {
@@ -994,7 +995,16 @@ __global__ __launch_bounds__(256) void k_assign_exact(
       for (;;) {
         const bool visit = valid && lane >= pos && lb < best && (ns || stats[iut(i, bi)] < best);
         if (visit && !have) {
-          dd = seq_sqdist(C + (int64_t)i * d, x, d);
+          // Vectors.sqdist(center, x) in order j = 0..d-1 (Vectors.scala:
+          // 580-587), center i read from the transposed copy: the visiting
+          // lanes' loads of one j are one coalesced row of Ct
+          const double* ci = Ct + i;
+          double sq = 0.0;
+          for (int j = 0; j < d; ++j) {
+            const double sc = dsub(ci[(int64_t)j * kpad], x[j]);
+            sq = dadd(sq, dmul(sc, sc));
+          }
+          dd = sq;
           have = true;
         }
         const bool brk = !ns && visit && dd < sii;
@@ -1857,7 +1867,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
     p->lastExact = h_slow;
     if (h_slow) {
       hipLaunchKernelGGL(k_assign_exact, dim3((unsigned)std::min<unsigned>((h_slow + 3) / 4, 4096)), dim3(256), 0, st, X, xnorm,
-                         p->d, C, cnorm, p->k, statsArg,
+                         p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm, p->k, statsArg,
                          (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr,
                          assign, cost);
       CYC_LAUNCH_CHECK("k_assign_exact");
@@ -1865,7 +1875,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
   } else {
     const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 2048);
     hipLaunchKernelGGL(k_assign_exact, dim3(grid), dim3(256), 0, st, X, xnorm,
-                       p->d, C, cnorm, p->k, statsArg,
+                       p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm, p->k, statsArg,
                        (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr, assign,
                        cost);
     CYC_LAUNCH_CHECK("k_assign_exact");
@@ -2086,6 +2096,12 @@ int cyc_kmeans_point_cost_dev(cyc_kmeans_plan p, const double* X, const double* 
   hipStream_t st = cyc::as_stream(stream);
   int rc = ensure_rows(p, n);
   if (rc) return rc;
+  // the fp64 screen reads the transposed centers, which cyc_kmeans_stats_dev
+  // would otherwise build: no statistics are needed here
+  const int64_t total = (int64_t)p->d4 * p->kpad;
+  hipLaunchKernelGGL(k_center_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     C, p->k, p->d, p->d4, p->kpad, (double*)p->ct.ptr);
+  CYC_LAUNCH_CHECK("k_center_transpose");
   if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st, true)))
     return rc;
   hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n, p->d, C,

@@ -131,3 +131,28 @@ def test_kmeans_parallel_cost_updates(cuda):
         got, tot = KMeans.updateParallelCosts(Xd, C, got)
         assert np.array_equal(got.cpu().numpy(), want)
         assert tot == pytest.approx(float(want.sum()), rel=1e-12)
+
+
+def test_point_cost_on_a_fresh_plan(cuda):
+    """cyc_kmeans_point_cost_dev needs no prior cyc_kmeans_stats_dev: a fresh
+    plan (no statistics, no center transpose yet) and a plan last used for
+    OTHER centers both give the restatement's bits."""
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    rng = np.random.default_rng(21)
+    n, d, k = 6000, 40, 64
+    X = rng.normal(size=(n, d)) + rng.integers(0, 8, size=(n, 1)) * 2.0
+    C = X[rng.choice(n, size=k, replace=False)].copy()
+    C2 = C + 0.5
+    a, c, _ = oracle.point_costs(X, oracle.row_norms(X), C, oracle.row_norms(C))
+    Xd, Cd, C2d = _dev(X, cuda), _dev(C, cuda), _dev(C2, cuda)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    for warm in (False, True):
+        plan = KMeansPlan(d, k, n)
+        if warm:
+            plan.stats(C2d)      # statistics / transpose of other centers
+        ga = torch.empty(n, dtype=torch.int32, device=cuda)
+        gc = torch.empty(n, dtype=torch.float64, device=cuda)
+        plan.point_cost(Xd, xn, Cd, cn, ga, gc)
+        assert np.array_equal(ga.cpu().numpy(), a)
+        assert np.array_equal(gc.cpu().numpy(), c)
