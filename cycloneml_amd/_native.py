@@ -136,6 +136,12 @@ SIGNATURES = {
     "cyc_dataset_append_dense": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64]),
     "cyc_dataset_append_csr": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64]),
     "cyc_kmeans_iter": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "cyc_svc_hinge_eval": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp, _vp, _vp, _vp]),
+    "cyc_linreg_least_squares_eval": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, _f64, _f64,
+                                                     _vp, _vp, _vp, _vp]),
+    "cyc_linreg_huber_eval": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _f64, _vp, _vp, _vp,
+                                             _vp]),
+    "cyc_aft_eval": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp, _vp, _vp, _vp]),
     "cyc_logreg_binary_eval": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, _vp,
                                               _vp, _vp]),
     "cyc_logreg_multinomial_eval": (ctypes.c_int, [_vp, _i32, _vp, ctypes.c_int, ctypes.c_int,

@@ -50,6 +50,8 @@ struct cyc_dataset_s {
   // plans
   std::map<int, cyc_kmeans_plan> kplans;
   std::map<std::tuple<int, int, int>, cyc_logistic_plan> lplans;
+  // hinge / least squares / Huber / AFT plans: (kind, fitIntercept, a, b)
+  std::map<std::tuple<int, int, double, double>, cyc_logistic_plan> xplans;
   cyc_gramian_plan gplan = nullptr;
   // model in / state out staging
   cyc::DeviceBuffer in0, in1, in2, out0, out1;
@@ -59,6 +61,7 @@ struct cyc_dataset_s {
     for (auto& kv : krows) cyc_kmeans_rows_destroy(kv.second);
     for (auto& kv : kplans) cyc_kmeans_plan_destroy(kv.second);
     for (auto& kv : lplans) cyc_logistic_plan_destroy(kv.second);
+    for (auto& kv : xplans) cyc_logistic_plan_destroy(kv.second);
     if (gplan) cyc_gramian_plan_destroy(gplan);
     if (csc) cyc_csc_destroy(csc);
     if (st) (void)hipStreamDestroy(st);
@@ -370,6 +373,114 @@ static int logreg_eval(cyc_dataset ds, int32_t C, const double* coef, int fi, in
     return rc;
   CYC_HIP(hipStreamSynchronize(ds->st));
   return CYC_OK;
+}
+
+// The other block aggregators on the resident rows: kind 1 hinge, 2 least
+// squares (a = labelStd, b = labelMean; inverseStd gives effectiveCoef),
+// 3 Huber (a = epsilon), 4 AFT (the dataset's weights are the censors).
+static int linear_eval(cyc_dataset ds, int kind, const double* coef, size_t dim, int fi,
+                       double a, double b, const double* inverseStd, const double* scaledMean,
+                       double* grad, double* lossSum, double* weightSum) {
+  CYC_REQUIRE(ds != nullptr && coef && grad && lossSum && weightSum,
+              "arguments must not be null");
+  CYC_REQUIRE(ds->has_labels, "the dataset holds no labels");
+  DeviceGuard g(ds->device);
+  int rc = CYC_OK;
+  const auto key = std::make_tuple(kind, fi != 0, a, b);
+  auto it = ds->xplans.find(key);
+  if (it == ds->xplans.end()) {
+    cyc_logistic_plan p = nullptr;
+    if (kind == 1) rc = cyc_hinge_plan_create(ds->F, fi, &p);
+    else if (kind == 2) rc = cyc_least_squares_plan_create(ds->F, fi, a, b, &p);
+    else if (kind == 3) rc = cyc_huber_plan_create(ds->F, fi, a, &p);
+    else rc = cyc_aft_plan_create(ds->F, fi, &p);
+    if (rc) return rc;
+    it = ds->xplans.emplace(key, p).first;
+  }
+  cyc_logistic_plan plan = it->second;
+  double *dCoef, *dMean = nullptr, *dInv = nullptr, *dG;
+  if ((rc = upload(ds->in0, coef, dim, ds->st, &dCoef)) ||
+      (rc = upload(ds->out0, grad, dim + 2, ds->st, &dG)))
+    return rc;
+  if (scaledMean && (rc = upload(ds->in1, scaledMean, ds->F, ds->st, &dMean))) return rc;
+  if (inverseStd && (rc = upload(ds->in2, inverseStd, ds->F, ds->st, &dInv))) return rc;
+  CYC_HIP(hipMemcpyAsync(dG + dim, lossSum, sizeof(double), hipMemcpyHostToDevice, ds->st));
+  CYC_HIP(hipMemcpyAsync(dG + dim + 1, weightSum, sizeof(double), hipMemcpyHostToDevice, ds->st));
+  const double* w = ds->has_weights ? (const double*)ds->weights.ptr : nullptr;
+  const double* y = (const double*)ds->labels.ptr;
+  if (ds->sparse && !ds->csc && ds->rows &&
+      (rc = cyc_csc_build_dev((const int64_t*)ds->rowptr.ptr, (const int32_t*)ds->colidx.ptr,
+                              (const double*)ds->vals.ptr, ds->rows, ds->F, ds->st, &ds->csc)))
+    return rc;
+  const int64_t* rp = (const int64_t*)ds->rowptr.ptr;
+  const int32_t* ci = (const int32_t*)ds->colidx.ptr;
+  const double* vv = (const double*)ds->vals.ptr;
+  const double* X = (const double*)ds->X.ptr;
+  double *L = dG + dim, *W = dG + dim + 1;
+  switch (kind) {
+    case 1:
+      rc = ds->sparse ? cyc_hinge_add_csr_dev(plan, rp, ci, vv, y, w, ds->rows, dCoef, dMean, dG, L,
+                                              W, ds->csc, ds->st)
+                      : cyc_hinge_add_dense_dev(plan, X, y, w, ds->rows, dCoef, dMean, dG, L, W,
+                                                ds->st);
+      break;
+    case 2:
+      rc = ds->sparse ? cyc_least_squares_add_csr_dev(plan, rp, ci, vv, y, w, ds->rows, dCoef,
+                                                      dInv, dMean, dG, L, W, ds->csc, ds->st)
+                      : cyc_least_squares_add_dense_dev(plan, X, y, w, ds->rows, dCoef, dInv,
+                                                        dMean, dG, L, W, ds->st);
+      break;
+    case 3:
+      rc = ds->sparse ? cyc_huber_add_csr_dev(plan, rp, ci, vv, y, w, ds->rows, dCoef, dMean, dG, L,
+                                              W, ds->csc, ds->st)
+                      : cyc_huber_add_dense_dev(plan, X, y, w, ds->rows, dCoef, dMean, dG, L, W,
+                                                ds->st);
+      break;
+    default:
+      rc = ds->sparse ? cyc_aft_add_csr_dev(plan, rp, ci, vv, y, w, ds->rows, dCoef, dMean, dG, L,
+                                            W, ds->csc, ds->st)
+                      : cyc_aft_add_dense_dev(plan, X, y, w, ds->rows, dCoef, dMean, dG, L, W,
+                                              ds->st);
+  }
+  if (rc) return rc;
+  if ((rc = download(grad, dG, dim, ds->st)) || (rc = download(lossSum, L, 1, ds->st)) ||
+      (rc = download(weightSum, W, 1, ds->st)))
+    return rc;
+  CYC_HIP(hipStreamSynchronize(ds->st));
+  return CYC_OK;
+}
+
+int cyc_svc_hinge_eval(cyc_dataset ds, const double* coef, int fitIntercept,
+                       const double* scaledMean, double* grad, double* lossSum,
+                       double* weightSum) {
+  if (!ds) return linear_eval(ds, 1, coef, 0, 0, 0, 0, nullptr, nullptr, grad, lossSum, weightSum);
+  return linear_eval(ds, 1, coef, (size_t)ds->F + (fitIntercept ? 1 : 0), fitIntercept, 0.0, 0.0,
+                     nullptr, scaledMean, grad, lossSum, weightSum);
+}
+
+int cyc_linreg_least_squares_eval(cyc_dataset ds, const double* coef, const double* inverseStd,
+                                  int fitIntercept, double labelStd, double labelMean,
+                                  const double* scaledMean, double* grad, double* lossSum,
+                                  double* weightSum) {
+  CYC_REQUIRE(inverseStd != nullptr, "inverseStd must not be null");
+  if (!ds) return linear_eval(ds, 2, coef, 0, 0, 0, 0, nullptr, nullptr, grad, lossSum, weightSum);
+  return linear_eval(ds, 2, coef, (size_t)ds->F, fitIntercept, labelStd, labelMean, inverseStd,
+                     scaledMean, grad, lossSum, weightSum);
+}
+
+int cyc_linreg_huber_eval(cyc_dataset ds, const double* params, int fitIntercept, double epsilon,
+                          const double* scaledMean, double* grad, double* lossSum,
+                          double* weightSum) {
+  if (!ds) return linear_eval(ds, 3, params, 0, 0, 0, 0, nullptr, nullptr, grad, lossSum, weightSum);
+  return linear_eval(ds, 3, params, (size_t)ds->F + (fitIntercept ? 2 : 1), fitIntercept, epsilon,
+                     0.0, nullptr, scaledMean, grad, lossSum, weightSum);
+}
+
+int cyc_aft_eval(cyc_dataset ds, const double* coef, int fitIntercept, const double* scaledMean,
+                 double* grad, double* lossSum, double* weightSum) {
+  if (!ds) return linear_eval(ds, 4, coef, 0, 0, 0, 0, nullptr, nullptr, grad, lossSum, weightSum);
+  return linear_eval(ds, 4, coef, (size_t)ds->F + 2, fitIntercept, 0.0, 0.0, nullptr, scaledMean,
+                     grad, lossSum, weightSum);
 }
 
 int cyc_logreg_binary_eval(cyc_dataset ds, const double* coef, int fitIntercept, int fitWithMean,

@@ -120,6 +120,40 @@ class ResidentDataset:
         return self._logreg(numClasses, coef, fitIntercept, fitWithMean, scaledMean, grad,
                             loss_weight)
 
+    def _linear(self, fn, coef, args_before, args_after, grad, loss_weight):
+        coef = _f64(coef)
+        grad = np.zeros(coef.size) if grad is None else grad
+        lw = np.zeros(2) if loss_weight is None else loss_weight
+        l_p = ctypes.c_void_p(lw.ctypes.data)
+        w_p = ctypes.c_void_p(lw.ctypes.data + 8)
+        N.check(fn(self._h, _p(coef), *args_before, *args_after, _p(grad), l_p, w_p))
+        return grad, lw
+
+    def hinge_eval(self, coef, fitIntercept, scaledMean=None, grad=None, loss_weight=None):
+        """RDDLossFunction seqOp with HingeBlockAggregator.add (LinearSVC)."""
+        return self._linear(N.load().cyc_svc_hinge_eval, coef, (int(fitIntercept),),
+                            (_p(_f64(scaledMean)),), grad, loss_weight)
+
+    def least_squares_eval(self, coef, inverseStd, fitIntercept, labelStd, labelMean,
+                           scaledMean=None, grad=None, loss_weight=None):
+        """... with LeastSquaresBlockAggregator.add (LinearRegression, dim F)."""
+        inv = _f64(inverseStd)
+        return self._linear(N.load().cyc_linreg_least_squares_eval, coef,
+                            (_p(inv), int(fitIntercept), float(labelStd), float(labelMean)),
+                            (_p(_f64(scaledMean)),), grad, loss_weight)
+
+    def huber_eval(self, params, fitIntercept, epsilon, scaledMean=None, grad=None,
+                   loss_weight=None):
+        """... with HuberBlockAggregator.add (params: linear, intercept, sigma)."""
+        return self._linear(N.load().cyc_linreg_huber_eval, params,
+                            (int(fitIntercept), float(epsilon)), (_p(_f64(scaledMean)),), grad,
+                            loss_weight)
+
+    def aft_eval(self, coef, fitIntercept, scaledMean=None, grad=None, loss_weight=None):
+        """... with AFTBlockAggregator.add (the dataset's weights are censors)."""
+        return self._linear(N.load().cyc_aft_eval, coef, (int(fitIntercept),),
+                            (_p(_f64(scaledMean)),), grad, loss_weight)
+
     def gramian(self, mean=None, U=None):
         """Packed upper Gramian (RowMatrix.scala:130-161); centered if mean."""
         n = self.numFeatures

@@ -405,6 +405,25 @@ int cyc_logreg_multinomial_eval(cyc_dataset ds, int32_t numClasses, const double
                                 int fitIntercept, int fitWithMean, const double* scaledMean,
                                 double* grad, double* lossSum, double* weightSum);
 /* U: packed upper n(n+1)/2 (column-major); mean_opt centers the rows. */
+/* The other block aggregators over the resident rows, same conventions as
+ * cyc_logreg_*_eval (host model in, host state out; grad / lossSum /
+ * weightSum accumulate): LinearSVC's HingeBlockAggregator (dim F +
+ * fitIntercept), LinearRegression's LeastSquaresBlockAggregator (dim F;
+ * inverseStd required) and HuberBlockAggregator (dim F + fitIntercept + 1),
+ * AFTSurvivalRegression's AFTBlockAggregator (dim F + 2; the dataset's
+ * weights are the censors). */
+int cyc_svc_hinge_eval(cyc_dataset ds, const double* coef, int fitIntercept,
+                       const double* scaledMean, double* grad, double* lossSum,
+                       double* weightSum);
+int cyc_linreg_least_squares_eval(cyc_dataset ds, const double* coef, const double* inverseStd,
+                                  int fitIntercept, double labelStd, double labelMean,
+                                  const double* scaledMean, double* grad, double* lossSum,
+                                  double* weightSum);
+int cyc_linreg_huber_eval(cyc_dataset ds, const double* params, int fitIntercept, double epsilon,
+                          const double* scaledMean, double* grad, double* lossSum,
+                          double* weightSum);
+int cyc_aft_eval(cyc_dataset ds, const double* coef, int fitIntercept, const double* scaledMean,
+                 double* grad, double* lossSum, double* weightSum);
 int cyc_gramian(cyc_dataset ds, const double* mean_opt, double* U);
 int cyc_col_sums(cyc_dataset ds, double* sums);
 

@@ -183,3 +183,63 @@ def test_dataset_csr_kmeans_iter(cuda):
     _rel_close(sums, rs, rtol=1e-12)
     _rel_close(wsum, rw, rtol=1e-12)
     _rel_close(cost[0], rc, rtol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sparse", [False, True])
+@pytest.mark.parametrize("fi", [False, True])
+def test_other_aggregator_evals(cuda, sparse, fi):
+    """Resident-dataset evaluators of the hinge / least squares / Huber / AFT
+    block aggregators vs the restatement (1e-10), dense and CSR rows appended
+    in two pieces."""
+    rng = np.random.default_rng(31 + fi + 2 * sparse)
+    n, F = 2500, 40
+    y01 = rng.integers(0, 2, size=n).astype(np.float64)
+    yr = rng.normal(size=n) * 2.0
+    yt = rng.exponential(2.0, size=n) + 1e-3
+    w = rng.uniform(0.1, 2.0, size=n)
+    cens = (rng.uniform(size=n) < 0.6).astype(np.float64)
+    sm = rng.normal(size=F) * 0.1 if fi else None
+    inv = rng.uniform(0.5, 2.0, size=F)
+    inv[3] = 0.0
+    if sparse:
+        rp, ci, vv = _csr(n, F, rng)
+        blk = lambda lab, wt: dict(labels=lab, weights=wt, rowptr=rp, colidx=ci, values=vv, F=F)
+    else:
+        X = rng.normal(size=(n, F))
+        blk = lambda lab, wt: dict(labels=lab, weights=wt, X=X)
+
+    def make(lab, wt):
+        if sparse:
+            ds = ResidentDataset.csr(F, n, ci.size, labels=True, weights=True)
+            h = n // 2
+            ds.append_csr(rp[:h + 1], ci[:rp[h]], vv[:rp[h]], lab[:h], wt[:h])
+            ds.append_csr(rp[h:], ci[rp[h]:], vv[rp[h]:], lab[h:], wt[h:])
+            return ds
+        return ResidentDataset.dense(F, n, labels=True, weights=True).append_dense(X, lab, wt)
+
+    def check(got, st):
+        grad, lw = got
+        _rel_close(grad, st["grad"])
+        assert abs(lw[0] - st["loss"]) <= 1e-10 * abs(st["loss"])
+        assert abs(lw[1] - st["weight"]) <= 1e-12 * st["weight"]
+
+    coef = rng.normal(size=F + (1 if fi else 0)) * 0.3
+    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+    oracle.hinge_add(blk(y01, w), coef, fi, sm, st)
+    check(make(y01, w).hinge_eval(coef, fi, sm), st)
+
+    coef = rng.normal(size=F) * 0.3
+    st = dict(grad=np.zeros(F), loss=0.0, weight=0.0)
+    oracle.least_squares_add(blk(yr, w), coef, inv, fi, 1.7, 0.2, sm, st)
+    check(make(yr, w).least_squares_eval(coef, inv, fi, 1.7, 0.2, sm), st)
+
+    params = np.concatenate([rng.normal(size=F) * 0.3, [0.4] if fi else [], [0.9]])
+    st = dict(grad=np.zeros(params.size), loss=0.0, weight=0.0)
+    oracle.huber_add(blk(yr, w), params, fi, 1.35, sm, st)
+    check(make(yr, w).huber_eval(params, fi, 1.35, sm), st)
+
+    coef = np.concatenate([rng.normal(size=F) * 0.1, [0.3 if fi else 0.0], [0.2]])
+    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+    oracle.aft_add(blk(yt, cens), coef, fi, sm, st)
+    check(make(yt, cens).aft_eval(coef, fi, sm), st)
