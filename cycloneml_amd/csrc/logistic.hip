@@ -1371,8 +1371,10 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
   const int CT = (C + 15) / 16, CP = CT * 16;
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
-  // Rows are processed in chunks so the multiplier matrix stays small.
-  const int64_t chunk = std::min<int64_t>(n, 4 << 20);
+  // Rows are processed in chunks of up to 8M so the multiplier matrix stays
+  // bounded (8M x CP doubles: 7.3 GB at C = 100); a whole 6.25M-row shard of
+  // the 8-GPU config is one launch (no second partial round of tiles).
+  const int64_t chunk = std::min<int64_t>(n, 8 << 20);
   const int mblocks = 256;   // persistent: one 8-wave workgroup per CU
   const int64_t mwaves = (int64_t)mblocks * (MT / 64);
   const int ftiles = (F + GF - 1) / GF;
