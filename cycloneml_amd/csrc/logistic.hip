@@ -253,34 +253,52 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
     const int64_t myr = g0 + lane < n ? g0 + lane : n;
     const int64_t rp0 = rowptr[myr];
     const int64_t rp1 = rowptr[myr + 1 < n ? myr + 1 : n];
-    // every round's first 16 nonzeros in flight at once (8 lanes x 2), then
-    // the gathers, then the products; longer rows finish in a tail loop
+    // the 8 rounds advance together in 16-nonzero chunks (8 lanes x 2 per
+    // row): each chunk issues all 16 index/value loads, then the 16 gathers,
+    // then the products, so every chunk has 16 loads in flight per lane and
+    // the dependent index->coefficient latency is paid once per chunk rather
+    // than once per nonzero.  A lane's products still add in ascending
+    // nonzero order (sub, sub+8, sub+16, ...), as the single-row loop did.
     int64_t beg[8], end[8];
-    int ci[8][2];
-    double vv[8][2], cf[8][2];
+    int64_t maxlen = rp1 - rp0;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+      const int64_t o = __shfl_xor(maxlen, m);
+      maxlen = o > maxlen ? o : maxlen;
+    }
+    double sr[8];
 #pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
       beg[rr] = __shfl(rp0, rr * 8 + grp);
       end[rr] = __shfl(rp1, rr * 8 + grp);
+      sr[rr] = 0.0;
+    }
+    for (int64_t k = 0; k < maxlen; k += 16) {
+      int ci[8][2];
+      double vv[8][2], cf[8][2];
 #pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        const int64_t p = beg[rr] + sub + 8 * it;
-        const bool ok = p < end[rr];
-        ci[rr][it] = ok ? __builtin_nontemporal_load(colidx + p) : 0;
-        vv[rr][it] = ok ? __builtin_nontemporal_load(vals + p) : 0.0;
+      for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const int64_t p = beg[rr] + k + sub + 8 * it;
+          const bool ok = p < end[rr];
+          ci[rr][it] = ok ? __builtin_nontemporal_load(colidx + p) : -1;
+          vv[rr][it] = ok ? __builtin_nontemporal_load(vals + p) : 0.0;
+        }
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+        for (int it = 0; it < 2; ++it) cf[rr][it] = ci[rr][it] >= 0 ? coef[ci[rr][it]] : 0.0;
+#pragma unroll
+      for (int rr = 0; rr < 8; ++rr) {
+        if (beg[rr] + k + sub < end[rr]) sr[rr] += vv[rr][0] * cf[rr][0];
+        if (beg[rr] + k + sub + 8 < end[rr]) sr[rr] += vv[rr][1] * cf[rr][1];
       }
     }
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr)
-#pragma unroll
-      for (int it = 0; it < 2; ++it) cf[rr][it] = coef[ci[rr][it]];
     double mydot = 0.0;
 #pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
-      double s = vv[rr][0] * cf[rr][0];
-      s += vv[rr][1] * cf[rr][1];
-      for (int64_t p = beg[rr] + sub + 16; p < end[rr]; p += 8)
-        s += __builtin_nontemporal_load(vals + p) * coef[__builtin_nontemporal_load(colidx + p)];
+      double s = sr[rr];
       s += __shfl_xor(s, 1);
       s += __shfl_xor(s, 2);
       s += __shfl_xor(s, 4);
