@@ -238,6 +238,7 @@ __global__ __launch_bounds__(256) void k_binlog_csc_grad(
 // CSR (csc.hip) the pass runs once per slice: dots[r] accumulates the slices'
 // partial dots in slice order (first: =, else +=) and the last slice turns
 // dots[r] into the multiplier in place, written coalesced.
+template <int CSR_IT>
 __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const double* __restrict__ vals, const double* __restrict__ labels,
@@ -273,13 +274,13 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
       end[rr] = __shfl(rp1, rr * 8 + grp);
       sr[rr] = 0.0;
     }
-    for (int64_t k = 0; k < maxlen; k += 16) {
-      int ci[8][2];
-      double vv[8][2], cf[8][2];
+    for (int64_t k = 0; k < maxlen; k += 8 * CSR_IT) {
+      int ci[8][CSR_IT];
+      double vv[8][CSR_IT], cf[8][CSR_IT];
 #pragma unroll
       for (int rr = 0; rr < 8; ++rr)
 #pragma unroll
-        for (int it = 0; it < 2; ++it) {
+        for (int it = 0; it < CSR_IT; ++it) {
           const int64_t p = beg[rr] + k + sub + 8 * it;
           const bool ok = p < end[rr];
           ci[rr][it] = ok ? __builtin_nontemporal_load(colidx + p) : -1;
@@ -288,12 +289,12 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
 #pragma unroll
       for (int rr = 0; rr < 8; ++rr)
 #pragma unroll
-        for (int it = 0; it < 2; ++it) cf[rr][it] = ci[rr][it] >= 0 ? coef[ci[rr][it]] : 0.0;
+        for (int it = 0; it < CSR_IT; ++it) cf[rr][it] = ci[rr][it] >= 0 ? coef[ci[rr][it]] : 0.0;
 #pragma unroll
-      for (int rr = 0; rr < 8; ++rr) {
-        if (beg[rr] + k + sub < end[rr]) sr[rr] += vv[rr][0] * cf[rr][0];
-        if (beg[rr] + k + sub + 8 < end[rr]) sr[rr] += vv[rr][1] * cf[rr][1];
-      }
+      for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+        for (int it = 0; it < CSR_IT; ++it)
+          if (ci[rr][it] >= 0) sr[rr] += vv[rr][it] * cf[rr][it];
     }
     double mydot = 0.0;
 #pragma unroll
@@ -1166,10 +1167,15 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
       const int32_t* colS = nullptr;
       const double* valS = nullptr;
       cyc_csc_slices(csc, &S, &width, &rowptrS, &colS, &valS);
+      // nonzeros per lane per chunk (2 = 16 loads in flight); measurement override
+      int csr_it = 2;
+      if (const char* e = std::getenv("CYC_CSR_IT")) csr_it = std::atoi(e);
       cyc::KernelTimer timer("k_binlog_csr", st);
       for (int sl = 0; sl < S; ++sl) {
         const int64_t* rp = S > 1 ? rowptrS + (int64_t)sl * n : rowptr;
-        hipLaunchKernelGGL(k_binlog_csr_mult8, dim3((unsigned)blocks), dim3(256), 0, st, rp,
+        auto kern = csr_it == 4 ? k_binlog_csr_mult8<4>
+                    : csr_it == 3 ? k_binlog_csr_mult8<3> : k_binlog_csr_mult8<2>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, rp,
                            S > 1 ? colS : colidx, S > 1 ? valS : vals, labels, weights, n, kc,
                            p->fitIntercept, p->loss, offset, lscale, sigma, eps, sl == 0 ? 1 : 0,
                            sl == S - 1 ? 1 : 0,
