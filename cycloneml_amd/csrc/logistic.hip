@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void k_binlog_csc_grad(
 // CSR (csc.hip) the pass runs once per slice: dots[r] accumulates the slices'
 // partial dots in slice order (first: =, else +=) and the last slice turns
 // dots[r] into the multiplier in place, written coalesced.
-template <int CSR_IT>
+template <int CSR_IT, int RP>
 __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const double* __restrict__ vals, const double* __restrict__ labels,
@@ -260,51 +260,55 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
     // the dependent index->coefficient latency is paid once per chunk rather
     // than once per nonzero.  A lane's products still add in ascending
     // nonzero order (sub, sub+8, sub+16, ...), as the single-row loop did.
-    int64_t beg[8], end[8];
+    // RP rows per pass (8 / RP passes per round group) bound the live state.
     int64_t maxlen = rp1 - rp0;
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) {
       const int64_t o = __shfl_xor(maxlen, m);
       maxlen = o > maxlen ? o : maxlen;
     }
-    double sr[8];
-#pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      beg[rr] = __shfl(rp0, rr * 8 + grp);
-      end[rr] = __shfl(rp1, rr * 8 + grp);
-      sr[rr] = 0.0;
-    }
-    for (int64_t k = 0; k < maxlen; k += 8 * CSR_IT) {
-      int ci[8][CSR_IT];
-      double vv[8][CSR_IT], cf[8][CSR_IT];
-#pragma unroll
-      for (int rr = 0; rr < 8; ++rr)
-#pragma unroll
-        for (int it = 0; it < CSR_IT; ++it) {
-          const int64_t p = beg[rr] + k + sub + 8 * it;
-          const bool ok = p < end[rr];
-          ci[rr][it] = ok ? __builtin_nontemporal_load(colidx + p) : -1;
-          vv[rr][it] = ok ? __builtin_nontemporal_load(vals + p) : 0.0;
-        }
-#pragma unroll
-      for (int rr = 0; rr < 8; ++rr)
-#pragma unroll
-        for (int it = 0; it < CSR_IT; ++it) cf[rr][it] = ci[rr][it] >= 0 ? coef[ci[rr][it]] : 0.0;
-#pragma unroll
-      for (int rr = 0; rr < 8; ++rr)
-#pragma unroll
-        for (int it = 0; it < CSR_IT; ++it)
-          if (ci[rr][it] >= 0) sr[rr] += vv[rr][it] * cf[rr][it];
-    }
     double mydot = 0.0;
 #pragma unroll
-    for (int rr = 0; rr < 8; ++rr) {
-      double s = sr[rr];
-      s += __shfl_xor(s, 1);
-      s += __shfl_xor(s, 2);
-      s += __shfl_xor(s, 4);
-      const double v = __shfl(s, 8 * (lane & 7));
-      if ((lane >> 3) == rr) mydot = v;
+    for (int h = 0; h < 8; h += RP) {
+      int64_t beg[RP], end[RP];
+      double sr[RP];
+#pragma unroll
+      for (int rr = 0; rr < RP; ++rr) {
+        beg[rr] = __shfl(rp0, (h + rr) * 8 + grp);
+        end[rr] = __shfl(rp1, (h + rr) * 8 + grp);
+        sr[rr] = 0.0;
+      }
+      for (int64_t k = 0; k < maxlen; k += 8 * CSR_IT) {
+        int ci[RP][CSR_IT];
+        double vv[RP][CSR_IT], cf[RP][CSR_IT];
+#pragma unroll
+        for (int rr = 0; rr < RP; ++rr)
+#pragma unroll
+          for (int it = 0; it < CSR_IT; ++it) {
+            const int64_t p = beg[rr] + k + sub + 8 * it;
+            const bool ok = p < end[rr];
+            ci[rr][it] = ok ? __builtin_nontemporal_load(colidx + p) : -1;
+            vv[rr][it] = ok ? __builtin_nontemporal_load(vals + p) : 0.0;
+          }
+#pragma unroll
+        for (int rr = 0; rr < RP; ++rr)
+#pragma unroll
+          for (int it = 0; it < CSR_IT; ++it) cf[rr][it] = ci[rr][it] >= 0 ? coef[ci[rr][it]] : 0.0;
+#pragma unroll
+        for (int rr = 0; rr < RP; ++rr)
+#pragma unroll
+          for (int it = 0; it < CSR_IT; ++it)
+            if (ci[rr][it] >= 0) sr[rr] += vv[rr][it] * cf[rr][it];
+      }
+#pragma unroll
+      for (int rr = 0; rr < RP; ++rr) {
+        double s = sr[rr];
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        s += __shfl_xor(s, 4);
+        const double v = __shfl(s, 8 * (lane & 7));
+        if ((lane >> 3) == h + rr) mydot = v;
+      }
     }
     const int64_t row = g0 + lane;
     if (row < n) {
@@ -1170,11 +1174,14 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
       // nonzeros per lane per chunk (2 = 16 loads in flight); measurement override
       int csr_it = 2;
       if (const char* e = std::getenv("CYC_CSR_IT")) csr_it = std::atoi(e);
+      int csr_rp = 8;  // rows per pass
+      if (const char* e = std::getenv("CYC_CSR_RP")) csr_rp = std::atoi(e);
       cyc::KernelTimer timer("k_binlog_csr", st);
       for (int sl = 0; sl < S; ++sl) {
         const int64_t* rp = S > 1 ? rowptrS + (int64_t)sl * n : rowptr;
-        auto kern = csr_it == 4 ? k_binlog_csr_mult8<4>
-                    : csr_it == 3 ? k_binlog_csr_mult8<3> : k_binlog_csr_mult8<2>;
+        auto kern = csr_rp == 4 ? (csr_it == 4 ? k_binlog_csr_mult8<4, 4> : k_binlog_csr_mult8<2, 4>)
+                    : csr_it == 4 ? k_binlog_csr_mult8<4, 8>
+                    : csr_it == 3 ? k_binlog_csr_mult8<3, 8> : k_binlog_csr_mult8<2, 8>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, rp,
                            S > 1 ? colS : colidx, S > 1 ? valS : vals, labels, weights, n, kc,
                            p->fitIntercept, p->loss, offset, lscale, sigma, eps, sl == 0 ? 1 : 0,
