@@ -344,26 +344,27 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
 // column, products vals * mult[row] (the block's 2 MB multiplier slice stays
 // in L2), fixed 4-step butterfly, gradAcc[c] = (first ? 0 : gradAcc[c]) + s.
 // Deterministic: blocks in order, a block's rows in order within each lane.
+template <int LPC, int IT>
 __global__ __launch_bounds__(256) void k_binlog_csc_grad_blk(
     const int64_t* __restrict__ colptrB, const int32_t* __restrict__ rowidx,
     const double* __restrict__ cvals, const double* __restrict__ mult, int F, int first,
     double* __restrict__ gradAcc) {
-  // 16 lanes per group of 4 consecutive columns; the first 32 nonzeros of
-  // each column are loaded before any gather (all in flight at once)
-  const int sub = threadIdx.x & 15, lane = threadIdx.x & 63, gbase = lane & 48;
-  const int64_t c0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4) * 4;
+  // LPC lanes per group of 4 consecutive columns; the first LPC*IT nonzeros
+  // of each column are loaded before any gather (all in flight at once)
+  const int sub = threadIdx.x & (LPC - 1), lane = threadIdx.x & 63, gbase = lane & (64 - LPC);
+  const int64_t c0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPC) * 4;
   const int64_t ci = c0 + (sub < 5 ? sub : 4);
   const int64_t cp = colptrB[ci < F ? ci : (int64_t)F];
   int64_t b[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) b[i] = __shfl(cp, gbase + i);
-  int ri[4][2];
-  double vv[4][2], mm[4][2];
+  int ri[4][IT];
+  double vv[4][IT], mm[4][IT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int64_t q = b[i] + sub + 16 * it;
+    for (int it = 0; it < IT; ++it) {
+      const int64_t q = b[i] + sub + LPC * it;
       const bool ok = c0 + i < F && q < b[i + 1];
       ri[i][it] = ok ? __builtin_nontemporal_load(rowidx + q) : -1;
       vv[i][it] = ok ? __builtin_nontemporal_load(cvals + q) : 0.0;
@@ -371,19 +372,18 @@ __global__ __launch_bounds__(256) void k_binlog_csc_grad_blk(
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int it = 0; it < 2; ++it) mm[i][it] = ri[i][it] >= 0 ? mult[ri[i][it]] : 0.0;
+    for (int it = 0; it < IT; ++it) mm[i][it] = ri[i][it] >= 0 ? mult[ri[i][it]] : 0.0;
   double sv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     double s = vv[i][0] * mm[i][0];
-    s += vv[i][1] * mm[i][1];
+#pragma unroll
+    for (int it = 1; it < IT; ++it) s += vv[i][it] * mm[i][it];
     if (c0 + i < F)
-      for (int64_t q = b[i] + sub + 32; q < b[i + 1]; q += 16)
+      for (int64_t q = b[i] + sub + LPC * IT; q < b[i + 1]; q += LPC)
         s += __builtin_nontemporal_load(cvals + q) * mult[__builtin_nontemporal_load(rowidx + q)];
-    s += __shfl_xor(s, 8);
-    s += __shfl_xor(s, 4);
-    s += __shfl_xor(s, 2);
-    s += __shfl_xor(s, 1);
+#pragma unroll
+    for (int m = LPC / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
     sv[i] = s;
   }
   if (sub < 4 && c0 + sub < F) {
@@ -1192,10 +1192,18 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
     }
     int64_t rpb = 0, nb = 0;
     cyc_csc_blocks(csc, &rpb, &nb);
-    const unsigned cgrid = (unsigned)((((int64_t)F + 3) / 4 * 16 + 255) / 256);
+    // lanes per group of 4 columns: 32 (12.8 ms per evaluation; 16 / 8 lanes
+    // 14.0 / 15.3 ms) -- CYC_CSC_LPC overrides for such measurements
+    int lpc = 32;
+    if (const char* e = std::getenv("CYC_CSC_LPC")) lpc = std::atoi(e);
+    if (lpc != 8 && lpc != 16 && lpc != 64) lpc = 32;
+    const unsigned cgrid = (unsigned)((((int64_t)F + 3) / 4 * lpc + 255) / 256);
+    auto gkern = lpc == 8    ? k_binlog_csc_grad_blk<8, 3>
+                 : lpc == 16 ? k_binlog_csc_grad_blk<16, 2>
+                 : lpc == 64 ? k_binlog_csc_grad_blk<64, 1> : k_binlog_csc_grad_blk<32, 1>;
     cyc::KernelTimer timer("k_binlog_csc_grad", st);
     for (int64_t b = 0; b < nb; ++b) {
-      hipLaunchKernelGGL(k_binlog_csc_grad_blk, dim3(cgrid), dim3(256), 0, st,
+      hipLaunchKernelGGL(gkern, dim3(cgrid), dim3(256), 0, st,
                          colptr + b * F, rowidx, cvals, (const double*)p->rowMult.ptr, F,
                          b == 0 ? 1 : 0, (double*)p->gradAcc.ptr);
     }
