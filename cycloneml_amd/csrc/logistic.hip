@@ -344,24 +344,24 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
 // column, products vals * mult[row] (the block's 2 MB multiplier slice stays
 // in L2), fixed 4-step butterfly, gradAcc[c] = (first ? 0 : gradAcc[c]) + s.
 // Deterministic: blocks in order, a block's rows in order within each lane.
-template <int LPC, int IT>
+template <int LPC, int IT, int CPG>
 __global__ __launch_bounds__(256) void k_binlog_csc_grad_blk(
     const int64_t* __restrict__ colptrB, const int32_t* __restrict__ rowidx,
     const double* __restrict__ cvals, const double* __restrict__ mult, int F, int first,
     double* __restrict__ gradAcc) {
-  // LPC lanes per group of 4 consecutive columns; the first LPC*IT nonzeros
-  // of each column are loaded before any gather (all in flight at once)
+  // LPC lanes per group of CPG consecutive columns; the first LPC*IT
+  // nonzeros of each column are loaded before any gather (all in flight)
   const int sub = threadIdx.x & (LPC - 1), lane = threadIdx.x & 63, gbase = lane & (64 - LPC);
-  const int64_t c0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPC) * 4;
-  const int64_t ci = c0 + (sub < 5 ? sub : 4);
+  const int64_t c0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPC) * CPG;
+  const int64_t ci = c0 + (sub < CPG + 1 ? sub : CPG);
   const int64_t cp = colptrB[ci < F ? ci : (int64_t)F];
-  int64_t b[5];
+  int64_t b[CPG + 1];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) b[i] = __shfl(cp, gbase + i);
-  int ri[4][IT];
-  double vv[4][IT], mm[4][IT];
+  for (int i = 0; i <= CPG; ++i) b[i] = __shfl(cp, gbase + i);
+  int ri[CPG][IT];
+  double vv[CPG][IT], mm[CPG][IT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < CPG; ++i)
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int64_t q = b[i] + sub + LPC * it;
@@ -370,12 +370,12 @@ __global__ __launch_bounds__(256) void k_binlog_csc_grad_blk(
       vv[i][it] = ok ? __builtin_nontemporal_load(cvals + q) : 0.0;
     }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < CPG; ++i)
 #pragma unroll
     for (int it = 0; it < IT; ++it) mm[i][it] = ri[i][it] >= 0 ? mult[ri[i][it]] : 0.0;
-  double sv[4];
+  double mine = 0.0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < CPG; ++i) {
     double s = vv[i][0] * mm[i][0];
 #pragma unroll
     for (int it = 1; it < IT; ++it) s += vv[i][it] * mm[i][it];
@@ -384,12 +384,9 @@ __global__ __launch_bounds__(256) void k_binlog_csc_grad_blk(
         s += __builtin_nontemporal_load(cvals + q) * mult[__builtin_nontemporal_load(rowidx + q)];
 #pragma unroll
     for (int m = LPC / 2; m >= 1; m >>= 1) s += __shfl_xor(s, m);
-    sv[i] = s;
+    if (sub == i) mine = s;
   }
-  if (sub < 4 && c0 + sub < F) {
-    const double s = sub == 0 ? sv[0] : sub == 1 ? sv[1] : sub == 2 ? sv[2] : sv[3];
-    gradAcc[c0 + sub] = first ? s : gradAcc[c0 + sub] + s;
-  }
+  if (sub < CPG && c0 + sub < F) gradAcc[c0 + sub] = first ? mine : gradAcc[c0 + sub] + mine;
 }
 
 // Fold per-wave scalars in wave order: out3 = {loss, wsum, msum}.
@@ -1194,13 +1191,18 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
     cyc_csc_blocks(csc, &rpb, &nb);
     // lanes per group of 4 columns: 32 (12.8 ms per evaluation; 16 / 8 lanes
     // 14.0 / 15.3 ms) -- CYC_CSC_LPC overrides for such measurements
-    int lpc = 32;
+    int lpc = 32, cpg = 4;
     if (const char* e = std::getenv("CYC_CSC_LPC")) lpc = std::atoi(e);
     if (lpc != 8 && lpc != 16 && lpc != 64) lpc = 32;
-    const unsigned cgrid = (unsigned)((((int64_t)F + 3) / 4 * lpc + 255) / 256);
-    auto gkern = lpc == 8    ? k_binlog_csc_grad_blk<8, 3>
-                 : lpc == 16 ? k_binlog_csc_grad_blk<16, 2>
-                 : lpc == 64 ? k_binlog_csc_grad_blk<64, 1> : k_binlog_csc_grad_blk<32, 1>;
+    if (const char* e = std::getenv("CYC_CSC_CPG")) cpg = std::atoi(e);
+    if (cpg != 2 && cpg != 8) cpg = 4;
+    if (lpc != 32) cpg = 4;
+    const unsigned cgrid = (unsigned)((((int64_t)F + cpg - 1) / cpg * lpc + 255) / 256);
+    auto gkern = lpc == 8    ? k_binlog_csc_grad_blk<8, 3, 4>
+                 : lpc == 16 ? k_binlog_csc_grad_blk<16, 2, 4>
+                 : lpc == 64 ? k_binlog_csc_grad_blk<64, 1, 4>
+                 : cpg == 2  ? k_binlog_csc_grad_blk<32, 1, 2>
+                 : cpg == 8  ? k_binlog_csc_grad_blk<32, 1, 8> : k_binlog_csc_grad_blk<32, 1, 4>;
     cyc::KernelTimer timer("k_binlog_csc_grad", st);
     for (int64_t b = 0; b < nb; ++b) {
       hipLaunchKernelGGL(gkern, dim3(cgrid), dim3(256), 0, st,
