@@ -1,7 +1,10 @@
 // capi.cpp -- misc C-ABI entry points, error plumbing and scratch buffers.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -17,6 +20,51 @@ static thread_local std::string g_err;
 
 void set_error(const std::string& msg) { g_err = msg; }
 const std::string& get_error() { return g_err; }
+
+// java.lang.Double.toString: shortest digits that round-trip; plain decimal
+// for 1e-3 <= |x| < 1e7 with at least one fractional digit ("1.0"), else
+// "d.dddE<exp>" ("1.0E10", "2.5E-4"); "NaN", "Infinity", "-0.0".
+std::string java_double(double x) {
+  if (x != x) return "NaN";
+  if (x == __builtin_inf()) return "Infinity";
+  if (x == -__builtin_inf()) return "-Infinity";
+  if (x == 0.0) return std::signbit(x) ? "-0.0" : "0.0";
+  char buf[64];
+  int prec = 0;
+  for (; prec < 17; ++prec) {
+    std::snprintf(buf, sizeof(buf), "%.*e", prec, x);
+    if (std::strtod(buf, nullptr) == x) break;
+  }
+  std::snprintf(buf, sizeof(buf), "%.*e", prec, x);
+  // buf = [-]D[.DDD]e[+-]XX
+  std::string s(buf);
+  std::string sign;
+  if (s[0] == '-') {
+    sign = "-";
+    s = s.substr(1);
+  }
+  const size_t epos = s.find('e');
+  const int exp10 = std::atoi(s.c_str() + epos + 1);
+  std::string digits;
+  for (size_t i = 0; i < epos; ++i)
+    if (s[i] != '.') digits += s[i];
+  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+  const double ax = std::fabs(x);
+  if (ax >= 1e-3 && ax < 1e7) {
+    std::string out;
+    if (exp10 >= 0) {
+      std::string ip = digits.substr(0, std::min<size_t>(digits.size(), exp10 + 1));
+      while ((int)ip.size() < exp10 + 1) ip += '0';
+      std::string fp = (int)digits.size() > exp10 + 1 ? digits.substr(exp10 + 1) : "0";
+      out = ip + "." + fp;
+    } else {
+      out = "0." + std::string(-exp10 - 1, '0') + digits;
+    }
+    return sign + out;
+  }
+  std::string mant = digits.substr(0, 1) + "." + (digits.size() > 1 ? digits.substr(1) : "0");
+  return sign + mant + "E" + std::to_string(exp10);
+}
 
 int hip_fail(hipError_t e, const char* what, const char* file, int line) {
   char buf[512];

@@ -19,6 +19,10 @@ namespace cyc {
 void set_error(const std::string& msg);
 const std::string& get_error();
 
+// java.lang.Double.toString(x), for `require` messages that interpolate a
+// Double (Scala's s"$x").
+std::string java_double(double x);
+
 // A hipError_t turned into a CYC_ERR_HIP status with a message.
 int hip_fail(hipError_t e, const char* what, const char* file, int line);
 

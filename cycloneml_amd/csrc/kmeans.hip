@@ -1036,6 +1036,33 @@ __global__ void k_nostats_cost_fix(int64_t n, double* __restrict__ cost) {
   if (r < n && __builtin_isnan(cost[r])) cost[r] = __builtin_inf();
 }
 
+// MLUtils.fastSquaredDistance's require(norm1 >= 0.0 && norm2 >= 0.0,
+// "Both norms should be greater or equal to 0.0, ...") (mllib/util/
+// MLUtils.scala:542-543), as a with-statistics Lloyd step meets it:
+// computeStatistics (DistanceMeasure.scala:48-76) measures every center pair,
+// so a center with a NaN norm fails (k >= 2), and findClosest (:282-287)
+// measures (center 0, point) first for every point.  Other centers are only
+// measured behind `lowerBound < bestDistance` (:295-297), which a NaN norm
+// never passes; findClosest WITHOUT statistics (:318-340) therefore never
+// fails.  A norm is NaN iff the vector holds a NaN (Vectors.scala:500-507).
+// req[0]: lowest center holding a NaN, req[1]: lowest row with a NaN norm
+// (~0 when none; set by the caller); req[2..4] as doubles: norm(c0),
+// norm(c1), xnorm[0] -- the values the reference's message interpolates.
+__global__ void k_require_norms(const double* __restrict__ C, int k, int d,
+                                const double* __restrict__ xnorm, int64_t n,
+                                unsigned long long* __restrict__ req) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t kd = (int64_t)k * d;
+  for (int64_t i = t0; i < kd; i += stride)
+    if (__builtin_isnan(C[i])) atomicMin(&req[0], (unsigned long long)(i / d));
+  for (int64_t r = t0; r < n; r += stride)
+    if (__builtin_isnan(xnorm[r])) atomicMin(&req[1], (unsigned long long)r);
+  double* out = reinterpret_cast<double*>(req + 2);
+  if (t0 < 2 && t0 < k) out[t0] = seq_norm2(C + t0 * d, d);
+  if (t0 == 2) out[2] = n > 0 ? xnorm[0] : 0.0;
+}
+
 // ------------------------------------------------------- counting sort
 __global__ void k_hist(const int32_t* __restrict__ assign, int64_t n, int k,
                        int32_t* __restrict__ hist) {
@@ -1692,6 +1719,15 @@ struct cyc_kmeans_plan_s {
   std::mutex mu;
   cyc::DeviceBuffer ct, stats, dmin, segsum, slowList, slowCount, assignTmp, costTmp;
   cyc::DeviceBuffer hist, total, cstart, chunkStart, perm, part, pw, pc, ccost;
+  // require(norm1 >= 0.0 && norm2 >= 0.0) check (k_require_norms): device
+  // result, its pinned host copy and the event that marks the copy landed
+  cyc::DeviceBuffer req;
+  unsigned long long* reqHost = nullptr;
+  hipEvent_t reqEv = nullptr;
+  ~cyc_kmeans_plan_s() {
+    if (reqHost) (void)hipHostFree(reqHost);
+    if (reqEv) (void)hipEventDestroy(reqEv);
+  }
 };
 
 // Per-fit row image for the i8 screen (cyc_kmeans_rows_create).
@@ -1883,6 +1919,48 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
   return CYC_OK;
 }
 
+// Enqueue k_require_norms and the copy of its result; require_check reads it
+// after the rest of the call is enqueued, so the host waits only for this
+// early, short kernel (its result lands long before the assign finishes).
+int require_enqueue(cyc_kmeans_plan p, const double* C, const double* xnorm, int64_t n,
+                    hipStream_t st) {
+  int rc;
+  if ((rc = p->req.reserve(5 * sizeof(unsigned long long)))) return rc;
+  if (!p->reqHost) CYC_HIP(hipHostMalloc((void**)&p->reqHost, 5 * sizeof(unsigned long long)));
+  if (!p->reqEv) CYC_HIP(hipEventCreateWithFlags(&p->reqEv, hipEventDisableTiming));
+  CYC_HIP(hipMemsetAsync(p->req.ptr, 0xff, 2 * sizeof(unsigned long long), st));
+  const int64_t work = std::max<int64_t>(n, (int64_t)p->k * p->d);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 2048));
+  hipLaunchKernelGGL(k_require_norms, dim3(grid), dim3(256), 0, st, C, p->k, p->d, xnorm, n,
+                     (unsigned long long*)p->req.ptr);
+  CYC_LAUNCH_CHECK("k_require_norms");
+  CYC_HIP(hipMemcpyAsync(p->reqHost, p->req.ptr, 5 * sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, st));
+  CYC_HIP(hipEventRecord(p->reqEv, st));
+  return CYC_OK;
+}
+
+// The IllegalArgumentException the reference raises first, if any:
+// computeStatistics' pair loop (i < j, DistanceMeasure.scala:55-66) meets
+// (0, m) for the lowest NaN center m > 0, or (0, 1) when center 0 is NaN;
+// with k == 1 there are no statistics and the first point meets center 0;
+// otherwise the first NaN-norm point meets center 0 (norm2 = NaN).
+int require_check(cyc_kmeans_plan p, int64_t n) {
+  CYC_HIP(hipEventSynchronize(p->reqEv));
+  const unsigned long long cbad = p->reqHost[0], rbad = p->reqHost[1];
+  const double* v = reinterpret_cast<const double*>(p->reqHost + 2);
+  const double nan = __builtin_nan("");
+  auto fail = [](double n1, double n2) {
+    cyc::set_error("requirement failed: Both norms should be greater or equal to 0.0, found "
+                   "norm1=" + cyc::java_double(n1) + ", norm2=" + cyc::java_double(n2));
+    return CYC_ERR_INVALID_ARG;
+  };
+  if (p->k >= 2 && cbad < (unsigned long long)p->k) return cbad == 0 ? fail(nan, v[1]) : fail(v[0], nan);
+  if (n > 0 && cbad == 0) return fail(nan, v[2]);
+  if (rbad < (unsigned long long)n) return fail(v[0], nan);
+  return CYC_OK;
+}
+
 int ensure_rows(cyc_kmeans_plan p, int64_t n) {
   if (n <= p->max_rows && p->slowList.ptr) return CYC_OK;
   int rc;
@@ -2007,12 +2085,13 @@ int cyc_kmeans_stats_dev(cyc_kmeans_plan p, const double* C, double* stats_out, 
   CYC_REQUIRE(p != nullptr && C != nullptr, "plan and centers must not be null");
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
-  int rc = do_stats(p, C, st);
+  int rc = require_enqueue(p, C, nullptr, 0, st);
   if (rc) return rc;
+  if ((rc = do_stats(p, C, st))) return rc;
   if (stats_out)
     CYC_HIP(hipMemcpyAsync(stats_out, p->stats.ptr, sizeof(double) * ((size_t)p->k * (p->k + 1) / 2),
                            hipMemcpyDeviceToDevice, st));
-  return CYC_OK;
+  return require_check(p, 0);
 }
 
 int cyc_kmeans_rows_create(cyc_kmeans_plan p, const double* X, int64_t n, void* stream,
@@ -2073,11 +2152,12 @@ int cyc_kmeans_assign_dev(cyc_kmeans_plan p, const double* X, const double* xnor
   hipStream_t st = cyc::as_stream(stream);
   int rc = ensure_rows(p, n);
   if (rc) return rc;
+  if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
   if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, n_exact_out, st))) return rc;
   hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n, p->d, C,
                      (const int32_t*)assign, cost);
   CYC_LAUNCH_CHECK("k_row_cost");
-  return CYC_OK;
+  return require_check(p, n);
 }
 
 int cyc_kmeans_point_cost_dev(cyc_kmeans_plan p, const double* X, const double* xnorm,
@@ -2135,6 +2215,7 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
     if ((rc = p->assignTmp.reserve(sizeof(int32_t) * (size_t)n))) return rc;
     assign = (int32_t*)p->assignTmp.ptr;
   }
+  if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
   if ((rc = do_stats(p, C, st))) return rc;
   if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st))) return rc;
   // d > 1024: per-row costs first (k_chunk_sums fuses them for d <= 1024)
@@ -2222,7 +2303,7 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   hipLaunchKernelGGL(k_cost_total, dim3(1), dim3(256), 0, st, (const double*)p->ccost.ptr, k,
                      cost_sum);
   CYC_LAUNCH_CHECK("k_cost_total");
-  return CYC_OK;
+  return require_check(p, n);
 }
 
 int cyc_kmeans_update_dev(cyc_kmeans_plan p, double* C, double* cnorm, const double* sums,
@@ -2274,8 +2355,12 @@ int cyc_kmeans_assign_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr, const in
   CYC_REQUIRE(assign != nullptr && cost != nullptr, "assign and cost must not be null");
   if (n == 0) return CYC_OK;
   std::lock_guard<std::mutex> g(p->mu);
-  return sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost,
-                       cyc::as_stream(stream));
+  hipStream_t st = cyc::as_stream(stream);
+  int rc;
+  if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
+  if ((rc = sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost, st)))
+    return rc;
+  return require_check(p, n);
 }
 
 int cyc_kmeans_point_cost_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
@@ -2311,6 +2396,7 @@ int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
     if ((rc = p->costTmp.reserve(sizeof(double) * (size_t)n))) return rc;
     cost = (double*)p->costTmp.ptr;
   }
+  if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
   if ((rc = do_stats(p, C, st))) return rc;
   if ((rc = sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost, st)))
     return rc;
@@ -2318,7 +2404,7 @@ int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
   hipLaunchKernelGGL(k_sparse_sums, dim3(grid), dim3(256), 0, st, rowptr, colidx, vals, weights, n,
                      p->d, (const int32_t*)assign, (const double*)cost, sums, wsum, cost_sum);
   CYC_LAUNCH_CHECK("k_sparse_sums");
-  return CYC_OK;
+  return require_check(p, n);
 }
 
 }  // extern "C"

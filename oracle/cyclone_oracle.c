@@ -110,6 +110,29 @@ double orc_fast_sqdist_dense_sparse(const double* v1, double norm1,
   return sqDist;
 }
 
+/* MLUtils.scala:542-543, the second require of fastSquaredDistance:
+ *   require(norm1 >= 0.0 && norm2 >= 0.0, s"Both norms should be greater or
+ *   equal to 0.0, found norm1=$norm1, norm2=$norm2")
+ * An IllegalArgumentException ends the Spark task, so the first failure is
+ * recorded (thread-local, per partition thread) and the loops below stop;
+ * the Python wrapper rethrows it with the reference's text.               */
+static _Thread_local int g_req_failed = 0;
+static _Thread_local double g_req_n1, g_req_n2;
+
+static int orc_require_norms(double norm1, double norm2) {
+  if (norm1 >= 0.0 && norm2 >= 0.0) return 1;
+  if (!g_req_failed) { g_req_failed = 1; g_req_n1 = norm1; g_req_n2 = norm2; }
+  return 0;
+}
+
+/* 1 (and the two norms) if a require failed since the last call; clears it */
+int orc_take_require_failure(double* norm1, double* norm2) {
+  int f = g_req_failed;
+  if (f) { *norm1 = g_req_n1; *norm2 = g_req_n2; }
+  g_req_failed = 0;
+  return f;
+}
+
 /* ml/impl/Utils.scala:70-80 indexUpperTriangular */
 static inline int64_t orc_iut(int64_t i, int64_t j) {
   return (i <= j) ? j * (j + 1) / 2 + i : i * (i + 1) / 2 + j;
@@ -125,9 +148,12 @@ static inline int64_t orc_iut(int64_t i, int64_t j) {
 void orc_kmeans_stats(const double* C, int64_t k, int64_t d, double* packed) {
   if (k == 1) { packed[0] = NAN; return; }
   double* diag = (double*)malloc(sizeof(double) * k);
+  double* norms = (double*)malloc(sizeof(double) * k);   /* VectorWithNorm.norm */
+  for (int64_t i = 0; i < k; ++i) norms[i] = orc_norm2(C + i * d, d);
   for (int64_t i = 0; i < k; ++i) diag[i] = INFINITY;
   for (int64_t i = 0; i < k; ++i) {
     for (int64_t j = i + 1; j < k; ++j) {
+      if (!orc_require_norms(norms[i], norms[j])) { free(diag); free(norms); return; }
       double dist = sqrt(orc_sqdist(C + i * d, C + j * d, d));
       double s = 0.25 * dist * dist;
       packed[orc_iut(i, j)] = s;
@@ -137,6 +163,7 @@ void orc_kmeans_stats(const double* C, int64_t k, int64_t d, double* packed) {
   }
   for (int64_t i = 0; i < k; ++i) packed[orc_iut(i, i)] = diag[i];
   free(diag);
+  free(norms);
 }
 
 /* DistanceMeasure.scala:282-313 EuclideanDistanceMeasure.findClosest with
@@ -144,6 +171,9 @@ void orc_kmeans_stats(const double* C, int64_t k, int64_t d, double* packed) {
 void orc_find_closest_stats(const double* C, const double* cnorm, int64_t k, int64_t d,
                             const double* stats, const double* x, double xnorm,
                             int32_t* out_idx, double* out_dist) {
+  *out_idx = -1;
+  *out_dist = NAN;
+  if (!orc_require_norms(cnorm[0], xnorm)) return;
   double best = orc_sqdist(C, x, d);
   if (best < stats[0]) { *out_idx = 0; *out_dist = best; return; }
   int64_t bestIndex = 0;
@@ -152,6 +182,7 @@ void orc_find_closest_stats(const double* C, const double* cnorm, int64_t k, int
     double lowerBound = normDiff * normDiff;
     if (lowerBound < best) {
       if (stats[orc_iut(i, bestIndex)] < best) {
+        if (!orc_require_norms(cnorm[i], xnorm)) return;
         double dd = orc_sqdist(C + i * d, x, d);
         if (dd < stats[orc_iut(i, i)]) { *out_idx = (int32_t)i; *out_dist = dd; return; }
         if (dd < best) { best = dd; bestIndex = i; }
@@ -171,6 +202,8 @@ void orc_find_closest(const double* C, const double* cnorm, int64_t k, int64_t d
     double lb = cnorm[i] - xnorm;
     lb = lb * lb;
     if (lb < best) {
+      /* a NaN norm never passes lb < best: this require cannot fail here */
+      if (!orc_require_norms(cnorm[i], xnorm)) { *out_idx = -1; *out_dist = NAN; return; }
       double dd = orc_sqdist(C + i * d, x, d);
       if (dd < best) { best = dd; bestIndex = i; }
     }
@@ -184,6 +217,9 @@ void orc_find_closest(const double* C, const double* cnorm, int64_t k, int64_t d
 void orc_find_closest_stats_sparse(const double* C, const double* cnorm, int64_t k, int64_t d,
                                    const double* stats, const int32_t* idx, const double* val,
                                    int64_t nnz, double xnorm, int32_t* out_idx, double* out_dist) {
+  *out_idx = -1;
+  *out_dist = NAN;
+  if (!orc_require_norms(cnorm[0], xnorm)) return;
   double best = orc_fast_sqdist_dense_sparse(C, cnorm[0], idx, val, nnz, xnorm, d);
   if (best < stats[0]) { *out_idx = 0; *out_dist = best; return; }
   int64_t bestIndex = 0;
@@ -192,6 +228,7 @@ void orc_find_closest_stats_sparse(const double* C, const double* cnorm, int64_t
     double lowerBound = normDiff * normDiff;
     if (lowerBound < best) {
       if (stats[orc_iut(i, bestIndex)] < best) {
+        if (!orc_require_norms(cnorm[i], xnorm)) return;
         double dd = orc_fast_sqdist_dense_sparse(C + i * d, cnorm[i], idx, val, nnz, xnorm, d);
         if (dd < stats[orc_iut(i, i)]) { *out_idx = (int32_t)i; *out_dist = dd; return; }
         if (dd < best) { best = dd; bestIndex = i; }
@@ -213,6 +250,7 @@ void orc_find_closest_sparse(const double* C, const double* cnorm, int64_t k, in
     double lb = cnorm[i] - xnorm;
     lb = lb * lb;
     if (lb < best) {
+      if (!orc_require_norms(cnorm[i], xnorm)) { *out_idx = -1; *out_dist = NAN; return; }
       double dd = orc_fast_sqdist_dense_sparse(C + i * d, cnorm[i], idx, val, nnz, xnorm, d);
       if (dd < best) { best = dd; bestIndex = i; }
     }
@@ -266,6 +304,7 @@ void orc_kmeans_partition(const double* X, const double* xnorm, const double* w,
   for (int64_t r = 0; r < n; ++r) {
     int32_t bi; double bd;
     orc_find_closest_stats(C, cnorm, k, d, stats, X + r * d, xnorm[r], &bi, &bd);
+    if (bi < 0) break;                     /* require failed: the task throws */
     double wt = w ? w[r] : 1.0;
     if (assign) assign[r] = bi;
     if (dist) dist[r] = bd;
@@ -951,6 +990,7 @@ void orc_kmeans_partition_sparse(const int64_t* rowptr, const int32_t* colidx,
     double bd;
     orc_find_closest_stats_sparse(C, cnorm, k, d, stats, colidx + q0, vals + q0, nnz, xnorm[r],
                                   &bi, &bd);
+    if (bi < 0) break;                     /* require failed: the task throws */
     const double wt = w ? w[r] : 1.0;
     *cost += bd * wt;
     double* y = sums + (int64_t)bi * d;

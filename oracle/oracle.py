@@ -47,6 +47,7 @@ def lib():
                 "orc_norm2": (ctypes.c_double, [_D, _i64]),
                 "orc_sqdist": (ctypes.c_double, [_D, _D, _i64]),
                 "orc_kmeans_stats": (None, [_D, _i64, _i64, _D]),
+                "orc_take_require_failure": (ctypes.c_int, [_D, _D]),
                 "orc_find_closest_stats": (None, [_D, _D, _i64, _i64, _D, _D, ctypes.c_double,
                                                   _I32, _D]),
                 "orc_find_closest": (None, [_D, _D, _i64, _i64, _D, ctypes.c_double, _I32, _D]),
@@ -107,6 +108,48 @@ def lib():
     return _lib
 
 
+class IllegalArgumentException(ValueError):
+    """A Scala `require` failed (the restatement's IllegalArgumentException)."""
+
+
+def java_double(x: float) -> str:
+    """java.lang.Double.toString: shortest round-trip digits, plain decimal
+    for 1e-3 <= |x| < 1e7 ("1.0", "0.001"), else "d.dddE<n>" ("1.0E7")."""
+    x = float(x)
+    if x != x:
+        return "NaN"
+    if x in (float("inf"), float("-inf")):
+        return "Infinity" if x > 0 else "-Infinity"
+    if x == 0.0:
+        return "-0.0" if np.signbit(x) else "0.0"
+    r = repr(abs(x))                       # shortest round-trip digits
+    mant, _, exp = r.partition("e")
+    ip, _, fp = mant.partition(".")
+    digits = (ip + fp).lstrip("0")
+    e10 = (int(exp) if exp else 0) + len(ip.lstrip("0")) - 1 if ip.strip("0") else \
+        (int(exp) if exp else 0) - (len(fp) - len(fp.lstrip("0"))) - 1
+    digits = digits.rstrip("0") or "0"
+    sign = "-" if x < 0 else ""
+    if 1e-3 <= abs(x) < 1e7:
+        if e10 >= 0:
+            ipart = digits[:e10 + 1].ljust(e10 + 1, "0")
+            fpart = digits[e10 + 1:] or "0"
+        else:
+            ipart, fpart = "0", "0" * (-e10 - 1) + digits
+        return f"{sign}{ipart}.{fpart}"
+    return f"{sign}{digits[0]}.{digits[1:] or '0'}E{e10}"
+
+
+def _raise_require():
+    """Rethrow a failed MLUtils.fastSquaredDistance require (MLUtils.scala:
+    542-543) recorded by the restatement on this thread."""
+    n1, n2 = ctypes.c_double(), ctypes.c_double()
+    if lib().orc_take_require_failure(ctypes.byref(n1), ctypes.byref(n2)):
+        raise IllegalArgumentException(
+            "requirement failed: Both norms should be greater or equal to 0.0, found "
+            f"norm1={java_double(n1.value)}, norm2={java_double(n2.value)}")
+
+
 def _p(a, ty=_D):
     if a is None:
         return None
@@ -144,6 +187,7 @@ def kmeans_stats(C) -> np.ndarray:
     k, d = C.shape
     out = np.empty(k * (k + 1) // 2, dtype=np.float64)
     lib().orc_kmeans_stats(_p(C), k, d, _p(out))
+    _raise_require()
     return out
 
 
@@ -154,6 +198,7 @@ def find_closest_stats(C, cnorm, stats, x, xnorm):
     dist = ctypes.c_double()
     lib().orc_find_closest_stats(_p(C), _p(cnorm), C.shape[0], C.shape[1], _p(stats), _p(x),
                                  float(xnorm), ctypes.byref(idx), ctypes.byref(dist))
+    _raise_require()
     return idx.value, dist.value
 
 
@@ -204,6 +249,7 @@ def find_closest_stats_sparse(C, cnorm, stats, idx, val, xnorm):
     lib().orc_find_closest_stats_sparse(_p(C), _p(cnorm), C.shape[0], C.shape[1], _p(stats),
                                         _p(idx, _I32), _p(val), idx.size, float(xnorm),
                                         ctypes.byref(oi), ctypes.byref(od))
+    _raise_require()
     return oi.value, od.value
 
 
@@ -223,6 +269,7 @@ def kmeans_partition(X, xnorm, w, C, cnorm, stats, want_assign=True):
     lib().orc_kmeans_partition(_p(X), _p(xnorm), _p(w), n, d, _p(C), _p(cnorm), _p(stats), k,
                                _p(assign, _I32), _p(dist), _p(sums), _p(wsum),
                                ctypes.byref(cost))
+    _raise_require()
     return assign, dist, sums, wsum, cost.value
 
 
@@ -253,6 +300,7 @@ def kmeans_partition_sparse(csr, xnorm, w, C, cnorm, stats):
                                       _p(None if w is None else _f64(w)), n, d, _p(C),
                                       _p(_f64(cnorm)), _p(_f64(stats)), k, _p(a, _I32), _p(dist),
                                       _p(sums), _p(wsum), _p(cost))
+    _raise_require()
     return a, dist, sums.reshape(k, d), wsum, cost[0]
 
 

@@ -127,16 +127,103 @@ def test_assign_ties_and_duplicates(cuda):
 
 
 def test_assign_nonfinite(cuda):
+    """+Inf norms pass the require (Inf >= 0.0) and rows with them keep the
+    reference's index / cost; 1e200 rows overflow sqdist to +Inf."""
     rng = np.random.default_rng(3)
     X = rng.normal(size=(200, 16))
-    X[5, 3] = np.nan
     X[7, 0] = np.inf
+    X[8, 3] = -np.inf
     X[9, :] = 1e200
     C = rng.normal(size=(9, 16))
     a, c, n_exact, *_ = _gpu_assign(X, C, cuda)
     ra, rc = _oracle_assign(X, C)
     np.testing.assert_array_equal(a, ra)
-    np.testing.assert_array_equal(c, rc)   # NaN == NaN under assert_array_equal
+    np.testing.assert_array_equal(c, rc)
+
+
+def _require_message(fn):
+    with pytest.raises(oracle.IllegalArgumentException) as e:
+        fn()
+    return str(e.value)
+
+
+@pytest.mark.parametrize("case", ["row", "rows", "center0", "center_m", "k1_center", "csr"])
+@pytest.mark.parametrize("path", ["assign", "accumulate"])
+def test_nan_norm_require(cuda, case, path):
+    """MLUtils.fastSquaredDistance's require(norm1 >= 0.0 && norm2 >= 0.0)
+    (MLUtils.scala:542-543) on the with-statistics paths: a NaN-norm point
+    fails at (center 0, point) (DistanceMeasure.scala:286), a NaN center
+    fails computeStatistics' pair loop (:55-66).  The device returns
+    CYC_ERR_INVALID_ARG with the restatement's exact message (Java
+    Double.toString of the norms)."""
+    import torch
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.clustering import KMeansPlan, row_norms, row_norms_csr
+    rng = np.random.default_rng(5)
+    n, d, k = 300, 24, 1 if case == "k1_center" else 7
+    X = rng.normal(size=(n, d)) * 3.0
+    C = rng.normal(size=(k, d))
+    if case == "row":
+        X[117, 4] = np.nan
+    elif case == "rows":
+        X[[250, 33, 180], [0, 5, 23]] = np.nan
+        X[10, 2] = np.inf                   # +Inf norm passes the require
+    elif case == "center0":
+        C[0, 3] = np.nan
+    elif case in ("center_m", "k1_center"):
+        C[k - 1 if case == "center_m" else 0, 1] = np.nan
+        if case == "center_m":
+            C[k - 3, 0] = np.nan            # the lowest NaN center is reported
+    if case == "csr":
+        X[X < 1.0] = 0.0                    # sparse rows
+        X[41, 7] = np.nan
+    xn, cn = oracle.row_norms(X), oracle.row_norms(C)
+    if case == "csr":
+        rowptr = np.concatenate([[0], np.cumsum((X != 0).sum(1))]).astype(np.int64)
+        nz = np.nonzero(X != 0)
+        colidx, vals = nz[1].astype(np.int32), X[nz]
+        xn = oracle.row_norms_csr(rowptr, vals)
+        want = _require_message(lambda: oracle.kmeans_partition_sparse(
+            (rowptr, colidx, vals), xn, None, C, cn, oracle.kmeans_stats(C)))
+    else:
+        want = _require_message(lambda: oracle.kmeans_iteration(X, xn, None, C, cn))
+    assert want.startswith("requirement failed: Both norms should be greater or equal to 0.0")
+    Cd = _dev(C, cuda)
+    cnd = row_norms(Cd)
+    plan = KMeansPlan(d, k, n)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    c = torch.empty(n, dtype=torch.float64, device=cuda)
+    sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+    wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+    cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+    with pytest.raises(N.IllegalArgumentException) as got:
+        if case == "csr":
+            R, I, V = _dev(rowptr, cuda), _dev(colidx, cuda), _dev(vals, cuda)
+            xnd = row_norms_csr(R, V)
+            if path == "assign":
+                try:
+                    plan.stats(Cd)
+                except N.IllegalArgumentException:
+                    raise AssertionError("centers are finite")
+                plan.assign_csr(R, I, V, xnd, Cd, cnd, a, c)
+            else:
+                plan.accumulate_csr(R, I, V, xnd, None, Cd, cnd, sums, wsum, cost)
+        else:
+            Xd = _dev(X, cuda)
+            xnd = row_norms(Xd)
+            if path == "assign":
+                plan.stats(Cd)            # NaN centers fail here (computeStatistics)
+                plan.assign(Xd, xnd, Cd, cnd, a, c, rows=plan.rows(Xd))
+            else:
+                plan.accumulate(Xd, xnd, None, Cd, cnd, sums, wsum, cost, rows=plan.rows(Xd))
+    assert str(got.value) == want
+    # the plan stays usable after the failure
+    Xf = np.nan_to_num(X, nan=0.5)
+    Cf = np.nan_to_num(C, nan=0.25)
+    af, cf, *_ = _gpu_assign(Xf, Cf, cuda)
+    ra, rc = _oracle_assign(Xf, Cf)
+    np.testing.assert_array_equal(af, ra)
+    np.testing.assert_array_equal(cf, rc)
 
 
 @pytest.mark.parametrize("use_rows", [False, True])
@@ -195,10 +282,15 @@ def test_weighted_centers_exact(cuda):
         assert got == expect
 
 
-def test_full_config_properties(cuda):
-    """BASELINE config 2 shape (10M x 256, k=1024): size-independent checks --
-    a sampled subset of rows equals the restatement bit for bit, weights sum
-    to n, and sum of cluster sums equals the column sums of X."""
+@pytest.mark.timeout(900)
+def test_full_config_all_rows(cuda):
+    """BASELINE config 2 at full size (10M x 256, k=1024, the bench's data and
+    initial centers): EVERY row's assignment and cost equals the restatement
+    bit for bit (oracle run as 16 row partitions on the host's threads, about
+    a minute), the cluster sums / weights / cost agree with the restatement's
+    partition-ordered merge to 1e-10, and the size-independent identities hold
+    (weights sum to n, cluster sums add up to the column sums of X)."""
+    import os
     import torch
     from cycloneml_amd.clustering import row_norms
     n, d, k = 10_000_000, 256, 1024
@@ -225,15 +317,22 @@ def test_full_config_properties(cuda):
     np.testing.assert_allclose(sums.view(k, d).sum(0).cpu().numpy(), colsum.cpu().numpy(),
                                rtol=1e-9, atol=1e-6)
     assert abs(cost.item() - pc.sum().item()) <= 1e-10 * cost.item()
-    rows = np.random.default_rng(0).choice(n, 300, replace=False)
+    # every row against the restatement (Spark local[16]: 16 partitions)
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or 16, os.cpu_count() or 1, 16)
+    Xh = X.cpu().numpy()
+    del X
+    xnh = xn.cpu().numpy()
+    np.testing.assert_array_equal(xnh[:1000], oracle.row_norms(Xh[:1000]))
     Ch = C.cpu().numpy()
-    chn = oracle.row_norms(Ch)
-    stats = oracle.kmeans_stats(Ch)
-    Xs = X[torch.from_numpy(rows).to(cuda)].cpu().numpy()
-    ah, ch = a.cpu().numpy()[rows], pc.cpu().numpy()[rows]
-    for i in range(len(rows)):
-        idx, dist = oracle.find_closest_stats(Ch, chn, stats, Xs[i], oracle.norm2(Xs[i]))
-        assert (idx, dist) == (int(ah[i]), float(ch[i]))
+    ref = oracle.kmeans_iteration(Xh, xnh, None, Ch, oracle.row_norms(Ch),
+                                  num_partitions=threads, threads=threads)
+    ah, ch = a.cpu().numpy(), pc.cpu().numpy()
+    bad = np.flatnonzero((ah != ref["assign"]) | (ch != ref["dist"]))
+    assert bad.size == 0, f"{bad.size} rows differ, first {bad[:10]}"
+    np.testing.assert_array_equal(wsum.cpu().numpy(), ref["wsum"])
+    np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
+                               atol=1e-10 * np.abs(ref["sums"]).max())
+    assert abs(cost.item() - ref["cost"]) <= 1e-10 * ref["cost"]
 
 
 def _assign_variant(X, C, cuda, variant, monkeypatch, use_rows=False):
@@ -280,7 +379,7 @@ def test_bf16_screen_matches_fp64_screen(cuda, monkeypatch, n, d, k):
 
 def test_bf16_screen_hard_cases(cuda, monkeypatch):
     """Near ties, duplicate centers, huge rows (> 2^56), tiny-scale rows and
-    NaN / Inf rows fall through the bf16 screen to the fp64 screen / exact
+    Inf rows fall through the bf16 screen to the fp64 screen / exact
     loop and still match the reference."""
     rng = np.random.default_rng(17)
     d, k = 64, 20
@@ -293,7 +392,7 @@ def test_bf16_screen_hard_cases(cuda, monkeypatch):
         C[rng.integers(0, k, 30)] * 1e-30,                # bf16 underflow scale
         C[:5] + 1e-14,
     ])
-    X[805, 2] = np.nan
+    X[805, 2] = np.inf                    # (NaN rows fail the require: test_nan_norm_require)
     X[806, 0] = -np.inf
     a3, c3, t2, ex = _assign_variant(X, C, cuda, 3, monkeypatch)
     ra, rc = _oracle_assign(X, C)
@@ -354,7 +453,7 @@ def test_i8_screen_near_ties_and_dense_clusters(cuda, monkeypatch):
 
 def test_i8_screen_hard_cases(cuda, monkeypatch):
     """Near ties, duplicate centers, huge rows (> 2^50), tiny-scale rows,
-    all-zero rows and NaN / Inf rows fall through the i8 screen to the fp64
+    all-zero rows and Inf rows fall through the i8 screen to the fp64
     screen / exact loop and still match the reference."""
     rng = np.random.default_rng(29)
     d, k = 64, 20
@@ -368,7 +467,7 @@ def test_i8_screen_hard_cases(cuda, monkeypatch):
         np.zeros((5, d)),
         C[:5] + 1e-14,
     ])
-    X[805, 2] = np.nan
+    X[805, 2] = np.inf                    # (NaN rows fail the require: test_nan_norm_require)
     X[806, 0] = -np.inf
     a8, c8, t2, ex = _assign_variant(X, C, cuda, 2, monkeypatch, use_rows=True)
     ra, rc = _oracle_assign(X, C)

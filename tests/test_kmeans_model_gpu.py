@@ -49,7 +49,11 @@ def test_dense_point_cost_and_predict_bit_exact(cuda, n, d, k):
         C[3] = C[1]                          # duplicate centers: ties -> exact tier
         X[:20] = C[2]                        # rows sitting on a center
         X[20:40] = 0.5 * (C[0] + C[4])       # near-equidistant rows
-    X[40, 0] = np.nan                        # no center reaches: cost +inf, index 0
+    # NaN norm: findClosest WITHOUT statistics never calls fastSquaredDistance
+    # (every `lowerBoundOfSqDist < bestDistance` is false, :327-329), so
+    # pointCost is +inf at index 0 and no require fails; predict (WITH
+    # statistics) measures center 0 first and fails MLUtils.scala:542-543
+    X[40, 0] = np.nan
     X[41, 1] = np.inf
     xn, cn = oracle.row_norms(X), oracle.row_norms(C)
     a, c, s = oracle.point_costs(X, xn, C, cn)
@@ -59,9 +63,17 @@ def test_dense_point_cost_and_predict_bit_exact(cuda, n, d, k):
     assert np.array_equal(gc.cpu().numpy(), c, equal_nan=True)
     assert np.isinf(gc[40].item()) and np.isinf(gc[41].item())
     # predict: findClosest with the model's statistics (a1)
+    from cycloneml_amd import _native as N
     stats = oracle.kmeans_stats(C)
-    want = np.array([oracle.find_closest_stats(C, cn, stats, X[r], xn[r])[0] for r in range(n)])
-    assert np.array_equal(m.predict(_dev(X, cuda)).cpu().numpy(), want)
+    with pytest.raises(oracle.IllegalArgumentException) as want_err:
+        oracle.find_closest_stats(C, cn, stats, X[40], xn[40])
+    with pytest.raises(N.IllegalArgumentException) as got_err:
+        m.predict(_dev(X, cuda))
+    assert str(got_err.value) == str(want_err.value)
+    keep = np.arange(n) != 40
+    want = np.array([oracle.find_closest_stats(C, cn, stats, X[r], xn[r])[0]
+                     for r in range(n) if keep[r]])
+    assert np.array_equal(m.predict(_dev(X[keep], cuda)).cpu().numpy(), want)
     fin = np.isfinite(c)
     mf = _model(C)
     got = mf.computeCost(_dev(X[fin], cuda))

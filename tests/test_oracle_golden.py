@@ -446,3 +446,36 @@ def test_aft_aggregator_vs_naive_loop(fit_intercept):
             assert st["weight"] == len(inst)
             assert abs(st["loss"] - loss) <= 1e-9 * abs(loss)
             np.testing.assert_allclose(st["grad"], g, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("x,s", [
+    (1.0, "1.0"), (0.001, "0.001"), (1e-4, "1.0E-4"), (1e7, "1.0E7"), (9999999.0, "9999999.0"),
+    (123.456, "123.456"), (-2.5e-4, "-2.5E-4"), (1.7976931348623157e308, "1.7976931348623157E308"),
+    (float("nan"), "NaN"), (float("inf"), "Infinity"), (-0.0, "-0.0"), (0.1, "0.1"),
+    (100.0, "100.0"), (1234567.0, "1234567.0"), (12345678.9, "1.23456789E7"),
+    (0.3333333333333333, "0.3333333333333333"), (2.0 ** 0.5, "1.4142135623730951")])
+def test_java_double_to_string(x, s):
+    """java.lang.Double.toString, which Scala's s"$norm" interpolation uses in
+    MLUtils.scala:542-543's require message."""
+    assert oracle.java_double(x) == s
+
+
+def test_fast_squared_distance_require():
+    """MLUtils.scala:542-543: require(norm1 >= 0.0 && norm2 >= 0.0).  With
+    statistics (Lloyd, predict) a NaN-norm point fails at center 0 and a NaN
+    center fails computeStatistics; without statistics (pointCost) no
+    distance with a NaN norm is ever measured, so nothing fails."""
+    rng = np.random.default_rng(2)
+    X = rng.normal(size=(50, 6))
+    C = rng.normal(size=(4, 6))
+    X[20, 1] = np.nan
+    xn, cn = oracle.row_norms(X), oracle.row_norms(C)
+    with pytest.raises(oracle.IllegalArgumentException) as e:
+        oracle.kmeans_iteration(X, xn, None, C, cn)
+    assert str(e.value) == ("requirement failed: Both norms should be greater or equal to 0.0, "
+                            f"found norm1={oracle.java_double(cn[0])}, norm2=NaN")
+    a, c, _ = oracle.point_costs(X, xn, C, cn)
+    assert a[20] == 0 and c[20] == np.inf
+    C[2, 0] = np.nan
+    with pytest.raises(oracle.IllegalArgumentException, match="norm1=.*, norm2=NaN"):
+        oracle.kmeans_stats(C)
