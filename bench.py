@@ -403,14 +403,34 @@ WORKLOADS = {"kmeans": KMeansWorkload, "gramian": GramianWorkload, "lr_multi": L
              "lr_sparse": LRSparseWorkload}
 
 
+def launch_ranks(args) -> int:
+    """`--gpus N` without a torch.distributed environment: start N fresh rank
+    processes (one per GPU) through torch.distributed.run as a CHILD process
+    -- this process has not touched the GPU -- and return its exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -420,6 +440,9 @@ def main():
     from cycloneml_amd import _native as N
     from cycloneml_amd import parallel
     N.load()
+    comm = parallel.init(dev)          # libcyclone's RCCL communicator (cyc_comm_*)
+    if comm is not None:
+        world = comm.world_size        # n_gpus as the live communicator reports it
     n = args.rows or DEFAULT_ROWS[args.workload]
     wl = WORKLOADS[args.workload](n, dev, rank)
 
@@ -493,6 +516,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if world > 1:
+        parallel.shutdown()
         dist.destroy_process_group()
 
 

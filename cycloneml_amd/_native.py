@@ -147,6 +147,17 @@ SIGNATURES = {
     "cyc_logreg_multinomial_eval": (ctypes.c_int, [_vp, _i32, _vp, ctypes.c_int, ctypes.c_int,
                                                    _vp, _vp, _vp, _vp]),
     "cyc_gramian": (ctypes.c_int, [_vp, _vp, _vp]),
+    # the aggregation step over RCCL (cyc_comm_*)
+    "cyc_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "cyc_comm_init": (ctypes.c_int, [ctypes.c_char_p, _i32, _i32, _i32, ctypes.POINTER(_vp)]),
+    "cyc_comm_destroy": (ctypes.c_int, [_vp]),
+    "cyc_comm_rank": (ctypes.c_int, [_vp, _pi32, _pi32]),
+    "cyc_allreduce_sum_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
+    "cyc_allreduce_max_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp]),
+    "cyc_broadcast_dev": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp]),
+    "cyc_allgather_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp]),
+    "cyc_allreduce_sum": (ctypes.c_int, [_vp, _vp, _i64]),
+    "cyc_broadcast": (ctypes.c_int, [_vp, _vp, _i64, _i32]),
     "cyc_col_sums": (ctypes.c_int, [_vp, _vp]),
 }
 

@@ -427,6 +427,41 @@ int cyc_aft_eval(cyc_dataset ds, const double* coef, int fitIntercept, const dou
 int cyc_gramian(cyc_dataset ds, const double* mean_opt, double* U);
 int cyc_col_sums(cyc_dataset ds, double* sums);
 
+/* ----------------------------------------- the aggregation step (RCCL) */
+/* One process per GPU, one communicator per process.
+ * Replaces RDD.treeAggregate (core/src/main/scala/org/apache/spark/rdd/
+ * RDD.scala:1210-1269: seqOp per partition, foldByKey tree levels
+ * :1244-1250, driver fold :1267), KMeans' reduceByKey + collectAsMap
+ * (mllib/clustering/KMeans.scala:308-311) and the DoubleAccumulator cost by
+ * ONE in-place fp64 sum of the flat aggregator state per iteration
+ * (gradient | loss | weight, sums | weights | cost, packed Gramian), and
+ * TorrentBroadcast of the model (SparkContext.scala:1524) by a broadcast.
+ * Rank 0 makes the id with cyc_comm_unique_id and ships the 128 bytes to
+ * every rank out of band (e.g. the Spark driver's broadcast); every rank then
+ * calls cyc_comm_init with the same id, world size and its own rank and
+ * device (collective: it returns once all ranks have joined; it sets the
+ * calling thread's current device).  The sum order across ranks is RCCL's
+ * (fixed for a topology), like Spark's completion-order fold it is not the
+ * 1-GPU order: results agree to ~1e-15 relative.
+ * _dev forms: device buffers, enqueued on `stream`.  Host forms: staged
+ * through the communicator's own device buffer and stream, synchronous. */
+#define CYC_COMM_ID_BYTES 128
+typedef struct cyc_comm_s* cyc_comm;
+int cyc_comm_unique_id(unsigned char* id /* CYC_COMM_ID_BYTES */);
+int cyc_comm_init(const unsigned char* id, int32_t rank, int32_t world, int32_t device,
+                  cyc_comm* out);
+int cyc_comm_destroy(cyc_comm comm);
+int cyc_comm_rank(cyc_comm comm, int32_t* rank, int32_t* world);
+int cyc_allreduce_sum_dev(cyc_comm comm, double* buf, int64_t count, void* stream);
+int cyc_allreduce_max_dev(cyc_comm comm, double* buf, int64_t count, void* stream);
+int cyc_broadcast_dev(cyc_comm comm, double* buf, int64_t count, int32_t root, void* stream);
+/* recv[r*count .. (r+1)*count) = rank r's send (the summarizer buffers,
+ * merged in rank order by cyc_summarizer_merge_dev) */
+int cyc_allgather_dev(cyc_comm comm, const double* send, double* recv, int64_t count,
+                      void* stream);
+int cyc_allreduce_sum(cyc_comm comm, double* host_buf, int64_t count);
+int cyc_broadcast(cyc_comm comm, double* host_buf, int64_t count, int32_t root);
+
 /* ------------------------------------------------------- LIBSVM input */
 /* MLUtils.loadLibSVMFile's parse (mllib/util/MLUtils.scala:91-151:
  * parseLibSVMFile, parseLibSVMRecord, computeNumFeatures) on the host, in

@@ -1,0 +1,205 @@
+"""GPU tests of the aggregation step.
+
+- libcyclone's C-ABI communicator over RCCL (cyc_comm_*, include/cyclone.h)
+  at world size 1 (the GPU box has one GPU; RCCL refuses two ranks on one
+  device): every entry point, device and host forms, and its argument checks.
+- two rank processes on the one GPU joined by a gloo group: each rank runs
+  the DEVICE kernels on its shard (KMeans accumulate, multinomial / sparse
+  binary logistic aggregators, Gramian), the partials meet in the all-reduce
+  (parallel.allreduce_) and the merged result must equal the single-process
+  restatement over all rows -- the path bench.py --gpus N runs with RCCL.
+"""
+import ctypes
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_comm_world_one(cuda):
+    import torch
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.parallel import Communicator
+    uid = Communicator.unique_id()
+    assert len(uid) == 128
+    comm = Communicator(uid, 0, 1, cuda.index or 0)
+    try:
+        rng = np.random.default_rng(0)
+        x = rng.normal(size=1001)
+        t = torch.from_numpy(x.copy()).to(cuda)
+        comm.allreduce_sum_(t)
+        comm.allreduce_max_(t)
+        comm.broadcast_(t, 0)
+        g = comm.allgather(t)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), x)
+        assert g.shape == (1, 1001) and np.array_equal(g[0].cpu().numpy(), x)
+        # host forms (the resident-dataset layer's outputs are host arrays)
+        L = N.load()
+        h = x.copy()
+        N.check(L.cyc_allreduce_sum(comm.handle, h.ctypes.data, h.size))
+        N.check(L.cyc_broadcast(comm.handle, h.ctypes.data, h.size, 0))
+        assert np.array_equal(h, x)
+        r, w = ctypes.c_int32(), ctypes.c_int32()
+        N.check(L.cyc_comm_rank(comm.handle, ctypes.byref(r), ctypes.byref(w)))
+        assert (r.value, w.value) == (0, 1)
+        with pytest.raises(N.IllegalArgumentException, match="count must be nonnegative"):
+            N.check(L.cyc_allreduce_sum_dev(comm.handle, N.ptr(t), -1, None))
+        with pytest.raises(N.IllegalArgumentException, match="root must be a rank"):
+            N.check(L.cyc_broadcast_dev(comm.handle, N.ptr(t), t.numel(), 1, None))
+        with pytest.raises(N.IllegalArgumentException, match="contiguous fp64"):
+            comm.allreduce_sum_(t.float())
+    finally:
+        comm.close()
+    with pytest.raises(N.IllegalArgumentException, match="rank must be in"):
+        Communicator(uid, 1, 1, 0)
+
+
+# ----------------------------------------------------- two ranks, one GPU
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, q):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, fn(rank, world)))
+    except Exception as e:  # surface failures to the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(fn, world=2):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = dict(q.get(timeout=150) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return out
+
+
+def _kmeans_rank(rank, world):
+    import torch
+    from cycloneml_amd import parallel
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(0)
+    n, d, k = 40_001, 64, 33
+    X = rng.normal(size=(n, d)) + rng.integers(0, 6, size=(n, 1)) * 3.0
+    C = X[:k].copy()
+    a, b = parallel.shard_bounds(n, rank, world)
+    Xd = torch.from_numpy(X[a:b].copy()).to(dev)
+    Cd = torch.from_numpy(C.copy() if rank == 0 else np.zeros_like(C)).to(dev)
+    parallel.broadcast_(Cd)                       # bcCenters
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    plan = KMeansPlan(d, k, b - a)
+    buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=dev)
+    sums, wsum, cost = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
+    asg = torch.empty(b - a, dtype=torch.int32, device=dev)
+    plan.accumulate(Xd, xn, None, Cd, cn, sums, wsum, cost, asg, rows=plan.rows(Xd))
+    parallel.allreduce_(buf)                      # reduceByKey + costAccum
+    conv = torch.zeros(1, dtype=torch.int32, device=dev)
+    plan.update(Cd, cn, sums, wsum, 1e-4, conv)
+    torch.cuda.synchronize()
+    ref = oracle.kmeans_iteration(X, oracle.row_norms(X), None, C, oracle.row_norms(C),
+                                  num_partitions=2)
+    return bool(np.array_equal(asg.cpu().numpy(), ref["assign"][a:b])
+                and np.array_equal(wsum.cpu().numpy(), ref["wsum"])
+                and np.allclose(Cd.cpu().numpy(), ref["centers"], rtol=1e-12, atol=1e-12)
+                and abs(cost.item() - ref["cost"]) <= 1e-12 * ref["cost"])
+
+
+def _lr_rank(rank, world):
+    import torch
+    from cycloneml_amd import parallel
+    from cycloneml_amd.optim import (BinaryLogisticBlockAggregator, DeviceInstanceBlock,
+                                     MultinomialLogisticBlockAggregator, RDDLossFunction)
+    rng = np.random.default_rng(1)
+    n, F, Cn = 3001, 40, 7
+    X = rng.normal(size=(n, F))
+    y = rng.integers(0, Cn, size=n).astype(float)
+    w = rng.uniform(0.5, 1.5, size=n)
+    coef = rng.normal(size=Cn * F + Cn) * 0.1
+    mean = rng.normal(size=F) * 0.1
+    a, b = parallel.shard_bounds(n, rank, world)
+    blk = DeviceInstanceBlock.from_numpy(y[a:b], w[a:b], X=X[a:b], device="cuda:0")
+    fn = RDDLossFunction([blk], lambda c: MultinomialLogisticBlockAggregator(
+        np.ones(F), mean, True, True, c, device="cuda:0"))
+    loss, grad = fn.calculate(coef)
+    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+    oracle.multinomial_logistic_add(dict(labels=y, weights=w, X=X), coef, Cn, True, True, mean,
+                                    st)
+    ok_m = (abs(loss - st["loss"] / st["weight"]) <= 1e-10 * abs(loss)
+            and np.allclose(grad, st["grad"] / st["weight"], rtol=1e-10, atol=1e-14))
+    # sparse binary with fitWithMean (per-row CSR, CSC gradient pass)
+    rows = [np.sort(rng.choice(F, size=rng.integers(1, 9), replace=False)) for _ in range(n)]
+    rowptr = np.concatenate([[0], np.cumsum([len(r) for r in rows])]).astype(np.int64)
+    colidx = np.concatenate(rows).astype(np.int32)
+    vals = rng.uniform(0.1, 2.0, size=colidx.size)
+    yb = (rng.uniform(size=n) < 0.4).astype(float)
+    cb = rng.normal(size=F + 1) * 0.2
+    lo, hi = rowptr[a], rowptr[b]
+    blk2 = DeviceInstanceBlock.from_numpy(yb[a:b], w[a:b],
+                                          csr=(rowptr[a:b + 1] - lo, colidx[lo:hi], vals[lo:hi]),
+                                          numFeatures=F, device="cuda:0")
+    blk2.prepare()
+    fn2 = RDDLossFunction([blk2], lambda c: BinaryLogisticBlockAggregator(
+        np.ones(F), mean, True, True, c, device="cuda:0"))
+    loss2, grad2 = fn2.calculate(cb)
+    st2 = dict(grad=np.zeros(F + 1), loss=0.0, weight=0.0)
+    oracle.binary_logistic_add(dict(labels=yb, weights=w, rowptr=rowptr, colidx=colidx,
+                                    values=vals, F=F), cb, True, True, mean, st2)
+    ok_b = (abs(loss2 - st2["loss"] / st2["weight"]) <= 1e-10 * abs(loss2)
+            and np.allclose(grad2, st2["grad"] / st2["weight"], rtol=1e-10, atol=1e-14))
+    return bool(ok_m and ok_b)
+
+
+def _gramian_rank(rank, world):
+    import torch
+    from cycloneml_amd import parallel
+    from cycloneml_amd.linalg import GramianPlan
+    rng = np.random.default_rng(2)
+    n, p = 5003, 96
+    X = rng.uniform(size=(n, p))
+    a, b = parallel.shard_bounds(n, rank, world)
+    U = torch.zeros(p * (p + 1) // 2, dtype=torch.float64, device="cuda:0")
+    GramianPlan(p).accumulate(torch.from_numpy(X[a:b].copy()).to("cuda:0"), U)
+    parallel.allreduce_(U)
+    return bool(np.allclose(U.cpu().numpy(), oracle.gramian_partition(X), rtol=1e-12))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("fn", [_kmeans_rank, _lr_rank, _gramian_rank])
+def test_two_ranks_device_kernels_meet_the_collective(fn):
+    out = _run(fn)
+    assert out == {0: True, 1: True}, out
