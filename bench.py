@@ -8,12 +8,14 @@ per-cluster sums/weights/cost, merge, centroid update).
 
 Other workloads (--workload), each one training iteration per step:
   gramian      RowMatrix.computeGramianMatrix pass (configs[2]; the 100M x 1024
-               matrix does not fit one GPU, so each GPU holds a 12.5M-row shard:
-               the 8-GPU split of the config)
+               matrix (819 GB) does not fit one GPU: each GPU holds the largest
+               resident shard, 30M rows = 246 GB)
   lr_multi     multinomial LR, 100 classes, 512 dense features (configs[3]);
-               one RDDLossFunction.calculate per step, 6.25M-row shard per GPU
+               one RDDLossFunction.calculate per step, the full 50M-row
+               config (205 GB) resident per GPU
   lr_sparse    binomial LR on CSR, 1M features, 64 nnz/row (configs[4]);
-               one RDDLossFunction.calculate per step, 25M-row shard per GPU
+               one RDDLossFunction.calculate per step, the full 200M-row
+               config resident per GPU in the tiles layout (157 GB)
 With --gpus N (one process per GPU via torch.distributed.run) every rank
 holds its own shard in HBM (weak scaling) and the merge is one RCCL
 all-reduce per iteration.
@@ -38,8 +40,8 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 (vector = matrix) spec, BASELINE.md sect
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 I8_PEAK_TOPS = 5000.0     # dense i8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md)
 
-DEFAULT_ROWS = {"kmeans": 10_000_000, "gramian": 12_500_000, "lr_multi": 6_250_000,
-                "lr_sparse": 25_000_000}
+DEFAULT_ROWS = {"kmeans": 10_000_000, "gramian": 30_000_000, "lr_multi": 50_000_000,
+                "lr_sparse": 200_000_000}
 
 
 def parse():
@@ -214,7 +216,7 @@ class GramianWorkload:
 
     def describe(self):
         return (f"RowMatrix.computeGramianMatrix pass, dense fp64 {self.n} x {self.p} rows per "
-                "GPU, U[0,1) (BASELINE configs[2], 8-GPU shard of 100M rows)")
+                "GPU, U[0,1) (BASELINE configs[2]; the largest resident shard of its 100M rows)")
 
     def cpu_baseline(self, seconds):
         import numpy as np
@@ -259,7 +261,16 @@ class LRMultiWorkload:
         self.block = DeviceInstanceBlock(y, None, X=X)
         import numpy as np
         self.coef = np.random.default_rng(3).normal(size=C * F + C) * 0.01
-        self.scaledMean = np.zeros(F)
+        # scaledMean = mean / std per feature of the shard (the Summarizer
+        # pre-pass of LogisticRegression.scala:511-516, :957-960), untimed
+        mean = torch.zeros(F, dtype=torch.float64, device=dev)
+        sq = torch.zeros(F, dtype=torch.float64, device=dev)
+        for s in range(0, n, 1 << 22):
+            mean += X[s:s + (1 << 22)].sum(0)
+            sq += (X[s:s + (1 << 22)] ** 2).sum(0)
+        mean /= n
+        std = (sq / n - mean ** 2).clamp_min(0).sqrt()
+        self.scaledMean = (mean / std).cpu().numpy()
         self.fn = RDDLossFunction([self.block], lambda c: MultinomialLogisticBlockAggregator(
             np.ones(F), self.scaledMean, True, True, c, device=dev))
 
@@ -272,7 +283,7 @@ class LRMultiWorkload:
     def describe(self):
         return (f"multinomial LR ({self.C} classes) RDDLossFunction.calculate, dense fp64 "
                 f"{self.n} x {self.F} rows per GPU, fitIntercept+standardization "
-                "(BASELINE configs[3], 8-GPU shard of 50M rows)")
+                "(BASELINE configs[3], the full 50M-row config per GPU)")
 
     def cpu_baseline(self, seconds):
         import numpy as np
@@ -305,47 +316,63 @@ class LRMultiWorkload:
 
 
 class LRSparseWorkload:
-    """Roofline on the margin pass (timed as k_binlog_csr; the slices'
-    k_binlog_csr_mult8 launches), whose read set is exactly SURVEY 8(d)'s
-    784 B/row; the gradient pass (k_binlog_csc_grad) is listed beside it."""
-    kernel = "k_binlog_csr"
-    kernels = ("k_binlog_csr", "k_binlog_csc_grad")
-    pmc_kernels = ("k_binlog_csr_mult8",)
+    """BASELINE configs[4] at full size on one GPU: 200M CSR rows x 1M
+    features, 64 nonzeros per row, fitIntercept => fitWithMean
+    (LogisticRegression.scala:950-954) with a scaledMean of the data's scale.
+    The shard lives only in the row-block x column-tile layout (tiles.hip):
+    it is generated on the device 512K rows at a time, appended, and each
+    CSR chunk freed (157 GB resident for 200M rows).  Roofline on the margin
+    pass (k_tiles_margin), whose HBM reads are SURVEY 8(d)'s 784 B/row; the
+    gradient pass (k_tiles_grad) is listed beside it."""
+    kernel = "k_tiles_margin"
+    kernels = ("k_tiles_margin", "k_tiles_grad")
+    pmc_kernels = ("k_tiles_margin",)
     bound = "hbm"
 
     def __init__(self, n, dev, rank):
+        import numpy as np
         import torch
         from cycloneml_amd.optim import (BinaryLogisticBlockAggregator, DeviceInstanceBlock,
-                                         RDDLossFunction)
+                                         RDDLossFunction, SparseTiles)
         self.n, self.F, self.k = n, 1_000_000, 64
         F, k = self.F, self.k
         g = torch.Generator(device=dev).manual_seed(2)
         w_true = torch.randn(F, generator=g, device=dev, dtype=torch.float64) * 0.5
         gr = torch.Generator(device=dev).manual_seed(900 + rank)
-        cols = torch.empty(n * k, dtype=torch.int32, device=dev)
-        vals = torch.empty(n * k, dtype=torch.float64, device=dev)
+        self.tiles = SparseTiles(F, n, n * k)
         y = torch.empty(n, dtype=torch.float64, device=dev)
-        step = 1 << 20
+        band = F // k
+        step = 64 * SparseTiles.ROW_BLOCK          # whole row blocks per append
+        self.sample = []                            # host copy of the first rows (CPU leg)
+        sample_rows = min(n, 4 * step)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         for s in range(0, n, step):
             e = min(n, s + step)
             # 64 distinct sorted columns per row: one per 1/64 band + offset
-            band = F // k
             c = (torch.arange(k, device=dev) * band).unsqueeze(0) + \
                 torch.randint(0, band, (e - s, k), generator=gr, device=dev)
-            cols[s * k:e * k] = c.to(torch.int32).reshape(-1)
             v = torch.rand(e - s, k, generator=gr, device=dev, dtype=torch.float64)
-            vals[s * k:e * k] = v.reshape(-1)
             m = (v * w_true[c]).sum(1)
             y[s:e] = (torch.rand(e - s, generator=gr, device=dev, dtype=torch.float64)
                       < torch.sigmoid(m)).to(torch.float64)
-        rowptr = torch.arange(0, n * k + 1, k, dtype=torch.int64, device=dev)
-        self.block = DeviceInstanceBlock(y, None, rowptr=rowptr, colidx=cols, values=vals,
-                                         numFeatures=F)
-        self.block.prepare()      # one-time CSC copy (untimed, like blokify)
-        import numpy as np
+            cols = c.to(torch.int32).reshape(-1)
+            vals = v.reshape(-1)
+            rowptr = torch.arange(0, (e - s) * k + 1, k, dtype=torch.int64, device=dev)
+            self.tiles.append(rowptr, cols, vals)
+            if s < sample_rows:
+                self.sample.append((cols.cpu().numpy(), vals.cpu().numpy()))
+            del c, v, m, cols, vals, rowptr
+        torch.cuda.synchronize()
+        self.prep_ms = (time.perf_counter() - t0) * 1e3
+        self.labels = y
+        self.block = DeviceInstanceBlock(y, None, tiles=self.tiles, numFeatures=F)
         self.coef = np.random.default_rng(4).normal(size=F + 1) * 0.01
+        # scaledMean = mean / std per feature: nonzero with probability k / F,
+        # values U(0, 1) -- mean ~ 3.2e-5, std ~ 4.6e-3 -> scaledMean ~ 7e-3
+        self.scaledMean = np.random.default_rng(5).uniform(0.0, 0.014, F)
         self.fn = RDDLossFunction([self.block], lambda c: BinaryLogisticBlockAggregator(
-            np.ones(F), None, True, False, c, device=dev))
+            np.ones(F), self.scaledMean, True, True, c, device=dev))
 
     def step(self):
         self.fn.calculate(self.coef)
@@ -353,21 +380,27 @@ class LRSparseWorkload:
     def work_per_launch(self, launches_per_step):
         return self.n * (self.k * 12 + 8 + 8) / launches_per_step   # bytes
 
+    def extra_roofline(self, launches_per_step, avg_s):
+        return {"layout_bytes": self.tiles.nbytes,
+                "note": "784 B/row = one fused pass (SURVEY 8d); the evaluation reads the "
+                        "layout twice (margin pass, then gradient pass), 12 B per nonzero each"}
+
     def describe(self):
         return (f"binomial LR RDDLossFunction.calculate on CSR {self.n} rows x {self.F} "
-                f"features, {self.k} nnz/row per GPU (BASELINE configs[4], 8-GPU shard "
-                "of 200M rows)")
+                f"features, {self.k} nnz/row per GPU, fitIntercept+fitWithMean "
+                "(BASELINE configs[4], full 200M-row shard resident on one GPU in the "
+                "row-block x column-tile layout)")
 
     def cpu_baseline(self, seconds):
         import numpy as np
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         threads = cpu_threads()
-        m = min(self.n, 25_000_000)
-        rp = self.block.rowptr[:m + 1].cpu().numpy()
-        ci = self.block.colidx[:m * self.k].cpu().numpy()
-        vv = self.block.values[:m * self.k].cpu().numpy()
-        y = self.block.labels[:m].cpu().numpy()
+        ci = np.concatenate([a for a, _ in self.sample])
+        vv = np.concatenate([b for _, b in self.sample])
+        m = ci.size // self.k
+        rp = np.arange(0, m * self.k + 1, self.k, dtype=np.int64)
+        y = self.labels[:m].cpu().numpy()
 
         def part(rng_):
             a, b = rng_
@@ -377,7 +410,8 @@ class LRSparseWorkload:
                 oracle.binary_logistic_add(dict(labels=y[s:e], weights=None,
                                                 rowptr=rp[s:e + 1] - rp[s],
                                                 colidx=ci[rp[s]:rp[e]], values=vv[rp[s]:rp[e]],
-                                                F=self.F), self.coef, True, False, None, st)
+                                                F=self.F), self.coef, True, True,
+                                           self.scaledMean, st)
             return st
         t0 = time.perf_counter()
         part((0, 1345 * 4))
@@ -389,14 +423,14 @@ class LRSparseWorkload:
         el, _ = timed_parallel(part, ranges, threads)
         reps = 1
         if seconds > 0 and el < 0.5 * seconds:
-            # the shard is smaller than the CPU budget: repeat the data pass
-            # (one RDDLossFunction.calculate each) to reach ~seconds of work
+            # the host sample is smaller than the CPU budget: repeat the data
+            # pass (one RDDLossFunction.calculate each) to reach ~seconds of work
             reps = max(2, int(round(seconds / el)))
             el, _ = timed_parallel(lambda r: [part(r) for _ in range(reps)], ranges, threads)
         return {"value": rows * reps / el, "unit": "rows/s", "cores": threads, "kind": "port",
                 "sample": f"{rows} rows of the same CSR data in 1345-row blocks (1 MiB), "
-                          f"{threads} partitions on {threads} threads, {reps} pass(es), "
-                          f"{el:.1f} s"}
+                          f"fitWithMean, {threads} partitions on {threads} threads, {reps} "
+                          f"pass(es), {el:.1f} s"}
 
 
 WORKLOADS = {"kmeans": KMeansWorkload, "gramian": GramianWorkload, "lr_multi": LRMultiWorkload,

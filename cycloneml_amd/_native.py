@@ -110,7 +110,6 @@ SIGNATURES = {
     "cyc_csc_destroy": (ctypes.c_int, [_vp]),
     "cyc_csc_rows": (_i64, [_vp]),
     "cyc_csc_blocks": (ctypes.c_int, [_vp, _pi64, _pi64]),
-    "cyc_csc_slices": (ctypes.c_int, [_vp, _pi32, _pi32, _vp, _vp, _vp]),
     "cyc_csc_arrays": (ctypes.c_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                                       ctypes.POINTER(_vp)]),
     "cyc_multinomial_logistic_add_dense_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp,
@@ -118,6 +117,16 @@ SIGNATURES = {
     "cyc_multinomial_logistic_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64,
                                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "cyc_csc_features": (_i32, [_vp]),
+    "cyc_tiles_create": (ctypes.c_int, [_i32, _i64, _i64, ctypes.POINTER(_vp)]),
+    "cyc_tiles_append_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp]),
+    "cyc_tiles_destroy": (ctypes.c_int, [_vp]),
+    "cyc_tiles_rows": (_i64, [_vp]),
+    "cyc_tiles_nnz": (_i64, [_vp]),
+    "cyc_tiles_features": (_i32, [_vp]),
+    "cyc_tiles_bytes": (_i64, [_vp]),
+    "cyc_tiles_row_block": (_i32, []),
+    "cyc_binary_add_tiles_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                _vp]),
     "cyc_summarizer_buffer_len": (_i64, [_i32]),
     "cyc_summarizer_dense_dev": (ctypes.c_int, [_vp, _vp, _i64, _i32, _i64, _vp, _vp]),
     "cyc_summarizer_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp]),

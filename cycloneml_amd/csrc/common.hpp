@@ -53,11 +53,15 @@ struct KernelTimer {
 // kCscRowBlock; colptr int64[nblocks F + 1] (block-major, then column),
 // rowidx int32, cvals fp64; each (block, column)'s rows in increasing order.
 constexpr int64_t kCscRowBlock = 1 << 18;
-// column-slice width of the sliced CSR copy (fp64 coefficients per slice)
-constexpr int kSliceCols = 1 << 18;
 int build_csc(const int64_t* rowptr, const int32_t* colidx, const double* vals, int64_t n, int F,
               int64_t rowBlock,
               DeviceBuffer& colptr, DeviceBuffer& rowidx, DeviceBuffer& cvals, hipStream_t st);
+
+// SparseVector's index requires (ml/linalg/Vectors.scala:617-625) over every
+// row of a device CSR (rowptr may start at any base): CYC_ERR_INVALID_ARG
+// with the reference's message for the lowest offending row.
+int check_csr_indices(const int64_t* rowptr, const int32_t* colidx, int64_t n, int F,
+                      hipStream_t st);
 
 // Fixed-margin round-up.
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }

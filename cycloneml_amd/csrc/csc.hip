@@ -15,18 +15,13 @@
 // gathers from it.  colptr has nblocks * F + 1 entries: block b, column c
 // is [colptr[b F + c], colptr[b F + c + 1]).
 //
-// Column-sliced CSR (the margin pass): for F beyond what one XCD's L2 holds
-// as fp64 coefficients, the columns are cut into S slices of sliceWidth and
-// the nonzeros regrouped slice-major, each slice a CSR over all rows
-// (rowptrS[s n + r] .. rowptrS[s n + r + 1]), a row's nonzeros in their
-// original order.  The margin pass then runs one slice at a time, so the
-// coefficients it gathers (2 MB per slice) stay in L2.  Built without a sort:
-// per-row counts, one exclusive scan, a per-row stable scatter.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <string>
+#include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -77,63 +72,74 @@ __global__ void k_colptr(const int64_t* __restrict__ keys, int64_t nnz, int64_t 
   }
 }
 
-// counts[s n + r] = nonzeros of row r in column slice s (8 lanes per row)
-__global__ void k_slice_count(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
-                              int64_t n, int S, int width, int64_t* __restrict__ counts) {
-  const int sub = threadIdx.x & 7;
-  const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> 3;
-  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 3; r < n; r += stride) {
-    int cnt[16];
-    for (int s = 0; s < S; ++s) cnt[s] = 0;
-    const int64_t p1 = rowptr[r + 1];
-    for (int64_t p = rowptr[r] + sub; p < p1; p += 8) {
-      const int sl = colidx[p] / width;
-      for (int s = 0; s < S; ++s) cnt[s] += (sl == s);
+// Lowest row whose column indices break SparseVector's requires
+// (ml/linalg/Vectors.scala:617-625: first index >= 0, strictly increasing,
+// last < size); the host re-derives that row's message.
+__global__ void k_check_csr(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
+                            int64_t n, int F, unsigned long long* __restrict__ bad) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+       r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p0 = rowptr[r] - rowptr[0], p1 = rowptr[r + 1] - rowptr[0];
+    bool ok = true;
+    int prev = -1;
+    for (int64_t p = p0; p < p1; ++p) {
+      const int c = colidx[p];
+      if (c <= prev || c < 0) { ok = false; break; }
+      prev = c;
     }
-    for (int s = 0; s < S; ++s) {
-      int c = cnt[s];
-      c += __shfl_xor(c, 1);
-      c += __shfl_xor(c, 2);
-      c += __shfl_xor(c, 4);
-      if (sub == 0) counts[(int64_t)s * n + r] = c;
-    }
-  }
-}
-
-// Stable per-row scatter into the slices (one wave per row, 64 nonzeros per
-// step; a nonzero's rank among the same slice's earlier ones by ballot).
-__global__ void k_slice_scatter(const int64_t* __restrict__ rowptr,
-                                const int32_t* __restrict__ colidx,
-                                const double* __restrict__ vals, int64_t n, int S, int width,
-                                const int64_t* __restrict__ rowptrS, int32_t* __restrict__ colS,
-                                double* __restrict__ valS) {
-  const int lane = threadIdx.x & 63;
-  const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < n; r += stride) {
-    int64_t base[16];
-    for (int s = 0; s < S; ++s) base[s] = rowptrS[(int64_t)s * n + r];
-    const int64_t p1 = rowptr[r + 1];
-    for (int64_t p0 = rowptr[r]; p0 < p1; p0 += 64) {
-      const int64_t p = p0 + lane;
-      const bool on = p < p1;
-      const int c = on ? colidx[p] : 0;
-      const int sl = on ? c / width : -1;
-      for (int s = 0; s < S; ++s) {
-        const unsigned long long m = __ballot(sl == s);
-        if (sl == s) {
-          const int rank = __popcll(m & ((1ull << lane) - 1ull));
-          colS[base[s] + rank] = c;
-          valS[base[s] + rank] = vals[p];
-        }
-        base[s] += __popcll(m);
-      }
-    }
+    if (ok && prev >= F) ok = false;
+    if (!ok) atomicMin(bad, (unsigned long long)r);
   }
 }
 
 }  // namespace
 
 namespace cyc {
+
+int check_csr_indices(const int64_t* rowptr, const int32_t* colidx, int64_t n, int F,
+                      hipStream_t st) {
+  if (n <= 0) return CYC_OK;
+  DeviceBuffer bad;
+  int rc;
+  if ((rc = bad.reserve(sizeof(unsigned long long)))) return rc;
+  CYC_HIP(hipMemsetAsync(bad.ptr, 0xff, sizeof(unsigned long long), st));
+  hipLaunchKernelGGL(k_check_csr, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 8192)),
+                     dim3(256), 0, st, rowptr, colidx, n, F, (unsigned long long*)bad.ptr);
+  CYC_LAUNCH_CHECK("k_check_csr");
+  unsigned long long r = 0;
+  CYC_HIP(hipMemcpyAsync(&r, bad.ptr, sizeof(r), hipMemcpyDeviceToHost, st));
+  CYC_HIP(hipStreamSynchronize(st));
+  if (r >= (unsigned long long)n) return CYC_OK;
+  int64_t b[3];
+  CYC_HIP(hipMemcpy(b, rowptr, sizeof(int64_t), hipMemcpyDeviceToHost));
+  CYC_HIP(hipMemcpy(b + 1, rowptr + r, 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+  std::vector<int32_t> idx((size_t)(b[2] - b[1]));
+  if (!idx.empty())
+    CYC_HIP(hipMemcpy(idx.data(), colidx + (b[1] - b[0]), idx.size() * sizeof(int32_t),
+                      hipMemcpyDeviceToHost));
+  std::string msg;
+  if ((int64_t)idx.size() > F) {
+    msg = "You provided " + std::to_string(idx.size()) +
+          " indices and values, which exceeds the specified vector size " + std::to_string(F) + ".";
+  } else if (idx[0] < 0) {
+    msg = "Found negative index: " + std::to_string(idx[0]) + ".";
+  } else {
+    int prev = -1;
+    for (int32_t i : idx) {
+      if (prev >= i) {
+        msg = "Index " + std::to_string(i) + " follows " + std::to_string(prev) +
+              " and is not strictly increasing";
+        break;
+      }
+      prev = i;
+    }
+    if (msg.empty())
+      msg = "Index " + std::to_string(prev) + " out of bounds for vector of size " +
+            std::to_string(F);
+  }
+  set_error("requirement failed: " + msg);
+  return CYC_ERR_INVALID_ARG;
+}
 
 int build_csc(const int64_t* rowptr, const int32_t* colidx, const double* vals, int64_t n, int F,
               int64_t rowBlock, DeviceBuffer& colptr, DeviceBuffer& rowidx, DeviceBuffer& cvals, hipStream_t st) {
@@ -185,44 +191,6 @@ int build_csc(const int64_t* rowptr, const int32_t* colidx, const double* vals, 
   return CYC_OK;
 }
 
-int build_slices(const int64_t* rowptr, const int32_t* colidx, const double* vals, int64_t n,
-                 int F, int S, int width, DeviceBuffer& rowptrS, DeviceBuffer& colS,
-                 DeviceBuffer& valS, hipStream_t st) {
-  int64_t nnz = 0;
-  CYC_HIP(hipMemcpyAsync(&nnz, rowptr + n, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-  CYC_HIP(hipStreamSynchronize(st));
-  const int64_t len = (int64_t)S * n;
-  int rc;
-  DeviceBuffer counts, tmp;
-  if ((rc = rowptrS.reserve(sizeof(int64_t) * ((size_t)len + 1))) ||
-      (rc = colS.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(nnz, 1))) ||
-      (rc = valS.reserve(sizeof(double) * (size_t)std::max<int64_t>(nnz, 1))) ||
-      (rc = counts.reserve(sizeof(int64_t) * ((size_t)len + 1))))
-    return rc;
-  CYC_HIP(hipMemsetAsync(counts.ptr, 0, sizeof(int64_t) * ((size_t)len + 1), st));
-  if (n > 0) {
-    hipLaunchKernelGGL(k_slice_count, dim3(8192), dim3(256), 0, st, rowptr, colidx, n, S, width,
-                       (int64_t*)counts.ptr);
-    CYC_LAUNCH_CHECK("k_slice_count");
-  }
-  size_t tmpBytes = 0;
-  CYC_HIP(rocprim::exclusive_scan(nullptr, tmpBytes, (const int64_t*)counts.ptr,
-                                  (int64_t*)rowptrS.ptr, (int64_t)0, (size_t)len + 1,
-                                  rocprim::plus<int64_t>(), st));
-  if ((rc = tmp.reserve(tmpBytes))) return rc;
-  CYC_HIP(rocprim::exclusive_scan(tmp.ptr, tmpBytes, (const int64_t*)counts.ptr,
-                                  (int64_t*)rowptrS.ptr, (int64_t)0, (size_t)len + 1,
-                                  rocprim::plus<int64_t>(), st));
-  if (n > 0) {
-    hipLaunchKernelGGL(k_slice_scatter, dim3(8192), dim3(256), 0, st, rowptr, colidx, vals, n, S,
-                       width, (const int64_t*)rowptrS.ptr, (int32_t*)colS.ptr,
-                       (double*)valS.ptr);
-    CYC_LAUNCH_CHECK("k_slice_scatter");
-  }
-  CYC_HIP(hipStreamSynchronize(st));
-  return CYC_OK;
-}
-
 }  // namespace cyc
 
 struct cyc_csc_s {
@@ -230,9 +198,6 @@ struct cyc_csc_s {
   int F = 0;
   int64_t rpb = cyc::kCscRowBlock;   // rows per CSC row block
   cyc::DeviceBuffer colptr, rowidx, cvals;
-  // column-sliced CSR (S > 1 only)
-  int S = 1, width = 0;
-  cyc::DeviceBuffer rowptrS, colS, valS;
 };
 
 extern "C" {
@@ -241,27 +206,16 @@ int cyc_csc_build_dev(const int64_t* rowptr, const int32_t* colidx, const double
                       int64_t n, int32_t numFeatures, void* stream, cyc_csc* out) {
   CYC_REQUIRE(out != nullptr && rowptr != nullptr, "output handle and rowptr must not be null");
   CYC_REQUIRE(n >= 0 && numFeatures > 0, "n >= 0 and numFeatures > 0");
+  if (int rc = cyc::check_csr_indices(rowptr, colidx, n, numFeatures, cyc::as_stream(stream)))
+    return rc;
   auto* c = new cyc_csc_s();
   c->n = n;
   c->F = numFeatures;
   // rows per row block: the gradient pass keeps one block's multipliers
-  // (8 B per row) in L2; CYC_CSC_ROWBLOCK_LOG2 overrides (measurement)
-  static const int64_t rowBlock = [] {
-    const char* e = std::getenv("CYC_CSC_ROWBLOCK_LOG2");
-    const int l = e ? std::atoi(e) : 0;
-    return (l >= 10 && l <= 24) ? ((int64_t)1 << l) : cyc::kCscRowBlock;
-  }();
-  c->rpb = rowBlock;
+  // (8 B per row) in L2 (2^17 / 2^19 / 2^20 measured no better in round 1)
+  c->rpb = cyc::kCscRowBlock;
   int rc = cyc::build_csc(rowptr, colidx, vals, n, numFeatures, c->rpb, c->colptr, c->rowidx,
-                          c->cvals,
-                          cyc::as_stream(stream));
-  // slices of at most kSliceCols columns (2 MB of fp64 coefficients)
-  c->S = (int)std::min<int64_t>(16, ((int64_t)numFeatures + cyc::kSliceCols - 1) / cyc::kSliceCols);
-  if (c->S < 1) c->S = 1;
-  c->width = (numFeatures + c->S - 1) / c->S;
-  if (rc == CYC_OK && c->S > 1)
-    rc = cyc::build_slices(rowptr, colidx, vals, n, numFeatures, c->S, c->width, c->rowptrS,
-                           c->colS, c->valS, cyc::as_stream(stream));
+                          c->cvals, cyc::as_stream(stream));
   if (rc) {
     delete c;
     return rc;
@@ -278,17 +232,6 @@ int cyc_csc_destroy(cyc_csc csc) {
 int64_t cyc_csc_rows(cyc_csc csc) { return csc ? csc->n : -1; }
 
 int32_t cyc_csc_features(cyc_csc csc) { return csc ? csc->F : -1; }
-
-int cyc_csc_slices(cyc_csc csc, int32_t* nslices, int32_t* width, const int64_t** rowptrS,
-                   const int32_t** colS, const double** valS) {
-  CYC_REQUIRE(csc != nullptr, "csc must not be null");
-  if (nslices) *nslices = csc->S;
-  if (width) *width = csc->width;
-  if (rowptrS) *rowptrS = (const int64_t*)csc->rowptrS.ptr;
-  if (colS) *colS = (const int32_t*)csc->colS.ptr;
-  if (valS) *valS = (const double*)csc->valS.ptr;
-  return CYC_OK;
-}
 
 int cyc_csc_blocks(cyc_csc csc, int64_t* rows_per_block, int64_t* nblocks) {
   CYC_REQUIRE(csc != nullptr, "csc must not be null");

@@ -35,86 +35,20 @@
 #include <cmath>
 #include <mutex>
 
+#include "binary_rows.hpp"
 #include "common.hpp"
+#include "tiles.hpp"
 
 namespace {
+
+using cyc::bin_row;
+using cyc::log1p_exp;
+using cyc::row_margin;
 
 __device__ __forceinline__ double wave_sum_bcast(double s) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) s += __shfl_xor(s, m);
   return __shfl(s, 0);  // every lane takes lane 0's association order
-}
-
-// ml/impl/Utils.scala:91-97
-__device__ __forceinline__ double log1p_exp(double x) {
-  return x > 0 ? x + log1p(exp(-x)) : log1p(exp(x));
-}
-
-// Row margin before the epilogue.  kind 0/1: offset + dot (dgemv "T" with
-// beta = 1 on the filled offset); kind 2 (LeastSquaresBlockAggregator.scala:
-// 84-86): arr = offset or 0.0, daxpy(-1/labelStd, labels, arr), then + dot.
-__device__ __forceinline__ double row_margin(int kind, int fitIntercept, double offset,
-                                             double lscale, double label, double dot) {
-  if (kind == 2) return ((fitIntercept ? offset : 0.0) + lscale * label) + dot;
-  return fitIntercept ? offset + dot : dot;
-}
-
-// Per-row epilogue by aggregator kind; returns the multiplier and
-// accumulates loss and weight.
-//   0 BinaryLogisticBlockAggregator.scala:104-122
-//   1 HingeBlockAggregator.scala:103-117 (labels {0,1} scaled to {-1,1};
-//     loss (1 - y' m) w and multiplier -y' w only where the loss is > 0)
-//   2 LeastSquaresBlockAggregator.scala:90-100 (every row: loss w d d / 2,
-//     multiplier w d)
-//   3 HuberBlockAggregator.scala:101-127 (quadratic inside sigma * epsilon,
-//     linear outside; sgs accumulates sigmaGradSum)
-//   4 AFTBlockAggregator.scala:95-108 (log-linear survival; w = censor)
-__device__ __forceinline__ double bin_row(int kind, double margin, double w, double label,
-                                          double& loss, double& wsum, double& sgs, double sigma,
-                                          double eps) {
-  if (kind == 4) {
-    // AFTBlockAggregator.scala:95-108: w is the censor delta, sigma =
-    // exp(log-sigma), every row counts 1 toward weightSum (:110)
-    const double e = (log(label) - margin) / sigma;
-    const double ee = exp(e);
-    loss += w * log(sigma) - w * e + ee;
-    const double m = (w - ee) / sigma;
-    sgs += w + m * sigma * e;
-    wsum += 1.0;
-    return m;
-  }
-  wsum += w;
-  if (w > 0 && kind == 3) {
-    const double ll = label - margin;
-    if (fabs(ll) <= sigma * eps) {
-      loss += 0.5 * w * (sigma + ll * ll / sigma);
-      const double lds = ll / sigma;
-      sgs += 0.5 * w * (1.0 - lds * lds);
-      return -1.0 * w * lds;
-    }
-    loss += 0.5 * w * (sigma + 2.0 * eps * fabs(ll) - sigma * eps * eps);
-    sgs += 0.5 * w * (1.0 - eps * eps);
-    return w * (ll >= 0 ? -1.0 : 1.0) * eps;
-  }
-  if (kind == 2) {
-    loss += w * margin * margin / 2;
-    return w * margin;
-  }
-  if (w > 0 && kind == 1) {
-    const double ls = label + label - 1.0;
-    const double l = (1.0 - ls * margin) * w;
-    if (l > 0) {
-      loss += l;
-      return -ls * w;
-    }
-    return 0.0;
-  }
-  if (w > 0) {
-    if (label > 0) loss += w * log1p_exp(-margin);
-    else loss += w * (log1p_exp(-margin) + margin);
-    return w * (1.0 / (1.0 + exp(-margin)) - label);
-  }
-  return 0.0;
 }
 
 template <int FPL>
@@ -234,17 +168,16 @@ __global__ __launch_bounds__(256) void k_binlog_csc_grad(
 // row (8 rows per round, each row's nonzeros strided over its 8 lanes and
 // summed by a 3-step butterfly), then hands row i's partial dot to lane i so
 // the per-row epilogue (log1p/exp, BinaryLogisticBlockAggregator.scala:
-// 104-122) runs once per row instead of once per lane.  Over a column-sliced
-// CSR (csc.hip) the pass runs once per slice: dots[r] accumulates the slices'
-// partial dots in slice order (first: =, else +=) and the last slice turns
-// dots[r] into the multiplier in place, written coalesced.
-template <int CSR_IT, int RP>
+// 104-122) runs once per row instead of once per lane; dots[r] receives the
+// multiplier, written coalesced.
+constexpr int CSR_IT = 2;   // nonzeros per lane per chunk (16 loads in flight)
+constexpr int RP = 8;       // rows per pass
 __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const double* __restrict__ vals, const double* __restrict__ labels,
     const double* __restrict__ weights, int64_t n, const double* __restrict__ coef,
-    int fitIntercept, int kind, double offset, double lscale, double sigma, double eps, int first, int last, double* __restrict__ dots,
-    double* __restrict__ slabS) {
+    int fitIntercept, int kind, double offset, double lscale, double sigma, double eps,
+    double* __restrict__ dots, double* __restrict__ slabS) {
   const int lane = threadIdx.x & 63, sub = lane & 7, grp = lane >> 3;
   const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -312,19 +245,13 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
     }
     const int64_t row = g0 + lane;
     if (row < n) {
-      const double dot = first ? mydot : dots[row] + mydot;
-      if (!last) {
-        dots[row] = dot;
-      } else {
-        const double margin = row_margin(kind, fitIntercept, offset, lscale, labels[row], dot);
-        const double w = weights ? weights[row] : 1.0;
-        const double m = bin_row(kind, margin, w, labels[row], loss, wsum, sgs, sigma, eps);
-        msum += m;
-        dots[row] = m;
-      }
+      const double margin = row_margin(kind, fitIntercept, offset, lscale, labels[row], mydot);
+      const double w = weights ? weights[row] : 1.0;
+      const double m = bin_row(kind, margin, w, labels[row], loss, wsum, sgs, sigma, eps);
+      msum += m;
+      dots[row] = m;
     }
   }
-  if (!last) return;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) {
     loss += __shfl_xor(loss, m);
@@ -344,7 +271,7 @@ __global__ __launch_bounds__(256) void k_binlog_csr_mult8(
 // column, products vals * mult[row] (the block's 2 MB multiplier slice stays
 // in L2), fixed 4-step butterfly, gradAcc[c] = (first ? 0 : gradAcc[c]) + s.
 // Deterministic: blocks in order, a block's rows in order within each lane.
-template <int LPC, int IT, int CPG>
+constexpr int LPC = 32, IT = 1, CPG = 4;   // lanes per group of CPG columns
 __global__ __launch_bounds__(256) void k_binlog_csc_grad_blk(
     const int64_t* __restrict__ colptrB, const int32_t* __restrict__ rowidx,
     const double* __restrict__ cvals, const double* __restrict__ mult, int F, int first,
@@ -1155,57 +1082,31 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
   const int32_t* rowidx = nullptr;
   const double* cvals = nullptr;
   if (csc) {
-    CYC_REQUIRE(cyc_csc_rows(csc) == n, "the CSC copy does not match the CSR rows");
+    CYC_REQUIRE(cyc_csc_rows(csc) == n && cyc_csc_features(csc) == F,
+                "the CSC copy does not match the CSR rows (cyc_csc_build_dev of these rows)");
     cyc_csc_arrays(csc, &colptr, &rowidx, &cvals);
   }
   if (csc) {
     // Deterministic two-pass path: CSR margins -> mult, then the row-blocked
-    // CSC's column sums, one row block at a time.
+    // CSC's column sums, one row block at a time.  (The row-block x
+    // column-tile layout, cyc_binary_add_tiles_dev, is the fast path for
+    // large sparse shards.)
     if ((rc = p->rowMult.reserve(sizeof(double) * (size_t)n))) return rc;
     {
-      int32_t S = 1, width = 0;
-      const int64_t* rowptrS = nullptr;
-      const int32_t* colS = nullptr;
-      const double* valS = nullptr;
-      cyc_csc_slices(csc, &S, &width, &rowptrS, &colS, &valS);
-      // nonzeros per lane per chunk (2 = 16 loads in flight); measurement override
-      int csr_it = 2;
-      if (const char* e = std::getenv("CYC_CSR_IT")) csr_it = std::atoi(e);
-      int csr_rp = 8;  // rows per pass
-      if (const char* e = std::getenv("CYC_CSR_RP")) csr_rp = std::atoi(e);
       cyc::KernelTimer timer("k_binlog_csr", st);
-      for (int sl = 0; sl < S; ++sl) {
-        const int64_t* rp = S > 1 ? rowptrS + (int64_t)sl * n : rowptr;
-        auto kern = csr_rp == 4 ? (csr_it == 4 ? k_binlog_csr_mult8<4, 4> : k_binlog_csr_mult8<2, 4>)
-                    : csr_it == 4 ? k_binlog_csr_mult8<4, 8>
-                    : csr_it == 3 ? k_binlog_csr_mult8<3, 8> : k_binlog_csr_mult8<2, 8>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, rp,
-                           S > 1 ? colS : colidx, S > 1 ? valS : vals, labels, weights, n, kc,
-                           p->fitIntercept, p->loss, offset, lscale, sigma, eps, sl == 0 ? 1 : 0,
-                           sl == S - 1 ? 1 : 0,
-                           (double*)p->rowMult.ptr, (double*)p->slabS.ptr);
-      }
+      hipLaunchKernelGGL(k_binlog_csr_mult8, dim3((unsigned)blocks), dim3(256), 0, st, rowptr,
+                         colidx, vals, labels, weights, n, kc, p->fitIntercept, p->loss, offset,
+                         lscale, sigma, eps, (double*)p->rowMult.ptr, (double*)p->slabS.ptr);
       CYC_LAUNCH_CHECK("k_binlog_csr_mult8");
     }
     int64_t rpb = 0, nb = 0;
     cyc_csc_blocks(csc, &rpb, &nb);
-    // lanes per group of 4 columns: 32 (12.8 ms per evaluation; 16 / 8 lanes
-    // 14.0 / 15.3 ms) -- CYC_CSC_LPC overrides for such measurements
-    int lpc = 32, cpg = 4;
-    if (const char* e = std::getenv("CYC_CSC_LPC")) lpc = std::atoi(e);
-    if (lpc != 8 && lpc != 16 && lpc != 64) lpc = 32;
-    if (const char* e = std::getenv("CYC_CSC_CPG")) cpg = std::atoi(e);
-    if (cpg != 2 && cpg != 8) cpg = 4;
-    if (lpc != 32) cpg = 4;
-    const unsigned cgrid = (unsigned)((((int64_t)F + cpg - 1) / cpg * lpc + 255) / 256);
-    auto gkern = lpc == 8    ? k_binlog_csc_grad_blk<8, 3, 4>
-                 : lpc == 16 ? k_binlog_csc_grad_blk<16, 2, 4>
-                 : lpc == 64 ? k_binlog_csc_grad_blk<64, 1, 4>
-                 : cpg == 2  ? k_binlog_csc_grad_blk<32, 1, 2>
-                 : cpg == 8  ? k_binlog_csc_grad_blk<32, 1, 8> : k_binlog_csc_grad_blk<32, 1, 4>;
+    // 32 lanes per group of 4 columns (round 1: 8 / 16 / 64 lanes and 2 / 8
+    // columns per group measured slower or flat)
+    const unsigned cgrid = (unsigned)((((int64_t)F + 3) / 4 * 32 + 255) / 256);
     cyc::KernelTimer timer("k_binlog_csc_grad", st);
     for (int64_t b = 0; b < nb; ++b) {
-      hipLaunchKernelGGL(gkern, dim3(cgrid), dim3(256), 0, st,
+      hipLaunchKernelGGL(k_binlog_csc_grad_blk, dim3(cgrid), dim3(256), 0, st,
                          colptr + b * F, rowidx, cvals, (const double*)p->rowMult.ptr, F,
                          b == 0 ? 1 : 0, (double*)p->gradAcc.ptr);
     }
@@ -1230,6 +1131,89 @@ int binary_add_csr(cyc_logistic_plan p, const int64_t* rowptr, const int32_t* co
 }
 
 }  // namespace
+
+namespace {
+int ls_prepare(cyc_logistic_plan p, const double* coef, const double* inverseStd,
+               const double* scaledMean, hipStream_t st, const double** eff) {
+  CYC_REQUIRE(p != nullptr && p->loss == 2,
+              "the plan is not a least squares plan (cyc_least_squares_plan_create)");
+  CYC_REQUIRE(coef != nullptr && inverseStd != nullptr, "coef and inverseStd must not be null");
+  CYC_REQUIRE(!p->fitIntercept || scaledMean != nullptr,
+              "scaled means is required when fitting an intercept");
+  int rc;
+  if ((rc = p->effCoef.reserve(sizeof(double) * (size_t)p->F))) return rc;
+  hipLaunchKernelGGL(k_effective_coef, dim3((p->F + 255) / 256), dim3(256), 0, st, coef,
+                     inverseStd, p->F, (double*)p->effCoef.ptr);
+  CYC_LAUNCH_CHECK("k_effective_coef");
+  *eff = (const double*)p->effCoef.ptr;
+  return CYC_OK;
+}
+}  // namespace
+
+int cyc_binary_add_tiles_dev(cyc_logistic_plan p, cyc_tiles tiles, const double* labels,
+                             const double* weights, const double* coef, const double* inverseStd,
+                             const double* scaledMean, double* grad, double* lossSum,
+                             double* weightSum, void* stream) {
+  int rc = check_common(p, coef, scaledMean);
+  if (rc) return rc;
+  CYC_REQUIRE(tiles != nullptr, "tiles must not be null");
+  cyc::TilesView v;
+  if ((rc = cyc::tiles_view(tiles, &v))) return rc;
+  const int F = p->F;
+  CYC_REQUIRE(v.F == F, "Dimensions mismatch when adding new instance. Expecting " +
+                            std::to_string(F) + " but got " + std::to_string(v.F) + ".");
+  const int64_t n = v.n;
+  if (n == 0) return CYC_OK;
+  CYC_REQUIRE(labels != nullptr, "labels must not be null");
+  hipStream_t st = cyc::as_stream(stream);
+  const double* kc = coef;
+  if (p->loss == 2) {      // LeastSquaresBlockAggregator.effectiveCoef (:48-55)
+    if ((rc = ls_prepare(p, coef, inverseStd, scaledMean, st, &kc))) return rc;
+  }
+  std::lock_guard<std::mutex> g(p->mu);
+  const int R = cyc::tiles_ranges(v);
+  const int64_t wgMax = cyc::device_cus();
+  if ((rc = p->rowMult.reserve(sizeof(double) * (size_t)n)) ||
+      (rc = p->slabG.reserve(sizeof(double) * (size_t)R * F)) ||
+      (rc = p->slabS.reserve(sizeof(double) * (size_t)wgMax * 4)) ||
+      (rc = p->scal.reserve(sizeof(double) * 4)) || (rc = p->offset.reserve(sizeof(double) * 2)))
+    return rc;
+  double offset = 0.0;
+  if ((rc = binary_offset(p, coef, scaledMean, st, &offset))) return rc;
+  const double lscale = -1.0 / p->labelStd;
+  const int foldIcpt = p->loss == 2 ? 0 : p->fitIntercept;
+  double sigma = 0.0;
+  const int sigIdx = p->loss == 3 ? F + (p->fitIntercept ? 1 : 0) : p->loss == 4 ? F + 1 : -1;
+  if (sigIdx >= 0) {
+    CYC_HIP(hipMemcpyAsync(&sigma, coef + sigIdx, sizeof(double), hipMemcpyDeviceToHost, st));
+    CYC_HIP(hipStreamSynchronize(st));
+    if (p->loss == 4) sigma = std::exp(sigma);
+  }
+  int64_t wgs = 0;
+  {
+    cyc::KernelTimer timer("k_tiles_margin", st);
+    if ((rc = cyc::tiles_margin(v, labels, weights, kc, p->fitIntercept, p->loss, offset, lscale,
+                                sigma, p->epsilon, (double*)p->rowMult.ptr,
+                                (double*)p->slabS.ptr, &wgs, st)))
+      return rc;
+  }
+  int ranges = 0;
+  {
+    cyc::KernelTimer timer("k_tiles_grad", st);
+    if ((rc = cyc::tiles_grad(v, (const double*)p->rowMult.ptr, (double*)p->slabG.ptr, &ranges,
+                              st)))
+      return rc;
+  }
+  hipLaunchKernelGGL(k_fold_scalars, dim3(1), dim3(256), 0, st, (const double*)p->slabS.ptr, wgs,
+                     4, (double*)p->scal.ptr);
+  CYC_LAUNCH_CHECK("k_fold_scalars");
+  hipLaunchKernelGGL(k_binlog_fold, dim3((F + 255) / 256), dim3(256), 0, st,
+                     (const double*)p->slabG.ptr, (int64_t)ranges, nullptr, F,
+                     (const double*)p->scal.ptr, foldIcpt, p->fitWithMean, sigIdx, scaledMean, grad,
+                     lossSum, weightSum);
+  CYC_LAUNCH_CHECK("k_binlog_fold");
+  return CYC_OK;
+}
 
 int cyc_binary_logistic_add_dense_dev(cyc_logistic_plan p, const double* X, const double* labels,
                                       const double* weights, int64_t n, const double* coef,
@@ -1344,23 +1328,6 @@ int cyc_least_squares_plan_create(int32_t numFeatures, int fitIntercept, double 
   return rc;
 }
 
-namespace {
-int ls_prepare(cyc_logistic_plan p, const double* coef, const double* inverseStd,
-               const double* scaledMean, hipStream_t st, const double** eff) {
-  CYC_REQUIRE(p != nullptr && p->loss == 2,
-              "the plan is not a least squares plan (cyc_least_squares_plan_create)");
-  CYC_REQUIRE(coef != nullptr && inverseStd != nullptr, "coef and inverseStd must not be null");
-  CYC_REQUIRE(!p->fitIntercept || scaledMean != nullptr,
-              "scaled means is required when fitting an intercept");
-  int rc;
-  if ((rc = p->effCoef.reserve(sizeof(double) * (size_t)p->F))) return rc;
-  hipLaunchKernelGGL(k_effective_coef, dim3((p->F + 255) / 256), dim3(256), 0, st, coef,
-                     inverseStd, p->F, (double*)p->effCoef.ptr);
-  CYC_LAUNCH_CHECK("k_effective_coef");
-  *eff = (const double*)p->effCoef.ptr;
-  return CYC_OK;
-}
-}  // namespace
 
 int cyc_least_squares_add_dense_dev(cyc_logistic_plan p, const double* X, const double* labels,
                                     const double* weights, int64_t n, const double* coef,
@@ -1522,9 +1489,9 @@ int cyc_multinomial_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* row
   if (rc) return rc;
   CYC_REQUIRE(n >= 0, "n >= 0");
   if (n == 0) return CYC_OK;
-  CYC_REQUIRE(csc != nullptr && cyc_csc_rows(csc) == n,
-              "a CSC copy of these rows is required (cyc_csc_build_dev)");
   const int F = p->F, C = p->C;
+  CYC_REQUIRE(csc != nullptr && cyc_csc_rows(csc) == n && cyc_csc_features(csc) == F,
+              "a CSC copy of these rows is required (cyc_csc_build_dev)");
   if (C > 1024) {
     cyc::set_error("multinomial CSR aggregator supports numClasses <= 1024");
     return CYC_ERR_UNSUPPORTED;

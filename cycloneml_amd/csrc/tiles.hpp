@@ -1,0 +1,55 @@
+// tiles.hpp -- internal interface of the row-block x column-tile layout
+// (tiles.hip) for the binary block aggregators (logistic.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "common.hpp"
+
+namespace cyc {
+
+constexpr int kTileRows = 8192;               // rows per row block (R)
+constexpr int kTileCols = 8192;               // columns per column tile (W, at most)
+constexpr int kTileWaves = 8;                 // waves per workgroup = sub-ranges per side
+constexpr int kTileSub = kTileWaves * kTileWaves;     // sub-segments per segment
+constexpr int kTileRowRange = kTileRows / kTileWaves; // rows per wave range (1024)
+
+// What the kernels need to walk a built layout.  Segment s = rb * T + t
+// (row block rb, column tile t) spans nonzeros [segStart[s], segStart[s+1]);
+// its sub-segment k = 8 i + j (row range i, column range j) starts at
+// segStart[s] + subRel[64 s + k].  idx packs (row in block << 16 | column in
+// tile), vals the fp64 values.
+struct TilesView {
+  int64_t n = 0;         // rows
+  int F = 0;             // numFeatures
+  int T = 1;             // column tiles
+  int Wt = 1;            // columns per tile (the last tile may be shorter)
+  int WS = 1;            // columns per wave range: ceil(Wt / 8)
+  int64_t nRB = 0;       // row blocks
+  const int64_t* segStart = nullptr;
+  const uint32_t* subRel = nullptr;
+  const uint32_t* idx = nullptr;
+  const double* vals = nullptr;
+};
+
+int tiles_view(cyc_tiles t, TilesView* v);
+
+// Margin pass: mult[r] = the per-row multiplier of aggregator `kind`
+// (binary_rows.hpp) from margin = row_margin(offset + dot_r); per-workgroup
+// (loss, weight, multiplierSum, sigmaGradSum) partials to slabS[wg * 4 + k].
+// Returns the number of workgroups (slabS rows) through *wgs.
+int tiles_margin(const TilesView& v, const double* labels, const double* weights,
+                 const double* coef, int fitIntercept, int kind, double offset, double lscale,
+                 double sigma, double eps, double* mult, double* slabS, int64_t* wgs,
+                 hipStream_t st);
+
+// Gradient pass: slabG[range * F + f] = sum over the rows of row range
+// `range` (row order) of vals * mult[row]; *ranges receives the range count.
+// slabG needs ranges_for(v) * F doubles.
+int tiles_ranges(const TilesView& v);
+int tiles_grad(const TilesView& v, const double* mult, double* slabG, int* ranges,
+               hipStream_t st);
+
+}  // namespace cyc

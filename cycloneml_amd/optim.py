@@ -28,15 +28,72 @@ def _torch():
     return torch
 
 
+class SparseTiles:
+    """RAII wrapper of cyc_tiles: the row-block x column-tile layout of a CSR
+    shard (cycloneml_amd/csrc/tiles.hip) that the binary aggregators' sparse
+    path runs on -- 12 B per nonzero, built by appending CSR rows (whole row
+    blocks of ROW_BLOCK rows, except the last append); the CSR can be freed
+    afterwards."""
+
+    ROW_BLOCK = 8192
+
+    def __init__(self, numFeatures: int, capacity_rows: int, capacity_nnz: int):
+        self._lib = N.load()
+        h = ctypes.c_void_p()
+        N.check(self._lib.cyc_tiles_create(int(numFeatures), int(capacity_rows),
+                                           int(capacity_nnz), ctypes.byref(h)))
+        self.handle = h
+        self.numFeatures = int(numFeatures)
+
+    def append(self, rowptr, colidx, values, stream=None):
+        n = int(rowptr.shape[0]) - 1
+        N.check(self._lib.cyc_tiles_append_dev(self.handle, N.ptr(rowptr), N.ptr(colidx),
+                                               N.ptr(values), n, N.stream_handle(stream)))
+        return self
+
+    @staticmethod
+    def from_csr(rowptr, colidx, values, numFeatures, stream=None):
+        n = int(rowptr.shape[0]) - 1
+        t = SparseTiles(numFeatures, n, int(colidx.shape[0]))
+        return t.append(rowptr, colidx, values, stream)
+
+    @property
+    def rows(self):
+        return int(self._lib.cyc_tiles_rows(self.handle))
+
+    @property
+    def nnz(self):
+        return int(self._lib.cyc_tiles_nnz(self.handle))
+
+    @property
+    def nbytes(self):
+        return int(self._lib.cyc_tiles_bytes(self.handle))
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._lib.cyc_tiles_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class DeviceInstanceBlock:
-    """InstanceBlock rows resident in HBM (dense or CSR, isTransposed=true)."""
+    """InstanceBlock rows resident in HBM (dense or CSR, isTransposed=true).
+    A sparse block may hold its CSR arrays, a SparseTiles layout, or both
+    (prepare(layout="tiles") derives the layout; release_csr() then drops the
+    CSR so the layout is the only copy)."""
 
     def __init__(self, labels, weights=None, X=None, rowptr=None, colidx=None, values=None,
-                 numFeatures=None):
+                 numFeatures=None, tiles=None):
         self.labels = labels
         self.weights = weights
         self.X = X
         self.rowptr, self.colidx, self.values = rowptr, colidx, values
+        self.tiles = tiles
         if X is not None:
             self.numFeatures = int(X.shape[1])
             self.size = int(X.shape[0])
@@ -44,7 +101,7 @@ class DeviceInstanceBlock:
             if numFeatures is None:
                 raise N.IllegalArgumentException("numFeatures is required for CSR blocks")
             self.numFeatures = int(numFeatures)
-            self.size = int(rowptr.shape[0]) - 1
+            self.size = int(rowptr.shape[0]) - 1 if rowptr is not None else tiles.rows
         if int(labels.shape[0]) != self.size:
             raise N.IllegalArgumentException("requirement failed")  # Instance.scala:43
         if weights is not None and int(weights.shape[0]) != self.size:
@@ -56,10 +113,17 @@ class DeviceInstanceBlock:
     def is_sparse(self):
         return self.X is None
 
-    def prepare(self, stream=None):
-        """Build the column-major copy of a CSR shard once (cyc_csc_build_dev),
-        so the sparse gradient runs as deterministic per-column sums instead
-        of an fp64-atomic scatter.  Costs 12 bytes per nonzero of HBM."""
+    def prepare(self, stream=None, layout="csc"):
+        """Derive a layout of a CSR shard once, outside the training loop.
+        layout="csc": the row-blocked column-major copy (cyc_csc_build_dev)
+        the multinomial / summarizer CSR paths use; layout="tiles": the
+        row-block x column-tile layout (SparseTiles) the binary aggregators
+        run on.  Either costs 12 bytes per nonzero of HBM."""
+        if self.is_sparse and layout == "tiles":
+            if self.tiles is None:
+                self.tiles = SparseTiles.from_csr(self.rowptr, self.colidx, self.values,
+                                                  self.numFeatures, stream)
+            return self
         if self.is_sparse and self.csc is None:
             h = ctypes.c_void_p()
             N.check(N.load().cyc_csc_build_dev(N.ptr(self.rowptr), N.ptr(self.colidx),
@@ -67,6 +131,14 @@ class DeviceInstanceBlock:
                                                N.stream_handle(stream), ctypes.byref(h)))
             self.csc = h
         return self
+
+    def release_csr(self):
+        """Drop the CSR arrays (and a CSC copy) once the tiles layout exists:
+        the binary aggregators then read only the layout."""
+        if self.tiles is None:
+            raise N.IllegalArgumentException("prepare(layout='tiles') first")
+        self.drop_derived()
+        self.rowptr = self.colidx = self.values = None
 
     def drop_derived(self):
         """Forget the CSC copy (after the values change, e.g. standardization)."""
@@ -238,6 +310,17 @@ def _check_block(agg, block):
             f"instance weights {'[' + ','.join(map(str, w)) + ']'} has to be >= 0.0")
 
 
+def _tiles_add(agg, block, stream, inverseStd=None):
+    """The binary aggregators' add over a block's SparseTiles layout
+    (cyc_binary_add_tiles_dev; the plan carries the loss kind)."""
+    N.check(N.load().cyc_binary_add_tiles_dev(
+        agg._plan.handle, block.tiles.handle, N.ptr(block.labels), N.ptr(block.weights),
+        N.ptr(agg.coef), N.ptr(inverseStd), N.ptr(agg.scaledMean),
+        N.ptr(agg.gradientSumArray), N.ptr(agg._loss_sum), N.ptr(agg._weight_sum),
+        N.stream_handle(stream)))
+    return agg
+
+
 class BinaryLogisticBlockAggregator(DifferentiableLossAggregator):
     """BinaryLogisticBlockAggregator(bcInverseStd, bcScaledMean, fitIntercept,
     fitWithMean)(bcCoefficients)."""
@@ -274,6 +357,8 @@ class BinaryLogisticBlockAggregator(DifferentiableLossAggregator):
         _check_block(self, block)
         lib = N.load()
         s = N.stream_handle(stream)
+        if block.is_sparse and block.tiles is not None:
+            return _tiles_add(self, block, stream)
         if block.is_sparse:
             N.check(lib.cyc_binary_logistic_add_csr_dev(
                 self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx), N.ptr(block.values),
@@ -320,6 +405,8 @@ class HingeBlockAggregator(DifferentiableLossAggregator):
         _check_block(self, block)
         lib = N.load()
         s = N.stream_handle(stream)
+        if block.is_sparse and block.tiles is not None:
+            return _tiles_add(self, block, stream)
         if block.is_sparse:
             N.check(lib.cyc_hinge_add_csr_dev(
                 self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx), N.ptr(block.values),
@@ -373,6 +460,8 @@ class LeastSquaresBlockAggregator(DifferentiableLossAggregator):
         _check_block(self, block)
         lib = N.load()
         s = N.stream_handle(stream)
+        if block.is_sparse and block.tiles is not None:
+            return _tiles_add(self, block, stream, self.inverseStd)
         if block.is_sparse:
             N.check(lib.cyc_least_squares_add_csr_dev(
                 self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx), N.ptr(block.values),
@@ -422,6 +511,8 @@ class HuberBlockAggregator(DifferentiableLossAggregator):
         _check_block(self, block)
         lib = N.load()
         s = N.stream_handle(stream)
+        if block.is_sparse and block.tiles is not None:
+            return _tiles_add(self, block, stream)
         if block.is_sparse:
             N.check(lib.cyc_huber_add_csr_dev(
                 self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx), N.ptr(block.values),
@@ -485,6 +576,8 @@ class AFTBlockAggregator(DifferentiableLossAggregator):
                 "requirement failed: The lifetime or label should be greater than 0.")
         lib = N.load()
         s = N.stream_handle(stream)
+        if block.is_sparse and block.tiles is not None:
+            return _tiles_add(self, block, stream)
         if block.is_sparse:
             N.check(lib.cyc_aft_add_csr_dev(
                 self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx), N.ptr(block.values),
@@ -552,6 +645,10 @@ class MultinomialLogisticBlockAggregator(DifferentiableLossAggregator):
         """MultinomialLogisticBlockAggregator.scala:101-189 over the shard."""
         _check_block(self, block)
         if block.is_sparse:
+            if block.rowptr is None:
+                raise N.IllegalArgumentException(
+                    "the multinomial aggregator needs the block's CSR rows (release_csr dropped "
+                    "them)")
             block.prepare(stream)          # CSC copy for the gradient (built once)
             N.check(N.load().cyc_multinomial_logistic_add_csr_dev(
                 self._plan.handle, N.ptr(block.rowptr), N.ptr(block.colidx),

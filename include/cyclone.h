@@ -212,14 +212,41 @@ int32_t cyc_csc_features(cyc_csc csc);
  * nblocks * numFeatures + 1 entries, block b / column c spanning
  * [colptr[b F + c], colptr[b F + c + 1]) of rowidx / values. */
 int cyc_csc_blocks(cyc_csc csc, int64_t* rows_per_block, int64_t* nblocks);
-/* For numFeatures > 2^18 the handle also holds a column-sliced CSR copy
- * (nslices slices of `width` columns, each a CSR over all rows: rowptrS has
- * nslices * n + 1 entries) that the margin pass walks slice by slice so the
- * gathered coefficients stay in L2.  nslices == 1: no sliced copy. */
-int cyc_csc_slices(cyc_csc csc, int32_t* nslices, int32_t* width, const int64_t** rowptrS,
-                   const int32_t** colS, const double** valS);
 int cyc_csc_arrays(cyc_csc csc, const int64_t** colptr, const int32_t** rowidx,
                    const double** values);
+
+/* Row-block x column-tile layout of a CSR shard (tiles.hip) for the binary
+ * aggregators' two sparse gemv (BinaryLogisticBlockAggregator.scala:97,130;
+ * ml/linalg/BLAS.scala:764-805): row blocks of cyc_tiles_row_block() = 8192
+ * rows, column tiles of 8192 columns, 12 bytes per nonzero (fp64 value +
+ * packed row/column ids) plus ~0.5 % offsets, so both gathers run from LDS.
+ * Built by appending CSR rows (rowptr[rows+1] of any base, colidx sorted
+ * within a row as in SparseVector, values) in order: every append except
+ * the last holds a whole number of row blocks.  Indices are validated with
+ * SparseVector's require messages (ml/linalg/Vectors.scala:617-625).  The
+ * CSR input is not referenced afterwards (free it: the layout is the shard's
+ * only copy).  capacity_*: upper bounds for the whole shard. */
+typedef struct cyc_tiles_s* cyc_tiles;
+int cyc_tiles_create(int32_t numFeatures, int64_t capacity_rows, int64_t capacity_nnz,
+                     cyc_tiles* out);
+int cyc_tiles_append_dev(cyc_tiles tiles, const int64_t* rowptr, const int32_t* colidx,
+                         const double* vals, int64_t rows, void* stream);
+int cyc_tiles_destroy(cyc_tiles tiles);
+int64_t cyc_tiles_rows(cyc_tiles tiles);
+int64_t cyc_tiles_nnz(cyc_tiles tiles);
+int32_t cyc_tiles_features(cyc_tiles tiles);
+int64_t cyc_tiles_bytes(cyc_tiles tiles);
+int32_t cyc_tiles_row_block(void);
+/* add() of the plan's binary aggregator over every row of the layout
+ * (BinaryLogisticBlockAggregator.scala:81-145, or the Hinge / LeastSquares /
+ * Huber / AFT plans' epilogues): labels / weights (AFT: censors; NULL =
+ * unit) have cyc_tiles_rows() entries; inverseStd is required by least
+ * squares plans (effectiveCoef) and ignored otherwise.  Two passes over the
+ * layout (margins, then gradient), deterministic. */
+int cyc_binary_add_tiles_dev(cyc_logistic_plan plan, cyc_tiles tiles, const double* labels,
+                             const double* weights, const double* coef, const double* inverseStd,
+                             const double* scaledMean, double* grad, double* lossSum,
+                             double* weightSum, void* stream);
 
 /* HingeBlockAggregator (ml/optim/aggregator/HingeBlockAggregator.scala:
  * 81-141, LinearSVC's loss): the binary kernels with the hinge epilogue

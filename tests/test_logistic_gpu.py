@@ -44,7 +44,7 @@ def _oracle_block(X, csr, labels, w, F):
     return dict(labels=labels, weights=w, X=X)
 
 
-@pytest.mark.parametrize("sparse", [False, True, "csc"])
+@pytest.mark.parametrize("sparse", [False, True, "csc", "tiles"])
 @pytest.mark.parametrize("fi,fwm", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("n,F", [(1, 3), (257, 17), (3000, 64), (2000, 300)])
 def test_binary_vs_oracle(cuda, sparse, fi, fwm, n, F):
@@ -56,8 +56,8 @@ def test_binary_vs_oracle(cuda, sparse, fi, fwm, n, F):
     st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
     oracle.binary_logistic_add(_oracle_block(X, csr, labels, w, F), coef, fi, fwm, sm, st)
     blk = DeviceInstanceBlock.from_numpy(labels, w, X=X, csr=csr, numFeatures=F, device=cuda)
-    if sparse == "csc":
-        blk.prepare()
+    if sparse in ("csc", "tiles"):
+        blk.prepare(layout=sparse)
     agg = BinaryLogisticBlockAggregator(np.ones(F), sm, fi, fwm, coef, device=cuda).add(blk)
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
@@ -144,56 +144,123 @@ def test_rdd_loss_function(cuda):
     _rel_close(grad, exp)
 
 
-def test_sparse_config5_shape_properties(cuda):
-    """Config 5 row shape (F = 1M, 64 nnz/row) on a 1M-row shard: a row subset
-    equals the oracle; the full shard's gradient equals the sum of two
-    half-shard calls (linearity of the merge)."""
+def _config5_rows(n, F, k, seed, cuda):
+    """BASELINE configs[4] row shape (bench.py's generator): k distinct
+    sorted columns per row, one per F/k band, values U(0, 1)."""
     import torch
-    from cycloneml_amd.optim import BinaryLogisticBlockAggregator, DeviceInstanceBlock
-    n, F, k = 1_000_000, 1_000_000, 64
-    g = torch.Generator(device=cuda).manual_seed(2)
-    cols = torch.sort(torch.randint(0, F, (n, k), generator=g, device=cuda), dim=1).values
-    cols = cols.to(torch.int32).reshape(-1)
-    vals = torch.rand(n * k, generator=g, device=cuda, dtype=torch.float64)
+    g = torch.Generator(device=cuda).manual_seed(seed)
+    band = F // k
+    cols = torch.empty(n * k, dtype=torch.int32, device=cuda)
+    vals = torch.empty(n * k, dtype=torch.float64, device=cuda)
+    step = 1 << 20
+    for s in range(0, n, step):
+        e = min(n, s + step)
+        c = (torch.arange(k, device=cuda) * band).unsqueeze(0) + \
+            torch.randint(0, band, (e - s, k), generator=g, device=cuda)
+        cols[s * k:e * k] = c.to(torch.int32).reshape(-1)
+        vals[s * k:e * k] = torch.rand((e - s) * k, generator=g, device=cuda, dtype=torch.float64)
     rowptr = torch.arange(0, n * k + 1, k, device=cuda, dtype=torch.int64)
     labels = (torch.rand(n, generator=g, device=cuda) < 0.5).to(torch.float64)
-    coef = torch.randn(F + 1, generator=g, device=cuda, dtype=torch.float64) * 0.01
+    return rowptr, cols, vals, labels
+
+
+def test_sparse_config5_csc_path(cuda):
+    """Config 5 row shape on a 1M-row shard through the CSR + CSC path: a row
+    subset equals the oracle, the CSC gradient equals the atomic one within
+    1e-10 and is bitwise reproducible."""
+    from cycloneml_amd.optim import BinaryLogisticBlockAggregator, DeviceInstanceBlock
+    import torch
+    n, F, k = 1_000_000, 1_000_000, 64
+    rowptr, cols, vals, labels = _config5_rows(n, F, k, 2, cuda)
+    coef = torch.randn(F + 1, generator=torch.Generator(device=cuda).manual_seed(3), device=cuda,
+                       dtype=torch.float64) * 0.01
+    sm = np.random.default_rng(4).uniform(0, 1, F) * 0.5
     blk = DeviceInstanceBlock(labels, None, rowptr=rowptr, colidx=cols, values=vals,
                               numFeatures=F)
-    agg = BinaryLogisticBlockAggregator(np.ones(F), None, True, False, coef, device=cuda).add(blk)
+    agg = BinaryLogisticBlockAggregator(np.ones(F), sm, True, True, coef, device=cuda).add(blk)
+    blk.prepare()
+    a3 = BinaryLogisticBlockAggregator(np.ones(F), sm, True, True, coef, device=cuda).add(blk)
+    a4 = BinaryLogisticBlockAggregator(np.ones(F), sm, True, True, coef, device=cuda).add(blk)
+    g3 = a3.gradientSumArray.cpu().numpy()
+    _rel_close(g3, agg.gradientSumArray.cpu().numpy(), rtol=1e-10)
+    assert np.array_equal(g3, a4.gradientSumArray.cpu().numpy())
     m = 20000
     st = dict(grad=np.zeros(F + 1), loss=0.0, weight=0.0)
     oracle.binary_logistic_add(dict(labels=labels[:m].cpu().numpy(), weights=None,
                                     rowptr=rowptr[:m + 1].cpu().numpy(),
                                     colidx=cols[:m * k].cpu().numpy(),
                                     values=vals[:m * k].cpu().numpy(), F=F),
-                               coef.cpu().numpy(), True, False, None, st)
+                               coef.cpu().numpy(), True, True, sm, st)
     sub = DeviceInstanceBlock(labels[:m], None, rowptr=rowptr[:m + 1], colidx=cols[:m * k],
-                              values=vals[:m * k], numFeatures=F)
-    a2 = BinaryLogisticBlockAggregator(np.ones(F), None, True, False, coef, device=cuda).add(sub)
-    _rel_close(a2.gradientSumArray.cpu().numpy(), st["grad"])
-    assert a2.weight == m and agg.weight == n
-    # deterministic CSC path: same result within tolerance, bitwise run to run
-    blk.prepare()
-    a3 = BinaryLogisticBlockAggregator(np.ones(F), None, True, False, coef, device=cuda).add(blk)
-    a4 = BinaryLogisticBlockAggregator(np.ones(F), None, True, False, coef, device=cuda).add(blk)
-    g3 = a3.gradientSumArray.cpu().numpy()
-    _rel_close(g3, agg.gradientSumArray.cpu().numpy(), rtol=1e-10)
-    assert np.array_equal(g3, a4.gradientSumArray.cpu().numpy())
-    sub.prepare()
-    a5 = BinaryLogisticBlockAggregator(np.ones(F), None, True, False, coef, device=cuda).add(sub)
+                              values=vals[:m * k], numFeatures=F).prepare()
+    a5 = BinaryLogisticBlockAggregator(np.ones(F), sm, True, True, coef, device=cuda).add(sub)
     _rel_close(a5.gradientSumArray.cpu().numpy(), st["grad"])
 
 
+@pytest.mark.timeout(600)
+def test_sparse_config5_bench_shard_tiles(cuda):
+    """bench.py's lr_sparse shard at its benched size (25M rows x 1M
+    features, 64 nonzeros per row, fitIntercept => fitWithMean with a real
+    scaledMean, LogisticRegression.scala:950-954), on the tiles layout built
+    by row-block-aligned appends with the CSR freed chunk by chunk, as the
+    bench does.  Checks: (1) the first 40,000 rows (5 row blocks) equal the
+    restatement within 1e-10; (2) linearity: the whole shard's state equals
+    the sum of its two halves' within 1e-12; (3) bitwise reproducible."""
+    import torch
+    from cycloneml_amd.optim import (BinaryLogisticBlockAggregator, DeviceInstanceBlock,
+                                     SparseTiles)
+    n, F, k = 25_000_000, 1_000_000, 64
+    chunk = 64 * 8192
+    half = (n // 2) // chunk * chunk
+    coef = np.random.default_rng(4).normal(size=F + 1) * 0.01
+    sm = np.random.default_rng(5).uniform(0, 1, F) * 0.5
+    whole = SparseTiles(F, n, n * k)
+    h1, h2 = SparseTiles(F, half, half * k), SparseTiles(F, n - half, (n - half) * k)
+    labels = torch.empty(n, dtype=torch.float64, device=cuda)
+    sub_m = 40_000
+    sub = None
+    for c, s in enumerate(range(0, n, chunk)):
+        e = min(n, s + chunk)
+        rp, ci, vv, lb = _config5_rows(e - s, F, k, 100 + c, cuda)
+        labels[s:e] = lb
+        whole.append(rp, ci, vv)
+        (h1 if s < half else h2).append(rp, ci, vv)
+        if s == 0:
+            sub = tuple(a.cpu().numpy() for a in (rp[:sub_m + 1], ci[:sub_m * k],
+                                                 vv[:sub_m * k], lb[:sub_m]))
+        del rp, ci, vv, lb
+    assert whole.rows == n and whole.nnz == n * k
+
+    def run(t, lab):
+        blk = DeviceInstanceBlock(lab, None, tiles=t, numFeatures=F)
+        return BinaryLogisticBlockAggregator(np.ones(F), sm, True, True, coef,
+                                             device=cuda).add(blk)._state.cpu().numpy()
+    full = run(whole, labels)
+    assert np.array_equal(full, run(whole, labels))
+    parts = run(h1, labels[:half]) + run(h2, labels[half:])
+    _rel_close(full, parts, rtol=1e-12)
+    del whole, h1, h2
+    rp, ci, vv, lb = sub
+    st = dict(grad=np.zeros(F + 1), loss=0.0, weight=0.0)
+    oracle.binary_logistic_add(dict(labels=lb, weights=None, rowptr=rp, colidx=ci, values=vv,
+                                    F=F), coef, True, True, sm, st)
+    ts = SparseTiles.from_csr(*(torch.as_tensor(a, device=cuda) for a in (rp, ci, vv)), F)
+    got = run(ts, torch.as_tensor(lb, device=cuda))
+    _rel_close(got[:F + 1], st["grad"])
+    assert abs(got[F + 1] - st["loss"]) <= 1e-12 * abs(st["loss"]) and got[F + 2] == sub_m
+
+
 @pytest.mark.parametrize("fi,fwm", [(True, False), (True, True), (False, False)])
-@pytest.mark.parametrize("n,F,nnz", [(700, 600_000, 40), (300, 1_100_000, 150), (50, 300_000, 1)])
-def test_binary_sliced_csr_vs_oracle(cuda, fi, fwm, n, F, nnz):
-    """numFeatures > 2^18: the prepared shard's margin pass walks a
-    column-sliced CSR copy (2-5 slices), empty rows and rows that span every
-    slice included; equals the restatement within 1e-10."""
-    from cycloneml_amd import _native as N
+@pytest.mark.parametrize("n,F,nnz", [(700, 600_000, 40), (300, 1_100_000, 150), (50, 300_000, 1),
+                                     (20_000, 30_000, 25), (9000, 8192, 300)])
+def test_binary_tiles_vs_oracle(cuda, fi, fwm, n, F, nnz):
+    """The row-block x column-tile layout: several column tiles (F up to
+    1.1M = 135 tiles), several row blocks (20000 rows = 3), empty rows, zero
+    weights, rows spanning every tile, and long sub-segment runs (9000 rows of
+    ~300 nonzeros in one tile: the batched tail path); equals the restatement
+    within 1e-10, the loss bit for bit-ish (same summation order), and is
+    bitwise reproducible run to run."""
     from cycloneml_amd.optim import BinaryLogisticBlockAggregator, DeviceInstanceBlock
-    import ctypes
     rng = np.random.default_rng(n + F // 1000 + nnz)
     X, csr, labels, w = _make(n, F, True, rng, nnz=nnz, zero_w=True)
     coef = rng.normal(size=F + (1 if fi else 0)) * 0.5
@@ -201,17 +268,66 @@ def test_binary_sliced_csr_vs_oracle(cuda, fi, fwm, n, F, nnz):
     st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
     oracle.binary_logistic_add(_oracle_block(X, csr, labels, w, F), coef, fi, fwm, sm, st)
     blk = DeviceInstanceBlock.from_numpy(labels, w, X=None, csr=csr, numFeatures=F, device=cuda)
-    blk.prepare()
-    S = ctypes.c_int32(0)
-    N.check(N.load().cyc_csc_slices(blk.csc, ctypes.byref(S), None, None, None, None))
-    assert S.value == (F + (1 << 18) - 1) >> 18
+    blk.prepare(layout="tiles").release_csr()
+    assert blk.tiles.rows == n and blk.tiles.nnz == csr[1].size
     agg = BinaryLogisticBlockAggregator(np.ones(F), sm, fi, fwm, coef, device=cuda).add(blk)
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
-    assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * abs(st["loss"])
+    assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-12 * abs(st["loss"])
+    again = BinaryLogisticBlockAggregator(np.ones(F), sm, fi, fwm, coef, device=cuda).add(blk)
+    assert np.array_equal(agg._state.cpu().numpy(), again._state.cpu().numpy())
 
 
-@pytest.mark.parametrize("sparse", [False, True, "csc"])
+def test_tiles_appends_and_requires(cuda):
+    """Appending whole row blocks in pieces builds the same layout as one
+    append; a partial row block seals the layout; SparseVector's index
+    requires (ml/linalg/Vectors.scala:617-625) come back with the reference's
+    text; capacity and dimension checks."""
+    import torch
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.optim import (BinaryLogisticBlockAggregator, DeviceInstanceBlock,
+                                     SparseTiles)
+    rng = np.random.default_rng(9)
+    n, F = 3 * 8192 + 100, 20_000
+    X, csr, labels, w = _make(n, F, True, rng, nnz=12)
+    rp, ci, vv = (torch.as_tensor(a, device=cuda) for a in csr)
+    coef = rng.normal(size=F + 1) * 0.3
+    one = SparseTiles.from_csr(rp, ci, vv, F)
+    parts = SparseTiles(F, n, ci.numel())
+    for a, b in [(0, 8192), (8192, 3 * 8192), (3 * 8192, n)]:
+        q0, q1 = int(csr[0][a]), int(csr[0][b])    # rowptr of any base
+        parts.append(rp[a:b + 1], ci[q0:q1], vv[q0:q1])
+    with pytest.raises(N.IllegalArgumentException, match="partial row block"):
+        parts.append(rp[:2], ci, vv)
+    lab = torch.as_tensor(labels, device=cuda)
+    res = []
+    for t in (one, parts):
+        blk = DeviceInstanceBlock(lab, None, tiles=t, numFeatures=F)
+        res.append(BinaryLogisticBlockAggregator(np.ones(F), None, True, False, coef,
+                                                 device=cuda).add(blk)._state.cpu().numpy())
+    assert np.array_equal(res[0], res[1])
+
+    def bad(rows, msg):
+        rpb = torch.as_tensor(np.array([0] + list(np.cumsum([len(r) for r in rows])),
+                                       dtype=np.int64), device=cuda)
+        cib = torch.as_tensor(np.array(sum(rows, []), dtype=np.int32), device=cuda)
+        vvb = torch.ones(cib.numel(), dtype=torch.float64, device=cuda)
+        with pytest.raises(N.IllegalArgumentException) as e:
+            SparseTiles.from_csr(rpb, cib, vvb, 10)
+        assert str(e.value) == "requirement failed: " + msg
+    bad([[0, 1], [2, -1, 3]], "Index -1 follows 2 and is not strictly increasing")
+    bad([[0], [-3, 4]], "Found negative index: -3.")
+    bad([[1, 1]], "Index 1 follows 1 and is not strictly increasing")
+    bad([[], [3, 9], [2, 10]], "Index 10 out of bounds for vector of size 10")
+    with pytest.raises(N.IllegalArgumentException, match="exceeds the capacity"):
+        SparseTiles(F, 10, 1000).append(rp[:12], ci, vv)
+    blk = DeviceInstanceBlock(lab, None, tiles=one, numFeatures=F)
+    with pytest.raises(N.IllegalArgumentException, match="Dimensions mismatch"):
+        BinaryLogisticBlockAggregator(np.ones(F + 1), None, True, False, np.zeros(F + 2),
+                                      device=cuda).add(blk)
+
+
+@pytest.mark.parametrize("sparse", [False, True, "csc", "tiles"])
 @pytest.mark.parametrize("fi", [False, True])
 @pytest.mark.parametrize("n,F", [(1, 3), (257, 17), (3000, 64), (2000, 300)])
 def test_hinge_vs_oracle(cuda, sparse, fi, n, F):
@@ -225,17 +341,17 @@ def test_hinge_vs_oracle(cuda, sparse, fi, n, F):
     st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
     oracle.hinge_add(_oracle_block(X, csr, labels, w, F), coef, fi, sm, st)
     blk = DeviceInstanceBlock.from_numpy(labels, w, X=X, csr=csr, numFeatures=F, device=cuda)
-    if sparse == "csc":
-        blk.prepare()
+    if sparse in ("csc", "tiles"):
+        blk.prepare(layout=sparse)
     agg = HingeBlockAggregator(np.ones(F), sm, fi, coef, device=cuda).add(blk)
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
     assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * max(abs(st["loss"]), 1e-300)
 
 
-def test_hinge_sliced_csr_and_plan_kinds(cuda):
-    """numFeatures > 2^18 (column-sliced margin pass) with the hinge
-    epilogue; a hinge plan refuses the logistic entry point and vice versa."""
+def test_hinge_tiles_large_f_and_plan_kinds(cuda):
+    """numFeatures = 600K (74 column tiles) with the hinge epilogue; a hinge
+    plan refuses the logistic entry point and vice versa."""
     import ctypes
     from cycloneml_amd import _native as N
     from cycloneml_amd.optim import DeviceInstanceBlock, HingeBlockAggregator
@@ -247,7 +363,7 @@ def test_hinge_sliced_csr_and_plan_kinds(cuda):
     st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
     oracle.hinge_add(_oracle_block(X, csr, labels, w, F), coef, True, sm, st)
     blk = DeviceInstanceBlock.from_numpy(labels, w, X=None, csr=csr, numFeatures=F, device=cuda)
-    blk.prepare()
+    blk.prepare(layout="tiles")
     agg = HingeBlockAggregator(np.ones(F), sm, True, coef, device=cuda).add(blk)
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * abs(st["loss"])
@@ -260,7 +376,7 @@ def test_hinge_sliced_csr_and_plan_kinds(cuda):
     lib.cyc_logistic_plan_destroy(h)
 
 
-@pytest.mark.parametrize("sparse", [False, True, "csc"])
+@pytest.mark.parametrize("sparse", [False, True, "csc", "tiles"])
 @pytest.mark.parametrize("fi", [False, True])
 @pytest.mark.parametrize("n,F", [(1, 3), (257, 17), (3000, 64), (2000, 300)])
 def test_least_squares_vs_oracle(cuda, sparse, fi, n, F):
@@ -280,8 +396,8 @@ def test_least_squares_vs_oracle(cuda, sparse, fi, n, F):
     oracle.least_squares_add(_oracle_block(X, csr, labels, w, F), coef, inv, fi, ystd, ymean, sm,
                              st)
     blk = DeviceInstanceBlock.from_numpy(labels, w, X=X, csr=csr, numFeatures=F, device=cuda)
-    if sparse == "csc":
-        blk.prepare()
+    if sparse in ("csc", "tiles"):
+        blk.prepare(layout=sparse)
     agg = LeastSquaresBlockAggregator(inv, sm, fi, ystd, ymean, coef, device=cuda).add(blk)
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
@@ -295,7 +411,7 @@ def test_least_squares_requires(cuda):
         LeastSquaresBlockAggregator(np.ones(3), None, False, 0.0, 0.0, np.zeros(3), device=cuda)
 
 
-@pytest.mark.parametrize("sparse", [False, True, "csc"])
+@pytest.mark.parametrize("sparse", [False, True, "csc", "tiles"])
 @pytest.mark.parametrize("fi", [False, True])
 @pytest.mark.parametrize("n,F", [(1, 3), (257, 17), (3000, 64), (2000, 300)])
 def test_huber_vs_oracle(cuda, sparse, fi, n, F):
@@ -311,15 +427,15 @@ def test_huber_vs_oracle(cuda, sparse, fi, n, F):
     st = dict(grad=np.zeros(params.size), loss=0.0, weight=0.0)
     oracle.huber_add(_oracle_block(X, csr, labels, w, F), params, fi, 1.35, sm, st)
     blk = DeviceInstanceBlock.from_numpy(labels, w, X=X, csr=csr, numFeatures=F, device=cuda)
-    if sparse == "csc":
-        blk.prepare()
+    if sparse in ("csc", "tiles"):
+        blk.prepare(layout=sparse)
     agg = HuberBlockAggregator(np.ones(F), sm, fi, 1.35, params, device=cuda).add(blk)
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
     assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-10 * abs(st["loss"])
 
 
-@pytest.mark.parametrize("sparse", [False, True, "csc"])
+@pytest.mark.parametrize("sparse", [False, True, "csc", "tiles"])
 @pytest.mark.parametrize("fi", [False, True])
 @pytest.mark.parametrize("n,F", [(1, 3), (257, 17), (3000, 64), (2000, 300)])
 def test_aft_vs_oracle(cuda, sparse, fi, n, F):
@@ -336,8 +452,8 @@ def test_aft_vs_oracle(cuda, sparse, fi, n, F):
     st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
     oracle.aft_add(_oracle_block(X, csr, labels, cens, F), coef, fi, sm, st)
     blk = DeviceInstanceBlock.from_numpy(labels, cens, X=X, csr=csr, numFeatures=F, device=cuda)
-    if sparse == "csc":
-        blk.prepare()
+    if sparse in ("csc", "tiles"):
+        blk.prepare(layout=sparse)
     agg = AFTBlockAggregator(sm, fi, coef, device=cuda).add(blk)
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert agg.weight == st["weight"] == n
