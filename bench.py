@@ -270,9 +270,10 @@ class LRMultiWorkload:
             sq += (X[s:s + (1 << 22)] ** 2).sum(0)
         mean /= n
         std = (sq / n - mean ** 2).clamp_min(0).sqrt()
-        self.scaledMean = (mean / std).cpu().numpy()
+        sm_dev = mean / std                                        # bcScaledMean, once
+        self.scaledMean = sm_dev.cpu().numpy()
         self.fn = RDDLossFunction([self.block], lambda c: MultinomialLogisticBlockAggregator(
-            np.ones(F), self.scaledMean, True, True, c, device=dev))
+            np.ones(F), sm_dev, True, True, c, device=dev))
 
     def step(self):
         self.fn.calculate(self.coef)
@@ -371,8 +372,9 @@ class LRSparseWorkload:
         # scaledMean = mean / std per feature: nonzero with probability k / F,
         # values U(0, 1) -- mean ~ 3.2e-5, std ~ 4.6e-3 -> scaledMean ~ 7e-3
         self.scaledMean = np.random.default_rng(5).uniform(0.0, 0.014, F)
+        sm_dev = torch.as_tensor(self.scaledMean, device=dev)    # bcScaledMean, once
         self.fn = RDDLossFunction([self.block], lambda c: BinaryLogisticBlockAggregator(
-            np.ones(F), self.scaledMean, True, True, c, device=dev))
+            np.ones(F), sm_dev, True, True, c, device=dev))
 
     def step(self):
         self.fn.calculate(self.coef)

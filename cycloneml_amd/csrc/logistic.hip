@@ -370,11 +370,26 @@ __global__ void k_binlog_fold(const double* __restrict__ slabG, int64_t waves,
 // marginOffset: coef[F] - ddot(coef, scaledMean) (Binary :67-72, Hinge
 // :62-71), or for least squares (:57-62) labelMean / labelStd - ddot(...)
 // (base passed in, useBase = 1).
-__global__ void k_binlog_offset(const double* __restrict__ coef, const double* __restrict__ sm,
-                                int F, int useBase, double base, double* __restrict__ out) {
+// One 1024-thread workgroup: thread t sums its contiguous stretch of the
+// products in index order, then a fixed tree -- deterministic (the
+// reference's sequential ddot order is not pinned below 1e-10 anyway).
+__global__ __launch_bounds__(1024) void k_binlog_offset(const double* __restrict__ coef,
+                                                        const double* __restrict__ sm, int F,
+                                                        int useBase, double base,
+                                                        double* __restrict__ out) {
+  __shared__ double sh[1024];
+  const int t = threadIdx.x;
+  const int per = (F + 1023) / 1024;
+  const int f0 = t * per, f1 = min(F, f0 + per);
   double dd = 0.0;
-  for (int f = 0; f < F; ++f) dd += coef[f] * sm[f];
-  out[0] = (useBase ? base : coef[F]) - dd;
+  for (int f = f0; f < f1; ++f) dd += coef[f] * sm[f];
+  sh[t] = dd;
+  __syncthreads();
+  for (int h = 512; h > 0; h >>= 1) {
+    if (t < h) sh[t] += sh[t + h];
+    __syncthreads();
+  }
+  if (t == 0) out[0] = (useBase ? base : coef[F]) - sh[0];
 }
 
 // LeastSquaresBlockAggregator.effectiveCoef (:48-55): coefficient or 0.0
@@ -966,7 +981,7 @@ int binary_offset(cyc_logistic_plan p, const double* coef, const double* scaledM
   *offset = 0.0;
   if (!p->fitIntercept) return CYC_OK;
   if (p->fitWithMean || p->loss == 2) {
-    hipLaunchKernelGGL(k_binlog_offset, dim3(1), dim3(1), 0, st, coef, scaledMean, p->F,
+    hipLaunchKernelGGL(k_binlog_offset, dim3(1), dim3(1024), 0, st, coef, scaledMean, p->F,
                        p->loss == 2 ? 1 : 0, p->labelMean / p->labelStd, (double*)p->offset.ptr);
     CYC_LAUNCH_CHECK("k_binlog_offset");
     CYC_HIP(hipMemcpyAsync(offset, p->offset.ptr, sizeof(double), hipMemcpyDeviceToHost, st));

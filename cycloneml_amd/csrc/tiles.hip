@@ -69,7 +69,7 @@ using cyc::kTileWaves;
 constexpr int kTPB = 512;                      // threads per workgroup (8 waves)
 constexpr int kCPT = kTileCols / kTPB;         // coefficient / gradient entries per thread
 constexpr int kRPT = kTileRows / kTPB;         // rows per thread
-constexpr int kCap = 12;                       // nonzeros per lane prefetched per segment
+constexpr int kCap = 10;                       // nonzeros per lane prefetched per run
 
 // ----------------------------------------------------------------- build
 
@@ -144,107 +144,134 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t by
                                            (int)std::min<int64_t>(bytes, 0x7fffffff), 0x00020000);
 }
 
-// Margin pass, persistent over row blocks.  Per column tile: the coefficient
-// tile goes registers -> LDS (the next one is loaded while this one is used),
-// and each wave walks its row range's sub-segments (one contiguous run) with
-// the next tile's run already in flight in registers.
+// Margin pass, persistent over (row block, column tile) steps: this
+// workgroup's row blocks rb = blockIdx.x + i * gridDim.x, each swept over the
+// T column tiles, as one flat sequence of steps g.  Per step: the
+// coefficient tile goes registers -> LDS (the next step's tile is loaded
+// meanwhile, an L2 hit), and each wave walks its row range's sub-segments
+// (one contiguous run); the runs of the next TWO steps are in flight in
+// registers (~100 KB per CU), across row-block boundaries too.
+// The layout's arrays come as separate __restrict__ arguments: the
+// per-step segment offsets are uniform, and only restrict-qualified
+// read-only pointers let the compiler fetch them with scalar loads (counted
+// by lgkmcnt), so reading them never waits on the runs in flight (vmcnt).
+struct TileDims {
+  int64_t n, nRB;
+  int F, T, Wt;
+};
+
 __global__ __launch_bounds__(kTPB) void k_tiles_margin(
-    cyc::TilesView v, const double* __restrict__ labels, const double* __restrict__ weights,
+    TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ subRel,
+    const uint32_t* __restrict__ vidx, const double* __restrict__ vvals,
+    const double* __restrict__ labels, const double* __restrict__ weights,
     const double* __restrict__ coef, int fitIntercept, int kind, double offset, double lscale,
     double sigma, double eps, double* __restrict__ mult, double* __restrict__ slabS) {
-  __shared__ double dots[kTileRows];
+  // dots[kTileRows + lane]: a per-lane sink for masked lanes (no branches,
+  // no shared address among them)
+  __shared__ double dots[kTileRows + 64];
   __shared__ double cf[kTileCols];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T = v.T;
-  double loss = 0.0, wsum = 0.0, msum = 0.0, sgs = 0.0;
+  const uint32_t sink = (uint32_t)(kTileRows + lane) << 16;
+  // steps per row block padded to a multiple of 3 (the unroll of the run
+  // buffers); the padding steps have empty runs and fetch nothing
+  const int Tp = (T + 2) / 3 * 3;
+  const int64_t myRB = v.nRB > blockIdx.x ? (v.nRB - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const int64_t G = myRB * Tp;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};     // loss, weight, multiplierSum, sigmaGradSum
   double creg[kCPT];
-  uint32_t iA[kCap], iB[kCap];
-  double vA[kCap], vB[kCap];
-  int64_t sA = 0, lA = 0, sB = 0, lB = 0;
+  uint32_t iA[kCap], iB[kCap], iC[kCap];
+  double vA[kCap], vB[kCap], vC[kCap];
+  int64_t sA = 0, lA = 0, sB = 0, lB = 0, sC = 0, lC = 0;
 
-  for (int64_t rb = blockIdx.x; rb < v.nRB; rb += gridDim.x) {
-    auto run_of = [&](int t, int64_t& s0, int64_t& len) {
-      if (t >= T) {      // past the last tile: an empty run (its loads fetch nothing)
-        s0 = 0;
-        len = 0;
-        return;
-      }
-      const int64_t seg = rb * T + t;
-      const int64_t base = v.segStart[seg];
-      const uint32_t* sr = v.subRel + seg * kTileSub;
-      const uint32_t a = sr[wave * kTileWaves];
-      const uint32_t b = wave == kTileWaves - 1 ? (uint32_t)(v.segStart[seg + 1] - base)
-                                                : sr[(wave + 1) * kTileWaves];
-      s0 = base + a;
-      len = (int64_t)b - (int64_t)a;
-    };
-    auto load_run = [&](int64_t s0, int64_t len, uint32_t (&ix)[kCap], double (&vx)[kCap]) {
-      const auto ri = rsrc(v.idx + s0, len * 4);
-      const auto rv = rsrc(v.vals + s0, len * 8);
+  auto rb_of = [&](int64_t g) { return (int64_t)blockIdx.x + (g / Tp) * gridDim.x; };
+  auto run_of = [&](int64_t g, int64_t& s0, int64_t& len) {
+    if (g >= G || g % Tp >= T) {   // past the end, or a padding step: an empty run
+      s0 = 0;
+      len = 0;
+      return;
+    }
+    const int64_t seg = rb_of(g) * T + g % Tp;
+    const int64_t base = segStart[seg];
+    const uint32_t* sr = subRel + seg * kTileSub;
+    const uint32_t a = sr[wave * kTileWaves];
+    const uint32_t b = wave == kTileWaves - 1 ? (uint32_t)(segStart[seg + 1] - base)
+                                              : sr[(wave + 1) * kTileWaves];
+    s0 = base + a;
+    len = (int64_t)b - (int64_t)a;
+  };
+  auto load_run = [&](int64_t s0, int64_t len, uint32_t (&ix)[kCap], double (&vx)[kCap]) {
+    const auto ri = rsrc(vidx + s0, len * 4);
+    const auto rv = rsrc(vvals + s0, len * 8);
+    // lane part in the VGPR offset, chunk part in the scalar offset: one
+    // offset register for all kCap loads
 #pragma unroll
-      for (int j = 0; j < kCap; ++j) {
-        const int off = j * 64 + lane;
-        ix[j] = __builtin_amdgcn_raw_buffer_load_b32(ri, off * 4, 0, 2);
-        vx[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, off * 8, 0, 2));
-      }
-    };
-    auto load_coef = [&](int t) {
-      const int64_t c0 = (int64_t)t * v.Wt;
-      const int wl = t < T ? (int)std::min<int64_t>(v.Wt, v.F - c0) : 0;
-      const auto rc = rsrc(coef + c0, (int64_t)wl * 8);
+    for (int j = 0; j < kCap; ++j) {
+      ix[j] = __builtin_amdgcn_raw_buffer_load_b32(ri, lane * 4, j * 256, 2);
+      vx[j] = __builtin_bit_cast(double,
+                                 __builtin_amdgcn_raw_buffer_load_b64(rv, lane * 8, j * 512, 2));
+    }
+  };
+  auto load_coef = [&](int64_t g) {
+    const int t = (int)(g % Tp);
+    const int64_t c0 = t < T ? (int64_t)t * v.Wt : 0;
+    const int wl = (g < G && t < T) ? (int)std::min<int64_t>(v.Wt, v.F - c0) : 0;
+    const auto rc = rsrc(coef + c0, (int64_t)wl * 8);
 #pragma unroll
-      for (int i = 0; i < kCPT; ++i)
-        creg[i] = __builtin_bit_cast(
-            double, __builtin_amdgcn_raw_buffer_load_b64(rc, (tid + kTPB * i) * 8, 0, 0));
-    };
-    auto consume = [&](int64_t len, const uint32_t (&ix)[kCap], const double (&vx)[kCap]) {
+    for (int i = 0; i < kCPT; ++i)
+      creg[i] = __builtin_bit_cast(
+          double, __builtin_amdgcn_raw_buffer_load_b64(rc, tid * 8, i * kTPB * 8, 0));
+  };
+  // branch-free: all gathers issue together, masked lanes add 0 to their sink
+  auto consume = [&](int64_t len, const uint32_t (&ix)[kCap], const double (&vx)[kCap]) {
+    double c[kCap];
 #pragma unroll
-      for (int j = 0; j < kCap; ++j) {
-        if (j * 64 + lane < len) {
-          const uint32_t q = ix[j];
-          lds_add(&dots[q >> 16], vx[j] * cf[q & 0xffff]);
-        }
-      }
-    };
-    // a run longer than the prefetched kCap x 64 nonzeros: the rest in
-    // batches of the same size (all loads of a batch in flight together)
-    auto process = [&](int64_t s0, int64_t len, uint32_t (&ix)[kCap],
-                       double (&vx)[kCap]) {
-      consume(len, ix, vx);
-      for (int64_t b = kCap * 64; b < len; b += kCap * 64) {
-        load_run(s0 + b, len - b, ix, vx);
-        consume(len - b, ix, vx);
-      }
-    };
+    for (int j = 0; j < kCap; ++j) c[j] = cf[(j * 64 + lane < len ? ix[j] : sink) & 0xffff];
+#pragma unroll
+    for (int j = 0; j < kCap; ++j) {
+      const bool on = j * 64 + lane < len;
+      lds_add(&dots[(on ? ix[j] : sink) >> 16], on ? vx[j] * c[j] : 0.0);
+    }
+  };
+  // One step g: coefficient tile to LDS, the loads of step g + 1's tile and
+  // step g + 2's run issued (unconditionally: past the end they fetch
+  // nothing, so the waits for the current run stay counted), the current
+  // run into the row sums, the epilogue after a row block's last tile.  The
+  // three run buffers rotate by unrolling (never by copying a register that
+  // a load is still filling).
+  auto step = [&](int64_t g, int64_t sc, int64_t lc, uint32_t (&ic)[kCap], double (&vc)[kCap],
+                  int64_t& sn, int64_t& ln, uint32_t (&in)[kCap], double (&vn)[kCap]) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kCPT; ++i) cf[tid + kTPB * i] = creg[i];
+    load_coef(g + 1);
+    run_of(g + 2, sn, ln);
+    load_run(sn, ln, in, vn);
+    __syncthreads();
+    consume(lc, ic, vc);
+    for (int64_t b = kCap * 64; b < lc; b += kCap * 64) {   // rare: a long run
+      load_run(sc + b, lc - b, ic, vc);
+      consume(lc - b, ic, vc);
+    }
+  };
+
+  load_coef(0);
+  run_of(0, sA, lA);
+  load_run(sA, lA, iA, vA);
+  run_of(1, sB, lB);
+  load_run(sB, lB, iB, vB);
+  for (int64_t g0 = 0; g0 < G; g0 += Tp) {      // one row block per pass
 #pragma unroll
     for (int i = 0; i < kRPT; ++i) dots[tid + kTPB * i] = 0.0;
-    load_coef(0);
-    run_of(0, sA, lA);
-    load_run(sA, lA, iA, vA);
-    for (int t = 0; t < T; ++t) {
-      // coefficients of tile t to LDS; tile t + 1's loads issued
-      // unconditionally (past the last tile they fetch nothing, so the
-      // waits for tile t's run stay counted); tile t's run into the sums
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < kCPT; ++i) cf[tid + kTPB * i] = creg[i];
-      load_coef(t + 1);
-      run_of(t + 1, sB, lB);
-      load_run(sB, lB, iB, vB);
-      __syncthreads();
-      process(sA, lA, iA, vA);
-      sA = sB;
-      lA = lB;
-#pragma unroll
-      for (int j = 0; j < kCap; ++j) {
-        iA[j] = iB[j];
-        vA[j] = vB[j];
-      }
+    for (int64_t g = g0; g < g0 + Tp; g += 3) {
+      step(g, sA, lA, iA, vA, sC, lC, iC, vC);
+      step(g + 1, sB, lB, iB, vB, sA, lA, iA, vA);
+      step(g + 2, sC, lC, iC, vC, sB, lB, iB, vB);
     }
     __syncthreads();
     // epilogue (BinaryLogisticBlockAggregator.scala:104-122 and siblings)
-#pragma unroll 1
+    const int64_t rb = rb_of(g0);
     for (int i = 0; i < kRPT; ++i) {
       const int rl = tid + kTPB * i;
       const int64_t r = rb * kTileRows + rl;
@@ -252,8 +279,8 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
         const double label = labels[r];
         const double margin = cyc::row_margin(kind, fitIntercept, offset, lscale, label, dots[rl]);
         const double w = weights ? weights[r] : 1.0;
-        const double m = cyc::bin_row(kind, margin, w, label, loss, wsum, sgs, sigma, eps);
-        msum += m;
+        const double m = cyc::bin_row(kind, margin, w, label, acc[0], acc[1], acc[3], sigma, eps);
+        acc[2] += m;
         mult[r] = m;
       }
     }
@@ -261,18 +288,13 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
   // workgroup partials: fixed shuffle tree per wave, then waves in order
   __shared__ double red[kTileWaves][4];
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    loss += __shfl_xor(loss, m);
-    wsum += __shfl_xor(wsum, m);
-    msum += __shfl_xor(msum, m);
-    sgs += __shfl_xor(sgs, m);
-  }
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) acc[k] += __shfl_xor(acc[k], m);
   __syncthreads();
   if (lane == 0) {
-    red[wave][0] = loss;
-    red[wave][1] = wsum;
-    red[wave][2] = msum;
-    red[wave][3] = sgs;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[wave][k] = acc[k];
   }
   __syncthreads();
   if (tid < 4) {
@@ -293,21 +315,23 @@ struct GradRun {
   uint32_t cum[kTileWaves + 1];     // prefix lengths
 };
 
-__global__ __launch_bounds__(kTPB) void k_tiles_grad(cyc::TilesView v,
-                                                     const double* __restrict__ mult, int ranges,
-                                                     double* __restrict__ slabG) {
-  __shared__ double gt[kTileCols];
+__global__ __launch_bounds__(kTPB) void k_tiles_grad(
+    TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ subRel,
+    const uint32_t* __restrict__ vidx, const double* __restrict__ vvals,
+    const double* __restrict__ mult, int ranges, double* __restrict__ slabG) {
+  __shared__ double gt[kTileCols + 64];     // + a per-lane sink for masked lanes
   __shared__ double mv[kTileRows];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t sink = (uint32_t)(kTileCols + lane);
   const int range = blockIdx.x % ranges, t = blockIdx.x / ranges;
   const int64_t rbA = v.nRB * range / ranges, rbB = v.nRB * (range + 1) / ranges;
   const int64_t c0 = (int64_t)t * v.Wt;
   const int wl = (int)std::min<int64_t>(v.Wt, v.F - c0);
   double mreg[kRPT];
-  uint32_t iA[kCap], iB[kCap];
-  double vA[kCap], vB[kCap];
-  GradRun rA, rB;
+  uint32_t iA[kCap], iB[kCap], iC[kCap];
+  double vA[kCap], vB[kCap], vC[kCap];
+  GradRun rA, rB, rC;
 
   auto run_of = [&](int64_t rb, GradRun& r) {
     if (rb >= rbB) {     // past the range: an empty run (its loads read element 0)
@@ -318,9 +342,9 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(cyc::TilesView v,
       return;
     }
     const int64_t seg = rb * v.T + t;
-    r.base = v.segStart[seg];
-    const uint32_t segLen = (uint32_t)(v.segStart[seg + 1] - r.base);
-    const uint32_t* sr = v.subRel + seg * kTileSub;
+    r.base = segStart[seg];
+    const uint32_t segLen = (uint32_t)(segStart[seg + 1] - r.base);
+    const uint32_t* sr = subRel + seg * kTileSub;
     uint32_t acc = 0;
 #pragma unroll
     for (int k = 0; k < kTileWaves; ++k) {
@@ -346,8 +370,8 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(cyc::TilesView v,
     for (int j = 0; j < kCap; ++j) {
       const uint32_t p = p0 + j * 64 + lane;
       const int64_t s = p < r.cum[kTileWaves] ? elem(r, p) : 0;   // masked lanes: element 0
-      ix[j] = __builtin_nontemporal_load(v.idx + s);
-      vx[j] = __builtin_nontemporal_load(v.vals + s);
+      ix[j] = __builtin_nontemporal_load(vidx + s);
+      vx[j] = __builtin_nontemporal_load(vvals + s);
     }
   };
   auto load_mult = [&](int64_t rb) {
@@ -357,44 +381,54 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(cyc::TilesView v,
 #pragma unroll
     for (int i = 0; i < kRPT; ++i)
       mreg[i] = __builtin_bit_cast(
-          double, __builtin_amdgcn_raw_buffer_load_b64(rm, (tid + kTPB * i) * 8, 0, 0));
+          double, __builtin_amdgcn_raw_buffer_load_b64(rm, tid * 8, i * kTPB * 8, 0));
   };
   auto consume = [&](int64_t rem, const uint32_t (&ix)[kCap], const double (&vx)[kCap]) {
+    double m[kCap];
+#pragma unroll
+    for (int j = 0; j < kCap; ++j) m[j] = mv[(j * 64 + lane < rem ? ix[j] : 0u) >> 16];
 #pragma unroll
     for (int j = 0; j < kCap; ++j) {
-      if (j * 64 + lane < rem) {
-        const uint32_t q = ix[j];
-        lds_add(&gt[q & 0xffff], vx[j] * mv[q >> 16]);
-      }
+      const bool on = j * 64 + lane < rem;
+      lds_add(&gt[on ? (ix[j] & 0xffff) : sink], on ? vx[j] * m[j] : 0.0);
     }
   };
 
 #pragma unroll
   for (int i = 0; i < kCPT; ++i) gt[tid + kTPB * i] = 0.0;
-  load_mult(rbA);
-  run_of(rbA, rA);
-  load_run(rA, 0, iA, vA);
-  for (int64_t rb = rbA; rb < rbB; ++rb) {
+  // one row block: multiplier slice to LDS, the next slice and the run two
+  // row blocks ahead issued (unconditionally), the current run into the
+  // column sums; run buffers rotate by unrolling
+  auto step = [&](int64_t rb, const GradRun& rc, uint32_t (&ic)[kCap], double (&vc)[kCap],
+                  GradRun& rn, uint32_t (&in)[kCap], double (&vn)[kCap]) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kRPT; ++i) mv[tid + kTPB * i] = mreg[i];
     load_mult(rb + 1);
-    run_of(rb + 1, rB);
-    load_run(rB, 0, iB, vB);
+    run_of(rb + 2, rn);
+    load_run(rn, 0, in, vn);
     __syncthreads();
-    const uint32_t len = rA.cum[kTileWaves];
-    consume(len, iA, vA);
+    const uint32_t len = rc.cum[kTileWaves];
+    consume(len, ic, vc);
     for (uint32_t b = kCap * 64; b < len; b += kCap * 64) {   // rare: a long run
-      load_run(rA, b, iA, vA);
-      consume(len - b, iA, vA);
+      load_run(rc, b, ic, vc);
+      consume(len - b, ic, vc);
     }
-    rA = rB;
-#pragma unroll
-    for (int j = 0; j < kCap; ++j) {
-      iA[j] = iB[j];
-      vA[j] = vB[j];
-    }
+  };
+
+  load_mult(rbA);
+  run_of(rbA, rA);
+  load_run(rA, 0, iA, vA);
+  run_of(rbA + 1, rB);
+  load_run(rB, 0, iB, vB);
+  int64_t rb = rbA;
+  for (; rb + 3 <= rbB; rb += 3) {
+    step(rb, rA, iA, vA, rC, iC, vC);
+    step(rb + 1, rB, iB, vB, rA, iA, vA);
+    step(rb + 2, rC, iC, vC, rB, iB, vB);
   }
+  if (rb < rbB) step(rb, rA, iA, vA, rC, iC, vC);
+  if (rb + 1 < rbB) step(rb + 1, rB, iB, vB, rA, iA, vA);
   __syncthreads();
   double* out = slabG + (int64_t)range * v.F + c0;
 #pragma unroll
@@ -429,8 +463,10 @@ int tiles_margin(const TilesView& v, const double* labels, const double* weights
                  hipStream_t st) {
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(v.nRB, device_cus()));
   *wgs = grid;
-  hipLaunchKernelGGL(k_tiles_margin, dim3((unsigned)grid), dim3(kTPB), 0, st, v, labels, weights,
-                     coef, fitIntercept, kind, offset, lscale, sigma, eps, mult, slabS);
+  const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
+  hipLaunchKernelGGL(k_tiles_margin, dim3((unsigned)grid), dim3(kTPB), 0, st, d, v.segStart,
+                     v.subRel, v.idx, v.vals, labels, weights, coef, fitIntercept, kind, offset,
+                     lscale, sigma, eps, mult, slabS);
   CYC_LAUNCH_CHECK("k_tiles_margin");
   return CYC_OK;
 }
@@ -445,8 +481,9 @@ int tiles_grad(const TilesView& v, const double* mult, double* slabG, int* range
                hipStream_t st) {
   const int R = tiles_ranges(v);
   *ranges = R;
-  hipLaunchKernelGGL(k_tiles_grad, dim3((unsigned)((int64_t)v.T * R)), dim3(kTPB), 0, st, v, mult,
-                     R, slabG);
+  const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
+  hipLaunchKernelGGL(k_tiles_grad, dim3((unsigned)((int64_t)v.T * R)), dim3(kTPB), 0, st, d,
+                     v.segStart, v.subRel, v.idx, v.vals, mult, R, slabG);
   CYC_LAUNCH_CHECK("k_tiles_grad");
   return CYC_OK;
 }

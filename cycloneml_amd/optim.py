@@ -197,6 +197,17 @@ def _upload(a, device):
     return out
 
 
+def _dev_vector(x, device):
+    """bcScaledMean-style model constants on the device: a device tensor is
+    used as is (the caller broadcast it once), host arrays are uploaded."""
+    if x is None:
+        return None
+    torch = _torch()
+    if torch.is_tensor(x):
+        return x.to(device=device, dtype=torch.float64)
+    return torch.as_tensor(np.asarray(x, dtype=np.float64), device=device)
+
+
 def _download(t):
     """Device vector -> new host numpy array via the pinned staging buffer."""
     if t.device.type != "cuda" or t.numel() == 0:
@@ -346,8 +357,7 @@ class BinaryLogisticBlockAggregator(DifferentiableLossAggregator):
         self.coef = _upload(coefficients, device) \
             if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
         self.dim = int(self.coef.shape[0])
-        self.scaledMean = None if scaledMean is None else torch.as_tensor(
-            np.asarray(scaledMean, dtype=np.float64), device=device)
+        self.scaledMean = _dev_vector(scaledMean, device)
         self._plan = _logistic_plan(self.numFeatures, 1, self.fitIntercept, self.fitWithMean,
                                     device)
         self._init_state(device)
@@ -394,8 +404,7 @@ class HingeBlockAggregator(DifferentiableLossAggregator):
         self.coef = _upload(coefficients, device) \
             if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
         self.dim = int(self.coef.shape[0])
-        self.scaledMean = None if scaledMean is None else torch.as_tensor(
-            np.asarray(scaledMean, dtype=np.float64), device=device)
+        self.scaledMean = _dev_vector(scaledMean, device)
         self._plan = _logistic_plan(self.numFeatures, 1, self.fitIntercept, self.fitIntercept,
                                     device, hinge=True)
         self._init_state(device)
@@ -445,8 +454,7 @@ class LeastSquaresBlockAggregator(DifferentiableLossAggregator):
         self.coef = _upload(coefficients, device) \
             if not torch.is_tensor(coefficients) else coefficients.to(device, torch.float64)
         self.dim = self.numFeatures
-        self.scaledMean = None if scaledMean is None else torch.as_tensor(
-            np.asarray(scaledMean, dtype=np.float64), device=device)
+        self.scaledMean = _dev_vector(scaledMean, device)
         key = ("ls", self.numFeatures, self.fitIntercept, float(labelStd), float(labelMean),
                str(device))
         self._plan = _PLANS.get(key)
@@ -498,8 +506,7 @@ class HuberBlockAggregator(DifferentiableLossAggregator):
             raise N.IllegalArgumentException(
                 f"requirement failed: parameters size {self.dim} does not match numFeatures "
                 f"{self.numFeatures} (+ intercept) + sigma")
-        self.scaledMean = None if scaledMean is None else torch.as_tensor(
-            np.asarray(scaledMean, dtype=np.float64), device=device)
+        self.scaledMean = _dev_vector(scaledMean, device)
         key = ("huber", self.numFeatures, self.fitIntercept, float(epsilon), str(device))
         self._plan = _PLANS.get(key)
         if self._plan is None:
@@ -557,8 +564,7 @@ class AFTBlockAggregator(DifferentiableLossAggregator):
         if self.fitIntercept and (scaledMean is None or len(scaledMean) != self.numFeatures):
             raise N.IllegalArgumentException(
                 "requirement failed: scaled means is required when center the vectors")
-        self.scaledMean = None if scaledMean is None else torch.as_tensor(
-            np.asarray(scaledMean, dtype=np.float64), device=device)
+        self.scaledMean = _dev_vector(scaledMean, device)
         key = ("aft", self.numFeatures, self.fitIntercept, str(device))
         self._plan = _PLANS.get(key)
         if self._plan is None:
@@ -635,8 +641,7 @@ class MultinomialLogisticBlockAggregator(DifferentiableLossAggregator):
         self.numClasses = self.dim // fpi
         if self.dim != self.numClasses * fpi:
             raise N.IllegalArgumentException("requirement failed")
-        self.scaledMean = None if scaledMean is None else torch.as_tensor(
-            np.asarray(scaledMean, dtype=np.float64), device=device)
+        self.scaledMean = _dev_vector(scaledMean, device)
         self._plan = _logistic_plan(self.numFeatures, self.numClasses, self.fitIntercept,
                                     self.fitWithMean, device)
         self._init_state(device)
