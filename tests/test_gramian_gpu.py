@@ -110,3 +110,46 @@ def test_gramian_large_shard_properties(cuda):
     Us = torch.zeros_like(Ufull)
     plan.accumulate(X[:2000], Us)
     np.testing.assert_allclose(Us.cpu().numpy(), oracle.gramian_partition(sub), rtol=1e-11)
+
+
+@pytest.mark.timeout(600)
+def test_gramian_bench_shard(cuda):
+    """bench.py's gramian shard at its benched size (30M x 1024 = 246 GB, the
+    largest resident shard of BASELINE configs[2]; smaller if the device has
+    less free memory): the whole-shard Gramian equals the sum of its two
+    halves' (split-K sizing differs between them) within 1e-12, equals the
+    restatement on a 2000-row subset, and satisfies G 1 = X^T (X 1)."""
+    import torch
+    from cycloneml_amd.linalg import GramianPlan
+    p = 1024
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info(cuda)
+    n = int(min(30_000_000, (free - (24 << 30)) // (8 * p)))
+    n -= n % 1024
+    X = torch.empty(n, p, dtype=torch.float64, device=cuda)
+    g = torch.Generator(device=cuda).manual_seed(77)
+    for s in range(0, n, 1 << 20):
+        X[s:s + (1 << 20)] = torch.rand(min(1 << 20, n - s), p, generator=g, device=cuda,
+                                        dtype=torch.float64)
+    plan = GramianPlan(p)
+    U = torch.zeros(p * (p + 1) // 2, dtype=torch.float64, device=cuda)
+    plan.accumulate(X, U)
+    Uh = torch.zeros_like(U)
+    h = n // 2 + 777
+    plan.accumulate(X[:h], Uh)
+    plan.accumulate(X[h:], Uh)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(Uh.cpu().numpy(), U.cpu().numpy(), rtol=1e-12)
+    # G 1 = X^T (X 1), accumulated in 1M-row chunks
+    w = torch.zeros(p, dtype=torch.float64, device=cuda)
+    for s in range(0, n, 1 << 20):
+        xs = X[s:s + (1 << 20)]
+        w += xs.T @ xs.sum(1)
+    Gf = np.asarray(oracle.triu_to_full(p, U.cpu().numpy())).reshape(p, p)
+    np.testing.assert_allclose(Gf.sum(1), w.cpu().numpy(), rtol=1e-11)
+    Us = torch.zeros_like(U)
+    plan.accumulate(X[n - 2000:], Us)
+    np.testing.assert_allclose(Us.cpu().numpy(),
+                               oracle.gramian_partition(X[n - 2000:].cpu().numpy()), rtol=1e-11)

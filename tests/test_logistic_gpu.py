@@ -467,3 +467,47 @@ def test_aft_requires_positive_labels(cuda):
                                          device=cuda)
     with pytest.raises(N.IllegalArgumentException, match="greater than 0"):
         AFTBlockAggregator(None, False, np.zeros(4), device=cuda).add(blk)
+
+
+@pytest.mark.timeout(600)
+def test_multinomial_bench_shard(cuda):
+    """bench.py's lr_multi shard at its benched size (the full configs[3]:
+    50M x 512, C = 100, fitIntercept + fitWithMean with the shard's real
+    scaledMean; smaller if the device has less free memory): several 8M-row
+    launch chunks and the 32-bit buffer-descriptor caps.  The whole shard's
+    state equals the sum of two unequal parts' (chunk boundaries differ)
+    within 1e-11, and the last 5000 rows equal the restatement within 1e-10."""
+    import torch
+    from cycloneml_amd.optim import DeviceInstanceBlock, MultinomialLogisticBlockAggregator
+    F, C = 512, 100
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info(cuda)
+    n = int(min(50_000_000, (free - (24 << 30)) // (8 * F)))
+    g = torch.Generator(device=cuda).manual_seed(11)
+    X = torch.empty(n, F, dtype=torch.float64, device=cuda)
+    for s in range(0, n, 1 << 20):
+        X[s:s + (1 << 20)] = torch.randn(min(1 << 20, n - s), F, generator=g, device=cuda,
+                                         dtype=torch.float64)
+    y = torch.randint(0, C, (n,), generator=g, device=cuda).to(torch.float64)
+    mean = torch.zeros(F, dtype=torch.float64, device=cuda)
+    for s in range(0, n, 1 << 22):
+        mean += X[s:s + (1 << 22)].sum(0)
+    sm = (mean / n).cpu().numpy()
+    coef = np.random.default_rng(3).normal(size=C * F + C) * 0.01
+
+    def run(a, b):
+        blk = DeviceInstanceBlock(y[a:b], None, X=X[a:b])
+        return MultinomialLogisticBlockAggregator(np.ones(F), sm, True, True, coef,
+                                                  device=cuda).add(blk)._state.cpu().numpy()
+    full = run(0, n)
+    cut = 19_000_001
+    _rel_close(run(0, cut) + run(cut, n), full, rtol=1e-11)
+    m = 5000
+    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+    oracle.multinomial_logistic_add(dict(labels=y[n - m:].cpu().numpy(), weights=None,
+                                         X=X[n - m:].cpu().numpy()), coef, C, True, True, sm, st)
+    tail = run(n - m, n)
+    _rel_close(tail[:coef.size], st["grad"])
+    assert abs(tail[coef.size] - st["loss"]) <= 1e-10 * abs(st["loss"])
