@@ -500,6 +500,276 @@ __global__ __launch_bounds__(256, KS <= 4 ? 3 : 2) void k_screen(
   }
 }
 
+// ---------------------------------------------------------------------------
+// 32x32 form (d <= 256): v_mfma_i32_32x32x32_i8 holds the SIMD's issue for 8
+// of its 32 cycles (the 16x16x64 form: 8 of 16), leaving room for the top-2
+// epilogue (9 VALU per (row, center): ~3 per MFMA).
+//
+// One wave = 32 rows, held in REGISTERS in the MFMA A layout (lane l: row
+// l & 31, dims 32 s + 16 (l >> 5) + 0..15 of substep s, three limbs: 96
+// VGPRs at d = 256).  A workgroup of 4 waves (128 rows) sweeps every
+// 32-center tile; each tile's B fragments (24 KiB at d = 256) are DMA'd
+// into a ring of three LDS slots (global_load_lds, 1 KiB per wave-
+// instruction, split over the waves, counted vmcnt + raw s_barrier so the
+// next tile stays in flight) and read by conflict-free ds_read_b128.
+// 252 VGPRs: two waves per SIMD (two workgroups per CU, 2 x 74.5 KB LDS).
+// Measured at 10M x 256, k = 1024 (profiles/r02_kmeans_*): 14.4 ms per
+// launch vs 14.0-15.4 for the 16x16x64 screen; PMC: 32 MFMA-busy cycles per
+// MFMA, 53 % of the SIMD cycles at the 1.89 GHz the chip holds under this
+// load.  Tried and slower: B fragments per wave straight from L2 (18.1 ms),
+// one wave per SIMD with two accumulator sets so the epilogue of tile t
+// interleaves tile t+1's MFMAs (18.1 ms), 8-wave workgroups (one tile load
+// per 256 rows: 14.8-15.0 ms).
+//
+// B fragments: lane l of 32-center tile ct, 32-dim substep s holds center
+// 32 ct + (l & 31), dims 32 s + 16 (l >> 5) + 0..15, limb planes a', b', c':
+// Cb[((ct S + s) 3 + limb) 64 + l]; the tile count is even (padding centers
+// are zero with cq = +inf).
+__global__ __launch_bounds__(256) void k_centers_pack32(
+    const double* __restrict__ C, const double* __restrict__ cnorm, int k, int d, int S, int ktp,
+    const double* __restrict__ cn1, const CenterParams* __restrict__ prm, uint4* __restrict__ Cb,
+    float* __restrict__ cq, double* __restrict__ g) {
+  const CenterParams p = *prm;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)ktp * S * 64;
+  if (idx < total) {
+    const int lane = (int)(idx & 63);
+    const int64_t t = idx >> 6;
+    const int s = (int)(t % S), ct = (int)(t / S);
+    const int c = ct * 32 + (lane & 31), j0 = s * 32 + 16 * (lane >> 5);
+    int a[16], b[16], cc[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int j = j0 + e;
+      const double v = (p.ok && c < k && j < d) ? C[(int64_t)c * d + j] : 0.0;
+      quant3(v, p.ec, a[e], b[e], cc[e]);
+    }
+    uint4 pa, pb, pc;
+    pa.x = pack4(a); pa.y = pack4(a + 4); pa.z = pack4(a + 8); pa.w = pack4(a + 12);
+    pb.x = pack4(b); pb.y = pack4(b + 4); pb.z = pack4(b + 8); pb.w = pack4(b + 12);
+    pc.x = pack4(cc); pc.y = pack4(cc + 4); pc.z = pack4(cc + 8); pc.w = pack4(cc + 12);
+    uint4* dst = Cb + (t * 3) * 64 + lane;
+    dst[0] = pa;
+    dst[64] = pb;
+    dst[128] = pc;
+  }
+  if (idx < (int64_t)ktp * 32) {
+    const int c = (int)idx;
+    if (c < k && p.ok) {
+      const double gc = err_term(p.ec, cn1[c], p.mu, d);
+      const double cn = cnorm[c];
+      g[c] = gc;
+      cq[c] = fdown((cn * cn) * (1.0 - kEpsF) - 2.0 * gc);
+    } else {
+      g[c] = 0.0;
+      cq[c] = __builtin_inff();
+    }
+  }
+}
+
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+template <int S, int W>   // 32-dim substeps (D = 32 S <= 256); W waves per workgroup
+__global__ __launch_bounds__(64 * W, 2) void k_screen32(
+    const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
+    int64_t n, int d, const uint4* __restrict__ Cb, const float* __restrict__ cq,
+    const double* __restrict__ g, const double* __restrict__ cnorm,
+    const CenterParams* __restrict__ prm, int ktp, int32_t* __restrict__ assign,
+    int32_t* __restrict__ list, unsigned int* __restrict__ listCount) {
+  constexpr int D = 32 * S, CH = 3 * D / 16;      // 16-byte chunks per image row
+  constexpr int FR = 3 * S;                        // 1 KiB B fragments per center tile
+  constexpr int TB = FR * 1024 + 256;              // tile slot: fragments, then 64 cq floats
+  constexpr int G = FR / W + 1;                    // LDS-DMA instructions per wave per tile
+  static_assert(FR % W == 0, "fragments split evenly over the waves");
+  // ONE shared array (a second __shared__ object can make hipcc drain vmcnt
+  // before every ds_read): three tile slots, reused for the final reduction.
+  __shared__ __attribute__((aligned(16))) char lds[3 * TB];
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t row0 = ((int64_t)blockIdx.x * W + wave) * 32;
+  // waves past the end still take part in every barrier (zero rows)
+  const int rows = (int)max<int64_t>(0, min<int64_t>(32, n - row0));
+  const CenterParams P = *prm;
+  if (!P.ok) {   // uniform over the grid
+    if (lane < rows) list[atomicAdd(listCount, 1u)] = (int32_t)(row0 + lane);
+    return;
+  }
+  // tile t -> slot t % 3: each wave DMAs fragments wave, wave + 4, ... and the
+  // tile's cq (all four waves write the same 256 bytes); past the last tile
+  // the last one is re-read into the free slot, so every wave always has
+  // exactly G DMAs per tile in flight and one counted wait fits all tiles.
+  auto issue = [&](int t) {
+    const int tt = t < ktp ? t : ktp - 1;
+    const char* src = (const char*)Cb + (size_t)tt * FR * 1024 + lane * 16;
+    char* dst = lds + (t % 3) * TB;
+#pragma unroll
+    for (int j = 0; j < FR / W; ++j) {
+      const int f = wave + W * j;
+      __builtin_amdgcn_global_load_lds((const void*)(src + f * 1024),
+                                       (__attribute__((address_space(3))) void*)(dst + f * 1024),
+                                       16, 0, 0);
+    }
+    __builtin_amdgcn_global_load_lds((const void*)(cq + (size_t)tt * 32 + r),
+                                     (__attribute__((address_space(3))) void*)(dst + FR * 1024),
+                                     4, 0, 0);
+  };
+  issue(0);
+  issue(1);
+  // A fragments of the wave's 32 rows, all substeps and limbs
+  v4i A[S][3];
+  {
+    // loads from a clamped row (always in range), zeroed after the load
+    const bool ok = r < rows;
+    const uint4* src = Xq + min<int64_t>(row0 + r, n - 1) * CH + h;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int L = 0; L < 3; ++L) {
+        const v4u t = __builtin_nontemporal_load((const v4u*)(src + L * (D / 16) + 2 * s));
+        A[s][L] = ok ? __builtin_bit_cast(v4i, t) : v4i{0, 0, 0, 0};
+      }
+  }
+  // row of accumulator register reg: (reg & 3) + 8 (reg >> 2) + 4 h
+  float F1[16];
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+    const int ex0 = meta[min<int64_t>(row0 + row, n - 1)].x;
+    const int ex = row < rows ? ex0 : INT_MIN;
+    F1[reg] = ex == INT_MIN ? 0.0f : __builtin_ldexpf(1.0f, ex + P.ec - 20);
+  }
+  float sL1[16], sL2[16];
+  int sI1[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    sL1[q] = sL2[q] = __builtin_inff();
+    sI1[q] = -1;
+  }
+  // tile ct from its slot: 6 limb products per substep, B fragments by
+  // conflict-free ds_read_b128 (lane-linear 1 KiB fragments)
+  auto tile = [&](int ct, v16i (&acc)[3]) {
+    const v4i* B = (const v4i*)(lds + (ct % 3) * TB) + lane;
+#pragma unroll
+    for (int L = 0; L < 3; ++L) acc[L] = v16i{};
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const v4i B0 = B[(3 * s + 0) * 64], B1 = B[(3 * s + 1) * 64], B2 = B[(3 * s + 2) * 64];
+      acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B1, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B2, acc[2], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B0, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B1, acc[2], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][2], B0, acc[2], 0, 0, 0);
+    }
+  };
+  // the two smallest lower bounds per row and the index of the smallest;
+  // cqv is read from the tile's slot before that slot can be refilled
+  auto epi = [&](int ct, float cqv, const v16i (&acc)[3]) {
+    const int c = ct * 32 + r;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int T = acc[0][reg] * 128 + acc[1][reg];
+      const float V = __builtin_fmaf((float)acc[2][reg], 0x1p-7f, (float)T);
+      const float L = __builtin_fmaf(-F1[reg], V, cqv);
+      const bool lt = L < sL1[reg];
+      sL2[reg] = __builtin_amdgcn_fmed3f(sL1[reg], sL2[reg], L);
+      sI1[reg] = lt ? c : sI1[reg];
+      sL1[reg] = lt ? L : sL1[reg];   // L is never NaN: a select, no canonicalize
+    }
+  };
+  auto cq_of = [&](int ct) { return *(const float*)(lds + (ct % 3) * TB + FR * 1024 + r * 4); };
+  // tile t: wait for this wave's DMAs of t (the G of t + 1 may stay in
+  // flight), barrier (every wave's part of t landed; every wave is past
+  // t - 1, whose slot the DMAs of t + 2 now refill)
+  auto arrive = [&](int t) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(t + 2);
+  };
+
+  // MODE.FP_ROUND single precision = toward -inf (the L' are lower bounds)
+  __builtin_amdgcn_s_setreg(0x801, 2);
+  for (int ct = 0; ct < ktp; ++ct) {
+    v16i X[3];
+    arrive(ct);
+    const float cqv = cq_of(ct);
+    tile(ct, X);
+    epi(ct, cqv, X);
+  }
+  __builtin_amdgcn_s_setreg(0x801, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing re-read DMAs
+
+  // each row's slots over the 32 lanes (centers) of its half
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) {
+      const float oL1 = __shfl_xor(sL1[q], m), oL2 = __shfl_xor(sL2[q], m);
+      const int oI1 = __shfl_xor(sI1[q], m);
+      sL2[q] = __builtin_fminf(__builtin_fmaxf(sL1[q], oL1), __builtin_fminf(sL2[q], oL2));
+      const bool take = oL1 < sL1[q] || (oL1 == sL1[q] && oI1 >= 0 && (sI1[q] < 0 || oI1 < sI1[q]));
+      sI1[q] = take ? oI1 : sI1[q];
+      sL1[q] = take ? oL1 : sL1[q];
+    }
+  }
+  // per-wave reduction area in the (now idle) slots: L1, L2, I1 x 32 rows
+  __syncthreads();
+  float* redL1 = (float*)lds + wave * 96;
+  float* redL2 = redL1 + 32;
+  int* redI1 = (int*)(redL1 + 64);
+  if (r == 0) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      redL1[row] = sL1[reg];
+      redL2[row] = sL2[reg];
+      redI1[row] = sI1[reg];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  if (lane < rows) {
+    const int row = lane;
+    const int2 mt = meta[row0 + row];
+    const float L1 = redL1[row], L2 = redL2[row];
+    const int I1 = redI1[row];
+    bool decided = false;
+    if (mt.x != INT_MIN && I1 >= 0 && __builtin_isfinite(L1)) {
+      const double xn = xnorm[row0 + row], cn = cnorm[I1];
+      const double xx = xn * xn, cc = cn * cn;
+      const double n1 = (double)__int_as_float(mt.y);
+      const double fx = err_term(mt.x, n1, P.mu, d);
+      const double l1 = (double)L1;
+      const double M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) +
+                        0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g[I1]) +
+                        0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
+                                   __builtin_fmin(__builtin_fabs((double)L2), 0x1p120)) +
+                        0x1p-90) *
+                       (1.0 + 0x1p-30);
+      decided = !__builtin_isfinite(L2) || ((double)L2 - l1) > M;
+    }
+    if (decided) {
+      assign[row0 + row] = I1;
+    } else {
+      list[atomicAdd(listCount, 1u)] = (int32_t)(row0 + row);
+    }
+  }
+}
+
+template <int S, int W>
+int launch_screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
+                    const void* Cb, const float* cq, const double* g, const double* cnorm,
+                    const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
+                    unsigned int* listCount, hipStream_t st) {
+  KernelTimer timer("k_kmeans_assign", st);
+  const int64_t wg = (n + 32 * W - 1) / (32 * W);   // W waves x 32 rows
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32<S, W>), dim3((unsigned)wg), dim3(64 * W), 0, st,
+                     (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb, cq, g, cnorm, prm,
+                     ktp, assign, list, listCount);
+  CYC_LAUNCH_CHECK("k_kmeans_screen32_i8");
+  return CYC_OK;
+}
+
 template <int KS>
 int launch_screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
                   const void* Cb, const float* cq, const double* g, const double* cnorm,
@@ -544,6 +814,17 @@ int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp,
   hipLaunchKernelGGL(k_centers_params, dim3(1), dim3(256), 0, st, k, (const double*)cmax,
                      (const double*)cn1, prm);
   CYC_LAUNCH_CHECK("k_centers_params");
+  if (uses32(d)) {
+    // 32-center tiles, an even number of them (ktp 16-center tiles, a
+    // multiple of kWaves = 4, cover them), 32-dim substeps
+    const int ktp32 = tiles32(k), S = 2 * KS;
+    const int64_t total = std::max<int64_t>((int64_t)ktp32 * S * 64, (int64_t)ktp32 * 32);
+    hipLaunchKernelGGL(k_centers_pack32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                       C, cnorm, k, d, S, ktp32, (const double*)cn1, (const CenterParams*)prm,
+                       (uint4*)Cb, cq, g);
+    CYC_LAUNCH_CHECK("k_centers_pack32");
+    return CYC_OK;
+  }
   const int64_t total = std::max<int64_t>((int64_t)ktp * KS * 64, (int64_t)ktp * 16);
   hipLaunchKernelGGL(k_centers_pack, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, C,
                      cnorm, k, d, KS, ktp, (const double*)cn1, (const CenterParams*)prm,
@@ -557,6 +838,13 @@ int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, in
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
            unsigned int* listCount, hipStream_t st) {
   if (n <= 0) return CYC_OK;
+  if (uses32(d)) {
+    const int k32 = ktp * 16 / 32;   // launch over the padded center range (cq = +inf)
+    switch (ksteps(d)) {
+      case 2: return launch_screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, st);
+      default: return launch_screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, st);
+    }
+  }
   switch (ksteps(d)) {
 #define CYC_S8(K) \
   case K: return launch_screen<K>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp, assign, list, listCount, st);

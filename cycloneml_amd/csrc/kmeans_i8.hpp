@@ -25,6 +25,13 @@ struct CenterParams {
 // rings alternate per step); the padding limbs are zero.
 inline int ksteps(int d) { return ((d + 127) / 128) * 2; }
 
+// d <= 256 screens with the 32x32x32 i8 form (row tiles of 32 in registers,
+// 32-center tiles); larger d with the 16x16x64 form (64-row LDS tiles).
+inline bool uses32(int d) { return d <= 256; }
+// 32-center tiles of the 32x32 screen: even, and covered by the 16-center
+// tile padding (a multiple of kWaves = 4 tiles, i.e. of 64 centers).
+inline int tiles32(int k) { return 2 * ((k + 63) / 64); }
+
 // Bytes per row of the image: three int8 limb planes of D = 64 ksteps(d).
 inline int64_t image_row_bytes(int d) { return 3 * 64 * (int64_t)ksteps(d); }
 
