@@ -602,6 +602,145 @@ class JavaRandom:
         return v1 * mul
 
 
+class XORShiftRandom(JavaRandom):
+    """org.apache.spark.util.random.XORShiftRandom
+    (core/src/main/scala/org/apache/spark/util/random/XORShiftRandom.scala:36-67):
+    java.util.Random's nextDouble / nextGaussian over an xorshift next(bits),
+    the seed hashed by scala.util.hashing.MurmurHash3.bytesHash (scala-library
+    2.12, not in the reference tree: its published x86_32 MurmurHash3 with
+    arraySeed 0x3c074a61).  Pinned by RandomSuite.scala:26,29: Rand(30) ->
+    0.2762195585886885, Rand(null = 0) -> 0.7604953758285915."""
+
+    _M32 = 0xFFFFFFFF
+    _M64 = (1 << 64) - 1
+
+    def __init__(self, seed: int):
+        b = (seed & self._M64).to_bytes(8, "big")          # ByteBuffer.putLong
+        lo = _murmur3_bytes(b, 0x3C074A61)
+        hi = _murmur3_bytes(b, lo)
+        self.seed = ((hi << 32) | lo) & self._M64
+        self._next_gaussian = None
+
+    def _next(self, bits: int) -> int:
+        x = self.seed ^ ((self.seed << 21) & self._M64)
+        x ^= x >> 35
+        x ^= (x << 4) & self._M64
+        self.seed = x
+        r = x & ((1 << bits) - 1)
+        if bits == 32 and r >= 1 << 31:
+            r -= 1 << 32
+        return r
+
+
+def _murmur3_bytes(data: bytes, seed: int) -> int:
+    """scala.util.hashing.MurmurHash3.bytesHash (x86_32, little-endian blocks)."""
+    M = 0xFFFFFFFF
+
+    def rotl(x, r):
+        return ((x << r) | (x >> (32 - r))) & M
+
+    def mix_last(h, k):
+        k = (k * 0xCC9E2D51) & M
+        k = rotl(k, 15)
+        k = (k * 0x1B873593) & M
+        return h ^ k
+
+    h = seed & M
+    n = len(data)
+    i = 0
+    while n - i >= 4:
+        k = data[i] | data[i + 1] << 8 | data[i + 2] << 16 | data[i + 3] << 24
+        h = mix_last(h, k)
+        h = (rotl(h, 13) * 5 + 0xE6546B64) & M
+        i += 4
+    rem, k = n - i, 0
+    if rem == 3:
+        k ^= data[i + 2] << 16
+    if rem >= 2:
+        k ^= data[i + 1] << 8
+    if rem >= 1:
+        k ^= data[i]
+        h = mix_last(h, k)
+    h ^= n
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & M
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M
+    h ^= h >> 16
+    return h
+
+
+def generate_multinomial_logistic_input(weights, xMean, xVariance, addIntercept, nPoints, seed):
+    """LogisticRegressionSuite.generateMultinomialLogisticInput
+    (mllib/src/test/scala/org/apache/spark/ml/classification/LogisticRegressionSuite.scala:3061-3128),
+    scala.util.Random(seed) = java.util.Random.  Returns (labels, X)."""
+    import math
+    rnd = JavaRandom(seed)
+    xDim = len(xMean)
+    xwi = xDim + 1 if addIntercept else xDim
+    nClasses = len(weights) // xwi + 1
+    X = np.empty((nPoints, xDim))
+    for i in range(nPoints):
+        for j in range(xDim):
+            X[i, j] = rnd.next_gaussian()
+    for i in range(nPoints):
+        for j in range(xDim):
+            X[i, j] = X[i, j] * math.sqrt(xVariance[j]) + xMean[j]
+    y = np.empty(nPoints)
+    for idx in range(nPoints):
+        margins = [0.0] * nClasses
+        for i in range(nClasses - 1):
+            for j in range(xDim):
+                margins[i + 1] += weights[i * xwi + j] * X[idx, j]
+            if addIntercept:
+                margins[i + 1] += weights[(i + 1) * xwi - 1]
+        mx = max(margins)
+        if mx > 0:
+            margins = [m - mx for m in margins]
+        probs = [math.exp(m) for m in margins]
+        norm = 0.0
+        for pr in probs:
+            norm += pr
+        probs = [pr / norm for pr in probs]
+        for i in range(1, nClasses):
+            probs[i] += probs[i - 1]
+        p = rnd.next_double()
+        lab = 0
+        for i in range(nClasses):
+            if p < probs[i]:
+                lab = i
+                break
+        y[idx] = lab
+    return y, X
+
+
+def generate_logistic_input(offset, scale, nPoints, seed):
+    """LogisticRegressionSuite.generateLogisticInput (:3021-3036)."""
+    import math
+    rnd = JavaRandom(seed)
+    x1 = np.array([rnd.next_gaussian() for _ in range(nPoints)])
+    y = np.empty(nPoints)
+    for i in range(nPoints):
+        p = 1.0 / (1.0 + math.exp(-(offset + scale * x1[i])))
+        y[i] = 1.0 if rnd.next_double() < p else 0.0
+    return y, x1.reshape(-1, 1)
+
+
+def spark_rand_column(seed, nRows, numSlices):
+    """functions.rand(seed) over sc.parallelize(rows, numSlices): partition i
+    holds rows [i n / s, (i + 1) n / s) (ParallelCollectionRDD.slice,
+    core/src/main/scala/org/apache/spark/rdd/ParallelCollectionRDD.scala:116-128)
+    and draws XORShiftRandom(seed + i).nextDouble() per row (Rand,
+    sql/catalyst/.../expressions/randomExpressions.scala:43-44)."""
+    out = np.empty(nRows)
+    for i in range(numSlices):
+        a, b = (i * nRows) // numSlices, ((i + 1) * nRows) // numSlices
+        r = XORShiftRandom(seed + i)
+        for j in range(a, b):
+            out[j] = r.next_double()
+    return out
+
+
 # --------------------------------------------------------------------------
 # Summarizer pre-pass (ml/stat/Summarizer.scala:428-770,
 # ml/stat/MultiClassSummarizer.scala:30-98)
