@@ -135,6 +135,8 @@ SIGNATURES = {
     "cyc_label_summarizer_dev": (ctypes.c_int, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp]),
     "cyc_scale_columns_dense_dev": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "cyc_scale_columns_csr_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
+    "cyc_blokify_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, ctypes.c_int32, _i64, _vp, _vp,
+                                        _vp, _vp]),
     # resident datasets: host pointers
     "cyc_dataset_dense_create": (ctypes.c_int, [_i32, _i64, ctypes.c_int, ctypes.c_int,
                                                 ctypes.POINTER(_vp)]),

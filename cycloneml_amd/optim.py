@@ -167,6 +167,30 @@ class DeviceInstanceBlock:
                                    X=t(X, np.float64))
 
 
+def blokify(block: "DeviceInstanceBlock", maxBlockSizeInMB: float = 1.0, stream=None):
+    """InstanceBlock.blokifyWithMaxMemUsage (ml/feature/Instance.scala:146-187)
+    over a device shard with maxMemUsage = ceil(maxBlockSizeInMB * 2^20)
+    (LogisticRegression.scala:967): (starts int64[nblocks + 1], dense
+    bool[nblocks]) as device tensors -- the reference's block boundaries and
+    each block's dense-or-CSR storage, computed where the rows live."""
+    import math
+    torch = _torch()
+    if block.rowptr is None and block.X is None:
+        raise N.IllegalArgumentException("blokify needs the block's rows (dense or CSR)")
+    maxMem = int(math.ceil(maxBlockSizeInMB * 1024 * 1024))
+    dev = block.labels.device
+    n = block.size
+    starts = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    dense = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    nb = torch.empty(1, dtype=torch.int64, device=dev)
+    N.check(N.load().cyc_blokify_dev(N.ptr(block.X), N.ptr(block.rowptr), N.ptr(block.values),
+                                     N.ptr(block.weights), n, block.numFeatures, maxMem,
+                                     N.ptr(starts), N.ptr(dense), N.ptr(nb),
+                                     N.stream_handle(stream)))
+    k = int(nb.item())
+    return starts[:k + 1], dense[:k].bool()
+
+
 _PLANS = {}
 _PINNED = {}
 

@@ -385,6 +385,16 @@ int cyc_scale_columns_dense_dev(double* X, int64_t n, int32_t F, const double* s
                                 void* stream);
 int cyc_scale_columns_csr_dev(const int32_t* colidx, double* vals, int64_t nnz,
                               const double* scale, void* stream);
+/* InstanceBlock.blokifyWithMaxMemUsage (ml/feature/Instance.scala:146-187;
+ * Matrices.fromVectors's dense-or-sparse choice, Matrices.scala:1010-1049)
+ * over one partition's device rows -- dense X (n x F) OR CSR (rowptr, vals),
+ * weights optional (null = all 1): starts[0..nblocks] (int64, capacity n + 1,
+ * starts[nblocks] = n), dense[b] = 1 iff block b is stored dense, *nblocks;
+ * all device.  maxMemUsage <= 0 -> "requirement failed: maxMemUsage > 0".
+ * Replaces the per-partition iterator the reference runs on the executor. */
+int cyc_blokify_dev(const double* X, const int64_t* rowptr, const double* vals,
+                    const double* weights, int64_t n, int32_t F, int64_t maxMemUsage,
+                    int64_t* starts, uint8_t* dense, int64_t* nblocks, void* stream);
 
 /* ------------------------------------------- resident datasets (host API) */
 /* Layer 2 for a JVM shim: a library-owned HBM copy of one

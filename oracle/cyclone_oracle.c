@@ -1196,3 +1196,35 @@ void orc_label_summarize(int64_t n, const double* y, const double* w, int64_t R,
   }
   free(part);
 }
+
+/* InstanceBlock.blokifyWithMaxMemUsage (ml/feature/Instance.scala:146-180)
+ * over rows given by their numNonzeros (values != 0) and weights: rows are
+ * appended while the running getBlockMemUsage (:114-129) is below maxMem;
+ * the crossing row stays in the block.  Block b = rows [starts[b],
+ * starts[b+1]); dense[b] = Matrices.fromVectors's choice (:1010-1049:
+ * getDenseSize < getSparseSize, :1317-1336).  Returns the block count. */
+static int64_t orc_dense_size(int64_t cols, int64_t rows) { return 8 * cols * rows + 12 + 9; }
+static int64_t orc_sparse_size(int64_t nnz, int64_t ptrs) {
+  return 8 * nnz + 4 * nnz + 4 * ptrs + 12 * 3 + 9;
+}
+int64_t orc_blokify(int64_t n, int64_t F, const int64_t* rowNnz, const double* w, int64_t maxMem,
+                    int64_t* starts, uint8_t* dense) {
+  int64_t nb = 0, r = 0;
+  starts[0] = 0;
+  while (r < n) {                                   /* iterator.next() */
+    int64_t cnt = 0, nnz = 0, mem = 0;
+    int unit = 1;
+    while (r < n && mem < maxMem) {
+      cnt += 1;
+      nnz += rowNnz[r];
+      unit = unit && (w == NULL || w[r] == 1.0);
+      const int64_t ds = orc_dense_size(F, cnt), ss = orc_sparse_size(nnz, cnt + 1);
+      const int64_t m = ds < ss ? ds : ss;
+      mem = unit ? m + 8 * cnt + 12 * 2 : m + 8 * cnt * 2 + 12 * 2;
+      r += 1;
+    }
+    dense[nb] = orc_dense_size(F, cnt) < orc_sparse_size(nnz, cnt + 1);
+    starts[++nb] = r;
+  }
+  return nb;
+}

@@ -99,6 +99,8 @@ def lib():
                 "orc_spr_sparse": (None, [ctypes.c_double, _I32, _D, _i64, _D]),
                 "orc_gramian_partition": (None, [_D, _i64, _i64, _D, _D]),
                 "orc_triu_to_full": (None, [_i64, _D, _D]),
+                "orc_blokify": (_i64, [_i64, _i64, _I64, _D, _i64, _I64,
+                                       ctypes.POINTER(ctypes.c_uint8)]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(L, name)
@@ -814,6 +816,32 @@ def label_summarize(y, w=None, rows_per_partition=1 << 62, max_classes=1024):
                               _p(inv, _I64), _p(mx, _I64))
     nc = int(mx[0]) + 1
     return hist[:nc].copy(), int(inv[0]), nc
+
+
+def row_numnonzeros(X=None, csr=None):
+    """Vector.numNonzeros per row (values != 0, explicit zeros excluded)."""
+    if X is not None:
+        return np.count_nonzero(np.asarray(X) != 0.0, axis=1).astype(np.int64)
+    rp, _, v = csr
+    nz = (np.asarray(v) != 0.0).astype(np.int64)
+    c = np.concatenate([[0], np.cumsum(nz)])
+    rp = np.asarray(rp, dtype=np.int64)
+    return (c[rp[1:]] - c[rp[:-1]]).astype(np.int64)
+
+
+def blokify(F, row_nnz, weights, max_mem_usage):
+    """InstanceBlock.blokifyWithMaxMemUsage (Instance.scala:146-180):
+    (starts[nblocks + 1], dense[nblocks] bool)."""
+    if not max_mem_usage > 0:
+        raise IllegalArgumentException("requirement failed")
+    nnz = np.ascontiguousarray(row_nnz, dtype=np.int64)
+    n = nnz.size
+    starts = np.zeros(n + 1, np.int64)
+    dense = np.zeros(max(n, 1), np.uint8)
+    nb = lib().orc_blokify(n, int(F), _p(nnz, _I64), _p(None if weights is None else _f64(weights)),
+                           int(max_mem_usage), _p(starts, _I64),
+                           dense.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+    return starts[:nb + 1].copy(), dense[:nb].astype(bool)
 
 
 def parse_libsvm(text, num_features=-1):
