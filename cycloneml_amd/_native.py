@@ -70,6 +70,12 @@ SIGNATURES = {
     "cyc_col_sums_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "cyc_triu_to_full_dev": (ctypes.c_int, [_i32, _vp, _vp, _vp]),
     "cyc_covariance_finalize_dev": (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp]),
+    "cyc_gramian_accumulate_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "cyc_col_sums_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "cyc_rowmatrix_dense_rows_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, ctypes.c_int32, _vp,
+                                                    _vp]),
+    "cyc_sparse_covariance_finalize_dev": (ctypes.c_int, [ctypes.c_int32, _vp, _i64, _vp, _vp,
+                                                          _vp]),
     "cyc_logistic_plan_create": (ctypes.c_int, [_i32, _i32, ctypes.c_int, ctypes.c_int,
                                                 ctypes.POINTER(_vp)]),
     "cyc_logistic_plan_destroy": (ctypes.c_int, [_vp]),

@@ -203,13 +203,98 @@ __global__ void k_col_fold(const double* __restrict__ part, int splits, int p,
   out[c] = dadd(out[c], s);
 }
 
+
+// CSR rows [r0, r0 + rows) scattered into a zeroed dense row-major chunk
+// (one wave per row): the sparse rows of a RowMatrix reach the same syrk.
+// For a nonzero x_j the sparse spr branch (mllib/linalg/BLAS.scala:269-298)
+// adds (alpha x_j) x_i exactly as dspr does, so the densified rows give the
+// reference's per-row products.
+__global__ __launch_bounds__(256) void k_csr_densify(const int64_t* __restrict__ rowptr,
+                                                     const int32_t* __restrict__ colidx,
+                                                     const double* __restrict__ vals, int64_t r0,
+                                                     int64_t rows, int p,
+                                                     double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  double* o = out + r * p;
+  const int64_t a = rowptr[r0 + r], b = rowptr[r0 + r + 1];
+  for (int64_t k = a + lane; k < b; k += 64) o[colidx[k]] = vals[k];
+}
+
+// RowMatrix.isSparseMatrix (:439-441): rows with sparsity() < 0.5, where
+// sparsity = 1.0 - numNonzeros / size (mllib Vector.sparsity); the matrix is
+// sparse iff the count is 0.
+__global__ __launch_bounds__(256) void k_dense_rows(const double* __restrict__ X,
+                                                    const int64_t* __restrict__ rowptr,
+                                                    const double* __restrict__ vals, int64_t n,
+                                                    int p, unsigned long long* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool dense = false;
+  if (i < n) {
+    int64_t nz = 0;
+    if (X) {
+      for (int j = 0; j < p; ++j) nz += X[i * p + j] != 0.0;
+    } else {
+      for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) nz += vals[k] != 0.0;
+    }
+    dense = 1.0 - (double)nz / (double)p < 0.5;
+  }
+  const unsigned long long m = __ballot(dense);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(cnt, (unsigned long long)__popcll(m));
+}
+
+// computeSparseVectorCovariance (:222-246) from the packed Gramian:
+// alpha = m / m1 * mean(i); G(i, j) = G(i, j) / m1 - alpha * mean(j) for
+// i <= j, mirrored.
+__global__ void k_sparse_cov_finalize(int n, const double* __restrict__ U, double m,
+                                      const double* __restrict__ mean, double* __restrict__ G) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)n * n) return;
+  const int col = (int)(e / n), row = (int)(e % n);
+  const int i = min(row, col), j = max(row, col);
+  const double m1 = m - 1.0;
+  const double alpha = m / m1 * mean[i];
+  G[e] = U[iut(i, j)] / m1 - alpha * mean[j];
+}
+
 }  // namespace
 
 struct cyc_gramian_plan_s {
   int p = 0;
   std::mutex mu;
   cyc::DeviceBuffer slab;
+  cyc::DeviceBuffer chunk;   // densified CSR rows
 };
+
+namespace {
+
+int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, const double* mean,
+                      double* U, hipStream_t st);
+int col_sums_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
+                    hipStream_t st);
+
+// CSR rows in chunks of about 1 GiB of dense rows: densify, then `dense`.
+template <class F>
+int over_csr_chunks(cyc_gramian_plan plan, const int64_t* rowptr, const int32_t* colidx,
+                    const double* vals, int64_t nrows, hipStream_t st, F dense) {
+  const int p = plan->p;
+  const int64_t R = std::max<int64_t>(256, ((int64_t)1 << 30) / (8 * (int64_t)p)) / 256 * 256;
+  const int64_t rows = std::min<int64_t>(R, nrows);
+  if (int rc = plan->chunk.reserve(sizeof(double) * (size_t)rows * p)) return rc;
+  double* buf = (double*)plan->chunk.ptr;
+  for (int64_t r0 = 0; r0 < nrows; r0 += R) {
+    const int64_t nr = std::min<int64_t>(R, nrows - r0);
+    CYC_HIP(hipMemsetAsync(buf, 0, sizeof(double) * (size_t)nr * p, st));
+    hipLaunchKernelGGL(k_csr_densify, dim3((unsigned)((nr + 3) / 4)), dim3(256), 0, st, rowptr,
+                       colidx, vals, r0, nr, p, buf);
+    CYC_LAUNCH_CHECK("k_csr_densify");
+    if (int rc = dense((const double*)buf, nr)) return rc;
+  }
+  return CYC_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -240,7 +325,101 @@ int cyc_gramian_accumulate_dev(cyc_gramian_plan plan, const double* X, int64_t n
   CYC_REQUIRE(nrows >= 0, "nrows >= 0");
   if (nrows == 0) return CYC_OK;
   std::lock_guard<std::mutex> g(plan->mu);
+  return accumulate_locked(plan, X, nrows, mean, U, cyc::as_stream(stream));
+}
+
+int cyc_gramian_accumulate_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr,
+                                   const int32_t* colidx, const double* vals, int64_t nrows,
+                                   const double* mean, double* U, void* stream) {
+  CYC_REQUIRE(plan != nullptr && U != nullptr, "plan and U must not be null");
+  CYC_REQUIRE(nrows >= 0, "nrows >= 0");
+  if (nrows == 0) return CYC_OK;
+  CYC_REQUIRE(rowptr && colidx && vals, "non-null CSR arrays");
   hipStream_t st = cyc::as_stream(stream);
+  if (int rc = cyc::check_csr_indices(rowptr, colidx, nrows, plan->p, st)) return rc;
+  std::lock_guard<std::mutex> g(plan->mu);
+  return over_csr_chunks(plan, rowptr, colidx, vals, nrows, st, [&](const double* D, int64_t nr) {
+    return accumulate_locked(plan, D, nr, mean, U, st);
+  });
+}
+
+int cyc_col_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
+                     void* stream) {
+  CYC_REQUIRE(plan != nullptr && sums != nullptr, "plan and sums must not be null");
+  CYC_REQUIRE(nrows >= 0, "nrows >= 0");
+  if (nrows == 0) return CYC_OK;
+  std::lock_guard<std::mutex> g(plan->mu);
+  return col_sums_locked(plan, X, nrows, sums, cyc::as_stream(stream));
+}
+
+int cyc_col_sums_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr, const int32_t* colidx,
+                         const double* vals, int64_t nrows, double* sums, void* stream) {
+  CYC_REQUIRE(plan != nullptr && sums != nullptr, "plan and sums must not be null");
+  CYC_REQUIRE(nrows >= 0, "nrows >= 0");
+  if (nrows == 0) return CYC_OK;
+  CYC_REQUIRE(rowptr && colidx && vals, "non-null CSR arrays");
+  hipStream_t st = cyc::as_stream(stream);
+  if (int rc = cyc::check_csr_indices(rowptr, colidx, nrows, plan->p, st)) return rc;
+  std::lock_guard<std::mutex> g(plan->mu);
+  return over_csr_chunks(plan, rowptr, colidx, vals, nrows, st, [&](const double* D, int64_t nr) {
+    return col_sums_locked(plan, D, nr, sums, st);
+  });
+}
+
+int cyc_rowmatrix_dense_rows_dev(const double* X, const int64_t* rowptr, const double* vals,
+                                 int64_t nrows, int32_t ncols, int64_t* count, void* stream) {
+  CYC_REQUIRE(nrows >= 0 && ncols > 0 && count, "nrows >= 0, ncols > 0, non-null count");
+  CYC_REQUIRE(nrows == 0 || (X != nullptr) != (rowptr != nullptr && vals != nullptr),
+              "exactly one of the dense rows or the CSR (rowptr, values)");
+  hipStream_t st = cyc::as_stream(stream);
+  CYC_HIP(hipMemsetAsync(count, 0, sizeof(int64_t), st));
+  if (nrows == 0) return CYC_OK;
+  hipLaunchKernelGGL(k_dense_rows, dim3((unsigned)((nrows + 255) / 256)), dim3(256), 0, st, X,
+                     rowptr, vals, nrows, (int)ncols, (unsigned long long*)count);
+  CYC_LAUNCH_CHECK("k_dense_rows");
+  return CYC_OK;
+}
+
+int cyc_sparse_covariance_finalize_dev(int32_t n, const double* U, int64_t m, const double* mean,
+                                       double* G, void* stream) {
+  CYC_REQUIRE(m > 1, "RowMatrix.computeCovariance called on matrix with only " +
+                         std::to_string(m) + " rows.  Cannot compute the covariance of a "
+                         "RowMatrix with <= 1 row.");
+  CYC_REQUIRE(n > 0 && U && G && mean, "n > 0 and non-null buffers");
+  const int64_t tot = (int64_t)n * n;
+  hipLaunchKernelGGL(k_sparse_cov_finalize, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     cyc::as_stream(stream), n, U, (double)m, mean, G);
+  CYC_LAUNCH_CHECK("k_sparse_cov_finalize");
+  return CYC_OK;
+}
+
+int cyc_triu_to_full_dev(int32_t n, const double* U, double* G, void* stream) {
+  CYC_REQUIRE(n > 0 && U && G, "n > 0 and non-null buffers");
+  const int64_t tot = (int64_t)n * n;
+  hipLaunchKernelGGL(k_triu_to_full, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     cyc::as_stream(stream), n, U, G);
+  CYC_LAUNCH_CHECK("k_triu_to_full");
+  return CYC_OK;
+}
+
+int cyc_covariance_finalize_dev(int32_t n, const double* U, int64_t m, double* G, void* stream) {
+  CYC_REQUIRE(m > 1, "RowMatrix.computeCovariance called on matrix with only " +
+                         std::to_string(m) + " rows.  Cannot compute the covariance of a "
+                         "RowMatrix with <= 1 row.");
+  CYC_REQUIRE(n > 0 && U && G, "n > 0 and non-null buffers");
+  const int64_t tot = (int64_t)n * n;
+  hipLaunchKernelGGL(k_cov_finalize, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     cyc::as_stream(stream), n, U, (double)m - 1.0, G);
+  CYC_LAUNCH_CHECK("k_cov_finalize");
+  return CYC_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, const double* mean,
+                      double* U, hipStream_t st) {
   const int p = plan->p;
   const int tps = (p + TILE - 1) / TILE;
   const int pairs = tps * (tps + 1) / 2;
@@ -268,13 +447,8 @@ int cyc_gramian_accumulate_dev(cyc_gramian_plan plan, const double* X, int64_t n
   return CYC_OK;
 }
 
-int cyc_col_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
-                     void* stream) {
-  CYC_REQUIRE(plan != nullptr && sums != nullptr, "plan and sums must not be null");
-  CYC_REQUIRE(nrows >= 0, "nrows >= 0");
-  if (nrows == 0) return CYC_OK;
-  std::lock_guard<std::mutex> g(plan->mu);
-  hipStream_t st = cyc::as_stream(stream);
+int col_sums_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
+                    hipStream_t st) {
   const int p = plan->p;
   const int ctiles = (p + 255) / 256;
   int64_t splits = std::max<int64_t>(1, std::min<int64_t>(4096 / ctiles, nrows / 256));
@@ -291,25 +465,4 @@ int cyc_col_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, doub
   return CYC_OK;
 }
 
-int cyc_triu_to_full_dev(int32_t n, const double* U, double* G, void* stream) {
-  CYC_REQUIRE(n > 0 && U && G, "n > 0 and non-null buffers");
-  const int64_t tot = (int64_t)n * n;
-  hipLaunchKernelGGL(k_triu_to_full, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                     cyc::as_stream(stream), n, U, G);
-  CYC_LAUNCH_CHECK("k_triu_to_full");
-  return CYC_OK;
-}
-
-int cyc_covariance_finalize_dev(int32_t n, const double* U, int64_t m, double* G, void* stream) {
-  CYC_REQUIRE(m > 1, "RowMatrix.computeCovariance called on matrix with only " +
-                         std::to_string(m) + " rows.  Cannot compute the covariance of a "
-                         "RowMatrix with <= 1 row.");
-  CYC_REQUIRE(n > 0 && U && G, "n > 0 and non-null buffers");
-  const int64_t tot = (int64_t)n * n;
-  hipLaunchKernelGGL(k_cov_finalize, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                     cyc::as_stream(stream), n, U, (double)m - 1.0, G);
-  CYC_LAUNCH_CHECK("k_cov_finalize");
-  return CYC_OK;
-}
-
-}  // extern "C"
+}  // namespace

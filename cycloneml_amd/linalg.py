@@ -1,8 +1,9 @@
 """RowMatrix on MI355X: host-side mirror of
 mllib/linalg/distributed/RowMatrix.scala (Gramian, covariance, PCA).
 
-`rows` is this rank's device-resident shard (torch fp64 CUDA tensor, n x p,
-row-major: an RDD of DenseVector rows).  computeGramianMatrix /
+`rows` is this rank's device-resident shard: a torch fp64 CUDA tensor (n x p,
+row-major: an RDD of DenseVector rows) or a CSRRows triple (an RDD of
+SparseVector rows; rowptr int64, colidx int32, values fp64).  computeGramianMatrix /
 computeCovariance run the fp64-MFMA syrk of libcyclone and, when
 torch.distributed is initialised, merge the packed triangle with one
 all-reduce (the treeAggregate combOp U1 += U2, :149-157).  The eigensolve of
@@ -58,6 +59,27 @@ class GramianPlan:
         N.check(self._lib.cyc_col_sums_dev(self.handle, N.ptr(X), int(X.shape[0]), N.ptr(out),
                                            N.stream_handle(stream)))
 
+    def accumulate_csr(self, rows: "CSRRows", U, mean=None, stream=None):
+        N.check(self._lib.cyc_gramian_accumulate_csr_dev(
+            self.handle, N.ptr(rows.rowptr), N.ptr(rows.colidx), N.ptr(rows.values), rows.n,
+            N.ptr(mean), N.ptr(U), N.stream_handle(stream)))
+
+    def col_sums_csr(self, rows: "CSRRows", out, stream=None):
+        N.check(self._lib.cyc_col_sums_csr_dev(
+            self.handle, N.ptr(rows.rowptr), N.ptr(rows.colidx), N.ptr(rows.values), rows.n,
+            N.ptr(out), N.stream_handle(stream)))
+
+
+class CSRRows:
+    """SparseVector rows of a RowMatrix shard in HBM (CSR, rowptr may start at
+    any base)."""
+
+    def __init__(self, rowptr, colidx, values, numCols: int):
+        self.rowptr, self.colidx, self.values = rowptr, colidx, values
+        self.numCols = int(numCols)
+        self.n = int(rowptr.shape[0]) - 1
+        self.device = values.device
+
 
 def triu_to_full(n, U, stream=None):
     """RowMatrix.triuToFull (:845-867) on device; returns the (n, n) matrix."""
@@ -68,27 +90,41 @@ def triu_to_full(n, U, stream=None):
 
 
 class RowMatrix:
-    """RowMatrix(rows) over a device-resident shard."""
+    """RowMatrix(rows) over a device-resident shard (dense tensor or CSRRows)."""
 
     def __init__(self, rows, nRows: int = 0, nCols: int = 0):
         self.rows = rows
         self._nRows = nRows
         self._nCols = nCols
 
+    @property
+    def _sparse(self):
+        return isinstance(self.rows, CSRRows)
+
+    @property
+    def _device(self):
+        return self.rows.device
+
+    def _local_rows(self):
+        return self.rows.n if self._sparse else int(self.rows.shape[0])
+
     def numCols(self) -> int:
         if self._nCols <= 0:
-            if self.rows.shape[0] == 0 and _dist() is None:
-                raise RuntimeError("Cannot determine the number of cols because it is not "
-                                   "specified in the constructor and the rows RDD is empty.")
-            self._nCols = int(self.rows.shape[1])
+            if self._sparse:
+                self._nCols = self.rows.numCols
+            else:
+                if self.rows.shape[0] == 0 and _dist() is None:
+                    raise RuntimeError("Cannot determine the number of cols because it is not "
+                                       "specified in the constructor and the rows RDD is empty.")
+                self._nCols = int(self.rows.shape[1])
         return self._nCols
 
     def numRows(self) -> int:
         if self._nRows <= 0:
-            n = int(self.rows.shape[0])
+            n = self._local_rows()
             d = _dist()
             if d is not None:
-                t = _torch().tensor([n], dtype=_torch().int64, device=self.rows.device)
+                t = _torch().tensor([n], dtype=_torch().int64, device=self._device)
                 d.all_reduce(t)
                 n = int(t.item())
             if n == 0:
@@ -106,9 +142,12 @@ class RowMatrix:
         torch = _torch()
         n = self.numCols()
         self._checkNumColumns(n)
-        U = torch.zeros(n * (n + 1) // 2, dtype=torch.float64, device=self.rows.device)
+        U = torch.zeros(n * (n + 1) // 2, dtype=torch.float64, device=self._device)
         plan = GramianPlan(n)
-        plan.accumulate(self.rows, U, mean)
+        if self._sparse:
+            plan.accumulate_csr(self.rows, U, mean)
+        else:
+            plan.accumulate(self.rows, U, mean)
         parallel.allreduce_(U)             # treeAggregate combOp U1 += U2
         return U
 
@@ -123,14 +162,36 @@ class RowMatrix:
     def _column_mean(self):
         torch = _torch()
         n = self.numCols()
-        s = torch.zeros(n, dtype=torch.float64, device=self.rows.device)
-        GramianPlan(n).col_sums(self.rows, s)
+        s = torch.zeros(n, dtype=torch.float64, device=self._device)
+        if self._sparse:
+            GramianPlan(n).col_sums_csr(self.rows, s)
+        else:
+            GramianPlan(n).col_sums(self.rows, s)
         parallel.allreduce_(s)
         m = self.numRows()
         return s / m, m
 
+    def isSparseMatrix(self) -> bool:
+        """RowMatrix.isSparseMatrix (:439-441): no row has sparsity() < 0.5
+        (over all ranks)."""
+        torch = _torch()
+        cnt = torch.zeros(1, dtype=torch.int64, device=self._device)
+        n = self._local_rows()
+        if self._sparse:
+            N.check(N.load().cyc_rowmatrix_dense_rows_dev(
+                None, N.ptr(self.rows.rowptr), N.ptr(self.rows.values), n, self.numCols(),
+                N.ptr(cnt), N.stream_handle()))
+        else:
+            N.check(N.load().cyc_rowmatrix_dense_rows_dev(N.ptr(self.rows), None, None, n,
+                                                          self.numCols(), N.ptr(cnt),
+                                                          N.stream_handle()))
+        parallel.allreduce_(cnt)
+        return int(cnt.item()) == 0
+
     def computeCovariance(self) -> np.ndarray:
-        """RowMatrix.scala:452-467 -> computeDenseVectorCovariance (:163-220)."""
+        """RowMatrix.scala:452-467: computeDenseVectorCovariance (:163-220) or,
+        when every row has sparsity >= 0.5, computeSparseVectorCovariance
+        (:222-246) from the Gramian."""
         torch = _torch()
         n = self.numCols()
         self._checkNumColumns(n)
@@ -139,10 +200,15 @@ class RowMatrix:
             raise N.IllegalArgumentException(
                 f"RowMatrix.computeCovariance called on matrix with only {m} rows.  Cannot "
                 "compute the covariance of a RowMatrix with <= 1 row.")
-        U = self._packed(mean)
-        G = torch.empty(n * n, dtype=torch.float64, device=U.device)
-        N.check(N.load().cyc_covariance_finalize_dev(int(n), N.ptr(U), int(m), N.ptr(G),
-                                                     N.stream_handle()))
+        G = torch.empty(n * n, dtype=torch.float64, device=self._device)
+        if not self.isSparseMatrix():
+            U = self._packed(mean)
+            N.check(N.load().cyc_covariance_finalize_dev(int(n), N.ptr(U), int(m), N.ptr(G),
+                                                         N.stream_handle()))
+        else:
+            U = self._packed()
+            N.check(N.load().cyc_sparse_covariance_finalize_dev(
+                int(n), N.ptr(U), int(m), N.ptr(mean), N.ptr(G), N.stream_handle()))
         return G.view(n, n).t().cpu().numpy()
 
     def computePrincipalComponentsAndExplainedVariance(self, k: int):

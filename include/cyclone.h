@@ -182,6 +182,26 @@ int cyc_col_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, doub
 int cyc_triu_to_full_dev(int32_t n, const double* U, double* G, void* stream);
 /* computeDenseVectorCovariance's finish (:203-217): G = full(U) / (m - 1). */
 int cyc_covariance_finalize_dev(int32_t n, const double* U, int64_t m, double* G, void* stream);
+/* The same two passes over CSR rows (rowptr int64[nrows + 1], any base;
+ * colidx int32 validated as SparseVector indices): the sparse spr branch of
+ * BLAS.spr (mllib/linalg/BLAS.scala:269-298) -- the rows are densified in
+ * ~1 GiB chunks and go through the fp64 MFMA syrk, mean subtracted when
+ * given (the dense-covariance path on CSR rows) -- and the column sums. */
+int cyc_gramian_accumulate_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr,
+                                   const int32_t* colidx, const double* vals, int64_t nrows,
+                                   const double* mean, double* U, void* stream);
+int cyc_col_sums_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr, const int32_t* colidx,
+                         const double* vals, int64_t nrows, double* sums, void* stream);
+/* RowMatrix.isSparseMatrix (:439-441): *count (device int64) = rows whose
+ * sparsity() = 1 - numNonzeros / ncols is below 0.5, over dense X OR CSR
+ * (rowptr, vals); the matrix is sparse iff the count (summed over ranks) is 0. */
+int cyc_rowmatrix_dense_rows_dev(const double* X, const int64_t* rowptr, const double* vals,
+                                 int64_t nrows, int32_t ncols, int64_t* count, void* stream);
+/* computeSparseVectorCovariance (:222-246) from the packed Gramian U:
+ * G(i, j) = U(i, j) / (m - 1) - (m / (m - 1) * mean(i)) * mean(j), i <= j,
+ * mirrored (n x n column-major). */
+int cyc_sparse_covariance_finalize_dev(int32_t n, const double* U, int64_t m, const double* mean,
+                                       double* G, void* stream);
 
 /* ---------------------------------------------- logistic block aggregators */
 /* BinaryLogisticBlockAggregator.add (ml/optim/aggregator/

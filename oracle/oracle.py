@@ -561,6 +561,44 @@ def triu_to_full(n, U) -> np.ndarray:
     return G
 
 
+def gramian_csr(rowptr, colidx, vals, n, U=None):
+    """computeGramianMatrix's seqOp over SparseVector rows: the sparse spr
+    branch (mllib/linalg/BLAS.scala:269-298) per row, in row order."""
+    if U is None:
+        U = np.zeros(n * (n + 1) // 2, dtype=np.float64)
+    for r in range(len(rowptr) - 1):
+        a, b = int(rowptr[r]), int(rowptr[r + 1])
+        if b > a:
+            spr_sparse(colidx[a:b], vals[a:b], U)
+    return U
+
+
+def is_sparse_matrix(row_nnz, ncols) -> bool:
+    """RowMatrix.isSparseMatrix (RowMatrix.scala:439-441): no row with
+    sparsity() = 1.0 - numNonzeros / size below 0.5."""
+    nz = np.asarray(row_nnz, dtype=np.float64)
+    return not bool(np.any(1.0 - nz / float(ncols) < 0.5))
+
+
+def sparse_vector_covariance(n, U, mean, m):
+    """computeSparseVectorCovariance (RowMatrix.scala:222-246) on the packed
+    Gramian: column-major n*n, the i <= j loop mirrored."""
+    G = triu_to_full(n, U).reshape(n, n).T.copy()      # G[i, j]
+    m1 = m - 1.0
+    for i in range(n):
+        alpha = m / m1 * mean[i]
+        for j in range(i, n):
+            gij = G[i, j] / m1 - alpha * mean[j]
+            G[i, j] = gij
+            G[j, i] = gij
+    return G
+
+
+def dense_vector_covariance(n, U, m):
+    """computeDenseVectorCovariance's finish (:203-217): full(U) / (m - 1)."""
+    return triu_to_full(n, U).reshape(n, n).T / (m - 1.0)
+
+
 # --------------------------------------------------------------------------
 # java.util.Random (for regenerating the reference suites' datasets)
 # --------------------------------------------------------------------------

@@ -479,3 +479,30 @@ def test_fast_squared_distance_require():
     C[2, 0] = np.nan
     with pytest.raises(oracle.IllegalArgumentException, match="norm1=.*, norm2=NaN"):
         oracle.kmeans_stats(C)
+
+
+def test_rowmatrix_sparse_paths_restated():
+    """RowMatrixSuite sparseData (RowMatrixSuite.scala:45-50): the sparse spr
+    Gramian is the exact gram [126, 54, 72, ...] (:95-102); the rows have
+    sparsity 1/3 or 0, so isSparseMatrix is false and computeCovariance takes
+    the dense path; a matrix whose rows are all at least half zeros takes
+    computeSparseVectorCovariance, which equals breeze-style cov (np.cov)
+    to rounding."""
+    rp = np.array([0, 2, 5, 8, 10])
+    ci = np.array([1, 2, 0, 1, 2, 0, 1, 2, 0, 2])
+    v = np.array([1.0, 2.0, 3.0, 4.0, 5.0, 6.0, 7.0, 8.0, 9.0, 1.0])
+    U = oracle.gramian_csr(rp, ci, v, 3)
+    G = oracle.triu_to_full(3, U)
+    assert list(G) == [126.0, 54.0, 72.0, 54.0, 66.0, 78.0, 72.0, 78.0, 94.0]
+    assert not oracle.is_sparse_matrix(np.diff(rp), 3)
+    assert oracle.is_sparse_matrix([2, 1, 0], 4)      # sparsity 0.5 is not < 0.5
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(50, 6))
+    X[rng.random(X.shape) < 0.6] = 0.0
+    X[:, 0] = np.where(np.arange(50) % 2 == 0, 0.0, 1.5)
+    nz = np.count_nonzero(X, axis=1)
+    X[nz > 3, 1:] = 0.0
+    assert oracle.is_sparse_matrix(np.count_nonzero(X, axis=1), 6)
+    U = oracle.gramian_partition(X)
+    cov = oracle.sparse_vector_covariance(6, U, X.mean(0), 50)
+    np.testing.assert_allclose(cov, np.cov(X.T), rtol=1e-10, atol=1e-12)
