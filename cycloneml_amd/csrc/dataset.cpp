@@ -500,10 +500,6 @@ int cyc_logreg_multinomial_eval(cyc_dataset ds, int32_t numClasses, const double
 
 int cyc_gramian(cyc_dataset ds, const double* mean_opt, double* U) {
   CYC_REQUIRE(ds != nullptr && U, "arguments must not be null");
-  if (ds->sparse) {
-    cyc::set_error("Gramian over a CSR dataset is not supported by the device path");
-    return CYC_ERR_UNSUPPORTED;
-  }
   DeviceGuard g(ds->device);
   int rc;
   if (!ds->gplan && (rc = cyc_gramian_plan_create(ds->F, &ds->gplan))) return rc;
@@ -511,9 +507,13 @@ int cyc_gramian(cyc_dataset ds, const double* mean_opt, double* U) {
   double *dU, *dM = nullptr;
   if ((rc = upload(ds->out0, U, nu, ds->st, &dU))) return rc;
   if (mean_opt && (rc = upload(ds->in1, mean_opt, ds->F, ds->st, &dM))) return rc;
-  if ((rc = cyc_gramian_accumulate_dev(ds->gplan, (const double*)ds->X.ptr, ds->rows, dM, dU,
-                                       ds->st)))
-    return rc;
+  rc = ds->sparse
+           ? cyc_gramian_accumulate_csr_dev(ds->gplan, (const int64_t*)ds->rowptr.ptr,
+                                            (const int32_t*)ds->colidx.ptr,
+                                            (const double*)ds->vals.ptr, ds->rows, dM, dU, ds->st)
+           : cyc_gramian_accumulate_dev(ds->gplan, (const double*)ds->X.ptr, ds->rows, dM, dU,
+                                        ds->st);
+  if (rc) return rc;
   if ((rc = download(U, dU, nu, ds->st))) return rc;
   CYC_HIP(hipStreamSynchronize(ds->st));
   return CYC_OK;
@@ -521,17 +521,16 @@ int cyc_gramian(cyc_dataset ds, const double* mean_opt, double* U) {
 
 int cyc_col_sums(cyc_dataset ds, double* sums) {
   CYC_REQUIRE(ds != nullptr && sums, "arguments must not be null");
-  if (ds->sparse) {
-    cyc::set_error("column sums over a CSR dataset are not supported by the device path");
-    return CYC_ERR_UNSUPPORTED;
-  }
   DeviceGuard g(ds->device);
   int rc;
   if (!ds->gplan && (rc = cyc_gramian_plan_create(ds->F, &ds->gplan))) return rc;
   double* dS;
   if ((rc = upload(ds->out1, sums, ds->F, ds->st, &dS))) return rc;
-  if ((rc = cyc_col_sums_dev(ds->gplan, (const double*)ds->X.ptr, ds->rows, dS, ds->st)))
-    return rc;
+  rc = ds->sparse ? cyc_col_sums_csr_dev(ds->gplan, (const int64_t*)ds->rowptr.ptr,
+                                         (const int32_t*)ds->colidx.ptr,
+                                         (const double*)ds->vals.ptr, ds->rows, dS, ds->st)
+                  : cyc_col_sums_dev(ds->gplan, (const double*)ds->X.ptr, ds->rows, dS, ds->st);
+  if (rc) return rc;
   if ((rc = download(sums, dS, ds->F, ds->st))) return rc;
   CYC_HIP(hipStreamSynchronize(ds->st));
   return CYC_OK;

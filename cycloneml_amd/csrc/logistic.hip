@@ -418,18 +418,27 @@ __global__ void k_mlr_offset(const double* __restrict__ coef, const double* __re
   off[c] = o;
 }
 
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+typedef int v2i32 __attribute__((ext_vector_type(2)));
+
 constexpr int MR = 256;    // rows per margin tile (8 waves x 32 rows)
 constexpr int MK = 16;     // features per LDS chunk
-constexpr int MKS = MK + 2;  // X chunk row stride: 36 dwords, conflict-free ds_read_b64
 constexpr int MT = 512;    // threads per margin workgroup
 
-// margins = X W^T (+ offset) for 256-row tiles; X and W chunks of 16
-// features staged through LDS (coalesced loads), 2 row tiles x CT class tiles
-// of 16x16 per wave on v_mfma_f64_16x16x4f64; softmax/loss/multiplier
-// epilogue in registers.  Persistent over tiles, one 8-wave workgroup per CU;
-// the next chunk of X and W is loaded into registers while the current one is
-// multiplied (one LDS buffer, no load latency on the MFMA path), and the
-// 256-row tile halves the W re-reads per row of a 4-wave tile.
+// margins = X W^T (+ offset) for 256-row tiles, 16-feature chunks, on
+// v_mfma_f64_16x16x4f64: 2 row tiles x CT class tiles of 16x16 per wave;
+// softmax / loss / multiplier epilogue in registers.  Persistent over tiles,
+// one 8-wave workgroup per CU.
+// X goes from HBM straight into registers in the MFMA A layout -- lane (row
+// r = l & 15, group g = l >> 4) holds features f0 + 4g .. 4g + 3 of its row
+// for k-steps 0..3 (the contraction order within a chunk is permuted: 128
+// contiguous bytes per row per chunk, two dwordx4 loads per lane per row
+// tile) -- loaded one chunk ahead into a second register set: no LDS, no
+// barrier for X.  W chunks (16 features x C classes, contiguous in coef,
+// 12.8 KB at C = 100) are DMA'd into two LDS buffers (buffer_load ... lds,
+// 1 KiB pieces spread over the waves, one chunk ahead; no registers), one
+// barrier per chunk.  Padding classes read the next coefficients (finite;
+// their margins are never used) or zero past the end of coef.
 template <int CT>
 __global__ __launch_bounds__(MT) void k_mlr_margins(
     const double* __restrict__ X, const double* __restrict__ labels,
@@ -437,82 +446,59 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
     const double* __restrict__ offset, double* __restrict__ mult, double* __restrict__ slabS,
     double* __restrict__ slabMS) {
   constexpr int CP = CT * 16;
-  constexpr int CPS = CP + ((16 - CP % 32) + 32) % 32;  // == 16 (mod 32) doubles
-  constexpr int XPT = MR * MK / MT;                     // X doubles per thread (16)
-  constexpr int WPT = (MK * CP + MT - 1) / MT;          // W doubles per thread
-  __shared__ __attribute__((aligned(16))) double Xs[MR * MKS];
-  __shared__ __attribute__((aligned(16))) double Ws[MK * CPS];
+  static_assert(MK == 16, "the A layout covers 16 features per chunk");
+  constexpr int WBUF = MK * CP + 128;   // doubles per W buffer (whole 1 KiB pieces)
+  __shared__ __attribute__((aligned(16))) double Ws[2][WBUF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4;
   const int64_t tiles = (n + MR - 1) / MR;
   const int nch = (F + MK - 1) / MK;
   double loss = 0.0, wsum = 0.0;
   double ms[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) ms[ct] = 0.0;
-  double xr[XPT], wr[WPT];
-  // Loads go through buffer descriptors: one 32-bit VGPR offset per element
-  // (no 64-bit address math held across the loop); rows past n and padding
-  // classes read as zero (out-of-range offsets).  Host guarantees
-  // MR * F * 8 < 2^31 and C * F * 8 < 2^31.
+  // Loads go through buffer descriptors: 32-bit offsets; rows past n read
+  // as zero (out-of-range offsets).  Host guarantees MR * F * 8 < 2^31 and
+  // (C * F + C) * 8 < 2^31.
   constexpr int OOB = 0x7ff00000;
-  const auto wR = __builtin_amdgcn_make_buffer_rsrc((void*)coef, (short)0, C * F * 8, 0x00020000);
-  const int xlane = ((tid / MK) * F + (tid % MK)) * 8;
-  auto load_regs = [&](int64_t r0, int f0) {
+  const auto wR = __builtin_amdgcn_make_buffer_rsrc((void*)coef, (short)0, (C * F + C) * 8,
+                                                    0x00020000);
+  // pieces covering every index the B reads touch: (MK - 1) C + CP doubles
+  const int wpieces = (((MK - 1) * C + CP) * 8 + 1023) / 1024;
+  auto loadW = [&](int ch) {      // chunk ch's 16 x C run of coef into buffer ch & 1
+    double* dst = Ws[ch & 1];
+    const int base = ch * MK * C * 8;
+    for (int q = wave; q < wpieces; q += MT / 64)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wR, (__attribute__((address_space(3))) void*)(dst + q * 128), 16, base + q * 1024 +
+          lane * 16, 0, 0, 0);
+  };
+  auto loadX = [&](int64_t r0, int ch, double (&x)[2][4]) {
+    const int f0 = ch * MK + 4 * g;
     const int64_t nr = min<int64_t>(MR, n - r0);
     const auto xR = __builtin_amdgcn_make_buffer_rsrc((void*)(X + r0 * F), (short)0,
                                                       (int)(nr * F * 8), 0x00020000);
-    const bool fok = f0 + (tid % MK) < F;
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int off = fok ? xlane + i * (MT / MK) * F * 8 + f0 * 8 : OOB;
-      xr[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xR, off, 0, 0));
-    }
-    // features f0..f0+MK-1 are one contiguous run of coef (f*C + c)
-    const int fl = min(MK, F - f0);
+    for (int t = 0; t < 2; ++t) {
+      const int off = ((wave * 32 + t * 16 + (lane & 15)) * F + f0) * 8;
+      if (f0 + 3 < F) {
+        const v4i32 lo = __builtin_amdgcn_raw_buffer_load_b128(xR, off, 0, 0);
+        const v4i32 hi = __builtin_amdgcn_raw_buffer_load_b128(xR, off + 16, 0, 0);
+        x[t][0] = __builtin_bit_cast(double, (v2i32){lo[0], lo[1]});
+        x[t][1] = __builtin_bit_cast(double, (v2i32){lo[2], lo[3]});
+        x[t][2] = __builtin_bit_cast(double, (v2i32){hi[0], hi[1]});
+        x[t][3] = __builtin_bit_cast(double, (v2i32){hi[2], hi[3]});
+      } else {
 #pragma unroll
-    for (int i = 0; i < WPT; ++i) {
-      const int e = tid + MT * i;
-      const int ff = e / CP, c = e - ff * CP;
-      const int off = (e < MK * CP && ff < fl && c < C) ? ((f0 + ff) * C + c) * 8 : OOB;
-      wr[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(wR, off, 0, 0));
+        for (int j = 0; j < 4; ++j)
+          x[t][j] = __builtin_bit_cast(
+              double, __builtin_amdgcn_raw_buffer_load_b64(xR, f0 + j < F ? off + 8 * j : OOB, 0,
+                                                           0));
+      }
     }
   };
-
-  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    const int64_t r0 = tile * MR;
-    cyc_double4 acc[2][CT];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) acc[t][ct] = cyc_double4{0.0, 0.0, 0.0, 0.0};
-    load_regs(r0, 0);
-    for (int ch = 0; ch < nch; ++ch) {
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < XPT; ++i) {
-        const int e = tid + MT * i;
-        Xs[(e / MK) * MKS + (e % MK)] = xr[i];
-      }
-#pragma unroll
-      for (int i = 0; i < WPT; ++i) {
-        const int e = tid + MT * i;
-        const int ff = e / CP, c = e - ff * CP;
-        if (e < MK * CP) Ws[ff * CPS + c] = wr[i];
-      }
-      __syncthreads();
-      if (ch + 1 < nch) load_regs(r0, (ch + 1) * MK);
-#pragma unroll
-      for (int kk = 0; kk < MK; kk += 4) {
-        const double a0 = Xs[(wave * 32 + (lane & 15)) * MKS + kk + (lane >> 4)];
-        const double a1 = Xs[(wave * 32 + 16 + (lane & 15)) * MKS + kk + (lane >> 4)];
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          const double b = Ws[(kk + (lane >> 4)) * CPS + ct * 16 + (lane & 15)];
-          acc[0][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b, acc[0][ct], 0, 0, 0);
-          acc[1][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b, acc[1][ct], 0, 0, 0);
-        }
-      }
-    }
+  cyc_double4 acc[2][CT];
+  auto epilogue = [&](int64_t r0) {
     // Epilogue: lane holds rows 32 wave + 16 t + (lane>>4) + 4r, classes
     // 16 ct + (lane & 15).
 #pragma unroll
@@ -588,6 +574,42 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
         }
       }
     }
+  };
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int64_t r0 = tile * MR;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[t][ct] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+    double xa[2][4], xb[2][4];
+    __syncthreads();   // the previous tile's last W buffer is free
+    loadX(r0, 0, xa);
+    loadW(0);
+    // chunk ch: wait for its loads, barrier (its W visible everywhere, every
+    // wave past chunk ch - 1), issue chunk ch + 1's loads, multiply
+    auto step = [&](int ch, double (&xc)[2][4], double (&xn)[2][4]) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (ch + 1 < nch) {
+        loadX(r0, ch + 1, xn);
+        loadW(ch + 1);
+      }
+      const double* W = Ws[ch & 1];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const double b = W[(4 * g + kk) * C + ct * 16 + (lane & 15)];
+          acc[0][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(xc[0][kk], b, acc[0][ct], 0, 0, 0);
+          acc[1][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(xc[1][kk], b, acc[1][ct], 0, 0, 0);
+        }
+      }
+    };
+    for (int ch = 0; ch < nch; ch += 2) {
+      step(ch, xa, xb);
+      if (ch + 1 < nch) step(ch + 1, xb, xa);
+    }
+    epilogue(r0);
   }
   // per-wave partials: loss/wsum from lanes with (lane & 15) == 0, multSum
   // per class summed over the 4 row groups of the wave.
@@ -1386,7 +1408,7 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
     cyc::set_error("multinomial aggregator supports numClasses <= 128");
     return CYC_ERR_UNSUPPORTED;
   }
-  if ((int64_t)C * F * 8 >= INT32_MAX || (int64_t)MR * F * 8 >= INT32_MAX) {
+  if (((int64_t)C * F + C) * 8 >= INT32_MAX || (int64_t)MR * F * 8 >= INT32_MAX) {
     cyc::set_error("dense multinomial aggregator supports numClasses * numFeatures < 2^28 "
                    "and numFeatures < 2^20");
     return CYC_ERR_UNSUPPORTED;

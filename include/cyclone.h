@@ -430,8 +430,8 @@ int cyc_blokify_dev(const double* X, const int64_t* rowptr, const double* vals,
  *   cyc_logreg_*_eval           RDDLossFunction.scala:56-70's seqOp over the
  *                               partition's blocks
  *   cyc_gramian, cyc_col_sums   RowMatrix.scala:130-161, :163-220, :456
- * Dense datasets serve every entry point; CSR datasets serve KMeans and both
- * logistic aggregators (the Gramian calls return CYC_ERR_UNSUPPORTED). */
+ * Dense and CSR datasets serve every entry point (CSR Gramian / column sums:
+ * the sparse spr rows densified in chunks, cyc_gramian_accumulate_csr_dev). */
 typedef struct cyc_dataset_s* cyc_dataset;
 
 int cyc_dataset_dense_create(int32_t numFeatures, int64_t capacity_rows, int has_labels,
