@@ -1705,7 +1705,8 @@ struct cyc_kmeans_plan_s {
   size_t assignLds2 = 0;
   // bf16x3 screen (variant 3): k-steps of 32 dims, padded 16-center tiles,
   // center tiles per wave group, LDS bytes, error-bound constants
-  int ks3 = 0, ktp3 = 0, tb3 = 2;
+  int ks3 = 0, ktp3 = 0;
+  static constexpr int tb3 = 2;
   size_t lds3 = 0;
   double omE3 = 1.0, tauL3 = 0.0, facU3 = 0.0, tauU3 = 0.0;
   int64_t lastTier2 = 0;    // rows the bf16 screen queued (last counted call)
@@ -1743,8 +1744,7 @@ namespace {
 
 int pick_bm(int d4, int& stride, size_t& lds) {
   const int cands[3] = {64, 32, 16};
-  int maxbm = 64;
-  if (const char* v = std::getenv("CYC_KMEANS_BM")) maxbm = std::atoi(v);
+  const int maxbm = 64;
   for (int bm : cands) {
     if (bm > maxbm) continue;
     int s = d4 + ((2 - d4 % 32) + 32) % 32;  // stride == 2 (mod 32)
@@ -1876,8 +1876,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
                        cnorm, p->k, p->d, p->ks3, p->ktp3, p->omE3, (uint4*)p->cb3.ptr,
                        (float*)p->cq3.ptr, (int*)p->ok3.ptr);
     CYC_LAUNCH_CHECK("k_center_split");
-    rc = p->tb3 == 4 ? launch_assign3<4>(p, X, xnorm, n, C, cnorm, assign, cost, st)
-                     : launch_assign3<2>(p, X, xnorm, n, C, cnorm, assign, cost, st);
+    rc = launch_assign3<2>(p, X, xnorm, n, C, cnorm, assign, cost, st);
     if (rc) return rc;
     rowList = (const int32_t*)p->list3.ptr;
     rowCount = (const unsigned int*)p->list3Count.ptr;
@@ -2020,7 +2019,6 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
                       (want != 3 || fits3)))
       p->variant = want;
   }
-  if (const char* v = std::getenv("CYC_S3_TB")) p->tb3 = std::atoi(v) == 4 ? 4 : 2;
   {
     p->ktp3 = (int)cyc::round_up((k + 15) / 16, kS3Waves * p->tb3);
     const double d32 = 32.0 * p->ks3;

@@ -631,19 +631,25 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
   }
 }
 
-constexpr int GR = 32;    // rows per LDS chunk in the gradient GEMM
+constexpr int GR = 32;    // rows per chunk in the gradient GEMM
 constexpr int GF = 256;   // features per workgroup
-constexpr int GFS = GF + 16;
 
+// grad^T (CP x GF per workgroup) = mult^T X over one split of rows, on
+// v_mfma_f64_16x16x4f64 (8 waves x 32 features x CP classes).  Per 32-row
+// chunk: the multipliers (32 x CP, contiguous) are DMA'd into one of two LDS
+// buffers (buffer_load ... lds, 1 KiB pieces over the waves), X goes from
+// HBM straight into registers in the MFMA B layout (lane: feature l & 15 of
+// its 16-feature tile, row 4 kk + (l >> 4) of k-step kk; 128 contiguous
+// bytes per row), both one chunk ahead; one barrier per chunk.
 template <int CT>
 __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mult,
                                                   const double* __restrict__ X, int64_t n, int F,
                                                   int64_t rowsPerSplit,
                                                   double* __restrict__ slab) {
   constexpr int CP = CT * 16;
-  constexpr int CPS = CP + ((16 - CP % 32) + 32) % 32;
-  __shared__ __attribute__((aligned(16))) double Ms[GR * CPS];
-  __shared__ __attribute__((aligned(16))) double Xs[GR * GFS];
+  constexpr int MB = GR * CP;                       // doubles per multiplier chunk
+  constexpr int MPIECES = (MB * 8 + 1023) / 1024;
+  __shared__ __attribute__((aligned(16))) double Ms[2][MPIECES * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int F0 = blockIdx.x * GF;
   const int64_t r0 = (int64_t)blockIdx.y * rowsPerSplit;
@@ -651,63 +657,60 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
   cyc_double4 acc[CT][2];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) acc[ct][0] = acc[ct][1] = cyc_double4{0.0, 0.0, 0.0, 0.0};
-  // Register prefetch of the next GR-row chunk while this one is multiplied.
-  // Loads go through buffer descriptors over this split's rows: 32-bit
-  // offsets, rows past the split and features past F read as zero
-  // (out-of-range offsets).  Host: rowsPerSplit * max(F, CP) * 8 < 2^31.
-  constexpr int MPT = (GR * CP + 511) / 512;   // mult doubles per thread
-  constexpr int XPT = GR * GF / 512;           // X doubles per thread
+  // Buffer descriptors over this split's rows: 32-bit offsets, rows past the
+  // split and features past F read as zero.  Host: rowsPerSplit * max(F, CP)
+  // * 8 < 2^31.
   constexpr int OOB = 0x7ff00000;
-  double mreg[MPT], xreg[XPT];
   const int64_t nr = r1 > r0 ? r1 - r0 : 0;
   const auto mR = __builtin_amdgcn_make_buffer_rsrc((void*)(mult + r0 * CP), (short)0,
                                                     (int)(nr * CP * 8), 0x00020000);
   const auto xR = __builtin_amdgcn_make_buffer_rsrc((void*)(X + r0 * F), (short)0,
                                                     (int)(nr * F * 8), 0x00020000);
-  const bool fok = F0 + (tid & (GF - 1)) < F;
-  auto load_regs = [&](int64_t rb) {
+  const int g = lane >> 4;
+  const int fcol = F0 + wave * 32 + (lane & 15);
+  auto loadM = [&](int64_t rb, int buf) {
+    const int base = (int)(rb - r0) * CP * 8;
+    for (int q = wave; q < MPIECES; q += 8)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          mR, (__attribute__((address_space(3))) void*)(&Ms[buf][q * 128]), 16,
+          base + q * 1024 + lane * 16, 0, 0, 0);
+  };
+  auto loadX = [&](int64_t rb, double (&x)[GR / 4][2]) {
     const int rowOff = (int)(rb - r0);
 #pragma unroll
-    for (int i = 0; i < MPT; ++i) {
-      const int e = tid + 512 * i;
-      const int off = e < GR * CP ? (rowOff * CP + e) * 8 : OOB;
-      mreg[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(mR, off, 0, 0));
-    }
+    for (int kk = 0; kk < GR / 4; ++kk)
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int e = tid + 512 * i;
-      const int rr = e / GF, ff = e & (GF - 1);
-      const int off = fok ? ((rowOff + rr) * F + F0 + ff) * 8 : OOB;
-      xreg[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xR, off, 0, 0));
-    }
+      for (int q = 0; q < 2; ++q) {
+        const int f = fcol + 16 * q;
+        const int off = f < F ? ((rowOff + 4 * kk + g) * F + f) * 8 : OOB;
+        x[kk][q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xR, off, 0, 0));
+      }
   };
-  if (r0 < r1) load_regs(r0);
-  for (int64_t rb = r0; rb < r1; rb += GR) {
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < MPT; ++i) {
-      const int e = tid + 512 * i;
-      const int rr = e / CP, c = e - rr * CP;
-      if (e < GR * CP) Ms[rr * CPS + c] = mreg[i];
+  auto step = [&](int64_t rb, int buf, double (&xc)[GR / 4][2], double (&xn)[GR / 4][2]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // chunk rb's multipliers visible; every wave past the previous chunk
+    if (rb + GR < r1) {
+      loadX(rb + GR, xn);
+      loadM(rb + GR, buf ^ 1);
     }
+    const double* M = Ms[buf];
 #pragma unroll
-    for (int i = 0; i < XPT; ++i) {
-      const int e = tid + 512 * i;
-      Xs[(e / GF) * GFS + (e & (GF - 1))] = xreg[i];
-    }
-    __syncthreads();
-    if (rb + GR < r1) load_regs(rb + GR);
-#pragma unroll
-    for (int kk = 0; kk < GR; kk += 4) {
-      const int krow = kk + (lane >> 4);
-      double b0 = Xs[krow * GFS + wave * 32 + (lane & 15)];
-      double b1 = Xs[krow * GFS + wave * 32 + 16 + (lane & 15)];
+    for (int kk = 0; kk < GR / 4; ++kk) {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        const double a = Ms[krow * CPS + ct * 16 + (lane & 15)];
-        acc[ct][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b0, acc[ct][0], 0, 0, 0);
-        acc[ct][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b1, acc[ct][1], 0, 0, 0);
+        const double a = M[(4 * kk + g) * CP + ct * 16 + (lane & 15)];
+        acc[ct][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, xc[kk][0], acc[ct][0], 0, 0, 0);
+        acc[ct][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, xc[kk][1], acc[ct][1], 0, 0, 0);
       }
+    }
+  };
+  if (r0 < r1) {
+    double xa[GR / 4][2], xb[GR / 4][2];
+    loadX(r0, xa);
+    loadM(r0, 0);
+    for (int64_t rb = r0; rb < r1; rb += 2 * GR) {
+      step(rb, 0, xa, xb);
+      if (rb + GR < r1) step(rb + GR, 1, xb, xa);
     }
   }
   // slab[split][ftile][c][f_local]
