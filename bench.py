@@ -67,7 +67,10 @@ def pmc_traffic(workload, kernels, launches_per_step, rows):
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            per_step = sum(d[k]["hbm_bytes_per_step"] for k in kernels)
+            have = [k for k in kernels if k in d]
+            if not have:
+                continue
+            per_step = sum(d[k]["hbm_bytes_per_step"] for k in have)
             return per_step / launches_per_step * rows / d["_rows"], os.path.basename(f)
         except Exception:
             continue
@@ -94,7 +97,7 @@ class KMeansWorkload:
     (row, padded center, 64-dim step), priced against the dense i8 MFMA peak;
     the fp64-equivalent rate (2 k d flop per row) is reported beside it."""
     kernel = "k_kmeans_assign"
-    pmc_kernels = ("k_screen",)
+    pmc_kernels = ("k_screen32", "k_screen")   # d <= 256 / d <= 512 forms
     bound = "mfma"
     unit = "TOPS"
     peak = I8_PEAK_TOPS
