@@ -63,7 +63,9 @@ def test_csr_buffer_bitexact_two_row_blocks(cuda):
     from cycloneml_amd.stat import SummarizerBuffer
     rng = np.random.default_rng(3)
     n, F, k = 300_000, 1000, 8
-    cols = np.sort(rng.choice(F, size=(n, k)), axis=1).astype(np.int32)
+    # k distinct increasing columns per row (one per stratum of F / k), as a
+    # SparseVector requires (Vectors.scala:617-625)
+    cols = (np.arange(k) * (F // k) + rng.integers(0, F // k, size=(n, k))).astype(np.int32)
     vals = rng.normal(size=(n, k))
     vals[rng.random((n, k)) < 0.05] = 0.0        # explicit zeros are skipped
     rp = np.arange(0, n * k + 1, k, dtype=np.int64)
