@@ -67,6 +67,17 @@ class LogisticRegressionModel:
     def numFeatures(self) -> int:
         return int(self.coefficientMatrix.shape[1])
 
+    def save(self, path, estimator=None, overwrite=False):
+        """model.write.save(path) in Spark's format (cycloneml_amd.persist)."""
+        from . import persist
+        persist.save_logistic_model(self, path, estimator, getattr(self, "uid", None),
+                                    overwrite=overwrite)
+
+    @staticmethod
+    def load(path) -> "LogisticRegressionModel":
+        from . import persist
+        return persist.load_logistic_model(path)
+
     @property
     def coefficients(self) -> np.ndarray:
         if self.isMultinomial:

@@ -178,6 +178,17 @@ class KMeansModel:
     def k(self):
         return self.clusterCenters.shape[0]
 
+    # ---- persistence (KMeansModel.scala:148-224, format "2.0") -----------
+    def save(self, path, overwrite=False):
+        from . import persist
+        persist.save_kmeans_model(self, path, getattr(self, "distanceMeasure", "euclidean"),
+                                  overwrite=overwrite)
+
+    @staticmethod
+    def load(path):
+        from . import persist
+        return persist.load_kmeans_model(path)
+
     # ---- device-side scoring (KMeansModel.scala:82-117) -----------------
     def _device_state(self, device, n, csr_d=None):
         torch = _torch()
