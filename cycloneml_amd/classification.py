@@ -8,8 +8,8 @@ Host-side mirror of ml/classification/LogisticRegression.scala:
   createInitialSolution :822-933
   trainImpl         :935-1035 (fitWithMean, the initial / final intercept
                                adaptation, the optimizer loop)
-with the reference's parameter names, defaults and error texts.  Bounds on
-coefficients (LBFGS-B) are not built here.
+with the reference's parameter names, defaults and error texts, including
+bound-constrained fits (createBounds :732-775, LBFGS-B).
 
 Standardization.  The reference scales every instance by inverseStd into a
 new RDD before blockifying (:962-968) and runs the aggregators on the scaled
@@ -131,7 +131,90 @@ class LogisticRegression:
         self.aggregationDepth = int(aggregationDepth)
         self.maxBlockSizeInMB = float(maxBlockSizeInMB)
         self.initialModel: Optional[LogisticRegressionModel] = None
+        self.lowerBoundsOnCoefficients = None     # (numCoefficientSets, numFeatures)
+        self.upperBoundsOnCoefficients = None
+        self.lowerBoundsOnIntercepts = None       # (numCoefficientSets,)
+        self.upperBoundsOnIntercepts = None
         self._validate()
+
+    @property
+    def usingBoundConstrainedOptimization(self) -> bool:
+        """:251-254"""
+        return any(b is not None for b in (self.lowerBoundsOnCoefficients,
+                                           self.upperBoundsOnCoefficients,
+                                           self.lowerBoundsOnIntercepts,
+                                           self.upperBoundsOnIntercepts))
+
+    def setLowerBoundsOnCoefficients(self, M):
+        self.lowerBoundsOnCoefficients = np.atleast_2d(np.asarray(M, dtype=np.float64)); return self
+
+    def setUpperBoundsOnCoefficients(self, M):
+        self.upperBoundsOnCoefficients = np.atleast_2d(np.asarray(M, dtype=np.float64)); return self
+
+    def setLowerBoundsOnIntercepts(self, v):
+        self.lowerBoundsOnIntercepts = np.atleast_1d(np.asarray(v, dtype=np.float64)); return self
+
+    def setUpperBoundsOnIntercepts(self, v):
+        self.upperBoundsOnIntercepts = np.atleast_1d(np.asarray(v, dtype=np.float64)); return self
+
+    def _check_bounds(self, numCoefficientSets, numFeatures):
+        """validateAndTransformSchema (:258-268) and
+        assertBoundConstrainedOptimizationParamsValid (:442-485)."""
+        def req(c, msg):
+            if not c:
+                raise N.IllegalArgumentException("requirement failed: " + msg)
+        if not self.usingBoundConstrainedOptimization:
+            return
+        req(self.elasticNetParam == 0.0, "Fitting under bound constrained optimization only "
+            f"supports L2 regularization, but got elasticNetParam = {self.elasticNetParam}.")
+        if not self.fitIntercept:
+            req(self.lowerBoundsOnIntercepts is None and self.upperBoundsOnIntercepts is None,
+                "Please don't set bounds on intercepts if fitting without intercept.")
+        for name, M in (("LowerBoundsOnCoefficients", self.lowerBoundsOnCoefficients),
+                        ("upperBoundsOnCoefficients", self.upperBoundsOnCoefficients)):
+            if M is not None:
+                req(M.shape == (numCoefficientSets, numFeatures),
+                    f"The shape of {name} must be compatible with (1, number of features) for "
+                    "binomial regression, or (number of classes, number of features) for "
+                    f"multinomial regression, but found: ({M.shape[0]}, {M.shape[1]}).")
+        for name, v in (("lowerBoundsOnIntercepts", self.lowerBoundsOnIntercepts),
+                        ("upperBoundsOnIntercepts", self.upperBoundsOnIntercepts)):
+            if v is not None:
+                req(v.shape[0] == numCoefficientSets, f"The size of {name} must be equal to 1 "
+                    "for binomial regression, or the number of classes for multinomial "
+                    f"regression, but found: {v.shape[0]}.")
+        if self.lowerBoundsOnCoefficients is not None and \
+                self.upperBoundsOnCoefficients is not None:
+            req(bool(np.all(self.lowerBoundsOnCoefficients <= self.upperBoundsOnCoefficients)),
+                "LowerBoundsOnCoefficients should always be less than or equal to "
+                "upperBoundsOnCoefficients")
+        if self.lowerBoundsOnIntercepts is not None and self.upperBoundsOnIntercepts is not None:
+            req(bool(np.all(self.lowerBoundsOnIntercepts <= self.upperBoundsOnIntercepts)),
+                "LowerBoundsOnIntercepts should always be less than or equal to "
+                "upperBoundsOnIntercepts")
+
+    def _create_bounds(self, numCoefficientSets, numFeatures, featuresStd):
+        """createBounds (:732-775): column-major (index i -> class i % nCS,
+        feature i / nCS), coefficient bounds scaled by featuresStd."""
+        if not self.usingBoundConstrainedOptimization:
+            return None, None
+        nFPI = numFeatures + 1 if self.fitIntercept else numFeatures
+        n = nFPI * numCoefficientSets
+        lo = np.full(n, -np.inf)
+        hi = np.full(n, np.inf)
+        for i in range(n):
+            cs, fi = i % numCoefficientSets, i // numCoefficientSets
+            if fi < numFeatures:
+                if self.lowerBoundsOnCoefficients is not None:
+                    lo[i] = self.lowerBoundsOnCoefficients[cs, fi] * featuresStd[fi]
+                if self.upperBoundsOnCoefficients is not None:
+                    hi[i] = self.upperBoundsOnCoefficients[cs, fi] * featuresStd[fi]
+            else:
+                if self.lowerBoundsOnIntercepts is not None:
+                    lo[i] = self.lowerBoundsOnIntercepts[cs]
+                if self.upperBoundsOnIntercepts is not None:
+                    hi[i] = self.upperBoundsOnIntercepts[cs]
+        return lo, hi
 
     def _validate(self):
         if not self.regParam >= 0:
@@ -207,7 +290,7 @@ class LogisticRegression:
         numCoefficientSets = numClasses if isMultinomial else 1
 
         isConstantLabel = int(np.count_nonzero(histogram)) == 1
-        if fitIntercept and isConstantLabel:
+        if fitIntercept and isConstantLabel and not self.usingBoundConstrainedOptimization:
             # :564-577 -- all labels the same: zero coefficients, infinite intercept
             idx = int(np.argmax(histogram))
             coef = np.zeros((numCoefficientSets, numFeatures))
@@ -218,6 +301,8 @@ class LogisticRegression:
                 icpt = np.array([math.inf if numClasses == 2 else -math.inf])
             return LogisticRegressionModel(coef, icpt, numClasses, isMultinomial, [0.0])
 
+        self._check_bounds(numCoefficientSets, numFeatures)
+        bounded = self.usingBoundConstrainedOptimization
         regParamL2 = (1.0 - self.elasticNetParam) * self.regParam
         regularization = None
         if regParamL2 != 0.0:
@@ -226,9 +311,13 @@ class LogisticRegression:
                 np.repeat(featuresStd, numCoefficientSets)     # j -> featuresStd(j / nCS)
             regularization = _L2(regParamL2, nreg, stdOf)
 
-        optimizer = self._create_optimizer(numCoefficientSets, numFeatures, featuresStd)
+        lower, upper = self._create_bounds(numCoefficientSets, numFeatures, featuresStd)
+        optimizer = self._create_optimizer(numCoefficientSets, numFeatures, featuresStd,
+                                           lower, upper)
         init = self._initial_solution(numClasses, numFeatures, histogram, featuresStd,
                                       isMultinomial)
+        if bounded:      # :912-930, every initial value inside its bounds
+            init = np.minimum(np.maximum(init, lower), upper)
         solution, history = self._train_impl(numFeatures, featuresMean, featuresStd, numClasses,
                                              isMultinomial, init, regularization, optimizer,
                                              make_cost)
@@ -241,17 +330,20 @@ class LogisticRegression:
         nz = featuresStd != 0.0
         coefM[:, nz] = all_[:, :numFeatures][:, nz] / featuresStd[nz]
         icpt = all_[:, numFeatures].copy() if fitIntercept else np.zeros(numCoefficientSets)
-        if self.regParam == 0.0 and isMultinomial:
+        if self.regParam == 0.0 and isMultinomial and not bounded:
             # :656-674 -- mean-centred coefficients (identifiability, as glmnet)
             coefM = coefM - coefM.sum(axis=0) / numCoefficientSets
-        if fitIntercept and isMultinomial:
+        if fitIntercept and isMultinomial and not bounded:
             icpt = icpt - icpt.sum() / len(icpt)
         return LogisticRegressionModel(coefM, icpt, numClasses, isMultinomial, history)
 
-    def _create_optimizer(self, numCoefficientSets, numFeatures, featuresStd):
+    def _create_optimizer(self, numCoefficientSets, numFeatures, featuresStd, lower=None,
+                          upper=None):
         """createOptimizer (:777-816)."""
         regParamL1 = self.elasticNetParam * self.regParam
         if self.elasticNetParam == 0.0 or self.regParam == 0.0:
+            if lower is not None and upper is not None:
+                return optimize.LBFGSB(lower, upper, self.maxIter, 10, self.tol)
             return optimize.LBFGS(self.maxIter, 10, self.tol)
         n = (numFeatures + (1 if self.fitIntercept else 0)) * numCoefficientSets
         w = np.zeros(n)
@@ -288,7 +380,12 @@ class LogisticRegression:
     def _train_impl(self, numFeatures, featuresMean, featuresStd, numClasses, multinomial,
                     init, regularization, optimizer, make_cost):
         """trainImpl (:935-1035)."""
-        fitWithMean = self.fitIntercept       # no bounds on the intercepts here
+        # :950-954: centre only without (finite) bounds on the intercepts
+        fitWithMean = self.fitIntercept and \
+            (self.lowerBoundsOnIntercepts is None or
+             bool(np.all(np.isneginf(self.lowerBoundsOnIntercepts)))) and \
+            (self.upperBoundsOnIntercepts is None or
+             bool(np.all(np.isposinf(self.upperBoundsOnIntercepts))))
         inverseStd = np.where(featuresStd != 0, 1.0 / np.where(featuresStd != 0, featuresStd, 1),
                               0.0)
         scaledMean = inverseStd * featuresMean

@@ -354,3 +354,175 @@ class OWLQN(LBFGS):
         it = state.iter
         init = 0.5 / np.linalg.norm(state.grad) if it < 1 else 1.0
         return backtracking(phi, init, shrinkStep=0.1 if it < 1 else 0.5)
+
+
+class LBFGSB:
+    """breeze LBFGSB(lowerBounds, upperBounds, maxIter, m, tolerance) as
+    LogisticRegression.createOptimizer builds it for bound-constrained fits
+    (LogisticRegression.scala:786-789): the L-BFGS-B method of Byrd, Lu,
+    Nocedal and Zhu (1995), restated -- compact limited-memory matrices
+    W = [Y, theta S] and M; the generalized Cauchy point along the projected
+    steepest-descent path (breakpoints in order); direct primal minimization
+    of the quadratic model over the free variables, its point projected into
+    the box; a backtracking Armijo search along the feasible segment
+    (step <= 1 keeps every iterate in the box).  Convergence: maxIter, the
+    relative function change of the default check (FunctionValuesConverged
+    with tolerance), or the projected gradient's inf-norm <= max(tol |f|,
+    1e-8)."""
+
+    fvalMemory = 20
+
+    def __init__(self, lower, upper, maxIter=100, m=10, tolerance=1e-6):
+        self.l = np.asarray(lower, dtype=np.float64)
+        self.u = np.asarray(upper, dtype=np.float64)
+        if np.any(self.l > self.u):
+            raise ValueError("requirement failed: lower bounds must not exceed upper bounds")
+        self.maxIter, self.m, self.tolerance = int(maxIter), int(m), float(tolerance)
+
+    def _proj(self, x):
+        return np.minimum(np.maximum(x, self.l), self.u)
+
+    def _pg_norm(self, x, g):
+        return float(np.max(np.abs(self._proj(x - g) - x), initial=0.0))
+
+    def _cauchy(self, x, g, W, M, theta):
+        l, u = self.l, self.u
+        n = x.size
+        t = np.full(n, np.inf)
+        neg, pos = g < 0, g > 0
+        t[neg] = (x[neg] - u[neg]) / g[neg]
+        t[pos] = (x[pos] - l[pos]) / g[pos]
+        d = np.where(t > 0, -g, 0.0)
+        xc = x.copy()
+        p = W.T @ d if W.shape[1] else np.zeros(0)
+        c = np.zeros_like(p)
+        fp = -float(d @ d)
+        fpp = -theta * fp - (float(p @ (M @ p)) if p.size else 0.0)
+        fpp = max(fpp, 1e-300)
+        dtmin = -fp / fpp
+        told = 0.0
+        order = np.argsort(t)
+        order = order[(t[order] > 0) & np.isfinite(t[order])]
+        for b in order:
+            dt = t[b] - told
+            if dtmin < dt:
+                break
+            xc[b] = u[b] if d[b] > 0 else l[b]
+            zb = xc[b] - x[b]
+            c = c + dt * p
+            gb = g[b]
+            wb = W[b]
+            Mc = M @ c if c.size else c
+            Mp = M @ p if p.size else p
+            fp = fp + dt * fpp + gb * gb + theta * gb * zb - (gb * float(wb @ Mc) if c.size else 0.0)
+            fpp = fpp - theta * gb * gb - (2.0 * gb * float(wb @ Mp) + gb * gb * float(wb @ (M @ wb))
+                                           if p.size else 0.0)
+            fpp = max(fpp, 1e-300)
+            p = p + gb * wb
+            d[b] = 0.0
+            dtmin = -fp / fpp
+            told = t[b]
+        dtmin = max(dtmin, 0.0)
+        told += dtmin
+        free = d != 0
+        xc[free] = x[free] + told * d[free]
+        c = c + dtmin * p
+        return self._proj(xc), c
+
+    def _subspace(self, x, g, xc, c, W, M, theta):
+        free = (xc > self.l) & (xc < self.u)
+        if not np.any(free):
+            return xc
+        if W.shape[1] == 0:
+            r = g + theta * (xc - x)
+            xb = xc.copy()
+            xb[free] = xc[free] - r[free] / theta
+            return self._proj(xb)
+        r = g + theta * (xc - x) - W @ (M @ c)
+        rF = r[free]
+        WF = W[free]
+        v = M @ (WF.T @ rF)
+        Nm = np.eye(M.shape[0]) - (M @ (WF.T @ WF)) / theta
+        try:
+            v = np.linalg.solve(Nm, v)
+        except np.linalg.LinAlgError:
+            v = np.linalg.lstsq(Nm, v, rcond=None)[0]
+        du = -rF / theta - (WF @ v) / (theta * theta)
+        xb = xc.copy()
+        xb[free] = xc[free] + du
+        return self._proj(xb)
+
+    def iterations(self, fn, init):
+        f = fn if isinstance(fn, CachedDiffFunction) else CachedDiffFunction(fn)
+        x = self._proj(np.array(init, dtype=np.float64, copy=True))
+        v, g = f.calculate(x)
+        S, Y = [], []
+        theta = 1.0
+        fvals = [math.inf]
+        it = 0
+        v0 = v
+        while True:
+            reason = None
+            if self.maxIter >= 0 and it >= self.maxIter:
+                reason = "max iterations reached"
+            elif len(fvals) >= 2 and abs(v - max(fvals)) <= self.tolerance * abs(v0):
+                reason = "function values converged"
+            elif self._pg_norm(x, g) <= max(self.tolerance * abs(v), 1e-8):
+                reason = "projected gradient converged"
+            st = State(x, v, g, v, g, it, v0, None, list(fvals), convergenceReason=reason)
+            yield st
+            if reason is not None:
+                return
+            if S:
+                Sm, Ym = np.stack(S, 1), np.stack(Y, 1)
+                W = np.concatenate([Ym, theta * Sm], axis=1)
+                SY = Sm.T @ Ym
+                D = np.diag(np.diag(SY))
+                L = np.tril(SY, -1)
+                K = np.block([[-D, L.T], [L, theta * (Sm.T @ Sm)]])
+                M = np.linalg.inv(K)
+            else:
+                W = np.zeros((x.size, 0))
+                M = np.zeros((0, 0))
+            xc, c = self._cauchy(x, g, W, M, theta)
+            xb = self._subspace(x, g, xc, c, W, M, theta)
+            d = xb - x
+            dg = float(d @ g)
+            if not dg < 0:           # not a descent direction: restart from steepest descent
+                S, Y, theta = [], [], 1.0
+                d = self._proj(x - g) - x
+                dg = float(d @ g)
+                if not dg < 0:
+                    st.convergenceReason = "no descent direction"
+                    yield st
+                    return
+            alpha = 1.0
+            for _ in range(30):
+                xn = self._proj(x + alpha * d)
+                vn, gn = f.calculate(xn)
+                if vn <= v + 1e-4 * alpha * dg:
+                    break
+                alpha *= 0.5
+            else:
+                st.searchFailed = True
+                st.convergenceReason = "line search failed"
+                yield st
+                return
+            s, y = xn - x, gn - g
+            sy = float(s @ y)
+            if sy > 2.2e-16 * float(y @ y):
+                S.append(s)
+                Y.append(y)
+                if len(S) > self.m:
+                    S.pop(0)
+                    Y.pop(0)
+                theta = float(y @ y) / sy
+            x, v, g = xn, vn, gn
+            fvals = (fvals + [v])[-self.fvalMemory:]
+            it += 1
+
+    def minimize(self, fn, init):
+        s = None
+        for s in self.iterations(fn, init):
+            pass
+        return s.x

@@ -55,17 +55,31 @@ def spark_close(actual, expected, tol):
 
 def estimator(case):
     p = dict(case["params"])
-    return LogisticRegression(regParam=p.get("regParam", 0.0),
-                              elasticNetParam=p.get("elasticNetParam", 0.0),
-                              maxIter=p.get("maxIter", 100), tol=p.get("tol", 1e-6),
-                              fitIntercept=p["fitIntercept"],
-                              standardization=p["standardization"])
+    lr = LogisticRegression(regParam=p.get("regParam", 0.0),
+                            elasticNetParam=p.get("elasticNetParam", 0.0),
+                            maxIter=p.get("maxIter", 100), tol=p.get("tol", 1e-6),
+                            fitIntercept=p["fitIntercept"],
+                            standardization=p["standardization"])
+    for k in ("lowerBoundsOnCoefficients", "upperBoundsOnCoefficients",
+              "lowerBoundsOnIntercepts", "upperBoundsOnIntercepts"):
+        if k in p:
+            getattr(lr, "set" + k[0].upper() + k[1:])(p[k])
+    return lr
 
 
 def check_model(case, model):
     nC = len(case["intercept"])
-    coef = model.coefficientMatrix.reshape(-1) if nC > 1 else model.coefficients
-    spark_close(coef, case["coef"], case["coef_tol"])
+    if case.get("coef_check") == "bounded_mlor_equivalent":
+        # checkBoundedMLORCoefficientsEquivalent (LogisticRegressionSuite.scala:3138-3144):
+        # per feature, the class-wise differences to the expected column are equal
+        # (absTol 1e-2) -- unregularized MLOR is identifiable only up to a shift
+        diff = model.coefficientMatrix - np.asarray(case["coef"]).reshape(nC, -1)
+        for j in range(diff.shape[1]):
+            for a, b in zip(diff[:-1, j], diff[1:, j]):
+                assert abs(a - b) < 1e-2, (j, diff[:, j])
+    else:
+        coef = model.coefficientMatrix.reshape(-1) if nC > 1 else model.coefficients
+        spark_close(coef, case["coef"], case["coef_tol"])
     icpt = model.interceptVector if nC > 1 else [model.intercept]
     spark_close(icpt, case["intercept"], case["intercept_tol"])
     if case.get("centered"):
@@ -183,3 +197,36 @@ def test_fit_device_csr_matches_dense(cuda):
     blk.prepare(layout="tiles")
     case = CASES["binary_intercept_l2_std"]
     check_model(case, estimator(case).fit(blk))
+
+
+def test_lbfgsb_box_quadratic_kkt():
+    rng = np.random.default_rng(0)
+    n = 8
+    Q = rng.normal(size=(n, n))
+    A = Q @ Q.T + n * np.eye(n)
+    b = rng.normal(size=n) * 5
+    lo, hi = np.full(n, -0.3), np.full(n, 0.4)
+    x = optimize.LBFGSB(lo, hi, 500, 10, 1e-12).minimize(
+        lambda z: (0.5 * z @ A @ z - b @ z, A @ z - b), np.zeros(n))
+    g = A @ x - b
+    assert np.abs(np.clip(x - g, lo, hi) - x).max() < 1e-8       # projected gradient = 0
+    assert np.all(x >= lo) and np.all(x <= hi) and np.any(x == hi) and np.any(x == lo)
+
+
+def test_bound_params_checks():
+    from cycloneml_amd import _native as N
+    hist, mean, std = [3.0, 4.0], np.zeros(4), np.ones(4)
+    lr = LogisticRegression(elasticNetParam=0.5, regParam=0.1) \
+        .setUpperBoundsOnCoefficients([[1.0, 0.0, 1.0, 0.0]])
+    with pytest.raises(N.IllegalArgumentException, match="only supports L2 regularization"):
+        lr.train_from_summary(4, hist, mean, std, None)
+    lr = LogisticRegression(fitIntercept=False).setUpperBoundsOnIntercepts([1.0])
+    with pytest.raises(N.IllegalArgumentException, match="bounds on intercepts"):
+        lr.train_from_summary(4, hist, mean, std, None)
+    lr = LogisticRegression().setUpperBoundsOnCoefficients([[1.0, 0.0, 1.0]])
+    with pytest.raises(N.IllegalArgumentException, match="shape of upperBoundsOnCoefficients"):
+        lr.train_from_summary(4, hist, mean, std, None)
+    lr = LogisticRegression().setUpperBoundsOnCoefficients([[0.0] * 4]) \
+        .setLowerBoundsOnCoefficients([[1.0] * 4])
+    with pytest.raises(N.IllegalArgumentException, match="less than or equal"):
+        lr.train_from_summary(4, hist, mean, std, None)
