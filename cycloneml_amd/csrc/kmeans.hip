@@ -1714,7 +1714,7 @@ struct cyc_kmeans_plan_s {
   cyc::DeviceBuffer cb3, cq3, ok3, list3, list3Count;
   // i8 exact-integer screen (kmeans_i8.hip), used with a row image
   int ktp8 = 0;
-  cyc::DeviceBuffer cb8, cq8, g8, prm8, scr8;
+  cyc::DeviceBuffer cb8, cq8, g8, prm8, scr8, list8Count;   // list8 = slowList (idle then)
   int64_t max_rows = 0;
   size_t assignLds = 0;
   std::mutex mu;
@@ -1863,7 +1863,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
                                p->cb8.ptr, (const float*)p->cq8.ptr, (const double*)p->g8.ptr,
                                cnorm, (const cyc::km8::CenterParams*)p->prm8.ptr, p->ktp8,
                                assign, (int32_t*)p->list3.ptr, (unsigned int*)p->list3Count.ptr,
-                               st)))
+                               (int32_t*)p->slowList.ptr, (unsigned int*)p->list8Count.ptr, st)))
       return rc;
     rowList = (const int32_t*)p->list3.ptr;
     rowCount = (const unsigned int*)p->list3Count.ptr;
@@ -2047,8 +2047,9 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
     const int ks8 = cyc::km8::ksteps(d);
     p->ktp8 = (int)cyc::round_up((k + 15) / 16, cyc::km8::kWaves);
     if ((rc = p->cb8.reserve((size_t)p->ktp8 * ks8 * 3 * 64 * 16)) ||
-        (rc = p->cq8.reserve(sizeof(float) * (size_t)p->ktp8 * 16)) ||
-        (rc = p->g8.reserve(sizeof(double) * (size_t)p->ktp8 * 16)) ||
+        (rc = p->cq8.reserve(sizeof(float) * (size_t)p->ktp8 * 32)) ||
+        (rc = p->g8.reserve(sizeof(double) * (size_t)p->ktp8 * 32)) ||
+        (rc = p->list8Count.reserve(64)) ||
         (rc = p->prm8.reserve(sizeof(cyc::km8::CenterParams))) ||
         (rc = p->scr8.reserve(sizeof(double) * 2 * (size_t)k))) {
       delete p;

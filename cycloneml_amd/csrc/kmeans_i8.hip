@@ -223,6 +223,7 @@ __global__ __launch_bounds__(256) void k_centers_params(int k, const double* __r
     const double Ac = __builtin_ldexp(1.0, ec - 22);
     const double mu = sn[0] / Ac;
     p.mu = (mu > 0.0 && __builtin_isfinite(mu)) ? mu : 1.0;
+    p.k = k;
     *prm = p;
   }
 }
@@ -525,10 +526,13 @@ __global__ __launch_bounds__(256, KS <= 4 ? 3 : 2) void k_screen(
 // 32 ct + (l & 31), dims 32 s + 16 (l >> 5) + 0..15, limb planes a', b', c':
 // Cb[((ct S + s) 3 + limb) 64 + l]; the tile count is even (padding centers
 // are zero with cq = +inf).
+
+__device__ __forceinline__ double err_term2(int e, double n1, double mu, int d);
 __global__ __launch_bounds__(256) void k_centers_pack32(
     const double* __restrict__ C, const double* __restrict__ cnorm, int k, int d, int S, int ktp,
     const double* __restrict__ cn1, const CenterParams* __restrict__ prm, uint4* __restrict__ Cb,
-    float* __restrict__ cq, double* __restrict__ g) {
+    float* __restrict__ cq, double* __restrict__ g, float* __restrict__ cq2,
+    double* __restrict__ g2) {
   const CenterParams p = *prm;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)ktp * S * 64;
@@ -557,27 +561,51 @@ __global__ __launch_bounds__(256) void k_centers_pack32(
     const int c = (int)idx;
     if (c < k && p.ok) {
       const double gc = err_term(p.ec, cn1[c], p.mu, d);
+      const double gc2 = err_term2(p.ec, cn1[c], p.mu * 0x1p-7, d);
       const double cn = cnorm[c];
       g[c] = gc;
       cq[c] = fdown((cn * cn) * (1.0 - kEpsF) - 2.0 * gc);
+      g2[c] = gc2;
+      cq2[c] = fdown((cn * cn) * (1.0 - kEpsF) - 2.0 * gc2);
     } else {
-      g[c] = 0.0;
+      g[c] = g2[c] = 0.0;
       cq[c] = __builtin_inff();
+      cq2[c] = 0x1.fffffep127f;   // finite: the two-limb pass keeps index bits in L
     }
   }
 }
 
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-template <int S, int W>   // 32-dim substeps (D = 32 S <= 256); W waves per workgroup
+// fx / gc of the TWO-limb screen: |x_j - xh2_j| <= 2^(e-15) (u - a - b/128
+// = (t - b)/128 with |t - b| <= 1/2), the dropped b.b' / 2^14 term <=
+// d 2^(ex+ec-16) = d 2^14 A2x A2c <= 0.5 d 2^14 (A2x^2 + A2c^2) (AM-GM);
+// A2 carries a 2^-7 slack.  n1 must bound |xh2|_1 (rows) or |c|_1 (centers).
+__device__ __forceinline__ double err_term2(int e, double n1, double mu, int d) {
+  const double A = __builtin_ldexp(1.0078125, e - 15);
+  const double kd = 0.502 * (double)d * 0x1p14;
+  return (0.5 * mu * A * A + 0.5 * n1 * n1 / mu + kd * A * A) * (1.0 + 0x1p-40);
+}
+
+// One screen pass over 32-row groups.  LIMBS = 3: the exact-integer screen
+// (S1, S2, S3: six MFMAs per 32-dim substep).  LIMBS = 2: the same over the
+// a and b limbs only (S1, S2: three MFMAs), certified with err_term2 --
+// config 2's rows certify 90 % of the time at this precision vs 99.9 % at
+// three limbs, so the two-limb pass runs over every row and the three-limb
+// pass only over its leftovers (LIST: rows taken from `rowsIn`, a device
+// list of *rowsInCount row indices).  Both read the
+// same center image (3 limb fragments per substep; LIMBS = 2 DMAs the first
+// two) and write assign[] for certified rows, the rest to list.
+template <int S, int W, int LIMBS, bool LIST>
 __global__ __launch_bounds__(64 * W, 2) void k_screen32(
     const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
     int64_t n, int d, const uint4* __restrict__ Cb, const float* __restrict__ cq,
     const double* __restrict__ g, const double* __restrict__ cnorm,
-    const CenterParams* __restrict__ prm, int ktp, int32_t* __restrict__ assign,
+    const CenterParams* __restrict__ prm, int ktp, const int32_t* __restrict__ rowsIn,
+    const unsigned int* __restrict__ rowsInCount, int32_t* __restrict__ assign,
     int32_t* __restrict__ list, unsigned int* __restrict__ listCount) {
   constexpr int D = 32 * S, CH = 3 * D / 16;      // 16-byte chunks per image row
-  constexpr int FR = 3 * S;                        // 1 KiB B fragments per center tile
+  constexpr int FR = LIMBS * S;                    // 1 KiB B fragments per center tile
   constexpr int TB = FR * 1024 + 256;              // tile slot: fragments, then 64 cq floats
   constexpr int G = FR / W + 1;                    // LDS-DMA instructions per wave per tile
   static_assert(FR % W == 0, "fragments split evenly over the waves");
@@ -586,26 +614,35 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
   __shared__ __attribute__((aligned(16))) char lds[3 * TB];
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t row0 = ((int64_t)blockIdx.x * W + wave) * 32;
-  // waves past the end still take part in every barrier (zero rows)
-  const int rows = (int)max<int64_t>(0, min<int64_t>(32, n - row0));
   const CenterParams P = *prm;
+  const double mu = LIMBS == 3 ? P.mu : P.mu * 0x1p-7;   // any mu > 0 is valid
+  const int64_t total = LIST ? (int64_t)*rowsInCount : n;
+  // one group of 32 W rows (positions)
+  auto group = [&](int64_t grp) {
+  const int64_t pos0 = (grp * W + wave) * 32;        // first position of this wave
+  // waves past the end still take part in every barrier (zero rows)
+  const int rows = (int)max<int64_t>(0, min<int64_t>(32, total - pos0));
+  auto rowAt = [&](int i) -> int64_t {   // global row of position pos0 + i (i < rows)
+    if constexpr (LIST) return rowsIn[pos0 + i];
+    else return pos0 + i;
+  };
   if (!P.ok) {   // uniform over the grid
-    if (lane < rows) list[atomicAdd(listCount, 1u)] = (int32_t)(row0 + lane);
+    if (lane < rows) list[atomicAdd(listCount, 1u)] = (int32_t)rowAt(lane);
     return;
   }
-  // tile t -> slot t % 3: each wave DMAs fragments wave, wave + 4, ... and the
-  // tile's cq (all four waves write the same 256 bytes); past the last tile
-  // the last one is re-read into the free slot, so every wave always has
-  // exactly G DMAs per tile in flight and one counted wait fits all tiles.
+  // tile t -> slot t % 3: each wave DMAs fragments wave, wave + W, ... and the
+  // tile's cq (all waves write the same 256 bytes); past the last tile the
+  // last one is re-read into the free slot, so every wave always has exactly
+  // G DMAs per tile in flight and one counted wait fits all tiles.
   auto issue = [&](int t) {
     const int tt = t < ktp ? t : ktp - 1;
-    const char* src = (const char*)Cb + (size_t)tt * FR * 1024 + lane * 16;
+    const char* src = (const char*)Cb + (size_t)tt * (3 * S) * 1024 + lane * 16;
     char* dst = lds + (t % 3) * TB;
 #pragma unroll
     for (int j = 0; j < FR / W; ++j) {
-      const int f = wave + W * j;
-      __builtin_amdgcn_global_load_lds((const void*)(src + f * 1024),
+      const int f = wave + W * j;                     // fragment (substep f / LIMBS, limb f % LIMBS)
+      const int piece = (f / LIMBS) * 3 + f % LIMBS;  // its 1 KiB piece in the 3-limb image
+      __builtin_amdgcn_global_load_lds((const void*)(src + piece * 1024),
                                        (__attribute__((address_space(3))) void*)(dst + f * 1024),
                                        16, 0, 0);
     }
@@ -616,27 +653,28 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
   issue(0);
   issue(1);
   // A fragments of the wave's 32 rows, all substeps and limbs
-  v4i A[S][3];
+  v4i A[S][LIMBS];
+  const bool rowOk = r < rows;
+  const int64_t myRow = rowOk ? rowAt(r) : 0;   // lane's row (row 0 exists: n > 0)
   {
-    // loads from a clamped row (always in range), zeroed after the load
-    const bool ok = r < rows;
-    const uint4* src = Xq + min<int64_t>(row0 + r, n - 1) * CH + h;
+    // loads from a valid row, zeroed after the load
+    const bool ok = rowOk;
+    const uint4* src = Xq + myRow * CH + h;
 #pragma unroll
     for (int s = 0; s < S; ++s)
 #pragma unroll
-      for (int L = 0; L < 3; ++L) {
+      for (int L = 0; L < LIMBS; ++L) {
         const v4u t = __builtin_nontemporal_load((const v4u*)(src + L * (D / 16) + 2 * s));
         A[s][L] = ok ? __builtin_bit_cast(v4i, t) : v4i{0, 0, 0, 0};
       }
   }
   // row of accumulator register reg: (reg & 3) + 8 (reg >> 2) + 4 h
   float F1[16];
+  {
+    const int ex = rowOk ? meta[myRow].x : INT_MIN;
+    const float f = ex == INT_MIN ? 0.0f : __builtin_ldexpf(1.0f, ex + P.ec - 20);
 #pragma unroll
-  for (int reg = 0; reg < 16; ++reg) {
-    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-    const int ex0 = meta[min<int64_t>(row0 + row, n - 1)].x;
-    const int ex = row < rows ? ex0 : INT_MIN;
-    F1[reg] = ex == INT_MIN ? 0.0f : __builtin_ldexpf(1.0f, ex + P.ec - 20);
+    for (int reg = 0; reg < 16; ++reg) F1[reg] = __shfl(f, (reg & 3) + 8 * (reg >> 2) + 4 * h);
   }
   float sL1[16], sL2[16];
   int sI1[16];
@@ -645,36 +683,58 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
     sL1[q] = sL2[q] = __builtin_inff();
     sI1[q] = -1;
   }
-  // tile ct from its slot: 6 limb products per substep, B fragments by
-  // conflict-free ds_read_b128 (lane-linear 1 KiB fragments)
-  auto tile = [&](int ct, v16i (&acc)[3]) {
+  // tile ct from its slot: LIMBS = 3: six limb products per substep,
+  // LIMBS = 2: three; B fragments by conflict-free ds_read_b128
+  auto tile = [&](int ct, v16i (&acc)[LIMBS]) {
     const v4i* B = (const v4i*)(lds + (ct % 3) * TB) + lane;
 #pragma unroll
-    for (int L = 0; L < 3; ++L) acc[L] = v16i{};
+    for (int L = 0; L < LIMBS; ++L) acc[L] = v16i{};
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const v4i B0 = B[(3 * s + 0) * 64], B1 = B[(3 * s + 1) * 64], B2 = B[(3 * s + 2) * 64];
+      const v4i B0 = B[(LIMBS * s + 0) * 64], B1 = B[(LIMBS * s + 1) * 64];
       acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B0, acc[0], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B1, acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B2, acc[2], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B0, acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B1, acc[2], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][2], B0, acc[2], 0, 0, 0);
+      if constexpr (LIMBS == 3) {
+        const v4i B2 = B[(LIMBS * s + 2) * 64];
+        acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B2, acc[2], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B1, acc[2], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][2], B0, acc[2], 0, 0, 0);
+      }
     }
   };
-  // the two smallest lower bounds per row and the index of the smallest;
-  // cqv is read from the tile's slot before that slot can be refilled
-  auto epi = [&](int ct, float cqv, const v16i (&acc)[3]) {
+  // the two smallest lower bounds per row and the index of the smallest.
+  // LIMBS = 2 keeps the tile index in the low IB mantissa bits of L (moving
+  // L by < 2^IB ulp either way, charged in the certification): a min and a
+  // med3 per (row, center) instead of a compare, a med3 and two selects.
+  const int IB = 32 - __builtin_clz((unsigned)max(ktp - 1, 1));
+  const unsigned IM = (1u << IB) - 1u;
+  auto epi = [&](int ct, float cqv, const v16i (&acc)[LIMBS]) {
     const int c = ct * 32 + r;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       const int T = acc[0][reg] * 128 + acc[1][reg];
-      const float V = __builtin_fmaf((float)acc[2][reg], 0x1p-7f, (float)T);
-      const float L = __builtin_fmaf(-F1[reg], V, cqv);
-      const bool lt = L < sL1[reg];
-      sL2[reg] = __builtin_amdgcn_fmed3f(sL1[reg], sL2[reg], L);
-      sI1[reg] = lt ? c : sI1[reg];
-      sL1[reg] = lt ? L : sL1[reg];   // L is never NaN: a select, no canonicalize
+      if constexpr (LIMBS == 3) {
+        const float V = __builtin_fmaf((float)acc[2][reg], 0x1p-7f, (float)T);
+        const float L = __builtin_fmaf(-F1[reg], V, cqv);
+        const bool lt = L < sL1[reg];
+        sL2[reg] = __builtin_amdgcn_fmed3f(sL1[reg], sL2[reg], L);
+        sI1[reg] = lt ? c : sI1[reg];
+        sL1[reg] = lt ? L : sL1[reg];   // L is never NaN: a select, no canonicalize
+      } else {
+        // cq2 is finite (padding: FLT_MAX) and round-down keeps L finite
+        const float L0 = __builtin_fmaf(-F1[reg], (float)T, cqv);
+        // raw v_bfi / v_med3 / v_min: L comes out of integer ops, and
+        // hipcc would quiet it (two v_max per element) before any IEEE
+        // min or med3 -- L is never NaN
+        float L;
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(L) : "s"(IM), "v"(ct), "v"(L0));
+        float m2, m1;
+        asm("v_med3_f32 %0, %1, %2, %3" : "=v"(m2) : "v"(sL1[reg]), "v"(sL2[reg]), "v"(L));
+        asm("v_min_f32 %0, %1, %2" : "=v"(m1) : "v"(sL1[reg]), "v"(L));
+        sL2[reg] = m2;
+        sL1[reg] = m1;
+      }
     }
   };
   auto cq_of = [&](int ct) { return *(const float*)(lds + (ct % 3) * TB + FR * 1024 + r * 4); };
@@ -689,58 +749,103 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
 
   // MODE.FP_ROUND single precision = toward -inf (the L' are lower bounds)
   __builtin_amdgcn_s_setreg(0x801, 2);
-  for (int ct = 0; ct < ktp; ++ct) {
-    v16i X[3];
-    arrive(ct);
-    const float cqv = cq_of(ct);
-    tile(ct, X);
-    epi(ct, cqv, X);
+  if constexpr (LIMBS == 2) {
+    // software-pipelined: tile ct's MFMAs beside tile ct - 1's epilogue (two
+    // accumulator sets; the slot of ct - 1 is refilled only by the DMAs that
+    // arrive(ct + 1) issues, and its cq is already in a register)
+    v16i Xp[LIMBS];
+    arrive(0);
+    float cqp = cq_of(0);
+    tile(0, Xp);
+    for (int ct = 1; ct < ktp; ++ct) {
+      v16i X[LIMBS];
+      arrive(ct);
+      const float cqv = cq_of(ct);
+      tile(ct, X);
+      epi(ct - 1, cqp, Xp);
+#pragma unroll
+      for (int L = 0; L < LIMBS; ++L) Xp[L] = X[L];   // 16 v_mov_b64 (unrolling by two spills)
+      cqp = cqv;
+    }
+    epi(ktp - 1, cqp, Xp);
+  } else {
+    for (int ct = 0; ct < ktp; ++ct) {
+      v16i X[LIMBS];
+      arrive(ct);
+      const float cqv = cq_of(ct);
+      tile(ct, X);
+      epi(ct, cqv, X);
+    }
   }
   __builtin_amdgcn_s_setreg(0x801, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing re-read DMAs
 
-  // each row's slots over the 32 lanes (centers) of its half
+  if constexpr (LIMBS == 2) {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
+    for (int q = 0; q < 16; ++q) sI1[q] = (int)(__float_as_uint(sL1[q]) & IM) * 32 + r;
+  }
+  // each row's (L1, L2, I1) over the 32 lanes (centers) of its half: every
+  // xor step halves the registers a lane keeps (lanes with the step's bit
+  // keep the upper half and send the lower), so 16 rows cost 8 + 4 + 2 + 1 + 1
+  // shuffles per quantity.  Equal L1 from two centers leave L2 = L1, which
+  // never certifies, so the merge needs no index tie-break.
+  auto merge = [](float& L1, float& L2, int& I1, float oL1, float oL2, int oI1) {
+    L2 = __builtin_fminf(__builtin_fmaxf(L1, oL1), __builtin_fminf(L2, oL2));
+    I1 = oL1 < L1 ? oI1 : I1;
+    L1 = __builtin_fminf(L1, oL1);
+  };
 #pragma unroll
-    for (int m = 1; m < 32; m <<= 1) {
-      const float oL1 = __shfl_xor(sL1[q], m), oL2 = __shfl_xor(sL2[q], m);
-      const int oI1 = __shfl_xor(sI1[q], m);
-      sL2[q] = __builtin_fminf(__builtin_fmaxf(sL1[q], oL1), __builtin_fminf(sL2[q], oL2));
-      const bool take = oL1 < sL1[q] || (oL1 == sL1[q] && oI1 >= 0 && (sI1[q] < 0 || oI1 < sI1[q]));
-      sI1[q] = take ? oI1 : sI1[q];
-      sL1[q] = take ? oL1 : sL1[q];
+  for (int lev = 0; lev < 4; ++lev) {
+    const int half = 8 >> lev, m = 16 >> lev;
+    const bool hi = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const float oL1 = __shfl_xor(hi ? sL1[i] : sL1[i + half], m);
+      const float oL2 = __shfl_xor(hi ? sL2[i] : sL2[i + half], m);
+      const int oI1 = __shfl_xor(hi ? sI1[i] : sI1[i + half], m);
+      float L1 = hi ? sL1[i + half] : sL1[i], L2 = hi ? sL2[i + half] : sL2[i];
+      int I1 = hi ? sI1[i + half] : sI1[i];
+      merge(L1, L2, I1, oL1, oL2, oI1);
+      sL1[i] = L1;
+      sL2[i] = L2;
+      sI1[i] = I1;
     }
   }
+  merge(sL1[0], sL2[0], sI1[0], __shfl_xor(sL1[0], 1), __shfl_xor(sL2[0], 1),
+        __shfl_xor(sI1[0], 1));
+  // lane holds row register q = lane bits 1..4
   // per-wave reduction area in the (now idle) slots: L1, L2, I1 x 32 rows
   __syncthreads();
   float* redL1 = (float*)lds + wave * 96;
   float* redL2 = redL1 + 32;
   int* redI1 = (int*)(redL1 + 64);
-  if (r == 0) {
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-      const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
-      redL1[row] = sL1[reg];
-      redL2[row] = sL2[reg];
-      redI1[row] = sI1[reg];
-    }
+  if ((lane & 1) == 0) {
+    const int q = (lane >> 1) & 15;
+    const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
+    redL1[row] = sL1[0];
+    redL2[row] = sL2[0];
+    redI1[row] = sI1[0];
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   if (lane < rows) {
-    const int row = lane;
-    const int2 mt = meta[row0 + row];
-    const float L1 = redL1[row], L2 = redL2[row];
-    const int I1 = redI1[row];
+    const int64_t grow = rowAt(lane);
+    const int2 mt = meta[grow];
+    const float L1 = redL1[lane], L2 = redL2[lane];
+    const int I1 = redI1[lane];
     bool decided = false;
-    if (mt.x != INT_MIN && I1 >= 0 && __builtin_isfinite(L1)) {
-      const double xn = xnorm[row0 + row], cn = cnorm[I1];
+    if (mt.x != INT_MIN && I1 >= 0 && I1 < P.k && __builtin_isfinite(L1)) {
+      const double xn = xnorm[grow], cn = cnorm[I1];
       const double xx = xn * xn, cc = cn * cn;
-      const double n1 = (double)__int_as_float(mt.y);
-      const double fx = err_term(mt.x, n1, P.mu, d);
+      const double n1 = (double)__int_as_float(mt.y);   // bounds |xh3|_1
+      const double fx = LIMBS == 3 ? err_term(mt.x, n1, mu, d)
+                                   : err_term2(mt.x, n1 + (double)d * __builtin_ldexp(1.0078125, mt.x - 15),
+                                               mu, d);
       const double l1 = (double)L1;
-      const double M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) +
+      // LIMBS = 2: the index bits move each L by < 2^IB ulp <= 2^(IB-23) |L|
+      const double enc = LIMBS == 3 ? 0.0
+                                    : __builtin_ldexp(__builtin_fabs(l1) + __builtin_fabs((double)L2), IB - 23) + 0x1p-120;
+      const double M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) + 2.0 * enc +
                         0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g[I1]) +
                         0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
                                    __builtin_fmin(__builtin_fabs((double)L2), 0x1p120)) +
@@ -749,25 +854,46 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
       decided = !__builtin_isfinite(L2) || ((double)L2 - l1) > M;
     }
     if (decided) {
-      assign[row0 + row] = I1;
+      assign[grow] = I1;
     } else {
-      list[atomicAdd(listCount, 1u)] = (int32_t)(row0 + row);
+      list[atomicAdd(listCount, 1u)] = (int32_t)grow;
     }
   }
+  __syncthreads();   // the reduction area is the next group's tile ring
+  };
+  // LIST: the grid covers n rows; groups past the count leave at once (a
+  // grid-stride loop here costs the three-limb S = 8 form ~30 spilled VGPRs)
+  if ((int64_t)blockIdx.x * 32 * W < total) group(blockIdx.x);
 }
 
-template <int S, int W>
+template <int S, int W, int LIMBS, bool LIST>
 int launch_screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
                     const void* Cb, const float* cq, const double* g, const double* cnorm,
-                    const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
+                    const CenterParams* prm, int ktp, const int32_t* rowsIn,
+                    const unsigned int* rowsInCount, int32_t* assign, int32_t* list,
                     unsigned int* listCount, hipStream_t st) {
   KernelTimer timer("k_kmeans_assign", st);
   const int64_t wg = (n + 32 * W - 1) / (32 * W);   // W waves x 32 rows
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32<S, W>), dim3((unsigned)wg), dim3(64 * W), 0, st,
-                     (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb, cq, g, cnorm, prm,
-                     ktp, assign, list, listCount);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32<S, W, LIMBS, LIST>), dim3((unsigned)wg),
+                     dim3(64 * W), 0, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
+                     cq, g, cnorm, prm, ktp, rowsIn, rowsInCount, assign, list, listCount);
   CYC_LAUNCH_CHECK("k_kmeans_screen32_i8");
   return CYC_OK;
+}
+
+// Two-limb pass over every row, three-limb pass over its leftovers.
+template <int S, int W>
+int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
+             const void* Cb, const float* cq, const double* g, const double* cnorm,
+             const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
+             unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st) {
+  CYC_HIP(hipMemsetAsync(list2Count, 0, sizeof(unsigned int), st));
+  int rc = launch_screen32<S, W, 2, false>(img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 32,
+                                           g + (size_t)ktp * 32, cnorm, prm, ktp, nullptr,
+                                           nullptr, assign, list2, list2Count, st);
+  if (rc) return rc;
+  return launch_screen32<S, W, 3, true>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp, list2,
+                                        list2Count, assign, list, listCount, st);
 }
 
 template <int KS>
@@ -821,7 +947,7 @@ int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp,
     const int64_t total = std::max<int64_t>((int64_t)ktp32 * S * 64, (int64_t)ktp32 * 32);
     hipLaunchKernelGGL(k_centers_pack32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                        C, cnorm, k, d, S, ktp32, (const double*)cn1, (const CenterParams*)prm,
-                       (uint4*)Cb, cq, g);
+                       (uint4*)Cb, cq, g, cq + (size_t)ktp * 16, g + (size_t)ktp * 16);
     CYC_LAUNCH_CHECK("k_centers_pack32");
     return CYC_OK;
   }
@@ -836,13 +962,13 @@ int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp,
 int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
            const void* Cb, const float* cq, const double* g, const double* cnorm,
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
-           unsigned int* listCount, hipStream_t st) {
+           unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st) {
   if (n <= 0) return CYC_OK;
   if (uses32(d)) {
     const int k32 = ktp * 16 / 32;   // launch over the padded center range (cq = +inf)
     switch (ksteps(d)) {
-      case 2: return launch_screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, st);
-      default: return launch_screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, st);
+      case 2: return screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, st);
+      default: return screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, st);
     }
   }
   switch (ksteps(d)) {

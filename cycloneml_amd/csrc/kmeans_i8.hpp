@@ -19,6 +19,7 @@ struct CenterParams {
   int ec;      // global center exponent: every |c_j| <= 2^ec * 127.5/128
   int ok;      // 0: some center is non-finite or beyond 2^50 (screen off)
   double mu;   // AM-GM balance of the separable error bound
+  int k;       // centers (the padded tiles hold no center)
 };
 
 // 64-dim k-steps of the i8 MFMA, rounded up to even (the kernel's register
@@ -43,15 +44,18 @@ int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipS
 // Centers -> packed B fragments (Cb), per-center lower-bound constants cq
 // (float, +inf for padding), error terms g (fp64) and the launch's params.
 // scratch: >= 2k doubles + 1 int.  ktp: 16-center tiles, a multiple of kWaves.
+// cq and g hold 2 ktp 16 entries: the 32x32 screen's two-limb pass keeps its
+// constants in the second half.
 int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp, void* Cb,
                     float* cq, double* g, CenterParams* prm, double* scratch, hipStream_t st);
 
 // Screen every row: certified rows get assign[row]; the others are appended
-// to list (listCount is NOT cleared here).
+// to list (listCount is NOT cleared here).  list2 / list2Count (n entries +
+// one counter): scratch for the rows the 32x32 two-limb pass leaves.
 int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
            const void* Cb, const float* cq, const double* g, const double* cnorm,
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
-           unsigned int* listCount, hipStream_t st);
+           unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st);
 
 }  // namespace km8
 }  // namespace cyc

@@ -5,3 +5,6 @@ timeout -k 10 500 python -u -m pytest tests/test_kmeans_gpu.py tests/test_kmeans
 tail -2 gpurun_out/pytest_km.log
 timeout -k 10 300 python -u bench.py --workload kmeans --cpu-seconds 0 > gpurun_out/bench_kmeans.json 2> gpurun_out/bench_kmeans.err || { echo BENCH FAIL; tail -20 gpurun_out/bench_kmeans.err; exit 1; }
 cat gpurun_out/bench_kmeans.json
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/km_prof -o km -- python3 -u bench.py --workload kmeans --cpu-seconds 0 --steps 5 --warmup 2 > gpurun_out/km_prof.log 2>&1 || { echo PROF FAIL; tail -20 gpurun_out/km_prof.log; exit 1; }
+find gpurun_out/km_prof -name "*kernel_stats.csv" | head -1 | xargs -I{} head -12 {}
