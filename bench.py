@@ -92,12 +92,15 @@ def timed_parallel(fn, parts, threads):
 # ---------------------------------------------------------------- workloads
 
 class KMeansWorkload:
-    """The dominant kernel is the exact-integer i8 screen (k_screen, timed as
-    k_kmeans_assign): its work is 6 i8 limb products of 2 x 64 ops per
-    (row, padded center, 64-dim step), priced against the dense i8 MFMA peak;
-    the fp64-equivalent rate (2 k d flop per row) is reported beside it."""
-    kernel = "k_kmeans_assign"
-    pmc_kernels = ("k_screen32", "k_screen")   # d <= 256 / d <= 512 forms
+    """The dominant kernel is the two-limb pass of the exact-integer i8 screen
+    (k_screen32<.., 2, false>, timed as k_kmeans_screen2): its work is 3 i8
+    limb products of 2 ops per (row, padded center, dimension), priced
+    against the dense i8 MFMA peak; the fp64-equivalent rate (2 k d flop per
+    row) is reported beside it, and the three-limb pass over the rows it
+    leaves (k_kmeans_screen3) is timed too."""
+    kernel = "k_kmeans_screen2"
+    kernels = ("k_kmeans_screen2", "k_kmeans_screen3", "k_kmeans_assign_fp64", "k_chunk_sums")
+    pmc_kernels = ("k_screen32_l2",)
     bound = "mfma"
     unit = "TOPS"
     peak = I8_PEAK_TOPS
@@ -148,16 +151,26 @@ class KMeansWorkload:
         self.plan.update(self.C, self.cnorm, sums, wsum, 1e-4, self.conv)
 
     def work_per_launch(self, launches_per_step):
-        D = 128 * ((self.d + 127) // 128)                 # 64-dim steps, even count
-        kpad = 16 * (((self.k + 15) // 16 + 3) // 4 * 4)  # 16-center tiles, 4 waves
-        return 12.0 * D * kpad * self.n / launches_per_step   # i8 ops
+        D = 128 * ((self.d + 127) // 128)                 # 32-dim substeps, padded
+        kpad = 16 * (((self.k + 15) // 16 + 3) // 4 * 4)  # 32-center tiles
+        return 6.0 * D * kpad * self.n / launches_per_step   # i8 ops
 
     def extra_roofline(self, launches_per_step, avg_s):
+        import torch
         flops = 2.0 * self.k * self.d * self.n / launches_per_step
+        # screen tiers of one counted assign, after the timed region
+        a = torch.empty(self.n, dtype=torch.int32, device=self.X.device)
+        c = torch.empty(self.n, dtype=torch.float64, device=self.X.device)
+        self.plan.stats(self.C)
+        exact = self.plan.assign(self.X, self.xnorm, self.C, self.cnorm, a, c,
+                                 count_exact=True, rows=self.rows)
+        tier2, _ = self.plan.last_tiers()
         return {"algorithmic_fp64_flop_per_launch": flops,
                 "fp64_equivalent_tflops": flops / avg_s / 1e12,
-                "note": "i8 ops = exact 3-limb integer screen (6 MFMA limb products); "
-                        "fp64-equivalent = 2kd flop/row over the same time"}
+                "rows_left_by_two_limb_pass": self.plan.last_screen(),
+                "rows_left_by_three_limb_pass": tier2, "rows_left_to_exact": exact,
+                "note": "i8 ops = two-limb integer screen (3 MFMA limb products, every "
+                        "row); fp64-equivalent = 2kd flop/row over the same time"}
 
     def describe(self):
         return (f"KMeans k={self.k} Lloyd iteration, dense fp64 {self.n} x {self.d} rows per GPU "

@@ -85,6 +85,13 @@ class KMeansPlan:
         N.check(self._lib.cyc_kmeans_last_tiers(self.handle, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
 
+    def last_screen(self):
+        """Rows the two-limb i8 pass left to the three-limb pass on the last
+        assign(count_exact=True) (-1: that call ran no two-limb pass)."""
+        a = ctypes.c_int64(0)
+        N.check(self._lib.cyc_kmeans_last_screen(self.handle, ctypes.byref(a)))
+        return a.value
+
     def accumulate(self, X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, assign=None,
                    cost=None, stream=None, rows=None):
         N.check(self._lib.cyc_kmeans_accumulate_dev(

@@ -1711,6 +1711,7 @@ struct cyc_kmeans_plan_s {
   double omE3 = 1.0, tauL3 = 0.0, facU3 = 0.0, tauU3 = 0.0;
   int64_t lastTier2 = 0;    // rows the bf16 screen queued (last counted call)
   int64_t lastExact = 0;    // rows the fp64 screen queued (last counted call)
+  int64_t lastLimb3 = -1;   // rows the two-limb i8 pass left (-1: no such pass)
   cyc::DeviceBuffer cb3, cq3, ok3, list3, list3Count;
   // i8 exact-integer screen (kmeans_i8.hip), used with a row image
   int ktp8 = 0;
@@ -1891,15 +1892,19 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
   // Exact emulation of the reference loop for undecided rows.  The queue
   // length is read back only when the caller asks for it; otherwise a
   // grid-stride launch drains whatever the queue holds without a host sync.
-  unsigned int h_slow = 0, h_tier2 = 0;
+  unsigned int h_slow = 0, h_tier2 = 0, h_limb3 = 0;
   if (n_exact_out) {
+    const bool twoPass = rows && rows->usable && cyc::km8::uses32(p->d);
     CYC_HIP(hipMemcpyAsync(&h_slow, p->slowCount.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     if (rowCount)
       CYC_HIP(hipMemcpyAsync(&h_tier2, rowCount, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    if (twoPass)
+      CYC_HIP(hipMemcpyAsync(&h_limb3, p->list8Count.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     CYC_HIP(hipStreamSynchronize(st));
     *n_exact_out = h_slow;
     p->lastTier2 = rowCount ? (int64_t)h_tier2 : n;
     p->lastExact = h_slow;
+    p->lastLimb3 = twoPass ? (int64_t)h_limb3 : -1;
     if (h_slow) {
       hipLaunchKernelGGL(k_assign_exact, dim3((unsigned)std::min<unsigned>((h_slow + 3) / 4, 4096)), dim3(256), 0, st, X, xnorm,
                          p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm, p->k, statsArg,
@@ -2072,6 +2077,13 @@ int cyc_kmeans_last_tiers(cyc_kmeans_plan p, int64_t* fp64_screen_rows, int64_t*
   std::lock_guard<std::mutex> g(p->mu);
   *fp64_screen_rows = p->lastTier2;
   *exact_rows = p->lastExact;
+  return CYC_OK;
+}
+
+int cyc_kmeans_last_screen(cyc_kmeans_plan p, int64_t* three_limb_rows) {
+  CYC_REQUIRE(p != nullptr && three_limb_rows, "arguments must not be null");
+  std::lock_guard<std::mutex> g(p->mu);
+  *three_limb_rows = p->lastLimb3;
   return CYC_OK;
 }
 

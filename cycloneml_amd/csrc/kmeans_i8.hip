@@ -596,8 +596,10 @@ __device__ __forceinline__ double err_term2(int e, double n1, double mu, int d) 
 // list of *rowsInCount row indices).  Both read the
 // same center image (3 limb fragments per substep; LIMBS = 2 DMAs the first
 // two) and write assign[] for certified rows, the rest to list.
+// Two workgroups per CU; three for the two-limb pass (<= 168 VGPRs, LDS
+// 3 x 49 KB at S = 8), measured 7 % faster than two.
 template <int S, int W, int LIMBS, bool LIST>
-__global__ __launch_bounds__(64 * W, 2) void k_screen32(
+__global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
     const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
     int64_t n, int d, const uint4* __restrict__ Cb, const float* __restrict__ cq,
     const double* __restrict__ g, const double* __restrict__ cnorm,
@@ -607,7 +609,7 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
   constexpr int D = 32 * S, CH = 3 * D / 16;      // 16-byte chunks per image row
   constexpr int FR = LIMBS * S;                    // 1 KiB B fragments per center tile
   constexpr int TB = FR * 1024 + 256;              // tile slot: fragments, then 64 cq floats
-  constexpr int G = FR / W + 1;                    // LDS-DMA instructions per wave per tile
+  constexpr int G = FR / W;                        // fragment DMAs per wave per tile (+1: wave 0's cq)
   static_assert(FR % W == 0, "fragments split evenly over the waves");
   // ONE shared array (a second __shared__ object can make hipcc drain vmcnt
   // before every ds_read): three tile slots, reused for the final reduction.
@@ -634,10 +636,10 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
   // tile's cq (all waves write the same 256 bytes); past the last tile the
   // last one is re-read into the free slot, so every wave always has exactly
   // G DMAs per tile in flight and one counted wait fits all tiles.
-  auto issue = [&](int t) {
+  auto issue = [&](int t, int slot) {
     const int tt = t < ktp ? t : ktp - 1;
     const char* src = (const char*)Cb + (size_t)tt * (3 * S) * 1024 + lane * 16;
-    char* dst = lds + (t % 3) * TB;
+    char* dst = lds + slot * TB;
 #pragma unroll
     for (int j = 0; j < FR / W; ++j) {
       const int f = wave + W * j;                     // fragment (substep f / LIMBS, limb f % LIMBS)
@@ -646,12 +648,13 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
                                        (__attribute__((address_space(3))) void*)(dst + f * 1024),
                                        16, 0, 0);
     }
-    __builtin_amdgcn_global_load_lds((const void*)(cq + (size_t)tt * 32 + r),
-                                     (__attribute__((address_space(3))) void*)(dst + FR * 1024),
-                                     4, 0, 0);
+    if (wave == 0)   // the tile's 32 cq (lanes 32..63 repeat them)
+      __builtin_amdgcn_global_load_lds((const void*)(cq + (size_t)tt * 32 + r),
+                                       (__attribute__((address_space(3))) void*)(dst + FR * 1024),
+                                       4, 0, 0);
   };
-  issue(0);
-  issue(1);
+  issue(0, 0);
+  issue(1, 1);
   // A fragments of the wave's 32 rows, all substeps and limbs
   v4i A[S][LIMBS];
   const bool rowOk = r < rows;
@@ -685,18 +688,22 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
   }
   // tile ct from its slot: LIMBS = 3: six limb products per substep,
   // LIMBS = 2: three; B fragments by conflict-free ds_read_b128
-  auto tile = [&](int ct, v16i (&acc)[LIMBS]) {
-    const v4i* B = (const v4i*)(lds + (ct % 3) * TB) + lane;
+  auto tile = [&](int slot, v16i (&acc)[LIMBS]) {
+    const v4i* B = (const v4i*)(lds + slot * TB) + lane;
 #pragma unroll
     for (int L = 0; L < LIMBS; ++L) acc[L] = v16i{};
+    // (reading the B fragments a substep ahead measured no faster)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const v4i B0 = B[(LIMBS * s + 0) * 64], B1 = B[(LIMBS * s + 1) * 64];
+      v4i Bc[LIMBS];
+#pragma unroll
+      for (int L = 0; L < LIMBS; ++L) Bc[L] = B[(LIMBS * s + L) * 64];
+      const v4i B0 = Bc[0], B1 = Bc[1];
       acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B0, acc[0], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B1, acc[1], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B0, acc[1], 0, 0, 0);
       if constexpr (LIMBS == 3) {
-        const v4i B2 = B[(LIMBS * s + 2) * 64];
+        const v4i B2 = Bc[2];
         acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B2, acc[2], 0, 0, 0);
         acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B1, acc[2], 0, 0, 0);
         acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][2], B0, acc[2], 0, 0, 0);
@@ -709,6 +716,24 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
   // med3 per (row, center) instead of a compare, a med3 and two selects.
   const int IB = 32 - __builtin_clz((unsigned)max(ktp - 1, 1));
   const unsigned IM = (1u << IB) - 1u;
+  // LIMBS = 2: on T = 128 S1 + S2, formed right after the tile's MFMAs
+  auto epi2 = [&](int ct, float cqv, const int (&T)[16]) {
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      // cq2 is finite (padding: FLT_MAX) and round-down keeps L finite
+      const float L0 = __builtin_fmaf(-F1[reg], (float)T[reg], cqv);
+      // raw v_bfi / v_med3 / v_min: L comes out of integer ops, and hipcc
+      // would quiet it (two v_max per element) before any IEEE min or
+      // med3 -- L is never NaN
+      float L;
+      asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(L) : "s"(IM), "v"(ct), "v"(L0));
+      float m2, m1;
+      asm("v_med3_f32 %0, %1, %2, %3" : "=v"(m2) : "v"(sL1[reg]), "v"(sL2[reg]), "v"(L));
+      asm("v_min_f32 %0, %1, %2" : "=v"(m1) : "v"(sL1[reg]), "v"(L));
+      sL2[reg] = m2;
+      sL1[reg] = m1;
+    }
+  };
   auto epi = [&](int ct, float cqv, const v16i (&acc)[LIMBS]) {
     const int c = ct * 32 + r;
 #pragma unroll
@@ -721,61 +746,41 @@ __global__ __launch_bounds__(64 * W, 2) void k_screen32(
         sL2[reg] = __builtin_amdgcn_fmed3f(sL1[reg], sL2[reg], L);
         sI1[reg] = lt ? c : sI1[reg];
         sL1[reg] = lt ? L : sL1[reg];   // L is never NaN: a select, no canonicalize
-      } else {
-        // cq2 is finite (padding: FLT_MAX) and round-down keeps L finite
-        const float L0 = __builtin_fmaf(-F1[reg], (float)T, cqv);
-        // raw v_bfi / v_med3 / v_min: L comes out of integer ops, and
-        // hipcc would quiet it (two v_max per element) before any IEEE
-        // min or med3 -- L is never NaN
-        float L;
-        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(L) : "s"(IM), "v"(ct), "v"(L0));
-        float m2, m1;
-        asm("v_med3_f32 %0, %1, %2, %3" : "=v"(m2) : "v"(sL1[reg]), "v"(sL2[reg]), "v"(L));
-        asm("v_min_f32 %0, %1, %2" : "=v"(m1) : "v"(sL1[reg]), "v"(L));
-        sL2[reg] = m2;
-        sL1[reg] = m1;
       }
     }
   };
-  auto cq_of = [&](int ct) { return *(const float*)(lds + (ct % 3) * TB + FR * 1024 + r * 4); };
-  // tile t: wait for this wave's DMAs of t (the G of t + 1 may stay in
-  // flight), barrier (every wave's part of t landed; every wave is past
+  auto cq_of = [&](int slot) { return *(const float*)(lds + slot * TB + FR * 1024 + r * 4); };
+  // tile t in `slot`: wait for this wave's DMAs of t (those of t + 1 may stay
+  // in flight), barrier (every wave's part of t landed; every wave is past
   // t - 1, whose slot the DMAs of t + 2 now refill)
-  auto arrive = [&](int t) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+  auto arrive = [&](int t, int slot) {
+    if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + 1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
     __builtin_amdgcn_s_barrier();
-    issue(t + 2);
+    issue(t + 2, slot == 0 ? 2 : slot - 1);
   };
+  auto next_slot = [](int slot) { return slot == 2 ? 0 : slot + 1; };
 
   // MODE.FP_ROUND single precision = toward -inf (the L' are lower bounds)
   __builtin_amdgcn_s_setreg(0x801, 2);
-  if constexpr (LIMBS == 2) {
-    // software-pipelined: tile ct's MFMAs beside tile ct - 1's epilogue (two
-    // accumulator sets; the slot of ct - 1 is refilled only by the DMAs that
-    // arrive(ct + 1) issues, and its cq is already in a register)
-    v16i Xp[LIMBS];
-    arrive(0);
-    float cqp = cq_of(0);
-    tile(0, Xp);
-    for (int ct = 1; ct < ktp; ++ct) {
-      v16i X[LIMBS];
-      arrive(ct);
-      const float cqv = cq_of(ct);
-      tile(ct, X);
-      epi(ct - 1, cqp, Xp);
+  // (software-pipelining the epilogue beside the next tile's MFMAs needs a
+  // second accumulator set: 193 VGPRs, two waves per SIMD, 4 % slower than
+  // this form at 168 VGPRs and three waves per SIMD)
+  int sl = 0;
+  for (int ct = 0; ct < ktp; ++ct) {
+    v16i X[LIMBS];
+    arrive(ct, sl);
+    const float cqv = cq_of(sl);
+    tile(sl, X);
+    if constexpr (LIMBS == 2) {
+      int T[16];
 #pragma unroll
-      for (int L = 0; L < LIMBS; ++L) Xp[L] = X[L];   // 16 v_mov_b64 (unrolling by two spills)
-      cqp = cqv;
-    }
-    epi(ktp - 1, cqp, Xp);
-  } else {
-    for (int ct = 0; ct < ktp; ++ct) {
-      v16i X[LIMBS];
-      arrive(ct);
-      const float cqv = cq_of(ct);
-      tile(ct, X);
+      for (int reg = 0; reg < 16; ++reg) T[reg] = X[0][reg] * 128 + X[1][reg];
+      epi2(ct, cqv, T);
+    } else {
       epi(ct, cqv, X);
     }
+    sl = next_slot(sl);
   }
   __builtin_amdgcn_s_setreg(0x801, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing re-read DMAs
@@ -872,7 +877,7 @@ int launch_screen32(const void* img, const int2* meta, const double* xnorm, int6
                     const CenterParams* prm, int ktp, const int32_t* rowsIn,
                     const unsigned int* rowsInCount, int32_t* assign, int32_t* list,
                     unsigned int* listCount, hipStream_t st) {
-  KernelTimer timer("k_kmeans_assign", st);
+  KernelTimer timer(LIMBS == 2 ? "k_kmeans_screen2" : "k_kmeans_screen3", st);
   const int64_t wg = (n + 32 * W - 1) / (32 * W);   // W waves x 32 rows
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32<S, W, LIMBS, LIST>), dim3((unsigned)wg),
                      dim3(64 * W), 0, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
@@ -909,7 +914,7 @@ int launch_screen(const void* img, const int2* meta, const double* xnorm, int64_
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr = true;
   }
-  KernelTimer timer("k_kmeans_assign", st);
+  KernelTimer timer("k_kmeans_screen3", st);
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen<KS>), dim3((unsigned)((n + kBM - 1) / kBM)),
                      dim3(256), lds, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
                      cq, g, cnorm, prm, ktp, assign, list, listCount);

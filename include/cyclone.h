@@ -117,6 +117,10 @@ int cyc_kmeans_point_cost_dev(cyc_kmeans_plan plan, const double* X, const doubl
  * to the fp64 MFMA screen (all rows when neither runs), and rows left to the
  * exact emulation. */
 int cyc_kmeans_last_tiers(cyc_kmeans_plan plan, int64_t* fp64_screen_rows, int64_t* exact_rows);
+/* Rows the d <= 256 screen's two-limb i8 pass left to its three-limb pass on
+ * the last counted assign (-1 when that call ran no two-limb pass).  A
+ * statistic of the tiered findClosest; no reference counterpart. */
+int cyc_kmeans_last_screen(cyc_kmeans_plan plan, int64_t* three_limb_rows);
 
 /* One partition's contribution to a Lloyd iteration: statistics + assign +
  * per-cluster sums.  sums[k*d] += sum of w*x, wsum[k] += sum of w,

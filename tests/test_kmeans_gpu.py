@@ -493,6 +493,40 @@ def test_i8_screen_extreme_centers(cuda, monkeypatch, scale):
     np.testing.assert_array_equal(c8, rc)
 
 
+@pytest.mark.parametrize("n,d,k,sep", [(6000, 256, 1024, True), (5000, 128, 300, False),
+                                       (3000, 200, 65, True), (2000, 512, 40, True)])
+def test_i8_two_limb_pass(cuda, monkeypatch, n, d, k, sep):
+    """d <= 256: the two-limb i8 pass screens every row and the three-limb
+    pass only its leftovers (a subset of the rows), bit-identical to the
+    restatement; separated clusters leave few rows to the three-limb pass.
+    d > 256 runs no two-limb pass (-1)."""
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    monkeypatch.setenv("CYC_KMEANS_ASSIGN", "2")
+    rng = np.random.default_rng(n + d + k)
+    true_c = rng.normal(scale=4.0 if sep else 0.7, size=(k, d))
+    X = true_c[rng.integers(0, k, n)] + rng.normal(size=(n, d))
+    C = true_c + rng.normal(scale=0.1, size=true_c.shape) if sep else X[:k].copy()
+    Xd, Cd = _dev(X, cuda), _dev(C, cuda)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = KMeansPlan(d, k, n)
+    p.stats(Cd)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    c = torch.empty(n, dtype=torch.float64, device=cuda)
+    ex = p.assign(Xd, xn, Cd, cn, a, c, count_exact=True, rows=p.rows(Xd))
+    l3 = p.last_screen()
+    t2, _ = p.last_tiers()
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a.cpu().numpy(), ra)
+    np.testing.assert_array_equal(c.cpu().numpy(), rc)
+    if d > 256:
+        assert l3 == -1
+        return
+    assert 0 <= t2 <= l3 <= n and ex <= t2
+    if sep:
+        assert l3 <= n // 10, l3
+
+
 def test_rows_image_guard(cuda):
     """The row image is bound to its rows: other X or n is refused with the
     reference-style message."""

@@ -7,4 +7,5 @@ timeout -k 10 300 python -u bench.py --workload kmeans --cpu-seconds 0 > gpurun_
 cat gpurun_out/bench_kmeans.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/km_prof -o km -- python3 -u bench.py --workload kmeans --cpu-seconds 0 --steps 5 --warmup 2 > gpurun_out/km_prof.log 2>&1 || { echo PROF FAIL; tail -20 gpurun_out/km_prof.log; exit 1; }
-find gpurun_out/km_prof -name "*kernel_stats.csv" | head -1 | xargs -I{} head -12 {}
+python3 tools/rocpd_stats.py gpurun_out/km_prof/km_results.db 8
+if [ -n "$PMC" ]; then timeout -k 10 400 bash tools/pmc_mfma.sh km2 k_screen32 --workload kmeans > gpurun_out/pmc_km2.txt 2>&1 && cat gpurun_out/pmc_km2.txt; fi
