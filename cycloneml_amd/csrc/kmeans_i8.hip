@@ -672,26 +672,45 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
       }
   }
   // row of accumulator register reg: (reg & 3) + 8 (reg >> 2) + 4 h
+  const int exr = rowOk ? meta[myRow].x : INT_MIN;
+  // LIMBS = 3: per-row unit F1 = 2^(ex + ec - 20) of T in f32 bounds.
+  // LIMBS = 2: integer bounds in the same units: L / F1 = Q - T with
+  // Q = cq / F1 rounded, from one per-lane base per tile at the wave's
+  // smallest exponent exmin, shifted right by sh = ex - exmin per row.
   float F1[16];
-  {
-    const int ex = rowOk ? meta[myRow].x : INT_MIN;
-    const float f = ex == INT_MIN ? 0.0f : __builtin_ldexpf(1.0f, ex + P.ec - 20);
+  int sh[16];
+  int exmin = 0;
+  if constexpr (LIMBS == 3) {
+    const float f = exr == INT_MIN ? 0.0f : __builtin_ldexpf(1.0f, exr + P.ec - 20);
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) F1[reg] = __shfl(f, (reg & 3) + 8 * (reg >> 2) + 4 * h);
+  } else {
+    int e = exr == INT_MIN ? INT_MAX : exr;
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) e = min(e, __shfl_xor(e, m));
+    exmin = __builtin_amdgcn_readfirstlane(e == INT_MAX ? 0 : e);
+    const int s0 = exr == INT_MIN ? 31 : min(exr - exmin, 31);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) sh[reg] = __shfl(s0, (reg & 3) + 8 * (reg >> 2) + 4 * h);
   }
+  // cq scaled to the units 2^(exmin + ec - 20)
+  const float qscale = __builtin_ldexpf(1.0f, max(-160, min(160, 20 - P.ec - exmin)));
+  bool qbad = false;   // a cq below -2^30 units: the wave certifies nothing
+  // LIMBS = 3: the two smallest f32 bounds; LIMBS = 2: the two largest
+  // V = T - Q (the smallest L = -F1 V), tile index in the low IB bits
   float sL1[16], sL2[16];
+  int sV1[16], sV2[16];
   int sI1[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     sL1[q] = sL2[q] = __builtin_inff();
+    sV1[q] = sV2[q] = INT_MIN;
     sI1[q] = -1;
   }
   // tile ct from its slot: LIMBS = 3: six limb products per substep,
   // LIMBS = 2: three; B fragments by conflict-free ds_read_b128
-  auto tile = [&](int slot, v16i (&acc)[LIMBS]) {
+  auto tile = [&](int slot, v16i (&acc)[LIMBS]) {   // acc: initialised by the caller
     const v4i* B = (const v4i*)(lds + slot * TB) + lane;
-#pragma unroll
-    for (int L = 0; L < LIMBS; ++L) acc[L] = v16i{};
     // (reading the B fragments a substep ahead measured no faster)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
@@ -710,28 +729,22 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
       }
     }
   };
-  // the two smallest lower bounds per row and the index of the smallest.
-  // LIMBS = 2 keeps the tile index in the low IB mantissa bits of L (moving
-  // L by < 2^IB ulp either way, charged in the certification): a min and a
-  // med3 per (row, center) instead of a compare, a med3 and two selects.
+  // LIMBS = 2 keeps the tile index in the low IB bits of V (moving it by
+  // < 2^IB units either way, charged in the certification): a max and a med3
+  // per (row, center) instead of a compare, a med3 and two selects.
   const int IB = 32 - __builtin_clz((unsigned)max(ktp - 1, 1));
   const unsigned IM = (1u << IB) - 1u;
-  // LIMBS = 2: on T = 128 S1 + S2, formed right after the tile's MFMAs
-  auto epi2 = [&](int ct, float cqv, const int (&T)[16]) {
+  // LIMBS = 2, after the tile's MFMAs: acc[1] started at -Q
+  auto epi2 = [&](int ct, const v16i (&acc)[LIMBS]) {
+    // ct in a VGPR: one v_and_or_b32 may read only one SGPR (the mask)
+    unsigned ctv;
+    asm("v_mov_b32 %0, %1" : "=v"(ctv) : "s"(ct));
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      // cq2 is finite (padding: FLT_MAX) and round-down keeps L finite
-      const float L0 = __builtin_fmaf(-F1[reg], (float)T[reg], cqv);
-      // raw v_bfi / v_med3 / v_min: L comes out of integer ops, and hipcc
-      // would quiet it (two v_max per element) before any IEEE min or
-      // med3 -- L is never NaN
-      float L;
-      asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(L) : "s"(IM), "v"(ct), "v"(L0));
-      float m2, m1;
-      asm("v_med3_f32 %0, %1, %2, %3" : "=v"(m2) : "v"(sL1[reg]), "v"(sL2[reg]), "v"(L));
-      asm("v_min_f32 %0, %1, %2" : "=v"(m1) : "v"(sL1[reg]), "v"(L));
-      sL2[reg] = m2;
-      sL1[reg] = m1;
+      const int V = acc[0][reg] * 128 + acc[1][reg];                 // T - Q
+      const int Ve = (int)(((unsigned)V & ~IM) | ctv);                  // ct < 2^IB
+      sV2[reg] = max(min(sV1[reg], sV2[reg]), min(max(sV1[reg], sV2[reg]), Ve));   // v_med3_i32
+      sV1[reg] = max(sV1[reg], Ve);
     }
   };
   auto epi = [&](int ct, float cqv, const v16i (&acc)[LIMBS]) {
@@ -771,13 +784,21 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
     v16i X[LIMBS];
     arrive(ct, sl);
     const float cqv = cq_of(sl);
-    tile(sl, X);
     if constexpr (LIMBS == 2) {
-      int T[16];
+      // -Q per row: ceil(floor(cq 2^k) / 2^sh) >= Q - 1 unit; cq above 2^30
+      // units clamps (a smaller Q: still a lower bound)
+      const float pf = cqv * qscale;   // exact (a power of two; round-down mode)
+      qbad |= pf < -0x1p30f;
+      const int nb = -(int)__builtin_floorf(__builtin_fminf(pf, 0x1p30f));
+      X[0] = v16i{};
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) T[reg] = X[0][reg] * 128 + X[1][reg];
-      epi2(ct, cqv, T);
+      for (int reg = 0; reg < 16; ++reg) X[1][reg] = nb >> sh[reg];
+      tile(sl, X);
+      epi2(ct, X);
     } else {
+#pragma unroll
+      for (int L = 0; L < LIMBS; ++L) X[L] = v16i{};
+      tile(sl, X);
       epi(ct, cqv, X);
     }
     sl = next_slot(sl);
@@ -787,76 +808,101 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
 
   if constexpr (LIMBS == 2) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) sI1[q] = (int)(__float_as_uint(sL1[q]) & IM) * 32 + r;
+    for (int q = 0; q < 16; ++q) sI1[q] = (int)((unsigned)sV1[q] & IM) * 32 + r;
   }
   // each row's (L1, L2, I1) over the 32 lanes (centers) of its half: every
   // xor step halves the registers a lane keeps (lanes with the step's bit
   // keep the upper half and send the lower), so 16 rows cost 8 + 4 + 2 + 1 + 1
   // shuffles per quantity.  Equal L1 from two centers leave L2 = L1, which
   // never certifies, so the merge needs no index tie-break.
-  auto merge = [](float& L1, float& L2, int& I1, float oL1, float oL2, int oI1) {
+  auto mergeL = [](float& L1, float& L2, int& I1, float oL1, float oL2, int oI1) {
     L2 = __builtin_fminf(__builtin_fmaxf(L1, oL1), __builtin_fminf(L2, oL2));
     I1 = oL1 < L1 ? oI1 : I1;
     L1 = __builtin_fminf(L1, oL1);
   };
-#pragma unroll
-  for (int lev = 0; lev < 4; ++lev) {
-    const int half = 8 >> lev, m = 16 >> lev;
-    const bool hi = (lane & m) != 0;
-#pragma unroll
-    for (int i = 0; i < half; ++i) {
-      const float oL1 = __shfl_xor(hi ? sL1[i] : sL1[i + half], m);
-      const float oL2 = __shfl_xor(hi ? sL2[i] : sL2[i + half], m);
-      const int oI1 = __shfl_xor(hi ? sI1[i] : sI1[i + half], m);
-      float L1 = hi ? sL1[i + half] : sL1[i], L2 = hi ? sL2[i + half] : sL2[i];
-      int I1 = hi ? sI1[i + half] : sI1[i];
-      merge(L1, L2, I1, oL1, oL2, oI1);
-      sL1[i] = L1;
-      sL2[i] = L2;
-      sI1[i] = I1;
-    }
-  }
-  merge(sL1[0], sL2[0], sI1[0], __shfl_xor(sL1[0], 1), __shfl_xor(sL2[0], 1),
+  auto mergeV = [](int& V1, int& V2, int& I1, int oV1, int oV2, int oI1) {
+    V2 = max(min(V1, oV1), max(V2, oV2));
+    I1 = oV1 > V1 ? oI1 : I1;
+    V1 = max(V1, oV1);
+  };
+#define CYC_REDUCE(K1, K2, MERGE)                                                   \
+  _Pragma("unroll") for (int lev = 0; lev < 4; ++lev) {                             \
+    const int half = 8 >> lev, m = 16 >> lev;                                       \
+    const bool hi = (lane & m) != 0;                                                \
+    _Pragma("unroll") for (int i = 0; i < half; ++i) {                              \
+      const auto o1 = __shfl_xor(hi ? K1[i] : K1[i + half], m);                     \
+      const auto o2 = __shfl_xor(hi ? K2[i] : K2[i + half], m);                     \
+      const int oI1 = __shfl_xor(hi ? sI1[i] : sI1[i + half], m);                   \
+      auto k1 = hi ? K1[i + half] : K1[i];                                          \
+      auto k2 = hi ? K2[i + half] : K2[i];                                          \
+      int I1 = hi ? sI1[i + half] : sI1[i];                                         \
+      MERGE(k1, k2, I1, o1, o2, oI1);                                               \
+      K1[i] = k1;                                                                   \
+      K2[i] = k2;                                                                   \
+      sI1[i] = I1;                                                                  \
+    }                                                                               \
+  }                                                                                 \
+  MERGE(K1[0], K2[0], sI1[0], __shfl_xor(K1[0], 1), __shfl_xor(K2[0], 1),           \
         __shfl_xor(sI1[0], 1));
+  if constexpr (LIMBS == 2) {
+    CYC_REDUCE(sV1, sV2, mergeV)
+  } else {
+    CYC_REDUCE(sL1, sL2, mergeL)
+  }
+#undef CYC_REDUCE
   // lane holds row register q = lane bits 1..4
   // per-wave reduction area in the (now idle) slots: L1, L2, I1 x 32 rows
   __syncthreads();
-  float* redL1 = (float*)lds + wave * 96;
+  float* redL1 = (float*)lds + wave * 96;   // LIMBS = 2: the V1, V2 bits
   float* redL2 = redL1 + 32;
   int* redI1 = (int*)(redL1 + 64);
   if ((lane & 1) == 0) {
     const int q = (lane >> 1) & 15;
     const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
-    redL1[row] = sL1[0];
-    redL2[row] = sL2[0];
+    redL1[row] = LIMBS == 2 ? __int_as_float(sV1[0]) : sL1[0];
+    redL2[row] = LIMBS == 2 ? __int_as_float(sV2[0]) : sL2[0];
     redI1[row] = sI1[0];
   }
+  const bool waveBad = __builtin_amdgcn_ballot_w64(qbad) != 0;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   if (lane < rows) {
     const int64_t grow = rowAt(lane);
     const int2 mt = meta[grow];
-    const float L1 = redL1[lane], L2 = redL2[lane];
     const int I1 = redI1[lane];
+    // L1, L2 as fp64 (LIMBS = 2: -F1 V, exact; V2 = INT_MIN: no second)
+    double l1, l2;
+    bool clamped = false;
+    if constexpr (LIMBS == 2) {
+      const double f1 = __builtin_ldexp(1.0, mt.x + P.ec - 20);
+      const int v1 = __float_as_int(redL1[lane]), v2 = __float_as_int(redL2[lane]);
+      l1 = -f1 * (double)v1;
+      l2 = v2 == INT_MIN ? __builtin_inf() : -f1 * (double)v2;
+      // the winner's Q must not have clamped (its bound would be too low)
+      if (I1 >= 0 && I1 < P.k) clamped = !((double)cq[I1] * (double)qscale <= 0x1p30);
+    } else {
+      l1 = (double)redL1[lane];
+      l2 = (double)redL2[lane];
+    }
     bool decided = false;
-    if (mt.x != INT_MIN && I1 >= 0 && I1 < P.k && __builtin_isfinite(L1)) {
+    if (mt.x != INT_MIN && I1 >= 0 && I1 < P.k && !clamped && !waveBad && __builtin_isfinite(l1)) {
       const double xn = xnorm[grow], cn = cnorm[I1];
       const double xx = xn * xn, cc = cn * cn;
       const double n1 = (double)__int_as_float(mt.y);   // bounds |xh3|_1
       const double fx = LIMBS == 3 ? err_term(mt.x, n1, mu, d)
                                    : err_term2(mt.x, n1 + (double)d * __builtin_ldexp(1.0078125, mt.x - 15),
                                                mu, d);
-      const double l1 = (double)L1;
-      // LIMBS = 2: the index bits move each L by < 2^IB ulp <= 2^(IB-23) |L|
+      // LIMBS = 2: the index bits move each V by < 2^IB units and the
+      // rounded Q adds < 1 more: |L1 - L1'|, |L2 - L2'| < (2^IB + 1) F1
       const double enc = LIMBS == 3 ? 0.0
-                                    : __builtin_ldexp(__builtin_fabs(l1) + __builtin_fabs((double)L2), IB - 23) + 0x1p-120;
+                                    : __builtin_ldexp((double)(IM + 3u), mt.x + P.ec - 20);
       const double M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) + 2.0 * enc +
                         0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g[I1]) +
                         0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
-                                   __builtin_fmin(__builtin_fabs((double)L2), 0x1p120)) +
+                                   __builtin_fmin(__builtin_fabs(l2), 0x1p120)) +
                         0x1p-90) *
                        (1.0 + 0x1p-30);
-      decided = !__builtin_isfinite(L2) || ((double)L2 - l1) > M;
+      decided = !__builtin_isfinite(l2) || (l2 - l1) > M;
     }
     if (decided) {
       assign[grow] = I1;
