@@ -439,6 +439,8 @@ constexpr int MT = 512;    // threads per margin workgroup
 // 1 KiB pieces spread over the waves, one chunk ahead; no registers), one
 // barrier per chunk.  Padding classes read the next coefficients (finite;
 // their margins are never used) or zero past the end of coef.
+// (The last class tile on v_mfma_f64_4x4x4f64, as k_mlr_grad does, spills
+// here at CT = 7 and measured 4.6 % slower.)
 template <int CT>
 __global__ __launch_bounds__(MT) void k_mlr_margins(
     const double* __restrict__ X, const double* __restrict__ labels,
@@ -641,7 +643,14 @@ constexpr int GF = 256;   // features per workgroup
 // HBM straight into registers in the MFMA B layout (lane: feature l & 15 of
 // its 16-feature tile, row 4 kk + (l >> 4) of k-step kk; 128 contiguous
 // bytes per row), both one chunk ahead; one barrier per chunk.
-template <int CT>
+// T4 (C mod 16 in 1..4): the last class tile on v_mfma_f64_4x4x4f64, a
+// quarter of the 16x16x4 cycles: 4 blocks of 4 x 4 x 4, lane 16k + 4b + i
+// holding A(i, k), lane 16k + 4b + j B(k, j) of block b and lane 16i + 4b + j
+// the result (measured on gfx950: tools/probe/mfma_f64_4x4.hip).  Here A =
+// the 4 classes' multipliers of row k (the same for every block), B = the
+// 16x16x4 X operand (block b: features 4b .. 4b + 3), so the result is class
+// l >> 4, feature l & 15.
+template <int CT, bool T4>
 __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mult,
                                                   const double* __restrict__ X, int64_t n, int F,
                                                   int64_t rowsPerSplit,
@@ -657,6 +666,7 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
   cyc_double4 acc[CT][2];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) acc[ct][0] = acc[ct][1] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+  double acc4[2] = {0.0, 0.0};
   // Buffer descriptors over this split's rows: 32-bit offsets, rows past the
   // split and features past F read as zero.  Host: rowsPerSplit * max(F, CP)
   // * 8 < 2^31.
@@ -697,10 +707,15 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
 #pragma unroll
     for (int kk = 0; kk < GR / 4; ++kk) {
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
+      for (int ct = 0; ct < (T4 ? CT - 1 : CT); ++ct) {
         const double a = M[(4 * kk + g) * CP + ct * 16 + (lane & 15)];
         acc[ct][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, xc[kk][0], acc[ct][0], 0, 0, 0);
         acc[ct][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, xc[kk][1], acc[ct][1], 0, 0, 0);
+      }
+      if constexpr (T4) {
+        const double a = M[(4 * kk + g) * CP + (CT - 1) * 16 + (lane & 3)];
+        acc4[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, xc[kk][0], acc4[0], 0, 0, 0);
+        acc4[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, xc[kk][1], acc4[1], 0, 0, 0);
       }
     }
   };
@@ -716,7 +731,7 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
   // slab[split][ftile][c][f_local]
   double* out = slab + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * CP * GF;
 #pragma unroll
-  for (int ct = 0; ct < CT; ++ct)
+  for (int ct = 0; ct < (T4 ? CT - 1 : CT); ++ct)
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -725,6 +740,11 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
         const int fl = wave * 32 + q * 16 + (lane & 15);
         out[(size_t)c * GF + fl] = acc[ct][q][r];
       }
+  if constexpr (T4) {   // classes (CT - 1) 16 + 0..3; the fold reads only c < C
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      out[(size_t)((CT - 1) * 16 + (lane >> 4)) * GF + wave * 32 + q * 16 + (lane & 15)] = acc4[q];
+  }
 }
 
 // grad[f*C + c] += sum_s slab (fixed order); the dger fitWithMean correction
@@ -1423,6 +1443,9 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
   // bounded (8M x CP doubles: 7.3 GB at C = 100); a whole 6.25M-row shard of
   // the 8-GPU config is one launch (no second partial round of tiles).
   const int64_t chunk = std::min<int64_t>(n, 8 << 20);
+  // k_mlr_grad: the last class tile on the 4x4x4 form when it holds 1..4
+  // classes (2.6 % faster at C = 100)
+  const bool t4 = C % 16 != 0 && C % 16 <= 4;
   const int mblocks = 256;   // persistent: one 8-wave workgroup per CU
   const int64_t mwaves = (int64_t)mblocks * (MT / 64);
   const int ftiles = (F + GF - 1) / GF;
@@ -1482,7 +1505,9 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
     splits = (m + rps - 1) / rps;
     if ((rc = p->gslab.reserve(sizeof(double) * (size_t)splits * ftiles * CP * GF))) return rc;
 #define CYC_MLR_G(CTV)                                                                         \
-  hipLaunchKernelGGL(k_mlr_grad<CTV>, dim3(ftiles, (unsigned)splits), dim3(512), 0, st,         \
+  if (t4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_grad<CTV, true>), dim3(ftiles, (unsigned)splits), dim3(512), 0, st, \
+                     (const double*)p->multBuf.ptr, Xc, m, F, rps, (double*)p->gslab.ptr); \
+  else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_grad<CTV, false>), dim3(ftiles, (unsigned)splits), dim3(512), 0, st, \
                      (const double*)p->multBuf.ptr, Xc, m, F, rps, (double*)p->gslab.ptr)
     {
     cyc::KernelTimer tg("k_mlr_grad", st);
