@@ -439,8 +439,8 @@ constexpr int MT = 512;    // threads per margin workgroup
 // 1 KiB pieces spread over the waves, one chunk ahead; no registers), one
 // barrier per chunk.  Padding classes read the next coefficients (finite;
 // their margins are never used) or zero past the end of coef.
-// (The last class tile on v_mfma_f64_4x4x4f64, as k_mlr_grad does, spills
-// here at CT = 7 and measured 4.6 % slower.)
+// (The last class tile on v_mfma_f64_4x4x4f64, as k_mlr_grad does, measured
+// 4-5 % slower here at C = 100, with or without sched_barrier fences.)
 template <int CT>
 __global__ __launch_bounds__(MT) void k_mlr_margins(
     const double* __restrict__ X, const double* __restrict__ labels,
