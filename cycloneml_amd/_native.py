@@ -22,6 +22,10 @@ CYC_ERR_HIP = 2
 CYC_ERR_ALLOC = 3
 CYC_ERR_UNSUPPORTED = 4
 CYC_ERR_NO_DEVICE = 5
+CYC_ERR_ASSERTION = 6
+
+CYC_DISTANCE_EUCLIDEAN = 0
+CYC_DISTANCE_COSINE = 1
 
 _lib = None
 _lock = threading.Lock()
@@ -45,6 +49,7 @@ SIGNATURES = {
     "cyc_row_norms_dev": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "cyc_kmeans_plan_create": (ctypes.c_int, [_i32, _i32, _i64, ctypes.POINTER(_vp)]),
     "cyc_kmeans_plan_destroy": (ctypes.c_int, [_vp]),
+    "cyc_kmeans_plan_set_distance_measure": (ctypes.c_int, [_vp, _i32]),
     "cyc_kmeans_stats_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     "cyc_kmeans_assign_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
                                              _pi64, _vp]),
@@ -192,6 +197,10 @@ class IllegalArgumentException(ValueError):
     """A reference `require` failed (Scala IllegalArgumentException)."""
 
 
+class JavaAssertionError(AssertionError):
+    """A reference `assert` failed (java.lang.AssertionError)."""
+
+
 def load():
     """Load libcyclone.so; raises if it is missing (no silent fallback)."""
     global _lib
@@ -217,6 +226,8 @@ def check(rc: int):
     msg = load().cyc_last_error().decode(errors="replace")
     if rc == CYC_ERR_INVALID_ARG:
         raise IllegalArgumentException(msg)
+    if rc == CYC_ERR_ASSERTION:
+        raise JavaAssertionError(msg)
     raise CycloneError(rc, msg)
 
 

@@ -25,15 +25,33 @@ def _torch():
     return torch
 
 
-class KMeansPlan:
-    """RAII wrapper of cyc_kmeans_plan (device scratch for one (d, k) shape)."""
+EUCLIDEAN = "euclidean"
+COSINE = "cosine"
+_MEASURES = {EUCLIDEAN: N.CYC_DISTANCE_EUCLIDEAN, COSINE: N.CYC_DISTANCE_COSINE}
 
-    def __init__(self, d: int, k: int, max_rows: int = 1):
+
+def _decode_measure(dm: str) -> int:
+    """DistanceMeasure.decodeFromString (DistanceMeasure.scala:241-247)."""
+    if dm not in _MEASURES:
+        raise N.IllegalArgumentException(
+            f"distanceMeasure must be one of: {EUCLIDEAN}, {COSINE}. {dm} provided.")
+    return _MEASURES[dm]
+
+
+class KMeansPlan:
+    """RAII wrapper of cyc_kmeans_plan (device scratch for one (d, k) shape
+    and one DistanceMeasure)."""
+
+    def __init__(self, d: int, k: int, max_rows: int = 1, distanceMeasure: str = EUCLIDEAN):
         self._lib = N.load()
+        measure = _decode_measure(distanceMeasure)
         h = ctypes.c_void_p()
         N.check(self._lib.cyc_kmeans_plan_create(int(d), int(k), int(max_rows), ctypes.byref(h)))
         self.handle = h
         self.d, self.k = int(d), int(k)
+        self.distanceMeasure = distanceMeasure
+        if measure != N.CYC_DISTANCE_EUCLIDEAN:
+            N.check(self._lib.cyc_kmeans_plan_set_distance_measure(h, measure))
 
     def close(self):
         if self.handle:
@@ -174,12 +192,16 @@ def row_norms_csr(rowptr, values, out=None, stream=None):
 
 
 class KMeansModel:
-    """mllib/clustering/KMeansModel.scala: centers (k x d), cost, numIter."""
+    """mllib/clustering/KMeansModel.scala: centers (k x d), distanceMeasure,
+    cost, numIter."""
 
-    def __init__(self, clusterCenters, trainingCost=0.0, numIter=0):
+    def __init__(self, clusterCenters, trainingCost=0.0, numIter=0,
+                 distanceMeasure: str = EUCLIDEAN):
+        _decode_measure(distanceMeasure)
         self.clusterCenters = np.ascontiguousarray(clusterCenters, dtype=np.float64)
         self.trainingCost = float(trainingCost)
         self.numIter = int(numIter)
+        self.distanceMeasure = distanceMeasure
 
     @property
     def k(self):
@@ -204,7 +226,8 @@ class KMeansModel:
         if st is None or st["key"] != key:
             C = torch.from_numpy(self.clusterCenters).to(device)
             d = self.clusterCenters.shape[1]
-            plan = KMeansPlan(d if csr_d is None else csr_d, self.k, max(1, n))
+            plan = KMeansPlan(d if csr_d is None else csr_d, self.k, max(1, n),
+                              self.distanceMeasure)
             cnorm = row_norms(C)
             # the model's lazy statistics (KMeansModel.scala:51-56)
             plan.stats(C)
@@ -325,14 +348,15 @@ class KMeans:
         return self
 
     def setDistanceMeasure(self, dm: str):
-        if dm != "euclidean":
-            raise N.IllegalArgumentException(
-                "only the euclidean distance measure runs on the MI355X path")
+        """KMeans.scala:184-188.  validateDistanceMeasure's result is not
+        checked there, so an unknown name fails at the run's
+        DistanceMeasure.decodeFromString (KMeans.scala:248), as here."""
         self.distanceMeasure = dm
         return self
 
     @staticmethod
-    def updateParallelCosts(X, newCenters, costs=None, xnorm=None, stream=None):
+    def updateParallelCosts(X, newCenters, costs=None, xnorm=None, stream=None,
+                            distanceMeasure=EUCLIDEAN):
         """One k-means|| cost update on the device (KMeans.scala:392-396):
         costs = min(pointCost(newCenters, x), cost) per row, pointCost being
         findClosest without statistics (bit-exact per row).  costs=None starts
@@ -341,7 +365,8 @@ class KMeans:
         all-reduce across ranks.  The sampling (XORShiftRandom per partition)
         and LocalKMeans stay on the host, as in the reference driver."""
         torch = _torch()
-        m = KMeansModel(np.asarray(newCenters, dtype=np.float64))
+        m = KMeansModel(np.asarray(newCenters, dtype=np.float64),
+                        distanceMeasure=distanceMeasure)
         _, c = m.pointCosts(X, xnorm, stream)
         if costs is not None:
             c = torch.minimum(c, costs)   # math.min: NaN propagates either way
@@ -365,7 +390,7 @@ class KMeans:
         k = self.k
         if xnorm is None:
             xnorm = row_norms(X, stream=stream)
-        plan = KMeansPlan(d, k, n)
+        plan = KMeansPlan(d, k, n, self.distanceMeasure)   # decodeFromString (:248)
         rows = plan.rows(X, stream=stream)     # once per fit, like the cached norms
         C = torch.from_numpy(self.initialModel.clusterCenters.copy()).to(dev)
         parallel.broadcast_(C)             # bcCenters (KMeans.scala:276)
@@ -387,7 +412,7 @@ class KMeans:
             iteration += 1
         rows.close()
         plan.close()
-        return KMeansModel(C.cpu().numpy(), cost, iteration)
+        return KMeansModel(C.cpu().numpy(), cost, iteration, self.distanceMeasure)
 
     def run_csr(self, rowptr, colidx, values, numFeatures, weights=None, stream=None,
                 iteration_callback=None):
@@ -403,7 +428,7 @@ class KMeans:
         d, k = int(numFeatures), self.k
         n = int(rowptr.shape[0]) - 1
         xnorm = row_norms_csr(rowptr, values, stream=stream)
-        plan = KMeansPlan(d, k, n)
+        plan = KMeansPlan(d, k, n, self.distanceMeasure)
         C = torch.from_numpy(self.initialModel.clusterCenters.copy()).to(dev)
         parallel.broadcast_(C)
         cnorm = row_norms(C, stream=stream)
@@ -423,4 +448,4 @@ class KMeans:
                 iteration_callback(iteration, cost)
             iteration += 1
         plan.close()
-        return KMeansModel(C.cpu().numpy(), cost, iteration)
+        return KMeansModel(C.cpu().numpy(), cost, iteration, self.distanceMeasure)

@@ -35,6 +35,7 @@
 
 #include "common.hpp"
 #include "kmeans_i8.hpp"
+#include "kmeans_cos.hpp"
 
 namespace {
 
@@ -1699,6 +1700,10 @@ __global__ __launch_bounds__(256) void k_sparse_sums(
 // ------------------------------------------------------------------ plan
 struct cyc_kmeans_plan_s {
   int d = 0, k = 0, d4 = 0, kpad = 0, bm = 0, ldsStride = 0;
+  int measure = CYC_DISTANCE_EUCLIDEAN;   // DistanceMeasure of the plan
+  // cosine: unit center directions for the screen, their norms, computed
+  // center norms (statistics without given norms)
+  cyc::DeviceBuffer cosV, cosVn, cosCn;
   bool dense_ok = true;     // d fits the LDS-resident dense assign kernels (d <= 1240)
   int variant = 1;          // 2: k_kmeans_assign2 (fp64 screen), 3: bf16x3 screen
   int ldsStride2 = 0;
@@ -1738,7 +1743,8 @@ struct cyc_kmeans_rows_s {
   int64_t n = 0;
   int d = 0;
   bool usable = false;     // d <= 512
-  cyc::DeviceBuffer img, meta;
+  bool cosine = false;     // image of the unit directions x / |x|
+  cyc::DeviceBuffer img, meta, unorm;   // unorm: |x / |x|| per row (cosine)
 };
 
 namespace {
@@ -1974,6 +1980,104 @@ int ensure_rows(cyc_kmeans_plan p, int64_t n) {
   return CYC_OK;
 }
 
+// ------------------------------------------------------------ cosine plan
+bool is_cos(cyc_kmeans_plan p) { return p->measure == CYC_DISTANCE_COSINE; }
+
+// The zero-length assert of CosineDistanceMeasure.distance (DistanceMeasure.
+// scala:453-456): enqueued first, read by cos_check at the end of the call.
+// Every center norm is checked when checkCenters (computeStatistics measures
+// every pair for k >= 2; findClosest measures center 0, and without
+// statistics every center, for each point), every row norm when n > 0.
+int cos_enqueue(cyc_kmeans_plan p, const double* cnorm, bool checkCenters, const double* xnorm,
+                int64_t n, hipStream_t st) {
+  int rc;
+  if ((rc = p->req.reserve(5 * sizeof(unsigned long long)))) return rc;
+  if (!p->reqHost) CYC_HIP(hipHostMalloc((void**)&p->reqHost, 5 * sizeof(unsigned long long)));
+  if (!p->reqEv) CYC_HIP(hipEventCreateWithFlags(&p->reqEv, hipEventDisableTiming));
+  if ((rc = cyc::kmcos::assert_norms(cnorm, p->k, checkCenters, xnorm, n,
+                                     (unsigned long long*)p->req.ptr, st)))
+    return rc;
+  CYC_HIP(hipMemcpyAsync(p->reqHost, p->req.ptr, sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost, st));
+  CYC_HIP(hipEventRecord(p->reqEv, st));
+  return CYC_OK;
+}
+
+int cos_check(cyc_kmeans_plan p) {
+  CYC_HIP(hipEventSynchronize(p->reqEv));
+  if (p->reqHost[0]) {
+    cyc::set_error("assertion failed: Cosine distance is not defined for zero-length vectors.");
+    return CYC_ERR_ASSERTION;
+  }
+  return CYC_OK;
+}
+
+int cos_transpose(cyc_kmeans_plan p, const double* C, hipStream_t st) {
+  const int64_t total = (int64_t)p->d4 * p->kpad;
+  hipLaunchKernelGGL(k_center_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     C, p->k, p->d, p->d4, p->kpad, (double*)p->ct.ptr);
+  CYC_LAUNCH_CHECK("k_center_transpose");
+  return CYC_OK;
+}
+
+int cos_stats(cyc_kmeans_plan p, const double* C, const double* cnorm, hipStream_t st) {
+  return cyc::kmcos::stats(C, cnorm, p->k, p->d, (double*)p->stats.ptr,
+                           (unsigned long long*)p->dmin.ptr, st);
+}
+
+// CosineDistanceMeasure.findClosest for n dense rows: the i8 screen on the
+// unit directions (row image built for cosine), then the reference loop for
+// every row it leaves (every row without an image).
+int cos_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmeans_rows rows,
+               int64_t n, const double* C, const double* cnorm, int32_t* assign, double* cost,
+               int64_t* n_exact_out, hipStream_t st, bool nostats) {
+  int rc;
+  if ((rc = cos_transpose(p, C, st))) return rc;
+  int32_t* list = (int32_t*)p->list3.ptr;
+  unsigned int* count = (unsigned int*)p->list3Count.ptr;
+  const bool screen = rows && rows->usable && p->ktp8 > 0;
+  if (screen) {
+    if ((rc = p->cosV.reserve(sizeof(double) * (size_t)p->k * p->d)) ||
+        (rc = p->cosVn.reserve(sizeof(double) * (size_t)p->k)))
+      return rc;
+    double* V = (double*)p->cosV.ptr;
+    double* Vn = (double*)p->cosVn.ptr;
+    if ((rc = cyc::kmcos::centers_unit(C, cnorm, p->k, p->d, V, Vn, st))) return rc;
+    CYC_HIP(hipMemsetAsync(count, 0, sizeof(unsigned int), st));
+    if ((rc = cyc::km8::centers_prepare(V, Vn, p->k, p->d, p->ktp8, p->cb8.ptr,
+                                        (float*)p->cq8.ptr, (double*)p->g8.ptr,
+                                        (cyc::km8::CenterParams*)p->prm8.ptr,
+                                        (double*)p->scr8.ptr, st)) ||
+        (rc = cyc::km8::screen(rows->img.ptr, (const int2*)rows->meta.ptr,
+                               (const double*)rows->unorm.ptr, n, p->d, p->cb8.ptr,
+                               (const float*)p->cq8.ptr, (const double*)p->g8.ptr, Vn,
+                               (const cyc::km8::CenterParams*)p->prm8.ptr, p->ktp8, assign, list,
+                               count, (int32_t*)p->slowList.ptr,
+                               (unsigned int*)p->list8Count.ptr, st)))
+      return rc;
+  } else if ((rc = cyc::kmcos::list_all(list, count, n, st))) {
+    return rc;
+  }
+  int64_t maxRows = n;
+  if (n_exact_out) {
+    unsigned int h = 0, h3 = 0;
+    const bool twoPass = screen && cyc::km8::uses32(p->d);
+    CYC_HIP(hipMemcpyAsync(&h, count, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    if (twoPass)
+      CYC_HIP(hipMemcpyAsync(&h3, p->list8Count.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    CYC_HIP(hipStreamSynchronize(st));
+    *n_exact_out = h;
+    p->lastTier2 = h;   // no fp64 screen tier: the screen's leftovers are exact
+    p->lastExact = h;
+    p->lastLimb3 = twoPass ? (int64_t)h3 : -1;
+    maxRows = h;
+  }
+  if (maxRows == 0) return CYC_OK;
+  return cyc::kmcos::assign_exact(X, xnorm, p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm,
+                                  p->k, nostats ? nullptr : (const double*)p->stats.ptr, list,
+                                  count, maxRows, assign, cost, st);
+}
+
 }  // namespace
 
 extern "C" {
@@ -2092,17 +2196,40 @@ int cyc_kmeans_plan_destroy(cyc_kmeans_plan plan) {
   return CYC_OK;
 }
 
+int cyc_kmeans_plan_set_distance_measure(cyc_kmeans_plan p, int32_t measure) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  // DistanceMeasure.decodeFromString (DistanceMeasure.scala:241-247)
+  CYC_REQUIRE(measure == CYC_DISTANCE_EUCLIDEAN || measure == CYC_DISTANCE_COSINE,
+              "distanceMeasure must be one of: euclidean, cosine. " + std::to_string(measure) +
+                  " provided.");
+  std::lock_guard<std::mutex> g(p->mu);
+  p->measure = measure;
+  return CYC_OK;
+}
+
 int cyc_kmeans_stats_dev(cyc_kmeans_plan p, const double* C, double* stats_out, void* stream) {
   CYC_REQUIRE(p != nullptr && C != nullptr, "plan and centers must not be null");
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
-  int rc = require_enqueue(p, C, nullptr, 0, st);
-  if (rc) return rc;
-  if ((rc = do_stats(p, C, st))) return rc;
+  int rc;
+  if (is_cos(p)) {
+    // new VectorWithNorm(center): norms computed here (KMeansModel.scala:47-56)
+    if ((rc = p->cosCn.reserve(sizeof(double) * (size_t)p->k))) return rc;
+    const double* cn = (const double*)p->cosCn.ptr;
+    hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((p->k + 63) / 64)), dim3(64), 0, st, C,
+                       (int64_t)p->k, p->d, (double*)p->cosCn.ptr);
+    CYC_LAUNCH_CHECK("k_row_norms");
+    if ((rc = cos_enqueue(p, cn, p->k >= 2, nullptr, 0, st))) return rc;
+    if (p->dense_ok && (rc = cos_transpose(p, C, st))) return rc;
+    if ((rc = cos_stats(p, C, cn, st))) return rc;
+  } else {
+    if ((rc = require_enqueue(p, C, nullptr, 0, st))) return rc;
+    if ((rc = do_stats(p, C, st))) return rc;
+  }
   if (stats_out)
     CYC_HIP(hipMemcpyAsync(stats_out, p->stats.ptr, sizeof(double) * ((size_t)p->k * (p->k + 1) / 2),
                            hipMemcpyDeviceToDevice, st));
-  return require_check(p, 0);
+  return is_cos(p) ? cos_check(p) : require_check(p, 0);
 }
 
 int cyc_kmeans_rows_create(cyc_kmeans_plan p, const double* X, int64_t n, void* stream,
@@ -2115,12 +2242,33 @@ int cyc_kmeans_rows_create(cyc_kmeans_plan p, const double* X, int64_t n, void* 
   r->n = n;
   r->d = p->d;
   r->usable = p->d <= cyc::km8::kMaxD && p->ktp8 > 0;
+  r->cosine = is_cos(p);
   if (r->usable && n > 0) {
     int rc;
+    hipStream_t st = cyc::as_stream(stream);
     if ((rc = r->img.reserve((size_t)n * cyc::km8::image_row_bytes(p->d))) ||
-        (rc = r->meta.reserve(sizeof(int2) * (size_t)n)) ||
-        (rc = cyc::km8::rows_quantize(X, n, p->d, r->img.ptr, (int2*)r->meta.ptr,
-                                      cyc::as_stream(stream)))) {
+        (rc = r->meta.reserve(sizeof(int2) * (size_t)n))) {
+      delete r;
+      return rc;
+    }
+    if (r->cosine) {
+      // the image of x / |x|, and |x / |x|| for the screen's margins
+      cyc::DeviceBuffer xn;
+      if ((rc = r->unorm.reserve(sizeof(double) * (size_t)n)) ||
+          (rc = xn.reserve(sizeof(double) * (size_t)n))) {
+        delete r;
+        return rc;
+      }
+      hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n,
+                         p->d, (double*)xn.ptr);
+      CYC_LAUNCH_CHECK("k_row_norms");
+      rc = cyc::km8::rows_quantize(X, n, p->d, r->img.ptr, (int2*)r->meta.ptr, st,
+                                   (const double*)xn.ptr, (double*)r->unorm.ptr);
+      if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = CYC_ERR_HIP;   // xn freed here
+    } else {
+      rc = cyc::km8::rows_quantize(X, n, p->d, r->img.ptr, (int2*)r->meta.ptr, st);
+    }
+    if (rc) {
       delete r;
       return rc;
     }
@@ -2142,6 +2290,8 @@ namespace {
 int check_rows(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* X, int64_t n) {
   CYC_REQUIRE(rows == nullptr || (rows->X == X && rows->n == n && rows->d == p->d),
               "the row image was built for other rows (cyc_kmeans_rows_create)");
+  CYC_REQUIRE(rows == nullptr || rows->cosine == is_cos(p),
+              "the row image was built for another distance measure");
   return CYC_OK;
 }
 }  // namespace
@@ -2163,6 +2313,13 @@ int cyc_kmeans_assign_dev(cyc_kmeans_plan p, const double* X, const double* xnor
   hipStream_t st = cyc::as_stream(stream);
   int rc = ensure_rows(p, n);
   if (rc) return rc;
+  if (is_cos(p)) {
+    if ((rc = cos_enqueue(p, cnorm, true, xnorm, n, st)) ||
+        (rc = cos_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, n_exact_out, st, false)) ||
+        (rc = cyc::kmcos::row_cost(X, n, p->d, C, cnorm, xnorm, assign, cost, st)))
+      return rc;
+    return cos_check(p);
+  }
   if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
   if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, n_exact_out, st))) return rc;
   hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n, p->d, C,
@@ -2187,6 +2344,17 @@ int cyc_kmeans_point_cost_dev(cyc_kmeans_plan p, const double* X, const double* 
   hipStream_t st = cyc::as_stream(stream);
   int rc = ensure_rows(p, n);
   if (rc) return rc;
+  if (is_cos(p)) {
+    if ((rc = cos_enqueue(p, cnorm, true, xnorm, n, st)) ||
+        (rc = cos_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st, true)) ||
+        (rc = cyc::kmcos::row_cost(X, n, p->d, C, cnorm, xnorm, assign, cost, st)))
+      return rc;
+    // a row no center beats +Infinity for keeps it (:136-148)
+    hipLaunchKernelGGL(k_nostats_cost_fix, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n,
+                       cost);
+    CYC_LAUNCH_CHECK("k_nostats_cost_fix");
+    return cos_check(p);
+  }
   // the fp64 screen reads the transposed centers, which cyc_kmeans_stats_dev
   // would otherwise build: no statistics are needed here
   const int64_t total = (int64_t)p->d4 * p->kpad;
@@ -2226,12 +2394,26 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
     if ((rc = p->assignTmp.reserve(sizeof(int32_t) * (size_t)n))) return rc;
     assign = (int32_t*)p->assignTmp.ptr;
   }
-  if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
-  if ((rc = do_stats(p, C, st))) return rc;
-  if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st))) return rc;
-  // d > 1024: per-row costs first (k_chunk_sums fuses them for d <= 1024)
+  const bool cosm = is_cos(p);
+  if (cosm) {
+    if ((rc = cos_enqueue(p, cnorm, true, xnorm, n, st)) || (rc = cos_stats(p, C, cnorm, st)) ||
+        (rc = cos_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st, false)))
+      return rc;
+  } else {
+    if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
+    if ((rc = do_stats(p, C, st))) return rc;
+    if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st))) return rc;
+  }
+  // d > 1024: per-row costs first (k_chunk_sums fuses them for d <= 1024);
+  // cosine: always (the cost is a ddot, summed per row)
   const int nj = (d + 255) / 256;
-  if (nj > 4) {
+  if (cosm) {
+    if (!cost) {
+      if ((rc = p->costTmp.reserve(sizeof(double) * (size_t)n))) return rc;
+      cost = (double*)p->costTmp.ptr;
+    }
+    if ((rc = cyc::kmcos::row_cost(X, n, d, C, cnorm, xnorm, assign, cost, st))) return rc;
+  } else if (nj > 4) {
     if (!cost) {
       if ((rc = p->costTmp.reserve(sizeof(double) * (size_t)n))) return rc;
       cost = (double*)p->costTmp.ptr;
@@ -2279,7 +2461,14 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   CYC_LAUNCH_CHECK("k_scatter");
   // Number of chunks is data dependent; launch the upper bound and let the
   // surplus blocks (ch >= chunkStart[k]) exit.
-  {
+  if (cosm) {
+    if ((rc = cyc::kmcos::chunk_sums(X, d, weights, xnorm, cost, (const int32_t*)p->perm.ptr,
+                                     (const int64_t*)p->cstart.ptr,
+                                     (const int64_t*)p->chunkStart.ptr, k, maxChunks,
+                                     (double*)p->part.ptr, (double*)p->pw.ptr,
+                                     (double*)p->pc.ptr, st)))
+      return rc;
+  } else {
     cyc::KernelTimer timer("k_chunk_sums", st);
     const dim3 grid((unsigned)maxChunks);
 #define CYC_CS(NJ)                                                                              \
@@ -2314,7 +2503,7 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   hipLaunchKernelGGL(k_cost_total, dim3(1), dim3(256), 0, st, (const double*)p->ccost.ptr, k,
                      cost_sum);
   CYC_LAUNCH_CHECK("k_cost_total");
-  return require_check(p, n);
+  return cosm ? cos_check(p) : require_check(p, n);
 }
 
 int cyc_kmeans_update_dev(cyc_kmeans_plan p, double* C, double* cnorm, const double* sums,
@@ -2325,6 +2514,8 @@ int cyc_kmeans_update_dev(cyc_kmeans_plan p, double* C, double* cnorm, const dou
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
   if (converged_out) CYC_HIP(hipMemsetD32Async((hipDeviceptr_t)converged_out, 1, 1, st));
+  if (is_cos(p))
+    return cyc::kmcos::update(C, cnorm, sums, wsum, p->k, p->d, epsilon, converged_out, st);
   hipLaunchKernelGGL(k_update_centers, dim3((unsigned)p->k), dim3(64),
                      p->d <= kUpdLds ? sizeof(double) * 2 * (size_t)p->d : 0, st, C, cnorm, sums, wsum, p->k, p->d,
                      epsilon * epsilon, converged_out);
@@ -2364,6 +2555,10 @@ int cyc_kmeans_assign_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr, const in
   CYC_REQUIRE(p != nullptr, "plan must not be null");
   CYC_REQUIRE(n >= 0, "n >= 0");
   CYC_REQUIRE(assign != nullptr && cost != nullptr, "assign and cost must not be null");
+  if (is_cos(p)) {
+    cyc::set_error("the cosine distance measure runs on dense rows only");
+    return CYC_ERR_UNSUPPORTED;
+  }
   if (n == 0) return CYC_OK;
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
@@ -2381,6 +2576,10 @@ int cyc_kmeans_point_cost_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
   CYC_REQUIRE(p != nullptr, "plan must not be null");
   CYC_REQUIRE(n >= 0, "n >= 0");
   CYC_REQUIRE(assign != nullptr && cost != nullptr, "assign and cost must not be null");
+  if (is_cos(p)) {
+    cyc::set_error("the cosine distance measure runs on dense rows only");
+    return CYC_ERR_UNSUPPORTED;
+  }
   if (n == 0) return CYC_OK;
   std::lock_guard<std::mutex> g(p->mu);
   return sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost,
@@ -2395,6 +2594,10 @@ int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
   CYC_REQUIRE(p != nullptr, "plan must not be null");
   CYC_REQUIRE(n >= 0, "n >= 0");
   CYC_REQUIRE(sums && wsum && cost_sum, "sums, wsum and cost_sum must not be null");
+  if (is_cos(p)) {
+    cyc::set_error("the cosine distance measure runs on dense rows only");
+    return CYC_ERR_UNSUPPORTED;
+  }
   if (n == 0) return CYC_OK;
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);

@@ -115,30 +115,42 @@ __device__ __forceinline__ double err_term(int e, double n1, double mu, int d) {
 }
 
 // One wave per row: limbs into the image, exponent and |xh|_1 bound into meta.
+// scale (optional): the row is x / scale[row] (the cosine plan's unit
+// directions), whose norm goes to unorm[row] (any summation order: it only
+// enters the certification margins, like the fp64 norms do).
 __global__ __launch_bounds__(256) void k_rows_quantize(const double* __restrict__ X, int64_t n,
                                                        int d, int D, unsigned* __restrict__ img,
-                                                       int2* __restrict__ meta) {
+                                                       int2* __restrict__ meta,
+                                                       const double* __restrict__ scale,
+                                                       double* __restrict__ unorm) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < n; row += nw) {
     const double* x = X + row * d;
     double v[8];
-    double m = 0.0, s1 = 0.0;
+    double m = 0.0, s1 = 0.0, s2 = 0.0;
     bool fin = true;
+    const double sc = scale ? scale[row] : 1.0;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = p * 256 + 4 * lane + q;
-        const double t = j < d ? x[j] : 0.0;
+        double t = j < d ? x[j] : 0.0;
+        if (scale) t = t / sc;
         v[4 * p + q] = t;
         fin = fin && __builtin_isfinite(t);
         m = __builtin_fmax(m, __builtin_fabs(t));
         s1 += __builtin_fabs(t);
+        s2 += t * t;
       }
     }
     m = wave_max(m);
     s1 = wave_sum(s1);
+    if (unorm) {
+      s2 = wave_sum(s2);
+      if (lane == 0) unorm[row] = __builtin_sqrt(s2);
+    }
     const bool allFin = __all(fin);
     const int e = choose_exp(m);
     const bool bad = !allFin || e > kMaxExp;
@@ -971,12 +983,13 @@ int launch_screen(const void* img, const int2* meta, const double* xnorm, int64_
 
 }  // namespace
 
-int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipStream_t st) {
+int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipStream_t st,
+                  const double* scale, double* unorm) {
   if (n <= 0) return CYC_OK;
   const int D = 64 * ksteps(d);
   const int64_t blocks = std::min<int64_t>((n + 3) / 4, 65536);
   hipLaunchKernelGGL(k_rows_quantize, dim3((unsigned)blocks), dim3(256), 0, st, X, n, d, D,
-                     (unsigned*)img, meta);
+                     (unsigned*)img, meta, scale, unorm);
   CYC_LAUNCH_CHECK("k_rows_quantize");
   return CYC_OK;
 }

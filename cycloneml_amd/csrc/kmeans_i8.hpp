@@ -39,7 +39,10 @@ inline int64_t image_row_bytes(int d) { return 3 * 64 * (int64_t)ksteps(d); }
 // X (n x d, row-major fp64) -> img (n rows of image_row_bytes) and meta
 // (per row: int exponent or INT32_MIN when the row cannot be screened, and
 // the float bits of an upper bound of the 1-norm of the quantized row).
-int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipStream_t st);
+// scale (optional, n entries): image the rows x / scale[row] instead, and
+// write their norms to unorm (the cosine plan's unit directions).
+int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipStream_t st,
+                  const double* scale = nullptr, double* unorm = nullptr);
 
 // Centers -> packed B fragments (Cb), per-center lower-bound constants cq
 // (float, +inf for padding), error terms g (fp64) and the launch's params.

@@ -227,9 +227,8 @@ def load_kmeans_model(path):
         raise ValueError(f"expected {meta['k']} centers, found {len(rows)}")
     rows.sort(key=lambda r: r["id"])
     C = np.stack([decode_vector(r["point"]) for r in rows])
-    m = KMeansModel(C, trainingCost=float(meta.get("trainingCost", 0.0)), numIter=-1)
-    m.distanceMeasure = meta.get("distanceMeasure", "euclidean")
-    return m
+    return KMeansModel(C, trainingCost=float(meta.get("trainingCost", 0.0)), numIter=-1,
+                       distanceMeasure=meta.get("distanceMeasure", "euclidean"))
 
 
 # -- ml LogisticRegressionModel -----------------------------------------------

@@ -40,6 +40,7 @@ extern "C" {
 #define CYC_ERR_ALLOC 3       /* device allocation failed                   */
 #define CYC_ERR_UNSUPPORTED 4 /* shape outside what the kernels support     */
 #define CYC_ERR_NO_DEVICE 5   /* no usable gfx950 device                    */
+#define CYC_ERR_ASSERTION 6   /* a reference `assert` failed (AssertionError) */
 
 /* ------------------------------------------------------------------ misc */
 const char* cyc_last_error(void);
@@ -76,8 +77,26 @@ typedef struct cyc_kmeans_plan_s* cyc_kmeans_plan;
 int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_plan* plan);
 int cyc_kmeans_plan_destroy(cyc_kmeans_plan plan);
 
+/* The plan's DistanceMeasure (DistanceMeasure.decodeFromString,
+ * DistanceMeasure.scala:241-247): CYC_DISTANCE_EUCLIDEAN (the default) or
+ * CYC_DISTANCE_COSINE (CosineDistanceMeasure, :395-514).  Set it before any
+ * other call on the plan; a row image (cyc_kmeans_rows_create) is built for
+ * the plan's measure.  With COSINE every call below uses the cosine forms:
+ * distance 1 - dot(c, x) / |c| / |x| (:453-456), the statistic
+ * 1 - sqrt(1 - d / 2) (:412-417), updateClusterSum axpy(w / |x|, x, sum)
+ * (:466-469), the unit-norm centroid whose norm is set to 1.0 (:477-483) and
+ * isCenterConverged distance <= epsilon (:161-166); a zero-length (or NaN)
+ * norm returns CYC_ERR_ASSERTION with the reference's assert text.  The CSR
+ * entry points support only EUCLIDEAN (CYC_ERR_UNSUPPORTED). */
+#define CYC_DISTANCE_EUCLIDEAN 0
+#define CYC_DISTANCE_COSINE 1
+int cyc_kmeans_plan_set_distance_measure(cyc_kmeans_plan plan, int32_t measure);
+
 /* computeStatistics for the given centers: fills the plan's packed k(k+1)/2
- * statistics (and copies them to stats_out if non-NULL, device memory). */
+ * statistics (and copies them to stats_out if non-NULL, device memory).
+ * With COSINE the centers' norms are computed here (new VectorWithNorm(c),
+ * as KMeansModel's lazy statistics do); cyc_kmeans_accumulate_dev uses the
+ * cnorm it is given. */
 int cyc_kmeans_stats_dev(cyc_kmeans_plan plan, const double* C, double* stats_out, void* stream);
 
 /* Per-fit row image (KMeans.scala:263-270 caches the rows with their norms

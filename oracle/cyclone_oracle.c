@@ -348,6 +348,160 @@ int orc_kmeans_update_centers(double* C, double* cnorm, const double* sums, cons
 }
 
 /* ------------------------------------------------------------------------ */
+/* KMeans, CosineDistanceMeasure (DistanceMeasure.scala:395-514)            */
+/* ------------------------------------------------------------------------ */
+
+/* mllib/linalg/BLAS.scala:145-148 dot(dense, dense) = ddot: netlib's loop,
+ * dtemp + dx(i)*dy(i) in index order (the unrolled groups add left to right) */
+double orc_ddot(const double* x, const double* y, int64_t n) {
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) s += x[i] * y[i];
+  return s;
+}
+
+/* assert(v1.norm > 0 && v2.norm > 0, "Cosine distance is not defined for
+ * zero-length vectors.") (:454, and :467 for updateClusterSum): an
+ * AssertionError ends the Spark task; recorded like the require above. */
+static _Thread_local int g_assert_failed = 0;
+
+static int orc_cos_assert(double n1, double n2) {
+  if (n1 > 0 && n2 > 0) return 1;
+  g_assert_failed = 1;
+  return 0;
+}
+
+/* 1 if the cosine assert failed since the last call; clears it */
+int orc_take_assert_failure(void) {
+  int f = g_assert_failed;
+  g_assert_failed = 0;
+  return f;
+}
+
+/* :453-456 distance(v1, v2) = 1 - dot(v1.vector, v2.vector) / v1.norm / v2.norm */
+static double orc_cos_distance(const double* v1, double n1, const double* v2, double n2,
+                               int64_t d) {
+  return 1.0 - orc_ddot(v1, v2, d) / n1 / n2;
+}
+
+/* computeStatistics (:48-76) with the cosine statistic (:412-417):
+ * s = 1 - sqrt(1 - distance / 2).  cnorm: the centers' VectorWithNorm norms. */
+void orc_cos_stats(const double* C, const double* cnorm, int64_t k, int64_t d, double* packed) {
+  if (k == 1) { packed[0] = NAN; return; }
+  double* diag = (double*)malloc(sizeof(double) * k);
+  for (int64_t i = 0; i < k; ++i) diag[i] = INFINITY;
+  for (int64_t i = 0; i < k; ++i) {
+    for (int64_t j = i + 1; j < k; ++j) {
+      if (!orc_cos_assert(cnorm[i], cnorm[j])) { free(diag); return; }
+      double dist = orc_cos_distance(C + i * d, cnorm[i], C + j * d, cnorm[j], d);
+      double s = 1.0 - sqrt(1.0 - dist / 2.0);
+      packed[orc_iut(i, j)] = s;
+      if (s < diag[i]) diag[i] = s;
+      if (s < diag[j]) diag[j] = s;
+    }
+  }
+  for (int64_t i = 0; i < k; ++i) packed[orc_iut(i, i)] = diag[i];
+  free(diag);
+}
+
+/* CosineDistanceMeasure.findClosest with statistics (:421-447) */
+void orc_cos_find_closest_stats(const double* C, const double* cnorm, int64_t k, int64_t d,
+                                const double* stats, const double* x, double xnorm,
+                                int32_t* out_idx, double* out_dist) {
+  *out_idx = -1;
+  *out_dist = NAN;
+  if (!orc_cos_assert(cnorm[0], xnorm)) return;
+  double best = orc_cos_distance(C, cnorm[0], x, xnorm, d);
+  if (best < stats[0]) { *out_idx = 0; *out_dist = best; return; }
+  int64_t bestIndex = 0;
+  for (int64_t i = 1; i < k; ++i) {
+    if (stats[orc_iut(i, bestIndex)] < best) {
+      if (!orc_cos_assert(cnorm[i], xnorm)) return;
+      double dd = orc_cos_distance(C + i * d, cnorm[i], x, xnorm, d);
+      if (dd < stats[orc_iut(i, i)]) { *out_idx = (int32_t)i; *out_dist = dd; return; }
+      if (dd < best) { best = dd; bestIndex = i; }
+    }
+  }
+  *out_idx = (int32_t)bestIndex;
+  *out_dist = best;
+}
+
+/* findClosest without statistics (:131-150), the cosine distance */
+void orc_cos_find_closest(const double* C, const double* cnorm, int64_t k, int64_t d,
+                          const double* x, double xnorm, int32_t* out_idx, double* out_dist) {
+  double best = INFINITY;
+  int64_t bestIndex = 0;
+  for (int64_t i = 0; i < k; ++i) {
+    if (!orc_cos_assert(cnorm[i], xnorm)) { *out_idx = -1; *out_dist = NAN; return; }
+    double dd = orc_cos_distance(C + i * d, cnorm[i], x, xnorm, d);
+    if (dd < best) { best = dd; bestIndex = i; }
+  }
+  *out_idx = (int32_t)bestIndex;
+  *out_dist = best;
+}
+
+/* pointCost (:152-156) for every row plus the partition's sum fold. */
+double orc_cos_point_costs(const double* X, const double* xnorm, int64_t n, int64_t d,
+                           const double* C, const double* cnorm, int64_t k, int32_t* assign,
+                           double* cost) {
+  double sum = 0.0;
+  for (int64_t r = 0; r < n; ++r) {
+    orc_cos_find_closest(C, cnorm, k, d, X + r * d, xnorm[r], assign + r, cost + r);
+    if (assign[r] < 0) break;
+    sum += cost[r];
+  }
+  return sum;
+}
+
+/* One partition of the Lloyd body (KMeans.scala:287-306) with the cosine
+ * updateClusterSum (:466-469): axpy(point.weight / point.norm, x, sum). */
+void orc_cos_kmeans_partition(const double* X, const double* xnorm, const double* w, int64_t n,
+                              int64_t d, const double* C, const double* cnorm,
+                              const double* stats, int64_t k, int32_t* assign, double* dist,
+                              double* sums, double* wsum, double* cost) {
+  double c = *cost;
+  for (int64_t r = 0; r < n; ++r) {
+    int32_t bi; double bd;
+    orc_cos_find_closest_stats(C, cnorm, k, d, stats, X + r * d, xnorm[r], &bi, &bd);
+    if (bi < 0) break;                     /* assert failed: the task throws */
+    double wt = w ? w[r] : 1.0;
+    if (assign) assign[r] = bi;
+    if (dist) dist[r] = bd;
+    c += bd * wt;
+    double a = wt / xnorm[r];
+    if (a != 0.0) {                        /* netlib daxpy: da == 0 returns */
+      double* s = sums + (int64_t)bi * d;
+      const double* x = X + r * d;
+      for (int64_t j = 0; j < d; ++j) s[j] = s[j] + a * x[j];
+    }
+    wsum[bi] += wt;
+  }
+  *cost = c;
+}
+
+/* centroid (:477-483): scal(1/weightSum, sum), norm, scal(1/norm, sum),
+ * new VectorWithNorm(sum, 1); isCenterConverged (:161-166): distance(old,
+ * new) <= epsilon.  Returns 1 if every updated center converged. */
+int orc_cos_update_centers(double* C, double* cnorm, const double* sums, const double* wsum,
+                           int64_t k, int64_t d, double epsilon) {
+  int converged = 1;
+  double* nc = (double*)malloc(sizeof(double) * d);
+  for (int64_t j = 0; j < k; ++j) {
+    if (!(wsum[j] > 0)) continue;
+    double a = 1.0 / wsum[j];
+    for (int64_t t = 0; t < d; ++t) nc[t] = a * sums[j * d + t];
+    double norm = orc_norm2(nc, d);
+    double b = 1.0 / norm;
+    for (int64_t t = 0; t < d; ++t) nc[t] = b * nc[t];
+    if (converged && !(orc_cos_distance(C + j * d, cnorm[j], nc, 1.0, d) <= epsilon))
+      converged = 0;
+    memcpy(C + j * d, nc, sizeof(double) * d);
+    cnorm[j] = 1.0;
+  }
+  free(nc);
+  return converged;
+}
+
+/* ------------------------------------------------------------------------ */
 /* ml.impl.Utils                                                            */
 /* ------------------------------------------------------------------------ */
 

@@ -62,6 +62,19 @@ def lib():
                 "orc_axpy": (None, [_i64, ctypes.c_double, _D, _D]),
                 "orc_kmeans_update_centers": (ctypes.c_int, [_D, _D, _D, _D, _i64, _i64,
                                                              ctypes.c_double]),
+                "orc_ddot": (ctypes.c_double, [_D, _D, _i64]),
+                "orc_take_assert_failure": (ctypes.c_int, []),
+                "orc_cos_stats": (None, [_D, _D, _i64, _i64, _D]),
+                "orc_cos_find_closest_stats": (None, [_D, _D, _i64, _i64, _D, _D,
+                                                      ctypes.c_double, _I32, _D]),
+                "orc_cos_find_closest": (None, [_D, _D, _i64, _i64, _D, ctypes.c_double, _I32,
+                                                _D]),
+                "orc_cos_point_costs": (ctypes.c_double, [_D, _D, _i64, _i64, _D, _D, _i64,
+                                                          _I32, _D]),
+                "orc_cos_kmeans_partition": (None, [_D, _D, _D, _i64, _i64, _D, _D, _D, _i64,
+                                                    _I32, _D, _D, _D, _D]),
+                "orc_cos_update_centers": (ctypes.c_int, [_D, _D, _D, _D, _i64, _i64,
+                                                          ctypes.c_double]),
                 "orc_log1pexp": (ctypes.c_double, [ctypes.c_double]),
                 "orc_softmax": (None, [_D, _i64, _i64, _i64]),
                 "orc_hinge_add_dense": (None, [_i64, _i64, _D, _D, _D, _D, ctypes.c_int, _D, _D,
@@ -358,6 +371,100 @@ def update_centers(C, cnorm, sums, wsum, epsilon=1e-4) -> bool:
     k, d = C.shape
     return bool(lib().orc_kmeans_update_centers(_p(C), _p(cnorm), _p(sums), _p(wsum), k, d,
                                                 float(epsilon)))
+
+
+# --------------------------------------------------------------------------
+# KMeans with CosineDistanceMeasure (DistanceMeasure.scala:395-514)
+# --------------------------------------------------------------------------
+
+class JavaAssertionError(AssertionError):
+    """A Scala `assert` failed (java.lang.AssertionError)."""
+
+
+COSINE_ASSERT = "assertion failed: Cosine distance is not defined for zero-length vectors."
+
+
+def _raise_assert():
+    if lib().orc_take_assert_failure():
+        raise JavaAssertionError(COSINE_ASSERT)
+
+
+def cos_stats(C, cnorm) -> np.ndarray:
+    """computeStatistics with the cosine statistic (:48-76, :412-417)."""
+    C, cnorm = _f64(C), _f64(cnorm)
+    k, d = C.shape
+    out = np.empty(k * (k + 1) // 2)
+    lib().orc_cos_stats(_p(C), _p(cnorm), k, d, _p(out))
+    _raise_assert()
+    return out
+
+
+def cos_find_closest_stats(C, cnorm, stats, x, xnorm):
+    C, cnorm, stats, x = _f64(C), _f64(cnorm), _f64(stats), _f64(x)
+    i, dd = ctypes.c_int32(), ctypes.c_double()
+    lib().orc_cos_find_closest_stats(_p(C), _p(cnorm), C.shape[0], C.shape[1], _p(stats), _p(x),
+                                     float(xnorm), ctypes.byref(i), ctypes.byref(dd))
+    _raise_assert()
+    return i.value, dd.value
+
+
+def cos_find_closest(C, cnorm, x, xnorm):
+    C, cnorm, x = _f64(C), _f64(cnorm), _f64(x)
+    i, dd = ctypes.c_int32(), ctypes.c_double()
+    lib().orc_cos_find_closest(_p(C), _p(cnorm), C.shape[0], C.shape[1], _p(x), float(xnorm),
+                               ctypes.byref(i), ctypes.byref(dd))
+    _raise_assert()
+    return i.value, dd.value
+
+
+def cos_point_costs(X, xnorm, C, cnorm):
+    """pointCost with the cosine distance for every row; (assign, cost, sum)."""
+    X, xnorm, C, cnorm = _f64(X), _f64(xnorm), _f64(C), _f64(cnorm)
+    n, d = X.shape
+    a = np.empty(n, dtype=np.int32)
+    c = np.empty(n)
+    s = lib().orc_cos_point_costs(_p(X), _p(xnorm), n, d, _p(C), _p(cnorm), C.shape[0],
+                                  _p(a, _I32), _p(c))
+    _raise_assert()
+    return a, c, s
+
+
+def cos_kmeans_partition(X, xnorm, w, C, cnorm, stats):
+    X, xnorm, C, cnorm, stats = _f64(X), _f64(xnorm), _f64(C), _f64(cnorm), _f64(stats)
+    n, d = X.shape
+    k = C.shape[0]
+    a = np.full(n, -1, dtype=np.int32)
+    dist = np.full(n, np.nan)
+    sums = np.zeros(k * d)
+    wsum = np.zeros(k)
+    cost = np.zeros(1)
+    lib().orc_cos_kmeans_partition(_p(X), _p(xnorm), _p(None if w is None else _f64(w)), n, d,
+                                   _p(C), _p(cnorm), _p(stats), k, _p(a, _I32), _p(dist),
+                                   _p(sums), _p(wsum), _p(cost))
+    _raise_assert()
+    return a, dist, sums.reshape(k, d), wsum, cost[0]
+
+
+def cos_update_centers(C, cnorm, sums, wsum, epsilon=1e-4) -> bool:
+    """centroid + isCenterConverged of the cosine measure, in place."""
+    assert C.flags.c_contiguous and cnorm.flags.c_contiguous
+    sums, wsum = _f64(sums), _f64(wsum)
+    k, d = C.shape
+    return bool(lib().orc_cos_update_centers(_p(C), _p(cnorm), _p(sums), _p(wsum), k, d,
+                                             float(epsilon)))
+
+
+def cos_kmeans_iteration(X, xnorm, w, C, cnorm, epsilon=1e-4):
+    """One cosine Lloyd iteration over a single partition (KMeans.scala:
+    275-334): dict(assign, dist, sums, wsum, cost, centers, cnorm,
+    converged, stats)."""
+    C, cnorm = _f64(C), _f64(cnorm)
+    stats = cos_stats(C, cnorm)
+    a, dist, sums, wsum, cost = cos_kmeans_partition(X, xnorm, w, C, cnorm, stats)
+    C2, cn2 = C.copy(), cnorm.copy()
+    conv = cos_update_centers(C2, cn2, sums, wsum, epsilon)
+    return dict(assign=a, dist=dist, sums=sums, wsum=wsum, cost=cost, centers=C2, cnorm=cn2,
+                converged=conv, stats=stats)
 
 
 # --------------------------------------------------------------------------

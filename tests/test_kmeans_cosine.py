@@ -1,0 +1,347 @@
+"""KMeans with CosineDistanceMeasure (mllib/clustering/DistanceMeasure.scala:
+395-514): the oracle restatement on CPU, and the device plan (i8 screen on unit
+directions + the reference loop) against it on the GPU.
+
+Bar: assignments and per-point costs bit-exact; cluster sums, weights, cost
+sum and updated centers within 1e-10 relative (the sums are folded in another
+order than a Spark partition's).
+
+Parity pins: DistanceMeasureSuite "predict with statistics" (cosine,
+java.util.Random(42), k=10, dim=8), ml KMeansSuite "KMeans using cosine
+distance" / "... not supported for 0-length vectors" assertions.  The suite's
+RANDOM initialisation (takeSample over Spark partitions) is not restated: the
+Lloyd runs below start from given centers (parity of the init: unpinned).
+"""
+import numpy as np
+import pytest
+
+import oracle
+
+SUITE_POINTS = np.array([[1.0, 1.0], [10.0, 10.0], [1.0, 0.5], [10.0, 4.4], [-1.0, 1.0],
+                         [-100.0, 90.0]])
+
+
+def _suite_data():
+    rng = oracle.JavaRandom(42)
+    C = np.array([[rng.next_gaussian() for _ in range(8)] for _ in range(10)])
+    X = np.array([[rng.next_gaussian() for _ in range(8)] for _ in range(1000)])
+    return C, X
+
+
+# ------------------------------------------------------------------ CPU
+
+def test_oracle_predict_with_statistics_cosine():
+    """DistanceMeasureSuite.scala:53-64 for COSINE: findClosest with and
+    without statistics return the same index, costs within relTol 1e-10."""
+    C, X = _suite_data()
+    cn = oracle.row_norms(C)
+    stats = oracle.cos_stats(C, cn)
+    for x in X:
+        xn = oracle.norm2(x)
+        i1, c1 = oracle.cos_find_closest(C, cn, x, xn)
+        i2, c2 = oracle.cos_find_closest_stats(C, cn, stats, x, xn)
+        assert i1 == i2
+        assert abs(c1 - c2) <= 1e-10 * max(abs(c1), abs(c2))
+
+
+def test_oracle_statistic_definition():
+    """computeStatistics(distance) = 1 - sqrt(1 - distance / 2) (:412-417)
+    on the pair distance 1 - dot / |ci| / |cj| (:453-456); diag = row min."""
+    C, _ = _suite_data()
+    cn = oracle.row_norms(C)
+    st = oracle.cos_stats(C, cn)
+    k = C.shape[0]
+    iut = lambda i, j: j * (j + 1) // 2 + i if i <= j else i * (i + 1) // 2 + j  # noqa: E731
+    for i in range(k):
+        row = []
+        for j in range(k):
+            if i == j:
+                continue
+            dist = 1.0 - oracle.lib().orc_ddot(oracle._p(np.ascontiguousarray(C[min(i, j)])),
+                                               oracle._p(np.ascontiguousarray(C[max(i, j)])),
+                                               8) / cn[min(i, j)] / cn[max(i, j)]
+            s = 1.0 - np.sqrt(1.0 - dist / 2.0)
+            assert st[iut(i, j)] == s
+            row.append(s)
+        assert st[iut(i, i)] == min(row)
+
+
+def test_oracle_suite_cosine_lloyd():
+    """ml KMeansSuite "KMeans using cosine distance" (KMeansSuite.scala:160-190)
+    assertions on a Lloyd run from three of the points: the three direction
+    groups are separated and every center has unit norm."""
+    X = SUITE_POINTS
+    xn = oracle.row_norms(X)
+    C = X[[0, 2, 4]].copy()
+    cn = oracle.row_norms(C)
+    for _ in range(20):
+        r = oracle.cos_kmeans_iteration(X, xn, None, C, cn, epsilon=1e-6)
+        C, cn = r["centers"], r["cnorm"]
+        if r["converged"]:
+            break
+    a = r["assign"]
+    assert len(set(a.tolist())) == 3
+    assert a[0] == a[1] and a[2] == a[3] and a[4] == a[5]
+    np.testing.assert_allclose(np.linalg.norm(C, axis=1), 1.0, rtol=1e-15)
+    assert np.all(cn == 1.0)
+
+
+def test_oracle_zero_length_asserts():
+    """KMeansSuite.scala:192-202: a zero vector raises AssertionError
+    "Cosine distance is not defined ..." (from distance, :454)."""
+    X = np.array([[0.0, 0.0], [10.0, 10.0], [1.0, 0.5]])
+    C = X[[1, 2]].copy()
+    with pytest.raises(AssertionError, match="Cosine distance is not defined"):
+        oracle.cos_kmeans_iteration(X, oracle.row_norms(X), None, C, oracle.row_norms(C))
+
+
+def test_unknown_measure_fails_at_decode():
+    """setDistanceMeasure keeps any name (KMeans.scala:184-188); the run's
+    DistanceMeasure.decodeFromString raises (DistanceMeasure.scala:241-247)."""
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.clustering import KMeans, KMeansPlan
+    km = KMeans(k=2).setDistanceMeasure("manhattan")
+    assert km.distanceMeasure == "manhattan"
+    with pytest.raises(N.IllegalArgumentException,
+                       match="distanceMeasure must be one of: euclidean, cosine. manhattan"):
+        KMeansPlan(4, 2, 1, "manhattan")
+
+
+# ------------------------------------------------------------------ GPU
+
+def _dev(a, cuda):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+
+
+def _gpu(X, C, cuda, mode="assign", image=True, w=None):
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    n, d = X.shape
+    k = C.shape[0]
+    Xd, Cd = _dev(X, cuda), _dev(C, cuda)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = KMeansPlan(d, k, n, "cosine")
+    rows = p.rows(Xd) if image else None
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    c = torch.empty(n, dtype=torch.float64, device=cuda)
+    out = {}
+    if mode == "assign":
+        st = torch.empty(k * (k + 1) // 2, dtype=torch.float64, device=cuda)
+        p.stats(Cd, st)
+        out["n_exact"] = p.assign(Xd, xn, Cd, cn, a, c, count_exact=True, rows=rows)
+        out["stats"] = st.cpu().numpy()
+    elif mode == "point_cost":
+        p.point_cost(Xd, xn, Cd, cn, a, c, rows=rows)
+    else:
+        buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=cuda)
+        sums, wsum, cost = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
+        wd = None if w is None else _dev(w, cuda)
+        p.accumulate(Xd, xn, wd, Cd, cn, sums, wsum, cost, a, c, rows=rows)
+        conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+        p.update(Cd, cn, sums, wsum, 1e-4, conv)
+        torch.cuda.synchronize()
+        out.update(sums=sums.cpu().numpy().reshape(k, d), wsum=wsum.cpu().numpy(),
+                   cost=float(cost.item()), centers=Cd.cpu().numpy(), cnorm=cn.cpu().numpy(),
+                   converged=bool(conv.item()))
+    torch.cuda.synchronize()
+    out["assign"], out["cost_rows"] = a.cpu().numpy(), c.cpu().numpy()
+    out["tiers"] = p.last_tiers()
+    out["limb3"] = p.last_screen()
+    if rows is not None:
+        rows.close()
+    p.close()
+    return out
+
+
+def _clustered(rng, n, d, k, spread=0.15, signs=True):
+    dirs = rng.normal(size=(k, d))
+    lab = rng.integers(0, k, n)
+    scale = rng.uniform(0.5, 20.0, size=(n, 1))
+    X = (dirs[lab] + spread * rng.normal(size=(n, d))) * scale
+    if signs:
+        X[rng.random(n) < 0.1] *= -1.0
+    return X
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,d,k", [(3000, 8, 10), (5000, 33, 17), (20000, 64, 100),
+                                   (20000, 256, 256), (6000, 300, 64), (4000, 512, 40),
+                                   (2000, 700, 24)])
+@pytest.mark.parametrize("image", [True, False])
+def test_cos_assign_vs_oracle(cuda, n, d, k, image):
+    """findClosest with statistics: index and cost bit-exact for every row;
+    the statistics bit-exact too."""
+    rng = np.random.default_rng(n + d + k)
+    X = _clustered(rng, n, d, k)
+    C = X[rng.choice(n, size=k, replace=False)].copy()
+    g = _gpu(X, C, cuda, "assign", image)
+    cn = oracle.row_norms(C)
+    stats = oracle.cos_stats(C, cn)
+    np.testing.assert_array_equal(g["stats"], stats)
+    ra, rd, *_ = oracle.cos_kmeans_partition(X, oracle.row_norms(X), None, C, cn, stats)
+    np.testing.assert_array_equal(g["assign"], ra)
+    np.testing.assert_array_equal(g["cost_rows"], rd)
+    if image and d <= 512:
+        assert g["n_exact"] < n // 5        # the screen certified most rows
+    else:
+        assert g["n_exact"] == n
+
+
+@pytest.mark.gpu
+def test_cos_distance_measure_suite(cuda):
+    """DistanceMeasureSuite data: the device equals the restatement with and
+    without statistics (which agree with each other, the suite's assertion)."""
+    C, X = _suite_data()
+    g = _gpu(X, C, cuda, "assign")
+    cn, xn = oracle.row_norms(C), oracle.row_norms(X)
+    ra, rd, *_ = oracle.cos_kmeans_partition(X, xn, None, C, cn, oracle.cos_stats(C, cn))
+    np.testing.assert_array_equal(g["assign"], ra)
+    np.testing.assert_array_equal(g["cost_rows"], rd)
+    g2 = _gpu(X, C, cuda, "point_cost")
+    pa, pc, _ = oracle.cos_point_costs(X, xn, C, cn)
+    np.testing.assert_array_equal(g2["assign"], pa)
+    np.testing.assert_array_equal(g2["cost_rows"], pc)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("image", [True, False])
+def test_cos_point_cost_vs_oracle(cuda, image):
+    rng = np.random.default_rng(11)
+    X = _clustered(rng, 8000, 48, 30)
+    C = rng.normal(size=(30, 48))
+    g = _gpu(X, C, cuda, "point_cost", image)
+    pa, pc, _ = oracle.cos_point_costs(X, oracle.row_norms(X), C, oracle.row_norms(C))
+    np.testing.assert_array_equal(g["assign"], pa)
+    np.testing.assert_array_equal(g["cost_rows"], pc)
+
+
+@pytest.mark.gpu
+def test_cos_ties_duplicates_antipodes(cuda):
+    """Duplicate centers, scaled copies of a center (cosine distance 0, which
+    rounds to +-2^-53), antipodal centers and points on bisectors: the
+    screen leaves these to the reference loop; results stay bit-exact."""
+    rng = np.random.default_rng(5)
+    d = 32
+    base = rng.normal(size=(6, d))
+    C = np.vstack([base, base[:2] * 3.0, -base[2:4], base[4:5]])
+    mid = C[0] / np.linalg.norm(C[0]) + C[1] / np.linalg.norm(C[1])
+    X = np.vstack([rng.normal(size=(600, d)), np.repeat(mid[None], 40, 0) * 7.0, C * 2.5,
+                   -C, C[:4] + 1e-13])
+    for mode in ("assign", "point_cost"):
+        g = _gpu(X, C, cuda, mode)
+        cn, xn = oracle.row_norms(C), oracle.row_norms(X)
+        if mode == "assign":
+            ra, rd, *_ = oracle.cos_kmeans_partition(X, xn, None, C, cn, oracle.cos_stats(C, cn))
+            assert g["n_exact"] > 0
+        else:
+            ra, rd, _ = oracle.cos_point_costs(X, xn, C, cn)
+        np.testing.assert_array_equal(g["assign"], ra)
+        np.testing.assert_array_equal(g["cost_rows"], rd)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("n,d,k", [(20000, 64, 50), (30000, 256, 128), (5000, 600, 20)])
+def test_cos_lloyd_iteration_vs_oracle(cuda, n, d, k, weighted):
+    """accumulate + update: assignment / costs bit-exact, sums, weights, cost
+    and the new unit centers within 1e-10; cnorm = 1.0 after the update."""
+    rng = np.random.default_rng(100 + n + k)
+    X = _clustered(rng, n, d, k)
+    C = X[rng.choice(n, size=k, replace=False)].copy()
+    w = rng.uniform(0.1, 3.0, n) if weighted else None
+    g = _gpu(X, C, cuda, "lloyd", True, w)
+    xn, cn = oracle.row_norms(X), oracle.row_norms(C)
+    r = oracle.cos_kmeans_iteration(X, xn, w, C, cn)
+    np.testing.assert_array_equal(g["assign"], r["assign"])
+    np.testing.assert_array_equal(g["cost_rows"], r["dist"])
+    np.testing.assert_allclose(g["sums"], r["sums"], rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(g["wsum"], r["wsum"], rtol=1e-12)
+    np.testing.assert_allclose(g["cost"], r["cost"], rtol=1e-10)
+    np.testing.assert_allclose(g["centers"], r["centers"], rtol=1e-10, atol=1e-12)
+    assert np.all(g["cnorm"][r["wsum"] > 0] == 1.0)
+    assert g["converged"] == r["converged"]
+
+
+@pytest.mark.gpu
+def test_cos_zero_length_asserts(cuda):
+    """KMeansSuite.scala:192-202 on the device: AssertionError with the
+    reference text for a zero row, and for a zero center (statistics)."""
+    from cycloneml_amd import _native as N
+    X = np.array([[0.0, 0.0], [10.0, 10.0], [1.0, 0.5]])
+    with pytest.raises(N.JavaAssertionError,
+                       match="assertion failed: Cosine distance is not defined for zero-length"):
+        _gpu(X, X[[1, 2]].copy(), cuda, "lloyd")
+    X2 = np.array([[1.0, 0.0], [10.0, 10.0], [1.0, 0.5]])
+    with pytest.raises(N.JavaAssertionError, match="Cosine distance is not defined"):
+        _gpu(X2, np.array([[0.0, 0.0], [1.0, 1.0]]), cuda, "assign")
+
+
+@pytest.mark.gpu
+def test_cos_kmeans_run_suite_points(cuda):
+    """KMeans(distanceMeasure=cosine).run on the KMeansSuite points from three
+    of them: the suite's grouping assertions, unit-norm centers, the model's
+    predict, and the whole run equal to the restated Lloyd loop."""
+    from cycloneml_amd.clustering import KMeans, KMeansModel
+    X = SUITE_POINTS
+    init = KMeansModel(X[[0, 2, 4]].copy(), distanceMeasure="cosine")
+    km = KMeans(k=3, maxIterations=20, epsilon=1e-6).setDistanceMeasure("cosine")
+    km.setInitialModel(init)
+    m = km.run(_dev(X, cuda))
+    assert m.distanceMeasure == "cosine"
+    p = m.predict(_dev(X, cuda)).cpu().numpy()
+    assert len(set(p.tolist())) == 3
+    assert p[0] == p[1] and p[2] == p[3] and p[4] == p[5]
+    np.testing.assert_allclose(np.linalg.norm(m.clusterCenters, axis=1), 1.0, rtol=1e-15)
+    xn = oracle.row_norms(X)
+    C, cn = X[[0, 2, 4]].copy(), oracle.row_norms(X[[0, 2, 4]])
+    it = 0
+    while it < 20:
+        r = oracle.cos_kmeans_iteration(X, xn, None, C, cn, epsilon=1e-6)
+        C, cn = r["centers"], r["cnorm"]
+        it += 1
+        if r["converged"]:
+            break
+    assert m.numIter == it
+    np.testing.assert_allclose(m.clusterCenters, C, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(m.trainingCost, r["cost"], rtol=1e-10, atol=1e-14)
+
+
+@pytest.mark.gpu
+def test_cos_bench_scale_all_rows(cuda):
+    """A 2M x 256, k = 1024 cosine assignment (the KMeans bench shape at a
+    fifth of its rows): every row's index and cost against the restatement,
+    run as 16 partitions on host threads; the screen certifies most rows."""
+    import torch
+    from concurrent.futures import ThreadPoolExecutor
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    n, d, k = 2_000_000, 256, 1024
+    g = torch.Generator(device=cuda).manual_seed(77)
+    dirs = torch.randn(k, d, generator=g, device=cuda, dtype=torch.float64)
+    lab = torch.randint(0, k, (n,), generator=g, device=cuda)
+    X = (dirs[lab] + 0.3 * torch.randn(n, d, generator=g, device=cuda, dtype=torch.float64)) * \
+        torch.rand(n, 1, generator=g, device=cuda, dtype=torch.float64).add_(0.1)
+    C = X[:k].clone()
+    xn, cn = row_norms(X), row_norms(C)
+    p = KMeansPlan(d, k, n, "cosine")
+    rows = p.rows(X)
+    p.stats(C)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    c = torch.empty(n, dtype=torch.float64, device=cuda)
+    n_exact = p.assign(X, xn, C, cn, a, c, count_exact=True, rows=rows)
+    torch.cuda.synchronize()
+    assert n_exact < n // 10
+    Xh, Ch = X.cpu().numpy(), C.cpu().numpy()
+    xnh, cnh = xn.cpu().numpy(), cn.cpu().numpy()
+    stats = oracle.cos_stats(Ch, cnh)
+    bounds = np.linspace(0, n, 17).astype(np.int64)
+
+    def part(i):
+        s, e = bounds[i], bounds[i + 1]
+        ra, rd, *_ = oracle.cos_kmeans_partition(Xh[s:e], xnh[s:e], None, Ch, cnh, stats)
+        return ra, rd
+
+    with ThreadPoolExecutor(16) as ex:
+        res = list(ex.map(part, range(16)))
+    np.testing.assert_array_equal(a.cpu().numpy(), np.concatenate([r[0] for r in res]))
+    np.testing.assert_array_equal(c.cpu().numpy(), np.concatenate([r[1] for r in res]))

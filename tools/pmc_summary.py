@@ -2,7 +2,7 @@
 """Summarise a tools/prof.sh run into profiles/<prefix>_pmc.json and
 profiles/<prefix>_kernel_stats.csv.
 
-Per kernel (rocprofv3 -T names): calls and mean duration (kernel trace +
+Per kernel (base names of the untruncated rocprofv3 names, see short_name): calls and mean duration (kernel trace +
 --stats), the mean FETCH_SIZE / WRITE_SIZE per dispatch from the two
 separate --pmc passes (KB), and HBM bytes per dispatch and per step.
 
@@ -30,19 +30,49 @@ FETCH_X2 = {"k_screen", "k_screen32", "k_tiles_margin", "k_tiles_grad", "k_csr_d
             "k_binlog_csc_grad_blk", "k_summ_dense"}
 
 
+def short_name(full):
+    """Kernel base name from a full (untruncated) rocprofv3 name; the two
+    passes of the d <= 256 KMeans screen (k_screen32<S, W, LIMBS, LIST>)
+    become k_screen32_l2 / k_screen32_l3."""
+    name = full.split("(")[0].strip()
+    if name.startswith("void "):
+        name = name[5:]
+    tmpl = ""
+    if "<" in name:
+        name, tmpl = name.split("<", 1)
+    base = name.split("::")[-1].strip()
+    if base == "k_screen32" and tmpl:
+        args = [a.strip() for a in tmpl.rstrip(">").split(",")]
+        if len(args) >= 3:
+            base += "_l" + args[2]
+    return base
+
+
 def mean_counter(path):
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+        agg[(short_name(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in agg.items()}
 
 
+def kernel_stats(path):
+    """rocprofv3 --stats rows merged per short name (calls summed, mean
+    duration weighted by calls)."""
+    acc = {}
+    for r in csv.DictReader(open(path)):
+        n = short_name(r["Name"])
+        c, t = int(r["Calls"]), float(r["TotalDurationNs"])
+        a = acc.setdefault(n, {"calls": 0, "total_ns": 0.0, "pct": 0.0})
+        a["calls"] += c
+        a["total_ns"] += t
+        a["pct"] += float(r["Percentage"])
+    return {n: {"calls": a["calls"], "avg_ns": a["total_ns"] / max(a["calls"], 1),
+                "pct": a["pct"]} for n, a in acc.items()}
+
+
 def main(src, dst_prefix, rows, iters):
-    stats = {}
     ks = os.path.join(src, "trace", "run_kernel_stats.csv")
-    for r in csv.DictReader(open(ks)):
-        stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
-                            "pct": float(r["Percentage"])}
+    stats = kernel_stats(ks)
     fetch = mean_counter(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
     write = mean_counter(os.path.join(src, "pmc_write", "run_counter_collection.csv"))
     out = {"_rows": int(rows), "_iterations": int(iters),
@@ -51,7 +81,7 @@ def main(src, dst_prefix, rows, iters):
     for name, s in stats.items():
         f = fetch.get((name, "FETCH_SIZE"))
         w = write.get((name, "WRITE_SIZE"))
-        if name in FETCH_X2:
+        if name in FETCH_X2 or name.rsplit("_l", 1)[0] in FETCH_X2:
             fac, cal = 2.0, "x2 (streaming read, gfx950 half count)"
         else:
             fac, cal = 1.0, "uncalibrated"
