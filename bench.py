@@ -99,7 +99,8 @@ class KMeansWorkload:
     row) is reported beside it, and the three-limb pass over the rows it
     leaves (k_kmeans_screen3) is timed too."""
     kernel = "k_kmeans_screen2"
-    kernels = ("k_kmeans_screen2", "k_kmeans_screen3", "k_kmeans_assign_fp64", "k_chunk_sums")
+    kernels = ("k_kmeans_screen2", "k_kmeans_cands", "k_kmeans_screen3", "k_kmeans_assign_fp64",
+               "k_chunk_sums")
     pmc_kernels = ("k_screen32_l2",)
     bound = "mfma"
     unit = "TOPS"
@@ -167,8 +168,9 @@ class KMeansWorkload:
         tier2, _ = self.plan.last_tiers()
         return {"algorithmic_fp64_flop_per_launch": flops,
                 "fp64_equivalent_tflops": flops / avg_s / 1e12,
-                "rows_left_by_two_limb_pass": self.plan.last_screen(),
-                "rows_left_by_three_limb_pass": tier2, "rows_left_to_exact": exact,
+                "rows_to_candidate_pass": self.plan.last_candidates(),
+                "rows_to_three_limb_pass": self.plan.last_screen(),
+                "rows_to_fp64_screen": tier2, "rows_to_exact": exact,
                 "note": "i8 ops = two-limb integer screen (3 MFMA limb products, every "
                         "row); fp64-equivalent = 2kd flop/row over the same time"}
 

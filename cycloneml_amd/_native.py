@@ -64,6 +64,7 @@ SIGNATURES = {
     "cyc_kmeans_rows_bytes": (_i64, [_vp]),
     "cyc_kmeans_last_tiers": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_last_screen": (ctypes.c_int, [_vp, _pi64]),
+    "cyc_kmeans_last_candidates": (ctypes.c_int, [_vp, _pi64]),
     "cyc_kmeans_update_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _f64, _vp, _vp]),
     "cyc_row_norms_csr_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "cyc_kmeans_assign_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,

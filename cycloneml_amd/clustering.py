@@ -110,6 +110,13 @@ class KMeansPlan:
         N.check(self._lib.cyc_kmeans_last_screen(self.handle, ctypes.byref(a)))
         return a.value
 
+    def last_candidates(self):
+        """Rows the two-limb pass handed to its candidate pass on the last
+        assign(count_exact=True) (-1: no two-limb pass)."""
+        a = ctypes.c_int64(0)
+        N.check(self._lib.cyc_kmeans_last_candidates(self.handle, ctypes.byref(a)))
+        return a.value
+
     def accumulate(self, X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, assign=None,
                    cost=None, stream=None, rows=None):
         N.check(self._lib.cyc_kmeans_accumulate_dev(

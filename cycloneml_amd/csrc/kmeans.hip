@@ -1716,11 +1716,14 @@ struct cyc_kmeans_plan_s {
   double omE3 = 1.0, tauL3 = 0.0, facU3 = 0.0, tauU3 = 0.0;
   int64_t lastTier2 = 0;    // rows the bf16 screen queued (last counted call)
   int64_t lastExact = 0;    // rows the fp64 screen queued (last counted call)
-  int64_t lastLimb3 = -1;   // rows the two-limb i8 pass left (-1: no such pass)
+  int64_t lastLimb3 = -1;   // rows the two-limb i8 pass left to the three-limb pass (-1: none)
+  int64_t lastCands = -1;   // rows the two-limb i8 pass left to the candidate pass
   cyc::DeviceBuffer cb3, cq3, ok3, list3, list3Count;
   // i8 exact-integer screen (kmeans_i8.hip), used with a row image
   int ktp8 = 0;
   cyc::DeviceBuffer cb8, cq8, g8, prm8, scr8, list8Count;   // list8 = slowList (idle then)
+  // candidate pass of the d <= 256 screen (kmeans_i8.hpp CandArgs)
+  cyc::DeviceBuffer candRows, cands, candCount;
   int64_t max_rows = 0;
   size_t assignLds = 0;
   std::mutex mu;
@@ -1847,6 +1850,25 @@ int launch_assign3(cyc_kmeans_plan p, const double* X, const double* xnorm, int6
   return CYC_OK;
 }
 
+// The candidate pass's buffers and arguments (d <= 256 screens only).
+int cand_args(cyc_kmeans_plan p, int64_t n, const double* X, const double* xnorm,
+              const double* C, const double* cnorm, bool unit, cyc::km8::CandArgs& ca,
+              bool& use) {
+  use = cyc::km8::uses32(p->d);
+  if (!use) return CYC_OK;
+  int rc;
+  if ((rc = p->candRows.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = p->cands.reserve(sizeof(int32_t) * (size_t)n * cyc::km8::kCandMax)) ||
+      (rc = p->candCount.reserve(64)))
+    return rc;
+  // Euclidean: a 2^-30 relative gap is far above fp64 rounding; the cosine
+  // plan keeps the screen's own 2^-19 (the statistic's sqrt, kmeans_cos.hip)
+  ca = cyc::km8::CandArgs{X, xnorm, C, cnorm, p->k, unit, unit ? 0x1p-19 : 0x1p-30,
+                          (int32_t*)p->candRows.ptr, (int32_t*)p->cands.ptr,
+                          (unsigned int*)p->candCount.ptr};
+  return CYC_OK;
+}
+
 int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmeans_rows rows,
               int64_t n, const double* C, const double* cnorm, int32_t* assign, double* cost,
               int64_t* n_exact_out, hipStream_t st, bool nostats = false) {
@@ -1866,11 +1888,15 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
                                         (cyc::km8::CenterParams*)p->prm8.ptr,
                                         (double*)p->scr8.ptr, st)))
       return rc;
+    cyc::km8::CandArgs ca;
+    bool useCa = false;
+    if ((rc = cand_args(p, n, X, nullptr, C, cnorm, false, ca, useCa))) return rc;
     if ((rc = cyc::km8::screen(rows->img.ptr, (const int2*)rows->meta.ptr, xnorm, n, p->d,
                                p->cb8.ptr, (const float*)p->cq8.ptr, (const double*)p->g8.ptr,
                                cnorm, (const cyc::km8::CenterParams*)p->prm8.ptr, p->ktp8,
                                assign, (int32_t*)p->list3.ptr, (unsigned int*)p->list3Count.ptr,
-                               (int32_t*)p->slowList.ptr, (unsigned int*)p->list8Count.ptr, st)))
+                               (int32_t*)p->slowList.ptr, (unsigned int*)p->list8Count.ptr, st,
+                               useCa ? &ca : nullptr)))
       return rc;
     rowList = (const int32_t*)p->list3.ptr;
     rowCount = (const unsigned int*)p->list3Count.ptr;
@@ -1898,19 +1924,22 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
   // Exact emulation of the reference loop for undecided rows.  The queue
   // length is read back only when the caller asks for it; otherwise a
   // grid-stride launch drains whatever the queue holds without a host sync.
-  unsigned int h_slow = 0, h_tier2 = 0, h_limb3 = 0;
+  unsigned int h_slow = 0, h_tier2 = 0, h_limb3 = 0, h_cand = 0;
   if (n_exact_out) {
     const bool twoPass = rows && rows->usable && cyc::km8::uses32(p->d);
     CYC_HIP(hipMemcpyAsync(&h_slow, p->slowCount.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     if (rowCount)
       CYC_HIP(hipMemcpyAsync(&h_tier2, rowCount, sizeof(unsigned), hipMemcpyDeviceToHost, st));
-    if (twoPass)
+    if (twoPass) {
       CYC_HIP(hipMemcpyAsync(&h_limb3, p->list8Count.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+      CYC_HIP(hipMemcpyAsync(&h_cand, p->candCount.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    }
     CYC_HIP(hipStreamSynchronize(st));
     *n_exact_out = h_slow;
     p->lastTier2 = rowCount ? (int64_t)h_tier2 : n;
     p->lastExact = h_slow;
     p->lastLimb3 = twoPass ? (int64_t)h_limb3 : -1;
+    p->lastCands = twoPass ? (int64_t)h_cand : -1;
     if (h_slow) {
       hipLaunchKernelGGL(k_assign_exact, dim3((unsigned)std::min<unsigned>((h_slow + 3) / 4, 4096)), dim3(256), 0, st, X, xnorm,
                          p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm, p->k, statsArg,
@@ -2044,6 +2073,9 @@ int cos_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmea
     double* Vn = (double*)p->cosVn.ptr;
     if ((rc = cyc::kmcos::centers_unit(C, cnorm, p->k, p->d, V, Vn, st))) return rc;
     CYC_HIP(hipMemsetAsync(count, 0, sizeof(unsigned int), st));
+    cyc::km8::CandArgs ca;
+    bool useCa = false;
+    if ((rc = cand_args(p, n, X, xnorm, V, Vn, true, ca, useCa))) return rc;
     if ((rc = cyc::km8::centers_prepare(V, Vn, p->k, p->d, p->ktp8, p->cb8.ptr,
                                         (float*)p->cq8.ptr, (double*)p->g8.ptr,
                                         (cyc::km8::CenterParams*)p->prm8.ptr,
@@ -2053,23 +2085,26 @@ int cos_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmea
                                (const float*)p->cq8.ptr, (const double*)p->g8.ptr, Vn,
                                (const cyc::km8::CenterParams*)p->prm8.ptr, p->ktp8, assign, list,
                                count, (int32_t*)p->slowList.ptr,
-                               (unsigned int*)p->list8Count.ptr, st)))
+                               (unsigned int*)p->list8Count.ptr, st, useCa ? &ca : nullptr)))
       return rc;
   } else if ((rc = cyc::kmcos::list_all(list, count, n, st))) {
     return rc;
   }
   int64_t maxRows = n;
   if (n_exact_out) {
-    unsigned int h = 0, h3 = 0;
+    unsigned int h = 0, h3 = 0, hc = 0;
     const bool twoPass = screen && cyc::km8::uses32(p->d);
     CYC_HIP(hipMemcpyAsync(&h, count, sizeof(unsigned), hipMemcpyDeviceToHost, st));
-    if (twoPass)
+    if (twoPass) {
       CYC_HIP(hipMemcpyAsync(&h3, p->list8Count.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+      CYC_HIP(hipMemcpyAsync(&hc, p->candCount.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    }
     CYC_HIP(hipStreamSynchronize(st));
     *n_exact_out = h;
     p->lastTier2 = h;   // no fp64 screen tier: the screen's leftovers are exact
     p->lastExact = h;
     p->lastLimb3 = twoPass ? (int64_t)h3 : -1;
+    p->lastCands = twoPass ? (int64_t)hc : -1;
     maxRows = h;
   }
   if (maxRows == 0) return CYC_OK;
@@ -2188,6 +2223,13 @@ int cyc_kmeans_last_screen(cyc_kmeans_plan p, int64_t* three_limb_rows) {
   CYC_REQUIRE(p != nullptr && three_limb_rows, "arguments must not be null");
   std::lock_guard<std::mutex> g(p->mu);
   *three_limb_rows = p->lastLimb3;
+  return CYC_OK;
+}
+
+int cyc_kmeans_last_candidates(cyc_kmeans_plan p, int64_t* candidate_rows) {
+  CYC_REQUIRE(p != nullptr && candidate_rows, "arguments must not be null");
+  std::lock_guard<std::mutex> g(p->mu);
+  *candidate_rows = p->lastCands;
   return CYC_OK;
 }
 
@@ -2555,14 +2597,17 @@ int cyc_kmeans_assign_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr, const in
   CYC_REQUIRE(p != nullptr, "plan must not be null");
   CYC_REQUIRE(n >= 0, "n >= 0");
   CYC_REQUIRE(assign != nullptr && cost != nullptr, "assign and cost must not be null");
-  if (is_cos(p)) {
-    cyc::set_error("the cosine distance measure runs on dense rows only");
-    return CYC_ERR_UNSUPPORTED;
-  }
   if (n == 0) return CYC_OK;
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
   int rc;
+  if (is_cos(p)) {
+    if ((rc = cos_enqueue(p, cnorm, true, xnorm, n, st)) ||
+        (rc = cyc::kmcos::assign_sparse(rowptr, colidx, vals, xnorm, n, p->d, C, cnorm, p->k,
+                                        (const double*)p->stats.ptr, assign, cost, st)))
+      return rc;
+    return cos_check(p);
+  }
   if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
   if ((rc = sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost, st)))
     return rc;
@@ -2576,14 +2621,21 @@ int cyc_kmeans_point_cost_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
   CYC_REQUIRE(p != nullptr, "plan must not be null");
   CYC_REQUIRE(n >= 0, "n >= 0");
   CYC_REQUIRE(assign != nullptr && cost != nullptr, "assign and cost must not be null");
-  if (is_cos(p)) {
-    cyc::set_error("the cosine distance measure runs on dense rows only");
-    return CYC_ERR_UNSUPPORTED;
-  }
   if (n == 0) return CYC_OK;
   std::lock_guard<std::mutex> g(p->mu);
-  return sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost,
-                       cyc::as_stream(stream), true);
+  hipStream_t st = cyc::as_stream(stream);
+  if (is_cos(p)) {
+    int rc;
+    if ((rc = cos_enqueue(p, cnorm, true, xnorm, n, st)) ||
+        (rc = cyc::kmcos::assign_sparse(rowptr, colidx, vals, xnorm, n, p->d, C, cnorm, p->k,
+                                        nullptr, assign, cost, st)))
+      return rc;
+    hipLaunchKernelGGL(k_nostats_cost_fix, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n,
+                       cost);
+    CYC_LAUNCH_CHECK("k_nostats_cost_fix");
+    return cos_check(p);
+  }
+  return sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost, st, true);
 }
 
 int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
@@ -2594,10 +2646,6 @@ int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
   CYC_REQUIRE(p != nullptr, "plan must not be null");
   CYC_REQUIRE(n >= 0, "n >= 0");
   CYC_REQUIRE(sums && wsum && cost_sum, "sums, wsum and cost_sum must not be null");
-  if (is_cos(p)) {
-    cyc::set_error("the cosine distance measure runs on dense rows only");
-    return CYC_ERR_UNSUPPORTED;
-  }
   if (n == 0) return CYC_OK;
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
@@ -2609,6 +2657,15 @@ int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
   if (!cost) {
     if ((rc = p->costTmp.reserve(sizeof(double) * (size_t)n))) return rc;
     cost = (double*)p->costTmp.ptr;
+  }
+  if (is_cos(p)) {
+    if ((rc = cos_enqueue(p, cnorm, true, xnorm, n, st)) || (rc = cos_stats(p, C, cnorm, st)) ||
+        (rc = cyc::kmcos::assign_sparse(rowptr, colidx, vals, xnorm, n, p->d, C, cnorm, p->k,
+                                        (const double*)p->stats.ptr, assign, cost, st)) ||
+        (rc = cyc::kmcos::sparse_sums(rowptr, colidx, vals, weights, xnorm, n, p->d, assign,
+                                      cost, sums, wsum, cost_sum, st)))
+      return rc;
+    return cos_check(p);
   }
   if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
   if ((rc = do_stats(p, C, st))) return rc;

@@ -264,6 +264,93 @@ __global__ __launch_bounds__(256) void k_cos_assign_exact(
   }
 }
 
+// The same loop for SparseVector points (libsvm input): distance(center,
+// point) = 1 - dot(c, x) / |c| / |x| with BLAS.dot(dense, sparse) =
+// dot(sparse, dense) (mllib/linalg/BLAS.scala:128-134, 153-169), the sum
+// over the point's stored entries in order.  Every row (no screen for sparse
+// points), one wave per row, grid-stride.
+__global__ __launch_bounds__(256) void k_cos_assign_sparse(
+    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
+    const double* __restrict__ vals, const double* __restrict__ xnorm, int64_t n, int d,
+    const double* __restrict__ C, const double* __restrict__ cnorm, int k,
+    const double* __restrict__ stats, int32_t* __restrict__ assign, double* __restrict__ cost) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const bool ns = stats == nullptr;
+  for (int64_t r = wid; r < n; r += nw) {
+    const int64_t q0 = rowptr[r], nnz = rowptr[r + 1] - q0;
+    const int32_t* idx = colidx + q0;
+    const double* val = vals + q0;
+    const double xn = xnorm[r];
+    auto dist = [&](const double* c, double cn) {
+      double dot = 0.0;
+      for (int64_t q = 0; q < nnz; ++q) dot = dadd(dot, dmul(val[q], c[idx[q]]));
+      return 1.0 - dot / cn / xn;
+    };
+    double best = ns ? __builtin_inf() : dist(C, cnorm[0]);
+    int bi = 0;
+    bool done = !ns && best < stats[0];
+    for (int i0 = ns ? 0 : 1; !done && i0 < k; i0 += 64) {
+      const int i = i0 + lane;
+      const bool valid = i < k;
+      const double sii = (valid && !ns) ? stats[iut(i, i)] : 0.0;
+      double dd = 0.0;
+      bool have = false;
+      int pos = 0;
+      for (;;) {
+        const bool visit = valid && lane >= pos && (ns || stats[iut(i, bi)] < best);
+        if (visit && !have) {
+          dd = dist(C + (int64_t)i * d, cnorm[i]);
+          have = true;
+        }
+        const bool brk = !ns && visit && dd < sii;
+        const bool ev = visit && (brk || dd < best);
+        const unsigned long long m = __ballot(ev);
+        if (!m) break;
+        const int f = __ffsll((long long)m) - 1;
+        best = __shfl(dd, f);
+        bi = i0 + f;
+        if (__shfl((int)brk, f)) {
+          done = true;
+          break;
+        }
+        pos = f + 1;
+      }
+    }
+    if (lane == 0) {
+      assign[r] = bi;
+      if (cost) cost[r] = best;
+    }
+  }
+}
+
+// updateClusterSum for sparse points: axpy(w / |x|, x, sum) with the sparse
+// axpy (mllib/linalg/BLAS.scala:93-112), clusterWeightSum and costAccum; one
+// wave per row with fp64 atomics, as the Euclidean sparse path.
+__global__ __launch_bounds__(256) void k_cos_sparse_sums(
+    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
+    const double* __restrict__ vals, const double* __restrict__ w,
+    const double* __restrict__ xnorm, int64_t n, int d, const int32_t* __restrict__ assign,
+    const double* __restrict__ cost, double* __restrict__ sums, double* __restrict__ wsum,
+    double* __restrict__ costSum) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t r = wid; r < n; r += nw) {
+    const int c = assign[r];
+    const double wr = w ? w[r] : 1.0;
+    const double a = wr / xnorm[r];
+    double* y = sums + (int64_t)c * d;
+    for (int64_t q = rowptr[r] + lane; q < rowptr[r + 1]; q += 64)
+      unsafeAtomicAdd(&y[colidx[q]], a == 1.0 ? vals[q] : dmul(a, vals[q]));
+    if (lane == 0) {
+      unsafeAtomicAdd(&wsum[c], wr);
+      unsafeAtomicAdd(costSum, dmul(cost[r], wr));
+    }
+  }
+}
+
 // 64-row tiles staged through LDS 8 columns at a time, one lane per row.
 __global__ void k_cos_row_cost(const double* __restrict__ X, int64_t n, int d,
                                const double* __restrict__ C, const double* __restrict__ cnorm,
@@ -436,6 +523,30 @@ int assign_exact(const double* X, const double* xnorm, int d, const double* C, c
   hipLaunchKernelGGL(k_cos_assign_exact, dim3(grid), dim3(256), 0, st, X, xnorm, d, C, Ct, kpad,
                      cnorm, k, stats, list, count, assign, cost);
   CYC_LAUNCH_CHECK("k_cos_assign_exact");
+  return CYC_OK;
+}
+
+int assign_sparse(const int64_t* rowptr, const int32_t* colidx, const double* vals,
+                  const double* xnorm, int64_t n, int d, const double* C, const double* cnorm,
+                  int k, const double* stats, int32_t* assign, double* cost, hipStream_t st) {
+  if (n <= 0) return CYC_OK;
+  KernelTimer timer("k_kmeans_cos_sparse", st);
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_cos_assign_sparse, dim3(grid), dim3(256), 0, st, rowptr, colidx, vals,
+                     xnorm, n, d, C, cnorm, k, stats, assign, cost);
+  CYC_LAUNCH_CHECK("k_cos_assign_sparse");
+  return CYC_OK;
+}
+
+int sparse_sums(const int64_t* rowptr, const int32_t* colidx, const double* vals,
+                const double* w, const double* xnorm, int64_t n, int d, const int32_t* assign,
+                const double* cost, double* sums, double* wsum, double* costSum,
+                hipStream_t st) {
+  if (n <= 0) return CYC_OK;
+  const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_cos_sparse_sums, dim3(grid), dim3(256), 0, st, rowptr, colidx, vals, w,
+                     xnorm, n, d, assign, cost, sums, wsum, costSum);
+  CYC_LAUNCH_CHECK("k_cos_sparse_sums");
   return CYC_OK;
 }
 

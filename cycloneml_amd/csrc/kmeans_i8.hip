@@ -617,7 +617,9 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
     const double* __restrict__ g, const double* __restrict__ cnorm,
     const CenterParams* __restrict__ prm, int ktp, const int32_t* __restrict__ rowsIn,
     const unsigned int* __restrict__ rowsInCount, int32_t* __restrict__ assign,
-    int32_t* __restrict__ list, unsigned int* __restrict__ listCount) {
+    int32_t* __restrict__ list, unsigned int* __restrict__ listCount,
+    int32_t* __restrict__ candRows, int32_t* __restrict__ cands,
+    unsigned int* __restrict__ candCount) {
   constexpr int D = 32 * S, CH = 3 * D / 16;      // 16-byte chunks per image row
   constexpr int FR = LIMBS * S;                    // 1 KiB B fragments per center tile
   constexpr int TB = FR * 1024 + 256;              // tile slot: fragments, then 64 cq floats
@@ -819,9 +821,16 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
   __builtin_amdgcn_s_setreg(0x801, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing re-read DMAs
 
+  // LIMBS = 2: each lane's own best and second best (one center column per
+  // lane) before the reduction merges them: the candidate sets below
+  int cV1[16], cV2[16];
   if constexpr (LIMBS == 2) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) sI1[q] = (int)((unsigned)sV1[q] & IM) * 32 + r;
+    for (int q = 0; q < 16; ++q) {
+      sI1[q] = (int)((unsigned)sV1[q] & IM) * 32 + r;
+      cV1[q] = sV1[q];
+      cV2[q] = sV2[q];
+    }
   }
   // each row's (L1, L2, I1) over the 32 lanes (centers) of its half: every
   // xor step halves the registers a lane keeps (lanes with the step's bit
@@ -879,16 +888,21 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
   const bool waveBad = __builtin_amdgcn_ballot_w64(qbad) != 0;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  bool want = false;   // LIMBS = 2: an undecided row for the candidate pass
+  int thrV = 0;
+  int64_t grow = 0;
   if (lane < rows) {
-    const int64_t grow = rowAt(lane);
+    grow = rowAt(lane);
     const int2 mt = meta[grow];
     const int I1 = redI1[lane];
     // L1, L2 as fp64 (LIMBS = 2: -F1 V, exact; V2 = INT_MIN: no second)
-    double l1, l2;
+    double l1, l2, f1 = 0.0;
+    int v1 = 0;
     bool clamped = false;
     if constexpr (LIMBS == 2) {
-      const double f1 = __builtin_ldexp(1.0, mt.x + P.ec - 20);
-      const int v1 = __float_as_int(redL1[lane]), v2 = __float_as_int(redL2[lane]);
+      f1 = __builtin_ldexp(1.0, mt.x + P.ec - 20);
+      v1 = __float_as_int(redL1[lane]);
+      const int v2 = __float_as_int(redL2[lane]);
       l1 = -f1 * (double)v1;
       l2 = v2 == INT_MIN ? __builtin_inf() : -f1 * (double)v2;
       // the winner's Q must not have clamped (its bound would be too low)
@@ -897,7 +911,8 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
       l1 = (double)redL1[lane];
       l2 = (double)redL2[lane];
     }
-    bool decided = false;
+    bool decided = false, eligible = false;
+    double M = 0.0;
     if (mt.x != INT_MIN && I1 >= 0 && I1 < P.k && !clamped && !waveBad && __builtin_isfinite(l1)) {
       const double xn = xnorm[grow], cn = cnorm[I1];
       const double xx = xn * xn, cc = cn * cn;
@@ -909,18 +924,81 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
       // rounded Q adds < 1 more: |L1 - L1'|, |L2 - L2'| < (2^IB + 1) F1
       const double enc = LIMBS == 3 ? 0.0
                                     : __builtin_ldexp((double)(IM + 3u), mt.x + P.ec - 20);
-      const double M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) + 2.0 * enc +
-                        0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g[I1]) +
-                        0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
-                                   __builtin_fmin(__builtin_fabs(l2), 0x1p120)) +
-                        0x1p-90) *
-                       (1.0 + 0x1p-30);
+      M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) + 2.0 * enc +
+           0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g[I1]) +
+           0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
+                      __builtin_fmin(__builtin_fabs(l2), 0x1p120)) +
+           0x1p-90) *
+          (1.0 + 0x1p-30);
       decided = !__builtin_isfinite(l2) || (l2 - l1) > M;
+      eligible = __builtin_isfinite(M);
     }
     if (decided) {
       assign[grow] = I1;
+    } else if (LIMBS == 2 && candRows != nullptr && eligible) {
+      // candidates: the centers c with f1 (V1 - V_c) <= M, i.e. V_c >= v1 -
+      // floor(M / f1) -- the certification test against I1, failed by
+      // every candidate and passed by every other center
+      const double tv = (double)v1 - __builtin_floor(M / f1);
+      if (tv > (double)INT_MIN + 2.0) {
+        want = true;
+        thrV = (int)tv;
+      } else {
+        list[atomicAdd(listCount, 1u)] = (int32_t)grow;
+      }
     } else {
       list[atomicAdd(listCount, 1u)] = (int32_t)grow;
+    }
+  }
+  if constexpr (LIMBS == 2) {
+    if (candRows != nullptr) {
+      // Candidate sets of the undecided rows from the saved per-lane states:
+      // lane (r, h) saw the centers 32 ct + r of row (reg & 3) + 8 (reg >> 2)
+      // + 4 h; its best is a candidate when it reaches the row's threshold,
+      // and a lane whose SECOND best reaches it too (an index not kept)
+      // sends the row to the three-limb pass.  <= kCandMax candidates go to
+      // the candidate list (exact fp64 distances, screen_cands).
+      int* thrS = (int*)lds + W * 96 + wave * (64 + 32 * (kCandMax + 1));
+      int* wantS = thrS + 32;
+      int* candS = thrS + 64;
+      if (lane < 32) {
+        thrS[lane] = thrV;
+        wantS[lane] = want ? 1 : 0;
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const bool w = wantS[row] != 0;
+        const int t = thrS[row];
+        const bool ok = w && cV1[reg] >= t;
+        const bool ov = w && cV2[reg] >= t;
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
+        const unsigned long long mo = __builtin_amdgcn_ballot_w64(ov);
+        const unsigned bits = (unsigned)(m >> (32 * h));
+        if (ok) {
+          const int slot = __builtin_popcount(bits & ((1u << r) - 1u));
+          if (slot < kCandMax)
+            candS[row * (kCandMax + 1) + 1 + slot] = (int)((unsigned)cV1[reg] & IM) * 32 + r;
+        }
+        if (r == 0 && w)
+          candS[row * (kCandMax + 1)] = (unsigned)(mo >> (32 * h)) ? -1 : __builtin_popcount(bits);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (want) {
+        const int* cs = candS + lane * (kCandMax + 1);
+        const int cnt = cs[0];
+        if (cnt >= 1 && cnt <= kCandMax) {
+          const unsigned idx = atomicAdd(candCount, 1u);
+          candRows[idx] = (int32_t)grow;
+#pragma unroll
+          for (int i = 0; i < kCandMax; ++i) cands[(size_t)idx * kCandMax + i] = i < cnt ? cs[1 + i] : -1;
+        } else {
+          list[atomicAdd(listCount, 1u)] = (int32_t)grow;
+        }
+      }
     }
   }
   __syncthreads();   // the reduction area is the next group's tile ring
@@ -935,29 +1013,146 @@ int launch_screen32(const void* img, const int2* meta, const double* xnorm, int6
                     const void* Cb, const float* cq, const double* g, const double* cnorm,
                     const CenterParams* prm, int ktp, const int32_t* rowsIn,
                     const unsigned int* rowsInCount, int32_t* assign, int32_t* list,
-                    unsigned int* listCount, hipStream_t st) {
+                    unsigned int* listCount, hipStream_t st, int32_t* candRows = nullptr,
+                    int32_t* cands = nullptr, unsigned int* candCount = nullptr) {
   KernelTimer timer(LIMBS == 2 ? "k_kmeans_screen2" : "k_kmeans_screen3", st);
   const int64_t wg = (n + 32 * W - 1) / (32 * W);   // W waves x 32 rows
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32<S, W, LIMBS, LIST>), dim3((unsigned)wg),
                      dim3(64 * W), 0, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
-                     cq, g, cnorm, prm, ktp, rowsIn, rowsInCount, assign, list, listCount);
+                     cq, g, cnorm, prm, ktp, rowsIn, rowsInCount, assign, list, listCount,
+                     candRows, cands, candCount);
   CYC_LAUNCH_CHECK("k_kmeans_screen32_i8");
   return CYC_OK;
 }
 
-// Two-limb pass over every row, three-limb pass over its leftovers.
+// Candidate rows (one wave each): fp64 squared distances to the <= kCandMax
+// candidates, summed over the lanes' dimensions (any order: the error is
+// <= (d + 2) 2^-53 2 (|x|^2 + |c|^2) < 2^-40 (|x|^2 + |c|^2)); |c| from the
+// screen's center norms (an fp64 norm: its rounding sits far inside margin).  The row is
+// certified when the second smallest exceeds the smallest by margin (|x|^2
+// + |c_best|^2) plus both errors: every other center was already excluded by
+// the two-limb bounds (by the screen's own margin), so the best candidate
+// is the reference loop's answer as for any certified row.  Ties and near
+// ties go on to list (the fp64 screen, then the reference loop).
+__global__ __launch_bounds__(256) void k_screen_cands(
+    const double* __restrict__ X, const double* __restrict__ xnorm, int d,
+    const double* __restrict__ C, const double* __restrict__ cnorm, int k, bool unit,
+    double margin, const int32_t* __restrict__ candRows, const int32_t* __restrict__ cands,
+    const unsigned int* __restrict__ candCount, int32_t* __restrict__ assign,
+    int32_t* __restrict__ list, unsigned int* __restrict__ listCount) {
+  const unsigned cnt = *candCount;
+  const int lane = threadIdx.x & 63;
+  const unsigned nw = (gridDim.x * blockDim.x) >> 6;
+  const unsigned w0 = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  for (unsigned idx = w0; idx < cnt; idx += nw) {
+    // every load of the row up front (the candidates' rows in flight together)
+    const int64_t row = candRows[idx];
+    int ci[kCandMax];
+#pragma unroll
+    for (int i = 0; i < kCandMax; ++i) ci[i] = cands[(size_t)idx * kCandMax + i];
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < kCandMax; ++i) bad = bad || ci[i] >= k;   // a padding center
+    const double* x = X + row * d;
+    double u[4], cv[kCandMax][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = lane + 64 * q;   // d <= 256
+      u[q] = j < d ? x[j] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kCandMax; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = lane + 64 * q;
+        cv[i][q] = (ci[i] >= 0 && ci[i] < k && j < d) ? C[(int64_t)ci[i] * d + j] : 0.0;
+      }
+    const double inv = unit ? 1.0 / xnorm[row] : 1.0;
+    double part[kCandMax + 1];
+    part[kCandMax] = 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (unit) u[q] = u[q] * inv;
+      part[kCandMax] += u[q] * u[q];
+    }
+#pragma unroll
+    for (int i = 0; i < kCandMax; ++i) {
+      double s2 = 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double t = cv[i][q] - u[q];
+        s2 += t * t;
+      }
+      part[i] = s2;
+    }
+    // seven butterfly sums side by side
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1)
+#pragma unroll
+      for (int i = 0; i <= kCandMax; ++i) part[i] += __shfl_xor(part[i], m);
+    const double xx = part[kCandMax];
+    double best = __builtin_inf(), second = __builtin_inf();
+    int bi = -1, si = -1;
+#pragma unroll
+    for (int i = 0; i < kCandMax; ++i) {
+      if (ci[i] < 0 || ci[i] >= k) continue;
+      const double s2 = part[i];
+      if (s2 < best) {
+        second = best;
+        si = bi;
+        best = s2;
+        bi = ci[i];
+      } else if (s2 < second) {   // an equal distance lands here: no certification
+        second = s2;
+        si = ci[i];
+      }
+    }
+    bool ok = !bad && bi >= 0 && __builtin_isfinite(best) && __builtin_isfinite(xx);
+    if (ok && second != __builtin_inf()) {   // one candidate: certified as it is
+      const double cb = cnorm[bi], cs = si >= 0 ? cnorm[si] : 0.0;
+      const double ccb = cb * cb, ccs = cs * cs;
+      const double M = margin * (xx + ccb) + 0x1p-40 * (2.0 * xx + ccb + ccs);
+      ok = __builtin_isfinite(M) && (second - best) > M * (1.0 + 0x1p-30);
+    }
+    if (lane == 0) {
+      if (ok) assign[row] = bi;
+      else list[atomicAdd(listCount, 1u)] = (int32_t)row;
+    }
+  }
+}
+
+int launch_cands(const CandArgs& ca, int64_t n, int d, int32_t* assign, int32_t* list,
+                 unsigned int* listCount, hipStream_t st) {
+  KernelTimer timer("k_kmeans_cands", st);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 31) / 32, 8192));
+  hipLaunchKernelGGL(k_screen_cands, dim3(grid), dim3(256), 0, st, ca.X, ca.xnorm, d, ca.C,
+                     ca.cnorm, ca.k, ca.unit, ca.margin, (const int32_t*)ca.candRows, (const int32_t*)ca.cands,
+                     (const unsigned int*)ca.candCount, assign, list, listCount);
+  CYC_LAUNCH_CHECK("k_screen_cands");
+  return CYC_OK;
+}
+
+// Two-limb pass over every row; its undecided rows with a small candidate
+// set get exact fp64 distances to those candidates (k_screen_cands), the
+// others the three-limb pass.
 template <int S, int W>
 int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
              const void* Cb, const float* cq, const double* g, const double* cnorm,
              const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
-             unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st) {
+             unsigned int* listCount, int32_t* list2, unsigned int* list2Count,
+             const CandArgs* ca, hipStream_t st) {
   CYC_HIP(hipMemsetAsync(list2Count, 0, sizeof(unsigned int), st));
+  if (ca) CYC_HIP(hipMemsetAsync(ca->candCount, 0, sizeof(unsigned int), st));
   int rc = launch_screen32<S, W, 2, false>(img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 32,
                                            g + (size_t)ktp * 32, cnorm, prm, ktp, nullptr,
-                                           nullptr, assign, list2, list2Count, st);
+                                           nullptr, assign, list2, list2Count, st,
+                                           ca ? ca->candRows : nullptr, ca ? ca->cands : nullptr,
+                                           ca ? ca->candCount : nullptr);
   if (rc) return rc;
-  return launch_screen32<S, W, 3, true>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp, list2,
-                                        list2Count, assign, list, listCount, st);
+  if ((rc = launch_screen32<S, W, 3, true>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp,
+                                           list2, list2Count, assign, list, listCount, st)))
+    return rc;
+  return ca ? launch_cands(*ca, n, d, assign, list, listCount, st) : CYC_OK;
 }
 
 template <int KS>
@@ -1027,13 +1222,14 @@ int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp,
 int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
            const void* Cb, const float* cq, const double* g, const double* cnorm,
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
-           unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st) {
+           unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st,
+           const CandArgs* ca) {
   if (n <= 0) return CYC_OK;
   if (uses32(d)) {
     const int k32 = ktp * 16 / 32;   // launch over the padded center range (cq = +inf)
     switch (ksteps(d)) {
-      case 2: return screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, st);
-      default: return screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, st);
+      case 2: return screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st);
+      default: return screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st);
     }
   }
   switch (ksteps(d)) {

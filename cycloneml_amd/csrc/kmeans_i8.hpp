@@ -52,13 +52,36 @@ int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipS
 int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp, void* Cb,
                     float* cq, double* g, CenterParams* prm, double* scratch, hipStream_t st);
 
+// Candidate pass of the d <= 256 screen: the two-limb pass hands each row
+// it cannot certify, whose candidate set (the centers the certification
+// test cannot exclude) has <= kCandMax members, to k_screen_cands: exact
+// fp64 distances (any order, error-bounded) to those candidates, certified
+// by a relative gap of `margin` (|x|^2 + |c|^2).  The rows and centers are
+// the screened vectors: X / xnorm[row] when unit (the cosine plan), C as
+// given (the screen's centers).
+constexpr int kCandMax = 6;
+struct CandArgs {
+  const double* X;        // n x d fp64 rows
+  const double* xnorm;    // unit: the row norms X is divided by
+  const double* C;        // k x d screened centers
+  const double* cnorm;    // their norms
+  int k;
+  bool unit;
+  double margin;
+  int32_t* candRows;      // n entries
+  int32_t* cands;         // n * kCandMax entries
+  unsigned int* candCount;
+};
+
 // Screen every row: certified rows get assign[row]; the others are appended
 // to list (listCount is NOT cleared here).  list2 / list2Count (n entries +
 // one counter): scratch for the rows the 32x32 two-limb pass leaves.
+// ca (d <= 256, optional): the candidate pass.
 int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
            const void* Cb, const float* cq, const double* g, const double* cnorm,
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
-           unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st);
+           unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st,
+           const CandArgs* ca = nullptr);
 
 }  // namespace km8
 }  // namespace cyc

@@ -577,16 +577,19 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
       }
     }
   };
+  double xa[2][4], xb[2][4];
+  bool pre = false;   // chunk 0 of this tile already in flight (xa, Ws[0])
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t r0 = tile * MR;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[t][ct] = cyc_double4{0.0, 0.0, 0.0, 0.0};
-    double xa[2][4], xb[2][4];
-    __syncthreads();   // the previous tile's last W buffer is free
+    if (!pre) {
+      __syncthreads();   // the previous tile's last W buffer is free
+      loadW(0);
+    }
     loadX(r0, 0, xa);
-    loadW(0);
     // chunk ch: wait for its loads, barrier (its W visible everywhere, every
     // wave past chunk ch - 1), issue chunk ch + 1's loads, multiply
     auto step = [&](int ch, double (&xc)[2][4], double (&xn)[2][4]) {
@@ -611,6 +614,13 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
       step(ch, xa, xb);
       if (ch + 1 < nch) step(ch + 1, xb, xa);
     }
+    // the next tile's W chunk 0 goes out before this tile's epilogue (the X
+    // registers stay free for it: prefetching X too spills at CT = 7): with
+    // an even chunk count the last chunk read Ws[1], and every wave is past
+    // chunk nch - 2 (Ws[0]) since the last barrier
+    const int64_t next = tile + gridDim.x;
+    pre = (nch % 2) == 0 && next < tiles;
+    if (pre) loadW(0);
     epilogue(r0);
   }
   // per-wave partials: loss/wsum from lanes with (lane & 15) == 0, multSum

@@ -86,8 +86,8 @@ int cyc_kmeans_plan_destroy(cyc_kmeans_plan plan);
  * 1 - sqrt(1 - d / 2) (:412-417), updateClusterSum axpy(w / |x|, x, sum)
  * (:466-469), the unit-norm centroid whose norm is set to 1.0 (:477-483) and
  * isCenterConverged distance <= epsilon (:161-166); a zero-length (or NaN)
- * norm returns CYC_ERR_ASSERTION with the reference's assert text.  The CSR
- * entry points support only EUCLIDEAN (CYC_ERR_UNSUPPORTED). */
+ * norm returns CYC_ERR_ASSERTION with the reference's assert text.  Dense and
+ * CSR points (sparse: dot(sparse, dense) and the sparse axpy). */
 #define CYC_DISTANCE_EUCLIDEAN 0
 #define CYC_DISTANCE_COSINE 1
 int cyc_kmeans_plan_set_distance_measure(cyc_kmeans_plan plan, int32_t measure);
@@ -136,10 +136,14 @@ int cyc_kmeans_point_cost_dev(cyc_kmeans_plan plan, const double* X, const doubl
  * to the fp64 MFMA screen (all rows when neither runs), and rows left to the
  * exact emulation. */
 int cyc_kmeans_last_tiers(cyc_kmeans_plan plan, int64_t* fp64_screen_rows, int64_t* exact_rows);
-/* Rows the d <= 256 screen's two-limb i8 pass left to its three-limb pass on
- * the last counted assign (-1 when that call ran no two-limb pass).  A
+/* Rows the d <= 256 screen's two-limb i8 pass left to its three-limb pass
+ * (rows whose candidate set it could not list) on the last counted assign (-1 when that call ran no two-limb pass).  A
  * statistic of the tiered findClosest; no reference counterpart. */
 int cyc_kmeans_last_screen(cyc_kmeans_plan plan, int64_t* three_limb_rows);
+/* Rows the two-limb pass handed to its candidate pass (exact fp64 distances
+ * to the <= 6 centers its bounds could not exclude) on the last counted
+ * assign (-1 when no two-limb pass ran).  Also a tier statistic. */
+int cyc_kmeans_last_candidates(cyc_kmeans_plan plan, int64_t* candidate_rows);
 
 /* One partition's contribution to a Lloyd iteration: statistics + assign +
  * per-cluster sums.  sums[k*d] += sum of w*x, wsum[k] += sum of w,

@@ -478,6 +478,85 @@ void orc_cos_kmeans_partition(const double* X, const double* xnorm, const double
   *cost = c;
 }
 
+/* distance(center dense, point sparse): BLAS.dot(dense, sparse) dispatches
+ * to dot(sparse, dense) (mllib/linalg/BLAS.scala:128-134, 153-169) */
+static double orc_cos_distance_sparse(const double* c, double nc, const int32_t* idx,
+                                      const double* val, int64_t nnz, double nx) {
+  return 1.0 - orc_dot_sparse_dense(idx, val, nnz, c) / nc / nx;
+}
+
+/* findClosest with (stats != NULL, :421-447) or without (:131-150)
+ * statistics for a SparseVector point */
+static void orc_cos_find_closest_sparse(const double* C, const double* cnorm, int64_t k,
+                                        int64_t d, const double* stats, const int32_t* idx,
+                                        const double* val, int64_t nnz, double xnorm,
+                                        int32_t* out_idx, double* out_dist) {
+  *out_idx = -1;
+  *out_dist = NAN;
+  double best = INFINITY;
+  int64_t bestIndex = 0;
+  int64_t i0 = 0;
+  if (stats) {
+    if (!orc_cos_assert(cnorm[0], xnorm)) return;
+    best = orc_cos_distance_sparse(C, cnorm[0], idx, val, nnz, xnorm);
+    if (best < stats[0]) { *out_idx = 0; *out_dist = best; return; }
+    i0 = 1;
+  }
+  for (int64_t i = i0; i < k; ++i) {
+    if (stats && !(stats[orc_iut(i, bestIndex)] < best)) continue;
+    if (!orc_cos_assert(cnorm[i], xnorm)) return;
+    double dd = orc_cos_distance_sparse(C + i * d, cnorm[i], idx, val, nnz, xnorm);
+    if (stats && dd < stats[orc_iut(i, i)]) { *out_idx = (int32_t)i; *out_dist = dd; return; }
+    if (dd < best) { best = dd; bestIndex = i; }
+  }
+  *out_idx = (int32_t)bestIndex;
+  *out_dist = best;
+}
+
+double orc_cos_point_costs_sparse(const int64_t* rowptr, const int32_t* colidx,
+                                  const double* vals, const double* xnorm, int64_t n, int64_t d,
+                                  const double* C, const double* cnorm, int64_t k,
+                                  int32_t* assign, double* cost) {
+  double sum = 0.0;
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t q0 = rowptr[r];
+    orc_cos_find_closest_sparse(C, cnorm, k, d, NULL, colidx + q0, vals + q0, rowptr[r + 1] - q0,
+                                xnorm[r], assign + r, cost + r);
+    if (assign[r] < 0) break;
+    sum += cost[r];
+  }
+  return sum;
+}
+
+/* the Lloyd partition body for SparseVector points: updateClusterSum =
+ * mllib BLAS.axpy(w / norm, sparse x, sum) (BLAS.scala:93-112) */
+void orc_cos_kmeans_partition_sparse(const int64_t* rowptr, const int32_t* colidx,
+                                     const double* vals, const double* xnorm, const double* w,
+                                     int64_t n, int64_t d, const double* C, const double* cnorm,
+                                     const double* stats, int64_t k, int32_t* assign,
+                                     double* dist, double* sums, double* wsum, double* cost) {
+  double c = *cost;
+  for (int64_t r = 0; r < n; ++r) {
+    const int64_t q0 = rowptr[r], nnz = rowptr[r + 1] - q0;
+    int32_t bi; double bd;
+    orc_cos_find_closest_sparse(C, cnorm, k, d, stats, colidx + q0, vals + q0, nnz, xnorm[r],
+                                &bi, &bd);
+    if (bi < 0) break;
+    double wt = w ? w[r] : 1.0;
+    if (assign) assign[r] = bi;
+    if (dist) dist[r] = bd;
+    c += bd * wt;
+    double a = wt / xnorm[r];
+    double* s = sums + (int64_t)bi * d;
+    for (int64_t q = 0; q < nnz; ++q) {
+      if (a == 1.0) s[colidx[q0 + q]] += vals[q0 + q];
+      else s[colidx[q0 + q]] += a * vals[q0 + q];
+    }
+    wsum[bi] += wt;
+  }
+  *cost = c;
+}
+
 /* centroid (:477-483): scal(1/weightSum, sum), norm, scal(1/norm, sum),
  * new VectorWithNorm(sum, 1); isCenterConverged (:161-166): distance(old,
  * new) <= epsilon.  Returns 1 if every updated center converged. */

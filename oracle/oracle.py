@@ -75,6 +75,11 @@ def lib():
                                                     _I32, _D, _D, _D, _D]),
                 "orc_cos_update_centers": (ctypes.c_int, [_D, _D, _D, _D, _i64, _i64,
                                                           ctypes.c_double]),
+                "orc_cos_point_costs_sparse": (ctypes.c_double, [_I64, _I32, _D, _D, _i64, _i64,
+                                                                 _D, _D, _i64, _I32, _D]),
+                "orc_cos_kmeans_partition_sparse": (None, [_I64, _I32, _D, _D, _D, _i64, _i64,
+                                                           _D, _D, _D, _i64, _I32, _D, _D, _D,
+                                                           _D]),
                 "orc_log1pexp": (ctypes.c_double, [ctypes.c_double]),
                 "orc_softmax": (None, [_D, _i64, _i64, _i64]),
                 "orc_hinge_add_dense": (None, [_i64, _i64, _D, _D, _D, _D, ctypes.c_int, _D, _D,
@@ -441,6 +446,40 @@ def cos_kmeans_partition(X, xnorm, w, C, cnorm, stats):
     lib().orc_cos_kmeans_partition(_p(X), _p(xnorm), _p(None if w is None else _f64(w)), n, d,
                                    _p(C), _p(cnorm), _p(stats), k, _p(a, _I32), _p(dist),
                                    _p(sums), _p(wsum), _p(cost))
+    _raise_assert()
+    return a, dist, sums.reshape(k, d), wsum, cost[0]
+
+
+def cos_point_costs_sparse(csr, xnorm, C, cnorm):
+    rp, ci, v, d = csr
+    rp = np.ascontiguousarray(rp, dtype=np.int64)
+    ci = np.ascontiguousarray(ci, dtype=np.int32)
+    v, C, cnorm = _f64(v), _f64(C), _f64(cnorm)
+    n = rp.shape[0] - 1
+    a = np.empty(n, dtype=np.int32)
+    c = np.empty(n)
+    s = lib().orc_cos_point_costs_sparse(_p(rp, _I64), _p(ci, _I32), _p(v), _p(_f64(xnorm)), n,
+                                         d, _p(C), _p(cnorm), C.shape[0], _p(a, _I32), _p(c))
+    _raise_assert()
+    return a, c, s
+
+
+def cos_kmeans_partition_sparse(csr, xnorm, w, C, cnorm, stats):
+    """csr = (rowptr, colidx, values, numFeatures)."""
+    rp, ci, v, d = csr
+    rp = np.ascontiguousarray(rp, dtype=np.int64)
+    ci = np.ascontiguousarray(ci, dtype=np.int32)
+    v, C, cnorm, stats = _f64(v), _f64(C), _f64(cnorm), _f64(stats)
+    n, k = rp.shape[0] - 1, C.shape[0]
+    a = np.full(n, -1, dtype=np.int32)
+    dist = np.full(n, np.nan)
+    sums = np.zeros(k * d)
+    wsum = np.zeros(k)
+    cost = np.zeros(1)
+    lib().orc_cos_kmeans_partition_sparse(_p(rp, _I64), _p(ci, _I32), _p(v), _p(_f64(xnorm)),
+                                          _p(None if w is None else _f64(w)), n, d, _p(C),
+                                          _p(cnorm), _p(stats), k, _p(a, _I32), _p(dist),
+                                          _p(sums), _p(wsum), _p(cost))
     _raise_assert()
     return a, dist, sums.reshape(k, d), wsum, cost[0]
 

@@ -345,3 +345,49 @@ def test_cos_bench_scale_all_rows(cuda):
         res = list(ex.map(part, range(16)))
     np.testing.assert_array_equal(a.cpu().numpy(), np.concatenate([r[0] for r in res]))
     np.testing.assert_array_equal(c.cpu().numpy(), np.concatenate([r[1] for r in res]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("weighted", [False, True])
+def test_cos_csr_vs_oracle(cuda, weighted):
+    """SparseVector points (libsvm input) with the cosine measure: findClosest
+    with and without statistics bit-exact (dot(sparse, dense) in stored
+    order), the Lloyd sums (sparse axpy of w / |x|) within 1e-10."""
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms, row_norms_csr
+    rng = np.random.default_rng(21)
+    n, d, k = 6000, 300, 40
+    D = _clustered(rng, n, d, k, spread=0.3)
+    D[rng.random(D.shape) < 0.7] = 0.0
+    D[:, 0] += 0.5                       # no zero rows
+    rows = [np.flatnonzero(D[i]) for i in range(n)]
+    rp = np.zeros(n + 1, dtype=np.int64)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    ci = np.concatenate(rows).astype(np.int32)
+    vals = np.concatenate([D[i, r] for i, r in enumerate(rows)])
+    C = D[rng.choice(n, size=k, replace=False)].copy()
+    w = rng.uniform(0.2, 2.0, n) if weighted else None
+    rpd, cid, vd, Cd = _dev(rp, cuda), _dev(ci, cuda), _dev(vals, cuda), _dev(C, cuda)
+    xn, cn = row_norms_csr(rpd, vd), row_norms(Cd)
+    p = KMeansPlan(d, k, n, "cosine")
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    c = torch.empty(n, dtype=torch.float64, device=cuda)
+    p.point_cost_csr(rpd, cid, vd, xn, Cd, cn, a, c)
+    xnh, cnh = xn.cpu().numpy(), oracle.row_norms(C)
+    pa, pc, _ = oracle.cos_point_costs_sparse((rp, ci, vals, d), xnh, C, cnh)
+    np.testing.assert_array_equal(a.cpu().numpy(), pa)
+    np.testing.assert_array_equal(c.cpu().numpy(), pc)
+    buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=cuda)
+    sums, wsum, cost = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
+    p.accumulate_csr(rpd, cid, vd, xn, None if w is None else _dev(w, cuda), Cd, cn, sums, wsum,
+                     cost, a, c)
+    torch.cuda.synchronize()
+    stats = oracle.cos_stats(C, cnh)
+    ra, rd, rs, rw, rc = oracle.cos_kmeans_partition_sparse((rp, ci, vals, d), xnh, w, C, cnh,
+                                                            stats)
+    np.testing.assert_array_equal(a.cpu().numpy(), ra)
+    np.testing.assert_array_equal(c.cpu().numpy(), rd)
+    np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), rs, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(wsum.cpu().numpy(), rw, rtol=1e-12)
+    np.testing.assert_allclose(float(cost.item()), rc, rtol=1e-10)
+    p.close()
