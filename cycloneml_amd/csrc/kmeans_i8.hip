@@ -1034,63 +1034,86 @@ int launch_screen32(const void* img, const int2* meta, const double* xnorm, int6
 // the two-limb bounds (by the screen's own margin), so the best candidate
 // is the reference loop's answer as for any certified row.  Ties and near
 // ties go on to list (the fp64 screen, then the reference loop).
+// 16-lane row sum by DPP row rotations (VALU, no LDS): every lane of the
+// row ends with the total.
+__device__ __forceinline__ double row16_sum(double v) {
+#define CYC_ROR(CTRL)                                                                        \
+  {                                                                                          \
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false); \
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false); \
+    v += __hiloint2double(hi, lo);                                                           \
+  }
+  CYC_ROR(0x128) CYC_ROR(0x124) CYC_ROR(0x122) CYC_ROR(0x121)
+#undef CYC_ROR
+  return v;
+}
+
 __global__ __launch_bounds__(256) void k_screen_cands(
     const double* __restrict__ X, const double* __restrict__ xnorm, int d,
     const double* __restrict__ C, const double* __restrict__ cnorm, int k, bool unit,
     double margin, const int32_t* __restrict__ candRows, const int32_t* __restrict__ cands,
     const unsigned int* __restrict__ candCount, int32_t* __restrict__ assign,
     int32_t* __restrict__ list, unsigned int* __restrict__ listCount) {
+  // 4 rows per wave, 16 lanes per row; lane s of a row holds the dimensions
+  // s, s + 16, ... (each load instruction reads one 128-byte line per row)
   const unsigned cnt = *candCount;
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, q = lane >> 4, sl = lane & 15;
   const unsigned nw = (gridDim.x * blockDim.x) >> 6;
-  const unsigned w0 = __builtin_amdgcn_readfirstlane((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  for (unsigned idx = w0; idx < cnt; idx += nw) {
-    // every load of the row up front (the candidates' rows in flight together)
-    const int64_t row = candRows[idx];
+  const unsigned w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  for (unsigned base = w0 * 4; base < cnt; base += nw * 4) {
+    const unsigned idx = base + q;
+    const bool live = idx < cnt;
+    const int64_t row = live ? candRows[idx] : 0;
     int ci[kCandMax];
 #pragma unroll
-    for (int i = 0; i < kCandMax; ++i) ci[i] = cands[(size_t)idx * kCandMax + i];
+    for (int i = 0; i < kCandMax; ++i) ci[i] = live ? cands[(size_t)idx * kCandMax + i] : -1;
     bool bad = false;
 #pragma unroll
     for (int i = 0; i < kCandMax; ++i) bad = bad || ci[i] >= k;   // a padding center
     const double* x = X + row * d;
-    double u[4], cv[kCandMax][4];
+    double u[16];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = lane + 64 * q;   // d <= 256
-      u[q] = j < d ? x[j] : 0.0;
+    for (int e = 0; e < 16; ++e) {
+      const int j = e * 16 + sl;   // d <= 256
+      u[e] = (live && j < d) ? x[j] : 0.0;
     }
+    if (unit) {
+      const double inv = live ? 1.0 / xnorm[row] : 0.0;
 #pragma unroll
-    for (int i = 0; i < kCandMax; ++i)
+      for (int e = 0; e < 16; ++e) u[e] = u[e] * inv;
+    }
+    double xx = 0.0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = lane + 64 * q;
-        cv[i][q] = (ci[i] >= 0 && ci[i] < k && j < d) ? C[(int64_t)ci[i] * d + j] : 0.0;
+    for (int e = 0; e < 16; ++e) xx += u[e] * u[e];
+    double part[kCandMax];
+#pragma unroll
+    for (int h = 0; h < kCandMax; h += 3) {
+      double cv[3][16];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int c = ci[h + i];
+        const bool on = c >= 0 && c < k;
+        const double* cr = C + (int64_t)(on ? c : 0) * d;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int j = e * 16 + sl;
+          cv[i][e] = (on && j < d) ? cr[j] : 0.0;
+        }
       }
-    const double inv = unit ? 1.0 / xnorm[row] : 1.0;
-    double part[kCandMax + 1];
-    part[kCandMax] = 0.0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (unit) u[q] = u[q] * inv;
-      part[kCandMax] += u[q] * u[q];
-    }
+      for (int i = 0; i < 3; ++i) {
+        double s2 = 0.0;
 #pragma unroll
-    for (int i = 0; i < kCandMax; ++i) {
-      double s2 = 0.0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const double t = cv[i][q] - u[q];
-        s2 += t * t;
+        for (int e = 0; e < 16; ++e) {
+          const double t = cv[i][e] - u[e];
+          s2 += t * t;
+        }
+        part[h + i] = s2;
       }
-      part[i] = s2;
     }
-    // seven butterfly sums side by side
+    xx = row16_sum(xx);
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1)
-#pragma unroll
-      for (int i = 0; i <= kCandMax; ++i) part[i] += __shfl_xor(part[i], m);
-    const double xx = part[kCandMax];
+    for (int i = 0; i < kCandMax; ++i) part[i] = row16_sum(part[i]);
     double best = __builtin_inf(), second = __builtin_inf();
     int bi = -1, si = -1;
 #pragma unroll
@@ -1114,7 +1137,7 @@ __global__ __launch_bounds__(256) void k_screen_cands(
       const double M = margin * (xx + ccb) + 0x1p-40 * (2.0 * xx + ccb + ccs);
       ok = __builtin_isfinite(M) && (second - best) > M * (1.0 + 0x1p-30);
     }
-    if (lane == 0) {
+    if (live && sl == 0) {
       if (ok) assign[row] = bi;
       else list[atomicAdd(listCount, 1u)] = (int32_t)row;
     }
@@ -1124,7 +1147,7 @@ __global__ __launch_bounds__(256) void k_screen_cands(
 int launch_cands(const CandArgs& ca, int64_t n, int d, int32_t* assign, int32_t* list,
                  unsigned int* listCount, hipStream_t st) {
   KernelTimer timer("k_kmeans_cands", st);
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 31) / 32, 8192));
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 127) / 128, 4096));
   hipLaunchKernelGGL(k_screen_cands, dim3(grid), dim3(256), 0, st, ca.X, ca.xnorm, d, ca.C,
                      ca.cnorm, ca.k, ca.unit, ca.margin, (const int32_t*)ca.candRows, (const int32_t*)ca.cands,
                      (const unsigned int*)ca.candCount, assign, list, listCount);
