@@ -65,6 +65,9 @@ SIGNATURES = {
     "cyc_kmeans_last_tiers": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_last_screen": (ctypes.c_int, [_vp, _pi64]),
     "cyc_kmeans_last_candidates": (ctypes.c_int, [_vp, _pi64]),
+    "cyc_kmeans_parallel_sample_dev": (ctypes.c_int, [_vp, _pi64, _i32, _i32, _i32, _i32, _i32,
+                                                      _f64, _vp, _vp]),
+    "cyc_xorshift_hash_seed": (ctypes.c_uint64, [_i64]),
     "cyc_kmeans_update_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _f64, _vp, _vp]),
     "cyc_row_norms_csr_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
     "cyc_kmeans_assign_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,

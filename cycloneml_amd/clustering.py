@@ -38,6 +38,20 @@ def _decode_measure(dm: str) -> int:
     return _MEASURES[dm]
 
 
+def xorshift_next_int(seed: int) -> int:
+    """new XORShiftRandom(seed).nextInt() (core/.../util/random/
+    XORShiftRandom.scala:44-66): the hashed state (cyc_xorshift_hash_seed)
+    advanced once, its low 32 bits as a signed Int.  KMeans.scala:377 seeds
+    the k-means|| steps with it."""
+    m64 = (1 << 64) - 1
+    x = int(N.load().cyc_xorshift_hash_seed(int(seed))) & m64
+    x ^= (x << 21) & m64
+    x ^= x >> 35
+    x ^= (x << 4) & m64
+    v = x & 0xFFFFFFFF
+    return v - (1 << 32) if v >= 1 << 31 else v
+
+
 class KMeansPlan:
     """RAII wrapper of cyc_kmeans_plan (device scratch for one (d, k) shape
     and one DistanceMeasure)."""
@@ -381,6 +395,30 @@ class KMeans:
                                                                device=c.device)
         parallel.allreduce_(tot)
         return c, float(tot.item())
+
+    @staticmethod
+    def parallelSample(costs, sumCosts, seed, step, k, partition_starts, first_partition=0,
+                       stream=None):
+        """The executor side of one k-means|| step (KMeans.scala:398-404) on
+        the device: a uint8 mask of the rows whose partition's
+        XORShiftRandom(seed ^ (step << 16) ^ index) draws nextDouble() <
+        2.0 * cost * k / sumCosts, one draw per row in partition order --
+        the points the reference collects (X[mask.bool()] keeps their
+        order).  costs: the updated point costs (updateParallelCosts);
+        seed: xorshift_next_int(KMeans seed); partition_starts: the shard's
+        rows split into Spark partitions (host ints, from 0), partition p
+        having index first_partition + p."""
+        torch = _torch()
+        starts = np.ascontiguousarray(partition_starts, dtype=np.int64)
+        if starts.size < 2 or starts[0] != 0 or starts[-1] != costs.numel():
+            raise N.IllegalArgumentException(
+                "partition_starts must run from 0 to the number of rows")
+        mask = torch.empty(costs.numel(), dtype=torch.uint8, device=costs.device)
+        N.check(N.load().cyc_kmeans_parallel_sample_dev(
+            N.ptr(costs), starts.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+            int(starts.size - 1), int(first_partition), int(seed), int(step), int(k),
+            float(sumCosts), N.ptr(mask), N.stream_handle(stream)))
+        return mask
 
     def run(self, X, weights=None, xnorm=None, stream=None, iteration_callback=None):
         """Lloyd's algorithm, KMeans.scala:240-349, on a device-resident shard.

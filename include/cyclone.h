@@ -188,6 +188,22 @@ int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan plan, const int64_t* rowptr,
                                   const double* cnorm, double* sums, double* wsum,
                                   double* cost_sum, int32_t* assign, double* cost, void* stream);
 
+/* k-means|| initialisation, the executor side of one step (KMeans.scala:
+ * 398-404): chosen[i] = 1 iff the partition's XORShiftRandom(seed ^ (step <<
+ * 16) ^ index) draws nextDouble() < 2.0 * costs[i] * k / sum_costs, one draw
+ * per point in the partition's order -- the same points the reference keeps.
+ * part_starts (HOST, num_parts + 1 offsets from 0): the shard's rows split
+ * into Spark partitions; partition p has index first_part_index + p.
+ * seed: the Int `new XORShiftRandom(this.seed).nextInt()` (:377).  costs and
+ * chosen (uint8) are device arrays of part_starts[num_parts] entries. */
+int cyc_kmeans_parallel_sample_dev(const double* costs, const int64_t* part_starts,
+                                   int32_t num_parts, int32_t first_part_index, int32_t seed,
+                                   int32_t step, int32_t k, double sum_costs, uint8_t* chosen,
+                                   void* stream);
+/* XORShiftRandom.hashSeed (core/.../util/random/XORShiftRandom.scala:60-66):
+ * the generator's initial state for a Long seed (host). */
+uint64_t cyc_xorshift_hash_seed(int64_t seed);
+
 /* ------------------------------------------------------ RowMatrix Gramian */
 /* Replaces the BLAS.spr seqOp of RowMatrix.computeGramianMatrix
  * (mllib/linalg/distributed/RowMatrix.scala:130-161) and of

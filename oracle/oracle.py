@@ -818,6 +818,24 @@ class XORShiftRandom(JavaRandom):
         return r
 
 
+def kmeans_parallel_sample(costs, part_starts, first_index, seed, step, k, sum_costs):
+    """One k-means|| step's filter (KMeans.scala:398-404) per partition:
+    XORShiftRandom(seed ^ (step << 16) ^ index) (Int arithmetic, widened to
+    Long), keep the point iff rand.nextDouble() < 2.0 * c * k / sumCosts.
+    Returns the uint8 mask."""
+    def i32(v):
+        v &= 0xFFFFFFFF
+        return v - (1 << 32) if v >= 1 << 31 else v
+    costs = np.asarray(costs, dtype=np.float64)
+    out = np.zeros(costs.size, dtype=np.uint8)
+    for p in range(len(part_starts) - 1):
+        init = i32(i32(seed) ^ i32(step << 16) ^ i32(first_index + p))
+        rand = XORShiftRandom(init)
+        for i in range(int(part_starts[p]), int(part_starts[p + 1])):
+            out[i] = 1 if rand.next_double() < 2.0 * float(costs[i]) * k / sum_costs else 0
+    return out
+
+
 def _murmur3_bytes(data: bytes, seed: int) -> int:
     """scala.util.hashing.MurmurHash3.bytesHash (x86_32, little-endian blocks)."""
     M = 0xFFFFFFFF
