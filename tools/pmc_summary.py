@@ -34,7 +34,7 @@ def short_name(full):
     """Kernel base name from a full (untruncated) rocprofv3 name; the two
     passes of the d <= 256 KMeans screen (k_screen32<S, W, LIMBS, LIST>)
     become k_screen32_l2 / k_screen32_l3."""
-    name = full.split("(")[0].strip()
+    name = full.replace("(anonymous namespace)", "").split("(")[0].strip()
     if name.startswith("void "):
         name = name[5:]
     tmpl = ""
