@@ -432,10 +432,7 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
 //     load that would force a vmcnt(0) drain of the B prefetch);
 //   - B fragments for 32 dims (8 MFMA k-steps) ping-pong between two named
 //     register sets, one step ahead.
-// ABL (timing ablations for tools/kmeans_ab.py, wrong results by design):
-// 0 = real kernel; 1 = no epilogue; 2 = no B loads (B from registers);
-// 3 = neither.
-template <int BM, int ABL>
+template <int BM>
 __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign2(
     const double* __restrict__ X, const double* __restrict__ xnorm, int64_t n, int d, int d4,
     int ldsStride, const double* __restrict__ Ct, const double* __restrict__ C,
@@ -506,13 +503,9 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign2(
   do {                                                                               \
     const int nb_ = wave * 16 + ((I) / G) * (kWaves * 16);                           \
     const int so_ = ((((I) % G) * 32) * kpad + nb_) * 8;                             \
-    if (ABL & 2) {                                                                   \
-      _Pragma("unroll") for (int s = 0; s < 8; ++s) B[s] = (double)(so_ + s);        \
-    } else {                                                                         \
     _Pragma("unroll") for (int s = 0; s < 8; ++s)                                    \
       B[s] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(          \
           ctR, laneOff, so_ + s * 32 * kpad, 0));                                    \
-    }                                                                                \
   } while (0)
 #define CYC_COMPUTE(B, I)                                                            \
   do {                                                                               \
@@ -526,10 +519,7 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign2(
         acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a_, B[s], acc[t], 0, 0, 0);    \
       }                                                                              \
     }                                                                                \
-    if ((ABL & 1) && g_ == G - 1) {                                                  \
-      _Pragma("unroll") for (int t = 0; t < T; ++t) __builtin_nontemporal_store(acc[t][0], (double*)xnS + 0 * t + BM); \
-    }                                                                                \
-    if (!(ABL & 1) && g_ == G - 1) {                                                 \
+    if (g_ == G - 1) {                                                               \
       const int c_ = wave * 16 + ((I) / G) * (kWaves * 16) + (lane & 15);            \
       const double cn_ = cnS[c_];                                                    \
       const double cq_ = (cn_ * cn_) * (1.0 - fac2);                                 \
@@ -1777,13 +1767,7 @@ int launch_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64
   if (!attr_set) {
     CYC_HIP(hipFuncSetAttribute((const void*)k_kmeans_assign<BM>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_kmeans_assign2<BM, 0>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_kmeans_assign2<BM, 1>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_kmeans_assign2<BM, 2>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_kmeans_assign2<BM, 3>),
+    CYC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_kmeans_assign2<BM>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
@@ -1791,15 +1775,12 @@ int launch_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64
   // list mode (rows queued by the bf16 screen): persistent grid over the queue
   const int64_t blocks = rowList ? std::min<int64_t>((n + BM - 1) / BM, 1024) : (n + BM - 1) / BM;
   cyc::KernelTimer timer(rowList ? "k_kmeans_assign_fp64" : "k_kmeans_assign", st);
-#define CYC_A2(ABLV)                                                                          \
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_kmeans_assign2<BM, ABLV>), dim3((unsigned)blocks), dim3(kAssignThreads), \
+#define CYC_A2()                                                                              \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_kmeans_assign2<BM>), dim3((unsigned)blocks), dim3(kAssignThreads), \
                      p->assignLds2, st, X, xnorm, n, p->d, p->d4, p->ldsStride2,               \
                      (const double*)p->ct.ptr, C, cnorm, p->k, p->kpad, marginFac, assign, cost, \
                      (int32_t*)p->slowList.ptr, (unsigned int*)p->slowCount.ptr, rowList, rowCount)
-  if (p->variant == 2 || p->variant == 3) CYC_A2(0);
-  else if (p->variant == 21) CYC_A2(1);
-  else if (p->variant == 22) CYC_A2(2);
-  else if (p->variant == 23) CYC_A2(3);
+  if (p->variant == 2 || p->variant == 3) CYC_A2();
   else
   hipLaunchKernelGGL(k_kmeans_assign<BM>, dim3((unsigned)blocks), dim3(kAssignThreads),
                      p->assignLds, st, X, xnorm, n, p->d, p->d4, p->ldsStride,
@@ -2157,9 +2138,12 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
             (size_t)kS3BM * 8;
   const bool fits3 = p->variant == 2 && p->lds3 <= 160 * 1024;
   if (fits3) p->variant = 3;
+  // test hook (tests/test_kmeans_gpu.py): the screen tier a plan uses
+  // without a row image -- 1 fp64 screen, 2 fp64 screen with the
+  // conflict-free stride, 3 bf16x3 screen in front of it
   if (const char* v = std::getenv("CYC_KMEANS_ASSIGN")) {
     const int want = std::atoi(v);
-    if (want == 1 || (p->d4 % 32 == 0 && p->assignLds2 <= 160 * 1024 && want >= 2 && want <= 23 &&
+    if (want == 1 || (p->d4 % 32 == 0 && p->assignLds2 <= 160 * 1024 && want >= 2 && want <= 3 &&
                       (want != 3 || fits3)))
       p->variant = want;
   }
