@@ -332,6 +332,9 @@ class KMeans:
     """mllib.clustering.KMeans with the reference's parameters and defaults
     (KMeans.scala:48-60: k=2, maxIterations=20, epsilon=1e-4)."""
 
+    RANDOM = "random"
+    K_MEANS_PARALLEL = "k-means||"
+
     def __init__(self, k: int = 2, maxIterations: int = 20, epsilon: float = 1e-4,
                  seed: int = 0):
         self.k = k
@@ -340,6 +343,45 @@ class KMeans:
         self.seed = seed
         self.initialModel = None
         self.distanceMeasure = "euclidean"
+        self.initializationMode = KMeans.K_MEANS_PARALLEL
+        self.initializationSteps = 2
+
+    def setInitializationMode(self, mode: str):
+        """KMeans.scala:117-121 (validateInitMode's result is not checked
+        there either; an unknown mode runs k-means||, :255-258)."""
+        self.initializationMode = mode
+        return self
+
+    def setInitializationSteps(self, steps: int):
+        if not steps > 0:
+            raise N.IllegalArgumentException(
+                f"requirement failed: Number of initialization steps must be positive but got "
+                f"{steps}")
+        self.initializationSteps = steps
+        return self
+
+    def setSeed(self, seed: int):
+        self.seed = int(seed)
+        return self
+
+    def initial_centers(self, X, xnorm=None, partition_starts=None):
+        """The initial centers of a run without an initial model
+        (KMeans.scala:250-259): initRandom or initKMeansParallel over the
+        shard split into Spark partitions at partition_starts (default: one
+        partition).  One process only: the driver-side sampling sees every
+        partition."""
+        from . import kmeans_init
+        if parallel.world()[1] > 1:
+            raise N.IllegalArgumentException(
+                "the k-means|| / random initialisation runs on one process; pass "
+                "setInitialModel for a multi-GPU run")
+        n = int(X.shape[0])
+        starts = np.asarray([0, n] if partition_starts is None else partition_starts,
+                            dtype=np.int64)
+        if self.initializationMode == KMeans.RANDOM:
+            return kmeans_init.init_random(X, self.k, self.seed, starts)
+        return kmeans_init.init_kmeans_parallel(X, self.k, self.seed, self.initializationSteps,
+                                                starts, self.distanceMeasure, xnorm)
 
     # Builder setters (KMeans.scala:87-200)
     def setK(self, k):
@@ -420,21 +462,34 @@ class KMeans:
             float(sumCosts), N.ptr(mask), N.stream_handle(stream)))
         return mask
 
-    def run(self, X, weights=None, xnorm=None, stream=None, iteration_callback=None):
+    def run(self, X, weights=None, xnorm=None, stream=None, iteration_callback=None,
+            partition_starts=None):
         """Lloyd's algorithm, KMeans.scala:240-349, on a device-resident shard.
 
         X: torch.float64 CUDA tensor (n, d).  weights: optional (n,) tensor.
+        Without an initial model the centers come from initial_centers
+        (partition_starts: the Spark partitions of the shard's rows).
         Returns KMeansModel (centers on the host)."""
         torch = _torch()
-        if self.initialModel is None:
-            raise N.IllegalArgumentException(
-                "initialModel is required on the device path (setInitialModel); "
-                "k-means|| / random initialisation are host-side (SURVEY.md 8f)")
         dev = X.device
         n, d = X.shape
-        k = self.k
         if xnorm is None:
             xnorm = row_norms(X, stream=stream)
+        if self.initialModel is None:
+            C0 = self.initial_centers(X, xnorm, partition_starts)
+            # the run's k is the number of initial centers (KMeans.scala:250-259
+            # may return fewer than k distinct points)
+            self.initialModel = KMeansModel(C0, distanceMeasure=self.distanceMeasure)
+            try:
+                return self._run(X, weights, xnorm, stream, iteration_callback, C0.shape[0])
+            finally:
+                self.initialModel = None
+        return self._run(X, weights, xnorm, stream, iteration_callback, self.k)
+
+    def _run(self, X, weights, xnorm, stream, iteration_callback, k):
+        torch = _torch()
+        dev = X.device
+        n, d = X.shape
         plan = KMeansPlan(d, k, n, self.distanceMeasure)   # decodeFromString (:248)
         rows = plan.rows(X, stream=stream)     # once per fit, like the cached norms
         C = torch.from_numpy(self.initialModel.clusterCenters.copy()).to(dev)

@@ -836,6 +836,75 @@ def kmeans_parallel_sample(costs, part_starts, first_index, seed, step, k, sum_c
     return out
 
 
+def local_kmeans_pp(points, weights, k, max_iterations, seed):
+    """LocalKMeans.kMeansPlusPlus (mllib/clustering/LocalKMeans.scala:35-134)
+    in plain loops: k-means++ seeding with java.util.Random(seed), then
+    Lloyd rounds with EuclideanDistanceMeasure.findClosest (orc_find_closest)."""
+    points = _f64(points)
+    w = [float(v) for v in weights]
+    m, d = points.shape
+    rand = JavaRandom(seed)
+
+    def next_int(bound):
+        r = rand._next(31) & 0x7FFFFFFF
+        mm = bound - 1
+        if bound & mm == 0:
+            return (bound * r) >> 31
+        u = r
+        while True:
+            r = u % bound
+            v = (u - r + mm) & 0xFFFFFFFF
+            if v < 1 << 31:
+                return r
+            u = rand._next(31) & 0x7FFFFFFF
+
+    tot = 0.0
+    for v in w:
+        tot += v
+    r = rand.next_double() * tot
+    i, cur = 0, 0.0
+    while i < m and cur < r:
+        cur += w[i]
+        i += 1
+    centers = [points[i - 1].copy()]
+    cost = [sqdist(points[p], centers[0]) for p in range(m)]
+    for c in range(1, k):
+        s = 0.0
+        for p in range(m):
+            s += cost[p] * w[p]
+        r = rand.next_double() * s
+        cum, j = 0.0, 0
+        while j < m and cum < r:
+            cum += w[j] * cost[j]
+            j += 1
+        centers.append(points[0].copy() if j == 0 else points[j - 1].copy())
+        for p in range(m):
+            cost[p] = min(sqdist(points[p], centers[c]), cost[p])
+    old = [-1] * m
+    it, moved = 0, True
+    while moved and it < max_iterations:
+        moved = False
+        C = np.array(centers)
+        cn = row_norms(C)
+        counts = [0.0] * k
+        sums = np.zeros((k, d))
+        for p in range(m):
+            idx, _ = find_closest(C, cn, points[p], norm2(points[p]))
+            if w[p] != 0.0:
+                sums[idx] = sums[idx] + w[p] * points[p]
+            counts[idx] += w[p]
+            if idx != old[p]:
+                moved = True
+                old[p] = idx
+        for j in range(k):
+            if counts[j] == 0.0:
+                centers[j] = points[next_int(m)].copy()
+            else:
+                centers[j] = (1.0 / counts[j]) * sums[j]
+        it += 1
+    return np.array(centers)
+
+
 def _murmur3_bytes(data: bytes, seed: int) -> int:
     """scala.util.hashing.MurmurHash3.bytesHash (x86_32, little-endian blocks)."""
     M = 0xFFFFFFFF

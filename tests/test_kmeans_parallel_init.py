@@ -86,3 +86,89 @@ def test_kmeans_parallel_steps_end_to_end(cuda):
         new = X[mask.astype(bool)]
         assert new.shape[0] > 0
         centers.extend(new)
+
+
+# ------------------------------------------------------- driver-side init
+
+def test_java_random_known_values():
+    """java.util.Random known answers: new Random(42).nextInt() =
+    -1170105035, nextLong() = -5025562857975149833 for seed 42; the
+    product generator equals the test-side restatement on nextDouble."""
+    from cycloneml_amd.kmeans_init import JavaRandom, XORShiftRandom
+    assert JavaRandom(42).next_int() == -1170105035
+    assert JavaRandom(42).next_long() == -5025562857975149833
+    a, b = JavaRandom(7), oracle.JavaRandom(7)
+    assert [a.next_double() for _ in range(50)] == [b.next_double() for _ in range(50)]
+    x, y = XORShiftRandom(30), oracle.XORShiftRandom(30)
+    assert x.next_double() == 0.2762195585886885          # RandomSuite Rand(30)
+    y.next_double()
+    assert [x.next_double() for _ in range(50)] == [y.next_double() for _ in range(50)]
+    r = JavaRandom(3)
+    vals = [r.next_int(10) for _ in range(2000)] + [r.next_int(64) for _ in range(200)]
+    assert min(vals) >= 0 and max(vals[:2000]) <= 9 and max(vals[2000:]) <= 63
+
+
+def test_take_sample_shapes():
+    """RDD.takeSample(false, num, seed): num distinct positions in range;
+    num >= count returns every item permuted; deterministic in the seed."""
+    from cycloneml_amd.kmeans_init import take_sample_indices
+    lens = [1000, 0, 2500, 7]
+    for num in (1, 5, 40):
+        s = take_sample_indices(lens, num, 123)
+        assert len(s) == num and len(set(s)) == num and all(0 <= i < 3507 for i in s)
+        assert s == take_sample_indices(lens, num, 123)
+    allp = take_sample_indices([3, 4], 10, 9)
+    assert sorted(allp) == list(range(7))
+    assert take_sample_indices([5], 0, 1) == [] and take_sample_indices([0, 0], 3, 1) == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["k-means||", "random"])
+def test_kmeans_run_without_initial_model(cuda, mode):
+    """KMeans.run with the default k-means|| (or random) initialisation
+    (KMeans.scala:250-259): the initial centers equal the host composition
+    of the restated pieces -- takeSample, the cost passes and draws of
+    oracle.kmeans_parallel_sample, oracle.local_kmeans_pp -- and the Lloyd
+    run from them equals a run from those centers given as the model."""
+    import torch
+    from cycloneml_amd.clustering import KMeans, KMeansModel, xorshift_next_int
+    from cycloneml_amd.kmeans_init import take_sample_indices
+    rng = np.random.default_rng(4)
+    n, d, k = 3000, 8, 4
+    X = rng.normal(size=(n, d)) + rng.integers(0, 4, size=(n, 1)) * 5.0
+    starts = np.array([0, 1000, 2200, n], dtype=np.int64)
+    Xd = torch.from_numpy(X).to(cuda)
+    km = KMeans(k=k, maxIterations=10).setSeed(77).setInitializationMode(mode)
+    C0 = km.initial_centers(Xd, partition_starts=starts)
+    s = xorshift_next_int(77)
+    lens = np.diff(starts)
+    if mode == "random":
+        ref = X[take_sample_indices(lens, k, s)]
+    else:
+        cands = [X[take_sample_indices(lens, 1, s)[0]]]
+        new = np.array(cands)
+        costs = np.full(n, np.inf)
+        for step in range(2):
+            _, pc, _ = oracle.point_costs(X, oracle.row_norms(X), new, oracle.row_norms(new))
+            costs = np.minimum(pc, costs)
+            total = float(torch.from_numpy(costs).to(cuda).sum().item())   # the device fold
+            mask = oracle.kmeans_parallel_sample(costs, starts, 0, s, step, k, total)
+            new = X[mask.astype(bool)]
+            cands.extend(new)
+        uniq = []
+        for c in cands:
+            if not any(np.array_equal(c, u) for u in uniq):
+                uniq.append(c)
+        uniq = np.array(uniq)
+        if uniq.shape[0] > k:
+            a, _, _ = oracle.point_costs(X, oracle.row_norms(X), uniq, oracle.row_norms(uniq))
+            wts = np.bincount(a, minlength=uniq.shape[0]).astype(np.float64)
+            ref = oracle.local_kmeans_pp(uniq, wts, k, 30, 0)
+        else:
+            ref = uniq
+    np.testing.assert_array_equal(C0, ref)
+    m1 = km.run(Xd, partition_starts=starts)
+    km2 = KMeans(k=C0.shape[0], maxIterations=10).setInitialModel(KMeansModel(C0))
+    m2 = km2.run(Xd)
+    np.testing.assert_array_equal(m1.clusterCenters, m2.clusterCenters)
+    assert m1.numIter == m2.numIter
