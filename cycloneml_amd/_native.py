@@ -163,6 +163,7 @@ SIGNATURES = {
     "cyc_dataset_append_dense": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64]),
     "cyc_dataset_append_csr": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64]),
     "cyc_kmeans_iter": (ctypes.c_int, [_vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "cyc_kmeans_iter_measure": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i32, _vp, _vp, _vp, _vp]),
     "cyc_svc_hinge_eval": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp, _vp, _vp, _vp]),
     "cyc_linreg_least_squares_eval": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int, _f64, _f64,
                                                      _vp, _vp, _vp, _vp]),

@@ -261,19 +261,33 @@ int cyc_dataset_append_csr(cyc_dataset ds, const int64_t* rowptr, const int32_t*
 
 int cyc_kmeans_iter(cyc_dataset ds, const double* centers, int32_t k, double* sums, double* wsum,
                     double* cost, int32_t* assign_opt) {
+  return cyc_kmeans_iter_measure(ds, CYC_DISTANCE_EUCLIDEAN, centers, nullptr, k, sums, wsum, cost,
+                                 assign_opt);
+}
+
+int cyc_kmeans_iter_measure(cyc_dataset ds, int32_t measure, const double* centers,
+                            const double* center_norms, int32_t k, double* sums, double* wsum,
+                            double* cost, int32_t* assign_opt) {
   CYC_REQUIRE(ds != nullptr && centers && sums && wsum && cost, "arguments must not be null");
+  CYC_REQUIRE(k >= 1, "Number of clusters must be positive but got " + std::to_string(k));
   DeviceGuard g(ds->device);
+  // plans and row images per (k, measure)
+  const int key = k * 2 + (measure == CYC_DISTANCE_COSINE ? 1 : 0);
   cyc_kmeans_plan plan;
-  auto it = ds->kplans.find(k);
+  auto it = ds->kplans.find(key);
   if (it != ds->kplans.end()) {
     plan = it->second;
   } else {
     if (int rc = cyc_kmeans_plan_create(ds->F, k, ds->rows, &plan)) return rc;
-    ds->kplans[k] = plan;
+    if (int rc = cyc_kmeans_plan_set_distance_measure(plan, measure)) {
+      cyc_kmeans_plan_destroy(plan);
+      return rc;
+    }
+    ds->kplans[key] = plan;
   }
   if (int rc = ensure_norms(ds)) return rc;
   cyc_kmeans_rows img = nullptr;
-  auto ri = ds->krows.find(k);
+  auto ri = ds->krows.find(key);
   if (ds->sparse) {
     // sparse rows: no row image (the screens are dense-only)
   } else if (ri != ds->krows.end()) {
@@ -281,7 +295,7 @@ int cyc_kmeans_iter(cyc_dataset ds, const double* centers, int32_t k, double* su
   } else {
     if (int rc = cyc_kmeans_rows_create(plan, (const double*)ds->X.ptr, ds->rows, ds->st, &img))
       return rc;
-    ds->krows[k] = img;
+    ds->krows[key] = img;
   }
   const size_t kd = (size_t)k * ds->F;
   double *dC, *dCn, *dS, *dW;
@@ -292,7 +306,12 @@ int cyc_kmeans_iter(cyc_dataset ds, const double* centers, int32_t k, double* su
       (rc = upload(ds->out1, wsum, k, ds->st, &dW)))
     return rc;
   CYC_HIP(hipMemcpyAsync(dS + kd, cost, sizeof(double), hipMemcpyHostToDevice, ds->st));
-  if ((rc = cyc_row_norms_dev(dC, k, ds->F, dCn, ds->st))) return rc;
+  // the centers' VectorWithNorm norms: given (cosine after an update: 1.0),
+  // else computed (new VectorWithNorm(center))
+  if (center_norms)
+    CYC_HIP(hipMemcpyAsync(dCn, center_norms, sizeof(double) * k, hipMemcpyHostToDevice, ds->st));
+  else if ((rc = cyc_row_norms_dev(dC, k, ds->F, dCn, ds->st)))
+    return rc;
   int32_t* dA = nullptr;
   if (assign_opt) {
     if ((rc = ds->in2.reserve(sizeof(int32_t) * std::max<int64_t>(ds->rows, 1)))) return rc;

@@ -80,16 +80,23 @@ class ResidentDataset:
         return self
 
     # ---- per-iteration entry points (outputs are ADDED to)
-    def kmeans_iter(self, centers, sums=None, wsum=None, cost=None, want_assign=False):
-        """One partition of a Lloyd iteration (KMeans.scala:287-311)."""
+    def kmeans_iter(self, centers, sums=None, wsum=None, cost=None, want_assign=False,
+                    distanceMeasure="euclidean", center_norms=None):
+        """One partition of a Lloyd iteration (KMeans.scala:287-311) with the
+        given DistanceMeasure; center_norms: the centers' VectorWithNorm
+        norms (None = computed)."""
+        from .clustering import _decode_measure
+        measure = _decode_measure(distanceMeasure)
         centers = np.ascontiguousarray(centers, dtype=np.float64)
         k, d = centers.shape
         sums = np.zeros((k, d)) if sums is None else sums
         wsum = np.zeros(k) if wsum is None else wsum
         cost = np.zeros(1) if cost is None else cost
         assign = np.empty(self.numRows, dtype=np.int32) if want_assign else None
-        N.check(N.load().cyc_kmeans_iter(self._h, _p(centers), k, _p(sums), _p(wsum), _p(cost),
-                                         _p(assign)))
+        cn = None if center_norms is None else np.ascontiguousarray(center_norms,
+                                                                   dtype=np.float64)
+        N.check(N.load().cyc_kmeans_iter_measure(self._h, measure, _p(centers), _p(cn), k,
+                                                 _p(sums), _p(wsum), _p(cost), _p(assign)))
         return sums, wsum, cost, assign
 
     def _logreg(self, C, coef, fi, fwm, scaledMean, grad, loss_weight):

@@ -498,6 +498,13 @@ int cyc_dataset_append_csr(cyc_dataset ds, const int64_t* rowptr, const int32_t*
  * cluster indices. */
 int cyc_kmeans_iter(cyc_dataset ds, const double* centers, int32_t k, double* sums, double* wsum,
                     double* cost, int32_t* assign_opt);
+/* The same for a DistanceMeasure (CYC_DISTANCE_*, cyc_kmeans_plan_set_distance
+ * _measure); center_norms (host, k; may be NULL = computed) are the centers'
+ * VectorWithNorm norms -- with COSINE 1.0 after an update (DistanceMeasure.
+ * scala:477-483), which the distances divide by. */
+int cyc_kmeans_iter_measure(cyc_dataset ds, int32_t measure, const double* centers,
+                            const double* center_norms, int32_t k, double* sums, double* wsum,
+                            double* cost, int32_t* assign_opt);
 int cyc_logreg_binary_eval(cyc_dataset ds, const double* coef, int fitIntercept, int fitWithMean,
                            const double* scaledMean, double* grad, double* lossSum,
                            double* weightSum);

@@ -264,3 +264,52 @@ def test_other_aggregator_evals(cuda, sparse, fi):
     st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
     oracle.aft_add(blk(yt, cens), coef, fi, sm, st)
     check(make(yt, cens).aft_eval(coef, fi, sm), st)
+
+
+@pytest.mark.gpu
+def test_kmeans_iter_cosine_two_iterations(cuda):
+    """The resident-dataset Lloyd body with the cosine measure
+    (cyc_kmeans_iter_measure): the second iteration passes the updated
+    centers' VectorWithNorm norms (1.0, DistanceMeasure.scala:477-483);
+    dense and CSR datasets vs the restatement."""
+    rng = np.random.default_rng(31)
+    n, d, k = 4000, 24, 10
+    X = rng.normal(size=(n, d)) + rng.integers(0, 5, size=(n, 1)) * 2.0
+    C = X[:k].copy()
+    ds = ResidentDataset.dense(d, n)
+    ds.append_dense(X)
+    xn = oracle.row_norms(X)
+    cn = oracle.row_norms(C)
+    for it in range(2):
+        sums, wsum, cost, assign = ds.kmeans_iter(C, want_assign=True, distanceMeasure="cosine",
+                                                  center_norms=None if it == 0 else cn)
+        ref = oracle.cos_kmeans_iteration(X, xn, None, C, cn)
+        assert np.array_equal(assign, ref["assign"])
+        _rel_close(sums, ref["sums"])
+        _rel_close(wsum, ref["wsum"])
+        assert abs(cost[0] - ref["cost"]) <= 1e-10 * abs(ref["cost"])
+        C, cn = ref["centers"], ref["cnorm"]
+    # CSR rows, every one with stored nonzeros (the cosine assert needs |x| > 0)
+    rp, ci, vv = [0], [], []
+    for _ in range(n):
+        cols = np.sort(rng.choice(d, size=int(rng.integers(1, 9)), replace=False))
+        ci += list(cols)
+        vv += list(rng.uniform(0.1, 1.0, size=cols.size))
+        rp.append(len(ci))
+    rp, ci, vv = np.array(rp, np.int64), np.array(ci, np.int32), np.array(vv)
+    dcs = ResidentDataset.csr(d, n, int(rp[-1]))
+    dcs.append_csr(rp, ci, vv)
+    C2 = rng.normal(size=(k, d))
+    sums, wsum, cost, assign = dcs.kmeans_iter(C2, want_assign=True, distanceMeasure="cosine")
+    c2n = oracle.row_norms(C2)
+    xn2 = oracle.row_norms_csr(rp, vv)
+    ra, rd, rs, rw, rc = oracle.cos_kmeans_partition_sparse((rp, ci, vv, d), xn2, None, C2, c2n,
+                                                            oracle.cos_stats(C2, c2n))
+    assert np.array_equal(assign, ra)
+    _rel_close(sums, rs)
+    # a zero-length row: the reference's AssertionError
+    rp0 = np.array([0, 0, 1], np.int64)
+    dz = ResidentDataset.csr(d, 2, 1)
+    dz.append_csr(rp0, np.array([3], np.int32), np.array([1.0]))
+    with pytest.raises(N.JavaAssertionError, match="Cosine distance is not defined"):
+        dz.kmeans_iter(rng.normal(size=(2, d)), distanceMeasure="cosine")
