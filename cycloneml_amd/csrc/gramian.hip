@@ -22,7 +22,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <type_traits>
 #include <mutex>
 
 #include "common.hpp"
@@ -106,44 +105,28 @@ __global__ __launch_bounds__(GT, 2) void k_gram_tiles(
     }
   };
 
-  // On a diagonal tile only the upper triangle is used (k_gram_fold reads
-  // i <= j): the wave below the diagonal (wy > wx) multiplies nothing and the
-  // two on it skip their 16 x 16 blocks below it (qa > qb) -- 28 of the
-  // tile's 64 blocks, ~10 % of the launch's MFMAs at p = 1024.  The mode is
-  // wave-uniform; each mode is its own copy of the loop.
-  const int mode = ti != tj ? 0 : (wy == wx ? 1 : (wy < wx ? 0 : 2));
-  auto sweep = [&](auto MODE) {
-    constexpr int M = decltype(MODE)::value;
-    if (r0 < r1) load(r0);
-    for (int64_t rb = r0; rb < r1; rb += KC) {
-      __syncthreads();
-      store();
-      __syncthreads();
-      if (rb + KC < r1) load(rb + KC);
-      if constexpr (M != 2) {
+  if (r0 < r1) load(r0);
+  for (int64_t rb = r0; rb < r1; rb += KC) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (rb + KC < r1) load(rb + KC);
 #pragma unroll
-        for (int kk = 0; kk < KC; kk += 4) {
-          double a[4], b[4];
-          const int krow = kk + (lane >> 4);
+    for (int kk = 0; kk < KC; kk += 4) {
+      double a[4], b[4];
+      const int krow = kk + (lane >> 4);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            a[q] = Ai[krow * LDSW + wy * 64 + q * 16 + (lane & 15)];
-            b[q] = Aj[krow * LDSW + wx * 64 + q * 16 + (lane & 15)];
-          }
-#pragma unroll
-          for (int qa = 0; qa < 4; ++qa)
-#pragma unroll
-            for (int qb = 0; qb < 4; ++qb)
-              if (M == 0 || qa <= qb)
-                acc[qa][qb] =
-                    __builtin_amdgcn_mfma_f64_16x16x4f64(a[qa], b[qb], acc[qa][qb], 0, 0, 0);
-        }
+      for (int q = 0; q < 4; ++q) {
+        a[q] = Ai[krow * LDSW + wy * 64 + q * 16 + (lane & 15)];
+        b[q] = Aj[krow * LDSW + wx * 64 + q * 16 + (lane & 15)];
       }
+#pragma unroll
+      for (int qa = 0; qa < 4; ++qa)
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb)
+          acc[qa][qb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[qa], b[qb], acc[qa][qb], 0, 0, 0);
     }
-  };
-  if (mode == 0) sweep(std::integral_constant<int, 0>{});
-  else if (mode == 1) sweep(std::integral_constant<int, 1>{});
-  else sweep(std::integral_constant<int, 2>{});
+  }
 
   // slab layout: [split][tilepair][i (128)][j (128)]
   const int pairs = tilesPerSide * (tilesPerSide + 1) / 2;
