@@ -357,19 +357,26 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
     }
     r.cum[kTileWaves] = acc;
   };
-  // element of virtual position p (p < cum[8])
-  auto elem = [&](const GradRun& r, uint32_t p) {
+  // element of virtual position p (p < cum[8]): p + rel[k] - cum[k] for the
+  // piece k holding p, as p + rel[0] plus the (uniform, modulo 2^32) steps
+  // of the pieces it has passed -- a compare, a select and an add per piece
+  // (the steps are scalar work, once per run)
+  auto elem = [&](const GradRun& r, const uint32_t (&step)[kTileWaves], uint32_t p) {
     uint32_t s = r.rel[0] + p;
 #pragma unroll
-    for (int kk = 1; kk < kTileWaves; ++kk)
-      s = p >= r.cum[kk] ? r.rel[kk] + (p - r.cum[kk]) : s;
+    for (int kk = 1; kk < kTileWaves; ++kk) s += p >= r.cum[kk] ? step[kk] : 0u;
     return r.base + s;
   };
   auto load_run = [&](const GradRun& r, uint32_t p0, uint32_t (&ix)[kCap], double (&vx)[kCap]) {
+    uint32_t step[kTileWaves];
+    step[0] = 0;
+#pragma unroll
+    for (int k = 1; k < kTileWaves; ++k)
+      step[k] = (r.rel[k] - r.cum[k]) - (r.rel[k - 1] - r.cum[k - 1]);
 #pragma unroll
     for (int j = 0; j < kCap; ++j) {
       const uint32_t p = p0 + j * 64 + lane;
-      const int64_t s = p < r.cum[kTileWaves] ? elem(r, p) : 0;   // masked lanes: element 0
+      const int64_t s = p < r.cum[kTileWaves] ? elem(r, step, p) : 0;   // masked lanes: element 0
       ix[j] = __builtin_nontemporal_load(vidx + s);
       vx[j] = __builtin_nontemporal_load(vvals + s);
     }
