@@ -368,13 +368,10 @@ class KMeans:
         """The initial centers of a run without an initial model
         (KMeans.scala:250-259): initRandom or initKMeansParallel over the
         shard split into Spark partitions at partition_starts (default: one
-        partition).  One process only: the driver-side sampling sees every
-        partition."""
+        partition).  Across ranks every process passes its own shard and
+        partitions; the partitions are numbered in rank order and the
+        driver-side sampling sees all of them (kmeans_init)."""
         from . import kmeans_init
-        if parallel.world()[1] > 1:
-            raise N.IllegalArgumentException(
-                "the k-means|| / random initialisation runs on one process; pass "
-                "setInitialModel for a multi-GPU run")
         n = int(X.shape[0])
         starts = np.asarray([0, n] if partition_starts is None else partition_starts,
                             dtype=np.int64)

@@ -256,28 +256,74 @@ def _seq_sum(a) -> float:
     return s
 
 
+class _Shards:
+    """The Spark partitions of every rank's shard, numbered in rank order
+    (rank r's partitions follow rank r-1's), and the rank's place in them."""
+
+    def __init__(self, partition_starts):
+        from . import parallel
+        starts = np.asarray(partition_starts, dtype=np.int64)
+        self.local_starts = starts
+        lens = [int(v) for v in np.diff(starts)]
+        every = parallel.allgather_object(lens)
+        rank = parallel.world()[0]
+        self.lens = [m for r in every for m in r]
+        self.first_partition = sum(len(r) for r in every[:rank])
+        self.row_offset = sum(sum(r) for r in every[:rank])
+        self.rows = int(starts[-1])
+
+    def rows_at(self, X, positions) -> np.ndarray:
+        """The rows at global positions (any order), gathered from the ranks
+        that hold them."""
+        from . import parallel
+        pos = np.asarray(positions, dtype=np.int64)
+        mine = np.nonzero((pos >= self.row_offset) & (pos < self.row_offset + self.rows))[0]
+        local = X[torch_index(pos[mine] - self.row_offset, X.device)].cpu().numpy() \
+            if mine.size else None
+        out = np.empty((pos.size, int(X.shape[1])))
+        for got in parallel.allgather_object((mine, local)):
+            if got[0].size:
+                out[got[0]] = got[1]
+        return out
+
+    def concat(self, rows: np.ndarray) -> np.ndarray:
+        """`collect()` of per-partition results: every rank's rows in rank
+        (= partition) order."""
+        from . import parallel
+        parts = parallel.allgather_object(rows)
+        return np.concatenate(parts) if parts else rows
+
+
+def torch_index(idx, device):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(idx, dtype=np.int64)).to(device)
+
+
 def init_random(X, k: int, seed: int, partition_starts) -> np.ndarray:
     """KMeans.initRandom (KMeans.scala:354-358)."""
     from .clustering import xorshift_next_int
-    lens = np.diff(np.asarray(partition_starts, dtype=np.int64))
-    idx = take_sample_indices(lens, k, xorshift_next_int(seed))
-    rows = X[np.asarray(idx, dtype=np.int64)].cpu().numpy() if idx else np.empty((0, X.shape[1]))
+    sh = _Shards(partition_starts)
+    idx = take_sample_indices(sh.lens, k, xorshift_next_int(seed))
+    rows = sh.rows_at(X, idx) if idx else np.empty((0, X.shape[1]))
     return _distinct_rows(rows)
 
 
 def init_kmeans_parallel(X, k: int, seed: int, steps: int, partition_starts,
                          distanceMeasure: str = "euclidean", xnorm=None) -> np.ndarray:
-    """KMeans.initKMeansParallel (KMeans.scala:370-432) on one shard: the
-    cost passes, the draws and the candidate counts on the device, the
-    sampling of the first center and LocalKMeans on the host."""
+    """KMeans.initKMeansParallel (KMeans.scala:370-432) over the ranks'
+    shards: the cost passes, the draws and the candidate counts on each
+    rank's device, the sums and counts merged across ranks, the sampling of
+    the first center and LocalKMeans on the host (identically on every
+    rank, as the reference's driver)."""
     import torch
+    from . import parallel
     from .clustering import KMeans, KMeansModel, xorshift_next_int
-    starts = np.asarray(partition_starts, dtype=np.int64)
+    sh = _Shards(partition_starts)
     s = xorshift_next_int(seed)
-    first = take_sample_indices(np.diff(starts), 1, s)
+    first = take_sample_indices(sh.lens, 1, s)
     if not first:
         raise N.IllegalArgumentException("requirement failed: No samples available from data")
-    centers = [X[first[0]].cpu().numpy()]
+    centers = [sh.rows_at(X, first)[0]]
     new = np.array(centers)
     costs = None
     total = 0.0
@@ -285,12 +331,14 @@ def init_kmeans_parallel(X, k: int, seed: int, steps: int, partition_starts,
         if new.shape[0] > 0:       # no new centers: every min(pointCost, cost) is the cost
             costs, total = KMeans.updateParallelCosts(X, new, costs, xnorm=xnorm,
                                                       distanceMeasure=distanceMeasure)
-        mask = KMeans.parallelSample(costs, total, s, step, k, starts)
-        new = X[mask.bool()].cpu().numpy()
+        mask = KMeans.parallelSample(costs, total, s, step, k, sh.local_starts,
+                                     sh.first_partition)
+        new = sh.concat(X[mask.bool()].cpu().numpy())
         centers.extend(list(new))
     distinct = _distinct_rows(np.array(centers))
     if distinct.shape[0] <= k:
         return distinct
     idx, _ = KMeansModel(distinct, distanceMeasure=distanceMeasure).pointCosts(X, xnorm)
     counts = torch.bincount(idx.long(), minlength=distinct.shape[0]).cpu().numpy()
+    counts = np.sum(parallel.allgather_object(counts), axis=0)     # countByValue
     return local_kmeans_pp(distinct, counts.astype(np.float64), k, 30, 0, X.device)

@@ -169,6 +169,17 @@ def broadcast_(t, src=0, group=None):
     return t
 
 
+def allgather_object(obj) -> list:
+    """Every rank's `obj` in rank order (the driver's `collect()` of small
+    host data: partition lengths, sampled candidate rows, counts)."""
+    d = _dist()
+    if d is None or d.get_world_size() == 1:
+        return [obj]
+    out = [None] * d.get_world_size()
+    d.all_gather_object(out, obj)
+    return out
+
+
 def max_over_ranks(x: float, device=None) -> float:
     import torch
     d = _dist()

@@ -198,8 +198,78 @@ def _gramian_rank(rank, world):
     return bool(np.allclose(U.cpu().numpy(), oracle.gramian_partition(X), rtol=1e-12))
 
 
+def _init_reference(X, dev, part_starts, shard_rows, k, s, mode):
+    """The host composition of KMeans.initRandom / initKMeansParallel over all
+    partitions (numbered in rank order), with sumCosts the rank-order sum of
+    the ranks' device sums (the all-reduce)."""
+    import torch
+    from cycloneml_amd.kmeans_init import take_sample_indices
+    n = X.shape[0]
+    lens = np.diff(part_starts)
+    if mode == "random":
+        return X[take_sample_indices(lens, k, s)]
+    cands = [X[take_sample_indices(lens, 1, s)[0]]]
+    new = np.array(cands)
+    costs = np.full(n, np.inf)
+    for step in range(2):
+        _, pc, _ = oracle.point_costs(X, oracle.row_norms(X), new, oracle.row_norms(new))
+        costs = np.minimum(pc, costs)
+        total = 0.0
+        for a, b in shard_rows:
+            total += float(torch.from_numpy(costs[a:b].copy()).to(dev).sum().item())
+        mask = oracle.kmeans_parallel_sample(costs, part_starts, 0, s, step, k, total)
+        new = X[mask.astype(bool)]
+        cands.extend(new)
+    uniq = []
+    for c in cands:
+        if not any(np.array_equal(c, u) for u in uniq):
+            uniq.append(c)
+    uniq = np.array(uniq)
+    if uniq.shape[0] <= k:
+        return uniq
+    a_, _, _ = oracle.point_costs(X, oracle.row_norms(X), uniq, oracle.row_norms(uniq))
+    wts = np.bincount(a_, minlength=uniq.shape[0]).astype(np.float64)
+    return oracle.local_kmeans_pp(uniq, wts, k, 30, 0)
+
+
+def _kmeans_init_rank(rank, world):
+    """k-means|| and random initialisation across two ranks
+    (KMeans.scala:354-432): each rank holds a shard split into its own Spark
+    partitions; the initial centers on every rank equal the one-driver
+    composition over all partitions, and the Lloyd run from them matches a
+    single-process run from those centers."""
+    import torch
+    from cycloneml_amd import parallel
+    from cycloneml_amd.clustering import KMeans, KMeansModel, xorshift_next_int
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(5)
+    n, d, k = 4001, 8, 5
+    X = rng.normal(size=(n, d)) + rng.integers(0, 5, size=(n, 1)) * 4.0
+    shard_rows = [parallel.shard_bounds(n, r, world) for r in range(world)]
+    local_parts = [[0, 700, 2001], [0, 333, 999, 1400, 2000]]
+    glob = [0]
+    for r in range(world):
+        glob += [shard_rows[r][0] + v for v in local_parts[r][1:]]
+    a, b = shard_rows[rank]
+    assert local_parts[rank][-1] == b - a
+    Xd = torch.from_numpy(X[a:b].copy()).to(dev)
+    ok = True
+    for mode in ("k-means||", "random"):
+        km = KMeans(k=k, maxIterations=20).setSeed(31).setInitializationMode(mode)
+        C0 = km.initial_centers(Xd, partition_starts=local_parts[rank])
+        ref = _init_reference(X, dev, np.array(glob, dtype=np.int64), shard_rows, k,
+                              xorshift_next_int(31), mode)
+        ok = ok and C0.shape == ref.shape and bool(np.array_equal(C0, ref))
+        m = km.run(Xd, partition_starts=local_parts[rank])
+        single = KMeans(k=C0.shape[0], maxIterations=20).setInitialModel(
+            KMeansModel(C0)).run(torch.from_numpy(X).to(dev))
+        ok = ok and bool(np.allclose(m.clusterCenters, single.clusterCenters, rtol=1e-12,
+                                     atol=1e-12))
+    return ok
+
+
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("fn", [_kmeans_rank, _lr_rank, _gramian_rank])
+@pytest.mark.parametrize("fn", [_kmeans_rank, _lr_rank, _gramian_rank, _kmeans_init_rank])
 def test_two_ranks_device_kernels_meet_the_collective(fn):
     out = _run(fn)
     assert out == {0: True, 1: True}, out

@@ -120,7 +120,29 @@ def _gramian_rank(rank, world):
     return bool(np.allclose(U.numpy(), oracle.gramian_partition(X), rtol=1e-13))
 
 
-@pytest.mark.parametrize("fn", [_kmeans_rank, _aggregator_rank, _gramian_rank])
+def _init_shards_rank(rank, world):
+    """The host side of the multi-rank k-means|| / random initialisation
+    (kmeans_init._Shards): the partitions numbered in rank order, the rows at
+    global sampled positions gathered from their owners, collect() in rank
+    order, and takeSample over the global partition lengths."""
+    from cycloneml_amd import parallel
+    from cycloneml_amd.kmeans_init import _Shards, take_sample_indices
+    n, d = 901, 3
+    X = np.arange(n * d, dtype=np.float64).reshape(n, d)
+    a, b = parallel.shard_bounds(n, rank, world)
+    parts = [[0, 100, 451], [0, 0, 200, 450]][rank]
+    sh = _Shards(parts)
+    ok = sh.lens == [100, 351, 0, 200, 250] and sh.first_partition == (0, 2)[rank]
+    ok = ok and sh.row_offset == a and sh.rows == b - a
+    pos = take_sample_indices(sh.lens, 37, 99)
+    got = sh.rows_at(torch.from_numpy(X[a:b].copy()), pos)
+    ok = ok and np.array_equal(got, X[pos])
+    cat = sh.concat(X[a:b][::100])
+    return bool(ok and np.array_equal(cat, np.concatenate([X[0:451][::100], X[451:][::100]])))
+
+
+@pytest.mark.parametrize("fn", [_kmeans_rank, _aggregator_rank, _gramian_rank,
+                                _init_shards_rank])
 def test_two_rank_merge(fn):
     out = _run(fn)
     assert out == {0: True, 1: True}, out
