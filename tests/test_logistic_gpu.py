@@ -66,7 +66,10 @@ def test_binary_vs_oracle(cuda, sparse, fi, fwm, n, F):
 
 @pytest.mark.parametrize("fi,fwm", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("n,F,C", [(1, 2, 3), (300, 5, 3), (2000, 64, 10), (1500, 100, 17),
-                                   (5000, 512, 100), (700, 33, 128)])
+                                   (5000, 512, 100), (700, 33, 128),
+                                   # several 256-row tiles per workgroup: the DMA
+                                   # ring and label slots across tile boundaries
+                                   (200_003, 5, 3), (140_000, 16, 10), (70_001, 40, 17)])
 def test_multinomial_vs_oracle(cuda, fi, fwm, n, F, C):
     from cycloneml_amd.optim import DeviceInstanceBlock, MultinomialLogisticBlockAggregator
     rng = np.random.default_rng(n + F * 3 + C)
