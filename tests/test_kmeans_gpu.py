@@ -229,7 +229,10 @@ def test_nan_norm_require(cuda, case, path):
 @pytest.mark.parametrize("use_rows", [False, True])
 @pytest.mark.parametrize("n,d,k,weighted", [(5000, 16, 12, False), (20000, 256, 64, True),
                                             (3000, 7, 1, False), (4000, 600, 9, True),
-                                            (1500, 1100, 5, False)])
+                                            (1500, 1100, 5, False),
+                                            # >= 2^20 rows with the row image: the
+                                            # parts pipeline (sums stream)
+                                            (1_200_001, 32, 40, True)])
 def test_lloyd_iteration(cuda, n, d, k, weighted, use_rows):
     import torch
     from cycloneml_amd.clustering import row_norms
@@ -546,7 +549,8 @@ def test_rows_image_guard(cuda):
 
 
 @pytest.mark.parametrize("n,d,k,weighted", [(5000, 16, 12, False), (20000, 256, 64, True),
-                                            (3000, 300, 7, True), (2000, 700, 5, False)])
+                                            (3000, 300, 7, True), (2000, 700, 5, False),
+                                            (1_100_003, 256, 64, True), (1_048_579, 100, 3, False)])
 def test_lloyd_iteration_no_row_costs(cuda, n, d, k, weighted):
     """accumulate without per-row outputs (the training loop's call): the
     streaming cluster-sum pass folds w (c - x)^2 per dimension; sums, weights
