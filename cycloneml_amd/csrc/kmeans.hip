@@ -939,18 +939,22 @@ __global__ __launch_bounds__(kS3Threads, 2) void k_kmeans_assign3(
 }
 
 // EuclideanDistanceMeasure.findClosest with statistics, DistanceMeasure.scala:
-// 282-313, for the rows the screens could not decide.  One wave per queued row.
-// The reference loop visits centers in order; its state (bestDistance,
-// bestIndex) changes only at an update, so the wave evaluates 64 consecutive
-// centers at once against the current state: every lane whose center the
-// loop would visit computes the exact sequential sqdist (Vectors.scala:580-587,
-// the same operation order as the reference), a ballot finds the first lane
+// 282-313, for the rows the screens could not decide.  One workgroup per
+// queued row: the exact sequential sqdist (Vectors.scala:580-587, the same
+// operation order as the reference) of every center, 1024 at a time, then
+// the replay on one wave.  The reference loop visits centers in order; its
+// state (bestDistance, bestIndex) changes only at an update, so the wave
+// evaluates 64 consecutive centers at once against the current state: a
+// ballot over the lanes whose center the loop would visit finds the first lane
 // whose visit changes the state (a `return` at :303 or an update at :304-306),
 // the state advances to it, and the lanes after it are re-evaluated against
 // the new state (reusing the distances already computed).  Lanes before the
 // first event have no side effect in the reference either, so the returned
 // (index, distance) is the reference's, bit for bit; distances of centers the
 // reference would not visit may be computed speculatively and are discarded.
+constexpr int kExactChunk = 1024;   // centers whose distances one pass stages in LDS
+constexpr int kExactX = 1280;       // widest row staged in LDS
+
 __global__ __launch_bounds__(256) void k_assign_exact(
     const double* __restrict__ X, const double* __restrict__ xnorm, int d,
     const double* __restrict__ C, const double* __restrict__ Ct, int kpad,
@@ -958,61 +962,92 @@ __global__ __launch_bounds__(256) void k_assign_exact(
     const double* __restrict__ stats, const int32_t* __restrict__ slowList,
     const unsigned int* __restrict__ slowCount, int32_t* __restrict__ assign,
     double* __restrict__ cost) {
+  // One workgroup per listed row.  A distance is a pure function of (center,
+  // row), so the workgroup first computes Vectors.sqdist(center, x) -- in
+  // order j = 0..d-1 (Vectors.scala:580-587) -- for a chunk of 1024 centers
+  // at once (thread t: centers t, t + 256, ..; center i read from the
+  // transposed copy, coalesced over the threads), and wave 0 then replays the
+  // reference loop's visits and events over them.
+  __shared__ double xs[kExactX];
+  __shared__ double dds[kExactChunk];
+  __shared__ int doneS;
   const unsigned cnt = *slowCount;
-  const int lane = threadIdx.x & 63;
-  const unsigned wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const unsigned nw = (gridDim.x * blockDim.x) >> 6;
-  for (unsigned idx = wid; idx < cnt; idx += nw) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  // stats == nullptr: findClosest(centers, point) (:318-340), best from +inf
+  const bool ns = stats == nullptr;
+  for (unsigned idx = blockIdx.x; idx < cnt; idx += gridDim.x) {
     const int64_t r = slowList[idx];
     const double* x = X + r * d;
     const double xn = xnorm[r];
-    // stats == nullptr: findClosest(centers, point) (:318-340), best from +inf
-    const bool ns = stats == nullptr;
-    double best = ns ? __builtin_inf() : seq_sqdist(C, x, d);   // :286
+    __syncthreads();   // the previous row's reads of xs / dds are done
+    const bool xl = d <= kExactX;
+    if (xl)
+      for (int j = tid; j < d; j += 256) xs[j] = x[j];
+    const double* xv = xl ? xs : x;
+    double best = __builtin_inf();   // wave 0's replay state
     int bi = 0;
-    bool done = !ns && best < stats[0];                // :287
-    for (int i0 = ns ? 0 : 1; !done && i0 < k; i0 += 64) {
-      const int i = i0 + lane;
-      const bool valid = i < k;
-      double lb = __builtin_inf(), sii = 0.0;
-      if (valid) {
-        const double nd = dsub(cnorm[i], xn);     // :294-295
-        lb = dmul(nd, nd);
-        sii = ns ? 0.0 : stats[iut(i, i)];
-      }
-      double dd = 0.0;
-      bool have = false;
-      int pos = 0;
-      for (;;) {
-        const bool visit = valid && lane >= pos && lb < best && (ns || stats[iut(i, bi)] < best);
-        if (visit && !have) {
-          // Vectors.sqdist(center, x) in order j = 0..d-1 (Vectors.scala:
-          // 580-587), center i read from the transposed copy: the visiting
-          // lanes' loads of one j are one coalesced row of Ct
-          const double* ci = Ct + i;
-          double sq = 0.0;
-          for (int j = 0; j < d; ++j) {
-            const double sc = dsub(ci[(int64_t)j * kpad], x[j]);
-            sq = dadd(sq, dmul(sc, sc));
+    bool done = false;
+    for (int c0 = 0; c0 < k; c0 += kExactChunk) {
+      __syncthreads();   // xs written; the previous chunk's replay is done
+      double acc[kExactChunk / 256];
+#pragma unroll
+      for (int u = 0; u < kExactChunk / 256; ++u) acc[u] = 0.0;
+#pragma unroll 4
+      for (int j = 0; j < d; ++j) {
+        const double xj = xv[j];
+        const double* row = Ct + (int64_t)j * kpad + c0 + tid;
+#pragma unroll
+        for (int u = 0; u < kExactChunk / 256; ++u)
+          if (c0 + tid + 256 * u < k) {
+            const double sc = dsub(row[256 * u], xj);
+            acc[u] = dadd(acc[u], dmul(sc, sc));
           }
-          dd = sq;
-          have = true;
-        }
-        const bool brk = !ns && visit && dd < sii;
-        const bool ev = visit && (brk || dd < best);
-        const unsigned long long m = __ballot(ev);
-        if (!m) break;
-        const int f = __ffsll((long long)m) - 1;
-        best = __shfl(dd, f);
-        bi = i0 + f;
-        if (__shfl((int)brk, f)) {
-          done = true;
-          break;
-        }
-        pos = f + 1;
       }
+#pragma unroll
+      for (int u = 0; u < kExactChunk / 256; ++u)
+        if (c0 + tid + 256 * u < k) dds[tid + 256 * u] = acc[u];
+      __syncthreads();
+      if (tid < 64) {
+        int first = c0;
+        if (c0 == 0 && !ns) {
+          best = dds[0];                      // :286
+          done = best < stats[0];             // :287
+          first = 1;
+        }
+        const int end = min(k, c0 + kExactChunk);
+        for (int i0 = first; !done && i0 < end; i0 += 64) {
+          const int i = i0 + lane;
+          const bool valid = i < end;
+          double lb = __builtin_inf(), sii = 0.0, dd = 0.0;
+          if (valid) {
+            const double nd = dsub(cnorm[i], xn);     // :294-295
+            lb = dmul(nd, nd);
+            sii = ns ? 0.0 : stats[iut(i, i)];
+            dd = dds[i - c0];
+          }
+          int pos = 0;
+          for (;;) {
+            const bool visit = valid && lane >= pos && lb < best && (ns || stats[iut(i, bi)] < best);
+            const bool brk = !ns && visit && dd < sii;
+            const bool ev = visit && (brk || dd < best);
+            const unsigned long long m = __ballot(ev);
+            if (!m) break;
+            const int f = __ffsll((long long)m) - 1;
+            best = __shfl(dd, f);
+            bi = i0 + f;
+            if (__shfl((int)brk, f)) {
+              done = true;
+              break;
+            }
+            pos = f + 1;
+          }
+        }
+        if (tid == 0) doneS = done;
+      }
+      __syncthreads();
+      if (doneS) break;
     }
-    if (lane == 0) {
+    if (tid == 0) {
       assign[r] = bi;
       if (cost) cost[r] = best;
     }
@@ -1156,6 +1191,7 @@ __global__ void k_scatter(const int32_t* __restrict__ assign, int64_t n, int k,
                           int32_t* __restrict__ perm) {
   extern __shared__ int64_t pos[];
   const int lane = threadIdx.x;
+  const int kb = 32 - __builtin_clz((unsigned)max(k - 1, 1));   // bits of a cluster index
   for (int c = lane; c < k; c += 64) pos[c] = cstart[c] + tileOff[(int64_t)blockIdx.x * k + c];
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * kSortTile;
@@ -1163,14 +1199,15 @@ __global__ void k_scatter(const int32_t* __restrict__ assign, int64_t n, int k,
   for (int64_t base = r0; base < r1; base += 64) {
     const int64_t r = base + lane;
     const int c = (r < r1) ? assign[r] : -1;
-    int prior = 0, last = lane;
-    for (int j = 0; j < 64; ++j) {
-      int cj = __shfl(c, j);
-      if (cj == c) {
-        if (j < lane) ++prior;
-        last = j;
-      }
+    // the lanes holding the same cluster: one ballot per bit of the index
+    unsigned long long m = __ballot(c >= 0);
+    for (int b = 0; b < kb; ++b) {
+      const bool bit = (c >> b) & 1;
+      const unsigned long long bal = __ballot(bit);
+      m &= bit ? bal : ~bal;
     }
+    const int prior = __popcll(m & ((1ull << lane) - 1));
+    const int last = 63 - __clzll(m);
     int64_t p = (c >= 0) ? pos[c] + prior : 0;
     __builtin_amdgcn_wave_barrier();
     if (c >= 0) {
@@ -1922,7 +1959,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
     p->lastLimb3 = twoPass ? (int64_t)h_limb3 : -1;
     p->lastCands = twoPass ? (int64_t)h_cand : -1;
     if (h_slow) {
-      hipLaunchKernelGGL(k_assign_exact, dim3((unsigned)std::min<unsigned>((h_slow + 3) / 4, 4096)), dim3(256), 0, st, X, xnorm,
+      hipLaunchKernelGGL(k_assign_exact, dim3((unsigned)std::min<unsigned>(h_slow, 4096)), dim3(256), 0, st, X, xnorm,
                          p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm, p->k, statsArg,
                          (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr,
                          assign, cost);
