@@ -992,16 +992,28 @@ __global__ __launch_bounds__(256) void k_assign_exact(
       double acc[kExactChunk / 256];
 #pragma unroll
       for (int u = 0; u < kExactChunk / 256; ++u) acc[u] = 0.0;
-#pragma unroll 4
-      for (int j = 0; j < d; ++j) {
-        const double xj = xv[j];
-        const double* row = Ct + (int64_t)j * kpad + c0 + tid;
+      // 16 dimensions' loads go out before their adds (the add chains are
+      // sequential; the loads are not)
+      for (int j0 = 0; j0 < d; j0 += 16) {
+        double cv[16][kExactChunk / 256];
 #pragma unroll
-        for (int u = 0; u < kExactChunk / 256; ++u)
-          if (c0 + tid + 256 * u < k) {
-            const double sc = dsub(row[256 * u], xj);
-            acc[u] = dadd(acc[u], dmul(sc, sc));
+        for (int jj = 0; jj < 16; ++jj) {
+          const double* row = Ct + (int64_t)(j0 + jj) * kpad + c0 + tid;
+#pragma unroll
+          for (int u = 0; u < kExactChunk / 256; ++u)
+            cv[jj][u] = (j0 + jj < d && c0 + tid + 256 * u < k) ? row[256 * u] : 0.0;
+        }
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+          if (j0 + jj < d) {
+            const double xj = xv[j0 + jj];
+#pragma unroll
+            for (int u = 0; u < kExactChunk / 256; ++u) {
+              const double sc = dsub(cv[jj][u], xj);
+              acc[u] = dadd(acc[u], dmul(sc, sc));
+            }
           }
+        }
       }
 #pragma unroll
       for (int u = 0; u < kExactChunk / 256; ++u)
