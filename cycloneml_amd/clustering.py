@@ -511,16 +511,44 @@ class KMeans:
         plan.close()
         return KMeansModel(C.cpu().numpy(), cost, iteration, self.distanceMeasure)
 
+    def initial_centers_csr(self, rowptr, colidx, values, numFeatures, xnorm=None,
+                            partition_starts=None):
+        """initial_centers for a CSR shard (dense centers)."""
+        from . import kmeans_init
+        _decode_measure(self.distanceMeasure)
+        if self.distanceMeasure != EUCLIDEAN:
+            raise N.IllegalArgumentException(
+                "the device path runs the cosine measure on dense rows only")
+        n = int(rowptr.shape[0]) - 1
+        starts = np.asarray([0, n] if partition_starts is None else partition_starts,
+                            dtype=np.int64)
+        if self.initializationMode == KMeans.RANDOM:
+            return kmeans_init.init_random_csr(rowptr, colidx, values, int(numFeatures), self.k,
+                                               self.seed, starts)
+        return kmeans_init.init_kmeans_parallel_csr(rowptr, colidx, values, int(numFeatures),
+                                                    self.k, self.seed,
+                                                    self.initializationSteps, starts, xnorm)
+
     def run_csr(self, rowptr, colidx, values, numFeatures, weights=None, stream=None,
-                iteration_callback=None):
+                iteration_callback=None, partition_starts=None):
         """Lloyd's algorithm over sparse points (libsvm input, KMeansExample):
         CSR rowptr (int64), colidx (int32), values (fp64) CUDA tensors; the
-        centers are dense, as in the reference after the first iteration."""
-        torch = _torch()
+        centers are dense, as in the reference after the first iteration.
+        Without an initial model the centers come from initial_centers_csr."""
         if self.initialModel is None:
-            raise N.IllegalArgumentException(
-                "initialModel is required on the device path (setInitialModel); "
-                "k-means|| / random initialisation are host-side (SURVEY.md 8f)")
+            xn = row_norms_csr(rowptr, values, stream=stream)
+            C0 = self.initial_centers_csr(rowptr, colidx, values, numFeatures, xn,
+                                          partition_starts)
+            self.initialModel = KMeansModel(C0, distanceMeasure=self.distanceMeasure)
+            k0 = self.k
+            self.k = C0.shape[0]
+            try:
+                return self.run_csr(rowptr, colidx, values, numFeatures, weights, stream,
+                                    iteration_callback)
+            finally:
+                self.initialModel = None
+                self.k = k0
+        torch = _torch()
         dev = values.device
         d, k = int(numFeatures), self.k
         n = int(rowptr.shape[0]) - 1

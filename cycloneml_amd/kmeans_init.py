@@ -193,16 +193,32 @@ def _sqdist_to(points: np.ndarray, c: np.ndarray) -> np.ndarray:
 
 
 def local_kmeans_pp(points: np.ndarray, weights: np.ndarray, k: int, max_iterations: int,
-                    seed: int, device) -> np.ndarray:
+                    seed: int, device, closest=None) -> np.ndarray:
     """LocalKMeans.kMeansPlusPlus (LocalKMeans.scala:35-134) with the
     Euclidean measure; the Lloyd rounds' findClosest (without statistics)
-    on the device, bit-exact."""
+    on the device, bit-exact.  points: dense rows.  closest(C) -> (index,
+    cost) host arrays of every point against centers C, for points that are
+    sparse in the reference (fastSquaredDistance's norm-trick branch, also
+    for the seeding costs: one center); default the dense rows themselves
+    (Vectors.sqdist)."""
     import torch
     from .clustering import KMeansModel
     points = np.ascontiguousarray(points, dtype=np.float64)
     weights = np.asarray(weights, dtype=np.float64)
     m, d = points.shape
     rand = JavaRandom(seed)
+    if closest is None:
+        pd = torch.from_numpy(points).to(device)
+
+        def closest(C):
+            idx, c = KMeansModel(C).pointCosts(pd)
+            return idx.cpu().numpy().astype(np.int64), c.cpu().numpy()
+
+        def cost_to(c):
+            return _sqdist_to(points, c)
+    else:
+        def cost_to(c):
+            return closest(c[None, :])[1]
 
     def pick_weighted():
         r = rand.next_double() * _seq_sum(weights)
@@ -214,7 +230,7 @@ def local_kmeans_pp(points: np.ndarray, weights: np.ndarray, k: int, max_iterati
 
     centers = np.empty((k, d))
     centers[0] = pick_weighted()
-    cost = _sqdist_to(points, centers[0])
+    cost = cost_to(centers[0])
     for i in range(1, k):
         total = _seq_sum(cost * weights)
         r = rand.next_double() * total
@@ -223,14 +239,13 @@ def local_kmeans_pp(points: np.ndarray, weights: np.ndarray, k: int, max_iterati
             cum += weights[j] * cost[j]
             j += 1
         centers[i] = points[0] if j == 0 else points[j - 1]
-        cost = np.minimum(_sqdist_to(points, centers[i]), cost)
-    pd = torch.from_numpy(points).to(device)
+        cost = np.minimum(cost_to(centers[i]), cost)
     old = np.full(m, -1, dtype=np.int64)
     iteration, moved = 0, True
     while moved and iteration < max_iterations:
         moved = False
-        idx, _ = KMeansModel(centers).pointCosts(pd)
-        idx = idx.cpu().numpy().astype(np.int64)
+        idx, _ = closest(centers)
+        idx = np.asarray(idx, dtype=np.int64)
         counts = np.zeros(k)
         sums = np.zeros((k, d))
         for p in range(m):
@@ -281,6 +296,18 @@ class _Shards:
         local = X[torch_index(pos[mine] - self.row_offset, X.device)].cpu().numpy() \
             if mine.size else None
         out = np.empty((pos.size, int(X.shape[1])))
+        for got in parallel.allgather_object((mine, local)):
+            if got[0].size:
+                out[got[0]] = got[1]
+        return out
+
+    def rows_of(self, gather, positions, d: int) -> np.ndarray:
+        """rows_at with a gather(local row indices) -> dense host rows."""
+        from . import parallel
+        pos = np.asarray(positions, dtype=np.int64)
+        mine = np.nonzero((pos >= self.row_offset) & (pos < self.row_offset + self.rows))[0]
+        local = gather(pos[mine] - self.row_offset) if mine.size else None
+        out = np.empty((pos.size, d))
         for got in parallel.allgather_object((mine, local)):
             if got[0].size:
                 out[got[0]] = got[1]
@@ -342,3 +369,96 @@ def init_kmeans_parallel(X, k: int, seed: int, steps: int, partition_starts,
     counts = torch.bincount(idx.long(), minlength=distinct.shape[0]).cpu().numpy()
     counts = np.sum(parallel.allgather_object(counts), axis=0)     # countByValue
     return local_kmeans_pp(distinct, counts.astype(np.float64), k, 30, 0, X.device)
+
+
+# --------------------------------------------------------------- CSR shards
+
+def csr_rows_dense(rowptr, colidx, values, d: int, rows) -> np.ndarray:
+    """Rows of a device CSR shard as dense host rows (a SparseVector's
+    toDense; explicit zeros and missing entries both 0.0)."""
+    import torch
+    rows = torch.as_tensor(np.asarray(rows, dtype=np.int64), device=values.device)
+    m = int(rows.numel())
+    out = torch.zeros((m, d), dtype=torch.float64, device=values.device)
+    if m:
+        st, en = rowptr[rows], rowptr[rows + 1]
+        lens = en - st
+        tot = int(lens.sum().item())
+        if tot:
+            rid = torch.repeat_interleave(torch.arange(m, device=values.device), lens)
+            first = torch.cumsum(lens, 0) - lens
+            flat = torch.arange(tot, device=values.device) - first[rid] + st[rid]
+            out[rid, colidx[flat].long()] = values[flat]
+    return out.cpu().numpy()
+
+
+def _csr_of_dense(rows: np.ndarray, device):
+    """Device CSR of dense rows (their nonzeros)."""
+    import torch
+    nz = rows != 0.0
+    rowptr = np.concatenate([[0], np.cumsum(nz.sum(1))]).astype(np.int64)
+    r, c = np.nonzero(nz)
+    return (torch.from_numpy(rowptr).to(device),
+            torch.from_numpy(c.astype(np.int32)).to(device),
+            torch.from_numpy(np.ascontiguousarray(rows[r, c])).to(device))
+
+
+def init_random_csr(rowptr, colidx, values, d: int, k: int, seed: int,
+                    partition_starts) -> np.ndarray:
+    """KMeans.initRandom over sparse points (centers dense)."""
+    from .clustering import xorshift_next_int
+    sh = _Shards(partition_starts)
+    idx = take_sample_indices(sh.lens, k, xorshift_next_int(seed))
+    return _distinct_rows(sh.rows_of(lambda loc: csr_rows_dense(rowptr, colidx, values, d, loc),
+                                     idx, d))
+
+
+def init_kmeans_parallel_csr(rowptr, colidx, values, d: int, k: int, seed: int, steps: int,
+                             partition_starts, xnorm=None) -> np.ndarray:
+    """KMeans.initKMeansParallel (KMeans.scala:370-432) over sparse points:
+    as init_kmeans_parallel, the cost passes fastSquaredDistance(center,
+    sparse point) on the device (cyc_kmeans_point_cost_csr_dev; dot(sparse,
+    sparse) of the reference equals dot(sparse, dense) here, the centers'
+    absent entries adding zeros), LocalKMeans over the sparse candidates."""
+    import torch
+    from . import parallel
+    from .clustering import KMeans, KMeansModel, row_norms_csr, xorshift_next_int
+    sh = _Shards(partition_starts)
+    gather = lambda loc: csr_rows_dense(rowptr, colidx, values, d, loc)   # noqa: E731
+    if xnorm is None:
+        xnorm = row_norms_csr(rowptr, values)
+    s = xorshift_next_int(seed)
+    first = take_sample_indices(sh.lens, 1, s)
+    if not first:
+        raise N.IllegalArgumentException("requirement failed: No samples available from data")
+    centers = [sh.rows_of(gather, first, d)[0]]
+    new = np.array(centers)
+    costs = None
+    total = 0.0
+    for step in range(steps):
+        if new.shape[0] > 0:
+            _, c = KMeansModel(new).pointCosts_csr(rowptr, colidx, values, xnorm)
+            costs = c if costs is None else torch.minimum(c, costs)
+            tot = costs.sum().reshape(1) if costs.numel() else torch.zeros(
+                1, dtype=torch.float64, device=values.device)
+            parallel.allreduce_(tot)
+            total = float(tot.item())
+        mask = KMeans.parallelSample(costs, total, s, step, k, sh.local_starts,
+                                     sh.first_partition)
+        new = sh.concat(gather(torch.nonzero(mask).flatten().cpu().numpy()))
+        centers.extend(list(new))
+    distinct = _distinct_rows(np.array(centers))
+    if distinct.shape[0] <= k:
+        return distinct
+    idx, _ = KMeansModel(distinct).pointCosts_csr(rowptr, colidx, values, xnorm)
+    counts = torch.bincount(idx.long(), minlength=distinct.shape[0]).cpu().numpy()
+    counts = np.sum(parallel.allgather_object(counts), axis=0)     # countByValue
+    cand = _csr_of_dense(distinct, values.device)
+    cand_norm = row_norms_csr(cand[0], cand[2])
+
+    def closest(C):
+        a, c = KMeansModel(np.asarray(C)).pointCosts_csr(*cand, cand_norm)
+        return a.cpu().numpy().astype(np.int64), c.cpu().numpy()
+
+    return local_kmeans_pp(distinct, counts.astype(np.float64), k, 30, 0, values.device,
+                           closest=closest)

@@ -836,10 +836,14 @@ def kmeans_parallel_sample(costs, part_starts, first_index, seed, step, k, sum_c
     return out
 
 
-def local_kmeans_pp(points, weights, k, max_iterations, seed):
+def local_kmeans_pp(points, weights, k, max_iterations, seed, closest=None):
     """LocalKMeans.kMeansPlusPlus (mllib/clustering/LocalKMeans.scala:35-134)
     in plain loops: k-means++ seeding with java.util.Random(seed), then
-    Lloyd rounds with EuclideanDistanceMeasure.findClosest (orc_find_closest)."""
+    Lloyd rounds with EuclideanDistanceMeasure.findClosest (orc_find_closest).
+    closest(C) -> (index, cost) of every point against centers C replaces both
+    distance steps for points that are sparse in the reference (e.g.
+    point_costs_sparse over the points' CSR: fastSquaredDistance(dense
+    center, sparse point))."""
     points = _f64(points)
     w = [float(v) for v in weights]
     m, d = points.shape
@@ -867,7 +871,10 @@ def local_kmeans_pp(points, weights, k, max_iterations, seed):
         cur += w[i]
         i += 1
     centers = [points[i - 1].copy()]
-    cost = [sqdist(points[p], centers[0]) for p in range(m)]
+    if closest is None:
+        cost = [sqdist(points[p], centers[0]) for p in range(m)]
+    else:
+        cost = [float(v) for v in closest(np.array([centers[0]]))[1]]
     for c in range(1, k):
         s = 0.0
         for p in range(m):
@@ -878,8 +885,12 @@ def local_kmeans_pp(points, weights, k, max_iterations, seed):
             cum += w[j] * cost[j]
             j += 1
         centers.append(points[0].copy() if j == 0 else points[j - 1].copy())
+        if closest is None:
+            nc = [sqdist(points[p], centers[c]) for p in range(m)]
+        else:
+            nc = [float(v) for v in closest(np.array([centers[c]]))[1]]
         for p in range(m):
-            cost[p] = min(sqdist(points[p], centers[c]), cost[p])
+            cost[p] = min(nc[p], cost[p])
     old = [-1] * m
     it, moved = 0, True
     while moved and it < max_iterations:
@@ -888,8 +899,12 @@ def local_kmeans_pp(points, weights, k, max_iterations, seed):
         cn = row_norms(C)
         counts = [0.0] * k
         sums = np.zeros((k, d))
+        ids = None if closest is None else closest(C)[0]
         for p in range(m):
-            idx, _ = find_closest(C, cn, points[p], norm2(points[p]))
+            if ids is None:
+                idx, _ = find_closest(C, cn, points[p], norm2(points[p]))
+            else:
+                idx = int(ids[p])
             if w[p] != 0.0:
                 sums[idx] = sums[idx] + w[p] * points[p]
             counts[idx] += w[p]

@@ -172,3 +172,85 @@ def test_kmeans_run_without_initial_model(cuda, mode):
     m2 = km2.run(Xd)
     np.testing.assert_array_equal(m1.clusterCenters, m2.clusterCenters)
     assert m1.numIter == m2.numIter
+
+
+def _sparse_data(rng, n, d):
+    """CSR rows with ~8 nonzeros each around a few cluster patterns."""
+    rows = []
+    for _ in range(n):
+        c = rng.integers(0, 4)
+        cols = np.unique(np.concatenate([rng.choice(d, size=6, replace=False),
+                                         [c * 5, c * 5 + 1]]))
+        vals = rng.normal(size=cols.size) + (cols // 5 == c) * 4.0
+        rows.append((cols, vals))
+    rowptr = np.concatenate([[0], np.cumsum([r[0].size for r in rows])]).astype(np.int64)
+    colidx = np.concatenate([r[0] for r in rows]).astype(np.int32)
+    vals = np.concatenate([r[1] for r in rows])
+    dense = np.zeros((n, d))
+    for i, (c, v) in enumerate(rows):
+        dense[i, c] = v
+    return (rowptr, colidx, vals), dense
+
+
+def _csr_of(rows):
+    nz = rows != 0.0
+    rp = np.concatenate([[0], np.cumsum(nz.sum(1))]).astype(np.int64)
+    r, c = np.nonzero(nz)
+    return rp, c.astype(np.int32), rows[r, c]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["k-means||", "random"])
+def test_kmeans_run_csr_without_initial_model(cuda, mode):
+    """KMeans.run over sparse points without an initial model: the initial
+    centers equal the host composition over the CSR restatement
+    (oracle.point_costs_sparse: fastSquaredDistance(dense center, sparse
+    point)), LocalKMeans over the sparse candidates through the same
+    restatement; the Lloyd run from them equals a run given those centers."""
+    import torch
+    from cycloneml_amd.clustering import KMeans, KMeansModel, xorshift_next_int
+    from cycloneml_amd.kmeans_init import take_sample_indices
+    rng = np.random.default_rng(12)
+    n, d, k = 3000, 40, 4
+    csr, X = _sparse_data(rng, n, d)
+    xn = oracle.row_norms_csr(csr[0], csr[2])
+    starts = np.array([0, 1100, 2000, n], dtype=np.int64)
+    dev = [torch.from_numpy(a).to(cuda) for a in csr]
+    km = KMeans(k=k, maxIterations=10).setSeed(5).setInitializationMode(mode)
+    C0 = km.initial_centers_csr(*dev, d, partition_starts=starts)
+    s = xorshift_next_int(5)
+    lens = np.diff(starts)
+    if mode == "random":
+        ref = X[take_sample_indices(lens, k, s)]
+    else:
+        cands = [X[take_sample_indices(lens, 1, s)[0]]]
+        new = np.array(cands)
+        costs = np.full(n, np.inf)
+        for step in range(2):
+            _, pc, _ = oracle.point_costs_sparse(csr, xn, new, oracle.row_norms(new))
+            costs = np.minimum(pc, costs)
+            total = float(torch.from_numpy(costs).to(cuda).sum().item())   # the device fold
+            mask = oracle.kmeans_parallel_sample(costs, starts, 0, s, step, k, total)
+            new = X[mask.astype(bool)]
+            cands.extend(new)
+        uniq = []
+        for c in cands:
+            if not any(np.array_equal(c, u) for u in uniq):
+                uniq.append(c)
+        uniq = np.array(uniq)
+        assert uniq.shape[0] > k
+        a, _, _ = oracle.point_costs_sparse(csr, xn, uniq, oracle.row_norms(uniq))
+        wts = np.bincount(a, minlength=uniq.shape[0]).astype(np.float64)
+        cc = _csr_of(uniq)
+        cn = oracle.row_norms_csr(cc[0], cc[2])
+
+        def closest(C):
+            ia, ic, _ = oracle.point_costs_sparse(cc, cn, C, oracle.row_norms(C))
+            return ia, ic
+
+        ref = oracle.local_kmeans_pp(uniq, wts, k, 30, 0, closest=closest)
+    np.testing.assert_array_equal(C0, ref)
+    m1 = km.run_csr(*dev, d, partition_starts=starts)
+    m2 = KMeans(k=C0.shape[0], maxIterations=10).setInitialModel(KMeansModel(C0)).run_csr(*dev, d)
+    # the CSR cluster sums are device atomics: equal to rounding
+    np.testing.assert_allclose(m1.clusterCenters, m2.clusterCenters, rtol=1e-12, atol=1e-12)
