@@ -268,8 +268,72 @@ def _kmeans_init_rank(rank, world):
     return ok
 
 
+def _kmeans_init_csr_rank(rank, world):
+    """k-means|| over CSR shards on two ranks: the initial centers on every
+    rank equal the one-driver composition over the CSR restatement."""
+    import torch
+    from cycloneml_amd import parallel
+    from cycloneml_amd.clustering import KMeans, xorshift_next_int
+    from cycloneml_amd.kmeans_init import take_sample_indices
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(9)
+    n, d, k = 2001, 30, 4
+    X = np.zeros((n, d))
+    for i in range(n):
+        c = rng.integers(0, 4)
+        cols = np.unique(np.concatenate([rng.choice(d, size=5, replace=False), [c * 7]]))
+        X[i, cols] = rng.normal(size=cols.size) + (cols // 7 == c) * 4.0
+
+    def csr(rows):
+        nz = rows != 0.0
+        rp = np.concatenate([[0], np.cumsum(nz.sum(1))]).astype(np.int64)
+        r, c = np.nonzero(nz)
+        return rp, c.astype(np.int32), rows[r, c]
+
+    shard_rows = [parallel.shard_bounds(n, r, world) for r in range(world)]
+    local_parts = [[0, 400, 1001], [0, 999, 1000]]
+    glob = np.array([0, 400, 1001, 2000, 2001], dtype=np.int64)
+    a, b = shard_rows[rank]
+    mine = [torch.from_numpy(v).to(dev) for v in csr(X[a:b])]
+    km = KMeans(k=k, maxIterations=5).setSeed(3)
+    C0 = km.initial_centers_csr(*mine, d, partition_starts=local_parts[rank])
+    # the one-driver composition
+    full = csr(X)
+    xn = oracle.row_norms_csr(full[0], full[2])
+    s = xorshift_next_int(3)
+    cands = [X[take_sample_indices(np.diff(glob), 1, s)[0]]]
+    new = np.array(cands)
+    costs = np.full(n, np.inf)
+    for step in range(2):
+        _, pc, _ = oracle.point_costs_sparse(full, xn, new, oracle.row_norms(new))
+        costs = np.minimum(pc, costs)
+        total = 0.0
+        for lo, hi in shard_rows:
+            total += float(torch.from_numpy(costs[lo:hi].copy()).to(dev).sum().item())
+        mask = oracle.kmeans_parallel_sample(costs, glob, 0, s, step, k, total)
+        new = X[mask.astype(bool)]
+        cands.extend(new)
+    uniq = []
+    for c in cands:
+        if not any(np.array_equal(c, u) for u in uniq):
+            uniq.append(c)
+    uniq = np.array(uniq)
+    if uniq.shape[0] > k:
+        asg, _, _ = oracle.point_costs_sparse(full, xn, uniq, oracle.row_norms(uniq))
+        wts = np.bincount(asg, minlength=uniq.shape[0]).astype(np.float64)
+        cc = csr(uniq)
+        cn = oracle.row_norms_csr(cc[0], cc[2])
+        ref = oracle.local_kmeans_pp(
+            uniq, wts, k, 30, 0,
+            closest=lambda C: oracle.point_costs_sparse(cc, cn, C, oracle.row_norms(C))[:2])
+    else:
+        ref = uniq
+    return C0.shape == ref.shape and bool(np.array_equal(C0, ref))
+
+
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("fn", [_kmeans_rank, _lr_rank, _gramian_rank, _kmeans_init_rank])
+@pytest.mark.parametrize("fn", [_kmeans_rank, _lr_rank, _gramian_rank, _kmeans_init_rank,
+                                _kmeans_init_csr_rank])
 def test_two_ranks_device_kernels_meet_the_collective(fn):
     out = _run(fn)
     assert out == {0: True, 1: True}, out
