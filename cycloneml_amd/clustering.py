@@ -516,9 +516,6 @@ class KMeans:
         """initial_centers for a CSR shard (dense centers)."""
         from . import kmeans_init
         _decode_measure(self.distanceMeasure)
-        if self.distanceMeasure != EUCLIDEAN:
-            raise N.IllegalArgumentException(
-                "the device path runs the cosine measure on dense rows only")
         n = int(rowptr.shape[0]) - 1
         starts = np.asarray([0, n] if partition_starts is None else partition_starts,
                             dtype=np.int64)
@@ -527,7 +524,8 @@ class KMeans:
                                                self.seed, starts)
         return kmeans_init.init_kmeans_parallel_csr(rowptr, colidx, values, int(numFeatures),
                                                     self.k, self.seed,
-                                                    self.initializationSteps, starts, xnorm)
+                                                    self.initializationSteps, starts, xnorm,
+                                                    self.distanceMeasure)
 
     def run_csr(self, rowptr, colidx, values, numFeatures, weights=None, stream=None,
                 iteration_callback=None, partition_starts=None):

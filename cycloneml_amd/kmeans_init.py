@@ -414,7 +414,8 @@ def init_random_csr(rowptr, colidx, values, d: int, k: int, seed: int,
 
 
 def init_kmeans_parallel_csr(rowptr, colidx, values, d: int, k: int, seed: int, steps: int,
-                             partition_starts, xnorm=None) -> np.ndarray:
+                             partition_starts, xnorm=None,
+                             distanceMeasure: str = "euclidean") -> np.ndarray:
     """KMeans.initKMeansParallel (KMeans.scala:370-432) over sparse points:
     as init_kmeans_parallel, the cost passes fastSquaredDistance(center,
     sparse point) on the device (cyc_kmeans_point_cost_csr_dev; dot(sparse,
@@ -437,7 +438,8 @@ def init_kmeans_parallel_csr(rowptr, colidx, values, d: int, k: int, seed: int, 
     total = 0.0
     for step in range(steps):
         if new.shape[0] > 0:
-            _, c = KMeansModel(new).pointCosts_csr(rowptr, colidx, values, xnorm)
+            _, c = KMeansModel(new, distanceMeasure=distanceMeasure).pointCosts_csr(
+                rowptr, colidx, values, xnorm)
             costs = c if costs is None else torch.minimum(c, costs)
             tot = costs.sum().reshape(1) if costs.numel() else torch.zeros(
                 1, dtype=torch.float64, device=values.device)
@@ -450,9 +452,11 @@ def init_kmeans_parallel_csr(rowptr, colidx, values, d: int, k: int, seed: int, 
     distinct = _distinct_rows(np.array(centers))
     if distinct.shape[0] <= k:
         return distinct
-    idx, _ = KMeansModel(distinct).pointCosts_csr(rowptr, colidx, values, xnorm)
+    idx, _ = KMeansModel(distinct, distanceMeasure=distanceMeasure).pointCosts_csr(
+        rowptr, colidx, values, xnorm)
     counts = torch.bincount(idx.long(), minlength=distinct.shape[0]).cpu().numpy()
     counts = np.sum(parallel.allgather_object(counts), axis=0)     # countByValue
+    # LocalKMeans is Euclidean whatever the run's measure (LocalKMeans.scala:49)
     cand = _csr_of_dense(distinct, values.device)
     cand_norm = row_norms_csr(cand[0], cand[2])
 

@@ -200,8 +200,9 @@ def _csr_of(rows):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["k-means||", "random"])
-def test_kmeans_run_csr_without_initial_model(cuda, mode):
+@pytest.mark.parametrize("mode,measure", [("k-means||", "euclidean"), ("random", "euclidean"),
+                                          ("k-means||", "cosine")])
+def test_kmeans_run_csr_without_initial_model(cuda, mode, measure):
     """KMeans.run over sparse points without an initial model: the initial
     centers equal the host composition over the CSR restatement
     (oracle.point_costs_sparse: fastSquaredDistance(dense center, sparse
@@ -217,7 +218,14 @@ def test_kmeans_run_csr_without_initial_model(cuda, mode):
     starts = np.array([0, 1100, 2000, n], dtype=np.int64)
     dev = [torch.from_numpy(a).to(cuda) for a in csr]
     km = KMeans(k=k, maxIterations=10).setSeed(5).setInitializationMode(mode)
+    km.setDistanceMeasure(measure)
     C0 = km.initial_centers_csr(*dev, d, partition_starts=starts)
+    if measure == "cosine":     # the run's measure for the costs and counts
+        def run_costs(C):
+            return oracle.cos_point_costs_sparse(csr + (d,), xn, C, oracle.row_norms(C))
+    else:
+        def run_costs(C):
+            return oracle.point_costs_sparse(csr, xn, C, oracle.row_norms(C))
     s = xorshift_next_int(5)
     lens = np.diff(starts)
     if mode == "random":
@@ -227,7 +235,7 @@ def test_kmeans_run_csr_without_initial_model(cuda, mode):
         new = np.array(cands)
         costs = np.full(n, np.inf)
         for step in range(2):
-            _, pc, _ = oracle.point_costs_sparse(csr, xn, new, oracle.row_norms(new))
+            _, pc, _ = run_costs(new)
             costs = np.minimum(pc, costs)
             total = float(torch.from_numpy(costs).to(cuda).sum().item())   # the device fold
             mask = oracle.kmeans_parallel_sample(costs, starts, 0, s, step, k, total)
@@ -239,7 +247,7 @@ def test_kmeans_run_csr_without_initial_model(cuda, mode):
                 uniq.append(c)
         uniq = np.array(uniq)
         assert uniq.shape[0] > k
-        a, _, _ = oracle.point_costs_sparse(csr, xn, uniq, oracle.row_norms(uniq))
+        a, _, _ = run_costs(uniq)
         wts = np.bincount(a, minlength=uniq.shape[0]).astype(np.float64)
         cc = _csr_of(uniq)
         cn = oracle.row_norms_csr(cc[0], cc[2])
@@ -251,6 +259,7 @@ def test_kmeans_run_csr_without_initial_model(cuda, mode):
         ref = oracle.local_kmeans_pp(uniq, wts, k, 30, 0, closest=closest)
     np.testing.assert_array_equal(C0, ref)
     m1 = km.run_csr(*dev, d, partition_starts=starts)
-    m2 = KMeans(k=C0.shape[0], maxIterations=10).setInitialModel(KMeansModel(C0)).run_csr(*dev, d)
+    m2 = KMeans(k=C0.shape[0], maxIterations=10).setDistanceMeasure(measure).setInitialModel(
+        KMeansModel(C0, distanceMeasure=measure)).run_csr(*dev, d)
     # the CSR cluster sums are device atomics: equal to rounding
     np.testing.assert_allclose(m1.clusterCenters, m2.clusterCenters, rtol=1e-12, atol=1e-12)
