@@ -137,6 +137,8 @@ def _init_shards_rank(rank, world):
     pos = take_sample_indices(sh.lens, 37, 99)
     got = sh.rows_at(torch.from_numpy(X[a:b].copy()), pos)
     ok = ok and np.array_equal(got, X[pos])
+    got2 = sh.rows_of(lambda loc: X[a:b][loc], pos, d)      # the CSR shards' gather
+    ok = ok and np.array_equal(got2, X[pos])
     cat = sh.concat(X[a:b][::100])
     return bool(ok and np.array_equal(cat, np.concatenate([X[0:451][::100], X[451:][::100]])))
 
