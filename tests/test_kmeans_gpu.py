@@ -575,3 +575,31 @@ def test_lloyd_iteration_no_row_costs(cuda, n, d, k, weighted):
     np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
                                atol=1e-10 * np.abs(ref["sums"]).max())
     assert abs(cost.item() - ref["cost"]) <= 1e-12 * abs(ref["cost"])
+
+
+@pytest.mark.parametrize("k,d,nostats", [(2500, 16, False), (2500, 16, True), (1030, 300, False)])
+def test_exact_tier_many_centers(cuda, k, d, nostats):
+    """Rows the screens cannot decide (exact ties between duplicated centers)
+    go to the exact tier; with k > 1024 its distances are staged in several
+    1024-center chunks.  Index and cost bit-exact vs the restatement, with
+    statistics (findClosest :282-313) and without (pointCost :318-340)."""
+    import torch
+    from cycloneml_amd.clustering import KMeansModel
+    rng = np.random.default_rng(k + d)
+    base = rng.integers(-3, 4, size=(k // 2, d)).astype(np.float64)
+    C = np.concatenate([base, base])[:k]            # every center twice
+    if C.shape[0] < k:
+        C = np.concatenate([C, base[: k - C.shape[0]]])
+    rng.shuffle(C)
+    X = C[rng.integers(0, k, 3000)] + rng.integers(0, 2, size=(3000, d)) * 0.5
+    if nostats:
+        a, c = KMeansModel(C).pointCosts(_dev(X, cuda))
+        ra, rc, _ = oracle.point_costs(X, oracle.row_norms(X), C, oracle.row_norms(C))
+        np.testing.assert_array_equal(a.cpu().numpy(), ra)
+        np.testing.assert_array_equal(c.cpu().numpy(), rc)
+        return
+    a, c, n_exact, *_ = _gpu_assign(X, C, cuda)
+    assert n_exact > 0
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a, ra)
+    np.testing.assert_array_equal(c, rc)
