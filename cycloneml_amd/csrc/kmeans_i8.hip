@@ -1172,10 +1172,28 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
                                            ca ? ca->candRows : nullptr, ca ? ca->cands : nullptr,
                                            ca ? ca->candCount : nullptr);
   if (rc) return rc;
+  if (!ca)
+    return launch_screen32<S, W, 3, true>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp,
+                                          list2, list2Count, assign, list, listCount, st);
+  // the three-limb pass (rows with more than kCandMax candidates) and the
+  // candidate pass touch disjoint rows and only append to `list`: the
+  // three-limb pass runs on a side stream of this host thread beside it
+  thread_local hipStream_t side = nullptr;
+  thread_local hipEvent_t fork = nullptr, join = nullptr;
+  if (!side) {
+    CYC_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    CYC_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+    CYC_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  }
+  CYC_HIP(hipEventRecord(fork, st));
+  CYC_HIP(hipStreamWaitEvent(side, fork, 0));
   if ((rc = launch_screen32<S, W, 3, true>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp,
-                                           list2, list2Count, assign, list, listCount, st)))
+                                           list2, list2Count, assign, list, listCount, side)))
     return rc;
-  return ca ? launch_cands(*ca, n, d, assign, list, listCount, st) : CYC_OK;
+  rc = launch_cands(*ca, n, d, assign, list, listCount, st);
+  CYC_HIP(hipEventRecord(join, side));
+  CYC_HIP(hipStreamWaitEvent(st, join, 0));
+  return rc;
 }
 
 template <int KS>
