@@ -1486,16 +1486,16 @@ __global__ void k_reduce_clusters(const double* __restrict__ part, const double*
     if (threadIdx.x == 0) ccost[c] = 0.0;
     return;
   }
-  // chunk order kept; 8 chunks' loads in flight per step
+  // chunk order kept; 16 chunks' loads in flight per step
   for (int j = threadIdx.x; j < d; j += blockDim.x) {
     double s = 0.0;
     int64_t ch = a;
-    for (; ch + 8 <= b; ch += 8) {
-      double v[8];
+    for (; ch + 16 <= b; ch += 16) {
+      double v[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(ch + u) * d + j];
+      for (int u = 0; u < 16; ++u) v[u] = part[(ch + u) * d + j];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) s = dadd(s, v[u]);
+      for (int u = 0; u < 16; ++u) s = dadd(s, v[u]);
     }
     for (; ch < b; ++ch) s = dadd(s, part[ch * d + j]);
     sums[(int64_t)c * d + j] = dadd(sums[(int64_t)c * d + j], s);
