@@ -1,33 +1,41 @@
 #!/usr/bin/env python3
 """bench.py -- rows/s per training iteration on MI355X (BASELINE.json metric).
 
-Default workload (BASELINE.json configs[1], the config the metric is quoted
-on): KMeans k=1024 on synthetic dense fp64 10M x 256, one Lloyd iteration per
-step (KMeans.scala:275-334: statistics, findClosest for every row,
-per-cluster sums/weights/cost, merge, centroid update).
+A default run times all four BASELINE workloads, one after the other, each
+with its own data resident in HBM and freed before the next:
+  kmeans       (headline, BASELINE configs[1], the config the metric is
+               quoted on) KMeans k=1024 on synthetic dense fp64 10M x 256, one
+               Lloyd iteration per step (KMeans.scala:275-334: statistics,
+               findClosest for every row, per-cluster sums/weights/cost,
+               merge, centroid update)
+  gramian      RowMatrix.computeGramianMatrix pass (configs[2]: 100M x 1024)
+  lr_multi     multinomial LR, 100 classes, 512 dense features (configs[3]:
+               50M rows); one RDDLossFunction.calculate per step
+  lr_sparse    binomial LR on CSR, 1M features, 64 nnz/row (configs[4]: 200M
+               rows, tiles layout); one RDDLossFunction.calculate per step
+The headline JSON line is KMeans's; the other three ride along under
+"workloads", each with its own value, roofline and cpu_baseline.
+--workload NAME times one of them alone.
 
-Other workloads (--workload), each one training iteration per step:
-  gramian      RowMatrix.computeGramianMatrix pass (configs[2]; the 100M x 1024
-               matrix (819 GB) does not fit one GPU: each GPU holds the largest
-               resident shard, 30M rows = 246 GB)
-  lr_multi     multinomial LR, 100 classes, 512 dense features (configs[3]);
-               one RDDLossFunction.calculate per step, the full 50M-row
-               config (205 GB) resident per GPU
-  lr_sparse    binomial LR on CSR, 1M features, 64 nnz/row (configs[4]);
-               one RDDLossFunction.calculate per step, the full 200M-row
-               config resident per GPU in the tiles layout (157 GB)
-With --gpus N (one process per GPU via torch.distributed.run) every rank
-holds its own shard in HBM (weak scaling) and the merge is one RCCL
-all-reduce per iteration.
+Rows per GPU (--scaling auto): KMeans config 2 is a one-GPU config, so each
+GPU holds 10M rows (weak scaling); configs 3-5 are totals split over the N
+GPUs by contiguous row ranges (strong scaling, parallel.shard_bounds), capped
+at the largest shard one GPU holds resident (Gramian: 30M rows = 246 GB, so
+100M rows need N >= 4 to be whole).  --scaling weak|strong forces one mode
+for every workload; --rows overrides the rows per GPU.
+With --gpus N (one process per GPU via torch.distributed.run) the merge is
+one RCCL all-reduce per iteration.
 
 Prints ONE JSON line on rank 0.  `roofline` is for the workload's dominant
-kernel, timed with HIP events on the stream it runs on inside the timed
-region (cyc_profile_*); `cpu_baseline` is the CPU restatement (oracle/, a C
-port of the reference loops) on a bounded sample of the same data.
+kernel (the slowest of its priced kernels), timed with HIP events on the
+stream it runs on inside the timed region (cyc_profile_*); `cpu_baseline` is
+the CPU restatement (oracle/, a C port of the reference loops) on a bounded
+sample of the same data.
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -40,25 +48,53 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 (vector = matrix) spec, BASELINE.md sect
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 I8_PEAK_TOPS = 5000.0     # dense i8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md)
 
-DEFAULT_ROWS = {"kmeans": 10_000_000, "gramian": 30_000_000, "lr_multi": 50_000_000,
-                "lr_sparse": 200_000_000}
+ORDER = ("kmeans", "gramian", "lr_multi", "lr_sparse")
+# BASELINE configs: rows of the whole problem, and whether it is per GPU
+CONFIG_ROWS = {"kmeans": 10_000_000, "gramian": 100_000_000, "lr_multi": 50_000_000,
+               "lr_sparse": 200_000_000}
+PER_GPU_CONFIG = {"kmeans": True, "gramian": False, "lr_multi": False, "lr_sparse": False}
+# the largest shard one MI355X holds resident (288 GB HBM)
+MAX_RESIDENT_ROWS = {"kmeans": 10_000_000, "gramian": 30_000_000, "lr_multi": 50_000_000,
+                     "lr_sparse": 200_000_000}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="kmeans", choices=sorted(DEFAULT_ROWS))
-    ap.add_argument("--rows", type=int, default=0, help="rows per GPU (0 = workload default)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="target CPU time of the cpu_baseline sample (0 disables)")
-    return ap.parse_args()
+    ap.add_argument("--workload", default="all", choices=("all",) + ORDER)
+    ap.add_argument("--scaling", default="auto", choices=("auto", "weak", "strong"))
+    ap.add_argument("--rows", type=int, default=0, help="rows per GPU (0 = from --scaling)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU time of each cpu_baseline sample (0 disables)")
+    return ap.parse_args(argv)
 
 
-def pmc_traffic(workload, kernels, launches_per_step, rows):
-    """HBM bytes per timed launch of the dominant kernel, from the latest
-    committed rocprofv3 --pmc summary of this workload
+def rows_per_gpu(workload, scaling, world, rank, override=0):
+    """(rows this rank holds, scaling mode, rows of the whole job) for a
+    workload: weak = the config's per-GPU rows on every GPU; strong = the
+    config's total split by parallel.shard_bounds, each shard capped at
+    MAX_RESIDENT_ROWS."""
+    from cycloneml_amd.parallel import shard_bounds
+    mode = scaling
+    if mode == "auto":
+        mode = "weak" if PER_GPU_CONFIG[workload] else "strong"
+    if override:
+        return override, mode, override * world
+    if mode == "weak":
+        n = min(CONFIG_ROWS[workload], MAX_RESIDENT_ROWS[workload])
+        return n, mode, n * world
+    s, e = shard_bounds(CONFIG_ROWS[workload], rank, world)
+    cap = MAX_RESIDENT_ROWS[workload]
+    total = sum(min(b - a, cap) for a, b in
+                (shard_bounds(CONFIG_ROWS[workload], r, world) for r in range(world)))
+    return min(e - s, cap), mode, total
+
+
+def pmc_traffic(workload, kernel, launches_per_step, rows):
+    """HBM bytes per timed launch of `kernel`, from the latest committed
+    rocprofv3 --pmc summary of this workload
     (profiles/r<NN>_<workload>_pmc.json, tools/pmc_summary.py: separate
     FETCH_SIZE / WRITE_SIZE passes, gfx950 corrections applied there), scaled
     to this run's rows; (None, None) when there is none."""
@@ -67,10 +103,9 @@ def pmc_traffic(workload, kernels, launches_per_step, rows):
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            have = [k for k in kernels if k in d]
-            if not have:
+            if kernel not in d:
                 continue
-            per_step = sum(d[k]["hbm_bytes_per_step"] for k in have)
+            per_step = d[kernel]["hbm_bytes_per_step"]
             return per_step / launches_per_step * rows / d["_rows"], os.path.basename(f)
         except Exception:
             continue
@@ -89,6 +124,55 @@ def timed_parallel(fn, parts, threads):
     return time.perf_counter() - t0, out
 
 
+# ------------------------------------------------------------ synthetic data
+# Shared with the parity tests that check the timed data itself
+# (tests/test_kmeans_gpu.py::test_full_config_all_rows,
+# tests/test_logistic_gpu.py::test_sparse_config5_full_size).
+
+def kmeans_data(n, dev, rank=0, d=256, k=1024):
+    """BASELINE config 2 / SURVEY 8d: k true centers ~ N(0, 4^2) per dim plus
+    point noise N(0, 1), fp64 row-major n x d; torch Philox on the device,
+    the centers seeded 1234, the rows 1000 + rank in 1M-row chunks."""
+    import torch
+    g = torch.Generator(device=dev).manual_seed(1234)
+    true_c = torch.randn(k, d, generator=g, device=dev, dtype=torch.float64) * 4.0
+    gr = torch.Generator(device=dev).manual_seed(1000 + rank)
+    X = torch.empty(n, d, dtype=torch.float64, device=dev)
+    for s in range(0, n, 1 << 20):
+        e = min(n, s + (1 << 20))
+        lab = torch.randint(0, k, (e - s,), generator=gr, device=dev)
+        X[s:e] = true_c[lab] + torch.randn(e - s, d, generator=gr, device=dev,
+                                           dtype=torch.float64)
+    return X
+
+
+LR_SPARSE_CHUNK = 64 * 8192            # whole row blocks of the tiles layout per append
+
+
+def lr_sparse_chunks(n, dev, rank=0, F=1_000_000, k=64):
+    """BASELINE config 5 / SURVEY 8d rows, LR_SPARSE_CHUNK rows at a time:
+    yields (start, end, rowptr, colidx, values, labels) with k distinct sorted
+    columns per row (one per F/k band + a uniform offset), values U(0, 1),
+    labels ~ Bernoulli(sigmoid(w . x)) for w ~ N(0, 0.5^2) seeded 2; the rows
+    seeded 900 + rank."""
+    import torch
+    g = torch.Generator(device=dev).manual_seed(2)
+    w_true = torch.randn(F, generator=g, device=dev, dtype=torch.float64) * 0.5
+    gr = torch.Generator(device=dev).manual_seed(900 + rank)
+    band = F // k
+    for s in range(0, n, LR_SPARSE_CHUNK):
+        e = min(n, s + LR_SPARSE_CHUNK)
+        c = (torch.arange(k, device=dev) * band).unsqueeze(0) + \
+            torch.randint(0, band, (e - s, k), generator=gr, device=dev)
+        v = torch.rand(e - s, k, generator=gr, device=dev, dtype=torch.float64)
+        m = (v * w_true[c]).sum(1)
+        y = (torch.rand(e - s, generator=gr, device=dev, dtype=torch.float64)
+             < torch.sigmoid(m)).to(torch.float64)
+        del m
+        rowptr = torch.arange(0, (e - s) * k + 1, k, dtype=torch.int64, device=dev)
+        yield s, e, rowptr, c.to(torch.int32).reshape(-1), v.reshape(-1), y
+
+
 # ---------------------------------------------------------------- workloads
 
 class KMeansWorkload:
@@ -101,7 +185,7 @@ class KMeansWorkload:
     kernel = "k_kmeans_screen2"
     kernels = ("k_kmeans_screen2", "k_kmeans_cands", "k_kmeans_screen3", "k_kmeans_assign_fp64",
                "k_chunk_sums")
-    pmc_kernels = ("k_screen32_l2",)
+    pmc_names = {"k_kmeans_screen2": "k_screen32_l2"}
     bound = "mfma"
     unit = "TOPS"
     peak = I8_PEAK_TOPS
@@ -112,31 +196,28 @@ class KMeansWorkload:
         from cycloneml_amd.clustering import KMeansPlan, row_norms
         self.n, self.d, self.k = n, 256, 1024
         d, k = self.d, self.k
-        # BASELINE config 2 / SURVEY 8d: 1024 true centers ~ N(0, 4^2) per dim
-        # + point noise N(0, 1); torch Philox on device, seeded per rank.
-        g = torch.Generator(device=dev).manual_seed(1234)
-        true_c = torch.randn(k, d, generator=g, device=dev, dtype=torch.float64) * 4.0
-        gr = torch.Generator(device=dev).manual_seed(1000 + rank)
-        X = torch.empty(n, d, dtype=torch.float64, device=dev)
-        for s in range(0, n, 1 << 20):
-            e = min(n, s + (1 << 20))
-            lab = torch.randint(0, k, (e - s,), generator=gr, device=dev)
-            X[s:e] = true_c[lab] + torch.randn(e - s, d, generator=gr, device=dev,
-                                               dtype=torch.float64)
+        X = kmeans_data(n, dev, rank)
         self.X = X
-        self.xnorm = row_norms(X)
         self.C0 = X[:k].clone()           # setInitialModel semantics: rows 0..k-1
         parallel.broadcast_(self.C0)
         self.C = self.C0.clone()
         self.cnorm = row_norms(self.C)
         self.plan = KMeansPlan(d, k, n)
-        # per-fit row image (int8 limbs, 3 B/element): built once before the
-        # Lloyd loop like the cached norms (KMeans.scala:263-270), untimed
+        # per-fit preparation, once before the Lloyd loop and outside the
+        # timed iterations: the cached norms (KMeans.scala:263-270) and the
+        # row image (int8 limbs, 3 B/element).  Reported as prep_ms.
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        self.xnorm = row_norms(X)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         self.rows = self.plan.rows(X)
         torch.cuda.synchronize()
-        self.prep_ms = (time.perf_counter() - t0) * 1e3
+        t2 = time.perf_counter()
+        self.prep = {"norms_ms": (t1 - t0) * 1e3, "row_image_ms": (t2 - t1) * 1e3,
+                     "per_fit_ms": (t2 - t0) * 1e3,
+                     "per_iteration_ms_at_maxIter_20": (t2 - t0) * 1e3 / 20,
+                     "note": "once per fit, before the Lloyd loop; not in ms_per_step"}
         self.buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=dev)
         self.conv = torch.zeros(1, dtype=torch.int32, device=dev)
         self.parallel = parallel
@@ -151,7 +232,9 @@ class KMeansWorkload:
         self.parallel.allreduce_(buf)
         self.plan.update(self.C, self.cnorm, sums, wsum, 1e-4, self.conv)
 
-    def work_per_launch(self, launches_per_step):
+    def work(self, kname, launches_per_step):
+        if kname != self.kernel:
+            return None
         D = 128 * ((self.d + 127) // 128)                 # 32-dim substeps, padded
         kpad = 16 * (((self.k + 15) // 16 + 3) // 4 * 4)  # 32-center tiles
         return 6.0 * D * kpad * self.n / launches_per_step   # i8 ops
@@ -207,7 +290,6 @@ class KMeansWorkload:
 
 class GramianWorkload:
     kernel = "k_gram_tiles"
-    pmc_kernels = ("k_gram_tiles",)
     bound = "mfma"
 
     def __init__(self, n, dev, rank):
@@ -229,24 +311,26 @@ class GramianWorkload:
         self.plan.accumulate(self.X, self.U)
         self.parallel.allreduce_(self.U)
 
-    def work_per_launch(self, launches_per_step):
+    def work(self, kname, launches_per_step):
         return float(self.n) * self.p * (self.p + 1) / launches_per_step   # flops (upper)
 
     def describe(self):
         return (f"RowMatrix.computeGramianMatrix pass, dense fp64 {self.n} x {self.p} rows per "
-                "GPU, U[0,1) (BASELINE configs[2]; the largest resident shard of its 100M rows)")
+                "GPU, U[0,1) (BASELINE configs[2]: 100M rows in total, split over the GPUs; "
+                "one GPU holds at most a 30M-row shard, 246 GB)")
 
     def cpu_baseline(self, seconds):
         import numpy as np
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         threads = cpu_threads()
-        Xs = np.ascontiguousarray(self.X[:1_500_000].cpu().numpy())
+        Xs = np.ascontiguousarray(self.X[:200].cpu().numpy())
         t0 = time.perf_counter()
-        oracle.gramian_partition(Xs[:200])
+        oracle.gramian_partition(Xs)
         per_row = (time.perf_counter() - t0) / 200
-        rows = int(min(Xs.shape[0], max(threads * 50, seconds * threads / per_row)))
+        rows = int(min(self.n, 1_500_000, max(threads * 50, seconds * threads / per_row)))
         rows -= rows % threads
+        Xs = np.ascontiguousarray(self.X[:rows].cpu().numpy())
         parts = np.array_split(Xs[:rows], threads)
         el, Us = timed_parallel(oracle.gramian_partition, parts, threads)
         return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
@@ -257,7 +341,6 @@ class GramianWorkload:
 class LRMultiWorkload:
     kernel = "k_mlr_margins"
     kernels = ("k_mlr_margins", "k_mlr_grad")
-    pmc_kernels = ("k_mlr_margins",)
     bound = "mfma"
 
     def __init__(self, n, dev, rank):
@@ -286,8 +369,12 @@ class LRMultiWorkload:
         for s in range(0, n, 1 << 22):
             mean += X[s:s + (1 << 22)].sum(0)
             sq += (X[s:s + (1 << 22)] ** 2).sum(0)
-        mean /= n
-        std = (sq / n - mean ** 2).clamp_min(0).sqrt()
+        from cycloneml_amd import parallel
+        tot = torch.cat([mean, sq, torch.tensor([float(n)], dtype=torch.float64, device=dev)])
+        parallel.allreduce_(tot)                   # the summary over every rank's rows
+        mean, sq, n_all = tot[:F], tot[F:2 * F], tot[2 * F]
+        mean = mean / n_all
+        std = (sq / n_all - mean ** 2).clamp_min(0).sqrt()
         sm_dev = mean / std                                        # bcScaledMean, once
         self.scaledMean = sm_dev.cpu().numpy()
         self.fn = RDDLossFunction([self.block], lambda c: MultinomialLogisticBlockAggregator(
@@ -296,21 +383,21 @@ class LRMultiWorkload:
     def step(self):
         self.fn.calculate(self.coef)
 
-    def work_per_launch(self, launches_per_step):
-        return 2.0 * self.n * self.F * self.C / launches_per_step
+    def work(self, kname, launches_per_step):
+        return 2.0 * self.n * self.F * self.C / launches_per_step    # each pass: one gemm
 
     def describe(self):
         return (f"multinomial LR ({self.C} classes) RDDLossFunction.calculate, dense fp64 "
                 f"{self.n} x {self.F} rows per GPU, fitIntercept+standardization "
-                "(BASELINE configs[3], the full 50M-row config per GPU)")
+                "(BASELINE configs[3]: 50M rows in total, split over the GPUs)")
 
     def cpu_baseline(self, seconds):
         import numpy as np
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         threads = cpu_threads()
-        X = self.block.X[:2_000_000].cpu().numpy()
-        y = self.block.labels[:2_000_000].cpu().numpy()
+        X = self.block.X[:256].cpu().numpy()
+        y = self.block.labels[:256].cpu().numpy()
 
         def part(rng_):
             a, b = rng_
@@ -324,8 +411,10 @@ class LRMultiWorkload:
         t0 = time.perf_counter()
         part((0, 256))
         per_row = (time.perf_counter() - t0) / 256
-        rows = int(min(X.shape[0], max(threads * 256, seconds * threads / per_row)))
+        rows = int(min(self.n, 2_000_000, max(threads * 256, seconds * threads / per_row)))
         rows -= rows % (threads * 256)
+        X = self.block.X[:rows].cpu().numpy()
+        y = self.block.labels[:rows].cpu().numpy()
         step = rows // threads
         el, _ = timed_parallel(part, [(i * step, (i + 1) * step) for i in range(threads)],
                                threads)
@@ -340,12 +429,11 @@ class LRSparseWorkload:
     (LogisticRegression.scala:950-954) with a scaledMean of the data's scale.
     The shard lives only in the row-block x column-tile layout (tiles.hip):
     it is generated on the device 512K rows at a time, appended, and each
-    CSR chunk freed (157 GB resident for 200M rows).  Roofline on the margin
-    pass (k_tiles_margin), whose HBM reads are SURVEY 8(d)'s 784 B/row; the
-    gradient pass (k_tiles_grad) is listed beside it."""
-    kernel = "k_tiles_margin"
+    CSR chunk freed (157 GB resident for 200M rows).  Both passes are priced
+    at SURVEY 8(d)'s 784 B/row (one fused pass's reads); the roofline line
+    names the slower (dominant) one."""
+    kernel = "k_tiles_grad"
     kernels = ("k_tiles_margin", "k_tiles_grad")
-    pmc_kernels = ("k_tiles_margin",)
     bound = "hbm"
 
     def __init__(self, n, dev, rank):
@@ -355,33 +443,18 @@ class LRSparseWorkload:
                                          RDDLossFunction, SparseTiles)
         self.n, self.F, self.k = n, 1_000_000, 64
         F, k = self.F, self.k
-        g = torch.Generator(device=dev).manual_seed(2)
-        w_true = torch.randn(F, generator=g, device=dev, dtype=torch.float64) * 0.5
-        gr = torch.Generator(device=dev).manual_seed(900 + rank)
         self.tiles = SparseTiles(F, n, n * k)
         y = torch.empty(n, dtype=torch.float64, device=dev)
-        band = F // k
-        step = 64 * SparseTiles.ROW_BLOCK          # whole row blocks per append
         self.sample = []                            # host copy of the first rows (CPU leg)
-        sample_rows = min(n, 4 * step)
+        sample_rows = min(n, 4 * LR_SPARSE_CHUNK)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for s in range(0, n, step):
-            e = min(n, s + step)
-            # 64 distinct sorted columns per row: one per 1/64 band + offset
-            c = (torch.arange(k, device=dev) * band).unsqueeze(0) + \
-                torch.randint(0, band, (e - s, k), generator=gr, device=dev)
-            v = torch.rand(e - s, k, generator=gr, device=dev, dtype=torch.float64)
-            m = (v * w_true[c]).sum(1)
-            y[s:e] = (torch.rand(e - s, generator=gr, device=dev, dtype=torch.float64)
-                      < torch.sigmoid(m)).to(torch.float64)
-            cols = c.to(torch.int32).reshape(-1)
-            vals = v.reshape(-1)
-            rowptr = torch.arange(0, (e - s) * k + 1, k, dtype=torch.int64, device=dev)
-            self.tiles.append(rowptr, cols, vals)
+        for s, e, rowptr, cols, vals, yc in lr_sparse_chunks(n, dev, rank, F, k):
+            y[s:e] = yc
+            self.tiles.append(rowptr, cols, vals)   # the CSR chunk is freed after
             if s < sample_rows:
                 self.sample.append((cols.cpu().numpy(), vals.cpu().numpy()))
-            del c, v, m, cols, vals, rowptr
+            del rowptr, cols, vals, yc
         torch.cuda.synchronize()
         self.prep_ms = (time.perf_counter() - t0) * 1e3
         self.labels = y
@@ -397,7 +470,7 @@ class LRSparseWorkload:
     def step(self):
         self.fn.calculate(self.coef)
 
-    def work_per_launch(self, launches_per_step):
+    def work(self, kname, launches_per_step):
         return self.n * (self.k * 12 + 8 + 8) / launches_per_step   # bytes
 
     def extra_roofline(self, launches_per_step, avg_s):
@@ -408,8 +481,8 @@ class LRSparseWorkload:
     def describe(self):
         return (f"binomial LR RDDLossFunction.calculate on CSR {self.n} rows x {self.F} "
                 f"features, {self.k} nnz/row per GPU, fitIntercept+fitWithMean "
-                "(BASELINE configs[4], full 200M-row shard resident on one GPU in the "
-                "row-block x column-tile layout)")
+                "(BASELINE configs[4]: 200M rows in total, split over the GPUs, resident "
+                "in the row-block x column-tile layout)")
 
     def cpu_baseline(self, seconds):
         import numpy as np
@@ -473,6 +546,101 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd)
 
 
+def run_workload(name, args, dev, rank, world, cpu_seconds):
+    """Build one workload's resident data, time args.steps steps after
+    args.warmup, and return its result dict (the JSON line's fields)."""
+    import torch
+    import torch.distributed as dist
+    from cycloneml_amd import _native as N
+    from cycloneml_amd import parallel
+    n, mode, total_rows = rows_per_gpu(name, args.scaling, world, rank, args.rows)
+    t_build = time.perf_counter()
+    wl = WORKLOADS[name](n, dev, rank)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t_build
+    for _ in range(args.warmup):
+        wl.step()
+    torch.cuda.synchronize()
+    kernels = getattr(wl, "kernels", (wl.kernel,))
+    N.profile_enable(True)
+    for kname in kernels:
+        N.profile_query(kname)            # reset
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    prof = {kname: N.profile_query(kname) for kname in kernels}
+    N.profile_enable(False)
+    el = parallel.max_over_ranks(el, dev)
+    value = total_rows * args.steps / el
+
+    # dominant kernel: the slowest of the priced kernels
+    priced = [k for k in kernels if prof[k][1] and wl.work(k, 1) is not None]
+    kname = max(priced, key=lambda k: prof[k][0]) if priced else wl.kernel
+    kms, launches = prof[kname]
+    avg_s = kms / max(launches, 1) / 1e3
+    per_launch = wl.work(kname, launches / args.steps) if launches else 0.0
+    achieved = per_launch / avg_s if launches else None
+    if wl.bound == "mfma":
+        unit = getattr(wl, "unit", "TFLOP/s")
+        peak = getattr(wl, "peak", FP64_PEAK_TFLOPS)
+        achieved = achieved / 1e12 if achieved else None
+    else:
+        unit, peak = "GB/s", HBM_PEAK_GBS
+        achieved = achieved / 1e9 if achieved else None
+    pmc_name = getattr(wl, "pmc_names", {}).get(kname, kname)
+    traffic, traffic_src = (pmc_traffic(name, pmc_name, launches / args.steps, n)
+                            if launches else (None, None))
+    extra = wl.extra_roofline(launches / args.steps, avg_s) if (
+        launches and hasattr(wl, "extra_roofline")) else {}
+    cpu = None
+    if rank == 0 and world == 1 and cpu_seconds > 0:
+        cpu = wl.cpu_baseline(cpu_seconds)
+    out = {
+        "metric": "rows/s per training iteration",
+        "value": value,
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": mode,
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic, generated on device (torch Philox, seeded per rank)",
+        "config": {"workload": wl.describe(), "rows_per_gpu": n, "rows_total": total_rows,
+                   "config_rows": CONFIG_ROWS[name],
+                   "config_rows_are": "per GPU" if PER_GPU_CONFIG[name] else "total",
+                   "parallelism": f"dp{world} (row shards, RCCL all-reduce merge)"},
+        "roofline": {"kernel": kname, "bound": wl.bound, "achieved": achieved,
+                     "peak": peak, "unit": unit,
+                     "frac": (achieved / peak) if achieved else None,
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "avg_launch_ms": avg_s * 1e3, "launches": launches,
+                     "work_per_launch": per_launch,
+                     "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
+                     **extra},
+        "cpu_baseline": cpu,
+        "build_s": build_s,
+    }
+    if getattr(wl, "prep", None):
+        out["prep_ms"] = wl.prep
+    if hasattr(wl, "close"):
+        wl.close()
+    del wl
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -497,77 +665,22 @@ def main():
     comm = parallel.init(dev)          # libcyclone's RCCL communicator (cyc_comm_*)
     if comm is not None:
         world = comm.world_size        # n_gpus as the live communicator reports it
-    n = args.rows or DEFAULT_ROWS[args.workload]
-    wl = WORKLOADS[args.workload](n, dev, rank)
-
-    for _ in range(args.warmup):
-        wl.step()
-    torch.cuda.synchronize()
-    kernels = getattr(wl, "kernels", (wl.kernel,))
-    N.profile_enable(True)
-    for kname in kernels:
-        N.profile_query(kname)            # reset
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        wl.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    prof = {kname: N.profile_query(kname) for kname in kernels}
-    N.profile_enable(False)
-    el = parallel.max_over_ranks(el, dev)
-    value = n * world * args.steps / el
-
-    kms, launches = prof[wl.kernel]
-    avg_s = kms / max(launches, 1) / 1e3
-    per_launch = wl.work_per_launch(launches / args.steps) if launches else 0.0
-    achieved = per_launch / avg_s if launches else None
-    if wl.bound == "mfma":
-        unit = getattr(wl, "unit", "TFLOP/s")
-        peak = getattr(wl, "peak", FP64_PEAK_TFLOPS)
-        achieved = achieved / 1e12 if achieved else None
-    else:
-        unit, peak = "GB/s", HBM_PEAK_GBS
-        achieved = achieved / 1e9 if achieved else None
-    traffic, traffic_src = (pmc_traffic(args.workload, wl.pmc_kernels, launches / args.steps, n)
-                            if launches else (None, None))
-    extra = wl.extra_roofline(launches / args.steps, avg_s) if (
-        launches and hasattr(wl, "extra_roofline")) else {}
-
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = wl.cpu_baseline(args.cpu_seconds)
-
+    names = ORDER if args.workload == "all" else (args.workload,)
+    results = {}
+    for name in names:
+        t0 = time.perf_counter()
+        results[name] = run_workload(name, args, dev, rank, world,
+                                     args.cpu_seconds if name == names[0]
+                                     else min(args.cpu_seconds, 8.0))
+        if rank == 0:
+            print(f"[bench] {name}: {results[name]['value'] / 1e6:.1f} M rows/s, "
+                  f"{results[name]['ms_per_step']:.2f} ms/step "
+                  f"({time.perf_counter() - t0:.0f} s with data build)",
+                  file=sys.stderr, flush=True)
     if rank == 0:
-        line = {
-            "metric": "rows/s per training iteration",
-            "value": value,
-            "unit": "rows/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": el / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic, generated on device (torch Philox, seeded per rank)",
-            "config": {"workload": wl.describe(), "rows_per_gpu": n,
-                       "parallelism": f"dp{world} (row shards, RCCL all-reduce merge)"},
-            "roofline": {"kernel": wl.kernel, "bound": wl.bound, "achieved": achieved,
-                         "peak": peak, "unit": unit,
-                         "frac": (achieved / peak) if achieved else None,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "avg_launch_ms": avg_s * 1e3, "launches": launches,
-                         "work_per_launch": per_launch,
-                         "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
-                         **extra},
-            "cpu_baseline": cpu,
-        }
+        line = dict(results[names[0]])
+        if len(names) > 1:
+            line["workloads"] = {k: results[k] for k in names[1:]}
         print(json.dumps(line), flush=True)
     if world > 1:
         parallel.shutdown()

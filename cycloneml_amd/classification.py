@@ -56,8 +56,10 @@ class LogisticRegressionModel:
     interceptVector, as LogisticRegressionModel holds them."""
 
     def __init__(self, coefficientMatrix, interceptVector, numClasses, isMultinomial,
-                 objectiveHistory=()):
+                 objectiveHistory=(), fitIntercept=True):
         self.coefficientMatrix = np.asarray(coefficientMatrix, dtype=np.float64)
+        # the model's fitIntercept param (copyValues of its estimator; default true)
+        self.fitIntercept = bool(fitIntercept)
         self.interceptVector = np.asarray(interceptVector, dtype=np.float64)
         self.numClasses = int(numClasses)
         self.isMultinomial = bool(isMultinomial)
@@ -299,7 +301,8 @@ class LogisticRegression:
                 icpt[idx] = math.inf
             else:
                 icpt = np.array([math.inf if numClasses == 2 else -math.inf])
-            return LogisticRegressionModel(coef, icpt, numClasses, isMultinomial, [0.0])
+            return LogisticRegressionModel(coef, icpt, numClasses, isMultinomial, [0.0],
+                                           fitIntercept=self.fitIntercept)
 
         self._check_bounds(numCoefficientSets, numFeatures)
         bounded = self.usingBoundConstrainedOptimization
@@ -335,7 +338,8 @@ class LogisticRegression:
             coefM = coefM - coefM.sum(axis=0) / numCoefficientSets
         if fitIntercept and isMultinomial and not bounded:
             icpt = icpt - icpt.sum() / len(icpt)
-        return LogisticRegressionModel(coefM, icpt, numClasses, isMultinomial, history)
+        return LogisticRegressionModel(coefM, icpt, numClasses, isMultinomial, history,
+                                       fitIntercept=self.fitIntercept)
 
     def _create_optimizer(self, numCoefficientSets, numFeatures, featuresStd, lower=None,
                           upper=None):
@@ -364,8 +368,10 @@ class LogisticRegression:
         nFPI = numFeatures + 1 if self.fitIntercept else numFeatures
         M = np.zeros((nCS, nFPI))
         m = self.initialModel
+        # :838-844 -- shape, intercept count AND the same fitIntercept
         valid = m is not None and m.coefficientMatrix.shape == (nCS, numFeatures) and \
-            m.interceptVector.shape[0] == nCS
+            m.interceptVector.shape[0] == nCS and \
+            getattr(m, "fitIntercept", True) == self.fitIntercept
         if valid:
             M[:, :numFeatures] = m.coefficientMatrix * featuresStd
             if self.fitIntercept:

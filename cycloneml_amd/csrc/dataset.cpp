@@ -270,6 +270,11 @@ int cyc_kmeans_iter_measure(cyc_dataset ds, int32_t measure, const double* cente
                             double* cost, int32_t* assign_opt) {
   CYC_REQUIRE(ds != nullptr && centers && sums && wsum && cost, "arguments must not be null");
   CYC_REQUIRE(k >= 1, "Number of clusters must be positive but got " + std::to_string(k));
+  // validated before the plan cache: an unknown measure must not reuse a
+  // cached Euclidean plan
+  CYC_REQUIRE(measure == CYC_DISTANCE_EUCLIDEAN || measure == CYC_DISTANCE_COSINE,
+              "distanceMeasure must be one of: euclidean, cosine. " + std::to_string(measure) +
+                  " provided.");
   DeviceGuard g(ds->device);
   // plans and row images per (k, measure)
   const int key = k * 2 + (measure == CYC_DISTANCE_COSINE ? 1 : 0);

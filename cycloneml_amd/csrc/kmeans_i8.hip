@@ -1178,13 +1178,24 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
   // the three-limb pass (rows with more than kCandMax candidates) and the
   // candidate pass touch disjoint rows and only append to `list`: the
   // three-limb pass runs on a side stream of this host thread beside it
-  thread_local hipStream_t side = nullptr;
-  thread_local hipEvent_t fork = nullptr, join = nullptr;
-  if (!side) {
-    CYC_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-    CYC_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
-    CYC_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+  // (one per device: a host thread may drive plans on several GPUs; the
+  // caller's DeviceGuard made `st`'s device current)
+  constexpr int kMaxDev = 64;
+  thread_local hipStream_t sides[kMaxDev] = {};
+  thread_local hipEvent_t forks[kMaxDev] = {}, joins[kMaxDev] = {};
+  int dev = 0;
+  CYC_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDev) {
+    cyc::set_error("device index out of range");
+    return CYC_ERR_INVALID_ARG;
   }
+  if (!sides[dev]) {
+    CYC_HIP(hipStreamCreateWithFlags(&sides[dev], hipStreamNonBlocking));
+    CYC_HIP(hipEventCreateWithFlags(&forks[dev], hipEventDisableTiming));
+    CYC_HIP(hipEventCreateWithFlags(&joins[dev], hipEventDisableTiming));
+  }
+  hipStream_t side = sides[dev];
+  hipEvent_t fork = forks[dev], join = joins[dev];
   CYC_HIP(hipEventRecord(fork, st));
   CYC_HIP(hipStreamWaitEvent(side, fork, 0));
   if ((rc = launch_screen32<S, W, 3, true>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp,

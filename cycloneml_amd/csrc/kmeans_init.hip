@@ -168,15 +168,23 @@ int cyc_kmeans_parallel_sample_dev(const double* costs, const int64_t* part_star
   }
   // the jump matrices stay resident for the process (never freed: no
   // device call from a static destructor after the runtime's teardown)
+  // (one copy per device: the caller's stream may live on any GPU)
+  constexpr int kMaxDev = 64;
   static std::mutex mu;
-  static uint64_t* jump = nullptr;
+  static uint64_t* jumps[kMaxDev] = {};
   std::lock_guard<std::mutex> g(mu);
-  int rc;
-  if (!jump) {
-    CYC_HIP(hipMalloc((void**)&jump, sizeof(uint64_t) * 64 * 64));
-    CYC_HIP(hipMemcpy(jump, jump_matrices_host(), sizeof(uint64_t) * 64 * 64,
+  int rc, dev = 0;
+  CYC_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDev) {
+    cyc::set_error("device index out of range");
+    return CYC_ERR_INVALID_ARG;
+  }
+  if (!jumps[dev]) {
+    CYC_HIP(hipMalloc((void**)&jumps[dev], sizeof(uint64_t) * 64 * 64));
+    CYC_HIP(hipMemcpy(jumps[dev], jump_matrices_host(), sizeof(uint64_t) * 64 * 64,
                       hipMemcpyHostToDevice));
   }
+  uint64_t* jump = jumps[dev];
   cyc::DeviceBuffer meta;
   const size_t b1 = sizeof(int64_t) * (num_parts + 1), b2 = b1, b3 = sizeof(uint64_t) * num_parts;
   if ((rc = meta.reserve(b1 + b2 + b3))) return rc;

@@ -172,11 +172,17 @@ def take_sample_indices(partition_lengths, num: int, seed: int) -> list:
 
 
 def _distinct_rows(rows: np.ndarray) -> np.ndarray:
-    """`.map(_.vector).distinct`: first occurrences in order (vectors equal
-    when their values' bits are)."""
+    """`.map(_.vector).distinct` (Scala Seq.distinct): first occurrences in
+    order, vectors equal as Vector.equals compares them -- element by
+    element with `!=` on doubles (mllib Vectors.equals), so -0.0 equals 0.0
+    and a vector holding a NaN equals nothing, not even another copy of
+    itself (Scala's HashSet tests `==`, i.e. equals, not identity)."""
     seen, keep = set(), []
     for i in range(rows.shape[0]):
-        key = rows[i].tobytes()
+        if np.isnan(rows[i]).any():
+            keep.append(i)
+            continue
+        key = (rows[i] + 0.0).tobytes()          # -0.0 + 0.0 = +0.0
         if key not in seen:
             seen.add(key)
             keep.append(i)

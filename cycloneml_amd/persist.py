@@ -200,13 +200,22 @@ def _check_new_path(path, overwrite):
 KMEANS_CLASS = "org.apache.spark.mllib.clustering.KMeansModel"
 
 
-def save_kmeans_model(model, path, distanceMeasure="euclidean", overwrite=False):
-    """KMeansModel.SaveLoadV2_0.save (KMeansModel.scala:195-206)."""
+def save_kmeans_model(model, path, distanceMeasure="euclidean", overwrite=False,
+                      version="2.0"):
+    """KMeansModel.SaveLoadV2_0.save (KMeansModel.scala:195-206); version
+    "1.0" writes SaveLoadV1_0's layout (:162-171: metadata without
+    distanceMeasure / trainingCost), the format of older Spark releases."""
     pa, _ = _pa()
     _check_new_path(path, overwrite)
-    meta = json.dumps({"class": KMEANS_CLASS, "version": "2.0", "k": int(model.k),
-                       "distanceMeasure": distanceMeasure,
-                       "trainingCost": float(model.trainingCost)}, separators=(",", ":"))
+    if version == "1.0":
+        meta = json.dumps({"class": KMEANS_CLASS, "version": "1.0", "k": int(model.k)},
+                          separators=(",", ":"))
+    elif version == "2.0":
+        meta = json.dumps({"class": KMEANS_CLASS, "version": "2.0", "k": int(model.k),
+                           "distanceMeasure": distanceMeasure,
+                           "trainingCost": float(model.trainingCost)}, separators=(",", ":"))
+    else:
+        raise ValueError(f"unsupported KMeansModel format version {version}")
     _write_text(os.path.join(path, "metadata"), meta)
     fields = [pa.field("id", pa.int32(), nullable=False), pa.field("point", _arrow_vector())]
     spark = [_field("id", "integer", False), _field("point", _udt("vector", ml=False))]
@@ -215,13 +224,20 @@ def save_kmeans_model(model, path, distanceMeasure="euclidean", overwrite=False)
 
 
 def load_kmeans_model(path):
-    """KMeansModel.SaveLoadV2_0.load (:208-222): centers sorted by id;
-    trainingCost from the metadata; numIter unknown (-1 in the reference)."""
+    """KMeansModel.load (KMeansModel.scala:130-145): SaveLoadV2_0.load
+    (:208-222) -- centers sorted by id, trainingCost and distanceMeasure from
+    the metadata -- or SaveLoadV1_0.load (:173-185), whose model is
+    `new KMeansModel(centers)`: Euclidean, trainingCost 0.0.  numIter is
+    unknown (-1 in the reference) either way."""
     from .clustering import KMeansModel
     meta = json.loads(_read_text(os.path.join(path, "metadata")))
-    if meta.get("class") != KMEANS_CLASS or meta.get("version") != "2.0":
+    version = meta.get("version")
+    if meta.get("class") != KMEANS_CLASS or version not in ("1.0", "2.0"):
         raise ValueError(f"KMeansModel.load did not recognize model with (className, format "
-                         f"version): ({meta.get('class')}, {meta.get('version')}).")
+                         f"version):({meta.get('class')}, {version}).  Supported:\n"
+                         f"  ({KMEANS_CLASS}, 1.0)\n  ({KMEANS_CLASS}, 2.0)")
+    if version == "1.0":
+        meta = {"k": meta["k"]}             # V1 defaults below: euclidean, cost 0.0
     rows = _read_parquet_rows(os.path.join(path, "data"))
     if len(rows) != int(meta["k"]):
         raise ValueError(f"expected {meta['k']} centers, found {len(rows)}")
@@ -260,10 +276,13 @@ def save_logistic_model(model, path, estimator=None, uid=None, overwrite=False):
     """LogisticRegressionModelWriter.saveImpl (LogisticRegression.scala:1314-1322)."""
     pa, _ = _pa()
     _check_new_path(path, overwrite)
+    params = _lr_params(estimator)
+    if estimator is None and not getattr(model, "fitIntercept", True):
+        params["fitIntercept"] = False          # the model's own param, when set
     meta = {"class": LR_CLASS, "timestamp": int(time.time() * 1000),
             "sparkVersion": SPARK_VERSION,
             "uid": uid or f"logreg_{uuid.uuid4().hex[:12]}",
-            "paramMap": _lr_params(estimator), "defaultParamMap": dict(_LR_DEFAULTS)}
+            "paramMap": params, "defaultParamMap": dict(_LR_DEFAULTS)}
     _write_text(os.path.join(path, "metadata"), json.dumps(meta, separators=(",", ":")))
     fields = [pa.field("numClasses", pa.int32(), nullable=False),
               pa.field("numFeatures", pa.int32(), nullable=False),
@@ -303,6 +322,7 @@ def load_logistic_model(path):
                                 bool(r["isMultinomial"]))
     m.uid = meta.get("uid")
     m.params = dict(meta.get("defaultParamMap", {}), **meta.get("paramMap", {}))
+    m.fitIntercept = bool(m.params.get("fitIntercept", True))
     return m
 
 

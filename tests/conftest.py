@@ -18,3 +18,14 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+def heartbeat(msg: str) -> None:
+    """Progress of a long GPU test, appended to gpurun_out/heartbeat.log when
+    that directory exists (pytest captures stdout; a GPU run whose outputs
+    stay silent for minutes is taken to be hung)."""
+    import time
+    d = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(d):
+        with open(os.path.join(d, "heartbeat.log"), "a") as f:
+            f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")

@@ -158,3 +158,49 @@ def test_shard_bounds_cover_rows():
             assert b[0][0] == 0 and b[-1][1] == n
             assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
             assert max(e - s for s, e in b) - min(e - s for s, e in b) <= 1
+
+
+def _bench_rows_rank(rank, world):
+    """bench.py's strong-scaling split at world size 2: every rank's rows of
+    configs 3-5 summed over the ranks (one all-reduce, as the bench's
+    max_over_ranks) equal the job's rows, and the uncapped totals are the
+    BASELINE configs' rows; KMeans config 2 stays 10M per GPU (weak)."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    import bench
+    ok = True
+    for name in bench.ORDER:
+        n, mode, total = bench.rows_per_gpu(name, "auto", world, rank)
+        t = torch.tensor([n], dtype=torch.int64)
+        dist.all_reduce(t)
+        ok = ok and int(t.item()) == total
+        if name == "kmeans":
+            ok = ok and mode == "weak" and n == 10_000_000
+        else:
+            ok = ok and mode == "strong"
+            if name != "gramian":          # 100M Gramian rows exceed 2 x 30M resident
+                ok = ok and total == bench.CONFIG_ROWS[name]
+    return bool(ok)
+
+
+def test_bench_strong_split_two_ranks():
+    assert _run(_bench_rows_rank) == {0: True, 1: True}
+
+
+def test_bench_rows_per_gpu_table():
+    """The split of BASELINE's totals for N = 1..8 (bench.py --scaling auto)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for world in (1, 2, 4, 8):
+        for name in bench.ORDER:
+            per = [bench.rows_per_gpu(name, "auto", world, r) for r in range(world)]
+            assert all(p[2] == per[0][2] for p in per)
+            assert sum(p[0] for p in per) == per[0][2]
+            assert max(p[0] for p in per) <= bench.MAX_RESIDENT_ROWS[name]
+    assert bench.rows_per_gpu("gramian", "auto", 1, 0) == (30_000_000, "strong", 30_000_000)
+    assert bench.rows_per_gpu("gramian", "auto", 4, 3) == (25_000_000, "strong", 100_000_000)
+    assert bench.rows_per_gpu("lr_sparse", "auto", 8, 7) == (25_000_000, "strong", 200_000_000)
+    assert bench.rows_per_gpu("lr_multi", "auto", 8, 0) == (6_250_000, "strong", 50_000_000)
+    assert bench.rows_per_gpu("kmeans", "auto", 8, 5) == (10_000_000, "weak", 80_000_000)
+    assert bench.rows_per_gpu("lr_sparse", "weak", 2, 1) == (200_000_000, "weak", 400_000_000)

@@ -263,3 +263,18 @@ def test_kmeans_run_csr_without_initial_model(cuda, mode, measure):
         KMeansModel(C0, distanceMeasure=measure)).run_csr(*dev, d)
     # the CSR cluster sums are device atomics: equal to rounding
     np.testing.assert_allclose(m1.clusterCenters, m2.clusterCenters, rtol=1e-12, atol=1e-12)
+
+
+def test_distinct_rows_vector_equality():
+    """`.distinct` with Vector.equals semantics (mllib Vectors.equals: `!=`
+    on doubles): -0.0 equals 0.0 (the first occurrence is kept), NaN rows are
+    never merged, order of first occurrence."""
+    from cycloneml_amd.kmeans_init import _distinct_rows
+    nan = float("nan")
+    R = np.array([[0.0, 1.0], [-0.0, 1.0], [nan, 2.0], [nan, 2.0], [3.0, -0.0], [3.0, 0.0],
+                  [0.0, 1.0]])
+    got = _distinct_rows(R)
+    assert got.shape == (4, 2)
+    assert np.signbit(got[0, 0]) == False and got[0, 1] == 1.0       # noqa: E712
+    assert np.isnan(got[1, 0]) and np.isnan(got[2, 0])
+    assert got[3, 0] == 3.0 and np.signbit(got[3, 1])                 # first: -0.0

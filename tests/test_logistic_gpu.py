@@ -200,57 +200,85 @@ def test_sparse_config5_csc_path(cuda):
     _rel_close(a5.gradientSumArray.cpu().numpy(), st["grad"])
 
 
-@pytest.mark.timeout(600)
-def test_sparse_config5_bench_shard_tiles(cuda):
-    """bench.py's lr_sparse shard at its benched size (25M rows x 1M
-    features, 64 nonzeros per row, fitIntercept => fitWithMean with a real
-    scaledMean, LogisticRegression.scala:950-954), on the tiles layout built
-    by row-block-aligned appends with the CSR freed chunk by chunk, as the
-    bench does.  Checks: (1) the first 40,000 rows (5 row blocks) equal the
-    restatement within 1e-10; (2) linearity: the whole shard's state equals
-    the sum of its two halves' within 1e-12; (3) bitwise reproducible."""
+@pytest.mark.timeout(900)
+def test_sparse_config5_full_size(cuda):
+    """BASELINE config 5 at the size bench.py times, on the rows it times:
+    200M rows x 1M features, 64 nonzeros per row (12.8G nonzeros, past 2^32,
+    154 GB of tiles layout), generated by bench.lr_sparse_chunks and appended
+    chunk by chunk with the CSR freed, fitIntercept => fitWithMean with a
+    real scaledMean (BinaryLogisticBlockAggregator.scala:81-145).  Checks:
+    (1) bitwise reproducible; (2) the layout's FIRST and LAST 40,000 rows --
+    the last ones at nonzero offsets above 2^32 -- equal the restatement
+    within 1e-10, selected inside the full 200M-row layout by a weight mask
+    (zero-weight rows add nothing, :107-125); (3) linearity: the whole
+    layout's state equals the sum of two unequal parts' (120M + 80M rows,
+    rebuilt from the same seeds) within 1e-12."""
+    import os
+    import sys
     import torch
     from cycloneml_amd.optim import (BinaryLogisticBlockAggregator, DeviceInstanceBlock,
                                      SparseTiles)
-    n, F, k = 25_000_000, 1_000_000, 64
-    chunk = 64 * 8192
-    half = (n // 2) // chunk * chunk
-    coef = np.random.default_rng(4).normal(size=F + 1) * 0.01
-    sm = np.random.default_rng(5).uniform(0, 1, F) * 0.5
-    whole = SparseTiles(F, n, n * k)
-    h1, h2 = SparseTiles(F, half, half * k), SparseTiles(F, n - half, (n - half) * k)
-    labels = torch.empty(n, dtype=torch.float64, device=cuda)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from conftest import heartbeat
+    n, F, k = 200_000_000, 1_000_000, 64
     sub_m = 40_000
-    sub = None
-    for c, s in enumerate(range(0, n, chunk)):
-        e = min(n, s + chunk)
-        rp, ci, vv, lb = _config5_rows(e - s, F, k, 100 + c, cuda)
-        labels[s:e] = lb
-        whole.append(rp, ci, vv)
-        (h1 if s < half else h2).append(rp, ci, vv)
-        if s == 0:
-            sub = tuple(a.cpu().numpy() for a in (rp[:sub_m + 1], ci[:sub_m * k],
-                                                 vv[:sub_m * k], lb[:sub_m]))
-        del rp, ci, vv, lb
-    assert whole.rows == n and whole.nnz == n * k
+    coef = np.random.default_rng(4).normal(size=F + 1) * 0.01
+    sm = np.random.default_rng(5).uniform(0.0, 0.014, F)
+    sm_dev = torch.as_tensor(sm, device=cuda)
 
-    def run(t, lab):
-        blk = DeviceInstanceBlock(lab, None, tiles=t, numFeatures=F)
-        return BinaryLogisticBlockAggregator(np.ones(F), sm, True, True, coef,
+    def run(t, lab, w=None):
+        blk = DeviceInstanceBlock(lab, w, tiles=t, numFeatures=F)
+        return BinaryLogisticBlockAggregator(np.ones(F), sm_dev, True, True, coef,
                                              device=cuda).add(blk)._state.cpu().numpy()
+
+    def host_rows(rp, ci, vv, lb, lo, hi):
+        a, b = int(rp[lo]), int(rp[hi])
+        return ((rp[lo:hi + 1] - a).cpu().numpy(), ci[a:b].cpu().numpy(),
+                vv[a:b].cpu().numpy(), lb[lo:hi].cpu().numpy())
+
+    whole = SparseTiles(F, n, n * k)
+    labels = torch.empty(n, dtype=torch.float64, device=cuda)
+    head = tail = None
+    for s, e, rp, ci, vv, yc in bench.lr_sparse_chunks(n, cuda, 0, F, k):
+        labels[s:e] = yc
+        whole.append(rp, ci, vv)
+        if s == 0:
+            head = host_rows(rp, ci, vv, yc, 0, sub_m)
+        if e == n:
+            tail = host_rows(rp, ci, vv, yc, e - s - sub_m, e - s)
+        if s % (64 * bench.LR_SPARSE_CHUNK) == 0:
+            heartbeat(f"config5 whole layout: {e} rows")
+        del rp, ci, vv, yc
+    assert whole.rows == n and whole.nnz == n * k and whole.nnz > 2 ** 32
     full = run(whole, labels)
     assert np.array_equal(full, run(whole, labels))
-    parts = run(h1, labels[:half]) + run(h2, labels[half:])
+    assert full[F + 2] == n
+    for lo, rows in ((0, head), (n - sub_m, tail)):
+        w = torch.zeros(n, dtype=torch.float64, device=cuda)
+        w[lo:lo + sub_m] = 1.0
+        got = run(whole, labels, w)
+        del w
+        rp, ci, vv, lb = rows
+        st = dict(grad=np.zeros(F + 1), loss=0.0, weight=0.0)
+        oracle.binary_logistic_add(dict(labels=lb, weights=None, rowptr=rp, colidx=ci,
+                                        values=vv, F=F), coef, True, True, sm, st)
+        _rel_close(got[:F + 1], st["grad"])
+        assert abs(got[F + 1] - st["loss"]) <= 1e-10 * abs(st["loss"])
+        assert got[F + 2] == sub_m
+        heartbeat(f"config5 rows {lo}.. vs the restatement: ok")
+    del whole
+    torch.cuda.empty_cache()
+    cut = 229 * bench.LR_SPARSE_CHUNK                  # 120,061,952 rows: unequal parts
+    h1, h2 = SparseTiles(F, cut, cut * k), SparseTiles(F, n - cut, (n - cut) * k)
+    for s, e, rp, ci, vv, yc in bench.lr_sparse_chunks(n, cuda, 0, F, k):
+        assert torch.equal(yc, labels[s:e])            # the same rows again
+        (h1 if s < cut else h2).append(rp, ci, vv)
+        if s % (64 * bench.LR_SPARSE_CHUNK) == 0:
+            heartbeat(f"config5 parts: {e} rows")
+        del rp, ci, vv, yc
+    parts = run(h1, labels[:cut]) + run(h2, labels[cut:])
     _rel_close(full, parts, rtol=1e-12)
-    del whole, h1, h2
-    rp, ci, vv, lb = sub
-    st = dict(grad=np.zeros(F + 1), loss=0.0, weight=0.0)
-    oracle.binary_logistic_add(dict(labels=lb, weights=None, rowptr=rp, colidx=ci, values=vv,
-                                    F=F), coef, True, True, sm, st)
-    ts = SparseTiles.from_csr(*(torch.as_tensor(a, device=cuda) for a in (rp, ci, vv)), F)
-    got = run(ts, torch.as_tensor(lb, device=cuda))
-    _rel_close(got[:F + 1], st["grad"])
-    assert abs(got[F + 1] - st["loss"]) <= 1e-12 * abs(st["loss"]) and got[F + 2] == sub_m
 
 
 @pytest.mark.parametrize("fi,fwm", [(True, False), (True, True), (False, False)])

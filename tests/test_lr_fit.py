@@ -230,3 +230,22 @@ def test_bound_params_checks():
         .setLowerBoundsOnCoefficients([[1.0] * 4])
     with pytest.raises(N.IllegalArgumentException, match="less than or equal"):
         lr.train_from_summary(4, hist, mean, std, None)
+
+
+def test_initial_model_needs_same_fit_intercept():
+    """createInitialSolution (LogisticRegression.scala:836-848): an initial
+    model is used only when its shape AND its fitIntercept match; otherwise
+    the fit starts from the histogram's intercept as without a model."""
+    from cycloneml_amd.classification import LogisticRegressionModel
+    F = 3
+    hist = np.array([30.0, 70.0])
+    std = np.array([1.0, 2.0, 0.5])
+    lr = LogisticRegression(fitIntercept=True)
+    base = lr._initial_solution(2, F, hist, std, False)
+    m_no = LogisticRegressionModel([[0.5, -1.0, 2.0]], [0.25], 2, False, fitIntercept=False)
+    lr.setInitialModel(m_no)
+    assert np.array_equal(lr._initial_solution(2, F, hist, std, False), base)
+    m_yes = LogisticRegressionModel([[0.5, -1.0, 2.0]], [0.25], 2, False, fitIntercept=True)
+    lr.setInitialModel(m_yes)
+    np.testing.assert_array_equal(lr._initial_solution(2, F, hist, std, False),
+                                  [0.5, -2.0, 1.0, 0.25])

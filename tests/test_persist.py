@@ -115,3 +115,26 @@ def test_wrong_class_is_refused(tmp_path):
     KMeansModel(np.zeros((2, 2))).save(p)
     with pytest.raises(ValueError, match="Expected class name"):
         LogisticRegressionModel.load(p)
+
+
+def test_kmeans_model_v1_format(tmp_path):
+    """KMeansModel.load of SaveLoadV1_0's layout (KMeansModel.scala:156-186:
+    metadata {class, version 1.0, k} only): `new KMeansModel(centers)`, so
+    Euclidean with trainingCost 0.0; an unknown version is refused with the
+    reference's message."""
+    rng = np.random.default_rng(1)
+    C = rng.normal(size=(4, 3))
+    p = str(tmp_path / "km1")
+    persist.save_kmeans_model(KMeansModel(C, trainingCost=3.0), p, version="1.0")
+    assert persist.read_metadata(p) == {"class": "org.apache.spark.mllib.clustering.KMeansModel",
+                                        "version": "1.0", "k": 4}
+    m = KMeansModel.load(p)
+    assert np.array_equal(m.clusterCenters, C)
+    assert m.trainingCost == 0.0 and m.numIter == -1 and m.distanceMeasure == "euclidean"
+    meta = os.path.join(p, "metadata")
+    for f in os.listdir(meta):
+        if f.startswith("part-"):
+            txt = open(os.path.join(meta, f)).read().replace('"1.0"', '"3.0"')
+            open(os.path.join(meta, f), "w").write(txt)
+    with pytest.raises(ValueError, match="did not recognize model"):
+        KMeansModel.load(p)
