@@ -1,5 +1,5 @@
-// tiles.hip -- the row-block x column-tile layout of a sparse (CSR) shard for
-// the binary block aggregators: BinaryLogisticBlockAggregator.add
+// tiles.hip -- the row-block x column-chunk layout of a sparse (CSR) shard
+// for the binary block aggregators: BinaryLogisticBlockAggregator.add
 // (ml/optim/aggregator/BinaryLogisticBlockAggregator.scala:81-145) and the
 // Hinge / LeastSquares / Huber / AFT aggregators of the same shape.
 //
@@ -9,32 +9,36 @@
 // gathers one fp64 multiplier per nonzero.  At F = 1M with 64 random columns
 // per row those gathers are L2 requests, and round 1 measured both passes
 // bound by that request rate (~146 G gathers/s), not by HBM.  Here the shard
-// is cut into row blocks of R = 8192 rows and column tiles of W = 8192
-// columns; a (row block, column tile) segment stores its nonzeros with the
-// row inside the block and the column inside the tile packed into 32 bits,
-// so both gathers become LDS reads:
-//   margin pass    one workgroup per row block holds the block's 8192 partial
-//                  dots in LDS and streams the coefficient tiles through LDS
-//                  (all workgroups sweep the same tiles: L2 hits);
-//   gradient pass  one workgroup per column tile (and row range) holds the
-//                  tile's 8192 gradient sums in LDS and streams the
-//                  multiplier slices through LDS.
-// Either pass reads 12 B per nonzero (value + packed ids) and nothing else
-// per nonzero.  Every segment is cut into 8 x 8 sub-segments (row range i x
-// column range j, an eighth of each); wave i owns the rows of range i in the
-// margin pass and wave j the columns of range j in the gradient pass, so each
-// LDS sum has exactly one writer wave and its adds land in a fixed order:
-// a row's dot in column order from 0.0 (the reference's CSR row loop,
-// BLAS.scala:777-789, bit for bit), a column's gradient sum in row order
-// within a row range (the transposed loop :790-804).
+// is cut into row blocks of R = 2048 rows and column chunks of W <= 2048
+// columns; a (row block, column chunk) segment stores its nonzeros in CSR
+// order with the row inside the block and the column inside the chunk
+// packed into 32 bits, so both gathers become LDS reads:
+//   margin pass    one workgroup per 8 row blocks (16384 rows): their partial
+//                  dots in LDS (128 KB), the coefficient chunks streamed
+//                  through LDS (16 KB each; all workgroups sweep the same
+//                  chunks: L2 hits); wave i walks segment (8 sb + i, c), ONE
+//                  contiguous run;
+//   gradient pass  one workgroup per 8 column chunks (16384 columns) and row
+//                  range: their gradient sums in LDS (128 KB), the multiplier
+//                  slices streamed through LDS (16 KB each); wave j walks
+//                  segment (rb, 8 st + j), ONE contiguous run.
+// Either pass reads 12 B per nonzero (value + packed ids) from HBM and
+// stages one 16 KB slice (L2) per 8 segments: 7.6 B per nonzero at F = 1M,
+// 64 nonzeros per row (the 8192 x 8192 tiles of round 2 staged 15.3 B per
+// nonzero, and their waves walked 8 sub-segments each).  Each LDS sum
+// has exactly one writer wave and its adds land in a fixed order: a row's
+// dot in column order from 0.0 (the reference's CSR row loop, BLAS.scala:
+// 777-789, bit for bit: chunks in order, CSR order inside a segment), a
+// column's gradient sum in row order within a row range (the transposed
+// loop :790-804).
 //
 // Built once per dataset (like InstanceBlock.blokifyWithMaxMemUsage +
 // persist, ml/feature/Instance.scala:146-187, LogisticRegression.scala:
 // 967-970) by appending CSR row blocks: per chunk a stable radix sort of the
-// nonzeros by (row block, tile, row range, column range) keeps each
-// sub-segment in CSR order.  The CSR input can be freed after the append, so
-// the layout is the only copy of the shard in HBM (12 B per nonzero + 0.5 %
-// of segment offsets): a 200M x 1M, 64-per-row shard takes 157 GB.
+// nonzeros by segment keeps each segment in CSR order.  The CSR input can be
+// freed after the append, so the layout is the only copy of the shard in
+// HBM (12 B per nonzero + 8 B per segment): a 200M x 1M, 64-per-row shard
+// takes 154 GB.
 #pragma clang fp contract(off)
 
 #include <hip/hip_runtime.h>
@@ -51,45 +55,52 @@
 #include "tiles.hpp"
 
 struct cyc_tiles_s {
-  int F = 0, T = 1, Wt = 1, WS = 1;
+  int F = 0, T = 1, Wt = 1;
   int64_t capRows = 0, capNnz = 0, n = 0, nnz = 0;
   bool sealed = false;    // ends with a partial row block: no further appends
   std::mutex mu;
-  cyc::DeviceBuffer segStart, subRel, idx, vals;
+  cyc::DeviceBuffer segStart, idx, vals;
 };
 
 namespace {
 
 using cyc::kTileCols;
-using cyc::kTileRowRange;
 using cyc::kTileRows;
-using cyc::kTileSub;
+using cyc::kTileSuperCols;
+using cyc::kTileSuperRows;
 using cyc::kTileWaves;
 
-constexpr int kTPB = 512;                      // threads per workgroup (8 waves)
-constexpr int kCPT = kTileCols / kTPB;         // coefficient / gradient entries per thread
-constexpr int kRPT = kTileRows / kTPB;         // rows per thread
-constexpr int kCap = 10;                       // nonzeros per lane prefetched per run
+constexpr int kTPB = 64 * kTileWaves;          // threads per workgroup (8 waves)
+constexpr int kCPT = kTileCols / kTPB;         // staged coefficients per thread
+constexpr int kMPT = kTileRows / kTPB;         // staged multipliers per thread
+constexpr int kDPT = kTileSuperRows / kTPB;    // dots per thread (margin)
+constexpr int kGPT = kTileSuperCols / kTPB;    // gradient sums per thread
+constexpr int kCap = 5;                        // nonzeros per lane in flight per run
+
+// columns per chunk: an eighth of F (so a gradient workgroup's 8 waves all
+// have a chunk when F is small), a multiple of 64, at most kTileCols
+int chunk_cols(int F) {
+  const int w = (int)std::min<int64_t>(kTileCols, ((int64_t)F + 8 * 64 - 1) / (8 * 64) * 64);
+  return std::max(w, 64);
+}
 
 // ----------------------------------------------------------------- build
 
-// Per nonzero of rows [0, rows) of a chunk: its sub-segment key
-// ((rb * T + t) * 8 + i) * 8 + j and its packed ids.  Wave per row.
+// Per nonzero of rows [0, rows) of a chunk: its segment key rb * T + c and
+// its packed ids.  Wave per row.
 __global__ void k_tile_keys(const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
-                            int64_t rows, int64_t q0, int T, int Wt, int WS,
+                            int64_t rows, int64_t q0, int T, int Wt,
                             uint32_t* __restrict__ keys, uint32_t* __restrict__ packed) {
   const int lane = threadIdx.x & 63;
   const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < rows; r += stride) {
     const int64_t rbl = r / kTileRows;
     const uint32_t rin = (uint32_t)(r % kTileRows);
-    const uint32_t i = rin / kTileRowRange;
     const int64_t p1 = rowptr[r + 1] - q0;
     for (int64_t p = rowptr[r] - q0 + lane; p < p1; p += 64) {
       const int c = colidx[p];
       const int t = c / Wt, cin = c - t * Wt;
-      const uint32_t j = (uint32_t)(cin / WS);
-      keys[p] = ((uint32_t)(rbl * T + t) * kTileWaves + i) * kTileWaves + j;
+      keys[p] = (uint32_t)(rbl * T + t);
       packed[p] = (rin << 16) | (uint32_t)cin;
     }
   }
@@ -106,27 +117,15 @@ __global__ void k_tile_gather(const uint32_t* __restrict__ perm, int64_t cnt,
   }
 }
 
-// starts[key] = first sorted position with key' >= key, key in [0, nkeys]
+// segStart[seg0 + key] = base + first sorted position with key' >= key,
+// key in [0, nkeys)
 __global__ void k_tile_starts(const uint32_t* __restrict__ keys, int64_t cnt, int64_t nkeys,
-                              int64_t* __restrict__ starts) {
+                              int64_t seg0, int64_t base, int64_t* __restrict__ segStart) {
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= cnt;
        q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t prev = q == 0 ? -1 : (int64_t)keys[q - 1];
     const int64_t cur = q == cnt ? nkeys : (int64_t)keys[q];
-    for (int64_t k = prev + 1; k <= cur; ++k) starts[k] = q;
-  }
-}
-
-// segment starts (absolute) and sub-segment offsets (relative) of the chunk
-__global__ void k_tile_offsets(const int64_t* __restrict__ starts, int64_t nkeys, int64_t seg0,
-                               int64_t base, int64_t* __restrict__ segStart,
-                               uint32_t* __restrict__ subRel) {
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nkeys;
-       k += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = k / kTileSub;
-    const int64_t s0 = starts[s * kTileSub];
-    if (k % kTileSub == 0) segStart[seg0 + s] = base + s0;
-    subRel[(seg0 + s) * kTileSub + k % kTileSub] = (uint32_t)(starts[k] - s0);
+    for (int64_t k = prev + 1; k <= cur && k < nkeys; ++k) segStart[seg0 + k] = base + q;
   }
 }
 
@@ -144,137 +143,152 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t by
                                            (int)std::min<int64_t>(bytes, 0x7fffffff), 0x00020000);
 }
 
-// Margin pass, persistent over (row block, column tile) steps: this
-// workgroup's row blocks rb = blockIdx.x + i * gridDim.x, each swept over the
-// T column tiles, as one flat sequence of steps g.  Per step: the
-// coefficient tile goes registers -> LDS (the next step's tile is loaded
-// meanwhile, an L2 hit), and each wave walks its row range's sub-segments
-// (one contiguous run); the runs of the next TWO steps are in flight in
-// registers (~100 KB per CU), across row-block boundaries too.
-// The layout's arrays come as separate __restrict__ arguments: the
-// per-step segment offsets are uniform, and only restrict-qualified
-// read-only pointers let the compiler fetch them with scalar loads (counted
-// by lgkmcnt), so reading them never waits on the runs in flight (vmcnt).
 struct TileDims {
   int64_t n, nRB;
   int F, T, Wt;
 };
 
+// One wave's run: a segment's nonzeros [s0, s0 + len).  The segment offsets
+// come through __restrict__ read-only pointers, so the compiler fetches
+// them with scalar loads (lgkmcnt): reading them never waits on the runs in
+// flight (vmcnt).
+struct Run {
+  int64_t s0, len;
+};
+
+__device__ __forceinline__ Run seg_run(const int64_t* __restrict__ segStart, int64_t seg,
+                                       bool on) {
+  if (!on) return Run{0, 0};
+  const int64_t a = segStart[seg];
+  return Run{a, segStart[seg + 1] - a};
+}
+
+// the first kCap x 64 nonzeros of a run from `from` on, lane-strided; lanes
+// past the end read 0 (buffer range check)
+__device__ __forceinline__ void load_run(const uint32_t* __restrict__ vidx,
+                                         const double* __restrict__ vvals, const Run& r,
+                                         int64_t from, int lane, uint32_t (&ix)[kCap],
+                                         double (&vx)[kCap]) {
+  const int64_t len = r.len - from;
+  const auto ri = rsrc(vidx + r.s0 + from, len > 0 ? len * 4 : 0);
+  const auto rv = rsrc(vvals + r.s0 + from, len > 0 ? len * 8 : 0);
+  // lane part in the VGPR offset, batch part in the immediate offset
+#pragma unroll
+  for (int j = 0; j < kCap; ++j) {
+    ix[j] = __builtin_amdgcn_raw_buffer_load_b32(ri, lane * 4, j * 256, 2);
+    vx[j] = __builtin_bit_cast(double,
+                               __builtin_amdgcn_raw_buffer_load_b64(rv, lane * 8, j * 512, 2));
+  }
+}
+
+// Margin pass, persistent over (super row block sb, column chunk c) steps:
+// this workgroup's super blocks sb = blockIdx.x + i * gridDim.x (8 row blocks
+// each), each swept over the T chunks, as one flat sequence of steps g.  Per
+// step: the coefficient chunk goes registers -> LDS (the next step's chunk
+// is loaded meanwhile, an L2 hit), and wave i walks segment (8 sb + i, c);
+// the runs of the next TWO steps are in flight in registers, across super
+// block boundaries too.
 __global__ __launch_bounds__(kTPB) void k_tiles_margin(
-    TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ subRel,
-    const uint32_t* __restrict__ vidx, const double* __restrict__ vvals,
-    const double* __restrict__ labels, const double* __restrict__ weights,
-    const double* __restrict__ coef, int fitIntercept, int kind, double offset, double lscale,
-    double sigma, double eps, double* __restrict__ mult, double* __restrict__ slabS) {
-  // dots[kTileRows + lane]: a per-lane sink for masked lanes (no branches,
-  // no shared address among them)
-  __shared__ double dots[kTileRows + 64];
+    TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
+    const double* __restrict__ vvals, const double* __restrict__ labels,
+    const double* __restrict__ weights, const double* __restrict__ coef, int fitIntercept,
+    int kind, double offset, double lscale, double sigma, double eps, double* __restrict__ mult,
+    double* __restrict__ slabS) {
+  __shared__ double dots[kTileSuperRows];
   __shared__ double cf[kTileCols];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T = v.T;
-  const uint32_t sink = (uint32_t)(kTileRows + lane) << 16;
-  // steps per row block padded to a multiple of 3 (the unroll of the run
+  const int64_t nSB = (v.nRB + kTileWaves - 1) / kTileWaves;
+  // steps per super block padded to a multiple of 3 (the unroll of the run
   // buffers); the padding steps have empty runs and fetch nothing
   const int Tp = (T + 2) / 3 * 3;
-  const int64_t myRB = v.nRB > blockIdx.x ? (v.nRB - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  const int64_t G = myRB * Tp;
+  const int64_t mySB = nSB > blockIdx.x ? (nSB - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};     // loss, weight, multiplierSum, sigmaGradSum
   double creg[kCPT];
   uint32_t iA[kCap], iB[kCap], iC[kCap];
   double vA[kCap], vB[kCap], vC[kCap];
-  int64_t sA = 0, lA = 0, sB = 0, lB = 0, sC = 0, lC = 0;
+  Run rA, rB, rC;
 
-  auto rb_of = [&](int64_t g) { return (int64_t)blockIdx.x + (g / Tp) * gridDim.x; };
-  auto run_of = [&](int64_t g, int64_t& s0, int64_t& len) {
-    if (g >= G || g % Tp >= T) {   // past the end, or a padding step: an empty run
-      s0 = 0;
-      len = 0;
-      return;
-    }
-    const int64_t seg = rb_of(g) * T + g % Tp;
-    const int64_t base = segStart[seg];
-    const uint32_t* sr = subRel + seg * kTileSub;
-    const uint32_t a = sr[wave * kTileWaves];
-    const uint32_t b = wave == kTileWaves - 1 ? (uint32_t)(segStart[seg + 1] - base)
-                                              : sr[(wave + 1) * kTileWaves];
-    s0 = base + a;
-    len = (int64_t)b - (int64_t)a;
+  // a step is (k, c): this workgroup's k-th super block, chunk c < Tp; the
+  // positions one and two steps ahead by compare-and-wrap (no divisions)
+  auto ahead = [&](int64_t k, int c, int by, int64_t& k2, int& c2) {
+    c2 = c + by;
+    k2 = k;
+    if (c2 >= Tp) c2 -= Tp, k2 += 1;
   };
-  auto load_run = [&](int64_t s0, int64_t len, uint32_t (&ix)[kCap], double (&vx)[kCap]) {
-    const auto ri = rsrc(vidx + s0, len * 4);
-    const auto rv = rsrc(vvals + s0, len * 8);
-    // lane part in the VGPR offset, chunk part in the scalar offset: one
-    // offset register for all kCap loads
-#pragma unroll
-    for (int j = 0; j < kCap; ++j) {
-      ix[j] = __builtin_amdgcn_raw_buffer_load_b32(ri, lane * 4, j * 256, 2);
-      vx[j] = __builtin_bit_cast(double,
-                                 __builtin_amdgcn_raw_buffer_load_b64(rv, lane * 8, j * 512, 2));
-    }
+  auto run_of = [&](int64_t k, int c) {
+    const int64_t rb = ((int64_t)blockIdx.x + k * gridDim.x) * kTileWaves + wave;
+    return seg_run(segStart, rb * T + c, k < mySB && c < T && rb < v.nRB);
   };
-  auto load_coef = [&](int64_t g) {
-    const int t = (int)(g % Tp);
-    const int64_t c0 = t < T ? (int64_t)t * v.Wt : 0;
-    const int wl = (g < G && t < T) ? (int)std::min<int64_t>(v.Wt, v.F - c0) : 0;
+  auto load_coef = [&](int64_t k, int c) {
+    const bool on = k < mySB && c < T;
+    const int64_t c0 = on ? (int64_t)c * v.Wt : 0;
+    const int wl = on ? (int)std::min<int64_t>(v.Wt, v.F - c0) : 0;
     const auto rc = rsrc(coef + c0, (int64_t)wl * 8);
 #pragma unroll
     for (int i = 0; i < kCPT; ++i)
       creg[i] = __builtin_bit_cast(
           double, __builtin_amdgcn_raw_buffer_load_b64(rc, tid * 8, i * kTPB * 8, 0));
   };
-  // branch-free: all gathers issue together, masked lanes add 0 to their sink
+  double* myDots = dots + wave * kTileRows;
   auto consume = [&](int64_t len, const uint32_t (&ix)[kCap], const double (&vx)[kCap]) {
     double c[kCap];
 #pragma unroll
-    for (int j = 0; j < kCap; ++j) c[j] = cf[(j * 64 + lane < len ? ix[j] : sink) & 0xffff];
+    for (int j = 0; j < kCap; ++j) c[j] = cf[ix[j] & 0xffff];   // lanes past the end read cf[0]
 #pragma unroll
-    for (int j = 0; j < kCap; ++j) {
-      const bool on = j * 64 + lane < len;
-      lds_add(&dots[(on ? ix[j] : sink) >> 16], on ? vx[j] * c[j] : 0.0);
-    }
+    for (int j = 0; j < kCap; ++j)
+      if (j * 64 + lane < len) lds_add(&myDots[ix[j] >> 16], vx[j] * c[j]);
   };
-  // One step g: coefficient tile to LDS, the loads of step g + 1's tile and
-  // step g + 2's run issued (unconditionally: past the end they fetch
-  // nothing, so the waits for the current run stay counted), the current
-  // run into the row sums, the epilogue after a row block's last tile.  The
-  // three run buffers rotate by unrolling (never by copying a register that
-  // a load is still filling).
-  auto step = [&](int64_t g, int64_t sc, int64_t lc, uint32_t (&ic)[kCap], double (&vc)[kCap],
-                  int64_t& sn, int64_t& ln, uint32_t (&in)[kCap], double (&vn)[kCap]) {
+  // One step (k, c): coefficient chunk to LDS, the loads of the next step's
+  // chunk and of the run two steps ahead issued (unconditionally: past the
+  // end they fetch nothing, so the waits for the current run stay counted),
+  // the current run into the row sums.  The three run buffers rotate by
+  // unrolling (never by copying a register that a load is still filling).
+  auto step = [&](int64_t k, int c, const Run& rc, uint32_t (&ic)[kCap], double (&vc)[kCap],
+                  Run& rn, uint32_t (&in)[kCap], double (&vn)[kCap]) {
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kCPT; ++i) cf[tid + kTPB * i] = creg[i];
-    load_coef(g + 1);
-    run_of(g + 2, sn, ln);
-    load_run(sn, ln, in, vn);
+    int64_t k1, k2;
+    int c1, c2;
+    ahead(k, c, 1, k1, c1);
+    ahead(k, c, 2, k2, c2);
+    load_coef(k1, c1);
+    rn = run_of(k2, c2);
+    load_run(vidx, vvals, rn, 0, lane, in, vn);
     __syncthreads();
-    consume(lc, ic, vc);
-    for (int64_t b = kCap * 64; b < lc; b += kCap * 64) {   // rare: a long run
-      load_run(sc + b, lc - b, ic, vc);
-      consume(lc - b, ic, vc);
+    consume(rc.len, ic, vc);
+    for (int64_t b = kCap * 64; b < rc.len; b += kCap * 64) {   // rare: a long run
+      load_run(vidx, vvals, rc, b, lane, ic, vc);
+      consume(rc.len - b, ic, vc);
     }
   };
 
-  load_coef(0);
-  run_of(0, sA, lA);
-  load_run(sA, lA, iA, vA);
-  run_of(1, sB, lB);
-  load_run(sB, lB, iB, vB);
-  for (int64_t g0 = 0; g0 < G; g0 += Tp) {      // one row block per pass
+  load_coef(0, 0);
+  rA = run_of(0, 0);
+  load_run(vidx, vvals, rA, 0, lane, iA, vA);
+  {
+    int64_t k1;
+    int c1;
+    ahead(0, 0, 1, k1, c1);
+    rB = run_of(k1, c1);
+  }
+  load_run(vidx, vvals, rB, 0, lane, iB, vB);
+  for (int64_t k = 0; k < mySB; ++k) {          // one super block per pass
 #pragma unroll
-    for (int i = 0; i < kRPT; ++i) dots[tid + kTPB * i] = 0.0;
-    for (int64_t g = g0; g < g0 + Tp; g += 3) {
-      step(g, sA, lA, iA, vA, sC, lC, iC, vC);
-      step(g + 1, sB, lB, iB, vB, sA, lA, iA, vA);
-      step(g + 2, sC, lC, iC, vC, sB, lB, iB, vB);
+    for (int i = 0; i < kDPT; ++i) dots[tid + kTPB * i] = 0.0;
+    for (int c = 0; c < Tp; c += 3) {
+      step(k, c, rA, iA, vA, rC, iC, vC);
+      step(k, c + 1, rB, iB, vB, rA, iA, vA);
+      step(k, c + 2, rC, iC, vC, rB, iB, vB);
     }
     __syncthreads();
     // epilogue (BinaryLogisticBlockAggregator.scala:104-122 and siblings)
-    const int64_t rb = rb_of(g0);
-    for (int i = 0; i < kRPT; ++i) {
+    const int64_t r0 = ((int64_t)blockIdx.x + k * gridDim.x) * kTileSuperRows;
+    for (int i = 0; i < kDPT; ++i) {
       const int rl = tid + kTPB * i;
-      const int64_t r = rb * kTileRows + rl;
+      const int64_t r = r0 + rl;
       if (r < v.n) {
         const double label = labels[r];
         const double margin = cyc::row_margin(kind, fitIntercept, offset, lscale, label, dots[rl]);
@@ -304,130 +318,73 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
   }
 }
 
-// Gradient pass: workgroup (tile t, row range) over its row blocks.  Per row
-// block: the multiplier slice goes registers -> LDS (the next one loaded
-// while this one is used); wave j walks the 8 sub-segments (i, j) of the
-// segment as one virtual run -- lane position p lies in piece k when
-// cum[k] <= p < cum[k + 1] -- with the next row block's run in flight.
-struct GradRun {
-  int64_t base;                     // segment start (absolute)
-  uint32_t rel[kTileWaves];         // piece k's start, relative to base
-  uint32_t cum[kTileWaves + 1];     // prefix lengths
-};
-
+// Gradient pass: workgroup (super chunk st = 8 column chunks, row range)
+// over its row blocks.  Per row block: the multiplier slice goes registers
+// -> LDS (the next one loaded while this one is used); wave j walks segment
+// (rb, 8 st + j) into its chunk's column sums, with the runs of the next two
+// row blocks in flight.
 __global__ __launch_bounds__(kTPB) void k_tiles_grad(
-    TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ subRel,
-    const uint32_t* __restrict__ vidx, const double* __restrict__ vvals,
-    const double* __restrict__ mult, int ranges, double* __restrict__ slabG) {
-  __shared__ double gt[kTileCols + 64];     // + a per-lane sink for masked lanes
+    TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
+    const double* __restrict__ vvals, const double* __restrict__ mult, int ranges,
+    double* __restrict__ slabG) {
+  __shared__ double gt[kTileSuperCols];
   __shared__ double mv[kTileRows];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t sink = (uint32_t)(kTileCols + lane);
-  const int range = blockIdx.x % ranges, t = blockIdx.x / ranges;
+  const int range = blockIdx.x % ranges, st = blockIdx.x / ranges;
   const int64_t rbA = v.nRB * range / ranges, rbB = v.nRB * (range + 1) / ranges;
-  const int64_t c0 = (int64_t)t * v.Wt;
-  const int wl = (int)std::min<int64_t>(v.Wt, v.F - c0);
-  double mreg[kRPT];
+  const int c = st * kTileWaves + wave;                 // this wave's column chunk
+  double mreg[kMPT];
   uint32_t iA[kCap], iB[kCap], iC[kCap];
   double vA[kCap], vB[kCap], vC[kCap];
-  GradRun rA, rB, rC;
+  Run rA, rB, rC;
 
-  auto run_of = [&](int64_t rb, GradRun& r) {
-    if (rb >= rbB) {     // past the range: an empty run (its loads read element 0)
-      r.base = 0;
-#pragma unroll
-      for (int k = 0; k < kTileWaves; ++k) r.rel[k] = 0, r.cum[k] = 0;
-      r.cum[kTileWaves] = 0;
-      return;
-    }
-    const int64_t seg = rb * v.T + t;
-    r.base = segStart[seg];
-    const uint32_t segLen = (uint32_t)(segStart[seg + 1] - r.base);
-    const uint32_t* sr = subRel + seg * kTileSub;
-    uint32_t acc = 0;
-#pragma unroll
-    for (int k = 0; k < kTileWaves; ++k) {
-      const int e = k * kTileWaves + wave;
-      const uint32_t a = sr[e];
-      const uint32_t b = e + 1 < kTileSub ? sr[e + 1] : segLen;
-      r.rel[k] = a;
-      r.cum[k] = acc;
-      acc += b - a;
-    }
-    r.cum[kTileWaves] = acc;
-  };
-  // element of virtual position p (p < cum[8]): p + rel[k] - cum[k] for the
-  // piece k holding p, as p + rel[0] plus the (uniform, modulo 2^32) steps
-  // of the pieces it has passed -- a compare, a select and an add per piece
-  // (the steps are scalar work, once per run)
-  auto elem = [&](const GradRun& r, const uint32_t (&step)[kTileWaves], uint32_t p) {
-    uint32_t s = r.rel[0] + p;
-#pragma unroll
-    for (int kk = 1; kk < kTileWaves; ++kk) s += p >= r.cum[kk] ? step[kk] : 0u;
-    return r.base + s;
-  };
-  auto load_run = [&](const GradRun& r, uint32_t p0, uint32_t (&ix)[kCap], double (&vx)[kCap]) {
-    uint32_t step[kTileWaves];
-    step[0] = 0;
-#pragma unroll
-    for (int k = 1; k < kTileWaves; ++k)
-      step[k] = (r.rel[k] - r.cum[k]) - (r.rel[k - 1] - r.cum[k - 1]);
-#pragma unroll
-    for (int j = 0; j < kCap; ++j) {
-      const uint32_t p = p0 + j * 64 + lane;
-      const int64_t s = p < r.cum[kTileWaves] ? elem(r, step, p) : 0;   // masked lanes: element 0
-      ix[j] = __builtin_nontemporal_load(vidx + s);
-      vx[j] = __builtin_nontemporal_load(vvals + s);
-    }
-  };
+  auto run_of = [&](int64_t rb) { return seg_run(segStart, rb * v.T + c, rb < rbB && c < v.T); };
   auto load_mult = [&](int64_t rb) {
     const int64_t r0 = rb * kTileRows;
     const auto rm = rsrc(mult + (rb < rbB ? r0 : 0),
                          rb < rbB ? std::min<int64_t>(kTileRows, v.n - r0) * 8 : 0);
 #pragma unroll
-    for (int i = 0; i < kRPT; ++i)
+    for (int i = 0; i < kMPT; ++i)
       mreg[i] = __builtin_bit_cast(
           double, __builtin_amdgcn_raw_buffer_load_b64(rm, tid * 8, i * kTPB * 8, 0));
   };
-  auto consume = [&](int64_t rem, const uint32_t (&ix)[kCap], const double (&vx)[kCap]) {
+  double* myG = gt + wave * v.Wt;
+  auto consume = [&](int64_t len, const uint32_t (&ix)[kCap], const double (&vx)[kCap]) {
     double m[kCap];
 #pragma unroll
-    for (int j = 0; j < kCap; ++j) m[j] = mv[(j * 64 + lane < rem ? ix[j] : 0u) >> 16];
+    for (int j = 0; j < kCap; ++j) m[j] = mv[ix[j] >> 16];     // lanes past the end read mv[0]
 #pragma unroll
-    for (int j = 0; j < kCap; ++j) {
-      const bool on = j * 64 + lane < rem;
-      lds_add(&gt[on ? (ix[j] & 0xffff) : sink], on ? vx[j] * m[j] : 0.0);
-    }
+    for (int j = 0; j < kCap; ++j)
+      if (j * 64 + lane < len) lds_add(&myG[ix[j] & 0xffff], vx[j] * m[j]);
   };
 
 #pragma unroll
-  for (int i = 0; i < kCPT; ++i) gt[tid + kTPB * i] = 0.0;
+  for (int i = 0; i < kGPT; ++i) gt[tid + kTPB * i] = 0.0;
   // one row block: multiplier slice to LDS, the next slice and the run two
   // row blocks ahead issued (unconditionally), the current run into the
   // column sums; run buffers rotate by unrolling
-  auto step = [&](int64_t rb, const GradRun& rc, uint32_t (&ic)[kCap], double (&vc)[kCap],
-                  GradRun& rn, uint32_t (&in)[kCap], double (&vn)[kCap]) {
+  auto step = [&](int64_t rb, const Run& rc, uint32_t (&ic)[kCap], double (&vc)[kCap], Run& rn,
+                  uint32_t (&in)[kCap], double (&vn)[kCap]) {
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kRPT; ++i) mv[tid + kTPB * i] = mreg[i];
+    for (int i = 0; i < kMPT; ++i) mv[tid + kTPB * i] = mreg[i];
     load_mult(rb + 1);
-    run_of(rb + 2, rn);
-    load_run(rn, 0, in, vn);
+    rn = run_of(rb + 2);
+    load_run(vidx, vvals, rn, 0, lane, in, vn);
     __syncthreads();
-    const uint32_t len = rc.cum[kTileWaves];
-    consume(len, ic, vc);
-    for (uint32_t b = kCap * 64; b < len; b += kCap * 64) {   // rare: a long run
-      load_run(rc, b, ic, vc);
-      consume(len - b, ic, vc);
+    consume(rc.len, ic, vc);
+    for (int64_t b = kCap * 64; b < rc.len; b += kCap * 64) {   // rare: a long run
+      load_run(vidx, vvals, rc, b, lane, ic, vc);
+      consume(rc.len - b, ic, vc);
     }
   };
 
   load_mult(rbA);
-  run_of(rbA, rA);
-  load_run(rA, 0, iA, vA);
-  run_of(rbA + 1, rB);
-  load_run(rB, 0, iB, vB);
+  rA = run_of(rbA);
+  load_run(vidx, vvals, rA, 0, lane, iA, vA);
+  rB = run_of(rbA + 1);
+  load_run(vidx, vvals, rB, 0, lane, iB, vB);
   int64_t rb = rbA;
   for (; rb + 3 <= rbB; rb += 3) {
     step(rb, rA, iA, vA, rC, iC, vC);
@@ -437,9 +394,11 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
   if (rb < rbB) step(rb, rA, iA, vA, rC, iC, vC);
   if (rb + 1 < rbB) step(rb + 1, rB, iB, vB, rA, iA, vA);
   __syncthreads();
-  double* out = slabG + (int64_t)range * v.F + c0;
+  const int64_t col0 = (int64_t)st * kTileWaves * v.Wt;
+  double* out = slabG + (int64_t)range * v.F + col0;
+  const int64_t wl = std::min<int64_t>((int64_t)kTileWaves * v.Wt, v.F - col0);
 #pragma unroll
-  for (int i = 0; i < kCPT; ++i) {
+  for (int i = 0; i < kGPT; ++i) {
     const int e = tid + kTPB * i;
     if (e < wl) out[e] = gt[e];
   }
@@ -455,10 +414,8 @@ int tiles_view(cyc_tiles t, TilesView* v) {
   v->F = t->F;
   v->T = t->T;
   v->Wt = t->Wt;
-  v->WS = t->WS;
   v->nRB = (t->n + kTileRows - 1) / kTileRows;
   v->segStart = (const int64_t*)t->segStart.ptr;
-  v->subRel = (const uint32_t*)t->subRel.ptr;
   v->idx = (const uint32_t*)t->idx.ptr;
   v->vals = (const double*)t->vals.ptr;
   return CYC_OK;
@@ -468,29 +425,31 @@ int tiles_margin(const TilesView& v, const double* labels, const double* weights
                  const double* coef, int fitIntercept, int kind, double offset, double lscale,
                  double sigma, double eps, double* mult, double* slabS, int64_t* wgs,
                  hipStream_t st) {
-  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(v.nRB, device_cus()));
+  const int64_t nSB = (v.nRB + kTileWaves - 1) / kTileWaves;
+  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nSB, device_cus()));
   *wgs = grid;
   const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
   hipLaunchKernelGGL(k_tiles_margin, dim3((unsigned)grid), dim3(kTPB), 0, st, d, v.segStart,
-                     v.subRel, v.idx, v.vals, labels, weights, coef, fitIntercept, kind, offset,
-                     lscale, sigma, eps, mult, slabS);
+                     v.idx, v.vals, labels, weights, coef, fitIntercept, kind, offset, lscale,
+                     sigma, eps, mult, slabS);
   CYC_LAUNCH_CHECK("k_tiles_margin");
   return CYC_OK;
 }
 
 int tiles_ranges(const TilesView& v) {
   const int64_t cus = device_cus();
-  return (int)std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(v.nRB, 1),
-                                                     cus / std::max(v.T, 1)));
+  const int64_t sts = (v.T + kTileWaves - 1) / kTileWaves;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(v.nRB, 1), cus / sts));
 }
 
 int tiles_grad(const TilesView& v, const double* mult, double* slabG, int* ranges,
                hipStream_t st) {
   const int R = tiles_ranges(v);
   *ranges = R;
+  const int64_t sts = (v.T + kTileWaves - 1) / kTileWaves;
   const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
-  hipLaunchKernelGGL(k_tiles_grad, dim3((unsigned)((int64_t)v.T * R)), dim3(kTPB), 0, st, d,
-                     v.segStart, v.subRel, v.idx, v.vals, mult, R, slabG);
+  hipLaunchKernelGGL(k_tiles_grad, dim3((unsigned)(sts * R)), dim3(kTPB), 0, st, d, v.segStart,
+                     v.idx, v.vals, mult, R, slabG);
   CYC_LAUNCH_CHECK("k_tiles_grad");
   return CYC_OK;
 }
@@ -511,15 +470,13 @@ int cyc_tiles_create(int32_t numFeatures, int64_t capacity_rows, int64_t capacit
   }
   auto* t = new cyc_tiles_s();
   t->F = numFeatures;
-  t->Wt = std::min(numFeatures, kTileCols);
-  t->T = (numFeatures + t->Wt - 1) / t->Wt;
-  t->WS = (t->Wt + kTileWaves - 1) / kTileWaves;
+  t->Wt = chunk_cols(numFeatures);
+  t->T = (int)(((int64_t)numFeatures + t->Wt - 1) / t->Wt);
   t->capRows = capacity_rows;
   t->capNnz = capacity_nnz;
   const int64_t segs = (capacity_rows + kTileRows - 1) / kTileRows * t->T;
   int rc;
   if ((rc = t->segStart.reserve(sizeof(int64_t) * (size_t)(segs + 1))) ||
-      (rc = t->subRel.reserve(sizeof(uint32_t) * (size_t)std::max<int64_t>(segs * kTileSub, 1))) ||
       (rc = t->idx.reserve(sizeof(uint32_t) * (size_t)std::max<int64_t>(capacity_nnz, 1))) ||
       (rc = t->vals.reserve(sizeof(double) * (size_t)std::max<int64_t>(capacity_nnz, 1)))) {
     delete t;
@@ -541,7 +498,7 @@ int32_t cyc_tiles_features(cyc_tiles t) { return t ? t->F : -1; }
 int32_t cyc_tiles_row_block(void) { return kTileRows; }
 
 int64_t cyc_tiles_bytes(cyc_tiles t) {
-  return t ? (int64_t)(t->segStart.bytes + t->subRel.bytes + t->idx.bytes + t->vals.bytes) : 0;
+  return t ? (int64_t)(t->segStart.bytes + t->idx.bytes + t->vals.bytes) : 0;
 }
 
 int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* colidx,
@@ -569,10 +526,12 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
               "colidx and values must not be null");
   if (int rc = cyc::check_csr_indices(rowptr, colidx, rows, t->F, st)) return rc;
   const int T = t->T;
-  // sub-chunks of at most 128 row blocks: bounded scratch, 32-bit sort keys
-  const int64_t chRows = (int64_t)128 * kTileRows;
+  // sub-chunks of whole row blocks, at most 2^24 segment keys (bounded
+  // scratch, 32-bit sort keys)
+  const int64_t nrbSub = std::max<int64_t>(1, std::min<int64_t>(512, ((int64_t)1 << 24) / T));
+  const int64_t chRows = nrbSub * kTileRows;
   const int64_t rb0 = t->n / kTileRows;
-  cyc::DeviceBuffer keys, packed, keysOut, perm, starts, tmp;
+  cyc::DeviceBuffer keys, packed, keysOut, perm, tmp;
   for (int64_t a = 0; a < rows; a += chRows) {
     const int64_t b = std::min(rows, a + chRows);
     int64_t qa = 0, qb = 0;
@@ -581,11 +540,11 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
     CYC_HIP(hipStreamSynchronize(st));
     const int64_t cnt = qb - qa;
     const int64_t nrb = (b - a + kTileRows - 1) / kTileRows;
-    const int64_t nkeys = nrb * T * kTileSub;
+    const int64_t nkeys = nrb * T;
     const int64_t seg0 = (rb0 + a / kTileRows) * T;
-    CYC_REQUIRE(cnt < ((int64_t)1 << 32), "a chunk of 128 row blocks holds 2^32 nonzeros or more");
+    CYC_REQUIRE(cnt < ((int64_t)1 << 32), "a chunk of " + std::to_string(nrbSub) +
+                                              " row blocks holds 2^32 nonzeros or more");
     int rc;
-    if ((rc = starts.reserve(sizeof(int64_t) * (size_t)(nkeys + 1)))) return rc;
     if (cnt > 0) {
       if ((rc = keys.reserve(sizeof(uint32_t) * (size_t)cnt)) ||
           (rc = packed.reserve(sizeof(uint32_t) * (size_t)cnt)) ||
@@ -593,7 +552,7 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
           (rc = perm.reserve(sizeof(uint32_t) * (size_t)cnt)))
         return rc;
       hipLaunchKernelGGL(k_tile_keys, dim3(8192), dim3(256), 0, st, rowptr + a, colidx + (qa - q0),
-                         b - a, qa, T, t->Wt, t->WS, (uint32_t*)keys.ptr, (uint32_t*)packed.ptr);
+                         b - a, qa, T, t->Wt, (uint32_t*)keys.ptr, (uint32_t*)packed.ptr);
       CYC_LAUNCH_CHECK("k_tile_keys");
       unsigned endBit = 1;
       while (endBit < 32 && ((int64_t)1 << endBit) < nkeys) ++endBit;
@@ -612,14 +571,9 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
       CYC_LAUNCH_CHECK("k_tile_gather");
     }
     hipLaunchKernelGGL(k_tile_starts, dim3((unsigned)std::min<int64_t>((cnt + 256) / 256, 8192)),
-                       dim3(256), 0, st, (const uint32_t*)keysOut.ptr, cnt, nkeys,
-                       (int64_t*)starts.ptr);
+                       dim3(256), 0, st, (const uint32_t*)keysOut.ptr, cnt, nkeys, seg0, t->nnz,
+                       (int64_t*)t->segStart.ptr);
     CYC_LAUNCH_CHECK("k_tile_starts");
-    hipLaunchKernelGGL(k_tile_offsets,
-                       dim3((unsigned)std::min<int64_t>((nkeys + 255) / 256, 8192)), dim3(256), 0,
-                       st, (const int64_t*)starts.ptr, nkeys, seg0, t->nnz,
-                       (int64_t*)t->segStart.ptr, (uint32_t*)t->subRel.ptr);
-    CYC_LAUNCH_CHECK("k_tile_offsets");
     t->nnz += cnt;
     // scratch is reused by the next sub-chunk on this stream; freed on return
   }

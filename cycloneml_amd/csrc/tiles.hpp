@@ -10,26 +10,23 @@
 
 namespace cyc {
 
-constexpr int kTileRows = 8192;               // rows per row block (R)
-constexpr int kTileCols = 8192;               // columns per column tile (W, at most)
-constexpr int kTileWaves = 8;                 // waves per workgroup = sub-ranges per side
-constexpr int kTileSub = kTileWaves * kTileWaves;     // sub-segments per segment
-constexpr int kTileRowRange = kTileRows / kTileWaves; // rows per wave range (1024)
+constexpr int kTileRows = 2048;               // rows per row block (R)
+constexpr int kTileCols = 2048;               // columns per column chunk (W, at most)
+constexpr int kTileWaves = 8;                 // waves per workgroup
+constexpr int kTileSuperRows = kTileWaves * kTileRows;   // rows of one margin workgroup step
+constexpr int kTileSuperCols = kTileWaves * kTileCols;   // columns of one gradient workgroup
 
-// What the kernels need to walk a built layout.  Segment s = rb * T + t
-// (row block rb, column tile t) spans nonzeros [segStart[s], segStart[s+1]);
-// its sub-segment k = 8 i + j (row range i, column range j) starts at
-// segStart[s] + subRel[64 s + k].  idx packs (row in block << 16 | column in
-// tile), vals the fp64 values.
+// What the kernels need to walk a built layout.  Segment s = rb * T + c
+// (row block rb, column chunk c) spans nonzeros [segStart[s], segStart[s+1])
+// in CSR order; idx packs (row in block << 16 | column in chunk), vals the
+// fp64 values.
 struct TilesView {
   int64_t n = 0;         // rows
   int F = 0;             // numFeatures
-  int T = 1;             // column tiles
-  int Wt = 1;            // columns per tile (the last tile may be shorter)
-  int WS = 1;            // columns per wave range: ceil(Wt / 8)
+  int T = 1;             // column chunks
+  int Wt = 1;            // columns per chunk (the last chunk may be shorter)
   int64_t nRB = 0;       // row blocks
   const int64_t* segStart = nullptr;
-  const uint32_t* subRel = nullptr;
   const uint32_t* idx = nullptr;
   const double* vals = nullptr;
 };

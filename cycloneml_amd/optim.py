@@ -35,7 +35,7 @@ class SparseTiles:
     blocks of ROW_BLOCK rows, except the last append); the CSR can be freed
     afterwards."""
 
-    ROW_BLOCK = 8192
+    ROW_BLOCK = 2048          # cyc_tiles_row_block()
 
     def __init__(self, numFeatures: int, capacity_rows: int, capacity_nnz: int):
         self._lib = N.load()

@@ -41,3 +41,10 @@ def test_no_device_no_fallback():
     lib = N.load()
     rc = lib.cyc_kmeans_plan_create(8, 2, 1, ctypes.byref(ctypes.c_void_p()))
     assert rc == N.CYC_ERR_NO_DEVICE
+
+
+def test_tiles_row_block_matches_python():
+    """SparseTiles.ROW_BLOCK (the append granularity callers use) is the
+    library's row block (a constant getter: no device call)."""
+    from cycloneml_amd.optim import SparseTiles
+    assert N.load().cyc_tiles_row_block() == SparseTiles.ROW_BLOCK == 2048

@@ -283,12 +283,16 @@ def test_sparse_config5_full_size(cuda):
 
 @pytest.mark.parametrize("fi,fwm", [(True, False), (True, True), (False, False)])
 @pytest.mark.parametrize("n,F,nnz", [(700, 600_000, 40), (300, 1_100_000, 150), (50, 300_000, 1),
-                                     (20_000, 30_000, 25), (9000, 8192, 300)])
+                                     (20_000, 30_000, 25), (9000, 8192, 300),
+                                     (40_000, 1_000_000, 64), (5000, 100, 10), (3000, 3, 2)])
 def test_binary_tiles_vs_oracle(cuda, fi, fwm, n, F, nnz):
-    """The row-block x column-tile layout: several column tiles (F up to
-    1.1M = 135 tiles), several row blocks (20000 rows = 3), empty rows, zero
-    weights, rows spanning every tile, and long sub-segment runs (9000 rows of
-    ~300 nonzeros in one tile: the batched tail path); equals the restatement
+    """The row-block x column-chunk layout: many column chunks (F up to 1.1M
+    = 538 chunks of 2048, 68 gradient workgroups of 8 chunks), several row
+    blocks and super blocks (40000 rows = 20 row blocks of 2048 = 3 margin
+    super blocks of 8), empty rows, zero weights, rows spanning every chunk,
+    long runs (9000 rows of ~300 nonzeros over 8 chunks: the batched tail
+    path), and narrow F (100 and 3 columns: chunks of 64, most waves without
+    a chunk); equals the restatement
     within 1e-10, the loss bit for bit-ish (same summation order), and is
     bitwise reproducible run to run."""
     from cycloneml_amd.optim import BinaryLogisticBlockAggregator, DeviceInstanceBlock
