@@ -373,23 +373,32 @@ __global__ void k_binlog_fold(const double* __restrict__ slabG, int64_t waves,
 // One 1024-thread workgroup: thread t sums its contiguous stretch of the
 // products in index order, then a fixed tree -- deterministic (the
 // reference's sequential ddot order is not pinned below 1e-10 anyway).
-__global__ __launch_bounds__(1024) void k_binlog_offset(const double* __restrict__ coef,
-                                                        const double* __restrict__ sm, int F,
-                                                        int useBase, double base,
-                                                        double* __restrict__ out) {
-  __shared__ double sh[1024];
+constexpr int kOffParts = 256;                 // partial sums of the offset dot
+
+// stage 1: part p sums the products of its contiguous range, lane-strided
+// (coalesced), each thread in index order, then a fixed shuffle / wave tree
+__global__ __launch_bounds__(256) void k_binlog_offset_part(const double* __restrict__ coef,
+                                                            const double* __restrict__ sm, int F,
+                                                            double* __restrict__ part) {
+  __shared__ double sh[4];
   const int t = threadIdx.x;
-  const int per = (F + 1023) / 1024;
-  const int f0 = t * per, f1 = min(F, f0 + per);
+  const int64_t per = ((int64_t)F + kOffParts - 1) / kOffParts;
+  const int64_t f0 = blockIdx.x * per, f1 = std::min<int64_t>(F, f0 + per);
   double dd = 0.0;
-  for (int f = f0; f < f1; ++f) dd += coef[f] * sm[f];
-  sh[t] = dd;
+  for (int64_t f = f0 + t; f < f1; f += 256) dd += coef[f] * sm[f];
+  for (int m = 32; m >= 1; m >>= 1) dd += __shfl_xor(dd, m);
+  if ((t & 63) == 0) sh[t >> 6] = dd;
   __syncthreads();
-  for (int h = 512; h > 0; h >>= 1) {
-    if (t < h) sh[t] += sh[t + h];
-    __syncthreads();
-  }
-  if (t == 0) out[0] = (useBase ? base : coef[F]) - sh[0];
+  if (t == 0) part[blockIdx.x] = ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
+// stage 2: the parts in order; out = (base or intercept) - dot
+__global__ void k_binlog_offset(const double* __restrict__ part, const double* __restrict__ coef,
+                                int F, int useBase, double base, double* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < kOffParts; ++i) s += part[i];
+  out[0] = (useBase ? base : coef[F]) - s;
 }
 
 // LeastSquaresBlockAggregator.effectiveCoef (:48-55): coefficient or 0.0
@@ -1036,7 +1045,14 @@ int binary_offset(cyc_logistic_plan p, const double* coef, const double* scaledM
   *offset = 0.0;
   if (!p->fitIntercept) return CYC_OK;
   if (p->fitWithMean || p->loss == 2) {
-    hipLaunchKernelGGL(k_binlog_offset, dim3(1), dim3(1024), 0, st, coef, scaledMean, p->F,
+    // marginOffset = intercept - dot(coef, scaledMean) (:62-70); least
+    // squares: labelMean / labelStd - dot (LeastSquaresBlockAggregator :59-66)
+    if (int rc = p->offset.reserve(sizeof(double) * (2 + kOffParts))) return rc;
+    double* part = (double*)p->offset.ptr + 2;
+    hipLaunchKernelGGL(k_binlog_offset_part, dim3(kOffParts), dim3(256), 0, st, coef, scaledMean,
+                       p->F, part);
+    CYC_LAUNCH_CHECK("k_binlog_offset_part");
+    hipLaunchKernelGGL(k_binlog_offset, dim3(1), dim3(64), 0, st, (const double*)part, coef, p->F,
                        p->loss == 2 ? 1 : 0, p->labelMean / p->labelStd, (double*)p->offset.ptr);
     CYC_LAUNCH_CHECK("k_binlog_offset");
     CYC_HIP(hipMemcpyAsync(offset, p->offset.ptr, sizeof(double), hipMemcpyDeviceToHost, st));

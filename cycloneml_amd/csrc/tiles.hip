@@ -194,8 +194,11 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
     const double* __restrict__ weights, const double* __restrict__ coef, int fitIntercept,
     int kind, double offset, double lscale, double sigma, double eps, double* __restrict__ mult,
     double* __restrict__ slabS) {
-  __shared__ double dots[kTileSuperRows];
-  __shared__ double cf[kTileCols];
+  // 160 KiB: the super block's dots and two coefficient chunk buffers (the
+  // chunk of step s in cf[s & 1]); the final reduction reuses cf
+  __shared__ double lds[kTileSuperRows + 2 * kTileCols];
+  double* const dots = lds;
+  double* const cf = lds + kTileSuperRows;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T = v.T;
@@ -232,40 +235,53 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
           double, __builtin_amdgcn_raw_buffer_load_b64(rc, tid * 8, i * kTPB * 8, 0));
   };
   double* myDots = dots + wave * kTileRows;
-  auto consume = [&](int64_t len, const uint32_t (&ix)[kCap], const double (&vx)[kCap]) {
+  auto consume = [&](int64_t len, const double* cfp, const uint32_t (&ix)[kCap],
+                     const double (&vx)[kCap]) {
     double c[kCap];
 #pragma unroll
-    for (int j = 0; j < kCap; ++j) c[j] = cf[ix[j] & 0xffff];   // lanes past the end read cf[0]
+    for (int j = 0; j < kCap; ++j) c[j] = cfp[ix[j] & 0xffff];  // lanes past the end read [0]
 #pragma unroll
     for (int j = 0; j < kCap; ++j)
       if (j * 64 + lane < len) lds_add(&myDots[ix[j] >> 16], vx[j] * c[j]);
   };
-  // One step (k, c): coefficient chunk to LDS, the loads of the next step's
-  // chunk and of the run two steps ahead issued (unconditionally: past the
-  // end they fetch nothing, so the waits for the current run stay counted),
-  // the current run into the row sums.  The three run buffers rotate by
-  // unrolling (never by copying a register that a load is still filling).
+  // One step (k, c), ONE barrier: the current run into the row sums with
+  // chunk s in cf[s & 1], the next chunk (in registers since the last step)
+  // into the other buffer -- every wave left it behind the last barrier --,
+  // then the loads of the chunk one step and of the run two steps ahead of
+  // it issued (unconditionally: past the end they fetch nothing, so the
+  // waits for the current run stay counted).  The three run buffers rotate
+  // by unrolling (never by copying a register that a load is still filling).
   auto step = [&](int64_t k, int c, const Run& rc, uint32_t (&ic)[kCap], double (&vc)[kCap],
                   Run& rn, uint32_t (&in)[kCap], double (&vn)[kCap]) {
-    __syncthreads();
+    const int par = (int)((k * Tp + c) & 1);
+    const double* cur = cf + par * kTileCols;
+    consume(rc.len, cur, ic, vc);
+    for (int64_t b = kCap * 64; b < rc.len; b += kCap * 64) {   // rare: a long run
+      load_run(vidx, vvals, rc, b, lane, ic, vc);
+      consume(rc.len - b, cur, ic, vc);
+    }
+    double* nxt = cf + (par ^ 1) * kTileCols;
 #pragma unroll
-    for (int i = 0; i < kCPT; ++i) cf[tid + kTPB * i] = creg[i];
-    int64_t k1, k2;
-    int c1, c2;
-    ahead(k, c, 1, k1, c1);
+    for (int i = 0; i < kCPT; ++i) nxt[tid + kTPB * i] = creg[i];
+    int64_t k2;
+    int c2;
     ahead(k, c, 2, k2, c2);
-    load_coef(k1, c1);
+    load_coef(k2, c2);
     rn = run_of(k2, c2);
     load_run(vidx, vvals, rn, 0, lane, in, vn);
     __syncthreads();
-    consume(rc.len, ic, vc);
-    for (int64_t b = kCap * 64; b < rc.len; b += kCap * 64) {   // rare: a long run
-      load_run(vidx, vvals, rc, b, lane, ic, vc);
-      consume(rc.len - b, ic, vc);
-    }
   };
 
+  // prologue: chunk 0 into cf[0], chunk 1 in registers, runs 0 and 1 in flight
   load_coef(0, 0);
+#pragma unroll
+  for (int i = 0; i < kCPT; ++i) cf[tid + kTPB * i] = creg[i];
+  {
+    int64_t k1;
+    int c1;
+    ahead(0, 0, 1, k1, c1);
+    load_coef(k1, c1);
+  }
   rA = run_of(0, 0);
   load_run(vidx, vvals, rA, 0, lane, iA, vA);
   {
@@ -278,12 +294,12 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
   for (int64_t k = 0; k < mySB; ++k) {          // one super block per pass
 #pragma unroll
     for (int i = 0; i < kDPT; ++i) dots[tid + kTPB * i] = 0.0;
+    __syncthreads();                            // zeroed dots, chunk 0 in cf[0]
     for (int c = 0; c < Tp; c += 3) {
       step(k, c, rA, iA, vA, rC, iC, vC);
       step(k, c + 1, rB, iB, vB, rA, iA, vA);
       step(k, c + 2, rC, iC, vC, rB, iB, vB);
     }
-    __syncthreads();
     // epilogue (BinaryLogisticBlockAggregator.scala:104-122 and siblings)
     const int64_t r0 = ((int64_t)blockIdx.x + k * gridDim.x) * kTileSuperRows;
     for (int i = 0; i < kDPT; ++i) {
@@ -298,9 +314,10 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
         mult[r] = m;
       }
     }
+    __syncthreads();                            // dots read before the next zeroing
   }
   // workgroup partials: fixed shuffle tree per wave, then waves in order
-  __shared__ double red[kTileWaves][4];
+  double (*red)[4] = reinterpret_cast<double (*)[4]>(cf);
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
@@ -327,8 +344,11 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
     TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
     const double* __restrict__ vvals, const double* __restrict__ mult, int ranges,
     double* __restrict__ slabG) {
-  __shared__ double gt[kTileSuperCols];
-  __shared__ double mv[kTileRows];
+  // 160 KiB: the 8 chunks' column sums and two multiplier slice buffers
+  // (row block rb's slice in mv[(rb - rbA) & 1])
+  __shared__ double lds[kTileSuperCols + 2 * kTileRows];
+  double* const gt = lds;
+  double* const mv = lds + kTileSuperCols;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int range = blockIdx.x % ranges, st = blockIdx.x / ranges;
@@ -350,10 +370,11 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
           double, __builtin_amdgcn_raw_buffer_load_b64(rm, tid * 8, i * kTPB * 8, 0));
   };
   double* myG = gt + wave * v.Wt;
-  auto consume = [&](int64_t len, const uint32_t (&ix)[kCap], const double (&vx)[kCap]) {
+  auto consume = [&](int64_t len, const double* mvp, const uint32_t (&ix)[kCap],
+                     const double (&vx)[kCap]) {
     double m[kCap];
 #pragma unroll
-    for (int j = 0; j < kCap; ++j) m[j] = mv[ix[j] >> 16];     // lanes past the end read mv[0]
+    for (int j = 0; j < kCap; ++j) m[j] = mvp[ix[j] >> 16];    // lanes past the end read [0]
 #pragma unroll
     for (int j = 0; j < kCap; ++j)
       if (j * 64 + lane < len) lds_add(&myG[ix[j] & 0xffff], vx[j] * m[j]);
@@ -361,30 +382,40 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
 
 #pragma unroll
   for (int i = 0; i < kGPT; ++i) gt[tid + kTPB * i] = 0.0;
-  // one row block: multiplier slice to LDS, the next slice and the run two
-  // row blocks ahead issued (unconditionally), the current run into the
-  // column sums; run buffers rotate by unrolling
+  // one row block, ONE barrier: the current run into the column sums with
+  // the slice in mv[par], the next slice (in registers since the last step)
+  // into the other buffer -- every wave left it behind the last barrier --,
+  // then the slice two row blocks ahead and the run two row blocks ahead
+  // issued (unconditionally); run buffers rotate by unrolling
   auto step = [&](int64_t rb, const Run& rc, uint32_t (&ic)[kCap], double (&vc)[kCap], Run& rn,
                   uint32_t (&in)[kCap], double (&vn)[kCap]) {
-    __syncthreads();
+    const int par = (int)((rb - rbA) & 1);
+    const double* cur = mv + par * kTileRows;
+    consume(rc.len, cur, ic, vc);
+    for (int64_t b = kCap * 64; b < rc.len; b += kCap * 64) {   // rare: a long run
+      load_run(vidx, vvals, rc, b, lane, ic, vc);
+      consume(rc.len - b, cur, ic, vc);
+    }
+    double* nxt = mv + (par ^ 1) * kTileRows;
 #pragma unroll
-    for (int i = 0; i < kMPT; ++i) mv[tid + kTPB * i] = mreg[i];
-    load_mult(rb + 1);
+    for (int i = 0; i < kMPT; ++i) nxt[tid + kTPB * i] = mreg[i];
+    load_mult(rb + 2);
     rn = run_of(rb + 2);
     load_run(vidx, vvals, rn, 0, lane, in, vn);
     __syncthreads();
-    consume(rc.len, ic, vc);
-    for (int64_t b = kCap * 64; b < rc.len; b += kCap * 64) {   // rare: a long run
-      load_run(vidx, vvals, rc, b, lane, ic, vc);
-      consume(rc.len - b, ic, vc);
-    }
   };
 
+  // prologue: slice rbA into mv[0], slice rbA + 1 in registers, runs rbA
+  // and rbA + 1 in flight
   load_mult(rbA);
+#pragma unroll
+  for (int i = 0; i < kMPT; ++i) mv[tid + kTPB * i] = mreg[i];
+  load_mult(rbA + 1);
   rA = run_of(rbA);
   load_run(vidx, vvals, rA, 0, lane, iA, vA);
   rB = run_of(rbA + 1);
   load_run(vidx, vvals, rB, 0, lane, iB, vB);
+  __syncthreads();                              // zeroed sums, slice rbA in mv[0]
   int64_t rb = rbA;
   for (; rb + 3 <= rbB; rb += 3) {
     step(rb, rA, iA, vA, rC, iC, vC);

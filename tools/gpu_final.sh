@@ -1,5 +1,8 @@
-# Round-end validation: every GPU test + smoke (PART=tests), the four bench
-# lines with CPU baselines (PART=bench), or both (default).
+# Round-end validation: every GPU test + smoke (PART=tests), the bench line
+# of all four workloads with CPU baselines (PART=bench), or both (default).
+# The maintained tools: prof.sh (rocprofv3 stats + FETCH/WRITE passes),
+# pmc_summary.py, pmc_kernel.sh / pmc_mfma.sh / pmc_pass.sh (SQ counters),
+# asm_mix.py (ISA mix), probe/ (MFMA layout probes).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -11,9 +14,15 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 tail -1 gpurun_out/smoke.log
 fi
 if [ $PART != tests ]; then
-for w in ${WL:-kmeans gramian lr_multi lr_sparse}; do
-  timeout -k 10 400 python -u bench.py --workload $w > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err || { echo BENCH $w FAIL; tail -20 gpurun_out/bench_$w.err; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/bench_$w.json'));print('$w', round(d['value']/1e6,1), 'M rows/s', round(d['ms_per_step'],2), 'ms', d['roofline']['kernel'], round(d['roofline']['frac'],3), (d['cpu_baseline'] or {}).get('value'))"
-done
+# the driver's command: every workload in one run, KMeans as the headline line
+timeout -k 10 500 python -u bench.py --steps ${STEPS:-20} --warmup ${WARMUP:-5} > gpurun_out/bench_all.json 2> gpurun_out/bench_all.err || { echo BENCH FAIL; tail -20 gpurun_out/bench_all.err; exit 1; }
+python - <<'PY'
+import json
+d = json.loads(open("gpurun_out/bench_all.json").read().strip().splitlines()[-1])
+for name, w in [("kmeans", d)] + list(d.get("workloads", {}).items()):
+    print(name, round(w["value"] / 1e6, 1), "M rows/s", round(w["ms_per_step"], 2), "ms",
+          w["roofline"]["kernel"], round(w["roofline"]["frac"], 3),
+          (w["cpu_baseline"] or {}).get("value"))
+PY
 fi
 echo ALLDONE
