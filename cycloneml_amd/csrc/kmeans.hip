@@ -36,6 +36,7 @@
 #include "common.hpp"
 #include "kmeans_i8.hpp"
 #include "kmeans_cos.hpp"
+#include "kmeans_sparse.hpp"
 
 namespace {
 
@@ -1708,32 +1709,6 @@ __global__ __launch_bounds__(256) void k_assign_sparse(
   }
 }
 
-// updateClusterSum for sparse points (DistanceMeasure.scala:189-191, i.e.
-// mllib BLAS.axpy(w, sparse x, sum), BLAS.scala:93-112), clusterWeightSum and
-// costAccum (KMeans.scala:301-304).  One wave per row with fp64 atomics: the
-// sums agree with any partition order of the reference to rounding (they are
-// not bitwise reproducible run to run, unlike the dense path).
-__global__ __launch_bounds__(256) void k_sparse_sums(
-    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
-    const double* __restrict__ vals, const double* __restrict__ w, int64_t n, int d,
-    const int32_t* __restrict__ assign, const double* __restrict__ cost,
-    double* __restrict__ sums, double* __restrict__ wsum, double* __restrict__ costSum) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t r = wid; r < n; r += nw) {
-    const int c = assign[r];
-    const double wr = w ? w[r] : 1.0;
-    double* y = sums + (int64_t)c * d;
-    for (int64_t q = rowptr[r] + lane; q < rowptr[r + 1]; q += 64)
-      unsafeAtomicAdd(&y[colidx[q]], wr == 1.0 ? vals[q] : dmul(wr, vals[q]));
-    if (lane == 0) {
-      unsafeAtomicAdd(&wsum[c], wr);
-      unsafeAtomicAdd(costSum, dmul(cost[r], wr));
-    }
-  }
-}
-
 }  // namespace
 
 // ------------------------------------------------------------------ plan
@@ -2695,8 +2670,8 @@ int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
     if ((rc = cos_enqueue(p, cnorm, true, xnorm, n, st)) || (rc = cos_stats(p, C, cnorm, st)) ||
         (rc = cyc::kmcos::assign_sparse(rowptr, colidx, vals, xnorm, n, p->d, C, cnorm, p->k,
                                         (const double*)p->stats.ptr, assign, cost, st)) ||
-        (rc = cyc::kmcos::sparse_sums(rowptr, colidx, vals, weights, xnorm, n, p->d, assign,
-                                      cost, sums, wsum, cost_sum, st)))
+        (rc = cyc::kmsparse::cluster_sums(rowptr, colidx, vals, weights, xnorm, n, p->d, p->k,
+                                          assign, cost, sums, wsum, cost_sum, st)))
       return rc;
     return cos_check(p);
   }
@@ -2704,10 +2679,9 @@ int cyc_kmeans_accumulate_csr_dev(cyc_kmeans_plan p, const int64_t* rowptr,
   if ((rc = do_stats(p, C, st))) return rc;
   if ((rc = sparse_assign(p, rowptr, colidx, vals, xnorm, n, C, cnorm, assign, cost, st)))
     return rc;
-  const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 8192);
-  hipLaunchKernelGGL(k_sparse_sums, dim3(grid), dim3(256), 0, st, rowptr, colidx, vals, weights, n,
-                     p->d, (const int32_t*)assign, (const double*)cost, sums, wsum, cost_sum);
-  CYC_LAUNCH_CHECK("k_sparse_sums");
+  if ((rc = cyc::kmsparse::cluster_sums(rowptr, colidx, vals, weights, nullptr, n, p->d, p->k,
+                                        assign, cost, sums, wsum, cost_sum, st)))
+    return rc;
   return require_check(p, n);
 }
 

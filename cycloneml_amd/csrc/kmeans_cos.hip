@@ -325,32 +325,6 @@ __global__ __launch_bounds__(256) void k_cos_assign_sparse(
   }
 }
 
-// updateClusterSum for sparse points: axpy(w / |x|, x, sum) with the sparse
-// axpy (mllib/linalg/BLAS.scala:93-112), clusterWeightSum and costAccum; one
-// wave per row with fp64 atomics, as the Euclidean sparse path.
-__global__ __launch_bounds__(256) void k_cos_sparse_sums(
-    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
-    const double* __restrict__ vals, const double* __restrict__ w,
-    const double* __restrict__ xnorm, int64_t n, int d, const int32_t* __restrict__ assign,
-    const double* __restrict__ cost, double* __restrict__ sums, double* __restrict__ wsum,
-    double* __restrict__ costSum) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t r = wid; r < n; r += nw) {
-    const int c = assign[r];
-    const double wr = w ? w[r] : 1.0;
-    const double a = wr / xnorm[r];
-    double* y = sums + (int64_t)c * d;
-    for (int64_t q = rowptr[r] + lane; q < rowptr[r + 1]; q += 64)
-      unsafeAtomicAdd(&y[colidx[q]], a == 1.0 ? vals[q] : dmul(a, vals[q]));
-    if (lane == 0) {
-      unsafeAtomicAdd(&wsum[c], wr);
-      unsafeAtomicAdd(costSum, dmul(cost[r], wr));
-    }
-  }
-}
-
 // 64-row tiles staged through LDS 8 columns at a time, one lane per row.
 __global__ void k_cos_row_cost(const double* __restrict__ X, int64_t n, int d,
                                const double* __restrict__ C, const double* __restrict__ cnorm,
@@ -535,18 +509,6 @@ int assign_sparse(const int64_t* rowptr, const int32_t* colidx, const double* va
   hipLaunchKernelGGL(k_cos_assign_sparse, dim3(grid), dim3(256), 0, st, rowptr, colidx, vals,
                      xnorm, n, d, C, cnorm, k, stats, assign, cost);
   CYC_LAUNCH_CHECK("k_cos_assign_sparse");
-  return CYC_OK;
-}
-
-int sparse_sums(const int64_t* rowptr, const int32_t* colidx, const double* vals,
-                const double* w, const double* xnorm, int64_t n, int d, const int32_t* assign,
-                const double* cost, double* sums, double* wsum, double* costSum,
-                hipStream_t st) {
-  if (n <= 0) return CYC_OK;
-  const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 8192);
-  hipLaunchKernelGGL(k_cos_sparse_sums, dim3(grid), dim3(256), 0, st, rowptr, colidx, vals, w,
-                     xnorm, n, d, assign, cost, sums, wsum, costSum);
-  CYC_LAUNCH_CHECK("k_cos_sparse_sums");
   return CYC_OK;
 }
 

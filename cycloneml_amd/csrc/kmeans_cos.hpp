@@ -40,15 +40,10 @@ int assign_exact(const double* X, const double* xnorm, int d, const double* C, c
                  hipStream_t st);
 
 // Sparse (CSR) points: the reference loop for every row (dot(sparse, dense)),
-// cost written when non-null; and the sparse updateClusterSum with fp64
-// atomics (sums / wsum / costSum accumulate).
+// cost written when non-null (the sums: kmeans_sparse.hpp).
 int assign_sparse(const int64_t* rowptr, const int32_t* colidx, const double* vals,
                   const double* xnorm, int64_t n, int d, const double* C, const double* cnorm,
                   int k, const double* stats, int32_t* assign, double* cost, hipStream_t st);
-int sparse_sums(const int64_t* rowptr, const int32_t* colidx, const double* vals,
-                const double* w, const double* xnorm, int64_t n, int d, const int32_t* assign,
-                const double* cost, double* sums, double* wsum, double* costSum,
-                hipStream_t st);
 
 // cost[r] = distance(centers(assign[r]), x_r), the value findClosest returns.
 int row_cost(const double* X, int64_t n, int d, const double* C, const double* cnorm,

@@ -29,3 +29,17 @@ def heartbeat(msg: str) -> None:
     if os.path.isdir(d):
         with open(os.path.join(d, "heartbeat.log"), "a") as f:
             f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
+
+
+@pytest.fixture(autouse=True)
+def _release_cached_device_memory(request):
+    """Before every device test: free what earlier tests left in torch's
+    caching allocator, so the full-size tests (150-250 GB shards allocated by
+    libcyclone's own hipMalloc) find the HBM free."""
+    if "cuda" in request.fixturenames:
+        import gc
+        import torch
+        gc.collect()
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+    yield

@@ -390,4 +390,8 @@ def test_cos_csr_vs_oracle(cuda, weighted):
     np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), rs, rtol=1e-10, atol=1e-12)
     np.testing.assert_allclose(wsum.cpu().numpy(), rw, rtol=1e-12)
     np.testing.assert_allclose(float(cost.item()), rc, rtol=1e-10)
+    buf2 = torch.zeros_like(buf)            # fixed-order folds: bitwise reproducible
+    p.accumulate_csr(rpd, cid, vd, xn, None if w is None else _dev(w, cuda), Cd, cn,
+                     buf2[:k * d], buf2[k * d:k * d + k], buf2[k * d + k:])
+    assert torch.equal(buf2, buf)
     p.close()

@@ -89,6 +89,12 @@ def test_sparse_accumulate_vs_oracle(cuda, n, d, k, density, weighted):
     _rel_close(b[:k * d].reshape(k, d), rs, 1e-12)
     _rel_close(b[k * d:k * d + k], rw, 1e-12)
     _rel_close(b[k * d + k], rc, 1e-12)
+    # the sums fold in a fixed order (kmeans_sparse.hip): bitwise reproducible
+    for _ in range(2):
+        buf2 = torch.zeros_like(buf)
+        p.accumulate_csr(rp, ci, v, xn, None if w is None else _dev(w, cuda), Cd, cn,
+                         buf2[:k * d], buf2[k * d:k * d + k], buf2[k * d + k:])
+        assert torch.equal(buf2, buf)
     # centroid update (wide centers for d > 3072 use the global-memory path)
     conv = torch.zeros(1, dtype=torch.int32, device=cuda)
     p.update(Cd, cn, buf[:k * d], buf[k * d:k * d + k], 1e-4, conv)
