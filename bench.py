@@ -47,6 +47,10 @@ sys.path.insert(0, ROOT)
 FP64_PEAK_TFLOPS = 78.6   # MI355X fp64 (vector = matrix) spec, BASELINE.md section 2
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md chip table (spec)
 I8_PEAK_TOPS = 5000.0     # dense i8 MFMA: 2x the ~2.5 PF dense bf16 rate (MI355X_MICROARCH.md)
+# (bound, unit, peak, unit scale) of a priced kernel
+HBM = ("hbm", "GB/s", HBM_PEAK_GBS, 1e9)
+FP64 = ("mfma", "TFLOP/s", FP64_PEAK_TFLOPS, 1e12)
+I8 = ("mfma", "TOPS", I8_PEAK_TOPS, 1e12)
 
 ORDER = ("kmeans", "gramian", "lr_multi", "lr_sparse")
 # BASELINE configs: rows of the whole problem, and whether it is per GPU
@@ -176,19 +180,21 @@ def lr_sparse_chunks(n, dev, rank=0, F=1_000_000, k=64):
 # ---------------------------------------------------------------- workloads
 
 class KMeansWorkload:
-    """The dominant kernel is the two-limb pass of the exact-integer i8 screen
-    (k_screen32<.., 2, false>, timed as k_kmeans_screen2): its work is 3 i8
-    limb products of 2 ops per (row, padded center, dimension), priced
-    against the dense i8 MFMA peak; the fp64-equivalent rate (2 k d flop per
-    row) is reported beside it, and the three-limb pass over the rows it
-    leaves (k_kmeans_screen3) is timed too."""
-    kernel = "k_kmeans_screen2"
-    kernels = ("k_kmeans_screen2", "k_kmeans_cands", "k_kmeans_screen3", "k_kmeans_assign_fp64",
-               "k_chunk_sums")
-    pmc_names = {"k_kmeans_screen2": "k_screen32_l2"}
-    bound = "mfma"
-    unit = "TOPS"
-    peak = I8_PEAK_TOPS
+    """One Lloyd iteration per step over a row image built once per fit.
+    findClosest runs as the tiered exact screen of kmeans_i8.hip: the
+    one-limb exact-integer i8 pass over every (row, center) pair
+    (k_screen32<.., 1, false>, timed as k_kmeans_screen1), the two-limb
+    refinement over each 32 rows' candidate union (k_kmeans_refine2), the
+    full two-limb pass only for the rows those hand on (k_kmeans_screen2),
+    then the fp64 tiers.  Kernels are priced in their own units: the
+    one-limb pass against the i8 MFMA peak (2 ops per row, padded center
+    and dimension), the cluster sums (k_chunk_sums) against HBM; the
+    roofline line names the slowest priced kernel."""
+    kernel = "k_chunk_sums"
+    kernels = ("k_kmeans_screen1", "k_kmeans_refine2", "k_kmeans_screen2", "k_kmeans_cands",
+               "k_kmeans_screen3", "k_kmeans_assign_fp64", "k_chunk_sums")
+    pmc_names = {"k_kmeans_screen1": "k_screen32_l1", "k_kmeans_screen2": "k_screen32_l2",
+                 "k_kmeans_refine2": "k_screen32r", "k_chunk_sums": "k_chunk_sums_fast"}
 
     def __init__(self, n, dev, rank):
         import torch
@@ -221,6 +227,7 @@ class KMeansWorkload:
         self.buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=dev)
         self.conv = torch.zeros(1, dtype=torch.int32, device=dev)
         self.parallel = parallel
+        self._refine = (-1, -1, -1)
 
     def step(self):
         k, d = self.k, self.d
@@ -233,29 +240,39 @@ class KMeansWorkload:
         self.plan.update(self.C, self.cnorm, sums, wsum, 1e-4, self.conv)
 
     def work(self, kname, launches_per_step):
-        if kname != self.kernel:
-            return None
         D = 128 * ((self.d + 127) // 128)                 # 32-dim substeps, padded
-        kpad = 16 * (((self.k + 15) // 16 + 3) // 4 * 4)  # 32-center tiles
-        return 6.0 * D * kpad * self.n / launches_per_step   # i8 ops
+        kpad = 32 * (2 * ((self.k + 63) // 64))           # 32-center tiles (even count)
+        if kname == "k_kmeans_screen1":       # one limb product: 2 ops per (row, center, dim)
+            return 2.0 * D * kpad * self.n / launches_per_step, I8
+        if kname == "k_chunk_sums":           # every row once (fp64) + its perm entry
+            return self.n * (8 * self.d + 4) / launches_per_step, HBM
+        if kname == "k_kmeans_screen2" and self._refine[0] < 0:   # no refinement: every row
+            return 6.0 * D * kpad * self.n / launches_per_step, I8
+        return None
+
+    def after_timing(self):
+        self._refine = self.plan.last_refine()
 
     def extra_roofline(self, launches_per_step, avg_s):
         import torch
-        flops = 2.0 * self.k * self.d * self.n / launches_per_step
-        # screen tiers of one counted assign, after the timed region
+        listed, full, union = self._refine
+        waves = (listed - 0) / 32 if listed and listed > 0 else None
+        # screen tiers of one counted assign of every row, after the timed region
         a = torch.empty(self.n, dtype=torch.int32, device=self.X.device)
         c = torch.empty(self.n, dtype=torch.float64, device=self.X.device)
         self.plan.stats(self.C)
         exact = self.plan.assign(self.X, self.xnorm, self.C, self.cnorm, a, c,
                                  count_exact=True, rows=self.rows)
         tier2, _ = self.plan.last_tiers()
-        return {"algorithmic_fp64_flop_per_launch": flops,
-                "fp64_equivalent_tflops": flops / avg_s / 1e12,
-                "rows_to_candidate_pass": self.plan.last_candidates(),
-                "rows_to_three_limb_pass": self.plan.last_screen(),
-                "rows_to_fp64_screen": tier2, "rows_to_exact": exact,
-                "note": "i8 ops = two-limb integer screen (3 MFMA limb products, every "
-                        "row); fp64-equivalent = 2kd flop/row over the same time"}
+        return {"screen_tiers": {
+            "rows_listed_by_one_limb_pass": listed,
+            "rows_to_full_two_limb_pass": full,
+            "mean_union_centers_per_32_listed_rows": union / waves if waves else None,
+            "rows_to_candidate_pass": self.plan.last_candidates(),
+            "rows_to_three_limb_pass": self.plan.last_screen(),
+            "rows_to_fp64_screen": tier2, "rows_to_exact": exact,
+            "note": "the last timed iteration's one-limb pass / refinement, then one counted "
+                    "assign after the timed region for the later tiers"}}
 
     def describe(self):
         return (f"KMeans k={self.k} Lloyd iteration, dense fp64 {self.n} x {self.d} rows per GPU "
@@ -290,7 +307,6 @@ class KMeansWorkload:
 
 class GramianWorkload:
     kernel = "k_gram_tiles"
-    bound = "mfma"
 
     def __init__(self, n, dev, rank):
         import torch
@@ -312,7 +328,7 @@ class GramianWorkload:
         self.parallel.allreduce_(self.U)
 
     def work(self, kname, launches_per_step):
-        return float(self.n) * self.p * (self.p + 1) / launches_per_step   # flops (upper)
+        return float(self.n) * self.p * (self.p + 1) / launches_per_step, FP64   # flops (upper)
 
     def describe(self):
         return (f"RowMatrix.computeGramianMatrix pass, dense fp64 {self.n} x {self.p} rows per "
@@ -341,7 +357,6 @@ class GramianWorkload:
 class LRMultiWorkload:
     kernel = "k_mlr_margins"
     kernels = ("k_mlr_margins", "k_mlr_grad")
-    bound = "mfma"
 
     def __init__(self, n, dev, rank):
         import torch
@@ -384,7 +399,7 @@ class LRMultiWorkload:
         self.fn.calculate(self.coef)
 
     def work(self, kname, launches_per_step):
-        return 2.0 * self.n * self.F * self.C / launches_per_step    # each pass: one gemm
+        return 2.0 * self.n * self.F * self.C / launches_per_step, FP64   # each pass: one gemm
 
     def describe(self):
         return (f"multinomial LR ({self.C} classes) RDDLossFunction.calculate, dense fp64 "
@@ -434,7 +449,6 @@ class LRSparseWorkload:
     names the slower (dominant) one."""
     kernel = "k_tiles_grad"
     kernels = ("k_tiles_margin", "k_tiles_grad")
-    bound = "hbm"
 
     def __init__(self, n, dev, rank):
         import numpy as np
@@ -471,7 +485,7 @@ class LRSparseWorkload:
         self.fn.calculate(self.coef)
 
     def work(self, kname, launches_per_step):
-        return self.n * (self.k * 12 + 8 + 8) / launches_per_step   # bytes
+        return self.n * (self.k * 12 + 8 + 8) / launches_per_step, HBM   # bytes
 
     def extra_roofline(self, launches_per_step, avg_s):
         return {"layout_bytes": self.tiles.nbytes,
@@ -580,20 +594,16 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
     el = parallel.max_over_ranks(el, dev)
     value = total_rows * args.steps / el
 
-    # dominant kernel: the slowest of the priced kernels
+    if hasattr(wl, "after_timing"):
+        wl.after_timing()
+    # dominant kernel: the slowest of the priced kernels, in its own units
     priced = [k for k in kernels if prof[k][1] and wl.work(k, 1) is not None]
     kname = max(priced, key=lambda k: prof[k][0]) if priced else wl.kernel
     kms, launches = prof[kname]
     avg_s = kms / max(launches, 1) / 1e3
-    per_launch = wl.work(kname, launches / args.steps) if launches else 0.0
-    achieved = per_launch / avg_s if launches else None
-    if wl.bound == "mfma":
-        unit = getattr(wl, "unit", "TFLOP/s")
-        peak = getattr(wl, "peak", FP64_PEAK_TFLOPS)
-        achieved = achieved / 1e12 if achieved else None
-    else:
-        unit, peak = "GB/s", HBM_PEAK_GBS
-        achieved = achieved / 1e9 if achieved else None
+    per_launch, price = wl.work(kname, launches / args.steps) if (launches and priced) else (0.0, HBM)
+    bound, unit, peak, scale = price
+    achieved = per_launch / avg_s / scale if launches and priced else None
     pmc_name = getattr(wl, "pmc_names", {}).get(kname, kname)
     traffic, traffic_src = (pmc_traffic(name, pmc_name, launches / args.steps, n)
                             if launches else (None, None))
@@ -619,7 +629,7 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
                    "config_rows": CONFIG_ROWS[name],
                    "config_rows_are": "per GPU" if PER_GPU_CONFIG[name] else "total",
                    "parallelism": f"dp{world} (row shards, RCCL all-reduce merge)"},
-        "roofline": {"kernel": kname, "bound": wl.bound, "achieved": achieved,
+        "roofline": {"kernel": kname, "bound": bound, "achieved": achieved,
                      "peak": peak, "unit": unit,
                      "frac": (achieved / peak) if achieved else None,
                      "traffic": traffic, "traffic_source": traffic_src,

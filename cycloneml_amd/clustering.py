@@ -131,6 +131,16 @@ class KMeansPlan:
         N.check(self._lib.cyc_kmeans_last_candidates(self.handle, ctypes.byref(a)))
         return a.value
 
+    def last_refine(self):
+        """(rows the one-limb pass listed, rows handed to the full two-limb
+        pass, candidate centers the refinement screened in total) of the
+        last i8 screen; (-1, -1, -1) when it ran the two-limb pass over every
+        center (k <= 96)."""
+        a, b, c = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(self._lib.cyc_kmeans_last_refine(self.handle, ctypes.byref(a), ctypes.byref(b),
+                                                 ctypes.byref(c)))
+        return a.value, b.value, c.value
+
     def accumulate(self, X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, assign=None,
                    cost=None, stream=None, rows=None):
         N.check(self._lib.cyc_kmeans_accumulate_dev(

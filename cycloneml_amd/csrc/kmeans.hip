@@ -1738,6 +1738,9 @@ struct cyc_kmeans_plan_s {
   cyc::DeviceBuffer cb8, cq8, g8, prm8, scr8, list8Count;   // list8 = slowList (idle then)
   // candidate pass of the d <= 256 screen (kmeans_i8.hpp CandArgs)
   cyc::DeviceBuffer candRows, cands, candCount;
+  // the one-limb pass + two-limb refinement (kmeans_i8.hpp RefineArgs)
+  cyc::DeviceBuffer cand1Rows, cand1, cand1Count, fullList, fullCount;
+  bool lastRefined = false;  // the last i8 screen ran the refinement path
   int64_t max_rows = 0;
   size_t assignLds = 0;
   std::mutex mu;
@@ -1874,6 +1877,27 @@ int cand_args(cyc_kmeans_plan p, int64_t n, const double* X, const double* xnorm
   return CYC_OK;
 }
 
+// The one-limb pass + two-limb refinement of the d <= 256 screen, for k >
+// 96 (below that the two-limb pass over every center is as cheap) and k <=
+// 4096 (the refinement's union bitmap).
+int refine_args(cyc_kmeans_plan p, int64_t n, bool useCa, cyc::km8::RefineArgs& ra, bool& use) {
+  const int kstride = cyc::km8::tiles32(p->k) * 32;
+  use = useCa && p->k > 96 && kstride <= 4096 && std::getenv("CYC_KMEANS_NO_REFINE") == nullptr;
+  p->lastRefined = use;
+  if (!use) return CYC_OK;
+  int rc;
+  if ((rc = p->cand1Rows.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = p->cand1.reserve(sizeof(int32_t) * (size_t)n * cyc::km8::kCand1)) ||
+      (rc = p->cand1Count.reserve(64)) ||
+      (rc = p->fullList.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = p->fullCount.reserve(64)))
+    return rc;
+  ra = cyc::km8::RefineArgs{kstride, (int32_t*)p->cand1Rows.ptr, (int32_t*)p->cand1.ptr,
+                            (unsigned int*)p->cand1Count.ptr, (int32_t*)p->fullList.ptr,
+                            (unsigned int*)p->fullCount.ptr};
+  return CYC_OK;
+}
+
 int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmeans_rows rows,
               int64_t n, const double* C, const double* cnorm, int32_t* assign, double* cost,
               int64_t* n_exact_out, hipStream_t st, bool nostats = false) {
@@ -1896,12 +1920,15 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
     cyc::km8::CandArgs ca;
     bool useCa = false;
     if ((rc = cand_args(p, n, X, nullptr, C, cnorm, false, ca, useCa))) return rc;
+    cyc::km8::RefineArgs ra;
+    bool useRa = false;
+    if ((rc = refine_args(p, n, useCa, ra, useRa))) return rc;
     if ((rc = cyc::km8::screen(rows->img.ptr, (const int2*)rows->meta.ptr, xnorm, n, p->d,
                                p->cb8.ptr, (const float*)p->cq8.ptr, (const double*)p->g8.ptr,
                                cnorm, (const cyc::km8::CenterParams*)p->prm8.ptr, p->ktp8,
                                assign, (int32_t*)p->list3.ptr, (unsigned int*)p->list3Count.ptr,
                                (int32_t*)p->slowList.ptr, (unsigned int*)p->list8Count.ptr, st,
-                               useCa ? &ca : nullptr)))
+                               useCa ? &ca : nullptr, useRa ? &ra : nullptr)))
       return rc;
     rowList = (const int32_t*)p->list3.ptr;
     rowCount = (const unsigned int*)p->list3Count.ptr;
@@ -2199,8 +2226,8 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
     const int ks8 = cyc::km8::ksteps(d);
     p->ktp8 = (int)cyc::round_up((k + 15) / 16, cyc::km8::kWaves);
     if ((rc = p->cb8.reserve((size_t)p->ktp8 * ks8 * 3 * 64 * 16)) ||
-        (rc = p->cq8.reserve(sizeof(float) * (size_t)p->ktp8 * 32)) ||
-        (rc = p->g8.reserve(sizeof(double) * (size_t)p->ktp8 * 32)) ||
+        (rc = p->cq8.reserve(sizeof(float) * (size_t)p->ktp8 * 48)) ||
+        (rc = p->g8.reserve(sizeof(double) * (size_t)p->ktp8 * 48)) ||
         (rc = p->list8Count.reserve(64)) ||
         (rc = p->prm8.reserve(sizeof(cyc::km8::CenterParams))) ||
         (rc = p->scr8.reserve(sizeof(double) * 2 * (size_t)k))) {
@@ -2238,6 +2265,22 @@ int cyc_kmeans_last_candidates(cyc_kmeans_plan p, int64_t* candidate_rows) {
   CYC_REQUIRE(p != nullptr && candidate_rows, "arguments must not be null");
   std::lock_guard<std::mutex> g(p->mu);
   *candidate_rows = p->lastCands;
+  return CYC_OK;
+}
+
+int cyc_kmeans_last_refine(cyc_kmeans_plan p, int64_t* listed_rows, int64_t* full_rows,
+                           int64_t* union_centers) {
+  CYC_REQUIRE(p != nullptr && listed_rows && full_rows && union_centers,
+              "arguments must not be null");
+  std::lock_guard<std::mutex> g(p->mu);
+  *listed_rows = *full_rows = *union_centers = -1;
+  if (!p->lastRefined) return CYC_OK;
+  unsigned int h[3] = {0, 0, 0};
+  CYC_HIP(hipMemcpy(h, p->cand1Count.ptr, sizeof(unsigned int), hipMemcpyDeviceToHost));
+  CYC_HIP(hipMemcpy(h + 1, p->fullCount.ptr, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost));
+  *listed_rows = h[0];
+  *full_rows = h[1];
+  *union_centers = h[2];
   return CYC_OK;
 }
 

@@ -540,11 +540,12 @@ __global__ __launch_bounds__(256, KS <= 4 ? 3 : 2) void k_screen(
 // are zero with cq = +inf).
 
 __device__ __forceinline__ double err_term2(int e, double n1, double mu, int d);
+__device__ __forceinline__ double err_term1(int e, double n1, double mu);
 __global__ __launch_bounds__(256) void k_centers_pack32(
     const double* __restrict__ C, const double* __restrict__ cnorm, int k, int d, int S, int ktp,
     const double* __restrict__ cn1, const CenterParams* __restrict__ prm, uint4* __restrict__ Cb,
     float* __restrict__ cq, double* __restrict__ g, float* __restrict__ cq2,
-    double* __restrict__ g2) {
+    double* __restrict__ g2, float* __restrict__ cq1, double* __restrict__ g1) {
   const CenterParams p = *prm;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t total = (int64_t)ktp * S * 64;
@@ -574,15 +575,19 @@ __global__ __launch_bounds__(256) void k_centers_pack32(
     if (c < k && p.ok) {
       const double gc = err_term(p.ec, cn1[c], p.mu, d);
       const double gc2 = err_term2(p.ec, cn1[c], p.mu * 0x1p-7, d);
+      const double gc1 = err_term1(p.ec, cn1[c], p.mu * 0x1p-14);
       const double cn = cnorm[c];
       g[c] = gc;
       cq[c] = fdown((cn * cn) * (1.0 - kEpsF) - 2.0 * gc);
       g2[c] = gc2;
       cq2[c] = fdown((cn * cn) * (1.0 - kEpsF) - 2.0 * gc2);
+      g1[c] = gc1;
+      cq1[c] = fdown((cn * cn) * (1.0 - kEpsF) - 2.0 * gc1);
     } else {
-      g[c] = g2[c] = 0.0;
+      g[c] = g2[c] = g1[c] = 0.0;
       cq[c] = __builtin_inff();
-      cq2[c] = 0x1.fffffep127f;   // finite: the two-limb pass keeps index bits in L
+      // finite: the integer passes keep index bits in L
+      cq2[c] = cq1[c] = 0x1.fffffep127f;
     }
   }
 }
@@ -593,6 +598,15 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 // = (t - b)/128 with |t - b| <= 1/2), the dropped b.b' / 2^14 term <=
 // d 2^(ex+ec-16) = d 2^14 A2x A2c <= 0.5 d 2^14 (A2x^2 + A2c^2) (AM-GM);
 // A2 carries a 2^-7 slack.  n1 must bound |xh2|_1 (rows) or |c|_1 (centers).
+// fx / gc of the ONE-limb screen: |x_j - xh1_j| <= 2^(e-8) (a = rint(u)),
+// no dropped products (S1 = a.a' exactly): |x.c - xh1.ch1| <= A1x |c|_1 +
+// A1c |xh1|_1, split by AM-GM as for the other limb counts; A1 carries a
+// 2^-7 slack.  n1 must bound |xh1|_1 (rows) or |c|_1 (centers).
+__device__ __forceinline__ double err_term1(int e, double n1, double mu) {
+  const double A = __builtin_ldexp(1.0078125, e - 8);
+  return (0.5 * mu * A * A + 0.5 * n1 * n1 / mu) * (1.0 + 0x1p-40);
+}
+
 __device__ __forceinline__ double err_term2(int e, double n1, double mu, int d) {
   const double A = __builtin_ldexp(1.0078125, e - 15);
   const double kd = 0.502 * (double)d * 0x1p14;
@@ -611,7 +625,7 @@ __device__ __forceinline__ double err_term2(int e, double n1, double mu, int d) 
 // Two workgroups per CU; three for the two-limb pass (<= 168 VGPRs, LDS
 // 3 x 49 KB at S = 8), measured 7 % faster than two.
 template <int S, int W, int LIMBS, bool LIST>
-__global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
+__global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
     const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
     int64_t n, int d, const uint4* __restrict__ Cb, const float* __restrict__ cq,
     const double* __restrict__ g, const double* __restrict__ cnorm,
@@ -631,7 +645,13 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const CenterParams P = *prm;
-  const double mu = LIMBS == 3 ? P.mu : P.mu * 0x1p-7;   // any mu > 0 is valid
+  // any mu > 0 is valid; scaled with each limb count's quantum
+  const double mu = LIMBS == 3 ? P.mu : LIMBS == 2 ? P.mu * 0x1p-7 : P.mu * 0x1p-14;
+  // integer bounds (LIMBS < 3) in units F1 = 2^(ex + ec - SH): 2 s = F1 T
+  constexpr int SH = LIMBS == 1 ? 13 : 20;
+  // candidate sets per row: the two-limb pass's for the fp64 candidate pass
+  // (kCandMax), the one-limb pass's for the two-limb refinement (kCand1)
+  constexpr int CMAX = LIMBS == 1 ? kCand1 : kCandMax;
   const int64_t total = LIST ? (int64_t)*rowsInCount : n;
   // one group of 32 W rows (positions)
   auto group = [&](int64_t grp) {
@@ -707,8 +727,8 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) sh[reg] = __shfl(s0, (reg & 3) + 8 * (reg >> 2) + 4 * h);
   }
-  // cq scaled to the units 2^(exmin + ec - 20)
-  const float qscale = __builtin_ldexpf(1.0f, max(-160, min(160, 20 - P.ec - exmin)));
+  // cq scaled to the units 2^(exmin + ec - SH)
+  const float qscale = __builtin_ldexpf(1.0f, max(-160, min(160, SH - P.ec - exmin)));
   bool qbad = false;   // a cq below -2^30 units: the wave certifies nothing
   // LIMBS = 3: the two smallest f32 bounds; LIMBS = 2: the two largest
   // V = T - Q (the smallest L = -F1 V), tile index in the low IB bits
@@ -731,11 +751,13 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
       v4i Bc[LIMBS];
 #pragma unroll
       for (int L = 0; L < LIMBS; ++L) Bc[L] = B[(LIMBS * s + L) * 64];
-      const v4i B0 = Bc[0], B1 = Bc[1];
+      const v4i B0 = Bc[0], B1 = Bc[LIMBS >= 2 ? 1 : 0];
       // (separating the two acc[1] products by sched_barrier measured 3 % slower)
       acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B0, acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B1, acc[1], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B0, acc[1], 0, 0, 0);
+      if constexpr (LIMBS >= 2) {
+        acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B1, acc[1], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B0, acc[1], 0, 0, 0);
+      }
       if constexpr (LIMBS == 3) {
         const v4i B2 = Bc[2];
         acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B2, acc[2], 0, 0, 0);
@@ -756,7 +778,8 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
     asm("v_mov_b32 %0, %1" : "=v"(ctv) : "s"(ct));
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const int V = acc[0][reg] * 128 + acc[1][reg];                 // T - Q
+      // T - Q (LIMBS = 1: acc[0] started at -Q)
+      const int V = LIMBS == 1 ? acc[0][reg] : acc[0][reg] * 128 + acc[LIMBS - 1][reg];
       const int Ve = (int)(((unsigned)V & ~IM) | ctv);                  // ct < 2^IB
       sV2[reg] = max(min(sV1[reg], sV2[reg]), min(max(sV1[reg], sV2[reg]), Ve));   // v_med3_i32
       sV1[reg] = max(sV1[reg], Ve);
@@ -766,8 +789,8 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
     const int c = ct * 32 + r;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
-      const int T = acc[0][reg] * 128 + acc[1][reg];
       if constexpr (LIMBS == 3) {
+        const int T = acc[0][reg] * 128 + acc[1][reg];
         const float V = __builtin_fmaf((float)acc[2][reg], 0x1p-7f, (float)T);
         const float L = __builtin_fmaf(-F1[reg], V, cqv);
         const bool lt = L < sL1[reg];
@@ -799,7 +822,7 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
     v16i X[LIMBS];
     arrive(ct, sl);
     const float cqv = cq_of(sl);
-    if constexpr (LIMBS == 2) {
+    if constexpr (LIMBS < 3) {
       // -Q per row: ceil(floor(cq 2^k) / 2^sh) >= Q - 1 unit; cq above 2^30
       // units clamps (a smaller Q: still a lower bound)
       const float pf = cqv * qscale;   // exact (a power of two; round-down mode)
@@ -807,7 +830,7 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
       const int nb = -(int)__builtin_floorf(__builtin_fminf(pf, 0x1p30f));
       X[0] = v16i{};
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) X[1][reg] = nb >> sh[reg];
+      for (int reg = 0; reg < 16; ++reg) X[LIMBS - 1][reg] = nb >> sh[reg];
       tile(sl, X);
       epi2(ct, X);
     } else {
@@ -824,7 +847,7 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
   // LIMBS = 2: each lane's own best and second best (one center column per
   // lane) before the reduction merges them: the candidate sets below
   int cV1[16], cV2[16];
-  if constexpr (LIMBS == 2) {
+  if constexpr (LIMBS < 3) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       sI1[q] = (int)((unsigned)sV1[q] & IM) * 32 + r;
@@ -866,7 +889,7 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
   }                                                                                 \
   MERGE(K1[0], K2[0], sI1[0], __shfl_xor(K1[0], 1), __shfl_xor(K2[0], 1),           \
         __shfl_xor(sI1[0], 1));
-  if constexpr (LIMBS == 2) {
+  if constexpr (LIMBS < 3) {
     CYC_REDUCE(sV1, sV2, mergeV)
   } else {
     CYC_REDUCE(sL1, sL2, mergeL)
@@ -881,8 +904,8 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
   if ((lane & 1) == 0) {
     const int q = (lane >> 1) & 15;
     const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
-    redL1[row] = LIMBS == 2 ? __int_as_float(sV1[0]) : sL1[0];
-    redL2[row] = LIMBS == 2 ? __int_as_float(sV2[0]) : sL2[0];
+    redL1[row] = LIMBS < 3 ? __int_as_float(sV1[0]) : sL1[0];
+    redL2[row] = LIMBS < 3 ? __int_as_float(sV2[0]) : sL2[0];
     redI1[row] = sI1[0];
   }
   const bool waveBad = __builtin_amdgcn_ballot_w64(qbad) != 0;
@@ -899,8 +922,8 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
     double l1, l2, f1 = 0.0;
     int v1 = 0;
     bool clamped = false;
-    if constexpr (LIMBS == 2) {
-      f1 = __builtin_ldexp(1.0, mt.x + P.ec - 20);
+    if constexpr (LIMBS < 3) {
+      f1 = __builtin_ldexp(1.0, mt.x + P.ec - SH);
       v1 = __float_as_int(redL1[lane]);
       const int v2 = __float_as_int(redL2[lane]);
       l1 = -f1 * (double)v1;
@@ -917,13 +940,14 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
       const double xn = xnorm[grow], cn = cnorm[I1];
       const double xx = xn * xn, cc = cn * cn;
       const double n1 = (double)__int_as_float(mt.y);   // bounds |xh3|_1
-      const double fx = LIMBS == 3 ? err_term(mt.x, n1, mu, d)
-                                   : err_term2(mt.x, n1 + (double)d * __builtin_ldexp(1.0078125, mt.x - 15),
-                                               mu, d);
+      const double fx =
+          LIMBS == 3 ? err_term(mt.x, n1, mu, d)
+          : LIMBS == 2 ? err_term2(mt.x, n1 + (double)d * __builtin_ldexp(1.0078125, mt.x - 15), mu, d)
+                       : err_term1(mt.x, n1 + (double)d * __builtin_ldexp(1.0078125, mt.x - 8), mu);
       // LIMBS = 2: the index bits move each V by < 2^IB units and the
       // rounded Q adds < 1 more: |L1 - L1'|, |L2 - L2'| < (2^IB + 1) F1
       const double enc = LIMBS == 3 ? 0.0
-                                    : __builtin_ldexp((double)(IM + 3u), mt.x + P.ec - 20);
+                                    : __builtin_ldexp((double)(IM + 3u), mt.x + P.ec - SH);
       M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) + 2.0 * enc +
            0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g[I1]) +
            0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
@@ -935,7 +959,7 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
     }
     if (decided) {
       assign[grow] = I1;
-    } else if (LIMBS == 2 && candRows != nullptr && eligible) {
+    } else if (LIMBS < 3 && candRows != nullptr && eligible) {
       // candidates: the centers c with f1 (V1 - V_c) <= M, i.e. V_c >= v1 -
       // floor(M / f1) -- the certification test against I1, failed by
       // every candidate and passed by every other center
@@ -950,7 +974,7 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
       list[atomicAdd(listCount, 1u)] = (int32_t)grow;
     }
   }
-  if constexpr (LIMBS == 2) {
+  if constexpr (LIMBS < 3) {
     if (candRows != nullptr) {
       // Candidate sets of the undecided rows from the saved per-lane states:
       // lane (r, h) saw the centers 32 ct + r of row (reg & 3) + 8 (reg >> 2)
@@ -958,7 +982,7 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
       // and a lane whose SECOND best reaches it too (an index not kept)
       // sends the row to the three-limb pass.  <= kCandMax candidates go to
       // the candidate list (exact fp64 distances, screen_cands).
-      int* thrS = (int*)lds + W * 96 + wave * (64 + 32 * (kCandMax + 1));
+      int* thrS = (int*)lds + W * 96 + wave * (64 + 32 * (CMAX + 1));
       int* wantS = thrS + 32;
       int* candS = thrS + 64;
       if (lane < 32) {
@@ -979,22 +1003,22 @@ __global__ __launch_bounds__(64 * W, (LIMBS == 2 ? 12 : 8) / W) void k_screen32(
         const unsigned bits = (unsigned)(m >> (32 * h));
         if (ok) {
           const int slot = __builtin_popcount(bits & ((1u << r) - 1u));
-          if (slot < kCandMax)
-            candS[row * (kCandMax + 1) + 1 + slot] = (int)((unsigned)cV1[reg] & IM) * 32 + r;
+          if (slot < CMAX)
+            candS[row * (CMAX + 1) + 1 + slot] = (int)((unsigned)cV1[reg] & IM) * 32 + r;
         }
         if (r == 0 && w)
-          candS[row * (kCandMax + 1)] = (unsigned)(mo >> (32 * h)) ? -1 : __builtin_popcount(bits);
+          candS[row * (CMAX + 1)] = (unsigned)(mo >> (32 * h)) ? -1 : __builtin_popcount(bits);
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       if (want) {
-        const int* cs = candS + lane * (kCandMax + 1);
+        const int* cs = candS + lane * (CMAX + 1);
         const int cnt = cs[0];
-        if (cnt >= 1 && cnt <= kCandMax) {
+        if (cnt >= 1 && cnt <= CMAX) {
           const unsigned idx = atomicAdd(candCount, 1u);
           candRows[idx] = (int32_t)grow;
 #pragma unroll
-          for (int i = 0; i < kCandMax; ++i) cands[(size_t)idx * kCandMax + i] = i < cnt ? cs[1 + i] : -1;
+          for (int i = 0; i < CMAX; ++i) cands[(size_t)idx * CMAX + i] = i < cnt ? cs[1 + i] : -1;
         } else {
           list[atomicAdd(listCount, 1u)] = (int32_t)grow;
         }
@@ -1015,7 +1039,8 @@ int launch_screen32(const void* img, const int2* meta, const double* xnorm, int6
                     const unsigned int* rowsInCount, int32_t* assign, int32_t* list,
                     unsigned int* listCount, hipStream_t st, int32_t* candRows = nullptr,
                     int32_t* cands = nullptr, unsigned int* candCount = nullptr) {
-  KernelTimer timer(LIMBS == 2 ? "k_kmeans_screen2" : "k_kmeans_screen3", st);
+  KernelTimer timer(LIMBS == 1 ? "k_kmeans_screen1" : LIMBS == 2 ? "k_kmeans_screen2"
+                                                    : "k_kmeans_screen3", st);
   const int64_t wg = (n + 32 * W - 1) / (32 * W);   // W waves x 32 rows
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32<S, W, LIMBS, LIST>), dim3((unsigned)wg),
                      dim3(64 * W), 0, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
@@ -1024,6 +1049,337 @@ int launch_screen32(const void* img, const int2* meta, const double* xnorm, int6
   CYC_LAUNCH_CHECK("k_kmeans_screen32_i8");
   return CYC_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Two-limb refinement (d <= 256) of the one-limb pass.
+//
+// The one-limb pass (k_screen32<S, W, 1, false>: S1 = a.a' only, one MFMA
+// per 32-dim substep, a third of the two-limb pass's) screens every row
+// against every center.  It certifies the rows it can; for each other row
+// it lists the centers its bounds cannot exclude (<= kCand1: rowsIn /
+// candsIn) -- every other center c has a one-limb lower bound above the
+// one-limb winner w1's upper bound, i.e. |x - c|^2 > |x - w1|^2 (by the
+// certification margin).  Here each wave takes 32 listed rows, forms the
+// UNION of their candidate sets (<= 32 kPruneTiles centers: virtual tiles
+// of 32, B fragments gathered per lane from the center image) and runs the
+// two-limb screen over that union only.  A row certified there (w2 beats
+// every union center by the two-limb margin) beats w1 (in the union, or w2
+// = w1), hence every center outside the union too, by more than the
+// reference's fp64 rounding: the reference's pruned loop returns w2.  Its
+// other rows get the two-limb pass's treatment: candidate sets (<=
+// kCandMax, within the union) for the fp64 candidate pass, else the
+// three-limb pass.  Waves whose union is too large go to fullList (the
+// full two-limb pass over every center).
+constexpr int kPruneTiles = 3;
+
+template <int S>
+__global__ __launch_bounds__(256, 2) void k_screen32r(
+    const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
+    int64_t n, int d, const uint4* __restrict__ Cb, const float* __restrict__ cq,
+    const double* __restrict__ g, const double* __restrict__ cnorm,
+    const CenterParams* __restrict__ prm, int kstride, const int32_t* __restrict__ rowsIn,
+    const unsigned int* __restrict__ rowsInCount, const int32_t* __restrict__ candsIn,
+    int32_t* __restrict__ assign, int32_t* __restrict__ list, unsigned int* __restrict__ listCount,
+    int32_t* __restrict__ candRows, int32_t* __restrict__ cands,
+    unsigned int* __restrict__ candCount, int32_t* __restrict__ fullList,
+    unsigned int* __restrict__ fullCount, unsigned int* __restrict__ stat) {
+  constexpr int D = 32 * S, CH = 3 * D / 16;
+  constexpr int W = 4;
+  // per wave: the candidate list, then the candidate-set scratch (the union
+  // bitmap, kstride bits, aliases the latter)
+  constexpr int PER_WAVE = 32 * kPruneTiles + 64 + 32 * (kCandMax + 1);
+  static_assert(64 + 32 * (kCandMax + 1) >= 4096 / 32, "bitmap fits the scratch");
+  __shared__ int ldsw[W * PER_WAVE];
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int* candL = ldsw + wave * PER_WAVE;
+  const CenterParams P = *prm;
+  const double mu = P.mu * 0x1p-7;
+  const int64_t total = (int64_t)*rowsInCount;
+  const int64_t pos0 = ((int64_t)blockIdx.x * W + wave) * 32;
+  const int rows = (int)max<int64_t>(0, min<int64_t>(32, total - pos0));
+  if (rows == 0) return;
+  const bool rowOk = r < rows;
+  const int64_t myRow = rowOk ? rowsIn[pos0 + r] : 0;
+  auto to_full = [&]() {
+    if (lane < rows) fullList[atomicAdd(fullCount, 1u)] = (int32_t)myRow;
+  };
+  if (!P.ok) {   // uniform over the grid: every row to the fp64 tier
+    if (lane < rows) list[atomicAdd(listCount, 1u)] = (int32_t)myRow;
+    return;
+  }
+  // the union of the rows' candidate sets: bitmap, then the compacted list
+  unsigned* bm = (unsigned*)(candL + 32 * kPruneTiles);
+  const int words = kstride >> 5;                      // <= 128
+  for (int q = lane; q < words; q += 64) bm[q] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  bool bad = false;
+  if (lane < 32 && rowOk) {
+    const int32_t* cs = candsIn + (pos0 + r) * kCand1;
+#pragma unroll
+    for (int i = 0; i < kCand1; ++i) {
+      const int c = cs[i];
+      if (c >= P.k) bad = true;
+      if (c >= 0 && c < P.k) atomicOr(&bm[c >> 5], 1u << (c & 31));
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const unsigned wA = lane < words ? bm[lane] : 0u;
+  const unsigned wB = lane + 64 < words ? bm[lane + 64] : 0u;
+  const int cnt = __builtin_popcount(wA) + __builtin_popcount(wB);
+  int pre = cnt;                                       // inclusive prefix over lanes
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const int t = __shfl_up(pre, m);
+    if (lane >= m) pre += t;
+  }
+  const int ncand = __shfl(pre, 63);
+  if (__builtin_amdgcn_ballot_w64(bad) != 0 || ncand > 32 * kPruneTiles || ncand == 0) {
+    to_full();
+    return;
+  }
+  {
+    int o = pre - cnt;
+    for (unsigned b = wA; b; b &= b - 1) candL[o++] = lane * 32 + __builtin_ffs((int)b) - 1;
+    for (unsigned b = wB; b; b &= b - 1) candL[o++] = (lane + 64) * 32 + __builtin_ffs((int)b) - 1;
+    const int nt = (ncand + 31) >> 5;
+    for (int q = ncand + lane; q < nt * 32; q += 64) candL[q] = -1;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const int ntiles = (ncand + 31) >> 5;
+  // A fragments of the wave's rows (two limbs)
+  v4i A[S][2];
+  {
+    const uint4* src = Xq + myRow * CH + h;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int L = 0; L < 2; ++L) {
+        const v4u t = __builtin_nontemporal_load((const v4u*)(src + L * (D / 16) + 2 * s));
+        A[s][L] = rowOk ? __builtin_bit_cast(v4i, t) : v4i{0, 0, 0, 0};
+      }
+  }
+  const int2 mt = rowOk ? meta[myRow] : make_int2(INT_MIN, 0);
+  const int exr = mt.x;
+  int e0 = exr == INT_MIN ? INT_MAX : exr;
+#pragma unroll
+  for (int m = 1; m < 32; m <<= 1) e0 = min(e0, __shfl_xor(e0, m));
+  const int exmin = __builtin_amdgcn_readfirstlane(e0 == INT_MAX ? 0 : e0);
+  int sh[16];
+  {
+    const int s0 = exr == INT_MIN ? 31 : min(exr - exmin, 31);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) sh[reg] = __shfl(s0, (reg & 3) + 8 * (reg >> 2) + 4 * h);
+  }
+  const float qscale = __builtin_ldexpf(1.0f, max(-160, min(160, 20 - P.ec - exmin)));
+  bool qbad = false;
+  double xxj = 0.0;
+  if (lane < 32 && rowOk) {
+    const double xn = xnorm[myRow];
+    xxj = xn * xn;
+  }
+  // B fragments of center c (c < 0: a padding column, zero)
+  auto loadB = [&](int c, v4i (&B)[S][2]) {
+    const bool on = c >= 0;
+    const uint4* src = Cb + ((size_t)((on ? c : 0) >> 5) * S * 3) * 64 + ((on ? c : 0) & 31) + 32 * h;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int L = 0; L < 2; ++L) {
+        const v4u t = *(const v4u*)(src + (s * 3 + L) * 64);
+        B[s][L] = on ? __builtin_bit_cast(v4i, t) : v4i{0, 0, 0, 0};
+      }
+  };
+  // one virtual tile: column r holds center col (lane's), acc[1] from -Q
+  auto tileMfma = [&](int col, const v4i (&B)[S][2], v16i (&X)[2]) {
+    const float cqv = col >= 0 ? cq[col] : 0x1.fffffep127f;
+    const float pf = cqv * qscale;
+    qbad |= pf < -0x1p30f;
+    const int nb = -(int)__builtin_floorf(__builtin_fminf(pf, 0x1p30f));
+    X[0] = v16i{};
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) X[1][reg] = nb >> sh[reg];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      X[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B[s][0], X[0], 0, 0, 0);
+      X[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B[s][1], X[1], 0, 0, 0);
+      X[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B[s][0], X[1], 0, 0, 0);
+    }
+  };
+  // the two-limb certification margin of row (mt, xx) against center c
+  // (lower bounds l1, runner-up l2; IM: the index bits in V)
+  auto margin = [&](int c, double xx, double l1, double l2, unsigned IM) {
+    const double cn = cnorm[c];
+    const double cc = cn * cn;
+    const double n1 = (double)__int_as_float(mt.y);
+    const double fx = err_term2(mt.x, n1 + (double)d * __builtin_ldexp(1.0078125, mt.x - 15), mu, d);
+    const double enc = __builtin_ldexp((double)(IM + 3u), mt.x + P.ec - 20);
+    return (4.0 * (fx + g[c]) + 2.0 * kEpsF * (xx + cc) + 2.0 * enc +
+            0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g[c]) +
+            0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
+                       __builtin_fmin(__builtin_fabs(l2), 0x1p120)) +
+            0x1p-90) *
+           (1.0 + 0x1p-30);
+  };
+  __builtin_amdgcn_s_setreg(0x801, 2);     // f32 rounding toward -inf (lower bounds)
+  const int total_ = ncand;
+  // 4. the screen over the candidate tiles (top two V per row slot, the
+  // virtual tile index in the low IB bits)
+  const int IB = 32 - __builtin_clz((unsigned)max(ntiles - 1, 1));
+  const unsigned IM = (1u << IB) - 1u;
+  int sV1[16], sV2[16], sI1[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) sV1[q] = sV2[q] = INT_MIN;
+  for (int t = 0; t < ntiles; ++t) {
+    const int col = candL[t * 32 + r];
+    v4i B[S][2];
+    loadB(col, B);
+    v16i X[2];
+    tileMfma(col, B, X);
+    unsigned ctv;
+    asm("v_mov_b32 %0, %1" : "=v"(ctv) : "s"(t));
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int V = X[0][reg] * 128 + X[1][reg];
+      const int Ve = (int)(((unsigned)V & ~IM) | ctv);
+      sV2[reg] = max(min(sV1[reg], sV2[reg]), min(max(sV1[reg], sV2[reg]), Ve));
+      sV1[reg] = max(sV1[reg], Ve);
+    }
+  }
+  __builtin_amdgcn_s_setreg(0x801, 0);
+  const bool waveBad = __builtin_amdgcn_ballot_w64(qbad) != 0;
+  // each lane's own best / second best (its column) before the reduction:
+  // the candidate sets; centers through the candidate list
+  int cV1[16], cV2[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    sI1[q] = candL[(int)((unsigned)sV1[q] & IM) * 32 + r];
+    cV1[q] = sV1[q];
+    cV2[q] = sV2[q];
+  }
+  auto mergeV = [](int& V1, int& V2, int& I1, int oV1, int oV2, int oI1) {
+    V2 = max(min(V1, oV1), max(V2, oV2));
+    I1 = oV1 > V1 ? oI1 : I1;
+    V1 = max(V1, oV1);
+  };
+#pragma unroll
+  for (int lev = 0; lev < 4; ++lev) {
+    const int half = 8 >> lev, m = 16 >> lev;
+    const bool hi = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const int o1 = __shfl_xor(hi ? sV1[i] : sV1[i + half], m);
+      const int o2 = __shfl_xor(hi ? sV2[i] : sV2[i + half], m);
+      const int oI1 = __shfl_xor(hi ? sI1[i] : sI1[i + half], m);
+      int k1 = hi ? sV1[i + half] : sV1[i];
+      int k2 = hi ? sV2[i + half] : sV2[i];
+      int I1 = hi ? sI1[i + half] : sI1[i];
+      mergeV(k1, k2, I1, o1, o2, oI1);
+      sV1[i] = k1;
+      sV2[i] = k2;
+      sI1[i] = I1;
+    }
+  }
+  mergeV(sV1[0], sV2[0], sI1[0], __shfl_xor(sV1[0], 1), __shfl_xor(sV2[0], 1),
+         __shfl_xor(sI1[0], 1));
+  // lane holds row register q = lane bits 1..4: per-row results through LDS
+  int* red = candL + 32 * kPruneTiles;                // 3 x 32 ints (reused below)
+  int* redV1 = red;
+  int* redV2 = red + 32;
+  int* thrS = red;                                    // after the reads below
+  int* wantS = red + 32;
+  int* candS = red + 64;
+  int* redI1 = candS;                                 // 32 ints, read before candS is written
+  if ((lane & 1) == 0) {
+    const int q = (lane >> 1) & 15;
+    const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
+    redV1[row] = sV1[0];
+    redV2[row] = sV2[0];
+    redI1[row] = sI1[0];
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  bool want = false;
+  int thrV = 0;
+  if (lane < rows) {
+    const int I1 = redI1[lane];
+    const int v1 = redV1[lane];
+    const int v2 = redV2[lane];
+    const double f1 = __builtin_ldexp(1.0, exr + P.ec - 20);
+    const double l1 = -f1 * (double)v1;
+    const double l2 = v2 == INT_MIN ? __builtin_inf() : -f1 * (double)v2;
+    bool decided = false, eligible = false;
+    double M = 0.0;
+    if (exr != INT_MIN && I1 >= 0 && I1 < P.k && !waveBad && __builtin_isfinite(l1) &&
+        (double)cq[I1] * (double)qscale <= 0x1p30) {
+      M = margin(I1, xxj, l1, l2, IM);
+      decided = !__builtin_isfinite(l2) || (l2 - l1) > M;
+      eligible = __builtin_isfinite(M);
+    }
+    if (decided) {
+      assign[myRow] = I1;
+    } else if (candRows != nullptr && eligible) {
+      const double tv = (double)v1 - __builtin_floor(M / f1);
+      if (tv > (double)INT_MIN + 2.0) {
+        want = true;
+        thrV = (int)tv;
+      } else {
+        list[atomicAdd(listCount, 1u)] = (int32_t)myRow;
+      }
+    } else {
+      list[atomicAdd(listCount, 1u)] = (int32_t)myRow;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  if (candRows != nullptr) {
+    // candidate sets of the undecided rows (as the full pass; the centers
+    // pruned in step 3 are excluded by margin)
+    if (lane < 32) {
+      thrS[lane] = thrV;
+      wantS[lane] = want ? 1 : 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      const bool w = wantS[row] != 0;
+      const int t = thrS[row];
+      const bool ok = w && cV1[reg] >= t;
+      const bool ov = w && cV2[reg] >= t;
+      const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
+      const unsigned long long mo = __builtin_amdgcn_ballot_w64(ov);
+      const unsigned bts = (unsigned)(m >> (32 * h));
+      if (ok) {
+        const int slot = __builtin_popcount(bts & ((1u << r) - 1u));
+        if (slot < kCandMax)
+          candS[row * (kCandMax + 1) + 1 + slot] = candL[(int)((unsigned)cV1[reg] & IM) * 32 + r];
+      }
+      if (r == 0 && w)
+        candS[row * (kCandMax + 1)] = (unsigned)(mo >> (32 * h)) ? -1 : __builtin_popcount(bts);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (want) {
+      const int* cs = candS + lane * (kCandMax + 1);
+      const int c0 = cs[0];
+      if (c0 >= 1 && c0 <= kCandMax) {
+        const unsigned idx = atomicAdd(candCount, 1u);
+        candRows[idx] = (int32_t)myRow;
+#pragma unroll
+        for (int i = 0; i < kCandMax; ++i) cands[(size_t)idx * kCandMax + i] = i < c0 ? cs[1 + i] : -1;
+      } else {
+        list[atomicAdd(listCount, 1u)] = (int32_t)myRow;
+      }
+    }
+  }
+  if (stat && lane == 0) atomicAdd(stat, (unsigned)total_);
+}
+
 
 // Candidate rows (one wave each): fp64 squared distances to the <= kCandMax
 // candidates, summed over the lanes' dimensions (any order: the error is
@@ -1163,14 +1519,43 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
              const void* Cb, const float* cq, const double* g, const double* cnorm,
              const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
              unsigned int* listCount, int32_t* list2, unsigned int* list2Count,
-             const CandArgs* ca, hipStream_t st) {
+             const CandArgs* ca, hipStream_t st, const RefineArgs* ra = nullptr) {
   CYC_HIP(hipMemsetAsync(list2Count, 0, sizeof(unsigned int), st));
   if (ca) CYC_HIP(hipMemsetAsync(ca->candCount, 0, sizeof(unsigned int), st));
-  int rc = launch_screen32<S, W, 2, false>(img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 32,
-                                           g + (size_t)ktp * 32, cnorm, prm, ktp, nullptr,
-                                           nullptr, assign, list2, list2Count, st,
-                                           ca ? ca->candRows : nullptr, ca ? ca->cands : nullptr,
-                                           ca ? ca->candCount : nullptr);
+  int rc;
+  if (ra && ca) {
+    // one-limb pass over every center; the two-limb refinement over the
+    // union of the listed rows' candidates; the full two-limb pass over the
+    // rows neither can handle (fullList)
+    CYC_HIP(hipMemsetAsync(ra->cand1Count, 0, sizeof(unsigned int), st));
+    CYC_HIP(hipMemsetAsync(ra->fullCount, 0, 2 * sizeof(unsigned int), st));
+    if ((rc = launch_screen32<S, W, 1, false>(img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 64,
+                                              g + (size_t)ktp * 64, cnorm, prm, ktp, nullptr,
+                                              nullptr, assign, ra->fullList, ra->fullCount, st,
+                                              ra->cand1Rows, ra->cand1, ra->cand1Count)))
+      return rc;
+    {
+      KernelTimer timer("k_kmeans_refine2", st);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32r<S>), dim3((unsigned)((n + 127) / 128)),
+                         dim3(256), 0, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
+                         cq + (size_t)ktp * 32, g + (size_t)ktp * 32, cnorm, prm, ra->kstride,
+                         (const int32_t*)ra->cand1Rows, (const unsigned int*)ra->cand1Count,
+                         (const int32_t*)ra->cand1, assign, list2, list2Count, ca->candRows,
+                         ca->cands, ca->candCount, ra->fullList, ra->fullCount,
+                         ra->fullCount + 1);
+      CYC_LAUNCH_CHECK("k_screen32r");
+    }
+    rc = launch_screen32<S, W, 2, true>(img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 32,
+                                        g + (size_t)ktp * 32, cnorm, prm, ktp, ra->fullList,
+                                        ra->fullCount, assign, list2, list2Count, st,
+                                        ca->candRows, ca->cands, ca->candCount);
+  } else {
+    rc = launch_screen32<S, W, 2, false>(img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 32,
+                                         g + (size_t)ktp * 32, cnorm, prm, ktp, nullptr,
+                                         nullptr, assign, list2, list2Count, st,
+                                         ca ? ca->candRows : nullptr, ca ? ca->cands : nullptr,
+                                         ca ? ca->candCount : nullptr);
+  }
   if (rc) return rc;
   if (!ca)
     return launch_screen32<S, W, 3, true>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp,
@@ -1259,7 +1644,8 @@ int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp,
     const int64_t total = std::max<int64_t>((int64_t)ktp32 * S * 64, (int64_t)ktp32 * 32);
     hipLaunchKernelGGL(k_centers_pack32, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                        C, cnorm, k, d, S, ktp32, (const double*)cn1, (const CenterParams*)prm,
-                       (uint4*)Cb, cq, g, cq + (size_t)ktp * 16, g + (size_t)ktp * 16);
+                       (uint4*)Cb, cq, g, cq + (size_t)ktp * 16, g + (size_t)ktp * 16,
+                       cq + (size_t)ktp * 32, g + (size_t)ktp * 32);
     CYC_LAUNCH_CHECK("k_centers_pack32");
     return CYC_OK;
   }
@@ -1275,13 +1661,13 @@ int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, in
            const void* Cb, const float* cq, const double* g, const double* cnorm,
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
            unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st,
-           const CandArgs* ca) {
+           const CandArgs* ca, const RefineArgs* ra) {
   if (n <= 0) return CYC_OK;
   if (uses32(d)) {
     const int k32 = ktp * 16 / 32;   // launch over the padded center range (cq = +inf)
     switch (ksteps(d)) {
-      case 2: return screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st);
-      default: return screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st);
+      case 2: return screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st, ra);
+      default: return screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st, ra);
     }
   }
   switch (ksteps(d)) {

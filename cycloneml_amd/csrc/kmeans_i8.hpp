@@ -47,8 +47,8 @@ int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipS
 // Centers -> packed B fragments (Cb), per-center lower-bound constants cq
 // (float, +inf for padding), error terms g (fp64) and the launch's params.
 // scratch: >= 2k doubles + 1 int.  ktp: 16-center tiles, a multiple of kWaves.
-// cq and g hold 2 ktp 16 entries: the 32x32 screen's two-limb pass keeps its
-// constants in the second half.
+// cq and g hold 3 ktp 16 entries: the 32x32 screen's two-limb pass keeps its
+// constants in the second third, its one-limb pass in the last.
 int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp, void* Cb,
                     float* cq, double* g, CenterParams* prm, double* scratch, hipStream_t st);
 
@@ -60,6 +60,8 @@ int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp,
 // the screened vectors: X / xnorm[row] when unit (the cosine plan), C as
 // given (the screen's centers).
 constexpr int kCandMax = 6;
+// candidate centers per row the one-limb pass hands to the two-limb refinement
+constexpr int kCand1 = 8;
 struct CandArgs {
   const double* X;        // n x d fp64 rows
   const double* xnorm;    // unit: the row norms X is divided by
@@ -73,6 +75,23 @@ struct CandArgs {
   unsigned int* candCount;
 };
 
+// The one-limb pass + two-limb refinement of the d <= 256 screen (k > 96,
+// k <= 4096; kmeans_i8.hip k_screen32r): the one-limb pass over every
+// center lists each row it cannot certify with <= kCand1 candidates
+// (cand1Rows / cand1, n and n kCand1 entries, cand1Count 1 counter); the
+// refinement screens 32 listed rows at a time over the union of their
+// candidates; rows neither pass can handle go to fullList (n entries,
+// fullCount 2 counters: rows; union centers screened) for the full
+// two-limb pass.  kstride = 32-center tiles x 32.
+struct RefineArgs {
+  int kstride;
+  int32_t* cand1Rows;
+  int32_t* cand1;
+  unsigned int* cand1Count;
+  int32_t* fullList;
+  unsigned int* fullCount;
+};
+
 // Screen every row: certified rows get assign[row]; the others are appended
 // to list (listCount is NOT cleared here).  list2 / list2Count (n entries +
 // one counter): scratch for the rows the 32x32 two-limb pass leaves.
@@ -81,7 +100,8 @@ int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, in
            const void* Cb, const float* cq, const double* g, const double* cnorm,
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
            unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st,
-           const CandArgs* ca = nullptr);
+           const CandArgs* ca = nullptr,
+           const RefineArgs* ra = nullptr);
 
 }  // namespace km8
 }  // namespace cyc

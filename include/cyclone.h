@@ -144,6 +144,14 @@ int cyc_kmeans_last_screen(cyc_kmeans_plan plan, int64_t* three_limb_rows);
  * to the <= 6 centers its bounds could not exclude) on the last counted
  * assign (-1 when no two-limb pass ran).  Also a tier statistic. */
 int cyc_kmeans_last_candidates(cyc_kmeans_plan plan, int64_t* candidate_rows);
+/* The last i8 screen's one-limb pass + two-limb refinement (d <= 256,
+ * 96 < k <= 4096): rows the one-limb pass listed with their candidate
+ * centers, rows handed to the full two-limb pass, and the candidate centers
+ * the refinement screened in total (each wave 32 listed rows); all -1 when
+ * that screen ran the two-limb pass over every center.  Statistics of the
+ * tiered findClosest; no reference counterpart. */
+int cyc_kmeans_last_refine(cyc_kmeans_plan plan, int64_t* listed_rows, int64_t* full_rows,
+                           int64_t* union_centers);
 
 /* One partition's contribution to a Lloyd iteration: statistics + assign +
  * per-cluster sums.  sums[k*d] += sum of w*x, wsum[k] += sum of w,

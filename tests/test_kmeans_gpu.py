@@ -600,3 +600,103 @@ def test_exact_tier_many_centers(cuda, k, d, nostats):
     ra, rc = _oracle_assign(X, C)
     np.testing.assert_array_equal(a, ra)
     np.testing.assert_array_equal(c, rc)
+
+
+@pytest.mark.parametrize("n,d,k,sep,dup", [(200_000, 64, 128, 4.0, False),
+                                           (120_000, 256, 1024, 4.0, False),
+                                           (150_000, 200, 300, 1.5, True),
+                                           (100_000, 32, 97, 4.0, False),
+                                           (60_000, 256, 96, 4.0, False)])
+def test_one_limb_refinement_lloyd(cuda, n, d, k, sep, dup):
+    """d <= 256, k > 96: the i8 screen runs the one-limb pass over every
+    center and the two-limb refinement over the union of each 32 rows'
+    candidates (kmeans_i8.hip k_screen32r), the full two-limb pass only for
+    the rows neither handles.  Over four Lloyd iterations (centers moving
+    between them) every assignment and cost equals the restatement's bit
+    for bit, sums within 1e-10.  Cases: separated clusters (d 64 / 256, k up
+    to 1024), close clusters with near-duplicate centers (near ties), k = 97
+    (the smallest refined k) and k = 96 (the two-limb pass over every
+    center: no refinement)."""
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    rng = np.random.default_rng(n + d + k)
+    true_c = rng.normal(scale=sep, size=(k, d))
+    X = true_c[rng.integers(0, k, n)] + rng.normal(size=(n, d))
+    C = X[:k].copy()
+    if dup:
+        C[k // 2:k // 2 + 10] = C[:10] + 1e-9          # near-duplicate centers
+    Xd, Cd = _dev(X, cuda), _dev(C, cuda)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = KMeansPlan(d, k, n)
+    rows = p.rows(Xd)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    pc = torch.empty(n, dtype=torch.float64, device=cuda)
+    conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+    for it in range(4):
+        Ch = Cd.cpu().numpy()
+        ref = oracle.kmeans_iteration(X, oracle.row_norms(X), None, Ch, oracle.row_norms(Ch),
+                                      num_partitions=8, threads=8)
+        sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+        wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+        cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+        p.accumulate(Xd, xn, None, Cd, cn, sums, wsum, cost, a, pc, rows=rows)
+        listed, full, union = p.last_refine()
+        torch.cuda.synchronize()
+        bad = np.flatnonzero((a.cpu().numpy() != ref["assign"]) | (pc.cpu().numpy() != ref["dist"]))
+        assert bad.size == 0, f"iteration {it}: {bad.size} rows differ, first {bad[:10]}"
+        np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
+                                   atol=1e-10 * np.abs(ref["sums"]).max())
+        if k <= 96:
+            assert (listed, full, union) == (-1, -1, -1)
+        else:
+            assert 0 <= listed <= n and 0 <= full <= n and union >= 0
+            if not dup:
+                assert full < n // 10, (it, full)
+        p.update(Cd, cn, sums, wsum, 1e-4, conv)
+
+
+@pytest.mark.timeout(900)
+def test_full_config_third_iteration(cuda):
+    """BASELINE config 2 on bench.py's rows as the bench times it: two Lloyd
+    iterations, then the third (centers that moved, as in the timed steps)
+    compared with the restatement for EVERY row (assignment and cost bit for
+    bit, sums within 1e-10); the one-limb pass + refinement handled it."""
+    import os
+    import sys
+    import torch
+    from cycloneml_amd.clustering import row_norms
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    n, d, k = 10_000_000, 256, 1024
+    X = bench.kmeans_data(n, cuda, 0, d, k)
+    C = X[:k].clone()
+    xn, cn = row_norms(X), row_norms(C)
+    p = _plan(d, k, n)
+    rows = p.rows(X)
+    conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    pc = torch.empty(n, dtype=torch.float64, device=cuda)
+    for it in range(3):
+        if it == 2:
+            Ch = C.cpu().numpy()
+        sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+        wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+        cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+        p.accumulate(X, xn, None, C, cn, sums, wsum, cost, a, pc, rows=rows)
+        if it < 2:
+            p.update(C, cn, sums, wsum, 1e-4, conv)
+    listed, full, union = p.last_refine()
+    torch.cuda.synchronize()
+    assert 0 <= full < n // 4 and listed >= 0 and union >= 0
+    del rows
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or 16, os.cpu_count() or 1, 16)
+    Xh = X.cpu().numpy()
+    del X
+    ref = oracle.kmeans_iteration(Xh, xn.cpu().numpy(), None, Ch, oracle.row_norms(Ch),
+                                  num_partitions=threads, threads=threads)
+    ah, ch = a.cpu().numpy(), pc.cpu().numpy()
+    bad = np.flatnonzero((ah != ref["assign"]) | (ch != ref["dist"]))
+    assert bad.size == 0, f"{bad.size} rows differ, first {bad[:10]}"
+    np.testing.assert_array_equal(wsum.cpu().numpy(), ref["wsum"])
+    np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
+                               atol=1e-10 * np.abs(ref["sums"]).max())
