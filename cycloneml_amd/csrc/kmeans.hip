@@ -223,7 +223,8 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
     int ldsStride, const double* __restrict__ Ct, const double* __restrict__ C,
     const double* __restrict__ cnorm, int k, int kpad, double marginFac,
     int32_t* __restrict__ assign, double* __restrict__ cost, int32_t* __restrict__ slowList,
-    unsigned int* __restrict__ slowCount) {
+    unsigned int* __restrict__ slowCount, const int32_t* __restrict__ rowList,
+    const unsigned int* __restrict__ rowCount) {
   constexpr int T = BM / 16;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double* Xs = smem;                                   // BM x ldsStride
@@ -231,22 +232,26 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
   double* mrg = xnS + BM;                              // kWaves x BM x 4
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t row0 = (int64_t)blockIdx.x * BM;
-  const int rows = (int)min<int64_t>(BM, n - row0);
+  // Row source: rows row0.. of X (full pass, one block per tile), or the
+  // rows an earlier screen queued in rowList (grid-stride over its tiles).
+  const int64_t nsrc = rowList ? (int64_t)*rowCount : n;
+  for (int64_t blk = blockIdx.x; blk * BM < nsrc; blk += gridDim.x) {
+#define CYC_GROW1(i) (rowList ? (int64_t)rowList[row0 + (i)] : row0 + (i))
+  const int64_t row0 = blk * BM;
+  const int rows = (int)min<int64_t>(BM, nsrc - row0);
 
-  // Stage the contiguous BM x d block of X (zero padded to d4 and BM).
+  // Stage the BM x d block of X (zero padded to d4 and BM).
   {
-    const double* src = X + row0 * d;
     const int total = rows * d;  // < 2^31: BM * d <= 64 * 1240
     for (int e = tid; e < total; e += kAssignThreads) {
       int r = e / d, c = e - r * d;
-      Xs[r * ldsStride + c] = src[e];
+      Xs[r * ldsStride + c] = X[CYC_GROW1(r) * d + c];
     }
     for (int e = tid; e < BM * d4; e += kAssignThreads) {
       int r = e / d4, c = e - r * d4;
       if (r >= rows || c >= d) Xs[r * ldsStride + c] = 0.0;
     }
-    if (tid < BM) xnS[tid] = (tid < rows) ? xnorm[row0 + tid] : 0.0;
+    if (tid < BM) xnS[tid] = (tid < rows) ? xnorm[CYC_GROW1(tid)] : 0.0;
   }
   __syncthreads();
 
@@ -400,7 +405,7 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
       const double* m = mrg + ((size_t)w * BM + row) * 4;
       slot_merge(S, (float)m[0], (float)m[1], (float)m[2], (int)m[3]);
     }
-    const int64_t grow = row0 + row;
+    const int64_t grow = CYC_GROW1(row);
     if (S.I1 >= 0 && S.L2 > S.U1) {
       // Exact fastSquaredDistance(centers(I1), point) = Vectors.sqdist(c, x)
       // (when the caller wants per-row costs; the Lloyd path computes them
@@ -421,6 +426,9 @@ __global__ __launch_bounds__(kAssignThreads, 1) void k_kmeans_assign(
       slowList[slot] = (int32_t)grow;
     }
   }
+  __syncthreads();   // LDS is restaged by the next tile
+  }
+#undef CYC_GROW1
 }
 
 // Second-generation assign kernel (the default when d4 % 32 == 0 and the
@@ -1812,7 +1820,8 @@ int launch_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64
   hipLaunchKernelGGL(k_kmeans_assign<BM>, dim3((unsigned)blocks), dim3(kAssignThreads),
                      p->assignLds, st, X, xnorm, n, p->d, p->d4, p->ldsStride,
                      (const double*)p->ct.ptr, C, cnorm, p->k, p->kpad, marginFac, assign, cost,
-                     (int32_t*)p->slowList.ptr, (unsigned int*)p->slowCount.ptr);
+                     (int32_t*)p->slowList.ptr, (unsigned int*)p->slowCount.ptr, rowList,
+                     rowCount);
   CYC_LAUNCH_CHECK("k_kmeans_assign");
   return CYC_OK;
 }
