@@ -635,7 +635,10 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
     int32_t* __restrict__ candRows, int32_t* __restrict__ cands,
     unsigned int* __restrict__ candCount) {
   constexpr int D = 32 * S, CH = 3 * D / 16;      // 16-byte chunks per image row
-  constexpr int FR = LIMBS * S;                    // 1 KiB B fragments per center tile
+  // LIMBS = 1 takes two 32-center tiles per step (one barrier and one ring
+  // slot per 64 centers: its tiles carry a third of the MFMAs)
+  constexpr bool PAIR = LIMBS == 1;
+  constexpr int FR = PAIR ? 2 * S : LIMBS * S;     // 1 KiB B fragments per ring step
   constexpr int TB = FR * 1024 + 256;              // tile slot: fragments, then 64 cq floats
   constexpr int G = FR / W;                        // fragment DMAs per wave per tile (+1: wave 0's cq)
   static_assert(FR % W == 0, "fragments split evenly over the waves");
@@ -670,22 +673,26 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
   // tile's cq (all waves write the same 256 bytes); past the last tile the
   // last one is re-read into the free slot, so every wave always has exactly
   // G DMAs per tile in flight and one counted wait fits all tiles.
+  const int nsteps = PAIR ? ktp / 2 : ktp;          // ktp is even
   auto issue = [&](int t, int slot) {
-    const int tt = t < ktp ? t : ktp - 1;
-    const char* src = (const char*)Cb + (size_t)tt * (3 * S) * 1024 + lane * 16;
+    const int tt = t < nsteps ? t : nsteps - 1;
     char* dst = lds + slot * TB;
 #pragma unroll
     for (int j = 0; j < FR / W; ++j) {
-      const int f = wave + W * j;                     // fragment (substep f / LIMBS, limb f % LIMBS)
-      const int piece = (f / LIMBS) * 3 + f % LIMBS;  // its 1 KiB piece in the 3-limb image
+      const int f = wave + W * j;
+      // PAIR: fragment f = limb a of substep f % S of tile 2 tt + f / S;
+      // else substep f / LIMBS, limb f % LIMBS of tile tt
+      const int tile = PAIR ? 2 * tt + f / S : tt;
+      const int piece = PAIR ? (f % S) * 3 : (f / LIMBS) * 3 + f % LIMBS;
+      const char* src = (const char*)Cb + (size_t)tile * (3 * S) * 1024 + lane * 16;
       __builtin_amdgcn_global_load_lds((const void*)(src + piece * 1024),
                                        (__attribute__((address_space(3))) void*)(dst + f * 1024),
                                        16, 0, 0);
     }
-    if (wave == 0)   // the tile's 32 cq (lanes 32..63 repeat them)
-      __builtin_amdgcn_global_load_lds((const void*)(cq + (size_t)tt * 32 + r),
-                                       (__attribute__((address_space(3))) void*)(dst + FR * 1024),
-                                       4, 0, 0);
+    if (wave == 0)   // the step's cq: 32 (lanes 32..63 repeat them) or PAIR's 64
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(cq + (PAIR ? (size_t)tt * 64 + lane : (size_t)tt * 32 + r)),
+          (__attribute__((address_space(3))) void*)(dst + FR * 1024), 4, 0, 0);
   };
   issue(0, 0);
   issue(1, 1);
@@ -800,7 +807,9 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
       }
     }
   };
-  auto cq_of = [&](int slot) { return *(const float*)(lds + slot * TB + FR * 1024 + r * 4); };
+  auto cq_of = [&](int slot, int half = 0) {
+    return *(const float*)(lds + slot * TB + FR * 1024 + (half * 32 + r) * 4);
+  };
   // tile t in `slot`: wait for this wave's DMAs of t (those of t + 1 may stay
   // in flight), barrier (every wave's part of t landed; every wave is past
   // t - 1, whose slot the DMAs of t + 2 now refill)
@@ -818,7 +827,36 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
   // second accumulator set: 193 VGPRs, two waves per SIMD, 4 % slower than
   // this form at 168 VGPRs and three waves per SIMD)
   int sl = 0;
-  for (int ct = 0; ct < ktp; ++ct) {
+  if constexpr (PAIR) {
+    for (int st = 0; st < nsteps; ++st) {
+      arrive(st, sl);
+      // -Q per row of each half (see below); tiles 2 st and 2 st + 1
+      int nb[2];
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const float pf = cq_of(sl, hf) * qscale;
+        qbad |= pf < -0x1p30f;
+        nb[hf] = -(int)__builtin_floorf(__builtin_fminf(pf, 0x1p30f));
+      }
+      v16i X0[1], X1[1];
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        X0[0][reg] = nb[0] >> sh[reg];
+        X1[0][reg] = nb[1] >> sh[reg];
+      }
+      const v4i* B = (const v4i*)(lds + sl * TB) + lane;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const v4i B0 = B[s * 64], B1 = B[(S + s) * 64];
+        X0[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B0, X0[0], 0, 0, 0);
+        X1[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B1, X1[0], 0, 0, 0);
+      }
+      epi2(2 * st, X0);
+      epi2(2 * st + 1, X1);
+      sl = next_slot(sl);
+    }
+  }
+  for (int ct = 0; ct < (PAIR ? 0 : ktp); ++ct) {
     v16i X[LIMBS];
     arrive(ct, sl);
     const float cqv = cq_of(sl);
