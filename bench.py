@@ -192,7 +192,7 @@ class KMeansWorkload:
     roofline line names the slowest priced kernel."""
     kernel = "k_chunk_sums"
     kernels = ("k_kmeans_screen1", "k_kmeans_refine2", "k_kmeans_screen2", "k_kmeans_cands",
-               "k_kmeans_screen3", "k_kmeans_assign_fp64", "k_chunk_sums")
+               "k_kmeans_screen3", "k_kmeans_compact", "k_kmeans_assign_fp64", "k_chunk_sums")
     pmc_names = {"k_kmeans_screen1": "k_screen32_l1", "k_kmeans_screen2": "k_screen32_l2",
                  "k_kmeans_refine2": "k_screen32r", "k_chunk_sums": "k_chunk_sums_fast"}
 

@@ -1748,6 +1748,8 @@ struct cyc_kmeans_plan_s {
   cyc::DeviceBuffer candRows, cands, candCount;
   // the one-limb pass + two-limb refinement (kmeans_i8.hpp RefineArgs)
   cyc::DeviceBuffer cand1Rows, cand1, cand1Count, fullList, fullCount;
+  // the screens' sharded append stage (kmeans_i8.hpp AppendStage)
+  cyc::DeviceBuffer stgRowsA, stgRowsB, stgCandRows, stgCands, stgCounts;
   bool lastRefined = false;  // the last i8 screen ran the refinement path
   int64_t max_rows = 0;
   size_t assignLds = 0;
@@ -1907,6 +1909,28 @@ int refine_args(cyc_kmeans_plan p, int64_t n, bool useCa, cyc::km8::RefineArgs& 
   return CYC_OK;
 }
 
+// The screens' sharded append stage for n rows (with the candidate pass);
+// CYC_KMEANS_NO_STAGE=1 appends straight to the lists (one counter each).
+int stage_args(cyc_kmeans_plan p, int64_t n, bool useCa, cyc::km8::AppendStage& sg, bool& use) {
+  use = useCa && std::getenv("CYC_KMEANS_NO_STAGE") == nullptr;
+  if (!use) return CYC_OK;
+  namespace k8 = cyc::km8;
+  const unsigned cap = k8::shard_cap(n);
+  const size_t ent = (size_t)cap * k8::kShards;
+  const size_t cbytes = sizeof(unsigned int) * k8::kSets * k8::kShards * k8::kShardStride;
+  int rc;
+  if ((rc = p->stgRowsA.reserve(sizeof(int32_t) * ent)) ||
+      (rc = p->stgRowsB.reserve(sizeof(int32_t) * ent)) ||
+      (rc = p->stgCandRows.reserve(sizeof(int32_t) * ent)) ||
+      (rc = p->stgCands.reserve(sizeof(int32_t) * ent * k8::kCand1)) ||
+      (rc = p->stgCounts.reserve(cbytes)))
+    return rc;
+  sg = k8::AppendStage{(int32_t*)p->stgRowsA.ptr, (int32_t*)p->stgRowsB.ptr,
+                       (int32_t*)p->stgCandRows.ptr, (int32_t*)p->stgCands.ptr,
+                       (unsigned int*)p->stgCounts.ptr, cap};
+  return CYC_OK;
+}
+
 int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmeans_rows rows,
               int64_t n, const double* C, const double* cnorm, int32_t* assign, double* cost,
               int64_t* n_exact_out, hipStream_t st, bool nostats = false) {
@@ -1932,12 +1956,16 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
     cyc::km8::RefineArgs ra;
     bool useRa = false;
     if ((rc = refine_args(p, n, useCa, ra, useRa))) return rc;
+    cyc::km8::AppendStage sg;
+    bool useSg = false;
+    if ((rc = stage_args(p, n, useCa, sg, useSg))) return rc;
     if ((rc = cyc::km8::screen(rows->img.ptr, (const int2*)rows->meta.ptr, xnorm, n, p->d,
                                p->cb8.ptr, (const float*)p->cq8.ptr, (const double*)p->g8.ptr,
                                cnorm, (const cyc::km8::CenterParams*)p->prm8.ptr, p->ktp8,
                                assign, (int32_t*)p->list3.ptr, (unsigned int*)p->list3Count.ptr,
                                (int32_t*)p->slowList.ptr, (unsigned int*)p->list8Count.ptr, st,
-                               useCa ? &ca : nullptr, useRa ? &ra : nullptr)))
+                               useCa ? &ca : nullptr, useRa ? &ra : nullptr,
+                               useSg ? &sg : nullptr)))
       return rc;
     rowList = (const int32_t*)p->list3.ptr;
     rowCount = (const unsigned int*)p->list3Count.ptr;
@@ -2117,6 +2145,9 @@ int cos_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmea
     cyc::km8::CandArgs ca;
     bool useCa = false;
     if ((rc = cand_args(p, n, X, xnorm, V, Vn, true, ca, useCa))) return rc;
+    cyc::km8::AppendStage sg;
+    bool useSg = false;
+    if ((rc = stage_args(p, n, useCa, sg, useSg))) return rc;
     if ((rc = cyc::km8::centers_prepare(V, Vn, p->k, p->d, p->ktp8, p->cb8.ptr,
                                         (float*)p->cq8.ptr, (double*)p->g8.ptr,
                                         (cyc::km8::CenterParams*)p->prm8.ptr,
@@ -2126,7 +2157,8 @@ int cos_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmea
                                (const float*)p->cq8.ptr, (const double*)p->g8.ptr, Vn,
                                (const cyc::km8::CenterParams*)p->prm8.ptr, p->ktp8, assign, list,
                                count, (int32_t*)p->slowList.ptr,
-                               (unsigned int*)p->list8Count.ptr, st, useCa ? &ca : nullptr)))
+                               (unsigned int*)p->list8Count.ptr, st, useCa ? &ca : nullptr,
+                               nullptr, useSg ? &sg : nullptr)))
       return rc;
   } else if ((rc = cyc::kmcos::list_all(list, count, n, st))) {
     return rc;

@@ -633,7 +633,7 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
     const unsigned int* __restrict__ rowsInCount, int32_t* __restrict__ assign,
     int32_t* __restrict__ list, unsigned int* __restrict__ listCount,
     int32_t* __restrict__ candRows, int32_t* __restrict__ cands,
-    unsigned int* __restrict__ candCount) {
+    unsigned int* __restrict__ candCount, unsigned int scap) {
   constexpr int D = 32 * S, CH = 3 * D / 16;      // 16-byte chunks per image row
   // LIMBS = 1 takes two 32-center tiles per step (one barrier and one ring
   // slot per 64 centers: its tiles carry a third of the MFMAs)
@@ -661,12 +661,20 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
   const int64_t pos0 = (grp * W + wave) * 32;        // first position of this wave
   // waves past the end still take part in every barrier (zero rows)
   const int rows = (int)max<int64_t>(0, min<int64_t>(32, total - pos0));
+  // scap > 0: list / cand appends go to this group's shard (kmeans_i8.hpp)
+  const unsigned shard = (unsigned)((grp * W + wave) % kShards);
+  int32_t* const listS = scap ? list + (size_t)shard * scap : list;
+  unsigned int* const listCountS = scap ? listCount + shard * kShardStride : listCount;
+  int32_t* const candRowsS = scap && candRows ? candRows + (size_t)shard * scap : candRows;
+  int32_t* const candsS = scap && cands ? cands + (size_t)shard * scap * CMAX : cands;
+  unsigned int* const candCountS =
+      scap && candCount ? candCount + shard * kShardStride : candCount;
   auto rowAt = [&](int i) -> int64_t {   // global row of position pos0 + i (i < rows)
     if constexpr (LIST) return rowsIn[pos0 + i];
     else return pos0 + i;
   };
   if (!P.ok) {   // uniform over the grid
-    if (lane < rows) list[atomicAdd(listCount, 1u)] = (int32_t)rowAt(lane);
+    if (lane < rows) listS[atomicAdd(listCountS, 1u)] = (int32_t)rowAt(lane);
     return;
   }
   // tile t -> slot t % 3: each wave DMAs fragments wave, wave + W, ... and the
@@ -779,10 +787,13 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
   const int IB = 32 - __builtin_clz((unsigned)max(ktp - 1, 1));
   const unsigned IM = (1u << IB) - 1u;
   // LIMBS = 2, after the tile's MFMAs: acc[1] started at -Q
+  int vzero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
   auto epi2 = [&](int ct, const v16i (&acc)[LIMBS]) {
-    // ct in a VGPR: one v_and_or_b32 may read only one SGPR (the mask)
-    unsigned ctv;
-    asm("v_mov_b32 %0, %1" : "=v"(ctv) : "s"(ct));
+    // ct in a VGPR (one v_and_or_b32 may read only one SGPR, the mask), by
+    // a VALU add to an opaque zero: no inline asm in the loop, which would
+    // split its scheduling region
+    const unsigned ctv = (unsigned)(vzero + ct);
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       // T - Q (LIMBS = 1: acc[0] started at -Q)
@@ -828,6 +839,22 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
   // this form at 168 VGPRs and three waves per SIMD)
   int sl = 0;
   if constexpr (PAIR) {
+    // software-pipelined by hand: each gap between two MFMAs of one tile
+    // carries the epilogue of 16 / S rows of the tile before (tile 2 st - 1's
+    // beside 2 st's, across the barrier) and the B fragment of the next MFMA;
+    // sched_barrier pins that order.  X1 starts as INT_MIN rows of tile 0:
+    // an epilogue that changes no sV.
+    auto epi_reg = [&](int reg, unsigned ctv, int V) {
+      const int Ve = (int)(((unsigned)V & ~IM) | ctv);
+      sV2[reg] = max(min(sV1[reg], sV2[reg]), min(max(sV1[reg], sV2[reg]), Ve));
+      sV1[reg] = max(sV1[reg], Ve);
+    };
+    constexpr int RPG = 16 / S;   // accumulator rows per MFMA gap
+    static_assert(16 % S == 0, "the gaps split the 16 rows evenly");
+    v16i X0, X1;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) X1[reg] = INT_MIN;
+    int prev = 0;
     for (int st = 0; st < nsteps; ++st) {
       arrive(st, sl);
       // -Q per row of each half (see below); tiles 2 st and 2 st + 1
@@ -838,23 +865,38 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
         qbad |= pf < -0x1p30f;
         nb[hf] = -(int)__builtin_floorf(__builtin_fminf(pf, 0x1p30f));
       }
-      v16i X0[1], X1[1];
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        X0[0][reg] = nb[0] >> sh[reg];
-        X1[0][reg] = nb[1] >> sh[reg];
-      }
       const v4i* B = (const v4i*)(lds + sl * TB) + lane;
 #pragma unroll
+      for (int reg = 0; reg < 16; ++reg) X0[reg] = nb[0] >> sh[reg];
+      const unsigned ct1 = (unsigned)(vzero + prev), ct0 = (unsigned)(vzero + 2 * st);
+      v4i Bn = B[0];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
       for (int s = 0; s < S; ++s) {
-        const v4i B0 = B[s * 64], B1 = B[(S + s) * 64];
-        X0[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B0, X0[0], 0, 0, 0);
-        X1[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B1, X1[0], 0, 0, 0);
+        const v4i Bc = Bn;
+        Bn = B[(s + 1) * 64];   // s = S - 1: tile 2 st + 1's first fragment
+        X0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], Bc, X0, 0, 0, 0);
+#pragma unroll
+        for (int q = RPG * s; q < RPG * (s + 1); ++q) epi_reg(q, ct1, X1[q]);
+#pragma unroll
+        for (int q = RPG * s; q < RPG * (s + 1); ++q) X1[q] = nb[1] >> sh[q];
+        __builtin_amdgcn_sched_barrier(0);
       }
-      epi2(2 * st, X0);
-      epi2(2 * st + 1, X1);
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const v4i Bc = Bn;
+        if (s + 1 < S) Bn = B[(S + s + 1) * 64];
+        X1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], Bc, X1, 0, 0, 0);
+#pragma unroll
+        for (int q = RPG * s; q < RPG * (s + 1); ++q) epi_reg(q, ct0, X0[q]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      prev = 2 * st + 1;
       sl = next_slot(sl);
     }
+    const unsigned ct1 = (unsigned)(vzero + prev);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) epi_reg(reg, ct1, X1[reg]);
   }
   for (int ct = 0; ct < (PAIR ? 0 : ktp); ++ct) {
     v16i X[LIMBS];
@@ -1006,10 +1048,10 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
         want = true;
         thrV = (int)tv;
       } else {
-        list[atomicAdd(listCount, 1u)] = (int32_t)grow;
+        listS[atomicAdd(listCountS, 1u)] = (int32_t)grow;
       }
     } else {
-      list[atomicAdd(listCount, 1u)] = (int32_t)grow;
+      listS[atomicAdd(listCountS, 1u)] = (int32_t)grow;
     }
   }
   if constexpr (LIMBS < 3) {
@@ -1053,12 +1095,12 @@ __global__ __launch_bounds__(64 * W, (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
         const int* cs = candS + lane * (CMAX + 1);
         const int cnt = cs[0];
         if (cnt >= 1 && cnt <= CMAX) {
-          const unsigned idx = atomicAdd(candCount, 1u);
-          candRows[idx] = (int32_t)grow;
+          const unsigned idx = atomicAdd(candCountS, 1u);
+          candRowsS[idx] = (int32_t)grow;
 #pragma unroll
-          for (int i = 0; i < CMAX; ++i) cands[(size_t)idx * CMAX + i] = i < cnt ? cs[1 + i] : -1;
+          for (int i = 0; i < CMAX; ++i) candsS[(size_t)idx * CMAX + i] = i < cnt ? cs[1 + i] : -1;
         } else {
-          list[atomicAdd(listCount, 1u)] = (int32_t)grow;
+          listS[atomicAdd(listCountS, 1u)] = (int32_t)grow;
         }
       }
     }
@@ -1076,14 +1118,15 @@ int launch_screen32(const void* img, const int2* meta, const double* xnorm, int6
                     const CenterParams* prm, int ktp, const int32_t* rowsIn,
                     const unsigned int* rowsInCount, int32_t* assign, int32_t* list,
                     unsigned int* listCount, hipStream_t st, int32_t* candRows = nullptr,
-                    int32_t* cands = nullptr, unsigned int* candCount = nullptr) {
+                    int32_t* cands = nullptr, unsigned int* candCount = nullptr,
+                    unsigned int scap = 0) {
   KernelTimer timer(LIMBS == 1 ? "k_kmeans_screen1" : LIMBS == 2 ? "k_kmeans_screen2"
                                                     : "k_kmeans_screen3", st);
   const int64_t wg = (n + 32 * W - 1) / (32 * W);   // W waves x 32 rows
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32<S, W, LIMBS, LIST>), dim3((unsigned)wg),
                      dim3(64 * W), 0, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
                      cq, g, cnorm, prm, ktp, rowsIn, rowsInCount, assign, list, listCount,
-                     candRows, cands, candCount);
+                     candRows, cands, candCount, scap);
   CYC_LAUNCH_CHECK("k_kmeans_screen32_i8");
   return CYC_OK;
 }
@@ -1120,7 +1163,7 @@ __global__ __launch_bounds__(256, 2) void k_screen32r(
     int32_t* __restrict__ assign, int32_t* __restrict__ list, unsigned int* __restrict__ listCount,
     int32_t* __restrict__ candRows, int32_t* __restrict__ cands,
     unsigned int* __restrict__ candCount, int32_t* __restrict__ fullList,
-    unsigned int* __restrict__ fullCount, unsigned int* __restrict__ stat) {
+    unsigned int* __restrict__ fullCount, unsigned int* __restrict__ stat, unsigned int scap) {
   constexpr int D = 32 * S, CH = 3 * D / 16;
   constexpr int W = 4;
   // per wave: the candidate list, then the candidate-set scratch (the union
@@ -1139,6 +1182,20 @@ __global__ __launch_bounds__(256, 2) void k_screen32r(
   if (rows == 0) return;
   const bool rowOk = r < rows;
   const int64_t myRow = rowOk ? rowsIn[pos0 + r] : 0;
+  // scap > 0: appends (and the stat adds) go to this wave's shard
+  const unsigned shard = (unsigned)((blockIdx.x * W + wave) % kShards);
+  if (scap) {
+    list += (size_t)shard * scap;
+    listCount += shard * kShardStride;
+    fullList += (size_t)shard * scap;
+    fullCount += shard * kShardStride;
+    if (candRows) {
+      candRows += (size_t)shard * scap;
+      cands += (size_t)shard * scap * kCandMax;
+      candCount += shard * kShardStride;
+    }
+    if (stat) stat += shard * kShardStride;
+  }
   auto to_full = [&]() {
     if (lane < rows) fullList[atomicAdd(fullCount, 1u)] = (int32_t)myRow;
   };
@@ -1447,13 +1504,17 @@ __global__ __launch_bounds__(256) void k_screen_cands(
     const double* __restrict__ C, const double* __restrict__ cnorm, int k, bool unit,
     double margin, const int32_t* __restrict__ candRows, const int32_t* __restrict__ cands,
     const unsigned int* __restrict__ candCount, int32_t* __restrict__ assign,
-    int32_t* __restrict__ list, unsigned int* __restrict__ listCount) {
+    int32_t* __restrict__ list, unsigned int* __restrict__ listCount, unsigned int scap) {
   // 4 rows per wave, 16 lanes per row; lane s of a row holds the dimensions
   // s, s + 16, ... (each load instruction reads one 128-byte line per row)
   const unsigned cnt = *candCount;
   const int lane = threadIdx.x & 63, q = lane >> 4, sl = lane & 15;
   const unsigned nw = (gridDim.x * blockDim.x) >> 6;
   const unsigned w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (scap) {   // this wave's shard (<= 4 rows per grid stride: shard_cap)
+    list += (size_t)(w0 % kShards) * scap;
+    listCount += (w0 % kShards) * kShardStride;
+  }
   for (unsigned base = w0 * 4; base < cnt; base += nw * 4) {
     const unsigned idx = base + q;
     const bool live = idx < cnt;
@@ -1539,38 +1600,120 @@ __global__ __launch_bounds__(256) void k_screen_cands(
 }
 
 int launch_cands(const CandArgs& ca, int64_t n, int d, int32_t* assign, int32_t* list,
-                 unsigned int* listCount, hipStream_t st) {
+                 unsigned int* listCount, hipStream_t st, unsigned int scap = 0) {
   KernelTimer timer("k_kmeans_cands", st);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 127) / 128, 4096));
   hipLaunchKernelGGL(k_screen_cands, dim3(grid), dim3(256), 0, st, ca.X, ca.xnorm, d, ca.C,
                      ca.cnorm, ca.k, ca.unit, ca.margin, (const int32_t*)ca.candRows, (const int32_t*)ca.cands,
-                     (const unsigned int*)ca.candCount, assign, list, listCount);
+                     (const unsigned int*)ca.candCount, assign, list, listCount, scap);
   CYC_LAUNCH_CHECK("k_screen_cands");
+  return CYC_OK;
+}
+
+// Sharded appends, compacted (kmeans_i8.hpp): one wave scans the kShards
+// counters into bases behind *dstCount (and clears them), then a grid copies
+// each shard's entries to its base.
+__global__ __launch_bounds__(64) void k_shard_scan(unsigned int* __restrict__ counts,
+                                                   unsigned int* __restrict__ dstCount) {
+  const int j = threadIdx.x;
+  const unsigned c = counts[j * kShardStride];
+  unsigned incl = c;
+#pragma unroll
+  for (int m = 1; m < kShards; m <<= 1) {
+    const unsigned o = __shfl_up(incl, m);
+    if (j >= m) incl += o;
+  }
+  const unsigned old = *dstCount;   // read by every lane before lane 63's store
+  counts[j * kShardStride] = 0u;
+  counts[j * kShardStride + 1] = old + incl - c;
+  counts[j * kShardStride + 2] = c;
+  if (j == kShards - 1) *dstCount = old + incl;
+}
+
+__global__ __launch_bounds__(256) void k_shard_copy(const unsigned int* __restrict__ counts,
+                                                    unsigned int cap,
+                                                    const int32_t* __restrict__ src,
+                                                    int32_t* __restrict__ dst, int width,
+                                                    const int32_t* __restrict__ src2,
+                                                    int32_t* __restrict__ dst2, int width2) {
+  const int j = blockIdx.y;
+  const size_t base = counts[j * kShardStride + 1], c = counts[j * kShardStride + 2];
+  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  {
+    const int32_t* s1 = src + (size_t)j * cap * width;
+    int32_t* d1 = dst + base * width;
+    for (size_t i = t0; i < c * width; i += stride) d1[i] = s1[i];
+  }
+  if (src2) {
+    const int32_t* s2 = src2 + (size_t)j * cap * width2;
+    int32_t* d2 = dst2 + base * width2;
+    for (size_t i = t0; i < c * width2; i += stride) d2[i] = s2[i];
+  }
+}
+
+int compact(unsigned int* counts, unsigned int cap, const int32_t* src, int32_t* dst, int width,
+            const int32_t* src2, int32_t* dst2, int width2, unsigned int* dstCount,
+            hipStream_t st) {
+  KernelTimer timer("k_kmeans_compact", st);
+  hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kShards), 0, st, counts, dstCount);
+  CYC_LAUNCH_CHECK("k_shard_scan");
+  if (dst) {
+    hipLaunchKernelGGL(k_shard_copy, dim3(16, kShards), dim3(256), 0, st,
+                       (const unsigned int*)counts, cap, src, dst, width, src2, dst2, width2);
+    CYC_LAUNCH_CHECK("k_shard_copy");
+  }
   return CYC_OK;
 }
 
 // Two-limb pass over every row; its undecided rows with a small candidate
 // set get exact fp64 distances to those candidates (k_screen_cands), the
-// others the three-limb pass.
+// others the three-limb pass.  With `stg` (and ca) every 32x32 kernel
+// appends through its shards, compacted after each launch.
 template <int S, int W>
 int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
              const void* Cb, const float* cq, const double* g, const double* cnorm,
              const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
              unsigned int* listCount, int32_t* list2, unsigned int* list2Count,
-             const CandArgs* ca, hipStream_t st, const RefineArgs* ra = nullptr) {
+             const CandArgs* ca, hipStream_t st, const RefineArgs* ra = nullptr,
+             const AppendStage* stg = nullptr) {
   CYC_HIP(hipMemsetAsync(list2Count, 0, sizeof(unsigned int), st));
   if (ca) CYC_HIP(hipMemsetAsync(ca->candCount, 0, sizeof(unsigned int), st));
+  const AppendStage* sg = ca ? stg : nullptr;
+  const unsigned scap = sg ? sg->cap : 0u;
+  if (sg)
+    CYC_HIP(hipMemsetAsync(sg->counts, 0,
+                           sizeof(unsigned int) * kSets * kShards * kShardStride, st));
+  // append targets: the stage's shards, or the lists themselves
+  auto A = [&](int32_t* staged, int32_t* direct) { return sg ? staged : direct; };
+  auto N = [&](int set, unsigned int* direct) { return sg ? sg->set(set) : direct; };
   int rc;
+  // the two-limb kernels' outputs: list2 (rows) and the candidate lists
+  auto compact2 = [&]() -> int {
+    if (!sg) return CYC_OK;
+    int e;
+    if ((e = compact(sg->set(kSetRowsA), scap, sg->rowsA, list2, 1, nullptr, nullptr, 0,
+                     list2Count, st)))
+      return e;
+    return compact(sg->set(kSetCand), scap, sg->candRows, ca->candRows, 1, sg->cands, ca->cands,
+                   kCandMax, ca->candCount, st);
+  };
   if (ra && ca) {
     // one-limb pass over every center; the two-limb refinement over the
     // union of the listed rows' candidates; the full two-limb pass over the
     // rows neither can handle (fullList)
     CYC_HIP(hipMemsetAsync(ra->cand1Count, 0, sizeof(unsigned int), st));
     CYC_HIP(hipMemsetAsync(ra->fullCount, 0, 2 * sizeof(unsigned int), st));
-    if ((rc = launch_screen32<S, W, 1, false>(img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 64,
-                                              g + (size_t)ktp * 64, cnorm, prm, ktp, nullptr,
-                                              nullptr, assign, ra->fullList, ra->fullCount, st,
-                                              ra->cand1Rows, ra->cand1, ra->cand1Count)))
+    if ((rc = launch_screen32<S, W, 1, false>(
+             img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 64, g + (size_t)ktp * 64, cnorm, prm,
+             ktp, nullptr, nullptr, assign, A(sg ? sg->rowsA : nullptr, ra->fullList),
+             N(kSetRowsA, ra->fullCount), st, A(sg ? sg->candRows : nullptr, ra->cand1Rows),
+             A(sg ? sg->cands : nullptr, ra->cand1), N(kSetCand, ra->cand1Count), scap)))
+      return rc;
+    if (sg && ((rc = compact(sg->set(kSetRowsA), scap, sg->rowsA, ra->fullList, 1, nullptr,
+                             nullptr, 0, ra->fullCount, st)) ||
+               (rc = compact(sg->set(kSetCand), scap, sg->candRows, ra->cand1Rows, 1, sg->cands,
+                             ra->cand1, kCand1, ra->cand1Count, st))))
       return rc;
     {
       KernelTimer timer("k_kmeans_refine2", st);
@@ -1578,31 +1721,42 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
                          dim3(256), 0, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
                          cq + (size_t)ktp * 32, g + (size_t)ktp * 32, cnorm, prm, ra->kstride,
                          (const int32_t*)ra->cand1Rows, (const unsigned int*)ra->cand1Count,
-                         (const int32_t*)ra->cand1, assign, list2, list2Count, ca->candRows,
-                         ca->cands, ca->candCount, ra->fullList, ra->fullCount,
-                         ra->fullCount + 1);
+                         (const int32_t*)ra->cand1, assign, A(sg ? sg->rowsA : nullptr, list2),
+                         N(kSetRowsA, list2Count), A(sg ? sg->candRows : nullptr, ca->candRows),
+                         A(sg ? sg->cands : nullptr, ca->cands), N(kSetCand, ca->candCount),
+                         A(sg ? sg->rowsB : nullptr, ra->fullList), N(kSetRowsB, ra->fullCount),
+                         N(kSetStat, ra->fullCount + 1), scap);
       CYC_LAUNCH_CHECK("k_screen32r");
     }
-    rc = launch_screen32<S, W, 2, true>(img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 32,
-                                        g + (size_t)ktp * 32, cnorm, prm, ktp, ra->fullList,
-                                        ra->fullCount, assign, list2, list2Count, st,
-                                        ca->candRows, ca->cands, ca->candCount);
+    if (sg && ((rc = compact2()) ||
+               (rc = compact(sg->set(kSetRowsB), scap, sg->rowsB, ra->fullList, 1, nullptr,
+                             nullptr, 0, ra->fullCount, st)) ||
+               (rc = compact(sg->set(kSetStat), scap, nullptr, nullptr, 0, nullptr, nullptr, 0,
+                             ra->fullCount + 1, st))))
+      return rc;
+    rc = launch_screen32<S, W, 2, true>(
+        img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 32, g + (size_t)ktp * 32, cnorm, prm, ktp,
+        ra->fullList, ra->fullCount, assign, A(sg ? sg->rowsA : nullptr, list2),
+        N(kSetRowsA, list2Count), st, A(sg ? sg->candRows : nullptr, ca->candRows),
+        A(sg ? sg->cands : nullptr, ca->cands), N(kSetCand, ca->candCount), scap);
   } else {
-    rc = launch_screen32<S, W, 2, false>(img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 32,
-                                         g + (size_t)ktp * 32, cnorm, prm, ktp, nullptr,
-                                         nullptr, assign, list2, list2Count, st,
-                                         ca ? ca->candRows : nullptr, ca ? ca->cands : nullptr,
-                                         ca ? ca->candCount : nullptr);
+    rc = launch_screen32<S, W, 2, false>(
+        img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 32, g + (size_t)ktp * 32, cnorm, prm, ktp,
+        nullptr, nullptr, assign, A(sg ? sg->rowsA : nullptr, list2), N(kSetRowsA, list2Count),
+        st, ca ? A(sg ? sg->candRows : nullptr, ca->candRows) : nullptr,
+        ca ? A(sg ? sg->cands : nullptr, ca->cands) : nullptr,
+        ca ? N(kSetCand, ca->candCount) : nullptr, scap);
   }
-  if (rc) return rc;
+  if (rc || (rc = compact2())) return rc;
   if (!ca)
     return launch_screen32<S, W, 3, true>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp,
                                           list2, list2Count, assign, list, listCount, st);
   // the three-limb pass (rows with more than kCandMax candidates) and the
-  // candidate pass touch disjoint rows and only append to `list`: the
-  // three-limb pass runs on a side stream of this host thread beside it
-  // (one per device: a host thread may drive plans on several GPUs; the
-  // caller's DeviceGuard made `st`'s device current)
+  // candidate pass touch disjoint rows and only append to `list` (through
+  // two separate shard sets with a stage): the three-limb pass runs on a
+  // side stream of this host thread beside it (one per device: a host
+  // thread may drive plans on several GPUs; the caller's DeviceGuard made
+  // `st`'s device current)
   constexpr int kMaxDev = 64;
   thread_local hipStream_t sides[kMaxDev] = {};
   thread_local hipEvent_t forks[kMaxDev] = {}, joins[kMaxDev] = {};
@@ -1622,12 +1776,22 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
   CYC_HIP(hipEventRecord(fork, st));
   CYC_HIP(hipStreamWaitEvent(side, fork, 0));
   if ((rc = launch_screen32<S, W, 3, true>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp,
-                                           list2, list2Count, assign, list, listCount, side)))
+                                           list2, list2Count, assign,
+                                           A(sg ? sg->rowsA : nullptr, list),
+                                           N(kSetRowsA, listCount), side, nullptr, nullptr,
+                                           nullptr, scap)))
     return rc;
-  rc = launch_cands(*ca, n, d, assign, list, listCount, st);
+  rc = launch_cands(*ca, n, d, assign, A(sg ? sg->rowsB : nullptr, list), N(kSetRowsB, listCount),
+                    st, scap);
   CYC_HIP(hipEventRecord(join, side));
   CYC_HIP(hipStreamWaitEvent(st, join, 0));
-  return rc;
+  if (rc) return rc;
+  if (sg && ((rc = compact(sg->set(kSetRowsA), scap, sg->rowsA, list, 1, nullptr, nullptr, 0,
+                           listCount, st)) ||
+             (rc = compact(sg->set(kSetRowsB), scap, sg->rowsB, list, 1, nullptr, nullptr, 0,
+                           listCount, st))))
+    return rc;
+  return CYC_OK;
 }
 
 template <int KS>
@@ -1699,13 +1863,17 @@ int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, in
            const void* Cb, const float* cq, const double* g, const double* cnorm,
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
            unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st,
-           const CandArgs* ca, const RefineArgs* ra) {
+           const CandArgs* ca, const RefineArgs* ra, const AppendStage* stg) {
   if (n <= 0) return CYC_OK;
+  if (stg && stg->cap < shard_cap(n)) {
+    set_error("append stage smaller than shard_cap(n)");
+    return CYC_ERR_INVALID_ARG;
+  }
   if (uses32(d)) {
     const int k32 = ktp * 16 / 32;   // launch over the padded center range (cq = +inf)
     switch (ksteps(d)) {
-      case 2: return screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st, ra);
-      default: return screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st, ra);
+      case 2: return screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st, ra, stg);
+      default: return screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st, ra, stg);
     }
   }
   switch (ksteps(d)) {

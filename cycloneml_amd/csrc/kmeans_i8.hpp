@@ -92,16 +92,50 @@ struct RefineArgs {
   unsigned int* fullCount;
 };
 
+// Sharded appends.  A returning atomicAdd on ONE counter serialises at
+// ~11 ns per wave-aggregated add across the chip (tools/atomic_probe.hip:
+// 125k waves, one add each, 1.42 ms; 0.03 ms over 64 counters 256 B apart),
+// which made every list-producing screen kernel counter-bound.  So the
+// screen kernels append into kShards shards (one counter each; a wave's
+// 32-row group picks shard group % kShards, so a shard holds at most `cap`
+// entries), and compact() then moves the shards behind the list's current
+// count in two small launches.  Lists keep no order either way (the atomic
+// order was arbitrary too): nothing downstream depends on it.
+constexpr int kShards = 64;
+constexpr int kShardStride = 64;   // unsigned ints between two shard counters
+enum { kSetRowsA = 0, kSetRowsB = 1, kSetCand = 2, kSetStat = 3, kSets = 4 };
+struct AppendStage {
+  int32_t* rowsA;       // kShards x cap row indices
+  int32_t* rowsB;       // kShards x cap
+  int32_t* candRows;    // kShards x cap
+  int32_t* cands;       // kShards x cap x kCand1
+  unsigned int* counts; // kSets x kShards x kShardStride, zero between uses
+  unsigned int cap;     // entries per shard
+  unsigned int* set(int s) const { return counts + (size_t)s * kShards * kShardStride; }
+};
+// entries per shard for kernels over at most n rows (32-row groups, or the
+// candidate pass's grid-stride 4-row groups of <= 16384 waves)
+inline unsigned int shard_cap(int64_t n) {
+  return (unsigned int)((n + 32 * kShards - 1) / (32 * kShards) * 32 + 2048);
+}
+// Append the shards of count set `counts` (width-wide entries of src, and of
+// src2 when given) behind *dstCount in dst (dst2); the shard counters are
+// left zero.  dst == nullptr: only add the counters' total to *dstCount.
+int compact(unsigned int* counts, unsigned int cap, const int32_t* src, int32_t* dst, int width,
+            const int32_t* src2, int32_t* dst2, int width2, unsigned int* dstCount,
+            hipStream_t st);
+
 // Screen every row: certified rows get assign[row]; the others are appended
 // to list (listCount is NOT cleared here).  list2 / list2Count (n entries +
 // one counter): scratch for the rows the 32x32 two-limb pass leaves.
-// ca (d <= 256, optional): the candidate pass.
+// ca (d <= 256, optional): the candidate pass.  stg (optional, with ca; cap
+// >= shard_cap(n)): the 32x32 kernels append through it.
 int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
            const void* Cb, const float* cq, const double* g, const double* cnorm,
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
            unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st,
            const CandArgs* ca = nullptr,
-           const RefineArgs* ra = nullptr);
+           const RefineArgs* ra = nullptr, const AppendStage* stg = nullptr);
 
 }  // namespace km8
 }  // namespace cyc
