@@ -50,6 +50,10 @@ SIGNATURES = {
     "cyc_kmeans_plan_create": (ctypes.c_int, [_i32, _i32, _i64, ctypes.POINTER(_vp)]),
     "cyc_kmeans_plan_destroy": (ctypes.c_int, [_vp]),
     "cyc_kmeans_plan_set_distance_measure": (ctypes.c_int, [_vp, _i32]),
+    "cyc_kmeans_silhouette_stats_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                                       _vp]),
+    "cyc_kmeans_silhouette_score_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                                       _vp, _vp]),
     "cyc_kmeans_stats_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     "cyc_kmeans_assign_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
                                              _pi64, _vp]),

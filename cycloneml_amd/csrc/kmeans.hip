@@ -37,6 +37,7 @@
 #include "kmeans_i8.hpp"
 #include "kmeans_cos.hpp"
 #include "kmeans_sparse.hpp"
+#include "silhouette.hpp"
 
 namespace {
 
@@ -1759,6 +1760,9 @@ struct cyc_kmeans_plan_s {
   // require(norm1 >= 0.0 && norm2 >= 0.0) check (k_require_norms): device
   // result, its pinned host copy and the event that marks the copy landed
   cyc::DeviceBuffer req;
+  // ClusteringEvaluator's Silhouette (silhouette.hpp): check flags, row
+  // norms, per-block score partials
+  cyc::DeviceBuffer silFlags, silNorms, silPart;
   unsigned long long* reqHost = nullptr;
   hipEvent_t reqEv = nullptr;
   ~cyc_kmeans_plan_s() {
@@ -2188,6 +2192,57 @@ int cos_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmea
 
 }  // namespace
 
+namespace {
+
+// Counting sort of rows 0..n by assign[] into the plan's perm (stable: row
+// order kept within a cluster), with cstart (k + 1 cluster offsets) and
+// chunkStart (k + 1 offsets of kChunkRows-row chunks); part / pw / pc
+// reserved for maxChunks chunks of d columns.
+int sort_clusters(cyc_kmeans_plan p, const int32_t* assign, int64_t n, int d, hipStream_t st,
+                  int64_t& maxChunks) {
+  const int k = p->k;
+  int rc;
+  const int tiles = (int)((n + kSortTile - 1) / kSortTile);
+  maxChunks = (n + kChunkRows - 1) / kChunkRows + k;
+  if ((rc = p->hist.reserve(sizeof(int32_t) * (size_t)tiles * k)) ||
+      (rc = p->total.reserve(sizeof(int64_t) * (size_t)k)) ||
+      (rc = p->cstart.reserve(sizeof(int64_t) * (size_t)(k + 1))) ||
+      (rc = p->chunkStart.reserve(sizeof(int64_t) * (size_t)(k + 1))) ||
+      (rc = p->perm.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = p->part.reserve(sizeof(double) * (size_t)maxChunks * d)) ||
+      (rc = p->pw.reserve(sizeof(double) * (size_t)maxChunks)) ||
+      (rc = p->pc.reserve(sizeof(double) * (size_t)maxChunks)) ||
+      (rc = p->ccost.reserve(sizeof(double) * (size_t)k)))
+    return rc;
+  int32_t* hist = (int32_t*)p->hist.ptr;
+  hipLaunchKernelGGL(k_hist, dim3(tiles), dim3(256), sizeof(int32_t) * k, st, assign, n, k, hist);
+  CYC_LAUNCH_CHECK("k_hist");
+  {
+    const int segT = (tiles + std::min(kScanSegs, tiles) - 1) / std::min(kScanSegs, tiles);
+    const int segs = (tiles + segT - 1) / segT;
+    if ((rc = p->segsum.reserve(sizeof(int32_t) * (size_t)segs * k))) return rc;
+    int32_t* segsum = (int32_t*)p->segsum.ptr;
+    hipLaunchKernelGGL(k_scan_seg, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0, st,
+                       (const int32_t*)hist, tiles, k, segT, segsum);
+    CYC_LAUNCH_CHECK("k_scan_seg");
+    hipLaunchKernelGGL(k_scan_segoff, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, st, segsum,
+                       segs, k, (int64_t*)p->total.ptr);
+    CYC_LAUNCH_CHECK("k_scan_segoff");
+    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0,
+                       st, hist, tiles, k, segT, (const int32_t*)segsum);
+    CYC_LAUNCH_CHECK("k_scan_apply");
+  }
+  hipLaunchKernelGGL(k_scan_clusters, dim3(1), dim3(1024), 0, st, (const int64_t*)p->total.ptr, k,
+                     (int64_t*)p->cstart.ptr, (int64_t*)p->chunkStart.ptr);
+  CYC_LAUNCH_CHECK("k_scan_clusters");
+  hipLaunchKernelGGL(k_scatter, dim3(tiles), dim3(64), sizeof(int64_t) * k, st, assign, n, k,
+                     hist, (const int64_t*)p->cstart.ptr, (int32_t*)p->perm.ptr);
+  CYC_LAUNCH_CHECK("k_scatter");
+  return CYC_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int cyc_row_norms_dev(const double* X, int64_t n, int32_t d, double* norms, void* stream) {
@@ -2557,42 +2612,8 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
     CYC_LAUNCH_CHECK("k_row_cost");
   }
 
-  const int tiles = (int)((n + kSortTile - 1) / kSortTile);
-  const int64_t maxChunks = (n + kChunkRows - 1) / kChunkRows + k;
-  if ((rc = p->hist.reserve(sizeof(int32_t) * (size_t)tiles * k)) ||
-      (rc = p->total.reserve(sizeof(int64_t) * (size_t)k)) ||
-      (rc = p->cstart.reserve(sizeof(int64_t) * (size_t)(k + 1))) ||
-      (rc = p->chunkStart.reserve(sizeof(int64_t) * (size_t)(k + 1))) ||
-      (rc = p->perm.reserve(sizeof(int32_t) * (size_t)n)) ||
-      (rc = p->part.reserve(sizeof(double) * (size_t)maxChunks * d)) ||
-      (rc = p->pw.reserve(sizeof(double) * (size_t)maxChunks)) ||
-      (rc = p->pc.reserve(sizeof(double) * (size_t)maxChunks)) ||
-      (rc = p->ccost.reserve(sizeof(double) * (size_t)k)))
-    return rc;
-  int32_t* hist = (int32_t*)p->hist.ptr;
-  hipLaunchKernelGGL(k_hist, dim3(tiles), dim3(256), sizeof(int32_t) * k, st, assign, n, k, hist);
-  CYC_LAUNCH_CHECK("k_hist");
-  {
-    const int segT = (tiles + std::min(kScanSegs, tiles) - 1) / std::min(kScanSegs, tiles);
-    const int segs = (tiles + segT - 1) / segT;
-    if ((rc = p->segsum.reserve(sizeof(int32_t) * (size_t)segs * k))) return rc;
-    int32_t* segsum = (int32_t*)p->segsum.ptr;
-    hipLaunchKernelGGL(k_scan_seg, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0, st,
-                       (const int32_t*)hist, tiles, k, segT, segsum);
-    CYC_LAUNCH_CHECK("k_scan_seg");
-    hipLaunchKernelGGL(k_scan_segoff, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, st, segsum,
-                       segs, k, (int64_t*)p->total.ptr);
-    CYC_LAUNCH_CHECK("k_scan_segoff");
-    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0,
-                       st, hist, tiles, k, segT, (const int32_t*)segsum);
-    CYC_LAUNCH_CHECK("k_scan_apply");
-  }
-  hipLaunchKernelGGL(k_scan_clusters, dim3(1), dim3(1024), 0, st, (const int64_t*)p->total.ptr, k,
-                     (int64_t*)p->cstart.ptr, (int64_t*)p->chunkStart.ptr);
-  CYC_LAUNCH_CHECK("k_scan_clusters");
-  hipLaunchKernelGGL(k_scatter, dim3(tiles), dim3(64), sizeof(int64_t) * k, st, assign, n, k,
-                     hist, (const int64_t*)p->cstart.ptr, (int32_t*)p->perm.ptr);
-  CYC_LAUNCH_CHECK("k_scatter");
+  int64_t maxChunks = 0;
+  if ((rc = sort_clusters(p, assign, n, d, st, maxChunks))) return rc;
   // Number of chunks is data dependent; launch the upper bound and let the
   // surplus blocks (ch >= chunkStart[k]) exit.
   if (cosm) {
@@ -2655,6 +2676,118 @@ int cyc_kmeans_update_dev(cyc_kmeans_plan p, double* C, double* cnorm, const dou
                      epsilon * epsilon, converged_out);
   CYC_LAUNCH_CHECK("k_update_centers");
   return CYC_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// ClusteringEvaluator's Silhouette (ml/evaluation/ClusteringMetrics.scala,
+// silhouette.hpp): the plan's measure picks SquaredEuclideanSilhouette
+// (CYC_DISTANCE_EUCLIDEAN) or CosineSilhouette.
+// ---------------------------------------------------------------------------
+namespace {
+
+// pred in [0, k) and checkNonNegativeWeight over the rows (host sync).
+int sil_check(cyc_kmeans_plan p, const int32_t* pred, const double* w, int64_t n,
+              hipStream_t st) {
+  int rc;
+  if ((rc = p->silFlags.reserve(16))) return rc;
+  unsigned int* bad = (unsigned int*)p->silFlags.ptr;
+  unsigned long long* badW = (unsigned long long*)((char*)p->silFlags.ptr + 8);
+  CYC_HIP(hipMemsetAsync(bad, 0, 8, st));
+  CYC_HIP(hipMemsetAsync(badW, 0xff, 8, st));
+  if ((rc = cyc::silh::check_pred(pred, w, n, p->k, bad, badW, st))) return rc;
+  unsigned long long h[2] = {0, 0};
+  CYC_HIP(hipMemcpyAsync(h, p->silFlags.ptr, 16, hipMemcpyDeviceToHost, st));
+  CYC_HIP(hipStreamSynchronize(st));
+  if ((unsigned int)h[0] != 0u) {
+    cyc::set_error("requirement failed: predictions must lie in [0, k) for k = " +
+                   std::to_string(p->k));
+    return CYC_ERR_INVALID_ARG;
+  }
+  if (h[1] != ~0ull) {
+    double v = 0.0;
+    CYC_HIP(hipMemcpy(&v, w + h[1], sizeof(double), hipMemcpyDeviceToHost));
+    // ml/functions.scala:91
+    cyc::set_error("requirement failed: illegal weight value: " + cyc::java_double(v) +
+                   ". weight must be >= 0.0.");
+    return CYC_ERR_INVALID_ARG;
+  }
+  return CYC_OK;
+}
+
+// Vectors.norm(features, 2.0) per row (given, or into the plan's buffer).
+int sil_norms(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n, hipStream_t st,
+              const double*& out) {
+  if (xnorm) {
+    out = xnorm;
+    return CYC_OK;
+  }
+  int rc;
+  if ((rc = p->silNorms.reserve(sizeof(double) * (size_t)n))) return rc;
+  if ((rc = cyc_row_norms_dev(X, n, p->d, (double*)p->silNorms.ptr, st))) return rc;
+  out = (const double*)p->silNorms.ptr;
+  return CYC_OK;
+}
+
+}  // namespace
+
+int cyc_kmeans_silhouette_stats_dev(cyc_kmeans_plan p, const double* X, const double* xnorm,
+                                    int64_t n, const int32_t* pred, const double* weights,
+                                    double* stats, void* stream) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  CYC_REQUIRE(stats != nullptr, "stats must not be null");
+  if (n == 0) return CYC_OK;
+  CYC_REQUIRE(X != nullptr && pred != nullptr, "X and pred must not be null");
+  std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  int rc;
+  const double* xn = nullptr;
+  if ((rc = sil_check(p, pred, weights, n, st)) || (rc = sil_norms(p, X, xnorm, n, st, xn)))
+    return rc;
+  int64_t maxChunks = 0;
+  if ((rc = sort_clusters(p, pred, n, p->d, st, maxChunks))) return rc;
+  if ((rc = cyc::silh::chunk_sums(X, p->d, weights, xn, is_cos(p), (const int32_t*)p->perm.ptr,
+                                  (const int64_t*)p->cstart.ptr,
+                                  (const int64_t*)p->chunkStart.ptr, p->k, maxChunks, kChunkRows,
+                                  (double*)p->part.ptr, (double*)p->pw.ptr, (double*)p->pc.ptr,
+                                  st)))
+    return rc;
+  return cyc::silh::fold((const double*)p->part.ptr, (const double*)p->pw.ptr,
+                         (const double*)p->pc.ptr, (const int64_t*)p->cstart.ptr,
+                         (const int64_t*)p->chunkStart.ptr, p->d, p->k, stats, st);
+}
+
+int cyc_kmeans_silhouette_score_dev(cyc_kmeans_plan p, const double* X, const double* xnorm,
+                                    int64_t n, const int32_t* pred, const double* weights,
+                                    const double* stats, double* partial, void* stream) {
+  CYC_REQUIRE(p != nullptr, "plan must not be null");
+  CYC_REQUIRE(n >= 0, "n >= 0");
+  CYC_REQUIRE(stats != nullptr && partial != nullptr, "stats and partial must not be null");
+  std::lock_guard<std::mutex> g(p->mu);
+  hipStream_t st = cyc::as_stream(stream);
+  const int k = p->k, d = p->d;
+  // clustersStatsMap.size > 1 (ClusteringMetrics.scala:391 / :532): the
+  // clusters with rows, over every rank's rows once stats are merged
+  std::vector<double> cnt((size_t)k);
+  CYC_HIP(hipMemcpyAsync(cnt.data(), stats + (int64_t)k * d + 2 * (int64_t)k,
+                         sizeof(double) * (size_t)k, hipMemcpyDeviceToHost, st));
+  CYC_HIP(hipStreamSynchronize(st));
+  int present = 0;
+  for (int c = 0; c < k; ++c) present += cnt[(size_t)c] > 0.0 ? 1 : 0;
+  if (present <= 1) {
+    cyc::set_error("assertion failed: Number of clusters must be greater than one.");
+    return CYC_ERR_ASSERTION;
+  }
+  if (n == 0) return CYC_OK;
+  CYC_REQUIRE(X != nullptr && pred != nullptr, "X and pred must not be null");
+  int rc;
+  const double* xn = nullptr;
+  if ((rc = sil_check(p, pred, weights, n, st)) || (rc = sil_norms(p, X, xnorm, n, st, xn)))
+    return rc;
+  if ((rc = p->silPart.reserve(sizeof(double) * 2 * (size_t)((n + 63) / 64)))) return rc;
+  return cyc::silh::score(X, xn, n, d, pred, weights, k, is_cos(p), stats,
+                          (double*)p->silPart.ptr, partial, st);
 }
 
 

@@ -1,0 +1,132 @@
+"""ClusteringEvaluator / ClusteringMetrics: host-side mirror of
+org.apache.spark.ml.evaluation (ClusteringEvaluator.scala, ClusteringMetrics.scala).
+
+The Silhouette of a clustering (KMeansExample's printed score): the
+per-cluster statistics and every row's coefficient run in libcyclone
+(cyc_kmeans_silhouette_{stats,score}_dev, csrc/silhouette.hip) over rows
+resident in HBM.  With torch.distributed initialised each rank passes its
+own shard; the aggregateByKey merge of computeClusterStats
+(ClusteringMetrics.scala:299-337) and the two sums of overallScore (:101-103)
+are one all-reduce each, as the broadcast of the merged statistics (:393) is
+implicit in every rank holding them.
+"""
+from __future__ import annotations
+
+from . import _native as N
+from . import parallel
+from .clustering import COSINE, EUCLIDEAN, KMeansPlan
+
+
+def _torch():
+    import torch
+    return torch
+
+
+SQUARED_EUCLIDEAN = "squaredEuclidean"
+_EVAL_MEASURES = {SQUARED_EUCLIDEAN.lower(): EUCLIDEAN, COSINE: COSINE}
+
+
+class ClusteringMetrics:
+    """ClusteringMetrics (ClusteringMetrics.scala:34-60) over device rows X
+    (n x d fp64), predictions (n, integer cluster ids in [0, k)) and weights
+    (n fp64 or None: lit(1.0))."""
+
+    def __init__(self, X, predictions, weights=None, k=None):
+        self.X = X
+        self.predictions = predictions
+        self.weights = weights
+        self.k = k
+        self.distanceMeasure = SQUARED_EUCLIDEAN
+
+    def getDistanceMeasure(self) -> str:
+        return self.distanceMeasure
+
+    def setDistanceMeasure(self, value: str):
+        # :41-45: require(equalsIgnoreCase("squaredEuclidean") || ... "cosine")
+        if value.lower() not in _EVAL_MEASURES:
+            raise N.IllegalArgumentException("requirement failed")
+        self.distanceMeasure = value
+        return self
+
+    def silhouette(self, stream=None) -> float:
+        """ClusteringMetrics.silhouette (:48-60): SquaredEuclideanSilhouette
+        or CosineSilhouette .computeSilhouetteScore."""
+        torch = _torch()
+        X = self.X
+        if X.dtype != torch.float64 or not X.is_cuda or X.dim() != 2:
+            raise N.IllegalArgumentException("requirement failed: features must be a device "
+                                             "fp64 matrix (n x d)")
+        n, d = int(X.shape[0]), int(X.shape[1])
+        pred = self.predictions.to(device=X.device, dtype=torch.int32).contiguous()
+        w = None
+        if self.weights is not None:
+            w = self.weights.to(device=X.device, dtype=torch.float64).contiguous()
+        X = X.contiguous()
+        # the cluster ids: at least every predicted id, on every rank
+        k = self.k
+        if k is None:
+            local = int(pred.max().item()) + 1 if n > 0 else 0
+            k = max(parallel.allgather_object(local))
+        k = max(int(k), 1)
+        measure = _EVAL_MEASURES[self.distanceMeasure.lower()]
+        plan = KMeansPlan(d, k, max(n, 1), distanceMeasure=measure)
+        lib = N.load()
+        s = N.stream_handle(stream)
+        stats = torch.zeros(k * d + 3 * k, dtype=torch.float64, device=X.device)
+        N.check(lib.cyc_kmeans_silhouette_stats_dev(plan.handle, N.ptr(X), None, n, N.ptr(pred),
+                                                    N.ptr(w), N.ptr(stats), s))
+        parallel.allreduce_(stats)   # combOp across executors
+        partial = torch.zeros(2, dtype=torch.float64, device=X.device)
+        N.check(lib.cyc_kmeans_silhouette_score_dev(plan.handle, N.ptr(X), None, n, N.ptr(pred),
+                                                    N.ptr(w), N.ptr(stats), N.ptr(partial), s))
+        parallel.allreduce_(partial)
+        total = partial.cpu()
+        plan.close()
+        return float(total[0]) / float(total[1])
+
+
+class ClusteringEvaluator:
+    """ClusteringEvaluator (ClusteringEvaluator.scala): metricName
+    "silhouette", distanceMeasure "squaredEuclidean" (default) or "cosine";
+    evaluate(X, predictions, weights) plays evaluate(dataset) with the
+    features / prediction / weight columns given as device tensors."""
+
+    def __init__(self, distanceMeasure: str = SQUARED_EUCLIDEAN, metricName: str = "silhouette"):
+        self.metricName = metricName
+        self.distanceMeasure = distanceMeasure
+
+    def setDistanceMeasure(self, value: str):
+        # ParamValidators.inArray(Array("squaredEuclidean", "cosine")) (:89-92)
+        if value not in (SQUARED_EUCLIDEAN, COSINE):
+            raise N.IllegalArgumentException(
+                f"ClusteringEvaluator_distanceMeasure parameter distanceMeasure given invalid "
+                f"value {value}.")
+        self.distanceMeasure = value
+        return self
+
+    def getDistanceMeasure(self) -> str:
+        return self.distanceMeasure
+
+    def setMetricName(self, value: str):
+        if value != "silhouette":
+            raise N.IllegalArgumentException(
+                f"ClusteringEvaluator_metricName parameter metricName given invalid value "
+                f"{value}.")
+        self.metricName = value
+        return self
+
+    def isLargerBetter(self) -> bool:
+        return True
+
+    def getMetrics(self, X, predictions, weights=None, k=None) -> ClusteringMetrics:
+        """getMetrics (:125-150)."""
+        m = ClusteringMetrics(X, predictions, weights, k)
+        m.setDistanceMeasure(self.distanceMeasure)
+        return m
+
+    def evaluate(self, X, predictions, weights=None, k=None, stream=None) -> float:
+        """evaluate (:106-115)."""
+        metrics = self.getMetrics(X, predictions, weights, k)
+        if self.metricName == "silhouette":
+            return metrics.silhouette(stream)
+        raise N.IllegalArgumentException(f"No support for metric {self.metricName}")

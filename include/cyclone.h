@@ -170,6 +170,30 @@ int cyc_kmeans_update_dev(cyc_kmeans_plan plan, double* C, double* cnorm, const 
                           const double* wsum, double epsilon, int32_t* converged_out,
                           void* stream);
 
+/* ClusteringEvaluator's Silhouette (ml/evaluation/ClusteringEvaluator.scala
+ * :106-150 -> ClusteringMetrics.silhouette :48-60): the plan's distance
+ * measure selects SquaredEuclideanSilhouette (ClusteringMetrics.scala
+ * :254-400) or CosineSilhouette (:403-600).  Replaces the two Spark jobs of
+ * computeSilhouetteScore: the aggregateByKey of computeClusterStats and the
+ * per-row UDF + overallScore.  Rows X (n x d, plan d) with predictions
+ * pred[n] in [0, plan k), weights (nullable = 1.0, each >= 0: the
+ * checkNonNegativeWeight require, ml/functions.scala:91), xnorm (nullable:
+ * computed) = Vectors.norm(x, 2.0).
+ * _stats_dev ADDS this shard's cluster statistics into the device buffer
+ * stats[k d + 3 k] = [featureSum (k x d) | squaredNormSum (k) | weightSum
+ * (k) | rows (k)] (zero it first; all-reduce it across ranks: the combOp).
+ * _score_dev, on the merged stats, ADDS sum_i s_i w_i and sum_i w_i of this
+ * shard into partial[2] (device; all-reduce, then the score is
+ * partial[0] / partial[1]); fewer than two clusters with rows ->
+ * CYC_ERR_ASSERTION "assertion failed: Number of clusters must be greater
+ * than one." (:391 / :532). */
+int cyc_kmeans_silhouette_stats_dev(cyc_kmeans_plan plan, const double* X, const double* xnorm,
+                                    int64_t n, const int32_t* pred, const double* weights,
+                                    double* stats, void* stream);
+int cyc_kmeans_silhouette_score_dev(cyc_kmeans_plan plan, const double* X, const double* xnorm,
+                                    int64_t n, const int32_t* pred, const double* weights,
+                                    const double* stats, double* partial, void* stream);
+
 /* Sparse (CSR) points against dense centers: KMeansExample's libsvm input
  * (BASELINE configs[0]).  Distances are MLUtils.fastSquaredDistance's
  * norm-trick branch (MLUtils.scala:533-576: BLAS.dot(sparse, dense), the

@@ -1461,3 +1461,96 @@ int64_t orc_blokify(int64_t n, int64_t F, const int64_t* rowNnz, const double* w
   }
   return nb;
 }
+
+/* ------------------------------------------------------------------------ */
+/* ml/evaluation/ClusteringMetrics.scala: Silhouette (one partition)        */
+/* ------------------------------------------------------------------------ */
+
+/* SquaredEuclideanSilhouette (:254-400) or CosineSilhouette (:403-600) over
+ * n rows X (n x d) with predictions pred in [0, k) and weights w (NULL =
+ * lit(1.0)).  stats (k d + 3 k scratch) receives computeClusterStats' map
+ * as [featureSum | squaredNormSum | weightSum | rows]: the seqOp in row
+ * order (:310-318 / :451-458; the combOp of one partition is the identity).
+ * Then computeSilhouetteCoefficient per row (:350-366 / :489-504 through
+ * Silhouette.pointSilhouetteCoefficient :66-97, the other clusters' minimum
+ * taken in cluster-id order) and overallScore (:101-103) in row order.
+ * Returns 0 and *score, or -1 when fewer than two clusters have rows (the
+ * assert :391 / :532).                                                      */
+int orc_silhouette(const double* X, int64_t n, int64_t d, const int32_t* pred, const double* w,
+                   int64_t k, int cosine, double* stats, double* score) {
+  double* fs = stats;
+  double* psi = stats + k * d;
+  double* W = psi + k;
+  double* cnt = W + k;
+  double* xn = (double*)malloc(sizeof(double) * (d > 0 ? d : 1));
+  memset(stats, 0, sizeof(double) * (size_t)(k * d + 3 * k));
+  for (int64_t i = 0; i < n; ++i) {
+    const double* x = X + i * d;
+    const double wt = w ? w[i] : 1.0;
+    const int64_t c = pred[i];
+    const double nrm = orc_norm2(x, d);
+    double* sum = fs + c * d;
+    if (cosine) {
+      /* normalizeFeatureUDF: BLAS.scal(1.0 / norm, features) (:528-531) */
+      const double a = 1.0 / nrm;
+      for (int64_t j = 0; j < d; ++j) xn[j] = a * x[j];
+      for (int64_t j = 0; j < d; ++j) sum[j] = sum[j] + wt * xn[j];
+    } else {
+      /* math.pow(Vectors.norm(features, 2.0), 2.0) (:385-387) */
+      const double sq = nrm * nrm;
+      for (int64_t j = 0; j < d; ++j) sum[j] = sum[j] + wt * x[j];
+      psi[c] = psi[c] + sq * wt;
+    }
+    W[c] = W[c] + wt;
+    cnt[c] = cnt[c] + 1.0;
+  }
+  int64_t present = 0;
+  for (int64_t c = 0; c < k; ++c) present += cnt[c] > 0.0;
+  if (present <= 1) {
+    free(xn);
+    return -1;
+  }
+  double num = 0.0, den = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    const double* x = X + i * d;
+    const double wt = w ? w[i] : 1.0;
+    const int64_t own = pred[i];
+    const double nrm = orc_norm2(x, d);
+    const double* v = x;
+    double sq = 0.0;
+    if (cosine) {
+      const double a = 1.0 / nrm;
+      for (int64_t j = 0; j < d; ++j) xn[j] = a * x[j];
+      v = xn;
+    } else {
+      sq = nrm * nrm;
+    }
+    double s;
+    if (W[own] == wt) {
+      s = 0.0;
+    } else {
+      double nb = 0.0, cur = 0.0;
+      int have = 0;
+      for (int64_t c = 0; c < k; ++c) {
+        if (!(cnt[c] > 0.0)) continue;
+        const double dt = orc_ddot(v, fs + c * d, d);
+        const double dist = cosine ? 1.0 - dt / W[c] : sq + psi[c] / W[c] - 2 * dt / W[c];
+        if (c == own) {
+          cur = dist;
+        } else {
+          nb = (have && nb <= dist) ? nb : dist;
+          have = 1;
+        }
+      }
+      cur = cur * W[own] / (W[own] - wt);
+      if (cur < nb) s = 1 - (cur / nb);
+      else if (cur > nb) s = (nb / cur) - 1;
+      else s = 0.0;
+    }
+    num = num + s * wt;
+    den = den + wt;
+  }
+  free(xn);
+  *score = num / den;
+  return 0;
+}

@@ -117,6 +117,8 @@ def lib():
                 "orc_spr_sparse": (None, [ctypes.c_double, _I32, _D, _i64, _D]),
                 "orc_gramian_partition": (None, [_D, _i64, _i64, _D, _D]),
                 "orc_triu_to_full": (None, [_i64, _D, _D]),
+                "orc_silhouette": (ctypes.c_int, [_D, _i64, _i64, _I32, _D, _i64, ctypes.c_int,
+                                                  _D, _D]),
                 "orc_blokify": (_i64, [_i64, _i64, _I64, _D, _i64, _I64,
                                        ctypes.POINTER(ctypes.c_uint8)]),
             }
@@ -1163,3 +1165,25 @@ def parse_libsvm(text, num_features=-1):
     return (np.array(labels, dtype=np.float64),
             (np.array(rowptr, dtype=np.int64), np.array(colidx, dtype=np.int32),
              np.array(values, dtype=np.float64)), nf)
+
+
+# --------------------------------------------------------------------------
+# ClusteringEvaluator Silhouette
+# --------------------------------------------------------------------------
+
+def silhouette(X, pred, k, weights=None, cosine=False):
+    """ml/evaluation/ClusteringMetrics.scala SquaredEuclideanSilhouette
+    (:254-400) / CosineSilhouette (:403-600), one partition: returns (score,
+    stats) with stats = [featureSum | squaredNormSum | weightSum | rows];
+    raises JavaAssertionError when fewer than two clusters have rows."""
+    X = _f64(X)
+    n, d = X.shape
+    pred = np.ascontiguousarray(pred, dtype=np.int32)
+    w = None if weights is None else _f64(weights)
+    stats = np.zeros(k * d + 3 * k, dtype=np.float64)
+    score = ctypes.c_double()
+    rc = lib().orc_silhouette(_p(X), n, d, _p(pred, _I32), _p(w), k, 1 if cosine else 0,
+                              _p(stats), ctypes.byref(score))
+    if rc != 0:
+        raise JavaAssertionError("assertion failed: Number of clusters must be greater than one.")
+    return score.value, stats

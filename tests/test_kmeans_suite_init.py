@@ -230,3 +230,17 @@ def test_kmeans_example_default_init(cuda):
                                            oracle.row_norms(C))
     _, got = model.pointCosts_csr(blk.rowptr, blk.colidx, blk.values)
     assert np.array_equal(got.cpu().numpy(), want)
+    # KMeansExample.scala:51-56: ClusteringEvaluator().evaluate(predictions),
+    # the squared-Euclidean Silhouette of the fitted clustering (the sparse
+    # rows' dot / axpy / norm visit the same nonzeros as their dense form)
+    from cycloneml_amd.evaluation import ClusteringEvaluator
+    rowptr, colidx, vals = csr
+    Xd = np.zeros((6, blk.numFeatures))
+    for i in range(6):
+        Xd[i, colidx[rowptr[i]:rowptr[i + 1]]] = vals[rowptr[i]:rowptr[i + 1]]
+    import torch
+    sil = ClusteringEvaluator().evaluate(torch.as_tensor(Xd, device=cuda),
+                                         torch.as_tensor(p, device=cuda))
+    want_sil, _ = oracle.silhouette(Xd, p.astype(np.int32), 2)
+    assert abs(sil - want_sil) <= 1e-12 * abs(want_sil)
+    assert 0.99 < sil < 1.0
