@@ -46,6 +46,13 @@
 
 #include "common.hpp"
 
+// tools/probe/screen1_probe.hip builds the one-limb pass with parts removed
+// to time them (results then meaningless): 1 = no epilogue VALU, 2 = no
+// center DMA / barrier waits, 3 = both.  0 in the library.
+#ifndef CYC_PROBE_MODE
+#define CYC_PROBE_MODE 0
+#endif
+
 namespace cyc {
 namespace km8 {
 namespace {
@@ -624,8 +631,12 @@ __device__ __forceinline__ double err_term2(int e, double n1, double mu, int d) 
 // two) and write assign[] for certified rows, the rest to list.
 // Two workgroups per CU; three for the two-limb pass (<= 168 VGPRs, LDS
 // 3 x 49 KB at S = 8), measured 7 % faster than two.
+// the one-limb pass screens a row whose exponent exceeds its wave's smallest
+// by at most this much (larger shifts could overflow its 32-bit bounds)
+constexpr int kShMax = 2;
+
 template <int S, int W, int LIMBS, bool LIST>
-__global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
+__global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
     const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
     int64_t n, int d, const uint4* __restrict__ Cb, const float* __restrict__ cq,
     const double* __restrict__ g, const double* __restrict__ cnorm,
@@ -638,10 +649,6 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
   // LIMBS = 1 takes two 32-center tiles per step (one barrier and one ring
   // slot per 64 centers: its tiles carry a third of the MFMAs)
   constexpr bool PAIR = LIMBS == 1;
-  // row sets of 32 per wave: LIMBS = 1 holds 64 rows (two A sets), so each B
-  // fragment DMA'd into the ring serves twice the rows -- at 32 rows per
-  // wave the DMA pieces' issue cost, one per 4 MFMAs, set that pass's pace
-  constexpr int R = PAIR ? 2 : 1;
   constexpr int FR = PAIR ? 2 * S : LIMBS * S;     // 1 KiB B fragments per ring step
   constexpr int TB = FR * 1024 + 256;              // tile slot: fragments, then 64 cq floats
   constexpr int G = FR / W;                        // fragment DMAs per wave per tile (+1: wave 0's cq)
@@ -660,31 +667,25 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
   // (kCandMax), the one-limb pass's for the two-limb refinement (kCand1)
   constexpr int CMAX = LIMBS == 1 ? kCand1 : kCandMax;
   const int64_t total = LIST ? (int64_t)*rowsInCount : n;
-  // one group of W waves x R x 32 positions
+  // one group of 32 W rows (positions)
   auto group = [&](int64_t grp) {
-  const int64_t wg32 = (grp * W + wave) * R;         // the wave's first 32-row set
+  const int64_t pos0 = (grp * W + wave) * 32;        // first position of this wave
   // waves past the end still take part in every barrier (zero rows)
-  int rows[R];
-#pragma unroll
-  for (int rs = 0; rs < R; ++rs)
-    rows[rs] = (int)max<int64_t>(0, min<int64_t>(32, total - (wg32 + rs) * 32));
-  auto rowAt = [&](int64_t p) -> int64_t {   // global row of position p (p < total)
-    if constexpr (LIST) return rowsIn[p];
-    else return p;
-  };
-  // scap > 0: list / cand appends go to the 32-row set's shard (kmeans_i8.hpp)
-  auto shardList = [&](int rs, unsigned int*& cnt) -> int32_t* {
-    const unsigned shard = (unsigned)((wg32 + rs) % kShards);
-    cnt = scap ? listCount + shard * kShardStride : listCount;
-    return scap ? list + (size_t)shard * scap : list;
+  const int rows = (int)max<int64_t>(0, min<int64_t>(32, total - pos0));
+  // scap > 0: list / cand appends go to this group's shard (kmeans_i8.hpp)
+  const unsigned shard = (unsigned)((grp * W + wave) % kShards);
+  int32_t* const listS = scap ? list + (size_t)shard * scap : list;
+  unsigned int* const listCountS = scap ? listCount + shard * kShardStride : listCount;
+  int32_t* const candRowsS = scap && candRows ? candRows + (size_t)shard * scap : candRows;
+  int32_t* const candsS = scap && cands ? cands + (size_t)shard * scap * CMAX : cands;
+  unsigned int* const candCountS =
+      scap && candCount ? candCount + shard * kShardStride : candCount;
+  auto rowAt = [&](int i) -> int64_t {   // global row of position pos0 + i (i < rows)
+    if constexpr (LIST) return rowsIn[pos0 + i];
+    else return pos0 + i;
   };
   if (!P.ok) {   // uniform over the grid
-#pragma unroll
-    for (int rs = 0; rs < R; ++rs) {
-      unsigned int* cnt;
-      int32_t* listS = shardList(rs, cnt);
-      if (lane < rows[rs]) listS[atomicAdd(cnt, 1u)] = (int32_t)rowAt((wg32 + rs) * 32 + lane);
-    }
+    if (lane < rows) listS[atomicAdd(listCountS, 1u)] = (int32_t)rowAt(lane);
     return;
   }
   // tile t -> slot t % 3: each wave DMAs fragments wave, wave + W, ... and the
@@ -693,6 +694,7 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
   // G DMAs per tile in flight and one counted wait fits all tiles.
   const int nsteps = PAIR ? ktp / 2 : ktp;          // ktp is even
   auto issue = [&](int t, int slot) {
+    if constexpr (PAIR && (CYC_PROBE_MODE & 2)) return;
     const int tt = t < nsteps ? t : nsteps - 1;
     char* dst = lds + slot * TB;
 #pragma unroll
@@ -714,64 +716,59 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
   };
   issue(0, 0);
   issue(1, 1);
-  // A fragments of the wave's rows, all substeps and limbs
-  v4i A[R][S][LIMBS];
-  int exr[R];
-#pragma unroll
-  for (int rs = 0; rs < R; ++rs) {
-    const bool rowOk = r < rows[rs];
-    const int64_t myRow = rowOk ? rowAt((wg32 + rs) * 32 + r) : 0;   // row 0 exists: n > 0
+  // A fragments of the wave's 32 rows, all substeps and limbs
+  v4i A[S][LIMBS];
+  const bool rowOk = r < rows;
+  const int64_t myRow = rowOk ? rowAt(r) : 0;   // lane's row (row 0 exists: n > 0)
+  {
     // loads from a valid row, zeroed after the load
+    const bool ok = rowOk;
     const uint4* src = Xq + myRow * CH + h;
 #pragma unroll
     for (int s = 0; s < S; ++s)
 #pragma unroll
       for (int L = 0; L < LIMBS; ++L) {
         const v4u t = __builtin_nontemporal_load((const v4u*)(src + L * (D / 16) + 2 * s));
-        A[rs][s][L] = rowOk ? __builtin_bit_cast(v4i, t) : v4i{0, 0, 0, 0};
+        A[s][L] = ok ? __builtin_bit_cast(v4i, t) : v4i{0, 0, 0, 0};
       }
-    // row of accumulator register reg: (reg & 3) + 8 (reg >> 2) + 4 h
-    exr[rs] = rowOk ? meta[myRow].x : INT_MIN;
   }
+  // row of accumulator register reg: (reg & 3) + 8 (reg >> 2) + 4 h
+  const int exr = rowOk ? meta[myRow].x : INT_MIN;
   // LIMBS = 3: per-row unit F1 = 2^(ex + ec - 20) of T in f32 bounds.
-  // LIMBS < 3: integer bounds in the units 2^(ex + ec - SH): L / F1 = Q - T
-  // with Q = cq / F1 rounded, from one per-lane base per tile at the row
-  // set's smallest exponent exmin, shifted right by sh = ex - exmin per row.
+  // LIMBS = 2: integer bounds in the same units: L / F1 = Q - T with
+  // Q = cq / F1 rounded, from one per-lane base per tile at the wave's
+  // smallest exponent exmin, shifted right by sh = ex - exmin per row.
   float F1[16];
-  int sh[R][16];
-  float qscale[R];   // cq scaled to the units 2^(exmin + ec - SH)
-  bool qbad[R];      // a cq below -2^30 units: the row set certifies nothing
+  int sh[16];
+  int exmin = 0;
+  if constexpr (LIMBS == 3) {
+    const float f = exr == INT_MIN ? 0.0f : __builtin_ldexpf(1.0f, exr + P.ec - 20);
 #pragma unroll
-  for (int rs = 0; rs < R; ++rs) {
-    int exmin = 0;
-    qbad[rs] = false;
-    if constexpr (LIMBS == 3) {
-      const float f = exr[rs] == INT_MIN ? 0.0f : __builtin_ldexpf(1.0f, exr[rs] + P.ec - 20);
+    for (int reg = 0; reg < 16; ++reg) F1[reg] = __shfl(f, (reg & 3) + 8 * (reg >> 2) + 4 * h);
+  } else {
+    int e = exr == INT_MIN ? INT_MAX : exr;
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) F1[reg] = __shfl(f, (reg & 3) + 8 * (reg >> 2) + 4 * h);
-    } else {
-      int e = exr[rs] == INT_MIN ? INT_MAX : exr[rs];
+    for (int m = 1; m < 32; m <<= 1) e = min(e, __shfl_xor(e, m));
+    exmin = __builtin_amdgcn_readfirstlane(e == INT_MAX ? 0 : e);
+    const int s0 = exr == INT_MIN ? 31 : min(exr - exmin, 31);
 #pragma unroll
-      for (int m = 1; m < 32; m <<= 1) e = min(e, __shfl_xor(e, m));
-      exmin = __builtin_amdgcn_readfirstlane(e == INT_MAX ? 0 : e);
-      const int s0 = exr[rs] == INT_MIN ? 31 : min(exr[rs] - exmin, 31);
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg)
-        sh[rs][reg] = __shfl(s0, (reg & 3) + 8 * (reg >> 2) + 4 * h);
-    }
-    qscale[rs] = __builtin_ldexpf(1.0f, max(-160, min(160, SH - P.ec - exmin)));
+    for (int reg = 0; reg < 16; ++reg) sh[reg] = __shfl(s0, (reg & 3) + 8 * (reg >> 2) + 4 * h);
   }
-  // LIMBS = 3: the two smallest f32 bounds; LIMBS < 3: the two largest
+  // cq scaled to the units 2^(exmin + ec - SH)
+  const float qscale = __builtin_ldexpf(1.0f, max(-160, min(160, SH - P.ec - exmin)));
+  // |Q| clamp in those units: LIMBS = 1 keeps (Q << IB) in 31 bits
+  constexpr float QCLAMP = LIMBS == 1 ? 0x1p25f : 0x1p30f;
+  bool qbad = false;   // a cq below -QCLAMP units: the wave certifies nothing
+  // LIMBS = 3: the two smallest f32 bounds; LIMBS = 2: the two largest
   // V = T - Q (the smallest L = -F1 V), tile index in the low IB bits
   float sL1[16], sL2[16];
-  int sV1[R][16], sV2[R][16];
+  int sV1[16], sV2[16];
   int sI1[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     sL1[q] = sL2[q] = __builtin_inff();
+    sV1[q] = sV2[q] = INT_MIN;
     sI1[q] = -1;
-#pragma unroll
-    for (int rs = 0; rs < R; ++rs) sV1[rs][q] = sV2[rs][q] = INT_MIN;
   }
   // tile ct from its slot: LIMBS = 3: six limb products per substep,
   // LIMBS = 2: three; B fragments by conflict-free ds_read_b128
@@ -785,20 +782,20 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
       for (int L = 0; L < LIMBS; ++L) Bc[L] = B[(LIMBS * s + L) * 64];
       const v4i B0 = Bc[0], B1 = Bc[LIMBS >= 2 ? 1 : 0];
       // (separating the two acc[1] products by sched_barrier measured 3 % slower)
-      acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0][s][0], B0, acc[0], 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B0, acc[0], 0, 0, 0);
       if constexpr (LIMBS >= 2) {
-        acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0][s][0], B1, acc[1], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0][s][1], B0, acc[1], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B1, acc[1], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B0, acc[1], 0, 0, 0);
       }
       if constexpr (LIMBS == 3) {
         const v4i B2 = Bc[2];
-        acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0][s][0], B2, acc[2], 0, 0, 0);
-        acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0][s][1], B1, acc[2], 0, 0, 0);
-        acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0][s][2], B0, acc[2], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], B2, acc[2], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][1], B1, acc[2], 0, 0, 0);
+        acc[2] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][2], B0, acc[2], 0, 0, 0);
       }
     }
   };
-  // LIMBS < 3 keeps the tile index in the low IB bits of V (moving it by
+  // LIMBS = 2 keeps the tile index in the low IB bits of V (moving it by
   // < 2^IB units either way, charged in the certification): a max and a med3
   // per (row, center) instead of a compare, a med3 and two selects.
   const int IB = 32 - __builtin_clz((unsigned)max(ktp - 1, 1));
@@ -806,20 +803,19 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
   // LIMBS = 2, after the tile's MFMAs: acc[1] started at -Q
   int vzero;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
-  auto epi_reg = [&](int rs, int reg, unsigned ctv, int V) {
-    const int Ve = (int)(((unsigned)V & ~IM) | ctv);                  // ct < 2^IB
-    sV2[rs][reg] = max(min(sV1[rs][reg], sV2[rs][reg]),
-                       min(max(sV1[rs][reg], sV2[rs][reg]), Ve));      // v_med3_i32
-    sV1[rs][reg] = max(sV1[rs][reg], Ve);
-  };
   auto epi2 = [&](int ct, const v16i (&acc)[LIMBS]) {
     // ct in a VGPR (one v_and_or_b32 may read only one SGPR, the mask), by
     // a VALU add to an opaque zero: no inline asm in the loop, which would
     // split its scheduling region
     const unsigned ctv = (unsigned)(vzero + ct);
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg)
-      epi_reg(0, reg, ctv, acc[0][reg] * 128 + acc[LIMBS - 1][reg]);   // T - Q
+    for (int reg = 0; reg < 16; ++reg) {
+      // T - Q (LIMBS = 1: acc[0] started at -Q)
+      const int V = LIMBS == 1 ? acc[0][reg] : acc[0][reg] * 128 + acc[LIMBS - 1][reg];
+      const int Ve = (int)(((unsigned)V & ~IM) | ctv);                  // ct < 2^IB
+      sV2[reg] = max(min(sV1[reg], sV2[reg]), min(max(sV1[reg], sV2[reg]), Ve));   // v_med3_i32
+      sV1[reg] = max(sV1[reg], Ve);
+    }
   };
   auto epi = [&](int ct, float cqv, const v16i (&acc)[LIMBS]) {
     const int c = ct * 32 + r;
@@ -839,17 +835,14 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
   auto cq_of = [&](int slot, int half = 0) {
     return *(const float*)(lds + slot * TB + FR * 1024 + (half * 32 + r) * 4);
   };
-  // -Q per row (LIMBS < 3): ceil(floor(cq 2^k) / 2^sh) >= Q - 1 unit; cq
-  // above 2^30 units clamps (a smaller Q: still a lower bound)
-  auto negq = [&](float cqv, int rs) {
-    const float pf = cqv * qscale[rs];   // exact (a power of two; round-down mode)
-    qbad[rs] |= pf < -0x1p30f;
-    return -(int)__builtin_floorf(__builtin_fminf(pf, 0x1p30f));
-  };
   // tile t in `slot`: wait for this wave's DMAs of t (those of t + 1 may stay
   // in flight), barrier (every wave's part of t landed; every wave is past
   // t - 1, whose slot the DMAs of t + 2 now refill)
   auto arrive = [&](int t, int slot) {
+    if constexpr (PAIR && (CYC_PROBE_MODE & 2)) {
+      __builtin_amdgcn_s_barrier();
+      return;
+    }
     if (wave == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + 1) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
     __builtin_amdgcn_s_barrier();
@@ -864,86 +857,87 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
   // this form at 168 VGPRs and three waves per SIMD)
   int sl = 0;
   if constexpr (PAIR) {
-    // Software-pipelined by hand.  A step runs four phases of S MFMAs,
-    // (tile 2 st, row set 0) -> X0, (2 st, 1) -> X1, (2 st + 1, 0) -> X0,
-    // (2 st + 1, 1) -> X1; each gap between two MFMAs of a phase carries the
-    // epilogue of 16 / S rows of the phase before (the first phase: the last
-    // one of the step before, across the barrier), the initial -Q of those
-    // rows for the phase after, and the B fragment of the next MFMA;
-    // sched_barrier pins that order.  X1 starts as INT_MIN rows of tile 0:
-    // an epilogue that changes no sV.
+    // The one-limb bounds in the units 2^(exmin + ec - SH) of the wave's
+    // smallest exponent, shifted left by IB with the tile index in the low
+    // bits: Ve = (T << (sh + IB)) + ((-Q << IB) + ct), one v_lshl_add_u32 per
+    // (row, center) on an accumulator started at 0 (the -Q start value of
+    // the two-limb form is gone, and Q needs no per-row rounding).
+    // |T| < 2^22 (d <= 256), sh <= kShMax (rows past it are not screened),
+    // |Q| <= 2^25: |Ve| < 2^31.
+    int shIB[16];
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) shIB[reg] = min(sh[reg], kShMax) + IB;
+    auto epi_reg = [&](int reg, int cpr, int T) {
+      const int Ve = (int)(((unsigned)T << shIB[reg]) + (unsigned)cpr);
+      sV2[reg] = max(min(sV1[reg], sV2[reg]), min(max(sV1[reg], sV2[reg]), Ve));   // v_med3_i32
+      sV1[reg] = max(sV1[reg], Ve);
+    };
+    // Software-pipelined by hand: each gap between two MFMAs of one tile
+    // carries the epilogue of 16 / S rows of the tile before (tile 2 st - 1's
+    // beside 2 st's, across the barrier) and the B fragment of the next MFMA;
+    // sched_barrier pins that order.  X1 starts as zero rows with cpr =
+    // INT_MIN: an epilogue that changes no sV.
     constexpr int RPG = 16 / S;   // accumulator rows per MFMA gap
     static_assert(16 % S == 0, "the gaps split the 16 rows evenly");
-    v16i X0, X1;
-#pragma unroll
-    for (int reg = 0; reg < 16; ++reg) X1[reg] = INT_MIN;
-    int prev = 0;
+    const v16i Z = {};
+    v16i X0, X1 = Z;
+    int cprPrev = INT_MIN;
     for (int st = 0; st < nsteps; ++st) {
       arrive(st, sl);
-      // -Q of tiles 2 st (nb[.][0]) and 2 st + 1 (nb[.][1]) per row set
-      int nb[R][2];
+      // (-Q << IB) + ct of tiles 2 st and 2 st + 1
+      int cpr[2];
 #pragma unroll
       for (int hf = 0; hf < 2; ++hf) {
-        const float cqv = cq_of(sl, hf);
-#pragma unroll
-        for (int rs = 0; rs < R; ++rs) nb[rs][hf] = negq(cqv, rs);
+        const float pf = cq_of(sl, hf) * qscale;
+        qbad |= pf < -QCLAMP;
+        const int nb = -(int)__builtin_floorf(__builtin_fminf(pf, QCLAMP));
+        cpr[hf] = (int)(((unsigned)nb << IB) + (unsigned)(vzero + 2 * st + hf));
       }
+      // opaque: one register each, not re-associated into every element's add
+      asm volatile("" : "+v"(cpr[0]), "+v"(cpr[1]));
       const v4i* B = (const v4i*)(lds + sl * TB) + lane;
-#pragma unroll
-      for (int reg = 0; reg < 16; ++reg) X0[reg] = nb[0][0] >> sh[0][reg];
-      const unsigned ctp = (unsigned)(vzero + prev), ct0 = (unsigned)(vzero + 2 * st),
-                     ct1 = ct0 + 1u;
       v4i Bn = B[0];
       __builtin_amdgcn_sched_barrier(0);
-      // phase ph: tile 2 st + (ph >> 1), row set ph & 1, into X0 (even ph) or
-      // X1; the other accumulator holds phase ph - 1's tile
 #pragma unroll
-      for (int ph = 0; ph < 4; ++ph) {
-        const int tsel = ph >> 1, rs = ph & 1;
-        const int prs = rs ^ 1;                                  // phase ph - 1's row set
-        const unsigned pct = ph == 0 ? ctp : (ph <= 2 ? ct0 : ct1);
+      for (int s = 0; s < S; ++s) {
+        const v4i Bc = Bn;
+        Bn = B[(s + 1) * 64];   // s = S - 1: tile 2 st + 1's first fragment
+        X0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], Bc, s == 0 ? Z : X0, 0, 0, 0);
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-          const v4i Bc = Bn;
-          // the next MFMA's fragment: this tile's next substep, or the first
-          // substep of the next phase's tile
-          const int nf = s + 1 < S ? tsel * S + s + 1 : (ph < 3 ? ((ph + 1) >> 1) * S : -1);
-          if (nf >= 0) Bn = B[nf * 64];
-          if (ph & 1) X1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[rs][s][0], Bc, X1, 0, 0, 0);
-          else X0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[rs][s][0], Bc, X0, 0, 0, 0);
-#pragma unroll
-          for (int q = RPG * s; q < RPG * (s + 1); ++q)
-            epi_reg(prs, q, pct, (ph & 1) ? X0[q] : X1[q]);
-          if (ph < 3) {   // the freed rows start phase ph + 1: tile (ph + 1) >> 1, row set prs
-#pragma unroll
-            for (int q = RPG * s; q < RPG * (s + 1); ++q) {
-              const int v = nb[prs][(ph + 1) >> 1] >> sh[prs][q];
-              if (ph & 1) X0[q] = v;
-              else X1[q] = v;
-            }
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
+        for (int q = RPG * s; q < RPG * (s + 1); ++q) epi_reg(q, cprPrev, X1[q]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      prev = 2 * st + 1;
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const v4i Bc = Bn;
+        if (s + 1 < S) Bn = B[(S + s + 1) * 64];
+        X1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s][0], Bc, s == 0 ? Z : X1, 0, 0, 0);
+#pragma unroll
+        for (int q = RPG * s; q < RPG * (s + 1); ++q) epi_reg(q, cpr[0], X0[q]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      cprPrev = cpr[1];
       sl = next_slot(sl);
     }
-    const unsigned ctp = (unsigned)(vzero + prev);
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) epi_reg(R - 1, reg, ctp, X1[reg]);
+    for (int reg = 0; reg < 16; ++reg) epi_reg(reg, cprPrev, X1[reg]);
   }
   for (int ct = 0; ct < (PAIR ? 0 : ktp); ++ct) {
     v16i X[LIMBS];
     arrive(ct, sl);
     const float cqv = cq_of(sl);
-    if constexpr (LIMBS == 2) {
-      const int nb = negq(cqv, 0);
+    if constexpr (LIMBS < 3) {
+      // -Q per row: ceil(floor(cq 2^k) / 2^sh) >= Q - 1 unit; cq above 2^30
+      // units clamps (a smaller Q: still a lower bound)
+      const float pf = cqv * qscale;   // exact (a power of two; round-down mode)
+      qbad |= pf < -QCLAMP;
+      const int nb = -(int)__builtin_floorf(__builtin_fminf(pf, QCLAMP));
       X[0] = v16i{};
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) X[LIMBS - 1][reg] = nb >> sh[0][reg];
+      for (int reg = 0; reg < 16; ++reg) X[LIMBS - 1][reg] = nb >> sh[reg];
       tile(sl, X);
       epi2(ct, X);
-    } else if constexpr (LIMBS == 3) {
+    } else {
 #pragma unroll
       for (int L = 0; L < LIMBS; ++L) X[L] = v16i{};
       tile(sl, X);
@@ -954,25 +948,15 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
   __builtin_amdgcn_s_setreg(0x801, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing re-read DMAs
 
-  // per row set: certification, then the candidate sets of its undecided rows
-  auto finish = [&](int rs) {
-  const int64_t p0 = (wg32 + rs) * 32;   // the set's first position
-  unsigned int* listCountS;
-  int32_t* const listS = shardList(rs, listCountS);
-  const unsigned shard = (unsigned)((wg32 + rs) % kShards);
-  int32_t* const candRowsS = scap && candRows ? candRows + (size_t)shard * scap : candRows;
-  int32_t* const candsS = scap && cands ? cands + (size_t)shard * scap * CMAX : cands;
-  unsigned int* const candCountS =
-      scap && candCount ? candCount + shard * kShardStride : candCount;
-  // LIMBS < 3: each lane's own best and second best (one center column per
+  // LIMBS = 2: each lane's own best and second best (one center column per
   // lane) before the reduction merges them: the candidate sets below
   int cV1[16], cV2[16];
   if constexpr (LIMBS < 3) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      sI1[q] = (int)((unsigned)sV1[rs][q] & IM) * 32 + r;
-      cV1[q] = sV1[rs][q];
-      cV2[q] = sV2[rs][q];
+      sI1[q] = (int)((unsigned)sV1[q] & IM) * 32 + r;
+      cV1[q] = sV1[q];
+      cV2[q] = sV2[q];
     }
   }
   // each row's (L1, L2, I1) over the 32 lanes (centers) of its half: every
@@ -1010,7 +994,7 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
   MERGE(K1[0], K2[0], sI1[0], __shfl_xor(K1[0], 1), __shfl_xor(K2[0], 1),           \
         __shfl_xor(sI1[0], 1));
   if constexpr (LIMBS < 3) {
-    CYC_REDUCE(sV1[rs], sV2[rs], mergeV)
+    CYC_REDUCE(sV1, sV2, mergeV)
   } else {
     CYC_REDUCE(sL1, sL2, mergeL)
   }
@@ -1018,45 +1002,56 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
   // lane holds row register q = lane bits 1..4
   // per-wave reduction area in the (now idle) slots: L1, L2, I1 x 32 rows
   __syncthreads();
-  float* redL1 = (float*)lds + wave * 96;   // LIMBS < 3: the V1, V2 bits
+  float* redL1 = (float*)lds + wave * 96;   // LIMBS = 2: the V1, V2 bits
   float* redL2 = redL1 + 32;
   int* redI1 = (int*)(redL1 + 64);
   if ((lane & 1) == 0) {
     const int q = (lane >> 1) & 15;
     const int row = (q & 3) + 8 * (q >> 2) + 4 * h;
-    redL1[row] = LIMBS < 3 ? __int_as_float(sV1[rs][0]) : sL1[0];
-    redL2[row] = LIMBS < 3 ? __int_as_float(sV2[rs][0]) : sL2[0];
+    redL1[row] = LIMBS < 3 ? __int_as_float(sV1[0]) : sL1[0];
+    redL2[row] = LIMBS < 3 ? __int_as_float(sV2[0]) : sL2[0];
     redI1[row] = sI1[0];
   }
-  const bool waveBad = __builtin_amdgcn_ballot_w64(qbad[rs]) != 0;
+  const bool waveBad = __builtin_amdgcn_ballot_w64(qbad) != 0;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   bool want = false;   // LIMBS < 3: an undecided row for the candidate pass
   int thrV = 0;
   int64_t grow = 0;
-  if (lane < rows[rs]) {
-    grow = rowAt(p0 + lane);
+  if (lane < rows) {
+    grow = rowAt(lane);
     const int2 mt = meta[grow];
     const int I1 = redI1[lane];
-    // L1, L2 as fp64 (LIMBS < 3: -F1 V, exact; V2 = INT_MIN: no second)
+    // L1, L2 as fp64 (LIMBS < 3: -F1 V; V2 = INT_MIN: no second)
     double l1, l2, f1 = 0.0;
     int v1 = 0;
-    bool clamped = false;
+    bool clamped = false, shOk = true;
+    int sb = 0;   // LIMBS = 1: the row's Ve = V 2^sb (+ index bits)
     if constexpr (LIMBS < 3) {
       f1 = __builtin_ldexp(1.0, mt.x + P.ec - SH);
       v1 = __float_as_int(redL1[lane]);
-      const int v2 = __float_as_int(redL2[lane]);
+      int v2 = __float_as_int(redL2[lane]);
+      if constexpr (LIMBS == 1) {
+        // back to the row's units, floored (< 1 unit, inside enc below)
+        const int shr = mt.x - exmin;
+        shOk = shr >= 0 && shr <= kShMax;
+        sb = min(max(shr, 0), kShMax) + IB;
+        if (v1 != INT_MIN) v1 >>= sb;
+        if (v2 != INT_MIN) v2 >>= sb;
+      }
       l1 = -f1 * (double)v1;
       l2 = v2 == INT_MIN ? __builtin_inf() : -f1 * (double)v2;
       // the winner's Q must not have clamped (its bound would be too low)
-      if (I1 >= 0 && I1 < P.k) clamped = !((double)cq[I1] * (double)qscale[rs] <= 0x1p30);
+      if (I1 >= 0 && I1 < P.k)
+        clamped = !((double)cq[I1] * (double)qscale <= (double)QCLAMP);
     } else {
       l1 = (double)redL1[lane];
       l2 = (double)redL2[lane];
     }
     bool decided = false, eligible = false;
     double M = 0.0;
-    if (mt.x != INT_MIN && I1 >= 0 && I1 < P.k && !clamped && !waveBad && __builtin_isfinite(l1)) {
+    if (mt.x != INT_MIN && I1 >= 0 && I1 < P.k && !clamped && shOk && !waveBad &&
+        __builtin_isfinite(l1)) {
       const double xn = xnorm[grow], cn = cnorm[I1];
       const double xx = xn * xn, cc = cn * cn;
       const double n1 = (double)__int_as_float(mt.y);   // bounds |xh3|_1
@@ -1064,8 +1059,9 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
           LIMBS == 3 ? err_term(mt.x, n1, mu, d)
           : LIMBS == 2 ? err_term2(mt.x, n1 + (double)d * __builtin_ldexp(1.0078125, mt.x - 15), mu, d)
                        : err_term1(mt.x, n1 + (double)d * __builtin_ldexp(1.0078125, mt.x - 8), mu);
-      // LIMBS < 3: the index bits move each V by < 2^IB units and the
+      // LIMBS = 2: the index bits move each V by < 2^IB units and the
       // rounded Q adds < 1 more: |L1 - L1'|, |L2 - L2'| < (2^IB + 1) F1
+      // (LIMBS = 1: < 1 unit, the floor of V 2^sb)
       const double enc = LIMBS == 3 ? 0.0
                                     : __builtin_ldexp((double)(IM + 3u), mt.x + P.ec - SH);
       M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) + 2.0 * enc +
@@ -1087,6 +1083,9 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
       if (tv > (double)INT_MIN + 2.0) {
         want = true;
         thrV = (int)tv;
+        // LIMBS = 1: in the lanes' Ve units (a lower threshold only adds
+        // candidates)
+        if constexpr (LIMBS == 1) thrV = (int)((unsigned)max(thrV, -(1 << 23)) << sb);
       } else {
         listS[atomicAdd(listCountS, 1u)] = (int32_t)grow;
       }
@@ -1100,7 +1099,7 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
       // lane (r, h) saw the centers 32 ct + r of row (reg & 3) + 8 (reg >> 2)
       // + 4 h; its best is a candidate when it reaches the row's threshold,
       // and a lane whose SECOND best reaches it too (an index not kept)
-      // sends the row to the three-limb pass.  <= CMAX candidates go to
+      // sends the row to the three-limb pass.  <= kCandMax candidates go to
       // the candidate list (exact fp64 distances, screen_cands).
       int* thrS = (int*)lds + W * 96 + wave * (64 + 32 * (CMAX + 1));
       int* wantS = thrS + 32;
@@ -1145,14 +1144,11 @@ __global__ __launch_bounds__(64 * W, LIMBS == 1 ? 2 : (LIMBS < 3 ? 12 : 8) / W) 
       }
     }
   }
-  __syncthreads();   // the reduction area is the next row set's
-  };
-#pragma unroll
-  for (int rs = 0; rs < R; ++rs) finish(rs);
+  __syncthreads();   // the reduction area is the next group's tile ring
   };
   // LIST: the grid covers n rows; groups past the count leave at once (a
   // grid-stride loop here costs the three-limb S = 8 form ~30 spilled VGPRs)
-  if ((int64_t)blockIdx.x * 32 * W * R < total) group(blockIdx.x);
+  if ((int64_t)blockIdx.x * 32 * W < total) group(blockIdx.x);
 }
 
 template <int S, int W, int LIMBS, bool LIST>
@@ -1165,8 +1161,7 @@ int launch_screen32(const void* img, const int2* meta, const double* xnorm, int6
                     unsigned int scap = 0) {
   KernelTimer timer(LIMBS == 1 ? "k_kmeans_screen1" : LIMBS == 2 ? "k_kmeans_screen2"
                                                     : "k_kmeans_screen3", st);
-  constexpr int R = LIMBS == 1 ? 2 : 1;   // row sets of 32 per wave (k_screen32)
-  const int64_t wg = (n + 32 * W * R - 1) / (32 * W * R);   // W waves x R x 32 rows
+  const int64_t wg = (n + 32 * W - 1) / (32 * W);   // W waves x 32 rows
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32<S, W, LIMBS, LIST>), dim3((unsigned)wg),
                      dim3(64 * W), 0, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
                      cq, g, cnorm, prm, ktp, rowsIn, rowsInCount, assign, list, listCount,
