@@ -47,8 +47,9 @@
 #include "common.hpp"
 
 // tools/probe/screen1_probe.hip builds the one-limb pass with parts removed
-// to time them (results then meaningless): 1 = no epilogue VALU, 2 = no
-// center DMA / barrier waits, 3 = both.  0 in the library.
+// to time them (results then meaningless): bits 2 = no center DMA / waits,
+// 4 = no reduction / certification tail, 8 = every wave's rows read from row
+// 0 (no HBM stream).  0 in the library.
 #ifndef CYC_PROBE_MODE
 #define CYC_PROBE_MODE 0
 #endif
@@ -723,7 +724,7 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
   {
     // loads from a valid row, zeroed after the load
     const bool ok = rowOk;
-    const uint4* src = Xq + myRow * CH + h;
+    const uint4* src = Xq + ((PAIR && (CYC_PROBE_MODE & 8)) ? 0 : myRow) * CH + h;
 #pragma unroll
     for (int s = 0; s < S; ++s)
 #pragma unroll
@@ -947,6 +948,10 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
   }
   __builtin_amdgcn_s_setreg(0x801, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing re-read DMAs
+  if constexpr (PAIR && (CYC_PROBE_MODE & 4)) {   // probe: no reduction / certification
+    if (lane < rows) assign[rowAt(lane)] = sV1[lane & 15] ^ sV2[(lane + 1) & 15];
+    return;
+  }
 
   // LIMBS = 2: each lane's own best and second best (one center column per
   // lane) before the reduction merges them: the candidate sets below

@@ -1,8 +1,9 @@
 // Time the KMeans one-limb pass (k_screen32<8, 4, 1, false>) on synthetic
 // data at the bench's shape (10M rows, d = 256, k = 1024), built with
-// -DCYC_PROBE_MODE=0..3 (kmeans_i8.hip: 1 = no epilogue VALU, 2 = no center
-// DMA / waits, 3 = both) to see which part sets its pace.  Results of modes
-// 1-3 are meaningless; only the time is read.
+// -DCYC_PROBE_MODE=bits (kmeans_i8.hip: 2 = no center DMA / waits, 4 = no
+// reduction / certification tail, 8 = no row stream) to see which part sets
+// its pace.  Results of modes other than 0 are meaningless; only the time is
+// read.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fno-slp-vectorize
 //     -DCYC_PROBE_MODE=1 -I cycloneml_amd/csrc tools/probe/screen1_probe.hip
 //     -L cycloneml_amd -lcyclone -Wl,-rpath,cycloneml_amd -o tools/bin/screen1_m1
