@@ -430,6 +430,48 @@ __global__ void k_mlr_offset(const double* __restrict__ coef, const double* __re
 typedef int v4i32 __attribute__((ext_vector_type(4)));
 typedef int v2i32 __attribute__((ext_vector_type(2)));
 
+// tools/probe/mlr_probe.hip builds k_mlr_margins with parts removed to time
+// them (results then meaningless): bits 1 = X loaded for chunk 0 only, 2 = no
+// softmax epilogue, 4 = no W DMA, 8 = no multiplier stores, 16 = no exp.
+// 0 in the library.
+#ifndef CYC_MLR_PROBE
+#define CYC_MLR_PROBE 0
+#endif
+
+// 2^(j/32), j = 0..31, correctly rounded (exp_neg's table)
+__constant__ double kExp2Tab[32] = {
+    1.0, 1.0218971486541166, 1.0442737824274138, 1.0671404006768237,
+    1.0905077326652577, 1.1143867425958924, 1.1387886347566916, 1.1637248587775775,
+    1.189207115002721, 1.215247359980469, 1.241857812073484, 1.2690509571917332,
+    1.2968395546510096, 1.3252366431597413, 1.3542555469368927, 1.383909881963832,
+    1.4142135623730951, 1.4451808069770467, 1.4768261459394993, 1.5091644275934228,
+    1.5422108254079407, 1.5759808451078865, 1.6104903319492543, 1.645755478153965,
+    1.681792830507429, 1.718619298122478, 1.7562521603732995, 1.7947090750031072,
+    1.8340080864093424, 1.8741676341103, 1.9152065613971474, 1.9571441241754002};
+
+// e^x for x <= 0 (the softmax terms m - max): x = (32 e + j) ln2/32 + r with
+// |r| <= ln2/64 (Cody-Waite, a 38-bit high part), e^x = 2^e 2^(j/32) e^r,
+// e^r by its degree-6 Taylor polynomial (truncation < 2^-57 relative),
+// 2^(j/32) from the LDS table T: within a few ulp, against Math.exp's 1 ulp
+// in the reference -- far inside the aggregator's 1e-10 bar -- at 15 f64
+// VALU where the libm exp takes ~23.  Below -708 (terms under 1e-307 of the
+// largest, 1.0) it returns 0; NaN stays NaN.
+__device__ __forceinline__ double exp_neg(double x, const double* __restrict__ T) {
+  if (x < -708.0) return 0.0;
+  const double kd = __builtin_rint(x * 46.16624130844683);   // 32 / ln2
+  double r = __builtin_fma(kd, -0.021660849392446835, x);
+  r = __builtin_fma(kd, -5.145609244655338e-14, r);
+  const int k = (int)kd;
+  double q = 1.0 / 720.0;
+  q = __builtin_fma(q, r, 1.0 / 120.0);
+  q = __builtin_fma(q, r, 1.0 / 24.0);
+  q = __builtin_fma(q, r, 1.0 / 6.0);
+  q = __builtin_fma(q, r, 0.5);
+  q = __builtin_fma(q, r, 1.0);
+  q = __builtin_fma(q, r, 1.0);
+  return __builtin_ldexp(T[k & 31] * q, k >> 5);
+}
+
 constexpr int MR = 256;    // rows per margin tile (8 waves x 32 rows)
 constexpr int MK = 16;     // features per LDS chunk
 constexpr int MT = 512;    // threads per margin workgroup
@@ -450,20 +492,44 @@ constexpr int MT = 512;    // threads per margin workgroup
 // their margins are never used) or zero past the end of coef.
 // (The last class tile on v_mfma_f64_4x4x4f64, as k_mlr_grad does, measured
 // 4-5 % slower here at C = 100, with or without sched_barrier fences.)
-template <int CT>
-__global__ __launch_bounds__(MT) void k_mlr_margins(
+// NW waves per workgroup (32 NW rows per tile; NW = 4: two workgroups per
+// CU); DEPHASE: the workgroups whose index bit 0 differs from bit 8 start
+// half a tile late, so the two workgroups of a CU (consecutive indices, or
+// i and i + 256) run their softmax epilogues while the other one's MFMAs
+// keep the matrix pipe busy.
+template <int CT, int NW = 8, bool DEPHASE = false>
+__global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
     const double* __restrict__ X, const double* __restrict__ labels,
     const double* __restrict__ weights, int64_t n, int F, int C, const double* __restrict__ coef,
     const double* __restrict__ offset, double* __restrict__ mult, double* __restrict__ slabS,
     double* __restrict__ slabMS) {
+  constexpr int MR = 32 * NW, MT = 64 * NW;
   constexpr int CP = CT * 16;
   static_assert(MK == 16, "the A layout covers 16 features per chunk");
   constexpr int WBUF = MK * CP + 128;   // doubles per W buffer (whole 1 KiB pieces)
-  __shared__ __attribute__((aligned(16))) double Ws[2][WBUF];
+  // the two W buffers, then exp_neg's table and the per-class offsets (never
+  // DMA targets)
+  __shared__ __attribute__((aligned(16))) double Ws[2][WBUF + 32 + CP];
+  double* const expT = Ws[1] + WBUF;
+  double* const offS = expT + 32;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4;
   const int64_t tiles = (n + MR - 1) / MR;
   const int nch = (F + MK - 1) / MK;
+  if constexpr (DEPHASE) {
+    // half a tile at ~2 GHz with two waves per SIMD sharing the pipe:
+    // nch chunks x 8 CT MFMAs x 64 cycles, on the 100 MHz constant clock
+    if (((blockIdx.x ^ (blockIdx.x >> 8)) & 1) != 0) {
+      const int64_t ticks = (int64_t)nch * 8 * CT * 64 / 20;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks)
+        __builtin_amdgcn_s_sleep(32);
+    }
+  }
+  // read after a barrier: the epilogue reads them by ds_read, so none of
+  // its waits is a vmcnt that would also drain the multiplier stores
+  if (threadIdx.x < 32) expT[threadIdx.x] = kExp2Tab[threadIdx.x];
+  if (threadIdx.x < CP) offS[threadIdx.x] = (offset && (int)threadIdx.x < C) ? offset[threadIdx.x] : 0.0;
   double loss = 0.0, wsum = 0.0;
   double ms[CT];
 #pragma unroll
@@ -477,6 +543,7 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
   // pieces covering every index the B reads touch: (MK - 1) C + CP doubles
   const int wpieces = (((MK - 1) * C + CP) * 8 + 1023) / 1024;
   auto loadW = [&](int ch) {      // chunk ch's 16 x C run of coef into buffer ch & 1
+    if constexpr ((CYC_MLR_PROBE & 4) != 0) return;
     double* dst = Ws[ch & 1];
     const int base = ch * MK * C * 8;
     for (int q = wave; q < wpieces; q += MT / 64)
@@ -485,6 +552,9 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
           lane * 16, 0, 0, 0);
   };
   auto loadX = [&](int64_t r0, int ch, double (&x)[2][4]) {
+    if constexpr ((CYC_MLR_PROBE & 1) != 0) {
+      if (ch > 0) return;
+    }
     const int f0 = ch * MK + 4 * g;
     const int64_t nr = min<int64_t>(MR, n - r0);
     const auto xR = __builtin_amdgcn_make_buffer_rsrc((void*)(X + r0 * F), (short)0,
@@ -509,7 +579,15 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
     }
   };
   cyc_double4 acc[2][CT];
-  auto epilogue = [&](int64_t r0) {
+  // labL / wL: lane l holds label and weight of row 32 wave + (l & 31)
+  auto epilogue = [&](int64_t r0, double labL, double wL) {
+    if constexpr ((CYC_MLR_PROBE & 2) != 0) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) ms[ct] += acc[t][ct][0];
+      return;
+    }
     // Epilogue: lane holds rows 32 wave + 16 t + (lane>>4) + 4r, classes
     // 16 ct + (lane & 15).
 #pragma unroll
@@ -524,7 +602,7 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
           const int c = ct * 16 + (lane & 15);
-          const double oc = (offset && c < C) ? offset[c] : 0.0;
+          const double oc = offS[c];
           m[ct] = acc[t][ct][r] + oc;  // 1.0*temp + 1.0*offset (netlib dgemm)
           if (c < C) {
             if (m[ct] == __builtin_inf()) infc = min(infc, c);
@@ -536,7 +614,8 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
           mx = fmax(mx, __shfl_xor(mx, k));
           infc = min(infc, __shfl_xor(infc, k));
         }
-        double p[CT];
+        // the probabilities replace the margins in place (p = m)
+        double (&p)[CT] = m;
         if (infc < (1 << 30)) {
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) {
@@ -548,7 +627,8 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) {
             const int c = ct * 16 + (lane & 15);
-            p[ct] = (c < C) ? exp(m[ct] - mx) : 0.0;
+            p[ct] = (c < C) ? ((CYC_MLR_PROBE & 16) ? (m[ct] - mx) : exp_neg(m[ct] - mx, expT))
+                            : 0.0;
             sum += p[ct];
           }
 #pragma unroll
@@ -558,8 +638,12 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) p[ct] = inv * p[ct];
         }
-        const double w = rowok ? (weights ? weights[row] : 1.0) : 0.0;
-        const int label = rowok ? (int)labels[row] : 0;
+        // unconditional shuffles: a shuffle under `rowok` made the compiler
+        // wait vmcnt(0) on labL / wL at every row, draining the stores
+        const int q = 16 * t + 4 * r + (lane >> 4);   // the row within the wave's 32
+        const double wq = __shfl(wL, q), lq = __shfl(labL, q);
+        const double w = rowok ? wq : 0.0;
+        const int label = rowok ? (int)lq : 0;
         double pl = 0.0;
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
@@ -580,7 +664,7 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
             mu = 0.0 * p[ct];
           }
           if (c >= C || !rowok) mu = 0.0;
-          if (rowok) mult[row * CP + c] = mu;
+          if ((CYC_MLR_PROBE & 8) == 0 && rowok) mult[row * CP + c] = mu;
           ms[ct] += mu;
         }
       }
@@ -629,8 +713,13 @@ __global__ __launch_bounds__(MT) void k_mlr_margins(
     // chunk nch - 2 (Ws[0]) since the last barrier
     const int64_t next = tile + gridDim.x;
     pre = (nch % 2) == 0 && next < tiles;
+    // the tile's labels and weights, loaded (unconditionally, from a
+    // clamped row) before the W DMA and the stores of the epilogue
+    const int64_t lr = min<int64_t>(r0 + wave * 32 + (lane & 31), n - 1);
+    const double labL = labels[lr];
+    const double wL = weights ? weights[lr] : 1.0;
     if (pre) loadW(0);
-    epilogue(r0);
+    epilogue(r0, labL, wL);
   }
   // per-wave partials: loss/wsum from lanes with (lane & 15) == 0, multSum
   // per class summed over the 4 row groups of the wave.
