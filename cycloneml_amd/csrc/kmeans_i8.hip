@@ -722,14 +722,16 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
   const bool rowOk = r < rows;
   const int64_t myRow = rowOk ? rowAt(r) : 0;   // lane's row (row 0 exists: n > 0)
   {
-    // loads from a valid row, zeroed after the load
+    // loads from a valid row, zeroed after the load; the one-limb pass
+    // with plain loads (3.40 -> 3.30 ms measured against nontemporal ones)
     const bool ok = rowOk;
     const uint4* src = Xq + ((PAIR && (CYC_PROBE_MODE & 8)) ? 0 : myRow) * CH + h;
 #pragma unroll
     for (int s = 0; s < S; ++s)
 #pragma unroll
       for (int L = 0; L < LIMBS; ++L) {
-        const v4u t = __builtin_nontemporal_load((const v4u*)(src + L * (D / 16) + 2 * s));
+        const v4u* a = (const v4u*)(src + L * (D / 16) + 2 * s);
+        const v4u t = PAIR ? *a : __builtin_nontemporal_load(a);
         A[s][L] = ok ? __builtin_bit_cast(v4i, t) : v4i{0, 0, 0, 0};
       }
   }
