@@ -1551,17 +1551,20 @@ __global__ __launch_bounds__(256) void k_screen_cands(
     double margin, const int32_t* __restrict__ candRows, const int32_t* __restrict__ cands,
     const unsigned int* __restrict__ candCount, int32_t* __restrict__ assign,
     int32_t* __restrict__ list, unsigned int* __restrict__ listCount, unsigned int scap) {
-  // 4 rows per wave, 16 lanes per row; lane s of a row holds the dimensions
-  // s, s + 16, ... (each load instruction reads one 128-byte line per row)
+  // 2 rows per wave, 32 lanes per row; lane s of a row holds the dimensions
+  // s, s + 32, ... (each load instruction reads 256 contiguous bytes per
+  // row), and every load of a row -- its x and all kCandMax candidate rows
+  // -- is in flight at once: one memory latency per row after its indices
+  // (4 rows x 16 lanes with the candidates in two batches took three)
   const unsigned cnt = *candCount;
-  const int lane = threadIdx.x & 63, q = lane >> 4, sl = lane & 15;
+  const int lane = threadIdx.x & 63, q = lane >> 5, sl = lane & 31;
   const unsigned nw = (gridDim.x * blockDim.x) >> 6;
   const unsigned w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (scap) {   // this wave's shard (<= 4 rows per grid stride: shard_cap)
     list += (size_t)(w0 % kShards) * scap;
     listCount += (w0 % kShards) * kShardStride;
   }
-  for (unsigned base = w0 * 4; base < cnt; base += nw * 4) {
+  for (unsigned base = w0 * 2; base < cnt; base += nw * 2) {
     const unsigned idx = base + q;
     const bool live = idx < cnt;
     const int64_t row = live ? candRows[idx] : 0;
@@ -1572,49 +1575,51 @@ __global__ __launch_bounds__(256) void k_screen_cands(
 #pragma unroll
     for (int i = 0; i < kCandMax; ++i) bad = bad || ci[i] >= k;   // a padding center
     const double* x = X + row * d;
-    double u[16];
+    double u[8], cv[kCandMax][8];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int j = e * 16 + sl;   // d <= 256
+    for (int e = 0; e < 8; ++e) {
+      const int j = e * 32 + sl;   // d <= 256
       u[e] = (live && j < d) ? x[j] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < kCandMax; ++i) {
+      const int c = ci[i];
+      const bool on = c >= 0 && c < k;
+      const double* cr = C + (int64_t)(on ? c : 0) * d;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int j = e * 32 + sl;
+        cv[i][e] = (on && j < d) ? cr[j] : 0.0;
+      }
     }
     if (unit) {
       const double inv = live ? 1.0 / xnorm[row] : 0.0;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) u[e] = u[e] * inv;
+      for (int e = 0; e < 8; ++e) u[e] = u[e] * inv;
     }
     double xx = 0.0;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) xx += u[e] * u[e];
+    for (int e = 0; e < 8; ++e) xx += u[e] * u[e];
     double part[kCandMax];
 #pragma unroll
-    for (int h = 0; h < kCandMax; h += 3) {
-      double cv[3][16];
+    for (int i = 0; i < kCandMax; ++i) {
+      double s2 = 0.0;
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        const int c = ci[h + i];
-        const bool on = c >= 0 && c < k;
-        const double* cr = C + (int64_t)(on ? c : 0) * d;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int j = e * 16 + sl;
-          cv[i][e] = (on && j < d) ? cr[j] : 0.0;
-        }
+      for (int e = 0; e < 8; ++e) {
+        const double t = cv[i][e] - u[e];
+        s2 += t * t;
       }
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        double s2 = 0.0;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const double t = cv[i][e] - u[e];
-          s2 += t * t;
-        }
-        part[h + i] = s2;
-      }
+      part[i] = s2;
     }
+    // sums over the row's 32 lanes: within each 16-lane row by DPP, then
+    // the two halves
     xx = row16_sum(xx);
+    xx += __shfl_xor(xx, 16);
 #pragma unroll
-    for (int i = 0; i < kCandMax; ++i) part[i] = row16_sum(part[i]);
+    for (int i = 0; i < kCandMax; ++i) {
+      part[i] = row16_sum(part[i]);
+      part[i] += __shfl_xor(part[i], 16);
+    }
     double best = __builtin_inf(), second = __builtin_inf();
     int bi = -1, si = -1;
 #pragma unroll
