@@ -331,9 +331,35 @@ def _kmeans_init_csr_rank(rank, world):
     return C0.shape == ref.shape and bool(np.array_equal(C0, ref))
 
 
+def _silhouette_rank(rank, world):
+    """ClusteringEvaluator over two row shards: the cluster statistics and
+    the two score sums all-reduced (aggregateByKey's combOp, overallScore's
+    sums), the score equal to the one-partition restatement's."""
+    import torch
+    from cycloneml_amd import parallel
+    from cycloneml_amd.evaluation import ClusteringEvaluator
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(7)
+    n, d, k = 30_001, 24, 7
+    C = rng.normal(size=(k, d)) * 3.0
+    p = rng.integers(0, k, size=n).astype(np.int32)
+    X = C[p] + rng.normal(size=(n, d))
+    w = rng.random(n) * 2.0
+    a, b = parallel.shard_bounds(n, rank, world)
+    ok = True
+    for measure, cos in (("squaredEuclidean", False), ("cosine", True)):
+        ev = ClusteringEvaluator(distanceMeasure=measure)
+        s = ev.evaluate(torch.from_numpy(X[a:b].copy()).to(dev),
+                        torch.from_numpy(p[a:b].copy()).to(dev),
+                        torch.from_numpy(w[a:b].copy()).to(dev))
+        ref, _ = oracle.silhouette(X, p, k, w, cosine=cos)
+        ok = ok and abs(s - ref) <= 1e-12 * abs(ref)
+    return bool(ok)
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("fn", [_kmeans_rank, _lr_rank, _gramian_rank, _kmeans_init_rank,
-                                _kmeans_init_csr_rank])
+                                _kmeans_init_csr_rank, _silhouette_rank])
 def test_two_ranks_device_kernels_meet_the_collective(fn):
     out = _run(fn)
     assert out == {0: True, 1: True}, out
