@@ -15,3 +15,11 @@ print({k: round(v, 3) for k, v in r["kernels_ms_per_step"].items()})
 print(d.get("screen_tiers") or r.get("screen_tiers"))
 PY
 echo ALLDONE
+# KM_AB="VAR=value ...": the bench line again with those variables set
+if [ -n "${KM_AB:-}" ]; then
+  env $KM_AB timeout -k 10 300 python -u bench.py --workload kmeans --steps 20 --warmup 5 --cpu-seconds 0 > gpurun_out/bench_km_ab.json 2> gpurun_out/bench_km_ab.err || { echo AB BENCH FAIL; tail -20 gpurun_out/bench_km_ab.err; exit 1; }
+  python -c "
+import json
+d = json.loads(open('gpurun_out/bench_km_ab.json').read().strip().splitlines()[-1])
+print('AB', '$KM_AB', round(d['value'] / 1e6, 1), round(d['ms_per_step'], 3), {k: round(v, 3) for k, v in d['roofline']['kernels_ms_per_step'].items()})"
+fi
