@@ -24,6 +24,9 @@
 #include <algorithm>
 #include <mutex>
 
+#include <cstdlib>
+#include <string>
+
 #include "common.hpp"
 
 namespace {
@@ -129,6 +132,112 @@ __global__ __launch_bounds__(GT, 2) void k_gram_tiles(
   }
 
   // slab layout: [split][tilepair][i (128)][j (128)]
+  const int pairs = tilesPerSide * (tilesPerSide + 1) / 2;
+  double* out = slab + ((size_t)blockIdx.y * pairs + blockIdx.x) * TILE * TILE;
+#pragma unroll
+  for (int qa = 0; qa < 4; ++qa)
+#pragma unroll
+    for (int qb = 0; qb < 4; ++qb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = wy * 64 + qa * 16 + (lane >> 4) + 4 * r;
+        const int j = wx * 64 + qb * 16 + (lane & 15);
+        out[i * TILE + j] = acc[qa][qb][r];
+      }
+}
+
+// The same tiles with the panels DMA'd from HBM straight into LDS
+// (buffer_load ... lds, one 1 KiB row of a panel per wave instruction: no
+// staging registers, no ds_write) into two chunk buffers: the next chunk's
+// DMAs fly during this one's MFMAs, one barrier per chunk, two workgroups
+// per CU.  542.7 -> 515.0 ms at 30M x 1024 on one box; a one-buffer form
+// with three workgroups per CU (164 VGPRs) took 558.6.  A chunk's rows past
+// the split's end read as zero (buffer range); columns past p of the last
+// panel read the next row's values, which only reach tile entries the fold
+// discards.  MEAN: the mean is subtracted as the operands leave LDS (the
+// same dsub as the staged kernel), rows past the end masked to zero.
+// Needs p even (16-byte rows of a panel); odd p takes k_gram_tiles.
+template <bool MEAN>
+__global__ __launch_bounds__(GT, 2) void k_gram_dma(
+    const double* __restrict__ X, int64_t nrows, int p, const double* __restrict__ mean,
+    int tilesPerSide, int64_t rowsPerSplit, double* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) double Pn[2][2][KC * LDSW];
+  int t = blockIdx.x, ti = 0;
+  while (t >= tilesPerSide - ti) { t -= tilesPerSide - ti; ++ti; }
+  const int tj = ti + t;
+  const int I0 = ti * TILE, J0 = tj * TILE;
+  const int64_t r0 = (int64_t)blockIdx.y * rowsPerSplit;
+  const int64_t r1 = min<int64_t>(nrows, r0 + rowsPerSplit);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wy = wave >> 1, wx = wave & 1;
+
+  cyc_double4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+  double mI[4], mJ[4];
+  if constexpr (MEAN) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ci = I0 + wy * 64 + q * 16 + (lane & 15), cj = J0 + wx * 64 + q * 16 + (lane & 15);
+      mI[q] = ci < p ? mean[ci] : 0.0;
+      mJ[q] = cj < p ? mean[cj] : 0.0;
+    }
+  }
+  // chunk rb into buffer b: wave w DMAs rows 4w .. 4w + 3 of both panels
+  auto issue = [&](int64_t rb, int b) {
+    const int64_t nr = min<int64_t>(KC, r1 - rb);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + rb * p), (short)0,
+                                                      (int)(nr * p * 8), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int rr = wave * 4 + u;
+#pragma unroll
+      for (int pn = 0; pn < 2; ++pn)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(Pn[b][pn] + rr * LDSW), 16,
+            (rr * p + (pn ? J0 : I0)) * 8 + lane * 16, 0, 0, 0);
+    }
+  };
+  auto compute = [&](int b, int64_t rb) {
+    const double* Ai = Pn[b][0];
+    const double* Aj = Pn[b][1];
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 4) {
+      double a[4], bb[4];
+      const int krow = kk + (lane >> 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[q] = Ai[krow * LDSW + wy * 64 + q * 16 + (lane & 15)];
+        bb[q] = Aj[krow * LDSW + wx * 64 + q * 16 + (lane & 15)];
+      }
+      if constexpr (MEAN) {
+        const bool ok = rb + krow < r1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          a[q] = ok ? dsub(a[q], mI[q]) : 0.0;
+          bb[q] = ok ? dsub(bb[q], mJ[q]) : 0.0;
+        }
+      }
+#pragma unroll
+      for (int qa = 0; qa < 4; ++qa)
+#pragma unroll
+        for (int qb = 0; qb < 4; ++qb)
+          acc[qa][qb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[qa], bb[qb], acc[qa][qb], 0, 0, 0);
+    }
+  };
+  if (r0 < r1) issue(r0, 0);
+  int b = 0;
+  for (int64_t rb = r0; rb < r1; rb += KC) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // chunk rb landed everywhere; every wave is past rb - KC
+    if (rb + KC < r1) issue(rb + KC, b ^ 1);
+    compute(b, rb);
+    b ^= 1;
+  }
+
   const int pairs = tilesPerSide * (tilesPerSide + 1) / 2;
   double* out = slab + ((size_t)blockIdx.y * pairs + blockIdx.x) * TILE * TILE;
 #pragma unroll
@@ -427,6 +536,10 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   // per split, with the split count whose last round is fullest (36 tile
   // pairs x 57 splits = 2052 workgroups ran 5 rounds, the 5th holding 4;
   // 36 x 71 = 2556 fill 4.99 rounds).
+  // k_gram_dma for even p; CYC_GRAMIAN_KERNEL=tiles selects the staged
+  // k_gram_tiles (a measurement switch)
+  const char* gk = std::getenv("CYC_GRAMIAN_KERNEL");
+  const bool dma = (p % 2) == 0 && !(gk && std::string(gk) == "tiles");
   const int64_t slots = 2 * (int64_t)cyc::device_cus();
   const int64_t lo = std::max<int64_t>(1, (4 * slots + pairs - 1) / pairs);
   int64_t splits = cyc::balanced_splits(pairs, lo, 2 * lo, slots);
@@ -437,8 +550,16 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   if (rc) return rc;
   {
   cyc::KernelTimer timer("k_gram_tiles", st);
-  hipLaunchKernelGGL(k_gram_tiles, dim3(pairs, (unsigned)splits), dim3(GT), 0, st, X, nrows, p,
-                     mean, tps, rps, (double*)plan->slab.ptr);
+  const dim3 grid(pairs, (unsigned)splits);
+  double* slab = (double*)plan->slab.ptr;
+  if (dma && mean)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<true>), grid, dim3(GT), 0, st, X, nrows, p, mean,
+                       tps, rps, slab);
+  else if (dma)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<false>), grid, dim3(GT), 0, st, X, nrows, p,
+                       mean, tps, rps, slab);
+  else
+    hipLaunchKernelGGL(k_gram_tiles, grid, dim3(GT), 0, st, X, nrows, p, mean, tps, rps, slab);
   CYC_LAUNCH_CHECK("k_gram_tiles");
   }
   hipLaunchKernelGGL(k_gram_fold, dim3(TILE * TILE / 256, pairs), dim3(256), 0, st,
