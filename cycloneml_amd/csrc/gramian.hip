@@ -148,20 +148,23 @@ __global__ __launch_bounds__(GT, 2) void k_gram_tiles(
 
 // The same tiles with the panels DMA'd from HBM straight into LDS
 // (buffer_load ... lds, one 1 KiB row of a panel per wave instruction: no
-// staging registers, no ds_write) into two chunk buffers: the next chunk's
-// DMAs fly during this one's MFMAs, one barrier per chunk, two workgroups
-// per CU.  542.7 -> 515.0 ms at 30M x 1024 on one box; a one-buffer form
-// with three workgroups per CU (164 VGPRs) took 558.6.  A chunk's rows past
+// staging registers, no ds_write) into NB = 2 chunk buffers: the next
+// chunk's DMAs fly during this one's MFMAs, one barrier per chunk.  At
+// 30M x 1024 on one box: 8-row chunks with three workgroups per CU (166
+// VGPRs, 36 KB of LDS) 498.0 ms; 16-row chunks, two per CU 515.0; 8-row
+// chunks in three buffers, two per CU 525.8; 16-row chunks in three
+// buffers, one per CU 574.4; the staged k_gram_tiles 542.5.  A chunk's rows past
 // the split's end read as zero (buffer range); columns past p of the last
 // panel read the next row's values, which only reach tile entries the fold
 // discards.  MEAN: the mean is subtracted as the operands leave LDS (the
 // same dsub as the staged kernel), rows past the end masked to zero.
 // Needs p even (16-byte rows of a panel); odd p takes k_gram_tiles.
-template <bool MEAN>
-__global__ __launch_bounds__(GT, 2) void k_gram_dma(
+template <bool MEAN, int KCH = 8, int NB = 2, int OCC = 3>
+__global__ __launch_bounds__(GT, OCC) void k_gram_dma(
     const double* __restrict__ X, int64_t nrows, int p, const double* __restrict__ mean,
     int tilesPerSide, int64_t rowsPerSplit, double* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) double Pn[2][2][KC * LDSW];
+  __shared__ __attribute__((aligned(16))) double Pn[NB][2][KCH * LDSW];
+  constexpr int DPW = KCH / 2;   // DMAs per wave per chunk
   int t = blockIdx.x, ti = 0;
   while (t >= tilesPerSide - ti) { t -= tilesPerSide - ti; ++ti; }
   const int tj = ti + t;
@@ -186,14 +189,14 @@ __global__ __launch_bounds__(GT, 2) void k_gram_dma(
       mJ[q] = cj < p ? mean[cj] : 0.0;
     }
   }
-  // chunk rb into buffer b: wave w DMAs rows 4w .. 4w + 3 of both panels
+  // chunk rb into buffer b: wave w DMAs rows KCH/4 w .. of both panels
   auto issue = [&](int64_t rb, int b) {
-    const int64_t nr = min<int64_t>(KC, r1 - rb);
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + rb * p), (short)0,
+    const int64_t nr = max<int64_t>(0, min<int64_t>(KCH, r1 - rb));
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (nr ? rb : 0) * p), (short)0,
                                                       (int)(nr * p * 8), 0x00020000);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int rr = wave * 4 + u;
+    for (int u = 0; u < KCH / 4; ++u) {
+      const int rr = wave * (KCH / 4) + u;
 #pragma unroll
       for (int pn = 0; pn < 2; ++pn)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -205,7 +208,7 @@ __global__ __launch_bounds__(GT, 2) void k_gram_dma(
     const double* Ai = Pn[b][0];
     const double* Aj = Pn[b][1];
 #pragma unroll
-    for (int kk = 0; kk < KC; kk += 4) {
+    for (int kk = 0; kk < KCH; kk += 4) {
       double a[4], bb[4];
       const int krow = kk + (lane >> 4);
 #pragma unroll
@@ -228,15 +231,21 @@ __global__ __launch_bounds__(GT, 2) void k_gram_dma(
           acc[qa][qb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[qa], bb[qb], acc[qa][qb], 0, 0, 0);
     }
   };
-  if (r0 < r1) issue(r0, 0);
+  // NB - 1 chunks ahead; past the end the DMAs fetch nothing (empty
+  // range), so every wave always has (NB - 2) DPW newer DMAs to leave in
+  // flight at the counted wait
+#pragma unroll
+  for (int c = 0; c < NB - 1; ++c) issue(r0 + c * KCH, c);
   int b = 0;
-  for (int64_t rb = r0; rb < r1; rb += KC) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();   // chunk rb landed everywhere; every wave is past rb - KC
-    if (rb + KC < r1) issue(rb + KC, b ^ 1);
+  for (int64_t rb = r0; rb < r1; rb += KCH) {
+    if constexpr (NB == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * DPW) : "memory");
+    __syncthreads();   // chunk rb landed everywhere; every wave is past rb - KCH
+    issue(rb + (NB - 1) * KCH, b == 0 ? NB - 1 : b - 1);
     compute(b, rb);
-    b ^= 1;
+    b = b == NB - 1 ? 0 : b + 1;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   const int pairs = tilesPerSide * (tilesPerSide + 1) / 2;
   double* out = slab + ((size_t)blockIdx.y * pairs + blockIdx.x) * TILE * TILE;
@@ -540,7 +549,9 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   // k_gram_tiles (a measurement switch)
   const char* gk = std::getenv("CYC_GRAMIAN_KERNEL");
   const bool dma = (p % 2) == 0 && !(gk && std::string(gk) == "tiles");
-  const int64_t slots = 2 * (int64_t)cyc::device_cus();
+  // workgroups per CU: three for k_gram_dma's 8-row form, two for the
+  // 16-row MEAN form (the mean operands spill at three) and k_gram_tiles
+  const int64_t slots = (dma && !mean ? 3 : 2) * (int64_t)cyc::device_cus();
   const int64_t lo = std::max<int64_t>(1, (4 * slots + pairs - 1) / pairs);
   int64_t splits = cyc::balanced_splits(pairs, lo, 2 * lo, slots);
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, nrows / 64));
@@ -553,8 +564,8 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   const dim3 grid(pairs, (unsigned)splits);
   double* slab = (double*)plan->slab.ptr;
   if (dma && mean)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<true>), grid, dim3(GT), 0, st, X, nrows, p, mean,
-                       tps, rps, slab);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<true, 16, 2, 2>), grid, dim3(GT), 0, st, X, nrows,
+                       p, mean, tps, rps, slab);
   else if (dma)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<false>), grid, dim3(GT), 0, st, X, nrows, p,
                        mean, tps, rps, slab);
