@@ -49,7 +49,10 @@ def test_covariance_accuracy(cuda):
 
 
 @pytest.mark.parametrize("n,p", [(1, 1), (100, 3), (1000, 64), (777, 130), (5000, 257),
-                                 (20000, 512), (3000, 1024)])
+                                 (20000, 512), (3000, 1024),
+                                 # even widths take k_gram_dma (8-row LDS-DMA chunks):
+                                 # one row, rows not a multiple of 8, tiny and ragged panels
+                                 (1, 2), (9, 128), (37, 256), (10001, 130), (15, 2)])
 def test_gramian_vs_oracle(cuda, n, p):
     from cycloneml_amd.linalg import RowMatrix
     rng = np.random.default_rng(n + p)
@@ -59,7 +62,7 @@ def test_gramian_vs_oracle(cuda, n, p):
     np.testing.assert_allclose(U, R, rtol=1e-12)
 
 
-@pytest.mark.parametrize("n,p", [(500, 7), (4000, 200)])
+@pytest.mark.parametrize("n,p", [(500, 7), (4000, 200), (13, 2), (1001, 130)])
 def test_covariance_vs_oracle(cuda, n, p):
     from cycloneml_amd.linalg import RowMatrix
     rng = np.random.default_rng(p)
