@@ -2,7 +2,10 @@
 # of all four workloads with CPU baselines (PART=bench), or both (default).
 # The maintained tools: prof.sh (rocprofv3 stats + FETCH/WRITE passes),
 # pmc_summary.py, pmc_kernel.sh / pmc_mfma.sh / pmc_pass.sh (SQ counters),
-# asm_mix.py (ISA mix), probe/ (MFMA layout probes).
+# gpu_km.sh / gpu_lr.sh / gpu_gram.sh (one workload's GPU tests + bench line),
+# ab_km.sh (KMeans bench under environment switches), ab_lib.sh (a bench
+# line per library variant), asm_mix.py (ISA mix), probe/ + probe_*.sh
+# (kernel timing probes), screen_probe.py, rocpd_stats.py.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
