@@ -291,6 +291,53 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
     rB = run_of(k1, c1);
   }
   load_run(vidx, vvals, rB, 0, lane, iB, vB);
+  // The binary logistic epilogue (kind 0: BinaryLogisticBlockAggregator.
+  // scala:104-122) without branches, EB rows at a time with the next EB
+  // rows' labels and weights loaded before this batch's multiplier stores
+  // (vmcnt waits are in issue order: a load issued after a store waits for
+  // it too).  log1pExp(x) (ml/impl/Utils.scala:91-97) as max(x, 0) +
+  // log1p(exp(-|x|)): the same two branches, the same bits (0 + y == y for
+  // the x <= 0 one).  Rows are visited in the plain loop's order, so the
+  // sums are the same bits as well.
+  auto logistic_epilogue = [&](int64_t r0) {
+    constexpr int EB = 4;
+    double lab[2][EB], wt[2][EB];
+    auto ld = [&](int i0, double (&l)[EB], double (&w)[EB]) {
+#pragma unroll
+      for (int u = 0; u < EB; ++u) {
+        const int64_t rr = min<int64_t>(r0 + tid + (int64_t)kTPB * (i0 + u), v.n - 1);
+        l[u] = labels[rr];
+        w[u] = weights ? weights[rr] : 1.0;
+      }
+    };
+    ld(0, lab[0], wt[0]);
+#pragma unroll
+    for (int i0 = 0; i0 < kDPT; i0 += EB) {
+      const int cb = (i0 / EB) & 1;
+      if (i0 + EB < kDPT) ld(i0 + EB, lab[cb ^ 1], wt[cb ^ 1]);
+#pragma unroll
+      for (int u = 0; u < EB; ++u) {
+        const int rl = tid + kTPB * (i0 + u);
+        const int64_t r = r0 + rl;
+        const double label = lab[cb][u], w = wt[cb][u];
+        const double margin = fitIntercept ? offset + dots[rl] : dots[rl];
+        const double x = -margin;
+        const double lp = __builtin_fmax(x, 0.0) + log1p(exp(-__builtin_fabs(x)));
+        const double term = label > 0 ? lp : lp + margin;
+        const double mm = w * (1.0 / (1.0 + exp(-margin)) - label);
+        if (r < v.n) {
+          acc[1] += w;
+          double m = 0.0;
+          if (w > 0) {
+            acc[0] += w * term;
+            m = mm;
+          }
+          acc[2] += m;
+          mult[r] = m;
+        }
+      }
+    }
+  };
   for (int64_t k = 0; k < mySB; ++k) {          // one super block per pass
 #pragma unroll
     for (int i = 0; i < kDPT; ++i) dots[tid + kTPB * i] = 0.0;
@@ -302,6 +349,11 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
     }
     // epilogue (BinaryLogisticBlockAggregator.scala:104-122 and siblings)
     const int64_t r0 = ((int64_t)blockIdx.x + k * gridDim.x) * kTileSuperRows;
+    if (kind == 0) {
+      logistic_epilogue(r0);
+      __syncthreads();                          // dots read before the next zeroing
+      continue;
+    }
     for (int i = 0; i < kDPT; ++i) {
       const int rl = tid + kTPB * i;
       const int64_t r = r0 + rl;
