@@ -9,6 +9,8 @@ with its own data resident in HBM and freed before the next:
                findClosest for every row, per-cluster sums/weights/cost,
                merge, centroid update)
   gramian      RowMatrix.computeGramianMatrix pass (configs[2]: 100M x 1024)
+  pca          RowMatrix.computeCovariance, the PCA variant of configs[2], on
+               the same rows (mean pass, isSparseMatrix, centred syrk)
   lr_multi     multinomial LR, 100 classes, 512 dense features (configs[3]:
                50M rows); one RDDLossFunction.calculate per step
   lr_sparse    binomial LR on CSR, 1M features, 64 nnz/row (configs[4]: 200M
@@ -24,7 +26,9 @@ at the largest shard one GPU holds resident (Gramian: 30M rows = 246 GB, so
 100M rows need N >= 4 to be whole).  --scaling weak|strong forces one mode
 for every workload; --rows overrides the rows per GPU.
 With --gpus N (one process per GPU via torch.distributed.run) the merge is
-one RCCL all-reduce per iteration.
+one RCCL all-reduce per iteration over libcyclone's communicator (cyc_comm,
+the only RCCL communicator per GPU); torch.distributed runs on gloo for the
+rendezvous, the RCCL id and the host barriers.
 
 Prints ONE JSON line on rank 0.  `roofline` is for the workload's dominant
 kernel (the slowest of its priced kernels), timed with HIP events on the
@@ -52,14 +56,17 @@ HBM = ("hbm", "GB/s", HBM_PEAK_GBS, 1e9)
 FP64 = ("mfma", "TFLOP/s", FP64_PEAK_TFLOPS, 1e12)
 I8 = ("mfma", "TOPS", I8_PEAK_TOPS, 1e12)
 
-ORDER = ("kmeans", "gramian", "lr_multi", "lr_sparse")
+DIST_BACKEND = "gloo"     # torch.distributed's group: host only, no second RCCL communicator
+ORDER = ("kmeans", "gramian", "pca", "lr_multi", "lr_sparse")
 # BASELINE configs: rows of the whole problem, and whether it is per GPU
-CONFIG_ROWS = {"kmeans": 10_000_000, "gramian": 100_000_000, "lr_multi": 50_000_000,
-               "lr_sparse": 200_000_000}
-PER_GPU_CONFIG = {"kmeans": True, "gramian": False, "lr_multi": False, "lr_sparse": False}
+# (pca: the PCA variant of configs[2], on the same rows as gramian)
+CONFIG_ROWS = {"kmeans": 10_000_000, "gramian": 100_000_000, "pca": 100_000_000,
+               "lr_multi": 50_000_000, "lr_sparse": 200_000_000}
+PER_GPU_CONFIG = {"kmeans": True, "gramian": False, "pca": False, "lr_multi": False,
+                  "lr_sparse": False}
 # the largest shard one MI355X holds resident (288 GB HBM)
-MAX_RESIDENT_ROWS = {"kmeans": 10_000_000, "gramian": 30_000_000, "lr_multi": 50_000_000,
-                     "lr_sparse": 200_000_000}
+MAX_RESIDENT_ROWS = {"kmeans": 10_000_000, "gramian": 30_000_000, "pca": 30_000_000,
+                     "lr_multi": 50_000_000, "lr_sparse": 200_000_000}
 
 
 def parse(argv=None):
@@ -148,6 +155,51 @@ def kmeans_data(n, dev, rank=0, d=256, k=1024):
         X[s:e] = true_c[lab] + torch.randn(e - s, d, generator=gr, device=dev,
                                            dtype=torch.float64)
     return X
+
+
+def gramian_data(n, dev, rank=0, p=1024):
+    """BASELINE config 3 / SURVEY 8d rows: U[0, 1) fp64 n x p, torch Philox
+    seeded 77 + rank, 1M-row chunks (tests/test_gramian_gpu.py checks the
+    Gramian and the covariance on these rows)."""
+    import torch
+    g = torch.Generator(device=dev).manual_seed(77 + rank)
+    X = torch.empty(n, p, dtype=torch.float64, device=dev)
+    for s in range(0, n, 1 << 20):
+        e = min(n, s + (1 << 20))
+        X[s:e] = torch.rand(e - s, p, generator=g, device=dev, dtype=torch.float64)
+    return X
+
+
+def lr_multi_data(n, dev, rank=0, F=512, C=100):
+    """BASELINE config 4 / SURVEY 8d rows: X ~ N(0, 1) fp64 n x F (seeded
+    500 + rank, 512K-row chunks), labels drawn from softmax(X W) for
+    W ~ N(0, 1/F) seeded 11; and scaledMean = mean / std per feature over
+    every rank's rows (the Summarizer pre-pass of LogisticRegression.scala:
+    511-516, :957-960: the unbiased variance of Summarizer.scala:673-690),
+    a device tensor.  Returns (X, labels, scaledMean)."""
+    import torch
+    from cycloneml_amd import parallel
+    g = torch.Generator(device=dev).manual_seed(11)
+    Wt = torch.randn(F, C, generator=g, device=dev, dtype=torch.float64) / F ** 0.5
+    gr = torch.Generator(device=dev).manual_seed(500 + rank)
+    X = torch.empty(n, F, dtype=torch.float64, device=dev)
+    y = torch.empty(n, dtype=torch.float64, device=dev)
+    for s in range(0, n, 1 << 19):
+        e = min(n, s + (1 << 19))
+        X[s:e] = torch.randn(e - s, F, generator=gr, device=dev, dtype=torch.float64)
+        pr = torch.softmax(X[s:e] @ Wt, dim=1)
+        y[s:e] = torch.multinomial(pr, 1, generator=gr).squeeze(1).to(torch.float64)
+    mean = torch.zeros(F, dtype=torch.float64, device=dev)
+    sq = torch.zeros(F, dtype=torch.float64, device=dev)
+    for s in range(0, n, 1 << 22):
+        mean += X[s:s + (1 << 22)].sum(0)
+        sq += (X[s:s + (1 << 22)] ** 2).sum(0)
+    tot = torch.cat([mean, sq, torch.tensor([float(n)], dtype=torch.float64, device=dev)])
+    parallel.allreduce_(tot)                   # the summary over every rank's rows
+    s1, s2, n_all = tot[:F], tot[F:2 * F], tot[2 * F]
+    mean = s1 / n_all
+    std = ((s2 - n_all * mean ** 2) / (n_all - 1)).clamp_min(0).sqrt()
+    return X, y, mean / std
 
 
 LR_SPARSE_CHUNK = 64 * 8192            # whole row blocks of the tiles layout per append
@@ -253,6 +305,17 @@ class KMeansWorkload:
     def after_timing(self):
         self._refine = self.plan.last_refine()
 
+    def fit_once(self, max_iter=20):
+        """One fit as the ml estimator runs it -- maxIter 20, tol 1e-4
+        (ml/clustering/KMeans.scala:89, :336-343) -- from setInitialModel
+        (rows 0..k-1): the cached norms, the plan and row image, then every
+        Lloyd iteration (mllib/clustering/KMeans.scala:263-334) with its
+        convergence check read back on the host.  Returns the iterations run."""
+        from cycloneml_amd.clustering import KMeans, KMeansModel
+        km = KMeans(k=self.k, maxIterations=max_iter, epsilon=1e-4)
+        km.setInitialModel(KMeansModel(self.C0.cpu().numpy()))
+        return km.run(self.X).numIter
+
     def extra_roofline(self, launches_per_step, avg_s):
         import torch
         listed, full, union = self._refine
@@ -306,21 +369,15 @@ class KMeansWorkload:
 
 
 class GramianWorkload:
-    # the syrk launch is timed as k_gram_tiles; at p = 1024 it runs
-    # k_gram_dma (gramian.hip), the name in the rocprofv3 summaries
-    kernel = "k_gram_tiles"
-    pmc_names = {"k_gram_tiles": "k_gram_dma"}
+    # at p = 1024 the syrk is k_gram_dma (gramian.hip, 8-row LDS-DMA chunks)
+    kernel = "k_gram_dma"
 
     def __init__(self, n, dev, rank):
         import torch
         from cycloneml_amd import parallel
         from cycloneml_amd.linalg import GramianPlan
         self.n, self.p = n, 1024
-        g = torch.Generator(device=dev).manual_seed(77 + rank)
-        self.X = torch.empty(n, self.p, dtype=torch.float64, device=dev)
-        for s in range(0, n, 1 << 20):
-            e = min(n, s + (1 << 20))
-            self.X[s:e] = torch.rand(e - s, self.p, generator=g, device=dev, dtype=torch.float64)
+        self.X = gramian_data(n, dev, rank, self.p)
         self.U = torch.zeros(self.p * (self.p + 1) // 2, dtype=torch.float64, device=dev)
         self.plan = GramianPlan(self.p)
         self.parallel = parallel
@@ -357,44 +414,90 @@ class GramianWorkload:
                           f"{threads} partitions on {threads} threads, {el:.1f} s"}
 
 
+class PCAWorkload:
+    """The PCA variant of BASELINE configs[2]: RowMatrix.computeCovariance
+    (RowMatrix.scala:452-467) per step on the Gramian workload's rows -- the
+    column-mean pass (Statistics.colStats, :456), isSparseMatrix (:462, a
+    take(1): one 64K-row round on dense rows), the centred syrk
+    (computeDenseVectorCovariance, :163-220: k_gram_dma with the mean
+    subtracted as the operands leave LDS), the all-reduce and the (m - 1)
+    finish into the n x n matrix in HBM.  The breeze SVD of
+    computePrincipalComponentsAndExplainedVariance (:499-501) runs on the
+    driver in the reference; here it is the host eigensolve, timed once
+    outside the steps (eigensolve_ms)."""
+    kernel = "k_gram_dma_cov"
+    kernels = ("k_gram_dma_cov", "k_col_sums")
+    pmc_names = {"k_gram_dma_cov": "k_gram_dma"}
+
+    def __init__(self, n, dev, rank):
+        from cycloneml_amd.linalg import RowMatrix
+        self.n, self.p = n, 1024
+        self.X = gramian_data(n, dev, rank, self.p)
+        self.mat = RowMatrix(self.X)
+        self.G = None
+
+    def step(self):
+        self.G = self.mat.computeCovarianceDevice()
+
+    def work(self, kname, launches_per_step):
+        if kname == "k_col_sums":             # every row once (fp64)
+            return float(self.n) * self.p * 8 / launches_per_step, HBM
+        return float(self.n) * self.p * (self.p + 1) / launches_per_step, FP64   # flops (upper)
+
+    def after_timing(self):
+        import numpy as np
+        cov = self.G.cpu().numpy()
+        t0 = time.perf_counter()
+        _, s, _ = np.linalg.svd(cov)              # the driver's brzSvd(Cov) (:501)
+        self.eig_ms = (time.perf_counter() - t0) * 1e3
+        self.explained_top3 = (s[:3] / s.sum()).tolist()
+
+    def extra_roofline(self, launches_per_step, avg_s):
+        return {"eigensolve_ms": self.eig_ms, "explained_variance_top3": self.explained_top3,
+                "note": "step = computeCovariance on the device (mean pass, isSparseMatrix "
+                        "take(1), centred syrk, finish); the host SVD is timed once, outside"}
+
+    def describe(self):
+        return (f"RowMatrix.computeCovariance (PCA variant), dense fp64 {self.n} x {self.p} rows "
+                "per GPU, U[0,1) (BASELINE configs[2]: 100M rows in total, split over the GPUs; "
+                "one GPU holds at most a 30M-row shard, 246 GB)")
+
+    def cpu_baseline(self, seconds):
+        import numpy as np
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        threads = cpu_threads()
+        mean = (self.X[:1 << 20].sum(0) / (1 << 20)).cpu().numpy()
+        Xs = np.ascontiguousarray(self.X[:200].cpu().numpy())
+        t0 = time.perf_counter()
+        oracle.gramian_partition(Xs, mean)
+        per_row = (time.perf_counter() - t0) / 200
+        rows = int(min(self.n, 1_500_000, max(threads * 50, seconds * threads / per_row)))
+        rows -= rows % threads
+        Xs = np.ascontiguousarray(self.X[:rows].cpu().numpy())
+        parts = np.array_split(Xs[:rows], threads)
+        el, _ = timed_parallel(lambda x: oracle.gramian_partition(x, mean), parts, threads)
+        return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
+                "sample": f"{rows} rows x 1024 of the same data, x - mean then per-row netlib "
+                          f"dspr (computeDenseVectorCovariance's seqOp) as {threads} partitions "
+                          f"on {threads} threads, {el:.1f} s; the mean pass not included"}
+
+
 class LRMultiWorkload:
     kernel = "k_mlr_margins"
     kernels = ("k_mlr_margins", "k_mlr_grad")
 
     def __init__(self, n, dev, rank):
-        import torch
         from cycloneml_amd.optim import (DeviceInstanceBlock, MultinomialLogisticBlockAggregator,
                                          RDDLossFunction)
         self.n, self.F, self.C = n, 512, 100
         F, C = self.F, self.C
-        g = torch.Generator(device=dev).manual_seed(11)
-        Wt = torch.randn(F, C, generator=g, device=dev, dtype=torch.float64) / F ** 0.5
-        gr = torch.Generator(device=dev).manual_seed(500 + rank)
-        X = torch.empty(n, F, dtype=torch.float64, device=dev)
-        y = torch.empty(n, dtype=torch.float64, device=dev)
-        for s in range(0, n, 1 << 19):
-            e = min(n, s + (1 << 19))
-            X[s:e] = torch.randn(e - s, F, generator=gr, device=dev, dtype=torch.float64)
-            pr = torch.softmax(X[s:e] @ Wt, dim=1)
-            y[s:e] = torch.multinomial(pr, 1, generator=gr).squeeze(1).to(torch.float64)
+        # scaledMean = mean / std per feature (the Summarizer pre-pass), untimed
+        X, y, sm_dev = lr_multi_data(n, dev, rank, F, C)
         self.block = DeviceInstanceBlock(y, None, X=X)
         import numpy as np
         self.coef = np.random.default_rng(3).normal(size=C * F + C) * 0.01
-        # scaledMean = mean / std per feature of the shard (the Summarizer
-        # pre-pass of LogisticRegression.scala:511-516, :957-960), untimed
-        mean = torch.zeros(F, dtype=torch.float64, device=dev)
-        sq = torch.zeros(F, dtype=torch.float64, device=dev)
-        for s in range(0, n, 1 << 22):
-            mean += X[s:s + (1 << 22)].sum(0)
-            sq += (X[s:s + (1 << 22)] ** 2).sum(0)
-        from cycloneml_amd import parallel
-        tot = torch.cat([mean, sq, torch.tensor([float(n)], dtype=torch.float64, device=dev)])
-        parallel.allreduce_(tot)                   # the summary over every rank's rows
-        mean, sq, n_all = tot[:F], tot[F:2 * F], tot[2 * F]
-        mean = mean / n_all
-        std = (sq / n_all - mean ** 2).clamp_min(0).sqrt()
-        sm_dev = mean / std                                        # bcScaledMean, once
-        self.scaledMean = sm_dev.cpu().numpy()
+        self.scaledMean = sm_dev.cpu().numpy()                     # bcScaledMean, once
         self.fn = RDDLossFunction([self.block], lambda c: MultinomialLogisticBlockAggregator(
             np.ones(F), sm_dev, True, True, c, device=dev))
 
@@ -444,7 +547,8 @@ class LRMultiWorkload:
 class LRSparseWorkload:
     """BASELINE configs[4] at full size on one GPU: 200M CSR rows x 1M
     features, 64 nonzeros per row, fitIntercept => fitWithMean
-    (LogisticRegression.scala:950-954) with a scaledMean of the data's scale.
+    (LogisticRegression.scala:950-954) with a synthetic scaledMean of the
+    data's scale (U(0, 0.014) per feature, not computed from the rows).
     The shard lives only in the row-block x column-tile layout (tiles.hip):
     it is generated on the device 512K rows at a time, appended, and each
     CSR chunk freed (157 GB resident for 200M rows).  Both passes are priced
@@ -543,8 +647,8 @@ class LRSparseWorkload:
                           f"pass(es), {el:.1f} s"}
 
 
-WORKLOADS = {"kmeans": KMeansWorkload, "gramian": GramianWorkload, "lr_multi": LRMultiWorkload,
-             "lr_sparse": LRSparseWorkload}
+WORKLOADS = {"kmeans": KMeansWorkload, "gramian": GramianWorkload, "pca": PCAWorkload,
+             "lr_multi": LRMultiWorkload, "lr_sparse": LRSparseWorkload}
 
 
 def launch_ranks(args) -> int:
@@ -599,6 +703,25 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
 
     if hasattr(wl, "after_timing"):
         wl.after_timing()
+    fit = None
+    if hasattr(wl, "fit_once"):
+        # a whole fit beside the steady-state iterations (same clock rules)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        iters = wl.fit_once()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        fel = parallel.max_over_ranks(time.perf_counter() - t0, dev)
+        fit = {"fit_ms": fel * 1e3, "iterations": iters,
+               "fit_ms_per_iteration": fel * 1e3 / max(iters, 1),
+               "rows_per_s_per_iteration": total_rows * iters / fel,
+               "note": "one fit from setInitialModel (rows 0..k-1), maxIter 20, tol 1e-4: "
+                       "norms + plan + row image + every iteration with its host convergence "
+                       "check, over iterations 1..maxIter (value times steady-state iterations "
+                       "after the warmup)"}
     # dominant kernel: the slowest of the priced kernels, in its own units
     priced = [k for k in kernels if prof[k][1] and wl.work(k, 1) is not None]
     kname = max(priced, key=lambda k: prof[k][0]) if priced else wl.kernel
@@ -645,6 +768,9 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
     }
     if getattr(wl, "prep", None):
         out["prep_ms"] = wl.prep
+    if fit is not None:
+        out["fit"] = fit
+        out["fit_ms_per_iteration"] = fit["fit_ms_per_iteration"]
     if hasattr(wl, "close"):
         wl.close()
     del wl
@@ -666,11 +792,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        # host-side group only (rendezvous, RCCL id, barriers): every device
+        # collective goes through libcyclone's communicator below
+        dist.init_process_group(DIST_BACKEND)
 
     from cycloneml_amd import _native as N
     from cycloneml_amd import parallel

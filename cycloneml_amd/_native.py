@@ -137,6 +137,7 @@ SIGNATURES = {
                                                               _vp, _vp, _vp, _vp, _vp]),
     "cyc_multinomial_logistic_add_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64,
                                                             _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "cyc_softmax_exp_dev": (ctypes.c_int, [_vp, _i64, _vp, _vp]),
     "cyc_csc_features": (_i32, [_vp]),
     "cyc_tiles_create": (ctypes.c_int, [_i32, _i64, _i64, ctypes.POINTER(_vp)]),
     "cyc_tiles_append_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp]),

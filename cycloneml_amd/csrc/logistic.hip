@@ -454,10 +454,15 @@ __constant__ double kExp2Tab[32] = {
 // e^r by its degree-6 Taylor polynomial (truncation < 2^-57 relative),
 // 2^(j/32) from the LDS table T: within a few ulp, against Math.exp's 1 ulp
 // in the reference -- far inside the aggregator's 1e-10 bar -- at 15 f64
-// VALU where the libm exp takes ~23.  Below -708 (terms under 1e-307 of the
-// largest, 1.0) it returns 0; NaN stays NaN.
+// VALU where the libm exp takes ~23.  Below -708.4 the result is subnormal:
+// the final ldexp rounds it onto the subnormal grid (a second rounding, and
+// past kd = 2^15 the reduction's high product is no longer exact: a relative
+// error of ~1e-13 there), so a label whose probability is subnormal keeps
+// the reference's finite -log(p).  Below -746 (where e^x rounds to 0 in any
+// libm) it returns 0, so -inf gives 0; NaN stays NaN.  tests/
+// test_logistic_gpu.py sweeps it against the host libm.
 __device__ __forceinline__ double exp_neg(double x, const double* __restrict__ T) {
-  if (x < -708.0) return 0.0;
+  if (x < -746.0) return 0.0;
   const double kd = __builtin_rint(x * 46.16624130844683);   // 32 / ln2
   double r = __builtin_fma(kd, -0.021660849392446835, x);
   r = __builtin_fma(kd, -5.145609244655338e-14, r);
@@ -470,6 +475,16 @@ __device__ __forceinline__ double exp_neg(double x, const double* __restrict__ T
   q = __builtin_fma(q, r, 1.0);
   q = __builtin_fma(q, r, 1.0);
   return __builtin_ldexp(T[k & 31] * q, k >> 5);
+}
+
+// exp_neg over an array (cyc_softmax_exp_dev: its accuracy test)
+__global__ void k_softmax_exp(const double* __restrict__ x, int64_t n, double* __restrict__ out) {
+  __shared__ double T[32];
+  if (threadIdx.x < 32) T[threadIdx.x] = kExp2Tab[threadIdx.x];
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = exp_neg(x[i], T);
 }
 
 constexpr int MR = 256;    // rows per margin tile (8 waves x 32 rows)
@@ -1752,6 +1767,16 @@ int cyc_multinomial_logistic_add_csr_dev(cyc_logistic_plan p, const int64_t* row
   hipLaunchKernelGGL(k_add_scalars, dim3(1), dim3(1), 0, st, (const double*)p->scal.ptr, lossSum,
                      weightSum);
   CYC_LAUNCH_CHECK("k_add_scalars");
+  return CYC_OK;
+}
+
+int cyc_softmax_exp_dev(const double* x, int64_t n, double* out, void* stream) {
+  CYC_REQUIRE(n >= 0 && (n == 0 || (x && out)), "n >= 0 and non-null buffers");
+  if (n == 0) return CYC_OK;
+  const int64_t grid = std::min<int64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_softmax_exp, dim3((unsigned)grid), dim3(256), 0, cyc::as_stream(stream), x,
+                     n, out);
+  CYC_LAUNCH_CHECK("k_softmax_exp");
   return CYC_OK;
 }
 

@@ -28,8 +28,8 @@ _EVAL_MEASURES = {SQUARED_EUCLIDEAN.lower(): EUCLIDEAN, COSINE: COSINE}
 
 class ClusteringMetrics:
     """ClusteringMetrics (ClusteringMetrics.scala:34-60) over device rows X
-    (n x d fp64), predictions (n, integer cluster ids in [0, k)) and weights
-    (n fp64 or None: lit(1.0))."""
+    (n x d fp64), predictions (n, integer cluster ids; in [0, k) when k is
+    given) and weights (n fp64 or None: lit(1.0))."""
 
     def __init__(self, X, predictions, weights=None, k=None):
         self.X = X
@@ -50,39 +50,74 @@ class ClusteringMetrics:
 
     def silhouette(self, stream=None) -> float:
         """ClusteringMetrics.silhouette (:48-60): SquaredEuclideanSilhouette
-        or CosineSilhouette .computeSilhouetteScore."""
+        or CosineSilhouette .computeSilhouetteScore.
+
+        Prediction ids may be any integers (the reference keys its cluster
+        statistics by the prediction value, ClusteringMetrics.scala:299-337):
+        with k=None they are mapped to 0..K-1 in sorted order over every
+        rank's ids (the clustersStatsMap keys), which leaves the score as
+        is; a given k asserts ids in [0, k) instead.  The device statistics
+        sort handles K <= MAX_CLUSTERS distinct ids."""
         torch = _torch()
         X = self.X
         if X.dtype != torch.float64 or not X.is_cuda or X.dim() != 2:
             raise N.IllegalArgumentException("requirement failed: features must be a device "
                                              "fp64 matrix (n x d)")
         n, d = int(X.shape[0]), int(X.shape[1])
-        pred = self.predictions.to(device=X.device, dtype=torch.int32).contiguous()
+        pred = self.predictions.to(device=X.device)
         w = None
         if self.weights is not None:
             w = self.weights.to(device=X.device, dtype=torch.float64).contiguous()
         X = X.contiguous()
-        # the cluster ids: at least every predicted id, on every rank
         k = self.k
         if k is None:
-            local = int(pred.max().item()) + 1 if n > 0 else 0
-            k = max(parallel.allgather_object(local))
+            pred, k = dense_cluster_ids(pred)
+        else:
+            pred = pred.to(torch.int32).contiguous()
         k = max(int(k), 1)
+        if k > MAX_CLUSTERS:
+            raise N.IllegalArgumentException(
+                f"requirement failed: the device Silhouette supports at most {MAX_CLUSTERS} "
+                f"distinct cluster ids, got {k}")
         measure = _EVAL_MEASURES[self.distanceMeasure.lower()]
         plan = KMeansPlan(d, k, max(n, 1), distanceMeasure=measure)
-        lib = N.load()
-        s = N.stream_handle(stream)
-        stats = torch.zeros(k * d + 3 * k, dtype=torch.float64, device=X.device)
-        N.check(lib.cyc_kmeans_silhouette_stats_dev(plan.handle, N.ptr(X), None, n, N.ptr(pred),
-                                                    N.ptr(w), N.ptr(stats), s))
-        parallel.allreduce_(stats)   # combOp across executors
-        partial = torch.zeros(2, dtype=torch.float64, device=X.device)
-        N.check(lib.cyc_kmeans_silhouette_score_dev(plan.handle, N.ptr(X), None, n, N.ptr(pred),
-                                                    N.ptr(w), N.ptr(stats), N.ptr(partial), s))
-        parallel.allreduce_(partial)
-        total = partial.cpu()
-        plan.close()
+        try:
+            lib = N.load()
+            s = N.stream_handle(stream)
+            stats = torch.zeros(k * d + 3 * k, dtype=torch.float64, device=X.device)
+            # the per-rank input checks (ids in range, checkNonNegativeWeight)
+            # run first inside the stats call: agreed across ranks before the
+            # all-reduce, so every rank raises the same error
+            parallel.agree(lambda: N.check(lib.cyc_kmeans_silhouette_stats_dev(
+                plan.handle, N.ptr(X), None, n, N.ptr(pred), N.ptr(w), N.ptr(stats), s)))
+            parallel.allreduce_(stats)   # combOp across executors
+            partial = torch.zeros(2, dtype=torch.float64, device=X.device)
+            # the one-cluster assert reads the merged statistics: every rank agrees
+            N.check(lib.cyc_kmeans_silhouette_score_dev(plan.handle, N.ptr(X), None, n,
+                                                        N.ptr(pred), N.ptr(w), N.ptr(stats),
+                                                        N.ptr(partial), s))
+            parallel.allreduce_(partial)
+            total = partial.cpu()
+        finally:
+            plan.close()
         return float(total[0]) / float(total[1])
+
+
+# the device counting sort's bound on distinct cluster ids (KMeansPlan's k)
+MAX_CLUSTERS = 8192
+
+
+def dense_cluster_ids(pred):
+    """(ids in 0..K-1, K): every rank's distinct integer predictions, sorted
+    and numbered, and this shard's predictions mapped onto them."""
+    torch = _torch()
+    p = pred.to(torch.int64).reshape(-1)
+    mine = torch.unique(p).cpu().tolist()
+    keys = sorted(set().union(*[set(g) for g in parallel.allgather_object(mine)]))
+    if not keys:
+        return p.to(torch.int32), 1
+    kt = torch.tensor(keys, dtype=torch.int64, device=p.device)
+    return torch.searchsorted(kt, p).to(torch.int32).contiguous(), len(keys)
 
 
 class ClusteringEvaluator:

@@ -96,6 +96,14 @@ class RowMatrix:
         self.rows = rows
         self._nRows = nRows
         self._nCols = nCols
+        self._plan_ = None
+
+    def _plan(self) -> GramianPlan:
+        """One syrk plan per matrix: its split-K slab is reused by every pass."""
+        n = self.numCols()
+        if self._plan_ is None or self._plan_.p != n:
+            self._plan_ = GramianPlan(n)
+        return self._plan_
 
     @property
     def _sparse(self):
@@ -143,7 +151,7 @@ class RowMatrix:
         n = self.numCols()
         self._checkNumColumns(n)
         U = torch.zeros(n * (n + 1) // 2, dtype=torch.float64, device=self._device)
-        plan = GramianPlan(n)
+        plan = self._plan()
         if self._sparse:
             plan.accumulate_csr(self.rows, U, mean)
         else:
@@ -164,34 +172,66 @@ class RowMatrix:
         n = self.numCols()
         s = torch.zeros(n, dtype=torch.float64, device=self._device)
         if self._sparse:
-            GramianPlan(n).col_sums_csr(self.rows, s)
+            self._plan().col_sums_csr(self.rows, s)
         else:
-            GramianPlan(n).col_sums(self.rows, s)
+            self._plan().col_sums(self.rows, s)
         parallel.allreduce_(s)
         m = self.numRows()
         return s / m, m
 
-    def isSparseMatrix(self) -> bool:
-        """RowMatrix.isSparseMatrix (:439-441): no row has sparsity() < 0.5
-        (over all ranks)."""
+    # rows of the first isSparseMatrix round per rank, and the growth factor
+    SPARSITY_SCAN_FIRST = 1 << 16
+    SPARSITY_SCAN_GROWTH = 4
+
+    def _dense_rows(self, a: int, b: int):
+        """Rows of [a, b) of this shard with sparsity() < 0.5 (device count)."""
         torch = _torch()
         cnt = torch.zeros(1, dtype=torch.int64, device=self._device)
+        if b > a:
+            if self._sparse:
+                N.check(N.load().cyc_rowmatrix_dense_rows_dev(
+                    None, N.ptr(self.rows.rowptr[a:b + 1]), N.ptr(self.rows.values), b - a,
+                    self.numCols(), N.ptr(cnt), N.stream_handle()))
+            else:
+                N.check(N.load().cyc_rowmatrix_dense_rows_dev(
+                    N.ptr(self.rows[a:b]), None, None, b - a, self.numCols(), N.ptr(cnt),
+                    N.stream_handle()))
+        return cnt
+
+    def isSparseMatrix(self) -> bool:
+        """RowMatrix.isSparseMatrix (:439-442): rows.filter(_.sparsity() < 0.5)
+        .isEmpty().  isEmpty is take(1) (RDD.scala:1577-1579, :1443-1478): Spark
+        scans one partition, then 4x as many (the scale-up factor) and so on,
+        only until one dense row turns up, so a dense matrix costs it one row.
+        Here every rank scans its shard in growing row
+        ranges (SPARSITY_SCAN_FIRST rows, then x SPARSITY_SCAN_GROWTH) and one
+        all-reduce per round of [dense rows found, rows left] stops all ranks
+        together at the first round that finds one (over all ranks)."""
+        torch = _torch()
         n = self._local_rows()
-        if self._sparse:
-            N.check(N.load().cyc_rowmatrix_dense_rows_dev(
-                None, N.ptr(self.rows.rowptr), N.ptr(self.rows.values), n, self.numCols(),
-                N.ptr(cnt), N.stream_handle()))
-        else:
-            N.check(N.load().cyc_rowmatrix_dense_rows_dev(N.ptr(self.rows), None, None, n,
-                                                          self.numCols(), N.ptr(cnt),
-                                                          N.stream_handle()))
-        parallel.allreduce_(cnt)
-        return int(cnt.item()) == 0
+        a, size = 0, self.SPARSITY_SCAN_FIRST
+        while True:
+            b = min(n, a + size)
+            t = torch.zeros(2, dtype=torch.float64, device=self._device)
+            t[0] = self._dense_rows(a, b)[0]
+            t[1] = n - b
+            parallel.allreduce_(t)
+            found, left = t.tolist()
+            if found > 0:
+                return False
+            if left == 0:
+                return True
+            a, size = b, size * self.SPARSITY_SCAN_GROWTH
 
     def computeCovariance(self) -> np.ndarray:
         """RowMatrix.scala:452-467: computeDenseVectorCovariance (:163-220) or,
         when every row has sparsity >= 0.5, computeSparseVectorCovariance
         (:222-246) from the Gramian."""
+        return self.computeCovarianceDevice().cpu().numpy()
+
+    def computeCovarianceDevice(self):
+        """computeCovariance with the n x n result left in HBM (a torch view
+        G[i, j] of the column-major matrix)."""
         torch = _torch()
         n = self.numCols()
         self._checkNumColumns(n)
@@ -209,7 +249,7 @@ class RowMatrix:
             U = self._packed()
             N.check(N.load().cyc_sparse_covariance_finalize_dev(
                 int(n), N.ptr(U), int(m), N.ptr(mean), N.ptr(G), N.stream_handle()))
-        return G.view(n, n).t().cpu().numpy()
+        return G.view(n, n).t()
 
     def computePrincipalComponentsAndExplainedVariance(self, k: int):
         """RowMatrix.scala:486-513 (n <= 65535 branch); eigensolve on host."""

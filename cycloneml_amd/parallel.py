@@ -11,9 +11,10 @@ model once at start.  There is no other exchange on the data path.
 On GPUs the collective is libcyclone's own C-ABI communicator over RCCL
 (`Communicator`, cyc_comm_* in include/cyclone.h -- the same entry points a
 JVM executor-per-GPU binds), created by `init()` once torch.distributed is
-up (torch only carries the 128-byte RCCL id to every rank).  On the gloo
-backend (the CPU multi-process tests) the same functions use
-torch.distributed.
+up.  torch.distributed itself runs on gloo (host only: the rendezvous, the
+128-byte RCCL id, barriers and small host gathers), so each GPU holds ONE
+RCCL communicator.  Without `init()` (the CPU multi-process tests, the
+two-ranks-on-one-GPU device tests) the same functions use the gloo group.
 """
 from __future__ import annotations
 
@@ -113,24 +114,28 @@ class Communicator:
         return out
 
 
-def init(device=None):
-    """Create the process's RCCL communicator from the running torch.distributed
-    group (backend "nccl"): rank 0's id reaches every rank by one broadcast.
-    A no-op for world size 1 or a gloo group.  Returns the Communicator or None."""
+def init(device=None, communicator=Communicator):
+    """Create the process's RCCL communicator (one per GPU) from the running
+    torch.distributed group, which only carries rank 0's 128-byte RCCL id to
+    every rank (a host tensor over gloo -- bench.py's group -- or a device
+    tensor over an "nccl" group).  A no-op for world size 1.  `communicator`
+    is the class built from (id, rank, world, device index) -- the tests of
+    the rendezvous pass a host stand-in.  Returns it, or None."""
     global _comm
     import torch
     d = _dist()
-    if d is None or d.get_world_size() == 1 or d.get_backend() != "nccl":
+    if d is None or d.get_world_size() == 1:
         return None
     if _comm is not None:
         return _comm
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
-    uid = torch.zeros(Communicator.ID_BYTES, dtype=torch.uint8, device=dev)
+    uid = torch.zeros(communicator.ID_BYTES, dtype=torch.uint8,
+                      device=dev if d.get_backend() == "nccl" else "cpu")
     if d.get_rank() == 0:
-        uid.copy_(torch.frombuffer(bytearray(Communicator.unique_id()), dtype=torch.uint8))
+        uid.copy_(torch.frombuffer(bytearray(communicator.unique_id()), dtype=torch.uint8))
     d.broadcast(uid, 0)
-    _comm = Communicator(bytes(uid.cpu().numpy().tobytes()), d.get_rank(), d.get_world_size(),
-                         dev.index)
+    _comm = communicator(bytes(uid.cpu().numpy().tobytes()), d.get_rank(), d.get_world_size(),
+                         dev.index or 0)
     return _comm
 
 
@@ -178,6 +183,35 @@ def allgather_object(obj) -> list:
     out = [None] * d.get_world_size()
     d.all_gather_object(out, obj)
     return out
+
+
+def agree(fn):
+    """Run fn() on every rank and agree on failure before any collective that
+    depends on it: when fn raised on some rank, every rank raises the lowest
+    such rank's error (same class for the reference's require / assert, same
+    message) -- a failing Spark task fails the whole job with one exception,
+    where a lone raising rank would leave the others blocked in the next
+    all-reduce.  Returns fn()'s result."""
+    from . import _native as N
+    err, out = None, None
+    try:
+        out = fn()
+    except Exception as e:  # every rank must reach the gather below
+        err = e
+    d = _dist()
+    if d is None or d.get_world_size() == 1:
+        if err is not None:
+            raise err
+        return out
+    mine = None if err is None else (type(err).__name__, str(err))
+    first = next((g for g in allgather_object(mine) if g is not None), None)
+    if first is None:
+        return out
+    if err is not None and mine == first:
+        raise err
+    kinds = {"IllegalArgumentException": N.IllegalArgumentException,
+             "JavaAssertionError": N.JavaAssertionError}
+    raise kinds.get(first[0], RuntimeError)(first[1])
 
 
 def max_over_ranks(x: float, device=None) -> float:

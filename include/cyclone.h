@@ -441,6 +441,12 @@ int cyc_multinomial_logistic_add_csr_dev(cyc_logistic_plan plan, const int64_t* 
                                          const double* coef, const double* scaledMean,
                                          double* grad, double* lossSum, double* weightSum,
                                          cyc_csc csc, void* stream);
+/* out[i] = the exponential the dense multinomial margins kernel applies to
+ * the softmax terms m - max (Utils.softmax's math.exp, ml/impl/Utils.scala:
+ * 127-129): e^x for x <= 0 within a few ulp of libm, 0 below -708, NaN kept
+ * (inputs above 0 are outside its contract).  Exported so its accuracy is
+ * testable against the host libm. */
+int cyc_softmax_exp_dev(const double* x, int64_t n, double* out, void* stream);
 
 /* ------------------------------------------------ summarizer pre-pass */
 /* The first pass of LogisticRegression.train (LogisticRegression.scala:

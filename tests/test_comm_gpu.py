@@ -354,7 +354,24 @@ def _silhouette_rank(rank, world):
                         torch.from_numpy(w[a:b].copy()).to(dev))
         ref, _ = oracle.silhouette(X, p, k, w, cosine=cos)
         ok = ok and abs(s - ref) <= 1e-12 * abs(ref)
-    return bool(ok)
+    # a bad weight on rank 1's shard only: both ranks raise the same
+    # IllegalArgumentException (checkNonNegativeWeight) and neither is left
+    # in the statistics all-reduce
+    from cycloneml_amd import _native as N
+    wb = w[a:b].copy()
+    if rank == 1:
+        wb[5] = -2.5
+    try:
+        ClusteringEvaluator().evaluate(torch.from_numpy(X[a:b].copy()).to(dev),
+                                       torch.from_numpy(p[a:b].copy()).to(dev),
+                                       torch.from_numpy(wb).to(dev))
+        ok = False
+    except N.IllegalArgumentException as e:
+        ok = ok and str(e) == ("requirement failed: illegal weight value: -2.5. weight must be "
+                               ">= 0.0.")
+    t = torch.ones(1, dtype=torch.float64, device=dev)
+    parallel.allreduce_(t)
+    return bool(ok and t.item() == 2.0)
 
 
 @pytest.mark.timeout(300)

@@ -179,9 +179,95 @@ def _bench_rows_rank(rank, world):
             ok = ok and mode == "weak" and n == 10_000_000
         else:
             ok = ok and mode == "strong"
-            if name != "gramian":          # 100M Gramian rows exceed 2 x 30M resident
+            if name not in ("gramian", "pca"):   # 100M rows of 1024 exceed 2 x 30M resident
                 ok = ok and total == bench.CONFIG_ROWS[name]
     return bool(ok)
+
+
+def _agree_rank(rank, world):
+    """parallel.agree: a check that fails on ONE shard only (a bad weight on
+    rank 1, checkNonNegativeWeight's message) raises the same exception on
+    every rank before the next collective -- the all-reduce after it is
+    never entered by one rank alone; a check passing everywhere returns its
+    value.  And dense_cluster_ids numbers every rank's distinct ids."""
+    from cycloneml_amd import _native as N
+    from cycloneml_amd import parallel
+    from cycloneml_amd.evaluation import dense_cluster_ids
+    msg = "requirement failed: illegal weight value: -1.0. weight must be >= 0.0."
+
+    def check():
+        if rank == 1:
+            raise N.IllegalArgumentException(msg)
+        return rank
+
+    ok = False
+    try:
+        parallel.agree(check)
+    except N.IllegalArgumentException as e:
+        ok = str(e) == msg
+    t = torch.ones(1, dtype=torch.float64)
+    parallel.allreduce_(t)                        # both ranks reach the next collective
+    ok = ok and t.item() == 2.0 and parallel.agree(lambda: rank * 10) == rank * 10
+    # a JavaAssertionError on rank 0 wins over rank 1's require
+    try:
+        parallel.agree(lambda: (_ for _ in ()).throw(
+            N.JavaAssertionError("assertion failed: a") if rank == 0 else
+            N.IllegalArgumentException("requirement failed: b")))
+        ok = False
+    except N.JavaAssertionError as e:
+        ok = ok and str(e) == "assertion failed: a"
+    mine = torch.tensor([[5, -3, 5], [1_000_000, 5, 7]][rank])
+    ids, K = dense_cluster_ids(mine)
+    want = [[1, 0, 1], [3, 1, 2]][rank]
+    return bool(ok and K == 4 and ids.tolist() == want and ids.dtype == torch.int32)
+
+
+def test_agree_two_ranks():
+    assert _run(_agree_rank) == {0: True, 1: True}
+
+
+class _HostComm:
+    """A host stand-in for parallel.Communicator: records what init() hands it."""
+    ID_BYTES = 128
+
+    @staticmethod
+    def unique_id():
+        return bytes(range(128))
+
+    def __init__(self, uid, rank, world, device):
+        self.uid, self.rank, self.world_size, self.device = uid, rank, world, device
+
+
+def _rendezvous_rank(rank, world):
+    """bench.py --gpus N's control plane: torch.distributed on gloo carries
+    rank 0's RCCL id to every rank (a host tensor), and each rank builds ONE
+    communicator from it with its own rank and device (parallel.init); a
+    second init returns the same one."""
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    from cycloneml_amd import parallel
+    ok = bench.DIST_BACKEND == "gloo" and torch.distributed.get_backend() == "gloo"
+    try:
+        c = parallel.init(torch.device("cuda", rank), communicator=_HostComm)
+        ok = ok and isinstance(c, _HostComm) and c.uid == bytes(range(128))
+        ok = ok and (c.rank, c.world_size, c.device) == (rank, world, rank)
+        ok = ok and parallel.init(torch.device("cuda", rank), communicator=_HostComm) is c
+        ok = ok and parallel.communicator() is c
+    finally:
+        parallel._comm = None
+    return bool(ok)
+
+
+def test_rendezvous_one_communicator_two_ranks():
+    assert _run(_rendezvous_rank) == {0: True, 1: True}
+
+
+def test_bench_has_no_nccl_process_group():
+    """The only RCCL communicator per GPU is libcyclone's (cyc_comm):
+    bench.py's torch.distributed group is gloo."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'init_process_group("nccl"' not in src and "init_process_group(DIST_BACKEND)" in src
 
 
 def test_bench_strong_split_two_ranks():

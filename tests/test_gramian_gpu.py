@@ -115,27 +115,39 @@ def test_gramian_large_shard_properties(cuda):
     np.testing.assert_allclose(Us.cpu().numpy(), oracle.gramian_partition(sub), rtol=1e-11)
 
 
+@pytest.fixture(scope="module")
+def bench_gram_rows(cuda):
+    """bench.py's gramian / pca shard at its benched size (bench.gramian_data:
+    30M x 1024 = 246 GB, the largest resident shard of BASELINE configs[2];
+    the first rows of the same stream if the device has less free memory),
+    shared by the Gramian and covariance tests below."""
+    import gc
+    import sys
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    gc.collect()
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info(cuda)
+    n = int(min(30_000_000, (free - (24 << 30)) // (8 * 1024)))
+    n -= n % 1024
+    X = bench.gramian_data(n, cuda, 0, 1024)
+    yield X
+    del X
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.timeout(600)
-def test_gramian_bench_shard(cuda):
-    """bench.py's gramian shard at its benched size (30M x 1024 = 246 GB, the
-    largest resident shard of BASELINE configs[2]; smaller if the device has
-    less free memory): the whole-shard Gramian equals the sum of its two
+def test_gramian_bench_shard(cuda, bench_gram_rows):
+    """On the bench's rows: the whole-shard Gramian equals the sum of its two
     halves' (split-K sizing differs between them) within 1e-12, equals the
     restatement on a 2000-row subset, and satisfies G 1 = X^T (X 1)."""
     import torch
     from cycloneml_amd.linalg import GramianPlan
     p = 1024
-    import gc
-    gc.collect()
-    torch.cuda.empty_cache()
-    free, _ = torch.cuda.mem_get_info(cuda)
-    n = int(min(30_000_000, (free - (24 << 30)) // (8 * p)))
-    n -= n % 1024
-    X = torch.empty(n, p, dtype=torch.float64, device=cuda)
-    g = torch.Generator(device=cuda).manual_seed(77)
-    for s in range(0, n, 1 << 20):
-        X[s:s + (1 << 20)] = torch.rand(min(1 << 20, n - s), p, generator=g, device=cuda,
-                                        dtype=torch.float64)
+    X = bench_gram_rows
+    n = int(X.shape[0])
     plan = GramianPlan(p)
     U = torch.zeros(p * (p + 1) // 2, dtype=torch.float64, device=cuda)
     plan.accumulate(X, U)
@@ -156,6 +168,77 @@ def test_gramian_bench_shard(cuda):
     plan.accumulate(X[n - 2000:], Us)
     np.testing.assert_allclose(Us.cpu().numpy(),
                                oracle.gramian_partition(X[n - 2000:].cpu().numpy()), rtol=1e-11)
+
+
+@pytest.mark.timeout(600)
+def test_covariance_pca_bench_shard(cuda, bench_gram_rows):
+    """The PCA variant of configs[2] at its shape, on the bench's rows
+    (RowMatrix.computeCovariance, RowMatrix.scala:452-467 ->
+    computeDenseVectorCovariance :163-220, the centred syrk with 16-row
+    chunks and split-K over millions of rows; then
+    computePrincipalComponentsAndExplainedVariance :486-513):
+    - isSparseMatrix is false after its first round (take(1) semantics);
+    - the centred packed sum equals its two unequal halves' (the whole
+      shard's mean) within 1e-12 of its largest entry;
+    - the first and the last 2000 rows' centred sums equal the restatement
+      (x - mean, then netlib dspr per row) within 1e-10;
+    - the covariance is exactly symmetric, and Cov 1 equals
+      sum_r (x_r - mu) ((x_r - mu) . 1) / (m - 1) accumulated in 1M-row
+      chunks (the identity (X^T (X 1) - m mu (mu . 1)) / (m - 1) without its
+      cancellation) within 1e-11;
+    - PCA (k = 3) returns unit principal components and explained variances
+      that sum to at most 1."""
+    import torch
+    from cycloneml_amd.linalg import GramianPlan, RowMatrix
+    p = 1024
+    X = bench_gram_rows
+    n = int(X.shape[0])
+    mat = RowMatrix(X)
+    assert not mat.isSparseMatrix()
+    cov = mat.computeCovarianceDevice()
+    torch.cuda.synchronize()
+    mu = torch.zeros(p, dtype=torch.float64, device=cuda)
+    for s in range(0, n, 1 << 20):
+        mu += X[s:s + (1 << 20)].sum(0)
+    mean, m = mat._column_mean()
+    assert m == n
+    plan = GramianPlan(p)
+    U = torch.zeros(p * (p + 1) // 2, dtype=torch.float64, device=cuda)
+    plan.accumulate(X, U, mean)
+    Uh = torch.zeros_like(U)
+    h = n // 3 + 4099
+    plan.accumulate(X[:h], Uh, mean)
+    plan.accumulate(X[h:], Uh, mean)
+    torch.cuda.synchronize()
+    Uw = U.cpu().numpy()             # norm-wise: off-diagonal sums are small (cancellation)
+    np.testing.assert_allclose(Uh.cpu().numpy(), Uw, rtol=1e-12, atol=1e-12 * np.abs(Uw).max())
+    mean_h = mean.cpu().numpy()
+    np.testing.assert_allclose(mean_h, (mu / n).cpu().numpy(), rtol=1e-12)
+    for a in (0, n - 2000):
+        Us = torch.zeros_like(U)
+        plan.accumulate(X[a:a + 2000], Us, mean)
+        ref = oracle.gramian_partition(X[a:a + 2000].cpu().numpy(), mean_h)
+        got = Us.cpu().numpy()
+        scale = np.abs(ref).max()
+        np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-10 * scale)
+        cref = oracle.dense_vector_covariance(p, ref, 2000)
+        cgot = oracle.dense_vector_covariance(p, got, 2000)
+        np.testing.assert_allclose(cgot, cref, rtol=1e-10, atol=1e-10 * np.abs(cref).max())
+    C = cov.cpu().numpy()
+    assert np.array_equal(C, C.T)                               # SPARK-10875
+    np.testing.assert_allclose(C, oracle.dense_vector_covariance(p, U.cpu().numpy(), n),
+                               rtol=1e-13, atol=0)
+    w = torch.zeros(p, dtype=torch.float64, device=cuda)
+    for s in range(0, n, 1 << 20):
+        xc = X[s:s + (1 << 20)] - mean
+        w += xc.T @ xc.sum(1)
+    w /= (n - 1.0)
+    np.testing.assert_allclose(C.sum(1), w.cpu().numpy(), rtol=1e-11,
+                               atol=1e-11 * float(w.abs().max()))
+    pc, ev = mat.computePrincipalComponentsAndExplainedVariance(3)
+    assert pc.shape == (p, 3) and ev.shape == (3,)
+    np.testing.assert_allclose(np.linalg.norm(pc, axis=0), 1.0, rtol=1e-12)
+    assert np.all(ev > 0) and ev.sum() <= 1.0 and np.all(np.diff(ev) <= 0)
 
 
 # -- SparseVector rows (CSR): sparse spr, isSparseMatrix, both covariances --
@@ -261,3 +344,29 @@ def test_csr_gramian_index_require(cuda):
     from cycloneml_amd.linalg import RowMatrix
     with pytest.raises(N.IllegalArgumentException):
         RowMatrix(_csr([0, 2], [3, 1], [1.0, 2.0], 4, cuda)).computeGramianMatrix()
+
+
+def test_is_sparse_matrix_scan_rounds(cuda, monkeypatch):
+    """isSparseMatrix as take(1) (RDD.scala:1443-1478, 1577-1579): growing row
+    ranges until one row with sparsity() < 0.5 turns up -- here the last row
+    of the shard, so every round runs -- for dense tensors and CSR rows; a
+    matrix without such a row is sparse."""
+    import torch
+    from cycloneml_amd.linalg import RowMatrix
+    monkeypatch.setattr(RowMatrix, "SPARSITY_SCAN_FIRST", 7)
+    rng = np.random.default_rng(4)
+    n, p = 2000, 10
+    X = np.zeros((n, p))
+    for r in range(n):
+        X[r, rng.choice(p, size=5, replace=False)] = rng.uniform(0.5, 1.5, size=5)  # sparsity 0.5
+    assert RowMatrix(_dev(X, cuda)).isSparseMatrix()
+    for last in (n - 1, 0, 900):
+        Y = X.copy()
+        Y[last] = 1.0
+        assert not RowMatrix(_dev(Y, cuda)).isSparseMatrix()
+        nz = Y != 0
+        rp = np.concatenate([[0], np.cumsum(nz.sum(1))]).astype(np.int64)
+        r_, c_ = np.nonzero(nz)
+        assert not RowMatrix(_csr(rp, c_, Y[r_, c_], p, cuda)).isSparseMatrix()
+    assert RowMatrix(torch.zeros(0, p, dtype=torch.float64, device=cuda), nCols=p) \
+        .isSparseMatrix()

@@ -205,8 +205,10 @@ def test_sparse_config5_full_size(cuda):
     """BASELINE config 5 at the size bench.py times, on the rows it times:
     200M rows x 1M features, 64 nonzeros per row (12.8G nonzeros, past 2^32,
     154 GB of tiles layout), generated by bench.lr_sparse_chunks and appended
-    chunk by chunk with the CSR freed, fitIntercept => fitWithMean with a
-    real scaledMean (BinaryLogisticBlockAggregator.scala:81-145).  Checks:
+    chunk by chunk with the CSR freed, fitIntercept => fitWithMean with the
+    bench's synthetic scaledMean, U(0, 0.014) per feature -- the scale of
+    mean / std for these rows, not computed from them
+    (BinaryLogisticBlockAggregator.scala:81-145).  Checks:
     (1) bitwise reproducible; (2) the layout's FIRST and LAST 40,000 rows --
     the last ones at nonzero offsets above 2^32 -- equal the restatement
     within 1e-10, selected inside the full 200M-row layout by a weight mask
@@ -506,43 +508,105 @@ def test_aft_requires_positive_labels(cuda):
 
 @pytest.mark.timeout(600)
 def test_multinomial_bench_shard(cuda):
-    """bench.py's lr_multi shard at its benched size (the full configs[3]:
-    50M x 512, C = 100, fitIntercept + fitWithMean with the shard's real
-    scaledMean; smaller if the device has less free memory): several 8M-row
-    launch chunks and the 32-bit buffer-descriptor caps.  The whole shard's
-    state equals the sum of two unequal parts' (chunk boundaries differ)
-    within 1e-11, and the last 5000 rows equal the restatement within 1e-10."""
+    """bench.py's lr_multi shard at its benched size, on the rows it times
+    (bench.lr_multi_data: the full configs[3], 50M x 512, C = 100, labels from
+    softmax(X W), fitIntercept + fitWithMean with scaledMean = mean / std as
+    the bench sets it; the first rows of the same stream if the device has
+    less free memory), with the bench's coefficients: several 8M-row launch
+    chunks and the 32-bit buffer-descriptor caps.  The whole shard's state
+    equals the sum of two unequal parts' (chunk boundaries differ) within
+    1e-11, and the first and the last 5000 rows equal the restatement within
+    1e-10."""
+    import os
+    import sys
     import torch
     from cycloneml_amd.optim import DeviceInstanceBlock, MultinomialLogisticBlockAggregator
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
     F, C = 512, 100
     import gc
     gc.collect()
     torch.cuda.empty_cache()
     free, _ = torch.cuda.mem_get_info(cuda)
     n = int(min(50_000_000, (free - (24 << 30)) // (8 * F)))
-    g = torch.Generator(device=cuda).manual_seed(11)
-    X = torch.empty(n, F, dtype=torch.float64, device=cuda)
-    for s in range(0, n, 1 << 20):
-        X[s:s + (1 << 20)] = torch.randn(min(1 << 20, n - s), F, generator=g, device=cuda,
-                                         dtype=torch.float64)
-    y = torch.randint(0, C, (n,), generator=g, device=cuda).to(torch.float64)
-    mean = torch.zeros(F, dtype=torch.float64, device=cuda)
-    for s in range(0, n, 1 << 22):
-        mean += X[s:s + (1 << 22)].sum(0)
-    sm = (mean / n).cpu().numpy()
-    coef = np.random.default_rng(3).normal(size=C * F + C) * 0.01
+    X, y, sm_dev = bench.lr_multi_data(n, cuda, 0, F, C)
+    sm = sm_dev.cpu().numpy()
+    coef = np.random.default_rng(3).normal(size=C * F + C) * 0.01    # bench's coef
 
     def run(a, b):
         blk = DeviceInstanceBlock(y[a:b], None, X=X[a:b])
-        return MultinomialLogisticBlockAggregator(np.ones(F), sm, True, True, coef,
+        return MultinomialLogisticBlockAggregator(np.ones(F), sm_dev, True, True, coef,
                                                   device=cuda).add(blk)._state.cpu().numpy()
     full = run(0, n)
     cut = 19_000_001
     _rel_close(run(0, cut) + run(cut, n), full, rtol=1e-11)
     m = 5000
-    st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
-    oracle.multinomial_logistic_add(dict(labels=y[n - m:].cpu().numpy(), weights=None,
-                                         X=X[n - m:].cpu().numpy()), coef, C, True, True, sm, st)
-    tail = run(n - m, n)
-    _rel_close(tail[:coef.size], st["grad"])
-    assert abs(tail[coef.size] - st["loss"]) <= 1e-10 * abs(st["loss"])
+    for a in (0, n - m):
+        st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
+        oracle.multinomial_logistic_add(dict(labels=y[a:a + m].cpu().numpy(), weights=None,
+                                             X=X[a:a + m].cpu().numpy()), coef, C, True, True, sm,
+                                        st)
+        part = run(a, a + m)
+        _rel_close(part[:coef.size], st["grad"])
+        assert abs(part[coef.size] - st["loss"]) <= 1e-10 * abs(st["loss"])
+
+
+def test_softmax_exp_vs_libm(cuda):
+    """The softmax exponential of the dense multinomial margins (exp_neg,
+    cyc_softmax_exp_dev) against the host libm over [-750, 0]: within 4 ulp
+    where e^x is normal; where it is subnormal (below -708.4: the result
+    rounded onto the subnormal grid) within 2 units of 2^-1074 or 1e-12
+    relative; 0 below -746 and at -inf, 1 at -0.0, NaN kept."""
+    import torch
+    from cycloneml_amd import _native as N
+    rng = np.random.default_rng(12)
+    x = np.concatenate([np.linspace(-750.0, 0.0, 2_000_001), -rng.exponential(3.0, 500_000),
+                        -rng.uniform(700.0, 750.0, 200_000), [-0.0, -np.inf, np.nan, -708.0,
+                                                              -708.4, -745.1, -746.0, -1e-300]])
+    xd = torch.as_tensor(x, device=cuda)
+    out = torch.empty_like(xd)
+    N.check(N.load().cyc_softmax_exp_dev(N.ptr(xd), x.size, N.ptr(out), None))
+    got = out.cpu().numpy()
+    ref = np.exp(x)
+    fin = np.isfinite(x)
+    normal = fin & (ref >= np.finfo(np.float64).tiny)
+    ulps = np.abs(got[normal] - ref[normal]) / np.spacing(ref[normal])
+    assert ulps.max() <= 4.0, ulps.max()
+    sub = fin & ~normal
+    err = np.abs(got[sub] - ref[sub])
+    assert np.all(err <= np.maximum(2 * 2.0 ** -1074, 1e-12 * ref[sub]))
+    assert np.all(got[fin & (x < -746.0)] == 0.0)
+    assert got[-8 + 0] == 1.0 and got[-7] == 0.0 and np.isnan(got[-6])
+    assert got[-1] == 1.0
+
+
+def test_multinomial_margin_spread_past_708(cuda):
+    """Margins spread by more than 708 within a row, so softmax terms fall
+    into the subnormal range and below it (Utils.softmax, ml/impl/Utils.scala:
+    108-135): rows whose label's probability is subnormal keep a finite loss
+    term, as the reference's Math.exp gives; the state matches the
+    restatement within 1e-10."""
+    from cycloneml_amd.optim import DeviceInstanceBlock, MultinomialLogisticBlockAggregator
+    rng = np.random.default_rng(21)
+    n, F, C = 3000, 4, 6
+    X = rng.normal(size=(n, F))
+    X[:, 0] = rng.uniform(0.96, 1.03, size=n)
+    coef = np.zeros(C * F + C)                     # linear C x F column-major, then intercepts
+    coef[0 * C + 1] = 720.0                        # class 1 leads by 690..742
+    coef[0 * C + 2] = -30.0                        # class 2: terms below -746 (exactly 0)
+    coef[1 * C + 3] = 3.0
+    # labels never class 2 (a zero probability's log is -inf in both); the
+    # others' probabilities are subnormal for about half the rows
+    labels = rng.choice([0, 1, 3, 4, 5], size=n).astype(np.float64)
+    for fi in (False, True):
+        c = coef if fi else coef[:C * F]
+        st = dict(grad=np.zeros(c.size), loss=0.0, weight=0.0)
+        oracle.multinomial_logistic_add(dict(labels=labels, weights=None, X=X), c, C, fi, False,
+                                        None, st)
+        assert np.isfinite(st["loss"])
+        blk = DeviceInstanceBlock.from_numpy(labels, None, X=X, device=cuda)
+        agg = MultinomialLogisticBlockAggregator(np.ones(F), None, fi, False, c,
+                                                 device=cuda).add(blk)
+        _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
+        loss = float(agg._loss_sum.item())
+        assert np.isfinite(loss) and abs(loss - st["loss"]) <= 1e-10 * abs(st["loss"])

@@ -151,6 +151,24 @@ def test_device_errors(cuda, cosine):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cosine", [False, True])
+def test_device_arbitrary_cluster_ids(cuda, cosine):
+    """Any integer ids (negative, past the device sort's 8192, sparse) give
+    the score of the same clustering numbered 0..K-1 (the reference keys its
+    statistics by the prediction value); more than 8192 distinct ids raise."""
+    from cycloneml_amd import _native as N
+    X, p = iris()
+    ref = _evaluate(cuda, X, p, cosine=cosine)
+    ids = np.array([-7, 40_000, 9_999_999_999], dtype=np.int64)
+    assert _evaluate(cuda, X, ids[p], cosine=cosine) == ref
+    rng = np.random.default_rng(3)
+    n = 20_000
+    many = rng.permutation(n).astype(np.int64) * 3
+    with pytest.raises(N.IllegalArgumentException, match="at most 8192 distinct"):
+        _evaluate(cuda, rng.normal(size=(n, 4)), many, cosine=cosine)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,d,k,weighted,cosine", [
     (200_003, 64, 50, True, False), (200_003, 64, 50, True, True),
     (65_536, 256, 1024, False, False), (70_001, 17, 3, True, False),
