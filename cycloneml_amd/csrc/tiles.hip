@@ -58,8 +58,9 @@ struct cyc_tiles_s {
   int F = 0, T = 1, Wt = 1;
   int64_t capRows = 0, capNnz = 0, n = 0, nnz = 0;
   bool sealed = false;    // ends with a partial row block: no further appends
+  int64_t maxSeg = 0;     // nonzeros of the longest segment (picks the pass instances)
   std::mutex mu;
-  cyc::DeviceBuffer segStart, idx, vals;
+  cyc::DeviceBuffer segStart, idx, vals, maxDev;
 };
 
 namespace {
@@ -75,7 +76,6 @@ constexpr int kCPT = kTileCols / kTPB;         // staged coefficients per thread
 constexpr int kMPT = kTileRows / kTPB;         // staged multipliers per thread
 constexpr int kDPT = kTileSuperRows / kTPB;    // dots per thread (margin)
 constexpr int kGPT = kTileSuperCols / kTPB;    // gradient sums per thread
-constexpr int kCap = 5;                        // nonzeros per lane in flight per run
 
 // columns per chunk: an eighth of F (so a gradient workgroup's 8 waves all
 // have a chunk when F is small), a multiple of 64, at most kTileCols
@@ -131,10 +131,42 @@ __global__ void k_tile_starts(const uint32_t* __restrict__ keys, int64_t cnt, in
 
 __global__ void k_set_i64(int64_t* p, int64_t v) { *p = v; }
 
+// *mx = max(*mx, longest segment of [s0, s1)) -- a wave max, then one
+// atomic per wave
+__global__ void k_seg_max(const int64_t* __restrict__ segStart, int64_t s0, int64_t s1,
+                          unsigned long long* __restrict__ mx) {
+  unsigned long long m = 0;
+  for (int64_t q = s0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < s1;
+       q += (int64_t)gridDim.x * blockDim.x)
+    m = max(m, (unsigned long long)(segStart[q + 1] - segStart[q]));
+  for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(mx, m);
+}
+
 // ----------------------------------------------------------------- passes
 
+// tools/probe/tiles_mall_probe.py times library builds with parts of both
+// passes removed (results then meaningless): bits 1 = plain LDS stores in
+// place of the LDS atomic adds, 2 = no LDS gathers of coefficients /
+// multipliers, 4 = no per-step barrier, 8 = no staging of the chunk / slice,
+// 16 = no run loads (synthetic ids and values), 32 = no segment offset
+// loads (every run 256 long).  0 in the library.
+#ifndef CYC_TILES_PROBE
+#define CYC_TILES_PROBE 0
+#endif
+
 __device__ __forceinline__ void lds_add(double* p, double x) {
-  __hip_atomic_fetch_add(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if constexpr ((CYC_TILES_PROBE & 1) != 0) *p = x;
+  else __hip_atomic_fetch_add(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// s_waitcnt immediate for "at most n vector memory operations outstanding"
+// (gfx9 encoding: vmcnt in bits 3:0 and 15:14; expcnt and lgkmcnt left at
+// their maxima, i.e. not waited for)
+constexpr int vm_wait(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
+
+__device__ __forceinline__ void step_barrier() {
+  if constexpr ((CYC_TILES_PROBE & 4) == 0) __syncthreads();
 }
 
 // buffer resource over [p, p + bytes): lanes past the end read 0
@@ -159,41 +191,63 @@ struct Run {
 __device__ __forceinline__ Run seg_run(const int64_t* __restrict__ segStart, int64_t seg,
                                        bool on) {
   if (!on) return Run{0, 0};
+  if constexpr ((CYC_TILES_PROBE & 32) != 0) return Run{0, 256};   // the first 256 nonzeros
   const int64_t a = segStart[seg];
   return Run{a, segStart[seg + 1] - a};
 }
 
-// the first kCap x 64 nonzeros of a run from `from` on, lane-strided; lanes
+// the first KC x 64 nonzeros of a run from `from` on, lane-strided; lanes
 // past the end read 0 (buffer range check)
+template <int KC>
 __device__ __forceinline__ void load_run(const uint32_t* __restrict__ vidx,
                                          const double* __restrict__ vvals, const Run& r,
-                                         int64_t from, int lane, uint32_t (&ix)[kCap],
-                                         double (&vx)[kCap]) {
+                                         int64_t from, int lane, uint32_t (&ix)[KC],
+                                         double (&vx)[KC]) {
   const int64_t len = r.len - from;
+  if constexpr ((CYC_TILES_PROBE & 16) != 0) {
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      ix[j] = ((uint32_t)(lane * 31 + j * 7) & 2047) << 16 | ((uint32_t)(lane * 29 + j) & 1023);
+      vx[j] = 1.0 + j;
+    }
+    return;
+  }
   const auto ri = rsrc(vidx + r.s0 + from, len > 0 ? len * 4 : 0);
   const auto rv = rsrc(vvals + r.s0 + from, len > 0 ? len * 8 : 0);
   // lane part in the VGPR offset, batch part in the immediate offset
 #pragma unroll
-  for (int j = 0; j < kCap; ++j) {
+  for (int j = 0; j < KC; ++j) {
     ix[j] = __builtin_amdgcn_raw_buffer_load_b32(ri, lane * 4, j * 256, 2);
     vx[j] = __builtin_bit_cast(double,
                                __builtin_amdgcn_raw_buffer_load_b64(rv, lane * 8, j * 512, 2));
   }
 }
 
+// run buffers of the margin pass (the runs of the next NB - 1 steps in
+// flight) and coefficient chunks in registers (CS = 2: a chunk is loaded two
+// steps before it is staged; NB a multiple of CS)
+#ifndef CYC_TILES_MARGIN_NB
+#define CYC_TILES_MARGIN_NB 3
+#endif
+#ifndef CYC_TILES_MARGIN_CS
+#define CYC_TILES_MARGIN_CS 1
+#endif
+
 // Margin pass, persistent over (super row block sb, column chunk c) steps:
 // this workgroup's super blocks sb = blockIdx.x + i * gridDim.x (8 row blocks
 // each), each swept over the T chunks, as one flat sequence of steps g.  Per
-// step: the coefficient chunk goes registers -> LDS (the next step's chunk
-// is loaded meanwhile, an L2 hit), and wave i walks segment (8 sb + i, c);
-// the runs of the next TWO steps are in flight in registers, across super
-// block boundaries too.
+// step: the coefficient chunk goes registers -> LDS (the next CS steps'
+// chunks are loaded meanwhile, L2 hits), and wave i walks segment
+// (8 sb + i, c); the runs of the next NB - 1 steps are in flight in
+// registers, across super block boundaries too.
+template <int NB, int CS, int KC, bool LONG>
 __global__ __launch_bounds__(kTPB) void k_tiles_margin(
     TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
     const double* __restrict__ vvals, const double* __restrict__ labels,
     const double* __restrict__ weights, const double* __restrict__ coef, int fitIntercept,
     int kind, double offset, double lscale, double sigma, double eps, double* __restrict__ mult,
     double* __restrict__ slabS) {
+  static_assert(NB % CS == 0, "the chunk sets rotate within the unroll");
   // 160 KiB: the super block's dots and two coefficient chunk buffers (the
   // chunk of step s in cf[s & 1]); the final reduction reuses cf
   __shared__ double lds[kTileSuperRows + 2 * kTileCols];
@@ -203,18 +257,20 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T = v.T;
   const int64_t nSB = (v.nRB + kTileWaves - 1) / kTileWaves;
-  // steps per super block padded to a multiple of 3 (the unroll of the run
-  // buffers); the padding steps have empty runs and fetch nothing
-  const int Tp = (T + 2) / 3 * 3;
+  // steps per super block padded to a multiple of NB (the unroll of the run
+  // buffers; with CS = 2, NB and so Tp are even, and a step's chunk set is
+  // fixed by its place in the unroll); the padding steps have empty runs and
+  // fetch nothing
+  const int Tp = (T + NB - 1) / NB * NB;
   const int64_t mySB = nSB > blockIdx.x ? (nSB - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};     // loss, weight, multiplierSum, sigmaGradSum
-  double creg[kCPT];
-  uint32_t iA[kCap], iB[kCap], iC[kCap];
-  double vA[kCap], vB[kCap], vC[kCap];
-  Run rA, rB, rC;
+  double creg[CS][kCPT];                    // chunk of step g in creg[g % CS]
+  uint32_t ib[NB][KC];
+  double vb[NB][KC];
+  Run rr[NB];
 
   // a step is (k, c): this workgroup's k-th super block, chunk c < Tp; the
-  // positions one and two steps ahead by compare-and-wrap (no divisions)
+  // positions a few steps ahead by compare-and-wrap (no divisions)
   auto ahead = [&](int64_t k, int c, int by, int64_t& k2, int& c2) {
     c2 = c + by;
     k2 = k;
@@ -224,73 +280,94 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
     const int64_t rb = ((int64_t)blockIdx.x + k * gridDim.x) * kTileWaves + wave;
     return seg_run(segStart, rb * T + c, k < mySB && c < T && rb < v.nRB);
   };
-  auto load_coef = [&](int64_t k, int c) {
+  auto load_coef = [&](int64_t k, int c, double (&cr)[kCPT]) {
     const bool on = k < mySB && c < T;
     const int64_t c0 = on ? (int64_t)c * v.Wt : 0;
     const int wl = on ? (int)std::min<int64_t>(v.Wt, v.F - c0) : 0;
     const auto rc = rsrc(coef + c0, (int64_t)wl * 8);
 #pragma unroll
     for (int i = 0; i < kCPT; ++i)
-      creg[i] = __builtin_bit_cast(
+      cr[i] = __builtin_bit_cast(
           double, __builtin_amdgcn_raw_buffer_load_b64(rc, tid * 8, i * kTPB * 8, 0));
   };
   double* myDots = dots + wave * kTileRows;
-  auto consume = [&](int64_t len, const double* cfp, const uint32_t (&ix)[kCap],
-                     const double (&vx)[kCap]) {
-    double c[kCap];
+  // waits for the whole run first, on every path: its values are used only
+  // under the lanes' `< len` branches, and a path that skips one left the
+  // compiler's wait analysis treating the registers as still loading at the
+  // loop head, where it then drained every prefetched run (vmcnt(0)).  The
+  // runs of the other NB - 2 steps and the staging loads of the steps since
+  // -- (NB - 2) (2 KC + 4) operations -- stay in flight.
+  auto consume = [&](int64_t len, const double* cfp, const uint32_t (&ix)[KC],
+                     const double (&vx)[KC]) {
+    __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2) * (2 * KC + 4)));
+    double c[KC];
 #pragma unroll
-    for (int j = 0; j < kCap; ++j) c[j] = cfp[ix[j] & 0xffff];  // lanes past the end read [0]
+    for (int j = 0; j < KC; ++j)   // lanes past the end read [0]
+      c[j] = (CYC_TILES_PROBE & 2) ? vx[j] : cfp[ix[j] & 0xffff];
 #pragma unroll
-    for (int j = 0; j < kCap; ++j)
+    for (int j = 0; j < KC; ++j)
       if (j * 64 + lane < len) lds_add(&myDots[ix[j] >> 16], vx[j] * c[j]);
   };
   // One step (k, c), ONE barrier: the current run into the row sums with
-  // chunk s in cf[s & 1], the next chunk (in registers since the last step)
+  // chunk s in cf[s & 1], the next chunk (in registers since CS steps ago)
   // into the other buffer -- every wave left it behind the last barrier --,
-  // then the loads of the chunk one step and of the run two steps ahead of
-  // it issued (unconditionally: past the end they fetch nothing, so the
-  // waits for the current run stay counted).  The three run buffers rotate
-  // by unrolling (never by copying a register that a load is still filling).
-  auto step = [&](int64_t k, int c, const Run& rc, uint32_t (&ic)[kCap], double (&vc)[kCap],
-                  Run& rn, uint32_t (&in)[kCap], double (&vn)[kCap]) {
+  // then the loads of the chunk CS + 1 steps and of the run NB - 1 steps
+  // ahead issued (unconditionally: past the end they fetch nothing, so the
+  // waits for the current run stay counted).  The run buffers and chunk sets
+  // rotate by unrolling (never by copying a register that a load is still
+  // filling).
+  auto step = [&](int64_t k, int c, const Run& rc, uint32_t (&ic)[KC], double (&vc)[KC],
+                  Run& rn, uint32_t (&in)[KC], double (&vn)[KC], double (&cs)[kCPT]) {
     const int par = (int)((k * Tp + c) & 1);
     const double* cur = cf + par * kTileCols;
     consume(rc.len, cur, ic, vc);
-    for (int64_t b = kCap * 64; b < rc.len; b += kCap * 64) {   // rare: a long run
-      load_run(vidx, vvals, rc, b, lane, ic, vc);
-      consume(rc.len - b, cur, ic, vc);
+    // a run longer than KC x 64: only in the LONG instance (a layout with
+    // such segments), in registers of its own -- any load in this loop's
+    // body makes the compiler's wait analysis drain every prefetched run
+    // at the loop head
+    if constexpr (LONG) {
+      for (int64_t b = KC * 64; b < rc.len; b += KC * 64) {
+        uint32_t it[KC];
+        double vt[KC];
+        load_run(vidx, vvals, rc, b, lane, it, vt);
+        consume(rc.len - b, cur, it, vt);
+      }
     }
     double* nxt = cf + (par ^ 1) * kTileCols;
-#pragma unroll
-    for (int i = 0; i < kCPT; ++i) nxt[tid + kTPB * i] = creg[i];
     int64_t k2;
     int c2;
-    ahead(k, c, 2, k2, c2);
-    load_coef(k2, c2);
+    if constexpr ((CYC_TILES_PROBE & 8) == 0) {
+#pragma unroll
+      for (int i = 0; i < kCPT; ++i) nxt[tid + kTPB * i] = cs[i];
+      ahead(k, c, CS + 1, k2, c2);
+      load_coef(k2, c2, cs);
+    }
+    ahead(k, c, NB - 1, k2, c2);
     rn = run_of(k2, c2);
     load_run(vidx, vvals, rn, 0, lane, in, vn);
-    __syncthreads();
+    step_barrier();
   };
 
-  // prologue: chunk 0 into cf[0], chunk 1 in registers, runs 0 and 1 in flight
-  load_coef(0, 0);
+  // prologue: chunk 0 into cf[0], chunks 1 .. CS in registers, runs of
+  // steps 0 .. NB - 2 in flight
+  load_coef(0, 0, creg[0]);
 #pragma unroll
-  for (int i = 0; i < kCPT; ++i) cf[tid + kTPB * i] = creg[i];
-  {
+  for (int i = 0; i < kCPT; ++i) cf[tid + kTPB * i] = creg[0][i];
+#pragma unroll
+  for (int s1 = 1; s1 <= CS; ++s1) {
     int64_t k1;
     int c1;
-    ahead(0, 0, 1, k1, c1);
-    load_coef(k1, c1);
+    ahead(0, 0, s1, k1, c1);
+    load_coef(k1, c1, creg[s1 % CS]);
   }
-  rA = run_of(0, 0);
-  load_run(vidx, vvals, rA, 0, lane, iA, vA);
-  {
+#pragma unroll
+  for (int u = 0; u < NB - 1; ++u) {
     int64_t k1;
     int c1;
-    ahead(0, 0, 1, k1, c1);
-    rB = run_of(k1, c1);
+    ahead(0, 0, u, k1, c1);
+    rr[u] = run_of(k1, c1);
+    load_run(vidx, vvals, rr[u], 0, lane, ib[u], vb[u]);
   }
-  load_run(vidx, vvals, rB, 0, lane, iB, vB);
   // The binary logistic epilogue (kind 0: BinaryLogisticBlockAggregator.
   // scala:104-122) without branches, EB rows at a time with the next EB
   // rows' labels and weights loaded before this batch's multiplier stores
@@ -342,10 +419,11 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
 #pragma unroll
     for (int i = 0; i < kDPT; ++i) dots[tid + kTPB * i] = 0.0;
     __syncthreads();                            // zeroed dots, chunk 0 in cf[0]
-    for (int c = 0; c < Tp; c += 3) {
-      step(k, c, rA, iA, vA, rC, iC, vC);
-      step(k, c + 1, rB, iB, vB, rA, iA, vA);
-      step(k, c + 2, rC, iC, vC, rB, iB, vB);
+    for (int c = 0; c < Tp; c += NB) {
+#pragma unroll
+      for (int u = 0; u < NB; ++u)
+        step(k, c + u, rr[u], ib[u], vb[u], rr[(u + NB - 1) % NB], ib[(u + NB - 1) % NB],
+             vb[(u + NB - 1) % NB], creg[(u + 1) % CS]);
     }
     // epilogue (BinaryLogisticBlockAggregator.scala:104-122 and siblings)
     const int64_t r0 = ((int64_t)blockIdx.x + k * gridDim.x) * kTileSuperRows;
@@ -387,15 +465,27 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
   }
 }
 
+// run buffers of the gradient pass: the runs of the next NB - 1 row blocks
+// are in flight while one is consumed; MS multiplier slices in registers
+// (MS = 2: a slice is loaded two row blocks before it is staged; NB even)
+#ifndef CYC_TILES_GRAD_NB
+#define CYC_TILES_GRAD_NB 3
+#endif
+#ifndef CYC_TILES_GRAD_MS
+#define CYC_TILES_GRAD_MS 1
+#endif
+
 // Gradient pass: workgroup (super chunk st = 8 column chunks, row range)
 // over its row blocks.  Per row block: the multiplier slice goes registers
-// -> LDS (the next one loaded while this one is used); wave j walks segment
-// (rb, 8 st + j) into its chunk's column sums, with the runs of the next two
-// row blocks in flight.
+// -> LDS (the next ones loaded while this one is used); wave j walks segment
+// (rb, 8 st + j) into its chunk's column sums, with the runs of the next
+// NB - 1 row blocks in flight.
+template <int NB, int MS, int KC, bool LONG>
 __global__ __launch_bounds__(kTPB) void k_tiles_grad(
     TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
     const double* __restrict__ vvals, const double* __restrict__ mult, int ranges,
     double* __restrict__ slabG) {
+  static_assert(MS == 1 || (MS == 2 && NB % 2 == 0), "two slice sets need an even unroll");
   // 160 KiB: the 8 chunks' column sums and two multiplier slice buffers
   // (row block rb's slice in mv[(rb - rbA) & 1])
   __shared__ double lds[kTileSuperCols + 2 * kTileRows];
@@ -406,76 +496,94 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
   const int range = blockIdx.x % ranges, st = blockIdx.x / ranges;
   const int64_t rbA = v.nRB * range / ranges, rbB = v.nRB * (range + 1) / ranges;
   const int c = st * kTileWaves + wave;                 // this wave's column chunk
-  double mreg[kMPT];
-  uint32_t iA[kCap], iB[kCap], iC[kCap];
-  double vA[kCap], vB[kCap], vC[kCap];
-  Run rA, rB, rC;
+  double mreg[MS][kMPT];                                // slice r in mreg[(r - rbA) % MS]
+  uint32_t ib[NB][KC];
+  double vb[NB][KC];
+  Run rr[NB];
 
   auto run_of = [&](int64_t rb) { return seg_run(segStart, rb * v.T + c, rb < rbB && c < v.T); };
-  auto load_mult = [&](int64_t rb) {
+  auto load_mult = [&](int64_t rb, double (&m)[kMPT]) {
     const int64_t r0 = rb * kTileRows;
     const auto rm = rsrc(mult + (rb < rbB ? r0 : 0),
                          rb < rbB ? std::min<int64_t>(kTileRows, v.n - r0) * 8 : 0);
 #pragma unroll
     for (int i = 0; i < kMPT; ++i)
-      mreg[i] = __builtin_bit_cast(
+      m[i] = __builtin_bit_cast(
           double, __builtin_amdgcn_raw_buffer_load_b64(rm, tid * 8, i * kTPB * 8, 0));
   };
   double* myG = gt + wave * v.Wt;
-  auto consume = [&](int64_t len, const double* mvp, const uint32_t (&ix)[kCap],
-                     const double (&vx)[kCap]) {
-    double m[kCap];
+  // waits for the whole run first, on every path (the margin pass's
+  // consume says why)
+  auto consume = [&](int64_t len, const double* mvp, const uint32_t (&ix)[KC],
+                     const double (&vx)[KC]) {
+    __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2) * (2 * KC + 4 * MS)));
+    double m[KC];
 #pragma unroll
-    for (int j = 0; j < kCap; ++j) m[j] = mvp[ix[j] >> 16];    // lanes past the end read [0]
+    for (int j = 0; j < KC; ++j)   // lanes past the end read [0]
+      m[j] = (CYC_TILES_PROBE & 2) ? vx[j] : mvp[ix[j] >> 16];
 #pragma unroll
-    for (int j = 0; j < kCap; ++j)
+    for (int j = 0; j < KC; ++j)
       if (j * 64 + lane < len) lds_add(&myG[ix[j] & 0xffff], vx[j] * m[j]);
   };
 
 #pragma unroll
   for (int i = 0; i < kGPT; ++i) gt[tid + kTPB * i] = 0.0;
-  // one row block, ONE barrier: the current run into the column sums with
-  // the slice in mv[par], the next slice (in registers since the last step)
-  // into the other buffer -- every wave left it behind the last barrier --,
-  // then the slice two row blocks ahead and the run two row blocks ahead
-  // issued (unconditionally); run buffers rotate by unrolling
-  auto step = [&](int64_t rb, const Run& rc, uint32_t (&ic)[kCap], double (&vc)[kCap], Run& rn,
-                  uint32_t (&in)[kCap], double (&vn)[kCap]) {
+  // one row block (the u-th of an unrolled group), ONE barrier: the current
+  // run into the column sums with the slice in mv[par], the next slice (in
+  // registers since MS steps ago) into the other buffer -- every wave left
+  // it behind the last barrier --, then the slice MS + 1 row blocks ahead
+  // and the run NB - 1 row blocks ahead issued (unconditionally, into the
+  // registers just freed); run buffers and slice sets rotate by unrolling
+  auto step = [&](int64_t rb, const Run& rc, uint32_t (&ic)[KC], double (&vc)[KC],
+                  Run& rn, uint32_t (&in)[KC], double (&vn)[KC], double (&ms)[kMPT]) {
     const int par = (int)((rb - rbA) & 1);
     const double* cur = mv + par * kTileRows;
     consume(rc.len, cur, ic, vc);
-    for (int64_t b = kCap * 64; b < rc.len; b += kCap * 64) {   // rare: a long run
-      load_run(vidx, vvals, rc, b, lane, ic, vc);
-      consume(rc.len - b, cur, ic, vc);
+    // a run longer than KC x 64: only in the LONG instance (a layout with
+    // such segments), in registers of its own -- any load in this loop's
+    // body makes the compiler's wait analysis drain every prefetched run
+    // at the loop head
+    if constexpr (LONG) {
+      for (int64_t b = KC * 64; b < rc.len; b += KC * 64) {
+        uint32_t it[KC];
+        double vt[KC];
+        load_run(vidx, vvals, rc, b, lane, it, vt);
+        consume(rc.len - b, cur, it, vt);
+      }
     }
     double* nxt = mv + (par ^ 1) * kTileRows;
+    if constexpr ((CYC_TILES_PROBE & 8) == 0) {
 #pragma unroll
-    for (int i = 0; i < kMPT; ++i) nxt[tid + kTPB * i] = mreg[i];
-    load_mult(rb + 2);
-    rn = run_of(rb + 2);
+      for (int i = 0; i < kMPT; ++i) nxt[tid + kTPB * i] = ms[i];
+      load_mult(rb + 1 + MS, ms);
+    }
+    rn = run_of(rb + NB - 1);
     load_run(vidx, vvals, rn, 0, lane, in, vn);
-    __syncthreads();
+    step_barrier();
   };
 
-  // prologue: slice rbA into mv[0], slice rbA + 1 in registers, runs rbA
-  // and rbA + 1 in flight
-  load_mult(rbA);
+  // prologue: slice rbA into mv[0], slices rbA + 1 .. rbA + MS in
+  // registers, runs rbA .. rbA + NB - 2 in flight
+  load_mult(rbA, mreg[0]);
 #pragma unroll
-  for (int i = 0; i < kMPT; ++i) mv[tid + kTPB * i] = mreg[i];
-  load_mult(rbA + 1);
-  rA = run_of(rbA);
-  load_run(vidx, vvals, rA, 0, lane, iA, vA);
-  rB = run_of(rbA + 1);
-  load_run(vidx, vvals, rB, 0, lane, iB, vB);
-  __syncthreads();                              // zeroed sums, slice rbA in mv[0]
-  int64_t rb = rbA;
-  for (; rb + 3 <= rbB; rb += 3) {
-    step(rb, rA, iA, vA, rC, iC, vC);
-    step(rb + 1, rB, iB, vB, rA, iA, vA);
-    step(rb + 2, rC, iC, vC, rB, iB, vB);
+  for (int i = 0; i < kMPT; ++i) mv[tid + kTPB * i] = mreg[0][i];
+#pragma unroll
+  for (int s = 1; s <= MS; ++s) load_mult(rbA + s, mreg[s % MS]);
+#pragma unroll
+  for (int u = 0; u < NB - 1; ++u) {
+    rr[u] = run_of(rbA + u);
+    load_run(vidx, vvals, rr[u], 0, lane, ib[u], vb[u]);
   }
-  if (rb < rbB) step(rb, rA, iA, vA, rC, iC, vC);
-  if (rb + 1 < rbB) step(rb + 1, rB, iB, vB, rA, iA, vA);
+  __syncthreads();                              // zeroed sums, slice rbA in mv[0]
+  // whole groups of NB steps: the last group's steps past rbB have empty
+  // runs and slices (no guard inside the unroll: a skipped step left the
+  // compiler's wait analysis draining every prefetched run at the loop head)
+  for (int64_t rb = rbA; rb < rbB; rb += NB) {
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      step(rb + u, rr[u], ib[u], vb[u], rr[(u + NB - 1) % NB], ib[(u + NB - 1) % NB],
+           vb[(u + NB - 1) % NB], mreg[(u + 1) % MS]);
+  }
   __syncthreads();
   const int64_t col0 = (int64_t)st * kTileWaves * v.Wt;
   double* out = slabG + (int64_t)range * v.F + col0;
@@ -485,6 +593,15 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
     const int e = tid + kTPB * i;
     if (e < wl) out[e] = gt[e];
   }
+}
+
+// nonzeros per lane per run buffer for a layout whose longest segment has
+// maxSeg nonzeros: the smallest instance that takes every run in one load
+// (0: none does -- the LONG instance, 5 per lane and a loop for the rest)
+int run_capacity(int64_t maxSeg) {
+  for (int kc : {5, 6, 8})
+    if (maxSeg <= 64 * kc) return kc;
+  return 0;
 }
 
 }  // namespace
@@ -501,6 +618,7 @@ int tiles_view(cyc_tiles t, TilesView* v) {
   v->segStart = (const int64_t*)t->segStart.ptr;
   v->idx = (const uint32_t*)t->idx.ptr;
   v->vals = (const double*)t->vals.ptr;
+  v->maxSeg = t->maxSeg;
   return CYC_OK;
 }
 
@@ -512,9 +630,18 @@ int tiles_margin(const TilesView& v, const double* labels, const double* weights
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nSB, device_cus()));
   *wgs = grid;
   const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
-  hipLaunchKernelGGL(k_tiles_margin, dim3((unsigned)grid), dim3(kTPB), 0, st, d, v.segStart,
-                     v.idx, v.vals, labels, weights, coef, fitIntercept, kind, offset, lscale,
-                     sigma, eps, mult, slabS);
+#define CYC_TILES_MARGIN(KC, LONG)                                                              \
+  hipLaunchKernelGGL(                                                                           \
+      HIP_KERNEL_NAME(k_tiles_margin<CYC_TILES_MARGIN_NB, CYC_TILES_MARGIN_CS, KC, LONG>),       \
+      dim3((unsigned)grid), dim3(kTPB), 0, st, d, v.segStart, v.idx, v.vals, labels, weights,   \
+      coef, fitIntercept, kind, offset, lscale, sigma, eps, mult, slabS)
+  switch (run_capacity(v.maxSeg)) {
+    case 5: CYC_TILES_MARGIN(5, false); break;
+    case 6: CYC_TILES_MARGIN(6, false); break;
+    case 8: CYC_TILES_MARGIN(8, false); break;
+    default: CYC_TILES_MARGIN(5, true); break;
+  }
+#undef CYC_TILES_MARGIN
   CYC_LAUNCH_CHECK("k_tiles_margin");
   return CYC_OK;
 }
@@ -531,8 +658,17 @@ int tiles_grad(const TilesView& v, const double* mult, double* slabG, int* range
   *ranges = R;
   const int64_t sts = (v.T + kTileWaves - 1) / kTileWaves;
   const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
-  hipLaunchKernelGGL(k_tiles_grad, dim3((unsigned)(sts * R)), dim3(kTPB), 0, st, d, v.segStart,
-                     v.idx, v.vals, mult, R, slabG);
+#define CYC_TILES_GRAD(KC, LONG)                                                                \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_grad<CYC_TILES_GRAD_NB, CYC_TILES_GRAD_MS, KC, LONG>), \
+                     dim3((unsigned)(sts * R)), dim3(kTPB), 0, st, d, v.segStart, v.idx, v.vals,  \
+                     mult, R, slabG)
+  switch (run_capacity(v.maxSeg)) {
+    case 5: CYC_TILES_GRAD(5, false); break;
+    case 6: CYC_TILES_GRAD(6, false); break;
+    case 8: CYC_TILES_GRAD(8, false); break;
+    default: CYC_TILES_GRAD(5, true); break;
+  }
+#undef CYC_TILES_GRAD
   CYC_LAUNCH_CHECK("k_tiles_grad");
   return CYC_OK;
 }
@@ -665,7 +801,17 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
   const int64_t segs = (t->n + kTileRows - 1) / kTileRows * T;
   hipLaunchKernelGGL(k_set_i64, dim3(1), dim3(1), 0, st, (int64_t*)t->segStart.ptr + segs, t->nnz);
   CYC_LAUNCH_CHECK("k_set_i64");
+  if (int rc = t->maxDev.reserve(sizeof(unsigned long long))) return rc;
+  CYC_HIP(hipMemsetAsync(t->maxDev.ptr, 0, sizeof(unsigned long long), st));
+  const int64_t s0 = rb0 * T;
+  hipLaunchKernelGGL(k_seg_max, dim3((unsigned)std::min<int64_t>((segs - s0 + 255) / 256, 4096)),
+                     dim3(256), 0, st, (const int64_t*)t->segStart.ptr, s0, segs,
+                     (unsigned long long*)t->maxDev.ptr);
+  CYC_LAUNCH_CHECK("k_seg_max");
+  unsigned long long mx = 0;
+  CYC_HIP(hipMemcpyAsync(&mx, t->maxDev.ptr, sizeof(mx), hipMemcpyDeviceToHost, st));
   CYC_HIP(hipStreamSynchronize(st));
+  t->maxSeg = std::max<int64_t>(t->maxSeg, (int64_t)mx);
   return CYC_OK;
 }
 

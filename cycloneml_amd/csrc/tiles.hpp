@@ -26,6 +26,7 @@ struct TilesView {
   int T = 1;             // column chunks
   int Wt = 1;            // columns per chunk (the last chunk may be shorter)
   int64_t nRB = 0;       // row blocks
+  int64_t maxSeg = 0;    // nonzeros of the longest segment
   const int64_t* segStart = nullptr;
   const uint32_t* idx = nullptr;
   const double* vals = nullptr;

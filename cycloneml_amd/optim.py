@@ -321,8 +321,8 @@ class DifferentiableLossAggregator:
         if not ws > 0.0:
             raise N.IllegalArgumentException(
                 f"The effective number of instances should be greater than 0.0, but was {ws}.")
-        g = _download(self.gradientSumArray)
-        return (1.0 / ws) * g
+        # BLAS.scal(1.0 / weightSum, ...) on the device, then one copy out
+        return _download(self.gradientSumArray * (1.0 / ws))
 
     @property
     def loss(self) -> float:
