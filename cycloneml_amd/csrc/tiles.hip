@@ -595,14 +595,12 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
   }
 }
 
-// nonzeros per lane per run buffer for a layout whose longest segment has
-// maxSeg nonzeros: the smallest instance that takes every run in one load
-// (0: none does -- the LONG instance, 5 per lane and a loop for the rest)
-int run_capacity(int64_t maxSeg) {
-  for (int kc : {5, 6, 8})
-    if (maxSeg <= 64 * kc) return kc;
-  return 0;
-}
+// Five nonzeros per lane per run buffer: a layout whose longest segment has
+// at most 320 takes the instance without the reload loop, any other the
+// LONG one (config 5's 47.7M segments average 268, the longest ~360: LONG,
+// whose common path waits the same; six per lane without the loop costs
+// more load and LDS instructions per step for mostly idle lanes).
+bool long_runs(int64_t maxSeg) { return maxSeg > 5 * 64; }
 
 }  // namespace
 
@@ -635,12 +633,8 @@ int tiles_margin(const TilesView& v, const double* labels, const double* weights
       HIP_KERNEL_NAME(k_tiles_margin<CYC_TILES_MARGIN_NB, CYC_TILES_MARGIN_CS, KC, LONG>),       \
       dim3((unsigned)grid), dim3(kTPB), 0, st, d, v.segStart, v.idx, v.vals, labels, weights,   \
       coef, fitIntercept, kind, offset, lscale, sigma, eps, mult, slabS)
-  switch (run_capacity(v.maxSeg)) {
-    case 5: CYC_TILES_MARGIN(5, false); break;
-    case 6: CYC_TILES_MARGIN(6, false); break;
-    case 8: CYC_TILES_MARGIN(8, false); break;
-    default: CYC_TILES_MARGIN(5, true); break;
-  }
+  if (long_runs(v.maxSeg)) CYC_TILES_MARGIN(5, true);
+  else CYC_TILES_MARGIN(5, false);
 #undef CYC_TILES_MARGIN
   CYC_LAUNCH_CHECK("k_tiles_margin");
   return CYC_OK;
@@ -662,12 +656,8 @@ int tiles_grad(const TilesView& v, const double* mult, double* slabG, int* range
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_grad<CYC_TILES_GRAD_NB, CYC_TILES_GRAD_MS, KC, LONG>), \
                      dim3((unsigned)(sts * R)), dim3(kTPB), 0, st, d, v.segStart, v.idx, v.vals,  \
                      mult, R, slabG)
-  switch (run_capacity(v.maxSeg)) {
-    case 5: CYC_TILES_GRAD(5, false); break;
-    case 6: CYC_TILES_GRAD(6, false); break;
-    case 8: CYC_TILES_GRAD(8, false); break;
-    default: CYC_TILES_GRAD(5, true); break;
-  }
+  if (long_runs(v.maxSeg)) CYC_TILES_GRAD(5, true);
+  else CYC_TILES_GRAD(5, false);
 #undef CYC_TILES_GRAD
   CYC_LAUNCH_CHECK("k_tiles_grad");
   return CYC_OK;
