@@ -29,6 +29,12 @@
 
 #include "common.hpp"
 
+// 1: the covariance syrk in the 8-row, three-per-CU form with the means in
+// LDS; 0: the 16-row, two-per-CU form with the means in registers (A/B)
+#ifndef CYC_GRAM_COV_MLDS
+#define CYC_GRAM_COV_MLDS 0
+#endif
+
 namespace {
 
 constexpr int TILE = 128;
@@ -159,11 +165,16 @@ __global__ __launch_bounds__(GT, 2) void k_gram_tiles(
 // discards.  MEAN: the mean is subtracted as the operands leave LDS (the
 // same dsub as the staged kernel), rows past the end masked to zero.
 // Needs p even (16-byte rows of a panel); odd p takes k_gram_tiles.
-template <bool MEAN, int KCH = 8, int NB = 2, int OCC = 3>
+// MLDS: the tile's 2 x 128 means read from LDS at every k-step instead of
+// held in 16 VGPRs (which cost the MEAN form its third workgroup per CU).
+template <bool MEAN, int KCH = 8, int NB = 2, int OCC = 3, bool MLDS = false>
 __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
     const double* __restrict__ X, int64_t nrows, int p, const double* __restrict__ mean,
     int tilesPerSide, int64_t rowsPerSplit, double* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) double Pn[NB][2][KCH * LDSW];
+  // ONE shared array: the chunk panels, then (MLDS) the means
+  __shared__ __attribute__((aligned(16))) double lds[NB * 2 * KCH * LDSW + (MLDS ? 2 * TILE : 0)];
+  auto Pn = [&](int b, int pn) { return lds + (b * 2 + pn) * KCH * LDSW; };
+  double* const mS = lds + NB * 2 * KCH * LDSW;
   constexpr int DPW = KCH / 2;   // DMAs per wave per chunk
   int t = blockIdx.x, ti = 0;
   while (t >= tilesPerSide - ti) { t -= tilesPerSide - ti; ++ti; }
@@ -181,7 +192,12 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = cyc_double4{0.0, 0.0, 0.0, 0.0};
   double mI[4], mJ[4];
-  if constexpr (MEAN) {
+  if constexpr (MEAN && MLDS) {
+    // mS[0 .. 127]: the I panel's means, mS[128 .. 255]: the J panel's (one
+    // per thread, GT = 256; visible after the first chunk's barrier)
+    const int c = (tid < TILE ? I0 : J0) + (tid & (TILE - 1));
+    mS[tid] = c < p ? mean[c] : 0.0;
+  } else if constexpr (MEAN) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ci = I0 + wy * 64 + q * 16 + (lane & 15), cj = J0 + wx * 64 + q * 16 + (lane & 15);
@@ -200,13 +216,16 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
 #pragma unroll
       for (int pn = 0; pn < 2; ++pn)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(Pn[b][pn] + rr * LDSW), 16,
+            rs, (__attribute__((address_space(3))) void*)(Pn(b, pn) + rr * LDSW), 16,
             (rr * p + (pn ? J0 : I0)) * 8 + lane * 16, 0, 0, 0);
     }
   };
   auto compute = [&](int b, int64_t rb) {
-    const double* Ai = Pn[b][0];
-    const double* Aj = Pn[b][1];
+    // rows of the chunk inside the split (uniform); the rest read as zero,
+    // which the mean would turn nonzero: masked
+    const int left = (int)min<int64_t>(r1 - rb, KCH);
+    const double* Ai = Pn(b, 0);
+    const double* Aj = Pn(b, 1);
 #pragma unroll
     for (int kk = 0; kk < KCH; kk += 4) {
       double a[4], bb[4];
@@ -217,11 +236,13 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
         bb[q] = Aj[krow * LDSW + wx * 64 + q * 16 + (lane & 15)];
       }
       if constexpr (MEAN) {
-        const bool ok = rb + krow < r1;
+        const bool ok = krow < left;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          a[q] = ok ? dsub(a[q], mI[q]) : 0.0;
-          bb[q] = ok ? dsub(bb[q], mJ[q]) : 0.0;
+          const double mi = MLDS ? mS[wy * 64 + q * 16 + (lane & 15)] : mI[q];
+          const double mj = MLDS ? mS[TILE + wx * 64 + q * 16 + (lane & 15)] : mJ[q];
+          a[q] = ok ? dsub(a[q], mi) : 0.0;
+          bb[q] = ok ? dsub(bb[q], mj) : 0.0;
         }
       }
 #pragma unroll
@@ -586,7 +607,10 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   cyc::KernelTimer timer(!dma ? "k_gram_tiles" : mean ? "k_gram_dma_cov" : "k_gram_dma", st);
   const dim3 grid(pairs, (unsigned)splits);
   double* slab = (double*)plan->slab.ptr;
-  if (dma && mean)
+  if (dma && mean && CYC_GRAM_COV_MLDS)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<true, 8, 2, 3, true>), grid, dim3(GT), 0, st, X,
+                       nrows, p, mean, tps, rps, slab);
+  else if (dma && mean)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<true, 16, 2, 2>), grid, dim3(GT), 0, st, X, nrows,
                        p, mean, tps, rps, slab);
   else if (dma)

@@ -462,7 +462,9 @@ __constant__ double kExp2Tab[32] = {
 // libm) it returns 0, so -inf gives 0; NaN stays NaN.  tests/
 // test_logistic_gpu.py sweeps it against the host libm.
 __device__ __forceinline__ double exp_neg(double x, const double* __restrict__ T) {
-  if (x < -746.0) return 0.0;
+  // a select, not a branch (a branch here splits the softmax epilogue's wave)
+  const bool under = x < -746.0;
+  x = under ? -746.0 : x;
   const double kd = __builtin_rint(x * 46.16624130844683);   // 32 / ln2
   double r = __builtin_fma(kd, -0.021660849392446835, x);
   r = __builtin_fma(kd, -5.145609244655338e-14, r);
@@ -474,7 +476,9 @@ __device__ __forceinline__ double exp_neg(double x, const double* __restrict__ T
   q = __builtin_fma(q, r, 0.5);
   q = __builtin_fma(q, r, 1.0);
   q = __builtin_fma(q, r, 1.0);
-  return __builtin_ldexp(T[k & 31] * q, k >> 5);
+  double e = __builtin_ldexp(T[k & 31] * q, k >> 5);
+  asm volatile("" : "+v"(e));   // computed on every lane (no branch around it)
+  return under ? 0.0 : e;
 }
 
 // exp_neg over an array (cyc_softmax_exp_dev: its accuracy test)
@@ -485,6 +489,14 @@ __global__ void k_softmax_exp(const double* __restrict__ x, int64_t n, double* _
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
     out[i] = exp_neg(x[i], T);
+}
+
+// a row-16 DPP move of a double (both halves; all lanes active)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
 }
 
 constexpr int MR = 256;    // rows per margin tile (8 waves x 32 rows)
@@ -527,6 +539,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
   __shared__ __attribute__((aligned(16))) double Ws[2][WBUF + 32 + CP];
   double* const expT = Ws[1] + WBUF;
   double* const offS = expT + 32;
+  __shared__ double plS[MR];   // each wave's 32 label probabilities of a tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4;
   const int64_t tiles = (n + MR - 1) / MR;
@@ -604,86 +617,118 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
       return;
     }
     // Epilogue: lane holds rows 32 wave + 16 t + (lane>>4) + 4r, classes
-    // 16 ct + (lane & 15).
+    // 16 ct + (lane & 15).  Branch-free (selects, DPP row reductions, the
+    // multiplier stores through a per-tile buffer descriptor that drops rows
+    // past n), so the wave never splits; the only branch is the wave-uniform
+    // one into the +inf margin case.  Each row's label probability is parked
+    // in LDS and the tile's 32 logs per wave run once, one row per lane.
+    // l15: the lane's class within a tile, opaque to the optimizer: values derived
+    // from it are recomputed per tile instead of hoisted out of the tile loop
+    // into registers (which spilled)
+    int l15 = lane & 15;
+    asm volatile("" : "+v"(l15));
+    const int64_t nr = min<int64_t>(MR, n - r0);
+    const auto mR = __builtin_amdgcn_make_buffer_rsrc((void*)(mult + r0 * CP), (short)0,
+                                                      (int)(nr * CP * 8), 0x00020000);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int64_t row = r0 + wave * 32 + t * 16 + (lane >> 4) + 4 * r;
-        const bool rowok = row < n;
+        const int rl = wave * 32 + t * 16 + (lane >> 4) + 4 * r;   // row within the tile
+        const bool rowok = r0 + rl < n;
         double m[CT];
+        // the row's max by fmax, +inf included (the reference leaves +inf
+        // out of its max; a row holding one takes the branch below)
         double mx = -1.7976931348623157e308;  // Double.MinValue (Utils.scala:113)
-        int infc = 1 << 30;
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-          const int c = ct * 16 + (lane & 15);
-          const double oc = offS[c];
-          m[ct] = acc[t][ct][r] + oc;  // 1.0*temp + 1.0*offset (netlib dgemm)
-          if (c < C) {
-            if (m[ct] == __builtin_inf()) infc = min(infc, c);
-            else if (m[ct] > mx) mx = m[ct];
-          }
+          const int c = ct * 16 + l15;
+          m[ct] = acc[t][ct][r] + offS[c];  // 1.0*temp + 1.0*offset (netlib dgemm)
+          mx = fmax(mx, (ct < CT - 1 || c < C) ? m[ct] : mx);
         }
+        mx = fmax(mx, dpp_f64<0xB1>(mx));   // quad_perm [1,0,3,2]
+        mx = fmax(mx, dpp_f64<0x4E>(mx));   // quad_perm [2,3,0,1]
+        mx = fmax(mx, dpp_f64<0x141>(mx));  // row_half_mirror
+        mx = fmax(mx, dpp_f64<0x140>(mx));  // row_mirror
+        // the probabilities replace the margins in place (p = m).  INF: the
+        // wave holds a +inf margin (a wave-uniform branch, never taken on
+        // finite margins): the max over the other classes, and for a row
+        // holding one, probability 1 for the first such class and 0 * m for
+        // the rest.
+        auto softmax = [&](auto infTag) {
+          constexpr bool INF = decltype(infTag)::value;
+          int infc = 1 << 30;
+          if constexpr (INF) {
+            mx = -1.7976931348623157e308;
 #pragma unroll
-        for (int k = 1; k < 16; k <<= 1) {
-          mx = fmax(mx, __shfl_xor(mx, k));
-          infc = min(infc, __shfl_xor(infc, k));
-        }
-        // the probabilities replace the margins in place (p = m)
-        double (&p)[CT] = m;
-        if (infc < (1 << 30)) {
+            for (int ct = 0; ct < CT; ++ct) {
+              const int c = ct * 16 + l15;
+              const bool valid = ct < CT - 1 || c < C;
+              if (valid && m[ct] == __builtin_inf()) infc = min(infc, c);
+              else if (valid && m[ct] > mx) mx = m[ct];
+            }
 #pragma unroll
-          for (int ct = 0; ct < CT; ++ct) {
-            const int c = ct * 16 + (lane & 15);
-            p[ct] = (c == infc) ? 1.0 : 0.0 * m[ct];
+            for (int k = 1; k < 16; k <<= 1) {
+              mx = fmax(mx, __shfl_xor(mx, k));
+              infc = min(infc, __shfl_xor(infc, k));
+            }
           }
-        } else {
+          const bool rowInf = INF && infc < (1 << 30);
           double sum = 0.0;
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) {
-            const int c = ct * 16 + (lane & 15);
-            p[ct] = (c < C) ? ((CYC_MLR_PROBE & 16) ? (m[ct] - mx) : exp_neg(m[ct] - mx, expT))
-                            : 0.0;
-            sum += p[ct];
+            const int c = ct * 16 + l15;
+            const double e = (CYC_MLR_PROBE & 16) ? (m[ct] - mx) : exp_neg(m[ct] - mx, expT);
+            const double pe = (ct < CT - 1 || c < C) ? e : 0.0;
+            m[ct] = rowInf ? ((c == infc) ? 1.0 : 0.0 * m[ct]) : pe;
+            sum += m[ct];
           }
-#pragma unroll
-          for (int k = 1; k < 16; k <<= 1) sum += __shfl_xor(sum, k);
-          sum = __shfl(sum, lane & 48);  // one association order per row
+          // butterfly sums in which both lanes of a pair add the same two
+          // values: every lane of the row ends with the same bits
+          sum += dpp_f64<0xB1>(sum);
+          sum += dpp_f64<0x4E>(sum);
+          sum += dpp_f64<0x141>(sum);
+          sum += dpp_f64<0x140>(sum);
           const double inv = 1.0 / sum;
 #pragma unroll
-          for (int ct = 0; ct < CT; ++ct) p[ct] = inv * p[ct];
-        }
+          for (int ct = 0; ct < CT; ++ct) m[ct] = rowInf ? m[ct] : inv * m[ct];
+        };
+        if (__builtin_amdgcn_ballot_w64(mx == __builtin_inf()) != 0)
+          softmax(std::true_type{});
+        else
+          softmax(std::false_type{});
+        double (&p)[CT] = m;
         // unconditional shuffles: a shuffle under `rowok` made the compiler
         // wait vmcnt(0) on labL / wL at every row, draining the stores
         const int q = 16 * t + 4 * r + (lane >> 4);   // the row within the wave's 32
         const double wq = __shfl(wL, q), lq = __shfl(labL, q);
-        const double w = rowok ? wq : 0.0;
+        const double w = (rowok && wq > 0) ? wq : 0.0;
         const int label = rowok ? (int)lq : 0;
+        const int voff = rowok ? (rl * CP + l15) * 8 : OOB;   // rows past n: dropped
         double pl = 0.0;
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-          if (ct == (label >> 4)) pl = p[ct];
-        pl = __shfl(pl, (lane & 48) | (label & 15));
-        if (rowok && (lane & 15) == 0) {
-          wsum += w;
-          if (w > 0) loss -= w * log(pl);
-        }
+        for (int ct = 0; ct < CT; ++ct) pl = (ct == (label >> 4)) ? p[ct] : pl;
+        if ((lane & 15) == (label & 15)) plS[wave * 32 + q] = pl;
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-          const int c = ct * 16 + (lane & 15);
-          double mu;
-          if (w > 0) {
-            mu = (w != 1.0) ? w * p[ct] : p[ct];
-            if (c == label) mu -= w;
-          } else {
-            mu = 0.0 * p[ct];
-          }
-          if (c >= C || !rowok) mu = 0.0;
-          if ((CYC_MLR_PROBE & 8) == 0 && rowok) mult[row * CP + c] = mu;
+          const int c = ct * 16 + l15;
+          // w p - w at the label (w * p is p at w = 1); 0 * p at w <= 0
+          double mu = w * p[ct] - (c == label ? w : 0.0);
+          mu = (ct < CT - 1 || c < C) && rowok ? mu : 0.0;
+          if constexpr ((CYC_MLR_PROBE & 8) == 0)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i32, mu), mR,
+                                                  voff + ct * 128, 0, 0);
           ms[ct] += mu;
         }
+        // one row group at a time: interleaving them spills
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
+    // the loss: row 32 wave + (lane & 31) on lanes 0..31
+    const double pl = plS[wave * 32 + (lane & 31)];
+    const double wr = (lane < 32 && r0 + wave * 32 + lane < n) ? wL : 0.0;
+    wsum += wr;
+    loss -= (wr > 0) ? wr * log(pl) : 0.0;
   };
   double xa[2][4], xb[2][4];
   bool pre = false;   // chunk 0 of this tile already in flight (xa, Ws[0])
@@ -736,12 +781,15 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
     if (pre) loadW(0);
     epilogue(r0, labL, wL);
   }
-  // per-wave partials: loss/wsum from lanes with (lane & 15) == 0, multSum
-  // per class summed over the 4 row groups of the wave.
+  // per-wave partials: loss/wsum over the lanes (one row of each tile per
+  // lane 0..31), multSum per class summed over the 4 row groups of the wave.
 #pragma unroll
-  for (int k = 16; k < 64; k <<= 1) {
+  for (int k = 1; k < 64; k <<= 1) {
     loss += __shfl_xor(loss, k);
     wsum += __shfl_xor(wsum, k);
+  }
+#pragma unroll
+  for (int k = 16; k < 64; k <<= 1) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) ms[ct] += __shfl_xor(ms[ct], k);
   }
