@@ -636,12 +636,6 @@ __device__ __forceinline__ double err_term2(int e, double n1, double mu, int d) 
 // by at most this much (larger shifts could overflow its 32-bit bounds)
 constexpr int kShMax = 2;
 
-// 1: the one-limb pass runs persistent (k_screen32's PERSIST); 0: one row
-// group per workgroup (an A/B switch)
-#ifndef CYC_SCREEN1_PERSIST
-#define CYC_SCREEN1_PERSIST 0
-#endif
-
 template <int S, int W, int LIMBS, bool LIST>
 __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void k_screen32(
     const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
@@ -674,35 +668,26 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
   // (kCandMax), the one-limb pass's for the two-limb refinement (kCand1)
   constexpr int CMAX = LIMBS == 1 ? kCand1 : kCandMax;
   const int64_t total = LIST ? (int64_t)*rowsInCount : n;
-  // The one-limb pass is persistent: a workgroup takes row groups blockIdx.x,
-  // blockIdx.x + gridDim.x, ..., and the B-tile ring runs on across them --
-  // the last two steps of a group DMA the next group's tiles 0 and 1 (the
-  // centers are the same for every group), so a group starts with its first
-  // tiles in LDS instead of a DMA round trip, and the tail's reduction uses
-  // the slot of the group's last tile, the one no DMA is filling.  sl0: the
-  // ring slot of the group's tile 0; returns the next group's.
-  constexpr bool PERSIST = PAIR && !LIST && CYC_SCREEN1_PERSIST;
   // one group of 32 W rows (positions)
-  auto group = [&](int64_t grp, int sl0, bool first, bool hasNext) -> int {
+  auto group = [&](int64_t grp) {
   const int64_t pos0 = (grp * W + wave) * 32;        // first position of this wave
   // waves past the end still take part in every barrier (zero rows)
   const int rows = (int)max<int64_t>(0, min<int64_t>(32, total - pos0));
-  // scap > 0: list / cand appends go to this group's shard (kmeans_i8.hpp);
-  // the pointers are formed where the tail uses them (kept live across the
-  // step loop they cost the persistent form spilled SGPRs)
+  // scap > 0: list / cand appends go to this group's shard (kmeans_i8.hpp)
   const unsigned shard = (unsigned)((grp * W + wave) % kShards);
-#define listS (scap ? list + (size_t)shard * scap : list)
-#define listCountS (scap ? listCount + shard * kShardStride : listCount)
-#define candRowsS (scap && candRows ? candRows + (size_t)shard * scap : candRows)
-#define candsS (scap && cands ? cands + (size_t)shard * scap * CMAX : cands)
-#define candCountS (scap && candCount ? candCount + shard * kShardStride : candCount)
+  int32_t* const listS = scap ? list + (size_t)shard * scap : list;
+  unsigned int* const listCountS = scap ? listCount + shard * kShardStride : listCount;
+  int32_t* const candRowsS = scap && candRows ? candRows + (size_t)shard * scap : candRows;
+  int32_t* const candsS = scap && cands ? cands + (size_t)shard * scap * CMAX : cands;
+  unsigned int* const candCountS =
+      scap && candCount ? candCount + shard * kShardStride : candCount;
   auto rowAt = [&](int i) -> int64_t {   // global row of position pos0 + i (i < rows)
     if constexpr (LIST) return rowsIn[pos0 + i];
     else return pos0 + i;
   };
   if (!P.ok) {   // uniform over the grid
     if (lane < rows) listS[atomicAdd(listCountS, 1u)] = (int32_t)rowAt(lane);
-    return sl0;
+    return;
   }
   // tile t -> slot t % 3: each wave DMAs fragments wave, wave + W, ... and the
   // tile's cq (all waves write the same 256 bytes); past the last tile the
@@ -711,8 +696,7 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
   const int nsteps = PAIR ? ktp / 2 : ktp;          // ktp is even
   auto issue = [&](int t, int slot) {
     if constexpr (PAIR && (CYC_PROBE_MODE & 2)) return;
-    // past the last tile: the next group's first tiles, or a re-read
-    const int tt = t < nsteps ? t : (PERSIST && hasNext) ? t - nsteps : nsteps - 1;
+    const int tt = t < nsteps ? t : nsteps - 1;
     char* dst = lds + slot * TB;
 #pragma unroll
     for (int j = 0; j < FR / W; ++j) {
@@ -731,11 +715,8 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
           (const void*)(cq + (PAIR ? (size_t)tt * 64 + lane : (size_t)tt * 32 + r)),
           (__attribute__((address_space(3))) void*)(dst + FR * 1024), 4, 0, 0);
   };
-  auto next_slot = [](int slot) { return slot == 2 ? 0 : slot + 1; };
-  if (first) {
-    issue(0, sl0);
-    issue(1, next_slot(sl0));
-  }
+  issue(0, 0);
+  issue(1, 1);
   // A fragments of the wave's 32 rows, all substeps and limbs
   v4i A[S][LIMBS];
   const bool rowOk = r < rows;
@@ -870,13 +851,14 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
     __builtin_amdgcn_s_barrier();
     issue(t + 2, slot == 0 ? 2 : slot - 1);
   };
+  auto next_slot = [](int slot) { return slot == 2 ? 0 : slot + 1; };
 
   // MODE.FP_ROUND single precision = toward -inf (the L' are lower bounds)
   __builtin_amdgcn_s_setreg(0x801, 2);
   // (software-pipelining the epilogue beside the next tile's MFMAs needs a
   // second accumulator set: 193 VGPRs, two waves per SIMD, 4 % slower than
   // this form at 168 VGPRs and three waves per SIMD)
-  int sl = sl0;
+  int sl = 0;
   if constexpr (PAIR) {
     // The one-limb bounds in the units 2^(exmin + ec - SH) of the wave's
     // smallest exponent, shifted left by IB with the tile index in the low
@@ -967,15 +949,10 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
     sl = next_slot(sl);
   }
   __builtin_amdgcn_s_setreg(0x801, 0);
-  // the trailing re-read DMAs land before the tail (a next group's first
-  // tiles stay in flight into the two slots the tail does not touch)
-  if (!(PERSIST && hasNext)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // the tail's LDS: the slot of the group's last tile (persistent), else
-  // the ring's start
-  char* const red = PERSIST ? lds + ((sl + 2) % 3) * TB : lds;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing re-read DMAs
   if constexpr (PAIR && (CYC_PROBE_MODE & 4)) {   // probe: no reduction / certification
     if (lane < rows) assign[rowAt(lane)] = sV1[lane & 15] ^ sV2[(lane + 1) & 15];
-    return sl;
+    return;
   }
 
   // LIMBS = 2: each lane's own best and second best (one center column per
@@ -1032,7 +1009,7 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
   // lane holds row register q = lane bits 1..4
   // per-wave reduction area in the (now idle) slots: L1, L2, I1 x 32 rows
   __syncthreads();
-  float* redL1 = (float*)red + wave * 96;   // LIMBS = 2: the V1, V2 bits
+  float* redL1 = (float*)lds + wave * 96;   // LIMBS = 2: the V1, V2 bits
   float* redL2 = redL1 + 32;
   int* redI1 = (int*)(redL1 + 64);
   if ((lane & 1) == 0) {
@@ -1131,7 +1108,7 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
       // and a lane whose SECOND best reaches it too (an index not kept)
       // sends the row to the three-limb pass.  <= kCandMax candidates go to
       // the candidate list (exact fp64 distances, screen_cands).
-      int* thrS = (int*)red + W * 96 + wave * (64 + 32 * (CMAX + 1));
+      int* thrS = (int*)lds + W * 96 + wave * (64 + 32 * (CMAX + 1));
       int* wantS = thrS + 32;
       int* candS = thrS + 64;
       if (lane < 32) {
@@ -1175,25 +1152,10 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
     }
   }
   __syncthreads();   // the reduction area is the next group's tile ring
-  return sl;
-#undef listS
-#undef listCountS
-#undef candRowsS
-#undef candsS
-#undef candCountS
   };
-  static_assert(!PAIR || 4 * (W * 96 + W * (64 + 32 * (kCand1 + 1))) <= TB,
-                "the tail's reduction area fits one ring slot");
-  if constexpr (PERSIST) {
-    const int64_t groups = (total + 32 * W - 1) / (32 * W);
-    int sl = 0;
-    for (int64_t grp = blockIdx.x; grp < groups; grp += gridDim.x)
-      sl = group(grp, sl, grp == blockIdx.x, grp + gridDim.x < groups);
-  } else if ((int64_t)blockIdx.x * 32 * W < total) {
-    // LIST: the grid covers n rows; groups past the count leave at once (a
-    // grid-stride loop here costs the three-limb S = 8 form ~30 spilled VGPRs)
-    group(blockIdx.x, 0, true, false);
-  }
+  // LIST: the grid covers n rows; groups past the count leave at once (a
+  // grid-stride loop here costs the three-limb S = 8 form ~30 spilled VGPRs)
+  if ((int64_t)blockIdx.x * 32 * W < total) group(blockIdx.x);
 }
 
 template <int S, int W, int LIMBS, bool LIST>
@@ -1206,11 +1168,7 @@ int launch_screen32(const void* img, const int2* meta, const double* xnorm, int6
                     unsigned int scap = 0) {
   KernelTimer timer(LIMBS == 1 ? "k_kmeans_screen1" : LIMBS == 2 ? "k_kmeans_screen2"
                                                     : "k_kmeans_screen3", st);
-  int64_t wg = (n + 32 * W - 1) / (32 * W);   // W waves x 32 rows
-  // the persistent one-limb pass: every workgroup slot of the chip once
-  // (three per CU at 164 VGPRs and 3 x 49 KB of LDS)
-  if (LIMBS == 1 && !LIST && CYC_SCREEN1_PERSIST)
-    wg = std::min<int64_t>(wg, (int64_t)(12 / W) * device_cus());
+  const int64_t wg = (n + 32 * W - 1) / (32 * W);   // W waves x 32 rows
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32<S, W, LIMBS, LIST>), dim3((unsigned)wg),
                      dim3(64 * W), 0, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
                      cq, g, cnorm, prm, ktp, rowsIn, rowsInCount, assign, list, listCount,
