@@ -29,12 +29,6 @@
 
 #include "common.hpp"
 
-// 1: the covariance syrk in the 8-row, three-per-CU form with the means in
-// LDS; 0: the 16-row, two-per-CU form with the means in registers (A/B)
-#ifndef CYC_GRAM_COV_MLDS
-#define CYC_GRAM_COV_MLDS 0
-#endif
-
 namespace {
 
 constexpr int TILE = 128;
@@ -163,18 +157,22 @@ __global__ __launch_bounds__(GT, 2) void k_gram_tiles(
 // the split's end read as zero (buffer range); columns past p of the last
 // panel read the next row's values, which only reach tile entries the fold
 // discards.  MEAN: the mean is subtracted as the operands leave LDS (the
-// same dsub as the staged kernel), rows past the end masked to zero.
+// same dsub as the staged kernel).  Rows past the split's end read as zero,
+// which the mean would turn into -mean: their A operands are zeroed (one
+// select per A operand; a zero A makes the product zero).  Exact zeros, as
+// SPARK-26158's accuracy case needs: a correction after the loop (missing
+// rows x mean_i mean_j) cancels catastrophically there, and a second,
+// select-free copy of the loop body for the full chunks spilled (400 B).
+// The 8-row, three-per-CU form spills in the MEAN case (564 B), and the
+// means read from LDS instead of registers measured 611.7 vs 567.7 ms at
+// 30M x 1024.
 // Needs p even (16-byte rows of a panel); odd p takes k_gram_tiles.
-// MLDS: the tile's 2 x 128 means read from LDS at every k-step instead of
-// held in 16 VGPRs (which cost the MEAN form its third workgroup per CU).
-template <bool MEAN, int KCH = 8, int NB = 2, int OCC = 3, bool MLDS = false>
+template <bool MEAN, int KCH = 8, int NB = 2, int OCC = 3>
 __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
     const double* __restrict__ X, int64_t nrows, int p, const double* __restrict__ mean,
     int tilesPerSide, int64_t rowsPerSplit, double* __restrict__ slab) {
-  // ONE shared array: the chunk panels, then (MLDS) the means
-  __shared__ __attribute__((aligned(16))) double lds[NB * 2 * KCH * LDSW + (MLDS ? 2 * TILE : 0)];
+  __shared__ __attribute__((aligned(16))) double lds[NB * 2 * KCH * LDSW];   // the chunk panels
   auto Pn = [&](int b, int pn) { return lds + (b * 2 + pn) * KCH * LDSW; };
-  double* const mS = lds + NB * 2 * KCH * LDSW;
   constexpr int DPW = KCH / 2;   // DMAs per wave per chunk
   int t = blockIdx.x, ti = 0;
   while (t >= tilesPerSide - ti) { t -= tilesPerSide - ti; ++ti; }
@@ -192,12 +190,7 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = cyc_double4{0.0, 0.0, 0.0, 0.0};
   double mI[4], mJ[4];
-  if constexpr (MEAN && MLDS) {
-    // mS[0 .. 127]: the I panel's means, mS[128 .. 255]: the J panel's (one
-    // per thread, GT = 256; visible after the first chunk's barrier)
-    const int c = (tid < TILE ? I0 : J0) + (tid & (TILE - 1));
-    mS[tid] = c < p ? mean[c] : 0.0;
-  } else if constexpr (MEAN) {
+  if constexpr (MEAN) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ci = I0 + wy * 64 + q * 16 + (lane & 15), cj = J0 + wx * 64 + q * 16 + (lane & 15);
@@ -221,8 +214,7 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
     }
   };
   auto compute = [&](int b, int64_t rb) {
-    // rows of the chunk inside the split (uniform); the rest read as zero,
-    // which the mean would turn nonzero: masked
+    // rows of the chunk inside the split (uniform); the rest read as zero
     const int left = (int)min<int64_t>(r1 - rb, KCH);
     const double* Ai = Pn(b, 0);
     const double* Aj = Pn(b, 1);
@@ -239,10 +231,8 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
         const bool ok = krow < left;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const double mi = MLDS ? mS[wy * 64 + q * 16 + (lane & 15)] : mI[q];
-          const double mj = MLDS ? mS[TILE + wx * 64 + q * 16 + (lane & 15)] : mJ[q];
-          a[q] = ok ? dsub(a[q], mi) : 0.0;
-          bb[q] = ok ? dsub(bb[q], mj) : 0.0;
+          a[q] = ok ? dsub(a[q], mI[q]) : 0.0;
+          bb[q] = dsub(bb[q], mJ[q]);
         }
       }
 #pragma unroll
@@ -607,10 +597,7 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   cyc::KernelTimer timer(!dma ? "k_gram_tiles" : mean ? "k_gram_dma_cov" : "k_gram_dma", st);
   const dim3 grid(pairs, (unsigned)splits);
   double* slab = (double*)plan->slab.ptr;
-  if (dma && mean && CYC_GRAM_COV_MLDS)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<true, 8, 2, 3, true>), grid, dim3(GT), 0, st, X,
-                       nrows, p, mean, tps, rps, slab);
-  else if (dma && mean)
+  if (dma && mean)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<true, 16, 2, 2>), grid, dim3(GT), 0, st, X, nrows,
                        p, mean, tps, rps, slab);
   else if (dma)
