@@ -29,6 +29,13 @@
 
 #include "common.hpp"
 
+// 1: the plain k_gram_dma's blocks grouped by row split per XCD (an A/B
+// switch; the covariance form keeps the 2-D grid: grouped, it measured
+// 625.7 vs 586.0 ms at 30M x 1024 for a 6 % smaller FETCH_SIZE)
+#ifndef CYC_GRAM_XCDMAP
+#define CYC_GRAM_XCDMAP 1
+#endif
+
 namespace {
 
 constexpr int TILE = 128;
@@ -167,18 +174,35 @@ __global__ __launch_bounds__(GT, 2) void k_gram_tiles(
 // means read from LDS instead of registers measured 611.7 vs 567.7 ms at
 // 30M x 1024.
 // Needs p even (16-byte rows of a panel); odd p takes k_gram_tiles.
-template <bool MEAN, int KCH = 8, int NB = 2, int OCC = 3>
+template <bool MEAN, int KCH = 8, int NB = 2, int OCC = 3, bool XCDMAP = !MEAN && CYC_GRAM_XCDMAP>
 __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
     const double* __restrict__ X, int64_t nrows, int p, const double* __restrict__ mean,
-    int tilesPerSide, int64_t rowsPerSplit, double* __restrict__ slab) {
+    int tilesPerSide, int64_t rowsPerSplit, int splits, double* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) double lds[NB * 2 * KCH * LDSW];   // the chunk panels
   auto Pn = [&](int b, int pn) { return lds + (b * 2 + pn) * KCH * LDSW; };
   constexpr int DPW = KCH / 2;   // DMAs per wave per chunk
-  int t = blockIdx.x, ti = 0;
+  // a 1-D grid dealt round-robin over the 8 XCDs (blocks b and b + 8 share
+  // one): block b -> XCD slot b % 8, k = b / 8; the XCD's k-th block takes
+  // tile pair k % pairs of split 8 (k / pairs) + b % 8, so all tile pairs
+  // of a split run on one XCD, started together, and the panels they share
+  // can be L2 hits there (splits padded to a multiple of 8: the padding
+  // blocks leave at once)
+  const int pairs = tilesPerSide * (tilesPerSide + 1) / 2;
+  int pair, split;
+  if constexpr (XCDMAP) {
+    const int kq = blockIdx.x >> 3;
+    pair = kq % pairs;
+    split = (kq / pairs) * 8 + (blockIdx.x & 7);
+    if (split >= splits) return;
+  } else {
+    pair = blockIdx.x;
+    split = blockIdx.y;
+  }
+  int t = pair, ti = 0;
   while (t >= tilesPerSide - ti) { t -= tilesPerSide - ti; ++ti; }
   const int tj = ti + t;
   const int I0 = ti * TILE, J0 = tj * TILE;
-  const int64_t r0 = (int64_t)blockIdx.y * rowsPerSplit;
+  const int64_t r0 = (int64_t)split * rowsPerSplit;
   const int64_t r1 = min<int64_t>(nrows, r0 + rowsPerSplit);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -258,8 +282,7 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  const int pairs = tilesPerSide * (tilesPerSide + 1) / 2;
-  double* out = slab + ((size_t)blockIdx.y * pairs + blockIdx.x) * TILE * TILE;
+  double* out = slab + ((size_t)split * pairs + pair) * TILE * TILE;
 #pragma unroll
   for (int qa = 0; qa < 4; ++qa)
 #pragma unroll
@@ -596,13 +619,16 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   // k_gram_dma<true, 16, 2, 2> instance as k_gram_dma too)
   cyc::KernelTimer timer(!dma ? "k_gram_tiles" : mean ? "k_gram_dma_cov" : "k_gram_dma", st);
   const dim3 grid(pairs, (unsigned)splits);
+  // the plain k_gram_dma: one dimension, splits padded to a multiple of 8
+  // (XCDMAP)
+  const dim3 gridD = CYC_GRAM_XCDMAP ? dim3((unsigned)(pairs * ((splits + 7) / 8) * 8)) : grid;
   double* slab = (double*)plan->slab.ptr;
   if (dma && mean)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<true, 16, 2, 2>), grid, dim3(GT), 0, st, X, nrows,
-                       p, mean, tps, rps, slab);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<true, 16, 2, 2>), grid, dim3(GT), 0, st, X,
+                       nrows, p, mean, tps, rps, (int)splits, slab);
   else if (dma)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<false>), grid, dim3(GT), 0, st, X, nrows, p,
-                       mean, tps, rps, slab);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<false>), gridD, dim3(GT), 0, st, X, nrows, p,
+                       mean, tps, rps, (int)splits, slab);
   else
     hipLaunchKernelGGL(k_gram_tiles, grid, dim3(GT), 0, st, X, nrows, p, mean, tps, rps, slab);
   CYC_LAUNCH_CHECK("k_gram_dma / k_gram_tiles");
