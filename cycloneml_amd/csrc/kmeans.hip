@@ -48,26 +48,49 @@ constexpr int kChunkRows = 256;           // rows per deterministic partial sum
 constexpr int kMaxK = 8192;               // LDS histogram bound for the sort
 
 // ---------------------------------------------------------------- helpers
-__global__ void k_row_norms(const double* __restrict__ X, int64_t n, int d,
-                            double* __restrict__ norms) {
-  // One lane per row; rows are staged through LDS so the global reads are
-  // coalesced (64 rows x 8 columns per step).
-  __shared__ double tile[64][9];
-  const int lane = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * 64;
-  double s = 0.0;
-  for (int c0 = 0; c0 < d; c0 += 8) {
-    for (int e = lane; e < 64 * 8; e += 64) {
-      int r = e >> 3, c = e & 7;
-      int64_t gr = row0 + r;
-      tile[r][c] = (gr < n && c0 + c < d) ? X[gr * d + c0 + c] : 0.0;
+// Vectors.norm(dense, 2) (Vectors.scala:489-514): one thread per row, the
+// squares summed in column order.  256 rows per block; 16-column slices of
+// them staged through two LDS buffers (row stride 17 doubles: the row-wise
+// reads hit distinct banks), loaded coalesced (16 consecutive threads read
+// one row's 128 bytes) one slice ahead in registers: one barrier per slice.
+constexpr int kNormRows = 256, kNormCols = 16, kNormStride = kNormCols + 1;
+__global__ __launch_bounds__(kNormRows) void k_row_norms(const double* __restrict__ X, int64_t n,
+                                                         int d, double* __restrict__ norms) {
+  __shared__ double tile[2][kNormRows * kNormStride];
+  const int t = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * kNormRows;
+  constexpr int PER = kNormRows * kNormCols / kNormRows;   // loads per thread per slice
+  double v[PER];
+  // element e = t + 256 i of a slice: row e / 16, column e % 16
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = t + kNormRows * i, r = e / kNormCols, c = c0 + e % kNormCols;
+      const int64_t gr = row0 + r;
+      v[i] = (gr < n && c < d) ? X[gr * d + c] : 0.0;
     }
-    __syncthreads();
-    int lim = min(8, d - c0);
-    for (int c = 0; c < lim; ++c) s = dadd(s, dmul(tile[lane][c], tile[lane][c]));
-    __syncthreads();
+  };
+  auto store = [&](double* b) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = t + kNormRows * i;
+      b[(e / kNormCols) * kNormStride + e % kNormCols] = v[i];
+    }
+  };
+  double s = 0.0;
+  load(0);
+  store(tile[0]);
+  int buf = 0;
+  for (int c0 = 0; c0 < d; c0 += kNormCols) {
+    if (c0 + kNormCols < d) load(c0 + kNormCols);
+    __syncthreads();   // slice c0 in tile[buf]; every thread done with tile[buf ^ 1]
+    const double* row = tile[buf] + t * kNormStride;
+    const int lim = min(kNormCols, d - c0);
+    for (int c = 0; c < lim; ++c) s = dadd(s, dmul(row[c], row[c]));
+    if (c0 + kNormCols < d) store(tile[buf ^ 1]);
+    buf ^= 1;
   }
-  int64_t gr = row0 + lane;
+  const int64_t gr = row0 + t;
   if (gr < n) norms[gr] = __builtin_sqrt(s);
 }
 
@@ -2248,8 +2271,8 @@ extern "C" {
 int cyc_row_norms_dev(const double* X, int64_t n, int32_t d, double* norms, void* stream) {
   CYC_REQUIRE(n >= 0 && d > 0, "n >= 0 and d > 0");
   if (n == 0) return CYC_OK;
-  hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n + 63) / 64)), dim3(64), 0,
-                     cyc::as_stream(stream), X, n, d, norms);
+  hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n + kNormRows - 1) / kNormRows)),
+                     dim3(kNormRows), 0, cyc::as_stream(stream), X, n, d, norms);
   CYC_LAUNCH_CHECK("k_row_norms");
   return CYC_OK;
 }
@@ -2405,8 +2428,8 @@ int cyc_kmeans_stats_dev(cyc_kmeans_plan p, const double* C, double* stats_out, 
     // new VectorWithNorm(center): norms computed here (KMeansModel.scala:47-56)
     if ((rc = p->cosCn.reserve(sizeof(double) * (size_t)p->k))) return rc;
     const double* cn = (const double*)p->cosCn.ptr;
-    hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((p->k + 63) / 64)), dim3(64), 0, st, C,
-                       (int64_t)p->k, p->d, (double*)p->cosCn.ptr);
+    hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((p->k + kNormRows - 1) / kNormRows)),
+                       dim3(kNormRows), 0, st, C, (int64_t)p->k, p->d, (double*)p->cosCn.ptr);
     CYC_LAUNCH_CHECK("k_row_norms");
     if ((rc = cos_enqueue(p, cn, p->k >= 2, nullptr, 0, st))) return rc;
     if (p->dense_ok && (rc = cos_transpose(p, C, st))) return rc;
@@ -2448,8 +2471,8 @@ int cyc_kmeans_rows_create(cyc_kmeans_plan p, const double* X, int64_t n, void* 
         delete r;
         return rc;
       }
-      hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n,
-                         p->d, (double*)xn.ptr);
+      hipLaunchKernelGGL(k_row_norms, dim3((unsigned)((n + kNormRows - 1) / kNormRows)),
+                         dim3(kNormRows), 0, st, X, n, p->d, (double*)xn.ptr);
       CYC_LAUNCH_CHECK("k_row_norms");
       rc = cyc::km8::rows_quantize(X, n, p->d, r->img.ptr, (int2*)r->meta.ptr, st,
                                    (const double*)xn.ptr, (double*)r->unorm.ptr);
