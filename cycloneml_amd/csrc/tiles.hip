@@ -232,6 +232,10 @@ __device__ __forceinline__ void load_run(const uint32_t* __restrict__ vidx,
 #ifndef CYC_TILES_MARGIN_CS
 #define CYC_TILES_MARGIN_CS 1
 #endif
+// 1: the margin pass's coefficient chunks staged by LDS DMA (an A/B switch)
+#ifndef CYC_TILES_MARGIN_DMA
+#define CYC_TILES_MARGIN_DMA 1
+#endif
 
 // Margin pass, persistent over (super row block sb, column chunk c) steps:
 // this workgroup's super blocks sb = blockIdx.x + i * gridDim.x (8 row blocks
@@ -240,7 +244,10 @@ __device__ __forceinline__ void load_run(const uint32_t* __restrict__ vidx,
 // chunks are loaded meanwhile, L2 hits), and wave i walks segment
 // (8 sb + i, c); the runs of the next NB - 1 steps are in flight in
 // registers, across super block boundaries too.
-template <int NB, int CS, int KC, bool LONG>
+// DMA: the coefficient chunks go HBM/L2 -> LDS by buffer_load ... lds (two
+// 1 KiB pieces per wave, issued one step ahead), no staging registers or
+// ds_writes; else through registers, CS steps ahead.
+template <int NB, int CS, int KC, bool LONG, bool DMA>
 __global__ __launch_bounds__(kTPB) void k_tiles_margin(
     TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
     const double* __restrict__ vvals, const double* __restrict__ labels,
@@ -264,7 +271,7 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
   const int Tp = (T + NB - 1) / NB * NB;
   const int64_t mySB = nSB > blockIdx.x ? (nSB - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};     // loss, weight, multiplierSum, sigmaGradSum
-  double creg[CS][kCPT];                    // chunk of step g in creg[g % CS]
+  double creg[DMA ? 1 : CS][kCPT];          // chunk of step g in creg[g % CS]
   uint32_t ib[NB][KC];
   double vb[NB][KC];
   Run rr[NB];
@@ -297,9 +304,22 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
   // loop head, where it then drained every prefetched run (vmcnt(0)).  The
   // runs of the other NB - 2 steps and the staging loads of the steps since
   // -- (NB - 2) (2 KC + 4) operations -- stay in flight.
+  // the chunk of step (k, c) into b by DMA: wave w's pieces 2w, 2w + 1
+  auto dma_coef = [&](int64_t k, int c, double* b) {
+    const bool on = k < mySB && c < T;
+    const int64_t c0 = on ? (int64_t)c * v.Wt : 0;
+    const int wl = on ? (int)std::min<int64_t>(v.Wt, v.F - c0) : 0;
+    const auto rc = rsrc(coef + c0, (int64_t)wl * 8);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rc, (__attribute__((address_space(3))) void*)(b + (wave * 2 + i) * 128), 16,
+          (wave * 2 + i) * 1024 + lane * 16, 0, 0, 0);
+  };
+  static_assert(!DMA || kTileCols * 8 == kTileWaves * 2 * 1024, "two 1 KiB pieces per wave");
   auto consume = [&](int64_t len, const double* cfp, const uint32_t (&ix)[KC],
                      const double (&vx)[KC]) {
-    __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2) * (2 * KC + 4)));
+    __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2) * (2 * KC + (DMA ? 2 : 4))));
     double c[KC];
 #pragma unroll
     for (int j = 0; j < KC; ++j)   // lanes past the end read [0]
@@ -336,7 +356,13 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
     double* nxt = cf + (par ^ 1) * kTileCols;
     int64_t k2;
     int c2;
-    if constexpr ((CYC_TILES_PROBE & 8) == 0) {
+    if constexpr (DMA) {
+      // chunk of the next step into the buffer every wave left behind the
+      // last barrier; landed (this wave's pieces) before the next barrier:
+      // only this step's run loads are issued after it
+      ahead(k, c, 1, k2, c2);
+      dma_coef(k2, c2, nxt);
+    } else if constexpr ((CYC_TILES_PROBE & 8) == 0) {
 #pragma unroll
       for (int i = 0; i < kCPT; ++i) nxt[tid + kTPB * i] = cs[i];
       ahead(k, c, CS + 1, k2, c2);
@@ -345,20 +371,27 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
     ahead(k, c, NB - 1, k2, c2);
     rn = run_of(k2, c2);
     load_run(vidx, vvals, rn, 0, lane, in, vn);
+    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(vm_wait(2 * KC));
     step_barrier();
   };
 
-  // prologue: chunk 0 into cf[0], chunks 1 .. CS in registers, runs of
-  // steps 0 .. NB - 2 in flight
-  load_coef(0, 0, creg[0]);
+  // prologue: chunk 0 into cf[0], chunks 1 .. CS in registers (DMA: chunk
+  // 0 only, landed before the first barrier), runs of steps 0 .. NB - 2 in
+  // flight
+  if constexpr (DMA) {
+    dma_coef(0, 0, cf);
+    __builtin_amdgcn_s_waitcnt(vm_wait(0));
+  } else {
+    load_coef(0, 0, creg[0]);
 #pragma unroll
-  for (int i = 0; i < kCPT; ++i) cf[tid + kTPB * i] = creg[0][i];
+    for (int i = 0; i < kCPT; ++i) cf[tid + kTPB * i] = creg[0][i];
 #pragma unroll
-  for (int s1 = 1; s1 <= CS; ++s1) {
-    int64_t k1;
-    int c1;
-    ahead(0, 0, s1, k1, c1);
-    load_coef(k1, c1, creg[s1 % CS]);
+    for (int s1 = 1; s1 <= CS; ++s1) {
+      int64_t k1;
+      int c1;
+      ahead(0, 0, s1, k1, c1);
+      load_coef(k1, c1, creg[s1 % CS]);
+    }
   }
 #pragma unroll
   for (int u = 0; u < NB - 1; ++u) {
@@ -423,7 +456,7 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
 #pragma unroll
       for (int u = 0; u < NB; ++u)
         step(k, c + u, rr[u], ib[u], vb[u], rr[(u + NB - 1) % NB], ib[(u + NB - 1) % NB],
-             vb[(u + NB - 1) % NB], creg[(u + 1) % CS]);
+             vb[(u + NB - 1) % NB], creg[DMA ? 0 : (u + 1) % CS]);
     }
     // epilogue (BinaryLogisticBlockAggregator.scala:104-122 and siblings)
     const int64_t r0 = ((int64_t)blockIdx.x + k * gridDim.x) * kTileSuperRows;
@@ -474,13 +507,19 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
 #ifndef CYC_TILES_GRAD_MS
 #define CYC_TILES_GRAD_MS 1
 #endif
+// 1: the gradient pass's multiplier slices staged by LDS DMA (an A/B switch)
+#ifndef CYC_TILES_GRAD_DMA
+#define CYC_TILES_GRAD_DMA 1
+#endif
 
 // Gradient pass: workgroup (super chunk st = 8 column chunks, row range)
 // over its row blocks.  Per row block: the multiplier slice goes registers
 // -> LDS (the next ones loaded while this one is used); wave j walks segment
 // (rb, 8 st + j) into its chunk's column sums, with the runs of the next
 // NB - 1 row blocks in flight.
-template <int NB, int MS, int KC, bool LONG>
+// DMA: the multiplier slices go to LDS by buffer_load ... lds, one row
+// block ahead (as the margin pass's coefficient chunks).
+template <int NB, int MS, int KC, bool LONG, bool DMA>
 __global__ __launch_bounds__(kTPB) void k_tiles_grad(
     TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
     const double* __restrict__ vvals, const double* __restrict__ mult, int ranges,
@@ -496,7 +535,7 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
   const int range = blockIdx.x % ranges, st = blockIdx.x / ranges;
   const int64_t rbA = v.nRB * range / ranges, rbB = v.nRB * (range + 1) / ranges;
   const int c = st * kTileWaves + wave;                 // this wave's column chunk
-  double mreg[MS][kMPT];                                // slice r in mreg[(r - rbA) % MS]
+  double mreg[DMA ? 1 : MS][kMPT];                      // slice r in mreg[(r - rbA) % MS]
   uint32_t ib[NB][KC];
   double vb[NB][KC];
   Run rr[NB];
@@ -511,12 +550,24 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
       m[i] = __builtin_bit_cast(
           double, __builtin_amdgcn_raw_buffer_load_b64(rm, tid * 8, i * kTPB * 8, 0));
   };
+  // row block rb's slice into b by DMA: wave w's pieces 2w, 2w + 1
+  auto dma_mult = [&](int64_t rb, double* b) {
+    const int64_t r0 = rb * kTileRows;
+    const auto rm = rsrc(mult + (rb < rbB ? r0 : 0),
+                         rb < rbB ? std::min<int64_t>(kTileRows, v.n - r0) * 8 : 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rm, (__attribute__((address_space(3))) void*)(b + (wave * 2 + i) * 128), 16,
+          (wave * 2 + i) * 1024 + lane * 16, 0, 0, 0);
+  };
+  static_assert(!DMA || kTileRows * 8 == kTileWaves * 2 * 1024, "two 1 KiB pieces per wave");
   double* myG = gt + wave * v.Wt;
   // waits for the whole run first, on every path (the margin pass's
   // consume says why)
   auto consume = [&](int64_t len, const double* mvp, const uint32_t (&ix)[KC],
                      const double (&vx)[KC]) {
-    __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2) * (2 * KC + 4 * MS)));
+    __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2) * (2 * KC + (DMA ? 2 : 4 * MS))));
     double m[KC];
 #pragma unroll
     for (int j = 0; j < KC; ++j)   // lanes past the end read [0]
@@ -552,23 +603,31 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
       }
     }
     double* nxt = mv + (par ^ 1) * kTileRows;
-    if constexpr ((CYC_TILES_PROBE & 8) == 0) {
+    if constexpr (DMA) {
+      dma_mult(rb + 1, nxt);   // landed before the barrier: only the run loads follow it
+    } else if constexpr ((CYC_TILES_PROBE & 8) == 0) {
 #pragma unroll
       for (int i = 0; i < kMPT; ++i) nxt[tid + kTPB * i] = ms[i];
       load_mult(rb + 1 + MS, ms);
     }
     rn = run_of(rb + NB - 1);
     load_run(vidx, vvals, rn, 0, lane, in, vn);
+    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(vm_wait(2 * KC));
     step_barrier();
   };
 
   // prologue: slice rbA into mv[0], slices rbA + 1 .. rbA + MS in
   // registers, runs rbA .. rbA + NB - 2 in flight
-  load_mult(rbA, mreg[0]);
+  if constexpr (DMA) {
+    dma_mult(rbA, mv);
+    __builtin_amdgcn_s_waitcnt(vm_wait(0));
+  } else {
+    load_mult(rbA, mreg[0]);
 #pragma unroll
-  for (int i = 0; i < kMPT; ++i) mv[tid + kTPB * i] = mreg[0][i];
+    for (int i = 0; i < kMPT; ++i) mv[tid + kTPB * i] = mreg[0][i];
 #pragma unroll
-  for (int s = 1; s <= MS; ++s) load_mult(rbA + s, mreg[s % MS]);
+    for (int s = 1; s <= MS; ++s) load_mult(rbA + s, mreg[s % MS]);
+  }
 #pragma unroll
   for (int u = 0; u < NB - 1; ++u) {
     rr[u] = run_of(rbA + u);
@@ -582,7 +641,7 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
 #pragma unroll
     for (int u = 0; u < NB; ++u)
       step(rb + u, rr[u], ib[u], vb[u], rr[(u + NB - 1) % NB], ib[(u + NB - 1) % NB],
-           vb[(u + NB - 1) % NB], mreg[(u + 1) % MS]);
+           vb[(u + NB - 1) % NB], mreg[DMA ? 0 : (u + 1) % MS]);
   }
   __syncthreads();
   const int64_t col0 = (int64_t)st * kTileWaves * v.Wt;
@@ -628,13 +687,21 @@ int tiles_margin(const TilesView& v, const double* labels, const double* weights
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nSB, device_cus()));
   *wgs = grid;
   const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
-#define CYC_TILES_MARGIN(KC, LONG)                                                              \
+#define CYC_TILES_MARGIN(KC, LONG, DMA)                                                         \
   hipLaunchKernelGGL(                                                                           \
-      HIP_KERNEL_NAME(k_tiles_margin<CYC_TILES_MARGIN_NB, CYC_TILES_MARGIN_CS, KC, LONG>),       \
+      HIP_KERNEL_NAME(k_tiles_margin<CYC_TILES_MARGIN_NB, CYC_TILES_MARGIN_CS, KC, LONG, DMA>),  \
       dim3((unsigned)grid), dim3(kTPB), 0, st, d, v.segStart, v.idx, v.vals, labels, weights,   \
       coef, fitIntercept, kind, offset, lscale, sigma, eps, mult, slabS)
-  if (long_runs(v.maxSeg)) CYC_TILES_MARGIN(5, true);
-  else CYC_TILES_MARGIN(5, false);
+  // the DMA pieces are 16-byte loads: a coefficient vector that is not
+  // 16-byte aligned takes the register-staged instance
+  const bool dma = CYC_TILES_MARGIN_DMA && (reinterpret_cast<uintptr_t>(coef) & 15) == 0;
+  if (long_runs(v.maxSeg)) {
+    if (dma) CYC_TILES_MARGIN(5, true, true);
+    else CYC_TILES_MARGIN(5, true, false);
+  } else {
+    if (dma) CYC_TILES_MARGIN(5, false, true);
+    else CYC_TILES_MARGIN(5, false, false);
+  }
 #undef CYC_TILES_MARGIN
   CYC_LAUNCH_CHECK("k_tiles_margin");
   return CYC_OK;
@@ -652,12 +719,18 @@ int tiles_grad(const TilesView& v, const double* mult, double* slabG, int* range
   *ranges = R;
   const int64_t sts = (v.T + kTileWaves - 1) / kTileWaves;
   const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
-#define CYC_TILES_GRAD(KC, LONG)                                                                \
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_grad<CYC_TILES_GRAD_NB, CYC_TILES_GRAD_MS, KC, LONG>), \
-                     dim3((unsigned)(sts * R)), dim3(kTPB), 0, st, d, v.segStart, v.idx, v.vals,  \
-                     mult, R, slabG)
-  if (long_runs(v.maxSeg)) CYC_TILES_GRAD(5, true);
-  else CYC_TILES_GRAD(5, false);
+#define CYC_TILES_GRAD(KC, LONG, DMA)                                                           \
+  hipLaunchKernelGGL(                                                                           \
+      HIP_KERNEL_NAME(k_tiles_grad<CYC_TILES_GRAD_NB, CYC_TILES_GRAD_MS, KC, LONG, DMA>),        \
+      dim3((unsigned)(sts * R)), dim3(kTPB), 0, st, d, v.segStart, v.idx, v.vals, mult, R, slabG)
+  const bool dma = CYC_TILES_GRAD_DMA && (reinterpret_cast<uintptr_t>(mult) & 15) == 0;
+  if (long_runs(v.maxSeg)) {
+    if (dma) CYC_TILES_GRAD(5, true, true);
+    else CYC_TILES_GRAD(5, true, false);
+  } else {
+    if (dma) CYC_TILES_GRAD(5, false, true);
+    else CYC_TILES_GRAD(5, false, false);
+  }
 #undef CYC_TILES_GRAD
   CYC_LAUNCH_CHECK("k_tiles_grad");
   return CYC_OK;
