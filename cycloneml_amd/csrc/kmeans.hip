@@ -1387,7 +1387,8 @@ __global__ __launch_bounds__(256) void k_chunk_sums_fast(
 #pragma unroll
       for (int u = 0; u < NJ; ++u) {
         const int j = tid + 256 * u;
-        xv[v][u] = j < d ? X[r * d + j] : 0.0;
+        // nontemporal: the rows are read once per iteration
+        xv[v][u] = j < d ? __builtin_nontemporal_load(&X[r * d + j]) : 0.0;
       }
     }
 #pragma unroll

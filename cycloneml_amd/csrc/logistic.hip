@@ -591,8 +591,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
     for (int t = 0; t < 2; ++t) {
       const int off = ((wave * 32 + t * 16 + (lane & 15)) * F + f0) * 8;
       if (f0 + 3 < F) {
-        const v4i32 lo = __builtin_amdgcn_raw_buffer_load_b128(xR, off, 0, 0);
-        const v4i32 hi = __builtin_amdgcn_raw_buffer_load_b128(xR, off + 16, 0, 0);
+        // nontemporal (aux 2): X streams through once per evaluation pass
+        const v4i32 lo = __builtin_amdgcn_raw_buffer_load_b128(xR, off, 0, 2);
+        const v4i32 hi = __builtin_amdgcn_raw_buffer_load_b128(xR, off + 16, 0, 2);
         x[t][0] = __builtin_bit_cast(double, (v2i32){lo[0], lo[1]});
         x[t][1] = __builtin_bit_cast(double, (v2i32){lo[2], lo[3]});
         x[t][2] = __builtin_bit_cast(double, (v2i32){hi[0], hi[1]});
@@ -864,7 +865,7 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
       for (int q = 0; q < 2; ++q) {
         const int f = fcol + 16 * q;
         const int off = f < F ? ((rowOff + 4 * kk + g) * F + f) * 8 : OOB;
-        x[kk][q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xR, off, 0, 0));
+        x[kk][q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xR, off, 0, 2));
       }
   };
   auto step = [&](int64_t rb, int buf, double (&xc)[GR / 4][2], double (&xn)[GR / 4][2]) {
