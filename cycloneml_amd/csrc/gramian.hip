@@ -342,7 +342,8 @@ __global__ void k_col_partial(const double* __restrict__ X, int64_t nrows, int p
   const int64_t r0 = (int64_t)blockIdx.y * rowsPerSplit;
   const int64_t r1 = min<int64_t>(nrows, r0 + rowsPerSplit);
   double s = 0.0;
-  for (int64_t r = r0; r < r1; ++r) s = dadd(s, X[r * p + c]);
+  // nontemporal: the rows stream through once
+  for (int64_t r = r0; r < r1; ++r) s = dadd(s, __builtin_nontemporal_load(&X[r * p + c]));
   part[(int64_t)blockIdx.y * p + c] = s;
 }
 

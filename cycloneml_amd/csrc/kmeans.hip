@@ -67,7 +67,7 @@ __global__ __launch_bounds__(kNormRows) void k_row_norms(const double* __restric
     for (int i = 0; i < PER; ++i) {
       const int e = t + kNormRows * i, r = e / kNormCols, c = c0 + e % kNormCols;
       const int64_t gr = row0 + r;
-      v[i] = (gr < n && c < d) ? X[gr * d + c] : 0.0;
+      v[i] = (gr < n && c < d) ? __builtin_nontemporal_load(&X[gr * d + c]) : 0.0;
     }
   };
   auto store = [&](double* b) {
