@@ -718,7 +718,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
           mu = (ct < CT - 1 || c < C) && rowok ? mu : 0.0;
           if constexpr ((CYC_MLR_PROBE & 8) == 0)
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i32, mu), mR,
-                                                  voff + ct * 128, 0, 0);
+                                                  voff + ct * 128, 0, 2);   // nontemporal
           ms[ct] += mu;
         }
         // one row group at a time: interleaving them spills

@@ -416,8 +416,8 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
 #pragma unroll
       for (int u = 0; u < EB; ++u) {
         const int64_t rr = min<int64_t>(r0 + tid + (int64_t)kTPB * (i0 + u), v.n - 1);
-        l[u] = labels[rr];
-        w[u] = weights ? weights[rr] : 1.0;
+        l[u] = __builtin_nontemporal_load(&labels[rr]);   // streamed once
+        w[u] = weights ? __builtin_nontemporal_load(&weights[rr]) : 1.0;
       }
     };
     ld(0, lab[0], wt[0]);
@@ -443,7 +443,7 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
             m = mm;
           }
           acc[2] += m;
-          mult[r] = m;
+          __builtin_nontemporal_store(m, &mult[r]);
         }
       }
     }
