@@ -164,12 +164,12 @@ __global__ __launch_bounds__(GT, 2) void k_gram_tiles(
 // the split's end read as zero (buffer range); columns past p of the last
 // panel read the next row's values, which only reach tile entries the fold
 // discards.  MEAN: the mean is subtracted as the operands leave LDS (the
-// same dsub as the staged kernel).  Rows past the split's end read as zero,
-// which the mean would turn into -mean: their A operands are zeroed (one
-// select per A operand; a zero A makes the product zero).  Exact zeros, as
-// SPARK-26158's accuracy case needs: a correction after the loop (missing
-// rows x mean_i mean_j) cancels catastrophically there, and a second,
-// select-free copy of the loop body for the full chunks spilled (400 B).
+// same dsub as the staged kernel).  Rows past the split's end are DMA'd
+// from the mean vector, so they centre to exact zeros (as SPARK-26158's
+// accuracy case needs: a correction after the loop, missing rows x mean_i
+// mean_j, cancels catastrophically there) with no select in the loop
+// (zeroing them per operand cost two selects per operand and k-step; a
+// second, select-free copy of the loop body for the full chunks spilled).
 // The 8-row, three-per-CU form spills in the MEAN case (564 B), and the
 // means read from LDS instead of registers measured 611.7 vs 567.7 ms at
 // 30M x 1024.
@@ -222,24 +222,29 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
       mJ[q] = cj < p ? mean[cj] : 0.0;
     }
   }
-  // chunk rb into buffer b: wave w DMAs rows KCH/4 w .. of both panels
+  // chunk rb into buffer b: wave w DMAs rows KCH/4 w .. of both panels.
+  // MEAN: a row past the split's end is the mean itself (its panel columns
+  // DMA'd from the mean vector), which the subtraction below turns into
+  // exact zeros -- no masking in the loop (the row index is wave-uniform,
+  // so the choice is a scalar one)
   auto issue = [&](int64_t rb, int b) {
     const int64_t nr = max<int64_t>(0, min<int64_t>(KCH, r1 - rb));
     const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(X + (nr ? rb : 0) * p), (short)0,
                                                       (int)(nr * p * 8), 0x00020000);
+    const auto rm = __builtin_amdgcn_make_buffer_rsrc((void*)(MEAN ? mean : X), (short)0,
+                                                      MEAN ? p * 8 : 0, 0x00020000);
 #pragma unroll
     for (int u = 0; u < KCH / 4; ++u) {
       const int rr = wave * (KCH / 4) + u;
+      const bool pad = MEAN && rr >= nr;
 #pragma unroll
       for (int pn = 0; pn < 2; ++pn)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(Pn(b, pn) + rr * LDSW), 16,
-            (rr * p + (pn ? J0 : I0)) * 8 + lane * 16, 0, 0, 0);
+            pad ? rm : rs, (__attribute__((address_space(3))) void*)(Pn(b, pn) + rr * LDSW), 16,
+            ((pad ? 0 : rr * p) + (pn ? J0 : I0)) * 8 + lane * 16, 0, 0, 0);
     }
   };
-  auto compute = [&](int b, int64_t rb) {
-    // rows of the chunk inside the split (uniform); the rest read as zero
-    const int left = (int)min<int64_t>(r1 - rb, KCH);
+  auto compute = [&](int b) {
     const double* Ai = Pn(b, 0);
     const double* Aj = Pn(b, 1);
 #pragma unroll
@@ -252,10 +257,9 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
         bb[q] = Aj[krow * LDSW + wx * 64 + q * 16 + (lane & 15)];
       }
       if constexpr (MEAN) {
-        const bool ok = krow < left;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          a[q] = ok ? dsub(a[q], mI[q]) : 0.0;
+          a[q] = dsub(a[q], mI[q]);
           bb[q] = dsub(bb[q], mJ[q]);
         }
       }
@@ -277,7 +281,7 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * DPW) : "memory");
     __syncthreads();   // chunk rb landed everywhere; every wave is past rb - KCH
     issue(rb + (NB - 1) * KCH, b == 0 ? NB - 1 : b - 1);
-    compute(b, rb);
+    compute(b);
     b = b == NB - 1 ? 0 : b + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
