@@ -1480,30 +1480,51 @@ __global__ void k_chunk_sums_nocost(const double* __restrict__ X, int d,
 }
 
 // cost[r] = Vectors.sqdist(C[assign[r]], X[r]) (Vectors.scala:580-587): the
-// distance findClosest returns for the chosen center.  64-row tiles staged
-// through LDS 8 columns at a time (coalesced), one lane per row.
-__global__ void k_row_cost(const double* __restrict__ X, int64_t n, int d,
-                           const double* __restrict__ C, const int32_t* __restrict__ assign,
-                           double* __restrict__ cost) {
-  __shared__ double tile[64][9];
-  const int lane = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * 64;
-  const int64_t myr = row0 + lane;
+// distance findClosest returns for the chosen center.  One thread per row,
+// the rows staged as in k_row_norms (256 rows, 16-column slices through two
+// padded LDS buffers one slice ahead); the centers (L2-resident) read per
+// thread.
+__global__ __launch_bounds__(kNormRows) void k_row_cost(const double* __restrict__ X, int64_t n,
+                                                        int d, const double* __restrict__ C,
+                                                        const int32_t* __restrict__ assign,
+                                                        double* __restrict__ cost) {
+  __shared__ double tile[2][kNormRows * kNormStride];
+  const int t = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * kNormRows;
+  const int64_t myr = row0 + t;
   const double* crow = myr < n ? C + (int64_t)assign[myr] * d : C;
-  double s = 0.0;
-  for (int c0 = 0; c0 < d; c0 += 8) {
-    for (int e = lane; e < 64 * 8; e += 64) {
-      const int r = e >> 3, c = e & 7;
+  constexpr int PER = kNormCols;   // loads per thread per slice
+  double v[PER];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = t + kNormRows * i, r = e / kNormCols, c = c0 + e % kNormCols;
       const int64_t gr = row0 + r;
-      tile[r][c] = (gr < n && c0 + c < d) ? X[gr * d + c0 + c] : 0.0;
+      v[i] = (gr < n && c < d) ? __builtin_nontemporal_load(&X[gr * d + c]) : 0.0;
     }
-    __syncthreads();
-    const int lim = min(8, d - c0);
+  };
+  auto store = [&](double* b) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = t + kNormRows * i;
+      b[(e / kNormCols) * kNormStride + e % kNormCols] = v[i];
+    }
+  };
+  double s = 0.0;
+  load(0);
+  store(tile[0]);
+  int buf = 0;
+  for (int c0 = 0; c0 < d; c0 += kNormCols) {
+    if (c0 + kNormCols < d) load(c0 + kNormCols);
+    __syncthreads();   // slice c0 in tile[buf]; every thread done with tile[buf ^ 1]
+    const double* row = tile[buf] + t * kNormStride;
+    const int lim = min(kNormCols, d - c0);
     for (int c = 0; c < lim; ++c) {
-      const double df = dsub(crow[c0 + c], tile[lane][c]);
+      const double df = dsub(crow[c0 + c], row[c]);
       s = dadd(s, dmul(df, df));
     }
-    __syncthreads();
+    if (c0 + kNormCols < d) store(tile[buf ^ 1]);
+    buf ^= 1;
   }
   if (myr < n) cost[myr] = s;
 }
@@ -2535,7 +2556,8 @@ int cyc_kmeans_assign_dev(cyc_kmeans_plan p, const double* X, const double* xnor
   }
   if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
   if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, n_exact_out, st))) return rc;
-  hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n, p->d, C,
+  hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + kNormRows - 1) / kNormRows)),
+                     dim3(kNormRows), 0, st, X, n, p->d, C,
                      (const int32_t*)assign, cost);
   CYC_LAUNCH_CHECK("k_row_cost");
   return require_check(p, n);
@@ -2576,7 +2598,8 @@ int cyc_kmeans_point_cost_dev(cyc_kmeans_plan p, const double* X, const double* 
   CYC_LAUNCH_CHECK("k_center_transpose");
   if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st, true)))
     return rc;
-  hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n, p->d, C,
+  hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + kNormRows - 1) / kNormRows)),
+                     dim3(kNormRows), 0, st, X, n, p->d, C,
                      (const int32_t*)assign, cost);
   CYC_LAUNCH_CHECK("k_row_cost");
   hipLaunchKernelGGL(k_nostats_cost_fix, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n,
@@ -2631,7 +2654,8 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
       if ((rc = p->costTmp.reserve(sizeof(double) * (size_t)n))) return rc;
       cost = (double*)p->costTmp.ptr;
     }
-    hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n, d, C,
+    hipLaunchKernelGGL(k_row_cost, dim3((unsigned)((n + kNormRows - 1) / kNormRows)),
+                     dim3(kNormRows), 0, st, X, n, d, C,
                        (const int32_t*)assign, cost);
     CYC_LAUNCH_CHECK("k_row_cost");
   }
