@@ -325,28 +325,48 @@ __global__ __launch_bounds__(256) void k_cos_assign_sparse(
   }
 }
 
-// 64-row tiles staged through LDS 8 columns at a time, one lane per row.
-__global__ void k_cos_row_cost(const double* __restrict__ X, int64_t n, int d,
-                               const double* __restrict__ C, const double* __restrict__ cnorm,
-                               const double* __restrict__ xnorm,
-                               const int32_t* __restrict__ assign, double* __restrict__ cost) {
-  __shared__ double tile[64][9];
-  const int lane = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * 64;
-  const int64_t myr = row0 + lane;
+// One thread per row: 256 rows per block, 16-column slices of them staged
+// through two padded LDS buffers one slice ahead (coalesced loads, one
+// barrier per slice); the dot with the chosen center in column order.
+constexpr int kCostRows = 256, kCostCols = 16, kCostStride = kCostCols + 1;
+__global__ __launch_bounds__(kCostRows) void k_cos_row_cost(
+    const double* __restrict__ X, int64_t n, int d, const double* __restrict__ C,
+    const double* __restrict__ cnorm, const double* __restrict__ xnorm,
+    const int32_t* __restrict__ assign, double* __restrict__ cost) {
+  __shared__ double tile[2][kCostRows * kCostStride];
+  const int t = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * kCostRows;
+  const int64_t myr = row0 + t;
   const int a = myr < n ? assign[myr] : 0;
   const double* crow = C + (int64_t)a * d;
-  double s = 0.0;
-  for (int c0 = 0; c0 < d; c0 += 8) {
-    for (int e = lane; e < 64 * 8; e += 64) {
-      const int r = e >> 3, c = e & 7;
+  double v[kCostCols];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < kCostCols; ++i) {
+      const int e = t + kCostRows * i, r = e / kCostCols, c = c0 + e % kCostCols;
       const int64_t gr = row0 + r;
-      tile[r][c] = (gr < n && c0 + c < d) ? X[gr * d + c0 + c] : 0.0;
+      v[i] = (gr < n && c < d) ? __builtin_nontemporal_load(&X[gr * d + c]) : 0.0;
     }
-    __syncthreads();
-    const int lim = min(8, d - c0);
-    for (int c = 0; c < lim; ++c) s = dadd(s, dmul(crow[c0 + c], tile[lane][c]));
-    __syncthreads();
+  };
+  auto store = [&](double* b) {
+#pragma unroll
+    for (int i = 0; i < kCostCols; ++i) {
+      const int e = t + kCostRows * i;
+      b[(e / kCostCols) * kCostStride + e % kCostCols] = v[i];
+    }
+  };
+  double s = 0.0;
+  load(0);
+  store(tile[0]);
+  int buf = 0;
+  for (int c0 = 0; c0 < d; c0 += kCostCols) {
+    if (c0 + kCostCols < d) load(c0 + kCostCols);
+    __syncthreads();   // slice c0 in tile[buf]; every thread done with tile[buf ^ 1]
+    const double* row = tile[buf] + t * kCostStride;
+    const int lim = min(kCostCols, d - c0);
+    for (int c = 0; c < lim; ++c) s = dadd(s, dmul(crow[c0 + c], row[c]));
+    if (c0 + kCostCols < d) store(tile[buf ^ 1]);
+    buf ^= 1;
   }
   if (myr < n) cost[myr] = 1.0 - s / cnorm[a] / xnorm[myr];
 }
@@ -515,7 +535,8 @@ int assign_sparse(const int64_t* rowptr, const int32_t* colidx, const double* va
 int row_cost(const double* X, int64_t n, int d, const double* C, const double* cnorm,
              const double* xnorm, const int32_t* assign, double* cost, hipStream_t st) {
   if (n <= 0) return CYC_OK;
-  hipLaunchKernelGGL(k_cos_row_cost, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, X, n, d, C,
+  hipLaunchKernelGGL(k_cos_row_cost, dim3((unsigned)((n + kCostRows - 1) / kCostRows)),
+                     dim3(kCostRows), 0, st, X, n, d, C,
                      cnorm, xnorm, assign, cost);
   CYC_LAUNCH_CHECK("k_cos_row_cost");
   return CYC_OK;
