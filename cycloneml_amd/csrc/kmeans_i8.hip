@@ -60,6 +60,11 @@ namespace {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef double v2d __attribute__((ext_vector_type(2)));
+
+#ifndef CYC_QUANT_COAL
+#define CYC_QUANT_COAL 1   // k_rows_quantize: 16 B coalesced row loads
+#endif
 
 // one f32 ulp toward -inf; f32 rounded down / up from fp64
 __device__ __forceinline__ float ulp_dn(float f) {
@@ -130,7 +135,7 @@ __global__ __launch_bounds__(256) void k_rows_quantize(const double* __restrict_
                                                        int d, int D, unsigned* __restrict__ img,
                                                        int2* __restrict__ meta,
                                                        const double* __restrict__ scale,
-                                                       double* __restrict__ unorm) {
+                                                       double* __restrict__ unorm, int vec) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < n; row += nw) {
@@ -139,6 +144,31 @@ __global__ __launch_bounds__(256) void k_rows_quantize(const double* __restrict_
     double m = 0.0, s1 = 0.0, s2 = 0.0;
     bool fin = true;
     const double sc = scale ? scale[row] : 1.0;
+#if CYC_QUANT_COAL
+    // lane holds elements 128 h + 2 lane + {0, 1}: one 16 B load per lane and
+    // 1 KiB contiguous per wave instruction (vec: d even, X 16 B aligned)
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int j = h * 128 + 2 * lane;
+      v2d w = {0.0, 0.0};
+      if (vec) {
+        if (j < d) w = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(x + j));
+      } else {
+        if (j < d) w.x = x[j];
+        if (j + 1 < d) w.y = x[j + 1];
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        double t = q ? w.y : w.x;
+        if (scale) t = t / sc;
+        v[2 * h + q] = t;
+        fin = fin && __builtin_isfinite(t);
+        m = __builtin_fmax(m, __builtin_fabs(t));
+        s1 += __builtin_fabs(t);
+        s2 += t * t;
+      }
+    }
+#else
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
 #pragma unroll
@@ -153,6 +183,7 @@ __global__ __launch_bounds__(256) void k_rows_quantize(const double* __restrict_
         s2 += t * t;
       }
     }
+#endif
     m = wave_max(m);
     s1 = wave_sum(s1);
     if (unorm) {
@@ -162,6 +193,27 @@ __global__ __launch_bounds__(256) void k_rows_quantize(const double* __restrict_
     const bool allFin = __all(fin);
     const int e = choose_exp(m);
     const bool bad = !allFin || e > kMaxExp;
+#if CYC_QUANT_COAL
+    unsigned char* db = reinterpret_cast<unsigned char*>(img + row * (int64_t)(3 * D / 4));
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int j0 = h * 128 + 2 * lane;
+      if (j0 < D) {
+        int a[2], b[2], c[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (bad) {
+            a[q] = b[q] = c[q] = 0;
+          } else {
+            quant3(v[2 * h + q], e, a[q], b[q], c[q]);
+          }
+        }
+        *reinterpret_cast<unsigned short*>(db + j0) = (unsigned short)((a[0] & 0xff) | ((a[1] & 0xff) << 8));
+        *reinterpret_cast<unsigned short*>(db + D + j0) = (unsigned short)((b[0] & 0xff) | ((b[1] & 0xff) << 8));
+        *reinterpret_cast<unsigned short*>(db + 2 * D + j0) = (unsigned short)((c[0] & 0xff) | ((c[1] & 0xff) << 8));
+      }
+    }
+#else
     unsigned* dst = img + row * (int64_t)(3 * D / 4);
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
@@ -181,6 +233,7 @@ __global__ __launch_bounds__(256) void k_rows_quantize(const double* __restrict_
         dst[(2 * D + j0) / 4] = pack4(c);
       }
     }
+#endif
     if (lane == 0) {
       // |xh|_1 <= |x|_1 + d 2^(e-22); the fp64 sum is rounded up generously
       const double n1 = bad ? 0.0 : s1 * (1.0 + 0x1p-40) + (double)d * __builtin_ldexp(1.0, e - 22);
@@ -1873,8 +1926,9 @@ int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipS
   if (n <= 0) return CYC_OK;
   const int D = 64 * ksteps(d);
   const int64_t blocks = std::min<int64_t>((n + 3) / 4, 65536);
+  const int vec = (d % 2 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
   hipLaunchKernelGGL(k_rows_quantize, dim3((unsigned)blocks), dim3(256), 0, st, X, n, d, D,
-                     (unsigned*)img, meta, scale, unorm);
+                     (unsigned*)img, meta, scale, unorm, vec);
   CYC_LAUNCH_CHECK("k_rows_quantize");
   return CYC_OK;
 }

@@ -437,6 +437,17 @@ typedef int v2i32 __attribute__((ext_vector_type(2)));
 #ifndef CYC_MLR_PROBE
 #define CYC_MLR_PROBE 0
 #endif
+// k_mlr_margins: 16-feature chunks per barrier group; waves per workgroup;
+// dephased workgroup pairs (see the kernel)
+#ifndef CYC_MLR_GROUP
+#define CYC_MLR_GROUP 2
+#endif
+#ifndef CYC_MLR_NW
+#define CYC_MLR_NW 4
+#endif
+#ifndef CYC_MLR_DEPHASE
+#define CYC_MLR_DEPHASE false
+#endif
 
 // 2^(j/32), j = 0..31, correctly rounded (exp_neg's table)
 __constant__ double kExp2Tab[32] = {
@@ -499,23 +510,25 @@ __device__ __forceinline__ double dpp_f64(double v) {
   return __hiloint2double(hi, lo);
 }
 
-constexpr int MR = 256;    // rows per margin tile (8 waves x 32 rows)
+constexpr int MR = 256;    // rows per margin tile, at most (8 waves x 32 rows)
 constexpr int MK = 16;     // features per LDS chunk
-constexpr int MT = 512;    // threads per margin workgroup
 
-// margins = X W^T (+ offset) for 256-row tiles, 16-feature chunks, on
+// margins = X W^T (+ offset) for 32 NW-row tiles, 16-feature chunks, on
 // v_mfma_f64_16x16x4f64: 2 row tiles x CT class tiles of 16x16 per wave;
-// softmax / loss / multiplier epilogue in registers.  Persistent over tiles,
-// one 8-wave workgroup per CU.
+// softmax / loss / multiplier epilogue in registers.  Persistent over tiles:
+// two 4-wave workgroups per CU (NW = 4; each SIMD holds a wave of each, so
+// one's epilogue and barrier waits run beside the other's MFMAs -- 9 % faster
+// than one 8-wave workgroup per CU with the barrier grouping below).
 // X goes from HBM straight into registers in the MFMA A layout -- lane (row
 // r = l & 15, group g = l >> 4) holds features f0 + 4g .. 4g + 3 of its row
 // for k-steps 0..3 (the contraction order within a chunk is permuted: 128
 // contiguous bytes per row per chunk, two dwordx4 loads per lane per row
 // tile) -- loaded one chunk ahead into a second register set: no LDS, no
 // barrier for X.  W chunks (16 features x C classes, contiguous in coef,
-// 12.8 KB at C = 100) are DMA'd into two LDS buffers (buffer_load ... lds,
-// 1 KiB pieces spread over the waves, one chunk ahead; no registers), one
-// barrier per chunk.  Padding classes read the next coefficients (finite;
+// 12.8 KB at C = 100) are DMA'd into 2 G LDS buffers (buffer_load ... lds,
+// 1 KiB pieces spread over the waves, a group of G chunks ahead; no
+// registers), one barrier per group of G = 2 chunks (one per chunk: 4.5 %
+// slower).  Padding classes read the next coefficients (finite;
 // their margins are never used) or zero past the end of coef.
 // (The last class tile on v_mfma_f64_4x4x4f64, as k_mlr_grad does, measured
 // 4-5 % slower here at C = 100, with or without sched_barrier fences.)
@@ -534,11 +547,12 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
   constexpr int CP = CT * 16;
   static_assert(MK == 16, "the A layout covers 16 features per chunk");
   constexpr int WBUF = MK * CP + 128;   // doubles per W buffer (whole 1 KiB pieces)
-  // the two W buffers, then exp_neg's table and the per-class offsets (never
-  // DMA targets)
-  __shared__ __attribute__((aligned(16))) double Ws[2][WBUF + 32 + CP];
-  double* const expT = Ws[1] + WBUF;
-  double* const offS = expT + 32;
+  constexpr int G = CYC_MLR_GROUP, NBUF = 2 * G;
+  // the W buffers (two groups of G chunks), exp_neg's table and the per-class
+  // offsets (never DMA targets)
+  __shared__ __attribute__((aligned(16))) double Ws[NBUF][WBUF];
+  __shared__ double expT[32];
+  __shared__ double offS[CP];
   __shared__ double plS[MR];   // each wave's 32 label probabilities of a tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4;
@@ -570,9 +584,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
                                                     0x00020000);
   // pieces covering every index the B reads touch: (MK - 1) C + CP doubles
   const int wpieces = (((MK - 1) * C + CP) * 8 + 1023) / 1024;
-  auto loadW = [&](int ch) {      // chunk ch's 16 x C run of coef into buffer ch & 1
+  auto loadW = [&](int ch, int buf) {   // chunk ch's 16 x C run of coef into Ws[buf]
     if constexpr ((CYC_MLR_PROBE & 4) != 0) return;
-    double* dst = Ws[ch & 1];
+    double* dst = Ws[buf];
     const int base = ch * MK * C * 8;
     for (int q = wave; q < wpieces; q += MT / 64)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -732,28 +746,39 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
     loss -= (wr > 0) ? wr * log(pl) : 0.0;
   };
   double xa[2][4], xb[2][4];
-  bool pre = false;   // chunk 0 of this tile already in flight (xa, Ws[0])
+  // The workgroup's chunks (tile, ch) in order form one stream s = 0, 1, ..;
+  // chunk s's W sits in Ws[s % NBUF].  One barrier per group of G chunks (at
+  // s % G == 0): every wave's DMA of this group has landed (each waited for
+  // its own) and every wave is past the previous group, whose buffers then
+  // take the next group's W -- G chunks of MFMAs between barriers.
+  const int64_t myTiles = blockIdx.x < tiles ? (tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const int64_t S = myTiles * nch;
+  auto loadWs = [&](int64_t s) {
+    if (s < S) loadW((int)(s % nch), (int)(s % NBUF));
+  };
+#pragma unroll
+  for (int j = 0; j < G; ++j) loadWs(j);
+  int64_t s = 0;
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t r0 = tile * MR;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[t][ct] = cyc_double4{0.0, 0.0, 0.0, 0.0};
-    if (!pre) {
-      __syncthreads();   // the previous tile's last W buffer is free
-      loadW(0);
-    }
     loadX(r0, 0, xa);
-    // chunk ch: wait for its loads, barrier (its W visible everywhere, every
-    // wave past chunk ch - 1), issue chunk ch + 1's loads, multiply
+    // chunk ch: wait for its loads (barrier at a group start), issue chunk ch
+    // + 1's X (and at a group start the next group's W), multiply
     auto step = [&](int ch, double (&xc)[2][4], double (&xn)[2][4]) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (ch + 1 < nch) {
-        loadX(r0, ch + 1, xn);
-        loadW(ch + 1);
+      const bool gs = G == 1 || s % G == 0;
+      if (gs) __syncthreads();
+      if (ch + 1 < nch) loadX(r0, ch + 1, xn);
+      if (gs) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) loadWs(s + G + j);
       }
-      const double* W = Ws[ch & 1];
+      const double* W = Ws[s % NBUF];
+      ++s;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
 #pragma unroll
@@ -768,18 +793,11 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
       step(ch, xa, xb);
       if (ch + 1 < nch) step(ch + 1, xb, xa);
     }
-    // the next tile's W chunk 0 goes out before this tile's epilogue (the X
-    // registers stay free for it: prefetching X too spills at CT = 7): with
-    // an even chunk count the last chunk read Ws[1], and every wave is past
-    // chunk nch - 2 (Ws[0]) since the last barrier
-    const int64_t next = tile + gridDim.x;
-    pre = (nch % 2) == 0 && next < tiles;
     // the tile's labels and weights, loaded (unconditionally, from a
-    // clamped row) before the W DMA and the stores of the epilogue
+    // clamped row) before the stores of the epilogue
     const int64_t lr = min<int64_t>(r0 + wave * 32 + (lane & 31), n - 1);
     const double labL = labels[lr];
     const double wL = weights ? weights[lr] : 1.0;
-    if (pre) loadW(0);
     epilogue(r0, labL, wL);
   }
   // per-wave partials: loss/wsum over the lanes (one row of each tile per
@@ -1625,8 +1643,10 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
   // k_mlr_grad: the last class tile on the 4x4x4 form when it holds 1..4
   // classes (2.6 % faster at C = 100)
   const bool t4 = C % 16 != 0 && C % 16 <= 4;
-  const int mblocks = 256;   // persistent: one 8-wave workgroup per CU
-  const int64_t mwaves = (int64_t)mblocks * (MT / 64);
+  // persistent: two 4-wave workgroups per CU (CYC_MLR_NW = 8: one 8-wave one)
+  constexpr int mnw = CYC_MLR_NW, mrows = 32 * mnw;
+  const int mblocks = 256 * 8 / mnw;
+  const int64_t mwaves = (int64_t)mblocks * mnw;
   const int ftiles = (F + GF - 1) / GF;
   if ((rc = p->multBuf.reserve(sizeof(double) * (size_t)chunk * CP)) ||
       (rc = p->slabS.reserve(sizeof(double) * (size_t)mwaves * 2)) ||
@@ -1651,12 +1671,12 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
     const double* Xc = X + c0 * F;
     const double* lc = labels + c0;
     const double* wc = weights ? weights + c0 : nullptr;
-    const int64_t tiles = (m + MR - 1) / MR;
+    const int64_t tiles = (m + mrows - 1) / mrows;
     const unsigned mb = (unsigned)std::min<int64_t>(mblocks, tiles);
     CYC_HIP(hipMemsetAsync(p->slabS.ptr, 0, sizeof(double) * (size_t)mwaves * 2, st));
     CYC_HIP(hipMemsetAsync(p->slabMS.ptr, 0, sizeof(double) * (size_t)mwaves * CP, st));
 #define CYC_MLR_M(CTV)                                                                        \
-  hipLaunchKernelGGL(k_mlr_margins<CTV>, dim3(mb), dim3(MT), 0, st, Xc, lc, wc, m, F, C, coef, \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_margins<CTV, mnw, CYC_MLR_DEPHASE>), dim3(mb), dim3(64 * mnw), 0, st, Xc, lc, wc, m, F, C, coef, \
                      off, (double*)p->multBuf.ptr, (double*)p->slabS.ptr, (double*)p->slabMS.ptr)
     {
     cyc::KernelTimer tm("k_mlr_margins", st);
