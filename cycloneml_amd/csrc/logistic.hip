@@ -445,6 +445,16 @@ typedef int v2i32 __attribute__((ext_vector_type(2)));
 #ifndef CYC_MLR_NW
 #define CYC_MLR_NW 4
 #endif
+// k_mlr_grad: 32-row multiplier chunks per barrier group
+#ifndef CYC_MLR_GRAD_GROUP
+#define CYC_MLR_GRAD_GROUP 1
+#endif
+#ifndef CYC_MLR_GRAD_NW
+#define CYC_MLR_GRAD_NW 8
+#endif
+#ifndef CYC_MLR_GRAD_XCD
+#define CYC_MLR_GRAD_XCD 1   // a split's feature tiles on one XCD
+#endif
 #ifndef CYC_MLR_DEPHASE
 #define CYC_MLR_DEPHASE false
 #endif
@@ -824,7 +834,8 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
 }
 
 constexpr int GR = 32;    // rows per chunk in the gradient GEMM
-constexpr int GF = 256;   // features per workgroup
+constexpr int GNW = CYC_MLR_GRAD_NW;   // waves per gradient workgroup
+constexpr int GF = 32 * GNW;           // features per workgroup
 
 // grad^T (CP x GF per workgroup) = mult^T X over one split of rows, on
 // v_mfma_f64_16x16x4f64 (8 waves x 32 features x CP classes).  Per 32-row
@@ -841,17 +852,26 @@ constexpr int GF = 256;   // features per workgroup
 // 16x16x4 X operand (block b: features 4b .. 4b + 3), so the result is class
 // l >> 4, feature l & 15.
 template <int CT, bool T4>
-__global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mult,
+__global__ __launch_bounds__(64 * GNW) void k_mlr_grad(const double* __restrict__ mult,
                                                   const double* __restrict__ X, int64_t n, int F,
-                                                  int64_t rowsPerSplit,
+                                                  int64_t rowsPerSplit, int ftiles, int splits,
                                                   double* __restrict__ slab) {
   constexpr int CP = CT * 16;
   constexpr int MB = GR * CP;                       // doubles per multiplier chunk
   constexpr int MPIECES = (MB * 8 + 1023) / 1024;
-  __shared__ __attribute__((aligned(16))) double Ms[2][MPIECES * 128];
+  constexpr int GG = CYC_MLR_GRAD_GROUP, NMB = 2 * GG;
+  __shared__ __attribute__((aligned(16))) double Ms[NMB][MPIECES * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int F0 = blockIdx.x * GF;
-  const int64_t r0 = (int64_t)blockIdx.y * rowsPerSplit;
+  // 1-D grid: block b runs on XCD b % 8; the ftiles workgroups of a split
+  // share that XCD (consecutive b / 8), so the split's multipliers come from
+  // HBM once and from that XCD's L2 for the other feature tiles
+  const int xq = (int)blockIdx.x >> 3;
+  const int ft = CYC_MLR_GRAD_XCD ? xq % ftiles : (int)blockIdx.x % ftiles;
+  const int sp = CYC_MLR_GRAD_XCD ? (xq / ftiles) * 8 + ((int)blockIdx.x & 7)
+                                  : (int)blockIdx.x / ftiles;
+  if (sp >= splits) return;   // splits padded to a multiple of 8
+  const int F0 = ft * GF;
+  const int64_t r0 = (int64_t)sp * rowsPerSplit;
   const int64_t r1 = min<int64_t>(n, r0 + rowsPerSplit);
   cyc_double4 acc[CT][2];
 #pragma unroll
@@ -870,7 +890,7 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
   const int fcol = F0 + wave * 32 + (lane & 15);
   auto loadM = [&](int64_t rb, int buf) {
     const int base = (int)(rb - r0) * CP * 8;
-    for (int q = wave; q < MPIECES; q += 8)
+    for (int q = wave; q < MPIECES; q += GNW)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           mR, (__attribute__((address_space(3))) void*)(&Ms[buf][q * 128]), 16,
           base + q * 1024 + lane * 16, 0, 0, 0);
@@ -886,14 +906,23 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
         x[kk][q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xR, off, 0, 2));
       }
   };
-  auto step = [&](int64_t rb, int buf, double (&xc)[GR / 4][2], double (&xn)[GR / 4][2]) {
+  // chunk c's multipliers in Ms[c % NMB]; one barrier per group of GG chunks
+  // (c % GG == 0): every wave's DMA of the group has landed and every wave is
+  // past the previous group, whose buffers take the next group's multipliers
+  const int64_t nchunks = (nr + GR - 1) / GR;
+  auto loadMc = [&](int64_t c) {
+    if (c < nchunks) loadM(r0 + c * GR, (int)(c % NMB));
+  };
+  auto step = [&](int64_t c, double (&xc)[GR / 4][2], double (&xn)[GR / 4][2]) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();   // chunk rb's multipliers visible; every wave past the previous chunk
-    if (rb + GR < r1) {
-      loadX(rb + GR, xn);
-      loadM(rb + GR, buf ^ 1);
+    const bool gs = GG == 1 || c % GG == 0;
+    if (gs) __syncthreads();
+    if (c + 1 < nchunks) loadX(r0 + (c + 1) * GR, xn);
+    if (gs) {
+#pragma unroll
+      for (int j = 0; j < GG; ++j) loadMc(c + GG + j);
     }
-    const double* M = Ms[buf];
+    const double* M = Ms[c % NMB];
 #pragma unroll
     for (int kk = 0; kk < GR / 4; ++kk) {
 #pragma unroll
@@ -909,17 +938,18 @@ __global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mul
       }
     }
   };
-  if (r0 < r1) {
+  if (nchunks > 0) {
     double xa[GR / 4][2], xb[GR / 4][2];
     loadX(r0, xa);
-    loadM(r0, 0);
-    for (int64_t rb = r0; rb < r1; rb += 2 * GR) {
-      step(rb, 0, xa, xb);
-      if (rb + GR < r1) step(rb + GR, 1, xb, xa);
+#pragma unroll
+    for (int j = 0; j < GG; ++j) loadMc(j);
+    for (int64_t c = 0; c < nchunks; c += 2) {
+      step(c, xa, xb);
+      if (c + 1 < nchunks) step(c + 1, xb, xa);
     }
   }
   // slab[split][ftile][c][f_local]
-  double* out = slab + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * CP * GF;
+  double* out = slab + ((size_t)sp * ftiles + ft) * CP * GF;
 #pragma unroll
   for (int ct = 0; ct < (T4 ? CT - 1 : CT); ++ct)
 #pragma unroll
@@ -1703,11 +1733,12 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
     if (rps > maxRps) rps = std::max<int64_t>(GR, maxRps);
     splits = (m + rps - 1) / rps;
     if ((rc = p->gslab.reserve(sizeof(double) * (size_t)splits * ftiles * CP * GF))) return rc;
+    const unsigned gblocks = (unsigned)(ftiles * cyc::round_up(splits, (int64_t)8));
 #define CYC_MLR_G(CTV)                                                                         \
-  if (t4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_grad<CTV, true>), dim3(ftiles, (unsigned)splits), dim3(512), 0, st, \
-                     (const double*)p->multBuf.ptr, Xc, m, F, rps, (double*)p->gslab.ptr); \
-  else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_grad<CTV, false>), dim3(ftiles, (unsigned)splits), dim3(512), 0, st, \
-                     (const double*)p->multBuf.ptr, Xc, m, F, rps, (double*)p->gslab.ptr)
+  if (t4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_grad<CTV, true>), dim3(gblocks), dim3(64 * GNW), 0, st, \
+                     (const double*)p->multBuf.ptr, Xc, m, F, rps, ftiles, (int)splits, (double*)p->gslab.ptr); \
+  else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_grad<CTV, false>), dim3(gblocks), dim3(64 * GNW), 0, st, \
+                     (const double*)p->multBuf.ptr, Xc, m, F, rps, ftiles, (int)splits, (double*)p->gslab.ptr)
     {
     cyc::KernelTimer tg("k_mlr_grad", st);
     switch (CT) {
