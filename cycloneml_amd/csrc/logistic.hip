@@ -437,23 +437,9 @@ typedef int v2i32 __attribute__((ext_vector_type(2)));
 #ifndef CYC_MLR_PROBE
 #define CYC_MLR_PROBE 0
 #endif
-// k_mlr_margins: 16-feature chunks per barrier group; waves per workgroup;
-// dephased workgroup pairs (see the kernel)
-#ifndef CYC_MLR_GROUP
-#define CYC_MLR_GROUP 2
-#endif
+// k_mlr_margins: waves per workgroup; dephased workgroup pairs (see the kernel)
 #ifndef CYC_MLR_NW
-#define CYC_MLR_NW 4
-#endif
-// k_mlr_grad: 32-row multiplier chunks per barrier group
-#ifndef CYC_MLR_GRAD_GROUP
-#define CYC_MLR_GRAD_GROUP 1
-#endif
-#ifndef CYC_MLR_GRAD_NW
-#define CYC_MLR_GRAD_NW 8
-#endif
-#ifndef CYC_MLR_GRAD_XCD
-#define CYC_MLR_GRAD_XCD 1   // a split's feature tiles on one XCD
+#define CYC_MLR_NW 8
 #endif
 #ifndef CYC_MLR_DEPHASE
 #define CYC_MLR_DEPHASE false
@@ -523,22 +509,19 @@ __device__ __forceinline__ double dpp_f64(double v) {
 constexpr int MR = 256;    // rows per margin tile, at most (8 waves x 32 rows)
 constexpr int MK = 16;     // features per LDS chunk
 
-// margins = X W^T (+ offset) for 32 NW-row tiles, 16-feature chunks, on
+// margins = X W^T (+ offset) for 256-row tiles, 16-feature chunks, on
 // v_mfma_f64_16x16x4f64: 2 row tiles x CT class tiles of 16x16 per wave;
-// softmax / loss / multiplier epilogue in registers.  Persistent over tiles:
-// two 4-wave workgroups per CU (NW = 4; each SIMD holds a wave of each, so
-// one's epilogue and barrier waits run beside the other's MFMAs -- 9 % faster
-// than one 8-wave workgroup per CU with the barrier grouping below).
+// softmax / loss / multiplier epilogue in registers.  Persistent over tiles,
+// one 8-wave workgroup per CU.
 // X goes from HBM straight into registers in the MFMA A layout -- lane (row
 // r = l & 15, group g = l >> 4) holds features f0 + 4g .. 4g + 3 of its row
 // for k-steps 0..3 (the contraction order within a chunk is permuted: 128
 // contiguous bytes per row per chunk, two dwordx4 loads per lane per row
 // tile) -- loaded one chunk ahead into a second register set: no LDS, no
 // barrier for X.  W chunks (16 features x C classes, contiguous in coef,
-// 12.8 KB at C = 100) are DMA'd into 2 G LDS buffers (buffer_load ... lds,
-// 1 KiB pieces spread over the waves, a group of G chunks ahead; no
-// registers), one barrier per group of G = 2 chunks (one per chunk: 4.5 %
-// slower).  Padding classes read the next coefficients (finite;
+// 12.8 KB at C = 100) are DMA'd into two LDS buffers (buffer_load ... lds,
+// 1 KiB pieces spread over the waves, one chunk ahead; no registers), one
+// barrier per chunk.  Padding classes read the next coefficients (finite;
 // their margins are never used) or zero past the end of coef.
 // (The last class tile on v_mfma_f64_4x4x4f64, as k_mlr_grad does, measured
 // 4-5 % slower here at C = 100, with or without sched_barrier fences.)
@@ -557,12 +540,11 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
   constexpr int CP = CT * 16;
   static_assert(MK == 16, "the A layout covers 16 features per chunk");
   constexpr int WBUF = MK * CP + 128;   // doubles per W buffer (whole 1 KiB pieces)
-  constexpr int G = CYC_MLR_GROUP, NBUF = 2 * G;
-  // the W buffers (two groups of G chunks), exp_neg's table and the per-class
-  // offsets (never DMA targets)
-  __shared__ __attribute__((aligned(16))) double Ws[NBUF][WBUF];
-  __shared__ double expT[32];
-  __shared__ double offS[CP];
+  // the two W buffers, then exp_neg's table and the per-class offsets (never
+  // DMA targets)
+  __shared__ __attribute__((aligned(16))) double Ws[2][WBUF + 32 + CP];
+  double* const expT = Ws[1] + WBUF;
+  double* const offS = expT + 32;
   __shared__ double plS[MR];   // each wave's 32 label probabilities of a tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4;
@@ -594,9 +576,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
                                                     0x00020000);
   // pieces covering every index the B reads touch: (MK - 1) C + CP doubles
   const int wpieces = (((MK - 1) * C + CP) * 8 + 1023) / 1024;
-  auto loadW = [&](int ch, int buf) {   // chunk ch's 16 x C run of coef into Ws[buf]
+  auto loadW = [&](int ch) {      // chunk ch's 16 x C run of coef into buffer ch & 1
     if constexpr ((CYC_MLR_PROBE & 4) != 0) return;
-    double* dst = Ws[buf];
+    double* dst = Ws[ch & 1];
     const int base = ch * MK * C * 8;
     for (int q = wave; q < wpieces; q += MT / 64)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -756,39 +738,28 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
     loss -= (wr > 0) ? wr * log(pl) : 0.0;
   };
   double xa[2][4], xb[2][4];
-  // The workgroup's chunks (tile, ch) in order form one stream s = 0, 1, ..;
-  // chunk s's W sits in Ws[s % NBUF].  One barrier per group of G chunks (at
-  // s % G == 0): every wave's DMA of this group has landed (each waited for
-  // its own) and every wave is past the previous group, whose buffers then
-  // take the next group's W -- G chunks of MFMAs between barriers.
-  const int64_t myTiles = blockIdx.x < tiles ? (tiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  const int64_t S = myTiles * nch;
-  auto loadWs = [&](int64_t s) {
-    if (s < S) loadW((int)(s % nch), (int)(s % NBUF));
-  };
-#pragma unroll
-  for (int j = 0; j < G; ++j) loadWs(j);
-  int64_t s = 0;
+  bool pre = false;   // chunk 0 of this tile already in flight (xa, Ws[0])
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t r0 = tile * MR;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) acc[t][ct] = cyc_double4{0.0, 0.0, 0.0, 0.0};
+    if (!pre) {
+      __syncthreads();   // the previous tile's last W buffer is free
+      loadW(0);
+    }
     loadX(r0, 0, xa);
-    // chunk ch: wait for its loads (barrier at a group start), issue chunk ch
-    // + 1's X (and at a group start the next group's W), multiply
+    // chunk ch: wait for its loads, barrier (its W visible everywhere, every
+    // wave past chunk ch - 1), issue chunk ch + 1's loads, multiply
     auto step = [&](int ch, double (&xc)[2][4], double (&xn)[2][4]) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const bool gs = G == 1 || s % G == 0;
-      if (gs) __syncthreads();
-      if (ch + 1 < nch) loadX(r0, ch + 1, xn);
-      if (gs) {
-#pragma unroll
-        for (int j = 0; j < G; ++j) loadWs(s + G + j);
+      __syncthreads();
+      if (ch + 1 < nch) {
+        loadX(r0, ch + 1, xn);
+        loadW(ch + 1);
       }
-      const double* W = Ws[s % NBUF];
-      ++s;
+      const double* W = Ws[ch & 1];
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
 #pragma unroll
@@ -803,11 +774,18 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
       step(ch, xa, xb);
       if (ch + 1 < nch) step(ch + 1, xb, xa);
     }
+    // the next tile's W chunk 0 goes out before this tile's epilogue (the X
+    // registers stay free for it: prefetching X too spills at CT = 7): with
+    // an even chunk count the last chunk read Ws[1], and every wave is past
+    // chunk nch - 2 (Ws[0]) since the last barrier
+    const int64_t next = tile + gridDim.x;
+    pre = (nch % 2) == 0 && next < tiles;
     // the tile's labels and weights, loaded (unconditionally, from a
-    // clamped row) before the stores of the epilogue
+    // clamped row) before the W DMA and the stores of the epilogue
     const int64_t lr = min<int64_t>(r0 + wave * 32 + (lane & 31), n - 1);
     const double labL = labels[lr];
     const double wL = weights ? weights[lr] : 1.0;
+    if (pre) loadW(0);
     epilogue(r0, labL, wL);
   }
   // per-wave partials: loss/wsum over the lanes (one row of each tile per
@@ -834,8 +812,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
 }
 
 constexpr int GR = 32;    // rows per chunk in the gradient GEMM
-constexpr int GNW = CYC_MLR_GRAD_NW;   // waves per gradient workgroup
-constexpr int GF = 32 * GNW;           // features per workgroup
+constexpr int GF = 256;   // features per workgroup
 
 // grad^T (CP x GF per workgroup) = mult^T X over one split of rows, on
 // v_mfma_f64_16x16x4f64 (8 waves x 32 features x CP classes).  Per 32-row
@@ -852,23 +829,21 @@ constexpr int GF = 32 * GNW;           // features per workgroup
 // 16x16x4 X operand (block b: features 4b .. 4b + 3), so the result is class
 // l >> 4, feature l & 15.
 template <int CT, bool T4>
-__global__ __launch_bounds__(64 * GNW) void k_mlr_grad(const double* __restrict__ mult,
+__global__ __launch_bounds__(512) void k_mlr_grad(const double* __restrict__ mult,
                                                   const double* __restrict__ X, int64_t n, int F,
                                                   int64_t rowsPerSplit, int ftiles, int splits,
                                                   double* __restrict__ slab) {
   constexpr int CP = CT * 16;
   constexpr int MB = GR * CP;                       // doubles per multiplier chunk
   constexpr int MPIECES = (MB * 8 + 1023) / 1024;
-  constexpr int GG = CYC_MLR_GRAD_GROUP, NMB = 2 * GG;
-  __shared__ __attribute__((aligned(16))) double Ms[NMB][MPIECES * 128];
+  __shared__ __attribute__((aligned(16))) double Ms[2][MPIECES * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // 1-D grid: block b runs on XCD b % 8; the ftiles workgroups of a split
   // share that XCD (consecutive b / 8), so the split's multipliers come from
   // HBM once and from that XCD's L2 for the other feature tiles
   const int xq = (int)blockIdx.x >> 3;
-  const int ft = CYC_MLR_GRAD_XCD ? xq % ftiles : (int)blockIdx.x % ftiles;
-  const int sp = CYC_MLR_GRAD_XCD ? (xq / ftiles) * 8 + ((int)blockIdx.x & 7)
-                                  : (int)blockIdx.x / ftiles;
+  const int ft = xq % ftiles;
+  const int sp = (xq / ftiles) * 8 + ((int)blockIdx.x & 7);
   if (sp >= splits) return;   // splits padded to a multiple of 8
   const int F0 = ft * GF;
   const int64_t r0 = (int64_t)sp * rowsPerSplit;
@@ -890,7 +865,7 @@ __global__ __launch_bounds__(64 * GNW) void k_mlr_grad(const double* __restrict_
   const int fcol = F0 + wave * 32 + (lane & 15);
   auto loadM = [&](int64_t rb, int buf) {
     const int base = (int)(rb - r0) * CP * 8;
-    for (int q = wave; q < MPIECES; q += GNW)
+    for (int q = wave; q < MPIECES; q += 8)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           mR, (__attribute__((address_space(3))) void*)(&Ms[buf][q * 128]), 16,
           base + q * 1024 + lane * 16, 0, 0, 0);
@@ -906,23 +881,14 @@ __global__ __launch_bounds__(64 * GNW) void k_mlr_grad(const double* __restrict_
         x[kk][q] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xR, off, 0, 2));
       }
   };
-  // chunk c's multipliers in Ms[c % NMB]; one barrier per group of GG chunks
-  // (c % GG == 0): every wave's DMA of the group has landed and every wave is
-  // past the previous group, whose buffers take the next group's multipliers
-  const int64_t nchunks = (nr + GR - 1) / GR;
-  auto loadMc = [&](int64_t c) {
-    if (c < nchunks) loadM(r0 + c * GR, (int)(c % NMB));
-  };
-  auto step = [&](int64_t c, double (&xc)[GR / 4][2], double (&xn)[GR / 4][2]) {
+  auto step = [&](int64_t rb, int buf, double (&xc)[GR / 4][2], double (&xn)[GR / 4][2]) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const bool gs = GG == 1 || c % GG == 0;
-    if (gs) __syncthreads();
-    if (c + 1 < nchunks) loadX(r0 + (c + 1) * GR, xn);
-    if (gs) {
-#pragma unroll
-      for (int j = 0; j < GG; ++j) loadMc(c + GG + j);
+    __syncthreads();   // chunk rb's multipliers visible; every wave past the previous chunk
+    if (rb + GR < r1) {
+      loadX(rb + GR, xn);
+      loadM(rb + GR, buf ^ 1);
     }
-    const double* M = Ms[c % NMB];
+    const double* M = Ms[buf];
 #pragma unroll
     for (int kk = 0; kk < GR / 4; ++kk) {
 #pragma unroll
@@ -938,14 +904,13 @@ __global__ __launch_bounds__(64 * GNW) void k_mlr_grad(const double* __restrict_
       }
     }
   };
-  if (nchunks > 0) {
+  if (r0 < r1) {
     double xa[GR / 4][2], xb[GR / 4][2];
     loadX(r0, xa);
-#pragma unroll
-    for (int j = 0; j < GG; ++j) loadMc(j);
-    for (int64_t c = 0; c < nchunks; c += 2) {
-      step(c, xa, xb);
-      if (c + 1 < nchunks) step(c + 1, xb, xa);
+    loadM(r0, 0);
+    for (int64_t rb = r0; rb < r1; rb += 2 * GR) {
+      step(rb, 0, xa, xb);
+      if (rb + GR < r1) step(rb + GR, 1, xb, xa);
     }
   }
   // slab[split][ftile][c][f_local]
@@ -1673,7 +1638,7 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
   // k_mlr_grad: the last class tile on the 4x4x4 form when it holds 1..4
   // classes (2.6 % faster at C = 100)
   const bool t4 = C % 16 != 0 && C % 16 <= 4;
-  // persistent: two 4-wave workgroups per CU (CYC_MLR_NW = 8: one 8-wave one)
+  // persistent: one 8-wave workgroup per CU (CYC_MLR_NW = 4: two 4-wave ones)
   constexpr int mnw = CYC_MLR_NW, mrows = 32 * mnw;
   const int mblocks = 256 * 8 / mnw;
   const int64_t mwaves = (int64_t)mblocks * mnw;
@@ -1735,9 +1700,9 @@ int cyc_multinomial_logistic_add_dense_dev(cyc_logistic_plan p, const double* X,
     if ((rc = p->gslab.reserve(sizeof(double) * (size_t)splits * ftiles * CP * GF))) return rc;
     const unsigned gblocks = (unsigned)(ftiles * cyc::round_up(splits, (int64_t)8));
 #define CYC_MLR_G(CTV)                                                                         \
-  if (t4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_grad<CTV, true>), dim3(gblocks), dim3(64 * GNW), 0, st, \
+  if (t4) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_grad<CTV, true>), dim3(gblocks), dim3(512), 0, st, \
                      (const double*)p->multBuf.ptr, Xc, m, F, rps, ftiles, (int)splits, (double*)p->gslab.ptr); \
-  else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_grad<CTV, false>), dim3(gblocks), dim3(64 * GNW), 0, st, \
+  else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_mlr_grad<CTV, false>), dim3(gblocks), dim3(512), 0, st, \
                      (const double*)p->multBuf.ptr, Xc, m, F, rps, ftiles, (int)splits, (double*)p->gslab.ptr)
     {
     cyc::KernelTimer tg("k_mlr_grad", st);
