@@ -258,6 +258,32 @@ def test_lloyd_iteration(cuda, n, d, k, weighted, use_rows):
     assert bool(conv.item()) == ref["converged"]
 
 
+@pytest.mark.parametrize("d", [64, 256, 255])
+def test_rows_image_unaligned(cuda, d):
+    """The row image from rows that start 8 bytes past a 16-byte boundary
+    (k_rows_quantize's 8-byte load path; even d otherwise takes 16-byte
+    loads) gives the oracle's assignment and distances."""
+    import torch
+    from cycloneml_amd.clustering import row_norms
+    n, k = 3001, 24
+    rng = np.random.default_rng(d)
+    X = rng.normal(size=(n, d)) + rng.integers(0, 6, size=(n, 1)) * 2.5
+    C = X[rng.choice(n, size=k, replace=False)].copy()
+    buf = torch.empty(n * d + 1, dtype=torch.float64, device=cuda)
+    Xd = buf[1:].view(n, d)
+    Xd.copy_(torch.from_numpy(X))
+    assert Xd.data_ptr() % 16 == 8
+    Cd = _dev(C, cuda)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = _plan(d, k, n)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    c = torch.empty(n, dtype=torch.float64, device=cuda)
+    p.assign(Xd, xn, Cd, cn, a, c, rows=p.rows(Xd))
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a.cpu().numpy(), ra)
+    np.testing.assert_array_equal(c.cpu().numpy(), rc)
+
+
 def test_weighted_centers_exact(cuda):
     """ml/clustering/KMeansSuite.scala:323-411 'Two centers with weightCol':
     exact (===) centers after convergence, up to the order of the clusters."""
