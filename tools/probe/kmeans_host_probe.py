@@ -34,13 +34,23 @@ def main():
         t1 = time.perf_counter()
         wl.plan.accumulate(wl.X, wl.xnorm, None, wl.C, wl.cnorm, sums, wsum, cost, rows=wl.rows)
         t2 = time.perf_counter()
+        # did the GPU already finish this call's work when the host got back?
+        e = torch.cuda.Event()
+        e.record()
+        done = e.query()
+        tail_us = -1.0
+        if i == steps - 1:   # how much of this call's GPU work was left at the return
+            ts = time.perf_counter()
+            e.synchronize()
+            tail_us = (time.perf_counter() - ts) * 1e6
         wl.parallel.allreduce_(buf)
         t3 = time.perf_counter()
         wl.plan.update(wl.C, wl.cnorm, sums, wsum, 1e-4, wl.conv)
         t4 = time.perf_counter()
         ev[i + 1].record()
         rec.append({"zero_us": (t1 - t0) * 1e6, "accumulate_us": (t2 - t1) * 1e6,
-                    "allreduce_us": (t3 - t2) * 1e6, "update_us": (t4 - t3) * 1e6})
+                    "allreduce_us": (t3 - t2) * 1e6, "update_us": (t4 - t3) * 1e6,
+                    "gpu_done_at_return": int(done), "gpu_left_at_return_us": tail_us})
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t_all) * 1e3 / steps
     for i, r in enumerate(rec):
