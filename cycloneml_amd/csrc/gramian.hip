@@ -32,6 +32,9 @@
 // 1: the plain k_gram_dma's blocks grouped by row split per XCD (an A/B
 // switch; the covariance form keeps the 2-D grid: grouped, it measured
 // 625.7 vs 586.0 ms at 30M x 1024 for a 6 % smaller FETCH_SIZE)
+#ifndef CYC_GRAM_SKIPLOW
+#define CYC_GRAM_SKIPLOW 1   // k_gram_dma covariance: diagonal tiles skip lower MFMAs
+#endif
 #ifndef CYC_GRAM_XCDMAP
 #define CYC_GRAM_XCDMAP 1
 #endif
@@ -244,7 +247,17 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
             ((pad ? 0 : rr * p) + (pn ? J0 : I0)) * 8 + lane * 16, 0, 0, 0);
     }
   };
+  // Covariance form: on a diagonal tile the wave of rows 64..127 x columns
+  // 0..63 covers only entries the fold discards (below the diagonal): it
+  // skips its MFMAs and leaves the pipe to the other workgroup's waves on
+  // its SIMD (it still DMAs its rows and meets every barrier); with
+  // SKIPLOW 2 the two diagonal waves also skip their 16x16 blocks below the
+  // diagonal.  (The plain form, three workgroups per CU, measured slower
+  // with it: 507.7 vs 488.6 ms.)
+  const bool idle = CYC_GRAM_SKIPLOW && MEAN && ti == tj && wy > wx;
+  const bool tri = CYC_GRAM_SKIPLOW >= 2 && MEAN && ti == tj && wy == wx;
   auto compute = [&](int b) {
+    if (idle) return;
     const double* Ai = Pn(b, 0);
     const double* Aj = Pn(b, 1);
 #pragma unroll
@@ -267,7 +280,8 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
       for (int qa = 0; qa < 4; ++qa)
 #pragma unroll
         for (int qb = 0; qb < 4; ++qb)
-          acc[qa][qb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[qa], bb[qb], acc[qa][qb], 0, 0, 0);
+          if (qa <= qb || !tri)
+            acc[qa][qb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[qa], bb[qb], acc[qa][qb], 0, 0, 0);
     }
   };
   // NB - 1 chunks ahead; past the end the DMAs fetch nothing (empty
