@@ -31,10 +31,14 @@ the only RCCL communicator per GPU); torch.distributed runs on gloo for the
 rendezvous, the RCCL id and the host barriers.
 
 Prints ONE JSON line on rank 0.  `roofline` is for the workload's dominant
-kernel (the slowest of its priced kernels), timed with HIP events on the
-stream it runs on inside the timed region (cyc_profile_*); `cpu_baseline` is
-the CPU restatement (oracle/, a C port of the reference loops) on a bounded
-sample of the same data.
+kernel (the priced kernel with the most time per step; within 5 % of the
+workload's declared kernel, the declared one), timed with HIP events on the
+stream it runs on inside the timed region (cyc_profile_*), and lists every
+priced kernel's fraction under `priced_kernels`; `cpu_baseline` is the CPU
+restatement (oracle/, a C port of the reference loops) on a bounded sample of
+the same data, one partition per available host core.  On one GPU a `blas`
+leg follows: the per-call netlib layer (libcyclone_blas.so) at
+BLASBenchmark's shapes against its published rates.
 """
 from __future__ import annotations
 
@@ -56,6 +60,7 @@ HBM = ("hbm", "GB/s", HBM_PEAK_GBS, 1e9)
 FP64 = ("mfma", "TFLOP/s", FP64_PEAK_TFLOPS, 1e12)
 I8 = ("mfma", "TOPS", I8_PEAK_TOPS, 1e12)
 
+DOMINANT_MARGIN = 0.05    # roofline names the declared kernel unless another is 5 % slower
 DIST_BACKEND = "gloo"     # torch.distributed's group: host only, no second RCCL communicator
 ORDER = ("kmeans", "gramian", "pca", "lr_multi", "lr_sparse")
 # BASELINE configs: rows of the whole problem, and whether it is per GPU
@@ -74,7 +79,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="all", choices=("all",) + ORDER)
+    ap.add_argument("--workload", default="all", choices=("all",) + ORDER + ("blas",))
     ap.add_argument("--scaling", default="auto", choices=("auto", "weak", "strong"))
     ap.add_argument("--rows", type=int, default=0, help="rows per GPU (0 = from --scaling)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -103,12 +108,15 @@ def rows_per_gpu(workload, scaling, world, rank, override=0):
     return min(e - s, cap), mode, total
 
 
-def pmc_traffic(workload, kernel, launches_per_step, rows):
+def pmc_traffic(workload, kernel, rows):
     """HBM bytes per timed launch of `kernel`, from the latest committed
     rocprofv3 --pmc summary of this workload
     (profiles/r<NN>_<workload>_pmc.json, tools/pmc_summary.py: separate
-    FETCH_SIZE / WRITE_SIZE passes, gfx950 corrections applied there), scaled
-    to this run's rows; (None, None) when there is none."""
+    FETCH_SIZE / WRITE_SIZE passes, gfx950 corrections applied there): the
+    summary's bytes PER DISPATCH (not per step: a profiled run may dispatch
+    a kernel outside its steps too), scaled by this run's rows over the
+    profiled run's `_rows` (the same launch shape per step at equal rows);
+    (None, None) when there is none."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")))
     for f in reversed(files):
@@ -116,15 +124,48 @@ def pmc_traffic(workload, kernel, launches_per_step, rows):
             d = json.load(open(f))
             if kernel not in d:
                 continue
-            per_step = d[kernel]["hbm_bytes_per_step"]
-            return per_step / launches_per_step * rows / d["_rows"], os.path.basename(f)
+            return d[kernel]["hbm_bytes_per_dispatch"] * rows / d["_rows"], os.path.basename(f)
         except Exception:
             continue
     return None, None
 
 
+def _cgroup_cpus():
+    """CPUs the cgroup quota allows (cpu.max / cfs quota), None if unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(p)))
+    except Exception:
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, q // p)
+    except Exception:
+        pass
+    return None
+
+
+def host_cores():
+    """The host cores this process can use -- Spark's local[N] with N = all
+    of them (LocalSchedulerBackend.scala:87-93): the CPUs in
+    its affinity mask, capped by a cgroup CPU quota when one is set.  Every
+    cpu_baseline runs one partition per such core and records the counts."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = _cgroup_cpus()
+    n = min(aff, quota) if quota else aff
+    return max(1, n), {"os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+                       "cgroup_quota_cpus": quota}
+
+
 def cpu_threads():
-    return int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    return host_cores()[0]
+
+
+def _cores_info():
+    return host_cores()[1]
 
 
 def timed_parallel(fn, parts, threads):
@@ -555,7 +596,7 @@ class LRSparseWorkload:
     at SURVEY 8(d)'s 784 B/row (one fused pass's reads); the roofline line
     names the slower (dominant) one."""
     kernel = "k_tiles_grad"
-    kernels = ("k_tiles_margin", "k_tiles_grad")
+    kernels = ("k_tiles_margin", "k_tiles_rows", "k_tiles_grad")
 
     def __init__(self, n, dev, rank):
         import numpy as np
@@ -592,6 +633,8 @@ class LRSparseWorkload:
         self.fn.calculate(self.coef)
 
     def work(self, kname, launches_per_step):
+        if kname == "k_tiles_rows":           # the rows' epilogue: dot + label in, multiplier out
+            return self.n * 24.0 / launches_per_step, HBM
         return self.n * (self.k * 12 + 8 + 8) / launches_per_step, HBM   # bytes
 
     def extra_roofline(self, launches_per_step, avg_s):
@@ -649,6 +692,121 @@ class LRSparseWorkload:
 
 WORKLOADS = {"kmeans": KMeansWorkload, "gramian": GramianWorkload, "pca": PCAWorkload,
              "lr_multi": LRMultiWorkload, "lr_sparse": LRSparseWorkload}
+
+# BLASBenchmark's published rates (values/s, best of >= 100 iterations) on a
+# Xeon E5-2673 v4, OpenJDK 17: mllib-local/benchmarks/BLASBenchmark-jdk17-
+# results.txt (line of the java / native row), the shapes of
+# mllib-local/src/test/scala/org/apache/spark/ml/linalg/BLASBenchmark.scala.
+BLAS_PUBLISHED = {   # name: (values per call, java M/s, native M/s, results.txt lines)
+    "daxpy": (1e8, 175.0, 173.6, "10-11"),
+    "ddot": (1e8, 682.2, 663.7, "62-63"),
+    "dscal": (1e8, 190.9, 199.9, "114-115"),
+    "dgemv[N]": (1e8, 1152.8, 951.8, "140-141"),
+    "dgemv[T]": (1e8, 1241.1, 845.3, "153-154"),
+    "dger": (1e8, 200.3, 198.1, "192-193"),
+    "dspmv[U]": (1e4 * (1e4 + 1) / 2, 858.1, 815.4, "205-206"),
+    "dspr[U]": (1e4 * (1e4 + 1) / 2, 194.8, 201.2, "218-219"),
+    "dsyr[U]": (1e4 * (1e4 + 1) / 2, 111.8, 112.9, "231-232"),
+    "dgemm[N,N]": (1e9, 2511.5, 1429.6, "244-245"),
+    "dgemm[N,T]": (1e9, 2402.5, 1344.7, "257-258"),
+    "dgemm[T,N]": (1e9, 2448.6, 900.4, "270-271"),
+    "dgemm[T,T]": (1e9, 2818.4, 909.5, "283-284"),
+}
+
+
+def run_blas(args, cpu_seconds):
+    """The per-call drop-in layer (libcyclone_blas.so, include/cyclone_blas.h)
+    timed the way BLASBenchmark times netlib: host arrays in, host arrays
+    out, one synchronous Fortran-ABI call per iteration at the benchmark's
+    shapes (BLASBenchmark.scala:76-340), the output operand cloned inside
+    the iteration as the benchmark's `y.clone` / `a.clone` does; rate =
+    values / best time (core/src/test/.../benchmark/Benchmark.scala:163-169).
+    PCIe is inside every call (operands to HBM and the result back).
+    vs_baseline = rate / the published java rate (the faster JVM provider
+    on that host for every routine but dspr/dsyr)."""
+    import numpy as np
+    from cycloneml_amd import blas as B
+    L = B.load()
+    nb = B.nativeBLAS
+    rnd = np.random.default_rng(0)
+    iters = max(3, args.steps)
+    n1 = int(1e8)
+    x1, y1 = rnd.random(n1), rnd.random(n1)
+    m2 = int(1e4)
+    A2 = rnd.random(m2 * m2)
+    xv, yv = rnd.random(m2), rnd.random(m2)
+    AP = rnd.random(m2 * (m2 + 1) // 2)
+    g = int(1e3)
+    Ag, Bg, Cg = rnd.random(g * g), rnd.random(g * g), rnd.random(g * g)
+    a, b = 0.7, 0.3
+    cases = {
+        "daxpy": lambda: nb.daxpy(n1, a, x1, 1, y1.copy(), 1),
+        "ddot": lambda: nb.ddot(n1, x1, 1, y1, 1),
+        "dscal": lambda: nb.dscal(n1, a, x1.copy(), 1),
+        "dgemv[N]": lambda: nb.dgemv("N", m2, m2, a, A2, m2, xv, 1, b, yv.copy(), 1),
+        "dgemv[T]": lambda: nb.dgemv("T", m2, m2, a, A2, m2, xv, 1, b, yv.copy(), 1),
+        "dger": lambda: nb.dger(m2, m2, a, xv, 1, yv, 1, A2.copy(), m2),
+        "dspmv[U]": lambda: nb.dspmv("U", m2, a, AP, xv, 1, b, yv.copy(), 1),
+        "dspr[U]": lambda: nb.dspr("U", m2, a, xv, 1, AP.copy()),
+        "dsyr[U]": lambda: nb.dsyr("U", m2, a, xv, 1, A2.copy(), m2),
+        "dgemm[N,N]": lambda: nb.dgemm("N", "N", g, g, g, a, Ag, g, Bg, g, b, Cg.copy(), g),
+        "dgemm[N,T]": lambda: nb.dgemm("N", "T", g, g, g, a, Ag, g, Bg, g, b, Cg.copy(), g),
+        "dgemm[T,N]": lambda: nb.dgemm("T", "N", g, g, g, a, Ag, g, Bg, g, b, Cg.copy(), g),
+        "dgemm[T,T]": lambda: nb.dgemm("T", "T", g, g, g, a, Ag, g, Bg, g, b, Cg.copy(), g),
+    }
+    rates = {}
+    t_all = time.perf_counter()
+    for name, fn in cases.items():
+        vals, java, native, lines = BLAS_PUBLISHED[name]
+        for _ in range(2):
+            fn()
+        best, tot = float("inf"), 0.0
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            fn()
+            t = time.perf_counter() - t0
+            best, tot = min(best, t), tot + t
+        rate = vals / best / 1e6
+        rates[name] = {"rate_M_per_s": rate, "best_ms": best * 1e3, "avg_ms": tot / iters * 1e3,
+                       "published_java_M_per_s": java, "published_native_M_per_s": native,
+                       "vs_java": rate / java, "vs_native": rate / native,
+                       "published_source": f"BLASBenchmark-jdk17-results.txt:{lines}"}
+    el = time.perf_counter() - t_all
+    del L
+    # the oracle's netlib restatements on one host core, same shapes (a
+    # netlib call is single-threaded: docs/ml-linalg-guide.md:79-91)
+    cpu = None
+    if cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        O = oracle.lib()
+        t0 = time.perf_counter()
+        O.orc_ddot(oracle._p(x1), oracle._p(y1), n1)
+        t_dot = time.perf_counter() - t0
+        U = AP.copy()
+        t0 = time.perf_counter()
+        O.orc_dspr_upper(m2, a, oracle._p(xv), oracle._p(U))
+        t_spr = time.perf_counter() - t0
+        cpu = {"value": n1 / t_dot, "unit": "values/s (ddot n=1e8)", "cores": 1, "kind": "port",
+               "dspr_values_per_s": BLAS_PUBLISHED["dspr[U]"][0] / t_spr,
+               "sample": "the oracle's netlib ddot (n = 1e8) and dspr('U', n = 1e4) loops "
+                         "(-ffp-contract=off), one call each on one host core",
+               "host": _cores_info()}
+    geo = float(np.exp(np.mean([np.log(r["vs_java"]) for r in rates.values()])))
+    return {
+        "metric": "BLASBenchmark rate (values/s) through the per-call netlib ABI",
+        "value": rates["dgemm[N,N]"]["rate_M_per_s"] * 1e6, "unit": "values/s (dgemm[N,N])",
+        "n_gpus": 1, "steps": iters, "warmup": 2,
+        "ms_per_step": rates["dgemm[N,N]"]["best_ms"], "higher_is_better": True,
+        "scaling": "none", "vs_baseline": rates["dgemm[N,N]"]["vs_java"],
+        "vs_baseline_geomean_all_routines": geo,
+        "dtype": "f64", "data": "synthetic host arrays (numpy PCG64 seed 0)",
+        "config": {"workload": "BLASBenchmark shapes through libcyclone_blas.so: level 1 "
+                               "n = 1e8, level 2 1e4 x 1e4 (packed n = 1e4), dgemm 1e3^3; host "
+                               "operands, PCIe in every call",
+                   "baseline": "published java rate, Xeon E5-2673 v4 @ 2.3 GHz, OpenJDK 17"},
+        "routines": rates, "cpu_baseline": cpu, "elapsed_s": el,
+    }
 
 
 def launch_ranks(args) -> int:
@@ -722,22 +880,42 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
                        "norms + plan + row image + every iteration with its host convergence "
                        "check, over iterations 1..maxIter (value times steady-state iterations "
                        "after the warmup)"}
-    # dominant kernel: the slowest of the priced kernels, in its own units
-    priced = [k for k in kernels if prof[k][1] and wl.work(k, 1) is not None]
-    kname = max(priced, key=lambda k: prof[k][0]) if priced else wl.kernel
+    # Every priced kernel in its own units (work per launch / mean launch
+    # duration from its HIP events), and the dominant one by a fixed rule:
+    # the priced kernel with the most time per step, except that a kernel
+    # within DOMINANT_MARGIN of the workload's declared `kernel` yields to
+    # it -- so two kernels a few percent apart cannot swap between boxes.
+    priced_rows = {}
+    for k in kernels:
+        kms_k, launches_k = prof[k]
+        if not launches_k or wl.work(k, 1) is None:
+            continue
+        per_launch_k, (bound_k, unit_k, peak_k, scale_k) = wl.work(k, launches_k / args.steps)
+        avg_k = kms_k / launches_k / 1e3
+        ach = per_launch_k / avg_k / scale_k
+        pmc_k = getattr(wl, "pmc_names", {}).get(k, k)
+        traffic_k, src_k = pmc_traffic(name, pmc_k, n)
+        priced_rows[k] = {"bound": bound_k, "achieved": ach, "peak": peak_k, "unit": unit_k,
+                          "frac": ach / peak_k, "avg_launch_ms": avg_k * 1e3,
+                          "ms_per_step": kms_k / args.steps, "launches": launches_k,
+                          "work_per_launch": per_launch_k, "traffic": traffic_k,
+                          "traffic_source": src_k}
+    kname = wl.kernel
+    if priced_rows:
+        top = max(priced_rows, key=lambda k: priced_rows[k]["ms_per_step"])
+        decl = priced_rows.get(wl.kernel)
+        if decl is None or priced_rows[top]["ms_per_step"] > (1 + DOMINANT_MARGIN) * \
+                decl["ms_per_step"]:
+            kname = top
+    dom = priced_rows.get(kname)
     kms, launches = prof[kname]
     avg_s = kms / max(launches, 1) / 1e3
-    per_launch, price = wl.work(kname, launches / args.steps) if (launches and priced) else (0.0, HBM)
-    bound, unit, peak, scale = price
-    achieved = per_launch / avg_s / scale if launches and priced else None
-    pmc_name = getattr(wl, "pmc_names", {}).get(kname, kname)
-    traffic, traffic_src = (pmc_traffic(name, pmc_name, launches / args.steps, n)
-                            if launches else (None, None))
     extra = wl.extra_roofline(launches / args.steps, avg_s) if (
         launches and hasattr(wl, "extra_roofline")) else {}
     cpu = None
     if rank == 0 and world == 1 and cpu_seconds > 0:
         cpu = wl.cpu_baseline(cpu_seconds)
+        cpu["host"] = _cores_info()
     out = {
         "metric": "rows/s per training iteration",
         "value": value,
@@ -755,12 +933,20 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
                    "config_rows": CONFIG_ROWS[name],
                    "config_rows_are": "per GPU" if PER_GPU_CONFIG[name] else "total",
                    "parallelism": f"dp{world} (row shards, RCCL all-reduce merge)"},
-        "roofline": {"kernel": kname, "bound": bound, "achieved": achieved,
-                     "peak": peak, "unit": unit,
-                     "frac": (achieved / peak) if achieved else None,
-                     "traffic": traffic, "traffic_source": traffic_src,
+        "roofline": {"kernel": kname,
+                     "bound": dom["bound"] if dom else None,
+                     "achieved": dom["achieved"] if dom else None,
+                     "peak": dom["peak"] if dom else None,
+                     "unit": dom["unit"] if dom else None,
+                     "frac": dom["frac"] if dom else None,
+                     "traffic": dom["traffic"] if dom else None,
+                     "traffic_source": dom["traffic_source"] if dom else None,
                      "avg_launch_ms": avg_s * 1e3, "launches": launches,
-                     "work_per_launch": per_launch,
+                     "work_per_launch": dom["work_per_launch"] if dom else None,
+                     "dominant_rule": f"most time per step among priced kernels; within "
+                                      f"{DOMINANT_MARGIN:.0%} of the declared {wl.kernel} the "
+                                      f"declared one",
+                     "priced_kernels": priced_rows,
                      "kernels_ms_per_step": {k: v[0] / args.steps for k, v in prof.items()},
                      **extra},
         "cpu_baseline": cpu,
@@ -806,15 +992,20 @@ def main():
     if comm is not None:
         world = comm.world_size        # n_gpus as the live communicator reports it
     names = ORDER if args.workload == "all" else (args.workload,)
+    if args.workload == "all" and world == 1:
+        names = names + ("blas",)     # the per-call layer: one process, host operands
     results = {}
     for name in names:
         t0 = time.perf_counter()
-        results[name] = run_workload(name, args, dev, rank, world,
-                                     args.cpu_seconds if name == names[0]
-                                     else min(args.cpu_seconds, 8.0))
+        cpu_s = args.cpu_seconds if name == names[0] else min(args.cpu_seconds, 8.0)
+        if name == "blas":
+            results[name] = run_blas(args, cpu_s)
+        else:
+            results[name] = run_workload(name, args, dev, rank, world, cpu_s)
         if rank == 0:
             print(f"[bench] {name}: {results[name]['value'] / 1e6:.1f} M rows/s, "
                   f"{results[name]['ms_per_step']:.2f} ms/step "
+                  f"(value {results[name]['value']:.4g} {results[name]['unit']}) "
                   f"({time.perf_counter() - t0:.0f} s with data build)",
                   file=sys.stderr, flush=True)
     if rank == 0:

@@ -174,19 +174,31 @@ __global__ void k_dspmv(int upper, int n, double alpha, const double* __restrict
   y[i] = yb + alpha * t;
 }
 
-// Fixed-shape reductions (single block): dot and sum of squares.
-__global__ void k_dot(int n, const double* __restrict__ x, const double* __restrict__ y,
-                      double* __restrict__ out, int square) {
+// Dot and sum of squares in a fixed order (bitwise reproducible): block b
+// sums the grid-strided elements its threads own into out[1 + b] by a
+// fixed tree; k_dot_final adds the blocks' partials in block order.
+constexpr int kDotBlocks = 1024;
+__global__ __launch_bounds__(256) void k_dot(int n, const double* __restrict__ x,
+                                             const double* __restrict__ y,
+                                             double* __restrict__ out, int square) {
   __shared__ double sh[256];
   double a = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) a += square ? x[i] * x[i] : x[i] * y[i];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    a += square ? x[i] * x[i] : x[i] * y[i];
   sh[threadIdx.x] = a;
   __syncthreads();
   for (int s = 128; s > 0; s >>= 1) {
     if (threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = sh[0];
+  if (threadIdx.x == 0) out[1 + blockIdx.x] = sh[0];
+}
+
+__global__ void k_dot_final(int nb, double* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int b = 0; b < nb; ++b) s += out[1 + b];
+  out[0] = s;
 }
 
 __global__ void k_axpy(int n, double a, const double* __restrict__ x, double* __restrict__ y) {
@@ -232,6 +244,10 @@ bool xerbla(const char* name, int info) {
 
 inline char up(const char* c) { return (char)std::toupper((unsigned char)c[0]); }
 
+// a contiguous view of a host vector: the caller's own memory when inc == 1
+// (no host copy), else gathered into tmp by the BLAS negative-stride rule
+const double* view(int n, const double* x, int inc, std::vector<double>& tmp);
+
 // gather a strided host vector into a contiguous one (BLAS negative-stride rule)
 std::vector<double> gather(int n, const double* x, int inc) {
   std::vector<double> v((size_t)std::max(n, 0));
@@ -242,6 +258,21 @@ std::vector<double> gather(int n, const double* x, int inc) {
 void scatter(int n, const std::vector<double>& v, double* x, int inc) {
   const long start = inc < 0 ? (long)(1 - n) * inc : 0;
   for (int i = 0; i < n; ++i) x[start + (long)i * inc] = v[i];
+}
+const double* view(int n, const double* x, int inc, std::vector<double>& tmp) {
+  if (inc == 1) return x;
+  tmp = gather(n, x, inc);
+  return tmp.data();
+}
+// the host destination of a device result: x itself when inc == 1, else tmp
+// (scattered by scatter_back afterwards)
+double* out_view(int n, double* x, int inc, std::vector<double>& tmp) {
+  if (inc == 1) return x;
+  tmp.assign((size_t)std::max(n, 0), 0.0);
+  return tmp.data();
+}
+void scatter_back(int n, const std::vector<double>& tmp, double* x, int inc) {
+  if (inc != 1) scatter(n, tmp, x, inc);
 }
 
 // copy a column-major host matrix (rows x cols, leading dim ld) to/from device
@@ -387,26 +418,29 @@ bool level1(int op, int n, double a, const double* x, int incx, double* y, int i
     return true;
   }
   if (op == 1 && a == 0.0) return true;
-  Ctx* c = ctx();
-  if (!c) return fail("stream");
-  std::vector<double> hx = gather(n, x, incx);
   if (op == 3) {
+    std::vector<double> hx = gather(n, x, incx);
     scatter(n, hx, y, incy);
     return true;
   }
-  std::vector<double> hy = (op == 0 || op == 1) ? gather(n, y, incy) : std::vector<double>();
+  Ctx* c = ctx();
+  if (!c) return fail("stream");
+  std::vector<double> tx, ty;
+  const double* hx = view(n, x, incx, tx);
+  const double* hy = (op == 0 || op == 1) ? view(n, y, incy, ty) : nullptr;
   double* dx = c->reserve(0, n);
   double* dy = c->reserve(1, n);
-  double* dr = c->reserve(2, 1);
+  double* dr = c->reserve(2, 1 + kDotBlocks);
   if (!dx || !dy || !dr ||
-      hipMemcpyAsync(dx, hx.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->st))
+      hipMemcpyAsync(dx, hx, sizeof(double) * n, hipMemcpyHostToDevice, c->st))
     return fail("copy");
-  if (!hy.empty() &&
-      hipMemcpyAsync(dy, hy.data(), sizeof(double) * n, hipMemcpyHostToDevice, c->st))
+  if (hy && hipMemcpyAsync(dy, hy, sizeof(double) * n, hipMemcpyHostToDevice, c->st))
     return fail("copy");
   const dim3 g((n + 255) / 256);
   if (op == 0 || op == 4) {
-    hipLaunchKernelGGL(k_dot, dim3(1), dim3(256), 0, c->st, n, dx, dy, dr, op == 4);
+    const int nb = (int)std::min<int64_t>(kDotBlocks, ((int64_t)n + 2047) / 2048);
+    hipLaunchKernelGGL(k_dot, dim3(nb), dim3(256), 0, c->st, n, dx, dy, dr, op == 4);
+    hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(64), 0, c->st, nb, dr);
     double r = 0.0;
     if (hipMemcpyAsync(&r, dr, sizeof(double), hipMemcpyDeviceToHost, c->st) ||
         hipStreamSynchronize(c->st))
@@ -417,12 +451,13 @@ bool level1(int op, int n, double a, const double* x, int incx, double* y, int i
   if (op == 1) hipLaunchKernelGGL(k_axpy, g, dim3(256), 0, c->st, n, a, dx, dy);
   else hipLaunchKernelGGL(k_scal, g, dim3(256), 0, c->st, n, a, dx);
   double* src = op == 1 ? dy : dx;
-  std::vector<double>& hv = op == 1 ? hy : hx;
-  if (hipMemcpyAsync(hv.data(), src, sizeof(double) * n, hipMemcpyDeviceToHost, c->st) ||
+  std::vector<double> to;
+  double* dst = op == 1 ? out_view(n, y, incy, to) : out_view(n, const_cast<double*>(x), incx, to);
+  if (hipMemcpyAsync(dst, src, sizeof(double) * n, hipMemcpyDeviceToHost, c->st) ||
       hipStreamSynchronize(c->st))
     return fail("level1");
-  if (op == 1) scatter(n, hv, y, incy);
-  else scatter(n, hv, const_cast<double*>(x), incx);
+  if (op == 1) scatter_back(n, to, y, incy);
+  else scatter_back(n, to, const_cast<double*>(x), incx);
   return true;
 }
 

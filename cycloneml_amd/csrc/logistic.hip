@@ -1424,7 +1424,7 @@ int cyc_binary_add_tiles_dev(cyc_logistic_plan p, cyc_tiles tiles, const double*
   }
   std::lock_guard<std::mutex> g(p->mu);
   const int R = cyc::tiles_ranges(v);
-  const int64_t wgMax = cyc::device_cus();
+  const int64_t wgMax = cyc::tiles_rows_blocks(n);
   if ((rc = p->rowMult.reserve(sizeof(double) * (size_t)n)) ||
       (rc = p->slabG.reserve(sizeof(double) * (size_t)R * F)) ||
       (rc = p->slabS.reserve(sizeof(double) * (size_t)wgMax * 4)) ||
@@ -1444,9 +1444,13 @@ int cyc_binary_add_tiles_dev(cyc_logistic_plan p, cyc_tiles tiles, const double*
   int64_t wgs = 0;
   {
     cyc::KernelTimer timer("k_tiles_margin", st);
-    if ((rc = cyc::tiles_margin(v, labels, weights, kc, p->fitIntercept, p->loss, offset, lscale,
-                                sigma, p->epsilon, (double*)p->rowMult.ptr,
-                                (double*)p->slabS.ptr, &wgs, st)))
+    if ((rc = cyc::tiles_margin(v, kc, (double*)p->rowMult.ptr, st))) return rc;
+  }
+  {
+    cyc::KernelTimer timer("k_tiles_rows", st);
+    if ((rc = cyc::tiles_rows(n, labels, weights, p->fitIntercept, p->loss, offset, lscale, sigma,
+                              p->epsilon, (double*)p->rowMult.ptr, (double*)p->slabS.ptr, &wgs,
+                              st)))
       return rc;
   }
   int ranges = 0;

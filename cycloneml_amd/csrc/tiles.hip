@@ -71,10 +71,7 @@ using cyc::kTileSuperCols;
 using cyc::kTileSuperRows;
 using cyc::kTileWaves;
 
-constexpr int kTPB = 64 * kTileWaves;          // threads per workgroup (8 waves)
-constexpr int kCPT = kTileCols / kTPB;         // staged coefficients per thread
-constexpr int kMPT = kTileRows / kTPB;         // staged multipliers per thread
-constexpr int kDPT = kTileSuperRows / kTPB;    // dots per thread (margin)
+constexpr int kTPB = 64 * kTileWaves;          // threads of the compute waves (8 waves)
 constexpr int kGPT = kTileSuperCols / kTPB;    // gradient sums per thread
 
 // columns per chunk: an eighth of F (so a gradient workgroup's 8 waves all
@@ -148,9 +145,11 @@ __global__ void k_seg_max(const int64_t* __restrict__ segStart, int64_t s0, int6
 // tools/probe/tiles_mall_probe.py times library builds with parts of both
 // passes removed (results then meaningless): bits 1 = plain LDS stores in
 // place of the LDS atomic adds, 2 = no LDS gathers of coefficients /
-// multipliers, 4 = no per-step barrier, 8 = no staging of the chunk / slice,
+// multipliers, 8 = no staging of the chunk / slice (the loader wave idles),
 // 16 = no run loads (synthetic ids and values), 32 = no segment offset
-// loads (every run 256 long).  0 in the library.
+// loads (every run 256 long), 64 = ids loaded as 2 bytes each (the bytes of
+// a 16-bit index; ids synthesized from them), 128 = the margin epilogue
+// stores the dots (no logistic arithmetic).  0 in the library.
 #ifndef CYC_TILES_PROBE
 #define CYC_TILES_PROBE 0
 #endif
@@ -165,14 +164,49 @@ __device__ __forceinline__ void lds_add(double* p, double x) {
 // their maxima, i.e. not waited for)
 constexpr int vm_wait(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }
 
-__device__ __forceinline__ void step_barrier() {
-  if constexpr ((CYC_TILES_PROBE & 4) == 0) __syncthreads();
-}
-
 // buffer resource over [p, p + bytes): lanes past the end read 0
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
                                            (int)std::min<int64_t>(bytes, 0x7fffffff), 0x00020000);
+}
+
+// A/B switches of the step's shape (tools/build_variant.sh), measured at
+// 200M rows (config 5; the first value is kept):
+//   MARGIN_SYNC / GRAD_SYNC  0 = a bare s_barrier per step, 1 = a full
+//       __syncthreads (its fence waits for the step's LDS atomics and
+//       offset loads first): margin 30.3 (0) / 32.0-32.3 (1) ms, gradient
+//       27.0 (1) / 27.9 (0) ms;
+//   SCHED 1 = scheduling barriers that pin the issue order (no gain);
+//   LATE_LOADS 1 = the next run's loads issued after the current run's
+//       LDS work; issued before it (0) both passes took 36 / 33.4 ms.
+#ifndef CYC_TILES_MARGIN_SYNC
+#define CYC_TILES_MARGIN_SYNC 0
+#endif
+#ifndef CYC_TILES_GRAD_SYNC
+#define CYC_TILES_GRAD_SYNC 1
+#endif
+#ifndef CYC_TILES_SCHED
+#define CYC_TILES_SCHED 0
+#endif
+#ifndef CYC_TILES_LATE_LOADS
+#define CYC_TILES_LATE_LOADS 1
+#endif
+#define CYC_TILES_SCHED_BARRIER()                                \
+  do {                                                           \
+    if constexpr (CYC_TILES_SCHED) __builtin_amdgcn_sched_barrier(0); \
+  } while (0)
+
+// The per-step barrier (step_sync<0>: a bare s_barrier).  Within the step loops a barrier
+// only has to order the compute waves' LDS READS of the step's slice (their
+// values are consumed before it) before the loader's next DMA into that
+// buffer, and the loader waits for its own DMA before it; the LDS atomics
+// and the next step's offset loads may stay in flight across it (the
+// __syncthreads fence would wait for both: lgkmcnt(0)).  A full
+// __syncthreads follows each step loop before anything reads the sums.
+template <int FULL>
+__device__ __forceinline__ void step_sync() {
+  if constexpr (FULL) __syncthreads();
+  else __builtin_amdgcn_s_barrier();
 }
 
 struct TileDims {
@@ -180,20 +214,24 @@ struct TileDims {
   int F, T, Wt;
 };
 
-// One wave's run: a segment's nonzeros [s0, s0 + len).  The segment offsets
-// come through __restrict__ read-only pointers, so the compiler fetches
-// them with scalar loads (lgkmcnt): reading them never waits on the runs in
-// flight (vmcnt).
+// One wave's run: a segment's nonzeros [a, b), empty when !on.  The
+// segment offsets come through __restrict__ read-only pointers, so the
+// compiler fetches them with scalar loads (lgkmcnt): reading them never
+// waits on the runs in flight (vmcnt).  The loads are unconditional (from
+// segment 0 when off) and the length is formed only where it is used, a
+// step later: a branch around them, or the subtraction beside them, put an
+// s_waitcnt lgkmcnt(0) right behind every step's offset load.
 struct Run {
-  int64_t s0, len;
+  int64_t a, b;
+  bool on;
+  __device__ __forceinline__ int64_t len() const { return on ? b - a : 0; }
 };
 
 __device__ __forceinline__ Run seg_run(const int64_t* __restrict__ segStart, int64_t seg,
                                        bool on) {
-  if (!on) return Run{0, 0};
-  if constexpr ((CYC_TILES_PROBE & 32) != 0) return Run{0, 256};   // the first 256 nonzeros
-  const int64_t a = segStart[seg];
-  return Run{a, segStart[seg + 1] - a};
+  if constexpr ((CYC_TILES_PROBE & 32) != 0) return Run{0, 256, on};   // the first 256 nonzeros
+  const int64_t q = on ? seg : 0;
+  return Run{segStart[q], segStart[q + 1], on};
 }
 
 // the first KC x 64 nonzeros of a run from `from` on, lane-strided; lanes
@@ -203,7 +241,7 @@ __device__ __forceinline__ void load_run(const uint32_t* __restrict__ vidx,
                                          const double* __restrict__ vvals, const Run& r,
                                          int64_t from, int lane, uint32_t (&ix)[KC],
                                          double (&vx)[KC]) {
-  const int64_t len = r.len - from;
+  const int64_t len = r.len() - from;
   if constexpr ((CYC_TILES_PROBE & 16) != 0) {
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
@@ -212,8 +250,19 @@ __device__ __forceinline__ void load_run(const uint32_t* __restrict__ vidx,
     }
     return;
   }
-  const auto ri = rsrc(vidx + r.s0 + from, len > 0 ? len * 4 : 0);
-  const auto rv = rsrc(vvals + r.s0 + from, len > 0 ? len * 8 : 0);
+  const auto rv = rsrc(vvals + r.a + from, len > 0 ? len * 8 : 0);
+  if constexpr ((CYC_TILES_PROBE & 64) != 0) {   // 2-byte ids: the bytes of a 16-bit index
+    const auto rh = rsrc(vidx + r.a + from, len > 0 ? len * 2 : 0);
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const uint32_t h = __builtin_amdgcn_raw_buffer_load_b16(rh, lane * 2, j * 128, 2);
+      ix[j] = (h & 2047) << 16 | (h & 2047);
+      vx[j] = __builtin_bit_cast(double,
+                                 __builtin_amdgcn_raw_buffer_load_b64(rv, lane * 8, j * 512, 2));
+    }
+    return;
+  }
+  const auto ri = rsrc(vidx + r.a + from, len > 0 ? len * 4 : 0);
   // lane part in the VGPR offset, batch part in the immediate offset
 #pragma unroll
   for (int j = 0; j < KC; ++j) {
@@ -223,59 +272,135 @@ __device__ __forceinline__ void load_run(const uint32_t* __restrict__ vidx,
   }
 }
 
-// run buffers of the margin pass (the runs of the next NB - 1 steps in
-// flight) and coefficient chunks in registers (CS = 2: a chunk is loaded two
-// steps before it is staged; NB a multiple of CS)
-#ifndef CYC_TILES_MARGIN_NB
-#define CYC_TILES_MARGIN_NB 3
-#endif
-#ifndef CYC_TILES_MARGIN_CS
-#define CYC_TILES_MARGIN_CS 1
-#endif
-// 1: the margin pass's coefficient chunks staged by LDS DMA (an A/B switch)
-#ifndef CYC_TILES_MARGIN_DMA
-#define CYC_TILES_MARGIN_DMA 1
+// Both passes run 8 compute waves and ONE loader wave per workgroup.  The
+// loader stages the step's shared 16 KiB slice (the margin pass's
+// coefficient chunk, the gradient pass's multiplier slice) into LDS one step
+// ahead and waits for it itself; the compute waves only issue and wait for
+// their own runs.  vmcnt counts a wave's vector-memory operations in issue
+// order, so a compute wave that staged the slice itself had to wait, before
+// each barrier, for the slice AND every run it had prefetched before it --
+// its run prefetch was one step deep whatever its depth.  With the loader
+// the runs of the next NB - 1 steps stay in flight across barriers.
+constexpr int kLoaderWave = kTileWaves;
+constexpr int kTPBL = 64 * (kTileWaves + 1);
+
+// run buffers per compute wave: the runs of the next NB - 1 steps in flight
+#ifndef CYC_TILES_NB
+#define CYC_TILES_NB 6
 #endif
 
+// The loader wave's staging of one slice src[0, count) (count <= 2048
+// doubles, lanes past it read 0) into the LDS buffer b by LDS DMA (16
+// one-KiB wave-instructions, 16-byte pieces; 64 of 4-byte pieces when src
+// is not 16-byte aligned), waited for by the loader alone before the step's
+// barrier.  (Staging through the loader's registers two steps ahead, the
+// slice written by ds_write, measured slower: 36.8 / 33.9 against 30.8 /
+// 30.1 ms per margin / gradient pass at 200M rows.)
+__device__ __forceinline__ int dma_slice(const double* src, int64_t count, double* b, int lane) {
+  const auto rs = rsrc(src, count * 8);
+  if constexpr ((CYC_TILES_PROBE & 8) != 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(b + i * 128), 16, i * 1024 + lane * 16, 0,
+          0, 0);
+    return 16;
+  }
+#pragma unroll
+  for (int i = 0; i < 64; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rs, (__attribute__((address_space(3))) void*)(b + i * 32), 4, i * 256 + lane * 4, 0, 0, 0);
+  return 64;
+}
+__device__ __forceinline__ void stage_slice(const double* src, int64_t count, double* b,
+                                            int lane) {
+  dma_slice(src, count, b, lane);
+  __builtin_amdgcn_s_waitcnt(vm_wait(0));
+}
+static_assert(kTileCols == 16 * 128 && kTileRows == 16 * 128, "16 one-KiB pieces per slice");
+
+
 // Margin pass, persistent over (super row block sb, column chunk c) steps:
-// this workgroup's super blocks sb = blockIdx.x + i * gridDim.x (8 row blocks
-// each), each swept over the T chunks, as one flat sequence of steps g.  Per
-// step: the coefficient chunk goes registers -> LDS (the next CS steps'
-// chunks are loaded meanwhile, L2 hits), and wave i walks segment
-// (8 sb + i, c); the runs of the next NB - 1 steps are in flight in
-// registers, across super block boundaries too.
-// DMA: the coefficient chunks go HBM/L2 -> LDS by buffer_load ... lds (two
-// 1 KiB pieces per wave, issued one step ahead), no staging registers or
-// ds_writes; else through registers, CS steps ahead.
-template <int NB, int CS, int KC, bool LONG, bool DMA>
-__global__ __launch_bounds__(kTPB) void k_tiles_margin(
+// this workgroup's super blocks sb = blockIdx.x + i * gridDim.x (kMW = 7 row
+// blocks each), each swept over the T chunks (padded to Tp, a multiple of
+// NB), as one flat sequence of steps g = k * Tp + c.  Per step: compute wave
+// i walks segment (7 sb + i, c) with chunk c in cf[g % 3] (ONE barrier), the
+// runs of the next NB - 1 steps in flight across super block boundaries too;
+// the loader wave DMAs the chunk of step g + 2 into cf[(g + 2) % 3] -- the
+// buffer of step g - 1, free since the last barrier -- and waits only for
+// the chunk of step g + 1, issued a step ago: a whole step for every DMA to
+// land (with two buffers and 8 row blocks it had to land within the step it
+// was issued in; the coefficients' 8 MB drift out of L2 and the Infinity
+// Cache between two workgroups' uses).  7 row blocks of dots (112 KiB) + 3
+// chunk buffers (48 KiB) fill the 160 KiB.  The super block's finished dots
+// go to dotOut (the rows' epilogue is k_tiles_rows: in here each batch of
+// rows waited on a fresh label load from HBM while the CU streamed nothing,
+// ~2 ms of a 30 ms pass at 200M rows).
+constexpr int kMW = 7;                          // compute waves (row blocks) per margin workgroup
+constexpr int kMTPB = 64 * (kMW + 1);          // + the loader wave
+constexpr int kMRows = kMW * kTileRows;         // rows per margin super block
+
+template <int NB, int KC, bool LONG>
+__global__ __launch_bounds__(kMTPB) void k_tiles_margin(
     TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
-    const double* __restrict__ vvals, const double* __restrict__ labels,
-    const double* __restrict__ weights, const double* __restrict__ coef, int fitIntercept,
-    int kind, double offset, double lscale, double sigma, double eps, double* __restrict__ mult,
-    double* __restrict__ slabS) {
-  static_assert(NB % CS == 0, "the chunk sets rotate within the unroll");
-  // 160 KiB: the super block's dots and two coefficient chunk buffers (the
-  // chunk of step s in cf[s & 1]); the final reduction reuses cf
-  __shared__ double lds[kTileSuperRows + 2 * kTileCols];
+    const double* __restrict__ vvals, const double* __restrict__ coef,
+    double* __restrict__ dotOut) {
+  static_assert(NB >= 2, "at least one run in flight");
+  static_assert(kMRows * 8 + 3 * kTileCols * 8 <= 160 * 1024, "LDS");
+  __shared__ double lds[kMRows + 3 * kTileCols];
   double* const dots = lds;
-  double* const cf = lds + kTileSuperRows;
+  double* const cf = lds + kMRows;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T = v.T;
-  const int64_t nSB = (v.nRB + kTileWaves - 1) / kTileWaves;
-  // steps per super block padded to a multiple of NB (the unroll of the run
-  // buffers; with CS = 2, NB and so Tp are even, and a step's chunk set is
-  // fixed by its place in the unroll); the padding steps have empty runs and
-  // fetch nothing
+  const int64_t nSB = (v.nRB + kMW - 1) / kMW;
   const int Tp = (T + NB - 1) / NB * NB;
   const int64_t mySB = nSB > blockIdx.x ? (nSB - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};     // loss, weight, multiplierSum, sigmaGradSum
-  double creg[DMA ? 1 : CS][kCPT];          // chunk of step g in creg[g % CS]
+  // buffer of flat step g: g % 3 (the flat step count fits 32 bits: Tp *
+  // super blocks per workgroup is the launch's per-workgroup step count)
+  auto bufOf = [&](int64_t k, int c) { return cf + ((uint32_t)(k * Tp + c) % 3u) * kTileCols; };
+
+  if (wave == kMW) {
+    // the loader: the same barriers as the compute waves, in the same order
+    auto chunk = [&](int64_t k, int c) {
+      const bool on = k < mySB && c < T;
+      const int64_t c0 = on ? (int64_t)c * v.Wt : 0;
+      const int64_t wl = on ? std::min<int64_t>(v.Wt, v.F - c0) : 0;
+      return dma_slice(coef + c0, wl, bufOf(k, c), lane);
+    };
+    auto next = [&](int64_t& k, int& c) {
+      if (++c >= Tp) c = 0, ++k;
+    };
+    int64_t k2 = 0;
+    int c2 = 0;
+    chunk(k2, c2);                                // step 0
+    next(k2, c2);
+    const int n1 = chunk(k2, c2);                 // step 1
+    next(k2, c2);
+    if (n1 == 16) __builtin_amdgcn_s_waitcnt(vm_wait(16));     // step 0's landed
+    else __builtin_amdgcn_s_waitcnt(vm_wait(0));
+    for (int64_t k = 0; k < mySB; ++k) {
+      __syncthreads();                            // dots zeroed, chunk (k, 0) in place
+      for (int c = 0; c < Tp; ++c) {
+        // the chunk two steps ahead (k2, c2) into the buffer the last
+        // barrier freed; then the chunk of the next step (issued a step
+        // ago) landed: only the DMA just issued may stay in flight
+        const int n2 = chunk(k2, c2);
+        next(k2, c2);
+        if (n2 == 16) __builtin_amdgcn_s_waitcnt(vm_wait(16));
+        else __builtin_amdgcn_s_waitcnt(vm_wait(0));
+        step_sync<CYC_TILES_MARGIN_SYNC>();       // step (k, c)
+      }
+      __syncthreads();                            // the super block's dots complete
+      __syncthreads();                            // dots stored
+    }
+    return;
+  }
+
   uint32_t ib[NB][KC];
   double vb[NB][KC];
   Run rr[NB];
-
   // a step is (k, c): this workgroup's k-th super block, chunk c < Tp; the
   // positions a few steps ahead by compare-and-wrap (no divisions)
   auto ahead = [&](int64_t k, int c, int by, int64_t& k2, int& c2) {
@@ -284,42 +409,18 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
     if (c2 >= Tp) c2 -= Tp, k2 += 1;
   };
   auto run_of = [&](int64_t k, int c) {
-    const int64_t rb = ((int64_t)blockIdx.x + k * gridDim.x) * kTileWaves + wave;
+    const int64_t rb = ((int64_t)blockIdx.x + k * gridDim.x) * kMW + wave;
     return seg_run(segStart, rb * T + c, k < mySB && c < T && rb < v.nRB);
-  };
-  auto load_coef = [&](int64_t k, int c, double (&cr)[kCPT]) {
-    const bool on = k < mySB && c < T;
-    const int64_t c0 = on ? (int64_t)c * v.Wt : 0;
-    const int wl = on ? (int)std::min<int64_t>(v.Wt, v.F - c0) : 0;
-    const auto rc = rsrc(coef + c0, (int64_t)wl * 8);
-#pragma unroll
-    for (int i = 0; i < kCPT; ++i)
-      cr[i] = __builtin_bit_cast(
-          double, __builtin_amdgcn_raw_buffer_load_b64(rc, tid * 8, i * kTPB * 8, 0));
   };
   double* myDots = dots + wave * kTileRows;
   // waits for the whole run first, on every path: its values are used only
   // under the lanes' `< len` branches, and a path that skips one left the
   // compiler's wait analysis treating the registers as still loading at the
-  // loop head, where it then drained every prefetched run (vmcnt(0)).  The
-  // runs of the other NB - 2 steps and the staging loads of the steps since
-  // -- (NB - 2) (2 KC + 4) operations -- stay in flight.
-  // the chunk of step (k, c) into b by DMA: wave w's pieces 2w, 2w + 1
-  auto dma_coef = [&](int64_t k, int c, double* b) {
-    const bool on = k < mySB && c < T;
-    const int64_t c0 = on ? (int64_t)c * v.Wt : 0;
-    const int wl = on ? (int)std::min<int64_t>(v.Wt, v.F - c0) : 0;
-    const auto rc = rsrc(coef + c0, (int64_t)wl * 8);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rc, (__attribute__((address_space(3))) void*)(b + (wave * 2 + i) * 128), 16,
-          (wave * 2 + i) * 1024 + lane * 16, 0, 0, 0);
-  };
-  static_assert(!DMA || kTileCols * 8 == kTileWaves * 2 * 1024, "two 1 KiB pieces per wave");
+  // loop head, where it then drained every prefetched run (vmcnt(0)); the
+  // runs of the next NB - 2 steps stay in flight
   auto consume = [&](int64_t len, const double* cfp, const uint32_t (&ix)[KC],
                      const double (&vx)[KC]) {
-    __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2) * (2 * KC + (DMA ? 2 : 4))));
+    __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2 + !CYC_TILES_LATE_LOADS) * 2 * KC));
     double c[KC];
 #pragma unroll
     for (int j = 0; j < KC; ++j)   // lanes past the end read [0]
@@ -329,204 +430,157 @@ __global__ __launch_bounds__(kTPB) void k_tiles_margin(
       if (j * 64 + lane < len) lds_add(&myDots[ix[j] >> 16], vx[j] * c[j]);
   };
   // One step (k, c), ONE barrier: the current run into the row sums with
-  // chunk s in cf[s & 1], the next chunk (in registers since CS steps ago)
-  // into the other buffer -- every wave left it behind the last barrier --,
-  // then the loads of the chunk CS + 1 steps and of the run NB - 1 steps
-  // ahead issued (unconditionally: past the end they fetch nothing, so the
-  // waits for the current run stay counted).  The run buffers and chunk sets
-  // rotate by unrolling (never by copying a register that a load is still
-  // filling).
-  auto step = [&](int64_t k, int c, const Run& rc, uint32_t (&ic)[KC], double (&vc)[KC],
-                  Run& rn, uint32_t (&in)[KC], double (&vn)[KC], double (&cs)[kCPT]) {
-    const int par = (int)((k * Tp + c) & 1);
-    const double* cur = cf + par * kTileCols;
-    consume(rc.len, cur, ic, vc);
+  // chunk (k, c) in cf[g % 3], then the loads of the run NB - 1 steps ahead
+  // (its offsets loaded a step ago), then the scalar loads of the offsets of
+  // the run NB steps ahead (into this step's slot, its own offsets kept in
+  // `cur`): issued after the step's LDS reads, since an SMEM load in flight
+  // turns every lgkmcnt wait into lgkmcnt(0) (SMEM returns out of order),
+  // and waited for by the next step's first use -- before, a scalar load
+  // waited for in front of the run loads also drained the step's LDS
+  // atomics.  The loads are issued unconditionally (past the end they fetch
+  // nothing, so the waits stay counted); the run buffers rotate by
+  // unrolling (never by copying a register that a load is still filling).
+  auto step = [&](int64_t k, int c, Run& rc, uint32_t (&ic)[KC], double (&vc)[KC],
+                  const Run& rn, uint32_t (&in)[KC], double (&vn)[KC]) {
+    const Run cur = rc;
+    const double* buf = bufOf(k, c);
+    if constexpr (!CYC_TILES_LATE_LOADS) {
+      load_run(vidx, vvals, rn, 0, lane, in, vn);
+      CYC_TILES_SCHED_BARRIER();                  // the loads issue first
+    }
+    consume(cur.len(), buf, ic, vc);
     // a run longer than KC x 64: only in the LONG instance (a layout with
     // such segments), in registers of its own -- any load in this loop's
     // body makes the compiler's wait analysis drain every prefetched run
     // at the loop head
     if constexpr (LONG) {
-      for (int64_t b = KC * 64; b < rc.len; b += KC * 64) {
+      for (int64_t b = KC * 64; b < cur.len(); b += KC * 64) {
         uint32_t it[KC];
         double vt[KC];
-        load_run(vidx, vvals, rc, b, lane, it, vt);
-        consume(rc.len - b, cur, it, vt);
+        load_run(vidx, vvals, cur, b, lane, it, vt);
+        consume(cur.len() - b, buf, it, vt);
       }
     }
-    double* nxt = cf + (par ^ 1) * kTileCols;
+    if constexpr (CYC_TILES_LATE_LOADS) load_run(vidx, vvals, rn, 0, lane, in, vn);
+    CYC_TILES_SCHED_BARRIER();
     int64_t k2;
     int c2;
-    if constexpr (DMA) {
-      // chunk of the next step into the buffer every wave left behind the
-      // last barrier; landed (this wave's pieces) before the next barrier:
-      // only this step's run loads are issued after it
-      ahead(k, c, 1, k2, c2);
-      dma_coef(k2, c2, nxt);
-    } else if constexpr ((CYC_TILES_PROBE & 8) == 0) {
-#pragma unroll
-      for (int i = 0; i < kCPT; ++i) nxt[tid + kTPB * i] = cs[i];
-      ahead(k, c, CS + 1, k2, c2);
-      load_coef(k2, c2, cs);
-    }
-    ahead(k, c, NB - 1, k2, c2);
-    rn = run_of(k2, c2);
-    load_run(vidx, vvals, rn, 0, lane, in, vn);
-    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(vm_wait(2 * KC));
-    step_barrier();
+    ahead(k, c, NB, k2, c2);
+    rc = run_of(k2, c2);
+    step_sync<CYC_TILES_MARGIN_SYNC>();
   };
 
-  // prologue: chunk 0 into cf[0], chunks 1 .. CS in registers (DMA: chunk
-  // 0 only, landed before the first barrier), runs of steps 0 .. NB - 2 in
-  // flight
-  if constexpr (DMA) {
-    dma_coef(0, 0, cf);
-    __builtin_amdgcn_s_waitcnt(vm_wait(0));
-  } else {
-    load_coef(0, 0, creg[0]);
+  // prologue: the offsets of steps 0 .. NB - 1, the runs of steps
+  // 0 .. NB - 2 in flight
 #pragma unroll
-    for (int i = 0; i < kCPT; ++i) cf[tid + kTPB * i] = creg[0][i];
-#pragma unroll
-    for (int s1 = 1; s1 <= CS; ++s1) {
-      int64_t k1;
-      int c1;
-      ahead(0, 0, s1, k1, c1);
-      load_coef(k1, c1, creg[s1 % CS]);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < NB - 1; ++u) {
+  for (int u = 0; u < NB; ++u) {
     int64_t k1;
     int c1;
     ahead(0, 0, u, k1, c1);
     rr[u] = run_of(k1, c1);
-    load_run(vidx, vvals, rr[u], 0, lane, ib[u], vb[u]);
   }
-  // The binary logistic epilogue (kind 0: BinaryLogisticBlockAggregator.
-  // scala:104-122) without branches, EB rows at a time with the next EB
-  // rows' labels and weights loaded before this batch's multiplier stores
-  // (vmcnt waits are in issue order: a load issued after a store waits for
-  // it too).  log1pExp(x) (ml/impl/Utils.scala:91-97) as max(x, 0) +
-  // log1p(exp(-|x|)): the same two branches, the same bits (0 + y == y for
-  // the x <= 0 one).  Rows are visited in the plain loop's order, so the
-  // sums are the same bits as well.
-  auto logistic_epilogue = [&](int64_t r0) {
-    constexpr int EB = 4;
-    double lab[2][EB], wt[2][EB];
-    auto ld = [&](int i0, double (&l)[EB], double (&w)[EB]) {
 #pragma unroll
-      for (int u = 0; u < EB; ++u) {
-        const int64_t rr = min<int64_t>(r0 + tid + (int64_t)kTPB * (i0 + u), v.n - 1);
-        l[u] = __builtin_nontemporal_load(&labels[rr]);   // streamed once
-        w[u] = weights ? __builtin_nontemporal_load(&weights[rr]) : 1.0;
-      }
-    };
-    ld(0, lab[0], wt[0]);
-#pragma unroll
-    for (int i0 = 0; i0 < kDPT; i0 += EB) {
-      const int cb = (i0 / EB) & 1;
-      if (i0 + EB < kDPT) ld(i0 + EB, lab[cb ^ 1], wt[cb ^ 1]);
-#pragma unroll
-      for (int u = 0; u < EB; ++u) {
-        const int rl = tid + kTPB * (i0 + u);
-        const int64_t r = r0 + rl;
-        const double label = lab[cb][u], w = wt[cb][u];
-        const double margin = fitIntercept ? offset + dots[rl] : dots[rl];
-        const double x = -margin;
-        const double lp = __builtin_fmax(x, 0.0) + log1p(exp(-__builtin_fabs(x)));
-        const double term = label > 0 ? lp : lp + margin;
-        const double mm = w * (1.0 / (1.0 + exp(-margin)) - label);
-        if (r < v.n) {
-          acc[1] += w;
-          double m = 0.0;
-          if (w > 0) {
-            acc[0] += w * term;
-            m = mm;
-          }
-          acc[2] += m;
-          __builtin_nontemporal_store(m, &mult[r]);
-        }
-      }
-    }
-  };
+  for (int u = 0; u < NB - 1; ++u) load_run(vidx, vvals, rr[u], 0, lane, ib[u], vb[u]);
+  constexpr int kCT = 64 * kMW;                  // compute threads
+  static_assert(kMRows % kCT == 0, "whole dots per thread");
   for (int64_t k = 0; k < mySB; ++k) {          // one super block per pass
 #pragma unroll
-    for (int i = 0; i < kDPT; ++i) dots[tid + kTPB * i] = 0.0;
-    __syncthreads();                            // zeroed dots, chunk 0 in cf[0]
+    for (int i = 0; i < kMRows / kCT; ++i) dots[tid + kCT * i] = 0.0;
+    __syncthreads();                            // zeroed dots, chunk (k, 0) in place
     for (int c = 0; c < Tp; c += NB) {
 #pragma unroll
       for (int u = 0; u < NB; ++u)
         step(k, c + u, rr[u], ib[u], vb[u], rr[(u + NB - 1) % NB], ib[(u + NB - 1) % NB],
-             vb[(u + NB - 1) % NB], creg[DMA ? 0 : (u + 1) % CS]);
+             vb[(u + NB - 1) % NB]);
     }
-    // epilogue (BinaryLogisticBlockAggregator.scala:104-122 and siblings)
-    const int64_t r0 = ((int64_t)blockIdx.x + k * gridDim.x) * kTileSuperRows;
-    if (kind == 0) {
-      logistic_epilogue(r0);
-      __syncthreads();                          // dots read before the next zeroing
-      continue;
-    }
-    for (int i = 0; i < kDPT; ++i) {
-      const int rl = tid + kTPB * i;
-      const int64_t r = r0 + rl;
-      if (r < v.n) {
-        const double label = labels[r];
-        const double margin = cyc::row_margin(kind, fitIntercept, offset, lscale, label, dots[rl]);
-        const double w = weights ? weights[r] : 1.0;
-        const double m = cyc::bin_row(kind, margin, w, label, acc[0], acc[1], acc[3], sigma, eps);
-        acc[2] += m;
-        mult[r] = m;
-      }
+    __syncthreads();                            // every wave's atomics landed
+    const int64_t r0 = ((int64_t)blockIdx.x + k * gridDim.x) * kMRows;
+#pragma unroll
+    for (int i = 0; i < kMRows / kCT; ++i) {
+      const int64_t r = r0 + tid + kCT * i;
+      if (r < v.n) __builtin_nontemporal_store(dots[tid + kCT * i], &dotOut[r]);
     }
     __syncthreads();                            // dots read before the next zeroing
   }
-  // workgroup partials: fixed shuffle tree per wave, then waves in order
-  double (*red)[4] = reinterpret_cast<double (*)[4]>(cf);
+}
+
+// The rows' epilogue of the binary aggregators after the margin pass: per
+// row r, margin = row_margin(offset + dot_r) and the aggregator kind's
+// multiplier (binary_rows.hpp; kind 0 BinaryLogisticBlockAggregator.scala:
+// 104-122 without branches: log1pExp(x) (ml/impl/Utils.scala:91-97) as
+// max(x, 0) + log1p(exp(-|x|)), the same two branches and bits), written
+// over the dot in dm; per-workgroup (loss, weight, multiplierSum,
+// sigmaGradSum) partials to slabS[wg * 4 + k] -- each thread's rows in row
+// order, a fixed shuffle tree per wave, the waves in order.  Streams 24 B
+// per row (dot, label, multiplier; + 8 with weights).
+__global__ __launch_bounds__(256) void k_tiles_rows(
+    int64_t n, const double* __restrict__ labels, const double* __restrict__ weights,
+    int fitIntercept, int kind, double offset, double lscale, double sigma, double eps,
+    double* __restrict__ dm, double* __restrict__ slabS) {
+  __shared__ double red[4][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};     // loss, weight, multiplierSum, sigmaGradSum
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  constexpr int U = 4;
+  for (int64_t r0 = (int64_t)blockIdx.x * 256 + tid; r0 < n; r0 += U * stride) {
+    double dot[U], lab[U], w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = min<int64_t>(r0 + u * stride, n - 1);
+      dot[u] = __builtin_nontemporal_load(&dm[r]);
+      lab[u] = __builtin_nontemporal_load(&labels[r]);
+      w[u] = weights ? __builtin_nontemporal_load(&weights[r]) : 1.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = r0 + u * stride;
+      if (r >= n) break;
+      double m;
+      if (kind == 0) {
+        const double margin = fitIntercept ? offset + dot[u] : dot[u];
+        const double x = -margin;
+        const double lp = __builtin_fmax(x, 0.0) + log1p(exp(-__builtin_fabs(x)));
+        const double term = lab[u] > 0 ? lp : lp + margin;
+        const double mm = w[u] * (1.0 / (1.0 + exp(-margin)) - lab[u]);
+        acc[1] += w[u];
+        m = 0.0;
+        if (w[u] > 0) {
+          acc[0] += w[u] * term;
+          m = mm;
+        }
+      } else {
+        const double margin = cyc::row_margin(kind, fitIntercept, offset, lscale, lab[u], dot[u]);
+        m = cyc::bin_row(kind, margin, w[u], lab[u], acc[0], acc[1], acc[3], sigma, eps);
+      }
+      acc[2] += m;
+      __builtin_nontemporal_store(m, &dm[r]);
+    }
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) acc[k] += __shfl_xor(acc[k], m);
-  __syncthreads();
   if (lane == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) red[wave][k] = acc[k];
   }
   __syncthreads();
-  if (tid < 4) {
-    double s = 0.0;
-    for (int w = 0; w < kTileWaves; ++w) s += red[w][tid];
-    slabS[(int64_t)blockIdx.x * 4 + tid] = s;
-  }
+  if (tid < 4) slabS[(int64_t)blockIdx.x * 4 + tid] = ((red[0][tid] + red[1][tid]) + red[2][tid]) +
+                                                     red[3][tid];
 }
 
-// run buffers of the gradient pass: the runs of the next NB - 1 row blocks
-// are in flight while one is consumed; MS multiplier slices in registers
-// (MS = 2: a slice is loaded two row blocks before it is staged; NB even)
-#ifndef CYC_TILES_GRAD_NB
-#define CYC_TILES_GRAD_NB 3
-#endif
-#ifndef CYC_TILES_GRAD_MS
-#define CYC_TILES_GRAD_MS 1
-#endif
-// 1: the gradient pass's multiplier slices staged by LDS DMA (an A/B switch)
-#ifndef CYC_TILES_GRAD_DMA
-#define CYC_TILES_GRAD_DMA 1
-#endif
-
 // Gradient pass: workgroup (super chunk st = 8 column chunks, row range)
-// over its row blocks.  Per row block: the multiplier slice goes registers
-// -> LDS (the next ones loaded while this one is used); wave j walks segment
-// (rb, 8 st + j) into its chunk's column sums, with the runs of the next
-// NB - 1 row blocks in flight.
-// DMA: the multiplier slices go to LDS by buffer_load ... lds, one row
-// block ahead (as the margin pass's coefficient chunks).
-template <int NB, int MS, int KC, bool LONG, bool DMA>
-__global__ __launch_bounds__(kTPB) void k_tiles_grad(
+// over its row blocks.  Per row block: compute wave j walks segment
+// (rb, 8 st + j) into its chunk's column sums with the multiplier slice of
+// rb in mv[(rb - rbA) & 1] (ONE barrier), the runs of the next NB - 1 row
+// blocks in flight; the loader stages the next row block's slice.
+template <int NB, int KC, bool LONG>
+__global__ __launch_bounds__(kTPBL) void k_tiles_grad(
     TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
     const double* __restrict__ vvals, const double* __restrict__ mult, int ranges,
     double* __restrict__ slabG) {
-  static_assert(MS == 1 || (MS == 2 && NB % 2 == 0), "two slice sets need an even unroll");
+  static_assert(NB >= 2, "at least one run in flight");
   // 160 KiB: the 8 chunks' column sums and two multiplier slice buffers
-  // (row block rb's slice in mv[(rb - rbA) & 1])
   __shared__ double lds[kTileSuperCols + 2 * kTileRows];
   double* const gt = lds;
   double* const mv = lds + kTileSuperCols;
@@ -534,40 +588,39 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int range = blockIdx.x % ranges, st = blockIdx.x / ranges;
   const int64_t rbA = v.nRB * range / ranges, rbB = v.nRB * (range + 1) / ranges;
+  // whole groups of NB steps: the last group's steps past rbB have empty
+  // runs and slices (no guard inside the unroll: a skipped step left the
+  // compiler's wait analysis draining every prefetched run at the loop head)
+  const int64_t steps = (rbB - rbA + NB - 1) / NB * NB;
+
+  if (wave == kLoaderWave) {
+    auto slice = [&](int64_t rb) {
+      const bool on = rb < rbB;
+      const int64_t r0 = on ? rb * kTileRows : 0;
+      stage_slice(mult + r0, on ? std::min<int64_t>(kTileRows, v.n - r0) : 0,
+                  mv + ((rb - rbA) & 1) * kTileRows, lane);
+    };
+    slice(rbA);
+    __syncthreads();                              // sums zeroed, slice rbA in place
+    for (int64_t s = 0; s < steps; ++s) {
+      slice(rbA + s + 1);                         // into the buffer the last barrier freed
+      step_sync<CYC_TILES_GRAD_SYNC>();                                // step rbA + s
+    }
+    __syncthreads();                              // sums complete
+    return;
+  }
+
   const int c = st * kTileWaves + wave;                 // this wave's column chunk
-  double mreg[DMA ? 1 : MS][kMPT];                      // slice r in mreg[(r - rbA) % MS]
   uint32_t ib[NB][KC];
   double vb[NB][KC];
   Run rr[NB];
-
   auto run_of = [&](int64_t rb) { return seg_run(segStart, rb * v.T + c, rb < rbB && c < v.T); };
-  auto load_mult = [&](int64_t rb, double (&m)[kMPT]) {
-    const int64_t r0 = rb * kTileRows;
-    const auto rm = rsrc(mult + (rb < rbB ? r0 : 0),
-                         rb < rbB ? std::min<int64_t>(kTileRows, v.n - r0) * 8 : 0);
-#pragma unroll
-    for (int i = 0; i < kMPT; ++i)
-      m[i] = __builtin_bit_cast(
-          double, __builtin_amdgcn_raw_buffer_load_b64(rm, tid * 8, i * kTPB * 8, 0));
-  };
-  // row block rb's slice into b by DMA: wave w's pieces 2w, 2w + 1
-  auto dma_mult = [&](int64_t rb, double* b) {
-    const int64_t r0 = rb * kTileRows;
-    const auto rm = rsrc(mult + (rb < rbB ? r0 : 0),
-                         rb < rbB ? std::min<int64_t>(kTileRows, v.n - r0) * 8 : 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rm, (__attribute__((address_space(3))) void*)(b + (wave * 2 + i) * 128), 16,
-          (wave * 2 + i) * 1024 + lane * 16, 0, 0, 0);
-  };
-  static_assert(!DMA || kTileRows * 8 == kTileWaves * 2 * 1024, "two 1 KiB pieces per wave");
   double* myG = gt + wave * v.Wt;
   // waits for the whole run first, on every path (the margin pass's
   // consume says why)
   auto consume = [&](int64_t len, const double* mvp, const uint32_t (&ix)[KC],
                      const double (&vx)[KC]) {
-    __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2) * (2 * KC + (DMA ? 2 : 4 * MS))));
+    __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2 + !CYC_TILES_LATE_LOADS) * 2 * KC));
     double m[KC];
 #pragma unroll
     for (int j = 0; j < KC; ++j)   // lanes past the end read [0]
@@ -579,69 +632,47 @@ __global__ __launch_bounds__(kTPB) void k_tiles_grad(
 
 #pragma unroll
   for (int i = 0; i < kGPT; ++i) gt[tid + kTPB * i] = 0.0;
-  // one row block (the u-th of an unrolled group), ONE barrier: the current
-  // run into the column sums with the slice in mv[par], the next slice (in
-  // registers since MS steps ago) into the other buffer -- every wave left
-  // it behind the last barrier --, then the slice MS + 1 row blocks ahead
-  // and the run NB - 1 row blocks ahead issued (unconditionally, into the
-  // registers just freed); run buffers and slice sets rotate by unrolling
-  auto step = [&](int64_t rb, const Run& rc, uint32_t (&ic)[KC], double (&vc)[KC],
-                  Run& rn, uint32_t (&in)[KC], double (&vn)[KC], double (&ms)[kMPT]) {
-    const int par = (int)((rb - rbA) & 1);
-    const double* cur = mv + par * kTileRows;
-    consume(rc.len, cur, ic, vc);
-    // a run longer than KC x 64: only in the LONG instance (a layout with
-    // such segments), in registers of its own -- any load in this loop's
-    // body makes the compiler's wait analysis drain every prefetched run
-    // at the loop head
+  // one row block (the u-th of an unrolled group), ONE barrier: the run
+  // NB - 1 row blocks ahead issued (its offsets loaded a step ago), the
+  // current run into the column sums with the slice in mv[(rb - rbA) & 1],
+  // then the offsets of the run NB ahead loaded into this step's slot (the
+  // margin pass's step says why in this order); the run buffers rotate by
+  // unrolling
+  auto step = [&](int64_t rb, Run& rc, uint32_t (&ic)[KC], double (&vc)[KC], const Run& rn,
+                  uint32_t (&in)[KC], double (&vn)[KC]) {
+    const Run cur = rc;
+    const double* buf = mv + ((rb - rbA) & 1) * kTileRows;
+    if constexpr (!CYC_TILES_LATE_LOADS) {
+      load_run(vidx, vvals, rn, 0, lane, in, vn);
+      CYC_TILES_SCHED_BARRIER();                  // the loads issue first
+    }
+    consume(cur.len(), buf, ic, vc);
     if constexpr (LONG) {
-      for (int64_t b = KC * 64; b < rc.len; b += KC * 64) {
+      for (int64_t b = KC * 64; b < cur.len(); b += KC * 64) {
         uint32_t it[KC];
         double vt[KC];
-        load_run(vidx, vvals, rc, b, lane, it, vt);
-        consume(rc.len - b, cur, it, vt);
+        load_run(vidx, vvals, cur, b, lane, it, vt);
+        consume(cur.len() - b, buf, it, vt);
       }
     }
-    double* nxt = mv + (par ^ 1) * kTileRows;
-    if constexpr (DMA) {
-      dma_mult(rb + 1, nxt);   // landed before the barrier: only the run loads follow it
-    } else if constexpr ((CYC_TILES_PROBE & 8) == 0) {
-#pragma unroll
-      for (int i = 0; i < kMPT; ++i) nxt[tid + kTPB * i] = ms[i];
-      load_mult(rb + 1 + MS, ms);
-    }
-    rn = run_of(rb + NB - 1);
-    load_run(vidx, vvals, rn, 0, lane, in, vn);
-    if constexpr (DMA) __builtin_amdgcn_s_waitcnt(vm_wait(2 * KC));
-    step_barrier();
+    if constexpr (CYC_TILES_LATE_LOADS) load_run(vidx, vvals, rn, 0, lane, in, vn);
+    CYC_TILES_SCHED_BARRIER();                    // after the LDS reads (the margin pass's step)
+    rc = run_of(rb + NB);
+    step_sync<CYC_TILES_GRAD_SYNC>();
   };
 
-  // prologue: slice rbA into mv[0], slices rbA + 1 .. rbA + MS in
-  // registers, runs rbA .. rbA + NB - 2 in flight
-  if constexpr (DMA) {
-    dma_mult(rbA, mv);
-    __builtin_amdgcn_s_waitcnt(vm_wait(0));
-  } else {
-    load_mult(rbA, mreg[0]);
+  // prologue: the offsets of row blocks rbA .. rbA + NB - 1, the runs of
+  // rbA .. rbA + NB - 2 in flight
 #pragma unroll
-    for (int i = 0; i < kMPT; ++i) mv[tid + kTPB * i] = mreg[0][i];
+  for (int u = 0; u < NB; ++u) rr[u] = run_of(rbA + u);
 #pragma unroll
-    for (int s = 1; s <= MS; ++s) load_mult(rbA + s, mreg[s % MS]);
-  }
-#pragma unroll
-  for (int u = 0; u < NB - 1; ++u) {
-    rr[u] = run_of(rbA + u);
-    load_run(vidx, vvals, rr[u], 0, lane, ib[u], vb[u]);
-  }
-  __syncthreads();                              // zeroed sums, slice rbA in mv[0]
-  // whole groups of NB steps: the last group's steps past rbB have empty
-  // runs and slices (no guard inside the unroll: a skipped step left the
-  // compiler's wait analysis draining every prefetched run at the loop head)
-  for (int64_t rb = rbA; rb < rbB; rb += NB) {
+  for (int u = 0; u < NB - 1; ++u) load_run(vidx, vvals, rr[u], 0, lane, ib[u], vb[u]);
+  __syncthreads();                              // zeroed sums, slice rbA in place
+  for (int64_t s = 0; s < steps; s += NB) {
 #pragma unroll
     for (int u = 0; u < NB; ++u)
-      step(rb + u, rr[u], ib[u], vb[u], rr[(u + NB - 1) % NB], ib[(u + NB - 1) % NB],
-           vb[(u + NB - 1) % NB], mreg[DMA ? 0 : (u + 1) % MS]);
+      step(rbA + s + u, rr[u], ib[u], vb[u], rr[(u + NB - 1) % NB], ib[(u + NB - 1) % NB],
+           vb[(u + NB - 1) % NB]);
   }
   __syncthreads();
   const int64_t col0 = (int64_t)st * kTileWaves * v.Wt;
@@ -679,31 +710,33 @@ int tiles_view(cyc_tiles t, TilesView* v) {
   return CYC_OK;
 }
 
-int tiles_margin(const TilesView& v, const double* labels, const double* weights,
-                 const double* coef, int fitIntercept, int kind, double offset, double lscale,
-                 double sigma, double eps, double* mult, double* slabS, int64_t* wgs,
-                 hipStream_t st) {
-  const int64_t nSB = (v.nRB + kTileWaves - 1) / kTileWaves;
+int tiles_margin(const TilesView& v, const double* coef, double* dots, hipStream_t st) {
+  const int64_t nSB = (v.nRB + kMW - 1) / kMW;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nSB, device_cus()));
-  *wgs = grid;
   const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
-#define CYC_TILES_MARGIN(KC, LONG, DMA)                                                         \
-  hipLaunchKernelGGL(                                                                           \
-      HIP_KERNEL_NAME(k_tiles_margin<CYC_TILES_MARGIN_NB, CYC_TILES_MARGIN_CS, KC, LONG, DMA>),  \
-      dim3((unsigned)grid), dim3(kTPB), 0, st, d, v.segStart, v.idx, v.vals, labels, weights,   \
-      coef, fitIntercept, kind, offset, lscale, sigma, eps, mult, slabS)
-  // the DMA pieces are 16-byte loads: a coefficient vector that is not
-  // 16-byte aligned takes the register-staged instance
-  const bool dma = CYC_TILES_MARGIN_DMA && (reinterpret_cast<uintptr_t>(coef) & 15) == 0;
-  if (long_runs(v.maxSeg)) {
-    if (dma) CYC_TILES_MARGIN(5, true, true);
-    else CYC_TILES_MARGIN(5, true, false);
-  } else {
-    if (dma) CYC_TILES_MARGIN(5, false, true);
-    else CYC_TILES_MARGIN(5, false, false);
-  }
+#define CYC_TILES_MARGIN(KC, LONG)                                                              \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_margin<CYC_TILES_NB, KC, LONG>),                   \
+                     dim3((unsigned)grid), dim3(kMTPB), 0, st, d, v.segStart, v.idx, v.vals,    \
+                     coef, dots)
+  if (long_runs(v.maxSeg)) CYC_TILES_MARGIN(5, true);
+  else CYC_TILES_MARGIN(5, false);
 #undef CYC_TILES_MARGIN
   CYC_LAUNCH_CHECK("k_tiles_margin");
+  return CYC_OK;
+}
+
+int64_t tiles_rows_blocks(int64_t n) {
+  return std::max<int64_t>(1, std::min<int64_t>(4 * device_cus(), (n + 1023) / 1024));
+}
+
+int tiles_rows(int64_t n, const double* labels, const double* weights, int fitIntercept,
+               int kind, double offset, double lscale, double sigma, double eps, double* dm,
+               double* slabS, int64_t* wgs, hipStream_t st) {
+  const int64_t g = tiles_rows_blocks(n);
+  *wgs = g;
+  hipLaunchKernelGGL(k_tiles_rows, dim3((unsigned)g), dim3(256), 0, st, n, labels, weights,
+                     fitIntercept, kind, offset, lscale, sigma, eps, dm, slabS);
+  CYC_LAUNCH_CHECK("k_tiles_rows");
   return CYC_OK;
 }
 
@@ -719,18 +752,12 @@ int tiles_grad(const TilesView& v, const double* mult, double* slabG, int* range
   *ranges = R;
   const int64_t sts = (v.T + kTileWaves - 1) / kTileWaves;
   const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
-#define CYC_TILES_GRAD(KC, LONG, DMA)                                                           \
-  hipLaunchKernelGGL(                                                                           \
-      HIP_KERNEL_NAME(k_tiles_grad<CYC_TILES_GRAD_NB, CYC_TILES_GRAD_MS, KC, LONG, DMA>),        \
-      dim3((unsigned)(sts * R)), dim3(kTPB), 0, st, d, v.segStart, v.idx, v.vals, mult, R, slabG)
-  const bool dma = CYC_TILES_GRAD_DMA && (reinterpret_cast<uintptr_t>(mult) & 15) == 0;
-  if (long_runs(v.maxSeg)) {
-    if (dma) CYC_TILES_GRAD(5, true, true);
-    else CYC_TILES_GRAD(5, true, false);
-  } else {
-    if (dma) CYC_TILES_GRAD(5, false, true);
-    else CYC_TILES_GRAD(5, false, false);
-  }
+#define CYC_TILES_GRAD(KC, LONG)                                                                \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_grad<CYC_TILES_NB, KC, LONG>),                     \
+                     dim3((unsigned)(sts * R)), dim3(kTPBL), 0, st, d, v.segStart, v.idx, v.vals, \
+                     mult, R, slabG)
+  if (long_runs(v.maxSeg)) CYC_TILES_GRAD(5, true);
+  else CYC_TILES_GRAD(5, false);
 #undef CYC_TILES_GRAD
   CYC_LAUNCH_CHECK("k_tiles_grad");
   return CYC_OK;

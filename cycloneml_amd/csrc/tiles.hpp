@@ -34,14 +34,19 @@ struct TilesView {
 
 int tiles_view(cyc_tiles t, TilesView* v);
 
-// Margin pass: mult[r] = the per-row multiplier of aggregator `kind`
-// (binary_rows.hpp) from margin = row_margin(offset + dot_r); per-workgroup
-// (loss, weight, multiplierSum, sigmaGradSum) partials to slabS[wg * 4 + k].
-// Returns the number of workgroups (slabS rows) through *wgs.
-int tiles_margin(const TilesView& v, const double* labels, const double* weights,
-                 const double* coef, int fitIntercept, int kind, double offset, double lscale,
-                 double sigma, double eps, double* mult, double* slabS, int64_t* wgs,
-                 hipStream_t st);
+// Margin pass: dots[r] = row r's dot with coef over its nonzeros, in
+// column order.
+int tiles_margin(const TilesView& v, const double* coef, double* dots, hipStream_t st);
+
+// The rows' epilogue after it: dm[r] (the dot) becomes the per-row
+// multiplier of aggregator `kind` (binary_rows.hpp) from margin =
+// row_margin(offset + dot); per-workgroup (loss, weight, multiplierSum,
+// sigmaGradSum) partials to slabS[wg * 4 + k], the workgroup count through
+// *wgs (at most tiles_rows_blocks(n)).
+int64_t tiles_rows_blocks(int64_t n);
+int tiles_rows(int64_t n, const double* labels, const double* weights, int fitIntercept,
+               int kind, double offset, double lscale, double sigma, double eps, double* dm,
+               double* slabS, int64_t* wgs, hipStream_t st);
 
 // Gradient pass: slabG[range * F + f] = sum over the rows of row range
 // `range` (row order) of vals * mult[row]; *ranges receives the range count.

@@ -108,15 +108,28 @@ MAX_CLUSTERS = 8192
 
 
 def dense_cluster_ids(pred):
-    """(ids in 0..K-1, K): every rank's distinct integer predictions, sorted
-    and numbered, and this shard's predictions mapped onto them."""
+    """(ids in 0..K-1, K): every rank's distinct predictions, sorted and
+    numbered, and this shard's predictions mapped onto them.  The reference
+    casts the prediction column to double and keys the cluster statistics
+    by that value (ClusteringMetrics.scala), so distinct doubles -- 0.5 and
+    0.7 too -- stay distinct clusters.  Each rank checks its own distinct
+    count against MAX_CLUSTERS before anything is gathered (every rank
+    raises together through parallel.agree)."""
     torch = _torch()
-    p = pred.to(torch.int64).reshape(-1)
-    mine = torch.unique(p).cpu().tolist()
+    p = pred.to(torch.float64).reshape(-1)
+    local = torch.unique(p)
+
+    def bound():
+        if local.numel() > MAX_CLUSTERS:
+            raise N.IllegalArgumentException(
+                f"requirement failed: the device Silhouette supports at most {MAX_CLUSTERS} "
+                f"clusters, got at least {local.numel()}")
+    parallel.agree(bound)
+    mine = local.cpu().tolist()
     keys = sorted(set().union(*[set(g) for g in parallel.allgather_object(mine)]))
     if not keys:
-        return p.to(torch.int32), 1
-    kt = torch.tensor(keys, dtype=torch.int64, device=p.device)
+        return torch.zeros(p.numel(), dtype=torch.int32, device=p.device), 1
+    kt = torch.tensor(keys, dtype=torch.float64, device=p.device)
     return torch.searchsorted(kt, p).to(torch.int32).contiguous(), len(keys)
 
 

@@ -135,7 +135,7 @@ def init(device=None, communicator=Communicator):
         uid.copy_(torch.frombuffer(bytearray(communicator.unique_id()), dtype=torch.uint8))
     d.broadcast(uid, 0)
     _comm = communicator(bytes(uid.cpu().numpy().tobytes()), d.get_rank(), d.get_world_size(),
-                         dev.index or 0)
+                         dev.index if dev.index is not None else torch.cuda.current_device())
     return _comm
 
 

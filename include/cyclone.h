@@ -443,8 +443,10 @@ int cyc_multinomial_logistic_add_csr_dev(cyc_logistic_plan plan, const int64_t* 
                                          cyc_csc csc, void* stream);
 /* out[i] = the exponential the dense multinomial margins kernel applies to
  * the softmax terms m - max (Utils.softmax's math.exp, ml/impl/Utils.scala:
- * 127-129): e^x for x <= 0 within a few ulp of libm, 0 below -708, NaN kept
- * (inputs above 0 are outside its contract).  Exported so its accuracy is
+ * 127-129): e^x for x <= 0 within a few ulp of libm down to -708.4;
+ * subnormal results in (-746, -708.4] (about 1e-13 relative error there);
+ * 0 below -746 and at -inf; NaN kept (inputs above 0 are outside its
+ * contract).  Exported so its accuracy is
  * testable against the host libm. */
 int cyc_softmax_exp_dev(const double* x, int64_t n, double* out, void* stream);
 
