@@ -605,7 +605,9 @@ class LRSparseWorkload:
                                          RDDLossFunction, SparseTiles)
         self.n, self.F, self.k = n, 1_000_000, 64
         F, k = self.F, self.k
-        self.tiles = SparseTiles(F, n, n * k)
+        # the layout's entry format: "auto" (compact for these rows' density),
+        # CYC_TILES_FORMAT=wide|compact forces one
+        self.tiles = SparseTiles(F, n, n * k, format=os.environ.get("CYC_TILES_FORMAT", "auto"))
         y = torch.empty(n, dtype=torch.float64, device=dev)
         self.sample = []                            # host copy of the first rows (CPU leg)
         sample_rows = min(n, 4 * LR_SPARSE_CHUNK)
@@ -638,7 +640,8 @@ class LRSparseWorkload:
         return self.n * (self.k * 12 + 8 + 8) / launches_per_step, HBM   # bytes
 
     def extra_roofline(self, launches_per_step, avg_s):
-        return {"layout_bytes": self.tiles.nbytes,
+        return {"layout_bytes": self.tiles.nbytes, "layout_format": self.tiles.format,
+                "layout_entries": self.tiles.entries, "nonzeros": self.tiles.nnz,
                 "note": "784 B/row = one fused pass (SURVEY 8d); the evaluation reads the "
                         "layout twice (margin pass, then gradient pass), 12 B per nonzero each"}
 

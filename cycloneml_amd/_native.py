@@ -141,6 +141,9 @@ SIGNATURES = {
     "cyc_csc_features": (_i32, [_vp]),
     "cyc_tiles_create": (ctypes.c_int, [_i32, _i64, _i64, ctypes.POINTER(_vp)]),
     "cyc_tiles_append_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp]),
+    "cyc_tiles_set_format": (ctypes.c_int, [_vp, _i32]),
+    "cyc_tiles_format": (_i32, [_vp]),
+    "cyc_tiles_entries": (_i64, [_vp]),
     "cyc_tiles_destroy": (ctypes.c_int, [_vp]),
     "cyc_tiles_rows": (_i64, [_vp]),
     "cyc_tiles_nnz": (_i64, [_vp]),

@@ -48,6 +48,7 @@
 #include <string>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
 #include "binary_rows.hpp"
@@ -57,10 +58,15 @@
 struct cyc_tiles_s {
   int F = 0, T = 1, Wt = 1;
   int64_t capRows = 0, capNnz = 0, n = 0, nnz = 0;
+  // entry format: CYC_TILES_AUTO until the first append decides,
+  // CYC_TILES_WIDE (32-bit packed ids) or CYC_TILES_COMPACT (16-bit ids:
+  // column + row delta, with filler entries); entries = positions used
+  int fmt = CYC_TILES_AUTO;
+  int64_t capEntries = 0, entries = 0;
   bool sealed = false;    // ends with a partial row block: no further appends
-  int64_t maxSeg = 0;     // nonzeros of the longest segment (picks the pass instances)
+  int64_t maxSeg = 0;     // entries of the longest segment (picks the pass instances)
   std::mutex mu;
-  cyc::DeviceBuffer segStart, idx, vals, maxDev;
+  cyc::DeviceBuffer segStart, idx, vals, maxDev, scal;
 };
 
 namespace {
@@ -76,12 +82,30 @@ constexpr int kGPT = kTileSuperCols / kTPB;    // gradient sums per thread
 
 // columns per chunk: an eighth of F (so a gradient workgroup's 8 waves all
 // have a chunk when F is small), a multiple of 64, at most kTileCols
+// ... and at most kTileCols - 2 = 2046: column 2047 is the compact format's
+// filler code, and 2046 keeps a chunk's coefficients 16-byte aligned
+// (2046 x 8 = 16 x 1023) for the loader's DMA.
 int chunk_cols(int F) {
-  const int w = (int)std::min<int64_t>(kTileCols, ((int64_t)F + 8 * 64 - 1) / (8 * 64) * 64);
+  const int w = (int)std::min<int64_t>(kTileCols - 2, ((int64_t)F + 8 * 64 - 1) / (8 * 64) * 64);
   return std::max(w, 64);
 }
 
 // ----------------------------------------------------------------- build
+
+// Fix the entry format and reserve the entry arrays: the wide format
+// capNnz entries of 4 + 8 bytes; the compact one capNnz + capNnz / 16 +
+// 65536 entries of 2 + 8 bytes (a 6.25 % allowance for filler entries; an
+// append that would need more fails with a message naming the wide format).
+int set_storage(cyc_tiles t, int fmt) {
+  t->fmt = fmt;
+  const int64_t cap = std::max<int64_t>(t->capNnz, 1);
+  t->capEntries = fmt == CYC_TILES_COMPACT ? cap + cap / 16 + 65536 : cap;
+  int rc;
+  if ((rc = t->idx.reserve((fmt == CYC_TILES_COMPACT ? 2 : 4) * (size_t)t->capEntries)) ||
+      (rc = t->vals.reserve(sizeof(double) * (size_t)t->capEntries)))
+    return rc;
+  return CYC_OK;
+}
 
 // Per nonzero of rows [0, rows) of a chunk: its segment key rb * T + c and
 // its packed ids.  Wave per row.
@@ -114,15 +138,83 @@ __global__ void k_tile_gather(const uint32_t* __restrict__ perm, int64_t cnt,
   }
 }
 
-// segStart[seg0 + key] = base + first sorted position with key' >= key,
-// key in [0, nkeys)
+// The compact entry (CYC_TILES_COMPACT): 16 bits -- the row's low 5 bits
+// (row in block mod 32) and the column in the chunk (11 bits; column 2047,
+// never a chunk's since chunks hold at most 2046, marks a filler entry: no
+// nonzero, value 0.0).  Entries of a segment are in CSR order, so rows never
+// decrease; a row that is 32 or more past the previous entry's (row 0 for
+// the first) gets fillers at every 31 rows in front of it, so each step is
+// below 32 and a row's high part is the number of times the low part went
+// down so far -- a ballot + mbcnt per wave instruction in the passes, no
+// prefix sum.  10 bytes per entry instead of 12; at config 5's density
+// (268 nonzeros per segment, rows ~7.6 apart) ~1 % of the entries are
+// fillers.
+constexpr uint32_t kStep = 31;          // filler spacing (largest step without one)
+constexpr int kColBits = 11;
+constexpr uint32_t kFillCol = (1u << kColBits) - 1;
+
+// fillers in front of an entry whose row is d past the previous one
+__device__ __forceinline__ uint32_t fillers(uint32_t d) { return d == 0 ? 0 : (d - 1) / kStep; }
+
+__device__ __forceinline__ uint32_t prev_row(const uint32_t* __restrict__ keysOut,
+                                             const uint32_t* __restrict__ perm,
+                                             const uint32_t* __restrict__ packed, int64_t q) {
+  return (q > 0 && keysOut[q - 1] == keysOut[q]) ? packed[perm[q - 1]] >> 16 : 0u;
+}
+
+// entries per sorted position q: the fillers its row step needs + itself
+__global__ void k_tile_fill_counts(const uint32_t* __restrict__ keysOut,
+                                   const uint32_t* __restrict__ perm,
+                                   const uint32_t* __restrict__ packed, int64_t cnt,
+                                   uint32_t* __restrict__ counts) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < cnt;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t row = packed[perm[q]] >> 16;
+    counts[q] = 1 + fillers(row - prev_row(keysOut, perm, packed, q));
+  }
+}
+
+__global__ void k_tile_total(const uint32_t* __restrict__ counts,
+                             const unsigned long long* __restrict__ pos, int64_t cnt,
+                             int64_t* __restrict__ out) {
+  out[0] = cnt > 0 ? (int64_t)(pos[cnt - 1] + counts[cnt - 1]) : 0;
+}
+
+// position q's fillers and entry at pos[q] (sub-chunk relative)
+__global__ void k_tile_compact(const uint32_t* __restrict__ keysOut,
+                               const uint32_t* __restrict__ perm,
+                               const uint32_t* __restrict__ packed,
+                               const double* __restrict__ vals, int64_t cnt,
+                               const unsigned long long* __restrict__ pos,
+                               uint16_t* __restrict__ outIdx, double* __restrict__ outVals) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < cnt;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t p = perm[q], pk = packed[p];
+    const uint32_t row = pk >> 16, prev = prev_row(keysOut, perm, packed, q);
+    const uint32_t f = fillers(row - prev);
+    const int64_t o = (int64_t)pos[q];
+    for (uint32_t i = 0; i < f; ++i) {
+      outIdx[o + i] = (uint16_t)((((prev + kStep * (i + 1)) & 31u) << kColBits) | kFillCol);
+      outVals[o + i] = 0.0;
+    }
+    outIdx[o + f] = (uint16_t)(((row & 31u) << kColBits) | (pk & 0xffff));
+    outVals[o + f] = vals[p];
+  }
+}
+
+// segStart[seg0 + key] = base + the entry position of the first sorted
+// position q with key' >= key (q itself for the wide format, pos[q] for the
+// compact one, total past the end), key in [0, nkeys)
 __global__ void k_tile_starts(const uint32_t* __restrict__ keys, int64_t cnt, int64_t nkeys,
-                              int64_t seg0, int64_t base, int64_t* __restrict__ segStart) {
+                              int64_t seg0, int64_t base,
+                              const unsigned long long* __restrict__ pos, int64_t total,
+                              int64_t* __restrict__ segStart) {
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= cnt;
        q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t prev = q == 0 ? -1 : (int64_t)keys[q - 1];
     const int64_t cur = q == cnt ? nkeys : (int64_t)keys[q];
-    for (int64_t k = prev + 1; k <= cur && k < nkeys; ++k) segStart[seg0 + k] = base + q;
+    const int64_t at = pos == nullptr ? q : (q == cnt ? total : (int64_t)pos[q]);
+    for (int64_t k = prev + 1; k <= cur && k < nkeys; ++k) segStart[seg0 + k] = base + at;
   }
 }
 
@@ -147,16 +239,20 @@ __global__ void k_seg_max(const int64_t* __restrict__ segStart, int64_t s0, int6
 // place of the LDS atomic adds, 2 = no LDS gathers of coefficients /
 // multipliers, 8 = no staging of the chunk / slice (the loader wave idles),
 // 16 = no run loads (synthetic ids and values), 32 = no segment offset
-// loads (every run 256 long), 64 = ids loaded as 2 bytes each (the bytes of
-// a 16-bit index; ids synthesized from them), 128 = the margin epilogue
-// stores the dots (no logistic arithmetic).  0 in the library.
+// loads (every run 256 long).  0 in the library.
 #ifndef CYC_TILES_PROBE
 #define CYC_TILES_PROBE 0
 #endif
 
-__device__ __forceinline__ void lds_add(double* p, double x) {
+// LDS pointers are kept in address space 3 from the __shared__ array on
+// (the cast of the array folds): derived through generic pointers, the
+// compiler emitted an is-shared check for the DMA's LDS address that
+// gfx950's instruction selection rejects (src_shared_base in a VALU compare)
+using lds_f64 = __attribute__((address_space(3))) double;
+
+__device__ __forceinline__ void lds_add(lds_f64* p, double x) {
   if constexpr ((CYC_TILES_PROBE & 1) != 0) *p = x;
-  else __hip_atomic_fetch_add(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else __builtin_amdgcn_ds_atomic_fadd_f64(p, x);
 }
 
 // s_waitcnt immediate for "at most n vector memory operations outstanding"
@@ -234,29 +330,31 @@ __device__ __forceinline__ Run seg_run(const int64_t* __restrict__ segStart, int
   return Run{segStart[q], segStart[q + 1], on};
 }
 
-// the first KC x 64 nonzeros of a run from `from` on, lane-strided; lanes
-// past the end read 0 (buffer range check)
-template <int KC>
+// the first KC x 64 entries of a run from `from` on, lane-strided; lanes
+// past the end read 0 (buffer range check).  CPT: 16-bit compact ids
+// (zero-extended), else the 32-bit packed ones.
+template <int KC, bool CPT>
 __device__ __forceinline__ void load_run(const uint32_t* __restrict__ vidx,
                                          const double* __restrict__ vvals, const Run& r,
                                          int64_t from, int lane, uint32_t (&ix)[KC],
                                          double (&vx)[KC]) {
   const int64_t len = r.len() - from;
-  if constexpr ((CYC_TILES_PROBE & 16) != 0) {
+  if constexpr ((CYC_TILES_PROBE & 16) != 0) {   // in-range ids of both formats
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
-      ix[j] = ((uint32_t)(lane * 31 + j * 7) & 2047) << 16 | ((uint32_t)(lane * 29 + j) & 1023);
+      ix[j] = CPT ? ((uint32_t)(lane * 29 + j) & 1023)
+                  : ((uint32_t)(lane * 31 + j * 7) & 2047) << 16 | ((uint32_t)(lane * 29 + j) & 1023);
       vx[j] = 1.0 + j;
     }
     return;
   }
   const auto rv = rsrc(vvals + r.a + from, len > 0 ? len * 8 : 0);
-  if constexpr ((CYC_TILES_PROBE & 64) != 0) {   // 2-byte ids: the bytes of a 16-bit index
-    const auto rh = rsrc(vidx + r.a + from, len > 0 ? len * 2 : 0);
+  if constexpr (CPT) {
+    const auto rh = rsrc(reinterpret_cast<const uint16_t*>(vidx) + r.a + from,
+                         len > 0 ? len * 2 : 0);
 #pragma unroll
     for (int j = 0; j < KC; ++j) {
-      const uint32_t h = __builtin_amdgcn_raw_buffer_load_b16(rh, lane * 2, j * 128, 2);
-      ix[j] = (h & 2047) << 16 | (h & 2047);
+      ix[j] = __builtin_amdgcn_raw_buffer_load_b16(rh, lane * 2, j * 128, 2);
       vx[j] = __builtin_bit_cast(double,
                                  __builtin_amdgcn_raw_buffer_load_b64(rv, lane * 8, j * 512, 2));
     }
@@ -269,6 +367,40 @@ __device__ __forceinline__ void load_run(const uint32_t* __restrict__ vidx,
     ix[j] = __builtin_amdgcn_raw_buffer_load_b32(ri, lane * 4, j * 256, 2);
     vx[j] = __builtin_bit_cast(double,
                                __builtin_amdgcn_raw_buffer_load_b64(rv, lane * 8, j * 512, 2));
+  }
+}
+
+// The (row in block, column in chunk) of a slot's entries and whether each
+// is a nonzero.  Compact: low = row mod 32; each lane compares its low with
+// the previous entry's (the lane below, by DPP wave_shr:1; lane 0 the last
+// entry of the slot before, `lowc`), a drop means the row passed a multiple
+// of 32, and the row's high part is `highc` (the drops of the run's earlier
+// slots) + the drops in the lanes up to this one (ballot + mbcnt).  Lanes
+// past the run's end read 0; they only come after its last entry.
+template <int KC, bool CPT>
+__device__ __forceinline__ void decode(const uint32_t (&ix)[KC], uint32_t& highc,
+                                       uint32_t& lowc, uint32_t (&row)[KC],
+                                       uint32_t (&col)[KC], bool (&real)[KC]) {
+#pragma unroll
+  for (int j = 0; j < KC; ++j) {
+    if constexpr (CPT) {
+      const uint32_t low = ix[j] >> kColBits;
+      const uint32_t prev =
+          (uint32_t)__builtin_amdgcn_update_dpp((int)lowc, (int)low, 0x138, 0xf, 0xf, false);
+      const bool drop = low < prev;
+      const uint64_t m = __ballot(drop);
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      row[j] = ((highc + below + (drop ? 1u : 0u)) << 5) | low;
+      highc += (uint32_t)__builtin_popcountll(m);
+      lowc = (uint32_t)__builtin_amdgcn_readlane((int)low, 63);
+      col[j] = ix[j] & kFillCol;
+      real[j] = col[j] != kFillCol;
+    } else {
+      row[j] = ix[j] >> 16;
+      col[j] = ix[j] & 0xffff;
+      real[j] = true;
+    }
   }
 }
 
@@ -296,7 +428,7 @@ constexpr int kTPBL = 64 * (kTileWaves + 1);
 // barrier.  (Staging through the loader's registers two steps ahead, the
 // slice written by ds_write, measured slower: 36.8 / 33.9 against 30.8 /
 // 30.1 ms per margin / gradient pass at 200M rows.)
-__device__ __forceinline__ int dma_slice(const double* src, int64_t count, double* b, int lane) {
+__device__ __forceinline__ int dma_slice(const double* src, int64_t count, lds_f64* b, int lane) {
   const auto rs = rsrc(src, count * 8);
   if constexpr ((CYC_TILES_PROBE & 8) != 0) return 0;
   if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
@@ -313,7 +445,7 @@ __device__ __forceinline__ int dma_slice(const double* src, int64_t count, doubl
         rs, (__attribute__((address_space(3))) void*)(b + i * 32), 4, i * 256 + lane * 4, 0, 0, 0);
   return 64;
 }
-__device__ __forceinline__ void stage_slice(const double* src, int64_t count, double* b,
+__device__ __forceinline__ void stage_slice(const double* src, int64_t count, lds_f64* b,
                                             int lane) {
   dma_slice(src, count, b, lane);
   __builtin_amdgcn_s_waitcnt(vm_wait(0));
@@ -337,29 +469,40 @@ static_assert(kTileCols == 16 * 128 && kTileRows == 16 * 128, "16 one-KiB pieces
 // go to dotOut (the rows' epilogue is k_tiles_rows: in here each batch of
 // rows waited on a fresh label load from HBM while the CU streamed nothing,
 // ~2 ms of a 30 ms pass at 200M rows).
-constexpr int kMW = 7;                          // compute waves (row blocks) per margin workgroup
+// chunk buffers of the margin pass: 2 (8 row blocks per super block, the
+// DMA lands within the step it is issued in) or 3 (7 row blocks, each DMA a
+// step of lead) -- an A/B switch: with the compact entries and branch-free
+// adds, 25.7 (2) against 27.7 (3) ms per margin pass at 200M rows (9 % more
+// steps with 7 row blocks; before those two changes 3 buffers had won)
+#ifndef CYC_TILES_MARGIN_BUFS
+#define CYC_TILES_MARGIN_BUFS 2
+#endif
+constexpr int kMBufs = CYC_TILES_MARGIN_BUFS;
+constexpr int kMW = kMBufs == 3 ? 7 : 8;        // compute waves (row blocks) per margin workgroup
 constexpr int kMTPB = 64 * (kMW + 1);          // + the loader wave
 constexpr int kMRows = kMW * kTileRows;         // rows per margin super block
 
-template <int NB, int KC, bool LONG>
+template <int NB, int KC, bool LONG, bool CPT>
 __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
     TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
     const double* __restrict__ vvals, const double* __restrict__ coef,
     double* __restrict__ dotOut) {
   static_assert(NB >= 2, "at least one run in flight");
-  static_assert(kMRows * 8 + 3 * kTileCols * 8 <= 160 * 1024, "LDS");
-  __shared__ double lds[kMRows + 3 * kTileCols];
-  double* const dots = lds;
-  double* const cf = lds + kMRows;
+  static_assert(kMRows * 8 + kMBufs * kTileCols * 8 <= 160 * 1024, "LDS");
+  __shared__ double lds[kMRows + kMBufs * kTileCols];
+  lds_f64* const dots = (lds_f64*)lds;
+  lds_f64* const cf = dots + kMRows;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int T = v.T;
   const int64_t nSB = (v.nRB + kMW - 1) / kMW;
   const int Tp = (T + NB - 1) / NB * NB;
   const int64_t mySB = nSB > blockIdx.x ? (nSB - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  // buffer of flat step g: g % 3 (the flat step count fits 32 bits: Tp *
-  // super blocks per workgroup is the launch's per-workgroup step count)
-  auto bufOf = [&](int64_t k, int c) { return cf + ((uint32_t)(k * Tp + c) % 3u) * kTileCols; };
+  // buffer of flat step g: g % kMBufs (the flat step count fits 32 bits:
+  // Tp * super blocks per workgroup is the launch's per-workgroup steps)
+  auto bufOf = [&](int64_t k, int c) {
+    return cf + ((uint32_t)(k * Tp + c) % (uint32_t)kMBufs) * kTileCols;
+  };
 
   if (wave == kMW) {
     // the loader: the same barriers as the compute waves, in the same order
@@ -376,19 +519,23 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
     int c2 = 0;
     chunk(k2, c2);                                // step 0
     next(k2, c2);
-    const int n1 = chunk(k2, c2);                 // step 1
-    next(k2, c2);
-    if (n1 == 16) __builtin_amdgcn_s_waitcnt(vm_wait(16));     // step 0's landed
-    else __builtin_amdgcn_s_waitcnt(vm_wait(0));
+    if constexpr (kMBufs == 3) {
+      const int n1 = chunk(k2, c2);               // step 1
+      next(k2, c2);
+      if (n1 == 16) __builtin_amdgcn_s_waitcnt(vm_wait(16));   // step 0's landed
+      else __builtin_amdgcn_s_waitcnt(vm_wait(0));
+    } else {
+      __builtin_amdgcn_s_waitcnt(vm_wait(0));
+    }
     for (int64_t k = 0; k < mySB; ++k) {
       __syncthreads();                            // dots zeroed, chunk (k, 0) in place
       for (int c = 0; c < Tp; ++c) {
-        // the chunk two steps ahead (k2, c2) into the buffer the last
-        // barrier freed; then the chunk of the next step (issued a step
-        // ago) landed: only the DMA just issued may stay in flight
+        // the chunk kMBufs - 1 steps ahead (k2, c2) into the buffer the last
+        // barrier freed; then the chunk of the next step landed (3 buffers:
+        // issued a step ago, only the DMA just issued may stay in flight)
         const int n2 = chunk(k2, c2);
         next(k2, c2);
-        if (n2 == 16) __builtin_amdgcn_s_waitcnt(vm_wait(16));
+        if (kMBufs == 3 && n2 == 16) __builtin_amdgcn_s_waitcnt(vm_wait(16));
         else __builtin_amdgcn_s_waitcnt(vm_wait(0));
         step_sync<CYC_TILES_MARGIN_SYNC>();       // step (k, c)
       }
@@ -412,22 +559,34 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
     const int64_t rb = ((int64_t)blockIdx.x + k * gridDim.x) * kMW + wave;
     return seg_run(segStart, rb * T + c, k < mySB && c < T && rb < v.nRB);
   };
-  double* myDots = dots + wave * kTileRows;
+  lds_f64* const myDots = dots + wave * kTileRows;
   // waits for the whole run first, on every path: its values are used only
   // under the lanes' `< len` branches, and a path that skips one left the
   // compiler's wait analysis treating the registers as still loading at the
   // loop head, where it then drained every prefetched run (vmcnt(0)); the
   // runs of the next NB - 2 steps stay in flight
-  auto consume = [&](int64_t len, const double* cfp, const uint32_t (&ix)[KC],
-                     const double (&vx)[KC]) {
+  // The adds are branch-free: a lane past the run's end or on a filler adds
+  // +0.0 to the wave's own dot [lane] -- an exact no-op, since a sum that
+  // starts at +0.0 is never -0.0 (x + +0.0 == x for every other x, NaN and
+  // infinities included) -- so the compiler issues the step's gathers, ONE
+  // wait, then every atomic (behind an exec-mask branch each atomic waited
+  // lgkmcnt(0), i.e. for the atomic before it; one shared dummy address
+  // serialised the masked lanes).
+  auto consume = [&](int64_t len, lds_f64* cfp, const uint32_t (&ix)[KC],
+                     const double (&vx)[KC], uint32_t& highc, uint32_t& lowc) {
     __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2 + !CYC_TILES_LATE_LOADS) * 2 * KC));
+    uint32_t row[KC], col[KC];
+    bool real[KC];
+    decode<KC, CPT>(ix, highc, lowc, row, col, real);
     double c[KC];
 #pragma unroll
     for (int j = 0; j < KC; ++j)   // lanes past the end read [0]
-      c[j] = (CYC_TILES_PROBE & 2) ? vx[j] : cfp[ix[j] & 0xffff];
+      c[j] = (CYC_TILES_PROBE & 2) ? vx[j] : cfp[col[j]];
 #pragma unroll
-    for (int j = 0; j < KC; ++j)
-      if (j * 64 + lane < len) lds_add(&myDots[ix[j] >> 16], vx[j] * c[j]);
+    for (int j = 0; j < KC; ++j) {
+      const bool on = j * 64 + lane < len && real[j];
+      lds_add(&myDots[on ? row[j] : (uint32_t)lane], on ? vx[j] * c[j] : 0.0);
+    }
   };
   // One step (k, c), ONE barrier: the current run into the row sums with
   // chunk (k, c) in cf[g % 3], then the loads of the run NB - 1 steps ahead
@@ -443,12 +602,13 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
   auto step = [&](int64_t k, int c, Run& rc, uint32_t (&ic)[KC], double (&vc)[KC],
                   const Run& rn, uint32_t (&in)[KC], double (&vn)[KC]) {
     const Run cur = rc;
-    const double* buf = bufOf(k, c);
+    lds_f64* buf = bufOf(k, c);
     if constexpr (!CYC_TILES_LATE_LOADS) {
-      load_run(vidx, vvals, rn, 0, lane, in, vn);
+      load_run<KC, CPT>(vidx, vvals, rn, 0, lane, in, vn);
       CYC_TILES_SCHED_BARRIER();                  // the loads issue first
     }
-    consume(cur.len(), buf, ic, vc);
+    uint32_t highc = 0, lowc = 0;               // the run's row before each slot
+    consume(cur.len(), buf, ic, vc, highc, lowc);
     // a run longer than KC x 64: only in the LONG instance (a layout with
     // such segments), in registers of its own -- any load in this loop's
     // body makes the compiler's wait analysis drain every prefetched run
@@ -457,11 +617,11 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
       for (int64_t b = KC * 64; b < cur.len(); b += KC * 64) {
         uint32_t it[KC];
         double vt[KC];
-        load_run(vidx, vvals, cur, b, lane, it, vt);
-        consume(cur.len() - b, buf, it, vt);
+        load_run<KC, CPT>(vidx, vvals, cur, b, lane, it, vt);
+        consume(cur.len() - b, buf, it, vt, highc, lowc);
       }
     }
-    if constexpr (CYC_TILES_LATE_LOADS) load_run(vidx, vvals, rn, 0, lane, in, vn);
+    if constexpr (CYC_TILES_LATE_LOADS) load_run<KC, CPT>(vidx, vvals, rn, 0, lane, in, vn);
     CYC_TILES_SCHED_BARRIER();
     int64_t k2;
     int c2;
@@ -480,7 +640,7 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
     rr[u] = run_of(k1, c1);
   }
 #pragma unroll
-  for (int u = 0; u < NB - 1; ++u) load_run(vidx, vvals, rr[u], 0, lane, ib[u], vb[u]);
+  for (int u = 0; u < NB - 1; ++u) load_run<KC, CPT>(vidx, vvals, rr[u], 0, lane, ib[u], vb[u]);
   constexpr int kCT = 64 * kMW;                  // compute threads
   static_assert(kMRows % kCT == 0, "whole dots per thread");
   for (int64_t k = 0; k < mySB; ++k) {          // one super block per pass
@@ -513,6 +673,9 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
 // sigmaGradSum) partials to slabS[wg * 4 + k] -- each thread's rows in row
 // order, a fixed shuffle tree per wave, the waves in order.  Streams 24 B
 // per row (dot, label, multiplier; + 8 with weights).
+#ifndef CYC_TILES_ROWS_U
+#define CYC_TILES_ROWS_U 2
+#endif
 __global__ __launch_bounds__(256) void k_tiles_rows(
     int64_t n, const double* __restrict__ labels, const double* __restrict__ weights,
     int fitIntercept, int kind, double offset, double lscale, double sigma, double eps,
@@ -521,40 +684,58 @@ __global__ __launch_bounds__(256) void k_tiles_rows(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};     // loss, weight, multiplierSum, sigmaGradSum
   const int64_t stride = (int64_t)gridDim.x * 256;
-  constexpr int U = 4;
-  for (int64_t r0 = (int64_t)blockIdx.x * 256 + tid; r0 < n; r0 += U * stride) {
+  // U rows per batch, two batches in registers: the next batch's loads are
+  // in flight while this one's rows are computed (software-pipelined)
+  constexpr int U = CYC_TILES_ROWS_U;
+  struct Batch {
     double dot[U], lab[U], w[U];
+  };
+  auto ld = [&](int64_t r0, Batch& b) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t r = min<int64_t>(r0 + u * stride, n - 1);
-      dot[u] = __builtin_nontemporal_load(&dm[r]);
-      lab[u] = __builtin_nontemporal_load(&labels[r]);
-      w[u] = weights ? __builtin_nontemporal_load(&weights[r]) : 1.0;
+      b.dot[u] = __builtin_nontemporal_load(&dm[r]);
+      b.lab[u] = __builtin_nontemporal_load(&labels[r]);
+      b.w[u] = weights ? __builtin_nontemporal_load(&weights[r]) : 1.0;
     }
+  };
+  auto rows = [&](int64_t r0, const Batch& b) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t r = r0 + u * stride;
       if (r >= n) break;
       double m;
       if (kind == 0) {
-        const double margin = fitIntercept ? offset + dot[u] : dot[u];
+        const double margin = fitIntercept ? offset + b.dot[u] : b.dot[u];
         const double x = -margin;
         const double lp = __builtin_fmax(x, 0.0) + log1p(exp(-__builtin_fabs(x)));
-        const double term = lab[u] > 0 ? lp : lp + margin;
-        const double mm = w[u] * (1.0 / (1.0 + exp(-margin)) - lab[u]);
-        acc[1] += w[u];
+        const double term = b.lab[u] > 0 ? lp : lp + margin;
+        const double mm = b.w[u] * (1.0 / (1.0 + exp(-margin)) - b.lab[u]);
+        acc[1] += b.w[u];
         m = 0.0;
-        if (w[u] > 0) {
-          acc[0] += w[u] * term;
+        if (b.w[u] > 0) {
+          acc[0] += b.w[u] * term;
           m = mm;
         }
       } else {
-        const double margin = cyc::row_margin(kind, fitIntercept, offset, lscale, lab[u], dot[u]);
-        m = cyc::bin_row(kind, margin, w[u], lab[u], acc[0], acc[1], acc[3], sigma, eps);
+        const double margin =
+            cyc::row_margin(kind, fitIntercept, offset, lscale, b.lab[u], b.dot[u]);
+        m = cyc::bin_row(kind, margin, b.w[u], b.lab[u], acc[0], acc[1], acc[3], sigma, eps);
       }
       acc[2] += m;
       __builtin_nontemporal_store(m, &dm[r]);
     }
+  };
+  const int64_t first = (int64_t)blockIdx.x * 256 + tid;
+  Batch ba, bb;
+  if (first < n) ld(first, ba);
+#pragma unroll 1
+  for (int64_t r0 = first; r0 < n; r0 += 2 * U * stride) {
+    const int64_t r1 = r0 + U * stride, r2 = r1 + U * stride;
+    if (r1 < n) ld(r1, bb);
+    rows(r0, ba);
+    if (r2 < n) ld(r2, ba);
+    if (r1 < n) rows(r1, bb);
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -573,8 +754,15 @@ __global__ __launch_bounds__(256) void k_tiles_rows(
 // over its row blocks.  Per row block: compute wave j walks segment
 // (rb, 8 st + j) into its chunk's column sums with the multiplier slice of
 // rb in mv[(rb - rbA) & 1] (ONE barrier), the runs of the next NB - 1 row
-// blocks in flight; the loader stages the next row block's slice.
-template <int NB, int KC, bool LONG>
+// blocks in flight; the loader stages the next row block's slice.  Block b
+// is (st = b / R, range = b % R): the blocks of one XCD (b mod 8) walk the
+// same row ranges together, so a row block's multiplier slice is read from
+// the XCD's L2 by all but the first.  (A flat split of the sts * nRB units
+// over exactly one workgroup per CU -- config 5's 62 super chunks x 4
+// ranges leave 8 of 256 CUs idle -- took 29.7 against 24.6 ms: its
+// workgroups on an XCD walked different rows and every slice came from
+// HBM.)
+template <int NB, int KC, bool LONG, bool CPT>
 __global__ __launch_bounds__(kTPBL) void k_tiles_grad(
     TileDims v, const int64_t* __restrict__ segStart, const uint32_t* __restrict__ vidx,
     const double* __restrict__ vvals, const double* __restrict__ mult, int ranges,
@@ -582,8 +770,8 @@ __global__ __launch_bounds__(kTPBL) void k_tiles_grad(
   static_assert(NB >= 2, "at least one run in flight");
   // 160 KiB: the 8 chunks' column sums and two multiplier slice buffers
   __shared__ double lds[kTileSuperCols + 2 * kTileRows];
-  double* const gt = lds;
-  double* const mv = lds + kTileSuperCols;
+  lds_f64* const gt = (lds_f64*)lds;
+  lds_f64* const mv = gt + kTileSuperCols;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int range = blockIdx.x % ranges, st = blockIdx.x / ranges;
@@ -604,30 +792,37 @@ __global__ __launch_bounds__(kTPBL) void k_tiles_grad(
     __syncthreads();                              // sums zeroed, slice rbA in place
     for (int64_t s = 0; s < steps; ++s) {
       slice(rbA + s + 1);                         // into the buffer the last barrier freed
-      step_sync<CYC_TILES_GRAD_SYNC>();                                // step rbA + s
+      step_sync<CYC_TILES_GRAD_SYNC>();           // step rbA + s
     }
     __syncthreads();                              // sums complete
     return;
   }
 
-  const int c = st * kTileWaves + wave;                 // this wave's column chunk
+  const int c = st * kTileWaves + wave;           // this wave's column chunk
   uint32_t ib[NB][KC];
   double vb[NB][KC];
   Run rr[NB];
   auto run_of = [&](int64_t rb) { return seg_run(segStart, rb * v.T + c, rb < rbB && c < v.T); };
-  double* myG = gt + wave * v.Wt;
+  lds_f64* const myG = gt + wave * v.Wt;
   // waits for the whole run first, on every path (the margin pass's
-  // consume says why)
-  auto consume = [&](int64_t len, const double* mvp, const uint32_t (&ix)[KC],
-                     const double (&vx)[KC]) {
+  // consume says why); branch-free adds: a masked lane adds +0.0 to the
+  // wave's sum [lane] (the margin pass's consume says why; a chunk holds at
+  // least 64 columns)
+  auto consume = [&](int64_t len, const lds_f64* mvp, const uint32_t (&ix)[KC],
+                     const double (&vx)[KC], uint32_t& highc, uint32_t& lowc) {
     __builtin_amdgcn_s_waitcnt(vm_wait((NB - 2 + !CYC_TILES_LATE_LOADS) * 2 * KC));
+    uint32_t row[KC], col[KC];
+    bool real[KC];
+    decode<KC, CPT>(ix, highc, lowc, row, col, real);
     double m[KC];
 #pragma unroll
     for (int j = 0; j < KC; ++j)   // lanes past the end read [0]
-      m[j] = (CYC_TILES_PROBE & 2) ? vx[j] : mvp[ix[j] >> 16];
+      m[j] = (CYC_TILES_PROBE & 2) ? vx[j] : mvp[row[j]];
 #pragma unroll
-    for (int j = 0; j < KC; ++j)
-      if (j * 64 + lane < len) lds_add(&myG[ix[j] & 0xffff], vx[j] * m[j]);
+    for (int j = 0; j < KC; ++j) {
+      const bool on = j * 64 + lane < len && real[j];
+      lds_add(&myG[on ? col[j] : (uint32_t)lane], on ? vx[j] * m[j] : 0.0);
+    }
   };
 
 #pragma unroll
@@ -641,21 +836,22 @@ __global__ __launch_bounds__(kTPBL) void k_tiles_grad(
   auto step = [&](int64_t rb, Run& rc, uint32_t (&ic)[KC], double (&vc)[KC], const Run& rn,
                   uint32_t (&in)[KC], double (&vn)[KC]) {
     const Run cur = rc;
-    const double* buf = mv + ((rb - rbA) & 1) * kTileRows;
+    const lds_f64* buf = mv + ((rb - rbA) & 1) * kTileRows;
     if constexpr (!CYC_TILES_LATE_LOADS) {
-      load_run(vidx, vvals, rn, 0, lane, in, vn);
+      load_run<KC, CPT>(vidx, vvals, rn, 0, lane, in, vn);
       CYC_TILES_SCHED_BARRIER();                  // the loads issue first
     }
-    consume(cur.len(), buf, ic, vc);
+    uint32_t highc = 0, lowc = 0;                 // the run's row before each slot
+    consume(cur.len(), buf, ic, vc, highc, lowc);
     if constexpr (LONG) {
       for (int64_t b = KC * 64; b < cur.len(); b += KC * 64) {
         uint32_t it[KC];
         double vt[KC];
-        load_run(vidx, vvals, cur, b, lane, it, vt);
-        consume(cur.len() - b, buf, it, vt);
+        load_run<KC, CPT>(vidx, vvals, cur, b, lane, it, vt);
+        consume(cur.len() - b, buf, it, vt, highc, lowc);
       }
     }
-    if constexpr (CYC_TILES_LATE_LOADS) load_run(vidx, vvals, rn, 0, lane, in, vn);
+    if constexpr (CYC_TILES_LATE_LOADS) load_run<KC, CPT>(vidx, vvals, rn, 0, lane, in, vn);
     CYC_TILES_SCHED_BARRIER();                    // after the LDS reads (the margin pass's step)
     rc = run_of(rb + NB);
     step_sync<CYC_TILES_GRAD_SYNC>();
@@ -666,8 +862,8 @@ __global__ __launch_bounds__(kTPBL) void k_tiles_grad(
 #pragma unroll
   for (int u = 0; u < NB; ++u) rr[u] = run_of(rbA + u);
 #pragma unroll
-  for (int u = 0; u < NB - 1; ++u) load_run(vidx, vvals, rr[u], 0, lane, ib[u], vb[u]);
-  __syncthreads();                              // zeroed sums, slice rbA in place
+  for (int u = 0; u < NB - 1; ++u) load_run<KC, CPT>(vidx, vvals, rr[u], 0, lane, ib[u], vb[u]);
+  __syncthreads();                                // zeroed sums, slice rbA in place
   for (int64_t s = 0; s < steps; s += NB) {
 #pragma unroll
     for (int u = 0; u < NB; ++u)
@@ -707,6 +903,7 @@ int tiles_view(cyc_tiles t, TilesView* v) {
   v->idx = (const uint32_t*)t->idx.ptr;
   v->vals = (const double*)t->vals.ptr;
   v->maxSeg = t->maxSeg;
+  v->compact = t->fmt == CYC_TILES_COMPACT;
   return CYC_OK;
 }
 
@@ -714,19 +911,24 @@ int tiles_margin(const TilesView& v, const double* coef, double* dots, hipStream
   const int64_t nSB = (v.nRB + kMW - 1) / kMW;
   const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nSB, device_cus()));
   const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
-#define CYC_TILES_MARGIN(KC, LONG)                                                              \
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_margin<CYC_TILES_NB, KC, LONG>),                   \
+#define CYC_TILES_MARGIN(KC, LONG, CPT)                                                         \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_margin<CYC_TILES_NB, KC, LONG, CPT>),              \
                      dim3((unsigned)grid), dim3(kMTPB), 0, st, d, v.segStart, v.idx, v.vals,    \
                      coef, dots)
-  if (long_runs(v.maxSeg)) CYC_TILES_MARGIN(5, true);
-  else CYC_TILES_MARGIN(5, false);
+  if (v.compact) {
+    if (long_runs(v.maxSeg)) CYC_TILES_MARGIN(5, true, true);
+    else CYC_TILES_MARGIN(5, false, true);
+  } else {
+    if (long_runs(v.maxSeg)) CYC_TILES_MARGIN(5, true, false);
+    else CYC_TILES_MARGIN(5, false, false);
+  }
 #undef CYC_TILES_MARGIN
   CYC_LAUNCH_CHECK("k_tiles_margin");
   return CYC_OK;
 }
 
 int64_t tiles_rows_blocks(int64_t n) {
-  return std::max<int64_t>(1, std::min<int64_t>(4 * device_cus(), (n + 1023) / 1024));
+  return std::max<int64_t>(1, std::min<int64_t>(8 * device_cus(), (n + 1023) / 1024));
 }
 
 int tiles_rows(int64_t n, const double* labels, const double* weights, int fitIntercept,
@@ -752,12 +954,17 @@ int tiles_grad(const TilesView& v, const double* mult, double* slabG, int* range
   *ranges = R;
   const int64_t sts = (v.T + kTileWaves - 1) / kTileWaves;
   const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
-#define CYC_TILES_GRAD(KC, LONG)                                                                \
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_grad<CYC_TILES_NB, KC, LONG>),                     \
+#define CYC_TILES_GRAD(KC, LONG, CPT)                                                           \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_grad<CYC_TILES_NB, KC, LONG, CPT>),                \
                      dim3((unsigned)(sts * R)), dim3(kTPBL), 0, st, d, v.segStart, v.idx, v.vals, \
                      mult, R, slabG)
-  if (long_runs(v.maxSeg)) CYC_TILES_GRAD(5, true);
-  else CYC_TILES_GRAD(5, false);
+  if (v.compact) {
+    if (long_runs(v.maxSeg)) CYC_TILES_GRAD(5, true, true);
+    else CYC_TILES_GRAD(5, false, true);
+  } else {
+    if (long_runs(v.maxSeg)) CYC_TILES_GRAD(5, true, false);
+    else CYC_TILES_GRAD(5, false, false);
+  }
 #undef CYC_TILES_GRAD
   CYC_LAUNCH_CHECK("k_tiles_grad");
   return CYC_OK;
@@ -784,10 +991,9 @@ int cyc_tiles_create(int32_t numFeatures, int64_t capacity_rows, int64_t capacit
   t->capRows = capacity_rows;
   t->capNnz = capacity_nnz;
   const int64_t segs = (capacity_rows + kTileRows - 1) / kTileRows * t->T;
-  int rc;
-  if ((rc = t->segStart.reserve(sizeof(int64_t) * (size_t)(segs + 1))) ||
-      (rc = t->idx.reserve(sizeof(uint32_t) * (size_t)std::max<int64_t>(capacity_nnz, 1))) ||
-      (rc = t->vals.reserve(sizeof(double) * (size_t)std::max<int64_t>(capacity_nnz, 1)))) {
+  // the entry arrays are reserved once the format is known (set_format, or
+  // the first append that holds nonzeros)
+  if (int rc = t->segStart.reserve(sizeof(int64_t) * (size_t)(segs + 1))) {
     delete t;
     return rc;
   }
@@ -795,6 +1001,21 @@ int cyc_tiles_create(int32_t numFeatures, int64_t capacity_rows, int64_t capacit
   *out = t;
   return CYC_OK;
 }
+
+int cyc_tiles_set_format(cyc_tiles t, int32_t format) {
+  CYC_REQUIRE(t != nullptr, "tiles must not be null");
+  CYC_REQUIRE(format == CYC_TILES_AUTO || format == CYC_TILES_WIDE || format == CYC_TILES_COMPACT,
+              "format must be CYC_TILES_AUTO, CYC_TILES_WIDE or CYC_TILES_COMPACT");
+  std::lock_guard<std::mutex> g(t->mu);
+  CYC_REQUIRE(t->n == 0 && t->fmt == CYC_TILES_AUTO,
+              "the entry format is chosen before the first append");
+  if (format != CYC_TILES_AUTO) return set_storage(t, format);
+  return CYC_OK;
+}
+
+int32_t cyc_tiles_format(cyc_tiles t) { return t ? t->fmt : -1; }
+
+int64_t cyc_tiles_entries(cyc_tiles t) { return t ? t->entries : -1; }
 
 int cyc_tiles_destroy(cyc_tiles t) {
   delete t;
@@ -840,7 +1061,7 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
   const int64_t nrbSub = std::max<int64_t>(1, std::min<int64_t>(512, ((int64_t)1 << 24) / T));
   const int64_t chRows = nrbSub * kTileRows;
   const int64_t rb0 = t->n / kTileRows;
-  cyc::DeviceBuffer keys, packed, keysOut, perm, tmp;
+  cyc::DeviceBuffer keys, packed, keysOut, perm, tmp, counts, posb;
   for (int64_t a = 0; a < rows; a += chRows) {
     const int64_t b = std::min(rows, a + chRows);
     int64_t qa = 0, qb = 0;
@@ -854,6 +1075,8 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
     CYC_REQUIRE(cnt < ((int64_t)1 << 32), "a chunk of " + std::to_string(nrbSub) +
                                               " row blocks holds 2^32 nonzeros or more");
     int rc;
+    const unsigned long long* pos = nullptr;    // compact: entry positions
+    int64_t total = cnt;                        // entries of the sub-chunk
     if (cnt > 0) {
       if ((rc = keys.reserve(sizeof(uint32_t) * (size_t)cnt)) ||
           (rc = packed.reserve(sizeof(uint32_t) * (size_t)cnt)) ||
@@ -866,30 +1089,76 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
       unsigned endBit = 1;
       while (endBit < 32 && ((int64_t)1 << endBit) < nkeys) ++endBit;
       size_t tmpBytes = 0;
-      rocprim::counting_iterator<uint32_t> pos(0);
+      rocprim::counting_iterator<uint32_t> cpos(0);
       CYC_HIP(rocprim::radix_sort_pairs(nullptr, tmpBytes, (const uint32_t*)keys.ptr,
-                                        (uint32_t*)nullptr, pos, (uint32_t*)nullptr, (size_t)cnt,
+                                        (uint32_t*)nullptr, cpos, (uint32_t*)nullptr, (size_t)cnt,
                                         0, endBit, st));
       if ((rc = tmp.reserve(tmpBytes))) return rc;
       CYC_HIP(rocprim::radix_sort_pairs(tmp.ptr, tmpBytes, (const uint32_t*)keys.ptr,
-                                        (uint32_t*)keysOut.ptr, pos, (uint32_t*)perm.ptr,
+                                        (uint32_t*)keysOut.ptr, cpos, (uint32_t*)perm.ptr,
                                         (size_t)cnt, 0, endBit, st));
-      hipLaunchKernelGGL(k_tile_gather, dim3(8192), dim3(256), 0, st, (const uint32_t*)perm.ptr,
-                         cnt, (const uint32_t*)packed.ptr, vals + (qa - q0),
-                         (uint32_t*)t->idx.ptr + t->nnz, (double*)t->vals.ptr + t->nnz);
-      CYC_LAUNCH_CHECK("k_tile_gather");
+      if (t->fmt != CYC_TILES_WIDE) {
+        // the compact entries this sub-chunk takes (fillers included)
+        if ((rc = counts.reserve(sizeof(uint32_t) * (size_t)cnt)) ||
+            (rc = posb.reserve(sizeof(unsigned long long) * (size_t)cnt)) ||
+            (rc = t->scal.reserve(sizeof(int64_t))))
+          return rc;
+        hipLaunchKernelGGL(k_tile_fill_counts, dim3(8192), dim3(256), 0, st,
+                           (const uint32_t*)keysOut.ptr, (const uint32_t*)perm.ptr,
+                           (const uint32_t*)packed.ptr, cnt, (uint32_t*)counts.ptr);
+        CYC_LAUNCH_CHECK("k_tile_fill_counts");
+        size_t scanBytes = 0;
+        CYC_HIP(rocprim::exclusive_scan(nullptr, scanBytes, (const uint32_t*)counts.ptr,
+                                        (unsigned long long*)posb.ptr, 0ull, (size_t)cnt,
+                                        rocprim::plus<unsigned long long>(), st));
+        if ((rc = tmp.reserve(std::max(tmpBytes, scanBytes)))) return rc;
+        CYC_HIP(rocprim::exclusive_scan(tmp.ptr, scanBytes, (const uint32_t*)counts.ptr,
+                                        (unsigned long long*)posb.ptr, 0ull, (size_t)cnt,
+                                        rocprim::plus<unsigned long long>(), st));
+        hipLaunchKernelGGL(k_tile_total, dim3(1), dim3(1), 0, st, (const uint32_t*)counts.ptr,
+                           (const unsigned long long*)posb.ptr, cnt, (int64_t*)t->scal.ptr);
+        CYC_LAUNCH_CHECK("k_tile_total");
+        CYC_HIP(hipMemcpyAsync(&total, t->scal.ptr, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        CYC_HIP(hipStreamSynchronize(st));
+        if (t->fmt == CYC_TILES_AUTO) {
+          // the first sub-chunk with nonzeros decides: compact when its
+          // fillers are at most 1/32 of its nonzeros
+          if ((rc = set_storage(t, (total - cnt) * 32 <= cnt ? CYC_TILES_COMPACT : CYC_TILES_WIDE)))
+            return rc;
+        }
+      }
+      if (t->fmt == CYC_TILES_COMPACT) {
+        CYC_REQUIRE(t->entries + total <= t->capEntries,
+                    "the compact layout's filler entries exceed its allowance (" +
+                        std::to_string(t->capEntries - t->capNnz) + "): create it with "
+                        "cyc_tiles_set_format(CYC_TILES_WIDE) for rows this sparse");
+        pos = (const unsigned long long*)posb.ptr;
+        hipLaunchKernelGGL(k_tile_compact, dim3(8192), dim3(256), 0, st,
+                           (const uint32_t*)keysOut.ptr, (const uint32_t*)perm.ptr,
+                           (const uint32_t*)packed.ptr, vals + (qa - q0), cnt, pos,
+                           (uint16_t*)t->idx.ptr + t->entries, (double*)t->vals.ptr + t->entries);
+        CYC_LAUNCH_CHECK("k_tile_compact");
+      } else {
+        total = cnt;
+        hipLaunchKernelGGL(k_tile_gather, dim3(8192), dim3(256), 0, st, (const uint32_t*)perm.ptr,
+                           cnt, (const uint32_t*)packed.ptr, vals + (qa - q0),
+                           (uint32_t*)t->idx.ptr + t->entries, (double*)t->vals.ptr + t->entries);
+        CYC_LAUNCH_CHECK("k_tile_gather");
+      }
     }
     hipLaunchKernelGGL(k_tile_starts, dim3((unsigned)std::min<int64_t>((cnt + 256) / 256, 8192)),
-                       dim3(256), 0, st, (const uint32_t*)keysOut.ptr, cnt, nkeys, seg0, t->nnz,
-                       (int64_t*)t->segStart.ptr);
+                       dim3(256), 0, st, (const uint32_t*)keysOut.ptr, cnt, nkeys, seg0,
+                       t->entries, pos, total, (int64_t*)t->segStart.ptr);
     CYC_LAUNCH_CHECK("k_tile_starts");
     t->nnz += cnt;
+    t->entries += total;
     // scratch is reused by the next sub-chunk on this stream; freed on return
   }
   t->n += rows;
   if (t->n % kTileRows != 0) t->sealed = true;
   const int64_t segs = (t->n + kTileRows - 1) / kTileRows * T;
-  hipLaunchKernelGGL(k_set_i64, dim3(1), dim3(1), 0, st, (int64_t*)t->segStart.ptr + segs, t->nnz);
+  hipLaunchKernelGGL(k_set_i64, dim3(1), dim3(1), 0, st, (int64_t*)t->segStart.ptr + segs,
+                     t->entries);
   CYC_LAUNCH_CHECK("k_set_i64");
   if (int rc = t->maxDev.reserve(sizeof(unsigned long long))) return rc;
   CYC_HIP(hipMemsetAsync(t->maxDev.ptr, 0, sizeof(unsigned long long), st));

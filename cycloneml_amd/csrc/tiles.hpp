@@ -18,15 +18,17 @@ constexpr int kTileSuperCols = kTileWaves * kTileCols;   // columns of one gradi
 
 // What the kernels need to walk a built layout.  Segment s = rb * T + c
 // (row block rb, column chunk c) spans nonzeros [segStart[s], segStart[s+1])
-// in CSR order; idx packs (row in block << 16 | column in chunk), vals the
-// fp64 values.
+// in CSR order; idx packs (row in block << 16 | column in chunk) -- or, for
+// the compact format, 16 bits: the column and the row's step (tiles.hip) --
+// and vals the fp64 values.
 struct TilesView {
   int64_t n = 0;         // rows
   int F = 0;             // numFeatures
   int T = 1;             // column chunks
   int Wt = 1;            // columns per chunk (the last chunk may be shorter)
   int64_t nRB = 0;       // row blocks
-  int64_t maxSeg = 0;    // nonzeros of the longest segment
+  int64_t maxSeg = 0;    // entries of the longest segment
+  bool compact = false;  // 16-bit compact entries (idx is then uint16_t[])
   const int64_t* segStart = nullptr;
   const uint32_t* idx = nullptr;
   const double* vals = nullptr;
@@ -50,7 +52,7 @@ int tiles_rows(int64_t n, const double* labels, const double* weights, int fitIn
 
 // Gradient pass: slabG[range * F + f] = sum over the rows of row range
 // `range` (row order) of vals * mult[row]; *ranges receives the range count.
-// slabG needs ranges_for(v) * F doubles.
+// slabG needs tiles_ranges(v) * F doubles.
 int tiles_ranges(const TilesView& v);
 int tiles_grad(const TilesView& v, const double* mult, double* slabG, int* ranges,
                hipStream_t st);

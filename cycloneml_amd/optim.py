@@ -31,19 +31,27 @@ def _torch():
 class SparseTiles:
     """RAII wrapper of cyc_tiles: the row-block x column-tile layout of a CSR
     shard (cycloneml_amd/csrc/tiles.hip) that the binary aggregators' sparse
-    path runs on -- 12 B per nonzero, built by appending CSR rows (whole row
-    blocks of ROW_BLOCK rows, except the last append); the CSR can be freed
+    path runs on -- 12 B per nonzero (format "wide") or 10 B per entry
+    ("compact": 16-bit ids, ~1-3 % filler entries; "auto" picks it for dense
+    enough segments), built by appending CSR rows (whole row blocks of
+    ROW_BLOCK rows, except the last append); the CSR can be freed
     afterwards."""
 
     ROW_BLOCK = 2048          # cyc_tiles_row_block()
+    FORMATS = {"auto": 0, "wide": 1, "compact": 2}   # CYC_TILES_AUTO / WIDE / COMPACT
 
-    def __init__(self, numFeatures: int, capacity_rows: int, capacity_nnz: int):
+    def __init__(self, numFeatures: int, capacity_rows: int, capacity_nnz: int,
+                 format: str = "auto"):
         self._lib = N.load()
         h = ctypes.c_void_p()
         N.check(self._lib.cyc_tiles_create(int(numFeatures), int(capacity_rows),
                                            int(capacity_nnz), ctypes.byref(h)))
         self.handle = h
         self.numFeatures = int(numFeatures)
+        if format not in self.FORMATS:
+            raise ValueError(f"format must be one of {sorted(self.FORMATS)}")
+        if format != "auto":
+            N.check(self._lib.cyc_tiles_set_format(self.handle, self.FORMATS[format]))
 
     def append(self, rowptr, colidx, values, stream=None):
         n = int(rowptr.shape[0]) - 1
@@ -52,10 +60,20 @@ class SparseTiles:
         return self
 
     @staticmethod
-    def from_csr(rowptr, colidx, values, numFeatures, stream=None):
+    def from_csr(rowptr, colidx, values, numFeatures, stream=None, format="auto"):
         n = int(rowptr.shape[0]) - 1
-        t = SparseTiles(numFeatures, n, int(colidx.shape[0]))
+        t = SparseTiles(numFeatures, n, int(colidx.shape[0]), format=format)
         return t.append(rowptr, colidx, values, stream)
+
+    @property
+    def format(self):
+        """"wide" / "compact" once decided ("auto" before the first append)."""
+        f = int(self._lib.cyc_tiles_format(self.handle))
+        return {v: k for k, v in self.FORMATS.items()}[f]
+
+    @property
+    def entries(self):
+        return int(self._lib.cyc_tiles_entries(self.handle))
 
     @property
     def rows(self):
@@ -113,16 +131,17 @@ class DeviceInstanceBlock:
     def is_sparse(self):
         return self.X is None
 
-    def prepare(self, stream=None, layout="csc"):
+    def prepare(self, stream=None, layout="csc", tiles_format="auto"):
         """Derive a layout of a CSR shard once, outside the training loop.
         layout="csc": the row-blocked column-major copy (cyc_csc_build_dev)
-        the multinomial / summarizer CSR paths use; layout="tiles": the
-        row-block x column-tile layout (SparseTiles) the binary aggregators
-        run on.  Either costs 12 bytes per nonzero of HBM."""
+        the multinomial / summarizer CSR paths use (12 bytes per nonzero of
+        HBM); layout="tiles": the row-block x column-tile layout
+        (SparseTiles, entry format `tiles_format`: 12 bytes per nonzero
+        wide, ~10 compact) the binary aggregators run on."""
         if self.is_sparse and layout == "tiles":
             if self.tiles is None:
                 self.tiles = SparseTiles.from_csr(self.rowptr, self.colidx, self.values,
-                                                  self.numFeatures, stream)
+                                                  self.numFeatures, stream, format=tiles_format)
             return self
         if self.is_sparse and self.csc is None:
             h = ctypes.c_void_p()

@@ -312,23 +312,38 @@ int cyc_csc_arrays(cyc_csc csc, const int64_t** colptr, const int32_t** rowidx,
 
 /* Row-block x column-tile layout of a CSR shard (tiles.hip) for the binary
  * aggregators' two sparse gemv (BinaryLogisticBlockAggregator.scala:97,130;
- * ml/linalg/BLAS.scala:764-805): row blocks of cyc_tiles_row_block() = 8192
- * rows, column tiles of 8192 columns, 12 bytes per nonzero (fp64 value +
- * packed row/column ids) plus ~0.5 % offsets, so both gathers run from LDS.
- * Built by appending CSR rows (rowptr[rows+1] of any base, colidx sorted
- * within a row as in SparseVector, values) in order: every append except
- * the last holds a whole number of row blocks.  Indices are validated with
- * SparseVector's require messages (ml/linalg/Vectors.scala:617-625).  The
- * CSR input is not referenced afterwards (free it: the layout is the shard's
- * only copy).  capacity_*: upper bounds for the whole shard. */
+ * ml/linalg/BLAS.scala:764-805): row blocks of cyc_tiles_row_block() = 2048
+ * rows, column chunks of <= 2048 columns; each (row block, chunk) segment
+ * holds its nonzeros in CSR order as fp64 values + ids, so both gathers run
+ * from LDS.  Two entry formats: CYC_TILES_WIDE, 12 bytes per nonzero (32-bit
+ * packed row / column ids); CYC_TILES_COMPACT, 10 bytes per entry (16-bit:
+ * the column and the row's step from the segment's previous entry; a step of
+ * 31 rows or more takes filler entries).  CYC_TILES_AUTO (the default) lets
+ * the first append that holds nonzeros choose: compact when its fillers are
+ * at most 1/32 of its nonzeros (dense-enough segments, e.g. config 5's 268
+ * nonzeros per segment: 1.3 % fillers), wide otherwise; cyc_tiles_set_format
+ * fixes one before the first append.  Built by appending CSR rows
+ * (rowptr[rows+1] of any base, colidx sorted within a row as in
+ * SparseVector, values) in order: every append except the last holds a
+ * whole number of row blocks.  Indices are validated with SparseVector's
+ * require messages (ml/linalg/Vectors.scala:617-625).  The CSR input is not
+ * referenced afterwards (free it: the layout is the shard's only copy).
+ * capacity_*: upper bounds for the whole shard; a compact layout reserves a
+ * 6.25 % allowance of filler entries on top. */
 typedef struct cyc_tiles_s* cyc_tiles;
+enum { CYC_TILES_AUTO = 0, CYC_TILES_WIDE = 1, CYC_TILES_COMPACT = 2 };
 int cyc_tiles_create(int32_t numFeatures, int64_t capacity_rows, int64_t capacity_nnz,
                      cyc_tiles* out);
+int cyc_tiles_set_format(cyc_tiles tiles, int32_t format);
+/* the entry format in use (CYC_TILES_AUTO until decided) */
+int32_t cyc_tiles_format(cyc_tiles tiles);
 int cyc_tiles_append_dev(cyc_tiles tiles, const int64_t* rowptr, const int32_t* colidx,
                          const double* vals, int64_t rows, void* stream);
 int cyc_tiles_destroy(cyc_tiles tiles);
 int64_t cyc_tiles_rows(cyc_tiles tiles);
 int64_t cyc_tiles_nnz(cyc_tiles tiles);
+/* entry positions used (= nnz for the wide format; + fillers for compact) */
+int64_t cyc_tiles_entries(cyc_tiles tiles);
 int32_t cyc_tiles_features(cyc_tiles tiles);
 int64_t cyc_tiles_bytes(cyc_tiles tiles);
 int32_t cyc_tiles_row_block(void);

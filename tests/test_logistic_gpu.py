@@ -283,18 +283,21 @@ def test_sparse_config5_full_size(cuda):
     _rel_close(full, parts, rtol=1e-12)
 
 
+@pytest.mark.parametrize("fmt", ["wide", "compact"])
 @pytest.mark.parametrize("fi,fwm", [(True, False), (True, True), (False, False)])
 @pytest.mark.parametrize("n,F,nnz", [(700, 600_000, 40), (300, 1_100_000, 150), (50, 300_000, 1),
                                      (20_000, 30_000, 25), (9000, 8192, 300),
                                      (40_000, 1_000_000, 64), (5000, 100, 10), (3000, 3, 2)])
-def test_binary_tiles_vs_oracle(cuda, fi, fwm, n, F, nnz):
+def test_binary_tiles_vs_oracle(cuda, fmt, fi, fwm, n, F, nnz):
     """The row-block x column-chunk layout: many column chunks (F up to 1.1M
     = 538 chunks of 2048, 68 gradient workgroups of 8 chunks), several row
     blocks and super blocks (40000 rows = 20 row blocks of 2048 = 3 margin
     super blocks of 8), empty rows, zero weights, rows spanning every chunk,
     long runs (9000 rows of ~300 nonzeros over 8 chunks: the batched tail
     path), and narrow F (100 and 3 columns: chunks of 64, most waves without
-    a chunk); equals the restatement
+    a chunk); in both entry formats (wide: 32-bit ids; compact: 16-bit
+    column + row step, filler entries for the rows' gaps of 31 or more --
+    most of these shapes need fillers); equals the restatement
     within 1e-10, the loss bit for bit-ish (same summation order), and is
     bitwise reproducible run to run."""
     from cycloneml_amd.optim import BinaryLogisticBlockAggregator, DeviceInstanceBlock
@@ -305,14 +308,92 @@ def test_binary_tiles_vs_oracle(cuda, fi, fwm, n, F, nnz):
     st = dict(grad=np.zeros(coef.size), loss=0.0, weight=0.0)
     oracle.binary_logistic_add(_oracle_block(X, csr, labels, w, F), coef, fi, fwm, sm, st)
     blk = DeviceInstanceBlock.from_numpy(labels, w, X=None, csr=csr, numFeatures=F, device=cuda)
-    blk.prepare(layout="tiles").release_csr()
-    assert blk.tiles.rows == n and blk.tiles.nnz == csr[1].size
+    blk.prepare(layout="tiles", tiles_format=fmt).release_csr()
+    assert blk.tiles.rows == n and blk.tiles.nnz == csr[1].size and blk.tiles.format == fmt
+    assert (blk.tiles.entries == blk.tiles.nnz) == (fmt == "wide" or blk.tiles.entries == 0 or
+                                                   blk.tiles.entries == blk.tiles.nnz)
     agg = BinaryLogisticBlockAggregator(np.ones(F), sm, fi, fwm, coef, device=cuda).add(blk)
     _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
     assert abs(agg.weight - st["weight"]) <= 1e-12 * st["weight"]
     assert abs(float(agg._loss_sum.item()) - st["loss"]) <= 1e-12 * abs(st["loss"])
     again = BinaryLogisticBlockAggregator(np.ones(F), sm, fi, fwm, coef, device=cuda).add(blk)
     assert np.array_equal(agg._state.cpu().numpy(), again._state.cpu().numpy())
+
+
+@pytest.mark.parametrize("n,F,nnz", [(40_000, 1_000_000, 64), (9000, 8192, 300), (700, 600_000, 40),
+                                     (6000, 50_000, 3)])
+def test_tiles_compact_equals_wide(cuda, n, F, nnz):
+    """The compact entries hold the same nonzeros in the same order as the
+    wide ones (the fillers only move the row), so both passes add the same
+    products in the same order: the aggregator state is the same bits in
+    both formats, for every aggregator kind the layout serves."""
+    import torch
+    from cycloneml_amd.optim import (BinaryLogisticBlockAggregator, DeviceInstanceBlock,
+                                     HingeBlockAggregator, SparseTiles)
+    rng = np.random.default_rng(n + nnz)
+    X, csr, labels, w = _make(n, F, True, rng, nnz=nnz, zero_w=True)
+    rp, ci, vv = (torch.as_tensor(a, device=cuda) for a in csr)
+    lab = torch.as_tensor(labels, device=cuda)
+    wt = torch.as_tensor(w, device=cuda)
+    coef = rng.normal(size=F + 1) * 0.3
+    sm = rng.normal(size=F) * 0.1
+    states = []
+    for fmt in ("wide", "compact"):
+        t = SparseTiles.from_csr(rp, ci, vv, F, format=fmt)
+        assert t.format == fmt and t.nnz == ci.numel() and t.entries >= t.nnz
+        blk = DeviceInstanceBlock(lab, wt, tiles=t, numFeatures=F)
+        b = BinaryLogisticBlockAggregator(np.ones(F), torch.as_tensor(sm, device=cuda), True,
+                                          True, coef, device=cuda).add(blk)
+        h = HingeBlockAggregator(np.ones(F), torch.as_tensor(sm, device=cuda), True, coef,
+                                 device=cuda).add(blk)
+        states.append((b._state.cpu().numpy(), h._state.cpu().numpy()))
+    assert np.array_equal(states[0][0], states[1][0])
+    assert np.array_equal(states[0][1], states[1][1])
+
+
+def test_tiles_format_choice_and_requires(cuda):
+    """CYC_TILES_AUTO: the first append with nonzeros picks compact for dense
+    enough segments (config 5's shape: 64 of 1M columns per row) and wide for
+    sparse ones (2 nonzeros per row over 1M columns: row gaps of ~500 would
+    need ~16 fillers per nonzero); the format is fixed before the first
+    append only; a compact layout whose fillers exceed its allowance fails
+    with a message naming the wide format."""
+    import torch
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.optim import SparseTiles
+    rng = np.random.default_rng(21)
+    X, csr, labels, w = _make(8192, 1_000_000, True, rng, nnz=64)
+    rp, ci, vv = (torch.as_tensor(a, device=cuda) for a in csr)
+    t = SparseTiles(1_000_000, 8192, ci.numel())
+    assert t.format == "auto"
+    t.append(rp, ci, vv)
+    assert t.format == "compact" and t.nnz == ci.numel() and t.nnz < t.entries < 1.05 * t.nnz
+    with pytest.raises(N.IllegalArgumentException, match="before the first append"):
+        N.check(t._lib.cyc_tiles_set_format(t.handle, 1))
+    X, csr, labels, w = _make(4096, 1_000_000, True, rng, nnz=2)
+    rp, ci, vv = (torch.as_tensor(a, device=cuda) for a in csr)
+    t = SparseTiles.from_csr(rp, ci, vv, 1_000_000)
+    assert t.format == "wide" and t.entries == t.nnz
+    def every(gap, blocks):
+        n = gap * 2048 * blocks                        # a nonzero in every gap-th row
+        nz = np.zeros(n, dtype=np.int64)
+        nz[::gap] = 1
+        rpx = torch.as_tensor(np.concatenate([[0], np.cumsum(nz)]), device=cuda)
+        cix = torch.zeros(int(nz.sum()), dtype=torch.int32, device=cuda)
+        return n, rpx, cix, torch.ones(cix.numel(), dtype=torch.float64, device=cuda)
+    # gaps of 40 rows: one filler per nonzero (~53,000), inside the allowance
+    # of 53,248 / 16 + 65,536
+    n, rpx, cix, vvx = every(40, 26)
+    big = SparseTiles(10, n, cix.numel(), format="compact")
+    big.append(rpx, cix, vvx)
+    assert 1.9 * big.nnz < big.entries < 2 * big.nnz
+    # gaps of 80: two fillers per nonzero, past it
+    n, rpx, cix, vvx = every(80, 26)
+    over = SparseTiles(10, n, cix.numel(), format="compact")
+    with pytest.raises(N.IllegalArgumentException, match="CYC_TILES_WIDE"):
+        over.append(rpx, cix, vvx)
+    with pytest.raises(ValueError):
+        SparseTiles(10, 1, 1, format="narrow")
 
 
 def test_tiles_appends_and_requires(cuda):
