@@ -177,7 +177,17 @@ __global__ __launch_bounds__(GT, 2) void k_gram_tiles(
 // means read from LDS instead of registers measured 611.7 vs 567.7 ms at
 // 30M x 1024.
 // Needs p even (16-byte rows of a panel); odd p takes k_gram_tiles.
-template <bool MEAN, int KCH = 8, int NB = 2, int OCC = 3, bool XCDMAP = !MEAN && CYC_GRAM_XCDMAP>
+// MEAN 2 (CYC_COV_KERNEL=lds, a measurement switch): each wave centres the
+// rows it DMA'd once, in LDS, between its DMA's landing and the chunk's
+// barrier (x - mean by the same dsub, so the same bits), and the MFMAs read
+// centred operands -- half the subtractions of MEAN 1 (each panel element
+// is read by two waves), no mean registers in the loop (168 VGPRs), so it
+// runs the plain form's 8-row chunks at three workgroups per CU with the
+// XCD grouping.  Measured slower: 555.2 vs 548.4 ms at 30M x 1024 (29
+// Gramian tests green with it); the centring pass doubles the chunk's LDS
+// traffic and sits between the DMA wait and the barrier.
+template <int MEAN, int KCH = 8, int NB = 2, int OCC = 3,
+          bool XCDMAP = MEAN != 1 && CYC_GRAM_XCDMAP>
 __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
     const double* __restrict__ X, int64_t nrows, int p, const double* __restrict__ mean,
     int tilesPerSide, int64_t rowsPerSplit, int splits, double* __restrict__ slab) {
@@ -217,7 +227,7 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = cyc_double4{0.0, 0.0, 0.0, 0.0};
   double mI[4], mJ[4];
-  if constexpr (MEAN) {
+  if constexpr (MEAN == 1) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ci = I0 + wy * 64 + q * 16 + (lane & 15), cj = J0 + wx * 64 + q * 16 + (lane & 15);
@@ -239,7 +249,7 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
 #pragma unroll
     for (int u = 0; u < KCH / 4; ++u) {
       const int rr = wave * (KCH / 4) + u;
-      const bool pad = MEAN && rr >= nr;
+      const bool pad = MEAN != 0 && rr >= nr;
 #pragma unroll
       for (int pn = 0; pn < 2; ++pn)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -254,8 +264,8 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
   // SKIPLOW 2 the two diagonal waves also skip their 16x16 blocks below the
   // diagonal.  (The plain form, three workgroups per CU, measured slower
   // with it: 507.7 vs 488.6 ms.)
-  const bool idle = CYC_GRAM_SKIPLOW && MEAN && ti == tj && wy > wx;
-  const bool tri = CYC_GRAM_SKIPLOW >= 2 && MEAN && ti == tj && wy == wx;
+  const bool idle = CYC_GRAM_SKIPLOW && MEAN == 1 && ti == tj && wy > wx;
+  const bool tri = CYC_GRAM_SKIPLOW >= 2 && MEAN == 1 && ti == tj && wy == wx;
   auto compute = [&](int b) {
     if (idle) return;
     const double* Ai = Pn(b, 0);
@@ -269,7 +279,7 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
         a[q] = Ai[krow * LDSW + wy * 64 + q * 16 + (lane & 15)];
         bb[q] = Aj[krow * LDSW + wx * 64 + q * 16 + (lane & 15)];
       }
-      if constexpr (MEAN) {
+      if constexpr (MEAN == 1) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           a[q] = dsub(a[q], mI[q]);
@@ -287,13 +297,39 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
   // NB - 1 chunks ahead; past the end the DMAs fetch nothing (empty
   // range), so every wave always has (NB - 2) DPW newer DMAs to leave in
   // flight at the counted wait
+  // MEAN 2: the means of the two columns this lane DMAs in each panel
+  double cm[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+  if constexpr (MEAN == 2) {
+#pragma unroll
+    for (int pn = 0; pn < 2; ++pn)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int c = (pn ? J0 : I0) + lane * 2 + e;
+        cm[pn][e] = c < p ? mean[c] : 0.0;
+      }
+  }
+  auto centre = [&](int b) {   // this wave's DMA'd rows of chunk buffer b
+#pragma unroll
+    for (int u = 0; u < KCH / 4; ++u) {
+      const int rr = wave * (KCH / 4) + u;
+#pragma unroll
+      for (int pn = 0; pn < 2; ++pn) {
+        double2* q = reinterpret_cast<double2*>(Pn(b, pn) + rr * LDSW) + lane;
+        double2 x = *q;
+        x.x = dsub(x.x, cm[pn][0]);
+        x.y = dsub(x.y, cm[pn][1]);
+        *q = x;
+      }
+    }
+  };
 #pragma unroll
   for (int c = 0; c < NB - 1; ++c) issue(r0 + c * KCH, c);
   int b = 0;
   for (int64_t rb = r0; rb < r1; rb += KCH) {
     if constexpr (NB == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * DPW) : "memory");
-    __syncthreads();   // chunk rb landed everywhere; every wave is past rb - KCH
+    if constexpr (MEAN == 2) centre(b);
+    __syncthreads();   // chunk rb landed (centred) everywhere; every wave is past rb - KCH
     issue(rb + (NB - 1) * KCH, b == 0 ? NB - 1 : b - 1);
     compute(b);
     b = b == NB - 1 ? 0 : b + 1;
@@ -623,9 +659,14 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   // k_gram_tiles (a measurement switch)
   const char* gk = std::getenv("CYC_GRAMIAN_KERNEL");
   const bool dma = (p % 2) == 0 && !(gk && std::string(gk) == "tiles");
-  // workgroups per CU: three for k_gram_dma's 8-row form, two for the
-  // 16-row MEAN form (the mean operands spill at three) and k_gram_tiles
-  const int64_t slots = (dma && !mean ? 3 : 2) * (int64_t)cyc::device_cus();
+  // the covariance: the mean subtracted from every MFMA operand (MEAN 1), or
+  // CYC_COV_KERNEL=lds for the chunks centred in LDS (MEAN 2; a measurement
+  // switch)
+  const char* ck = std::getenv("CYC_COV_KERNEL");
+  const bool operand = mean && !(ck && std::string(ck) == "lds");
+  // workgroups per CU: three for k_gram_dma's 8-row forms, two for the
+  // 16-row MEAN 1 form (the mean operands spill at three) and k_gram_tiles
+  const int64_t slots = (dma && !operand ? 3 : 2) * (int64_t)cyc::device_cus();
   const int64_t lo = std::max<int64_t>(1, (4 * slots + pairs - 1) / pairs);
   int64_t splits = cyc::balanced_splits(pairs, lo, 2 * lo, slots);
   splits = std::min<int64_t>(splits, std::max<int64_t>(1, nrows / 64));
@@ -635,18 +676,21 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   if (rc) return rc;
   {
   // timed under the name of the kernel that runs (rocprofv3 lists the
-  // k_gram_dma<true, 16, 2, 2> instance as k_gram_dma too)
+  // covariance instances as k_gram_dma too)
   cyc::KernelTimer timer(!dma ? "k_gram_tiles" : mean ? "k_gram_dma_cov" : "k_gram_dma", st);
   const dim3 grid(pairs, (unsigned)splits);
   // the plain k_gram_dma: one dimension, splits padded to a multiple of 8
   // (XCDMAP)
   const dim3 gridD = CYC_GRAM_XCDMAP ? dim3((unsigned)(pairs * ((splits + 7) / 8) * 8)) : grid;
   double* slab = (double*)plan->slab.ptr;
-  if (dma && mean)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<true, 16, 2, 2>), grid, dim3(GT), 0, st, X,
+  if (dma && operand)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<1, 16, 2, 2>), grid, dim3(GT), 0, st, X,
                        nrows, p, mean, tps, rps, (int)splits, slab);
+  else if (dma && mean)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<2>), gridD, dim3(GT), 0, st, X, nrows, p,
+                       mean, tps, rps, (int)splits, slab);
   else if (dma)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<false>), gridD, dim3(GT), 0, st, X, nrows, p,
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<0>), gridD, dim3(GT), 0, st, X, nrows, p,
                        mean, tps, rps, (int)splits, slab);
   else
     hipLaunchKernelGGL(k_gram_tiles, grid, dim3(GT), 0, st, X, nrows, p, mean, tps, rps, slab);
