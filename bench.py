@@ -351,11 +351,15 @@ class KMeansWorkload:
         (ml/clustering/KMeans.scala:89, :336-343) -- from setInitialModel
         (rows 0..k-1): the cached norms, the plan and row image, then every
         Lloyd iteration (mllib/clustering/KMeans.scala:263-334) with its
-        convergence check read back on the host.  Returns the iterations run."""
+        convergence check read back on the host."""
         from cycloneml_amd.clustering import KMeans, KMeansModel
         km = KMeans(k=self.k, maxIterations=max_iter, epsilon=1e-4)
         km.setInitialModel(KMeansModel(self.C0.cpu().numpy()))
-        return km.run(self.X).numIter
+        return {"iterations": km.run(self.X).numIter,
+                "note": "one fit from setInitialModel (rows 0..k-1), maxIter 20, tol 1e-4: "
+                        "norms + plan + row image + every iteration with its host convergence "
+                        "check, over iterations 1..maxIter (value times steady-state "
+                        "iterations after the warmup)"}
 
     def extra_roofline(self, launches_per_step, avg_s):
         import torch
@@ -544,6 +548,25 @@ class LRMultiWorkload:
 
     def step(self):
         self.fn.calculate(self.coef)
+
+    def fit_once(self, max_iter=20):
+        """One LogisticRegression.fit as the reference runs it on these rows
+        (LogisticRegression.scala:495-685): the Summarizer pre-pass (:511),
+        standardization, then breeze LBFGS (m = 10, tol 1e-6, restated in
+        cycloneml_amd/optimize.py) driving RDDLossFunction.calculate --
+        coefficients broadcast, one device data pass, the gradient pulled
+        back -- at least once per iteration (the line search may evaluate
+        more: :999), maxIter 20, regParam 0, fitIntercept, multinomial."""
+        from cycloneml_amd.classification import LogisticRegression
+        lr = LogisticRegression(maxIter=max_iter, family="multinomial")
+        model = lr.fit([self.block])
+        ev = lr.lastCost.evaluations
+        return {"iterations": model.totalIterations, "evaluations": ev,
+                "evaluations_per_iteration": ev / max(model.totalIterations, 1),
+                "note": "one LogisticRegression.fit (multinomial, maxIter 20, tol 1e-6, "
+                        "regParam 0): Summarizer pass + LBFGS with its line-search "
+                        "evaluations; each evaluation = coefficients to HBM, one data pass, "
+                        "gradient to the host"}
 
     def work(self, kname, launches_per_step):
         return 2.0 * self.n * self.F * self.C / launches_per_step, FP64   # each pass: one gemm
@@ -876,13 +899,9 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
         if world > 1:
             dist.barrier()
         fel = parallel.max_over_ranks(time.perf_counter() - t0, dev)
-        fit = {"fit_ms": fel * 1e3, "iterations": iters,
-               "fit_ms_per_iteration": fel * 1e3 / max(iters, 1),
-               "rows_per_s_per_iteration": total_rows * iters / fel,
-               "note": "one fit from setInitialModel (rows 0..k-1), maxIter 20, tol 1e-4: "
-                       "norms + plan + row image + every iteration with its host convergence "
-                       "check, over iterations 1..maxIter (value times steady-state iterations "
-                       "after the warmup)"}
+        its = iters["iterations"]
+        fit = {"fit_ms": fel * 1e3, "fit_ms_per_iteration": fel * 1e3 / max(its, 1),
+               "rows_per_s_per_iteration": total_rows * its / fel, **iters}
     # Every priced kernel in its own units (work per launch / mean launch
     # duration from its HIP events), and the dominant one by a fixed rule:
     # the priced kernel with the most time per step, except that a kernel

@@ -271,8 +271,10 @@ class LogisticRegression:
         device = blocks[0].labels.device
 
         def make_cost(numClasses, multinomial, fitWithMean, inverseStd):
-            return _DeviceCost(blocks, numFeatures, numClasses, multinomial, self.fitIntercept,
-                               fitWithMean, mean, inverseStd, device)
+            # kept as lastCost: its evaluations count the data passes
+            self.lastCost = _DeviceCost(blocks, numFeatures, numClasses, multinomial,
+                                        self.fitIntercept, fitWithMean, mean, inverseStd, device)
+            return self.lastCost
         return self.train_from_summary(numFeatures, histogram, mean, std, make_cost)
 
     def train_from_summary(self, numFeatures: int, histogram, featuresMean, featuresStd,

@@ -123,7 +123,7 @@ def dense_cluster_ids(pred):
         if local.numel() > MAX_CLUSTERS:
             raise N.IllegalArgumentException(
                 f"requirement failed: the device Silhouette supports at most {MAX_CLUSTERS} "
-                f"clusters, got at least {local.numel()}")
+                f"distinct cluster ids, got at least {local.numel()}")
     parallel.agree(bound)
     mine = local.cpu().tolist()
     keys = sorted(set().union(*[set(g) for g in parallel.allgather_object(mine)]))

@@ -23,9 +23,10 @@ python - <<'PY'
 import json
 d = json.loads(open("gpurun_out/bench_all.json").read().strip().splitlines()[-1])
 for name, w in [("kmeans", d)] + list(d.get("workloads", {}).items()):
-    print(name, round(w["value"] / 1e6, 1), "M rows/s", round(w["ms_per_step"], 2), "ms",
-          w["roofline"]["kernel"], round(w["roofline"]["frac"], 3),
-          (w["cpu_baseline"] or {}).get("value"))
+    r = w.get("roofline") or {}
+    print(name, round(w["value"] / 1e6, 1), "M/s", round(w["ms_per_step"], 2), "ms",
+          r.get("kernel"), round(r.get("frac", 0), 3), w.get("vs_baseline"),
+          (w.get("cpu_baseline") or {}).get("value"), (w.get("fit") or {}).get("fit_ms"))
 PY
 fi
 echo ALLDONE

@@ -13,3 +13,10 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 "$@" > $OUT/trace.log 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 "$@" > $OUT/pmc_fetch.log 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python3 $R/bench.py --cpu-seconds 0 "$@" > $OUT/pmc_write.log 2>&1 || exit $?
+# With SUMMARY=<rows>:<iterations>, summarise on the box into
+# $OUT/summary_{pmc.json,kernel_stats.csv} and drop the raw per-dispatch
+# CSVs (they can exceed what gpurun copies back).
+if [ -n "$SUMMARY" ]; then
+  python3 $R/tools/pmc_summary.py $OUT $OUT/summary ${SUMMARY%%:*} ${SUMMARY##*:} > $OUT/summary.log 2>&1 || exit $?
+  find $OUT -name '*.csv' ! -name 'summary_*' ! -name 'run_kernel_stats.csv' -delete
+fi
