@@ -462,17 +462,24 @@ class GramianWorkload:
 class PCAWorkload:
     """The PCA variant of BASELINE configs[2]: RowMatrix.computeCovariance
     (RowMatrix.scala:452-467) per step on the Gramian workload's rows -- the
-    column-mean pass (Statistics.colStats, :456), isSparseMatrix (:462, a
-    take(1): one 64K-row round on dense rows), the centred syrk
-    (computeDenseVectorCovariance, :163-220: k_gram_dma with the mean
-    subtracted as the operands leave LDS), the all-reduce and the (m - 1)
-    finish into the n x n matrix in HBM.  The breeze SVD of
+    isSparseMatrix (:462, a take(1): one 64K-row round on dense rows), the
+    column moments of the leading 64K rows, then the syrk in the form the
+    moments allow (these U[0, 1) rows have mean^2 = 3 variance: the plain
+    syrk with the column sums (Statistics.colStats, :456) riding it, and the
+    Gramian finish of :222-246; linalg.RowMatrix._near_centred states the bound), the
+    all-reduce and the finish into the n x n matrix in HBM.  The reference's
+    centred syrk (computeDenseVectorCovariance, :163-220) is timed after the
+    steps for comparison (centred_form_ms_per_step).  The breeze SVD of
     computePrincipalComponentsAndExplainedVariance (:499-501) runs on the
     driver in the reference; here it is the host eigensolve, timed once
     outside the steps (eigensolve_ms)."""
-    kernel = "k_gram_dma_cov"
-    kernels = ("k_gram_dma_cov", "k_col_sums")
+    kernels = ("k_gram_dma", "k_gram_dma_cov", "k_col_sums")
     pmc_names = {"k_gram_dma_cov": "k_gram_dma"}
+
+    @property
+    def kernel(self):
+        return "k_gram_dma_cov" if getattr(self.mat, "lastCovarianceForm",
+                                           "centred") == "centred" else "k_gram_dma"
 
     def __init__(self, n, dev, rank):
         from cycloneml_amd.linalg import RowMatrix
@@ -491,16 +498,34 @@ class PCAWorkload:
 
     def after_timing(self):
         import numpy as np
+        import torch
         cov = self.G.cpu().numpy()
+        self.form = self.mat.lastCovarianceForm
+        self.passes = list(self.mat.lastCovariancePasses)
         t0 = time.perf_counter()
         _, s, _ = np.linalg.svd(cov)              # the driver's brzSvd(Cov) (:501)
         self.eig_ms = (time.perf_counter() - t0) * 1e3
         self.explained_top3 = (s[:3] / s.sum()).tolist()
+        # the reference's centred form on the same rows, for comparison
+        self.mat.covarianceForm = "centred"
+        self.mat.computeCovarianceDevice()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            Gc = self.mat.computeCovarianceDevice()
+        torch.cuda.synchronize()
+        self.centred_ms = (time.perf_counter() - t0) * 1e3 / 3
+        self.form_diff = float((Gc - self.G).abs().max() / Gc.abs().max())
+        self.mat.covarianceForm = "auto"
 
     def extra_roofline(self, launches_per_step, avg_s):
         return {"eigensolve_ms": self.eig_ms, "explained_variance_top3": self.explained_top3,
-                "note": "step = computeCovariance on the device (mean pass, isSparseMatrix "
-                        "take(1), centred syrk, finish); the host SVD is timed once, outside"}
+                "covariance_form": self.form, "centred_form_ms_per_step": self.centred_ms,
+                "forms_max_rel_diff": self.form_diff,
+                "covariance_passes": self.passes,
+                "note": "step = computeCovariance on the device (isSparseMatrix take(1), the "
+                        "passes of covariance_passes, finish); the reference's centred "
+                        "form timed after the steps (3 steps); the host SVD timed once, outside"}
 
     def describe(self):
         return (f"RowMatrix.computeCovariance (PCA variant), dense fp64 {self.n} x {self.p} rows "

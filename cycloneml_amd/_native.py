@@ -83,10 +83,13 @@ SIGNATURES = {
     "cyc_gramian_plan_destroy": (ctypes.c_int, [_vp]),
     "cyc_gramian_accumulate_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "cyc_col_sums_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp]),
+    "cyc_col_moments_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    "cyc_gramian_accumulate_sums_dev": (ctypes.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "cyc_triu_to_full_dev": (ctypes.c_int, [_i32, _vp, _vp, _vp]),
     "cyc_covariance_finalize_dev": (ctypes.c_int, [_i32, _vp, _i64, _vp, _vp]),
     "cyc_gramian_accumulate_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "cyc_col_sums_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "cyc_col_moments_csr_dev": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "cyc_rowmatrix_dense_rows_dev": (ctypes.c_int, [_vp, _vp, _vp, _i64, ctypes.c_int32, _vp,
                                                     _vp]),
     "cyc_sparse_covariance_finalize_dev": (ctypes.c_int, [ctypes.c_int32, _vp, _i64, _vp, _vp,

@@ -26,6 +26,7 @@
 
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -186,11 +187,23 @@ __global__ __launch_bounds__(GT, 2) void k_gram_tiles(
 // XCD grouping.  Measured slower: 555.2 vs 548.4 ms at 30M x 1024 (29
 // Gramian tests green with it); the centring pass doubles the chunk's LDS
 // traffic and sits between the DMA wait and the barrier.
+// SUMS (plain form only): the column sums ride the syrk.  On a diagonal
+// tile the wave of rows 64..127 x columns 0..63 computes entries the fold
+// discards (below the diagonal); in the SUMS form it runs 8 MFMAs per k-step
+// instead of 16, each with one operand the constant 1.0: acc[q][q] += 1 x
+// B[q] (the column sums of panel columns q*16 .. q*16+15, every output row
+// the same) and acc[q][q+1 mod 4] += A[q] x 1 (columns 64 + q*16 ..), and
+// writes the tile's 128 sums to sumsSlab[split][tile][128]
+// (k_gram_sums_fold).  The other waves run the plain loop.  (Adding the
+// rows with VALU from LDS on the diagonal workgroups cost 35-50 ms of 489:
+// the reads either waited out the DMA prefetch or stalled the wave.)
 template <int MEAN, int KCH = 8, int NB = 2, int OCC = 3,
-          bool XCDMAP = MEAN != 1 && CYC_GRAM_XCDMAP>
+          bool XCDMAP = MEAN != 1 && CYC_GRAM_XCDMAP, bool SUMS = false>
 __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
     const double* __restrict__ X, int64_t nrows, int p, const double* __restrict__ mean,
-    int tilesPerSide, int64_t rowsPerSplit, int splits, double* __restrict__ slab) {
+    int tilesPerSide, int64_t rowsPerSplit, int splits, double* __restrict__ slab,
+    double* __restrict__ sumsSlab) {
+  static_assert(!SUMS || MEAN == 0, "column sums ride the plain form only");
   __shared__ __attribute__((aligned(16))) double lds[NB * 2 * KCH * LDSW];   // the chunk panels
   auto Pn = [&](int b, int pn) { return lds + (b * 2 + pn) * KCH * LDSW; };
   constexpr int DPW = KCH / 2;   // DMAs per wave per chunk
@@ -266,7 +279,8 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
   // with it: 507.7 vs 488.6 ms.)
   const bool idle = CYC_GRAM_SKIPLOW && MEAN == 1 && ti == tj && wy > wx;
   const bool tri = CYC_GRAM_SKIPLOW >= 2 && MEAN == 1 && ti == tj && wy == wx;
-  auto compute = [&](int b) {
+  const bool sumsWave = SUMS && ti == tj && wy > wx && sumsSlab;   // wave-uniform
+  auto compute = [&](int b, auto asSums) {
     if (idle) return;
     const double* Ai = Pn(b, 0);
     const double* Aj = Pn(b, 1);
@@ -286,12 +300,22 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
           bb[q] = dsub(bb[q], mJ[q]);
         }
       }
+      if constexpr (decltype(asSums)::value) {
 #pragma unroll
-      for (int qa = 0; qa < 4; ++qa)
+        for (int q = 0; q < 4; ++q) {
+          acc[q][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(1.0, bb[q], acc[q][q], 0, 0, 0);
+          acc[q][(q + 1) & 3] =
+              __builtin_amdgcn_mfma_f64_16x16x4f64(a[q], 1.0, acc[q][(q + 1) & 3], 0, 0, 0);
+        }
+      } else {
 #pragma unroll
-        for (int qb = 0; qb < 4; ++qb)
-          if (qa <= qb || !tri)
-            acc[qa][qb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[qa], bb[qb], acc[qa][qb], 0, 0, 0);
+        for (int qa = 0; qa < 4; ++qa)
+#pragma unroll
+          for (int qb = 0; qb < 4; ++qb)
+            if (qa <= qb || !tri)
+              acc[qa][qb] =
+                  __builtin_amdgcn_mfma_f64_16x16x4f64(a[qa], bb[qb], acc[qa][qb], 0, 0, 0);
+      }
     }
   };
   // NB - 1 chunks ahead; past the end the DMAs fetch nothing (empty
@@ -322,19 +346,37 @@ __global__ __launch_bounds__(GT, OCC) void k_gram_dma(
       }
     }
   };
+  // the loop as one straight block per form (a branch inside it splits the
+  // block); the sums wave meets the same barriers the same number of times
+  auto mainLoop = [&](auto asSums) {
 #pragma unroll
-  for (int c = 0; c < NB - 1; ++c) issue(r0 + c * KCH, c);
-  int b = 0;
-  for (int64_t rb = r0; rb < r1; rb += KCH) {
-    if constexpr (NB == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * DPW) : "memory");
-    if constexpr (MEAN == 2) centre(b);
-    __syncthreads();   // chunk rb landed (centred) everywhere; every wave is past rb - KCH
-    issue(rb + (NB - 1) * KCH, b == 0 ? NB - 1 : b - 1);
-    compute(b);
-    b = b == NB - 1 ? 0 : b + 1;
-  }
+    for (int c = 0; c < NB - 1; ++c) issue(r0 + c * KCH, c);
+    int b = 0;
+    for (int64_t rb = r0; rb < r1; rb += KCH) {
+      if constexpr (NB == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * DPW) : "memory");
+      if constexpr (MEAN == 2) centre(b);
+      __syncthreads();   // chunk rb landed (centred) everywhere; every wave is past rb - KCH
+      issue(rb + (NB - 1) * KCH, b == 0 ? NB - 1 : b - 1);
+      compute(b, asSums);
+      b = b == NB - 1 ? 0 : b + 1;
+    }
+  };
+  if (sumsWave) mainLoop(std::true_type{});
+  else mainLoop(std::false_type{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (sumsWave) {
+    // acc[q][q]: column q*16 + (lane & 15), the same in every row r;
+    // acc[q][q+1]: column 64 + q*16 + (lane >> 4) + 4r, the same in every lane & 15
+    double* ts = sumsSlab + ((size_t)split * tilesPerSide + ti) * TILE;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (lane < 16) ts[q * 16 + lane] = acc[q][q][0];
+      if ((lane & 15) == 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ts[64 + q * 16 + (lane >> 4) + 4 * r] = acc[q][(q + 1) & 3][r];
+    }
+  }
 
   double* out = slab + ((size_t)split * pairs + pair) * TILE * TILE;
 #pragma unroll
@@ -368,6 +410,16 @@ __global__ void k_gram_fold(const double* __restrict__ slab, int splits, int til
   U[idx] = dadd(U[idx], s);
 }
 
+// sums[c] += the column sums of k_gram_dma<..., SUMS>, over splits in order.
+__global__ void k_gram_sums_fold(const double* __restrict__ part, int splits, int tilesPerSide,
+                                 int p, double* __restrict__ sums) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= p) return;
+  double s = 0.0;
+  for (int sp = 0; sp < splits; ++sp) s = dadd(s, part[(size_t)sp * tilesPerSide * TILE + c]);
+  sums[c] = dadd(sums[c], s);
+}
+
 // RowMatrix.triuToFull (:845-867): column-major full matrix from packed upper.
 __global__ void k_triu_to_full(int n, const double* __restrict__ U, double* __restrict__ G) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -389,16 +441,24 @@ __global__ void k_cov_finalize(int n, const double* __restrict__ U, double m1,
 // row), one partial per (split, column); folded in split order.  Feeds the
 // mean of Statistics.colStats (mllib/stat/Statistics.scala:57) used by
 // RowMatrix.computeCovariance (:452-467).
+// SQ: the sums of squares beside them (the same rows, same order; the sums
+// are the same bits either way), in the second half of the partials.
+template <bool SQ>
 __global__ void k_col_partial(const double* __restrict__ X, int64_t nrows, int p,
                               int64_t rowsPerSplit, double* __restrict__ part) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= p) return;
   const int64_t r0 = (int64_t)blockIdx.y * rowsPerSplit;
   const int64_t r1 = min<int64_t>(nrows, r0 + rowsPerSplit);
-  double s = 0.0;
+  double s = 0.0, q = 0.0;
   // nontemporal: the rows stream through once
-  for (int64_t r = r0; r < r1; ++r) s = dadd(s, __builtin_nontemporal_load(&X[r * p + c]));
+  for (int64_t r = r0; r < r1; ++r) {
+    const double x = __builtin_nontemporal_load(&X[r * p + c]);
+    s = dadd(s, x);
+    if constexpr (SQ) q = dadd(q, dmul(x, x));
+  }
   part[(int64_t)blockIdx.y * p + c] = s;
+  if constexpr (SQ) part[((int64_t)gridDim.y + blockIdx.y) * p + c] = q;
 }
 
 __global__ void k_col_fold(const double* __restrict__ part, int splits, int p,
@@ -487,14 +547,15 @@ struct cyc_gramian_plan_s {
   std::mutex mu;
   cyc::DeviceBuffer slab;
   cyc::DeviceBuffer chunk;   // densified CSR rows
+  cyc::DeviceBuffer sumSlab;  // k_gram_dma<..., SUMS> column-sum partials
 };
 
 namespace {
 
 int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, const double* mean,
-                      double* U, hipStream_t st);
+                      double* U, double* sums, hipStream_t st);
 int col_sums_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
-                    hipStream_t st);
+                    double* sumsq, hipStream_t st);
 
 // CSR rows in chunks of about 1 GiB of dense rows: densify, then `dense`.
 template <class F>
@@ -547,7 +608,17 @@ int cyc_gramian_accumulate_dev(cyc_gramian_plan plan, const double* X, int64_t n
   CYC_REQUIRE(nrows >= 0, "nrows >= 0");
   if (nrows == 0) return CYC_OK;
   std::lock_guard<std::mutex> g(plan->mu);
-  return accumulate_locked(plan, X, nrows, mean, U, cyc::as_stream(stream));
+  return accumulate_locked(plan, X, nrows, mean, U, nullptr, cyc::as_stream(stream));
+}
+
+int cyc_gramian_accumulate_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows,
+                                    double* U, double* sums, void* stream) {
+  CYC_REQUIRE(plan != nullptr && U != nullptr && sums != nullptr,
+              "plan, U and sums must not be null");
+  CYC_REQUIRE(nrows >= 0, "nrows >= 0");
+  if (nrows == 0) return CYC_OK;
+  std::lock_guard<std::mutex> g(plan->mu);
+  return accumulate_locked(plan, X, nrows, nullptr, U, sums, cyc::as_stream(stream));
 }
 
 int cyc_gramian_accumulate_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr,
@@ -561,21 +632,27 @@ int cyc_gramian_accumulate_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr,
   if (int rc = cyc::check_csr_indices(rowptr, colidx, nrows, plan->p, st)) return rc;
   std::lock_guard<std::mutex> g(plan->mu);
   return over_csr_chunks(plan, rowptr, colidx, vals, nrows, st, [&](const double* D, int64_t nr) {
-    return accumulate_locked(plan, D, nr, mean, U, st);
+    return accumulate_locked(plan, D, nr, mean, U, nullptr, st);
   });
 }
 
-int cyc_col_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
-                     void* stream) {
+int cyc_col_moments_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
+                        double* sumsq, void* stream) {
   CYC_REQUIRE(plan != nullptr && sums != nullptr, "plan and sums must not be null");
   CYC_REQUIRE(nrows >= 0, "nrows >= 0");
   if (nrows == 0) return CYC_OK;
   std::lock_guard<std::mutex> g(plan->mu);
-  return col_sums_locked(plan, X, nrows, sums, cyc::as_stream(stream));
+  return col_sums_locked(plan, X, nrows, sums, sumsq, cyc::as_stream(stream));
 }
 
-int cyc_col_sums_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr, const int32_t* colidx,
-                         const double* vals, int64_t nrows, double* sums, void* stream) {
+int cyc_col_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
+                     void* stream) {
+  return cyc_col_moments_dev(plan, X, nrows, sums, nullptr, stream);
+}
+
+int cyc_col_moments_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr, const int32_t* colidx,
+                            const double* vals, int64_t nrows, double* sums, double* sumsq,
+                            void* stream) {
   CYC_REQUIRE(plan != nullptr && sums != nullptr, "plan and sums must not be null");
   CYC_REQUIRE(nrows >= 0, "nrows >= 0");
   if (nrows == 0) return CYC_OK;
@@ -584,8 +661,13 @@ int cyc_col_sums_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr, const int
   if (int rc = cyc::check_csr_indices(rowptr, colidx, nrows, plan->p, st)) return rc;
   std::lock_guard<std::mutex> g(plan->mu);
   return over_csr_chunks(plan, rowptr, colidx, vals, nrows, st, [&](const double* D, int64_t nr) {
-    return col_sums_locked(plan, D, nr, sums, st);
+    return col_sums_locked(plan, D, nr, sums, sumsq, st);
   });
+}
+
+int cyc_col_sums_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr, const int32_t* colidx,
+                         const double* vals, int64_t nrows, double* sums, void* stream) {
+  return cyc_col_moments_csr_dev(plan, rowptr, colidx, vals, nrows, sums, nullptr, stream);
 }
 
 int cyc_rowmatrix_dense_rows_dev(const double* X, const int64_t* rowptr, const double* vals,
@@ -647,7 +729,7 @@ int cyc_covariance_finalize_dev(int32_t n, const double* U, int64_t m, double* G
 namespace {
 
 int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, const double* mean,
-                      double* U, hipStream_t st) {
+                      double* U, double* sums, hipStream_t st) {
   const int p = plan->p;
   const int tps = (p + TILE - 1) / TILE;
   const int pairs = tps * (tps + 1) / 2;
@@ -674,6 +756,12 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   splits = (nrows + rps - 1) / rps;
   int rc = plan->slab.reserve(sizeof(double) * (size_t)splits * pairs * TILE * TILE);
   if (rc) return rc;
+  // the column sums ride the plain k_gram_dma; other forms add a pass
+  const bool fusedSums = sums && dma && !mean;
+  if (fusedSums) {
+    rc = plan->sumSlab.reserve(sizeof(double) * (size_t)splits * tps * TILE);
+    if (rc) return rc;
+  }
   {
   // timed under the name of the kernel that runs (rocprofv3 lists the
   // covariance instances as k_gram_dma too)
@@ -683,15 +771,19 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   // (XCDMAP)
   const dim3 gridD = CYC_GRAM_XCDMAP ? dim3((unsigned)(pairs * ((splits + 7) / 8) * 8)) : grid;
   double* slab = (double*)plan->slab.ptr;
+  double* sumSlab = (double*)plan->sumSlab.ptr;
   if (dma && operand)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<1, 16, 2, 2>), grid, dim3(GT), 0, st, X,
-                       nrows, p, mean, tps, rps, (int)splits, slab);
+                       nrows, p, mean, tps, rps, (int)splits, slab, nullptr);
   else if (dma && mean)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<2>), gridD, dim3(GT), 0, st, X, nrows, p,
-                       mean, tps, rps, (int)splits, slab);
+                       mean, tps, rps, (int)splits, slab, nullptr);
+  else if (fusedSums)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<0, 8, 2, 3, CYC_GRAM_XCDMAP, true>), gridD,
+                       dim3(GT), 0, st, X, nrows, p, mean, tps, rps, (int)splits, slab, sumSlab);
   else if (dma)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_gram_dma<0>), gridD, dim3(GT), 0, st, X, nrows, p,
-                       mean, tps, rps, (int)splits, slab);
+                       mean, tps, rps, (int)splits, slab, nullptr);
   else
     hipLaunchKernelGGL(k_gram_tiles, grid, dim3(GT), 0, st, X, nrows, p, mean, tps, rps, slab);
   CYC_LAUNCH_CHECK("k_gram_dma / k_gram_tiles");
@@ -699,25 +791,42 @@ int accumulate_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, con
   hipLaunchKernelGGL(k_gram_fold, dim3(TILE * TILE / 256, pairs), dim3(256), 0, st,
                      (const double*)plan->slab.ptr, (int)splits, tps, p, U);
   CYC_LAUNCH_CHECK("k_gram_fold");
+  if (fusedSums) {
+    hipLaunchKernelGGL(k_gram_sums_fold, dim3((p + 255) / 256), dim3(256), 0, st,
+                       (const double*)plan->sumSlab.ptr, (int)splits, tps, p, sums);
+    CYC_LAUNCH_CHECK("k_gram_sums_fold");
+  } else if (sums) {
+    return col_sums_locked(plan, X, nrows, sums, nullptr, st);
+  }
   return CYC_OK;
 }
 
 int col_sums_locked(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
-                    hipStream_t st) {
+                    double* sumsq, hipStream_t st) {
   const int p = plan->p;
   const int ctiles = (p + 255) / 256;
   int64_t splits = std::max<int64_t>(1, std::min<int64_t>(4096 / ctiles, nrows / 256));
   const int64_t rps = (nrows + splits - 1) / splits;
   splits = (nrows + rps - 1) / rps;
-  int rc = plan->slab.reserve(sizeof(double) * (size_t)splits * p);
+  int rc = plan->slab.reserve(sizeof(double) * (size_t)splits * p * (sumsq ? 2 : 1));
   if (rc) return rc;
+  double* part = (double*)plan->slab.ptr;
   cyc::KernelTimer timer("k_col_sums", st);
-  hipLaunchKernelGGL(k_col_partial, dim3(ctiles, (unsigned)splits), dim3(256), 0, st, X, nrows, p,
-                     rps, (double*)plan->slab.ptr);
+  if (sumsq)
+    hipLaunchKernelGGL(k_col_partial<true>, dim3(ctiles, (unsigned)splits), dim3(256), 0, st, X,
+                       nrows, p, rps, part);
+  else
+    hipLaunchKernelGGL(k_col_partial<false>, dim3(ctiles, (unsigned)splits), dim3(256), 0, st, X,
+                       nrows, p, rps, part);
   CYC_LAUNCH_CHECK("k_col_partial");
-  hipLaunchKernelGGL(k_col_fold, dim3(ctiles), dim3(256), 0, st, (const double*)plan->slab.ptr,
+  hipLaunchKernelGGL(k_col_fold, dim3(ctiles), dim3(256), 0, st, (const double*)part,
                      (int)splits, p, sums);
   CYC_LAUNCH_CHECK("k_col_fold");
+  if (sumsq) {
+    hipLaunchKernelGGL(k_col_fold, dim3(ctiles), dim3(256), 0, st,
+                       (const double*)part + splits * p, (int)splits, p, sumsq);
+    CYC_LAUNCH_CHECK("k_col_fold");
+  }
   return CYC_OK;
 }
 

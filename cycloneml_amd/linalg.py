@@ -12,6 +12,7 @@ PCA stays on the host (breeze svd on the driver in the reference, :501).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -58,6 +59,16 @@ class GramianPlan:
     def col_sums(self, X, out, stream=None):
         N.check(self._lib.cyc_col_sums_dev(self.handle, N.ptr(X), int(X.shape[0]), N.ptr(out),
                                            N.stream_handle(stream)))
+
+    def col_moments(self, X, sums, sumsq, stream=None):
+        N.check(self._lib.cyc_col_moments_dev(self.handle, N.ptr(X), int(X.shape[0]),
+                                              N.ptr(sums), N.ptr(sumsq),
+                                              N.stream_handle(stream)))
+
+    def col_moments_csr(self, rows: "CSRRows", sums, sumsq, stream=None):
+        N.check(self._lib.cyc_col_moments_csr_dev(
+            self.handle, N.ptr(rows.rowptr), N.ptr(rows.colidx), N.ptr(rows.values), rows.n,
+            N.ptr(sums), N.ptr(sumsq), N.stream_handle(stream)))
 
     def accumulate_csr(self, rows: "CSRRows", U, mean=None, stream=None):
         N.check(self._lib.cyc_gramian_accumulate_csr_dev(
@@ -187,16 +198,138 @@ class RowMatrix:
             self.close()
 
     def _column_mean(self):
+        mean, m, _ = self._column_moments(squares=False)
+        return mean, m
+
+    def _column_moments(self, squares=True, rows=None):
+        """(mean, m, sum of squares or None): the colStats pass (:456) -- the
+        column sums, and beside them in the same pass the sums of squares
+        -- merged over ranks; over `rows` (a leading slice of this shard,
+        with m their count over ranks) when given."""
         torch = _torch()
         n = self.numCols()
-        s = torch.zeros(n, dtype=torch.float64, device=self._device)
+        s = torch.zeros(2 * n + 1 if squares else n, dtype=torch.float64, device=self._device)
+        sq = s[n:2 * n] if squares else None
+        rows = self.rows if rows is None else rows
         if self._sparse:
-            self._plan().col_sums_csr(self.rows, s)
+            self._plan().col_moments_csr(rows, s[:n], sq)
         else:
-            self._plan().col_sums(self.rows, s)
-        parallel.allreduce_(s)
-        m = self.numRows()
-        return s / m, m
+            self._plan().col_moments(rows, s[:n], sq)
+        if rows is self.rows:
+            parallel.allreduce_(s)         # one all-reduce for both
+            m = self.numRows()
+        else:
+            s[2 * n] = rows.n if self._sparse else int(rows.shape[0])
+            parallel.allreduce_(s)
+            m = int(s[2 * n].item())
+        return s[:n] / max(m, 1), m, sq
+
+    def _packed_sums(self):
+        """(U, sums): the plain syrk with the column sums riding it (one pass
+        over dense rows, cyc_gramian_accumulate_sums_dev; CSR rows add the
+        column-sum pass), merged over ranks in one all-reduce."""
+        torch = _torch()
+        n = self.numCols()
+        nt = n * (n + 1) // 2
+        B = torch.zeros(nt + n, dtype=torch.float64, device=self._device)
+        U, S = B[:nt], B[nt:]
+        plan = self._plan()
+        if self._sparse:
+            plan.accumulate_csr(self.rows, U)
+            plan.col_sums_csr(self.rows, S)
+        else:
+            N.check(plan._lib.cyc_gramian_accumulate_sums_dev(
+                plan.handle, N.ptr(self.rows), int(self.rows.shape[0]), N.ptr(U), N.ptr(S),
+                N.stream_handle()))
+        parallel.allreduce_(B)
+        return U, S
+
+    # computeCovariance's dense form: "auto" (below), "centred" (the
+    # reference's centred spr, always) or "uncentred" (the Gramian finish,
+    # always; for tests).  CYC_COV_FORM sets the default.
+    covarianceForm = os.environ.get("CYC_COV_FORM", "auto")
+    # the uncentred form needs mean^2 <= COV_MEAN_RATIO2 * variance in every
+    # column; "auto" first checks the leading COV_SAMPLE_ROWS rows of each
+    # shard to pick the pass order
+    COV_MEAN_RATIO2 = 64.0
+    COV_SAMPLE_ROWS = 1 << 16
+
+    def _near_centred(self, mean, sumsq, m) -> bool:
+        """The bound that lets the dense covariance skip the centring.  The
+        reference centres every row (computeDenseVectorCovariance,
+        :163-220) so that a large mean cannot cancel; the uncentred Gramian
+        finish -- the reference's own computeSparseVectorCovariance formula
+        (:222-246), G / (m-1) - m/(m-1) mean_i mean_j -- costs the plain syrk
+        instead of the centred one, and its cancellation is bounded by the
+        data: sum x_i^2 = (m-1) var_i + m mean_i^2, so with mean_i^2 <= R
+        var_i for every column the rounding error of each entry is at most
+        (1 + R m/(m-1)) times the centred form's, in units of sqrt(var_i
+        var_j) (R = 64: ~65x an error of a few ulp, far inside the 1e-10 the
+        parity tests hold).  A column failing it (a large mean, zero
+        variance, NaN/Inf) keeps the whole matrix centred.  Every rank sees
+        the same merged moments, so every rank decides the same."""
+        var = (sumsq - m * mean * mean) / (m - 1)
+        return bool((mean * mean <= self.COV_MEAN_RATIO2 * var).all().item())
+
+    def _dense_covariance(self, m, G):
+        """The dense covariance into G; returns (form, passes over the rows).
+        "auto": the leading rows' moments choose the order --
+          near-centred: the plain syrk with the column sums riding it, the
+          exact bound from its diagonal (sum x_i^2) and sums, and the
+          centred syrk after it only if the whole matrix fails the bound;
+          otherwise: the moments pass, then the form the bound allows."""
+        torch = _torch()
+        n = self.numCols()
+        form = self.covarianceForm
+        if form not in ("auto", "centred", "uncentred"):
+            raise N.IllegalArgumentException(f"covarianceForm {form!r}: auto, centred or "
+                                             "uncentred")
+        lib = N.load()
+        passes = []
+
+        def centred(mean):
+            passes.append("centred syrk")
+            U = self._packed(mean)
+            N.check(lib.cyc_covariance_finalize_dev(int(n), N.ptr(U), int(m), N.ptr(G),
+                                                    N.stream_handle()))
+            return "centred", passes
+
+        def uncentred(U, mean):
+            N.check(lib.cyc_sparse_covariance_finalize_dev(int(n), N.ptr(U), int(m),
+                                                           N.ptr(mean), N.ptr(G),
+                                                           N.stream_handle()))
+            return "uncentred", passes
+
+        if form == "centred":
+            passes.append("column sums")
+            return centred(self._column_moments(squares=False)[0])
+        sample_ok = form == "uncentred"
+        if form == "auto":
+            k = min(self._local_rows(), self.COV_SAMPLE_ROWS)
+            if self._sparse:
+                r = self.rows
+                head = CSRRows(r.rowptr[:k + 1], r.colidx, r.values, r.numCols)
+            else:
+                head = self.rows[:k]
+            passes.append(f"moments of the leading {k} rows")
+            ms, mk, sqs = self._column_moments(rows=head)
+            sample_ok = mk > 1 and self._near_centred(ms, sqs, mk)
+        if sample_ok:
+            passes.append("syrk + column sums")
+            U, S = self._packed_sums()
+            mean = S / m
+            if form == "uncentred":
+                return uncentred(U, mean)
+            i = torch.arange(n, device=self._device)
+            if self._near_centred(mean, U[i * (i + 1) // 2 + i], m):
+                return uncentred(U, mean)
+            return centred(mean)
+        passes.append("column moments")
+        mean, _, sumsq = self._column_moments()
+        if self._near_centred(mean, sumsq, m):
+            passes.append("syrk")
+            return uncentred(self._packed(), mean)
+        return centred(mean)
 
     # rows of the first isSparseMatrix round per rank, and the growth factor
     SPARSITY_SCAN_FIRST = 1 << 16
@@ -245,7 +378,10 @@ class RowMatrix:
     def computeCovariance(self) -> np.ndarray:
         """RowMatrix.scala:452-467: computeDenseVectorCovariance (:163-220) or,
         when every row has sparsity >= 0.5, computeSparseVectorCovariance
-        (:222-246) from the Gramian."""
+        (:222-246) from the Gramian.  The dense form is the centred syrk, or
+        the Gramian finish when the column moments bound its cancellation
+        (_near_centred, _dense_covariance); lastCovarianceForm names the one
+        that ran, lastCovariancePasses the passes over the rows."""
         try:
             return self.computeCovarianceDevice().cpu().numpy()
         finally:
@@ -257,20 +393,21 @@ class RowMatrix:
         torch = _torch()
         n = self.numCols()
         self._checkNumColumns(n)
-        mean, m = self._column_mean()
+        m = self.numRows()
         if not m > 1:
             raise N.IllegalArgumentException(
                 f"RowMatrix.computeCovariance called on matrix with only {m} rows.  Cannot "
                 "compute the covariance of a RowMatrix with <= 1 row.")
         G = torch.empty(n * n, dtype=torch.float64, device=self._device)
         if not self.isSparseMatrix():
-            U = self._packed(mean)
-            N.check(N.load().cyc_covariance_finalize_dev(int(n), N.ptr(U), int(m), N.ptr(G),
-                                                         N.stream_handle()))
-        else:
+            form, passes = self._dense_covariance(m, G)
+        else:                              # the Gramian finish (:222-246)
+            mean = self._column_mean()[0]
             U = self._packed()
             N.check(N.load().cyc_sparse_covariance_finalize_dev(
                 int(n), N.ptr(U), int(m), N.ptr(mean), N.ptr(G), N.stream_handle()))
+            form, passes = "sparse", ["column sums", "syrk"]
+        self.lastCovarianceForm, self.lastCovariancePasses = form, passes
         return G.view(n, n).t()
 
     def computePrincipalComponentsAndExplainedVariance(self, k: int):

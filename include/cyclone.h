@@ -249,10 +249,21 @@ int cyc_gramian_plan_create(int32_t ncols, cyc_gramian_plan* plan);
 int cyc_gramian_plan_destroy(cyc_gramian_plan plan);
 int cyc_gramian_accumulate_dev(cyc_gramian_plan plan, const double* X, int64_t nrows,
                                const double* mean, double* U, void* stream);
+/* U += sum_r x_r x_r^T and sums[c] += sum_r X[r][c] in one pass over the rows
+ * (the column sums ride the syrk's diagonal tiles; sums are the same values
+ * as cyc_col_sums_dev's to rounding, not the same bits): the uncentred
+ * covariance form of RowMatrix.computeCovariance (covariance). */
+int cyc_gramian_accumulate_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows,
+                                    double* U, double* sums, void* stream);
 /* sums[c] += sum over rows of X[r][c] (fixed order): the mean pre-pass of
  * RowMatrix.computeCovariance (Statistics.colStats, :456). */
 int cyc_col_sums_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
                      void* stream);
+/* The same pass with sumsq[c] += sum over rows of X[r][c]^2 beside it (sums
+ * bit-identical to cyc_col_sums_dev; sumsq may be NULL): the column
+ * variances that choose computeCovariance's form (covariance). */
+int cyc_col_moments_dev(cyc_gramian_plan plan, const double* X, int64_t nrows, double* sums,
+                        double* sumsq, void* stream);
 /* RowMatrix.triuToFull (:845-867): G (n x n column-major) from U. */
 int cyc_triu_to_full_dev(int32_t n, const double* U, double* G, void* stream);
 /* computeDenseVectorCovariance's finish (:203-217): G = full(U) / (m - 1). */
@@ -267,6 +278,9 @@ int cyc_gramian_accumulate_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr,
                                    const double* mean, double* U, void* stream);
 int cyc_col_sums_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr, const int32_t* colidx,
                          const double* vals, int64_t nrows, double* sums, void* stream);
+int cyc_col_moments_csr_dev(cyc_gramian_plan plan, const int64_t* rowptr, const int32_t* colidx,
+                            const double* vals, int64_t nrows, double* sums, double* sumsq,
+                            void* stream);
 /* RowMatrix.isSparseMatrix (:439-441): *count (device int64) = rows whose
  * sparsity() = 1 - numNonzeros / ncols is below 0.5, over dense X OR CSR
  * (rowptr, vals); the matrix is sparse iff the count (summed over ranks) is 0. */

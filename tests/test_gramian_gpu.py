@@ -62,17 +62,86 @@ def test_gramian_vs_oracle(cuda, n, p):
     np.testing.assert_allclose(U, R, rtol=1e-12)
 
 
+@pytest.mark.parametrize("form", ["auto", "centred", "uncentred"])
 @pytest.mark.parametrize("n,p", [(500, 7), (4000, 200), (13, 2), (1001, 130)])
-def test_covariance_vs_oracle(cuda, n, p):
+def test_covariance_vs_oracle(cuda, n, p, form):
+    """Both dense forms against the reference's centred restatement (mean
+    3 sigma: "auto" takes the uncentred Gramian finish)."""
     from cycloneml_amd.linalg import RowMatrix
     rng = np.random.default_rng(p)
     X = rng.normal(size=(n, p)) + 3.0
-    cov = RowMatrix(_dev(X, cuda)).computeCovariance()
+    mat = RowMatrix(_dev(X, cuda))
+    mat.covarianceForm = form
+    cov = mat.computeCovariance()
+    assert mat.lastCovarianceForm == ("uncentred" if form == "auto" else form)
     mean = X.sum(0) / n
     U = oracle.gramian_partition(X, mean)
     ref = oracle.triu_to_full(p, U).reshape(p, p).T / (n - 1.0)
     np.testing.assert_allclose(cov, ref, rtol=1e-10, atol=1e-12)
     assert (cov == cov.T).all()   # SPARK-10875 symmetry
+
+
+def _cov_ref(X):
+    n, p = X.shape
+    U = oracle.gramian_partition(X, X.sum(0) / n)
+    return np.asarray(oracle.triu_to_full(p, U)).reshape(p, p).T / (n - 1.0)
+
+
+def test_covariance_form_choice(cuda):
+    """RowMatrix._near_centred / _dense_covariance: the uncentred finish
+    only when every column has mean^2 <= 64 variance; a large mean, a
+    constant nonzero column or a NaN keep the reference's centred syrk; at
+    the bound the uncentred result still meets the 1e-10 parity bar
+    (norm-wise).  Leading rows that pass while the whole matrix fails take
+    the fused pass, then the centred syrk."""
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.linalg import RowMatrix
+    rng = np.random.default_rng(5)
+    n, p = 3000, 40
+    base = rng.normal(size=(n, p))
+    base = (base - base.mean(0)) / base.std(0, ddof=1)    # mean 0, variance 1 exactly-ish
+    cases = [(base + 7.9, "uncentred"), (base + 8.1, "centred"), (base * 1e-3 + 1e6, "centred")]
+    const = base.copy()
+    const[:, 3] = 2.5
+    cases.append((const, "centred"))
+    zero = base.copy()
+    zero[:, 3] = 0.0
+    cases.append((zero, "uncentred"))
+    for X, want in cases:
+        mat = RowMatrix(_dev(X, cuda))
+        cov = mat.computeCovariance()
+        assert mat.lastCovarianceForm == want
+        ref = _cov_ref(X)
+        np.testing.assert_allclose(cov, ref, rtol=1e-10, atol=1e-10 * np.abs(ref).max())
+    fused = ["moments of the leading 3000 rows", "syrk + column sums"]
+    mat = RowMatrix(_dev(base + 7.9, cuda))
+    mat.computeCovariance()
+    assert mat.lastCovariancePasses == fused
+    mat = RowMatrix(_dev(base + 8.1, cuda))
+    mat.computeCovariance()
+    assert mat.lastCovariancePasses == ["moments of the leading 3000 rows", "column moments",
+                                        "centred syrk"]
+    # the leading 16 rows near-centred, the rest far off: fused pass, exact
+    # bound fails, centred syrk
+    misled = base * 1e-3 + 1e6
+    misled[:16] = base[:16]
+    mat = RowMatrix(_dev(misled, cuda))
+    mat.COV_SAMPLE_ROWS = 16
+    cov = mat.computeCovariance()
+    assert mat.lastCovarianceForm == "centred"
+    assert mat.lastCovariancePasses == ["moments of the leading 16 rows", "syrk + column sums",
+                                        "centred syrk"]
+    ref = _cov_ref(misled)
+    np.testing.assert_allclose(cov, ref, rtol=1e-10, atol=1e-10 * np.abs(ref).max())
+    nan = base.copy()
+    nan[7, 2] = np.nan
+    mat = RowMatrix(_dev(nan, cuda))
+    cov = mat.computeCovariance()
+    assert mat.lastCovarianceForm == "centred" and np.isnan(cov[2]).all()
+    mat = RowMatrix(_dev(base, cuda))
+    mat.covarianceForm = "both"
+    with pytest.raises(N.IllegalArgumentException, match="covarianceForm"):
+        mat.computeCovariance()
 
 
 def test_gramian_accumulates_and_checks_columns(cuda):
@@ -174,15 +243,17 @@ def test_gramian_bench_shard(cuda, bench_gram_rows):
 def test_covariance_pca_bench_shard(cuda, bench_gram_rows):
     """The PCA variant of configs[2] at its shape, on the bench's rows
     (RowMatrix.computeCovariance, RowMatrix.scala:452-467 ->
-    computeDenseVectorCovariance :163-220, the centred syrk with 16-row
-    chunks and split-K over millions of rows; then
+    computeDenseVectorCovariance :163-220 -- the centred syrk with 16-row
+    chunks and split-K over millions of rows, and the uncentred Gramian
+    finish that "auto" picks for these rows; then
     computePrincipalComponentsAndExplainedVariance :486-513):
     - isSparseMatrix is false after its first round (take(1) semantics);
     - the centred packed sum equals its two unequal halves' (the whole
       shard's mean) within 1e-12 of its largest entry;
     - the first and the last 2000 rows' centred sums equal the restatement
       (x - mean, then netlib dspr per row) within 1e-10;
-    - the covariance is exactly symmetric, and Cov 1 equals
+    - both forms are exactly symmetric, the uncentred one within 1e-10 of
+      the centred one (norm-wise), and Cov 1 equals
       sum_r (x_r - mu) ((x_r - mu) . 1) / (m - 1) accumulated in 1M-row
       chunks (the identity (X^T (X 1) - m mu (mu . 1)) / (m - 1) without its
       cancellation) within 1e-11;
@@ -195,7 +266,11 @@ def test_covariance_pca_bench_shard(cuda, bench_gram_rows):
     n = int(X.shape[0])
     mat = RowMatrix(X)
     assert not mat.isSparseMatrix()
-    cov = mat.computeCovarianceDevice()
+    cov = mat.computeCovarianceDevice()          # U[0, 1): mean^2 = 3 variance
+    assert mat.lastCovarianceForm == "uncentred"
+    mat.covarianceForm = "centred"
+    cov_c = mat.computeCovarianceDevice()        # the reference's centred syrk
+    assert mat.lastCovarianceForm == "centred"
     torch.cuda.synchronize()
     mu = torch.zeros(p, dtype=torch.float64, device=cuda)
     for s in range(0, n, 1 << 20):
@@ -224,17 +299,24 @@ def test_covariance_pca_bench_shard(cuda, bench_gram_rows):
         cref = oracle.dense_vector_covariance(p, ref, 2000)
         cgot = oracle.dense_vector_covariance(p, got, 2000)
         np.testing.assert_allclose(cgot, cref, rtol=1e-10, atol=1e-10 * np.abs(cref).max())
-    C = cov.cpu().numpy()
+    C = cov_c.cpu().numpy()
     assert np.array_equal(C, C.T)                               # SPARK-10875
     np.testing.assert_allclose(C, oracle.dense_vector_covariance(p, U.cpu().numpy(), n),
                                rtol=1e-13, atol=0)
+    # the uncentred finish against the centred syrk: 1e-10 of the largest
+    # entry (the parity bar; the cancellation is bounded by mean^2 = 3 var)
+    Cu = cov.cpu().numpy()
+    assert np.array_equal(Cu, Cu.T)
+    np.testing.assert_allclose(Cu, C, rtol=1e-10, atol=1e-10 * np.abs(C).max())
     w = torch.zeros(p, dtype=torch.float64, device=cuda)
     for s in range(0, n, 1 << 20):
         xc = X[s:s + (1 << 20)] - mean
         w += xc.T @ xc.sum(1)
     w /= (n - 1.0)
-    np.testing.assert_allclose(C.sum(1), w.cpu().numpy(), rtol=1e-11,
-                               atol=1e-11 * float(w.abs().max()))
+    for CC in (C, Cu):
+        np.testing.assert_allclose(CC.sum(1), w.cpu().numpy(), rtol=1e-11,
+                                   atol=1e-11 * float(w.abs().max()))
+    mat.covarianceForm = "auto"
     pc, ev = mat.computePrincipalComponentsAndExplainedVariance(3)
     assert pc.shape == (p, 3) and ev.shape == (3,)
     np.testing.assert_allclose(np.linalg.norm(pc, axis=0), 1.0, rtol=1e-12)
