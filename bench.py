@@ -474,12 +474,12 @@ class PCAWorkload:
     driver in the reference; here it is the host eigensolve, timed once
     outside the steps (eigensolve_ms)."""
     kernels = ("k_gram_dma", "k_gram_dma_cov", "k_col_sums")
-    pmc_names = {"k_gram_dma_cov": "k_gram_dma"}
+    pmc_names = {"k_col_sums": "k_col_partial"}
 
     @property
-    def kernel(self):
-        return "k_gram_dma_cov" if getattr(self.mat, "lastCovarianceForm",
-                                           "centred") == "centred" else "k_gram_dma"
+    def kernel(self):   # the timed steps' form (after_timing runs the centred one after them)
+        form = getattr(self, "form", None) or getattr(self.mat, "lastCovarianceForm", "centred")
+        return "k_gram_dma_cov" if form == "centred" else "k_gram_dma"
 
     def __init__(self, n, dev, rank):
         from cycloneml_amd.linalg import RowMatrix
@@ -492,8 +492,15 @@ class PCAWorkload:
         self.G = self.mat.computeCovarianceDevice()
 
     def work(self, kname, launches_per_step):
-        if kname == "k_col_sums":             # every row once (fp64)
-            return float(self.n) * self.p * 8 / launches_per_step, HBM
+        if kname == "k_col_sums":             # the rows its passes read once (fp64)
+            rows = 0
+            for ps in getattr(self, "passes", None) or getattr(self.mat, "lastCovariancePasses",
+                                                                ["column sums"]):
+                if ps.startswith("moments of the leading"):
+                    rows += int(ps.split()[4])
+                elif ps in ("column moments", "column sums"):
+                    rows += self.n
+            return float(rows) * self.p * 8 / launches_per_step, HBM
         return float(self.n) * self.p * (self.p + 1) / launches_per_step, FP64   # flops (upper)
 
     def after_timing(self):
