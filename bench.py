@@ -474,7 +474,10 @@ class PCAWorkload:
     driver in the reference; here it is the host eigensolve, timed once
     outside the steps (eigensolve_ms)."""
     kernels = ("k_gram_dma", "k_gram_dma_cov", "k_col_sums")
-    pmc_names = {"k_col_sums": "k_col_partial"}
+    # no per-dispatch PMC figure for the column pass: the profiled
+    # k_col_partial dispatches mix the 64K-row sample with the centred
+    # comparison's whole-shard passes
+    pmc_names = {"k_col_sums": None}
 
     @property
     def kernel(self):   # the timed steps' form (after_timing runs the centred one after them)
