@@ -198,6 +198,39 @@ def _gramian_rank(rank, world):
     return bool(np.allclose(U.cpu().numpy(), oracle.gramian_partition(X), rtol=1e-12))
 
 
+def _covariance_rank(rank, world):
+    """RowMatrix.computeCovariance over two ranks' shards: the form chosen from
+    merged moments (the same on both ranks), the fused column sums and the
+    syrk all-reduced.  Rank 1's leading rows are far off centre while rank
+    0's are not: the merged leading-row moments and the whole matrix decide
+    together."""
+    import torch
+    from cycloneml_amd import parallel
+    from cycloneml_amd.linalg import RowMatrix
+    rng = np.random.default_rng(9)
+    n, p = 6001, 40
+    far = rng.normal(size=(n, p)) * 1e-3 + 1e5
+    far[:16] = rng.normal(size=(16, p))    # rank 0's leading rows near the origin
+    # uncentred on both ranks; then the 16-row samples (one centred, one far
+    # off) pass the bound together, the whole matrix does not: centred syrk
+    cases = [rng.normal(size=(n, p)) + 2.0, far]
+    ok = True
+    forms = []
+    for X in cases:
+        a, b = parallel.shard_bounds(n, rank, world)
+        mat = RowMatrix(torch.from_numpy(X[a:b].copy()).to("cuda:0"))
+        mat.COV_SAMPLE_ROWS = 16
+        cov = mat.computeCovariance()
+        U = oracle.gramian_partition(X, X.sum(0) / n)
+        ref = np.asarray(oracle.triu_to_full(p, U)).reshape(p, p).T / (n - 1.0)
+        ok = ok and bool(np.allclose(cov, ref, rtol=1e-10, atol=1e-10 * np.abs(ref).max()))
+        forms.append((mat.lastCovarianceForm, tuple(mat.lastCovariancePasses)))
+    mine = parallel.allgather_object(forms)
+    return bool(ok and [f for f, _ in forms] == ["uncentred", "centred"] and
+                forms[1][1][-2:] == ("syrk + column sums", "centred syrk") and
+                all(f == forms for f in mine))
+
+
 def _init_reference(X, dev, part_starts, shard_rows, k, s, mode):
     """The host composition of KMeans.initRandom / initKMeansParallel over all
     partitions (numbered in rank order), with sumCosts the rank-order sum of
@@ -375,8 +408,8 @@ def _silhouette_rank(rank, world):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("fn", [_kmeans_rank, _lr_rank, _gramian_rank, _kmeans_init_rank,
-                                _kmeans_init_csr_rank, _silhouette_rank])
+@pytest.mark.parametrize("fn", [_kmeans_rank, _lr_rank, _gramian_rank, _covariance_rank,
+                                _kmeans_init_rank, _kmeans_init_csr_rank, _silhouette_rank])
 def test_two_ranks_device_kernels_meet_the_collective(fn):
     out = _run(fn)
     assert out == {0: True, 1: True}, out
