@@ -578,8 +578,9 @@ class LRMultiWorkload:
         import numpy as np
         self.coef = np.random.default_rng(3).normal(size=C * F + C) * 0.01
         self.scaledMean = sm_dev.cpu().numpy()                     # bcScaledMean, once
+        inv_std = np.ones(F)                                      # bcInverseStd, once
         self.fn = RDDLossFunction([self.block], lambda c: MultinomialLogisticBlockAggregator(
-            np.ones(F), sm_dev, True, True, c, device=dev))
+            inv_std, sm_dev, True, True, c, device=dev))
 
     def step(self):
         self.fn.calculate(self.coef)
@@ -686,8 +687,9 @@ class LRSparseWorkload:
         # values U(0, 1) -- mean ~ 3.2e-5, std ~ 4.6e-3 -> scaledMean ~ 7e-3
         self.scaledMean = np.random.default_rng(5).uniform(0.0, 0.014, F)
         sm_dev = torch.as_tensor(self.scaledMean, device=dev)    # bcScaledMean, once
+        inv_std = np.ones(F)                                      # bcInverseStd, once
         self.fn = RDDLossFunction([self.block], lambda c: BinaryLogisticBlockAggregator(
-            np.ones(F), sm_dev, True, True, c, device=dev))
+            inv_std, sm_dev, True, True, c, device=dev))
 
     def step(self):
         self.fn.calculate(self.coef)

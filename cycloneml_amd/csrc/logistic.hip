@@ -1229,6 +1229,28 @@ int binary_offset(cyc_logistic_plan p, const double* coef, const double* scaledM
   return CYC_OK;
 }
 
+// The same offset left in HBM: *offDev points at it (nullptr without an
+// intercept: offset 0), no host copy and no stream sync.
+int binary_offset_dev(cyc_logistic_plan p, const double* coef, const double* scaledMean,
+                      hipStream_t st, const double** offDev) {
+  *offDev = nullptr;
+  if (!p->fitIntercept) return CYC_OK;
+  if (p->fitWithMean || p->loss == 2) {
+    if (int rc = p->offset.reserve(sizeof(double) * (2 + kOffParts))) return rc;
+    double* part = (double*)p->offset.ptr + 2;
+    hipLaunchKernelGGL(k_binlog_offset_part, dim3(kOffParts), dim3(256), 0, st, coef, scaledMean,
+                       p->F, part);
+    CYC_LAUNCH_CHECK("k_binlog_offset_part");
+    hipLaunchKernelGGL(k_binlog_offset, dim3(1), dim3(64), 0, st, (const double*)part, coef, p->F,
+                       p->loss == 2 ? 1 : 0, p->labelMean / p->labelStd, (double*)p->offset.ptr);
+    CYC_LAUNCH_CHECK("k_binlog_offset");
+    *offDev = (const double*)p->offset.ptr;
+  } else {
+    *offDev = coef + p->F;
+  }
+  return CYC_OK;
+}
+
 // kcoef: the coefficients the margins use when they differ from coef (least
 // squares' effectiveCoef); coef feeds the offset.
 int binary_add_dense(cyc_logistic_plan p, const double* X, const double* labels,
@@ -1430,8 +1452,10 @@ int cyc_binary_add_tiles_dev(cyc_logistic_plan p, cyc_tiles tiles, const double*
       (rc = p->slabS.reserve(sizeof(double) * (size_t)wgMax * 4)) ||
       (rc = p->scal.reserve(sizeof(double) * 4)) || (rc = p->offset.reserve(sizeof(double) * 2)))
     return rc;
-  double offset = 0.0;
-  if ((rc = binary_offset(p, coef, scaledMean, st, &offset))) return rc;
+  // the margin offset stays in HBM for k_tiles_rows: no host round trip
+  // (and no stream sync) before the margin pass
+  const double* offDev = nullptr;
+  if ((rc = binary_offset_dev(p, coef, scaledMean, st, &offDev))) return rc;
   const double lscale = -1.0 / p->labelStd;
   const int foldIcpt = p->loss == 2 ? 0 : p->fitIntercept;
   double sigma = 0.0;
@@ -1448,9 +1472,9 @@ int cyc_binary_add_tiles_dev(cyc_logistic_plan p, cyc_tiles tiles, const double*
   }
   {
     cyc::KernelTimer timer("k_tiles_rows", st);
-    if ((rc = cyc::tiles_rows(n, labels, weights, p->fitIntercept, p->loss, offset, lscale, sigma,
-                              p->epsilon, (double*)p->rowMult.ptr, (double*)p->slabS.ptr, &wgs,
-                              st)))
+    if ((rc = cyc::tiles_rows(n, labels, weights, p->fitIntercept, p->loss, 0.0, offDev, lscale,
+                              sigma, p->epsilon, (double*)p->rowMult.ptr, (double*)p->slabS.ptr,
+                              &wgs, st)))
       return rc;
   }
   int ranges = 0;

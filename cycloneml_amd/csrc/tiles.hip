@@ -678,8 +678,11 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
 #endif
 __global__ __launch_bounds__(256) void k_tiles_rows(
     int64_t n, const double* __restrict__ labels, const double* __restrict__ weights,
-    int fitIntercept, int kind, double offset, double lscale, double sigma, double eps,
-    double* __restrict__ dm, double* __restrict__ slabS) {
+    int fitIntercept, int kind, double offsetH, const double* __restrict__ offsetD,
+    double lscale, double sigma, double eps, double* __restrict__ dm,
+    double* __restrict__ slabS) {
+  // the margin offset from the device when given (no host round trip)
+  const double offset = offsetD ? *offsetD : offsetH;
   __shared__ double red[4][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};     // loss, weight, multiplierSum, sigmaGradSum
@@ -932,12 +935,12 @@ int64_t tiles_rows_blocks(int64_t n) {
 }
 
 int tiles_rows(int64_t n, const double* labels, const double* weights, int fitIntercept,
-               int kind, double offset, double lscale, double sigma, double eps, double* dm,
-               double* slabS, int64_t* wgs, hipStream_t st) {
+               int kind, double offset, const double* offsetDev, double lscale, double sigma,
+               double eps, double* dm, double* slabS, int64_t* wgs, hipStream_t st) {
   const int64_t g = tiles_rows_blocks(n);
   *wgs = g;
   hipLaunchKernelGGL(k_tiles_rows, dim3((unsigned)g), dim3(256), 0, st, n, labels, weights,
-                     fitIntercept, kind, offset, lscale, sigma, eps, dm, slabS);
+                     fitIntercept, kind, offset, offsetDev, lscale, sigma, eps, dm, slabS);
   CYC_LAUNCH_CHECK("k_tiles_rows");
   return CYC_OK;
 }

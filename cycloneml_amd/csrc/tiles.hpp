@@ -46,9 +46,10 @@ int tiles_margin(const TilesView& v, const double* coef, double* dots, hipStream
 // sigmaGradSum) partials to slabS[wg * 4 + k], the workgroup count through
 // *wgs (at most tiles_rows_blocks(n)).
 int64_t tiles_rows_blocks(int64_t n);
+// offsetDev: the offset in HBM (read by the kernel), else `offset`
 int tiles_rows(int64_t n, const double* labels, const double* weights, int fitIntercept,
-               int kind, double offset, double lscale, double sigma, double eps, double* dm,
-               double* slabS, int64_t* wgs, hipStream_t st);
+               int kind, double offset, const double* offsetDev, double lscale, double sigma,
+               double eps, double* dm, double* slabS, int64_t* wgs, hipStream_t st);
 
 // Gradient pass: slabG[range * F + f] = sum over the rows of row range
 // `range` (row order) of vals * mult[row]; *ranges receives the range count.
