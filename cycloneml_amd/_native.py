@@ -46,6 +46,7 @@ SIGNATURES = {
     "cyc_synchronize": (ctypes.c_int, [_vp]),
     "cyc_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "cyc_profile_query": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(_f64), _pi64]),
+    "cyc_profile_only": (ctypes.c_int, [ctypes.c_char_p]),
     "cyc_row_norms_dev": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "cyc_kmeans_plan_create": (ctypes.c_int, [_i32, _i32, _i64, ctypes.POINTER(_vp)]),
     "cyc_kmeans_plan_destroy": (ctypes.c_int, [_vp]),
@@ -257,6 +258,11 @@ def header_symbols(path: str = HEADER_PATH):
 
 def profile_enable(on: bool):
     check(load().cyc_profile_enable(int(on)))
+
+
+def profile_only(kernels):
+    """Time only these kernel names (None: all)."""
+    check(load().cyc_profile_only(None if kernels is None else ",".join(kernels).encode()))
 
 
 def profile_query(kernel: str):

@@ -7,6 +7,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <mutex>
 #include <string>
 #include <utility>
@@ -104,9 +105,14 @@ void DeviceBuffer::release() {
 static std::atomic<bool> g_prof{false};
 static std::mutex g_prof_mu;
 static std::map<std::string, std::vector<std::pair<hipEvent_t, hipEvent_t>>> g_prof_events;
+static std::set<std::string> g_prof_only;   // empty: every named kernel
 
 KernelTimer::KernelTimer(const char* n, hipStream_t s) : name(n), st(s) {
   if (!g_prof.load()) return;
+  {
+    std::lock_guard<std::mutex> g(g_prof_mu);
+    if (!g_prof_only.empty() && !g_prof_only.count(name)) return;
+  }
   if (hipEventCreate(&e0) != hipSuccess || hipEventRecord(e0, st) != hipSuccess) e0 = nullptr;
 }
 
@@ -124,6 +130,23 @@ extern "C" {
 
 int cyc_profile_enable(int enable) {
   cyc::g_prof.store(enable != 0);
+  return CYC_OK;
+}
+
+int cyc_profile_only(const char* kernels) {
+  std::lock_guard<std::mutex> g(cyc::g_prof_mu);
+  cyc::g_prof_only.clear();
+  if (!kernels) return CYC_OK;
+  std::string all(kernels), cur;
+  for (char c : all) {
+    if (c == ',') {
+      if (!cur.empty()) cyc::g_prof_only.insert(cur);
+      cur.clear();
+    } else {
+      cur += c;
+    }
+  }
+  if (!cur.empty()) cyc::g_prof_only.insert(cur);
   return CYC_OK;
 }
 

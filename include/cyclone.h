@@ -56,6 +56,9 @@ int cyc_synchronize(void* stream);
  * returns their summed time (ms) and count, and forgets them. */
 int cyc_profile_enable(int enable);
 int cyc_profile_query(const char* kernel, double* total_ms, int64_t* launches);
+/* Restrict the timers to the comma-separated kernel names (NULL or "": all
+ * of them), so a timed region carries only the events it reads. */
+int cyc_profile_only(const char* kernels);
 
 /* ------------------------------------------------------------- vectors */
 /* norms[i] = Vectors.norm(row i, 2.0) bit-exactly (mllib/linalg/Vectors.scala:

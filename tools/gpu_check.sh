@@ -14,7 +14,7 @@ w = sys.argv[1]
 d = json.loads(open(f"gpurun_out/check_{w}.json").read().strip().splitlines()[-1])
 r = d.get("roofline") or {}
 print(w, round(d["value"] / 1e6, 2), "M/s", round(d["ms_per_step"], 2), "ms", r.get("kernel"),
-      round(r.get("frac", 0), 4), {k: round(v, 2) for k, v in (r.get("kernels_ms_per_step") or {}).items()},
+      round(r.get("frac", 0), 4), {k: round(v, 2) for k, v in {**(r.get("kernels_ms_per_step") or {}), **(r.get("diag_kernels_ms_per_step") or {})}.items()},
       r.get("covariance_passes"), r.get("centred_form_ms_per_step"), (d.get("fit") or {}).get("fit_ms"))
 PY
 done
