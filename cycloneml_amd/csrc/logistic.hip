@@ -621,6 +621,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_mlr_margins(
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) ms[ct] += acc[t][ct][0];
+      wsum += lane < 32 ? 1.0 : 0.0;   // a nonzero weight for the host's check
       return;
     }
     // Epilogue: lane holds rows 32 wave + 16 t + (lane>>4) + 4r, classes
