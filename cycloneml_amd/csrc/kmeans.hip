@@ -2032,8 +2032,18 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
     rowList = (const int32_t*)p->list3.ptr;
     rowCount = (const unsigned int*)p->list3Count.ptr;
   }
-  // tier 2: fp64 MFMA screen (every row, or the queued ones)
-  switch (p->bm) {
+  // tier 2: fp64 MFMA screen (every row, or the queued ones).  Queued rows
+  // (a few thousand after the i8 tiers) go 16 to a workgroup: a 64-row
+  // tile kept ~50 CUs busy for ~110 us each (CYC_KMEANS_LIST_BM=0: the
+  // plan's tile); the dynamic LDS stays the plan's (64-row) size, which
+  // covers 16 rows
+  static const bool list16 = [] {
+    const char* e = std::getenv("CYC_KMEANS_LIST_BM");
+    return !(e && e[0] == '0');
+  }();
+  if (rowList && list16 && p->bm >= 16) {
+    rc = launch_assign<16>(p, X, xnorm, n, C, cnorm, assign, cost, st, rowList, rowCount);
+  } else switch (p->bm) {
     case 64: rc = launch_assign<64>(p, X, xnorm, n, C, cnorm, assign, cost, st, rowList, rowCount); break;
     case 32: rc = launch_assign<32>(p, X, xnorm, n, C, cnorm, assign, cost, st, rowList, rowCount); break;
     default: rc = launch_assign<16>(p, X, xnorm, n, C, cnorm, assign, cost, st, rowList, rowCount); break;
