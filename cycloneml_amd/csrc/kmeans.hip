@@ -1241,9 +1241,19 @@ __global__ void k_scatter(const int32_t* __restrict__ assign, int64_t n, int k,
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * kSortTile;
   const int64_t r1 = min<int64_t>(n, r0 + kSortTile);
-  for (int64_t base = r0; base < r1; base += 64) {
-    const int64_t r = base + lane;
-    const int c = (r < r1) ? assign[r] : -1;
+  // the tile's assignments loaded up front (one latency, not one per 64
+  // rows: 124 -> ~30 us at 10M rows), then the stable in-order walk
+  constexpr int PER = kSortTile / 64;
+  int cv[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int64_t r = r0 + i * 64 + lane;
+    cv[i] = (r < r1) ? assign[r] : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int64_t r = r0 + i * 64 + lane;
+    const int c = cv[i];
     // the lanes holding the same cluster: one ballot per bit of the index
     unsigned long long m = __ballot(c >= 0);
     for (int b = 0; b < kb; ++b) {
