@@ -1231,15 +1231,23 @@ __global__ void k_scan_clusters(const int64_t* __restrict__ total, int k,
 }
 
 // One wave per tile, rows in order: perm[cstart[c] + tileOffset[c] + rank] = row.
+// Tiles by XCD: block b runs on XCD b % 8 and takes tile (b % 8) * per +
+// b / 8, so each XCD walks a contiguous range of tiles.  A cluster's rows
+// from consecutive tiles land side by side in perm; with consecutive tiles
+// on one XCD their 4-byte writes meet in that XCD's L2 instead of partial
+// lines from eight L2s (the grid is 8 * per blocks; the spare ones leave).
 __global__ void k_scatter(const int32_t* __restrict__ assign, int64_t n, int k,
                           const int32_t* __restrict__ tileOff, const int64_t* __restrict__ cstart,
-                          int32_t* __restrict__ perm) {
+                          int32_t* __restrict__ perm, int64_t tiles) {
   extern __shared__ int64_t pos[];
+  const int64_t per = ((int64_t)gridDim.x + 7) / 8;
+  const int64_t tile = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (tile >= tiles) return;
   const int lane = threadIdx.x;
   const int kb = 32 - __builtin_clz((unsigned)max(k - 1, 1));   // bits of a cluster index
-  for (int c = lane; c < k; c += 64) pos[c] = cstart[c] + tileOff[(int64_t)blockIdx.x * k + c];
+  for (int c = lane; c < k; c += 64) pos[c] = cstart[c] + tileOff[tile * k + c];
   __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * kSortTile;
+  const int64_t r0 = tile * kSortTile;
   const int64_t r1 = min<int64_t>(n, r0 + kSortTile);
   // the tile's assignments loaded up front (one latency, not one per 64
   // rows: 124 -> ~30 us at 10M rows), then the stable in-order walk
@@ -2300,8 +2308,9 @@ int sort_clusters(cyc_kmeans_plan p, const int32_t* assign, int64_t n, int d, hi
   hipLaunchKernelGGL(k_scan_clusters, dim3(1), dim3(1024), 0, st, (const int64_t*)p->total.ptr, k,
                      (int64_t*)p->cstart.ptr, (int64_t*)p->chunkStart.ptr);
   CYC_LAUNCH_CHECK("k_scan_clusters");
-  hipLaunchKernelGGL(k_scatter, dim3(tiles), dim3(64), sizeof(int64_t) * k, st, assign, n, k,
-                     hist, (const int64_t*)p->cstart.ptr, (int32_t*)p->perm.ptr);
+  hipLaunchKernelGGL(k_scatter, dim3((unsigned)(8 * (((int64_t)tiles + 7) / 8))), dim3(64),
+                     sizeof(int64_t) * k, st, assign, n, k, hist, (const int64_t*)p->cstart.ptr,
+                     (int32_t*)p->perm.ptr, (int64_t)tiles);
   CYC_LAUNCH_CHECK("k_scatter");
   return CYC_OK;
 }
