@@ -676,6 +676,10 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
 #ifndef CYC_TILES_ROWS_U
 #define CYC_TILES_ROWS_U 2
 #endif
+// LOG: the logistic instance alone (kind 0, the bench's and LogisticRegression's
+// path): without the other kinds' code its registers stay low (more waves in
+// flight for the stream)
+template <bool LOG>
 __global__ __launch_bounds__(256) void k_tiles_rows(
     int64_t n, const double* __restrict__ labels, const double* __restrict__ weights,
     int fitIntercept, int kind, double offsetH, const double* __restrict__ offsetD,
@@ -708,7 +712,7 @@ __global__ __launch_bounds__(256) void k_tiles_rows(
       const int64_t r = r0 + u * stride;
       if (r >= n) break;
       double m;
-      if (kind == 0) {
+      if constexpr (LOG) {
         const double margin = fitIntercept ? offset + b.dot[u] : b.dot[u];
         const double x = -margin;
         const double lp = __builtin_fmax(x, 0.0) + log1p(exp(-__builtin_fabs(x)));
@@ -939,8 +943,14 @@ int tiles_rows(int64_t n, const double* labels, const double* weights, int fitIn
                double eps, double* dm, double* slabS, int64_t* wgs, hipStream_t st) {
   const int64_t g = tiles_rows_blocks(n);
   *wgs = g;
-  hipLaunchKernelGGL(k_tiles_rows, dim3((unsigned)g), dim3(256), 0, st, n, labels, weights,
-                     fitIntercept, kind, offset, offsetDev, lscale, sigma, eps, dm, slabS);
+  if (kind == 0)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_rows<true>), dim3((unsigned)g), dim3(256), 0, st, n,
+                       labels, weights, fitIntercept, kind, offset, offsetDev, lscale, sigma, eps,
+                       dm, slabS);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_rows<false>), dim3((unsigned)g), dim3(256), 0, st, n,
+                       labels, weights, fitIntercept, kind, offset, offsetDev, lscale, sigma, eps,
+                       dm, slabS);
   CYC_LAUNCH_CHECK("k_tiles_rows");
   return CYC_OK;
 }
