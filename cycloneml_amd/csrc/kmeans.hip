@@ -1807,6 +1807,7 @@ struct cyc_kmeans_plan_s {
   cyc::DeviceBuffer cb3, cq3, ok3, list3, list3Count;
   // i8 exact-integer screen (kmeans_i8.hip), used with a row image
   int ktp8 = 0;
+  // cb8: the center image (fragments, then the center-major copy, d <= 256)
   cyc::DeviceBuffer cb8, cq8, g8, prm8, scr8, list8Count;   // list8 = slowList (idle then)
   // candidate pass of the d <= 256 screen (kmeans_i8.hpp CandArgs)
   cyc::DeviceBuffer candRows, cands, candCount;
@@ -2395,7 +2396,7 @@ int cyc_kmeans_plan_create(int32_t d, int32_t k, int64_t max_rows, cyc_kmeans_pl
   if (d <= cyc::km8::kMaxD) {
     const int ks8 = cyc::km8::ksteps(d);
     p->ktp8 = (int)cyc::round_up((k + 15) / 16, cyc::km8::kWaves);
-    if ((rc = p->cb8.reserve((size_t)p->ktp8 * ks8 * 3 * 64 * 16)) ||
+    if ((rc = p->cb8.reserve((size_t)p->ktp8 * ks8 * 3 * 64 * 16 * 2)) ||
         (rc = p->cq8.reserve(sizeof(float) * (size_t)p->ktp8 * 48)) ||
         (rc = p->g8.reserve(sizeof(double) * (size_t)p->ktp8 * 48)) ||
         (rc = p->list8Count.reserve(64)) ||

@@ -631,6 +631,13 @@ __global__ __launch_bounds__(256) void k_centers_pack32(
     dst[0] = pa;
     dst[64] = pb;
     dst[128] = pc;
+    // the center-major copy behind the fragments (k_screen32r's per-lane
+    // gathers): center c's limb planes a', b', c' of D = 32 S bytes each,
+    // dimensions in order, 6 S 16-byte pieces per center
+    uint4* cr = Cb + (int64_t)ktp * S * 3 * 64 + (int64_t)c * (6 * S) + 2 * s + (lane >> 5);
+    cr[0] = pa;
+    cr[2 * S] = pb;
+    cr[4 * S] = pc;
   }
   if (idx < (int64_t)ktp * 32) {
     const int c = (int)idx;
@@ -1376,15 +1383,19 @@ __global__ __launch_bounds__(256, 2) void k_screen32r(
     const double xn = xnorm[myRow];
     xxj = xn * xn;
   }
-  // B fragments of center c (c < 0: a padding column, zero)
+  // B fragments of center c (c < 0: a padding column, zero), from the
+  // center-major copy behind the fragment image (k_centers_pack32): a lane's
+  // 16 pieces of its center lie in 512 contiguous bytes (from the fragments
+  // every piece was a separate cache line)
+  const uint4* Cr = Cb + (size_t)(kstride >> 5) * S * 3 * 64;
   auto loadB = [&](int c, v4i (&B)[S][2]) {
     const bool on = c >= 0;
-    const uint4* src = Cb + ((size_t)((on ? c : 0) >> 5) * S * 3) * 64 + ((on ? c : 0) & 31) + 32 * h;
+    const uint4* src = Cr + (size_t)(on ? c : 0) * (6 * S) + h;
 #pragma unroll
     for (int s = 0; s < S; ++s)
 #pragma unroll
       for (int L = 0; L < 2; ++L) {
-        const v4u t = *(const v4u*)(src + (s * 3 + L) * 64);
+        const v4u t = *(const v4u*)(src + L * 2 * S + 2 * s);
         B[s][L] = on ? __builtin_bit_cast(v4i, t) : v4i{0, 0, 0, 0};
       }
   };
