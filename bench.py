@@ -284,8 +284,9 @@ class KMeansWorkload:
     and dimension), the cluster sums (k_chunk_sums) against HBM; the
     roofline line names the slowest priced kernel."""
     kernel = "k_chunk_sums"
-    kernels = ("k_kmeans_screen1", "k_kmeans_refine2", "k_kmeans_screen2", "k_kmeans_cands",
-               "k_kmeans_screen3", "k_kmeans_compact", "k_kmeans_assign_fp64", "k_chunk_sums")
+    kernels = ("k_kmeans_screen1", "k_kmeans_refine2", "k_kmeans_screen2", "k_kmeans_cands3",
+               "k_kmeans_cands", "k_kmeans_screen3", "k_kmeans_compact", "k_kmeans_assign_fp64",
+               "k_chunk_sums")
     pmc_names = {"k_kmeans_screen1": "k_screen32_l1", "k_kmeans_screen2": "k_screen32_l2",
                  "k_kmeans_refine2": "k_screen32r", "k_chunk_sums": "k_chunk_sums_fast"}
 
@@ -377,6 +378,7 @@ class KMeansWorkload:
             "rows_to_full_two_limb_pass": full,
             "mean_union_centers_per_32_listed_rows": union / waves if waves else None,
             "rows_to_candidate_pass": self.plan.last_candidates(),
+            "rows_to_fp64_candidate_pass": self.plan.last_candidates3(),
             "rows_to_three_limb_pass": self.plan.last_screen(),
             "rows_to_fp64_screen": tier2, "rows_to_exact": exact,
             "note": "the last timed iteration's one-limb pass / refinement, then one counted "

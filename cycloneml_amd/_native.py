@@ -70,6 +70,7 @@ SIGNATURES = {
     "cyc_kmeans_last_tiers": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_last_screen": (ctypes.c_int, [_vp, _pi64]),
     "cyc_kmeans_last_candidates": (ctypes.c_int, [_vp, _pi64]),
+    "cyc_kmeans_last_candidates3": (ctypes.c_int, [_vp, _pi64]),
     "cyc_kmeans_last_refine": (ctypes.c_int, [_vp, _pi64, _pi64, _pi64]),
     "cyc_kmeans_parallel_sample_dev": (ctypes.c_int, [_vp, _pi64, _i32, _i32, _i32, _i32, _i32,
                                                       _f64, _vp, _vp]),

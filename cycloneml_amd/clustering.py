@@ -131,6 +131,14 @@ class KMeansPlan:
         N.check(self._lib.cyc_kmeans_last_candidates(self.handle, ctypes.byref(a)))
         return a.value
 
+    def last_candidates3(self):
+        """Of last_candidates(), the rows the three-limb candidate tier left to
+        the fp64 candidate pass on the last assign(count_exact=True) (-1: the
+        tier did not run)."""
+        a = ctypes.c_int64(0)
+        N.check(self._lib.cyc_kmeans_last_candidates3(self.handle, ctypes.byref(a)))
+        return a.value
+
     def last_refine(self):
         """(rows the one-limb pass listed, rows handed to the full two-limb
         pass, candidate centers the refinement screened in total) of the

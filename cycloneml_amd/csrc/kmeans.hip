@@ -1804,6 +1804,8 @@ struct cyc_kmeans_plan_s {
   int64_t lastExact = 0;    // rows the fp64 screen queued (last counted call)
   int64_t lastLimb3 = -1;   // rows the two-limb i8 pass left to the three-limb pass (-1: none)
   int64_t lastCands = -1;   // rows the two-limb i8 pass left to the candidate pass
+  int64_t lastCands2 = -1;  // rows the three-limb candidate tier left to the fp64 pass
+  bool cands3 = false;      // the last cand_args enabled the three-limb candidate tier
   cyc::DeviceBuffer cb3, cq3, ok3, list3, list3Count;
   // i8 exact-integer screen (kmeans_i8.hip), used with a row image
   int ktp8 = 0;
@@ -1811,6 +1813,8 @@ struct cyc_kmeans_plan_s {
   cyc::DeviceBuffer cb8, cq8, g8, prm8, scr8, list8Count;   // list8 = slowList (idle then)
   // candidate pass of the d <= 256 screen (kmeans_i8.hpp CandArgs)
   cyc::DeviceBuffer candRows, cands, candCount;
+  // the rows the three-limb candidate tier leaves to the fp64 pass
+  cyc::DeviceBuffer candRows2, cands2, candCount2;
   // the one-limb pass + two-limb refinement (kmeans_i8.hpp RefineArgs)
   cyc::DeviceBuffer cand1Rows, cand1, cand1Count, fullList, fullCount;
   // the screens' sharded append stage (kmeans_i8.hpp AppendStage)
@@ -1953,6 +1957,19 @@ int cand_args(cyc_kmeans_plan p, int64_t n, const double* X, const double* xnorm
   ca = cyc::km8::CandArgs{X, xnorm, C, cnorm, p->k, unit, unit ? 0x1p-19 : 0x1p-30,
                           (int32_t*)p->candRows.ptr, (int32_t*)p->cands.ptr,
                           (unsigned int*)p->candCount.ptr};
+  // the three-limb candidate tier (CYC_KMEANS_CANDS3=0: every candidate row
+  // straight to the fp64 pass)
+  const char* e3 = std::getenv("CYC_KMEANS_CANDS3");
+  p->cands3 = !(e3 && e3[0] == '0');
+  if (p->cands3) {
+    if ((rc = p->candRows2.reserve(sizeof(int32_t) * (size_t)n)) ||
+        (rc = p->cands2.reserve(sizeof(int32_t) * (size_t)n * cyc::km8::kCandMax)) ||
+        (rc = p->candCount2.reserve(64)))
+      return rc;
+    ca.candRows2 = (int32_t*)p->candRows2.ptr;
+    ca.cands2 = (int32_t*)p->cands2.ptr;
+    ca.candCount2 = (unsigned int*)p->candCount2.ptr;
+  }
   return CYC_OK;
 }
 
@@ -2071,7 +2088,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
   // Exact emulation of the reference loop for undecided rows.  The queue
   // length is read back only when the caller asks for it; otherwise a
   // grid-stride launch drains whatever the queue holds without a host sync.
-  unsigned int h_slow = 0, h_tier2 = 0, h_limb3 = 0, h_cand = 0;
+  unsigned int h_slow = 0, h_tier2 = 0, h_limb3 = 0, h_cand = 0, h_cand2 = 0;
   if (n_exact_out) {
     const bool twoPass = rows && rows->usable && cyc::km8::uses32(p->d);
     CYC_HIP(hipMemcpyAsync(&h_slow, p->slowCount.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
@@ -2080,6 +2097,8 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
     if (twoPass) {
       CYC_HIP(hipMemcpyAsync(&h_limb3, p->list8Count.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
       CYC_HIP(hipMemcpyAsync(&h_cand, p->candCount.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+      if (p->cands3)
+        CYC_HIP(hipMemcpyAsync(&h_cand2, p->candCount2.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     }
     CYC_HIP(hipStreamSynchronize(st));
     *n_exact_out = h_slow;
@@ -2087,6 +2106,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
     p->lastExact = h_slow;
     p->lastLimb3 = twoPass ? (int64_t)h_limb3 : -1;
     p->lastCands = twoPass ? (int64_t)h_cand : -1;
+    p->lastCands2 = twoPass && p->cands3 ? (int64_t)h_cand2 : -1;
     if (h_slow) {
       hipLaunchKernelGGL(k_assign_exact, dim3((unsigned)std::min<unsigned>(h_slow, 4096)), dim3(256), 0, st, X, xnorm,
                          p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm, p->k, statsArg,
@@ -2243,12 +2263,14 @@ int cos_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmea
   }
   int64_t maxRows = n;
   if (n_exact_out) {
-    unsigned int h = 0, h3 = 0, hc = 0;
+    unsigned int h = 0, h3 = 0, hc = 0, hc2 = 0;
     const bool twoPass = screen && cyc::km8::uses32(p->d);
     CYC_HIP(hipMemcpyAsync(&h, count, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     if (twoPass) {
       CYC_HIP(hipMemcpyAsync(&h3, p->list8Count.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
       CYC_HIP(hipMemcpyAsync(&hc, p->candCount.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+      if (p->cands3)
+        CYC_HIP(hipMemcpyAsync(&hc2, p->candCount2.ptr, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     }
     CYC_HIP(hipStreamSynchronize(st));
     *n_exact_out = h;
@@ -2256,6 +2278,7 @@ int cos_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmea
     p->lastExact = h;
     p->lastLimb3 = twoPass ? (int64_t)h3 : -1;
     p->lastCands = twoPass ? (int64_t)hc : -1;
+    p->lastCands2 = twoPass && p->cands3 ? (int64_t)hc2 : -1;
     maxRows = h;
   }
   if (maxRows == 0) return CYC_OK;
@@ -2436,6 +2459,13 @@ int cyc_kmeans_last_candidates(cyc_kmeans_plan p, int64_t* candidate_rows) {
   CYC_REQUIRE(p != nullptr && candidate_rows, "arguments must not be null");
   std::lock_guard<std::mutex> g(p->mu);
   *candidate_rows = p->lastCands;
+  return CYC_OK;
+}
+
+int cyc_kmeans_last_candidates3(cyc_kmeans_plan p, int64_t* fp64_rows) {
+  CYC_REQUIRE(p != nullptr && fp64_rows, "arguments must not be null");
+  std::lock_guard<std::mutex> g(p->mu);
+  *fp64_rows = p->lastCands2;
   return CYC_OK;
 }
 

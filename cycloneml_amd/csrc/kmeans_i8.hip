@@ -1715,6 +1715,145 @@ __global__ __launch_bounds__(256) void k_screen_cands(
   }
 }
 
+// Three-limb tier of the candidate rows, ahead of k_screen_cands: for each
+// of a row's <= kCandMax candidates the exact integer limb products S1 =
+// a.a', S2 = a.b' + b.a', S3 = a.c' + b.b' + c.a' of the row image and the
+// center-major copy of the center image (v_dot4 over 2S lanes per row, 16
+// dimensions a lane: 768 B per row and per candidate at d = 256, against
+// 2 KB of fp64 each in k_screen_cands), bounded exactly as the three-limb
+// pass bounds them (k_screen32<.., 3, ..>: the same f32 lower bounds L,
+// rounded down, and the same certification margin M), over the candidates
+// instead of every center.  A row is certified when its best candidate
+// beats every other candidate by M: the candidates exclude every other
+// center (by the two-limb margin against the two-limb winner, itself a
+// candidate), so the best candidate is the reference loop's answer, as in
+// k_screen_cands.  The other rows go on with their candidates to
+// k_screen_cands (out*).
+__device__ __forceinline__ int dot16(uint4 u, uint4 v, int acc) {
+  acc = __builtin_amdgcn_sdot4((int)u.x, (int)v.x, acc, false);
+  acc = __builtin_amdgcn_sdot4((int)u.y, (int)v.y, acc, false);
+  acc = __builtin_amdgcn_sdot4((int)u.z, (int)v.z, acc, false);
+  return __builtin_amdgcn_sdot4((int)u.w, (int)v.w, acc, false);
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void k_screen_cands3(
+    const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
+    int d, const uint4* __restrict__ Cr, const float* __restrict__ cq,
+    const double* __restrict__ g, const double* __restrict__ cnorm,
+    const CenterParams* __restrict__ prm, const int32_t* __restrict__ candRows,
+    const int32_t* __restrict__ cands, const unsigned int* __restrict__ candCount,
+    int32_t* __restrict__ assign, int32_t* __restrict__ outRows, int32_t* __restrict__ outCands,
+    unsigned int* __restrict__ outCount, unsigned int scap) {
+  constexpr int P16 = 2 * S;          // 16-byte pieces per limb plane = lanes per row
+  constexpr int RPW = 64 / P16;       // rows per wave
+  const unsigned cnt = *candCount;
+  const int lane = threadIdx.x & 63, q = lane / P16, li = lane % P16;
+  const unsigned nw = (gridDim.x * blockDim.x) >> 6;
+  const unsigned w0 = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (scap) {   // this wave's shard (<= RPW rows per grid stride: shard_cap)
+    const unsigned sh = w0 % kShards;
+    outRows += (size_t)sh * scap;
+    outCands += (size_t)sh * scap * kCandMax;
+    outCount += sh * kShardStride;
+  }
+  const CenterParams P = *prm;
+  for (unsigned base = w0 * RPW; base < cnt; base += nw * RPW) {
+    const unsigned idx = base + q;
+    const bool live = idx < cnt;
+    const int64_t row = live ? candRows[idx] : 0;
+    int ci[kCandMax];
+#pragma unroll
+    for (int i = 0; i < kCandMax; ++i) ci[i] = live ? cands[(size_t)idx * kCandMax + i] : -1;
+    const uint4* xr = Xq + row * (3 * P16) + li;
+    const uint4 xa = xr[0], xb = xr[P16], xc = xr[2 * P16];
+    int s1[kCandMax], s2[kCandMax], s3[kCandMax];
+#pragma unroll
+    for (int i = 0; i < kCandMax; ++i) {
+      const int c = ci[i];
+      const uint4* cr = Cr + (size_t)((c >= 0 && c < P.k) ? c : 0) * (3 * P16) + li;
+      const uint4 ca = cr[0], cb = cr[P16], cc = cr[2 * P16];
+      s1[i] = dot16(xa, ca, 0);
+      s2[i] = dot16(xb, ca, dot16(xa, cb, 0));
+      s3[i] = dot16(xc, ca, dot16(xb, cb, dot16(xa, cc, 0)));
+    }
+    // sums over the row's P16 lanes (integers: any order)
+#pragma unroll
+    for (int m = 1; m < P16; m <<= 1)
+#pragma unroll
+      for (int i = 0; i < kCandMax; ++i) {
+        s1[i] += __shfl_xor(s1[i], m);
+        s2[i] += __shfl_xor(s2[i], m);
+        s3[i] += __shfl_xor(s3[i], m);
+      }
+    const int2 mt = live ? meta[row] : make_int2(INT_MIN, 0);
+    // the three-limb pass's bounds: T = S1 2^7 + S2, V = T + S3 2^-7 and L =
+    // cq - F1 V in f32 rounded toward -inf (lower bounds), F1 = 2^(ex + ec - 20)
+    __builtin_amdgcn_s_setreg(0x801, 2);
+    const float F1 = mt.x == INT_MIN ? 0.0f : __builtin_ldexpf(1.0f, mt.x + P.ec - 20);
+    float L1 = __builtin_inff(), L2 = __builtin_inff();
+    int I1 = -1;
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < kCandMax; ++i) {
+      const int c = ci[i];
+      bad = bad || c >= P.k;   // a padding center
+      if (c < 0 || c >= P.k) continue;
+      const int T = s1[i] * 128 + s2[i];
+      const float V = __builtin_fmaf((float)s3[i], 0x1p-7f, (float)T);
+      const float L = __builtin_fmaf(-F1, V, cq[c]);
+      const bool lt = L < L1;
+      L2 = __builtin_amdgcn_fmed3f(L1, L2, L);
+      I1 = lt ? c : I1;
+      L1 = lt ? L : L1;
+    }
+    __builtin_amdgcn_s_setreg(0x801, 0);
+    bool decided = false;
+    const double l1 = (double)L1, l2 = (double)L2;
+    if (live && P.ok && !bad && mt.x != INT_MIN && I1 >= 0 && __builtin_isfinite(l1)) {
+      const double xn = xnorm[row], cn = cnorm[I1];
+      const double xx = xn * xn, cc = cn * cn;
+      const double n1 = (double)__int_as_float(mt.y);   // bounds |xh3|_1
+      const double fx = err_term(mt.x, n1, P.mu, d);
+      const double M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) +
+                        0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g[I1]) +
+                        0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
+                                   __builtin_fmin(__builtin_fabs(l2), 0x1p120)) +
+                        0x1p-90) *
+                       (1.0 + 0x1p-30);
+      decided = !__builtin_isfinite(l2) || (l2 - l1) > M;
+    }
+    if (live && li == 0) {
+      if (decided) {
+        assign[row] = I1;
+      } else {
+        const unsigned o = atomicAdd(outCount, 1u);
+        outRows[o] = (int32_t)row;
+#pragma unroll
+        for (int i = 0; i < kCandMax; ++i) outCands[(size_t)o * kCandMax + i] = ci[i];
+      }
+    }
+  }
+}
+
+template <int S>
+int launch_cands3(const CandArgs& ca, const void* img, const int2* meta, const double* xnorm,
+                  int64_t n, int d, const void* Cb, const float* cq, const double* g,
+                  const double* cnorm, const CenterParams* prm, int ktp, int32_t* assign,
+                  int32_t* outRows, int32_t* outCands, unsigned int* outCount, hipStream_t st,
+                  unsigned int scap) {
+  KernelTimer timer("k_kmeans_cands3", st);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 127) / 128, 4096));
+  // the center-major copy behind the fragment image (k_centers_pack32)
+  const uint4* Cr = (const uint4*)Cb + (size_t)ktp * S * 3 * 64;
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen_cands3<S>), dim3(grid), dim3(256), 0, st,
+                     (const uint4*)img, meta, xnorm, d, Cr, cq, g, cnorm, prm,
+                     (const int32_t*)ca.candRows, (const int32_t*)ca.cands,
+                     (const unsigned int*)ca.candCount, assign, outRows, outCands, outCount, scap);
+  CYC_LAUNCH_CHECK("k_screen_cands3");
+  return CYC_OK;
+}
+
 int launch_cands(const CandArgs& ca, int64_t n, int d, int32_t* assign, int32_t* list,
                  unsigned int* listCount, hipStream_t st, unsigned int scap = 0) {
   KernelTimer timer("k_kmeans_cands", st);
@@ -1877,6 +2016,24 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
   // the main stream before the candidate pass: beside it on a side stream
   // (CYC_KMEANS_SIDE=1, the round-4 form) the two shared the CUs and the
   // iteration measured 9.77 vs 9.71 ms (same box, interleaved).
+  // the three-limb tier of the candidate rows (CandArgs::candRows2 set):
+  // the rows it cannot certify go on, with their candidates, to the fp64
+  // candidate pass
+  CandArgs caF = *ca;
+  if (ca->candRows2) {
+    CYC_HIP(hipMemsetAsync(ca->candCount2, 0, sizeof(unsigned int), st));
+    if ((rc = launch_cands3<S>(*ca, img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp, assign,
+                               A(sg ? sg->candRows : nullptr, ca->candRows2),
+                               A(sg ? sg->cands : nullptr, ca->cands2),
+                               N(kSetCand, ca->candCount2), st, scap)))
+      return rc;
+    if (sg && (rc = compact(sg->set(kSetCand), scap, sg->candRows, ca->candRows2, 1, sg->cands,
+                            ca->cands2, kCandMax, ca->candCount2, st)))
+      return rc;
+    caF.candRows = ca->candRows2;
+    caF.cands = ca->cands2;
+    caF.candCount = ca->candCount2;
+  }
   static const bool sideStream = [] {
     const char* e = std::getenv("CYC_KMEANS_SIDE");
     return e && e[0] == '1';
@@ -1887,7 +2044,7 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
                                              A(sg ? sg->rowsA : nullptr, list),
                                              N(kSetRowsA, listCount), st, nullptr, nullptr,
                                              nullptr, scap)) ||
-        (rc = launch_cands(*ca, n, d, assign, A(sg ? sg->rowsB : nullptr, list),
+        (rc = launch_cands(caF, n, d, assign, A(sg ? sg->rowsB : nullptr, list),
                            N(kSetRowsB, listCount), st, scap)))
       return rc;
   } else {
@@ -1915,7 +2072,7 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
                                            N(kSetRowsA, listCount), side, nullptr, nullptr,
                                            nullptr, scap)))
     return rc;
-  rc = launch_cands(*ca, n, d, assign, A(sg ? sg->rowsB : nullptr, list), N(kSetRowsB, listCount),
+  rc = launch_cands(caF, n, d, assign, A(sg ? sg->rowsB : nullptr, list), N(kSetRowsB, listCount),
                     st, scap);
   CYC_HIP(hipEventRecord(join, side));
   CYC_HIP(hipStreamWaitEvent(st, join, 0));

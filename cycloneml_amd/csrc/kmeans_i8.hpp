@@ -73,6 +73,11 @@ struct CandArgs {
   int32_t* candRows;      // n entries
   int32_t* cands;         // n * kCandMax entries
   unsigned int* candCount;
+  // optional: the rows the three-limb candidate tier (k_screen_cands3)
+  // leaves to the fp64 pass (n, n * kCandMax entries and their count)
+  int32_t* candRows2 = nullptr;
+  int32_t* cands2 = nullptr;
+  unsigned int* candCount2 = nullptr;
 };
 
 // The one-limb pass + two-limb refinement of the d <= 256 screen (k > 96,

@@ -147,6 +147,11 @@ int cyc_kmeans_last_screen(cyc_kmeans_plan plan, int64_t* three_limb_rows);
  * to the <= 6 centers its bounds could not exclude) on the last counted
  * assign (-1 when no two-limb pass ran).  Also a tier statistic. */
 int cyc_kmeans_last_candidates(cyc_kmeans_plan plan, int64_t* candidate_rows);
+/* Of those, the rows the three-limb candidate tier (exact integer limb
+ * products over the candidates, k_screen_cands3) could not certify and left
+ * to the fp64 candidate pass (-1 when the tier did not run).  A tier
+ * statistic; no reference counterpart. */
+int cyc_kmeans_last_candidates3(cyc_kmeans_plan plan, int64_t* fp64_rows);
 /* The last i8 screen's one-limb pass + two-limb refinement (d <= 256,
  * 96 < k <= 4096): rows the one-limb pass listed with their candidate
  * centers, rows handed to the full two-limb pass, and the candidate centers

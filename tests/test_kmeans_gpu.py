@@ -679,6 +679,45 @@ def test_one_limb_refinement_lloyd(cuda, n, d, k, sep, dup):
         p.update(Cd, cn, sums, wsum, 1e-4, conv)
 
 
+@pytest.mark.parametrize("n,d,k", [(150_000, 200, 300), (100_000, 64, 128)])
+@pytest.mark.parametrize("cands3", ["1", "0"])
+def test_three_limb_candidate_tier(cuda, monkeypatch, n, d, k, cands3):
+    """Rows the two-limb tiers hand to the candidate pass first meet the
+    three-limb candidate tier (kmeans_i8.hip k_screen_cands3: exact integer
+    limb products over the row's <= 6 candidates, the three-limb pass's
+    bounds); the rows it cannot certify go on to the fp64 candidate pass.
+    Close clusters with near-duplicate centers (near ties); d = 200 (16
+    lanes per row) and d = 64 (8 lanes per row).  Index and cost bit-exact
+    vs the restatement with the tier on and off (CYC_KMEANS_CANDS3=0); on,
+    it leaves fewer rows to the fp64 pass than reach it."""
+    import torch
+    from cycloneml_amd.clustering import row_norms
+    monkeypatch.setenv("CYC_KMEANS_CANDS3", cands3)
+    rng = np.random.default_rng(n + d + k + 7)
+    true_c = rng.normal(scale=1.5, size=(k, d))
+    X = true_c[rng.integers(0, k, n)] + rng.normal(size=(n, d))
+    C = X[:k].copy()
+    C[k // 2:k // 2 + 10] = C[:10] + 1e-9
+    Xd, Cd = _dev(X, cuda), _dev(C, cuda)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = _plan(d, k, n)
+    p.stats(Cd)
+    rows = p.rows(Xd)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    c = torch.empty(n, dtype=torch.float64, device=cuda)
+    p.assign(Xd, xn, Cd, cn, a, c, count_exact=True, rows=rows)
+    torch.cuda.synchronize()
+    cand, fp64 = p.last_candidates(), p.last_candidates3()
+    assert cand > 0
+    if cands3 == "1":
+        assert 0 <= fp64 < cand
+    else:
+        assert fp64 == -1
+    ra, rc = _oracle_assign(X, C)
+    np.testing.assert_array_equal(a.cpu().numpy(), ra)
+    np.testing.assert_array_equal(c.cpu().numpy(), rc)
+
+
 @pytest.mark.timeout(900)
 def test_full_config_third_iteration(cuda):
     """BASELINE config 2 on bench.py's rows as the bench times it: two Lloyd
