@@ -43,6 +43,7 @@
 #include "kmeans_i8.hpp"
 
 #include <climits>
+#include <type_traits>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -1735,8 +1736,23 @@ __device__ __forceinline__ int dot16(uint4 u, uint4 v, int acc) {
   acc = __builtin_amdgcn_sdot4((int)u.z, (int)v.z, acc, false);
   return __builtin_amdgcn_sdot4((int)u.w, (int)v.w, acc, false);
 }
+__device__ __forceinline__ int dot16(uint2 u, uint2 v, int acc) {
+  acc = __builtin_amdgcn_sdot4((int)u.x, (int)v.x, acc, false);
+  return __builtin_amdgcn_sdot4((int)u.y, (int)v.y, acc, false);
+}
 
-template <int S>
+// 16-lane integer row sum by DPP row rotations: every lane of the row ends
+// with the total
+__device__ __forceinline__ int row16_isum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);   // row_ror:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);   // row_ror:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x122, 0xF, 0xF, false);   // row_ror:2
+  return v + __builtin_amdgcn_update_dpp(0, v, 0x121, 0xF, 0xF, false);   // row_ror:1
+}
+
+// PB: bytes of a limb plane per lane (16: 2S lanes per row; 8: 4S lanes,
+// measured 0.94 vs 0.59 ms at 5 waves per SIMD against 4)
+template <int S, int PB>
 __global__ __launch_bounds__(256) void k_screen_cands3(
     const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
     int d, const uint4* __restrict__ Cr, const float* __restrict__ cq,
@@ -1745,7 +1761,8 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     const int32_t* __restrict__ cands, const unsigned int* __restrict__ candCount,
     int32_t* __restrict__ assign, int32_t* __restrict__ outRows, int32_t* __restrict__ outCands,
     unsigned int* __restrict__ outCount, unsigned int scap) {
-  constexpr int P16 = 2 * S;          // 16-byte pieces per limb plane = lanes per row
+  using Pc = std::conditional_t<PB == 16, uint4, uint2>;
+  constexpr int P16 = 32 * S / PB;    // pieces per limb plane = lanes per row
   constexpr int RPW = 64 / P16;       // rows per wave
   const unsigned cnt = *candCount;
   const int lane = threadIdx.x & 63, q = lane / P16, li = lane % P16;
@@ -1765,27 +1782,37 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     int ci[kCandMax];
 #pragma unroll
     for (int i = 0; i < kCandMax; ++i) ci[i] = live ? cands[(size_t)idx * kCandMax + i] : -1;
-    const uint4* xr = Xq + row * (3 * P16) + li;
-    const uint4 xa = xr[0], xb = xr[P16], xc = xr[2 * P16];
+    const Pc* xr = (const Pc*)Xq + row * (3 * P16) + li;
+    const Pc xa = xr[0], xb = xr[P16], xc = xr[2 * P16];
     int s1[kCandMax], s2[kCandMax], s3[kCandMax];
 #pragma unroll
     for (int i = 0; i < kCandMax; ++i) {
       const int c = ci[i];
-      const uint4* cr = Cr + (size_t)((c >= 0 && c < P.k) ? c : 0) * (3 * P16) + li;
-      const uint4 ca = cr[0], cb = cr[P16], cc = cr[2 * P16];
+      const Pc* cr = (const Pc*)Cr + (size_t)((c >= 0 && c < P.k) ? c : 0) * (3 * P16) + li;
+      const Pc ca = cr[0], cb = cr[P16], cc = cr[2 * P16];
       s1[i] = dot16(xa, ca, 0);
       s2[i] = dot16(xb, ca, dot16(xa, cb, 0));
       s3[i] = dot16(xc, ca, dot16(xb, cb, dot16(xa, cc, 0)));
     }
-    // sums over the row's P16 lanes (integers: any order)
-#pragma unroll
-    for (int m = 1; m < P16; m <<= 1)
+    // sums over the row's P16 lanes (integers: any order); 16 lanes: DPP
+    // row rotations (VALU), else cross-lane permutes
+    if constexpr (P16 == 16) {
 #pragma unroll
       for (int i = 0; i < kCandMax; ++i) {
-        s1[i] += __shfl_xor(s1[i], m);
-        s2[i] += __shfl_xor(s2[i], m);
-        s3[i] += __shfl_xor(s3[i], m);
+        s1[i] = row16_isum(s1[i]);
+        s2[i] = row16_isum(s2[i]);
+        s3[i] = row16_isum(s3[i]);
       }
+    } else {
+#pragma unroll
+      for (int m = 1; m < P16; m <<= 1)
+#pragma unroll
+        for (int i = 0; i < kCandMax; ++i) {
+          s1[i] += __shfl_xor(s1[i], m);
+          s2[i] += __shfl_xor(s2[i], m);
+          s3[i] += __shfl_xor(s3[i], m);
+        }
+    }
     const int2 mt = live ? meta[row] : make_int2(INT_MIN, 0);
     // the three-limb pass's bounds: T = S1 2^7 + S2, V = T + S3 2^-7 and L =
     // cq - F1 V in f32 rounded toward -inf (lower bounds), F1 = 2^(ex + ec - 20)
@@ -1846,7 +1873,7 @@ int launch_cands3(const CandArgs& ca, const void* img, const int2* meta, const d
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 127) / 128, 4096));
   // the center-major copy behind the fragment image (k_centers_pack32)
   const uint4* Cr = (const uint4*)Cb + (size_t)ktp * S * 3 * 64;
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen_cands3<S>), dim3(grid), dim3(256), 0, st,
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen_cands3<S, 16>), dim3(grid), dim3(256), 0, st,
                      (const uint4*)img, meta, xnorm, d, Cr, cq, g, cnorm, prm,
                      (const int32_t*)ca.candRows, (const int32_t*)ca.cands,
                      (const unsigned int*)ca.candCount, assign, outRows, outCands, outCount, scap);
