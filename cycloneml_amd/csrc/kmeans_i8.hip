@@ -1952,6 +1952,17 @@ int compact(unsigned int* counts, unsigned int cap, const int32_t* src, int32_t*
 // set get exact fp64 distances to those candidates (k_screen_cands), the
 // others the three-limb pass.  With `stg` (and ca) every 32x32 kernel
 // appends through its shards, compacted after each launch.
+// Up to 8 counter ranges zeroed in one launch (a block per range).
+struct ZeroArgs {
+  unsigned int* p[8];
+  int w[8];
+  int n;
+};
+__global__ __launch_bounds__(256) void k_zero_counters(ZeroArgs z) {
+  unsigned int* q = z.p[blockIdx.x];
+  for (int i = threadIdx.x; i < z.w[blockIdx.x]; i += 256) q[i] = 0u;
+}
+
 template <int S, int W>
 int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
              const void* Cb, const float* cq, const double* g, const double* cnorm,
@@ -1959,13 +1970,32 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
              unsigned int* listCount, int32_t* list2, unsigned int* list2Count,
              const CandArgs* ca, hipStream_t st, const RefineArgs* ra = nullptr,
              const AppendStage* stg = nullptr) {
-  CYC_HIP(hipMemsetAsync(list2Count, 0, sizeof(unsigned int), st));
-  if (ca) CYC_HIP(hipMemsetAsync(ca->candCount, 0, sizeof(unsigned int), st));
   const AppendStage* sg = ca ? stg : nullptr;
   const unsigned scap = sg ? sg->cap : 0u;
-  if (sg)
-    CYC_HIP(hipMemsetAsync(sg->counts, 0,
-                           sizeof(unsigned int) * kSets * kShards * kShardStride, st));
+  {
+    // every counter of the pass zeroed by one launch (six fills before)
+    ZeroArgs z{};
+    auto add = [&](unsigned int* q, int words) {
+      if (q) {
+        z.p[z.n] = q;
+        z.w[z.n++] = words;
+      }
+    };
+    add(list2Count, 1);
+    if (ca) {
+      add(ca->candCount, 1);
+      add(ca->candCount2, 1);
+    }
+    if (ra && ca) {
+      add(ra->cand1Count, 1);
+      add(ra->fullCount, 2);
+    }
+    add(sg ? sg->counts : nullptr, kSets * kShards * kShardStride);
+    if (z.n) {
+      hipLaunchKernelGGL(k_zero_counters, dim3(z.n), dim3(256), 0, st, z);
+      CYC_LAUNCH_CHECK("k_zero_counters");
+    }
+  }
   // append targets: the stage's shards, or the lists themselves
   auto A = [&](int32_t* staged, int32_t* direct) { return sg ? staged : direct; };
   auto N = [&](int set, unsigned int* direct) { return sg ? sg->set(set) : direct; };
@@ -1984,8 +2014,6 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
     // one-limb pass over every center; the two-limb refinement over the
     // union of the listed rows' candidates; the full two-limb pass over the
     // rows neither can handle (fullList)
-    CYC_HIP(hipMemsetAsync(ra->cand1Count, 0, sizeof(unsigned int), st));
-    CYC_HIP(hipMemsetAsync(ra->fullCount, 0, 2 * sizeof(unsigned int), st));
     if ((rc = launch_screen32<S, W, 1, false>(
              img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 64, g + (size_t)ktp * 64, cnorm, prm,
              ktp, nullptr, nullptr, assign, A(sg ? sg->rowsA : nullptr, ra->fullList),
@@ -2048,7 +2076,6 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
   // candidate pass
   CandArgs caF = *ca;
   if (ca->candRows2) {
-    CYC_HIP(hipMemsetAsync(ca->candCount2, 0, sizeof(unsigned int), st));
     if ((rc = launch_cands3<S>(*ca, img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp, assign,
                                A(sg ? sg->candRows : nullptr, ca->candRows2),
                                A(sg ? sg->cands : nullptr, ca->cands2),
