@@ -31,10 +31,11 @@ the only RCCL communicator per GPU); torch.distributed runs on gloo for the
 rendezvous, the RCCL id and the host barriers.
 
 Prints ONE JSON line on rank 0.  `roofline` is for the workload's dominant
-kernel (the priced kernel with the most time per step; within 5 % of the
-workload's declared kernel, the declared one), timed with HIP events on the
-stream it runs on inside the timed region (cyc_profile_*), and lists every
-priced kernel's fraction under `priced_kernels`; `cpu_baseline` is the CPU
+kernel (the priced kernel with the most time per step), timed with HIP
+events on the stream it runs on inside the timed region (cyc_profile_*),
+lists every priced kernel's fraction under `priced_kernels`, and carries
+`step_frac`: the workload's algorithmic work per step (`step_work`) over
+`ms_per_step`, against the same kind of peak; `cpu_baseline` is the CPU
 restatement (oracle/, a C port of the reference loops) on a bounded sample of
 the same data, one partition per available host core.  On one GPU a `blas`
 leg follows: the per-call netlib layer (libcyclone_blas.so) at
@@ -60,7 +61,6 @@ HBM = ("hbm", "GB/s", HBM_PEAK_GBS, 1e9)
 FP64 = ("mfma", "TFLOP/s", FP64_PEAK_TFLOPS, 1e12)
 I8 = ("mfma", "TOPS", I8_PEAK_TOPS, 1e12)
 
-DOMINANT_MARGIN = 0.05    # roofline names the declared kernel unless another is 5 % slower
 DIST_BACKEND = "gloo"     # torch.distributed's group: host only, no second RCCL communicator
 ORDER = ("kmeans", "gramian", "pca", "lr_multi", "lr_sparse")
 # BASELINE configs: rows of the whole problem, and whether it is per GPU
@@ -286,7 +286,7 @@ class KMeansWorkload:
     kernel = "k_chunk_sums"
     kernels = ("k_kmeans_screen1", "k_kmeans_refine2", "k_kmeans_screen2", "k_kmeans_cands3",
                "k_kmeans_cands", "k_kmeans_screen3", "k_kmeans_compact", "k_kmeans_assign_fp64",
-               "k_chunk_sums")
+               "k_kmeans_bounds", "k_chunk_sums")
     pmc_names = {"k_kmeans_screen1": "k_screen32_l1", "k_kmeans_screen2": "k_screen32_l2",
                  "k_kmeans_refine2": "k_screen32r", "k_chunk_sums": "k_chunk_sums_fast"}
 
@@ -323,6 +323,18 @@ class KMeansWorkload:
         self.parallel = parallel
         self._refine = (-1, -1, -1)
 
+    def before_timing(self, steps):
+        """Centers of the first timed step (the cpu_baseline's) and the
+        carried bounds' screened-row counter at the start of the clock."""
+        self.C_timed = self.C.clone()
+        self.steps_timed = steps
+        self._b0 = self.rows.bounds_info()
+
+    def after_steps(self):
+        calls, screened = self.rows.bounds_info()
+        self.screened_timed = screened - self._b0[1]
+        self.bounded_calls = calls - self._b0[0]
+
     def step(self):
         k, d = self.k, self.d
         buf = self.buf
@@ -337,12 +349,20 @@ class KMeansWorkload:
         D = 128 * ((self.d + 127) // 128)                 # 32-dim substeps, padded
         kpad = 32 * (2 * ((self.k + 63) // 64))           # 32-center tiles (even count)
         if kname == "k_kmeans_screen1":       # one limb product: 2 ops per (row, center, dim)
-            return 2.0 * D * kpad * self.n / launches_per_step, I8
+            # over the rows it screened (those the carried bounds did not keep)
+            rows = getattr(self, "screened_timed", None)
+            rows = self.n if rows is None else rows / self.steps_timed
+            return 2.0 * D * kpad * rows / launches_per_step, I8
         if kname == "k_chunk_sums":           # every row once (fp64) + its perm entry
             return self.n * (8 * self.d + 4) / launches_per_step, HBM
         if kname == "k_kmeans_screen2" and self._refine[0] < 0:   # no refinement: every row
             return 6.0 * D * kpad * self.n / launches_per_step, I8
         return None
+
+    def step_work(self):
+        """A Lloyd iteration moves every row once (its fp64 values for the
+        cluster sums and their cost): 8 d bytes per row."""
+        return self.n * 8.0 * self.d, HBM
 
     def after_timing(self):
         self._refine = self.plan.last_refine()
@@ -373,7 +393,16 @@ class KMeansWorkload:
         exact = self.plan.assign(self.X, self.xnorm, self.C, self.cnorm, a, c,
                                  count_exact=True, rows=self.rows)
         tier2, _ = self.plan.last_tiers()
-        return {"screen_tiers": {
+        scr = getattr(self, "screened_timed", None)
+        return {"carried_bounds": {
+            "rows_screened_per_step": scr / self.steps_timed if scr is not None else None,
+            "rows_kept_per_step": self.n - scr / self.steps_timed if scr is not None else None,
+            "bounded_calls": getattr(self, "bounded_calls", None),
+            "note": "Hamerly bounds carried across the fit's iterations (cyclone.h "
+                    "cyc_kmeans_rows_set_bounds): a row whose moved bounds still certify its "
+                    "center keeps it and skips the screen; every row's cost and sums are "
+                    "computed every step"},
+            "screen_tiers": {
             "rows_listed_by_one_limb_pass": listed,
             "rows_to_full_two_limb_pass": full,
             "mean_union_centers_per_32_listed_rows": union / waves if waves else None,
@@ -381,8 +410,9 @@ class KMeansWorkload:
             "rows_to_fp64_candidate_pass": self.plan.last_candidates3(),
             "rows_to_three_limb_pass": self.plan.last_screen(),
             "rows_to_fp64_screen": tier2, "rows_to_exact": exact,
-            "note": "the last timed iteration's one-limb pass / refinement, then one counted "
-                    "assign after the timed region for the later tiers"}}
+            "note": "the last timed iteration's one-limb pass / refinement (over the rows the "
+                    "bounds left), then one counted assign of every row after the timed region "
+                    "for the later tiers"}}
 
     def describe(self):
         return (f"KMeans k={self.k} Lloyd iteration, dense fp64 {self.n} x {self.d} rows per GPU "
@@ -395,7 +425,8 @@ class KMeansWorkload:
         threads = cpu_threads()
         m = min(self.n, 2_000_000)
         Xs = np.ascontiguousarray(self.X[:m].cpu().numpy())
-        C = self.C0.cpu().numpy()
+        # the centers of the first timed step (after the warm-up iterations)
+        C = getattr(self, "C_timed", self.C0).cpu().numpy()
         xn, cn = oracle.row_norms(Xs), oracle.row_norms(C)
         t0 = time.perf_counter()
         oracle.kmeans_iteration(Xs[:2000], xn[:2000], None, C, cn)
@@ -410,9 +441,11 @@ class KMeansWorkload:
                                 threads=threads)
         el = time.perf_counter() - t0
         return {"value": rows / el, "unit": "rows/s", "cores": threads, "kind": "port",
-                "sample": f"{rows} rows of the same data, same k={self.k} centers, one Lloyd "
-                          f"iteration (stats+findClosest+sums+merge+update) as {threads} "
-                          f"partitions on {threads} threads, {el:.1f} s"}
+                "sample": f"{rows} rows of the same data, the k={self.k} centers of the first "
+                          f"timed step (iteration {getattr(self, 'warmup', 0) + 1} of the fit "
+                          f"from rows 0..k-1), one Lloyd iteration (stats+findClosest+sums+"
+                          f"merge+update) as {threads} partitions on {threads} threads, "
+                          f"{el:.1f} s"}
 
 
 class GramianWorkload:
@@ -436,6 +469,9 @@ class GramianWorkload:
 
     def work(self, kname, launches_per_step):
         return float(self.n) * self.p * (self.p + 1) / launches_per_step, FP64   # flops (upper)
+
+    def step_work(self):
+        return float(self.n) * self.p * (self.p + 1), FP64
 
     def describe(self):
         return (f"RowMatrix.computeGramianMatrix pass, dense fp64 {self.n} x {self.p} rows per "
@@ -508,6 +544,9 @@ class PCAWorkload:
             return float(rows) * self.p * 8 / launches_per_step, HBM
         return float(self.n) * self.p * (self.p + 1) / launches_per_step, FP64   # flops (upper)
 
+    def step_work(self):
+        return float(self.n) * self.p * (self.p + 1), FP64   # the syrk's n p (p + 1) flops
+
     def after_timing(self):
         import numpy as np
         import torch
@@ -527,13 +566,20 @@ class PCAWorkload:
             Gc = self.mat.computeCovarianceDevice()
         torch.cuda.synchronize()
         self.centred_ms = (time.perf_counter() - t0) * 1e3 / 3
-        self.form_diff = float((Gc - self.G).abs().max() / Gc.abs().max())
+        diff = (Gc - self.G).abs()
+        self.form_diff = float(diff.max() / Gc.abs().max())
+        dg = Gc.diagonal().clamp_min(0).sqrt()
+        self.form_diff_entry = float((diff / (dg[:, None] * dg[None, :]).clamp_min(1e-300)).max())
         self.mat.covarianceForm = "auto"
 
     def extra_roofline(self, launches_per_step, avg_s):
         return {"eigensolve_ms": self.eig_ms, "explained_variance_top3": self.explained_top3,
                 "covariance_form": self.form, "centred_form_ms_per_step": self.centred_ms,
-                "forms_max_rel_diff": self.form_diff,
+                "forms_normwise_diff": self.form_diff,
+                "forms_normwise_diff_is": "max |C_auto - C_centred| / max |C_centred|",
+                "forms_entrywise_diff": self.form_diff_entry,
+                "forms_entrywise_diff_is": "max over i, j of |C_auto - C_centred|_ij / "
+                                           "sqrt(C_ii C_jj) (centred form's diagonal)",
                 "covariance_passes": self.passes,
                 "note": "step = computeCovariance on the device (isSparseMatrix take(1), the "
                         "passes of covariance_passes, finish); the reference's centred "
@@ -608,6 +654,9 @@ class LRMultiWorkload:
 
     def work(self, kname, launches_per_step):
         return 2.0 * self.n * self.F * self.C / launches_per_step, FP64   # each pass: one gemm
+
+    def step_work(self):
+        return 2 * 2.0 * self.n * self.F * self.C, FP64   # margins gemm + gradient gemm
 
     def describe(self):
         return (f"multinomial LR ({self.C} classes) RDDLossFunction.calculate, dense fp64 "
@@ -700,6 +749,9 @@ class LRSparseWorkload:
         if kname == "k_tiles_rows":           # the rows' epilogue: dot + label in, multiplier out
             return self.n * 24.0 / launches_per_step, HBM
         return self.n * (self.k * 12 + 8 + 8) / launches_per_step, HBM   # bytes
+
+    def step_work(self):
+        return self.n * (self.k * 12 + 8 + 8.0), HBM   # one evaluation's reads
 
     def extra_roofline(self, launches_per_step, avg_s):
         return {"layout_bytes": self.tiles.nbytes, "layout_format": self.tiles.format,
@@ -913,6 +965,9 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
     # after the clock (diag_kernels_ms_per_step).  CYC_BENCH_NO_EVENTS=1: no
     # events at all (a measurement switch; the roofline fields read zero).
     priced = [k for k in kernels if wl.work(k, 1) is not None]
+    wl.warmup = args.warmup
+    if hasattr(wl, "before_timing"):
+        wl.before_timing(args.steps)
     N.profile_only(priced)
     N.profile_enable(os.environ.get("CYC_BENCH_NO_EVENTS") != "1")
     for kname in kernels:
@@ -927,6 +982,8 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    if hasattr(wl, "after_steps"):
+        wl.after_steps()
     prof = {kname: N.profile_query(kname) for kname in kernels}
     N.profile_enable(False)
     N.profile_only(None)
@@ -965,10 +1022,8 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
         fit = {"fit_ms": fel * 1e3, "fit_ms_per_iteration": fel * 1e3 / max(its, 1),
                "rows_per_s_per_iteration": total_rows * its / fel, **iters}
     # Every priced kernel in its own units (work per launch / mean launch
-    # duration from its HIP events), and the dominant one by a fixed rule:
-    # the priced kernel with the most time per step, except that a kernel
-    # within DOMINANT_MARGIN of the workload's declared `kernel` yields to
-    # it -- so two kernels a few percent apart cannot swap between boxes.
+    # duration from its HIP events), and the dominant one: the priced kernel
+    # with the most time per step.
     priced_rows = {}
     for k in kernels:
         kms_k, launches_k = prof[k]
@@ -986,12 +1041,14 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
                           "traffic_source": src_k}
     kname = wl.kernel
     if priced_rows:
-        top = max(priced_rows, key=lambda k: priced_rows[k]["ms_per_step"])
-        decl = priced_rows.get(wl.kernel)
-        if decl is None or priced_rows[top]["ms_per_step"] > (1 + DOMINANT_MARGIN) * \
-                decl["ms_per_step"]:
-            kname = top
+        kname = max(priced_rows, key=lambda k: priced_rows[k]["ms_per_step"])
     dom = priced_rows.get(kname)
+    # the whole step against the roofline of its algorithmic work
+    sw, (sbound, sunit, speak, sscale) = wl.step_work()
+    step_ach = sw / (el / args.steps) / sscale
+    step_frac = {"step_frac": step_ach / speak, "step_achieved": step_ach,
+                 "step_bound": sbound, "step_unit": sunit, "step_work": sw,
+                 "step_frac_rule": "algorithmic work per step / ms_per_step / peak"}
     kms, launches = prof[kname]
     avg_s = kms / max(launches, 1) / 1e3
     extra = wl.extra_roofline(launches / args.steps, avg_s) if (
@@ -1027,9 +1084,8 @@ def run_workload(name, args, dev, rank, world, cpu_seconds):
                      "traffic_source": dom["traffic_source"] if dom else None,
                      "avg_launch_ms": avg_s * 1e3, "launches": launches,
                      "work_per_launch": dom["work_per_launch"] if dom else None,
-                     "dominant_rule": f"most time per step among priced kernels; within "
-                                      f"{DOMINANT_MARGIN:.0%} of the declared {wl.kernel} the "
-                                      f"declared one",
+                     "dominant_rule": "the priced kernel with the most time per step",
+                     **step_frac,
                      "priced_kernels": priced_rows,
                      "kernels_ms_per_step": {k: prof[k][0] / args.steps for k in priced},
                      "diag_kernels_ms_per_step": diag,

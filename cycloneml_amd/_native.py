@@ -67,6 +67,8 @@ SIGNATURES = {
     "cyc_kmeans_rows_create": (ctypes.c_int, [_vp, _vp, _i64, _vp, ctypes.POINTER(_vp)]),
     "cyc_kmeans_rows_destroy": (ctypes.c_int, [_vp]),
     "cyc_kmeans_rows_bytes": (_i64, [_vp]),
+    "cyc_kmeans_rows_set_bounds": (ctypes.c_int, [_vp, _i32]),
+    "cyc_kmeans_rows_bounds_info": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_last_tiers": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_last_screen": (ctypes.c_int, [_vp, _pi64]),
     "cyc_kmeans_last_candidates": (ctypes.c_int, [_vp, _pi64]),

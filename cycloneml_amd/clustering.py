@@ -193,6 +193,20 @@ class KMeansRows:
     def nbytes(self):
         return int(self._lib.cyc_kmeans_rows_bytes(self.handle)) if self.handle else 0
 
+    def set_bounds(self, enable: bool):
+        """Carried bounds across this fit's Lloyd iterations (on by default,
+        cyclone.h cyc_kmeans_rows_set_bounds): rows whose Hamerly bounds still
+        certify their center skip the screen; either setting drops the state."""
+        N.check(self._lib.cyc_kmeans_rows_set_bounds(self.handle, 1 if enable else 0))
+
+    def bounds_info(self):
+        """(accumulate calls that used the bounds, rows those calls screened);
+        synchronises the device."""
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(self._lib.cyc_kmeans_rows_bounds_info(self.handle, ctypes.byref(a),
+                                                      ctypes.byref(b)))
+        return a.value, b.value
+
     def close(self):
         if self.handle:
             self._lib.cyc_kmeans_rows_destroy(self.handle)

@@ -1847,6 +1847,15 @@ struct cyc_kmeans_rows_s {
   bool usable = false;     // d <= 512
   bool cosine = false;     // image of the unit directions x / |x|
   cyc::DeviceBuffer img, meta, unorm;   // unorm: |x / |x|| per row (cosine)
+  // Carried bounds of one fit's Lloyd iterations (kmeans_i8.hpp Bounds):
+  // cyc_kmeans_accumulate_dev screens only the rows they cannot certify.
+  // State: per row (ub, lb) and the assignment they certify (bAssign), the
+  // centers they refer to (bCp, k x d); valid once a call has written them.
+  bool bEnabled = true;    // cyc_kmeans_rows_set_bounds (CYC_KMEANS_BOUNDS=0: off by default)
+  bool bValid = false;
+  int bk = 0;
+  cyc::DeviceBuffer bnd, bAssign, bCp, bDelta, bCcs, bPrm, bTmp, bCount, bList, bListCount, bCum;
+  int64_t bCalls = 0, bFullRows = 0;   // bounded calls; rows of their full (first) screens
 };
 
 namespace {
@@ -1994,6 +2003,63 @@ int refine_args(cyc_kmeans_plan p, int64_t n, bool useCa, cyc::km8::RefineArgs& 
   return CYC_OK;
 }
 
+// Carried bounds for a Lloyd call (cyc_kmeans_accumulate_dev): Euclidean
+// rows with an image whose screen runs the one-limb pass (refine_args).
+bool bounds_on(cyc_kmeans_plan p, cyc_kmeans_rows rows) {
+  static const bool envOff = [] {
+    const char* e = std::getenv("CYC_KMEANS_BOUNDS");
+    return e && e[0] == '0';
+  }();
+  return rows && rows->usable && !rows->cosine && rows->bEnabled && !envOff &&
+         p->measure == CYC_DISTANCE_EUCLIDEAN && cyc::km8::uses32(p->d) && p->k > 96 &&
+         cyc::km8::tiles32(p->k) * 32 <= 4096 && std::getenv("CYC_KMEANS_NO_REFINE") == nullptr;
+}
+
+// Moves the bounds to the centers C (the drift against the last call's,
+// then Cp = C) and lists the rows they cannot certify; bd for the screen.
+// The first call of a fit (or after a change of k) screens every row.
+int bounds_prepare(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* C,
+                   const double* xnorm, int64_t n, hipStream_t st, cyc::km8::Bounds& bd) {
+  namespace k8 = cyc::km8;
+  const int k = p->k, d = p->d;
+  int rc;
+  if ((rc = rows->bnd.reserve(sizeof(float2) * (size_t)n)) ||
+      (rc = rows->bAssign.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = rows->bCp.reserve(sizeof(double) * (size_t)k * d)) ||
+      (rc = rows->bDelta.reserve(sizeof(double) * (size_t)k)) ||
+      (rc = rows->bCcs.reserve(sizeof(double) * (size_t)k)) ||
+      (rc = rows->bPrm.reserve(sizeof(k8::DriftParams))) ||
+      (rc = rows->bTmp.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = rows->bCount.reserve(sizeof(unsigned int) * (size_t)(k8::bounds_blocks(n) + 1))) ||
+      (rc = rows->bList.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = rows->bListCount.reserve(64)))
+    return rc;
+  if (!rows->bCum.ptr) {
+    if ((rc = rows->bCum.reserve(64))) return rc;
+    CYC_HIP(hipMemsetAsync(rows->bCum.ptr, 0, 8, st));
+  }
+  const bool carry = rows->bValid && rows->bk == k;
+  rows->bValid = false;   // until the screen has written the bounds
+  if ((rc = k8::centers_drift(C, (double*)rows->bCp.ptr, k, d, (double*)rows->bDelta.ptr,
+                              (double*)rows->bCcs.ptr, (k8::DriftParams*)rows->bPrm.ptr, st)))
+    return rc;
+  bd = k8::Bounds{(float2*)rows->bnd.ptr, nullptr, nullptr};
+  if (carry) {
+    if ((rc = k8::bounds_filter((const int32_t*)rows->bAssign.ptr, (float2*)rows->bnd.ptr, xnorm,
+                                n, k, (const double*)rows->bDelta.ptr,
+                                (const k8::DriftParams*)rows->bPrm.ptr, (int32_t*)rows->bTmp.ptr,
+                                (unsigned int*)rows->bCount.ptr, (int32_t*)rows->bList.ptr,
+                                (unsigned int*)rows->bListCount.ptr,
+                                (unsigned long long*)rows->bCum.ptr, st)))
+      return rc;
+    bd.rowsIn = (const int32_t*)rows->bList.ptr;
+    bd.rowsInCount = (const unsigned int*)rows->bListCount.ptr;
+  } else {
+    rows->bFullRows += n;
+  }
+  return CYC_OK;
+}
+
 // The screens' sharded append stage for n rows (with the candidate pass);
 // CYC_KMEANS_NO_STAGE=1 appends straight to the lists (one counter each).
 int stage_args(cyc_kmeans_plan p, int64_t n, bool useCa, cyc::km8::AppendStage& sg, bool& use) {
@@ -2018,7 +2084,8 @@ int stage_args(cyc_kmeans_plan p, int64_t n, bool useCa, cyc::km8::AppendStage& 
 
 int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmeans_rows rows,
               int64_t n, const double* C, const double* cnorm, int32_t* assign, double* cost,
-              int64_t* n_exact_out, hipStream_t st, bool nostats = false) {
+              int64_t* n_exact_out, hipStream_t st, bool nostats = false,
+              const cyc::km8::Bounds* bd = nullptr) {
   // nostats: findClosest(centers, point) (DistanceMeasure.scala:318-340); the
   // screens certify only rows whose winner both loops return, so only the
   // exact tier differs (no statistics prunes, best starts at +inf)
@@ -2050,7 +2117,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
                                assign, (int32_t*)p->list3.ptr, (unsigned int*)p->list3Count.ptr,
                                (int32_t*)p->slowList.ptr, (unsigned int*)p->list8Count.ptr, st,
                                useCa ? &ca : nullptr, useRa ? &ra : nullptr,
-                               useSg ? &sg : nullptr)))
+                               useSg ? &sg : nullptr, bd)))
       return rc;
     rowList = (const int32_t*)p->list3.ptr;
     rowCount = (const unsigned int*)p->list3Count.ptr;
@@ -2580,6 +2647,26 @@ int64_t cyc_kmeans_rows_bytes(cyc_kmeans_rows rows) {
   return rows ? (int64_t)(rows->img.bytes + rows->meta.bytes) : 0;
 }
 
+int cyc_kmeans_rows_set_bounds(cyc_kmeans_rows rows, int32_t enable) {
+  CYC_REQUIRE(rows != nullptr, "rows must not be null");
+  rows->bEnabled = enable != 0;
+  rows->bValid = false;   // a re-enabled fit starts from a full screen
+  return CYC_OK;
+}
+
+int cyc_kmeans_rows_bounds_info(cyc_kmeans_rows rows, int64_t* calls, int64_t* screened_rows) {
+  CYC_REQUIRE(rows != nullptr && calls != nullptr && screened_rows != nullptr,
+              "arguments must not be null");
+  unsigned long long cum = 0;
+  if (rows->bCum.ptr) {
+    CYC_HIP(hipDeviceSynchronize());   // the counter is added on the callers' streams
+    CYC_HIP(hipMemcpy(&cum, rows->bCum.ptr, sizeof(cum), hipMemcpyDeviceToHost));
+  }
+  *calls = rows->bCalls;
+  *screened_rows = rows->bFullRows + (int64_t)cum;
+  return CYC_OK;
+}
+
 namespace {
 int check_rows(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* X, int64_t n) {
   CYC_REQUIRE(rows == nullptr || (rows->X == X && rows->n == n && rows->d == p->d),
@@ -2686,7 +2773,13 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   const int k = p->k, d = p->d;
   int rc = ensure_rows(p, n);
   if (rc) return rc;
-  if (!assign) {
+  // carried bounds: the assignment lives in the row image's state and is
+  // copied to the caller's array after the screen
+  const bool useBnd = bounds_on(p, rows);
+  int32_t* const userAssign = assign;
+  if (useBnd) {
+    assign = (int32_t*)nullptr;
+  } else if (!assign) {
     if ((rc = p->assignTmp.reserve(sizeof(int32_t) * (size_t)n))) return rc;
     assign = (int32_t*)p->assignTmp.ptr;
   }
@@ -2698,7 +2791,22 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   } else {
     if ((rc = require_enqueue(p, C, xnorm, n, st))) return rc;
     if ((rc = do_stats(p, C, st))) return rc;
-    if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st))) return rc;
+    cyc::km8::Bounds bd{};
+    if (useBnd) {
+      if ((rc = bounds_prepare(p, rows, C, xnorm, n, st, bd))) return rc;
+      assign = (int32_t*)rows->bAssign.ptr;
+    }
+    if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st, false,
+                        useBnd ? &bd : nullptr)))
+      return rc;
+    if (useBnd) {
+      rows->bValid = true;
+      rows->bk = k;
+      ++rows->bCalls;
+      if (userAssign)
+        CYC_HIP(hipMemcpyAsync(userAssign, assign, sizeof(int32_t) * (size_t)n,
+                               hipMemcpyDeviceToDevice, st));
+    }
   }
   // d > 1024: per-row costs first (k_chunk_sums fuses them for d <= 1024);
   // cosine: always (the cost is a ddot, summed per row)

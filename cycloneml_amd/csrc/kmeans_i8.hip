@@ -707,7 +707,7 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
     const unsigned int* __restrict__ rowsInCount, int32_t* __restrict__ assign,
     int32_t* __restrict__ list, unsigned int* __restrict__ listCount,
     int32_t* __restrict__ candRows, int32_t* __restrict__ cands,
-    unsigned int* __restrict__ candCount, unsigned int scap) {
+    unsigned int* __restrict__ candCount, unsigned int scap, float2* __restrict__ bnd) {
   constexpr int D = 32 * S, CH = 3 * D / 16;      // 16-byte chunks per image row
   // LIMBS = 1 takes two 32-center tiles per step (one barrier and one ring
   // slot per 64 centers: its tiles carry a third of the MFMAs)
@@ -748,7 +748,10 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
     else return pos0 + i;
   };
   if (!P.ok) {   // uniform over the grid
-    if (lane < rows) listS[atomicAdd(listCountS, 1u)] = (int32_t)rowAt(lane);
+    if (lane < rows) {
+      listS[atomicAdd(listCountS, 1u)] = (int32_t)rowAt(lane);
+      if (LIMBS == 1 && bnd) bnd[rowAt(lane)] = make_float2(-1.0f, -1.0f);
+    }
     return;
   }
   // tile t -> slot t % 3: each wave DMAs fragments wave, wave + W, ... and the
@@ -1119,6 +1122,7 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
     }
     bool decided = false, eligible = false;
     double M = 0.0;
+    float2 bb = make_float2(-1.0f, -1.0f);   // LIMBS = 1 with bnd: the row's bounds (none)
     if (mt.x != INT_MIN && I1 >= 0 && I1 < P.k && !clamped && shOk && !waveBad &&
         __builtin_isfinite(l1)) {
       const double xn = xnorm[grow], cn = cnorm[I1];
@@ -1141,7 +1145,28 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
           (1.0 + 0x1p-30);
       decided = !__builtin_isfinite(l2) || (l2 - l1) > M;
       eligible = __builtin_isfinite(M);
+      if constexpr (LIMBS == 1) {
+        if (bnd && decided && __builtin_isfinite(l2)) {
+          // Carried bounds (kmeans_i8.hpp Bounds).  With Lt_c = |c|^2 - 2 x.c
+          // and L'_c = cq_c - 2 s_c its exact integer form (cq_c <= |c|^2 -
+          // 2 g_c, |x.c - s_c| <= fx + g_c): Lt_c >= L'_c - 2 fx, and the
+          // computed bounds are within enc of L' (every center's >= l2 but
+          // the winner's, l1).  So |x - c|^2 >= xx + l2 - enc - 2 fx for c !=
+          // I1, and |x - c_I1|^2 <= xx + l1 + enc + 2 fx + 4 g_I1 + eps |c|^2
+          // (cq rounded down: the 2^-20 terms, as in M; xx = xnorm^2 within
+          // 2 kEpsF xx of the true |x|^2).
+          const double g1 = g[I1];
+          const double ub2 = (xx + l1 + enc + 2.0 * fx + 4.0 * g1 + 2.0 * kEpsF * (xx + cc) +
+                              0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g1) + 0x1p-90) *
+                             (1.0 + 0x1p-30);
+          const double lb2 = xx + l2 - enc - 2.0 * fx - 2.0 * kEpsF * (xx + cc) -
+                             0x1p-20 * (xx + cc + __builtin_fabs(l2) + 2.0 * fx + enc);
+          bb.x = fup(__builtin_sqrt(ub2) * (1.0 + 0x1p-50));
+          if (lb2 > 0.0 && bb.x < 0x1p120f) bb.y = fdown(__builtin_sqrt(lb2) * (1.0 - 0x1p-50));
+        }
+      }
     }
+    if (LIMBS == 1 && bnd) bnd[grow] = bb;
     if (decided) {
       assign[grow] = I1;
     } else if (LIMBS < 3 && candRows != nullptr && eligible) {
@@ -1227,14 +1252,14 @@ int launch_screen32(const void* img, const int2* meta, const double* xnorm, int6
                     const unsigned int* rowsInCount, int32_t* assign, int32_t* list,
                     unsigned int* listCount, hipStream_t st, int32_t* candRows = nullptr,
                     int32_t* cands = nullptr, unsigned int* candCount = nullptr,
-                    unsigned int scap = 0) {
+                    unsigned int scap = 0, float2* bnd = nullptr) {
   KernelTimer timer(LIMBS == 1 ? "k_kmeans_screen1" : LIMBS == 2 ? "k_kmeans_screen2"
                                                     : "k_kmeans_screen3", st);
   const int64_t wg = (n + 32 * W - 1) / (32 * W);   // W waves x 32 rows
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32<S, W, LIMBS, LIST>), dim3((unsigned)wg),
                      dim3(64 * W), 0, st, (const uint4*)img, meta, xnorm, n, d, (const uint4*)Cb,
                      cq, g, cnorm, prm, ktp, rowsIn, rowsInCount, assign, list, listCount,
-                     candRows, cands, candCount, scap);
+                     candRows, cands, candCount, scap, bnd);
   CYC_LAUNCH_CHECK("k_kmeans_screen32_i8");
   return CYC_OK;
 }
@@ -1969,7 +1994,7 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
              const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
              unsigned int* listCount, int32_t* list2, unsigned int* list2Count,
              const CandArgs* ca, hipStream_t st, const RefineArgs* ra = nullptr,
-             const AppendStage* stg = nullptr) {
+             const AppendStage* stg = nullptr, const Bounds* bd = nullptr) {
   const AppendStage* sg = ca ? stg : nullptr;
   const unsigned scap = sg ? sg->cap : 0u;
   {
@@ -2013,13 +2038,22 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
   if (ra && ca) {
     // one-limb pass over every center; the two-limb refinement over the
     // union of the listed rows' candidates; the full two-limb pass over the
-    // rows neither can handle (fullList)
-    if ((rc = launch_screen32<S, W, 1, false>(
-             img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 64, g + (size_t)ktp * 64, cnorm, prm,
-             ktp, nullptr, nullptr, assign, A(sg ? sg->rowsA : nullptr, ra->fullList),
-             N(kSetRowsA, ra->fullCount), st, A(sg ? sg->candRows : nullptr, ra->cand1Rows),
-             A(sg ? sg->cands : nullptr, ra->cand1), N(kSetCand, ra->cand1Count), scap)))
-      return rc;
+    // rows neither can handle (fullList).  With carried bounds (bd) the
+    // one-limb pass screens only the rows bounds_filter listed.
+    if (bd && bd->rowsIn)
+      rc = launch_screen32<S, W, 1, true>(
+          img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 64, g + (size_t)ktp * 64, cnorm, prm,
+          ktp, bd->rowsIn, bd->rowsInCount, assign, A(sg ? sg->rowsA : nullptr, ra->fullList),
+          N(kSetRowsA, ra->fullCount), st, A(sg ? sg->candRows : nullptr, ra->cand1Rows),
+          A(sg ? sg->cands : nullptr, ra->cand1), N(kSetCand, ra->cand1Count), scap, bd->ub_lb);
+    else
+      rc = launch_screen32<S, W, 1, false>(
+          img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 64, g + (size_t)ktp * 64, cnorm, prm,
+          ktp, nullptr, nullptr, assign, A(sg ? sg->rowsA : nullptr, ra->fullList),
+          N(kSetRowsA, ra->fullCount), st, A(sg ? sg->candRows : nullptr, ra->cand1Rows),
+          A(sg ? sg->cands : nullptr, ra->cand1), N(kSetCand, ra->cand1Count), scap,
+          bd ? bd->ub_lb : nullptr);
+    if (rc) return rc;
     if (sg && ((rc = compact(sg->set(kSetRowsA), scap, sg->rowsA, ra->fullList, 1, nullptr,
                              nullptr, 0, ra->fullCount, st)) ||
                (rc = compact(sg->set(kSetCand), scap, sg->candRows, ra->cand1Rows, 1, sg->cands,
@@ -2140,6 +2174,190 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
   return CYC_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Cross-iteration bounds (kmeans_i8.hpp Bounds).
+
+// One wave per center: the drift |C_c - Cp_c| and |C_c|^2, both rounded up
+// (fp64 sums of d <= 256 squares: relative error < (d + 2) 2^-53 < 2^-44),
+// then Cp_c = C_c.
+__global__ __launch_bounds__(256) void k_center_drift(const double* __restrict__ C,
+                                                      double* __restrict__ Cp, int k, int d,
+                                                      double* __restrict__ delta,
+                                                      double* __restrict__ ccs) {
+  const int lane = threadIdx.x & 63;
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (c >= k) return;
+  double s = 0.0, q = 0.0;
+  for (int j = lane; j < d; j += 64) {
+    const double v = C[(int64_t)c * d + j], o = Cp[(int64_t)c * d + j];
+    const double t = v - o;
+    s += t * t;
+    q += v * v;
+    Cp[(int64_t)c * d + j] = v;
+  }
+  s = wave_sum(s);
+  q = wave_sum(q);
+  if (lane == 0) {
+    delta[c] = __builtin_sqrt(s) * (1.0 + 0x1p-40) + 0x1p-500;
+    ccs[c] = q * (1.0 + 0x1p-40);
+  }
+}
+
+// Single block: the two largest drifts (and the largest one's center) and
+// max |c|^2; any non-finite drift or norm sets `bad`.
+__global__ __launch_bounds__(1024) void k_drift_top(const double* __restrict__ delta,
+                                                    const double* __restrict__ ccs, int k,
+                                                    DriftParams* __restrict__ prm) {
+  __shared__ double s1[1024], s2[1024], sc[1024];
+  __shared__ int si[1024];
+  const int t = threadIdx.x;
+  double d1 = 0.0, d2 = 0.0, cm = 0.0;
+  int i1 = -1;
+  bool bad = false;
+  for (int c = t; c < k; c += 1024) {
+    const double v = delta[c], q = ccs[c];
+    bad = bad || !(v <= 0x1p1000) || !(q <= 0x1p1000);   // NaN, inf
+    if (v > d1 || i1 < 0) {
+      d2 = i1 < 0 ? 0.0 : d1;
+      d1 = v;
+      i1 = c;
+    } else if (v > d2) {
+      d2 = v;
+    }
+    cm = __builtin_fmax(cm, q);
+  }
+  s1[t] = d1;
+  s2[t] = d2;
+  si[t] = i1;
+  sc[t] = cm;
+  bad = __syncthreads_or(bad);
+  for (int off = 512; off > 0; off >>= 1) {
+    if (t < off && si[t + off] >= 0) {
+      const double a1 = s1[t], a2 = s2[t], b1 = s1[t + off], b2 = s2[t + off];
+      const bool aEmpty = si[t] < 0;
+      if (aEmpty || b1 > a1) {
+        s1[t] = b1;
+        si[t] = si[t + off];
+        s2[t] = aEmpty ? b2 : __builtin_fmax(a1, b2);
+      } else {
+        s2[t] = __builtin_fmax(a2, b1);
+      }
+      sc[t] = __builtin_fmax(sc[t], sc[t + off]);
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    DriftParams p;
+    p.d1 = s1[0];
+    p.d2 = s2[0];
+    p.i1 = si[0];
+    p.cmax2 = sc[0];
+    p.bad = bad ? 1 : 0;
+    *prm = p;
+  }
+}
+
+// kBndRows rows per workgroup (8 per thread, coalesced): a row keeps its
+// assignment when its moved bounds still certify it (kmeans_i8.hpp Bounds);
+// the others are written, in row order, to tmp[block * kBndRows ...] and
+// counted in bcount[block].
+__global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict__ assign,
+                                                       float2* __restrict__ bnd,
+                                                       const double* __restrict__ xnorm,
+                                                       int64_t n, int k,
+                                                       const double* __restrict__ delta,
+                                                       const DriftParams* __restrict__ prm,
+                                                       int32_t* __restrict__ tmp,
+                                                       unsigned int* __restrict__ bcount) {
+  constexpr int IT = kBndRows / 256;
+  __shared__ unsigned wc[IT * 4];
+  const DriftParams P = *prm;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kBndRows;
+  unsigned long long masks[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int64_t r = base + it * 256 + tid;
+    bool listed = false;
+    if (r < n) {
+      listed = true;
+      const int a = assign[r];
+      const float2 b = bnd[r];
+      if (!P.bad && b.y > 0.0f && a >= 0 && a < k) {
+        const double U = (double)b.x + delta[a];
+        const double L = (double)b.y - (a == P.i1 ? P.d2 : P.d1);
+        const double xn = xnorm[r];
+        const double xx = xn * xn * (1.0 + 0x1p-40);
+        const double U2 = U * U, L2 = L * L;
+        // the reference's rounding slack, plus this test's own rounding
+        const double tau = 0x1p-29 * (xx + P.cmax2) + 0x1p-48 * (L2 + U2) + 0x1p-1000;
+        if (L > 0.0 && (L2 - U2) > tau) {
+          listed = false;
+          bnd[r] = make_float2(fup(U * (1.0 + 0x1p-50)), fdown(L * (1.0 - 0x1p-50)));
+        }
+      }
+    }
+    masks[it] = __builtin_amdgcn_ballot_w64(listed);
+    if (lane == 0) wc[it * 4 + wave] = (unsigned)__builtin_popcountll(masks[it]);
+  }
+  __syncthreads();
+  unsigned off = 0, total = 0;
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    unsigned before = 0;
+    for (int j = 0; j < it * 4 + wave; ++j) before += wc[j];
+    if ((masks[it] >> lane) & 1ull) {
+      off = before + (unsigned)__builtin_popcountll(masks[it] & below);
+      tmp[base + off] = (int32_t)(base + it * 256 + tid);
+    }
+  }
+  if (tid == 0) {
+    for (int j = 0; j < IT * 4; ++j) total += wc[j];
+    bcount[blockIdx.x] = total;
+  }
+}
+
+// Single block: bcount[0..nb) -> exclusive offsets, bcount[nb] = *listCount
+// = the total, added to *cum.
+__global__ __launch_bounds__(1024) void k_bounds_scan(unsigned int* __restrict__ bcount, int64_t nb,
+                                                      unsigned int* __restrict__ listCount,
+                                                      unsigned long long* __restrict__ cum) {
+  __shared__ unsigned part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t a = min<int64_t>(nb, t * per), e = min<int64_t>(nb, a + per);
+  unsigned s = 0;
+  for (int64_t i = a; i < e; ++i) s += bcount[i];
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const unsigned v = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  unsigned run = t ? part[t - 1] : 0u;
+  for (int64_t i = a; i < e; ++i) {
+    const unsigned c = bcount[i];
+    bcount[i] = run;
+    run += c;
+  }
+  if (t == 1023) {
+    bcount[nb] = part[1023];
+    *listCount = part[1023];
+    *cum += (unsigned long long)part[1023];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bounds_scatter(const int32_t* __restrict__ tmp,
+                                                        const unsigned int* __restrict__ off,
+                                                        int32_t* __restrict__ list) {
+  const int64_t b = blockIdx.x;
+  const unsigned o = off[b], c = off[b + 1] - o;
+  for (unsigned i = threadIdx.x; i < c; i += 256) list[o + i] = tmp[b * kBndRows + i];
+}
+
 template <int KS>
 int launch_screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
                   const void* Cb, const float* cq, const double* g, const double* cnorm,
@@ -2206,21 +2424,55 @@ int centers_prepare(const double* C, const double* cnorm, int k, int d, int ktp,
   return CYC_OK;
 }
 
+int centers_drift(const double* C, double* Cp, int k, int d, double* delta, double* ccs,
+                  DriftParams* prm, hipStream_t st) {
+  hipLaunchKernelGGL(k_center_drift, dim3((unsigned)((k + 3) / 4)), dim3(256), 0, st, C, Cp, k, d,
+                     delta, ccs);
+  CYC_LAUNCH_CHECK("k_center_drift");
+  hipLaunchKernelGGL(k_drift_top, dim3(1), dim3(1024), 0, st, (const double*)delta,
+                     (const double*)ccs, k, prm);
+  CYC_LAUNCH_CHECK("k_drift_top");
+  return CYC_OK;
+}
+
+int bounds_filter(const int32_t* assign, float2* ub_lb, const double* xnorm, int64_t n, int k,
+                  const double* delta, const DriftParams* prm, int32_t* tmp,
+                  unsigned int* bcount, int32_t* list, unsigned int* listCount,
+                  unsigned long long* cum, hipStream_t st) {
+  const int64_t nb = bounds_blocks(n);
+  if (nb <= 0) return CYC_OK;
+  KernelTimer timer("k_kmeans_bounds", st);
+  hipLaunchKernelGGL(k_bounds_filter, dim3((unsigned)nb), dim3(256), 0, st, assign, ub_lb, xnorm,
+                     n, k, delta, prm, tmp, bcount);
+  CYC_LAUNCH_CHECK("k_bounds_filter");
+  hipLaunchKernelGGL(k_bounds_scan, dim3(1), dim3(1024), 0, st, bcount, nb, listCount, cum);
+  CYC_LAUNCH_CHECK("k_bounds_scan");
+  hipLaunchKernelGGL(k_bounds_scatter, dim3((unsigned)nb), dim3(256), 0, st, (const int32_t*)tmp,
+                     (const unsigned int*)bcount, list);
+  CYC_LAUNCH_CHECK("k_bounds_scatter");
+  return CYC_OK;
+}
+
 int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
            const void* Cb, const float* cq, const double* g, const double* cnorm,
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
            unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st,
-           const CandArgs* ca, const RefineArgs* ra, const AppendStage* stg) {
+           const CandArgs* ca, const RefineArgs* ra, const AppendStage* stg,
+           const Bounds* bd) {
   if (n <= 0) return CYC_OK;
   if (stg && stg->cap < shard_cap(n)) {
     set_error("append stage smaller than shard_cap(n)");
     return CYC_ERR_INVALID_ARG;
   }
+  if (bd && !(ra && ca && uses32(d))) {
+    set_error("carried bounds need the one-limb pass (d <= 256, refinement, candidate pass)");
+    return CYC_ERR_INVALID_ARG;
+  }
   if (uses32(d)) {
     const int k32 = ktp * 16 / 32;   // launch over the padded center range (cq = +inf)
     switch (ksteps(d)) {
-      case 2: return screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st, ra, stg);
-      default: return screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st, ra, stg);
+      case 2: return screen32<4, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st, ra, stg, bd);
+      default: return screen32<8, 4>(img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, k32, assign, list, listCount, list2, list2Count, ca, st, ra, stg, bd);
     }
   }
   switch (ksteps(d)) {

@@ -130,17 +130,61 @@ int compact(unsigned int* counts, unsigned int cap, const int32_t* src, int32_t*
             const int32_t* src2, int32_t* dst2, int width2, unsigned int* dstCount,
             hipStream_t st);
 
+// Cross-iteration bounds of one fit (Hamerly's bounds, carried by the row
+// image's owner, cyc_kmeans_rows): per row the pair (ub, lb) of f32
+// DISTANCES (not squared), ub >= |x - c_a| for the row's assigned center a
+// and lb <= |x - c| for every other center, both for the centers of the
+// last call (kept in Cp); lb < 0 means "no bound".  The one-limb pass
+// writes them for every row it screens (rows it certifies get the bounds its
+// integer screen proves, the others lb = -1).  Before the next screen,
+// bounds_filter moves the bounds by the centers' drift (triangle inequality:
+// ub += |c_a' - c_a|, lb -= max over c != a of |c' - c|) and keeps a row's
+// assignment only when lb^2 - ub^2 still exceeds the reference's rounding
+// slack 2^-29 (|x|^2 + max |c|^2) -- the same standard as the candidate
+// pass's 2^-30 certification: the true distance to c_a is then below every
+// other center's by more than fp64 rounding, and the reference's pruned
+// loop returns a (the argument of the screens).  The
+// other rows are listed for the screen.
+struct DriftParams {
+  double d1, d2;     // the largest and second largest center drift (upper bounds)
+  double cmax2;      // an upper bound of max |c|^2 over the current centers
+  int i1;            // the center of d1
+  int bad;           // a non-finite drift or center: no row keeps its bounds
+};
+struct Bounds {
+  float2* ub_lb;               // n entries
+  const int32_t* rowsIn;       // the rows to screen (bounds_filter); nullptr: every row
+  const unsigned int* rowsInCount;
+};
+// Drift of the centers C against Cp (k x d, then Cp = C): delta (k doubles),
+// ccs (k doubles of scratch) and *prm.
+int centers_drift(const double* C, double* Cp, int k, int d, double* delta, double* ccs,
+                  DriftParams* prm, hipStream_t st);
+// The rows whose carried bounds still certify assign[row] keep it (their
+// bounds moved by the drift); the others go to list / *listCount (in row
+// order), and *cum (64-bit) accumulates their number.  tmp: n entries;
+// bcount: bounds_blocks(n) + 1 entries.
+constexpr int kBndRows = 2048;   // rows per filter workgroup
+inline int64_t bounds_blocks(int64_t n) { return (n + kBndRows - 1) / kBndRows; }
+int bounds_filter(const int32_t* assign, float2* ub_lb, const double* xnorm, int64_t n, int k,
+                  const double* delta, const DriftParams* prm, int32_t* tmp,
+                  unsigned int* bcount, int32_t* list, unsigned int* listCount,
+                  unsigned long long* cum, hipStream_t st);
+
 // Screen every row: certified rows get assign[row]; the others are appended
 // to list (listCount is NOT cleared here).  list2 / list2Count (n entries +
 // one counter): scratch for the rows the 32x32 two-limb pass leaves.
 // ca (d <= 256, optional): the candidate pass.  stg (optional, with ca; cap
-// >= shard_cap(n)): the 32x32 kernels append through it.
+// >= shard_cap(n)): the 32x32 kernels append through it.  bd (optional,
+// with ra): the one-limb pass screens bd->rowsIn (every row when null) and
+// writes the rows' bounds.
 int screen(const void* img, const int2* meta, const double* xnorm, int64_t n, int d,
            const void* Cb, const float* cq, const double* g, const double* cnorm,
            const CenterParams* prm, int ktp, int32_t* assign, int32_t* list,
            unsigned int* listCount, int32_t* list2, unsigned int* list2Count, hipStream_t st,
            const CandArgs* ca = nullptr,
-           const RefineArgs* ra = nullptr, const AppendStage* stg = nullptr);
+           const RefineArgs* ra = nullptr, const AppendStage* stg = nullptr,
+           const Bounds* bd = nullptr);
 
 }  // namespace km8
 }  // namespace cyc

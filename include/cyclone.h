@@ -115,6 +115,25 @@ int cyc_kmeans_rows_create(cyc_kmeans_plan plan, const double* X, int64_t n, voi
 int cyc_kmeans_rows_destroy(cyc_kmeans_rows rows);
 int64_t cyc_kmeans_rows_bytes(cyc_kmeans_rows rows);
 
+/* Carried bounds (Hamerly's, per fit): with a row image, every
+ * cyc_kmeans_accumulate_dev call (Euclidean, d <= 256, 96 < k <= 4096)
+ * keeps per row an upper bound of its distance to its assigned center and a
+ * lower bound to every other center, for the centers of that call.  The next
+ * call moves them by each center's drift (triangle inequality) and skips the
+ * screen only for rows whose moved bounds still separate the assigned center
+ * from every other by more than the reference's rounding slack
+ * (2^-29 (|x|^2 + max |c|^2)) -- the pruned reference loop (DistanceMeasure.
+ * scala:282-313) returns that same index, so assignments stay bit-identical;
+ * every other row is screened as before.  The first call of a fit screens
+ * every row.  State of the row image (one fit: one image, one Lloyd loop);
+ * cyc_kmeans_assign_dev / point_cost_dev neither use nor change it.
+ * set_bounds(rows, 0) turns it off (and either call drops the state; the
+ * environment CYC_KMEANS_BOUNDS=0 turns it off for every image).
+ * bounds_info: the accumulate calls that used it and the rows they screened
+ * (the rest kept their carried assignment); synchronises the device. */
+int cyc_kmeans_rows_set_bounds(cyc_kmeans_rows rows, int32_t enable);
+int cyc_kmeans_rows_bounds_info(cyc_kmeans_rows rows, int64_t* calls, int64_t* screened_rows);
+
 /* findClosest(centers, stats, point) for n points (stats from the last
  * cyc_kmeans_stats_dev on this plan).  assign[n], cost[n] device outputs.
  * rows: NULL or the image of exactly these X, n.

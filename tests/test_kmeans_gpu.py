@@ -763,3 +763,202 @@ def test_full_config_third_iteration(cuda):
     np.testing.assert_array_equal(wsum.cpu().numpy(), ref["wsum"])
     np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
                                atol=1e-10 * np.abs(ref["sums"]).max())
+
+
+def _lloyd_run(Xd, Cd0, cuda, iters, bounds, hook=None):
+    """`iters` Lloyd iterations through KMeansPlan.accumulate / update over a
+    row image with carried bounds on or off; per iteration the host copies of
+    (centers used, assign, cost, sums, wsum, cost_sum)."""
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    n, d = Xd.shape
+    k = Cd0.shape[0]
+    Cd = Cd0.clone()
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = KMeansPlan(d, k, n)
+    rows = p.rows(Xd)
+    rows.set_bounds(bounds)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    pc = torch.empty(n, dtype=torch.float64, device=cuda)
+    conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+    out = []
+    for it in range(iters):
+        if hook:
+            hook(it, Cd, cn)
+        Ch = Cd.cpu().numpy()
+        sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+        wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+        cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+        p.accumulate(Xd, xn, None, Cd, cn, sums, wsum, cost, a, pc, rows=rows)
+        out.append((Ch, a.cpu().numpy(), pc.cpu().numpy(), sums.cpu().numpy(),
+                    wsum.cpu().numpy(), cost.item()))
+        p.update(Cd, cn, sums, wsum, 1e-4, conv)
+    torch.cuda.synchronize()
+    return out, rows.bounds_info()
+
+
+@pytest.mark.parametrize("n,d,k,sep", [(200_000, 64, 128, 4.0), (120_000, 256, 1024, 3.0),
+                                       (150_000, 200, 300, 1.5)])
+def test_carried_bounds_bitwise(cuda, n, d, k, sep):
+    """Carried (Hamerly) bounds across the Lloyd iterations of one fit
+    (kmeans_i8.hpp Bounds): twelve iterations with the bounds on give the
+    SAME bits as with them off -- every row's assignment and cost, the
+    cluster sums, weights and cost -- and the last iteration equals the
+    restatement (KMeans.scala:275-334 on the same centers) for every row; the
+    bounds skipped the screen for rows (screened < n per call after the
+    first) without changing a bit."""
+    import torch
+    rng = np.random.default_rng(n + d + k + 11)
+    true_c = rng.normal(scale=sep, size=(k, d))
+    X = true_c[rng.integers(0, k, n)] + rng.normal(size=(n, d))
+    Xd = _dev(X, cuda)
+    C0 = Xd[:k].clone()
+    on, (calls, screened) = _lloyd_run(Xd, C0, cuda, 12, True)
+    off, (calls_off, _) = _lloyd_run(Xd, C0, cuda, 12, False)
+    assert calls == 12 and calls_off == 0
+    assert n <= screened < 12 * n
+    for it, (a, b) in enumerate(zip(on, off)):
+        np.testing.assert_array_equal(a[0], b[0], err_msg=f"centers, iteration {it}")
+        for j, name in ((1, "assign"), (2, "cost"), (3, "sums"), (4, "wsum")):
+            np.testing.assert_array_equal(a[j], b[j], err_msg=f"{name}, iteration {it}")
+        assert a[5] == b[5]
+    Ch, ah, ch = on[-1][0], on[-1][1], on[-1][2]
+    ref = oracle.kmeans_iteration(X, oracle.row_norms(X), None, Ch, oracle.row_norms(Ch),
+                                  num_partitions=8, threads=8)
+    bad = np.flatnonzero((ah != ref["assign"]) | (ch != ref["dist"]))
+    assert bad.size == 0, f"{bad.size} rows differ, first {bad[:10]}"
+
+
+def test_carried_bounds_moved_centers(cuda):
+    """The bounds follow whatever centers the caller passes: between Lloyd
+    iterations the centers are replaced (a jump of one center, a permutation
+    of two, a NaN center for one iteration, then finite again, identical
+    centers), and every iteration still equals the restatement bit for bit
+    (the NaN iteration raises the reference's require, as without bounds)."""
+    import torch
+    n, d, k = 60_000, 64, 130
+    rng = np.random.default_rng(5)
+    true_c = rng.normal(scale=3.0, size=(k, d))
+    X = true_c[rng.integers(0, k, n)] + rng.normal(size=(n, d))
+    Xd = _dev(X, cuda)
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    from cycloneml_amd import _native as N
+    xn = row_norms(Xd)
+    p = KMeansPlan(d, k, n)
+    rows = p.rows(Xd)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    pc = torch.empty(n, dtype=torch.float64, device=cuda)
+    Cd = Xd[:k].clone()
+    conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+    for it in range(9):
+        if it == 3:
+            Cd[7] += 5.0                      # one center jumps
+        if it == 4:
+            Cd[[1, 2]] = Cd[[2, 1]].clone()   # two centers swap indices
+        if it == 5:
+            Cd[9] = float("nan")
+        if it == 6:
+            Cd[9] = Xd[999]
+        if it == 7:
+            Cd[11] = Cd[12]                   # identical centers: ties
+        cn = row_norms(Cd)
+        Ch = Cd.cpu().numpy()
+        sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+        wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+        cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+        if it == 5:
+            with pytest.raises(N.IllegalArgumentException, match="norm2=NaN"):
+                p.accumulate(Xd, xn, None, Cd, cn, sums, wsum, cost, a, pc, rows=rows)
+            continue
+        p.accumulate(Xd, xn, None, Cd, cn, sums, wsum, cost, a, pc, rows=rows)
+        torch.cuda.synchronize()
+        ref = oracle.kmeans_iteration(X, oracle.row_norms(X), None, Ch, oracle.row_norms(Ch),
+                                      num_partitions=4, threads=4)
+        bad = np.flatnonzero((a.cpu().numpy() != ref["assign"]) |
+                             (pc.cpu().numpy() != ref["dist"]))
+        assert bad.size == 0, f"iteration {it}: {bad.size} rows differ, first {bad[:10]}"
+        p.update(Cd, cn, sums, wsum, 1e-4, conv)
+    calls, screened = rows.bounds_info()
+    assert calls == 9 and screened < 9 * n
+
+
+def test_carried_bounds_scope(cuda):
+    """Where the bounds do not apply they stay off: k <= 96 (no one-limb
+    pass), the cosine measure, and the calls other than accumulate
+    (assign / point_cost neither use nor move them)."""
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    n, d = 20_000, 32
+    rng = np.random.default_rng(8)
+    X = rng.normal(size=(n, d)) + rng.integers(0, 5, size=(n, 1)) * 3.0
+    Xd = _dev(X, cuda)
+    xn = row_norms(Xd)
+    for k, measure in ((96, "euclidean"), (200, "cosine"), (200, "euclidean")):
+        p = KMeansPlan(d, k, n, measure)
+        rows = p.rows(Xd)
+        Cd = Xd[:k].clone()
+        cn = row_norms(Cd)
+        a = torch.empty(n, dtype=torch.int32, device=cuda)
+        pc = torch.empty(n, dtype=torch.float64, device=cuda)
+        p.stats(Cd)
+        p.assign(Xd, xn, Cd, cn, a, pc, rows=rows)
+        p.point_cost(Xd, xn, Cd, cn, a, pc, rows=rows)
+        assert rows.bounds_info() == (0, 0)
+        sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+        wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+        cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+        p.accumulate(Xd, xn, None, Cd, cn, sums, wsum, cost, a, pc, rows=rows)
+        calls, screened = rows.bounds_info()
+        assert (calls, screened) == ((1, n) if (k, measure) == (200, "euclidean") else (0, 0))
+
+
+@pytest.mark.timeout(900)
+def test_full_config_late_iteration(cuda):
+    """BASELINE config 2 on bench.py's rows, one fit from setInitialModel
+    (rows 0..1023) as the bench and KMeans.run drive it: the carried bounds
+    on (the default), eleven Lloyd iterations, then the twelfth compared with
+    the restatement on the same centers for EVERY row (assignment and cost
+    bit for bit, weights exact, sums within 1e-10); by then the bounds let
+    most rows skip the screen."""
+    import os
+    import sys
+    import torch
+    from cycloneml_amd.clustering import row_norms
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    n, d, k = 10_000_000, 256, 1024
+    X = bench.kmeans_data(n, cuda, 0, d, k)
+    C = X[:k].clone()
+    xn, cn = row_norms(X), row_norms(C)
+    p = _plan(d, k, n)
+    rows = p.rows(X)
+    conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    pc = torch.empty(n, dtype=torch.float64, device=cuda)
+    last = 11
+    for it in range(last + 1):
+        if it == last:
+            Ch = C.cpu().numpy()
+            _, before = rows.bounds_info()
+        sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+        wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+        cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+        p.accumulate(X, xn, None, C, cn, sums, wsum, cost, a, pc, rows=rows)
+        if it < last:
+            p.update(C, cn, sums, wsum, 1e-4, conv)
+    calls, after = rows.bounds_info()
+    assert calls == last + 1
+    screened = after - before
+    assert 0 < screened < n // 2, screened
+    del rows
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or 16, os.cpu_count() or 1, 16)
+    Xh = X.cpu().numpy()
+    del X
+    ref = oracle.kmeans_iteration(Xh, xn.cpu().numpy(), None, Ch, oracle.row_norms(Ch),
+                                  num_partitions=threads, threads=threads)
+    ah, ch = a.cpu().numpy(), pc.cpu().numpy()
+    bad = np.flatnonzero((ah != ref["assign"]) | (ch != ref["dist"]))
+    assert bad.size == 0, f"{bad.size} rows differ, first {bad[:10]}"
+    np.testing.assert_array_equal(wsum.cpu().numpy(), ref["wsum"])
+    np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
+                               atol=1e-10 * np.abs(ref["sums"]).max())
