@@ -13,7 +13,10 @@ import re
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcyclone.so")
+# CYC_LIB_DIR: load the libraries from another directory (tools/asan_cpu.sh:
+# the AddressSanitizer build of the host code)
+LIB_DIR = os.environ.get("CYC_LIB_DIR") or _HERE
+LIB_PATH = os.path.join(LIB_DIR, "libcyclone.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cyclone.h")
 
 CYC_OK = 0

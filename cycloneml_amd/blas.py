@@ -29,7 +29,7 @@ import numpy as np
 from . import _native
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcyclone_blas.so")
+LIB_PATH = os.path.join(os.environ.get("CYC_LIB_DIR") or _HERE, "libcyclone_blas.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cyclone_blas.h")
 
 _P = ctypes.c_void_p

@@ -276,10 +276,11 @@ int cyc_libsvm_sizes(cyc_libsvm h, int64_t* n, int64_t* nnz, int32_t* numFeature
 int cyc_libsvm_copy(cyc_libsvm h, double* labels, int64_t* rowptr, int32_t* colidx,
                     double* values) {
   CYC_REQUIRE(h != nullptr, "handle must not be null");
-  if (labels) std::memcpy(labels, h->labels.data(), sizeof(double) * (size_t)h->n);
+  // (an empty parse has empty vectors, whose data() may be null: no memcpy)
+  if (labels && h->n) std::memcpy(labels, h->labels.data(), sizeof(double) * (size_t)h->n);
   if (rowptr) std::memcpy(rowptr, h->rowptr.data(), sizeof(int64_t) * (size_t)(h->n + 1));
-  if (colidx) std::memcpy(colidx, h->colidx.data(), sizeof(int32_t) * (size_t)h->nnz);
-  if (values) std::memcpy(values, h->values.data(), sizeof(double) * (size_t)h->nnz);
+  if (colidx && h->nnz) std::memcpy(colidx, h->colidx.data(), sizeof(int32_t) * (size_t)h->nnz);
+  if (values && h->nnz) std::memcpy(values, h->values.data(), sizeof(double) * (size_t)h->nnz);
   return CYC_OK;
 }
 

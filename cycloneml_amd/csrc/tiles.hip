@@ -62,6 +62,7 @@ struct cyc_tiles_s {
   // CYC_TILES_WIDE (32-bit packed ids) or CYC_TILES_COMPACT (16-bit ids:
   // column + row delta, with filler entries); entries = positions used
   int fmt = CYC_TILES_AUTO;
+  bool autoFmt = false;   // fmt chosen by AUTO (compact may still go wide: demote_to_wide)
   int64_t capEntries = 0, entries = 0;
   bool sealed = false;    // ends with a partial row block: no further appends
   int64_t maxSeg = 0;     // entries of the longest segment (picks the pass instances)
@@ -219,6 +220,96 @@ __global__ void k_tile_starts(const uint32_t* __restrict__ keys, int64_t cnt, in
 }
 
 __global__ void k_set_i64(int64_t* p, int64_t v) { *p = v; }
+
+// AUTO layouts demoted to WIDE (demote_to_wide): a thread per segment walks
+// its compact entries in order.  Pass 1 counts the fillers; pass 2 writes
+// the nonzeros as wide entries at segStart[s] - fillers before s, the row
+// rebuilt from the low bits (its high part = the times the low part went
+// down so far, k_tile_compact).
+__global__ void k_seg_fillers(const int64_t* __restrict__ segStart, const uint16_t* __restrict__ idx,
+                              int64_t segs, int64_t* __restrict__ fill) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < segs;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    int64_t f = 0;
+    for (int64_t q = segStart[s]; q < segStart[s + 1]; ++q) f += (idx[q] & kFillCol) == kFillCol;
+    fill[s] = f;
+  }
+}
+
+__global__ void k_seg_widen(const int64_t* __restrict__ segStart, const uint16_t* __restrict__ idx,
+                            const double* __restrict__ vals, int64_t segs,
+                            const int64_t* __restrict__ fillBefore, uint32_t* __restrict__ outIdx,
+                            double* __restrict__ outVals) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < segs;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    int64_t o = segStart[s] - fillBefore[s];
+    uint32_t hi = 0, lowPrev = 0;
+    for (int64_t q = segStart[s]; q < segStart[s + 1]; ++q) {
+      const uint32_t e = idx[q], low = e >> kColBits, col = e & kFillCol;
+      if (low < lowPrev) hi += 32;
+      lowPrev = low;
+      if (col == kFillCol) continue;
+      outIdx[o] = ((hi + low) << 16) | col;
+      outVals[o] = vals[q];
+      ++o;
+    }
+  }
+}
+
+__global__ void k_seg_shift(int64_t* __restrict__ segStart, const int64_t* __restrict__ fillBefore,
+                            int64_t segs) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= segs;
+       s += (int64_t)gridDim.x * blockDim.x)
+    segStart[s] -= fillBefore[s];
+}
+
+// An AUTO layout took COMPACT at its first append (dense enough rows) and an
+// append now meets rows too sparse for the filler allowance: rewrite the
+// first `segs` segments (everything committed) as WIDE entries in fresh
+// arrays, then free the compact ones.  Needs both layouts' memory at once;
+// on failure the layout is left as it was (still COMPACT).
+int demote_to_wide(cyc_tiles t, int64_t segs, hipStream_t st) {
+  cyc::DeviceBuffer fill, pre, tmp, idxW, valsW;
+  int rc;
+  const int64_t cap = std::max<int64_t>(t->capNnz, 1);
+  if ((rc = fill.reserve(sizeof(int64_t) * (size_t)(segs + 1))) ||
+      (rc = pre.reserve(sizeof(int64_t) * (size_t)(segs + 1))) ||
+      (rc = idxW.reserve(sizeof(uint32_t) * (size_t)cap)) ||
+      (rc = valsW.reserve(sizeof(double) * (size_t)cap)))
+    return rc;
+  CYC_HIP(hipMemsetAsync((int64_t*)fill.ptr + segs, 0, sizeof(int64_t), st));
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((segs + 255) / 256, 65536));
+  hipLaunchKernelGGL(k_seg_fillers, dim3(grid), dim3(256), 0, st, (const int64_t*)t->segStart.ptr,
+                     (const uint16_t*)t->idx.ptr, segs, (int64_t*)fill.ptr);
+  CYC_LAUNCH_CHECK("k_seg_fillers");
+  size_t bytes = 0;
+  CYC_HIP(rocprim::exclusive_scan(nullptr, bytes, (const int64_t*)fill.ptr, (int64_t*)pre.ptr,
+                                  (int64_t)0, (size_t)(segs + 1), rocprim::plus<int64_t>(), st));
+  if ((rc = tmp.reserve(std::max<size_t>(bytes, 1)))) return rc;
+  CYC_HIP(rocprim::exclusive_scan(tmp.ptr, bytes, (const int64_t*)fill.ptr, (int64_t*)pre.ptr,
+                                  (int64_t)0, (size_t)(segs + 1), rocprim::plus<int64_t>(), st));
+  hipLaunchKernelGGL(k_seg_widen, dim3(grid), dim3(256), 0, st, (const int64_t*)t->segStart.ptr,
+                     (const uint16_t*)t->idx.ptr, (const double*)t->vals.ptr, segs,
+                     (const int64_t*)pre.ptr, (uint32_t*)idxW.ptr, (double*)valsW.ptr);
+  CYC_LAUNCH_CHECK("k_seg_widen");
+  hipLaunchKernelGGL(k_seg_shift, dim3(grid), dim3(256), 0, st, (int64_t*)t->segStart.ptr,
+                     (const int64_t*)pre.ptr, segs);
+  CYC_LAUNCH_CHECK("k_seg_shift");
+  int64_t fillers = 0;
+  CYC_HIP(hipMemcpyAsync(&fillers, (const int64_t*)pre.ptr + segs, sizeof(int64_t),
+                         hipMemcpyDeviceToHost, st));
+  CYC_HIP(hipStreamSynchronize(st));
+  std::swap(t->idx.ptr, idxW.ptr);
+  std::swap(t->idx.bytes, idxW.bytes);
+  std::swap(t->idx.device, idxW.device);
+  std::swap(t->vals.ptr, valsW.ptr);
+  std::swap(t->vals.bytes, valsW.bytes);
+  std::swap(t->vals.device, valsW.device);
+  t->fmt = CYC_TILES_WIDE;
+  t->capEntries = cap;
+  t->entries -= fillers;   // the old arrays are freed with idxW / valsW
+  return CYC_OK;
+}
 
 // *mx = max(*mx, longest segment of [s0, s1)) -- a wave max, then one
 // atomic per wave
@@ -1075,6 +1166,11 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
   const int64_t chRows = nrbSub * kTileRows;
   const int64_t rb0 = t->n / kTileRows;
   cyc::DeviceBuffer keys, packed, keysOut, perm, tmp, counts, posb;
+  // an append that fails leaves the layout as it was before it (the
+  // segments it had written are rewritten by the next append of those rows)
+  const int64_t nnz0 = t->nnz;
+  int64_t entries0 = t->entries;
+  int arc = [&]() -> int {
   for (int64_t a = 0; a < rows; a += chRows) {
     const int64_t b = std::min(rows, a + chRows);
     int64_t qa = 0, qb = 0;
@@ -1138,6 +1234,13 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
           // fillers are at most 1/32 of its nonzeros
           if ((rc = set_storage(t, (total - cnt) * 32 <= cnt ? CYC_TILES_COMPACT : CYC_TILES_WIDE)))
             return rc;
+          t->autoFmt = true;
+        }
+        if (t->fmt == CYC_TILES_COMPACT && t->autoFmt && t->entries + total > t->capEntries) {
+          // AUTO chose compact on denser rows than these: the whole layout
+          // goes wide (this sub-chunk below in the wide form)
+          if ((rc = demote_to_wide(t, (rb0 + a / kTileRows) * T, st))) return rc;
+          entries0 = nnz0;
         }
       }
       if (t->fmt == CYC_TILES_COMPACT) {
@@ -1166,6 +1269,13 @@ int cyc_tiles_append_dev(cyc_tiles t, const int64_t* rowptr, const int32_t* coli
     t->nnz += cnt;
     t->entries += total;
     // scratch is reused by the next sub-chunk on this stream; freed on return
+  }
+  return CYC_OK;
+  }();
+  if (arc != CYC_OK) {
+    t->nnz = nnz0;
+    t->entries = entries0;
+    return arc;
   }
   t->n += rows;
   if (t->n % kTileRows != 0) t->sealed = true;

@@ -117,20 +117,34 @@ def dense_cluster_ids(pred):
     raises together through parallel.agree)."""
     torch = _torch()
     p = pred.to(torch.float64).reshape(-1)
-    local = torch.unique(p)
+    nan = torch.isnan(p)
+    has_nan = bool(nan.any())
+    # Spark groups every NaN prediction under ONE key (NaN equals NaN in
+    # grouping and sorts after every other double); torch.unique would not
+    local = torch.unique(p[~nan]) if has_nan else torch.unique(p)
 
     def bound():
-        if local.numel() > MAX_CLUSTERS:
+        if local.numel() + has_nan > MAX_CLUSTERS:
             raise N.IllegalArgumentException(
                 f"requirement failed: the device Silhouette supports at most {MAX_CLUSTERS} "
-                f"distinct cluster ids, got at least {local.numel()}")
+                f"distinct cluster ids, got at least {local.numel() + has_nan}")
     parallel.agree(bound)
-    mine = local.cpu().tolist()
-    keys = sorted(set().union(*[set(g) for g in parallel.allgather_object(mine)]))
-    if not keys:
+    mine = (local.cpu().tolist(), has_nan)
+    gathered = parallel.allgather_object(mine)
+    keys = sorted(set().union(*[set(g) for g, _ in gathered]))
+    any_nan = any(h for _, h in gathered)
+    K = len(keys) + (1 if any_nan else 0)
+    if K == 0:
         return torch.zeros(p.numel(), dtype=torch.int32, device=p.device), 1
     kt = torch.tensor(keys, dtype=torch.float64, device=p.device)
-    return torch.searchsorted(kt, p).to(torch.int32).contiguous(), len(keys)
+    ids = torch.searchsorted(kt, p) if keys else torch.zeros_like(p, dtype=torch.int64)
+    if has_nan:
+        ids = torch.where(nan, torch.full_like(ids, K - 1), ids)
+    ids = ids.to(torch.int32).contiguous()
+    if ids.numel() and int(ids.max()) >= K:   # the kernels index cluster statistics by id
+        raise N.IllegalArgumentException(
+            "requirement failed: a prediction maps outside the cluster ids")
+    return ids, K
 
 
 class ClusteringEvaluator:

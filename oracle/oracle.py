@@ -18,7 +18,9 @@ from concurrent.futures import ThreadPoolExecutor
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# CYC_ORACLE_LIB: a prebuilt copy to load instead (tools/asan_cpu.sh: the
+# AddressSanitizer build, `make -C oracle asan`)
+_LIB_PATH = os.environ.get("CYC_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 _lib = None
 _lock = threading.Lock()
 
@@ -39,7 +41,8 @@ def lib():
     with _lock:
         if _lib is None:
             src = os.path.join(_HERE, "cyclone_oracle.c")
-            if (not os.path.exists(_LIB_PATH)
+            if not os.environ.get("CYC_ORACLE_LIB") and (
+                    not os.path.exists(_LIB_PATH)
                     or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src)):
                 build()
             L = ctypes.CDLL(_LIB_PATH)

@@ -219,7 +219,14 @@ def _agree_rank(rank, world):
     mine = torch.tensor([[5, -3, 5], [1_000_000, 5, 7]][rank])
     ids, K = dense_cluster_ids(mine)
     want = [[1, 0, 1], [3, 1, 2]][rank]
-    return bool(ok and K == 4 and ids.tolist() == want and ids.dtype == torch.int32)
+    ok = bool(ok and K == 4 and ids.tolist() == want and ids.dtype == torch.int32)
+    # NaN predictions (rank 1 only) are ONE cluster, numbered after every
+    # other key, as Spark's grouping of the double column keys them
+    nan = float("nan")
+    mine = torch.tensor([[5.0, -3.0], [nan, 7.0, nan]][rank], dtype=torch.float64)
+    ids, K = dense_cluster_ids(mine)
+    want = [[1, 0], [3, 2, 3]][rank]
+    return bool(ok and K == 4 and ids.tolist() == want)
 
 
 def test_agree_two_ranks():

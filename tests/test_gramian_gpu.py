@@ -87,6 +87,44 @@ def _cov_ref(X):
     return np.asarray(oracle.triu_to_full(p, U)).reshape(p, p).T / (n - 1.0)
 
 
+def _assert_entrywise(got, ref, tol, what=""):
+    """|got - ref|_ij <= tol sqrt(ref_ii ref_jj) for EVERY entry: the
+    per-entry bar in units of the two columns' standard deviations (a
+    norm-wise bound says nothing about entries far below the largest)."""
+    d = np.sqrt(np.clip(np.diag(ref), 0.0, None))
+    lim = tol * np.outer(d, d)
+    bad = np.abs(got - ref) > lim
+    assert not bad.any(), (f"{what}: {int(bad.sum())} entries off, worst "
+                           f"{float((np.abs(got - ref) / np.maximum(lim / tol, 1e-300)).max()):.3g}")
+
+
+def test_covariance_entrywise_mixed_scales(cuda):
+    """Both dense covariance forms per ENTRY (|dC_ij| <= 1e-10 sqrt(C_ii
+    C_jj)) against the restatement of the reference's centred form
+    (computeDenseVectorCovariance, RowMatrix.scala:163-220): columns of
+    mixed scales (standard deviations 1e-3 .. 1e3 side by side) whose means
+    sit just inside the uncentred form's bound (mean = 7.9 sd, mean^2 = 62.4
+    variance) and exactly AT it (mean^2 = 64 variance, the bound's edge:
+    the auto choice's own check decides), and the centred syrk on the same
+    rows."""
+    from cycloneml_amd.linalg import RowMatrix
+    rng = np.random.default_rng(17)
+    n, p = 6000, 48
+    base = rng.normal(size=(n, p))
+    base = (base - base.mean(0)) / base.std(0, ddof=1)
+    scale = 10.0 ** rng.integers(-3, 4, size=p)
+    for shift in (7.9, 8.0):
+        X = (base + shift) * scale
+        ref = _cov_ref(X)
+        for form in ("auto", "uncentred", "centred"):
+            mat = RowMatrix(_dev(X, cuda))
+            mat.covarianceForm = form
+            cov = mat.computeCovariance()
+            if form == "auto" and shift == 7.9:
+                assert mat.lastCovarianceForm == "uncentred"
+            _assert_entrywise(cov, ref, 1e-10, f"shift {shift}, {form}")
+
+
 def test_covariance_form_choice(cuda):
     """RowMatrix._near_centred / _dense_covariance: the uncentred finish
     only when every column has mean^2 <= 64 variance; a large mean, a
@@ -308,6 +346,16 @@ def test_covariance_pca_bench_shard(cuda, bench_gram_rows):
     Cu = cov.cpu().numpy()
     assert np.array_equal(Cu, Cu.T)
     np.testing.assert_allclose(Cu, C, rtol=1e-10, atol=1e-10 * np.abs(C).max())
+    # per entry, in units of the columns' standard deviations
+    _assert_entrywise(Cu, C, 1e-10, "uncentred vs centred, whole shard")
+    # each form on the head and tail 2000 rows against the restatement
+    for a in (0, n - 2000):
+        Xs = X[a:a + 2000]
+        ref = _cov_ref(Xs.cpu().numpy())
+        for form in ("auto", "centred"):
+            sub = RowMatrix(Xs)
+            sub.covarianceForm = form
+            _assert_entrywise(sub.computeCovariance(), ref, 1e-10, f"rows {a}.., {form}")
     w = torch.zeros(p, dtype=torch.float64, device=cuda)
     for s in range(0, n, 1 << 20):
         xc = X[s:s + (1 << 20)] - mean

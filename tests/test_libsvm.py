@@ -143,3 +143,55 @@ def test_libsvm_binary_lr_on_device(cuda):
     g = agg.gradientSumArray.cpu().numpy()
     np.testing.assert_allclose(g, st["grad"], rtol=1e-10, atol=1e-10 * np.abs(st["grad"]).max())
     assert float(agg._loss_sum.item()) == pytest.approx(st["loss"], rel=1e-10)
+
+
+@pytest.mark.parametrize("bad,msg", [
+    ("1 3", 'For input string: "3" (index)'),          # no ':' (the reference: split(':')(1))
+    ("1 3:", 'For input string: "" (value)'),
+    ("1 :3", 'For input string: "" (index)'),
+    ("1 1: 2", 'For input string: "" (value)'),
+    ("1 99999999999:1", 'For input string: "99999999999" (index)'),   # past Int
+    ("1 2147483648:1", 'For input string: "2147483648" (index)'),
+    ("1 -5:1", "found current=-6, previous=-1"),
+    ("1 1:-0x", 'For input string: "-0x" (value)'),
+])
+def test_malformed_lines(bad, msg):
+    """parseLibSVMRecord's failures on malformed items (MLUtils.scala:129-151:
+    item.split(':'), toInt, toDouble, the ascending-index require) come back
+    as the reference's exception text; nothing reads past the line."""
+    from cycloneml_amd import _native as N, mlutils
+    with pytest.raises(N.IllegalArgumentException, match="requirement failed") as e:
+        mlutils.parseLibSVM("0 1:1\n" + bad + "\n2 1:3\n")
+    assert msg in str(e.value)
+
+
+def test_overlong_numbers_and_extra_fields():
+    """Java's toDouble of a decimal beyond the double range is Infinity (not an
+    error), a 5,000-digit mantissa included; an item "1:1:2" keeps fields 0
+    and 1 (split(':')); a 400-digit label parses as well."""
+    from cycloneml_amd import mlutils
+    text = ("1 1:1e999\n1 1:" + "1" * 5000 + "\n1 1:1:2\n1" + "0" * 400 + " 1:1\n"
+            "1 1:1  2:2 \n")
+    labels, (rp, ci, v), nf = mlutils.parseLibSVM(text)
+    assert list(rp) == [0, 1, 2, 3, 4, 6] and nf == 2
+    assert v[0] == np.inf and v[1] == np.inf and v[2] == 1.0 and np.isinf(labels[3])
+    assert list(ci) == [0, 0, 0, 0, 0, 1]
+
+
+def test_garbage_never_crashes():
+    """Random bytes (digits, ':', signs, exponents, whitespace, NUL and
+    non-ASCII) line by line: every line either parses or raises the
+    reference's IllegalArgumentException -- the parser stays inside its
+    buffer (tools/asan_cpu.sh runs this under AddressSanitizer)."""
+    from cycloneml_amd import _native as N, mlutils
+    rng = np.random.default_rng(7)
+    alphabet = np.frombuffer(b"0123456789:: +-.eE\tabxX\x00\xff\r9", dtype=np.uint8)
+    ok = bad = 0
+    for i in range(3000):
+        line = bytes(rng.choice(alphabet, size=int(rng.integers(0, 40)))).replace(b"\n", b" ")
+        try:
+            mlutils.parseLibSVM(b"0 1:1\n" + line + b"\n", nthreads=1 + i % 3)
+            ok += 1
+        except N.IllegalArgumentException:
+            bad += 1
+    assert ok + bad == 3000 and bad > 0

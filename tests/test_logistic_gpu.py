@@ -691,3 +691,54 @@ def test_multinomial_margin_spread_past_708(cuda):
         _rel_close(agg.gradientSumArray.cpu().numpy(), st["grad"])
         loss = float(agg._loss_sum.item())
         assert np.isfinite(loss) and abs(loss - st["loss"]) <= 1e-10 * abs(st["loss"])
+
+
+def test_tiles_auto_demotes_to_wide(cuda):
+    """CYC_TILES_AUTO decides at the first append; a later append whose rows
+    are too sparse for the compact format's filler allowance (a dense head of
+    config 5's shape, then a tail with a nonzero every 80th row over 26 row
+    blocks: two fillers per nonzero) turns the whole layout wide
+    (tiles.hip demote_to_wide) instead of failing, and the aggregator state
+    is the same bits as a layout built wide from the start.  An explicitly
+    compact layout still fails such an append with the message naming the
+    wide format -- and is left as it was before the append."""
+    import torch
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.optim import (BinaryLogisticBlockAggregator, DeviceInstanceBlock,
+                                     SparseTiles)
+    F = 1_000_000
+    rng = np.random.default_rng(33)
+    _, (rph, cih, vvh), _, _ = _make(8192, F, True, rng, nnz=64)
+    gap, blocks = 80, 26
+    nt = gap * 2048 * blocks
+    nzt = np.zeros(nt, dtype=np.int64)
+    nzt[::gap] = 1
+    rpt = np.concatenate([[0], np.cumsum(nzt)])
+    cit = rng.integers(0, F, size=int(nzt.sum())).astype(np.int32)
+    vvt = rng.uniform(-1, 1, size=cit.size)
+    n = 8192 + nt
+    rp = np.concatenate([rph, rpt[1:] + rph[-1]])
+    ci, vv = np.concatenate([cih, cit]), np.concatenate([vvh, vvt])
+    labels = rng.integers(0, 2, size=n).astype(np.float64)
+    w = rng.uniform(0.1, 2.0, size=n)
+    dev = lambda a: torch.as_tensor(a, device=cuda)
+    auto = SparseTiles(F, n, ci.size)
+    auto.append(dev(rph), dev(cih), dev(vvh))
+    assert auto.format == "compact"
+    auto.append(dev(rpt), dev(cit), dev(vvt))
+    assert auto.format == "wide" and auto.nnz == ci.size and auto.entries == auto.nnz
+    wide = SparseTiles.from_csr(dev(rp), dev(ci), dev(vv), F, format="wide")
+    coef = rng.normal(size=F + 1) * 0.3
+    sm = dev(rng.normal(size=F) * 0.1)
+    states = []
+    for t in (auto, wide):
+        blk = DeviceInstanceBlock(dev(labels), dev(w), tiles=t, numFeatures=F)
+        b = BinaryLogisticBlockAggregator(np.ones(F), sm, True, True, coef, device=cuda).add(blk)
+        states.append(b._state.cpu().numpy())
+    assert np.array_equal(states[0], states[1])
+    comp = SparseTiles(F, n, ci.size, format="compact")
+    comp.append(dev(rph), dev(cih), dev(vvh))
+    nnz0, ent0 = comp.nnz, comp.entries
+    with pytest.raises(N.IllegalArgumentException, match="CYC_TILES_WIDE"):
+        comp.append(dev(rpt), dev(cit), dev(vvt))
+    assert (comp.format, comp.nnz, comp.entries) == ("compact", nnz0, ent0)
