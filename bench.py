@@ -376,7 +376,13 @@ class KMeansWorkload:
         from cycloneml_amd.clustering import KMeans, KMeansModel
         km = KMeans(k=self.k, maxIterations=max_iter, epsilon=1e-4)
         km.setInitialModel(KMeansModel(self.C0.cpu().numpy()))
-        return {"iterations": km.run(self.X).numIter,
+        marks = [time.perf_counter()]
+        # each iteration ends with the host's convergence check (a sync)
+        model = km.run(self.X, iteration_callback=lambda it, c: marks.append(time.perf_counter()))
+        return {"iterations": model.numIter,
+                "iteration_ms": [round((b - a) * 1e3, 3) for a, b in zip(marks[:-1], marks[1:])],
+                "iteration_ms_note": "wall time between the host's convergence checks; the first "
+                                     "includes the norms, the plan and the row image",
                 "note": "one fit from setInitialModel (rows 0..k-1), maxIter 20, tol 1e-4: "
                         "norms + plan + row image + every iteration with its host convergence "
                         "check, over iterations 1..maxIter (value times steady-state "
