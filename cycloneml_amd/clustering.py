@@ -52,6 +52,9 @@ def xorshift_next_int(seed: int) -> int:
     return v - (1 << 32) if v >= 1 << 31 else v
 
 
+IMAGE_MAX_D = 512   # the i8 row image's widest rows (kmeans_i8.hpp kMaxD)
+
+
 class KMeansPlan:
     """RAII wrapper of cyc_kmeans_plan (device scratch for one (d, k) shape
     and one DistanceMeasure)."""
@@ -502,7 +505,13 @@ class KMeans:
         torch = _torch()
         dev = X.device
         n, d = X.shape
-        if xnorm is None:
+        # the cached norms (KMeans.scala:263-270): with setInitialModel and a
+        # Euclidean row image (d <= 512) the Lloyd loop needs none from the
+        # caller -- the image carries norms for the screens' margins and the
+        # exact tier computes the reference's own norm for the rows it takes
+        # (cyclone.h cyc_kmeans_accumulate_dev, xnorm NULL)
+        if xnorm is None and (self.initialModel is None or self.distanceMeasure != EUCLIDEAN
+                              or d > IMAGE_MAX_D):
             xnorm = row_norms(X, stream=stream)
         if self.initialModel is None:
             C0 = self.initial_centers(X, xnorm, partition_starts)

@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -10,6 +12,7 @@
 #include <set>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -77,13 +80,91 @@ int hip_fail(hipError_t e, const char* what, const char* file, int line) {
   return CYC_ERR_HIP;
 }
 
+// Deferred frees.  hipFree costs ~0.2 ms of host time per call (measured on
+// MI355X: tools/probe/hip_malloc_probe.py) and a plan + row image hold ~50
+// buffers, so tearing down one KMeans fit took ~14 ms of its caller's time.
+// Released buffers therefore go to one process-wide reaper thread that
+// frees them in the background (hipFree itself waits for the device, so no
+// buffer is freed under work still in flight); an allocation that fails
+// waits for the pending frees and retries.  CYC_SYNC_FREE=1 frees inline.
+namespace {
+struct Reaper {
+  std::mutex mu;
+  std::condition_variable cv, idle;
+  std::deque<std::pair<void*, int>> q;
+  bool started = false, busy = false, stop = false;
+  std::thread th;
+
+  void run() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return stop || !q.empty(); });
+      if (q.empty()) break;   // stop requested and nothing left
+      const auto it = q.front();
+      q.pop_front();
+      busy = true;
+      lk.unlock();
+      (void)hipSetDevice(it.second);
+      (void)hipFree(it.first);
+      lk.lock();
+      busy = false;
+      if (q.empty()) idle.notify_all();
+    }
+    idle.notify_all();
+  }
+  void push(void* p, int dev) {
+    std::lock_guard<std::mutex> g(mu);
+    if (!started) {
+      started = true;
+      th = std::thread([this] { run(); });
+      std::atexit([] { reaper_stop(); });
+    }
+    q.emplace_back(p, dev);
+    cv.notify_one();
+  }
+  void drain() {
+    std::unique_lock<std::mutex> lk(mu);
+    idle.wait(lk, [&] { return q.empty() && !busy; });
+  }
+  static Reaper& get() {
+    static Reaper* r = new Reaper();   // never destroyed: exit joins it below
+    return *r;
+  }
+  static void reaper_stop() {
+    Reaper& r = get();
+    {
+      std::lock_guard<std::mutex> g(r.mu);
+      r.stop = true;
+      r.cv.notify_all();
+    }
+    if (r.th.joinable()) r.th.join();   // the pending frees, before HIP's own teardown
+  }
+};
+bool sync_free() {
+  static const bool v = [] {
+    const char* e = std::getenv("CYC_SYNC_FREE");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+}  // namespace
+
 int DeviceBuffer::reserve(size_t n) {
   int dev = 0;
   CYC_HIP(hipGetDevice(&dev));
   if (ptr && bytes >= n && device == dev) return CYC_OK;
   release();
   if (n == 0) n = 16;
-  CYC_HIP(hipMalloc(&ptr, n));
+  hipError_t e = hipMalloc(&ptr, n);
+  if (e == hipErrorOutOfMemory && !sync_free()) {
+    (void)hipGetLastError();
+    Reaper::get().drain();   // the memory of pending frees, then once more
+    e = hipMalloc(&ptr, n);
+  }
+  if (e != hipSuccess) {
+    ptr = nullptr;
+    return cyc::hip_fail(e, "hipMalloc", __FILE__, __LINE__);
+  }
   bytes = n;
   device = dev;
   return CYC_OK;
@@ -93,9 +174,14 @@ void DeviceBuffer::release() {
   if (ptr) {
     int cur = 0;
     (void)hipGetDevice(&cur);
-    if (device >= 0 && device != cur) (void)hipSetDevice(device);
-    (void)hipFree(ptr);
-    if (device >= 0 && device != cur) (void)hipSetDevice(cur);
+    const int dev = device >= 0 ? device : cur;
+    if (sync_free()) {
+      if (dev != cur) (void)hipSetDevice(dev);
+      (void)hipFree(ptr);
+      if (dev != cur) (void)hipSetDevice(cur);
+    } else {
+      Reaper::get().push(ptr, dev);
+    }
   }
   ptr = nullptr;
   bytes = 0;

@@ -994,7 +994,7 @@ __global__ __launch_bounds__(256) void k_assign_exact(
     const double* __restrict__ cnorm, int k,
     const double* __restrict__ stats, const int32_t* __restrict__ slowList,
     const unsigned int* __restrict__ slowCount, int32_t* __restrict__ assign,
-    double* __restrict__ cost) {
+    double* __restrict__ cost, int exactNorm) {
   // One workgroup per listed row.  A distance is a pure function of (center,
   // row), so the workgroup first computes Vectors.sqdist(center, x) -- in
   // order j = 0..d-1 (Vectors.scala:580-587) -- for a chunk of 1024 centers
@@ -1004,6 +1004,7 @@ __global__ __launch_bounds__(256) void k_assign_exact(
   __shared__ double xs[kExactX];
   __shared__ double dds[kExactChunk];
   __shared__ int doneS;
+  __shared__ double xnS;
   const unsigned cnt = *slowCount;
   const int tid = threadIdx.x, lane = tid & 63;
   // stats == nullptr: findClosest(centers, point) (:318-340), best from +inf
@@ -1011,12 +1012,20 @@ __global__ __launch_bounds__(256) void k_assign_exact(
   for (unsigned idx = blockIdx.x; idx < cnt; idx += gridDim.x) {
     const int64_t r = slowList[idx];
     const double* x = X + r * d;
-    const double xn = xnorm[r];
-    __syncthreads();   // the previous row's reads of xs / dds are done
+    __syncthreads();   // the previous row's reads of xs / dds / xnS are done
     const bool xl = d <= kExactX;
     if (xl)
       for (int j = tid; j < d; j += 256) xs[j] = x[j];
     const double* xv = xl ? xs : x;
+    // exactNorm: the caller's norms are the row image's (any summation
+    // order, for the screens' margins); the loop's prune needs the
+    // reference's Vectors.norm, in index order (seq_norm2)
+    if (exactNorm) {
+      __syncthreads();
+      if (tid == 0) xnS = seq_norm2(xv, d);
+      __syncthreads();
+    }
+    const double xn = exactNorm ? xnS : xnorm[r];
     double best = __builtin_inf();   // wave 0's replay state
     int bi = 0;
     bool done = false;
@@ -1846,7 +1855,8 @@ struct cyc_kmeans_rows_s {
   int d = 0;
   bool usable = false;     // d <= 512
   bool cosine = false;     // image of the unit directions x / |x|
-  cyc::DeviceBuffer img, meta, unorm;   // unorm: |x / |x|| per row (cosine)
+  cyc::DeviceBuffer img, meta, unorm;   // unorm: |x / |x|| per row (cosine); |x| (Euclidean:
+                                        // any summation order, the screens' margins)
   // Carried bounds of one fit's Lloyd iterations (kmeans_i8.hpp Bounds):
   // cyc_kmeans_accumulate_dev screens only the rows they cannot certify.
   // State: per row (ub, lb) and the assignment they certify (bAssign), the
@@ -2085,7 +2095,7 @@ int stage_args(cyc_kmeans_plan p, int64_t n, bool useCa, cyc::km8::AppendStage& 
 int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmeans_rows rows,
               int64_t n, const double* C, const double* cnorm, int32_t* assign, double* cost,
               int64_t* n_exact_out, hipStream_t st, bool nostats = false,
-              const cyc::km8::Bounds* bd = nullptr) {
+              const cyc::km8::Bounds* bd = nullptr, bool approxNorm = false) {
   // nostats: findClosest(centers, point) (DistanceMeasure.scala:318-340); the
   // screens certify only rows whose winner both loops return, so only the
   // exact tier differs (no statistics prunes, best starts at +inf)
@@ -2178,7 +2188,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
       hipLaunchKernelGGL(k_assign_exact, dim3((unsigned)std::min<unsigned>(h_slow, 4096)), dim3(256), 0, st, X, xnorm,
                          p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm, p->k, statsArg,
                          (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr,
-                         assign, cost);
+                         assign, cost, approxNorm ? 1 : 0);
       CYC_LAUNCH_CHECK("k_assign_exact");
     }
   } else {
@@ -2186,7 +2196,7 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
     hipLaunchKernelGGL(k_assign_exact, dim3(grid), dim3(256), 0, st, X, xnorm,
                        p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm, p->k, statsArg,
                        (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr, assign,
-                       cost);
+                       cost, approxNorm ? 1 : 0);
     CYC_LAUNCH_CHECK("k_assign_exact");
   }
   return CYC_OK;
@@ -2218,10 +2228,19 @@ int require_enqueue(cyc_kmeans_plan p, const double* C, const double* xnorm, int
 // (0, m) for the lowest NaN center m > 0, or (0, 1) when center 0 is NaN;
 // with k == 1 there are no statistics and the first point meets center 0;
 // otherwise the first NaN-norm point meets center 0 (norm2 = NaN).
-int require_check(cyc_kmeans_plan p, int64_t n) {
+int require_check(cyc_kmeans_plan p, int64_t n, const double* Xrow0 = nullptr) {
   CYC_HIP(hipEventSynchronize(p->reqEv));
   const unsigned long long cbad = p->reqHost[0], rbad = p->reqHost[1];
-  const double* v = reinterpret_cast<const double*>(p->reqHost + 2);
+  double* v = reinterpret_cast<double*>(p->reqHost + 2);
+  if (Xrow0 && n > 0 && cbad == 0 && !(p->k >= 2)) {
+    // the message's norm2 is row 0's Vectors.norm: the image's norms (in
+    // another summation order) stand in for the caller's, so recompute it
+    std::vector<double> x0((size_t)p->d);
+    CYC_HIP(hipMemcpy(x0.data(), Xrow0, sizeof(double) * (size_t)p->d, hipMemcpyDeviceToHost));
+    double sq = 0.0;
+    for (int j = 0; j < p->d; ++j) sq = sq + x0[j] * x0[j];
+    v[2] = std::sqrt(sq);
+  }
   const double nan = __builtin_nan("");
   auto fail = [](double n1, double n2) {
     cyc::set_error("requirement failed: Both norms should be greater or equal to 0.0, found "
@@ -2627,7 +2646,14 @@ int cyc_kmeans_rows_create(cyc_kmeans_plan p, const double* X, int64_t n, void* 
                                    (const double*)xn.ptr, (double*)r->unorm.ptr);
       if (!rc && hipStreamSynchronize(st) != hipSuccess) rc = CYC_ERR_HIP;   // xn freed here
     } else {
-      rc = cyc::km8::rows_quantize(X, n, p->d, r->img.ptr, (int2*)r->meta.ptr, st);
+      // with the image, the norms in any summation order (a wave sum): what
+      // the screens need when the caller passes no norms (accumulate_dev)
+      if ((rc = r->unorm.reserve(sizeof(double) * (size_t)n))) {
+        delete r;
+        return rc;
+      }
+      rc = cyc::km8::rows_quantize(X, n, p->d, r->img.ptr, (int2*)r->meta.ptr, st, nullptr,
+                                   (double*)r->unorm.ptr);
     }
     if (rc) {
       delete r;
@@ -2768,6 +2794,12 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
     cyc::set_error("d > 1240 is not supported by the LDS-resident assign kernel (dense rows)");
     return CYC_ERR_UNSUPPORTED;
   }
+  // xnorm == NULL: the row image's norms for the screens (Euclidean), the
+  // reference's own norms computed where its loop needs them (k_assign_exact)
+  const bool approxNorm = xnorm == nullptr;
+  CYC_REQUIRE(!approxNorm || (rows && rows->usable && !rows->cosine && rows->unorm.ptr),
+              "xnorm may be null only with a Euclidean row image (cyc_kmeans_rows_create)");
+  if (approxNorm) xnorm = (const double*)rows->unorm.ptr;
   std::lock_guard<std::mutex> g(p->mu);
   hipStream_t st = cyc::as_stream(stream);
   const int k = p->k, d = p->d;
@@ -2797,7 +2829,7 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
       assign = (int32_t*)rows->bAssign.ptr;
     }
     if ((rc = do_assign(p, X, xnorm, rows, n, C, cnorm, assign, nullptr, nullptr, st, false,
-                        useBnd ? &bd : nullptr)))
+                        useBnd ? &bd : nullptr, approxNorm)))
       return rc;
     if (useBnd) {
       rows->bValid = true;
@@ -2874,7 +2906,7 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   hipLaunchKernelGGL(k_cost_total, dim3(1), dim3(256), 0, st, (const double*)p->ccost.ptr, k,
                      cost_sum);
   CYC_LAUNCH_CHECK("k_cost_total");
-  return cosm ? cos_check(p) : require_check(p, n);
+  return cosm ? cos_check(p) : require_check(p, n, approxNorm ? X : nullptr);
 }
 
 int cyc_kmeans_update_dev(cyc_kmeans_plan p, double* C, double* cnorm, const double* sums,

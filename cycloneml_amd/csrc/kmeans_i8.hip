@@ -129,6 +129,82 @@ __device__ __forceinline__ double err_term(int e, double n1, double mu, int d) {
   return (0.5 * mu * A * A + 0.5 * n1 * n1 / mu + kd * A * A) * (1.0 + 0x1p-40);
 }
 
+// The same for 16-byte aligned rows of even d <= 128 H, the next row's loads
+// issued before this row's reductions and stores (software-pipelined: two
+// rows in flight per wave; the row-at-a-time loop left the stream latency
+// bound at ~3.4 TB/s of reads + writes).  Same limbs, exponents and meta.
+template <int H>
+__global__ __launch_bounds__(256) void k_rows_quantize_pf(const double* __restrict__ X, int64_t n,
+                                                          int d, int D, unsigned* __restrict__ img,
+                                                          int2* __restrict__ meta,
+                                                          const double* __restrict__ scale,
+                                                          double* __restrict__ unorm) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  v2d cur[H];
+  auto load = [&](int64_t r, v2d (&w)[H]) {
+    const double* x = X + (r < n ? r : 0) * d;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const int j = h * 128 + 2 * lane;
+      w[h] = j < d ? __builtin_nontemporal_load(reinterpret_cast<const v2d*>(x + j)) : v2d{0.0, 0.0};
+    }
+  };
+  if (row < n) load(row, cur);
+  for (; row < n; row += nw) {
+    v2d nxt[H];
+    load(row + nw, nxt);   // in flight while this row is reduced and stored
+    double v[2 * H];
+    double m = 0.0, s1 = 0.0, s2 = 0.0;
+    bool fin = true;
+    const double sc = scale ? scale[row] : 1.0;
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        double t = q ? cur[h].y : cur[h].x;
+        if (scale) t = t / sc;
+        v[2 * h + q] = t;
+        fin = fin && __builtin_isfinite(t);
+        m = __builtin_fmax(m, __builtin_fabs(t));
+        s1 += __builtin_fabs(t);
+        s2 += t * t;
+      }
+    m = wave_max(m);
+    s1 = wave_sum(s1);
+    if (unorm) {
+      s2 = wave_sum(s2);
+      if (lane == 0) unorm[row] = __builtin_sqrt(s2);
+    }
+    const bool allFin = __all(fin);
+    const int e = choose_exp(m);
+    const bool bad = !allFin || e > kMaxExp;
+    unsigned char* db = reinterpret_cast<unsigned char*>(img + row * (int64_t)(3 * D / 4));
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      const int j0 = h * 128 + 2 * lane;
+      if (j0 < D) {
+        int a[2], b[2], c[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (bad) a[q] = b[q] = c[q] = 0;
+          else quant3(v[2 * h + q], e, a[q], b[q], c[q]);
+        }
+        *reinterpret_cast<unsigned short*>(db + j0) = (unsigned short)((a[0] & 0xff) | ((a[1] & 0xff) << 8));
+        *reinterpret_cast<unsigned short*>(db + D + j0) = (unsigned short)((b[0] & 0xff) | ((b[1] & 0xff) << 8));
+        *reinterpret_cast<unsigned short*>(db + 2 * D + j0) = (unsigned short)((c[0] & 0xff) | ((c[1] & 0xff) << 8));
+      }
+    }
+    if (lane == 0) {
+      const double n1 = bad ? 0.0 : s1 * (1.0 + 0x1p-40) + (double)d * __builtin_ldexp(1.0, e - 22);
+      meta[row] = make_int2(bad ? INT_MIN : e, __float_as_int(fup(n1)));
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) cur[h] = nxt[h];
+  }
+}
+
 // One wave per row: limbs into the image, exponent and |xh|_1 bound into meta.
 // scale (optional): the row is x / scale[row] (the cosine plan's unit
 // directions), whose norm goes to unorm[row] (any summation order: it only
@@ -683,6 +759,56 @@ __device__ __forceinline__ double err_term2(int e, double n1, double mu, int d) 
   return (0.5 * mu * A * A + 0.5 * n1 * n1 / mu + kd * A * A) * (1.0 + 0x1p-40);
 }
 
+// Carried bounds (kmeans_i8.hpp Bounds) from a screen's computed bounds.
+// With Lt_c = |c|^2 - 2 x.c and L'_c = cq_c - 2 s_c its exact integer form
+// (cq_c <= |c|^2 - 2 g_c, |x.c - s_c| <= fx + g_c): Lt_c >= L'_c - 2 fx, and
+// a computed bound l is within enc of L' (the integer passes' index bits and
+// floors; 0 for the three-limb f32 bounds, whose rounding the 2^-20 slack
+// covers together with xx = xnorm^2, within 2^-44 xx of the true |x|^2).
+// Every center whose computed bound is >= l therefore has
+//   |x - c|^2 >= xx + l - enc - 2 fx                       (bnd_lb_sq)
+// and the winner, bound l1, |x - c_w|^2 <= xx + l1 + enc + 2 fx + 4 g_w
+// + eps |c_w|^2 (cq rounded down; the 2^-20 terms as in the margins M).
+// `extra`: a further slack (the f32 three-limb bounds: 2^-20 max cq).
+__device__ __forceinline__ double bnd_ub_sq(double xx, double cc, double l1, double fx, double gw,
+                                            double enc) {
+  return (xx + l1 + enc + 2.0 * fx + 4.0 * gw + 2.0 * kEpsF * (xx + cc) +
+          0x1p-20 * (xx + __builtin_fabs(l1) + cc + 2.0 * gw) + 0x1p-90) *
+         (1.0 + 0x1p-30);
+}
+__device__ __forceinline__ double bnd_lb_sq(double xx, double l, double fx, double enc,
+                                            double extra) {
+  return xx + l - enc - 2.0 * fx - 2.0 * kEpsF * xx -
+         0x1p-20 * (xx + __builtin_fabs(l) + 2.0 * fx + enc) - extra;
+}
+// as f32 distances: up rounded up; a lower bound <= 0 (or NaN) is "none" (-1)
+__device__ __forceinline__ float bnd_dist_up(double s2) {
+  return fup(__builtin_sqrt(s2) * (1.0 + 0x1p-50));
+}
+__device__ __forceinline__ float bnd_dist_dn(double s2) {
+  return s2 > 0.0 ? fdown(__builtin_sqrt(s2) * (1.0 - 0x1p-50)) : -1.0f;
+}
+// the largest of each row's per-lane values over its 32 lanes (the screens'
+// register layout: lane (r, h) holds row (reg & 3) + 8 (reg >> 2) + 4 h of
+// register reg): halving shuffles, then per row into out[32] (LDS)
+__device__ __forceinline__ void rows_max32(int (&v)[16], int lane, int* out) {
+#pragma unroll
+  for (int lev = 0; lev < 4; ++lev) {
+    const int half = 8 >> lev, m = 16 >> lev;
+    const bool hi = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < half; ++i) {
+      const int o = __shfl_xor(hi ? v[i] : v[i + half], m);
+      v[i] = max(hi ? v[i + half] : v[i], o);
+    }
+  }
+  v[0] = max(v[0], __shfl_xor(v[0], 1));
+  if ((lane & 1) == 0) {
+    const int q = (lane >> 1) & 15;
+    out[(q & 3) + 8 * (q >> 2) + 4 * (lane >> 5)] = v[0];
+  }
+}
+
 // One screen pass over 32-row groups.  LIMBS = 3: the exact-integer screen
 // (S1, S2, S3: six MFMAs per 32-dim substep).  LIMBS = 2: the same over the
 // a and b limbs only (S1, S2: three MFMAs), certified with err_term2 --
@@ -1090,6 +1216,9 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
   bool want = false;   // LIMBS < 3: an undecided row for the candidate pass
   int thrV = 0;
   int64_t grow = 0;
+  // LIMBS = 1 with bnd: the row's terms for its candidate rows' bound
+  double bxx = 0.0, bfx = 0.0, benc = 0.0, bf1 = 0.0;
+  int bsb = 0;
   if (lane < rows) {
     grow = rowAt(lane);
     const int2 mt = meta[grow];
@@ -1125,6 +1254,8 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
     float2 bb = make_float2(-1.0f, -1.0f);   // LIMBS = 1 with bnd: the row's bounds (none)
     if (mt.x != INT_MIN && I1 >= 0 && I1 < P.k && !clamped && shOk && !waveBad &&
         __builtin_isfinite(l1)) {
+      bsb = sb;
+      bf1 = f1;
       const double xn = xnorm[grow], cn = cnorm[I1];
       const double xx = xn * xn, cc = cn * cn;
       const double n1 = (double)__int_as_float(mt.y);   // bounds |xh3|_1
@@ -1146,26 +1277,19 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
       decided = !__builtin_isfinite(l2) || (l2 - l1) > M;
       eligible = __builtin_isfinite(M);
       if constexpr (LIMBS == 1) {
+        bxx = xx;
+        bfx = fx;
+        benc = enc;
+        // carried bounds of a certified row: every center but I1 has a
+        // computed bound >= l2 (bnd_ub_sq / bnd_lb_sq)
         if (bnd && decided && __builtin_isfinite(l2)) {
-          // Carried bounds (kmeans_i8.hpp Bounds).  With Lt_c = |c|^2 - 2 x.c
-          // and L'_c = cq_c - 2 s_c its exact integer form (cq_c <= |c|^2 -
-          // 2 g_c, |x.c - s_c| <= fx + g_c): Lt_c >= L'_c - 2 fx, and the
-          // computed bounds are within enc of L' (every center's >= l2 but
-          // the winner's, l1).  So |x - c|^2 >= xx + l2 - enc - 2 fx for c !=
-          // I1, and |x - c_I1|^2 <= xx + l1 + enc + 2 fx + 4 g_I1 + eps |c|^2
-          // (cq rounded down: the 2^-20 terms, as in M; xx = xnorm^2 within
-          // 2 kEpsF xx of the true |x|^2).
-          const double g1 = g[I1];
-          const double ub2 = (xx + l1 + enc + 2.0 * fx + 4.0 * g1 + 2.0 * kEpsF * (xx + cc) +
-                              0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g1) + 0x1p-90) *
-                             (1.0 + 0x1p-30);
-          const double lb2 = xx + l2 - enc - 2.0 * fx - 2.0 * kEpsF * (xx + cc) -
-                             0x1p-20 * (xx + cc + __builtin_fabs(l2) + 2.0 * fx + enc);
-          bb.x = fup(__builtin_sqrt(ub2) * (1.0 + 0x1p-50));
-          if (lb2 > 0.0 && bb.x < 0x1p120f) bb.y = fdown(__builtin_sqrt(lb2) * (1.0 - 0x1p-50));
+          bb.x = bnd_dist_up(bnd_ub_sq(xx, cc, l1, fx, g[I1], enc));
+          if (bb.x < 0x1p120f) bb.y = bnd_dist_dn(bnd_lb_sq(xx, l2, fx, enc, 0.0));
         }
       }
     }
+    // (rows listed with candidates get their lower bound for the centers
+    // outside the set below; every other undecided row none)
     if (LIMBS == 1 && bnd) bnd[grow] = bb;
     if (decided) {
       assign[grow] = I1;
@@ -1224,6 +1348,26 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      // LIMBS = 1 with bnd: the best computed bound among the centers OUTSIDE
+      // each candidate row's set -- per lane its best below the threshold
+      // (a candidate row has at most one candidate per lane: cV2 is below),
+      // the largest V over the row's lanes -- into thrS (read above)
+      int* ncS = thrS;
+      if constexpr (LIMBS == 1) {
+        if (bnd) {
+          int nc[16];
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) {
+            const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const int t = thrS[row];
+            nc[reg] = cV1[reg] < t ? cV1[reg] : cV2[reg];
+          }
+          __builtin_amdgcn_wave_barrier();
+          rows_max32(nc, lane, ncS);
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        }
+      }
       if (want) {
         const int* cs = candS + lane * (CMAX + 1);
         const int cnt = cs[0];
@@ -1232,6 +1376,16 @@ __global__ __launch_bounds__(64 * W, W == 8 ? 2 : (LIMBS < 3 ? 12 : 8) / W) void
           candRowsS[idx] = (int32_t)grow;
 #pragma unroll
           for (int i = 0; i < CMAX; ++i) candsS[(size_t)idx * CMAX + i] = i < cnt ? cs[1 + i] : -1;
+          if constexpr (LIMBS == 1) {
+            if (bnd) {
+              // (-2, lower bound of every center outside the set): the
+              // refinement and the three-limb candidate tier finish it
+              const int vnc = ncS[lane];
+              const double lnc = vnc == INT_MIN ? __builtin_inf() : -bf1 * (double)(vnc >> bsb);
+              bnd[grow] = make_float2(-2.0f, vnc == INT_MIN ? __builtin_inff()
+                                                            : bnd_dist_dn(bnd_lb_sq(bxx, lnc, bfx, benc, 0.0)));
+            }
+          }
         } else {
           listS[atomicAdd(listCountS, 1u)] = (int32_t)grow;
         }
@@ -1296,7 +1450,8 @@ __global__ __launch_bounds__(256, 2) void k_screen32r(
     int32_t* __restrict__ assign, int32_t* __restrict__ list, unsigned int* __restrict__ listCount,
     int32_t* __restrict__ candRows, int32_t* __restrict__ cands,
     unsigned int* __restrict__ candCount, int32_t* __restrict__ fullList,
-    unsigned int* __restrict__ fullCount, unsigned int* __restrict__ stat, unsigned int scap) {
+    unsigned int* __restrict__ fullCount, unsigned int* __restrict__ stat, unsigned int scap,
+    float2* __restrict__ bnd) {
   constexpr int D = 32 * S, CH = 3 * D / 16;
   constexpr int W = 4;
   // per wave: the candidate list, then the candidate-set scratch (the union
@@ -1330,7 +1485,11 @@ __global__ __launch_bounds__(256, 2) void k_screen32r(
     if (stat) stat += shard * kShardStride;
   }
   auto to_full = [&]() {
-    if (lane < rows) fullList[atomicAdd(fullCount, 1u)] = (int32_t)myRow;
+    if (lane < rows) {
+      fullList[atomicAdd(fullCount, 1u)] = (int32_t)myRow;
+      // the full two-limb pass keeps no bound for the centers it excludes
+      if (bnd) bnd[myRow] = make_float2(-1.0f, -1.0f);
+    }
   };
   if (!P.ok) {   // uniform over the grid: every row to the fp64 tier
     if (lane < rows) list[atomicAdd(listCount, 1u)] = (int32_t)myRow;
@@ -1536,6 +1695,10 @@ __global__ __launch_bounds__(256, 2) void k_screen32r(
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   bool want = false;
   int thrV = 0;
+  // with bnd: the row's lower bound for the centers outside its one-limb
+  // set (the one-limb pass left it in bnd[row].y), and its terms
+  float lncPrev = -1.0f;
+  double bfx = 0.0, benc = 0.0, bf1 = 0.0;
   if (lane < rows) {
     const int I1 = redI1[lane];
     const int v1 = redV1[lane];
@@ -1550,6 +1713,23 @@ __global__ __launch_bounds__(256, 2) void k_screen32r(
       M = margin(I1, xxj, l1, l2, IM);
       decided = !__builtin_isfinite(l2) || (l2 - l1) > M;
       eligible = __builtin_isfinite(M);
+      if (bnd) {
+        const float2 pb = bnd[myRow];
+        lncPrev = pb.x == -2.0f ? pb.y : -1.0f;
+        const double n1 = (double)__int_as_float(mt.y);
+        bfx = err_term2(mt.x, n1 + (double)d * __builtin_ldexp(1.0078125, mt.x - 15), mu, d);
+        benc = __builtin_ldexp((double)(IM + 3u), mt.x + P.ec - 20);
+        bf1 = f1;
+        if (decided && __builtin_isfinite(l2) && lncPrev >= 0.0f) {
+          // certified over the union: the union's other centers have
+          // computed bounds >= l2, the rest the one-limb pass's bound
+          const double cn = cnorm[I1];
+          const float ub = bnd_dist_up(bnd_ub_sq(xxj, cn * cn, l1, bfx, g[I1], benc));
+          const float lb = bnd_dist_dn(bnd_lb_sq(xxj, l2, bfx, benc, 0.0));
+          bnd[myRow] = ub < 0x1p120f ? make_float2(ub, __builtin_fminf(lb, lncPrev))
+                                     : make_float2(-1.0f, -1.0f);
+        }
+      }
     }
     if (decided) {
       assign[myRow] = I1;
@@ -1596,6 +1776,22 @@ __global__ __launch_bounds__(256, 2) void k_screen32r(
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // with bnd: the best computed bound among the union's centers outside
+    // each candidate row's set (the one-limb pass's ncS, over the union)
+    int* ncS = thrS;
+    if (bnd) {
+      int nc[16];
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int row = (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const int t = thrS[row];
+        nc[reg] = cV1[reg] < t ? cV1[reg] : cV2[reg];
+      }
+      __builtin_amdgcn_wave_barrier();
+      rows_max32(nc, lane, ncS);
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
     if (want) {
       const int* cs = candS + lane * (kCandMax + 1);
       const int c0 = cs[0];
@@ -1604,6 +1800,15 @@ __global__ __launch_bounds__(256, 2) void k_screen32r(
         candRows[idx] = (int32_t)myRow;
 #pragma unroll
         for (int i = 0; i < kCandMax; ++i) cands[(size_t)idx * kCandMax + i] = i < c0 ? cs[1 + i] : -1;
+        if (bnd) {
+          // (-2, lower bound outside the set): the union's other centers and
+          // (lncPrev) the centers outside the union; the three-limb
+          // candidate tier finishes it
+          const int vnc = ncS[lane];
+          const float l2nc = vnc == INT_MIN ? __builtin_inff()
+                                            : bnd_dist_dn(bnd_lb_sq(xxj, -bf1 * (double)vnc, bfx, benc, 0.0));
+          bnd[myRow] = make_float2(-2.0f, lncPrev >= 0.0f ? __builtin_fminf(lncPrev, l2nc) : -1.0f);
+        }
       } else {
         list[atomicAdd(listCount, 1u)] = (int32_t)myRow;
       }
@@ -1785,7 +1990,7 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     const CenterParams* __restrict__ prm, const int32_t* __restrict__ candRows,
     const int32_t* __restrict__ cands, const unsigned int* __restrict__ candCount,
     int32_t* __restrict__ assign, int32_t* __restrict__ outRows, int32_t* __restrict__ outCands,
-    unsigned int* __restrict__ outCount, unsigned int scap) {
+    unsigned int* __restrict__ outCount, unsigned int scap, float2* __restrict__ bnd) {
   using Pc = std::conditional_t<PB == 16, uint4, uint2>;
   constexpr int P16 = 32 * S / PB;    // pieces per limb plane = lanes per row
   constexpr int RPW = 64 / P16;       // rows per wave
@@ -1846,6 +2051,7 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     float L1 = __builtin_inff(), L2 = __builtin_inff();
     int I1 = -1;
     bool bad = false;
+    float cqMax = 0.0f;   // the f32 bounds' rounding slack (carried bounds)
 #pragma unroll
     for (int i = 0; i < kCandMax; ++i) {
       const int c = ci[i];
@@ -1854,6 +2060,7 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
       const int T = s1[i] * 128 + s2[i];
       const float V = __builtin_fmaf((float)s3[i], 0x1p-7f, (float)T);
       const float L = __builtin_fmaf(-F1, V, cq[c]);
+      cqMax = __builtin_fmaxf(cqMax, __builtin_fabsf(cq[c]));
       const bool lt = L < L1;
       L2 = __builtin_amdgcn_fmed3f(L1, L2, L);
       I1 = lt ? c : I1;
@@ -1874,6 +2081,20 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
                         0x1p-90) *
                        (1.0 + 0x1p-30);
       decided = !__builtin_isfinite(l2) || (l2 - l1) > M;
+      if (bnd && decided && li == 0 && __builtin_isfinite(l2)) {
+        // carried bounds: the other candidates' bounds are >= l2 (f32,
+        // rounded down after a rounded-down V: slack 2^-20 max |cq|), the
+        // centers outside the set below the earlier tiers' bound in y
+        const float2 pb = bnd[row];
+        if (pb.x == -2.0f && pb.y >= 0.0f) {
+          const float ub = bnd_dist_up(bnd_ub_sq(xx, cc, l1, fx, g[I1], 0.0) +
+                                       0x1p-20 * (double)cqMax);
+          const float lb =
+              bnd_dist_dn(bnd_lb_sq(xx, l2, fx, 0.0, 0x1p-20 * (double)cqMax));
+          bnd[row] = ub < 0x1p120f ? make_float2(ub, __builtin_fminf(lb, pb.y))
+                                   : make_float2(-1.0f, -1.0f);
+        }
+      }
     }
     if (live && li == 0) {
       if (decided) {
@@ -1893,7 +2114,7 @@ int launch_cands3(const CandArgs& ca, const void* img, const int2* meta, const d
                   int64_t n, int d, const void* Cb, const float* cq, const double* g,
                   const double* cnorm, const CenterParams* prm, int ktp, int32_t* assign,
                   int32_t* outRows, int32_t* outCands, unsigned int* outCount, hipStream_t st,
-                  unsigned int scap) {
+                  unsigned int scap, float2* bnd = nullptr) {
   KernelTimer timer("k_kmeans_cands3", st);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 127) / 128, 4096));
   // the center-major copy behind the fragment image (k_centers_pack32)
@@ -1901,7 +2122,8 @@ int launch_cands3(const CandArgs& ca, const void* img, const int2* meta, const d
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen_cands3<S, 16>), dim3(grid), dim3(256), 0, st,
                      (const uint4*)img, meta, xnorm, d, Cr, cq, g, cnorm, prm,
                      (const int32_t*)ca.candRows, (const int32_t*)ca.cands,
-                     (const unsigned int*)ca.candCount, assign, outRows, outCands, outCount, scap);
+                     (const unsigned int*)ca.candCount, assign, outRows, outCands, outCount, scap,
+                     bnd);
   CYC_LAUNCH_CHECK("k_screen_cands3");
   return CYC_OK;
 }
@@ -2069,7 +2291,7 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
                          N(kSetRowsA, list2Count), A(sg ? sg->candRows : nullptr, ca->candRows),
                          A(sg ? sg->cands : nullptr, ca->cands), N(kSetCand, ca->candCount),
                          A(sg ? sg->rowsB : nullptr, ra->fullList), N(kSetRowsB, ra->fullCount),
-                         N(kSetStat, ra->fullCount + 1), scap);
+                         N(kSetStat, ra->fullCount + 1), scap, bd ? bd->ub_lb : nullptr);
       CYC_LAUNCH_CHECK("k_screen32r");
     }
     if (sg && ((rc = compact2()) ||
@@ -2113,7 +2335,8 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
     if ((rc = launch_cands3<S>(*ca, img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp, assign,
                                A(sg ? sg->candRows : nullptr, ca->candRows2),
                                A(sg ? sg->cands : nullptr, ca->cands2),
-                               N(kSetCand, ca->candCount2), st, scap)))
+                               N(kSetCand, ca->candCount2), st, scap,
+                               bd ? bd->ub_lb : nullptr)))
       return rc;
     if (sg && (rc = compact(sg->set(kSetCand), scap, sg->candRows, ca->candRows2, 1, sg->cands,
                             ca->cands2, kCandMax, ca->candCount2, st)))
@@ -2283,7 +2506,7 @@ __global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict
       listed = true;
       const int a = assign[r];
       const float2 b = bnd[r];
-      if (!P.bad && b.y > 0.0f && a >= 0 && a < k) {
+      if (!P.bad && b.x >= 0.0f && b.y > 0.0f && a >= 0 && a < k) {
         const double U = (double)b.x + delta[a];
         const double L = (double)b.y - (a == P.i1 ? P.d2 : P.d1);
         const double xn = xnorm[r];
@@ -2387,8 +2610,19 @@ int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipS
   const int D = 64 * ksteps(d);
   const int64_t blocks = std::min<int64_t>((n + 3) / 4, 65536);
   const int vec = (d % 2 == 0) && (reinterpret_cast<uintptr_t>(X) % 16 == 0);
-  hipLaunchKernelGGL(k_rows_quantize, dim3((unsigned)blocks), dim3(256), 0, st, X, n, d, D,
-                     (unsigned*)img, meta, scale, unorm, vec);
+  static const bool pf = [] {   // CYC_QUANT_PF=0: the row-at-a-time kernel
+    const char* e = std::getenv("CYC_QUANT_PF");
+    return !(e && e[0] == '0');
+  }();
+  if (vec && pf && d <= 256)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rows_quantize_pf<2>), dim3((unsigned)blocks), dim3(256), 0,
+                       st, X, n, d, D, (unsigned*)img, meta, scale, unorm);
+  else if (vec && pf)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rows_quantize_pf<4>), dim3((unsigned)blocks), dim3(256), 0,
+                       st, X, n, d, D, (unsigned*)img, meta, scale, unorm);
+  else
+    hipLaunchKernelGGL(k_rows_quantize, dim3((unsigned)blocks), dim3(256), 0, st, X, n, d, D,
+                       (unsigned*)img, meta, scale, unorm, vec);
   CYC_LAUNCH_CHECK("k_rows_quantize");
   return CYC_OK;
 }

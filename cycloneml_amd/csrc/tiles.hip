@@ -44,6 +44,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 
@@ -330,10 +331,17 @@ __global__ void k_seg_max(const int64_t* __restrict__ segStart, int64_t s0, int6
 // place of the LDS atomic adds, 2 = no LDS gathers of coefficients /
 // multipliers, 8 = no staging of the chunk / slice (the loader wave idles),
 // 16 = no run loads (synthetic ids and values), 32 = no segment offset
-// loads (every run 256 long).  0 in the library.
+// loads (every run 256 long), 64 = full-occupancy repeats (round 6's MALL
+// residency probe: every CU busy however small the layout -- the margin
+// pass on one workgroup per CU, each taking TileDims::reps super blocks
+// modulo the layout's; the gradient pass walking its row range reps times --
+// so a layout that fits the Infinity Cache is re-read by hundreds of steps
+// per workgroup, the per-step time comparable with a streamed layout's;
+// CYC_TILES_REPS sets reps).  0 in the library.
 #ifndef CYC_TILES_PROBE
 #define CYC_TILES_PROBE 0
 #endif
+constexpr bool kRepeatProbe = (CYC_TILES_PROBE & 64) != 0;
 
 // LDS pointers are kept in address space 3 from the __shared__ array on
 // (the cast of the array folds): derived through generic pointers, the
@@ -399,6 +407,7 @@ __device__ __forceinline__ void step_sync() {
 struct TileDims {
   int64_t n, nRB;
   int F, T, Wt;
+  int reps = 1;   // probe bit 64 only
 };
 
 // One wave's run: a segment's nonzeros [a, b), empty when !on.  The
@@ -588,7 +597,13 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
   const int T = v.T;
   const int64_t nSB = (v.nRB + kMW - 1) / kMW;
   const int Tp = (T + NB - 1) / NB * NB;
-  const int64_t mySB = nSB > blockIdx.x ? (nSB - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const int64_t mySB = kRepeatProbe ? v.reps
+                                    : nSB > blockIdx.x ? (nSB - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  // this workgroup's k-th super block (the probe: modulo the layout's)
+  auto sbOf = [&](int64_t k) {
+    const int64_t sb = (int64_t)blockIdx.x + k * gridDim.x;
+    return kRepeatProbe ? sb % nSB : sb;
+  };
   // buffer of flat step g: g % kMBufs (the flat step count fits 32 bits:
   // Tp * super blocks per workgroup is the launch's per-workgroup steps)
   auto bufOf = [&](int64_t k, int c) {
@@ -647,7 +662,7 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
     if (c2 >= Tp) c2 -= Tp, k2 += 1;
   };
   auto run_of = [&](int64_t k, int c) {
-    const int64_t rb = ((int64_t)blockIdx.x + k * gridDim.x) * kMW + wave;
+    const int64_t rb = sbOf(k) * kMW + wave;
     return seg_run(segStart, rb * T + c, k < mySB && c < T && rb < v.nRB);
   };
   lds_f64* const myDots = dots + wave * kTileRows;
@@ -745,7 +760,7 @@ __global__ __launch_bounds__(kMTPB) void k_tiles_margin(
              vb[(u + NB - 1) % NB]);
     }
     __syncthreads();                            // every wave's atomics landed
-    const int64_t r0 = ((int64_t)blockIdx.x + k * gridDim.x) * kMRows;
+    const int64_t r0 = sbOf(k) * kMRows;
 #pragma unroll
     for (int i = 0; i < kMRows / kCT; ++i) {
       const int64_t r = r0 + tid + kCT * i;
@@ -877,14 +892,20 @@ __global__ __launch_bounds__(kTPBL) void k_tiles_grad(
   // whole groups of NB steps: the last group's steps past rbB have empty
   // runs and slices (no guard inside the unroll: a skipped step left the
   // compiler's wait analysis draining every prefetched run at the loop head)
-  const int64_t steps = (rbB - rbA + NB - 1) / NB * NB;
+  const int64_t span = rbB - rbA;
+  const int64_t steps = ((kRepeatProbe ? span * v.reps : span) + NB - 1) / NB * NB;
+  // the probe's repeats: row block rb of the walk is rbA + (rb - rbA) % span
+  auto wrap = [&](int64_t rb) {
+    return kRepeatProbe && span > 0 ? rbA + (rb - rbA) % span : rb;
+  };
 
   if (wave == kLoaderWave) {
-    auto slice = [&](int64_t rb) {
+    auto slice = [&](int64_t rbu) {
+      const int64_t rb = wrap(rbu);
       const bool on = rb < rbB;
       const int64_t r0 = on ? rb * kTileRows : 0;
       stage_slice(mult + r0, on ? std::min<int64_t>(kTileRows, v.n - r0) : 0,
-                  mv + ((rb - rbA) & 1) * kTileRows, lane);
+                  mv + ((rbu - rbA) & 1) * kTileRows, lane);
     };
     slice(rbA);
     __syncthreads();                              // sums zeroed, slice rbA in place
@@ -900,7 +921,10 @@ __global__ __launch_bounds__(kTPBL) void k_tiles_grad(
   uint32_t ib[NB][KC];
   double vb[NB][KC];
   Run rr[NB];
-  auto run_of = [&](int64_t rb) { return seg_run(segStart, rb * v.T + c, rb < rbB && c < v.T); };
+  auto run_of = [&](int64_t rbu) {
+    const int64_t rb = wrap(rbu);
+    return seg_run(segStart, rb * v.T + c, rb < rbB && c < v.T);
+  };
   lds_f64* const myG = gt + wave * v.Wt;
   // waits for the whole run first, on every path (the margin pass's
   // consume says why); branch-free adds: a masked lane adds +0.0 to the
@@ -986,6 +1010,13 @@ __global__ __launch_bounds__(kTPBL) void k_tiles_grad(
 // more load and LDS instructions per step for mostly idle lanes).
 bool long_runs(int64_t maxSeg) { return maxSeg > 5 * 64; }
 
+// probe bit 64's repeats (CYC_TILES_REPS, default 1)
+int probe_reps() {
+  if constexpr (!kRepeatProbe) return 1;
+  const char* e = std::getenv("CYC_TILES_REPS");
+  return e ? std::max(1, std::atoi(e)) : 1;
+}
+
 }  // namespace
 
 namespace cyc {
@@ -1007,8 +1038,9 @@ int tiles_view(cyc_tiles t, TilesView* v) {
 
 int tiles_margin(const TilesView& v, const double* coef, double* dots, hipStream_t st) {
   const int64_t nSB = (v.nRB + kMW - 1) / kMW;
-  const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nSB, device_cus()));
-  const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
+  const int64_t grid =
+      kRepeatProbe ? device_cus() : std::max<int64_t>(1, std::min<int64_t>(nSB, device_cus()));
+  const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt, probe_reps()};
 #define CYC_TILES_MARGIN(KC, LONG, CPT)                                                         \
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_margin<CYC_TILES_NB, KC, LONG, CPT>),              \
                      dim3((unsigned)grid), dim3(kMTPB), 0, st, d, v.segStart, v.idx, v.vals,    \
@@ -1057,7 +1089,7 @@ int tiles_grad(const TilesView& v, const double* mult, double* slabG, int* range
   const int R = tiles_ranges(v);
   *ranges = R;
   const int64_t sts = (v.T + kTileWaves - 1) / kTileWaves;
-  const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt};
+  const TileDims d{v.n, v.nRB, v.F, v.T, v.Wt, probe_reps()};
 #define CYC_TILES_GRAD(KC, LONG, CPT)                                                           \
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_tiles_grad<CYC_TILES_NB, KC, LONG, CPT>),                \
                      dim3((unsigned)(sts * R)), dim3(kTPBL), 0, st, d, v.segStart, v.idx, v.vals, \

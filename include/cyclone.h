@@ -184,7 +184,13 @@ int cyc_kmeans_last_refine(cyc_kmeans_plan plan, int64_t* listed_rows, int64_t* 
  * per-cluster sums.  sums[k*d] += sum of w*x, wsum[k] += sum of w,
  * cost_sum[0] += sum of w*cost.  weights may be NULL (unit weights).
  * rows: NULL or the image of exactly these X, n.  assign/cost (per-row
- * outputs) may be NULL.  All pointers are device memory. */
+ * outputs) may be NULL.  All pointers are device memory.
+ * xnorm may be NULL with a Euclidean row image: the image's norms (built
+ * with it, in another summation order -- within the screens' margins) serve
+ * the screens, and the rows the reference loop itself decides
+ * (k_assign_exact) get the reference's Vectors.norm computed there, so the
+ * results are the same bits as with the caller's norms (the per-fit norm
+ * pass of KMeans.scala:263-270 is then not needed). */
 int cyc_kmeans_accumulate_dev(cyc_kmeans_plan plan, const double* X, const double* xnorm,
                               cyc_kmeans_rows rows, const double* weights, int64_t n,
                               const double* C, const double* cnorm, double* sums, double* wsum,

@@ -962,3 +962,74 @@ def test_full_config_late_iteration(cuda):
     np.testing.assert_array_equal(wsum.cpu().numpy(), ref["wsum"])
     np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
                                atol=1e-10 * np.abs(ref["sums"]).max())
+
+
+@pytest.mark.parametrize("n,d,k,dup", [(60_000, 64, 130, True), (40_000, 256, 1024, False),
+                                       (20_000, 300, 40, True)])
+def test_accumulate_without_norms(cuda, n, d, k, dup):
+    """cyc_kmeans_accumulate_dev with xnorm NULL and a Euclidean row image:
+    the image's norms for the screens, the reference's own norm where its
+    loop decides (k_assign_exact: duplicate centers force exact rows) --
+    the same bits as with the caller's norms over three Lloyd iterations
+    (assign, cost, sums, weights, cost sum), and the require message of a
+    NaN row names the same norms."""
+    import torch
+    from cycloneml_amd import _native as N
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    rng = np.random.default_rng(n + d + k)
+    true_c = rng.normal(scale=2.5, size=(k, d))
+    X = true_c[rng.integers(0, k, n)] + rng.normal(size=(n, d))
+    Xd = _dev(X, cuda)
+    C0 = Xd[:k].clone()
+    if dup:
+        C0[k // 2:k // 2 + 4] = C0[:4]                    # exact ties: the exact tier
+    out = []
+    for with_norms in (True, False):
+        p = KMeansPlan(d, k, n)
+        rows = p.rows(Xd)
+        C = C0.clone()
+        cn = row_norms(C)
+        xn = row_norms(Xd) if with_norms else None
+        a = torch.empty(n, dtype=torch.int32, device=cuda)
+        pc = torch.empty(n, dtype=torch.float64, device=cuda)
+        conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+        res = []
+        for it in range(3):
+            buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=cuda)
+            sums, wsum, cost = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
+            p.accumulate(Xd, xn, None, C, cn, sums, wsum, cost, a, pc, rows=rows)
+            res.append((a.cpu().numpy(), pc.cpu().numpy(), buf.cpu().numpy()))
+            p.update(C, cn, sums, wsum, 1e-4, conv)
+        out.append(res)
+    for (a1, c1, b1), (a2, c2, b2) in zip(*out):
+        np.testing.assert_array_equal(a1, a2)
+        np.testing.assert_array_equal(c1, c2)
+        np.testing.assert_array_equal(b1, b2)
+    Xn = X.copy()
+    Xn[7, 3] = np.nan
+    msgs = []
+    for with_norms in (True, False):
+        Xb = _dev(Xn, cuda)
+        p = KMeansPlan(d, k, n)
+        rows = p.rows(Xb)
+        C = C0.clone()
+        with pytest.raises(N.IllegalArgumentException) as e:
+            p.accumulate(Xb, row_norms(Xb) if with_norms else None, None, C, row_norms(C),
+                         torch.zeros(k * d, dtype=torch.float64, device=cuda),
+                         torch.zeros(k, dtype=torch.float64, device=cuda),
+                         torch.zeros(1, dtype=torch.float64, device=cuda), rows=rows)
+        msgs.append(str(e.value))
+    assert msgs[0] == msgs[1] and "norm2=NaN" in msgs[0]
+    # k = 1 with a NaN center: the message names row 0's norm (recomputed)
+    msgs = []
+    for with_norms in (True, False):
+        p = KMeansPlan(d, 1, n)
+        rows = p.rows(Xd)
+        C = torch.full((1, d), float("nan"), dtype=torch.float64, device=cuda)
+        with pytest.raises(N.IllegalArgumentException) as e:
+            p.accumulate(Xd, row_norms(Xd) if with_norms else None, None, C, row_norms(C),
+                         torch.zeros(d, dtype=torch.float64, device=cuda),
+                         torch.zeros(1, dtype=torch.float64, device=cuda),
+                         torch.zeros(1, dtype=torch.float64, device=cuda), rows=rows)
+        msgs.append(str(e.value))
+    assert msgs[0] == msgs[1] and "norm1=NaN" in msgs[0], msgs
