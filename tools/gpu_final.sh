@@ -11,7 +11,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 PART=${PART:-all}
 if [ $PART != bench ]; then
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread --durations=15 > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST FAIL; grep -E "FAILED|Error" gpurun_out/pytest_gpu.log | head; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+timeout -k 10 1080 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread --durations=15 > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST FAIL; grep -E "FAILED|Error" gpurun_out/pytest_gpu.log | head; tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo SMOKE FAIL; tail -20 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
