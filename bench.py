@@ -286,7 +286,7 @@ class KMeansWorkload:
     kernel = "k_chunk_sums"
     kernels = ("k_kmeans_screen1", "k_kmeans_refine2", "k_kmeans_screen2", "k_kmeans_cands3",
                "k_kmeans_cands", "k_kmeans_screen3", "k_kmeans_compact", "k_kmeans_assign_fp64",
-               "k_kmeans_bounds", "k_chunk_sums")
+               "k_kmeans_bounds", "k_kmeans_recheck", "k_chunk_sums")
     pmc_names = {"k_kmeans_screen1": "k_screen32_l1", "k_kmeans_screen2": "k_screen32_l2",
                  "k_kmeans_refine2": "k_screen32r", "k_chunk_sums": "k_chunk_sums_fast"}
 
@@ -329,11 +329,13 @@ class KMeansWorkload:
         self.C_timed = self.C.clone()
         self.steps_timed = steps
         self._b0 = self.rows.bounds_info()
+        self._rc0 = self.rows.bounds_rechecked()
 
     def after_steps(self):
         calls, screened = self.rows.bounds_info()
         self.screened_timed = screened - self._b0[1]
         self.bounded_calls = calls - self._b0[0]
+        self.rechecked_timed = self.rows.bounds_rechecked() - self._rc0
 
     def step(self):
         k, d = self.k, self.d
@@ -400,14 +402,18 @@ class KMeansWorkload:
                                  count_exact=True, rows=self.rows)
         tier2, _ = self.plan.last_tiers()
         scr = getattr(self, "screened_timed", None)
+        rc = getattr(self, "rechecked_timed", None)
         return {"carried_bounds": {
             "rows_screened_per_step": scr / self.steps_timed if scr is not None else None,
+            "rows_rechecked_per_step": rc / self.steps_timed if rc is not None else None,
             "rows_kept_per_step": self.n - scr / self.steps_timed if scr is not None else None,
             "bounded_calls": getattr(self, "bounded_calls", None),
             "note": "Hamerly bounds carried across the fit's iterations (cyclone.h "
                     "cyc_kmeans_rows_set_bounds): a row whose moved bounds still certify its "
-                    "center keeps it and skips the screen; every row's cost and sums are "
-                    "computed every step"},
+                    "center keeps it and skips the screen; a row whose bounds fail but whose "
+                    "carried candidate set still excludes every other center is re-checked "
+                    "against that set (three-limb bounds); the rest get the full screen "
+                    "(screened); every row's cost and sums are computed every step"},
             "screen_tiers": {
             "rows_listed_by_one_limb_pass": listed,
             "rows_to_full_two_limb_pass": full,

@@ -72,6 +72,7 @@ SIGNATURES = {
     "cyc_kmeans_rows_bytes": (_i64, [_vp]),
     "cyc_kmeans_rows_set_bounds": (ctypes.c_int, [_vp, _i32]),
     "cyc_kmeans_rows_bounds_info": (ctypes.c_int, [_vp, _pi64, _pi64]),
+    "cyc_kmeans_rows_bounds_rechecked": (ctypes.c_int, [_vp, _pi64]),
     "cyc_kmeans_last_tiers": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_last_screen": (ctypes.c_int, [_vp, _pi64]),
     "cyc_kmeans_last_candidates": (ctypes.c_int, [_vp, _pi64]),

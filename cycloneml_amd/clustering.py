@@ -202,6 +202,13 @@ class KMeansRows:
         certify their center skip the screen; either setting drops the state."""
         N.check(self._lib.cyc_kmeans_rows_set_bounds(self.handle, 1 if enable else 0))
 
+    def bounds_rechecked(self):
+        """Rows re-checked against their carried candidate sets (all calls;
+        synchronises the device)."""
+        a = ctypes.c_int64(0)
+        N.check(self._lib.cyc_kmeans_rows_bounds_rechecked(self.handle, ctypes.byref(a)))
+        return a.value
+
     def bounds_info(self):
         """(accumulate calls that used the bounds, rows those calls screened);
         synchronises the device."""

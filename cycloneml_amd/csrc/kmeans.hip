@@ -1865,6 +1865,9 @@ struct cyc_kmeans_rows_s {
   bool bValid = false;
   int bk = 0;
   cyc::DeviceBuffer bnd, bAssign, bCp, bDelta, bCcs, bPrm, bTmp, bCount, bList, bListCount, bCum;
+  // carried candidate sets (kmeans_i8.hpp Bounds): outside bound, sets,
+  // per-row state, the re-check list, its count and running total
+  cyc::DeviceBuffer bLnc, bSets, bState, bRc, bRcCount, bRcCum;
   int64_t bCalls = 0, bFullRows = 0;   // bounded calls; rows of their full (first) screens
 };
 
@@ -2042,11 +2045,17 @@ int bounds_prepare(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* C,
       (rc = rows->bTmp.reserve(sizeof(int32_t) * (size_t)n)) ||
       (rc = rows->bCount.reserve(sizeof(unsigned int) * (size_t)(k8::bounds_blocks(n) + 1))) ||
       (rc = rows->bList.reserve(sizeof(int32_t) * (size_t)n)) ||
-      (rc = rows->bListCount.reserve(64)))
+      (rc = rows->bListCount.reserve(64)) ||
+      (rc = rows->bLnc.reserve(sizeof(float) * (size_t)n)) ||
+      (rc = rows->bSets.reserve(sizeof(int32_t) * (size_t)n * k8::kCandMax)) ||
+      (rc = rows->bState.reserve((size_t)n)) ||
+      (rc = rows->bRc.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = rows->bRcCount.reserve(64)))
     return rc;
   if (!rows->bCum.ptr) {
-    if ((rc = rows->bCum.reserve(64))) return rc;
+    if ((rc = rows->bCum.reserve(64)) || (rc = rows->bRcCum.reserve(64))) return rc;
     CYC_HIP(hipMemsetAsync(rows->bCum.ptr, 0, 8, st));
+    CYC_HIP(hipMemsetAsync(rows->bRcCum.ptr, 0, 8, st));
   }
   const bool carry = rows->bValid && rows->bk == k;
   rows->bValid = false;   // until the screen has written the bounds
@@ -2054,17 +2063,32 @@ int bounds_prepare(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* C,
                               (double*)rows->bCcs.ptr, (k8::DriftParams*)rows->bPrm.ptr, st)))
     return rc;
   bd = k8::Bounds{(float2*)rows->bnd.ptr, nullptr, nullptr};
+  bd.lnc = (float*)rows->bLnc.ptr;
+  bd.sets = (int32_t*)rows->bSets.ptr;
+  bd.state = (unsigned char*)rows->bState.ptr;
+  bd.dp = (const k8::DriftParams*)rows->bPrm.ptr;
+  bd.tmp = (int32_t*)rows->bTmp.ptr;
+  bd.bcount = (unsigned int*)rows->bCount.ptr;
+  bd.list = (int32_t*)rows->bList.ptr;
+  bd.listCount = (unsigned int*)rows->bListCount.ptr;
+  bd.cum = (unsigned long long*)rows->bCum.ptr;
+  bd.n = n;
   if (carry) {
-    if ((rc = k8::bounds_filter((const int32_t*)rows->bAssign.ptr, (float2*)rows->bnd.ptr, xnorm,
-                                n, k, (const double*)rows->bDelta.ptr,
-                                (const k8::DriftParams*)rows->bPrm.ptr, (int32_t*)rows->bTmp.ptr,
-                                (unsigned int*)rows->bCount.ptr, (int32_t*)rows->bList.ptr,
-                                (unsigned int*)rows->bListCount.ptr,
-                                (unsigned long long*)rows->bCum.ptr, st)))
+    // kept rows, the re-check list (screen: the re-check, then the state-1
+    // rows collected into bList for the one-limb pass)
+    if ((rc = k8::bounds_filter((const int32_t*)rows->bAssign.ptr, (float2*)rows->bnd.ptr,
+                                bd.lnc, bd.state, xnorm, n, k, (const double*)rows->bDelta.ptr,
+                                bd.dp, bd.tmp, bd.bcount, (int32_t*)rows->bRc.ptr,
+                                (unsigned int*)rows->bRcCount.ptr,
+                                (unsigned long long*)rows->bRcCum.ptr, st)))
       return rc;
-    bd.rowsIn = (const int32_t*)rows->bList.ptr;
-    bd.rowsInCount = (const unsigned int*)rows->bListCount.ptr;
+    bd.rcRows = (const int32_t*)rows->bRc.ptr;
+    bd.rcCount = (const unsigned int*)rows->bRcCount.ptr;
+    bd.rowsIn = bd.list;
+    bd.rowsInCount = bd.listCount;
   } else {
+    // a full screen: no carried sets yet (NaN outside bounds)
+    CYC_HIP(hipMemsetAsync(bd.lnc, 0xff, sizeof(float) * (size_t)n, st));
     rows->bFullRows += n;
   }
   return CYC_OK;
@@ -2677,6 +2701,17 @@ int cyc_kmeans_rows_set_bounds(cyc_kmeans_rows rows, int32_t enable) {
   CYC_REQUIRE(rows != nullptr, "rows must not be null");
   rows->bEnabled = enable != 0;
   rows->bValid = false;   // a re-enabled fit starts from a full screen
+  return CYC_OK;
+}
+
+int cyc_kmeans_rows_bounds_rechecked(cyc_kmeans_rows rows, int64_t* rechecked_rows) {
+  CYC_REQUIRE(rows != nullptr && rechecked_rows != nullptr, "arguments must not be null");
+  unsigned long long cum = 0;
+  if (rows->bRcCum.ptr) {
+    CYC_HIP(hipDeviceSynchronize());
+    CYC_HIP(hipMemcpy(&cum, rows->bRcCum.ptr, sizeof(cum), hipMemcpyDeviceToHost));
+  }
+  *rechecked_rows = (int64_t)cum;
   return CYC_OK;
 }
 

@@ -1982,7 +1982,13 @@ __device__ __forceinline__ int row16_isum(int v) {
 
 // PB: bytes of a limb plane per lane (16: 2S lanes per row; 8: 4S lanes,
 // measured 0.94 vs 0.59 ms at 5 waves per SIMD against 4)
-template <int S, int PB>
+// RC (the carried candidate sets, kmeans_i8.hpp Bounds): the rows of
+// candRows re-checked against the candidate set their last screen left
+// (cands = Bounds::sets, indexed by ROW), certified when the best candidate
+// beats the others by M and its upper bound stays below the set's carried
+// lower bound for every other center (Bounds::lnc, moved by the drift) by
+// the reference's slack; state[row] = 0 (certified) or 1 (a full screen).
+template <int S, int PB, bool RC = false>
 __global__ __launch_bounds__(256) void k_screen_cands3(
     const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
     int d, const uint4* __restrict__ Cr, const float* __restrict__ cq,
@@ -1990,7 +1996,9 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     const CenterParams* __restrict__ prm, const int32_t* __restrict__ candRows,
     const int32_t* __restrict__ cands, const unsigned int* __restrict__ candCount,
     int32_t* __restrict__ assign, int32_t* __restrict__ outRows, int32_t* __restrict__ outCands,
-    unsigned int* __restrict__ outCount, unsigned int scap, float2* __restrict__ bnd) {
+    unsigned int* __restrict__ outCount, unsigned int scap, float2* __restrict__ bnd,
+    float* __restrict__ lncA, int32_t* __restrict__ sets, unsigned char* __restrict__ state,
+    const DriftParams* __restrict__ dp) {
   using Pc = std::conditional_t<PB == 16, uint4, uint2>;
   constexpr int P16 = 32 * S / PB;    // pieces per limb plane = lanes per row
   constexpr int RPW = 64 / P16;       // rows per wave
@@ -2011,7 +2019,8 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     const int64_t row = live ? candRows[idx] : 0;
     int ci[kCandMax];
 #pragma unroll
-    for (int i = 0; i < kCandMax; ++i) ci[i] = live ? cands[(size_t)idx * kCandMax + i] : -1;
+    for (int i = 0; i < kCandMax; ++i)
+      ci[i] = live ? cands[(size_t)(RC ? row : (int64_t)idx) * kCandMax + i] : -1;
     const Pc* xr = (const Pc*)Xq + row * (3 * P16) + li;
     const Pc xa = xr[0], xb = xr[P16], xc = xr[2 * P16];
     int s1[kCandMax], s2[kCandMax], s3[kCandMax];
@@ -2081,23 +2090,43 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
                         0x1p-90) *
                        (1.0 + 0x1p-30);
       decided = !__builtin_isfinite(l2) || (l2 - l1) > M;
-      if (bnd && decided && li == 0 && __builtin_isfinite(l2)) {
+      if (bnd && (decided || RC)) {
         // carried bounds: the other candidates' bounds are >= l2 (f32,
         // rounded down after a rounded-down V: slack 2^-20 max |cq|), the
-        // centers outside the set below the earlier tiers' bound in y
-        const float2 pb = bnd[row];
-        if (pb.x == -2.0f && pb.y >= 0.0f) {
-          const float ub = bnd_dist_up(bnd_ub_sq(xx, cc, l1, fx, g[I1], 0.0) +
-                                       0x1p-20 * (double)cqMax);
-          const float lb =
-              bnd_dist_dn(bnd_lb_sq(xx, l2, fx, 0.0, 0x1p-20 * (double)cqMax));
-          bnd[row] = ub < 0x1p120f ? make_float2(ub, __builtin_fminf(lb, pb.y))
+        // centers outside the set below the earlier tiers' bound (RC: the
+        // set's carried bound)
+        const float lnc0 = RC ? lncA[row] : bnd[row].y;
+        const bool mark = RC || bnd[row].x == -2.0f;
+        const double ub2 = bnd_ub_sq(xx, cc, l1, fx, g[I1], 0.0) + 0x1p-20 * (double)cqMax;
+        if (RC && decided) {
+          // every center outside the set: |x - c| >= lnc0, above the winner
+          // by the reference's slack (the filter's test)
+          const double L = (double)lnc0, tau = 0x1p-29 * (xx + dp->cmax2) + 0x1p-48 * (L * L + ub2);
+          decided = lnc0 >= 0.0f && !dp->bad && L * L - ub2 > tau;
+        }
+        if (decided && mark && lnc0 >= 0.0f && li == 0) {
+          const float ub = bnd_dist_up(ub2);
+          // (l2 = +inf: a set of one, nothing but the outside bound)
+          const float lb = __builtin_isfinite(l2)
+                               ? bnd_dist_dn(bnd_lb_sq(xx, l2, fx, 0.0, 0x1p-20 * (double)cqMax))
+                               : __builtin_inff();
+          bnd[row] = ub < 0x1p120f ? make_float2(ub, __builtin_fminf(lb, lnc0))
                                    : make_float2(-1.0f, -1.0f);
+          if (!RC && sets && ub < 0x1p120f) {
+            // the set and its outside bound, for the next iterations' re-checks
+            lncA[row] = lnc0;
+#pragma unroll
+            for (int i = 0; i < kCandMax; ++i) sets[(size_t)row * kCandMax + i] = ci[i];
+          }
         }
       }
     }
+    if (RC) decided = decided && bnd != nullptr;
     if (live && li == 0) {
-      if (decided) {
+      if (RC) {
+        if (decided) assign[row] = I1;
+        state[row] = decided ? 0 : 1;
+      } else if (decided) {
         assign[row] = I1;
       } else {
         const unsigned o = atomicAdd(outCount, 1u);
@@ -2114,7 +2143,7 @@ int launch_cands3(const CandArgs& ca, const void* img, const int2* meta, const d
                   int64_t n, int d, const void* Cb, const float* cq, const double* g,
                   const double* cnorm, const CenterParams* prm, int ktp, int32_t* assign,
                   int32_t* outRows, int32_t* outCands, unsigned int* outCount, hipStream_t st,
-                  unsigned int scap, float2* bnd = nullptr) {
+                  unsigned int scap, const Bounds* bd = nullptr) {
   KernelTimer timer("k_kmeans_cands3", st);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 127) / 128, 4096));
   // the center-major copy behind the fragment image (k_centers_pack32)
@@ -2123,7 +2152,8 @@ int launch_cands3(const CandArgs& ca, const void* img, const int2* meta, const d
                      (const uint4*)img, meta, xnorm, d, Cr, cq, g, cnorm, prm,
                      (const int32_t*)ca.candRows, (const int32_t*)ca.cands,
                      (const unsigned int*)ca.candCount, assign, outRows, outCands, outCount, scap,
-                     bnd);
+                     bd ? bd->ub_lb : nullptr, bd ? bd->lnc : nullptr, bd ? bd->sets : nullptr,
+                     nullptr, nullptr);
   CYC_LAUNCH_CHECK("k_screen_cands3");
   return CYC_OK;
 }
@@ -2261,7 +2291,22 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
     // one-limb pass over every center; the two-limb refinement over the
     // union of the listed rows' candidates; the full two-limb pass over the
     // rows neither can handle (fullList).  With carried bounds (bd) the
-    // one-limb pass screens only the rows bounds_filter listed.
+    // rows bounds_filter sent to a re-check against their carried candidate
+    // sets go first (k_screen_cands3<.., true>), then the one-limb pass
+    // screens only the rows that need a full screen.
+    if (bd && bd->rcRows) {
+      {
+        KernelTimer timer("k_kmeans_recheck", st);
+        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 127) / 128, 4096));
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen_cands3<S, 16, true>), dim3(grid), dim3(256), 0,
+                           st, (const uint4*)img, meta, xnorm, d,
+                           (const uint4*)Cb + (size_t)ktp * S * 3 * 64, cq, g, cnorm, prm,
+                           bd->rcRows, (const int32_t*)bd->sets, bd->rcCount, assign, nullptr,
+                           nullptr, nullptr, 0u, bd->ub_lb, bd->lnc, bd->sets, bd->state, bd->dp);
+        CYC_LAUNCH_CHECK("k_screen_cands3 (re-check)");
+      }
+      if ((rc = bounds_collect(*bd, st))) return rc;
+    }
     if (bd && bd->rowsIn)
       rc = launch_screen32<S, W, 1, true>(
           img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 64, g + (size_t)ktp * 64, cnorm, prm,
@@ -2335,8 +2380,7 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
     if ((rc = launch_cands3<S>(*ca, img, meta, xnorm, n, d, Cb, cq, g, cnorm, prm, ktp, assign,
                                A(sg ? sg->candRows : nullptr, ca->candRows2),
                                A(sg ? sg->cands : nullptr, ca->cands2),
-                               N(kSetCand, ca->candCount2), st, scap,
-                               bd ? bd->ub_lb : nullptr)))
+                               N(kSetCand, ca->candCount2), st, scap, bd)))
       return rc;
     if (sg && (rc = compact(sg->set(kSetCand), scap, sg->candRows, ca->candRows2, 1, sg->cands,
                             ca->cands2, kCandMax, ca->candCount2, st)))
@@ -2480,33 +2524,61 @@ __global__ __launch_bounds__(1024) void k_drift_top(const double* __restrict__ d
   }
 }
 
+// The listed rows of a kBndRows-row block in row order: tmp[block *
+// kBndRows ...], their count in bcount[block] (masks: the wave's ballot of
+// `listed` per 256-row step it, wc: IT x 4 counts in LDS)
+constexpr int kBndIT = kBndRows / 256;
+__device__ __forceinline__ void bnd_block_list(const unsigned long long (&masks)[kBndIT],
+                                               unsigned* wc, int64_t base, int32_t* tmp,
+                                               unsigned int* bcount) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  __syncthreads();
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int it = 0; it < kBndIT; ++it) {
+    unsigned before = 0;
+    for (int j = 0; j < it * 4 + wave; ++j) before += wc[j];
+    if ((masks[it] >> lane) & 1ull)
+      tmp[base + before + (unsigned)__builtin_popcountll(masks[it] & below)] =
+          (int32_t)(base + it * 256 + tid);
+  }
+  if (tid == 0) {
+    unsigned total = 0;
+    for (int j = 0; j < kBndIT * 4; ++j) total += wc[j];
+    bcount[blockIdx.x] = total;
+  }
+}
+
 // kBndRows rows per workgroup (8 per thread, coalesced): a row keeps its
-// assignment when its moved bounds still certify it (kmeans_i8.hpp Bounds);
-// the others are written, in row order, to tmp[block * kBndRows ...] and
-// counted in bcount[block].
+// assignment when its moved bounds still certify it (kmeans_i8.hpp Bounds,
+// state 0); else it is re-checked against its carried set when the set's
+// moved outside bound still stands (state 2, listed here), else screened
+// (state 1).  Every carried bound is moved by the drift.
 __global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict__ assign,
                                                        float2* __restrict__ bnd,
+                                                       float* __restrict__ lnc,
+                                                       unsigned char* __restrict__ state,
                                                        const double* __restrict__ xnorm,
                                                        int64_t n, int k,
                                                        const double* __restrict__ delta,
                                                        const DriftParams* __restrict__ prm,
                                                        int32_t* __restrict__ tmp,
                                                        unsigned int* __restrict__ bcount) {
-  constexpr int IT = kBndRows / 256;
-  __shared__ unsigned wc[IT * 4];
+  __shared__ unsigned wc[kBndIT * 4];
   const DriftParams P = *prm;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * kBndRows;
-  unsigned long long masks[IT];
+  unsigned long long masks[kBndIT];
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
+  for (int it = 0; it < kBndIT; ++it) {
     const int64_t r = base + it * 256 + tid;
-    bool listed = false;
+    int st = 1;
     if (r < n) {
-      listed = true;
       const int a = assign[r];
       const float2 b = bnd[r];
-      if (!P.bad && b.x >= 0.0f && b.y > 0.0f && a >= 0 && a < k) {
+      const float ln = lnc[r];
+      const bool okA = !P.bad && a >= 0 && a < k;
+      if (okA && b.x >= 0.0f && b.y > 0.0f) {
         const double U = (double)b.x + delta[a];
         const double L = (double)b.y - (a == P.i1 ? P.d2 : P.d1);
         const double xn = xnorm[r];
@@ -2515,30 +2587,39 @@ __global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict
         // the reference's rounding slack, plus this test's own rounding
         const double tau = 0x1p-29 * (xx + P.cmax2) + 0x1p-48 * (L2 + U2) + 0x1p-1000;
         if (L > 0.0 && (L2 - U2) > tau) {
-          listed = false;
+          st = 0;
           bnd[r] = make_float2(fup(U * (1.0 + 0x1p-50)), fdown(L * (1.0 - 0x1p-50)));
         }
       }
+      if (ln >= 0.0f) {   // a carried set (NaN / negative: none)
+        const double Ln = okA ? ((double)ln - P.d1) * (1.0 - 0x1p-50) : -1.0;
+        if (st == 1 && Ln > 0.0) st = 2;
+        lnc[r] = st != 1 && Ln > 0.0 ? fdown(Ln) : -1.0f;
+      }
+      state[r] = (unsigned char)st;
     }
-    masks[it] = __builtin_amdgcn_ballot_w64(listed);
+    masks[it] = __builtin_amdgcn_ballot_w64(st == 2);
     if (lane == 0) wc[it * 4 + wave] = (unsigned)__builtin_popcountll(masks[it]);
   }
-  __syncthreads();
-  unsigned off = 0, total = 0;
-  const unsigned long long below = (1ull << lane) - 1ull;
+  bnd_block_list(masks, wc, base, tmp, bcount);
+}
+
+// The rows a full screen takes (state 1), listed as the filter lists its
+// re-checks.
+__global__ __launch_bounds__(256) void k_bounds_collect(const unsigned char* __restrict__ state,
+                                                        int64_t n, int32_t* __restrict__ tmp,
+                                                        unsigned int* __restrict__ bcount) {
+  __shared__ unsigned wc[kBndIT * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kBndRows;
+  unsigned long long masks[kBndIT];
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    unsigned before = 0;
-    for (int j = 0; j < it * 4 + wave; ++j) before += wc[j];
-    if ((masks[it] >> lane) & 1ull) {
-      off = before + (unsigned)__builtin_popcountll(masks[it] & below);
-      tmp[base + off] = (int32_t)(base + it * 256 + tid);
-    }
+  for (int it = 0; it < kBndIT; ++it) {
+    const int64_t r = base + it * 256 + tid;
+    masks[it] = __builtin_amdgcn_ballot_w64(r < n && state[r] == 1);
+    if (lane == 0) wc[it * 4 + wave] = (unsigned)__builtin_popcountll(masks[it]);
   }
-  if (tid == 0) {
-    for (int j = 0; j < IT * 4; ++j) total += wc[j];
-    bcount[blockIdx.x] = total;
-  }
+  bnd_block_list(masks, wc, base, tmp, bcount);
 }
 
 // Single block: bcount[0..nb) -> exclusive offsets, bcount[nb] = *listCount
@@ -2569,7 +2650,7 @@ __global__ __launch_bounds__(1024) void k_bounds_scan(unsigned int* __restrict__
   if (t == 1023) {
     bcount[nb] = part[1023];
     *listCount = part[1023];
-    *cum += (unsigned long long)part[1023];
+    if (cum) *cum += (unsigned long long)part[1023];
   }
 }
 
@@ -2669,20 +2750,36 @@ int centers_drift(const double* C, double* Cp, int k, int d, double* delta, doub
   return CYC_OK;
 }
 
-int bounds_filter(const int32_t* assign, float2* ub_lb, const double* xnorm, int64_t n, int k,
-                  const double* delta, const DriftParams* prm, int32_t* tmp,
-                  unsigned int* bcount, int32_t* list, unsigned int* listCount,
-                  unsigned long long* cum, hipStream_t st) {
+int bounds_filter(const int32_t* assign, float2* ub_lb, float* lnc, unsigned char* state,
+                  const double* xnorm, int64_t n, int k, const double* delta,
+                  const DriftParams* prm, int32_t* tmp, unsigned int* bcount, int32_t* rcList,
+                  unsigned int* rcCount, unsigned long long* rcCum, hipStream_t st) {
   const int64_t nb = bounds_blocks(n);
   if (nb <= 0) return CYC_OK;
   KernelTimer timer("k_kmeans_bounds", st);
-  hipLaunchKernelGGL(k_bounds_filter, dim3((unsigned)nb), dim3(256), 0, st, assign, ub_lb, xnorm,
-                     n, k, delta, prm, tmp, bcount);
+  hipLaunchKernelGGL(k_bounds_filter, dim3((unsigned)nb), dim3(256), 0, st, assign, ub_lb, lnc,
+                     state, xnorm, n, k, delta, prm, tmp, bcount);
   CYC_LAUNCH_CHECK("k_bounds_filter");
-  hipLaunchKernelGGL(k_bounds_scan, dim3(1), dim3(1024), 0, st, bcount, nb, listCount, cum);
+  hipLaunchKernelGGL(k_bounds_scan, dim3(1), dim3(1024), 0, st, bcount, nb, rcCount, rcCum);
   CYC_LAUNCH_CHECK("k_bounds_scan");
   hipLaunchKernelGGL(k_bounds_scatter, dim3((unsigned)nb), dim3(256), 0, st, (const int32_t*)tmp,
-                     (const unsigned int*)bcount, list);
+                     (const unsigned int*)bcount, rcList);
+  CYC_LAUNCH_CHECK("k_bounds_scatter");
+  return CYC_OK;
+}
+
+// After the re-check: the state-1 rows into the screen's list (bd.list).
+int bounds_collect(const Bounds& bd, hipStream_t st) {
+  const int64_t nb = bounds_blocks(bd.n);
+  if (nb <= 0) return CYC_OK;
+  hipLaunchKernelGGL(k_bounds_collect, dim3((unsigned)nb), dim3(256), 0, st,
+                     (const unsigned char*)bd.state, bd.n, bd.tmp, bd.bcount);
+  CYC_LAUNCH_CHECK("k_bounds_collect");
+  hipLaunchKernelGGL(k_bounds_scan, dim3(1), dim3(1024), 0, st, bd.bcount, nb, bd.listCount,
+                     bd.cum);
+  CYC_LAUNCH_CHECK("k_bounds_scan");
+  hipLaunchKernelGGL(k_bounds_scatter, dim3((unsigned)nb), dim3(256), 0, st,
+                     (const int32_t*)bd.tmp, (const unsigned int*)bd.bcount, bd.list);
   CYC_LAUNCH_CHECK("k_bounds_scatter");
   return CYC_OK;
 }

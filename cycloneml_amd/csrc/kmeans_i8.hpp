@@ -151,25 +151,51 @@ struct DriftParams {
   int i1;            // the center of d1
   int bad;           // a non-finite drift or center: no row keeps its bounds
 };
+// Carried candidate sets: a row the three-limb candidate tier certified
+// keeps its set (<= kCandMax centers, sets) and the lower bound of every
+// center outside it (lnc, a distance, moved by the drift like lb).  When its
+// Hamerly bounds fail but lnc still stands, the row is re-checked against
+// its set alone (k_screen_cands3<.., RC>) instead of a full screen.
 struct Bounds {
   float2* ub_lb;               // n entries
-  const int32_t* rowsIn;       // the rows to screen (bounds_filter); nullptr: every row
+  const int32_t* rowsIn;       // the rows to screen; nullptr: every row
   const unsigned int* rowsInCount;
+  float* lnc = nullptr;        // n: the outside bound (< 0 or NaN: no set)
+  int32_t* sets = nullptr;     // n x kCandMax
+  unsigned char* state = nullptr;   // n: 0 kept, 1 full screen, 2 re-check
+  const int32_t* rcRows = nullptr;  // the re-check list (bounds_filter) and its count
+  const unsigned int* rcCount = nullptr;
+  const DriftParams* dp = nullptr;
+  // bounds_collect's scratch and output (rowsIn / rowsInCount), its count
+  // of fully screened rows added to *cum
+  int32_t* tmp = nullptr;
+  unsigned int* bcount = nullptr;
+  int32_t* list = nullptr;
+  unsigned int* listCount = nullptr;
+  unsigned long long* cum = nullptr;
+  int64_t n = 0;
 };
 // Drift of the centers C against Cp (k x d, then Cp = C): delta (k doubles),
 // ccs (k doubles of scratch) and *prm.
 int centers_drift(const double* C, double* Cp, int k, int d, double* delta, double* ccs,
                   DriftParams* prm, hipStream_t st);
 // The rows whose carried bounds still certify assign[row] keep it (their
-// bounds moved by the drift); the others go to list / *listCount (in row
-// order), and *cum (64-bit) accumulates their number.  tmp: n entries;
-// bcount: bounds_blocks(n) + 1 entries.
+// bounds moved by the drift, state 0); of the others, those with a carried
+// set whose outside bound still stands go to the re-check list (rcList /
+// *rcCount, in row order; state 2), the rest to a full screen (state 1;
+// their sets dropped).  *rcCum (64-bit) accumulates the re-checked rows.
+// tmp: n entries; bcount: bounds_blocks(n) + 1 entries.  bounds_collect
+// (in screen, after the re-check) lists the state-1 rows for the screen.
 constexpr int kBndRows = 2048;   // rows per filter workgroup
 inline int64_t bounds_blocks(int64_t n) { return (n + kBndRows - 1) / kBndRows; }
-int bounds_filter(const int32_t* assign, float2* ub_lb, const double* xnorm, int64_t n, int k,
-                  const double* delta, const DriftParams* prm, int32_t* tmp,
-                  unsigned int* bcount, int32_t* list, unsigned int* listCount,
-                  unsigned long long* cum, hipStream_t st);
+int bounds_filter(const int32_t* assign, float2* ub_lb, float* lnc, unsigned char* state,
+                  const double* xnorm, int64_t n, int k, const double* delta,
+                  const DriftParams* prm, int32_t* tmp, unsigned int* bcount, int32_t* rcList,
+                  unsigned int* rcCount, unsigned long long* rcCum, hipStream_t st);
+
+// After the re-check (inside screen): the state-1 rows into bd.list /
+// bd.listCount (the screen's rowsIn), their count added to *bd.cum.
+int bounds_collect(const Bounds& bd, hipStream_t st);
 
 // Screen every row: certified rows get assign[row]; the others are appended
 // to list (listCount is NOT cleared here).  list2 / list2Count (n entries +

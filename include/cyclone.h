@@ -133,6 +133,11 @@ int64_t cyc_kmeans_rows_bytes(cyc_kmeans_rows rows);
  * (the rest kept their carried assignment); synchronises the device. */
 int cyc_kmeans_rows_set_bounds(cyc_kmeans_rows rows, int32_t enable);
 int cyc_kmeans_rows_bounds_info(cyc_kmeans_rows rows, int64_t* calls, int64_t* screened_rows);
+/* Rows whose bounds failed but whose carried candidate set (the three-limb
+ * candidate tier's, with a lower bound for every center outside it) was
+ * re-checked instead of a full screen -- certified there or passed on to
+ * the screen (and then also counted in screened_rows).  Synchronises. */
+int cyc_kmeans_rows_bounds_rechecked(cyc_kmeans_rows rows, int64_t* rechecked_rows);
 
 /* findClosest(centers, stats, point) for n points (stats from the last
  * cyc_kmeans_stats_dev on this plan).  assign[n], cost[n] device outputs.

@@ -950,6 +950,7 @@ def test_full_config_late_iteration(cuda):
     assert calls == last + 1
     screened = after - before
     assert 0 < screened < n // 2, screened
+    assert rows.bounds_rechecked() > 0      # carried candidate sets re-checked
     del rows
     threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or 16, os.cpu_count() or 1, 16)
     Xh = X.cpu().numpy()
