@@ -286,7 +286,7 @@ class KMeansWorkload:
     kernel = "k_chunk_sums"
     kernels = ("k_kmeans_screen1", "k_kmeans_refine2", "k_kmeans_screen2", "k_kmeans_cands3",
                "k_kmeans_cands", "k_kmeans_screen3", "k_kmeans_compact", "k_kmeans_assign_fp64",
-               "k_kmeans_bounds", "k_kmeans_recheck", "k_chunk_sums")
+               "k_kmeans_bounds", "k_kmeans_recheck", "k_kmeans_inc", "k_chunk_sums")
     pmc_names = {"k_kmeans_screen1": "k_screen32_l1", "k_kmeans_screen2": "k_screen32_l2",
                  "k_kmeans_refine2": "k_screen32r", "k_chunk_sums": "k_chunk_sums_fast"}
 
@@ -325,17 +325,22 @@ class KMeansWorkload:
 
     def before_timing(self, steps):
         """Centers of the first timed step (the cpu_baseline's) and the
-        carried bounds' screened-row counter at the start of the clock."""
+        carried bounds' / incremental sums' counters at the start of the
+        clock."""
         self.C_timed = self.C.clone()
         self.steps_timed = steps
         self._b0 = self.rows.bounds_info()
         self._rc0 = self.rows.bounds_rechecked()
+        self._i0 = self.rows.incremental_info()
 
     def after_steps(self):
         calls, screened = self.rows.bounds_info()
         self.screened_timed = screened - self._b0[1]
         self.bounded_calls = calls - self._b0[0]
         self.rechecked_timed = self.rows.bounds_rechecked() - self._rc0
+        inc, moved = self.rows.incremental_info()
+        self.inc_timed = inc - self._i0[0]
+        self.moved_timed = moved - self._i0[1]
 
     def step(self):
         k, d = self.k, self.d
@@ -347,27 +352,73 @@ class KMeansWorkload:
         self.parallel.allreduce_(buf)
         self.plan.update(self.C, self.cnorm, sums, wsum, 1e-4, self.conv)
 
+    # bytes per re-checked row: its image (3 limb planes of D), its carried
+    # set (6 int32), outside bound, (ub, lb), state byte and list entry
+    RECHECK_BYTES = 3 * 256 + 24 + 4 + 8 + 1 + 4
+
+    def _per_step(self, attr, default):
+        v = getattr(self, attr, None)
+        return default if v is None else v / self.steps_timed
+
     def work(self, kname, launches_per_step):
         D = 128 * ((self.d + 127) // 128)                 # 32-dim substeps, padded
         kpad = 32 * (2 * ((self.k + 63) // 64))           # 32-center tiles (even count)
         if kname == "k_kmeans_screen1":       # one limb product: 2 ops per (row, center, dim)
             # over the rows it screened (those the carried bounds did not keep)
-            rows = getattr(self, "screened_timed", None)
-            rows = self.n if rows is None else rows / self.steps_timed
+            rows = self._per_step("screened_timed", self.n)
             return 2.0 * D * kpad * rows / launches_per_step, I8
+        if kname == "k_kmeans_recheck":       # the carried sets' rows: image + state
+            rows = self._per_step("rechecked_timed", self.n / 8)
+            return self.RECHECK_BYTES * rows / launches_per_step, HBM
+        if kname == "k_kmeans_inc":           # assignment + previous (8 B/row), moved rows twice,
+            moved = self._per_step("moved_timed", 0.0)   # the clusters' state (S, P, C, S out)
+            b = self.n * 8.0 + moved * 2 * 8 * self.d + 4.0 * self.k * self.d * 8
+            return b / launches_per_step, HBM
         if kname == "k_chunk_sums":           # every row once (fp64) + its perm entry
-            return self.n * (8 * self.d + 4) / launches_per_step, HBM
+            # launched every step; empty (gated off on the device) when the
+            # incremental sums took the step, so priced over the full passes
+            full = self.steps_timed - getattr(self, "inc_timed", 0) if hasattr(
+                self, "steps_timed") else 1
+            if full <= 0:
+                return None
+            per_step = self.n * (8 * self.d + 4) * full / getattr(self, "steps_timed", 1)
+            return per_step / launches_per_step, HBM
         if kname == "k_kmeans_screen2" and self._refine[0] < 0:   # no refinement: every row
             return 6.0 * D * kpad * self.n / launches_per_step, I8
         return None
 
     def step_work(self):
-        """A Lloyd iteration moves every row once (its fp64 values for the
-        cluster sums and their cost): 8 d bytes per row."""
-        return self.n * 8.0 * self.d, HBM
+        """The bytes a Lloyd iteration of this algorithm moves at least: every
+        row's carried state (ub/lb 8 B, assignment 4 B, outside bound 4 B,
+        norm 8 B read; bounds, state and outside bound 13 B written), the
+        re-checked rows' image and sets, the screened rows' one-limb image
+        (256 B), and the cluster sums' input -- every row's fp64 values on a
+        full pass, the moved rows' (twice) on an incremental one."""
+        steps = getattr(self, "steps_timed", None)
+        if steps is None:
+            return self.n * 8.0 * self.d, HBM
+        inc = getattr(self, "inc_timed", 0) / steps
+        sums = (1.0 - inc) * self.n * (8.0 * self.d + 4) + \
+            self._per_step("moved_timed", 0.0) * 2 * 8 * self.d + inc * self.n * 8.0
+        b = self.n * 37.0 + self._per_step("rechecked_timed", 0.0) * self.RECHECK_BYTES + \
+            self._per_step("screened_timed", 0.0) * 256 + sums
+        return b, HBM
 
     def after_timing(self):
+        import torch
         self._refine = self.plan.last_refine()
+        # the same steps with the full cluster-sums pass every step (the
+        # incremental sums off), for comparison; then back on (the fit)
+        self.rows.set_incremental(False)
+        for _ in range(2):
+            self.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(5):
+            self.step()
+        torch.cuda.synchronize()
+        self.full_sums_ms = (time.perf_counter() - t0) / 5 * 1e3
+        self.rows.set_incremental(True)
 
     def fit_once(self, max_iter=20):
         """One fit as the ml estimator runs it -- maxIter 20, tol 1e-4
@@ -403,7 +454,19 @@ class KMeansWorkload:
         tier2, _ = self.plan.last_tiers()
         scr = getattr(self, "screened_timed", None)
         rc = getattr(self, "rechecked_timed", None)
-        return {"carried_bounds": {
+        inc = getattr(self, "inc_timed", None)
+        return {"incremental_sums": {
+            "incremental_steps": inc, "full_pass_steps": (self.steps_timed - inc) if inc is not None
+            else None,
+            "moved_rows_per_step": self._per_step("moved_timed", None),
+            "full_sums_ms_per_step": getattr(self, "full_sums_ms", None),
+            "note": "cluster sums carried across the fit (cyclone.h "
+                    "cyc_kmeans_rows_set_incremental): a step folds only the rows whose "
+                    "center changed into the carried sums and takes the cost from "
+                    "Q + 2 (P - c).(S - W P) + W |P - c|^2 with its rounding bounded on the "
+                    "device (<= 2^-42 of the cost, else the full pass); full_sums_ms_per_step: "
+                    "the same steps with the full pass every step, timed after the clock"},
+            "carried_bounds": {
             "rows_screened_per_step": scr / self.steps_timed if scr is not None else None,
             "rows_rechecked_per_step": rc / self.steps_timed if rc is not None else None,
             "rows_kept_per_step": self.n - scr / self.steps_timed if scr is not None else None,

@@ -73,6 +73,8 @@ SIGNATURES = {
     "cyc_kmeans_rows_set_bounds": (ctypes.c_int, [_vp, _i32]),
     "cyc_kmeans_rows_bounds_info": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_rows_bounds_rechecked": (ctypes.c_int, [_vp, _pi64]),
+    "cyc_kmeans_rows_set_incremental": (ctypes.c_int, [_vp, _i32]),
+    "cyc_kmeans_rows_incremental_info": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_last_tiers": (ctypes.c_int, [_vp, _pi64, _pi64]),
     "cyc_kmeans_last_screen": (ctypes.c_int, [_vp, _pi64]),
     "cyc_kmeans_last_candidates": (ctypes.c_int, [_vp, _pi64]),

@@ -202,6 +202,22 @@ class KMeansRows:
         certify their center skip the screen; either setting drops the state."""
         N.check(self._lib.cyc_kmeans_rows_set_bounds(self.handle, 1 if enable else 0))
 
+    def set_incremental(self, enable: bool):
+        """Incremental cluster sums across this fit's Lloyd iterations (on by
+        default, cyclone.h cyc_kmeans_rows_set_incremental): with the carried
+        bounds, unit weights and no per-row costs, a call folds only the rows
+        that changed center into the carried sums; either setting drops the
+        state."""
+        N.check(self._lib.cyc_kmeans_rows_set_incremental(self.handle, 1 if enable else 0))
+
+    def incremental_info(self):
+        """(calls that took the incremental path, moved rows they folded);
+        synchronises the device."""
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(self._lib.cyc_kmeans_rows_incremental_info(self.handle, ctypes.byref(a),
+                                                           ctypes.byref(b)))
+        return a.value, b.value
+
     def bounds_rechecked(self):
         """Rows re-checked against their carried candidate sets (all calls;
         synchronises the device)."""

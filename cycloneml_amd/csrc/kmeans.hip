@@ -1145,7 +1145,8 @@ __global__ void k_require_norms(const double* __restrict__ C, int k, int d,
 
 // ------------------------------------------------------- counting sort
 __global__ void k_hist(const int32_t* __restrict__ assign, int64_t n, int k,
-                       int32_t* __restrict__ hist) {
+                       int32_t* __restrict__ hist, const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   extern __shared__ int32_t cnt[];
   for (int c = threadIdx.x; c < k; c += blockDim.x) cnt[c] = 0;
   __syncthreads();
@@ -1163,7 +1164,8 @@ __global__ void k_hist(const int32_t* __restrict__ assign, int64_t n, int k,
 constexpr int kScanSegs = 64;
 
 __global__ void k_scan_seg(const int32_t* __restrict__ hist, int tiles, int k, int segT,
-                           int32_t* __restrict__ segsum) {
+                           int32_t* __restrict__ segsum, const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   const int c = blockIdx.x * 64 + threadIdx.x, s = blockIdx.y;
   if (c >= k) return;
   const int t0 = s * segT, t1 = min(tiles, t0 + segT);
@@ -1174,7 +1176,8 @@ __global__ void k_scan_seg(const int32_t* __restrict__ hist, int tiles, int k, i
 }
 
 __global__ void k_scan_segoff(int32_t* __restrict__ segsum, int segs, int k,
-                              int64_t* __restrict__ total) {
+                              int64_t* __restrict__ total, const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= k) return;
   int64_t run = 0;
@@ -1187,7 +1190,8 @@ __global__ void k_scan_segoff(int32_t* __restrict__ segsum, int segs, int k,
 }
 
 __global__ void k_scan_apply(int32_t* __restrict__ hist, int tiles, int k, int segT,
-                             const int32_t* __restrict__ segoff) {
+                             const int32_t* __restrict__ segoff, const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   const int c = blockIdx.x * 64 + threadIdx.x, s = blockIdx.y;
   if (c >= k) return;
   const int t0 = s * segT, t1 = min(tiles, t0 + segT);
@@ -1201,7 +1205,9 @@ __global__ void k_scan_apply(int32_t* __restrict__ hist, int tiles, int k, int s
 
 // Single block: cluster start offsets and chunk start offsets (exclusive scans).
 __global__ void k_scan_clusters(const int64_t* __restrict__ total, int k,
-                                int64_t* __restrict__ cstart, int64_t* __restrict__ chunkStart) {
+                                int64_t* __restrict__ cstart, int64_t* __restrict__ chunkStart,
+                                const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   __shared__ int64_t s_rows[1024], s_chunks[1024];
   const int tid = threadIdx.x;
   const int per = (k + 1023) / 1024;
@@ -1247,7 +1253,8 @@ __global__ void k_scan_clusters(const int64_t* __restrict__ total, int k,
 // lines from eight L2s (the grid is 8 * per blocks; the spare ones leave).
 __global__ void k_scatter(const int32_t* __restrict__ assign, int64_t n, int k,
                           const int32_t* __restrict__ tileOff, const int64_t* __restrict__ cstart,
-                          int32_t* __restrict__ perm, int64_t tiles) {
+                          int32_t* __restrict__ perm, int64_t tiles, const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   extern __shared__ int64_t pos[];
   const int64_t per = ((int64_t)gridDim.x + 7) / 8;
   const int64_t tile = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
@@ -1383,9 +1390,11 @@ __global__ __launch_bounds__(256) void k_chunk_sums_fast(
     const double* __restrict__ X, int d, const double* __restrict__ w,
     const double* __restrict__ C, const int32_t* __restrict__ perm,
     const int64_t* __restrict__ cstart, const int64_t* __restrict__ chunkStart, int k,
-    double* __restrict__ part, double* __restrict__ pw, double* __restrict__ pc) {
+    double* __restrict__ part, double* __restrict__ pw, double* __restrict__ pc,
+    const double* __restrict__ xnorm, double* __restrict__ pa, const int* __restrict__ gate) {
   __shared__ int32_t rowsS[kChunkRows];
-  __shared__ double red[256];
+  __shared__ double red[256], reda[256];
+  if (gate && !*gate) return;
   const int64_t ch = blockIdx.x;
   if (ch >= chunkStart[k]) return;
   int lo = 0, hi = k;
@@ -1445,9 +1454,16 @@ __global__ __launch_bounds__(256) void k_chunk_sums_fast(
     qt = dadd(qt, q[u]);
   }
   red[tid] = qt;
+  // pa (incremental sums' error scale): the chunk's sum of w |x| (wave-order
+  // norms are enough, it only sizes a bound)
+  if (pa) reda[tid] = tid < cnt ? (w ? dmul(w[rowsS[tid]], xnorm[rowsS[tid]]) : xnorm[rowsS[tid]])
+                                : 0.0;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
-    if (tid < off) red[tid] = dadd(red[tid], red[tid + off]);
+    if (tid < off) {
+      red[tid] = dadd(red[tid], red[tid + off]);
+      if (pa) reda[tid] = dadd(reda[tid], reda[tid + off]);
+    }
     __syncthreads();
   }
   if (tid == 0) {
@@ -1459,6 +1475,7 @@ __global__ __launch_bounds__(256) void k_chunk_sums_fast(
     }
     pw[ch] = sw;
     pc[ch] = red[0];
+    if (pa) pa[ch] = reda[0];
   }
 }
 
@@ -1557,15 +1574,24 @@ __global__ __launch_bounds__(kNormRows) void k_row_cost(const double* __restrict
 }
 
 // Fold a cluster's chunks in chunk order and add into the caller's sums.
+// fS / fW / fA (optional, the incremental sums' state): the cluster's own
+// sums, weight and sum of w |x| (from pa) stored besides.
 __global__ void k_reduce_clusters(const double* __restrict__ part, const double* __restrict__ pw,
                                   const double* __restrict__ pc,
                                   const int64_t* __restrict__ chunkStart, int d,
                                   double* __restrict__ sums, double* __restrict__ wsum,
-                                  double* __restrict__ ccost) {
+                                  double* __restrict__ ccost, const double* __restrict__ pa,
+                                  double* __restrict__ fS, double* __restrict__ fW,
+                                  double* __restrict__ fA, const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   const int c = blockIdx.x;
   const int64_t a = chunkStart[c], b = chunkStart[c + 1];
   if (a == b) {
     if (threadIdx.x == 0) ccost[c] = 0.0;
+    if (fS) {
+      for (int j = threadIdx.x; j < d; j += blockDim.x) fS[(int64_t)c * d + j] = 0.0;
+      if (threadIdx.x == 0) fW[c] = fA[c] = 0.0;
+    }
     return;
   }
   // chunk order kept; 16 chunks' loads in flight per step
@@ -1581,9 +1607,15 @@ __global__ void k_reduce_clusters(const double* __restrict__ part, const double*
     }
     for (; ch < b; ++ch) s = dadd(s, part[ch * d + j]);
     sums[(int64_t)c * d + j] = dadd(sums[(int64_t)c * d + j], s);
+    if (fS) fS[(int64_t)c * d + j] = s;
   }
-  // the weight and cost folds on two other waves
-  const int tw = 64 % blockDim.x, tc = 128 % blockDim.x;
+  // the weight and cost folds on two other waves (pa on a third)
+  const int tw = 64 % blockDim.x, tc = 128 % blockDim.x, ta = 192 % blockDim.x;
+  if (fS && threadIdx.x == ta && ta != tw && ta != tc) {
+    double s = 0.0;
+    for (int64_t ch = a; ch < b; ++ch) s = dadd(s, pa[ch]);
+    fA[c] = s;
+  }
   if (threadIdx.x == tw || threadIdx.x == tc) {
     const double* src = threadIdx.x == tw ? pw : pc;
     double s = 0.0;
@@ -1596,13 +1628,19 @@ __global__ void k_reduce_clusters(const double* __restrict__ part, const double*
       for (int u = 0; u < 8; ++u) s = dadd(s, v[u]);
     }
     for (; ch < b; ++ch) s = dadd(s, src[ch]);
-    if (threadIdx.x == tw) wsum[c] = dadd(wsum[c], s);
-    else ccost[c] = s;
+    if (threadIdx.x == tw) {
+      wsum[c] = dadd(wsum[c], s);
+      if (fS) fW[c] = s;
+    } else {
+      ccost[c] = s;
+    }
   }
 }
 
 // Single block, fixed-shape tree: cost_sum += sum_c ccost[c].
-__global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __restrict__ out) {
+__global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __restrict__ out,
+                             const int* __restrict__ gate) {
+  if (gate && !*gate) return;
   __shared__ double s[256];
   double a = 0.0;
   for (int c = threadIdx.x; c < k; c += 256) a = dadd(a, ccost[c]);
@@ -1613,6 +1651,429 @@ __global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __
     __syncthreads();
   }
   if (threadIdx.x == 0) out[0] = dadd(out[0], s[0]);
+}
+
+// ------------------------------------------------- incremental cluster sums
+// (round 6) With the carried bounds most rows keep their center from one
+// Lloyd call of a fit to the next, so the cluster sums change only by the
+// rows that moved.  The row image's owner keeps, per cluster c, the sums S_c,
+// weight W_c (unit weights: the count), member count N_c, a reference point
+// P_c (the centers of the last full pass) with Q_c = sum |x - P_c|^2 over the
+// members, and A_c = sum |x| (error scale).  A call with few moved rows
+// (<= n / kIncMovedFrac) updates them by the moved rows alone (subtracted
+// from the old cluster, added to the new, in row order) and takes the cost
+// for the call's centers c from
+//   sum_x |x - c|^2 = Q_c + 2 (P_c - c).(S_c - W_c P_c) + W_c |P_c - c|^2,
+// which is exact algebra; the rounding of every term is bounded on the device
+// (ES_c, EQ_c and the correction's own).  When the bound
+// exceeds 2^-42 of the cost, a moved count is too large, or no state exists,
+// the call runs the full pass over every row instead (the sort by cluster and
+// k_chunk_sums_fast), which resets the state.  Gates: gate[0] = 1 runs the
+// full pass, gate[1] = 1 the incremental one; exactly one is set.
+constexpr int kIncRows = 2048;       // rows per k_inc_moved workgroup
+constexpr int kIncMovedFrac = 8;     // at most n / 8 moved rows take the incremental path
+
+// The rows whose assignment differs from prev (then prev = assign): per
+// kIncRows-row block, in row order, into tmpRow / tmpOld at the block's base;
+// the block's count in bcount[block].
+__global__ __launch_bounds__(256) void k_inc_moved(const int32_t* __restrict__ assign,
+                                                   int32_t* __restrict__ prev, int64_t n,
+                                                   int32_t* __restrict__ tmpRow,
+                                                   int32_t* __restrict__ tmpOld,
+                                                   unsigned int* __restrict__ bcount) {
+  constexpr int IT = kIncRows / 256;
+  __shared__ unsigned wc[IT * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kIncRows;
+  unsigned long long masks[IT];
+  int32_t olds[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int64_t r = base + it * 256 + tid;
+    bool moved = false;
+    olds[it] = -1;
+    if (r < n) {
+      const int32_t a = assign[r], b = prev[r];
+      moved = a != b;
+      olds[it] = b;
+      if (moved) prev[r] = a;
+    }
+    masks[it] = __builtin_amdgcn_ballot_w64(moved);
+    if (lane == 0) wc[it * 4 + wave] = (unsigned)__builtin_popcountll(masks[it]);
+  }
+  __syncthreads();
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    unsigned before = 0;
+    for (int j = 0; j < it * 4 + wave; ++j) before += wc[j];
+    if ((masks[it] >> lane) & 1ull) {
+      const int64_t pos = base + before + (unsigned)__builtin_popcountll(masks[it] & below);
+      tmpRow[pos] = (int32_t)(base + it * 256 + tid);
+      tmpOld[pos] = olds[it];
+    }
+  }
+  if (tid == 0) {
+    unsigned total = 0;
+    for (int j = 0; j < IT * 4; ++j) total += wc[j];
+    bcount[blockIdx.x] = total;
+  }
+}
+
+// Single block: bcount[0..nb) -> exclusive offsets, bcount[nb] = *count = the
+// moved rows; the gates (incremental when valid and count <= mcap); *movedCum
+// += count on the incremental path.
+__global__ __launch_bounds__(1024) void k_inc_scan(unsigned int* __restrict__ bcount, int64_t nb,
+                                                   unsigned int* __restrict__ count, int valid,
+                                                   int64_t mcap, int* __restrict__ gate,
+                                                   unsigned long long* __restrict__ movedCum) {
+  __shared__ unsigned part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t a = min<int64_t>(nb, t * per), e = min<int64_t>(nb, a + per);
+  unsigned s = 0;
+  for (int64_t i = a; i < e; ++i) s += bcount[i];
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const unsigned v = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  unsigned run = t ? part[t - 1] : 0u;
+  for (int64_t i = a; i < e; ++i) {
+    const unsigned c = bcount[i];
+    bcount[i] = run;
+    run += c;
+  }
+  if (t == 1023) {
+    const unsigned total = part[1023];
+    bcount[nb] = total;
+    *count = total;
+    const int inc = valid && (int64_t)total <= mcap;
+    gate[0] = inc ? 0 : 1;
+    gate[1] = inc ? 1 : 0;
+    if (inc) *movedCum += (unsigned long long)total;
+  }
+}
+
+// The blocks' moved rows behind their offsets (incremental path only).
+__global__ __launch_bounds__(256) void k_inc_gather(const int32_t* __restrict__ tmpRow,
+                                                    const int32_t* __restrict__ tmpOld,
+                                                    const unsigned int* __restrict__ bcount,
+                                                    int32_t* __restrict__ movedRow,
+                                                    int32_t* __restrict__ movedOld,
+                                                    const int* __restrict__ gate) {
+  if (!gate[1]) return;
+  const int64_t b = blockIdx.x, base = b * kIncRows;
+  const unsigned off = bcount[b], cnt = bcount[b + 1] - off;
+  for (unsigned i = threadIdx.x; i < cnt; i += 256) {
+    movedRow[off + i] = tmpRow[base + i];
+    movedOld[off + i] = tmpOld[base + i];
+  }
+}
+
+// Entries of the delta: e < m adds moved row e to its new cluster, e in
+// [m, 2m) subtracts moved row e - m from its old one.
+__device__ __forceinline__ int inc_key(int64_t e, unsigned m, const int32_t* __restrict__ movedRow,
+                                       const int32_t* __restrict__ movedOld,
+                                       const int32_t* __restrict__ assign) {
+  return e < (int64_t)m ? assign[movedRow[e]] : movedOld[e - m];
+}
+
+// Counting sort of the 2m entries by cluster (stable: entry order kept), in
+// kSortTile-entry tiles like k_hist / k_scatter; tiles past 2m hold zeros.
+__global__ void k_inc_hist(const int32_t* __restrict__ movedRow,
+                           const int32_t* __restrict__ movedOld,
+                           const int32_t* __restrict__ assign, const unsigned int* __restrict__ count,
+                           int k, int32_t* __restrict__ hist, const int* __restrict__ gate) {
+  if (!gate[1]) return;
+  extern __shared__ int32_t cnt[];
+  for (int c = threadIdx.x; c < k; c += blockDim.x) cnt[c] = 0;
+  __syncthreads();
+  const unsigned m = *count;
+  const int64_t E = 2 * (int64_t)m;
+  const int64_t e0 = (int64_t)blockIdx.x * kSortTile, e1 = min<int64_t>(E, e0 + kSortTile);
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
+    atomicAdd(&cnt[inc_key(e, m, movedRow, movedOld, assign)], 1);
+  __syncthreads();
+  for (int c = threadIdx.x; c < k; c += blockDim.x) hist[(int64_t)blockIdx.x * k + c] = cnt[c];
+}
+
+__global__ void k_inc_scatter(const int32_t* __restrict__ movedRow,
+                              const int32_t* __restrict__ movedOld,
+                              const int32_t* __restrict__ assign,
+                              const unsigned int* __restrict__ count, int k,
+                              const int32_t* __restrict__ tileOff, const int64_t* __restrict__ cstart,
+                              int32_t* __restrict__ eperm, int64_t tiles,
+                              const int* __restrict__ gate) {
+  if (!gate[1]) return;
+  extern __shared__ int64_t pos[];
+  const int64_t tile = blockIdx.x;
+  if (tile >= tiles) return;
+  const unsigned m = *count;
+  const int64_t E = 2 * (int64_t)m;
+  const int64_t e0 = tile * kSortTile;
+  if (e0 >= E) return;
+  const int lane = threadIdx.x;
+  const int kb = 32 - __builtin_clz((unsigned)max(k - 1, 1));
+  for (int c = lane; c < k; c += 64) pos[c] = cstart[c] + tileOff[tile * k + c];
+  __syncthreads();
+  const int64_t e1 = min<int64_t>(E, e0 + kSortTile);
+  for (int64_t b = e0; b < e1; b += 64) {
+    const int64_t e = b + lane;
+    const int c = e < e1 ? inc_key(e, m, movedRow, movedOld, assign) : -1;
+    unsigned long long msk = __ballot(c >= 0);
+    for (int q = 0; q < kb; ++q) {
+      const bool bit = (c >> q) & 1;
+      const unsigned long long bal = __ballot(bit);
+      msk &= bit ? bal : ~bal;
+    }
+    const int prior = __popcll(msk & ((1ull << lane) - 1));
+    const int last = 63 - __clzll(msk);
+    const int64_t p = (c >= 0) ? pos[c] + prior : 0;
+    __builtin_amdgcn_wave_barrier();
+    if (c >= 0) {
+      eperm[p] = (int32_t)e;
+      if (last == lane) pos[c] = p + 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Block sum of NV doubles per thread (fixed tree, results in every thread).
+template <int NV>
+__device__ __forceinline__ void inc_block_sum(double (&v)[NV], double* red) {
+  const int tid = threadIdx.x;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) red[i * 256 + tid] = v[i];
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) red[i * 256 + tid] = dadd(red[i * 256 + tid], red[i * 256 + tid + off]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = red[i * 256];
+}
+
+// One workgroup per cluster: fold the cluster's entries (in order) into its
+// state, then its cost for the call's centers C and the bound of that cost's
+// rounding (cerr), cbad = 1 when the state's error grew past 2^-38 of the
+// sum of the members' norms.  Unit weights only.
+template <int NJ>
+__global__ __launch_bounds__(256) void k_inc_fold(
+    const double* __restrict__ X, int d, const double* __restrict__ xnorm,
+    const double* __restrict__ C, const int32_t* __restrict__ movedRow,
+    const unsigned int* __restrict__ count, const int32_t* __restrict__ eperm,
+    const int64_t* __restrict__ ecstart, double* __restrict__ S, const double* __restrict__ P,
+    double* __restrict__ W, double* __restrict__ Q, int64_t* __restrict__ N,
+    double* __restrict__ A, double* __restrict__ ES, double* __restrict__ EQ,
+    double* __restrict__ ccost, double* __restrict__ cerr, int* __restrict__ cbad,
+    const int* __restrict__ gate) {
+  if (!gate[1]) return;
+  __shared__ int32_t rowsS[256];
+  __shared__ double sgS[256];
+  __shared__ double red[5 * 256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const unsigned m = *count;
+  const int64_t e0 = ecstart[c], e1 = ecstart[c + 1];
+  const int64_t ent = e1 - e0;
+  double ds[NJ], dq[NJ], dqa[NJ], pj[NJ];
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) {
+    const int j = tid + 256 * u;
+    ds[u] = dq[u] = dqa[u] = 0.0;
+    pj[u] = j < d ? P[(int64_t)c * d + j] : 0.0;
+  }
+  double tN = 0.0, tA = 0.0, tAbs = 0.0;   // this thread's entries: count, sum |x|
+  for (int64_t b0 = e0; b0 < e1; b0 += 256) {
+    const int cnt = (int)min<int64_t>(256, e1 - b0);
+    __syncthreads();
+    if (tid < cnt) {
+      const int64_t e = eperm[b0 + tid];
+      const bool add = e < (int64_t)m;
+      const int32_t r = add ? movedRow[e] : movedRow[e - m];
+      rowsS[tid] = r;
+      sgS[tid] = add ? 1.0 : -1.0;
+      const double xn = xnorm[r];
+      tN += add ? 1.0 : -1.0;
+      tA = add ? dadd(tA, xn) : dsub(tA, xn);
+      tAbs = dadd(tAbs, xn);
+    }
+    __syncthreads();
+    for (int p0 = 0; p0 < cnt; p0 += 8) {
+      double xv[8][NJ];
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const int64_t r = rowsS[min(p0 + v, cnt - 1)];
+#pragma unroll
+        for (int u = 0; u < NJ; ++u) {
+          const int j = tid + 256 * u;
+          xv[v][u] = j < d ? X[r * d + j] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        if (p0 + v < cnt) {
+          const bool add = sgS[p0 + v] > 0.0;
+#pragma unroll
+          for (int u = 0; u < NJ; ++u) {
+            const double x = xv[v][u];
+            const double df = dsub(pj[u], x);
+            const double t = dmul(df, df);
+            ds[u] = add ? dadd(ds[u], x) : dsub(ds[u], x);
+            dq[u] = add ? dadd(dq[u], t) : dsub(dq[u], t);
+            dqa[u] = dadd(dqa[u], t);
+          }
+        }
+      }
+    }
+  }
+  double r1[5] = {0.0, 0.0, tN, tA, tAbs};
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) {
+    r1[0] = dadd(r1[0], dq[u]);
+    r1[1] = dadd(r1[1], dqa[u]);
+  }
+  inc_block_sum<5>(r1, red);
+  const int64_t nNew = N[c] + (int64_t)r1[2];
+  const bool empty = nNew <= 0;
+  const double wNew = empty ? 0.0 : (double)nNew;    // unit weights: the count
+  double sv[NJ];
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) {
+    const int j = tid + 256 * u;
+    const double s0 = j < d ? S[(int64_t)c * d + j] : 0.0;
+    sv[u] = empty ? 0.0 : (ent ? dadd(s0, ds[u]) : s0);
+    if (j < d && ent) S[(int64_t)c * d + j] = sv[u];
+  }
+  // the cost's terms for the call's centers
+  double r2[4] = {0.0, 0.0, 0.0, 0.0};   // |S|^2, D.V, |D|^2, |P|^2
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) {
+    const int j = tid + 256 * u;
+    if (j < d) {
+      const double D = dsub(pj[u], C[(int64_t)c * d + j]);
+      const double V = dsub(sv[u], dmul(wNew, pj[u]));
+      r2[0] = dadd(r2[0], dmul(sv[u], sv[u]));
+      r2[1] = dadd(r2[1], dmul(D, V));
+      r2[2] = dadd(r2[2], dmul(D, D));
+      r2[3] = dadd(r2[3], dmul(pj[u], pj[u]));
+    }
+  }
+  inc_block_sum<4>(r2, red);
+  if (tid == 0) {
+    double q = Q[c], a = A[c], es = ES[c], eq = EQ[c];
+    if (empty) {
+      q = a = es = eq = 0.0;
+    } else if (ent) {
+      const double nS = sqrt(r2[0]) * (1.0 + 0x1p-50);
+      q = dadd(q, r1[0]);
+      a = dadd(a, r1[3]);
+      es += 0x1p-52 * ((double)(ent + 1) * r1[4] + nS);
+      eq += 0x1p-52 * ((double)(ent + 2) * r1[1] + fabs(q));
+    }
+    N[c] = empty ? 0 : nNew;
+    W[c] = wNew;
+    Q[c] = q;
+    A[c] = a;
+    ES[c] = es;
+    EQ[c] = eq;
+    double cost = 0.0, err = 0.0;
+    int bad = 0;
+    if (!empty) {
+      const double nS = sqrt(r2[0]) * (1.0 + 0x1p-50), nD = sqrt(r2[2]) * (1.0 + 0x1p-50),
+                   nP = sqrt(r2[3]) * (1.0 + 0x1p-50);
+      cost = dadd(q, dadd(dmul(2.0, r2[1]), dmul(wNew, r2[2])));
+      const double sv2 = nS + wNew * nP;
+      err = eq + 2.0 * nD * (es + 0x1p-51 * sv2) + 0x1p-41 * (nD * sv2 + wNew * r2[2]) +
+            0x1p-50 * fabs(cost);
+      bad = !(es <= 0x1p-38 * a) || !(fabs(cost) < INFINITY) || !(err < INFINITY);
+    }
+    ccost[c] = cost;
+    cerr[c] = err;
+    cbad[c] = bad;
+  }
+}
+
+// Single block: the clusters' costs and error bounds summed in a fixed
+// tree; the incremental result stands when no cluster is flagged and the
+// bound is within 2^-42 of the cost, else the gates switch to the full pass.
+__global__ __launch_bounds__(256) void k_inc_check(const double* __restrict__ ccost,
+                                                   const double* __restrict__ cerr,
+                                                   const int* __restrict__ cbad, int k,
+                                                   int* __restrict__ gate,
+                                                   double* __restrict__ tot,
+                                                   unsigned long long* __restrict__ incCum) {
+  if (!gate[1]) return;
+  __shared__ double red[3 * 256];
+  double v[3] = {0.0, 0.0, 0.0};
+  for (int c = threadIdx.x; c < k; c += 256) {
+    v[0] = dadd(v[0], ccost[c]);
+    v[1] += cerr[c];
+    v[2] += cbad[c] ? 1.0 : 0.0;
+  }
+  inc_block_sum<3>(v, red);
+  if (threadIdx.x == 0) {
+    const bool ok = v[2] == 0.0 && v[1] <= 0x1p-42 * fabs(v[0]) && fabs(v[0]) < INFINITY;
+    tot[0] = v[0];
+    tot[1] = v[1];
+    if (ok) {
+      *incCum += 1ull;
+    } else {
+      gate[0] = 1;
+      gate[1] = 0;
+    }
+  }
+}
+
+// The incremental result into the caller's buffers (sums += S, wsum += W,
+// cost_sum += the checked total).
+__global__ __launch_bounds__(256) void k_inc_emit(const double* __restrict__ S,
+                                                  const double* __restrict__ W, int d,
+                                                  const double* __restrict__ tot,
+                                                  double* __restrict__ sums,
+                                                  double* __restrict__ wsum,
+                                                  double* __restrict__ costSum,
+                                                  const int* __restrict__ gate) {
+  if (!gate[1]) return;
+  const int c = blockIdx.x;
+  for (int j = threadIdx.x; j < d; j += 256)
+    sums[(int64_t)c * d + j] = dadd(sums[(int64_t)c * d + j], S[(int64_t)c * d + j]);
+  if (threadIdx.x == 0) {
+    wsum[c] = dadd(wsum[c], W[c]);
+    if (c == 0) costSum[0] = dadd(costSum[0], tot[0]);
+  }
+}
+
+// After a full pass: its fresh sums are the state (written by
+// k_reduce_clusters), P = C, Q = the clusters' costs, N = the counts, and the
+// error bounds of the full pass's own summation (<= 256 rows per chunk
+// partial, the block tree, then the chunk fold).
+__global__ __launch_bounds__(256) void k_inc_reset(const double* __restrict__ C, int d,
+                                                   double* __restrict__ P,
+                                                   const double* __restrict__ ccost,
+                                                   const int64_t* __restrict__ total,
+                                                   const int64_t* __restrict__ chunkStart,
+                                                   double* __restrict__ Q, int64_t* __restrict__ N,
+                                                   const double* __restrict__ A,
+                                                   double* __restrict__ ES, double* __restrict__ EQ,
+                                                   const int* __restrict__ gate) {
+  if (!gate[0]) return;
+  const int c = blockIdx.x;
+  for (int j = threadIdx.x; j < d; j += 256) P[(int64_t)c * d + j] = C[(int64_t)c * d + j];
+  if (threadIdx.x == 0) {
+    const double f = 0x1p-52 * (double)(300 + (chunkStart[c + 1] - chunkStart[c]));
+    Q[c] = ccost[c];
+    N[c] = total[c];
+    ES[c] = f * A[c];
+    EQ[c] = f * fabs(ccost[c]);
+  }
 }
 
 constexpr int kUpdLds = 3072;   // widest center staged in LDS by k_update_centers
@@ -1869,6 +2330,17 @@ struct cyc_kmeans_rows_s {
   // per-row state, the re-check list, its count and running total
   cyc::DeviceBuffer bLnc, bSets, bState, bRc, bRcCount, bRcCum;
   int64_t bCalls = 0, bFullRows = 0;   // bounded calls; rows of their full (first) screens
+  // Incremental cluster sums (k_inc_*; with the carried bounds, unit
+  // weights, no per-row costs): the assignment the state refers to (iPrev),
+  // the per-cluster state S, P, W, Q, N, A, ES, EQ, and the scratch of the
+  // moved-row list and its sort by cluster.  iCum: moved rows and calls that
+  // took the incremental path (two 64-bit counters).
+  bool iEnabled = true;    // cyc_kmeans_rows_set_incremental (CYC_KMEANS_INCR=0: off)
+  bool iValid = false;
+  int ik = 0;
+  cyc::DeviceBuffer iPrev, iTmpRow, iTmpOld, iBcount, iCount, iGate, iMovedRow, iMovedOld, iHist,
+      iSegsum, iTotal, iCstart, iChunkStart, iPerm, iS, iP, iW, iQ, iN, iA, iES, iEQ, iCost, iErr,
+      iBad, iTot, iCum, iPa;
 };
 
 namespace {
@@ -2406,7 +2878,7 @@ namespace {
 // chunkStart (k + 1 offsets of kChunkRows-row chunks); part / pw / pc
 // reserved for maxChunks chunks of d columns.
 int sort_clusters(cyc_kmeans_plan p, const int32_t* assign, int64_t n, int d, hipStream_t st,
-                  int64_t& maxChunks) {
+                  int64_t& maxChunks, const int* gate = nullptr) {
   const int k = p->k;
   int rc;
   const int tiles = (int)((n + kSortTile - 1) / kSortTile);
@@ -2422,7 +2894,8 @@ int sort_clusters(cyc_kmeans_plan p, const int32_t* assign, int64_t n, int d, hi
       (rc = p->ccost.reserve(sizeof(double) * (size_t)k)))
     return rc;
   int32_t* hist = (int32_t*)p->hist.ptr;
-  hipLaunchKernelGGL(k_hist, dim3(tiles), dim3(256), sizeof(int32_t) * k, st, assign, n, k, hist);
+  hipLaunchKernelGGL(k_hist, dim3(tiles), dim3(256), sizeof(int32_t) * k, st, assign, n, k, hist,
+                     gate);
   CYC_LAUNCH_CHECK("k_hist");
   {
     const int segT = (tiles + std::min(kScanSegs, tiles) - 1) / std::min(kScanSegs, tiles);
@@ -2430,22 +2903,178 @@ int sort_clusters(cyc_kmeans_plan p, const int32_t* assign, int64_t n, int d, hi
     if ((rc = p->segsum.reserve(sizeof(int32_t) * (size_t)segs * k))) return rc;
     int32_t* segsum = (int32_t*)p->segsum.ptr;
     hipLaunchKernelGGL(k_scan_seg, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0, st,
-                       (const int32_t*)hist, tiles, k, segT, segsum);
+                       (const int32_t*)hist, tiles, k, segT, segsum, gate);
     CYC_LAUNCH_CHECK("k_scan_seg");
     hipLaunchKernelGGL(k_scan_segoff, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, st, segsum,
-                       segs, k, (int64_t*)p->total.ptr);
+                       segs, k, (int64_t*)p->total.ptr, gate);
     CYC_LAUNCH_CHECK("k_scan_segoff");
     hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0,
-                       st, hist, tiles, k, segT, (const int32_t*)segsum);
+                       st, hist, tiles, k, segT, (const int32_t*)segsum, gate);
     CYC_LAUNCH_CHECK("k_scan_apply");
   }
   hipLaunchKernelGGL(k_scan_clusters, dim3(1), dim3(1024), 0, st, (const int64_t*)p->total.ptr, k,
-                     (int64_t*)p->cstart.ptr, (int64_t*)p->chunkStart.ptr);
+                     (int64_t*)p->cstart.ptr, (int64_t*)p->chunkStart.ptr, gate);
   CYC_LAUNCH_CHECK("k_scan_clusters");
   hipLaunchKernelGGL(k_scatter, dim3((unsigned)(8 * (((int64_t)tiles + 7) / 8))), dim3(64),
                      sizeof(int64_t) * k, st, assign, n, k, hist, (const int64_t*)p->cstart.ptr,
-                     (int32_t*)p->perm.ptr, (int64_t)tiles);
+                     (int32_t*)p->perm.ptr, (int64_t)tiles, gate);
   CYC_LAUNCH_CHECK("k_scatter");
+  return CYC_OK;
+}
+
+bool inc_on(cyc_kmeans_rows rows) {
+  static const bool envOff = [] {
+    const char* e = std::getenv("CYC_KMEANS_INCR");
+    return e && e[0] == '0';
+  }();
+  return rows->iEnabled && !envOff;
+}
+
+// The Lloyd call's cluster sums, weights and cost through the incremental
+// state (k_inc_*) or, when the device decides so, the full pass; both paths
+// are enqueued and gated on the device (no host round trip).  assign: the
+// call's assignment (the bounds' bAssign).
+int inc_accumulate(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* X,
+                   const double* xnorm, const int32_t* assign, int64_t n, const double* C,
+                   double* sums, double* wsum, double* cost_sum, hipStream_t st) {
+  const int k = p->k, d = p->d, nj = (d + 255) / 256;
+  const int64_t nb = (n + kIncRows - 1) / kIncRows;
+  const int64_t mcap = n / kIncMovedFrac;
+  const int tilesE = (int)std::max<int64_t>(1, (2 * mcap + kSortTile - 1) / kSortTile);
+  const size_t kd = (size_t)k * d;
+  int rc;
+  const bool fresh = rows->iPrev.ptr == nullptr;
+  if ((rc = rows->iPrev.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = rows->iTmpRow.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = rows->iTmpOld.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = rows->iBcount.reserve(sizeof(unsigned int) * (size_t)(nb + 1))) ||
+      (rc = rows->iCount.reserve(64)) || (rc = rows->iGate.reserve(64)) ||
+      (rc = rows->iMovedRow.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(mcap, 1))) ||
+      (rc = rows->iMovedOld.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(mcap, 1))) ||
+      (rc = rows->iHist.reserve(sizeof(int32_t) * (size_t)tilesE * k)) ||
+      (rc = rows->iSegsum.reserve(sizeof(int32_t) * (size_t)kScanSegs * k)) ||
+      (rc = rows->iTotal.reserve(sizeof(int64_t) * (size_t)k)) ||
+      (rc = rows->iCstart.reserve(sizeof(int64_t) * (size_t)(k + 1))) ||
+      (rc = rows->iChunkStart.reserve(sizeof(int64_t) * (size_t)(k + 1))) ||
+      (rc = rows->iPerm.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(2 * mcap, 1))) ||
+      (rc = rows->iS.reserve(sizeof(double) * kd)) || (rc = rows->iP.reserve(sizeof(double) * kd)) ||
+      (rc = rows->iW.reserve(sizeof(double) * (size_t)k)) ||
+      (rc = rows->iQ.reserve(sizeof(double) * (size_t)k)) ||
+      (rc = rows->iN.reserve(sizeof(int64_t) * (size_t)k)) ||
+      (rc = rows->iA.reserve(sizeof(double) * (size_t)k)) ||
+      (rc = rows->iES.reserve(sizeof(double) * (size_t)k)) ||
+      (rc = rows->iEQ.reserve(sizeof(double) * (size_t)k)) ||
+      (rc = rows->iCost.reserve(sizeof(double) * (size_t)k)) ||
+      (rc = rows->iErr.reserve(sizeof(double) * (size_t)k)) ||
+      (rc = rows->iBad.reserve(sizeof(int) * (size_t)k)) || (rc = rows->iTot.reserve(64)) ||
+      (rc = rows->iCum.reserve(64)))
+    return rc;
+  if (fresh) {
+    CYC_HIP(hipMemsetAsync(rows->iPrev.ptr, 0xff, sizeof(int32_t) * (size_t)n, st));
+    CYC_HIP(hipMemsetAsync(rows->iCum.ptr, 0, 16, st));
+  }
+  const int valid = rows->iValid && rows->ik == k ? 1 : 0;
+  rows->iValid = false;   // until this call has completed
+  int* gate = (int*)rows->iGate.ptr;
+  unsigned long long* cum = (unsigned long long*)rows->iCum.ptr;
+  const unsigned int* cnt = (const unsigned int*)rows->iCount.ptr;
+  {
+    cyc::KernelTimer timer("k_kmeans_inc", st);
+    hipLaunchKernelGGL(k_inc_moved, dim3((unsigned)nb), dim3(256), 0, st, assign,
+                       (int32_t*)rows->iPrev.ptr, n, (int32_t*)rows->iTmpRow.ptr,
+                       (int32_t*)rows->iTmpOld.ptr, (unsigned int*)rows->iBcount.ptr);
+    CYC_LAUNCH_CHECK("k_inc_moved");
+    hipLaunchKernelGGL(k_inc_scan, dim3(1), dim3(1024), 0, st, (unsigned int*)rows->iBcount.ptr,
+                       nb, (unsigned int*)rows->iCount.ptr, valid, mcap, gate, cum);
+    CYC_LAUNCH_CHECK("k_inc_scan");
+    hipLaunchKernelGGL(k_inc_gather, dim3((unsigned)nb), dim3(256), 0, st,
+                       (const int32_t*)rows->iTmpRow.ptr, (const int32_t*)rows->iTmpOld.ptr,
+                       (const unsigned int*)rows->iBcount.ptr, (int32_t*)rows->iMovedRow.ptr,
+                       (int32_t*)rows->iMovedOld.ptr, (const int*)gate);
+    CYC_LAUNCH_CHECK("k_inc_gather");
+    int32_t* hist = (int32_t*)rows->iHist.ptr;
+    hipLaunchKernelGGL(k_inc_hist, dim3((unsigned)tilesE), dim3(256), sizeof(int32_t) * k, st,
+                       (const int32_t*)rows->iMovedRow.ptr, (const int32_t*)rows->iMovedOld.ptr,
+                       assign, cnt, k, hist, (const int*)gate);
+    CYC_LAUNCH_CHECK("k_inc_hist");
+    const int* g1 = gate + 1;
+    const int segT = (tilesE + std::min(kScanSegs, tilesE) - 1) / std::min(kScanSegs, tilesE);
+    const int segs = (tilesE + segT - 1) / segT;
+    int32_t* segsum = (int32_t*)rows->iSegsum.ptr;
+    hipLaunchKernelGGL(k_scan_seg, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0, st,
+                       (const int32_t*)hist, tilesE, k, segT, segsum, g1);
+    CYC_LAUNCH_CHECK("k_scan_seg");
+    hipLaunchKernelGGL(k_scan_segoff, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, st, segsum,
+                       segs, k, (int64_t*)rows->iTotal.ptr, g1);
+    CYC_LAUNCH_CHECK("k_scan_segoff");
+    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0,
+                       st, hist, tilesE, k, segT, (const int32_t*)segsum, g1);
+    CYC_LAUNCH_CHECK("k_scan_apply");
+    hipLaunchKernelGGL(k_scan_clusters, dim3(1), dim3(1024), 0, st,
+                       (const int64_t*)rows->iTotal.ptr, k, (int64_t*)rows->iCstart.ptr,
+                       (int64_t*)rows->iChunkStart.ptr, g1);
+    CYC_LAUNCH_CHECK("k_scan_clusters");
+    hipLaunchKernelGGL(k_inc_scatter, dim3((unsigned)tilesE), dim3(64), sizeof(int64_t) * k, st,
+                       (const int32_t*)rows->iMovedRow.ptr, (const int32_t*)rows->iMovedOld.ptr,
+                       assign, cnt, k, (const int32_t*)hist, (const int64_t*)rows->iCstart.ptr,
+                       (int32_t*)rows->iPerm.ptr, (int64_t)tilesE, (const int*)gate);
+    CYC_LAUNCH_CHECK("k_inc_scatter");
+#define CYC_IF(NJ)                                                                               \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_inc_fold<NJ>), dim3((unsigned)k), dim3(256), 0, st, X, d,  \
+                     xnorm, C, (const int32_t*)rows->iMovedRow.ptr, cnt,                        \
+                     (const int32_t*)rows->iPerm.ptr, (const int64_t*)rows->iCstart.ptr,        \
+                     (double*)rows->iS.ptr, (const double*)rows->iP.ptr, (double*)rows->iW.ptr,  \
+                     (double*)rows->iQ.ptr, (int64_t*)rows->iN.ptr, (double*)rows->iA.ptr,       \
+                     (double*)rows->iES.ptr, (double*)rows->iEQ.ptr, (double*)rows->iCost.ptr,   \
+                     (double*)rows->iErr.ptr, (int*)rows->iBad.ptr, (const int*)gate)
+    if (nj == 1) CYC_IF(1);
+    else if (nj == 2) CYC_IF(2);
+    else CYC_IF(4);
+#undef CYC_IF
+    CYC_LAUNCH_CHECK("k_inc_fold");
+    hipLaunchKernelGGL(k_inc_check, dim3(1), dim3(256), 0, st, (const double*)rows->iCost.ptr,
+                       (const double*)rows->iErr.ptr, (const int*)rows->iBad.ptr, k, gate,
+                       (double*)rows->iTot.ptr, cum + 1);
+    CYC_LAUNCH_CHECK("k_inc_check");
+  }
+  // the full pass (gate[0]): the counting sort, chunk sums, cluster folds,
+  // and the state reset from them
+  int64_t maxChunks = 0;
+  if ((rc = sort_clusters(p, assign, n, d, st, maxChunks, gate))) return rc;
+  if ((rc = rows->iPa.reserve(sizeof(double) * (size_t)maxChunks))) return rc;
+  {
+    cyc::KernelTimer timer("k_chunk_sums", st);
+#define CYC_CSF(NJ)                                                                              \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_chunk_sums_fast<NJ>), dim3((unsigned)maxChunks), dim3(256), 0, \
+                     st, X, d, (const double*)nullptr, C, (const int32_t*)p->perm.ptr,          \
+                     (const int64_t*)p->cstart.ptr, (const int64_t*)p->chunkStart.ptr, k,       \
+                     (double*)p->part.ptr, (double*)p->pw.ptr, (double*)p->pc.ptr, xnorm,        \
+                     (double*)rows->iPa.ptr, (const int*)gate)
+    if (nj == 1) CYC_CSF(1);
+    else if (nj == 2) CYC_CSF(2);
+    else CYC_CSF(4);
+#undef CYC_CSF
+    CYC_LAUNCH_CHECK("k_chunk_sums");
+  }
+  hipLaunchKernelGGL(k_reduce_clusters, dim3(k), dim3(256), 0, st, (const double*)p->part.ptr,
+                     (const double*)p->pw.ptr, (const double*)p->pc.ptr,
+                     (const int64_t*)p->chunkStart.ptr, d, sums, wsum, (double*)p->ccost.ptr,
+                     (const double*)rows->iPa.ptr, (double*)rows->iS.ptr, (double*)rows->iW.ptr,
+                     (double*)rows->iA.ptr, (const int*)gate);
+  CYC_LAUNCH_CHECK("k_reduce_clusters");
+  hipLaunchKernelGGL(k_cost_total, dim3(1), dim3(256), 0, st, (const double*)p->ccost.ptr, k,
+                     cost_sum, (const int*)gate);
+  CYC_LAUNCH_CHECK("k_cost_total");
+  hipLaunchKernelGGL(k_inc_reset, dim3(k), dim3(256), 0, st, C, d, (double*)rows->iP.ptr,
+                     (const double*)p->ccost.ptr, (const int64_t*)p->total.ptr,
+                     (const int64_t*)p->chunkStart.ptr, (double*)rows->iQ.ptr,
+                     (int64_t*)rows->iN.ptr, (const double*)rows->iA.ptr, (double*)rows->iES.ptr,
+                     (double*)rows->iEQ.ptr, (const int*)gate);
+  CYC_LAUNCH_CHECK("k_inc_reset");
+  hipLaunchKernelGGL(k_inc_emit, dim3(k), dim3(256), 0, st, (const double*)rows->iS.ptr,
+                     (const double*)rows->iW.ptr, d, (const double*)rows->iTot.ptr, sums, wsum,
+                     cost_sum, (const int*)gate);
+  CYC_LAUNCH_CHECK("k_inc_emit");
   return CYC_OK;
 }
 
@@ -2704,6 +3333,27 @@ int cyc_kmeans_rows_set_bounds(cyc_kmeans_rows rows, int32_t enable) {
   return CYC_OK;
 }
 
+int cyc_kmeans_rows_set_incremental(cyc_kmeans_rows rows, int32_t enable) {
+  CYC_REQUIRE(rows != nullptr, "rows must not be null");
+  rows->iEnabled = enable != 0;
+  rows->iValid = false;   // the next call runs the full pass
+  return CYC_OK;
+}
+
+int cyc_kmeans_rows_incremental_info(cyc_kmeans_rows rows, int64_t* incremental_calls,
+                                     int64_t* moved_rows) {
+  CYC_REQUIRE(rows != nullptr && incremental_calls != nullptr && moved_rows != nullptr,
+              "arguments must not be null");
+  unsigned long long cum[2] = {0, 0};
+  if (rows->iCum.ptr) {
+    CYC_HIP(hipDeviceSynchronize());
+    CYC_HIP(hipMemcpy(cum, rows->iCum.ptr, sizeof(cum), hipMemcpyDeviceToHost));
+  }
+  *incremental_calls = (int64_t)cum[1];
+  *moved_rows = (int64_t)cum[0];
+  return CYC_OK;
+}
+
 int cyc_kmeans_rows_bounds_rechecked(cyc_kmeans_rows rows, int64_t* rechecked_rows) {
   CYC_REQUIRE(rows != nullptr && rechecked_rows != nullptr, "arguments must not be null");
   unsigned long long cum = 0;
@@ -2875,9 +3525,21 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
                                hipMemcpyDeviceToDevice, st));
     }
   }
+  const int nj = (d + 255) / 256;
+  // incremental cluster sums (k_inc_*): with the carried bounds, unit
+  // weights and no per-row costs asked for
+  const bool useInc = useBnd && inc_on(rows) && !cost && !weights && nj <= 4;
+  if (rows && !useInc) rows->iValid = false;
+  if (useInc) {
+    if ((rc = inc_accumulate(p, rows, X, xnorm, assign, n, C, sums, wsum, cost_sum, st)))
+      return rc;
+    rc = require_check(p, n, approxNorm ? X : nullptr);
+    rows->iValid = rc == CYC_OK;
+    rows->ik = k;
+    return rc;
+  }
   // d > 1024: per-row costs first (k_chunk_sums fuses them for d <= 1024);
   // cosine: always (the cost is a ddot, summed per row)
-  const int nj = (d + 255) / 256;
   if (cosm) {
     if (!cost) {
       if ((rc = p->costTmp.reserve(sizeof(double) * (size_t)n))) return rc;
@@ -2918,7 +3580,8 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_chunk_sums_fast<NJ>), grid, dim3(256), 0, st, X, d, weights, \
                      C, (const int32_t*)p->perm.ptr, (const int64_t*)p->cstart.ptr,             \
                      (const int64_t*)p->chunkStart.ptr, k, (double*)p->part.ptr,                \
-                     (double*)p->pw.ptr, (double*)p->pc.ptr)
+                     (double*)p->pw.ptr, (double*)p->pc.ptr, (const double*)nullptr,             \
+                     (double*)nullptr, (const int*)nullptr)
     if (!cost && nj == 1) CYC_CSF(1);
     else if (!cost && nj == 2) CYC_CSF(2);
     else if (!cost && nj <= 4) CYC_CSF(4);
@@ -2936,10 +3599,12 @@ int cyc_kmeans_accumulate_dev(cyc_kmeans_plan p, const double* X, const double* 
   }
   hipLaunchKernelGGL(k_reduce_clusters, dim3(k), dim3(256), 0, st, (const double*)p->part.ptr,
                      (const double*)p->pw.ptr, (const double*)p->pc.ptr,
-                     (const int64_t*)p->chunkStart.ptr, d, sums, wsum, (double*)p->ccost.ptr);
+                     (const int64_t*)p->chunkStart.ptr, d, sums, wsum, (double*)p->ccost.ptr,
+                     (const double*)nullptr, (double*)nullptr, (double*)nullptr, (double*)nullptr,
+                     (const int*)nullptr);
   CYC_LAUNCH_CHECK("k_reduce_clusters");
   hipLaunchKernelGGL(k_cost_total, dim3(1), dim3(256), 0, st, (const double*)p->ccost.ptr, k,
-                     cost_sum);
+                     cost_sum, (const int*)nullptr);
   CYC_LAUNCH_CHECK("k_cost_total");
   return cosm ? cos_check(p) : require_check(p, n, approxNorm ? X : nullptr);
 }

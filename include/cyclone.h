@@ -139,6 +139,24 @@ int cyc_kmeans_rows_bounds_info(cyc_kmeans_rows rows, int64_t* calls, int64_t* s
  * the screen (and then also counted in screened_rows).  Synchronises. */
 int cyc_kmeans_rows_bounds_rechecked(cyc_kmeans_rows rows, int64_t* rechecked_rows);
 
+/* Incremental cluster sums across one fit's cyc_kmeans_accumulate_dev calls
+ * on these rows (round 6; on by default, CYC_KMEANS_INCR=0 turns the default
+ * off).  Applies with the carried bounds, weights == NULL and cost == NULL
+ * (no per-row costs).  The rows object keeps each cluster's sums, count and
+ * the sum of squared distances to a reference point.  A call whose moved rows
+ * are at most n / 8 updates them by those rows alone.  The cost for the call's
+ * centers then comes from Q + 2 (P - c).(S - W P) + W |P - c|^2, with its
+ * rounding bounded on the device.  A bound above 2^-42 of the cost, too many
+ * moved rows or no prior state run the full pass over every row (which resets
+ * the state).  The caller's buffers receive sums, weights and cost either way;
+ * the assignments are unaffected.  Replaces nothing in the reference: its
+ * KMeans.scala:287-306 re-sums every point.  enable = 0 drops the state. */
+int cyc_kmeans_rows_set_incremental(cyc_kmeans_rows rows, int32_t enable);
+/* Calls that took the incremental path, and the moved rows they folded, over
+ * the object's life.  Synchronises. */
+int cyc_kmeans_rows_incremental_info(cyc_kmeans_rows rows, int64_t* incremental_calls,
+                                     int64_t* moved_rows);
+
 /* findClosest(centers, stats, point) for n points (stats from the last
  * cyc_kmeans_stats_dev on this plan).  assign[n], cost[n] device outputs.
  * rows: NULL or the image of exactly these X, n.

@@ -916,10 +916,13 @@ def test_carried_bounds_scope(cuda):
 def test_full_config_late_iteration(cuda):
     """BASELINE config 2 on bench.py's rows, one fit from setInitialModel
     (rows 0..1023) as the bench and KMeans.run drive it: the carried bounds
-    on (the default), eleven Lloyd iterations, then the twelfth compared with
-    the restatement on the same centers for EVERY row (assignment and cost
-    bit for bit, weights exact, sums within 1e-10); by then the bounds let
-    most rows skip the screen."""
+    and the incremental cluster sums on (the defaults), eleven Lloyd
+    iterations without per-row costs, then the twelfth compared with the
+    restatement on the same centers for EVERY row: the sums, weights and cost
+    of the incremental call (sums within 1e-10, weights exact, cost within
+    1e-12), then the assignment and cost of every row bit for bit (a second
+    call with per-row costs on the same centers).  By then the bounds let most
+    rows skip the screen and the sums are carried."""
     import os
     import sys
     import torch
@@ -943,7 +946,7 @@ def test_full_config_late_iteration(cuda):
         sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
         wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
         cost = torch.zeros(1, dtype=torch.float64, device=cuda)
-        p.accumulate(X, xn, None, C, cn, sums, wsum, cost, a, pc, rows=rows)
+        p.accumulate(X, xn, None, C, cn, sums, wsum, cost, a, None, rows=rows)
         if it < last:
             p.update(C, cn, sums, wsum, 1e-4, conv)
     calls, after = rows.bounds_info()
@@ -951,6 +954,15 @@ def test_full_config_late_iteration(cuda):
     screened = after - before
     assert 0 < screened < n // 2, screened
     assert rows.bounds_rechecked() > 0      # carried candidate sets re-checked
+    inc_calls, moved = rows.incremental_info()
+    assert inc_calls >= 4, (inc_calls, moved)   # the late iterations fold moved rows only
+    a_inc = a.cpu().numpy()
+    # the same centers again with per-row costs (the full pass): every row's cost
+    s2 = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+    w2 = torch.zeros(k, dtype=torch.float64, device=cuda)
+    c2 = torch.zeros(1, dtype=torch.float64, device=cuda)
+    p.accumulate(X, xn, None, C, cn, s2, w2, c2, a, pc, rows=rows)
+    np.testing.assert_array_equal(a.cpu().numpy(), a_inc)
     del rows
     threads = min(int(os.environ.get("OMP_NUM_THREADS", "0")) or 16, os.cpu_count() or 1, 16)
     Xh = X.cpu().numpy()
@@ -963,6 +975,150 @@ def test_full_config_late_iteration(cuda):
     np.testing.assert_array_equal(wsum.cpu().numpy(), ref["wsum"])
     np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
                                atol=1e-10 * np.abs(ref["sums"]).max())
+    assert abs(cost.item() - ref["cost"]) <= 1e-12 * ref["cost"], (cost.item(), ref["cost"])
+    np.testing.assert_array_equal(w2.cpu().numpy(), ref["wsum"])
+    assert abs(c2.item() - ref["cost"]) <= 1e-12 * ref["cost"]
+
+
+def _lloyd_inc(Xd, Cd0, cuda, iters, inc, hook=None, check=()):
+    """`iters` Lloyd iterations through KMeansPlan.accumulate / update with
+    the carried bounds on, no per-row costs (the incremental sums' case),
+    incremental sums on or off; at the iterations in `check` the call is
+    compared with the restatement on the same centers (assign exact, weights
+    exact, sums within 1e-10, cost within 1e-12).  Returns the final
+    centers and (incremental calls, moved rows)."""
+    import torch
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    n, d = Xd.shape
+    k = Cd0.shape[0]
+    Cd = Cd0.clone()
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    p = KMeansPlan(d, k, n)
+    rows = p.rows(Xd)
+    rows.set_incremental(inc)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+    Xh = Xd.cpu().numpy() if check else None
+    for it in range(iters):
+        if hook:
+            hook(it, Cd, cn)
+        sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+        wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+        cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+        Ch = Cd.cpu().numpy()
+        p.accumulate(Xd, xn, None, Cd, cn, sums, wsum, cost, a, None, rows=rows)
+        if it in check:
+            ref = oracle.kmeans_iteration(Xh, oracle.row_norms(Xh), None, Ch,
+                                          oracle.row_norms(Ch), num_partitions=8, threads=8)
+            np.testing.assert_array_equal(a.cpu().numpy(), ref["assign"],
+                                          err_msg=f"assign, iteration {it}")
+            np.testing.assert_array_equal(wsum.cpu().numpy(), ref["wsum"],
+                                          err_msg=f"wsum, iteration {it}")
+            np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
+                                       atol=1e-10 * np.abs(ref["sums"]).max(),
+                                       err_msg=f"sums, iteration {it}")
+            assert abs(cost.item() - ref["cost"]) <= 1e-12 * ref["cost"], (it, cost.item(),
+                                                                          ref["cost"])
+        p.update(Cd, cn, sums, wsum, 1e-4, conv)
+    torch.cuda.synchronize()
+    return Cd, rows.incremental_info()
+
+
+@pytest.mark.parametrize("n,d,k,sep", [(200_000, 64, 128, 4.0), (120_000, 256, 1024, 3.0),
+                                       (150_000, 200, 300, 1.5), (60_000, 700, 40, 2.0)])
+def test_incremental_sums_fit(cuda, n, d, k, sep):
+    """Incremental cluster sums (cyclone.h cyc_kmeans_rows_set_incremental)
+    over a 14-iteration fit: every checked iteration equals the restatement
+    on the same centers (assignments and weights exactly, sums within 1e-10,
+    cost within 1e-12), most late iterations took the incremental path, and
+    the fit's centers stay within 1e-9 of the fit with the full pass every
+    iteration (d = 700 has no carried bounds: the full pass only)."""
+    rng = np.random.default_rng(n + d + k + 29)
+    true_c = rng.normal(scale=sep, size=(k, d))
+    X = true_c[rng.integers(0, k, n)] + rng.normal(size=(n, d))
+    Xd = _dev(X, cuda)
+    C0 = Xd[:k].clone()
+    C_on, (inc, moved) = _lloyd_inc(Xd, C0, cuda, 14, True, check=(0, 3, 7, 13))
+    C_off, (inc_off, _) = _lloyd_inc(Xd, C0, cuda, 14, False)
+    assert inc_off == 0
+    if d <= 256 and k > 96:
+        assert inc >= 6, (inc, moved)
+        assert moved > 0
+    else:
+        assert inc == 0
+    Con, Coff = C_on.cpu().numpy(), C_off.cpu().numpy()
+    np.testing.assert_allclose(Con, Coff, rtol=1e-9, atol=1e-9 * np.abs(Coff).max())
+
+
+def test_incremental_sums_edge_cases(cuda):
+    """The incremental state under the caller's hand: a center thrown far
+    away (the correction term's bound fails: the full pass), a center
+    duplicated (its copy empties: weight exactly 0, the centroid not
+    updated), a cluster emptied and refilled, the incremental switch toggled
+    mid-fit, and a NaN center for one call (the reference's require; the
+    next call starts over) -- every call equal to the restatement."""
+    import torch
+    from cycloneml_amd import _native as N
+    n, d, k = 60_000, 64, 130
+    rng = np.random.default_rng(17)
+    true_c = rng.normal(scale=3.0, size=(k, d))
+    X = true_c[rng.integers(0, k, n)] + rng.normal(size=(n, d))
+    Xd = _dev(X, cuda)
+    state = {}
+
+    def hook(it, Cd, cn):
+        from cycloneml_amd.clustering import row_norms
+        if it == 5:
+            Cd[7] += 50.0                       # far away: its rows leave
+        elif it == 7:
+            Cd[11] = Cd[12]                     # a duplicate: 12 empties
+        elif it == 9:
+            Cd[7] = Xd[3]                       # back among the rows
+        cn.copy_(row_norms(Cd))
+        state["it"] = it
+
+    _, (inc, moved) = _lloyd_inc(Xd, Xd[:k].clone(), cuda, 13, True, hook=hook,
+                                 check=tuple(range(13)))
+    assert inc >= 4, (inc, moved)
+    # toggling drops the state; a NaN center raises and the next call is full
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    p = KMeansPlan(d, k, n)
+    rows = p.rows(Xd)
+    C = Xd[:k].clone()
+    cn = row_norms(C)
+    xn = row_norms(Xd)
+    a = torch.empty(n, dtype=torch.int32, device=cuda)
+    conv = torch.zeros(1, dtype=torch.int32, device=cuda)
+    Xh = X
+    for it in range(8):
+        if it == 3:
+            rows.set_incremental(False)
+        if it == 4:
+            rows.set_incremental(True)
+        Cs = C.clone()
+        if it == 5:
+            Cs[2, 0] = float("nan")
+            with pytest.raises(N.IllegalArgumentException):
+                s0 = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+                p.accumulate(Xd, xn, None, Cs, row_norms(Cs), s0,
+                             torch.zeros(k, dtype=torch.float64, device=cuda),
+                             torch.zeros(1, dtype=torch.float64, device=cuda), a, None, rows=rows)
+            torch.cuda.synchronize()
+            continue
+        sums = torch.zeros(k * d, dtype=torch.float64, device=cuda)
+        wsum = torch.zeros(k, dtype=torch.float64, device=cuda)
+        cost = torch.zeros(1, dtype=torch.float64, device=cuda)
+        p.accumulate(Xd, xn, None, C, cn, sums, wsum, cost, a, None, rows=rows)
+        Ch = C.cpu().numpy()
+        ref = oracle.kmeans_iteration(Xh, oracle.row_norms(Xh), None, Ch, oracle.row_norms(Ch),
+                                      num_partitions=8, threads=8)
+        np.testing.assert_array_equal(a.cpu().numpy(), ref["assign"])
+        np.testing.assert_array_equal(wsum.cpu().numpy(), ref["wsum"])
+        np.testing.assert_allclose(sums.cpu().numpy().reshape(k, d), ref["sums"], rtol=1e-10,
+                                   atol=1e-10 * np.abs(ref["sums"]).max())
+        assert abs(cost.item() - ref["cost"]) <= 1e-12 * ref["cost"]
+        p.update(C, cn, sums, wsum, 1e-4, conv)
+    assert rows.incremental_info()[0] >= 1
 
 
 @pytest.mark.parametrize("n,d,k,dup", [(60_000, 64, 130, True), (40_000, 256, 1024, False),
