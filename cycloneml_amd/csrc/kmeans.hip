@@ -1661,7 +1661,8 @@ __global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __
 // P_c (the centers of the last full pass) with Q_c = sum |x - P_c|^2 over the
 // members, and A_c = sum |x| (error scale).  A call with few moved rows
 // (<= n / kIncMovedFrac) updates them by the moved rows alone (subtracted
-// from the old cluster, added to the new, in row order) and takes the cost
+// from the old cluster, added to the new, in row order: each cluster's
+// workgroup picks its entries from the row-ordered moved list) and takes the cost
 // for the call's centers c from
 //   sum_x |x - c|^2 = Q_c + 2 (P_c - c).(S_c - W_c P_c) + W_c |P_c - c|^2,
 // which is exact algebra; the rounding of every term is bounded on the device
@@ -1671,7 +1672,7 @@ __global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __
 // k_chunk_sums_fast), which resets the state.  Gates: gate[0] = 1 runs the
 // full pass, gate[1] = 1 the incremental one; exactly one is set.
 constexpr int kIncRows = 2048;       // rows per k_inc_moved workgroup
-constexpr int kIncMovedFrac = 8;     // at most n / 8 moved rows take the incremental path
+constexpr int kIncMovedFrac = 16;    // at most n / 16 moved rows take the incremental path
 
 // The rows whose assignment differs from prev (then prev = assign): per
 // kIncRows-row block, in row order, into tmpRow / tmpOld at the block's base;
@@ -1758,87 +1759,24 @@ __global__ __launch_bounds__(1024) void k_inc_scan(unsigned int* __restrict__ bc
   }
 }
 
-// The blocks' moved rows behind their offsets (incremental path only).
+// The blocks' moved rows behind their offsets, with their new and old
+// clusters (incremental path only).
 __global__ __launch_bounds__(256) void k_inc_gather(const int32_t* __restrict__ tmpRow,
                                                     const int32_t* __restrict__ tmpOld,
                                                     const unsigned int* __restrict__ bcount,
+                                                    const int32_t* __restrict__ assign,
                                                     int32_t* __restrict__ movedRow,
+                                                    int32_t* __restrict__ movedNew,
                                                     int32_t* __restrict__ movedOld,
                                                     const int* __restrict__ gate) {
   if (!gate[1]) return;
   const int64_t b = blockIdx.x, base = b * kIncRows;
   const unsigned off = bcount[b], cnt = bcount[b + 1] - off;
   for (unsigned i = threadIdx.x; i < cnt; i += 256) {
-    movedRow[off + i] = tmpRow[base + i];
+    const int32_t r = tmpRow[base + i];
+    movedRow[off + i] = r;
+    movedNew[off + i] = assign[r];
     movedOld[off + i] = tmpOld[base + i];
-  }
-}
-
-// Entries of the delta: e < m adds moved row e to its new cluster, e in
-// [m, 2m) subtracts moved row e - m from its old one.
-__device__ __forceinline__ int inc_key(int64_t e, unsigned m, const int32_t* __restrict__ movedRow,
-                                       const int32_t* __restrict__ movedOld,
-                                       const int32_t* __restrict__ assign) {
-  return e < (int64_t)m ? assign[movedRow[e]] : movedOld[e - m];
-}
-
-// Counting sort of the 2m entries by cluster (stable: entry order kept), in
-// kSortTile-entry tiles like k_hist / k_scatter; tiles past 2m hold zeros.
-__global__ void k_inc_hist(const int32_t* __restrict__ movedRow,
-                           const int32_t* __restrict__ movedOld,
-                           const int32_t* __restrict__ assign, const unsigned int* __restrict__ count,
-                           int k, int32_t* __restrict__ hist, const int* __restrict__ gate) {
-  if (!gate[1]) return;
-  extern __shared__ int32_t cnt[];
-  for (int c = threadIdx.x; c < k; c += blockDim.x) cnt[c] = 0;
-  __syncthreads();
-  const unsigned m = *count;
-  const int64_t E = 2 * (int64_t)m;
-  const int64_t e0 = (int64_t)blockIdx.x * kSortTile, e1 = min<int64_t>(E, e0 + kSortTile);
-  for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x)
-    atomicAdd(&cnt[inc_key(e, m, movedRow, movedOld, assign)], 1);
-  __syncthreads();
-  for (int c = threadIdx.x; c < k; c += blockDim.x) hist[(int64_t)blockIdx.x * k + c] = cnt[c];
-}
-
-__global__ void k_inc_scatter(const int32_t* __restrict__ movedRow,
-                              const int32_t* __restrict__ movedOld,
-                              const int32_t* __restrict__ assign,
-                              const unsigned int* __restrict__ count, int k,
-                              const int32_t* __restrict__ tileOff, const int64_t* __restrict__ cstart,
-                              int32_t* __restrict__ eperm, int64_t tiles,
-                              const int* __restrict__ gate) {
-  if (!gate[1]) return;
-  extern __shared__ int64_t pos[];
-  const int64_t tile = blockIdx.x;
-  if (tile >= tiles) return;
-  const unsigned m = *count;
-  const int64_t E = 2 * (int64_t)m;
-  const int64_t e0 = tile * kSortTile;
-  if (e0 >= E) return;
-  const int lane = threadIdx.x;
-  const int kb = 32 - __builtin_clz((unsigned)max(k - 1, 1));
-  for (int c = lane; c < k; c += 64) pos[c] = cstart[c] + tileOff[tile * k + c];
-  __syncthreads();
-  const int64_t e1 = min<int64_t>(E, e0 + kSortTile);
-  for (int64_t b = e0; b < e1; b += 64) {
-    const int64_t e = b + lane;
-    const int c = e < e1 ? inc_key(e, m, movedRow, movedOld, assign) : -1;
-    unsigned long long msk = __ballot(c >= 0);
-    for (int q = 0; q < kb; ++q) {
-      const bool bit = (c >> q) & 1;
-      const unsigned long long bal = __ballot(bit);
-      msk &= bit ? bal : ~bal;
-    }
-    const int prior = __popcll(msk & ((1ull << lane) - 1));
-    const int last = 63 - __clzll(msk);
-    const int64_t p = (c >= 0) ? pos[c] + prior : 0;
-    __builtin_amdgcn_wave_barrier();
-    if (c >= 0) {
-      eperm[p] = (int32_t)e;
-      if (last == lane) pos[c] = p + 1;
-    }
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1861,28 +1799,32 @@ __device__ __forceinline__ void inc_block_sum(double (&v)[NV], double* red) {
   for (int i = 0; i < NV; ++i) v[i] = red[i * 256];
 }
 
-// One workgroup per cluster: fold the cluster's entries (in order) into its
-// state, then its cost for the call's centers C and the bound of that cost's
+// One workgroup per cluster: its entries (the moved rows that left or joined
+// it) picked from the moved list in list order -- kIncScan entries per
+// thread per step, compacted in order through LDS -- folded into its state;
+// then its cost for the call's centers C and the bound of that cost's
 // rounding (cerr), cbad = 1 when the state's error grew past 2^-38 of the
 // sum of the members' norms.  Unit weights only.
+constexpr int kIncScan = 8;
 template <int NJ>
 __global__ __launch_bounds__(256) void k_inc_fold(
     const double* __restrict__ X, int d, const double* __restrict__ xnorm,
     const double* __restrict__ C, const int32_t* __restrict__ movedRow,
-    const unsigned int* __restrict__ count, const int32_t* __restrict__ eperm,
-    const int64_t* __restrict__ ecstart, double* __restrict__ S, const double* __restrict__ P,
+    const int32_t* __restrict__ movedNew, const int32_t* __restrict__ movedOld,
+    const unsigned int* __restrict__ count, double* __restrict__ S, const double* __restrict__ P,
     double* __restrict__ W, double* __restrict__ Q, int64_t* __restrict__ N,
     double* __restrict__ A, double* __restrict__ ES, double* __restrict__ EQ,
     double* __restrict__ ccost, double* __restrict__ cerr, int* __restrict__ cbad,
     const int* __restrict__ gate) {
   if (!gate[1]) return;
-  __shared__ int32_t rowsS[256];
-  __shared__ double sgS[256];
+  constexpr int B = 256 * kIncScan;
+  __shared__ int32_t rowsS[B];
+  __shared__ float sgS[B];
+  __shared__ unsigned wcS[kIncScan * 4];
   __shared__ double red[5 * 256];
-  const int c = blockIdx.x, tid = threadIdx.x;
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const unsigned m = *count;
-  const int64_t e0 = ecstart[c], e1 = ecstart[c + 1];
-  const int64_t ent = e1 - e0;
+  int64_t ent = 0;
   double ds[NJ], dq[NJ], dqa[NJ], pj[NJ];
 #pragma unroll
   for (int u = 0; u < NJ; ++u) {
@@ -1891,21 +1833,44 @@ __global__ __launch_bounds__(256) void k_inc_fold(
     pj[u] = j < d ? P[(int64_t)c * d + j] : 0.0;
   }
   double tN = 0.0, tA = 0.0, tAbs = 0.0;   // this thread's entries: count, sum |x|
-  for (int64_t b0 = e0; b0 < e1; b0 += 256) {
-    const int cnt = (int)min<int64_t>(256, e1 - b0);
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (unsigned base = 0; base < m; base += B) {
+    int nw[kIncScan], ol[kIncScan];
+#pragma unroll
+    for (int q = 0; q < kIncScan; ++q) {
+      const unsigned i = base + q * 256 + tid;
+      nw[q] = i < m ? movedNew[i] : -1;
+      ol[q] = i < m ? movedOld[i] : -1;
+    }
+    unsigned long long mk[kIncScan];
+    __syncthreads();   // the previous batch's entries are folded
+#pragma unroll
+    for (int q = 0; q < kIncScan; ++q) {
+      mk[q] = __builtin_amdgcn_ballot_w64(nw[q] == c || ol[q] == c);
+      if (lane == 0) wcS[q * 4 + wave] = (unsigned)__builtin_popcountll(mk[q]);
+    }
     __syncthreads();
-    if (tid < cnt) {
-      const int64_t e = eperm[b0 + tid];
-      const bool add = e < (int64_t)m;
-      const int32_t r = add ? movedRow[e] : movedRow[e - m];
-      rowsS[tid] = r;
-      sgS[tid] = add ? 1.0 : -1.0;
-      const double xn = xnorm[r];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < kIncScan; ++q) {
+      unsigned before = 0;
+      for (int j = 0; j < q * 4 + wave; ++j) before += wcS[j];
+      if ((mk[q] >> lane) & 1ull) {
+        const unsigned pos = before + (unsigned)__builtin_popcountll(mk[q] & below);
+        rowsS[pos] = movedRow[base + q * 256 + tid];
+        sgS[pos] = nw[q] == c ? 1.0f : -1.0f;
+      }
+    }
+    for (int j = 0; j < kIncScan * 4; ++j) cnt += (int)wcS[j];
+    __syncthreads();
+    ent += cnt;
+    for (int e = tid; e < cnt; e += 256) {
+      const bool add = sgS[e] > 0.0f;
+      const double xn = xnorm[rowsS[e]];
       tN += add ? 1.0 : -1.0;
       tA = add ? dadd(tA, xn) : dsub(tA, xn);
       tAbs = dadd(tAbs, xn);
     }
-    __syncthreads();
     for (int p0 = 0; p0 < cnt; p0 += 8) {
       double xv[8][NJ];
 #pragma unroll
@@ -1920,7 +1885,7 @@ __global__ __launch_bounds__(256) void k_inc_fold(
 #pragma unroll
       for (int v = 0; v < 8; ++v) {
         if (p0 + v < cnt) {
-          const bool add = sgS[p0 + v] > 0.0;
+          const bool add = sgS[p0 + v] > 0.0f;
 #pragma unroll
           for (int u = 0; u < NJ; ++u) {
             const double x = xv[v][u];
@@ -2338,9 +2303,8 @@ struct cyc_kmeans_rows_s {
   bool iEnabled = true;    // cyc_kmeans_rows_set_incremental (CYC_KMEANS_INCR=0: off)
   bool iValid = false;
   int ik = 0;
-  cyc::DeviceBuffer iPrev, iTmpRow, iTmpOld, iBcount, iCount, iGate, iMovedRow, iMovedOld, iHist,
-      iSegsum, iTotal, iCstart, iChunkStart, iPerm, iS, iP, iW, iQ, iN, iA, iES, iEQ, iCost, iErr,
-      iBad, iTot, iCum, iPa;
+  cyc::DeviceBuffer iPrev, iTmpRow, iTmpOld, iBcount, iCount, iGate, iMovedRow, iMovedNew,
+      iMovedOld, iS, iP, iW, iQ, iN, iA, iES, iEQ, iCost, iErr, iBad, iTot, iCum, iPa;
 };
 
 namespace {
@@ -2940,7 +2904,6 @@ int inc_accumulate(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* X,
   const int k = p->k, d = p->d, nj = (d + 255) / 256;
   const int64_t nb = (n + kIncRows - 1) / kIncRows;
   const int64_t mcap = n / kIncMovedFrac;
-  const int tilesE = (int)std::max<int64_t>(1, (2 * mcap + kSortTile - 1) / kSortTile);
   const size_t kd = (size_t)k * d;
   int rc;
   const bool fresh = rows->iPrev.ptr == nullptr;
@@ -2950,13 +2913,8 @@ int inc_accumulate(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* X,
       (rc = rows->iBcount.reserve(sizeof(unsigned int) * (size_t)(nb + 1))) ||
       (rc = rows->iCount.reserve(64)) || (rc = rows->iGate.reserve(64)) ||
       (rc = rows->iMovedRow.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(mcap, 1))) ||
+      (rc = rows->iMovedNew.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(mcap, 1))) ||
       (rc = rows->iMovedOld.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(mcap, 1))) ||
-      (rc = rows->iHist.reserve(sizeof(int32_t) * (size_t)tilesE * k)) ||
-      (rc = rows->iSegsum.reserve(sizeof(int32_t) * (size_t)kScanSegs * k)) ||
-      (rc = rows->iTotal.reserve(sizeof(int64_t) * (size_t)k)) ||
-      (rc = rows->iCstart.reserve(sizeof(int64_t) * (size_t)(k + 1))) ||
-      (rc = rows->iChunkStart.reserve(sizeof(int64_t) * (size_t)(k + 1))) ||
-      (rc = rows->iPerm.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(2 * mcap, 1))) ||
       (rc = rows->iS.reserve(sizeof(double) * kd)) || (rc = rows->iP.reserve(sizeof(double) * kd)) ||
       (rc = rows->iW.reserve(sizeof(double) * (size_t)k)) ||
       (rc = rows->iQ.reserve(sizeof(double) * (size_t)k)) ||
@@ -2989,41 +2947,15 @@ int inc_accumulate(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* X,
     CYC_LAUNCH_CHECK("k_inc_scan");
     hipLaunchKernelGGL(k_inc_gather, dim3((unsigned)nb), dim3(256), 0, st,
                        (const int32_t*)rows->iTmpRow.ptr, (const int32_t*)rows->iTmpOld.ptr,
-                       (const unsigned int*)rows->iBcount.ptr, (int32_t*)rows->iMovedRow.ptr,
+                       (const unsigned int*)rows->iBcount.ptr, assign,
+                       (int32_t*)rows->iMovedRow.ptr, (int32_t*)rows->iMovedNew.ptr,
                        (int32_t*)rows->iMovedOld.ptr, (const int*)gate);
     CYC_LAUNCH_CHECK("k_inc_gather");
-    int32_t* hist = (int32_t*)rows->iHist.ptr;
-    hipLaunchKernelGGL(k_inc_hist, dim3((unsigned)tilesE), dim3(256), sizeof(int32_t) * k, st,
-                       (const int32_t*)rows->iMovedRow.ptr, (const int32_t*)rows->iMovedOld.ptr,
-                       assign, cnt, k, hist, (const int*)gate);
-    CYC_LAUNCH_CHECK("k_inc_hist");
-    const int* g1 = gate + 1;
-    const int segT = (tilesE + std::min(kScanSegs, tilesE) - 1) / std::min(kScanSegs, tilesE);
-    const int segs = (tilesE + segT - 1) / segT;
-    int32_t* segsum = (int32_t*)rows->iSegsum.ptr;
-    hipLaunchKernelGGL(k_scan_seg, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0, st,
-                       (const int32_t*)hist, tilesE, k, segT, segsum, g1);
-    CYC_LAUNCH_CHECK("k_scan_seg");
-    hipLaunchKernelGGL(k_scan_segoff, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, st, segsum,
-                       segs, k, (int64_t*)rows->iTotal.ptr, g1);
-    CYC_LAUNCH_CHECK("k_scan_segoff");
-    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)((k + 63) / 64), (unsigned)segs), dim3(64), 0,
-                       st, hist, tilesE, k, segT, (const int32_t*)segsum, g1);
-    CYC_LAUNCH_CHECK("k_scan_apply");
-    hipLaunchKernelGGL(k_scan_clusters, dim3(1), dim3(1024), 0, st,
-                       (const int64_t*)rows->iTotal.ptr, k, (int64_t*)rows->iCstart.ptr,
-                       (int64_t*)rows->iChunkStart.ptr, g1);
-    CYC_LAUNCH_CHECK("k_scan_clusters");
-    hipLaunchKernelGGL(k_inc_scatter, dim3((unsigned)tilesE), dim3(64), sizeof(int64_t) * k, st,
-                       (const int32_t*)rows->iMovedRow.ptr, (const int32_t*)rows->iMovedOld.ptr,
-                       assign, cnt, k, (const int32_t*)hist, (const int64_t*)rows->iCstart.ptr,
-                       (int32_t*)rows->iPerm.ptr, (int64_t)tilesE, (const int*)gate);
-    CYC_LAUNCH_CHECK("k_inc_scatter");
 #define CYC_IF(NJ)                                                                               \
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_inc_fold<NJ>), dim3((unsigned)k), dim3(256), 0, st, X, d,  \
-                     xnorm, C, (const int32_t*)rows->iMovedRow.ptr, cnt,                        \
-                     (const int32_t*)rows->iPerm.ptr, (const int64_t*)rows->iCstart.ptr,        \
-                     (double*)rows->iS.ptr, (const double*)rows->iP.ptr, (double*)rows->iW.ptr,  \
+                     xnorm, C, (const int32_t*)rows->iMovedRow.ptr,                             \
+                     (const int32_t*)rows->iMovedNew.ptr, (const int32_t*)rows->iMovedOld.ptr,   \
+                     cnt, (double*)rows->iS.ptr, (const double*)rows->iP.ptr, (double*)rows->iW.ptr,  \
                      (double*)rows->iQ.ptr, (int64_t*)rows->iN.ptr, (double*)rows->iA.ptr,       \
                      (double*)rows->iES.ptr, (double*)rows->iEQ.ptr, (double*)rows->iCost.ptr,   \
                      (double*)rows->iErr.ptr, (int*)rows->iBad.ptr, (const int*)gate)

@@ -2013,6 +2013,9 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     outCount += sh * kShardStride;
   }
   const CenterParams P = *prm;
+  const auto cR = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)Cr, (short)0, (int)std::min<int64_t>((int64_t)P.k * 3 * P16 * PB, 0x7fffffff),
+      0x00020000);
   for (unsigned base = w0 * RPW; base < cnt; base += nw * RPW) {
     const unsigned idx = base + q;
     const bool live = idx < cnt;
@@ -2023,12 +2026,42 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
       ci[i] = live ? cands[(size_t)(RC ? row : (int64_t)idx) * kCandMax + i] : -1;
     const Pc* xr = (const Pc*)Xq + row * (3 * P16) + li;
     const Pc xa = xr[0], xb = xr[P16], xc = xr[2 * P16];
+    // the row's and the candidates' scalars issued with the gathers (each
+    // one waited for on its own after them cost a round trip apiece)
+    const int2 mt = live ? meta[row] : make_int2(INT_MIN, 0);
+    const double xnr = xnorm[row];
+    float cqv[kCandMax];
+#pragma unroll
+    for (int i = 0; i < kCandMax; ++i) cqv[i] = cq[(ci[i] >= 0 && ci[i] < P.k) ? ci[i] : 0];
+    float lncR = 0.0f;
+    float2 bndR = make_float2(0.0f, 0.0f);
+    if (bnd) {
+      if (RC) lncR = lncA[row];
+      else bndR = bnd[row];
+    }
     int s1[kCandMax], s2[kCandMax], s3[kCandMax];
 #pragma unroll
     for (int i = 0; i < kCandMax; ++i) {
       const int c = ci[i];
-      const Pc* cr = (const Pc*)Cr + (size_t)((c >= 0 && c < P.k) ? c : 0) * (3 * P16) + li;
-      const Pc ca = cr[0], cb = cr[P16], cc = cr[2 * P16];
+      Pc ca, cb, cc;
+      if constexpr (PB == 16) {
+        // empty slots fetch nothing: an out-of-range buffer offset reads
+        // zeros without a memory access (the kernel is bound by these L2
+        // gathers, 768 B per candidate), and every slot's loads stay in
+        // flight together
+        const unsigned off = (c >= 0 && c < P.k) ? (unsigned)(c * 3 * P16 + li) * 16u
+                                                 : 0x80000000u;
+        ca = __builtin_bit_cast(Pc, __builtin_amdgcn_raw_buffer_load_b128(cR, (int)off, 0, 0));
+        cb = __builtin_bit_cast(Pc, __builtin_amdgcn_raw_buffer_load_b128(
+                                        cR, (int)(off + 16u * P16), 0, 0));
+        cc = __builtin_bit_cast(Pc, __builtin_amdgcn_raw_buffer_load_b128(
+                                        cR, (int)(off + 32u * P16), 0, 0));
+      } else {
+        const Pc* cr = (const Pc*)Cr + (size_t)((c >= 0 && c < P.k) ? c : 0) * (3 * P16) + li;
+        ca = cr[0];
+        cb = cr[P16];
+        cc = cr[2 * P16];
+      }
       s1[i] = dot16(xa, ca, 0);
       s2[i] = dot16(xb, ca, dot16(xa, cb, 0));
       s3[i] = dot16(xc, ca, dot16(xb, cb, dot16(xa, cc, 0)));
@@ -2052,7 +2085,6 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
           s3[i] += __shfl_xor(s3[i], m);
         }
     }
-    const int2 mt = live ? meta[row] : make_int2(INT_MIN, 0);
     // the three-limb pass's bounds: T = S1 2^7 + S2, V = T + S3 2^-7 and L =
     // cq - F1 V in f32 rounded toward -inf (lower bounds), F1 = 2^(ex + ec - 20)
     __builtin_amdgcn_s_setreg(0x801, 2);
@@ -2068,8 +2100,8 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
       if (c < 0 || c >= P.k) continue;
       const int T = s1[i] * 128 + s2[i];
       const float V = __builtin_fmaf((float)s3[i], 0x1p-7f, (float)T);
-      const float L = __builtin_fmaf(-F1, V, cq[c]);
-      cqMax = __builtin_fmaxf(cqMax, __builtin_fabsf(cq[c]));
+      const float L = __builtin_fmaf(-F1, V, cqv[i]);
+      cqMax = __builtin_fmaxf(cqMax, __builtin_fabsf(cqv[i]));
       const bool lt = L < L1;
       L2 = __builtin_amdgcn_fmed3f(L1, L2, L);
       I1 = lt ? c : I1;
@@ -2079,12 +2111,13 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     bool decided = false;
     const double l1 = (double)L1, l2 = (double)L2;
     if (live && P.ok && !bad && mt.x != INT_MIN && I1 >= 0 && __builtin_isfinite(l1)) {
-      const double xn = xnorm[row], cn = cnorm[I1];
+      const double xn = xnr, cn = cnorm[I1];
+      const double gw = g[I1];
       const double xx = xn * xn, cc = cn * cn;
       const double n1 = (double)__int_as_float(mt.y);   // bounds |xh3|_1
       const double fx = err_term(mt.x, n1, P.mu, d);
-      const double M = (4.0 * (fx + g[I1]) + 2.0 * kEpsF * (xx + cc) +
-                        0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * g[I1]) +
+      const double M = (4.0 * (fx + gw) + 2.0 * kEpsF * (xx + cc) +
+                        0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * gw) +
                         0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
                                    __builtin_fmin(__builtin_fabs(l2), 0x1p120)) +
                         0x1p-90) *
@@ -2095,9 +2128,9 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
         // rounded down after a rounded-down V: slack 2^-20 max |cq|), the
         // centers outside the set below the earlier tiers' bound (RC: the
         // set's carried bound)
-        const float lnc0 = RC ? lncA[row] : bnd[row].y;
-        const bool mark = RC || bnd[row].x == -2.0f;
-        const double ub2 = bnd_ub_sq(xx, cc, l1, fx, g[I1], 0.0) + 0x1p-20 * (double)cqMax;
+        const float lnc0 = RC ? lncR : bndR.y;
+        const bool mark = RC || bndR.x == -2.0f;
+        const double ub2 = bnd_ub_sq(xx, cc, l1, fx, gw, 0.0) + 0x1p-20 * (double)cqMax;
         if (RC && decided) {
           // every center outside the set: |x - c| >= lnc0, above the winner
           // by the reference's slack (the filter's test)
@@ -2169,45 +2202,65 @@ int launch_cands(const CandArgs& ca, int64_t n, int d, int32_t* assign, int32_t*
   return CYC_OK;
 }
 
-// Sharded appends, compacted (kmeans_i8.hpp): one wave scans the kShards
-// counters into bases behind *dstCount (and clears them), then a grid copies
-// each shard's entries to its base.
-__global__ __launch_bounds__(64) void k_shard_scan(unsigned int* __restrict__ counts,
-                                                   unsigned int* __restrict__ dstCount) {
-  const int j = threadIdx.x;
-  const unsigned c = counts[j * kShardStride];
-  unsigned incl = c;
-#pragma unroll
-  for (int m = 1; m < kShards; m <<= 1) {
-    const unsigned o = __shfl_up(incl, m);
-    if (j >= m) incl += o;
-  }
-  const unsigned old = *dstCount;   // read by every lane before lane 63's store
-  counts[j * kShardStride] = 0u;
-  counts[j * kShardStride + 1] = old + incl - c;
-  counts[j * kShardStride + 2] = c;
-  if (j == kShards - 1) *dstCount = old + incl;
-}
-
-__global__ __launch_bounds__(256) void k_shard_copy(const unsigned int* __restrict__ counts,
-                                                    unsigned int cap,
-                                                    const int32_t* __restrict__ src,
-                                                    int32_t* __restrict__ dst, int width,
-                                                    const int32_t* __restrict__ src2,
-                                                    int32_t* __restrict__ dst2, int width2) {
+// Sharded appends, compacted (kmeans_i8.hpp) in ONE launch: every block's
+// first wave scans the kShards counters (64 values) for its shard's base
+// behind *dstCount, the block copies that shard's entries there, and the last
+// block to finish (a completion counter in shard 0's spare slot) clears the
+// counters and advances *dstCount.  (A scan launch + a copy launch took ~5
+// us each, nine pairs per screen call.)
+__global__ __launch_bounds__(256) void k_shard_compact(unsigned int* __restrict__ counts,
+                                                       unsigned int cap,
+                                                       const int32_t* __restrict__ src,
+                                                       int32_t* __restrict__ dst, int width,
+                                                       const int32_t* __restrict__ src2,
+                                                       int32_t* __restrict__ dst2, int width2,
+                                                       unsigned int* __restrict__ dstCount) {
+  __shared__ unsigned sb[2];
   const int j = blockIdx.y;
-  const size_t base = counts[j * kShardStride + 1], c = counts[j * kShardStride + 2];
-  const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  {
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
+    const unsigned c = counts[l * kShardStride];
+    unsigned incl = c;
+#pragma unroll
+    for (int m = 1; m < kShards; m <<= 1) {
+      const unsigned o = __shfl_up(incl, m);
+      if (l >= m) incl += o;
+    }
+    if (l == j) {
+      sb[0] = incl - c;
+      sb[1] = c;
+    }
+  }
+  const unsigned old = *dstCount;   // advanced only by the last block
+  __syncthreads();
+  if (dst) {
+    const size_t base = (size_t)old + sb[0], c = sb[1];
+    const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
     const int32_t* s1 = src + (size_t)j * cap * width;
     int32_t* d1 = dst + base * width;
     for (size_t i = t0; i < c * width; i += stride) d1[i] = s1[i];
+    if (src2) {
+      const int32_t* s2 = src2 + (size_t)j * cap * width2;
+      int32_t* d2 = dst2 + base * width2;
+      for (size_t i = t0; i < c * width2; i += stride) d2[i] = s2[i];
+    }
   }
-  if (src2) {
-    const int32_t* s2 = src2 + (size_t)j * cap * width2;
-    int32_t* d2 = dst2 + base * width2;
-    for (size_t i = t0; i < c * width2; i += stride) d2[i] = s2[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned blocks = gridDim.x * gridDim.y;
+    if (atomicAdd(&counts[3], 1u) == blocks - 1) {
+      // every block has read the counters and *dstCount
+      __threadfence();
+      unsigned tot = 0;
+      for (int l = 0; l < kShards; ++l) {
+        tot += counts[l * kShardStride];
+        counts[l * kShardStride] = 0u;
+      }
+      *dstCount = old + tot;
+      counts[3] = 0u;
+    }
   }
 }
 
@@ -2215,13 +2268,11 @@ int compact(unsigned int* counts, unsigned int cap, const int32_t* src, int32_t*
             const int32_t* src2, int32_t* dst2, int width2, unsigned int* dstCount,
             hipStream_t st) {
   KernelTimer timer("k_kmeans_compact", st);
-  hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kShards), 0, st, counts, dstCount);
-  CYC_LAUNCH_CHECK("k_shard_scan");
-  if (dst) {
-    hipLaunchKernelGGL(k_shard_copy, dim3(16, kShards), dim3(256), 0, st,
-                       (const unsigned int*)counts, cap, src, dst, width, src2, dst2, width2);
-    CYC_LAUNCH_CHECK("k_shard_copy");
-  }
+  // two blocks per shard: the completion counter's returning atomics
+  // serialise (~11 ns each), 16 per shard measured 3x the two launches
+  hipLaunchKernelGGL(k_shard_compact, dst ? dim3(2, kShards) : dim3(1, 1), dim3(256), 0, st,
+                     counts, cap, src, dst, width, src2, dst2, width2, dstCount);
+  CYC_LAUNCH_CHECK("k_shard_compact");
   return CYC_OK;
 }
 
@@ -2581,8 +2632,10 @@ __global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict
       if (okA && b.x >= 0.0f && b.y > 0.0f) {
         const double U = (double)b.x + delta[a];
         const double L = (double)b.y - (a == P.i1 ? P.d2 : P.d1);
-        const double xn = xnorm[r];
-        const double xx = xn * xn * (1.0 + 0x1p-40);
+        // |x| <= |x - c_a| + |c_a| <= U + max |c| (no norm read: 80 MB a
+        // call at 10M rows)
+        const double xr = U + __builtin_sqrt(P.cmax2);
+        const double xx = xr * xr * (1.0 + 0x1p-50);
         const double U2 = U * U, L2 = L * L;
         // the reference's rounding slack, plus this test's own rounding
         const double tau = 0x1p-29 * (xx + P.cmax2) + 0x1p-48 * (L2 + U2) + 0x1p-1000;
