@@ -45,6 +45,11 @@ def short_name(full):
         args = [a.strip() for a in tmpl.rstrip(">").split(",")]
         if len(args) >= 3:
             base += "_l" + args[2]
+    if base == "k_screen_cands3" and tmpl:
+        # the carried sets' re-check (RC = true) apart from the candidate tier
+        args = [a.strip() for a in tmpl.rstrip(">").split(",")]
+        if len(args) >= 3 and args[2] == "true":
+            base = "k_screen_cands3_rc"
     if base == "k_gram_dma" and tmpl:
         # the centred covariance form (MEAN 1 / 2) apart from the plain syrk
         # (MEAN 0, with or without the riding column sums): bench.py's timer
