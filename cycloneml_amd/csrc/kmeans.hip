@@ -1672,7 +1672,9 @@ __global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __
 // k_chunk_sums_fast), which resets the state.  Gates: gate[0] = 1 runs the
 // full pass, gate[1] = 1 the incremental one; exactly one is set.
 constexpr int kIncRows = 2048;       // rows per k_inc_moved workgroup
-constexpr int kIncMovedFrac = 16;    // at most n / 16 moved rows take the incremental path
+constexpr int kIncMovedFrac = 64;    // at most n / 64 moved rows take the incremental path (one
+                                     // workgroup per cluster folds its entries: a large churn
+                                     // concentrates on a few clusters and serialises there)
 
 // The rows whose assignment differs from prev (then prev = assign): per
 // kIncRows-row block, in row order, into tmpRow / tmpOld at the block's base;
@@ -2294,6 +2296,8 @@ struct cyc_kmeans_rows_s {
   // carried candidate sets (kmeans_i8.hpp Bounds): outside bound, sets,
   // per-row state, the re-check list, its count and running total
   cyc::DeviceBuffer bLnc, bSets, bState, bRc, bRcCount, bRcCum;
+  // the centers' neighbourhoods for the state-3 re-checks (k_center_nbrs)
+  cyc::DeviceBuffer bNbr, bNbrR;
   int64_t bCalls = 0, bFullRows = 0;   // bounded calls; rows of their full (first) screens
   // Incremental cluster sums (k_inc_*; with the carried bounds, unit
   // weights, no per-row costs): the assignment the state refers to (iPrev),
@@ -2464,6 +2468,15 @@ bool bounds_on(cyc_kmeans_plan p, cyc_kmeans_rows rows) {
          cyc::km8::tiles32(p->k) * 32 <= 4096 && std::getenv("CYC_KMEANS_NO_REFINE") == nullptr;
 }
 
+// CYC_KMEANS_NBR=0: no neighbourhood re-checks (state 3)
+bool nbrOff() {
+  static const bool off = [] {
+    const char* e = std::getenv("CYC_KMEANS_NBR");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
 // Moves the bounds to the centers C (the drift against the last call's,
 // then Cp = C) and lists the rows they cannot certify; bd for the screen.
 // The first call of a fit (or after a change of k) screens every row.
@@ -2486,7 +2499,9 @@ int bounds_prepare(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* C,
       (rc = rows->bSets.reserve(sizeof(int32_t) * (size_t)n * k8::kCandMax)) ||
       (rc = rows->bState.reserve((size_t)n)) ||
       (rc = rows->bRc.reserve(sizeof(int32_t) * (size_t)n)) ||
-      (rc = rows->bRcCount.reserve(64)))
+      (rc = rows->bRcCount.reserve(64)) ||
+      (rc = rows->bNbr.reserve(sizeof(int32_t) * (size_t)k * k8::kCandMax)) ||
+      (rc = rows->bNbrR.reserve(sizeof(float) * (size_t)k)))
     return rc;
   if (!rows->bCum.ptr) {
     if ((rc = rows->bCum.reserve(64)) || (rc = rows->bRcCum.reserve(64))) return rc;
@@ -2516,8 +2531,14 @@ int bounds_prepare(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* C,
                                 bd.lnc, bd.state, xnorm, n, k, (const double*)rows->bDelta.ptr,
                                 bd.dp, bd.tmp, bd.bcount, (int32_t*)rows->bRc.ptr,
                                 (unsigned int*)rows->bRcCount.ptr,
-                                (unsigned long long*)rows->bRcCum.ptr, st)))
+                                (unsigned long long*)rows->bRcCum.ptr,
+                                nbrOff() ? nullptr : (const double*)p->stats.ptr,
+                                (int32_t*)rows->bNbr.ptr, (float*)rows->bNbrR.ptr, st)))
       return rc;
+    if (!nbrOff()) {
+      bd.nbr = (const int32_t*)rows->bNbr.ptr;
+      bd.nbrR = (const float*)rows->bNbrR.ptr;
+    }
     bd.rcRows = (const int32_t*)rows->bRc.ptr;
     bd.rcCount = (const unsigned int*)rows->bRcCount.ptr;
     bd.rowsIn = bd.list;

@@ -1998,7 +1998,8 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     int32_t* __restrict__ assign, int32_t* __restrict__ outRows, int32_t* __restrict__ outCands,
     unsigned int* __restrict__ outCount, unsigned int scap, float2* __restrict__ bnd,
     float* __restrict__ lncA, int32_t* __restrict__ sets, unsigned char* __restrict__ state,
-    const DriftParams* __restrict__ dp) {
+    const DriftParams* __restrict__ dp, const int32_t* __restrict__ nbr,
+    const float* __restrict__ nbrR) {
   using Pc = std::conditional_t<PB == 16, uint4, uint2>;
   constexpr int P16 = 32 * S / PB;    // pieces per limb plane = lanes per row
   constexpr int RPW = 64 / P16;       // rows per wave
@@ -2019,11 +2020,16 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
   for (unsigned base = w0 * RPW; base < cnt; base += nw * RPW) {
     const unsigned idx = base + q;
     const bool live = idx < cnt;
-    const int64_t row = live ? candRows[idx] : 0;
+    const int32_t rw = live ? candRows[idx] : 0;
+    // RC: a row listed as ~row re-checks the neighbourhood of its center
+    // (set slot 0 = that center; the filter's state 3)
+    const bool nbrMode = RC && rw < 0;
+    const int64_t row = nbrMode ? ~rw : rw;
+    const int32_t* setp = nbrMode ? nbr + (size_t)assign[row] * kCandMax
+                                  : cands + (size_t)(RC ? row : (int64_t)idx) * kCandMax;
     int ci[kCandMax];
 #pragma unroll
-    for (int i = 0; i < kCandMax; ++i)
-      ci[i] = live ? cands[(size_t)(RC ? row : (int64_t)idx) * kCandMax + i] : -1;
+    for (int i = 0; i < kCandMax; ++i) ci[i] = live ? setp[i] : -1;
     const Pc* xr = (const Pc*)Xq + row * (3 * P16) + li;
     const Pc xa = xr[0], xb = xr[P16], xc = xr[2 * P16];
     // the row's and the candidates' scalars issued with the gathers (each
@@ -2035,9 +2041,17 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     for (int i = 0; i < kCandMax; ++i) cqv[i] = cq[(ci[i] >= 0 && ci[i] < P.k) ? ci[i] : 0];
     float lncR = 0.0f;
     float2 bndR = make_float2(0.0f, 0.0f);
+    double cnA = 0.0, gA = 0.0;
+    float RA = 0.0f;
     if (bnd) {
       if (RC) lncR = lncA[row];
       else bndR = bnd[row];
+    }
+    if (nbrMode) {   // the anchor's terms for its fresh upper bound
+      const int a0 = (ci[0] >= 0 && ci[0] < P.k) ? ci[0] : 0;
+      cnA = cnorm[a0];
+      gA = g[a0];
+      RA = nbrR[a0];
     }
     int s1[kCandMax], s2[kCandMax], s3[kCandMax];
 #pragma unroll
@@ -2093,6 +2107,7 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
     int I1 = -1;
     bool bad = false;
     float cqMax = 0.0f;   // the f32 bounds' rounding slack (carried bounds)
+    float LA = __builtin_inff();   // the anchor's bound (slot 0, state-3 re-checks)
 #pragma unroll
     for (int i = 0; i < kCandMax; ++i) {
       const int c = ci[i];
@@ -2101,6 +2116,7 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
       const int T = s1[i] * 128 + s2[i];
       const float V = __builtin_fmaf((float)s3[i], 0x1p-7f, (float)T);
       const float L = __builtin_fmaf(-F1, V, cqv[i]);
+      if (i == 0) LA = L;
       cqMax = __builtin_fmaxf(cqMax, __builtin_fabsf(cqv[i]));
       const bool lt = L < L1;
       L2 = __builtin_amdgcn_fmed3f(L1, L2, L);
@@ -2128,9 +2144,19 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
         // rounded down after a rounded-down V: slack 2^-20 max |cq|), the
         // centers outside the set below the earlier tiers' bound (RC: the
         // set's carried bound)
-        const float lnc0 = RC ? lncR : bndR.y;
+        float lnc0 = RC ? lncR : bndR.y;
         const bool mark = RC || bndR.x == -2.0f;
         const double ub2 = bnd_ub_sq(xx, cc, l1, fx, gw, 0.0) + 0x1p-20 * (double)cqMax;
+        if (nbrMode) {
+          // every center outside the neighbourhood: |x - c| >= |c - c_a| -
+          // |x - c_a| >= nbrR[a] - (the anchor's fresh upper bound)
+          const double ua2 = __builtin_isfinite(LA)
+                                 ? bnd_ub_sq(xx, cnA * cnA, (double)LA, fx, gA, 0.0) +
+                                       0x1p-20 * (double)cqMax
+                                 : __builtin_inf();
+          const double Ln = ((double)RA - __builtin_sqrt(ua2) * (1.0 + 0x1p-50)) * (1.0 - 0x1p-50);
+          lnc0 = Ln > 0.0 ? fdown(Ln) : -1.0f;
+        }
         if (RC && decided) {
           // every center outside the set: |x - c| >= lnc0, above the winner
           // by the reference's slack (the filter's test)
@@ -2145,7 +2171,7 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
                                : __builtin_inff();
           bnd[row] = ub < 0x1p120f ? make_float2(ub, __builtin_fminf(lb, lnc0))
                                    : make_float2(-1.0f, -1.0f);
-          if (!RC && sets && ub < 0x1p120f) {
+          if ((!RC || nbrMode) && sets && ub < 0x1p120f) {
             // the set and its outside bound, for the next iterations' re-checks
             lncA[row] = lnc0;
 #pragma unroll
@@ -2186,7 +2212,7 @@ int launch_cands3(const CandArgs& ca, const void* img, const int2* meta, const d
                      (const int32_t*)ca.candRows, (const int32_t*)ca.cands,
                      (const unsigned int*)ca.candCount, assign, outRows, outCands, outCount, scap,
                      bd ? bd->ub_lb : nullptr, bd ? bd->lnc : nullptr, bd ? bd->sets : nullptr,
-                     nullptr, nullptr);
+                     nullptr, nullptr, nullptr, nullptr);
   CYC_LAUNCH_CHECK("k_screen_cands3");
   return CYC_OK;
 }
@@ -2353,7 +2379,8 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
                            st, (const uint4*)img, meta, xnorm, d,
                            (const uint4*)Cb + (size_t)ktp * S * 3 * 64, cq, g, cnorm, prm,
                            bd->rcRows, (const int32_t*)bd->sets, bd->rcCount, assign, nullptr,
-                           nullptr, nullptr, 0u, bd->ub_lb, bd->lnc, bd->sets, bd->state, bd->dp);
+                           nullptr, nullptr, 0u, bd->ub_lb, bd->lnc, bd->sets, bd->state, bd->dp,
+                           bd->nbr, bd->nbrR);
         CYC_LAUNCH_CHECK("k_screen_cands3 (re-check)");
       }
       if ((rc = bounds_collect(*bd, st))) return rc;
@@ -2581,7 +2608,8 @@ __global__ __launch_bounds__(1024) void k_drift_top(const double* __restrict__ d
 constexpr int kBndIT = kBndRows / 256;
 __device__ __forceinline__ void bnd_block_list(const unsigned long long (&masks)[kBndIT],
                                                unsigned* wc, int64_t base, int32_t* tmp,
-                                               unsigned int* bcount) {
+                                               unsigned int* bcount,
+                                               const unsigned long long* flips = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   __syncthreads();
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -2591,7 +2619,8 @@ __device__ __forceinline__ void bnd_block_list(const unsigned long long (&masks)
     for (int j = 0; j < it * 4 + wave; ++j) before += wc[j];
     if ((masks[it] >> lane) & 1ull)
       tmp[base + before + (unsigned)__builtin_popcountll(masks[it] & below)] =
-          (int32_t)(base + it * 256 + tid);
+          (flips && ((flips[it] >> lane) & 1ull)) ? ~(int32_t)(base + it * 256 + tid)
+                                                  : (int32_t)(base + it * 256 + tid);
   }
   if (tid == 0) {
     unsigned total = 0;
@@ -2600,11 +2629,90 @@ __device__ __forceinline__ void bnd_block_list(const unsigned long long (&masks)
   }
 }
 
+// Each center's neighbourhood (one wave per center) from the packed
+// statistics 0.25 dist^2 (computeStatistics, exact to ~2^-45): nbr[a] =
+// a and its kCandMax - 1 nearest other centers (-1 padding when k is
+// smaller), nbrR[a] = a lower bound of the distance from c_a to every
+// other center (the next nearest; +inf when none is left).
+__global__ __launch_bounds__(64) void k_center_nbrs(const double* __restrict__ stats, int k,
+                                                    int32_t* __restrict__ nbr,
+                                                    float* __restrict__ nbrR) {
+  const int a = blockIdx.x, lane = threadIdx.x;
+  constexpr int T = kCandMax;   // kCandMax - 1 members + the next one
+  double v[T];
+  int ix[T];
+#pragma unroll
+  for (int i = 0; i < T; ++i) {
+    v[i] = INFINITY;
+    ix[i] = -1;
+  }
+  for (int j = lane; j < k; j += 64) {
+    if (j == a) continue;
+    const int64_t pi = a <= j ? (int64_t)j * (j + 1) / 2 + a : (int64_t)a * (a + 1) / 2 + j;
+    double x = stats[pi];
+    if (!(x >= 0.0)) x = INFINITY;   // NaN centers: the drift voids the bounds anyway
+    // insert into the lane's sorted T smallest
+    if (x < v[T - 1]) {
+      double cv = x;
+      int ci = j;
+#pragma unroll
+      for (int i = 0; i < T; ++i) {
+        const bool sw = cv < v[i];
+        const double tv = v[i];
+        const int ti = ix[i];
+        v[i] = sw ? cv : v[i];
+        ix[i] = sw ? ci : ix[i];
+        cv = sw ? tv : cv;
+        ci = sw ? ti : ci;
+      }
+    }
+  }
+  // T rounds: the wave's smallest head, popped from its lane
+  if (lane == 0) nbr[(int64_t)a * kCandMax] = a;
+  for (int t = 0; t < T; ++t) {
+    double bv = v[0];
+    int bl = lane;
+    for (int m = 32; m > 0; m >>= 1) {
+      const double ov = __shfl_xor(bv, m);
+      const int ol = __shfl_xor(bl, m);
+      if (ov < bv || (ov == bv && ol < bl)) {
+        bv = ov;
+        bl = ol;
+      }
+    }
+    const int bi = __shfl(ix[0], bl);
+    if (lane == bl) {
+#pragma unroll
+      for (int i = 0; i < T - 1; ++i) {
+        v[i] = v[i + 1];
+        ix[i] = ix[i + 1];
+      }
+      v[T - 1] = INFINITY;
+      ix[T - 1] = -1;
+    }
+    if (lane == 0) {
+      if (t < T - 1) {
+        nbr[(int64_t)a * kCandMax + 1 + t] = bv < INFINITY ? bi : -1;
+      } else {
+        // the next nearest: its distance, rounded down, bounds every center
+        // outside the neighbourhood
+        nbrR[a] = bv < INFINITY ? fdown(__builtin_sqrt(4.0 * bv) * (1.0 - 0x1p-40))
+                                : __builtin_inff();
+      }
+    }
+  }
+}
+
 // kBndRows rows per workgroup (8 per thread, coalesced): a row keeps its
 // assignment when its moved bounds still certify it (kmeans_i8.hpp Bounds,
 // state 0); else it is re-checked against its carried set when the set's
 // moved outside bound still stands (state 2, listed here), else screened
-// (state 1).  Every carried bound is moved by the drift.
+// (state 1).  Every carried bound is moved by the drift.  Round 6: a row
+// left for the screen whose center a has a usable neighbourhood (nbrR[a],
+// a lower bound of the distance from c_a to every center outside a and its
+// kCandMax - 1 nearest, over twice the row's moved upper bound, or no
+// bound at all) is re-checked against that neighbourhood instead (state 3,
+// listed as ~row).
 __global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict__ assign,
                                                        float2* __restrict__ bnd,
                                                        float* __restrict__ lnc,
@@ -2614,9 +2722,11 @@ __global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict
                                                        const double* __restrict__ delta,
                                                        const DriftParams* __restrict__ prm,
                                                        int32_t* __restrict__ tmp,
-                                                       unsigned int* __restrict__ bcount) {
+                                                       unsigned int* __restrict__ bcount,
+                                                       const float* __restrict__ nbrR) {
   __shared__ unsigned wc[kBndIT * 4];
   const DriftParams P = *prm;
+  unsigned long long flips[kBndIT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * kBndRows;
   unsigned long long masks[kBndIT];
@@ -2649,12 +2759,21 @@ __global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict
         if (st == 1 && Ln > 0.0) st = 2;
         lnc[r] = st != 1 && Ln > 0.0 ? fdown(Ln) : -1.0f;
       }
+      if (st == 1 && nbrR && okA) {
+        // the neighbourhood re-check certifies only when nbrR[a] exceeds the
+        // row's distance to c_a about twice: skip the rows whose moved bound
+        // already rules that out
+        const double R = (double)nbrR[a];
+        const double U = b.x >= 0.0f ? (double)b.x + delta[a] : 0.0;
+        if (R > 0.0 && R > 2.0 * U) st = 3;
+      }
       state[r] = (unsigned char)st;
     }
-    masks[it] = __builtin_amdgcn_ballot_w64(st == 2);
+    masks[it] = __builtin_amdgcn_ballot_w64(st >= 2);
+    flips[it] = __builtin_amdgcn_ballot_w64(st == 3);
     if (lane == 0) wc[it * 4 + wave] = (unsigned)__builtin_popcountll(masks[it]);
   }
-  bnd_block_list(masks, wc, base, tmp, bcount);
+  bnd_block_list(masks, wc, base, tmp, bcount, flips);
 }
 
 // The rows a full screen takes (state 1), listed as the filter lists its
@@ -2806,12 +2925,18 @@ int centers_drift(const double* C, double* Cp, int k, int d, double* delta, doub
 int bounds_filter(const int32_t* assign, float2* ub_lb, float* lnc, unsigned char* state,
                   const double* xnorm, int64_t n, int k, const double* delta,
                   const DriftParams* prm, int32_t* tmp, unsigned int* bcount, int32_t* rcList,
-                  unsigned int* rcCount, unsigned long long* rcCum, hipStream_t st) {
+                  unsigned int* rcCount, unsigned long long* rcCum, const double* stats,
+                  int32_t* nbr, float* nbrR, hipStream_t st) {
   const int64_t nb = bounds_blocks(n);
   if (nb <= 0) return CYC_OK;
   KernelTimer timer("k_kmeans_bounds", st);
+  if (stats) {
+    hipLaunchKernelGGL(k_center_nbrs, dim3((unsigned)k), dim3(64), 0, st, stats, k, nbr, nbrR);
+    CYC_LAUNCH_CHECK("k_center_nbrs");
+  }
   hipLaunchKernelGGL(k_bounds_filter, dim3((unsigned)nb), dim3(256), 0, st, assign, ub_lb, lnc,
-                     state, xnorm, n, k, delta, prm, tmp, bcount);
+                     state, xnorm, n, k, delta, prm, tmp, bcount,
+                     stats ? (const float*)nbrR : nullptr);
   CYC_LAUNCH_CHECK("k_bounds_filter");
   hipLaunchKernelGGL(k_bounds_scan, dim3(1), dim3(1024), 0, st, bcount, nb, rcCount, rcCum);
   CYC_LAUNCH_CHECK("k_bounds_scan");

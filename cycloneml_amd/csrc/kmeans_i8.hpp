@@ -162,10 +162,15 @@ struct Bounds {
   const unsigned int* rowsInCount;
   float* lnc = nullptr;        // n: the outside bound (< 0 or NaN: no set)
   int32_t* sets = nullptr;     // n x kCandMax
-  unsigned char* state = nullptr;   // n: 0 kept, 1 full screen, 2 re-check
+  unsigned char* state = nullptr;   // n: 0 kept, 1 full screen, 2 re-check, 3 re-check
+                                    // against the center's neighbourhood (nbr)
   const int32_t* rcRows = nullptr;  // the re-check list (bounds_filter) and its count
   const unsigned int* rcCount = nullptr;
   const DriftParams* dp = nullptr;
+  // the centers' neighbourhoods (k x kCandMax, k_center_nbrs) and their
+  // outside bounds, for the state-3 re-checks (null: none)
+  const int32_t* nbr = nullptr;
+  const float* nbrR = nullptr;
   // bounds_collect's scratch and output (rowsIn / rowsInCount), its count
   // of fully screened rows added to *cum
   int32_t* tmp = nullptr;
@@ -184,6 +189,13 @@ int centers_drift(const double* C, double* Cp, int k, int d, double* delta, doub
 // set whose outside bound still stands go to the re-check list (rcList /
 // *rcCount, in row order; state 2), the rest to a full screen (state 1;
 // their sets dropped).  *rcCum (64-bit) accumulates the re-checked rows.
+// stats (optional, the plan's computeStatistics of these centers): the
+// centers' neighbourhoods first (nbr: k x kCandMax, a and its nearest
+// others; nbrR: k, a lower bound of |c - c_a| for every c outside), and a
+// row left for the screen whose nbrR[a] exceeds twice its moved upper bound
+// (or that has none) goes to the re-check list as ~row (state 3): the
+// re-check tests the neighbourhood, with |x - c| >= nbrR[a] - |x - c_a| for
+// every center outside it, and certified rows keep it as their carried set.
 // tmp: n entries; bcount: bounds_blocks(n) + 1 entries.  bounds_collect
 // (in screen, after the re-check) lists the state-1 rows for the screen.
 constexpr int kBndRows = 2048;   // rows per filter workgroup
@@ -191,7 +203,8 @@ inline int64_t bounds_blocks(int64_t n) { return (n + kBndRows - 1) / kBndRows; 
 int bounds_filter(const int32_t* assign, float2* ub_lb, float* lnc, unsigned char* state,
                   const double* xnorm, int64_t n, int k, const double* delta,
                   const DriftParams* prm, int32_t* tmp, unsigned int* bcount, int32_t* rcList,
-                  unsigned int* rcCount, unsigned long long* rcCum, hipStream_t st);
+                  unsigned int* rcCount, unsigned long long* rcCum, const double* stats,
+                  int32_t* nbr, float* nbrR, hipStream_t st);
 
 // After the re-check (inside screen): the state-1 rows into bd.list /
 // bd.listCount (the screen's rowsIn), their count added to *bd.cum.
