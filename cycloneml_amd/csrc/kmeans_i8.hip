@@ -2274,11 +2274,12 @@ __global__ __launch_bounds__(256) void k_shard_compact(unsigned int* __restrict_
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
+    // no fence: this block's counter and count reads have returned (their
+    // values were used above), and the copies reach the next launch at the
+    // kernel boundary
     const unsigned blocks = gridDim.x * gridDim.y;
     if (atomicAdd(&counts[3], 1u) == blocks - 1) {
       // every block has read the counters and *dstCount
-      __threadfence();
       unsigned tot = 0;
       for (int l = 0; l < kShards; ++l) {
         tot += counts[l * kShardStride];
