@@ -10,7 +10,9 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "../../include/cyclone.h"
 
@@ -65,6 +67,27 @@ int check_csr_indices(const int64_t* rowptr, const int32_t* colidx, int64_t n, i
 
 // Fixed-margin round-up.
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// Diagnostics (CYC_KMEANS_DUMP=<dir>): the device bytes [p, p + bytes) of
+// one call, written to <dir>/<name> after a stream sync.  Never on by
+// default; tools/probe/kmeans_state_probe.py reads the files.
+inline const char* dump_dir() {
+  static const char* d = std::getenv("CYC_KMEANS_DUMP");
+  return d;
+}
+inline void dump_dev(const char* name, const void* p, size_t bytes, hipStream_t st) {
+  const char* dir = dump_dir();
+  if (!dir || !p) return;
+  std::vector<char> h(bytes);
+  if (hipStreamSynchronize(st) != hipSuccess ||
+      hipMemcpy(h.data(), p, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+    return;
+  const std::string path = std::string(dir) + "/" + name;
+  if (FILE* f = std::fopen(path.c_str(), "wb")) {
+    std::fwrite(h.data(), 1, bytes, f);
+    std::fclose(f);
+  }
+}
 
 // Compute units of the current device (256 on MI355X), for grid sizing.
 inline int device_cus() {

@@ -2539,6 +2539,21 @@ int bounds_prepare(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* C,
       bd.nbr = (const int32_t*)rows->bNbr.ptr;
       bd.nbrR = (const float*)rows->bNbrR.ptr;
     }
+    static const int dumpCall = [] {
+      const char* e = std::getenv("CYC_KMEANS_DUMP_CALL");
+      return e ? std::atoi(e) : 10;
+    }();
+    if (cyc::dump_dir() && rows->bCalls == dumpCall) {
+      bd.dump = 1;
+      cyc::dump_dev("state_filter", rows->bState.ptr, (size_t)n, st);
+      cyc::dump_dev("bnd", rows->bnd.ptr, sizeof(float2) * (size_t)n, st);
+      cyc::dump_dev("lnc", rows->bLnc.ptr, sizeof(float) * (size_t)n, st);
+      cyc::dump_dev("assign", rows->bAssign.ptr, sizeof(int32_t) * (size_t)n, st);
+      cyc::dump_dev("nbrR", rows->bNbrR.ptr, sizeof(float) * (size_t)k, st);
+      cyc::dump_dev("nbr", rows->bNbr.ptr, sizeof(int32_t) * (size_t)k * k8::kCandMax, st);
+      cyc::dump_dev("delta", rows->bDelta.ptr, sizeof(double) * (size_t)k, st);
+      cyc::dump_dev("prm", rows->bPrm.ptr, sizeof(k8::DriftParams), st);
+    }
     bd.rcRows = (const int32_t*)rows->bRc.ptr;
     bd.rcCount = (const unsigned int*)rows->bRcCount.ptr;
     bd.rowsIn = bd.list;

@@ -2384,6 +2384,7 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
                            bd->nbr, bd->nbrR);
         CYC_LAUNCH_CHECK("k_screen_cands3 (re-check)");
       }
+      if (bd->dump) dump_dev("state_rc", bd->state, (size_t)bd->n, st);
       if ((rc = bounds_collect(*bd, st))) return rc;
     }
     if (bd && bd->rowsIn)

@@ -171,6 +171,7 @@ struct Bounds {
   // outside bounds, for the state-3 re-checks (null: none)
   const int32_t* nbr = nullptr;
   const float* nbrR = nullptr;
+  int dump = 0;                     // diagnostics: dump the state after the re-check
   // bounds_collect's scratch and output (rowsIn / rowsInCount), its count
   // of fully screened rows added to *cum
   int32_t* tmp = nullptr;
