@@ -1195,7 +1195,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
-    dev = torch.device("cuda", local)
+    from cycloneml_amd.config import device_for_local_rank
+    dev = torch.device("cuda", device_for_local_rank(local))   # CYCLONE_DEVICES
     torch.cuda.set_device(dev)
     if world > 1:
         # host-side group only (rendezvous, RCCL id, barriers): every device

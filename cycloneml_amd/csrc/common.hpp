@@ -71,6 +71,15 @@ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // Diagnostics (CYC_KMEANS_DUMP=<dir>): the device bytes [p, p + bytes) of
 // one call, written to <dir>/<name> after a stream sync.  Never on by
 // default; tools/probe/kmeans_state_probe.py reads the files.
+// CYCLONE_STRICT_PARITY=1 (cycloneml_amd/config.py): no state carried
+// across calls (KMeans bounds, neighbourhoods, incremental sums)
+inline bool strict_parity() {
+  static const bool on = [] {
+    const char* e = std::getenv("CYCLONE_STRICT_PARITY");
+    return e && e[0] && e[0] != '0';
+  }();
+  return on;
+}
 inline const char* dump_dir() {
   static const char* d = std::getenv("CYC_KMEANS_DUMP");
   return d;

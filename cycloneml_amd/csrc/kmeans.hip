@@ -2464,6 +2464,7 @@ bool bounds_on(cyc_kmeans_plan p, cyc_kmeans_rows rows) {
     return e && e[0] == '0';
   }();
   return rows && rows->usable && !rows->cosine && rows->bEnabled && !envOff &&
+         !cyc::strict_parity() &&
          p->measure == CYC_DISTANCE_EUCLIDEAN && cyc::km8::uses32(p->d) && p->k > 96 &&
          cyc::km8::tiles32(p->k) * 32 <= 4096 && std::getenv("CYC_KMEANS_NO_REFINE") == nullptr;
 }
@@ -2474,7 +2475,7 @@ bool nbrOff() {
     const char* e = std::getenv("CYC_KMEANS_NBR");
     return e && e[0] == '0';
   }();
-  return off;
+  return off || cyc::strict_parity();
 }
 
 // Moves the bounds to the centers C (the drift against the last call's,
@@ -2927,7 +2928,7 @@ bool inc_on(cyc_kmeans_rows rows) {
     const char* e = std::getenv("CYC_KMEANS_INCR");
     return e && e[0] == '0';
   }();
-  return rows->iEnabled && !envOff;
+  return rows->iEnabled && !envOff && !cyc::strict_parity();
 }
 
 // The Lloyd call's cluster sums, weights and cost through the incremental

@@ -281,6 +281,9 @@ class RowMatrix:
         torch = _torch()
         n = self.numCols()
         form = self.covarianceForm
+        from .config import strict_parity
+        if strict_parity() and form == "auto":
+            form = "centred"          # CYCLONE_STRICT_PARITY: the reference's dense form
         if form not in ("auto", "centred", "uncentred"):
             raise N.IllegalArgumentException(f"covarianceForm {form!r}: auto, centred or "
                                              "uncentred")
