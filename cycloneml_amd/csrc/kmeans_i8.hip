@@ -2756,19 +2756,23 @@ __global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict
           bnd[r] = make_float2(fup(U * (1.0 + 0x1p-50)), fdown(L * (1.0 - 0x1p-50)));
         }
       }
-      if (ln >= 0.0f) {   // a carried set (NaN / negative: none)
-        const double Ln = okA ? ((double)ln - P.d1) * (1.0 - 0x1p-50) : -1.0;
-        if (st == 1 && Ln > 0.0) st = 2;
-        lnc[r] = st != 1 && Ln > 0.0 ? fdown(Ln) : -1.0f;
-      }
+      // which re-check: a carried set whose moved outside bound still
+      // clears the row's moved upper bound (it will most likely certify);
+      // else the neighbourhood when nbrR[a] exceeds twice that bound (or
+      // the row has none); else a carried set with any margin left.  Both
+      // tests only pick the work: the re-check itself decides.
+      const double Ln = ln >= 0.0f && okA ? ((double)ln - P.d1) * (1.0 - 0x1p-50) : -1.0;
+      const double Um = okA && b.x >= 0.0f ? (double)b.x + delta[a] : 0.0;
+      if (st == 1 && Ln > 0.0 && Ln > Um) st = 2;
       if (st == 1 && nbrR && okA) {
-        // the neighbourhood re-check certifies only when nbrR[a] exceeds the
-        // row's distance to c_a about twice: skip the rows whose moved bound
-        // already rules that out
+        // (a row without a bound: only when its center moved little
+        // against its neighbourhood -- early in a fit such rows mostly fail)
         const double R = (double)nbrR[a];
-        const double U = b.x >= 0.0f ? (double)b.x + delta[a] : 0.0;
-        if (R > 0.0 && R > 2.0 * U) st = 3;
+        if (R > 0.0 && R > 2.0 * Um && (b.x >= 0.0f || delta[a] < 0.125 * R)) st = 3;
       }
+      if (st == 1 && Ln > 0.0) st = 2;
+      if (ln >= 0.0f)   // a carried set (NaN / negative: none) kept while it has a margin
+        lnc[r] = (st == 0 || st == 2) && Ln > 0.0 ? fdown(Ln) : -1.0f;
       state[r] = (unsigned char)st;
     }
     masks[it] = __builtin_amdgcn_ballot_w64(st >= 2);

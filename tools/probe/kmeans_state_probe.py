@@ -16,6 +16,11 @@ os.environ["CYC_KMEANS_DUMP"] = out
 os.environ.setdefault("CYC_KMEANS_DUMP_CALL", "10")
 
 
+def qs(x, q):
+    import numpy as np
+    return [float(v) for v in np.quantile(x, q)] if len(x) else None
+
+
 def main():
     import numpy as np
     import torch
@@ -40,17 +45,18 @@ def main():
     Ra = R[a[m1]].astype(np.float64)
     ok = ub >= 0
     q = Ra[ok] / np.maximum(U[ok], 1e-30)
-    res["state1_R_over_U_quantiles"] = [float(x) for x in np.quantile(q, [0.05, 0.25, 0.5, 0.75, 0.95])]
-    res["state1_U_quantiles"] = [float(x) for x in np.quantile(U[ok], [0.05, 0.5, 0.95])]
-    res["nbrR_quantiles"] = [float(x) for x in np.quantile(R, [0.05, 0.25, 0.5, 0.75, 0.95])]
-    res["kept_ub_quantiles"] = [float(x) for x in np.quantile(bnd[s0 == 0, 0], [0.05, 0.5, 0.95])]
+    res["state1_R_over_U_quantiles"] = qs(q, [0.05, 0.25, 0.5, 0.75, 0.95])
+    res["state1_U_quantiles"] = qs(U[ok], [0.05, 0.5, 0.95])
+    res["nbrR_quantiles"] = qs(R, [0.05, 0.25, 0.5, 0.75, 0.95])
+    res["kept_ub_quantiles"] = qs(bnd[s0 == 0, 0], [0.05, 0.5, 0.95])
+    res["max_drift"] = float(delta.max())
     # failed re-checks (2 or 3 -> 1): their moved bounds
     for st in (2, 3):
         mf = (s0 == st) & (s1 == 1)
         if mf.any():
             u = bnd[mf, 0].astype(np.float64) + delta[a[mf]]
-            res[f"failed{st}_R_over_U_quantiles"] = [float(x) for x in np.quantile(
-                R[a[mf]] / np.maximum(u, 1e-30), [0.05, 0.5, 0.95])]
+            res[f"failed{st}_R_over_U_quantiles"] = qs(R[a[mf]] / np.maximum(u, 1e-30),
+                                                       [0.05, 0.5, 0.95])
     print(json.dumps(res), flush=True)
 
 
