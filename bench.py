@@ -434,6 +434,7 @@ class KMeansWorkload:
         # each iteration ends with the host's convergence check (a sync)
         model = km.run(self.X, iteration_callback=lambda it, c: marks.append(time.perf_counter()))
         return {"iterations": model.numIter,
+                "carried_state": {k: v for k, v in km.lastFitInfo.items() if k != "per_iteration"},
                 "iteration_ms": [round((b - a) * 1e3, 3) for a, b in zip(marks[:-1], marks[1:])],
                 "iteration_ms_note": "wall time between the host's convergence checks; the first "
                                      "includes the norms, the plan and the row image",

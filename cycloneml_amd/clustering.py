@@ -13,6 +13,7 @@ same centroid update (:322-330).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -560,6 +561,7 @@ class KMeans:
         sums, wsum, cost_sum = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
         converged_t = torch.zeros(1, dtype=torch.int32, device=dev)
         iteration, converged, cost = 0, False, 0.0
+        trace = [] if os.environ.get("CYC_KMEANS_FIT_TRACE") == "1" else None
         while iteration < self.maxIterations and not converged:
             buf.zero_()
             plan.accumulate(X, xnorm, weights, C, cnorm, sums, wsum, cost_sum, stream=stream,
@@ -568,9 +570,17 @@ class KMeans:
             plan.update(C, cnorm, sums, wsum, self.epsilon, converged_t, stream=stream)
             converged = bool(converged_t.item())
             cost = float(cost_sum.item())
+            if trace is not None:        # CYC_KMEANS_FIT_TRACE=1: the carried state per iteration
+                trace.append({"bounds": rows.bounds_info(), "rechecked": rows.bounds_rechecked(),
+                              "incremental": rows.incremental_info()})
             if iteration_callback:
                 iteration_callback(iteration, cost)
             iteration += 1
+        # diagnostics of the carried state (cumulative over the fit)
+        self.lastFitInfo = {"bounded_calls_and_screened_rows": rows.bounds_info(),
+                            "rechecked_rows": rows.bounds_rechecked(),
+                            "incremental_calls_and_moved_rows": rows.incremental_info(),
+                            "per_iteration": trace}
         rows.close()
         plan.close()
         return KMeansModel(C.cpu().numpy(), cost, iteration, self.distanceMeasure)
@@ -623,6 +633,7 @@ class KMeans:
         sums, wsum, cost_sum = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
         converged_t = torch.zeros(1, dtype=torch.int32, device=dev)
         iteration, converged, cost = 0, False, 0.0
+        trace = [] if os.environ.get("CYC_KMEANS_FIT_TRACE") == "1" else None
         while iteration < self.maxIterations and not converged:
             buf.zero_()
             plan.accumulate_csr(rowptr, colidx, values, xnorm, weights, C, cnorm, sums, wsum,

@@ -1672,9 +1672,9 @@ __global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __
 // k_chunk_sums_fast), which resets the state.  Gates: gate[0] = 1 runs the
 // full pass, gate[1] = 1 the incremental one; exactly one is set.
 constexpr int kIncRows = 2048;       // rows per k_inc_moved workgroup
-constexpr int kIncMovedFrac = 64;    // at most n / 64 moved rows take the incremental path (one
-                                     // workgroup per cluster folds its entries: a large churn
-                                     // concentrates on a few clusters and serialises there)
+constexpr int kIncMovedFrac = 64;    // at most n / 64 moved rows take the incremental path
+                                     // (kIncSplit workgroups fold a cluster's entries: a large
+                                     // churn concentrates on a few clusters)
 
 // The rows whose assignment differs from prev (then prev = assign): per
 // kIncRows-row block, in row order, into tmpRow / tmpOld at the block's base;
@@ -1801,22 +1801,20 @@ __device__ __forceinline__ void inc_block_sum(double (&v)[NV], double* red) {
   for (int i = 0; i < NV; ++i) v[i] = red[i * 256];
 }
 
-// One workgroup per cluster: its entries (the moved rows that left or joined
-// it) picked from the moved list in list order -- kIncScan entries per
-// thread per step, compacted in order through LDS -- folded into its state;
-// then its cost for the call's centers C and the bound of that cost's
-// rounding (cerr), cbad = 1 when the state's error grew past 2^-38 of the
-// sum of the members' norms.  Unit weights only.
+// kIncSplit workgroups per cluster, each over one contiguous slice of the
+// moved list: the cluster's entries there (the moved rows that left or
+// joined it) picked in list order -- kIncScan entries per thread per step,
+// compacted in order through LDS -- and folded into a partial (sums per
+// dimension; the cost terms, count and norm sums as scalars).  Unit weights.
 constexpr int kIncScan = 8;
+constexpr int kIncSplit = 4;
+constexpr int kIncPs = 6;   // scalars per partial: dq, |dq|, count, sum |x| signed, sum |x|, entries
 template <int NJ>
-__global__ __launch_bounds__(256) void k_inc_fold(
+__global__ __launch_bounds__(256) void k_inc_part(
     const double* __restrict__ X, int d, const double* __restrict__ xnorm,
-    const double* __restrict__ C, const int32_t* __restrict__ movedRow,
-    const int32_t* __restrict__ movedNew, const int32_t* __restrict__ movedOld,
-    const unsigned int* __restrict__ count, double* __restrict__ S, const double* __restrict__ P,
-    double* __restrict__ W, double* __restrict__ Q, int64_t* __restrict__ N,
-    double* __restrict__ A, double* __restrict__ ES, double* __restrict__ EQ,
-    double* __restrict__ ccost, double* __restrict__ cerr, int* __restrict__ cbad,
+    const int32_t* __restrict__ movedRow, const int32_t* __restrict__ movedNew,
+    const int32_t* __restrict__ movedOld, const unsigned int* __restrict__ count,
+    const double* __restrict__ P, double* __restrict__ pds, double* __restrict__ psc,
     const int* __restrict__ gate) {
   if (!gate[1]) return;
   constexpr int B = 256 * kIncScan;
@@ -1824,8 +1822,10 @@ __global__ __launch_bounds__(256) void k_inc_fold(
   __shared__ float sgS[B];
   __shared__ unsigned wcS[kIncScan * 4];
   __shared__ double red[5 * 256];
-  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const unsigned m = *count;
+  const unsigned s0 = (unsigned)((uint64_t)m * g / kIncSplit);
+  const unsigned s1 = (unsigned)((uint64_t)m * (g + 1) / kIncSplit);
   int64_t ent = 0;
   double ds[NJ], dq[NJ], dqa[NJ], pj[NJ];
 #pragma unroll
@@ -1836,13 +1836,13 @@ __global__ __launch_bounds__(256) void k_inc_fold(
   }
   double tN = 0.0, tA = 0.0, tAbs = 0.0;   // this thread's entries: count, sum |x|
   const unsigned long long below = (1ull << lane) - 1ull;
-  for (unsigned base = 0; base < m; base += B) {
+  for (unsigned base = s0; base < s1; base += B) {
     int nw[kIncScan], ol[kIncScan];
 #pragma unroll
     for (int q = 0; q < kIncScan; ++q) {
       const unsigned i = base + q * 256 + tid;
-      nw[q] = i < m ? movedNew[i] : -1;
-      ol[q] = i < m ? movedOld[i] : -1;
+      nw[q] = i < s1 ? movedNew[i] : -1;
+      ol[q] = i < s1 ? movedOld[i] : -1;
     }
     unsigned long long mk[kIncScan];
     __syncthreads();   // the previous batch's entries are folded
@@ -1908,6 +1908,51 @@ __global__ __launch_bounds__(256) void k_inc_fold(
     r1[1] = dadd(r1[1], dqa[u]);
   }
   inc_block_sum<5>(r1, red);
+  const int64_t slot = (int64_t)c * kIncSplit + g;
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) {
+    const int j = tid + 256 * u;
+    if (j < d) pds[slot * d + j] = ds[u];
+  }
+  if (tid < 5) psc[slot * kIncPs + tid] = r1[tid];
+  if (tid == 5) psc[slot * kIncPs + 5] = (double)ent;
+}
+
+// One workgroup per cluster: its partials summed in slice order, folded into
+// the state; then its cost for the call's centers C and the bound of that
+// cost's rounding (cerr), cbad = 1 when the state's error grew past 2^-38 of
+// the sum of the members' norms.
+template <int NJ>
+__global__ __launch_bounds__(256) void k_inc_combine(
+    int d, const double* __restrict__ C, const double* __restrict__ pds,
+    const double* __restrict__ psc, double* __restrict__ S, const double* __restrict__ P,
+    double* __restrict__ W, double* __restrict__ Q, int64_t* __restrict__ N,
+    double* __restrict__ A, double* __restrict__ ES, double* __restrict__ EQ,
+    double* __restrict__ ccost, double* __restrict__ cerr, int* __restrict__ cbad,
+    const int* __restrict__ gate) {
+  if (!gate[1]) return;
+  __shared__ double red[4 * 256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  double r1[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  int64_t ent = 0;
+  double ds[NJ], pj[NJ];
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) {
+    const int j = tid + 256 * u;
+    ds[u] = 0.0;
+    pj[u] = j < d ? P[(int64_t)c * d + j] : 0.0;
+  }
+  for (int g = 0; g < kIncSplit; ++g) {
+    const int64_t slot = (int64_t)c * kIncSplit + g;
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) {
+      const int j = tid + 256 * u;
+      if (j < d) ds[u] = dadd(ds[u], pds[slot * d + j]);
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) r1[i] = dadd(r1[i], psc[slot * kIncPs + i]);
+    ent += (int64_t)psc[slot * kIncPs + 5];
+  }
   const int64_t nNew = N[c] + (int64_t)r1[2];
   const bool empty = nNew <= 0;
   const double wNew = empty ? 0.0 : (double)nNew;    // unit weights: the count
@@ -1942,8 +1987,11 @@ __global__ __launch_bounds__(256) void k_inc_fold(
       const double nS = sqrt(r2[0]) * (1.0 + 0x1p-50);
       q = dadd(q, r1[0]);
       a = dadd(a, r1[3]);
-      es += 0x1p-52 * ((double)(ent + 1) * r1[4] + nS);
-      eq += 0x1p-52 * ((double)(ent + 2) * r1[1] + fabs(q));
+      // a slice's entries sum sequentially, then the slices and (for the
+      // cost terms) the dimensions and the block tree: <= ent + kIncSplit
+      // + 16 roundings per term
+      es += 0x1p-52 * ((double)(ent + kIncSplit + 1) * r1[4] + nS);
+      eq += 0x1p-52 * ((double)(ent + kIncSplit + 16) * r1[1] + fabs(q));
     }
     N[c] = empty ? 0 : nNew;
     W[c] = wNew;
@@ -1958,7 +2006,11 @@ __global__ __launch_bounds__(256) void k_inc_fold(
                    nP = sqrt(r2[3]) * (1.0 + 0x1p-50);
       cost = dadd(q, dadd(dmul(2.0, r2[1]), dmul(wNew, r2[2])));
       const double sv2 = nS + wNew * nP;
-      err = eq + 2.0 * nD * (es + 0x1p-51 * sv2) + 0x1p-41 * (nD * sv2 + wNew * r2[2]) +
+      // the correction's own rounding: D and V (one rounding each, the
+      // 2^-51 term), the dot's and |D|^2's sums (<= NJ + 8 + 2 <= 14
+      // roundings of terms bounded by |D| |V|, |D|^2: 2 x 16 x 2^-53 <=
+      // 2^-47, taken as 2^-46)
+      err = eq + 2.0 * nD * (es + 0x1p-51 * sv2) + 0x1p-46 * (nD * sv2 + wNew * r2[2]) +
             0x1p-50 * fabs(cost);
       bad = !(es <= 0x1p-38 * a) || !(fabs(cost) < INFINITY) || !(err < INFINITY);
     }
@@ -2308,7 +2360,7 @@ struct cyc_kmeans_rows_s {
   bool iValid = false;
   int ik = 0;
   cyc::DeviceBuffer iPrev, iTmpRow, iTmpOld, iBcount, iCount, iGate, iMovedRow, iMovedNew,
-      iMovedOld, iS, iP, iW, iQ, iN, iA, iES, iEQ, iCost, iErr, iBad, iTot, iCum, iPa;
+      iMovedOld, iS, iP, iW, iQ, iN, iA, iES, iEQ, iCost, iErr, iBad, iTot, iCum, iPa, iPds, iPsc;
 };
 
 namespace {
@@ -2953,6 +3005,8 @@ int inc_accumulate(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* X,
       (rc = rows->iMovedNew.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(mcap, 1))) ||
       (rc = rows->iMovedOld.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(mcap, 1))) ||
       (rc = rows->iS.reserve(sizeof(double) * kd)) || (rc = rows->iP.reserve(sizeof(double) * kd)) ||
+      (rc = rows->iPds.reserve(sizeof(double) * kd * kIncSplit)) ||
+      (rc = rows->iPsc.reserve(sizeof(double) * (size_t)k * kIncSplit * kIncPs)) ||
       (rc = rows->iW.reserve(sizeof(double) * (size_t)k)) ||
       (rc = rows->iQ.reserve(sizeof(double) * (size_t)k)) ||
       (rc = rows->iN.reserve(sizeof(int64_t) * (size_t)k)) ||
@@ -2989,18 +3043,24 @@ int inc_accumulate(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* X,
                        (int32_t*)rows->iMovedOld.ptr, (const int*)gate);
     CYC_LAUNCH_CHECK("k_inc_gather");
 #define CYC_IF(NJ)                                                                               \
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_inc_fold<NJ>), dim3((unsigned)k), dim3(256), 0, st, X, d,  \
-                     xnorm, C, (const int32_t*)rows->iMovedRow.ptr,                             \
+  do {                                                                                           \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_inc_part<NJ>), dim3((unsigned)k, kIncSplit), dim3(256), 0, \
+                     st, X, d, xnorm, (const int32_t*)rows->iMovedRow.ptr,                        \
                      (const int32_t*)rows->iMovedNew.ptr, (const int32_t*)rows->iMovedOld.ptr,   \
-                     cnt, (double*)rows->iS.ptr, (const double*)rows->iP.ptr, (double*)rows->iW.ptr,  \
+                     cnt, (const double*)rows->iP.ptr, (double*)rows->iPds.ptr,                 \
+                     (double*)rows->iPsc.ptr, (const int*)gate);                                 \
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_inc_combine<NJ>), dim3((unsigned)k), dim3(256), 0, st, d, C, \
+                     (const double*)rows->iPds.ptr, (const double*)rows->iPsc.ptr,              \
+                     (double*)rows->iS.ptr, (const double*)rows->iP.ptr, (double*)rows->iW.ptr,  \
                      (double*)rows->iQ.ptr, (int64_t*)rows->iN.ptr, (double*)rows->iA.ptr,       \
                      (double*)rows->iES.ptr, (double*)rows->iEQ.ptr, (double*)rows->iCost.ptr,   \
-                     (double*)rows->iErr.ptr, (int*)rows->iBad.ptr, (const int*)gate)
+                     (double*)rows->iErr.ptr, (int*)rows->iBad.ptr, (const int*)gate);         \
+  } while (0)
     if (nj == 1) CYC_IF(1);
     else if (nj == 2) CYC_IF(2);
     else CYC_IF(4);
 #undef CYC_IF
-    CYC_LAUNCH_CHECK("k_inc_fold");
+    CYC_LAUNCH_CHECK("k_inc_part / k_inc_combine");
     hipLaunchKernelGGL(k_inc_check, dim3(1), dim3(256), 0, st, (const double*)rows->iCost.ptr,
                        (const double*)rows->iErr.ptr, (const int*)rows->iBad.ptr, k, gate,
                        (double*)rows->iTot.ptr, cum + 1);
