@@ -205,6 +205,71 @@ __global__ __launch_bounds__(256) void k_rows_quantize_pf(const double* __restri
   }
 }
 
+// d % 4 == 0, d <= 256, rows 32-byte aligned: each lane quantises 4
+// consecutive elements, so every limb plane leaves as one 4-byte store per
+// lane (256 B per wave instruction; the 2-byte stores of k_rows_quantize_pf
+// wrote half lines), the next row's loads in flight as there.
+__global__ __launch_bounds__(256) void k_rows_quantize_q4(const double* __restrict__ X, int64_t n,
+                                                          int d, int D, unsigned* __restrict__ img,
+                                                          int2* __restrict__ meta,
+                                                          const double* __restrict__ scale,
+                                                          double* __restrict__ unorm) {
+  const int lane = threadIdx.x & 63;
+  const int j0 = 4 * lane;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  v2d cur[2];
+  auto load = [&](int64_t r, v2d (&w)[2]) {
+    const double* x = X + (r < n ? r : 0) * d + j0;
+    w[0] = j0 < d ? __builtin_nontemporal_load(reinterpret_cast<const v2d*>(x)) : v2d{0.0, 0.0};
+    w[1] = j0 < d ? __builtin_nontemporal_load(reinterpret_cast<const v2d*>(x + 2)) : v2d{0.0, 0.0};
+  };
+  if (row < n) load(row, cur);
+  for (; row < n; row += nw) {
+    v2d nxt[2];
+    load(row + nw, nxt);   // in flight while this row is reduced and stored
+    const double sc = scale ? scale[row] : 1.0;
+    double v[4] = {cur[0].x, cur[0].y, cur[1].x, cur[1].y};
+    double m = 0.0, s1 = 0.0, s2 = 0.0;
+    bool fin = true;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (scale) v[q] = v[q] / sc;
+      fin = fin && __builtin_isfinite(v[q]);
+      m = __builtin_fmax(m, __builtin_fabs(v[q]));
+      s1 += __builtin_fabs(v[q]);
+      s2 += v[q] * v[q];
+    }
+    m = wave_max(m);
+    s1 = wave_sum(s1);
+    if (unorm) {
+      s2 = wave_sum(s2);
+      if (lane == 0) unorm[row] = __builtin_sqrt(s2);
+    }
+    const bool allFin = __all(fin);
+    const int e = choose_exp(m);
+    const bool bad = !allFin || e > kMaxExp;
+    if (j0 < D) {
+      int a[4], b[4], c[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (bad) a[q] = b[q] = c[q] = 0;
+        else quant3(v[q], e, a[q], b[q], c[q]);
+      }
+      unsigned char* db = reinterpret_cast<unsigned char*>(img + row * (int64_t)(3 * D / 4));
+      *reinterpret_cast<unsigned*>(db + j0) = pack4(a);
+      *reinterpret_cast<unsigned*>(db + D + j0) = pack4(b);
+      *reinterpret_cast<unsigned*>(db + 2 * D + j0) = pack4(c);
+    }
+    if (lane == 0) {
+      const double n1 = bad ? 0.0 : s1 * (1.0 + 0x1p-40) + (double)d * __builtin_ldexp(1.0, e - 22);
+      meta[row] = make_int2(bad ? INT_MIN : e, __float_as_int(fup(n1)));
+    }
+    cur[0] = nxt[0];
+    cur[1] = nxt[1];
+  }
+}
+
 // One wave per row: limbs into the image, exponent and |xh|_1 bound into meta.
 // scale (optional): the row is x / scale[row] (the cosine plan's unit
 // directions), whose norm goes to unorm[row] (any summation order: it only
@@ -2873,7 +2938,11 @@ int rows_quantize(const double* X, int64_t n, int d, void* img, int2* meta, hipS
     const char* e = std::getenv("CYC_QUANT_PF");
     return !(e && e[0] == '0');
   }();
-  if (vec && pf && d <= 256)
+  const bool q4 = d % 4 == 0 && reinterpret_cast<uintptr_t>(X) % 32 == 0;
+  if (q4 && pf && d <= 256)
+    hipLaunchKernelGGL(k_rows_quantize_q4, dim3((unsigned)blocks), dim3(256), 0, st, X, n, d, D,
+                       (unsigned*)img, meta, scale, unorm);
+  else if (vec && pf && d <= 256)
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rows_quantize_pf<2>), dim3((unsigned)blocks), dim3(256), 0,
                        st, X, n, d, D, (unsigned*)img, meta, scale, unorm);
   else if (vec && pf)

@@ -20,8 +20,15 @@ def main():
     C0 = X[:k].clone()
     xn = row_norms(X)
     for fit in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
         p = KMeansPlan(d, k, n)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
         rows = p.rows(X)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        print(f"fit {fit}: plan {1e3 * (t1 - t0):.3f} ms, rows {1e3 * (t2 - t1):.3f} ms", flush=True)
         C = C0.clone()
         cn = row_norms(C)
         buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=dev)
