@@ -139,6 +139,52 @@ def _kmeans_rank(rank, world):
                 and abs(cost.item() - ref["cost"]) <= 1e-12 * ref["cost"])
 
 
+def _kmeans_carried_rank(rank, world):
+    """Eight Lloyd iterations on row shards with each rank's carried state on
+    (bounds, neighbourhoods, incremental sums: k > 96, d <= 256), the state
+    merged by the collective every iteration: every iteration equals the
+    restatement over the whole data on the same centers (the shard's
+    assignments exactly, weights exactly, sums within 1e-10, cost 1e-12)."""
+    import torch
+    from cycloneml_amd import parallel
+    from cycloneml_amd.clustering import KMeansPlan, row_norms
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(7)
+    n, d, k = 60_001, 64, 130
+    X = rng.normal(scale=3.0, size=(k, d))[rng.integers(0, k, n)] + rng.normal(size=(n, d))
+    a, b = parallel.shard_bounds(n, rank, world)
+    Xd = torch.from_numpy(X[a:b].copy()).to(dev)
+    Cd = torch.from_numpy(X[:k].copy()).to(dev)
+    parallel.broadcast_(Cd)
+    xn, cn = row_norms(Xd), row_norms(Cd)
+    plan = KMeansPlan(d, k, b - a)
+    rows = plan.rows(Xd)
+    buf = torch.zeros(k * d + k + 1, dtype=torch.float64, device=dev)
+    sums, wsum, cost = buf[:k * d], buf[k * d:k * d + k], buf[k * d + k:]
+    asg = torch.empty(b - a, dtype=torch.int32, device=dev)
+    conv = torch.zeros(1, dtype=torch.int32, device=dev)
+    ok = True
+    for it in range(8):
+        C = Cd.cpu().numpy()
+        buf.zero_()
+        plan.accumulate(Xd, None, None, Cd, cn, sums, wsum, cost, asg, rows=rows)
+        parallel.allreduce_(buf)
+        if it in (0, 3, 7):
+            ref = oracle.kmeans_iteration(X, oracle.row_norms(X), None, C, oracle.row_norms(C),
+                                          num_partitions=2)
+            S = sums.cpu().numpy().reshape(k, d)
+            ok = ok and bool(np.array_equal(asg.cpu().numpy(), ref["assign"][a:b])
+                             and np.array_equal(wsum.cpu().numpy(), ref["wsum"])
+                             and np.allclose(S, ref["sums"], rtol=1e-10,
+                                             atol=1e-10 * np.abs(ref["sums"]).max())
+                             and abs(cost.item() - ref["cost"]) <= 1e-12 * ref["cost"])
+        plan.update(Cd, cn, sums, wsum, 1e-4, conv)
+    torch.cuda.synchronize()
+    calls, _ = rows.bounds_info()
+    inc, _ = rows.incremental_info()
+    return bool(ok and calls == 8 and inc >= 1)
+
+
 def _lr_rank(rank, world):
     import torch
     from cycloneml_amd import parallel
@@ -408,7 +454,8 @@ def _silhouette_rank(rank, world):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("fn", [_kmeans_rank, _lr_rank, _gramian_rank, _covariance_rank,
+@pytest.mark.parametrize("fn", [_kmeans_rank, _kmeans_carried_rank, _lr_rank, _gramian_rank,
+                                _covariance_rank,
                                 _kmeans_init_rank, _kmeans_init_csr_rank, _silhouette_rank])
 def test_two_ranks_device_kernels_meet_the_collective(fn):
     out = _run(fn)
