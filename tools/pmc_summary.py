@@ -26,7 +26,7 @@ import sys
 
 FETCH_X2 = {"k_screen", "k_screen32", "k_tiles_margin", "k_tiles_grad", "k_tiles_rows", "k_csr_densify",
             "k_gram_tiles", "k_gram_dma", "k_gram_dma_cov", "k_rows_quantize", "k_chunk_sums_fast", "k_chunk_sums",
-            "k_row_norms", "k_rows_quantize_pf", "k_col_partial", "k_mlr_margins", "k_mlr_grad", "k_binlog_dense", "k_binlog_csr_mult8",
+            "k_row_norms", "k_rows_quantize_pf", "k_rows_quantize_q4", "k_col_partial", "k_mlr_margins", "k_mlr_grad", "k_binlog_dense", "k_binlog_csr_mult8",
             "k_binlog_csc_grad_blk", "k_summ_dense"}
 
 
