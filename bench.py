@@ -466,7 +466,7 @@ class KMeansWorkload:
                     "cyc_kmeans_rows_set_incremental): a step folds only the rows whose "
                     "center changed into the carried sums and takes the cost from "
                     "Q + 2 (P - c).(S - W P) + W |P - c|^2 with its rounding bounded on the "
-                    "device (<= 2^-42 of the cost, else the full pass); full_sums_ms_per_step: "
+                    "device (<= 2^-40 of the cost, else the full pass); full_sums_ms_per_step: "
                     "the same steps with the full pass every step, timed after the clock"},
             "carried_bounds": {
             "rows_screened_per_step": scr / self.steps_timed if scr is not None else None,

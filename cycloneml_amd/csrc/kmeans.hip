@@ -1667,12 +1667,12 @@ __global__ void k_cost_total(const double* __restrict__ ccost, int k, double* __
 //   sum_x |x - c|^2 = Q_c + 2 (P_c - c).(S_c - W_c P_c) + W_c |P_c - c|^2,
 // which is exact algebra; the rounding of every term is bounded on the device
 // (ES_c, EQ_c and the correction's own).  When the bound
-// exceeds 2^-42 of the cost, a moved count is too large, or no state exists,
+// exceeds 2^-40 of the cost, a moved count is too large, or no state exists,
 // the call runs the full pass over every row instead (the sort by cluster and
 // k_chunk_sums_fast), which resets the state.  Gates: gate[0] = 1 runs the
 // full pass, gate[1] = 1 the incremental one; exactly one is set.
 constexpr int kIncRows = 2048;       // rows per k_inc_moved workgroup
-constexpr int kIncMovedFrac = 64;    // at most n / 64 moved rows take the incremental path
+constexpr int kIncMovedFrac = 16;    // at most n / 16 moved rows take the incremental path
                                      // (kIncSplit workgroups fold a cluster's entries: a large
                                      // churn concentrates on a few clusters)
 
@@ -1807,7 +1807,7 @@ __device__ __forceinline__ void inc_block_sum(double (&v)[NV], double* red) {
 // compacted in order through LDS -- and folded into a partial (sums per
 // dimension; the cost terms, count and norm sums as scalars).  Unit weights.
 constexpr int kIncScan = 8;
-constexpr int kIncSplit = 4;
+constexpr int kIncSplit = 8;
 constexpr int kIncPs = 6;   // scalars per partial: dq, |dq|, count, sum |x| signed, sum |x|, entries
 template <int NJ>
 __global__ __launch_bounds__(256) void k_inc_part(
@@ -2022,7 +2022,7 @@ __global__ __launch_bounds__(256) void k_inc_combine(
 
 // Single block: the clusters' costs and error bounds summed in a fixed
 // tree; the incremental result stands when no cluster is flagged and the
-// bound is within 2^-42 of the cost, else the gates switch to the full pass.
+// bound is within 2^-40 of the cost, else the gates switch to the full pass.
 __global__ __launch_bounds__(256) void k_inc_check(const double* __restrict__ ccost,
                                                    const double* __restrict__ cerr,
                                                    const int* __restrict__ cbad, int k,
@@ -2039,7 +2039,7 @@ __global__ __launch_bounds__(256) void k_inc_check(const double* __restrict__ cc
   }
   inc_block_sum<3>(v, red);
   if (threadIdx.x == 0) {
-    const bool ok = v[2] == 0.0 && v[1] <= 0x1p-42 * fabs(v[0]) && fabs(v[0]) < INFINITY;
+    const bool ok = v[2] == 0.0 && v[1] <= 0x1p-40 * fabs(v[0]) && fabs(v[0]) < INFINITY;
     tot[0] = v[0];
     tot[1] = v[1];
     if (ok) {

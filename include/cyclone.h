@@ -144,9 +144,9 @@ int cyc_kmeans_rows_bounds_rechecked(cyc_kmeans_rows rows, int64_t* rechecked_ro
  * off).  Applies with the carried bounds, weights == NULL and cost == NULL
  * (no per-row costs).  The rows object keeps each cluster's sums, count and
  * the sum of squared distances to a reference point.  A call whose moved rows
- * are at most n / 8 updates them by those rows alone.  The cost for the call's
+ * are at most n / 16 updates them by those rows alone.  The cost for the call's
  * centers then comes from Q + 2 (P - c).(S - W P) + W |P - c|^2, with its
- * rounding bounded on the device.  A bound above 2^-42 of the cost, too many
+ * rounding bounded on the device.  A bound above 2^-40 of the cost, too many
  * moved rows or no prior state run the full pass over every row (which resets
  * the state).  The caller's buffers receive sums, weights and cost either way;
  * the assignments are unaffected.  Replaces nothing in the reference: its
