@@ -286,7 +286,8 @@ class KMeansWorkload:
     kernel = "k_chunk_sums"
     kernels = ("k_kmeans_screen1", "k_kmeans_refine2", "k_kmeans_screen2", "k_kmeans_cands3",
                "k_kmeans_cands", "k_kmeans_screen3", "k_kmeans_compact", "k_kmeans_assign_fp64",
-               "k_kmeans_bounds", "k_kmeans_recheck", "k_kmeans_inc", "k_chunk_sums")
+               "k_kmeans_bounds", "k_kmeans_recheck", "k_kmeans_inc", "k_kmeans_exact",
+               "k_chunk_sums")
     pmc_names = {"k_kmeans_screen1": "k_screen32_l1", "k_kmeans_screen2": "k_screen32_l2",
                  "k_kmeans_refine2": "k_screen32r", "k_chunk_sums": "k_chunk_sums_fast",
                  "k_kmeans_recheck": "k_screen_cands3_rc"}

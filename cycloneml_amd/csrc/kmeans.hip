@@ -971,6 +971,119 @@ __global__ __launch_bounds__(kS3Threads, 2) void k_kmeans_assign3(
   }
 }
 
+// The exact tier for a short queue (<= kExactCap rows, the usual few): the
+// distances of one row to all k centers spread over ceil(k / 256)
+// workgroups -- one thread per center, the same sequential sqdist as
+// k_assign_exact -- into dist (kExactCap x kpad), then one wave per row
+// replays the reference loop over them (k_exact_replay).  One workgroup per
+// row streamed all k centers' coordinates through a single CU (~2 MB at
+// k = 1024, d = 256: ~80 us for one row); spread over workgroups the queue
+// finishes in a few microseconds.  A longer queue takes k_assign_exact.
+constexpr int kExactCap = 512;
+
+__global__ __launch_bounds__(256) void k_exact_dist(const double* __restrict__ X, int d,
+                                                    const double* __restrict__ Ct, int kpad, int k,
+                                                    const int32_t* __restrict__ slowList,
+                                                    const unsigned int* __restrict__ slowCount,
+                                                    double* __restrict__ dist) {
+  __shared__ double xs[1280];
+  const unsigned cnt = *slowCount;
+  const unsigned idx = blockIdx.y;
+  if (cnt > (unsigned)kExactCap || idx >= cnt) return;
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x * 256 + tid;
+  const int64_t r = slowList[idx];
+  const double* x = X + r * d;
+  const bool xl = d <= 1280;
+  if (xl)
+    for (int j = tid; j < d; j += 256) xs[j] = x[j];
+  __syncthreads();
+  const double* xv = xl ? xs : x;
+  double acc = 0.0;
+  // 16 dimensions' loads out before their adds (the adds are sequential)
+  for (int j0 = 0; j0 < d; j0 += 16) {
+    double cv[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj)
+      cv[jj] = (j0 + jj < d && c < k) ? Ct[(int64_t)(j0 + jj) * kpad + c] : 0.0;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      if (j0 + jj < d) {
+        const double sc = dsub(cv[jj], xv[j0 + jj]);
+        acc = dadd(acc, dmul(sc, sc));
+      }
+    }
+  }
+  if (c < k) dist[(int64_t)idx * kpad + c] = acc;
+}
+
+__global__ __launch_bounds__(64) void k_exact_replay(const double* __restrict__ X,
+                                                     const double* __restrict__ xnorm, int d,
+                                                     int kpad, const double* __restrict__ cnorm,
+                                                     int k, const double* __restrict__ stats,
+                                                     const int32_t* __restrict__ slowList,
+                                                     const unsigned int* __restrict__ slowCount,
+                                                     const double* __restrict__ dist,
+                                                     int32_t* __restrict__ assign,
+                                                     double* __restrict__ cost, int exactNorm) {
+  const unsigned cnt = *slowCount;
+  const unsigned idx = blockIdx.x;
+  if (cnt > (unsigned)kExactCap || idx >= cnt) return;
+  const int lane = threadIdx.x;
+  const int64_t r = slowList[idx];
+  const bool ns = stats == nullptr;
+  // the reference's Vectors.norm in index order when the caller's norms are
+  // the row image's (k_assign_exact)
+  double xn = 0.0;
+  if (exactNorm) {
+    if (lane == 0) xn = seq_norm2(X + r * d, d);
+    xn = __shfl(xn, 0);
+  } else {
+    xn = xnorm[r];
+  }
+  const double* dds = dist + (int64_t)idx * kpad;
+  double best = __builtin_inf();
+  int bi = 0;
+  bool done = false;
+  int first = 0;
+  if (!ns) {
+    best = dds[0];                      // :286
+    done = best < stats[0];             // :287
+    first = 1;
+  }
+  for (int i0 = first; !done && i0 < k; i0 += 64) {
+    const int i = i0 + lane;
+    const bool valid = i < k;
+    double lb = __builtin_inf(), sii = 0.0, dd = 0.0;
+    if (valid) {
+      const double nd = dsub(cnorm[i], xn);     // :294-295
+      lb = dmul(nd, nd);
+      sii = ns ? 0.0 : stats[iut(i, i)];
+      dd = dds[i];
+    }
+    int pos = 0;
+    for (;;) {
+      const bool visit = valid && lane >= pos && lb < best && (ns || stats[iut(i, bi)] < best);
+      const bool brk = !ns && visit && dd < sii;
+      const bool ev = visit && (brk || dd < best);
+      const unsigned long long m = __ballot(ev);
+      if (!m) break;
+      const int f = __ffsll((long long)m) - 1;
+      best = __shfl(dd, f);
+      bi = i0 + f;
+      if (__shfl((int)brk, f)) {
+        done = true;
+        break;
+      }
+      pos = f + 1;
+    }
+  }
+  if (lane == 0) {
+    assign[r] = bi;
+    if (cost) cost[r] = best;
+  }
+}
+
 // EuclideanDistanceMeasure.findClosest with statistics, DistanceMeasure.scala:
 // 282-313, for the rows the screens could not decide.  One workgroup per
 // queued row: the exact sequential sqdist (Vectors.scala:580-587, the same
@@ -994,7 +1107,7 @@ __global__ __launch_bounds__(256) void k_assign_exact(
     const double* __restrict__ cnorm, int k,
     const double* __restrict__ stats, const int32_t* __restrict__ slowList,
     const unsigned int* __restrict__ slowCount, int32_t* __restrict__ assign,
-    double* __restrict__ cost, int exactNorm) {
+    double* __restrict__ cost, int exactNorm, unsigned int skipUpTo) {
   // One workgroup per listed row.  A distance is a pure function of (center,
   // row), so the workgroup first computes Vectors.sqdist(center, x) -- in
   // order j = 0..d-1 (Vectors.scala:580-587) -- for a chunk of 1024 centers
@@ -1006,6 +1119,7 @@ __global__ __launch_bounds__(256) void k_assign_exact(
   __shared__ int doneS;
   __shared__ double xnS;
   const unsigned cnt = *slowCount;
+  if (cnt <= skipUpTo) return;   // the split kernels took the queue
   const int tid = threadIdx.x, lane = tid & 63;
   // stats == nullptr: findClosest(centers, point) (:318-340), best from +inf
   const bool ns = stats == nullptr;
@@ -2314,6 +2428,7 @@ struct cyc_kmeans_plan_s {
   std::mutex mu;
   cyc::DeviceBuffer ct, stats, dmin, segsum, slowList, slowCount, assignTmp, costTmp;
   cyc::DeviceBuffer hist, total, cstart, chunkStart, perm, part, pw, pc, ccost;
+  cyc::DeviceBuffer exactDist;   // k_exact_dist's distances (kExactCap x kpad)
   // require(norm1 >= 0.0 && norm2 >= 0.0) check (k_require_norms): device
   // result, its pinned host copy and the event that marks the copy landed
   cyc::DeviceBuffer req;
@@ -2641,6 +2756,45 @@ int stage_args(cyc_kmeans_plan p, int64_t n, bool useCa, cyc::km8::AppendStage& 
   return CYC_OK;
 }
 
+// The exact tier over the plan's slow queue: the split kernels for a queue of
+// <= kExactCap rows, k_assign_exact for a longer one; known = the queue's
+// length when the host has it (-1: decided on the device, both enqueued).
+int launch_exact(cyc_kmeans_plan p, const double* X, const double* xnorm, int64_t n,
+                 const double* C, const double* cnorm, const double* statsArg, int32_t* assign,
+                 double* cost, bool approxNorm, int64_t known, hipStream_t st) {
+  cyc::KernelTimer timer("k_kmeans_exact", st);
+  const int k = p->k, kpad = p->kpad;
+  const unsigned* cnt = (const unsigned*)p->slowCount.ptr;
+  static const bool splitOff = [] {   // CYC_KMEANS_EXACT_SPLIT=0: k_assign_exact alone
+    const char* e = std::getenv("CYC_KMEANS_EXACT_SPLIT");
+    return e && e[0] == '0';
+  }();
+  const bool split = !splitOff && p->d <= 1280 && (known < 0 || known <= kExactCap);
+  if (split) {
+    int rc;
+    if ((rc = p->exactDist.reserve(sizeof(double) * (size_t)kExactCap * kpad))) return rc;
+    const unsigned rowsMax = (unsigned)std::min<int64_t>(known < 0 ? n : known, kExactCap);
+    hipLaunchKernelGGL(k_exact_dist, dim3((unsigned)((k + 255) / 256), rowsMax), dim3(256), 0, st,
+                       X, p->d, (const double*)p->ct.ptr, kpad, k, (const int32_t*)p->slowList.ptr,
+                       cnt, (double*)p->exactDist.ptr);
+    CYC_LAUNCH_CHECK("k_exact_dist");
+    hipLaunchKernelGGL(k_exact_replay, dim3(rowsMax), dim3(64), 0, st, X, xnorm, p->d, kpad, cnorm,
+                       k, statsArg, (const int32_t*)p->slowList.ptr, cnt,
+                       (const double*)p->exactDist.ptr, assign, cost, approxNorm ? 1 : 0);
+    CYC_LAUNCH_CHECK("k_exact_replay");
+    if (known >= 0) return CYC_OK;
+  }
+  // the long queue (or no split): one workgroup per row, grid-stride
+  const unsigned grid = known >= 0 ? (unsigned)std::min<int64_t>(known, 4096)
+                                   : (unsigned)std::min<int64_t>((n + 3) / 4, 2048);
+  hipLaunchKernelGGL(k_assign_exact, dim3(grid), dim3(256), 0, st, X, xnorm, p->d, C,
+                     (const double*)p->ct.ptr, kpad, cnorm, k, statsArg,
+                     (const int32_t*)p->slowList.ptr, cnt, assign, cost, approxNorm ? 1 : 0,
+                     split ? (unsigned)kExactCap : 0u);
+  CYC_LAUNCH_CHECK("k_assign_exact");
+  return CYC_OK;
+}
+
 int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmeans_rows rows,
               int64_t n, const double* C, const double* cnorm, int32_t* assign, double* cost,
               int64_t* n_exact_out, hipStream_t st, bool nostats = false,
@@ -2733,22 +2887,12 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
     p->lastLimb3 = twoPass ? (int64_t)h_limb3 : -1;
     p->lastCands = twoPass ? (int64_t)h_cand : -1;
     p->lastCands2 = twoPass && p->cands3 ? (int64_t)h_cand2 : -1;
-    if (h_slow) {
-      hipLaunchKernelGGL(k_assign_exact, dim3((unsigned)std::min<unsigned>(h_slow, 4096)), dim3(256), 0, st, X, xnorm,
-                         p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm, p->k, statsArg,
-                         (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr,
-                         assign, cost, approxNorm ? 1 : 0);
-      CYC_LAUNCH_CHECK("k_assign_exact");
-    }
-  } else {
-    const unsigned grid = (unsigned)std::min<int64_t>((n + 3) / 4, 2048);
-    hipLaunchKernelGGL(k_assign_exact, dim3(grid), dim3(256), 0, st, X, xnorm,
-                       p->d, C, (const double*)p->ct.ptr, p->kpad, cnorm, p->k, statsArg,
-                       (const int32_t*)p->slowList.ptr, (const unsigned*)p->slowCount.ptr, assign,
-                       cost, approxNorm ? 1 : 0);
-    CYC_LAUNCH_CHECK("k_assign_exact");
+    if (h_slow)
+      return launch_exact(p, X, xnorm, n, C, cnorm, statsArg, assign, cost, approxNorm,
+                          (int64_t)h_slow, st);
+    return CYC_OK;
   }
-  return CYC_OK;
+  return launch_exact(p, X, xnorm, n, C, cnorm, statsArg, assign, cost, approxNorm, -1, st);
 }
 
 // Enqueue k_require_norms and the copy of its result; require_check reads it
