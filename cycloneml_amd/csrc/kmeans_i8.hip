@@ -2262,6 +2262,198 @@ __global__ __launch_bounds__(256) void k_screen_cands3(
   }
 }
 
+// The re-check of the carried candidate sets and neighbourhoods (the rows of
+// bounds_filter's list; k_screen_cands3<.., RC>'s arithmetic, bit for bit)
+// in two phases per batch of kRcBatch listed rows.  Phase A, 2S lanes a row
+// as in k_screen_cands3: the limb products of the row's <= kCandMax
+// candidates, their f32 lower bounds L, and the row's best two, its
+// anchor's bound and its flags into LDS.  Phase B, one row a lane: the fp64
+// certification, the outside-bound test, the bounds and the state.  In
+// k_screen_cands3 every lane of a row ran that fp64 tail (~170 f64 of ~700
+// VALU instructions a 4-row step): the kernel was VALU-issue bound (neither
+// five waves per SIMD nor rows grouped by center changed its time).
+constexpr int kRcBatch = 256;
+template <int S>
+__global__ __launch_bounds__(kRcBatch) void k_recheck(
+    const uint4* __restrict__ Xq, const int2* __restrict__ meta, const double* __restrict__ xnorm,
+    int d, const uint4* __restrict__ Cr, const float* __restrict__ cq,
+    const double* __restrict__ g, const double* __restrict__ cnorm,
+    const CenterParams* __restrict__ prm, const int32_t* __restrict__ candRows,
+    const unsigned int* __restrict__ candCount, int32_t* __restrict__ assign,
+    float2* __restrict__ bnd, float* __restrict__ lncA, int32_t* __restrict__ sets,
+    unsigned char* __restrict__ state, const DriftParams* __restrict__ dp,
+    const int32_t* __restrict__ nbr, const float* __restrict__ nbrR) {
+  constexpr int P16 = 2 * S;        // lanes per row (16-byte pieces of a limb plane)
+  constexpr int RPW = 64 / P16;     // rows per wave and step; P16 steps fill a wave's 64 slots
+  __shared__ int sRow[kRcBatch], sI1[kRcBatch], sA0[kRcBatch], sMx[kRcBatch], sMy[kRcBatch],
+      sFl[kRcBatch];
+  __shared__ float sL1[kRcBatch], sL2[kRcBatch], sLA[kRcBatch], sCq[kRcBatch];
+  const unsigned cnt = *candCount;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, q = lane / P16, li = lane % P16;
+  const CenterParams P = *prm;
+  const auto cR = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)Cr, (short)0, (int)std::min<int64_t>((int64_t)P.k * 3 * P16 * 16, 0x7fffffff),
+      0x00020000);
+  for (unsigned bb = blockIdx.x * kRcBatch; bb < cnt; bb += gridDim.x * kRcBatch) {
+    // ---- phase A
+    for (int gi = 0; gi < P16; ++gi) {
+      const int slot = wave * 64 + gi * RPW + q;
+      const unsigned idx = bb + slot;
+      const bool live = idx < cnt;
+      const int32_t rw = live ? candRows[idx] : 0;
+      const bool nbrMode = rw < 0;   // ~row: the neighbourhood of its center
+      const int64_t row = nbrMode ? ~(int64_t)rw : (int64_t)rw;
+      const int32_t* setp = nbrMode ? nbr + (size_t)assign[row] * kCandMax
+                                    : sets + (size_t)row * kCandMax;
+      int ci[kCandMax];
+#pragma unroll
+      for (int i = 0; i < kCandMax; ++i) ci[i] = live ? setp[i] : -1;
+      const uint4* xr = Xq + row * (3 * P16) + li;
+      const uint4 xa = xr[0], xb = xr[P16], xc = xr[2 * P16];
+      const int2 mt = live ? meta[row] : make_int2(INT_MIN, 0);
+      float cqv[kCandMax];
+#pragma unroll
+      for (int i = 0; i < kCandMax; ++i) cqv[i] = cq[(ci[i] >= 0 && ci[i] < P.k) ? ci[i] : 0];
+      // T = 2^7 S1 + S2 summed per lane (integers: exact in any order; the
+      // row's total is k_screen_cands3's T), and S3
+      int tt[kCandMax], s3[kCandMax];
+#pragma unroll
+      for (int i = 0; i < kCandMax; ++i) {
+        const int c = ci[i];
+        const unsigned off = (c >= 0 && c < P.k) ? (unsigned)(c * 3 * P16 + li) * 16u : 0x80000000u;
+        const uint4 ca = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(cR, (int)off, 0, 0));
+        const uint4 cb = __builtin_bit_cast(
+            uint4, __builtin_amdgcn_raw_buffer_load_b128(cR, (int)(off + 16u * P16), 0, 0));
+        const uint4 cc = __builtin_bit_cast(
+            uint4, __builtin_amdgcn_raw_buffer_load_b128(cR, (int)(off + 32u * P16), 0, 0));
+        tt[i] = dot16(xb, ca, dot16(xa, cb, dot16(xa, ca, 0) * 128));
+        s3[i] = dot16(xc, ca, dot16(xb, cb, dot16(xa, cc, 0)));
+      }
+      if constexpr (P16 == 16) {
+#pragma unroll
+        for (int i = 0; i < kCandMax; ++i) {
+          tt[i] = row16_isum(tt[i]);
+          s3[i] = row16_isum(s3[i]);
+        }
+      } else {
+#pragma unroll
+        for (int m = 1; m < P16; m <<= 1)
+#pragma unroll
+          for (int i = 0; i < kCandMax; ++i) {
+            tt[i] += __shfl_xor(tt[i], m);
+            s3[i] += __shfl_xor(s3[i], m);
+          }
+      }
+      // the three-limb bounds L = cq - F1 (T + S3 2^-7), rounded toward -inf.
+      // The empty asm statements pin every rounding operation between the
+      // two mode switches (the compiler does not order FP arithmetic against
+      // s_setreg: without them it scheduled five candidates' conversions and
+      // FMAs after the switch back)
+      __builtin_amdgcn_s_setreg(0x801, 2);
+#pragma unroll
+      for (int i = 0; i < kCandMax; ++i) asm volatile("" : "+v"(tt[i]), "+v"(s3[i]));
+      const float F1 = mt.x == INT_MIN ? 0.0f : __builtin_ldexpf(1.0f, mt.x + P.ec - 20);
+      float L1 = __builtin_inff(), L2 = __builtin_inff(), LA = __builtin_inff(), cqMax = 0.0f;
+      int I1 = -1;
+      bool bad = false;
+      // (branch-free: an empty slot's L = +inf changes none of L1, L2, I1)
+#pragma unroll
+      for (int i = 0; i < kCandMax; ++i) {
+        const int c = ci[i];
+        const bool ok = c >= 0 && c < P.k;
+        bad = bad || c >= P.k;   // a padding center
+        const float V = __builtin_fmaf((float)s3[i], 0x1p-7f, (float)tt[i]);
+        const float L = ok ? __builtin_fmaf(-F1, V, cqv[i]) : __builtin_inff();
+        if (i == 0) LA = L;
+        cqMax = ok ? __builtin_fmaxf(cqMax, __builtin_fabsf(cqv[i])) : cqMax;
+        const bool lt = L < L1;
+        L2 = __builtin_amdgcn_fmed3f(L1, L2, L);
+        I1 = lt ? c : I1;
+        L1 = lt ? L : L1;
+      }
+      asm volatile("" : "+v"(L1), "+v"(L2), "+v"(LA), "+v"(cqMax), "+v"(I1));
+      __builtin_amdgcn_s_setreg(0x801, 0);
+      if (li == 0) {
+        sRow[slot] = live ? (int)row : -1;
+        sI1[slot] = I1;
+        sA0[slot] = ci[0];
+        sMx[slot] = mt.x;
+        sMy[slot] = mt.y;
+        sFl[slot] = (bad ? 1 : 0) | (nbrMode ? 2 : 0);
+        sL1[slot] = L1;
+        sL2[slot] = L2;
+        sLA[slot] = LA;
+        sCq[slot] = cqMax;
+      }
+    }
+    __syncthreads();
+    // ---- phase B: row sRow[t]
+    const int row = sRow[t];
+    if (row >= 0) {
+      const int I1 = sI1[t], mx = sMx[t], fl = sFl[t];
+      const bool bad = fl & 1, nbrMode = fl & 2;
+      const double l1 = (double)sL1[t], l2 = (double)sL2[t];
+      const float cqMax = sCq[t];
+      bool decided = false;
+      if (P.ok && !bad && mx != INT_MIN && I1 >= 0 && __builtin_isfinite(l1)) {
+        const double xn = xnorm[row], cn = cnorm[I1];
+        const double gw = g[I1];
+        const double xx = xn * xn, cc = cn * cn;
+        const double n1 = (double)__int_as_float(sMy[t]);   // bounds |xh3|_1
+        const double fx = err_term(mx, n1, P.mu, d);
+        const double M = (4.0 * (fx + gw) + 2.0 * kEpsF * (xx + cc) +
+                          0x1p-20 * (__builtin_fabs(l1) + cc + 2.0 * gw) +
+                          0x1p-24 * (2.0 * (xx + cc) + __builtin_fabs(l1) +
+                                     __builtin_fmin(__builtin_fabs(l2), 0x1p120)) +
+                          0x1p-90) *
+                         (1.0 + 0x1p-30);
+        decided = !__builtin_isfinite(l2) || (l2 - l1) > M;
+        // every center outside the set at least lnc0 away (the carried bound,
+        // or the neighbourhood's), the other members at least l2
+        float lnc0 = lncA[row];
+        const double ub2 = bnd_ub_sq(xx, cc, l1, fx, gw, 0.0) + 0x1p-20 * (double)cqMax;
+        const int a0 = (sA0[t] >= 0 && sA0[t] < P.k) ? sA0[t] : 0;
+        if (nbrMode) {
+          // |x - c| >= |c - c_a| - |x - c_a| >= nbrR[a] - (the anchor's fresh upper bound)
+          const float LA = sLA[t];
+          const double cnA = cnorm[a0];
+          const double ua2 = __builtin_isfinite(LA)
+                                 ? bnd_ub_sq(xx, cnA * cnA, (double)LA, fx, g[a0], 0.0) +
+                                       0x1p-20 * (double)cqMax
+                                 : __builtin_inf();
+          const double Ln =
+              ((double)nbrR[a0] - __builtin_sqrt(ua2) * (1.0 + 0x1p-50)) * (1.0 - 0x1p-50);
+          lnc0 = Ln > 0.0 ? fdown(Ln) : -1.0f;
+        }
+        if (decided) {
+          // above the winner by the reference's slack (the filter's test)
+          const double L = (double)lnc0, tau = 0x1p-29 * (xx + dp->cmax2) + 0x1p-48 * (L * L + ub2);
+          decided = lnc0 >= 0.0f && !dp->bad && L * L - ub2 > tau;
+        }
+        if (decided) {
+          const float ub = bnd_dist_up(ub2);
+          // (l2 = +inf: a set of one, nothing but the outside bound)
+          const float lb = __builtin_isfinite(l2)
+                               ? bnd_dist_dn(bnd_lb_sq(xx, l2, fx, 0.0, 0x1p-20 * (double)cqMax))
+                               : __builtin_inff();
+          bnd[row] = ub < 0x1p120f ? make_float2(ub, __builtin_fminf(lb, lnc0))
+                                   : make_float2(-1.0f, -1.0f);
+          if (nbrMode && ub < 0x1p120f) {
+            // the neighbourhood (slot 0: a itself) becomes the row's carried set
+            lncA[row] = lnc0;
+#pragma unroll
+            for (int i = 0; i < kCandMax; ++i)
+              sets[(size_t)row * kCandMax + i] = nbr[(size_t)a0 * kCandMax + i];
+          }
+        }
+      }
+      if (decided) assign[row] = I1;
+      state[row] = decided ? 0 : 1;
+    }
+    __syncthreads();   // the records are rewritten by the next batch
+  }
+}
+
 template <int S>
 int launch_cands3(const CandArgs& ca, const void* img, const int2* meta, const double* xnorm,
                   int64_t n, int d, const void* Cb, const float* cq, const double* g,
@@ -2440,14 +2632,30 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
     if (bd && bd->rcRows) {
       {
         KernelTimer timer("k_kmeans_recheck", st);
-        const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 127) / 128, 4096));
-        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen_cands3<S, 16, true>), dim3(grid), dim3(256), 0,
-                           st, (const uint4*)img, meta, xnorm, d,
-                           (const uint4*)Cb + (size_t)ktp * S * 3 * 64, cq, g, cnorm, prm,
-                           bd->rcRows, (const int32_t*)bd->sets, bd->rcCount, assign, nullptr,
-                           nullptr, nullptr, 0u, bd->ub_lb, bd->lnc, bd->sets, bd->state, bd->dp,
-                           bd->nbr, bd->nbrR);
-        CYC_LAUNCH_CHECK("k_screen_cands3 (re-check)");
+        // CYC_KMEANS_RECHECK=1: the one-phase form (k_screen_cands3<.., true>)
+        static const bool onePhase = [] {
+          const char* e = std::getenv("CYC_KMEANS_RECHECK");
+          return e && e[0] == '1';
+        }();
+        if (onePhase) {
+          const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 127) / 128, 4096));
+          hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen_cands3<S, 16, true>), dim3(grid), dim3(256), 0,
+                             st, (const uint4*)img, meta, xnorm, d,
+                             (const uint4*)Cb + (size_t)ktp * S * 3 * 64, cq, g, cnorm, prm,
+                             bd->rcRows, (const int32_t*)bd->sets, bd->rcCount, assign, nullptr,
+                             nullptr, nullptr, 0u, bd->ub_lb, bd->lnc, bd->sets, bd->state, bd->dp,
+                             bd->nbr, bd->nbrR);
+          CYC_LAUNCH_CHECK("k_screen_cands3 (re-check)");
+        } else {
+          const unsigned grid = (unsigned)std::max<int64_t>(
+              1, std::min<int64_t>((n + kRcBatch - 1) / kRcBatch, 2048));
+          hipLaunchKernelGGL(HIP_KERNEL_NAME(k_recheck<S>), dim3(grid), dim3(kRcBatch), 0, st,
+                             (const uint4*)img, meta, xnorm, d,
+                             (const uint4*)Cb + (size_t)ktp * S * 3 * 64, cq, g, cnorm, prm,
+                             bd->rcRows, bd->rcCount, assign, bd->ub_lb, bd->lnc, bd->sets,
+                             bd->state, bd->dp, bd->nbr, bd->nbrR);
+          CYC_LAUNCH_CHECK("k_recheck");
+        }
       }
       if (bd->dump) dump_dev("state_rc", bd->state, (size_t)bd->n, st);
       if ((rc = bounds_collect(*bd, st))) return rc;
