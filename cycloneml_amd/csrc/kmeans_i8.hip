@@ -2283,66 +2283,88 @@ __global__ __launch_bounds__(kRcBatch) void k_recheck(
     float2* __restrict__ bnd, float* __restrict__ lncA, int32_t* __restrict__ sets,
     unsigned char* __restrict__ state, const DriftParams* __restrict__ dp,
     const int32_t* __restrict__ nbr, const float* __restrict__ nbrR) {
-  constexpr int P16 = 2 * S;        // lanes per row (16-byte pieces of a limb plane)
-  constexpr int RPW = 64 / P16;     // rows per wave and step; P16 steps fill a wave's 64 slots
+  constexpr int P16 = 2 * S;        // 16-byte pieces of a limb plane
+  constexpr int LPR = 8;            // lanes per row, PPL pieces each
+  constexpr int PPL = P16 / LPR;
+  constexpr int RPW = 64 / LPR;     // rows per wave and step; LPR steps fill a wave's 64 slots
+  static_assert(P16 % LPR == 0, "whole pieces per lane");
   __shared__ int sRow[kRcBatch], sI1[kRcBatch], sA0[kRcBatch], sMx[kRcBatch], sMy[kRcBatch],
       sFl[kRcBatch];
   __shared__ float sL1[kRcBatch], sL2[kRcBatch], sLA[kRcBatch], sCq[kRcBatch];
   const unsigned cnt = *candCount;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, q = lane / P16, li = lane % P16;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, q = lane / LPR, li = lane % LPR;
   const CenterParams P = *prm;
   const auto cR = __builtin_amdgcn_make_buffer_rsrc(
       (void*)Cr, (short)0, (int)std::min<int64_t>((int64_t)P.k * 3 * P16 * 16, 0x7fffffff),
       0x00020000);
   for (unsigned bb = blockIdx.x * kRcBatch; bb < cnt; bb += gridDim.x * kRcBatch) {
     // ---- phase A
-    for (int gi = 0; gi < P16; ++gi) {
+    for (int gi = 0; gi < LPR; ++gi) {
       const int slot = wave * 64 + gi * RPW + q;
       const unsigned idx = bb + slot;
       const bool live = idx < cnt;
-      const int32_t rw = live ? candRows[idx] : 0;
+      // (a slot past the list reads the batch's first entry, then drops it:
+      // every load below is unconditional)
+      const int32_t rw = candRows[live ? idx : bb];
       const bool nbrMode = rw < 0;   // ~row: the neighbourhood of its center
       const int64_t row = nbrMode ? ~(int64_t)rw : (int64_t)rw;
       const int32_t* setp = nbrMode ? nbr + (size_t)assign[row] * kCandMax
                                     : sets + (size_t)row * kCandMax;
       int ci[kCandMax];
+      static_assert(kCandMax % 2 == 0, "sets read as int2");
 #pragma unroll
-      for (int i = 0; i < kCandMax; ++i) ci[i] = live ? setp[i] : -1;
+      for (int i = 0; i < kCandMax; i += 2) {
+        const int2 v = *reinterpret_cast<const int2*>(setp + i);   // 8-byte aligned rows
+        ci[i] = live ? v.x : -1;
+        ci[i + 1] = live ? v.y : -1;
+      }
       const uint4* xr = Xq + row * (3 * P16) + li;
-      const uint4 xa = xr[0], xb = xr[P16], xc = xr[2 * P16];
-      const int2 mt = live ? meta[row] : make_int2(INT_MIN, 0);
+      uint4 xa[PPL], xb[PPL], xc[PPL];
+#pragma unroll
+      for (int j = 0; j < PPL; ++j) {
+        xa[j] = xr[j * LPR];
+        xb[j] = xr[P16 + j * LPR];
+        xc[j] = xr[2 * P16 + j * LPR];
+      }
+      const int2 mt0 = meta[row];
+      const int2 mt = live ? mt0 : make_int2(INT_MIN, 0);
       float cqv[kCandMax];
 #pragma unroll
-      for (int i = 0; i < kCandMax; ++i) cqv[i] = cq[(ci[i] >= 0 && ci[i] < P.k) ? ci[i] : 0];
+      for (int i = 0; i < kCandMax; ++i) cqv[i] = cq[(unsigned)ci[i] < (unsigned)P.k ? ci[i] : 0];
       // T = 2^7 S1 + S2 summed per lane (integers: exact in any order; the
       // row's total is k_screen_cands3's T), and S3
       int tt[kCandMax], s3[kCandMax];
 #pragma unroll
       for (int i = 0; i < kCandMax; ++i) {
         const int c = ci[i];
-        const unsigned off = (c >= 0 && c < P.k) ? (unsigned)(c * 3 * P16 + li) * 16u : 0x80000000u;
-        const uint4 ca = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(cR, (int)off, 0, 0));
-        const uint4 cb = __builtin_bit_cast(
-            uint4, __builtin_amdgcn_raw_buffer_load_b128(cR, (int)(off + 16u * P16), 0, 0));
-        const uint4 cc = __builtin_bit_cast(
-            uint4, __builtin_amdgcn_raw_buffer_load_b128(cR, (int)(off + 32u * P16), 0, 0));
-        tt[i] = dot16(xb, ca, dot16(xa, cb, dot16(xa, ca, 0) * 128));
-        s3[i] = dot16(xc, ca, dot16(xb, cb, dot16(xa, cc, 0)));
-      }
-      if constexpr (P16 == 16) {
+        // an empty slot reads zeros without a memory access (out of range)
+        const unsigned off =
+            (unsigned)c < (unsigned)P.k ? (unsigned)(c * 3 * P16 + li) * 16u : 0x80000000u;
+        int ti = 0, si = 0;
 #pragma unroll
-        for (int i = 0; i < kCandMax; ++i) {
-          tt[i] = row16_isum(tt[i]);
-          s3[i] = row16_isum(s3[i]);
+        for (int j = 0; j < PPL; ++j) {
+          const unsigned o = off + 16u * LPR * j;
+          const uint4 ca = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(cR, (int)o, 0, 0));
+          const uint4 cb = __builtin_bit_cast(
+              uint4, __builtin_amdgcn_raw_buffer_load_b128(cR, (int)(o + 16u * P16), 0, 0));
+          const uint4 cc = __builtin_bit_cast(
+              uint4, __builtin_amdgcn_raw_buffer_load_b128(cR, (int)(o + 32u * P16), 0, 0));
+          ti = dot16(xb[j], ca, dot16(xa[j], cb, ti + dot16(xa[j], ca, 0) * 128));
+          si = dot16(xc[j], ca, dot16(xb[j], cb, dot16(xa[j], cc, si)));
         }
-      } else {
+        tt[i] = ti;
+        s3[i] = si;
+      }
+      // sums over the row's 8 lanes by DPP: quad_perm [1,0,3,2], [2,3,0,1],
+      // then row_half_mirror (lane i of a half with lane 7 - i: the other quad)
 #pragma unroll
-        for (int m = 1; m < P16; m <<= 1)
-#pragma unroll
-          for (int i = 0; i < kCandMax; ++i) {
-            tt[i] += __shfl_xor(tt[i], m);
-            s3[i] += __shfl_xor(s3[i], m);
-          }
+      for (int i = 0; i < kCandMax; ++i) {
+        tt[i] += __builtin_amdgcn_update_dpp(0, tt[i], 0xB1, 0xF, 0xF, false);
+        s3[i] += __builtin_amdgcn_update_dpp(0, s3[i], 0xB1, 0xF, 0xF, false);
+        tt[i] += __builtin_amdgcn_update_dpp(0, tt[i], 0x4E, 0xF, 0xF, false);
+        s3[i] += __builtin_amdgcn_update_dpp(0, s3[i], 0x4E, 0xF, 0xF, false);
+        tt[i] += __builtin_amdgcn_update_dpp(0, tt[i], 0x141, 0xF, 0xF, false);
+        s3[i] += __builtin_amdgcn_update_dpp(0, s3[i], 0x141, 0xF, 0xF, false);
       }
       // the three-limb bounds L = cq - F1 (T + S3 2^-7), rounded toward -inf.
       // The empty asm statements pin every rounding operation between the
