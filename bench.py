@@ -290,7 +290,7 @@ class KMeansWorkload:
                "k_chunk_sums")
     pmc_names = {"k_kmeans_screen1": "k_screen32_l1", "k_kmeans_screen2": "k_screen32_l2",
                  "k_kmeans_refine2": "k_screen32r", "k_chunk_sums": "k_chunk_sums_fast",
-                 "k_kmeans_recheck": "k_screen_cands3_rc"}
+                 "k_kmeans_recheck": "k_recheck"}
 
     def __init__(self, n, dev, rank):
         import torch
