@@ -118,7 +118,12 @@ def pmc_traffic(workload, kernel, rows):
     profiled run's `_rows` (the same launch shape per step at equal rows);
     (None, None) when there is none."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")))
+    import re
+
+    def tag(f):   # r06ak after r06z after r06y: round, then suffix length, then suffix
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")), key=tag)
     for f in reversed(files):
         try:
             d = json.load(open(f))
@@ -290,7 +295,10 @@ class KMeansWorkload:
                "k_chunk_sums")
     pmc_names = {"k_kmeans_screen1": "k_screen32_l1", "k_kmeans_screen2": "k_screen32_l2",
                  "k_kmeans_refine2": "k_screen32r", "k_chunk_sums": "k_chunk_sums_fast",
-                 "k_kmeans_recheck": "k_recheck"}
+                 # the re-check's bytes scale with the rows the bounds list
+                 # (data-dependent per launch): a profiled run's per-dispatch
+                 # average is not this run's launch, so no PMC traffic
+                 "k_kmeans_recheck": None}
 
     def __init__(self, n, dev, rank):
         import torch
