@@ -2513,15 +2513,24 @@ int launch_cands(const CandArgs& ca, int64_t n, int d, int32_t* assign, int32_t*
 // block to finish (a completion counter in shard 0's spare slot) clears the
 // counters and advances *dstCount.  (A scan launch + a copy launch took ~5
 // us each, nine pairs per screen call.)
-__global__ __launch_bounds__(256) void k_shard_compact(unsigned int* __restrict__ counts,
-                                                       unsigned int cap,
-                                                       const int32_t* __restrict__ src,
-                                                       int32_t* __restrict__ dst, int width,
-                                                       const int32_t* __restrict__ src2,
-                                                       int32_t* __restrict__ dst2, int width2,
-                                                       unsigned int* __restrict__ dstCount) {
+struct CompactJob {
+  unsigned int* counts;
+  const int32_t* src;
+  int32_t* dst;
+  int width;
+  const int32_t* src2;
+  int32_t* dst2;
+  int width2;
+  unsigned int* dstCount;
+};
+constexpr int kMaxCompactJobs = 4;
+struct CompactJobs {
+  CompactJob j[kMaxCompactJobs];
+};
+__device__ __forceinline__ void shard_compact(const CompactJob& J, unsigned int cap) {
   __shared__ unsigned sb[2];
   const int j = blockIdx.y;
+  unsigned int* counts = J.counts;
   if (threadIdx.x < 64) {
     const int l = threadIdx.x;
     const unsigned c = counts[l * kShardStride];
@@ -2536,19 +2545,19 @@ __global__ __launch_bounds__(256) void k_shard_compact(unsigned int* __restrict_
       sb[1] = c;
     }
   }
-  const unsigned old = *dstCount;   // advanced only by the last block
+  const unsigned old = *J.dstCount;   // advanced only by the last block
   __syncthreads();
-  if (dst) {
+  if (J.dst) {
     const size_t base = (size_t)old + sb[0], c = sb[1];
     const size_t t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    const int32_t* s1 = src + (size_t)j * cap * width;
-    int32_t* d1 = dst + base * width;
-    for (size_t i = t0; i < c * width; i += stride) d1[i] = s1[i];
-    if (src2) {
-      const int32_t* s2 = src2 + (size_t)j * cap * width2;
-      int32_t* d2 = dst2 + base * width2;
-      for (size_t i = t0; i < c * width2; i += stride) d2[i] = s2[i];
+    const int32_t* s1 = J.src + (size_t)j * cap * J.width;
+    int32_t* d1 = J.dst + base * J.width;
+    for (size_t i = t0; i < c * J.width; i += stride) d1[i] = s1[i];
+    if (J.src2) {
+      const int32_t* s2 = J.src2 + (size_t)j * cap * J.width2;
+      int32_t* d2 = J.dst2 + base * J.width2;
+      for (size_t i = t0; i < c * J.width2; i += stride) d2[i] = s2[i];
     }
   }
   __syncthreads();
@@ -2558,28 +2567,51 @@ __global__ __launch_bounds__(256) void k_shard_compact(unsigned int* __restrict_
     // kernel boundary
     const unsigned blocks = gridDim.x * gridDim.y;
     if (atomicAdd(&counts[3], 1u) == blocks - 1) {
-      // every block has read the counters and *dstCount
+      // every block of this job has read the counters and *dstCount
       unsigned tot = 0;
       for (int l = 0; l < kShards; ++l) {
         tot += counts[l * kShardStride];
         counts[l * kShardStride] = 0u;
       }
-      *dstCount = old + tot;
+      *J.dstCount = old + tot;
       counts[3] = 0u;
     }
   }
+}
+// Sharded appends, compacted (kmeans_i8.hpp) in ONE launch: every block's
+// first wave scans the kShards counters (64 values) for its shard's base
+// behind *dstCount, the block copies that shard's entries there, and the last
+// block to finish (a completion counter in shard 0's spare slot) clears the
+// counters and advances *dstCount.  (A scan launch + a copy launch took ~5
+// us each, nine pairs per screen call.)  Up to kMaxCompactJobs independent
+// compactions (distinct count sets and destination counters) share one
+// launch, one per blockIdx.z.
+__global__ __launch_bounds__(256) void k_shard_compact(CompactJobs jobs, unsigned int cap) {
+  shard_compact(jobs.j[blockIdx.z], cap);
+}
+
+int compact_jobs(const CompactJob* jobs, int nj, unsigned int cap, hipStream_t st) {
+  if (nj <= 0) return CYC_OK;
+  KernelTimer timer("k_kmeans_compact", st);
+  CompactJobs J{};
+  bool anyDst = false;
+  for (int i = 0; i < nj; ++i) {
+    J.j[i] = jobs[i];
+    anyDst = anyDst || jobs[i].dst;
+  }
+  // two blocks per shard: the completion counter's returning atomics
+  // serialise (~11 ns each), 16 per shard measured 3x the two launches
+  hipLaunchKernelGGL(k_shard_compact, anyDst ? dim3(2, kShards, nj) : dim3(1, 1, nj), dim3(256), 0,
+                     st, J, cap);
+  CYC_LAUNCH_CHECK("k_shard_compact");
+  return CYC_OK;
 }
 
 int compact(unsigned int* counts, unsigned int cap, const int32_t* src, int32_t* dst, int width,
             const int32_t* src2, int32_t* dst2, int width2, unsigned int* dstCount,
             hipStream_t st) {
-  KernelTimer timer("k_kmeans_compact", st);
-  // two blocks per shard: the completion counter's returning atomics
-  // serialise (~11 ns each), 16 per shard measured 3x the two launches
-  hipLaunchKernelGGL(k_shard_compact, dst ? dim3(2, kShards) : dim3(1, 1), dim3(256), 0, st,
-                     counts, cap, src, dst, width, src2, dst2, width2, dstCount);
-  CYC_LAUNCH_CHECK("k_shard_compact");
-  return CYC_OK;
+  const CompactJob j{counts, src, dst, width, src2, dst2, width2, dstCount};
+  return compact_jobs(&j, 1, cap, st);
 }
 
 // Two-limb pass over every row; its undecided rows with a small candidate
@@ -2637,12 +2669,11 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
   // the two-limb kernels' outputs: list2 (rows) and the candidate lists
   auto compact2 = [&]() -> int {
     if (!sg) return CYC_OK;
-    int e;
-    if ((e = compact(sg->set(kSetRowsA), scap, sg->rowsA, list2, 1, nullptr, nullptr, 0,
-                     list2Count, st)))
-      return e;
-    return compact(sg->set(kSetCand), scap, sg->candRows, ca->candRows, 1, sg->cands, ca->cands,
-                   kCandMax, ca->candCount, st);
+    const CompactJob jb[2] = {
+        {sg->set(kSetRowsA), sg->rowsA, list2, 1, nullptr, nullptr, 0, list2Count},
+        {sg->set(kSetCand), sg->candRows, ca->candRows, 1, sg->cands, ca->cands, kCandMax,
+         ca->candCount}};
+    return compact_jobs(jb, 2, scap, st);
   };
   if (ra && ca) {
     // one-limb pass over every center; the two-limb refinement over the
@@ -2696,11 +2727,14 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
           A(sg ? sg->cands : nullptr, ra->cand1), N(kSetCand, ra->cand1Count), scap,
           bd ? bd->ub_lb : nullptr);
     if (rc) return rc;
-    if (sg && ((rc = compact(sg->set(kSetRowsA), scap, sg->rowsA, ra->fullList, 1, nullptr,
-                             nullptr, 0, ra->fullCount, st)) ||
-               (rc = compact(sg->set(kSetCand), scap, sg->candRows, ra->cand1Rows, 1, sg->cands,
-                             ra->cand1, kCand1, ra->cand1Count, st))))
-      return rc;
+    if (sg) {
+      // (independent: distinct count sets and destinations, one launch)
+      const CompactJob jb[2] = {
+          {sg->set(kSetRowsA), sg->rowsA, ra->fullList, 1, nullptr, nullptr, 0, ra->fullCount},
+          {sg->set(kSetCand), sg->candRows, ra->cand1Rows, 1, sg->cands, ra->cand1, kCand1,
+           ra->cand1Count}};
+      if ((rc = compact_jobs(jb, 2, scap, st))) return rc;
+    }
     {
       KernelTimer timer("k_kmeans_refine2", st);
       hipLaunchKernelGGL(HIP_KERNEL_NAME(k_screen32r<S>), dim3((unsigned)((n + 127) / 128)),
@@ -2714,12 +2748,16 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
                          N(kSetStat, ra->fullCount + 1), scap, bd ? bd->ub_lb : nullptr);
       CYC_LAUNCH_CHECK("k_screen32r");
     }
-    if (sg && ((rc = compact2()) ||
-               (rc = compact(sg->set(kSetRowsB), scap, sg->rowsB, ra->fullList, 1, nullptr,
-                             nullptr, 0, ra->fullCount, st)) ||
-               (rc = compact(sg->set(kSetStat), scap, nullptr, nullptr, 0, nullptr, nullptr, 0,
-                             ra->fullCount + 1, st))))
-      return rc;
+    if (sg) {
+      // the refinement's four outputs: distinct count sets and counters
+      const CompactJob jb[4] = {
+          {sg->set(kSetRowsA), sg->rowsA, list2, 1, nullptr, nullptr, 0, list2Count},
+          {sg->set(kSetCand), sg->candRows, ca->candRows, 1, sg->cands, ca->cands, kCandMax,
+           ca->candCount},
+          {sg->set(kSetRowsB), sg->rowsB, ra->fullList, 1, nullptr, nullptr, 0, ra->fullCount},
+          {sg->set(kSetStat), nullptr, nullptr, 0, nullptr, nullptr, 0, ra->fullCount + 1}};
+      if ((rc = compact_jobs(jb, 4, scap, st))) return rc;
+    }
     rc = launch_screen32<S, W, 2, true>(
         img, meta, xnorm, n, d, Cb, cq + (size_t)ktp * 32, g + (size_t)ktp * 32, cnorm, prm, ktp,
         ra->fullList, ra->fullCount, assign, A(sg ? sg->rowsA : nullptr, list2),
