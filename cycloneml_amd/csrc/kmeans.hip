@@ -111,6 +111,22 @@ __global__ void k_fill_u64(unsigned long long* __restrict__ p, int n, unsigned l
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = v;
 }
+// k_center_transpose and the statistics' dmin fill in one launch
+__global__ void k_center_transpose_fill(const double* __restrict__ C, int k, int d, int d4,
+                                        int kpad, double* __restrict__ Ct,
+                                        unsigned long long* __restrict__ p, unsigned long long v) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < k) p[idx] = v;
+  const int64_t total = (int64_t)d4 * kpad;
+  if (idx >= total) return;
+  const int j = (int)(idx / kpad), i = (int)(idx % kpad);
+  Ct[idx] = (i < k && j < d) ? C[(int64_t)i * d + j] : 0.0;
+}
+// two counters zeroed by one launch (two fills before)
+__global__ void k_zero2(unsigned int* __restrict__ a, unsigned int* __restrict__ b) {
+  if (threadIdx.x == 0) *a = 0u;
+  if (threadIdx.x == 1 && b) *b = 0u;
+}
 
 // computeStatistics pairs (DistanceMeasure.scala:55-66, Euclidean :275-277):
 // s = 0.25 * distance * distance, distance = Math.sqrt(sqdist(c_i, c_j)).
@@ -2531,16 +2547,17 @@ int launch_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, int64
 
 int do_stats(cyc_kmeans_plan p, const double* C, hipStream_t st) {
   const int k = p->k, d = p->d;
-  if (p->dense_ok) {
-    int64_t total = (int64_t)p->d4 * p->kpad;
-    hipLaunchKernelGGL(k_center_transpose, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       st, C, k, d, p->d4, p->kpad, (double*)p->ct.ptr);
-    CYC_LAUNCH_CHECK("k_center_transpose");
-  }
   const int tps = (k + kStT - 1) / kStT;
   unsigned long long* dmin = (unsigned long long*)p->dmin.ptr;
-  hipLaunchKernelGGL(k_fill_u64, dim3((k + 255) / 256), dim3(256), 0, st, dmin, k, kInfBits);
-  CYC_LAUNCH_CHECK("k_fill_u64");
+  if (p->dense_ok) {
+    const int64_t total = std::max<int64_t>((int64_t)p->d4 * p->kpad, k);
+    hipLaunchKernelGGL(k_center_transpose_fill, dim3((unsigned)((total + 255) / 256)), dim3(256),
+                       0, st, C, k, d, p->d4, p->kpad, (double*)p->ct.ptr, dmin, kInfBits);
+    CYC_LAUNCH_CHECK("k_center_transpose_fill");
+  } else {
+    hipLaunchKernelGGL(k_fill_u64, dim3((k + 255) / 256), dim3(256), 0, st, dmin, k, kInfBits);
+    CYC_LAUNCH_CHECK("k_fill_u64");
+  }
   hipLaunchKernelGGL(k_stats_pairs, dim3((unsigned)(tps * (tps + 1) / 2)), dim3(256), 0, st, C, k,
                      d, tps, (double*)p->stats.ptr, dmin);
   CYC_LAUNCH_CHECK("k_stats_pairs");
@@ -2803,13 +2820,16 @@ int do_assign(cyc_kmeans_plan p, const double* X, const double* xnorm, cyc_kmean
   // screens certify only rows whose winner both loops return, so only the
   // exact tier differs (no statistics prunes, best starts at +inf)
   const double* statsArg = nostats ? nullptr : (const double*)p->stats.ptr;
-  CYC_HIP(hipMemsetAsync(p->slowCount.ptr, 0, sizeof(unsigned int), st));
+  const bool i8 = rows && rows->usable;
+  // slowCount (and list3Count for the i8 tier) zeroed by one launch
+  hipLaunchKernelGGL(k_zero2, dim3(1), dim3(64), 0, st, (unsigned int*)p->slowCount.ptr,
+                     i8 ? (unsigned int*)p->list3Count.ptr : nullptr);
+  CYC_LAUNCH_CHECK("k_zero2");
   int rc = CYC_OK;
   const int32_t* rowList = nullptr;
   const unsigned int* rowCount = nullptr;
-  if (rows && rows->usable) {
+  if (i8) {
     // tier 1: exact-integer i8 screen over every row; undecided rows -> list3
-    CYC_HIP(hipMemsetAsync(p->list3Count.ptr, 0, sizeof(unsigned int), st));
     if ((rc = cyc::km8::centers_prepare(C, cnorm, p->k, p->d, p->ktp8, p->cb8.ptr,
                                         (float*)p->cq8.ptr, (double*)p->g8.ptr,
                                         (cyc::km8::CenterParams*)p->prm8.ptr,
