@@ -2476,6 +2476,7 @@ struct cyc_kmeans_rows_s {
   bool bValid = false;
   int bk = 0;
   cyc::DeviceBuffer bnd, bAssign, bCp, bDelta, bCcs, bPrm, bTmp, bCount, bList, bListCount, bCum;
+  cyc::DeviceBuffer bTmp2, bCount2;   // the filter's state-1 list (k8::Bounds::collected)
   // carried candidate sets (kmeans_i8.hpp Bounds): outside bound, sets,
   // per-row state, the re-check list, its count and running total
   cyc::DeviceBuffer bLnc, bSets, bState, bRc, bRcCount, bRcCum;
@@ -2678,6 +2679,8 @@ int bounds_prepare(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* C,
       (rc = rows->bPrm.reserve(sizeof(k8::DriftParams))) ||
       (rc = rows->bTmp.reserve(sizeof(int32_t) * (size_t)n)) ||
       (rc = rows->bCount.reserve(sizeof(unsigned int) * (size_t)(k8::bounds_blocks(n) + 1))) ||
+      (rc = rows->bTmp2.reserve(sizeof(int32_t) * (size_t)n)) ||
+      (rc = rows->bCount2.reserve(sizeof(unsigned int) * (size_t)(k8::bounds_blocks(n) + 1))) ||
       (rc = rows->bList.reserve(sizeof(int32_t) * (size_t)n)) ||
       (rc = rows->bListCount.reserve(64)) ||
       (rc = rows->bLnc.reserve(sizeof(float) * (size_t)n)) ||
@@ -2711,15 +2714,23 @@ int bounds_prepare(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* C,
   bd.n = n;
   if (carry) {
     // kept rows, the re-check list (screen: the re-check, then the state-1
-    // rows collected into bList for the one-limb pass)
+    // rows collected into bList for the one-limb pass; with the two-phase
+    // re-check the filter lists its state-1 rows there itself and the
+    // re-check appends its failures)
+    const bool two = k8::recheck_two_phase();
     if ((rc = k8::bounds_filter((const int32_t*)rows->bAssign.ptr, (float2*)rows->bnd.ptr,
                                 bd.lnc, bd.state, xnorm, n, k, (const double*)rows->bDelta.ptr,
                                 bd.dp, bd.tmp, bd.bcount, (int32_t*)rows->bRc.ptr,
                                 (unsigned int*)rows->bRcCount.ptr,
                                 (unsigned long long*)rows->bRcCum.ptr,
                                 nbrOff() ? nullptr : (const double*)p->stats.ptr,
-                                (int32_t*)rows->bNbr.ptr, (float*)rows->bNbrR.ptr, st)))
+                                (int32_t*)rows->bNbr.ptr, (float*)rows->bNbrR.ptr, st,
+                                two ? (int32_t*)rows->bTmp2.ptr : nullptr,
+                                two ? (unsigned int*)rows->bCount2.ptr : nullptr,
+                                two ? bd.list : nullptr, two ? bd.listCount : nullptr,
+                                two ? bd.cum : nullptr)))
       return rc;
+    bd.collected = two;
     if (!nbrOff()) {
       bd.nbr = (const int32_t*)rows->bNbr.ptr;
       bd.nbrR = (const float*)rows->bNbrR.ptr;

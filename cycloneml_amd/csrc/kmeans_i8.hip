@@ -2282,9 +2282,12 @@ __global__ __launch_bounds__(kRcBatch) void k_recheck(
     const unsigned int* __restrict__ candCount, int32_t* __restrict__ assign,
     float2* __restrict__ bnd, float* __restrict__ lncA, int32_t* __restrict__ sets,
     unsigned char* __restrict__ state, const DriftParams* __restrict__ dp,
-    const int32_t* __restrict__ nbr, const float* __restrict__ nbrR) {
+    const int32_t* __restrict__ nbr, const float* __restrict__ nbrR,
+    int32_t* __restrict__ failList, unsigned int* __restrict__ failCount,
+    unsigned long long* __restrict__ failCum) {
   constexpr int P16 = 2 * S;        // 16-byte pieces of a limb plane
   constexpr int LPR = 8;            // lanes per row, PPL pieces each
+  __shared__ unsigned sFail, sFailBase;
   constexpr int PPL = P16 / LPR;
   constexpr int RPW = 64 / LPR;     // rows per wave and step; LPR steps fill a wave's 64 slots
   static_assert(P16 % LPR == 0, "whole pieces per lane");
@@ -2298,6 +2301,7 @@ __global__ __launch_bounds__(kRcBatch) void k_recheck(
       (void*)Cr, (short)0, (int)std::min<int64_t>((int64_t)P.k * 3 * P16 * 16, 0x7fffffff),
       0x00020000);
   for (unsigned bb = blockIdx.x * kRcBatch; bb < cnt; bb += gridDim.x * kRcBatch) {
+    if (t == 0) sFail = 0u;   // (ordered by the barrier after phase A)
     // ---- phase A
     for (int gi = 0; gi < LPR; ++gi) {
       const int slot = wave * 64 + gi * RPW + q;
@@ -2411,6 +2415,7 @@ __global__ __launch_bounds__(kRcBatch) void k_recheck(
     __syncthreads();
     // ---- phase B: row sRow[t]
     const int row = sRow[t];
+    unsigned rank = ~0u;   // this row's place among the batch's failures
     if (row >= 0) {
       const int I1 = sI1[t], mx = sMx[t], fl = sFl[t];
       const bool bad = fl & 1, nbrMode = fl & 2;
@@ -2471,6 +2476,18 @@ __global__ __launch_bounds__(kRcBatch) void k_recheck(
       }
       if (decided) assign[row] = I1;
       state[row] = decided ? 0 : 1;
+      if (failList && !decided) rank = atomicAdd(&sFail, 1u);
+    }
+    if (failList) {
+      // the failures behind the filter's state-1 rows in the screen's list:
+      // one reservation per workgroup and batch
+      __syncthreads();
+      if (t == 0 && sFail) {
+        sFailBase = atomicAdd(failCount, sFail);
+        atomicAdd(failCum, (unsigned long long)sFail);
+      }
+      __syncthreads();
+      if (rank != ~0u) failList[sFailBase + rank] = row;
     }
     __syncthreads();   // the records are rewritten by the next batch
   }
@@ -2706,12 +2723,15 @@ int screen32(const void* img, const int2* meta, const double* xnorm, int64_t n, 
                              (const uint4*)img, meta, xnorm, d,
                              (const uint4*)Cb + (size_t)ktp * S * 3 * 64, cq, g, cnorm, prm,
                              bd->rcRows, bd->rcCount, assign, bd->ub_lb, bd->lnc, bd->sets,
-                             bd->state, bd->dp, bd->nbr, bd->nbrR);
+                             bd->state, bd->dp, bd->nbr, bd->nbrR,
+                             bd->collected ? bd->list : nullptr,
+                             bd->collected ? bd->listCount : nullptr,
+                             bd->collected ? bd->cum : nullptr);
           CYC_LAUNCH_CHECK("k_recheck");
         }
       }
       if (bd->dump) dump_dev("state_rc", bd->state, (size_t)bd->n, st);
-      if ((rc = bounds_collect(*bd, st))) return rc;
+      if (!(bd->collected && recheck_two_phase()) && (rc = bounds_collect(*bd, st))) return rc;
     }
     if (bd && bd->rowsIn)
       rc = launch_screen32<S, W, 1, true>(
@@ -3058,8 +3078,11 @@ __global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict
                                                        const DriftParams* __restrict__ prm,
                                                        int32_t* __restrict__ tmp,
                                                        unsigned int* __restrict__ bcount,
-                                                       const float* __restrict__ nbrR) {
-  __shared__ unsigned wc[kBndIT * 4];
+                                                       const float* __restrict__ nbrR,
+                                                       int32_t* __restrict__ tmp2,
+                                                       unsigned int* __restrict__ bcount2) {
+  __shared__ unsigned wc[kBndIT * 4], wc2[kBndIT * 4];
+  unsigned long long masks2[kBndIT];
   const DriftParams P = *prm;
   unsigned long long flips[kBndIT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -3110,9 +3133,14 @@ __global__ __launch_bounds__(256) void k_bounds_filter(const int32_t* __restrict
     }
     masks[it] = __builtin_amdgcn_ballot_w64(st >= 2);
     flips[it] = __builtin_amdgcn_ballot_w64(st == 3);
-    if (lane == 0) wc[it * 4 + wave] = (unsigned)__builtin_popcountll(masks[it]);
+    masks2[it] = __builtin_amdgcn_ballot_w64(r < n && st == 1);
+    if (lane == 0) {
+      wc[it * 4 + wave] = (unsigned)__builtin_popcountll(masks[it]);
+      wc2[it * 4 + wave] = (unsigned)__builtin_popcountll(masks2[it]);
+    }
   }
   bnd_block_list(masks, wc, base, tmp, bcount, flips);
+  if (tmp2) bnd_block_list(masks2, wc2, base, tmp2, bcount2);
 }
 
 // The rows a full screen takes (state 1), listed as the filter lists its
@@ -3137,8 +3165,16 @@ __global__ __launch_bounds__(256) void k_bounds_collect(const unsigned char* __r
 // = the total, added to *cum.
 __global__ __launch_bounds__(1024) void k_bounds_scan(unsigned int* __restrict__ bcount, int64_t nb,
                                                       unsigned int* __restrict__ listCount,
-                                                      unsigned long long* __restrict__ cum) {
+                                                      unsigned long long* __restrict__ cum,
+                                                      unsigned int* __restrict__ bcount2 = nullptr,
+                                                      unsigned int* __restrict__ listCount2 = nullptr,
+                                                      unsigned long long* __restrict__ cum2 = nullptr) {
   __shared__ unsigned part[1024];
+  if (blockIdx.x == 1) {   // the second list of the same blocks
+    bcount = bcount2;
+    listCount = listCount2;
+    cum = cum2;
+  }
   const int t = threadIdx.x;
   const int64_t per = (nb + 1023) / 1024;
   const int64_t a = min<int64_t>(nb, t * per), e = min<int64_t>(nb, a + per);
@@ -3167,7 +3203,15 @@ __global__ __launch_bounds__(1024) void k_bounds_scan(unsigned int* __restrict__
 
 __global__ __launch_bounds__(256) void k_bounds_scatter(const int32_t* __restrict__ tmp,
                                                         const unsigned int* __restrict__ off,
-                                                        int32_t* __restrict__ list) {
+                                                        int32_t* __restrict__ list,
+                                                        const int32_t* __restrict__ tmp2 = nullptr,
+                                                        const unsigned int* __restrict__ off2 = nullptr,
+                                                        int32_t* __restrict__ list2 = nullptr) {
+  if (blockIdx.y == 1) {
+    tmp = tmp2;
+    off = off2;
+    list = list2;
+  }
   const int64_t b = blockIdx.x;
   const unsigned o = off[b], c = off[b + 1] - o;
   for (unsigned i = threadIdx.x; i < c; i += 256) list[o + i] = tmp[b * kBndRows + i];
@@ -3269,8 +3313,11 @@ int bounds_filter(const int32_t* assign, float2* ub_lb, float* lnc, unsigned cha
                   const double* xnorm, int64_t n, int k, const double* delta,
                   const DriftParams* prm, int32_t* tmp, unsigned int* bcount, int32_t* rcList,
                   unsigned int* rcCount, unsigned long long* rcCum, const double* stats,
-                  int32_t* nbr, float* nbrR, hipStream_t st) {
+                  int32_t* nbr, float* nbrR, hipStream_t st, int32_t* tmp2,
+                  unsigned int* bcount2, int32_t* list1, unsigned int* list1Count,
+                  unsigned long long* cum1) {
   const int64_t nb = bounds_blocks(n);
+  const bool two = tmp2 && bcount2 && list1 && list1Count;
   if (nb <= 0) return CYC_OK;
   KernelTimer timer("k_kmeans_bounds", st);
   if (stats) {
@@ -3279,14 +3326,29 @@ int bounds_filter(const int32_t* assign, float2* ub_lb, float* lnc, unsigned cha
   }
   hipLaunchKernelGGL(k_bounds_filter, dim3((unsigned)nb), dim3(256), 0, st, assign, ub_lb, lnc,
                      state, xnorm, n, k, delta, prm, tmp, bcount,
-                     stats ? (const float*)nbrR : nullptr);
+                     stats ? (const float*)nbrR : nullptr, two ? tmp2 : nullptr,
+                     two ? bcount2 : nullptr);
   CYC_LAUNCH_CHECK("k_bounds_filter");
-  hipLaunchKernelGGL(k_bounds_scan, dim3(1), dim3(1024), 0, st, bcount, nb, rcCount, rcCum);
+  // both lists' scans and scatters as one launch each (block / y index 1:
+  // the state-1 list)
+  hipLaunchKernelGGL(k_bounds_scan, dim3(two ? 2 : 1), dim3(1024), 0, st, bcount, nb, rcCount,
+                     rcCum, two ? bcount2 : nullptr, two ? list1Count : nullptr,
+                     two ? cum1 : nullptr);
   CYC_LAUNCH_CHECK("k_bounds_scan");
-  hipLaunchKernelGGL(k_bounds_scatter, dim3((unsigned)nb), dim3(256), 0, st, (const int32_t*)tmp,
-                     (const unsigned int*)bcount, rcList);
+  hipLaunchKernelGGL(k_bounds_scatter, dim3((unsigned)nb, two ? 2 : 1), dim3(256), 0, st,
+                     (const int32_t*)tmp, (const unsigned int*)bcount, rcList,
+                     two ? (const int32_t*)tmp2 : nullptr,
+                     two ? (const unsigned int*)bcount2 : nullptr, two ? list1 : nullptr);
   CYC_LAUNCH_CHECK("k_bounds_scatter");
   return CYC_OK;
+}
+
+bool recheck_two_phase() {
+  static const bool two = [] {
+    const char* e = std::getenv("CYC_KMEANS_RECHECK");
+    return !(e && e[0] == '1');
+  }();
+  return two;
 }
 
 // After the re-check: the state-1 rows into the screen's list (bd.list).

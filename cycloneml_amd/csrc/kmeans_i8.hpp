@@ -172,6 +172,9 @@ struct Bounds {
   const int32_t* nbr = nullptr;
   const float* nbrR = nullptr;
   int dump = 0;                     // diagnostics: dump the state after the re-check
+  // the filter already listed its state-1 rows in list / listCount (cum
+  // counted): the re-check appends its failures there, no bounds_collect
+  bool collected = false;
   // bounds_collect's scratch and output (rowsIn / rowsInCount), its count
   // of fully screened rows added to *cum
   int32_t* tmp = nullptr;
@@ -205,7 +208,14 @@ int bounds_filter(const int32_t* assign, float2* ub_lb, float* lnc, unsigned cha
                   const double* xnorm, int64_t n, int k, const double* delta,
                   const DriftParams* prm, int32_t* tmp, unsigned int* bcount, int32_t* rcList,
                   unsigned int* rcCount, unsigned long long* rcCum, const double* stats,
-                  int32_t* nbr, float* nbrR, hipStream_t st);
+                  int32_t* nbr, float* nbrR, hipStream_t st, int32_t* tmp2 = nullptr,
+                  unsigned int* bcount2 = nullptr, int32_t* list1 = nullptr,
+                  unsigned int* list1Count = nullptr, unsigned long long* cum1 = nullptr);
+// tmp2 .. cum1 (optional, with recheck_two_phase()): the filter also lists
+// its state-1 rows (tmp2 / bcount2 scratch like tmp / bcount) into list1 /
+// *list1Count, their count added to *cum1 -- the screen's list before the
+// re-check appends the rows it fails (Bounds::collected).
+bool recheck_two_phase();   // CYC_KMEANS_RECHECK != 1
 
 // After the re-check (inside screen): the state-1 rows into bd.list /
 // bd.listCount (the screen's rowsIn), their count added to *bd.cum.
