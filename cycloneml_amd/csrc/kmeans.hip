@@ -2181,47 +2181,39 @@ __global__ __launch_bounds__(256) void k_inc_check(const double* __restrict__ cc
   }
 }
 
-// The incremental result into the caller's buffers (sums += S, wsum += W,
-// cost_sum += the checked total).
-__global__ __launch_bounds__(256) void k_inc_emit(const double* __restrict__ S,
-                                                  const double* __restrict__ W, int d,
-                                                  const double* __restrict__ tot,
-                                                  double* __restrict__ sums,
-                                                  double* __restrict__ wsum,
-                                                  double* __restrict__ costSum,
-                                                  const int* __restrict__ gate) {
-  if (!gate[1]) return;
+// After the check (one launch, k_inc_finish): the incremental result into
+// the caller's buffers (gate[1]: sums += S, wsum += W, cost_sum += the
+// checked total); after a full pass (gate[0]) its fresh sums are the state
+// (written by k_reduce_clusters), P = C, Q = the clusters' costs, N = the
+// counts, and the error bounds of the full pass's own summation (<= 256
+// rows per chunk partial, the block tree, then the chunk fold).  The two
+// read and write disjoint buffers, so one after the other or side by side
+// is the same.
+__global__ __launch_bounds__(256) void k_inc_finish(
+    const double* __restrict__ C, int d, double* __restrict__ P, const double* __restrict__ ccost,
+    const int64_t* __restrict__ total, const int64_t* __restrict__ chunkStart,
+    double* __restrict__ Q, int64_t* __restrict__ N, const double* __restrict__ A,
+    double* __restrict__ ES, double* __restrict__ EQ, const double* __restrict__ S,
+    const double* __restrict__ W, const double* __restrict__ tot, double* __restrict__ sums,
+    double* __restrict__ wsum, double* __restrict__ costSum, const int* __restrict__ gate) {
   const int c = blockIdx.x;
-  for (int j = threadIdx.x; j < d; j += 256)
-    sums[(int64_t)c * d + j] = dadd(sums[(int64_t)c * d + j], S[(int64_t)c * d + j]);
-  if (threadIdx.x == 0) {
-    wsum[c] = dadd(wsum[c], W[c]);
-    if (c == 0) costSum[0] = dadd(costSum[0], tot[0]);
+  if (gate[0]) {
+    for (int j = threadIdx.x; j < d; j += 256) P[(int64_t)c * d + j] = C[(int64_t)c * d + j];
+    if (threadIdx.x == 0) {
+      const double f = 0x1p-52 * (double)(300 + (chunkStart[c + 1] - chunkStart[c]));
+      Q[c] = ccost[c];
+      N[c] = total[c];
+      ES[c] = f * A[c];
+      EQ[c] = f * fabs(ccost[c]);
+    }
   }
-}
-
-// After a full pass: its fresh sums are the state (written by
-// k_reduce_clusters), P = C, Q = the clusters' costs, N = the counts, and the
-// error bounds of the full pass's own summation (<= 256 rows per chunk
-// partial, the block tree, then the chunk fold).
-__global__ __launch_bounds__(256) void k_inc_reset(const double* __restrict__ C, int d,
-                                                   double* __restrict__ P,
-                                                   const double* __restrict__ ccost,
-                                                   const int64_t* __restrict__ total,
-                                                   const int64_t* __restrict__ chunkStart,
-                                                   double* __restrict__ Q, int64_t* __restrict__ N,
-                                                   const double* __restrict__ A,
-                                                   double* __restrict__ ES, double* __restrict__ EQ,
-                                                   const int* __restrict__ gate) {
-  if (!gate[0]) return;
-  const int c = blockIdx.x;
-  for (int j = threadIdx.x; j < d; j += 256) P[(int64_t)c * d + j] = C[(int64_t)c * d + j];
-  if (threadIdx.x == 0) {
-    const double f = 0x1p-52 * (double)(300 + (chunkStart[c + 1] - chunkStart[c]));
-    Q[c] = ccost[c];
-    N[c] = total[c];
-    ES[c] = f * A[c];
-    EQ[c] = f * fabs(ccost[c]);
+  if (gate[1]) {
+    for (int j = threadIdx.x; j < d; j += 256)
+      sums[(int64_t)c * d + j] = dadd(sums[(int64_t)c * d + j], S[(int64_t)c * d + j]);
+    if (threadIdx.x == 0) {
+      wsum[c] = dadd(wsum[c], W[c]);
+      if (c == 0) costSum[0] = dadd(costSum[0], tot[0]);
+    }
   }
 }
 
@@ -3269,16 +3261,14 @@ int inc_accumulate(cyc_kmeans_plan p, cyc_kmeans_rows rows, const double* X,
   hipLaunchKernelGGL(k_cost_total, dim3(1), dim3(256), 0, st, (const double*)p->ccost.ptr, k,
                      cost_sum, (const int*)gate);
   CYC_LAUNCH_CHECK("k_cost_total");
-  hipLaunchKernelGGL(k_inc_reset, dim3(k), dim3(256), 0, st, C, d, (double*)rows->iP.ptr,
+  hipLaunchKernelGGL(k_inc_finish, dim3(k), dim3(256), 0, st, C, d, (double*)rows->iP.ptr,
                      (const double*)p->ccost.ptr, (const int64_t*)p->total.ptr,
                      (const int64_t*)p->chunkStart.ptr, (double*)rows->iQ.ptr,
                      (int64_t*)rows->iN.ptr, (const double*)rows->iA.ptr, (double*)rows->iES.ptr,
-                     (double*)rows->iEQ.ptr, (const int*)gate);
-  CYC_LAUNCH_CHECK("k_inc_reset");
-  hipLaunchKernelGGL(k_inc_emit, dim3(k), dim3(256), 0, st, (const double*)rows->iS.ptr,
-                     (const double*)rows->iW.ptr, d, (const double*)rows->iTot.ptr, sums, wsum,
+                     (double*)rows->iEQ.ptr, (const double*)rows->iS.ptr,
+                     (const double*)rows->iW.ptr, (const double*)rows->iTot.ptr, sums, wsum,
                      cost_sum, (const int*)gate);
-  CYC_LAUNCH_CHECK("k_inc_emit");
+  CYC_LAUNCH_CHECK("k_inc_finish");
   return CYC_OK;
 }
 
